@@ -1,0 +1,128 @@
+"""GPT-2 (small: 12 layers, d=768, 12 heads, ctx 1024, vocab 50257) split into pipeline
+stages, bf16 (BASELINE config 5: "2-stage GPT-2-small transformer split bf16").
+
+Stage 0 owns the token/position embeddings, the last stage owns ``ln_f`` + ``lm_head``;
+the 12 blocks are divided evenly. Boundary tensor: [mb, S, 768] bf16 (1.5 MiB per sample
+at S=1024) — the large-activation send that RCCL p2p overlaps with compute.
+
+The output projection is untied from ``wte`` because the two live on different ranks
+(documented deviation from the 124M tied checkpoint; +38.6M parameters on the last stage).
+Parameter names follow the common GPT-2 layout (wte, wpe, h.{i}.ln_1, h.{i}.attn.c_attn,
+h.{i}.attn.c_proj, h.{i}.ln_2, h.{i}.mlp.c_fc, h.{i}.mlp.c_proj, ln_f, lm_head).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .base import ModelSpec, PipelineStage
+
+
+@dataclass
+class GPT2Config:
+    n_layer: int = 12
+    n_head: int = 12
+    n_embd: int = 768
+    vocab_size: int = 50257
+    block_size: int = 1024
+    dropout: float = 0.0
+
+
+class CausalSelfAttention(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
+        self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
+        self.n_head = cfg.n_head
+
+    def forward(self, x):
+        B, S, C = x.shape
+        qkv = self.c_attn(x)
+        q, k, v = qkv.split(C, dim=2)
+        h = self.n_head
+        q = q.view(B, S, h, C // h).transpose(1, 2)
+        k = k.view(B, S, h, C // h).transpose(1, 2)
+        v = v.view(B, S, h, C // h).transpose(1, 2)
+        y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        y = y.transpose(1, 2).contiguous().view(B, S, C)
+        return self.c_proj(y)
+
+
+class MLP(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+
+    def forward(self, x):
+        return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.ln_1 = nn.LayerNorm(cfg.n_embd)
+        self.attn = CausalSelfAttention(cfg)
+        self.ln_2 = nn.LayerNorm(cfg.n_embd)
+        self.mlp = MLP(cfg)
+
+    def forward(self, x):
+        x = x + self.attn(self.ln_1(x))
+        return x + self.mlp(self.ln_2(x))
+
+
+class GPT2Stage(PipelineStage):
+    def __init__(self, cfg: GPT2Config, stage_id: int, num_stages: int):
+        super().__init__()
+        if cfg.n_layer % num_stages:
+            raise ValueError("n_layer must be divisible by num_stages")
+        self.cfg = cfg
+        self.stage_id, self.num_stages = stage_id, num_stages
+        self.loss_kind = "ce"
+        per = cfg.n_layer // num_stages
+        if stage_id == 0:
+            self.wte = nn.Embedding(cfg.vocab_size, cfg.n_embd)
+            self.wpe = nn.Embedding(cfg.block_size, cfg.n_embd)
+        self.h = nn.ModuleDict({str(i): Block(cfg) for i in range(stage_id * per, (stage_id + 1) * per)})
+        if stage_id == num_stages - 1:
+            self.ln_f = nn.LayerNorm(cfg.n_embd)
+            self.lm_head = nn.Linear(cfg.n_embd, cfg.vocab_size, bias=False)
+        self._init()
+
+    def _init(self):
+        for name, p in self.named_parameters():
+            if name.endswith("c_proj.weight"):
+                nn.init.normal_(p, 0.0, 0.02 / math.sqrt(2 * self.cfg.n_layer))
+            elif p.dim() >= 2:
+                nn.init.normal_(p, 0.0, 0.02)
+            elif name.endswith("bias"):
+                nn.init.zeros_(p)
+
+    def forward(self, x):
+        if self.stage_id == 0:
+            S = x.shape[1]
+            pos = torch.arange(S, device=x.device)
+            x = self.wte(x) + self.wpe(pos)[None]
+        for blk in self.h.values():
+            x = blk(x)
+        if self.stage_id == self.num_stages - 1:
+            x = self.lm_head(self.ln_f(x))
+        return x
+
+
+def gpt2_spec(num_stages: int = 2, cfg: GPT2Config = None, seq_len: int = None, dtype=torch.bfloat16) -> ModelSpec:
+    cfg = cfg or GPT2Config()
+    S = seq_len or cfg.block_size
+
+    def build(s):
+        return GPT2Stage(cfg, s, num_stages)
+
+    def shape(s, mb):
+        return (mb, S, cfg.n_embd)
+
+    return ModelSpec(name="gpt2", num_stages=num_stages, build_stage=build, boundary_shape=shape,
+                     boundary_dtype=dtype, input_kind="tokens", param_dtype=dtype)

@@ -1,0 +1,157 @@
+"""MNIST-shape MLPs split into pipeline stages (BASELINE configs 1-3).
+
+* ``mlp``       784 -> 128 -> 10, 2 stages: stage 0 = fc1+ReLU, stage 1 = fc2+log_softmax
+                (the north-star model; same cut position as the reference, which sends the
+                flattened activation to the next rank: /root/reference/simple_distributed.py:46-49)
+* ``mlp4x1024`` 784 -> 1024 x4 -> 10, 4 stages (fc1 | fc2 | fc3 | fc4+fc5)
+
+On a ROCm device every stage runs hand-written gfx950 kernels with no autograd graph:
+
+* hidden layer forward  : fp32 MFMA GEMM with fused bias + ReLU epilogue
+* hidden layer backward : dX GEMM with the ReLU mask fused into the A-operand load,
+                          dW/db split-K MFMA GEMM accumulating straight into the flat grad buffer
+* classifier head       : ONE kernel for fc2 -> log_softmax -> NLL -> backward (dlogits, dW2,
+                          db2, dX) — the entire last stage of the 784-128-10 model.
+
+On CPU the same modules run through PyTorch autograd (Gloo multi-process tests).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .base import ModelSpec, PipelineStage
+from .. import ops
+
+
+def partition_layers(n_layers: int, n_stages: int) -> List[List[int]]:
+    """Contiguous layer ranges per stage; extra layers go to the LAST stages (the classifier
+    head is cheap, so the last stage takes the hidden layer + head)."""
+    if n_stages > n_layers:
+        raise ValueError(f"cannot split {n_layers} layers into {n_stages} stages")
+    base, extra = divmod(n_layers, n_stages)
+    out, i = [], 0
+    for s in range(n_stages):
+        k = base + (1 if s >= n_stages - extra else 0)
+        out.append(list(range(i, i + k)))
+        i += k
+    return out
+
+
+class MLPStage(PipelineStage):
+    """A contiguous run of Linear layers; ReLU after every layer except the final classifier."""
+
+    def __init__(self, dims: Sequence[int], layer_ids: Sequence[int], stage_id: int, num_stages: int,
+                 dropout: float = 0.0):
+        super().__init__()
+        self.stage_id, self.num_stages = stage_id, num_stages
+        self.n_total = len(dims) - 1
+        self.layer_ids = list(layer_ids)
+        self.names = [f"fc{i + 1}" for i in self.layer_ids]
+        for i, name in zip(self.layer_ids, self.names):
+            setattr(self, name, nn.Linear(dims[i], dims[i + 1]))
+        self.loss_kind = "nll"
+        self.in_features = dims[self.layer_ids[0]]
+
+    def layers(self) -> List[nn.Linear]:
+        return [getattr(self, n) for n in self.names]
+
+    def _is_classifier(self, i: int) -> bool:
+        return self.layer_ids[i] == self.n_total - 1
+
+    def forward(self, x):
+        x = x.reshape(x.shape[0], -1)
+        for i, lin in enumerate(self.layers()):
+            x = lin(x)
+            if self._is_classifier(i):
+                x = F.log_softmax(x, dim=1)
+            else:
+                x = F.relu(x)
+        return x
+
+    # ---- fused HIP path --------------------------------------------------------------------
+    def _fused(self, x) -> bool:
+        return x.is_cuda
+
+    def fwd(self, x, ctx, train):
+        if not self._fused(x):
+            return super().fwd(x, ctx, train)
+        x = x.reshape(x.shape[0], -1)
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            x = x.float().contiguous()
+        acts = [x]
+        for i, lin in enumerate(self.layers()):
+            assert not self._is_classifier(i), "classifier layers run in head_fwd"
+            x = ops.linear_relu_fwd(x, lin.weight, lin.bias)
+            acts.append(x)
+        if train:
+            ctx["acts"] = acts
+        return x
+
+    def bwd(self, grad_y, ctx):
+        if "acts" not in ctx:
+            return super().bwd(grad_y, ctx)
+        acts = ctx.pop("acts")
+        g = grad_y.contiguous()
+        layers = self.layers()
+        for i in range(len(layers) - 1, -1, -1):
+            lin = layers[i]
+            # g is dL/d(post-ReLU output); the mask (out > 0) is applied inside the kernels
+            need_dx = (i > 0) or (not self.is_first)
+            g = ops.linear_relu_bwd(acts[i], acts[i + 1], g, lin.weight, lin.weight.grad, lin.bias.grad, need_dx)
+        return g
+
+    def head_fwd(self, x, target, ctx, train, loss_scale):
+        if not self._fused(x):
+            return super().head_fwd(x, target, ctx, train, loss_scale)
+        x = x.reshape(x.shape[0], -1)
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            x = x.float().contiguous()
+        layers = self.layers()
+        acts = [x]
+        for i in range(len(layers) - 1):
+            x = ops.linear_relu_fwd(x, layers[i].weight, layers[i].bias)
+            acts.append(x)
+        head = layers[-1]
+        need_dx = train and (len(layers) > 1 or not self.is_first)
+        loss, correct, dx = ops.linear_logsoftmax_nll(
+            x, head.weight, head.bias, target,
+            head.weight.grad if train else None, head.bias.grad if train else None,
+            loss_scale, need_dx)
+        if train:
+            ctx["acts"] = acts
+            ctx["dx"] = dx
+        return loss, correct, target.numel()
+
+    def head_bwd(self, ctx):
+        if "dx" not in ctx:
+            return super().head_bwd(ctx)
+        acts = ctx.pop("acts")
+        g = ctx.pop("dx")
+        layers = self.layers()
+        for i in range(len(layers) - 2, -1, -1):
+            need_dx = (i > 0) or (not self.is_first)
+            g = ops.linear_relu_bwd(acts[i], acts[i + 1], g, layers[i].weight, layers[i].weight.grad,
+                                    layers[i].bias.grad, need_dx)
+        return g
+
+
+def mlp_spec(dims: Sequence[int], num_stages: int, name: str) -> ModelSpec:
+    dims = list(dims)
+    parts = partition_layers(len(dims) - 1, num_stages)
+
+    def build(s: int) -> PipelineStage:
+        return MLPStage(dims, parts[s], s, num_stages)
+
+    def shape(s: int, mb: int) -> Tuple[int, ...]:
+        return (mb, dims[parts[s][-1] + 1])
+
+    return ModelSpec(name=name, num_stages=num_stages, build_stage=build, boundary_shape=shape,
+                     boundary_dtype=torch.float32, input_kind="image")
+
+
+MLP_DIMS = (784, 128, 10)
+MLP4X1024_DIMS = (784, 1024, 1024, 1024, 1024, 10)

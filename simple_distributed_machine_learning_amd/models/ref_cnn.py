@@ -1,0 +1,79 @@
+"""The reference's own model: the PyTorch-examples MNIST CNN split after the conv stack.
+
+Stage 0 (reference ``Network1``, /root/reference/simple_distributed.py:26-50):
+    conv1(1->10,k5) -> maxpool2 -> relu -> conv2(10->20,k5) -> Dropout2d(0.5) -> maxpool2
+    -> relu -> flatten(320)
+Stage 1 (reference ``Network2``, :60-80):
+    fc1(320->50) -> relu -> dropout(0.5) -> fc2(50->10) -> log_softmax
+
+``state_dict`` keys match the reference exactly (stage 0: conv1.*, conv2.*; stage 1:
+fc1.*, fc2.*), so per-stage checkpoints are interchangeable.
+
+Reference quirk (Appendix B.3): ``F.dropout`` in Network2 has no ``training=`` argument, so
+it stays active during ``test()``. ``eval_dropout=True`` (default) reproduces that;
+``False`` gives the conventional behaviour.
+
+Ops run through PyTorch (MIOpen convolutions on ROCm) in this round; the stage boundary
+tensor [mb, 320] moves over RCCL exactly like the MLP's.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .base import ModelSpec, PipelineStage
+
+
+class Network1Stage(PipelineStage):
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(1, 10, kernel_size=5)
+        self.conv2 = nn.Conv2d(10, 20, kernel_size=5)
+        self.conv2_drop = nn.Dropout2d()
+        self.loss_kind = "nll"
+
+    def forward(self, x):
+        z1 = F.relu(F.max_pool2d(self.conv1(x), 2))
+        z2 = self.conv2(z1)
+        z3 = F.relu(F.max_pool2d(self.conv2_drop(z2), 2))
+        return z3.reshape(-1, 320)
+
+
+class Network2Stage(PipelineStage):
+    def __init__(self, eval_dropout: bool = True):
+        super().__init__()
+        self.fc1 = nn.Linear(320, 50)
+        self.fc2 = nn.Linear(50, 10)
+        self.eval_dropout = eval_dropout
+        self.loss_kind = "nll"
+
+    def forward(self, x):
+        z4 = F.dropout(F.relu(self.fc1(x)), p=0.5, training=self.training or self.eval_dropout)
+        z5 = self.fc2(z4)
+        return F.log_softmax(z5, dim=1)
+
+
+class RefCNNSingle(nn.Module):
+    """Both stages in one module (single-process parity reference)."""
+
+    def __init__(self, s0: Network1Stage, s1: Network2Stage):
+        super().__init__()
+        self.s0, self.s1 = s0, s1
+
+    def forward(self, x):
+        return self.s1(self.s0(x))
+
+
+def ref_cnn_spec(num_stages: int = 2, eval_dropout: bool = True) -> ModelSpec:
+    if num_stages != 2:
+        raise ValueError("ref_cnn is defined as the reference's 2-stage split")
+
+    def build(s: int) -> PipelineStage:
+        return Network1Stage() if s == 0 else Network2Stage(eval_dropout)
+
+    def shape(s: int, mb: int):
+        return (mb, 320)
+
+    return ModelSpec(name="ref_cnn", num_stages=2, build_stage=build, boundary_shape=shape,
+                     boundary_dtype=torch.float32, input_kind="image")

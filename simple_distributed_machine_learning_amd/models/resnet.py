@@ -1,0 +1,106 @@
+"""ResNet-18-style CNN on MNIST-shape input, split into up to 8 pipeline stages
+(BASELINE config 4: "8-stage ResNet-18-style CNN across 8 MI355X with 1F1B").
+
+Architecture (CIFAR-style stem for 28x28 inputs): conv3x3(1->64)+BN+ReLU, then 4 layers of
+2 BasicBlocks (64, 128/2, 256/2, 512/2), global average pool, fc(512->10).
+The 8 BasicBlocks are the cut units: stage k gets ``8 / num_stages`` consecutive blocks;
+the stem rides with the first stage and pool+fc with the last.
+
+BatchNorm runs per micro-batch (GPipe semantics). Convolutions use MIOpen through
+PyTorch in this round.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .base import ModelSpec, PipelineStage
+
+WIDTHS = (64, 128, 256, 512)
+
+
+class BasicBlock(nn.Module):
+    def __init__(self, cin: int, cout: int, stride: int):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.shortcut = None
+        if stride != 1 or cin != cout:
+            self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        sc = x if self.shortcut is None else self.shortcut(x)
+        return F.relu(out + sc)
+
+
+def block_defs(in_ch: int = 1):
+    defs = []
+    cin = 64
+    for li, w in enumerate(WIDTHS):
+        for bi in range(2):
+            stride = 2 if (li > 0 and bi == 0) else 1
+            defs.append((f"layer{li + 1}.{bi}", cin, w, stride))
+            cin = w
+    return defs
+
+
+class ResNetStage(PipelineStage):
+    def __init__(self, stage_id: int, num_stages: int, in_ch: int = 1, num_classes: int = 10):
+        super().__init__()
+        if 8 % num_stages:
+            raise ValueError("resnet18 splits into 1, 2, 4 or 8 stages")
+        self.stage_id, self.num_stages = stage_id, num_stages
+        per = 8 // num_stages
+        defs = block_defs(in_ch)[stage_id * per:(stage_id + 1) * per]
+        self.loss_kind = "ce"
+        if stage_id == 0:
+            self.stem_conv = nn.Conv2d(in_ch, 64, 3, 1, 1, bias=False)
+            self.stem_bn = nn.BatchNorm2d(64)
+        self.block_names = []
+        for name, cin, cout, stride in defs:
+            attr = name.replace(".", "_")
+            setattr(self, attr, BasicBlock(cin, cout, stride))
+            self.block_names.append(attr)
+        if stage_id == num_stages - 1:
+            self.fc = nn.Linear(512, num_classes)
+
+    def forward(self, x):
+        if self.stage_id == 0:
+            x = F.relu(self.stem_bn(self.stem_conv(x)))
+        for n in self.block_names:
+            x = getattr(self, n)(x)
+        if self.stage_id == self.num_stages - 1:
+            x = F.adaptive_avg_pool2d(x, 1).flatten(1)
+            x = self.fc(x)
+        return x
+
+
+def _out_shape(stage: int, num_stages: int, hw: int = 28):
+    per = 8 // num_stages
+    last_block = (stage + 1) * per - 1
+    defs = block_defs()
+    c = defs[last_block][2]
+    size = hw
+    for i in range(last_block + 1):
+        if defs[i][3] == 2:
+            size = (size + 1) // 2
+    return c, size
+
+
+def resnet18_spec(num_stages: int = 8) -> ModelSpec:
+    def build(s):
+        return ResNetStage(s, num_stages)
+
+    def shape(s, mb):
+        c, hw = _out_shape(s, num_stages)
+        return (mb, c, hw, hw)
+
+    return ModelSpec(name="resnet18", num_stages=num_stages, build_stage=build, boundary_shape=shape,
+                     boundary_dtype=torch.float32, input_kind="image")

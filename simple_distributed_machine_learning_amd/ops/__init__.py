@@ -1,0 +1,57 @@
+"""Fused ops: gfx950 HIP kernels on ROCm devices, PyTorch fp32 reference on CPU.
+
+A CUDA(ROCm) tensor ALWAYS goes to the HIP kernel extension; if it is missing this raises
+(no silent fallback to PyTorch on the GPU). CPU tensors use ``ops.reference``.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .._native import kernels
+from . import reference as ref
+
+
+def _k():
+    return kernels()
+
+
+def linear_relu_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """relu(x @ w.T + b); x [M,K], w [N,K] (nn.Linear layout), b [N]."""
+    if x.is_cuda:
+        return _k().linear_fwd_f32(x, w, b, True)
+    return ref.linear_relu_fwd(x, w, b)
+
+
+def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
+    if x.is_cuda:
+        return _k().linear_fwd_f32(x, w, b, False)
+    return ref.linear_fwd(x, w, b)
+
+
+def linear_relu_bwd(x, y, gy, w, gw, gb, need_dx: bool):
+    """Backward of y = relu(x @ w.T + b): accumulates gw += gz.T @ x, gb += sum(gz) with
+    gz = gy * (y > 0); returns gz @ w when need_dx."""
+    if x.is_cuda:
+        return _k().linear_bwd_f32(x, y, gy, w, gw, gb, need_dx, True)
+    return ref.linear_relu_bwd(x, y, gy, w, gw, gb, need_dx)
+
+
+def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool):
+    """Fused classifier head: z = x @ w.T + b -> log_softmax -> NLL (sum) and, when grads are
+    given, the full backward (gw/gb accumulated, dx returned) scaled by ``scale``.
+    Returns (loss_sum, correct, dx) — loss_sum/correct are 0-dim device tensors."""
+    if x.is_cuda:
+        stats, dx = _k().head_logsoftmax_nll_f32(x, w, b, target, gw, gb, float(scale), need_dx)
+        return stats[0], stats[1], dx
+    return ref.linear_logsoftmax_nll(x, w, b, target, gw, gb, scale, need_dx)
+
+
+def sgd_momentum_(p, g, buf, lr: float, momentum: float, dampening: float = 0.0, weight_decay: float = 0.0,
+                  nesterov: bool = False, first: bool = False):
+    if p.is_cuda:
+        _k().sgd_momentum_(p, g, buf, float(lr), float(momentum), float(dampening), float(weight_decay),
+                           bool(nesterov), bool(first))
+        return
+    ref.sgd_momentum_(p, g, buf, lr, momentum, dampening, weight_decay, nesterov, first)

@@ -1,0 +1,83 @@
+"""Plain-PyTorch fp32 reference implementations of every fused op.
+
+They define the exact semantics the HIP kernels (csrc/kernels/*.hip) must reproduce and are
+what the numerics tests compare against. They also serve the CPU (Gloo) path.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+
+def linear_relu_fwd(x, w, b):
+    return torch.relu(x @ w.t() + b)
+
+
+def linear_relu_bwd(x, y, gy, w, gw: Optional[torch.Tensor], gb: Optional[torch.Tensor], need_dx: bool):
+    gz = gy * (y > 0).to(gy.dtype)
+    if gw is not None:
+        gw += gz.t() @ x
+    if gb is not None:
+        gb += gz.sum(0)
+    return gz @ w if need_dx else None
+
+
+def linear_fwd(x, w, b):
+    return x @ w.t() + (b if b is not None else 0)
+
+
+def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool):
+    z = x @ w.t() + b
+    lp = F.log_softmax(z, dim=1)
+    loss = -lp.gather(1, target.view(-1, 1)).sum()
+    correct = (lp.argmax(1) == target).sum()
+    dx = None
+    if gw is not None or need_dx:
+        dz = lp.exp()
+        dz[torch.arange(z.shape[0]), target] -= 1.0
+        dz *= scale
+        if gw is not None:
+            gw += dz.t() @ x
+        if gb is not None:
+            gb += dz.sum(0)
+        if need_dx:
+            dx = dz @ w
+    return loss, correct, dx
+
+
+def sgd_momentum_(p, g, buf, lr: float, momentum: float, dampening: float = 0.0, weight_decay: float = 0.0,
+                  nesterov: bool = False, first: bool = False):
+    """torch.optim.SGD semantics (first step: buf = g, no dampening)."""
+    d = g if weight_decay == 0 else g + weight_decay * p
+    if momentum != 0:
+        if first:
+            buf.copy_(d)
+        else:
+            buf.mul_(momentum).add_(d, alpha=1 - dampening)
+        d = d + momentum * buf if nesterov else buf
+    p.add_(d, alpha=-lr)
+
+
+def cross_entropy_fwd_bwd(logits, target, scale: float, ignore_index: int = -100):
+    """Returns (loss_sum, correct, count, dlogits) with dlogits = scale * (softmax - onehot)."""
+    z = logits.float()
+    lse = torch.logsumexp(z, dim=1, keepdim=True)
+    valid = target != ignore_index
+    t = target.clamp_min(0)
+    loss = (lse.squeeze(1) - z.gather(1, t.view(-1, 1)).squeeze(1))[valid].sum()
+    correct = ((z.argmax(1) == target) & valid).sum()
+    g = torch.exp(z - lse)
+    g[torch.arange(z.shape[0]), t] -= 1.0
+    g *= scale
+    g[~valid] = 0
+    return loss, correct, int(valid.sum()), g.to(logits.dtype)
+
+
+def layernorm_fwd(x, w, b, eps: float = 1e-5):
+    return F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps).to(x.dtype)
+
+
+def gelu_tanh(x):
+    return F.gelu(x.float(), approximate="tanh").to(x.dtype)

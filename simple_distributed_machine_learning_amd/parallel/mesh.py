@@ -1,0 +1,165 @@
+"""Process-group bootstrap and the dp x pp rank mesh.
+
+Replaces the reference's RPC bootstrap (``rpc.init_rpc`` / ``rpc.shutdown``,
+/root/reference/simple_distributed.py:167-186): instead of a "master" that drives remote
+modules, every rank joins ONE ``torch.distributed`` process group (RCCL — PyTorch-ROCm's
+``"nccl"`` backend — on MI355X, Gloo on the CPU test path) and runs the same SPMD program.
+
+Rank layout: ``rank = dp_rank * pp + pp_rank`` — the ranks of one pipeline are adjacent,
+so on an 8-GPU node the stage pairs (0,1), (2,3), ... each talk over their own direct xGMI
+link and DP replicas of a stage all-reduce over the other links.
+
+Point-to-point traffic uses one 2-rank process group per *ordered* neighbour pair
+(direction). Each group owns its own RCCL communicator and HIP stream, so every
+direction is an independent FIFO channel — exactly the model the native schedule
+validator (csrc/runtime/schedule.cpp) proves deadlock-free.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class Mesh:
+    rank: int
+    world_size: int
+    local_rank: int
+    pp: int  # ranks per pipeline
+    dp: int  # pipeline replicas
+    schedule_kind: str
+    device: torch.device
+    backend: str
+    pp_rank: int = 0
+    dp_rank: int = 0
+    # (src_global, dst_global) -> group carrying src->dst messages
+    p2p_groups: Dict[Tuple[int, int], object] = field(default_factory=dict)
+    # group used to all-reduce this rank's gradients (None: nothing to reduce)
+    grad_group: Optional[object] = None
+    grad_group_ranks: List[int] = field(default_factory=list)
+    pipe_group: Optional[object] = None
+    initialized_here: bool = False
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+    def global_rank(self, dp_rank: int, pp_rank: int) -> int:
+        return dp_rank * self.pp + pp_rank
+
+    def pipe_ranks(self) -> List[int]:
+        return [self.global_rank(self.dp_rank, r) for r in range(self.pp)]
+
+    def is_master(self) -> bool:
+        return self.rank == 0
+
+
+def select_device(local_rank: int) -> torch.device:
+    if torch.cuda.is_available():
+        n = torch.cuda.device_count()
+        dev = torch.device("cuda", local_rank % max(n, 1))
+        torch.cuda.set_device(dev)
+        return dev
+    return torch.device("cpu")
+
+
+def default_backend(device: torch.device) -> str:
+    # "nccl" is RCCL on PyTorch-ROCm: the collective/p2p library over xGMI.
+    return "nccl" if device.type == "cuda" else "gloo"
+
+
+def replica_groups_spec(world_size: int, pp: int, kind: str) -> List[List[int]]:
+    """Lists of ranks that hold replicas of the same stage set (gradient all-reduce groups)."""
+    dp = world_size // pp
+    groups = []
+    seen = set()
+    for r in range(pp):
+        mirror = pp - 1 - r if kind == "chimera" else r
+        key = tuple(sorted({r, mirror}))
+        if key in seen:
+            continue
+        seen.add(key)
+        ranks = sorted(d * pp + x for d in range(dp) for x in key)
+        groups.append(ranks)
+    return groups
+
+
+def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = None,
+              timeout_s: float = 600.0, rank: Optional[int] = None, world_size: Optional[int] = None,
+              local_rank: Optional[int] = None, device: Optional[torch.device] = None) -> Mesh:
+    """Join (or reuse) the default process group and build the dp x pp mesh.
+
+    Rank/world come from arguments, else torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK).
+    ``MASTER_ADDR``/``MASTER_PORT`` must be set for world_size > 1 (TCPStore rendezvous, the
+    same store the reference's ``init_rpc`` used). The timeout is finite:
+    the reference's ``rpc_timeout=0`` means "wait forever" and, on torch 2.10, an instant
+    rendezvous failure.
+    """
+    if rank is None:
+        rank = int(os.environ.get("RANK", "0"))
+    if world_size is None:
+        world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    if local_rank is None:
+        local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device is None:
+        device = select_device(local_rank)
+    if backend is None:
+        backend = default_backend(device)
+    pp = max(1, min(pp, world_size))
+    if world_size % pp != 0:
+        raise ValueError(f"world_size={world_size} is not a multiple of pipeline ranks pp={pp}")
+    mesh = Mesh(rank=rank, world_size=world_size, local_rank=local_rank, pp=pp, dp=world_size // pp,
+                schedule_kind=schedule_kind, device=device, backend=backend)
+    mesh.pp_rank = rank % pp
+    mesh.dp_rank = rank // pp
+    if world_size == 1:
+        return mesh
+
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kwargs = dict(backend=backend, rank=rank, world_size=world_size,
+                      timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kwargs["device_id"] = device
+        dist.init_process_group(**kwargs)
+        mesh.initialized_here = True
+
+    # ---- groups: every rank creates every group in the same order (collective) ----
+    timeout = datetime.timedelta(seconds=timeout_s)
+    for d in range(mesh.dp):
+        ranks = [d * pp + r for r in range(pp)]
+        g = dist.new_group(ranks, timeout=timeout) if pp > 1 else None
+        if d == mesh.dp_rank:
+            mesh.pipe_group = g
+    for d in range(mesh.dp):
+        for r in range(pp - 1):
+            a, b = d * pp + r, d * pp + r + 1
+            for src, dst in ((a, b), (b, a)):
+                g = dist.new_group([a, b], timeout=timeout)
+                if mesh.rank in (a, b):
+                    mesh.p2p_groups[(src, dst)] = g
+    for ranks in replica_groups_spec(world_size, pp, schedule_kind):
+        g = dist.new_group(ranks, timeout=timeout) if len(ranks) > 1 else None
+        if rank in ranks and len(ranks) > 1:
+            mesh.grad_group = g
+            mesh.grad_group_ranks = ranks
+    return mesh
+
+
+def shutdown(mesh: Optional[Mesh] = None):
+    """Graceful teardown: barrier then destroy (the reference's ``rpc.shutdown()`` also
+    blocks until every rank arrives, simple_distributed.py:186)."""
+    if dist.is_initialized():
+        try:
+            if mesh is not None and mesh.device.type == "cuda":
+                dist.barrier(device_ids=[mesh.device.index])
+            else:
+                dist.barrier()
+        finally:
+            dist.destroy_process_group()

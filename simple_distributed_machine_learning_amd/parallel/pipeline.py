@@ -1,0 +1,308 @@
+"""SPMD pipeline engine: executes a validated schedule on one rank.
+
+What it replaces in the reference (/root/reference/simple_distributed.py):
+
+=====================================  ==================================================
+reference                              here
+=====================================  ==================================================
+``rpc.remote('worker1', Network2)``    every rank builds the stages it owns (:meth:`__init__`)
+(:33-37)
+``RRef(z3)`` + ``rpc_sync().forward``  ``isend`` of the boundary activation to the next
++ ``to_here()`` (:47-49, :71)          rank, ``irecv`` into a fresh buffer there
+``dist_autograd.context/backward``     explicit per-stage backward seeded by the received
+(:109-112)                             gradient; input-grad sent to the previous rank
+``DistributedOptimizer.step`` (:113)   one fused SGD launch over the rank's flat buffer
+``nll_loss`` on the master (:111)      loss on the LAST stage; labels read locally
+=====================================  ==================================================
+
+Within a step nothing blocks the host except optional metric reads: receives are
+stream-level waits, sends are drained at the end of the step, and the data-parallel
+gradient all-reduce for a stage is issued as soon as that stage's last backward is done
+(overlapping the remaining backward work of other stages on the rank).
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..models.base import ModelSpec, PipelineStage, build_stages
+from ..ops.optim import FusedSGD
+from ..utils.flat import FlatParams
+from .mesh import Mesh
+from .p2p import Transport, message_tag
+from .schedule import OP_BWD, OP_FWD, OP_RECV, OP_SEND, PL_ACT, PL_GRAD, Schedule, build_schedule
+
+
+def split_sizes(n: int, m: int) -> List[int]:
+    """Micro-batch sizes (torch.tensor_split convention): first ``n % m`` get one more."""
+    m = max(1, min(m, n))
+    base, extra = divmod(n, m)
+    return [base + (1 if i < extra else 0) for i in range(m)]
+
+
+@dataclass
+class StepResult:
+    loss_sum: torch.Tensor  # summed over the samples this rank's last stage(s) saw
+    correct: torch.Tensor
+    count: int
+    wall_s: float = 0.0
+
+    def mean_loss(self) -> float:
+        return float(self.loss_sum) / max(1, self.count)
+
+
+class GradSync:
+    """Data-parallel / Chimera-mirror gradient all-reduce over the flat grad buffer.
+
+    Stages are reduced in a canonical order (descending stage id) so every member of the
+    replica group issues the same collective sequence; a stage's all-reduce is launched as
+    soon as it and all stages before it in that order have finished backward.
+    """
+
+    def __init__(self, flat: FlatParams, mesh: Mesh, local_stages: Sequence[int]):
+        self.flat, self.mesh = flat, mesh
+        self.order = sorted(set(local_stages), reverse=True)
+        self.enabled = mesh.grad_group is not None
+        self._done = set()
+        self._ptr = 0
+        self._works = []
+        # merge consecutive stages into one contiguous bucket when they are adjacent in memory
+        self.group = mesh.grad_group
+
+    def reset(self):
+        self._done.clear()
+        self._ptr = 0
+        self._works = []
+
+    def stage_done(self, stage: int):
+        if not self.enabled:
+            return
+        self._done.add(stage)
+        while self._ptr < len(self.order) and self.order[self._ptr] in self._done:
+            s = self.order[self._ptr]
+            t = self.flat.stage_slice(s, "grads")
+            self._works.append(dist.all_reduce(t, group=self.group, async_op=True))
+            self._ptr += 1
+
+    def finish(self):
+        if not self.enabled:
+            return
+        for s in self.order:
+            self.stage_done(s)
+        for w in self._works:
+            w.wait()
+        self._works = []
+
+
+class PipelineEngine:
+    def __init__(self, spec: ModelSpec, mesh: Mesh, schedule_kind: str = "1f1b", num_microbatches: int = 1,
+                 lr: float = 0.1, momentum: float = 0.5, weight_decay: float = 0.0, seed: int = 0,
+                 dtype: Optional[torch.dtype] = None, debug_sync: bool = False):
+        self.spec, self.mesh = spec, mesh
+        self.kind = schedule_kind
+        self.M = max(1, int(num_microbatches))
+        self.P = spec.num_stages
+        if self.P % mesh.pp != 0:
+            raise ValueError(f"{spec.name}: {self.P} stages cannot be placed on {mesh.pp} pipeline ranks")
+        self.device = mesh.device
+        self.dtype = dtype or spec.param_dtype
+        self.debug_sync = debug_sync or os.environ.get("SDML_DEBUG_SYNC") == "1"
+        self._sched_cache: Dict[Tuple[int, bool], Schedule] = {}
+        sched = self.schedule(self.M, False)
+        self.local_pairs = sched.local_stages(mesh.pp_rank)
+        for p in range(sched.num_pipes):
+            for s in range(self.P):
+                if sched.stage_rank(p, s) == mesh.pp_rank and (p, s) not in self.local_pairs:
+                    self.local_pairs.append((p, s))
+        self.local_stage_ids = sorted({s for _, s in self.local_pairs})
+        mods = build_stages(spec, self.local_stage_ids, base_seed=seed)
+        self.stages: Dict[int, PipelineStage] = {}
+        for s, m in zip(self.local_stage_ids, mods):
+            m.to(self.device)
+            if self.dtype != torch.float32:
+                m.to(self.dtype)
+            self.stages[s] = m
+        self.flat = FlatParams([(s, m) for s, m in self.stages.items()], self.device, self.dtype)
+        self.optimizer = FusedSGD(self.flat, lr=lr, momentum=momentum, weight_decay=weight_decay)
+        self.transport = Transport(mesh) if mesh.pp > 1 else None
+        self.grad_sync = GradSync(self.flat, mesh, self.local_stage_ids)
+        self.training = True
+        self.global_step = 0
+
+    # ---------------------------------------------------------------------------------------
+    def schedule(self, m: int, forward_only: bool) -> Schedule:
+        key = (m, forward_only)
+        if key not in self._sched_cache:
+            self._sched_cache[key] = build_schedule(self.kind, self.P, m, self.mesh.pp, forward_only=forward_only)
+        return self._sched_cache[key]
+
+    def train(self, mode: bool = True):
+        self.training = mode
+        for m in self.stages.values():
+            m.train(mode)
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def holds_first_stage(self) -> bool:
+        return 0 in self.stages
+
+    def holds_last_stage(self) -> bool:
+        return (self.P - 1) in self.stages
+
+    # ---------------------------------------------------------------------------------------
+    def _boundary(self, producer_stage: int, mb: int):
+        return self.spec.boundary_shape(producer_stage, mb), self.spec.boundary_dtype
+
+    def run(self, dataset, start: int, batch_size: int, train: bool, global_batch: Optional[int] = None,
+            step_optimizer: bool = True) -> StepResult:
+        """One pipeline step over samples [start, start+batch_size) of ``dataset``.
+
+        ``global_batch`` (default: batch_size * dp) sets the loss scale so that the summed
+        gradients equal d(mean loss over the global batch)/dθ, matching a single-process
+        ``nll_loss(..., reduction='mean')`` step on the whole batch.
+        """
+        t0 = time.perf_counter()
+        dev = self.device
+        if batch_size <= 0:  # a DP replica with no samples in a ragged last batch
+            if train:
+                self.flat.zero_grad()
+                self.grad_sync.reset()
+                self.grad_sync.finish()  # still joins the collectives of its replica group
+                if step_optimizer:
+                    self.optimizer.step()
+                    self.global_step += 1
+            z = torch.zeros((), device=dev, dtype=torch.float32)
+            return StepResult(z, torch.zeros((), device=dev, dtype=torch.int64), 0, time.perf_counter() - t0)
+        sizes = split_sizes(batch_size, self.M)
+        M = len(sizes)
+        offs = [start]
+        for s in sizes[:-1]:
+            offs.append(offs[-1] + s)
+        sched = self.schedule(M, forward_only=not train)
+        prog = sched.program(self.mesh.pp_rank)
+        gb = global_batch if global_batch is not None else batch_size * self.mesh.dp
+        scale = 1.0 / float(gb)
+        if self.spec.input_kind == "tokens":
+            scale = scale / float(dataset.seq_len)
+
+        if train:
+            self.flat.zero_grad()
+            self.grad_sync.reset()
+        last_bwd = {}
+        if train:
+            for i, ins in enumerate(prog):
+                if ins.op == OP_BWD:
+                    last_bwd[ins.stage] = i
+
+        ctxs: Dict[Tuple[int, int, int], dict] = {}
+        local: Dict[Tuple[int, int, int, int], torch.Tensor] = {}
+        outbox: Dict[Tuple[int, int, int, int], torch.Tensor] = {}
+        inbox: Dict[Tuple[int, int, int, int], Tuple[object, torch.Tensor]] = {}
+        loss_sum = torch.zeros((), device=dev, dtype=torch.float32)
+        correct = torch.zeros((), device=dev, dtype=torch.int64)
+        count = 0
+
+        def take(key, peer_rank_is_local: bool):
+            if peer_rank_is_local:
+                return local.pop(key)
+            w, buf = inbox.pop(key)
+            w.wait()
+            return buf
+
+        for i, ins in enumerate(prog):
+            op = ins.op
+            if op == OP_RECV:
+                mbsz = sizes[ins.mb]
+                prod = ins.stage if ins.payload == PL_ACT else ins.stage - 1
+                shape, dt = self._boundary(prod, mbsz)
+                buf = torch.empty(shape, dtype=dt, device=dev)
+                src = self.mesh.global_rank(self.mesh.dp_rank, ins.peer)
+                w = self.transport.irecv(buf, src, message_tag(ins.payload, ins.pipe, ins.stage, ins.mb))
+                inbox[(ins.payload, ins.pipe, ins.stage, ins.mb)] = (w, buf)
+            elif op == OP_SEND:
+                key = (ins.payload, ins.pipe, ins.stage, ins.mb)
+                t = outbox.pop(key)
+                dst = self.mesh.global_rank(self.mesh.dp_rank, ins.peer)
+                self.transport.isend(t, dst, message_tag(*key))
+            elif op == OP_FWD:
+                mod = self.stages[ins.stage]
+                mbsz, off = sizes[ins.mb], offs[ins.mb]
+                if ins.stage == 0:
+                    x = dataset.inputs(off, mbsz)
+                    if x.device != dev:
+                        x = x.to(dev, non_blocking=True)
+                else:
+                    prev_local = sched.stage_rank(ins.pipe, ins.stage - 1) == self.mesh.pp_rank
+                    x = take((PL_ACT, ins.pipe, ins.stage - 1, ins.mb), prev_local)
+                ctx = ctxs.setdefault((ins.pipe, ins.stage, ins.mb), {})
+                if mod.is_last:
+                    tgt = dataset.targets(off, mbsz)
+                    if tgt.device != dev:
+                        tgt = tgt.to(dev, non_blocking=True)
+                    l, c, n = mod.head_fwd(x, tgt, ctx, train, scale)
+                    loss_sum += l.float()
+                    correct += c
+                    count += n
+                else:
+                    y = mod.fwd(x, ctx, train)
+                    key = (PL_ACT, ins.pipe, ins.stage, ins.mb)
+                    if sched.stage_rank(ins.pipe, ins.stage + 1) == self.mesh.pp_rank:
+                        local[key] = y
+                    else:
+                        outbox[key] = y
+                if not train:
+                    ctxs.pop((ins.pipe, ins.stage, ins.mb), None)
+            elif op == OP_BWD:
+                mod = self.stages[ins.stage]
+                ctx = ctxs.pop((ins.pipe, ins.stage, ins.mb))
+                if mod.is_last:
+                    gx = mod.head_bwd(ctx)
+                else:
+                    nxt_local = sched.stage_rank(ins.pipe, ins.stage + 1) == self.mesh.pp_rank
+                    gy = take((PL_GRAD, ins.pipe, ins.stage + 1, ins.mb), nxt_local)
+                    gx = mod.bwd(gy, ctx)
+                if ins.stage > 0:
+                    key = (PL_GRAD, ins.pipe, ins.stage, ins.mb)
+                    if sched.stage_rank(ins.pipe, ins.stage - 1) == self.mesh.pp_rank:
+                        local[key] = gx
+                    else:
+                        outbox[key] = gx
+                if last_bwd.get(ins.stage) == i:
+                    self.grad_sync.stage_done(ins.stage)
+            if self.debug_sync and dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+        if outbox or inbox or local:
+            raise RuntimeError(f"pipeline step left undelivered tensors: out={list(outbox)} "
+                               f"in={list(inbox)} local={list(local)}")
+        if self.transport is not None:
+            self.transport.drain_sends()
+        if train:
+            self.grad_sync.finish()
+            if step_optimizer:
+                self.optimizer.step()
+                self.global_step += 1
+        return StepResult(loss_sum, correct, count, time.perf_counter() - t0)
+
+    # ---------------------------------------------------------------------------------------
+    def reduce_metrics(self, res: StepResult, group=None) -> Tuple[float, int, int]:
+        """Sum (loss, correct, count) over all last-stage holders (world). Host-syncs."""
+        v = torch.stack([res.loss_sum.double(), res.correct.double(),
+                         torch.tensor(float(res.count), device=res.loss_sum.device, dtype=torch.float64)])
+        if self.mesh.world_size > 1:
+            # every pipeline's last stage contributes once; the other ranks contribute zeros
+            dist.all_reduce(v, group=group)
+        v = v.cpu()
+        return float(v[0]), int(v[1]), int(v[2])
+
+    def state_dicts(self) -> Dict[int, dict]:
+        return {s: {k: v.detach().cpu().clone() for k, v in m.state_dict().items()} for s, m in self.stages.items()}
+
+    def parameters_vector(self) -> torch.Tensor:
+        return self.flat.params.detach().clone()

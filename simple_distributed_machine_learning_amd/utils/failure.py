@@ -1,0 +1,94 @@
+"""Failure detection: peer heartbeats over the rendezvous store.
+
+The reference disables every timeout (``rpc_timeout=0`` / ``timeout=0``,
+/root/reference/simple_distributed.py:36, :167): a dead peer hangs the job forever
+(SURVEY.md §5). Here, besides finite process-group timeouts (parallel/mesh.py), each rank
+runs a tiny daemon thread that publishes ``hb/<rank> = <unix time>`` to the TCPStore and
+checks its peers; if a peer goes silent for ``timeout_s`` the rank reports it and exits
+non-zero instead of hanging in a collective.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import threading
+import time
+from typing import Callable, Optional, Sequence
+
+import torch.distributed as dist
+
+
+class Heartbeat:
+    def __init__(self, rank: int, peers: Sequence[int], interval_s: float = 2.0, timeout_s: float = 60.0,
+                 store=None, on_failure: Optional[Callable[[int, float], None]] = None):
+        self.rank, self.peers = rank, [p for p in peers if p != rank]
+        self.interval_s, self.timeout_s = interval_s, timeout_s
+        self.store = store if store is not None else _default_store()
+        self.on_failure = on_failure or _exit_on_failure
+        self._stop = threading.Event()
+        self._thread = None
+        self.failed_peer = None
+
+    def start(self):
+        if self.store is None:
+            return self
+        self._beat()
+        self._thread = threading.Thread(target=self._loop, name="sdml-heartbeat", daemon=True)
+        self._thread.start()
+        return self
+
+    def _beat(self):
+        self.store.set(f"hb/{self.rank}", repr(time.time()))
+
+    def _loop(self):
+        t_start = time.time()
+        while not self._stop.wait(self.interval_s):
+            try:
+                self._beat()
+                now = time.time()
+                for p in self.peers:
+                    key = f"hb/{p}"
+                    try:
+                        if not self.store.check([key]):
+                            if now - t_start > self.timeout_s:
+                                self._fail(p, now - t_start)
+                                return
+                            continue
+                        last = float(self.store.get(key).decode())
+                    except Exception:  # noqa: BLE001  store gone: master died
+                        self._fail(p, -1.0)
+                        return
+                    if now - last > self.timeout_s:
+                        self._fail(p, now - last)
+                        return
+            except Exception:  # noqa: BLE001
+                if self._stop.is_set():
+                    return
+                self._fail(-1, -1.0)
+                return
+
+    def _fail(self, peer: int, age: float):
+        if self._stop.is_set():
+            return
+        self.failed_peer = peer
+        self.on_failure(peer, age)
+
+    def stop(self):
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=self.interval_s * 2)
+
+
+def _default_store():
+    if not dist.is_initialized():
+        return None
+    try:
+        return dist.distributed_c10d._get_default_store()
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def _exit_on_failure(peer: int, age: float):
+    sys.stderr.write(f"[sdml] peer failure detected: rank {peer} silent for {age:.1f}s — aborting\n")
+    sys.stderr.flush()
+    os._exit(17)

@@ -1,0 +1,330 @@
+// fp32 GEMM on CDNA4 matrix cores: v_mfma_f32_32x32x2_f32 (exact f32: bitwise an fmaf chain).
+//
+// Used for every Linear of the MNIST MLPs (forward with fused bias+ReLU, dX with the ReLU
+// mask fused into the A-operand staging, dW split-K with atomic accumulation straight into
+// the flat gradient buffer and the bias gradient fused as a row-sum of the staged A tile).
+// These replace the ATen CPU GEMMs of the reference's fc layers
+// (/root/reference/simple_distributed.py:63-64, :75-77).
+//
+// Tiling (gfx950, wave64):
+//   block 256 threads = 4 waves in a 2x2 grid, block tile 128x128, K-step 32 floats;
+//   each wave owns a 64x64 output = 2x2 MFMA 32x32 accumulators (64 AGPR/VGPR floats).
+//   LDS: double-buffered A and B tiles (2 x 2 x 18 KiB = 72 KiB -> 2 blocks/CU).
+//   * K-contiguous operand tile is stored [row][32 + 4 pad] floats: one ds_read_b128 gives a
+//     lane 4 consecutive k of its row -> 4 MFMAs per read. The 144-B row pitch makes the
+//     16-lane groups of ds_read_b128 conflict-free (lanes l and l+16 never share a group).
+//   * K-major operand tile is stored [k][128] (straight copy of the global layout, no
+//     transpose in staging): fragments are ds_read_b32 of 32 consecutive floats (conflict-free).
+//   Both layouts use the same k permutation inside a k-group of 8: MFMA j of group s sums
+//   k = 8s+j (lanes 0-31) and 8s+4+j (lanes 32-63). Any permutation of the reduction is valid
+//   as long as A and B agree; the result is the same set of fmaf terms in a different order.
+//   Global->LDS staging is register-prefetched one K-step ahead (issue before the MFMAs,
+//   write after), so HBM latency hides under the matrix work.
+// MFMA C/D map (gfx950, dtype-independent): col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace sdml {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BM = 128, BN = 128, BK = 32, NTHR = 256;
+constexpr int KC_PITCH = BK + 4;            // K-contiguous tile row pitch (floats)
+constexpr int TILE_FLOATS = BM * KC_PITCH;  // >= BK*BM (K-major tile)
+static_assert(BK * BM <= TILE_FLOATS, "tile size");
+
+struct KParams {
+  const float* A;
+  const float* amask;
+  const float* B;
+  float* C;
+  const float* bias;
+  float* rowsum;
+  int M, N, K, lda, ldb, ldc;
+  int epi;
+  int a_vec, b_vec;  // 16-B vector loads legal for the operand
+  int kps;  // K elements per split (multiple of BK)
+  int tiles_m, tiles_n;
+};
+
+// ---- staging ---------------------------------------------------------------------------------
+// K-contiguous operand: tile rows [r0, r0+128), k [k0, k0+32): 1024 float4, 4 per thread.
+__device__ __forceinline__ void load_kc(const float* __restrict__ P, const float* __restrict__ mask, int ld,
+                                        int rows, int r0, int k0, int kend, bool vec, f32x4 (&v)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int idx = threadIdx.x + NTHR * i;
+    int r = idx >> 3, k4 = idx & 7;
+    int gr = r0 + r, gk = k0 + 4 * k4;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (!vec) {  // unaligned / K % 4 != 0: element loads (slow path, odd shapes only)
+      if (gr < rows) {
+        const float* src = P + (size_t)gr * ld;
+        const float* msk = mask ? mask + (size_t)gr * ld : nullptr;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (gk + e < kend) x[e] = (!msk || msk[gk + e] > 0.f) ? src[gk + e] : 0.f;
+      }
+    } else if (gr < rows && gk < kend) {
+      x = *reinterpret_cast<const f32x4*>(P + (size_t)gr * ld + gk);
+      if (mask) {
+        f32x4 mk = *reinterpret_cast<const f32x4*>(mask + (size_t)gr * ld + gk);
+        x[0] = mk[0] > 0.f ? x[0] : 0.f;
+        x[1] = mk[1] > 0.f ? x[1] : 0.f;
+        x[2] = mk[2] > 0.f ? x[2] : 0.f;
+        x[3] = mk[3] > 0.f ? x[3] : 0.f;
+      }
+    }
+    v[i] = x;
+  }
+}
+
+__device__ __forceinline__ void store_kc(float* __restrict__ T, const f32x4 (&v)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int idx = threadIdx.x + NTHR * i;
+    int r = idx >> 3, k4 = idx & 7;
+    *reinterpret_cast<f32x4*>(T + r * KC_PITCH + 4 * k4) = v[i];
+  }
+}
+
+// K-major operand: tile k [k0, k0+32), rows [r0, r0+128): 1024 float4 along rows.
+__device__ __forceinline__ void load_km(const float* __restrict__ P, const float* __restrict__ mask, int ld,
+                                        int rows, int r0, int k0, int kend, bool vec, f32x4 (&v)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int idx = threadIdx.x + NTHR * i;
+    int kk = idx >> 5, r4 = idx & 31;
+    int gk = k0 + kk, gr = r0 + 4 * r4;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (gk < kend) {
+      const float* src = P + (size_t)gk * ld + gr;
+      const float* msk = mask ? mask + (size_t)gk * ld + gr : nullptr;
+      if (vec && gr + 3 < rows) {
+        x = *reinterpret_cast<const f32x4*>(src);
+        if (msk) {
+          f32x4 mk = *reinterpret_cast<const f32x4*>(msk);
+          x[0] = mk[0] > 0.f ? x[0] : 0.f;
+          x[1] = mk[1] > 0.f ? x[1] : 0.f;
+          x[2] = mk[2] > 0.f ? x[2] : 0.f;
+          x[3] = mk[3] > 0.f ? x[3] : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (gr + e < rows) {
+            float a = src[e];
+            x[e] = (!msk || msk[e] > 0.f) ? a : 0.f;
+          }
+      }
+    }
+    v[i] = x;
+  }
+}
+
+__device__ __forceinline__ void store_km(float* __restrict__ T, const f32x4 (&v)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int idx = threadIdx.x + NTHR * i;
+    int kk = idx >> 5, r4 = idx & 31;
+    *reinterpret_cast<f32x4*>(T + kk * BM + 4 * r4) = v[i];
+  }
+}
+
+// fragment of a 32-row sub-tile for k-group s: f[j] = X(row, k = 8s + 4h + j)
+template <bool KM>
+__device__ __forceinline__ f32x4 frag(const float* __restrict__ T, int row, int s, int h) {
+  if constexpr (!KM) {
+    return *reinterpret_cast<const f32x4*>(T + row * KC_PITCH + 8 * s + 4 * h);
+  } else {
+    const float* p = T + (8 * s + 4 * h) * BM + row;
+    f32x4 f;
+    f[0] = p[0];
+    f[1] = p[BM];
+    f[2] = p[2 * BM];
+    f[3] = p[3 * BM];
+    return f;
+  }
+}
+
+template <bool A_KM, bool B_KM>
+__global__ void __launch_bounds__(NTHR, 2) gemm_f32_kernel(KParams p) {
+  __shared__ __attribute__((aligned(16))) float smem[4 * TILE_FLOATS];  // [buf][A|B]
+  // XCD-aware, bijective remap of the (m,n) tile index: consecutive tiles share operands,
+  // so give each XCD a contiguous chunk of the tile order (blocks b and b+8 share an XCD).
+  const int nwg = p.tiles_m * p.tiles_n;
+  int orig = blockIdx.x;
+  int wg = orig;
+  if (nwg >= 16) {
+    int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  }
+  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.z * p.kps;
+  const int kend = min(p.K, kbeg + p.kps);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int l32 = lane & 31, h = lane >> 5;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const bool do_rowsum = p.rowsum != nullptr && tn == 0;
+  float rs = 0.f;  // thread's partial row-sum of A (bias gradient)
+
+  f32x4 va[4], vb[4];
+  auto load = [&](int k0) {
+    if constexpr (A_KM) load_km(p.A, p.amask, p.lda, p.M, m0, k0, kend, p.a_vec, va);
+    else load_kc(p.A, p.amask, p.lda, p.M, m0, k0, kend, p.a_vec, va);
+    if constexpr (B_KM) load_km(p.B, nullptr, p.ldb, p.N, n0, k0, kend, p.b_vec, vb);
+    else load_kc(p.B, nullptr, p.ldb, p.N, n0, k0, kend, p.b_vec, vb);
+  };
+  auto store = [&](int buf) {
+    float* As = smem + (2 * buf) * TILE_FLOATS;
+    float* Bs = As + TILE_FLOATS;
+    if constexpr (A_KM) store_km(As, va);
+    else store_kc(As, va);
+    if constexpr (B_KM) store_km(Bs, vb);
+    else store_kc(Bs, vb);
+  };
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    load(kbeg);
+    store(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) load(kbeg + (t + 1) * BK);  // prefetch next tile into registers
+    const float* As = smem + (2 * cur) * TILE_FLOATS;
+    const float* Bs = As + TILE_FLOATS;
+    if (do_rowsum) {  // rows of the A tile (bias grad): thread -> row t%128, half of the k range
+      const int row = threadIdx.x & (BM - 1), half = threadIdx.x >> 7;
+#pragma unroll
+      for (int kk = 0; kk < BK / 2; ++kk) {
+        int k = half * (BK / 2) + kk;
+        rs += A_KM ? As[k * BM + row] : As[row * KC_PITCH + k];
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < BK / 8; ++s) {
+      f32x4 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = frag<A_KM>(As, wm * 64 + i * 32 + l32, s, h);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = frag<B_KM>(Bs, wn * 64 + j * 32 + l32, s, h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][e], fb[j][e], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (do_rowsum) {
+    const int row = threadIdx.x & (BM - 1);
+    if (m0 + row < p.M) atomicAdd(p.rowsum + m0 + row, rs);
+  }
+
+  // ---- epilogue ----
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 64 + j * 32 + l32;
+      if (col >= p.N) continue;
+      const float bv = (p.epi == EPI_BIAS || p.epi == EPI_BIAS_RELU) ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= p.M) continue;
+        float v = acc[i][j][r];
+        float* dst = p.C + (size_t)row * p.ldc + col;
+        switch (p.epi) {
+          case EPI_STORE: *dst = v; break;
+          case EPI_BIAS: *dst = v + bv; break;
+          case EPI_BIAS_RELU: *dst = fmaxf(v + bv, 0.f); break;
+          case EPI_ACCUM: *dst += v; break;
+          default: atomicAdd(dst, v); break;
+        }
+      }
+    }
+}
+
+}  // namespace
+
+static bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+
+// 16-B loads are legal when the base is aligned, the leading dimension keeps every row
+// aligned, and (for a k-contiguous operand) K is whole float4s
+static bool vec_ok(const float* P, const float* mask, int ld, bool kmajor, int K) {
+  if (!al16(P) || (mask && !al16(mask)) || ld % 4) return false;
+  return kmajor || K % 4 == 0;
+}
+
+bool gemm_f32_supported(const GemmArgs& g) {
+  if (g.M <= 0 || g.N <= 0 || g.K <= 0) return false;
+  if (g.splits > 1 && g.epi != EPI_ATOMIC) return false;
+  return true;
+}
+
+int gemm_f32_pick_splits(int M, int N, int K) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int splits = 1;
+  // aim for >= 2 blocks per CU (512) while keeping >= 8 K-steps per split
+  while (tiles * splits < 512 && K / (splits * 2) >= 8 * BK) splits *= 2;
+  return splits;
+}
+
+void gemm_f32(const GemmArgs& g, hipStream_t stream) {
+  KParams p;
+  p.A = g.A;
+  p.amask = g.amask;
+  p.B = g.B;
+  p.C = g.C;
+  p.bias = g.bias;
+  p.rowsum = g.rowsum;
+  p.M = g.M;
+  p.N = g.N;
+  p.K = g.K;
+  p.lda = g.lda;
+  p.ldb = g.ldb;
+  p.ldc = g.ldc;
+  p.epi = g.epi;
+  p.a_vec = vec_ok(g.A, g.amask, g.lda, g.a_kmajor, g.K);
+  p.b_vec = vec_ok(g.B, nullptr, g.ldb, g.b_kmajor, g.K);
+  int splits = g.splits < 1 ? 1 : g.splits;
+  int kps = (g.K + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = (g.K + kps - 1) / kps;
+  p.kps = kps;
+  p.tiles_m = (g.M + BM - 1) / BM;
+  p.tiles_n = (g.N + BN - 1) / BN;
+  dim3 grid(p.tiles_m * p.tiles_n, 1, splits);
+  dim3 block(NTHR);
+  if (!g.a_kmajor && !g.b_kmajor)
+    hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, block, 0, stream, p);
+  else if (!g.a_kmajor && g.b_kmajor)
+    hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, block, 0, stream, p);
+  else if (g.a_kmajor && !g.b_kmajor)
+    hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, block, 0, stream, p);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, block, 0, stream, p);
+}
+
+}  // namespace sdml

@@ -1,0 +1,267 @@
+// Fused classifier head: fc (K -> C) + log_softmax + NLL + the full backward, in ONE launch.
+//
+// For the 784-128-10 MLP this kernel IS the whole last pipeline stage (reference stage 1
+// does fc2 -> log_softmax on worker1 and nll_loss + backward on the master over RPC:
+// /root/reference/simple_distributed.py:77-79, :111-112). Per 64-row chunk:
+//   1. x chunk [64][128] -> LDS (float4, coalesced); W [C][128], b -> LDS once per block
+//   2. 4 threads per row: partial logits over 32 k each, 2-step xor-shuffle reduction
+//      -> log-sum-exp, NLL, argmax (correct), dz = scale * (softmax - onehot)
+//   3. dx[row][k] = sum_c dz_c W[c][k] written straight from registers (float4)
+//   4. dW partial (C x 128 outputs, 5 per thread for C=10) accumulated in registers across
+//      all chunks of the block, db in LDS; one atomicAdd per output per block at the end.
+// Memory-bound by design (0.5 KiB read + 0.5 KiB written per sample); all MACs on VALU.
+//
+// head_generic: any K (multiple of 4) / C <= 32: computes loss/dz/dx per row (one wave per
+// row); dW/db are then done by the MFMA GEMM (gemm_f32 with fused row-sum).
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace sdml {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int HK = 128;     // fused kernel: hidden width
+constexpr int CMAX = 16;    // fused kernel: max classes
+constexpr int ROWS = 64;    // rows per chunk
+constexpr int HTHR = 256;
+constexpr int XP = HK + 4;  // LDS row pitch of the x chunk
+
+template <int C>
+__global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                          const float* __restrict__ bias,
+                                                          const int64_t* __restrict__ target, int M, float scale,
+                                                          float* __restrict__ stats, float* __restrict__ dx,
+                                                          float* __restrict__ gW, float* __restrict__ gb,
+                                                          int chunks_per_block) {
+  __shared__ __attribute__((aligned(16))) float xs[ROWS * XP];
+  __shared__ __attribute__((aligned(16))) float ws[C * HK];
+  __shared__ float bs[CMAX];
+  __shared__ float dzs[ROWS * C];
+  __shared__ float red[2 * HTHR / 64];
+  const int t = threadIdx.x;
+  const bool train = dx != nullptr;
+  for (int i = t; i < C * HK / 4; i += HTHR)
+    reinterpret_cast<f32x4*>(ws)[i] = reinterpret_cast<const f32x4*>(W)[i];
+  if (t < C) bs[t] = bias[t];
+
+  constexpr int NOUT = (C * HK + HTHR - 1) / HTHR;  // dW outputs per thread
+  float gacc[NOUT];
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) gacc[o] = 0.f;
+  float gbacc = 0.f;
+  float loss_acc = 0.f, corr_acc = 0.f;
+
+  const int row_in = t >> 2, q = t & 3;  // 4 threads per row, 32 k each
+  for (int ch = 0; ch < chunks_per_block; ++ch) {
+    const int r0 = (blockIdx.x * chunks_per_block + ch) * ROWS;
+    if (r0 >= M) break;
+    __syncthreads();  // previous chunk fully consumed (and ws/bs visible on first pass)
+    // stage x chunk
+#pragma unroll
+    for (int i = 0; i < ROWS * HK / 4 / HTHR; ++i) {
+      int idx = t + HTHR * i;
+      int r = idx >> 5, k4 = idx & 31;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (r0 + r < M) v = *reinterpret_cast<const f32x4*>(x + (size_t)(r0 + r) * HK + 4 * k4);
+      *reinterpret_cast<f32x4*>(xs + r * XP + 4 * k4) = v;
+    }
+    __syncthreads();
+    const int grow = r0 + row_in;
+    const bool valid = grow < M;
+    float z[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) z[c] = 0.f;
+    // thread q covers k = 4*(q + 4*j) .. +3, j = 0..7 (interleaved -> conflict-light LDS reads)
+#pragma unroll
+    for (int j = 0; j < HK / 16; ++j) {
+      const int k = 4 * (q + 4 * j);
+      f32x4 xv = *reinterpret_cast<const f32x4*>(xs + row_in * XP + k);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        f32x4 wv = *reinterpret_cast<const f32x4*>(ws + c * HK + k);
+        z[c] += xv[0] * wv[0] + xv[1] * wv[1] + xv[2] * wv[2] + xv[3] * wv[3];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      z[c] += __shfl_xor(z[c], 1);
+      z[c] += __shfl_xor(z[c], 2);
+      z[c] += bs[c];
+    }
+    float mx = z[0];
+    int am = 0;
+#pragma unroll
+    for (int c = 1; c < C; ++c)
+      if (z[c] > mx) {
+        mx = z[c];
+        am = c;
+      }
+    float se = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) se += __expf(z[c] - mx);
+    const float lse = mx + __logf(se);
+    const int tg = valid ? (int)target[grow] : 0;
+    if (valid && q == 0) {
+      float zt = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) zt = (c == tg) ? z[c] : zt;
+      loss_acc += lse - zt;
+      corr_acc += (am == tg) ? 1.f : 0.f;
+    }
+    if (train) {
+      float dz[C];
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float pr = __expf(z[c] - lse);
+        dz[c] = valid ? scale * (pr - (c == tg ? 1.f : 0.f)) : 0.f;
+      }
+      if (q == 0) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) dzs[row_in * C + c] = dz[c];
+      }
+      if (valid) {
+#pragma unroll
+        for (int j = 0; j < HK / 16; ++j) {
+          const int k = 4 * (q + 4 * j);
+          f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < C; ++c) {
+            f32x4 wv = *reinterpret_cast<const f32x4*>(ws + c * HK + k);
+            o += dz[c] * wv;
+          }
+          *reinterpret_cast<f32x4*>(dx + (size_t)grow * HK + k) = o;
+        }
+      }
+      __syncthreads();  // dzs complete
+      // dW partial: output o = t + HTHR*u -> (c = o / HK, k = o % HK), sum over chunk rows
+#pragma unroll
+      for (int u = 0; u < NOUT; ++u) {
+        const int o = t + HTHR * u;
+        if (o < C * HK) {
+          const int c = o / HK, k = o % HK;
+          float s = 0.f;
+#pragma unroll 8
+          for (int r = 0; r < ROWS; ++r) s += dzs[r * C + c] * xs[r * XP + k];
+          gacc[u] += s;
+        }
+      }
+      if (t < C) {
+        float s = 0.f;
+        for (int r = 0; r < ROWS; ++r) s += dzs[r * C + t];
+        gbacc += s;
+      }
+    }
+  }
+  // ---- block reductions / global accumulation ----
+  if (train) {
+#pragma unroll
+    for (int u = 0; u < NOUT; ++u) {
+      const int o = t + HTHR * u;
+      if (o < C * HK) atomicAdd(gW + o, gacc[u]);
+    }
+    if (t < C) atomicAdd(gb + t, gbacc);
+  }
+  // loss/correct: wave reduce then one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) {
+    loss_acc += __shfl_xor(loss_acc, off);
+    corr_acc += __shfl_xor(corr_acc, off);
+  }
+  if ((t & 63) == 0) {
+    atomicAdd(stats, loss_acc);
+    atomicAdd(stats + 1, corr_acc);
+  }
+}
+
+// one wave per row, any K (%4 == 0), C <= 32: loss/correct, dz (to dz_out) and dx
+__global__ void __launch_bounds__(256) head_generic_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                           const float* __restrict__ bias,
+                                                           const int64_t* __restrict__ target, int M, int K, int C,
+                                                           float scale, float* __restrict__ stats,
+                                                           float* __restrict__ dx, float* __restrict__ dz_out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + (size_t)row * K;
+  float z[32];
+  for (int c = 0; c < 32; ++c) z[c] = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    float xv = xr[k];
+    for (int c = 0; c < C; ++c) z[c] += xv * W[(size_t)c * K + k];
+  }
+  for (int c = 0; c < C; ++c) {
+    float v = z[c];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    z[c] = v + bias[c];
+  }
+  float mx = z[0];
+  int am = 0;
+  for (int c = 1; c < C; ++c)
+    if (z[c] > mx) {
+      mx = z[c];
+      am = c;
+    }
+  float se = 0.f;
+  for (int c = 0; c < C; ++c) se += __expf(z[c] - mx);
+  const float lse = mx + __logf(se);
+  const int tg = (int)target[row];
+  if (lane == 0) {
+    float zt = 0.f;
+    for (int c = 0; c < C; ++c) zt = (c == tg) ? z[c] : zt;
+    atomicAdd(stats, lse - zt);
+    atomicAdd(stats + 1, am == tg ? 1.f : 0.f);
+  }
+  if (dx || dz_out) {
+    float dz[32];
+    for (int c = 0; c < C; ++c) dz[c] = scale * (__expf(z[c] - lse) - (c == tg ? 1.f : 0.f));
+    if (dz_out && lane < C) {
+      float v = 0.f;
+      for (int c = 0; c < C; ++c) v = (c == lane) ? dz[c] : v;
+      dz_out[(size_t)row * C + lane] = v;
+    }
+    if (dx)
+      for (int k = lane; k < K; k += 64) {
+        float o = 0.f;
+        for (int c = 0; c < C; ++c) o += dz[c] * W[(size_t)c * K + k];
+        dx[(size_t)row * K + k] = o;
+      }
+  }
+}
+
+}  // namespace
+
+bool head_fused_supported(int K, int C) { return K == HK && (C == 10 || C == 2 || C == 16); }
+
+void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K, int C,
+                         float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
+                         hipStream_t stream) {
+  if (M <= 0) return;
+  if (head_fused_supported(K, C) && dz_out == nullptr) {
+    const int chunks = (M + ROWS - 1) / ROWS;
+    // enough blocks to fill the chip, but each keeps its dW partial in registers over
+    // several chunks so the final atomics stay small (C*K per block)
+    int blocks = chunks < 512 ? chunks : 512;
+    int cpb = (chunks + blocks - 1) / blocks;
+    blocks = (chunks + cpb - 1) / cpb;
+    switch (C) {
+      case 10:
+        hipLaunchKernelGGL((head_fused_kernel<10>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
+                           stats, dx, gW, gb, cpb);
+        break;
+      case 2:
+        hipLaunchKernelGGL((head_fused_kernel<2>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
+                           stats, dx, gW, gb, cpb);
+        break;
+      default:
+        hipLaunchKernelGGL((head_fused_kernel<16>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
+                           stats, dx, gW, gb, cpb);
+        break;
+    }
+    return;
+  }
+  hipLaunchKernelGGL(head_generic_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, x, W, b, target, M, K, C, scale,
+                     stats, dx, dz_out);
+}
+
+}  // namespace sdml

@@ -1,0 +1,61 @@
+// Host-side launch API of the gfx950 HIP kernels (no torch headers here: kernel TUs compile fast).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace sdml {
+
+// ---- fp32 MFMA GEMM ------------------------------------------------------------------------
+// C[M,N] (op)= sum_k A(m,k) * B(n,k)
+//   A(m,k) = A[m*lda + k]        (a_kmajor = false)   or A[k*lda + m]   (a_kmajor = true)
+//   B(n,k) = B[n*ldb + k]        (b_kmajor = false)   or B[k*ldb + n]   (b_kmajor = true)
+//   if amask: A(m,k) *= (amask(m,k) > 0)   (same layout/ld as A) — fused ReLU backward
+// Epilogues: see GemmEpi. Split-K over grid.z requires EPI_ATOMIC.
+enum GemmEpi : int {
+  EPI_STORE = 0,          // C = acc
+  EPI_BIAS = 1,           // C = acc + bias[n]
+  EPI_BIAS_RELU = 2,      // C = relu(acc + bias[n])
+  EPI_ACCUM = 3,          // C += acc
+  EPI_ATOMIC = 4,         // atomicAdd(C, acc)           (split-K capable)
+};
+
+struct GemmArgs {
+  const float* A = nullptr;
+  const float* amask = nullptr;
+  const float* B = nullptr;
+  float* C = nullptr;
+  const float* bias = nullptr;
+  float* rowsum = nullptr;  // if set: rowsum[m] += sum_k A(m,k)  (atomic)   — fused bias-grad
+  int M = 0, N = 0, K = 0;
+  int lda = 0, ldb = 0, ldc = 0;
+  bool a_kmajor = false, b_kmajor = false;
+  int epi = EPI_STORE;
+  int splits = 1;  // split-K factor (EPI_ATOMIC only)
+};
+
+// returns false if the shape/alignment is not supported by the MFMA path
+bool gemm_f32_supported(const GemmArgs& g);
+void gemm_f32(const GemmArgs& g, hipStream_t stream);
+int gemm_f32_pick_splits(int M, int N, int K);
+
+// ---- fused classifier head: z = x W^T + b; log_softmax; NLL; backward --------------------
+// x [M,K] fp32, W [C,K], b [C], target [M] int64. stats[0] += sum loss, stats[1] += #correct.
+// If dx != nullptr: dx = scale * (softmax - onehot) @ W ; gW += dz^T x ; gb += sum dz.
+// K must be 128 for the fully fused kernel (the 784-128-10 model); head_generic handles others
+// (and writes dz for a follow-up GEMM).
+bool head_fused_supported(int K, int C);
+void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K,
+                         int C, float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
+                         hipStream_t stream);
+
+// ---- SGD with momentum over a flat buffer ------------------------------------------------
+void sgd_momentum(float* p, const float* g, float* buf, int64_t n, float lr, float momentum, float dampening,
+                  float wd, bool nesterov, bool first, hipStream_t stream);
+
+// ---- synthetic MNIST-shape data (counter-based; bit-identical to the host generator) -----
+void synth_mnist(uint64_t seed, int64_t start, int64_t n, int H, int W, int mode, float* x, int64_t* y,
+                 hipStream_t stream);
+
+}  // namespace sdml

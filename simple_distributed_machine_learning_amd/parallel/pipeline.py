@@ -248,7 +248,7 @@ class PipelineEngine:
                         tgt = tgt.to(dev, non_blocking=True)
                     l, c, n = mod.head_fwd(x, tgt, ctx, train, scale)
                     loss_sum += l.float()
-                    correct += c
+                    correct += c.to(torch.int64)
                     count += n
                 else:
                     y = mod.fwd(x, ctx, train)

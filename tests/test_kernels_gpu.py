@@ -1,0 +1,129 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference (GPU only)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no ROCm GPU", allow_module_level=True)
+
+from simple_distributed_machine_learning_amd import _native, ops  # noqa: E402
+from simple_distributed_machine_learning_amd.ops import reference as ref  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+K = _native.kernels()
+
+
+def rnd(*shape, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.empty(shape).uniform_(-1, 1, generator=g).to(DEV)
+
+
+def close(a, b, rtol=2e-5, atol=2e-5):
+    torch.testing.assert_close(a, b, rtol=rtol, atol=atol)
+
+
+def test_mfma_layout_identity_asymmetric():
+    # A = I, asymmetric B: catches a transposed C/D map (guide §3)
+    n = 128
+    A = torch.eye(n, device=DEV)
+    B = torch.arange(n * n, device=DEV, dtype=torch.float32).reshape(n, n) / (n * n)
+    C = torch.empty(n, n, device=DEV)
+    K.gemm_f32(A, B, C, False, False, 0)  # C = A @ B^T  (B given as [N,K])
+    close(C, B.t().contiguous(), rtol=0, atol=0)
+    K.gemm_f32(B, A, C, False, False, 0)
+    close(C, B, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("a_km,b_km", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,Kd", [(128, 128, 128), (60, 128, 784), (300, 50, 320), (1, 10, 4), (257, 129, 100)])
+def test_gemm_layouts(a_km, b_km, M, N, Kd):
+    A = rnd(M, Kd, seed=1)
+    B = rnd(N, Kd, seed=2)
+    A_in = A.t().contiguous() if a_km else A
+    B_in = B.t().contiguous() if b_km else B
+    C = torch.empty(M, N, device=DEV)
+    K.gemm_f32(A_in, B_in, C, a_km, b_km, 0)
+    close(C, A @ B.t(), rtol=1e-5, atol=1e-4)
+
+
+def test_gemm_epilogues_and_splitk():
+    M, N, Kd = 200, 130, 1000
+    A, B, bias = rnd(M, Kd, seed=3), rnd(N, Kd, seed=4), rnd(N, seed=5)
+    C = torch.empty(M, N, device=DEV)
+    K.gemm_f32(A, B, C, False, False, 2, 1, bias)
+    close(C, torch.relu(A @ B.t() + bias), atol=1e-4, rtol=1e-5)
+    K.gemm_f32(A, B, C, False, False, 1, 1, bias)
+    close(C, A @ B.t() + bias, atol=1e-4, rtol=1e-5)
+    C0 = rnd(M, N, seed=6)
+    C = C0.clone()
+    K.gemm_f32(A, B, C, False, False, 3)
+    close(C, C0 + A @ B.t(), atol=1e-4, rtol=1e-5)
+    for splits in (1, 3, 8):
+        C = C0.clone()
+        rs = torch.zeros(M, device=DEV)
+        K.gemm_f32(A, B, C, False, False, 4, splits, None, rs)
+        close(C, C0 + A @ B.t(), atol=2e-4, rtol=1e-5)
+        close(rs, A.sum(1), atol=2e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("M", [60, 1000, 4096])
+@pytest.mark.parametrize("N,Kd", [(128, 784), (1024, 1024), (50, 320)])
+def test_linear_relu_fwd_bwd(M, N, Kd):
+    x, w, b = rnd(M, Kd, seed=7), rnd(N, Kd, seed=8) * 0.05, rnd(N, seed=9) * 0.1
+    y = ops.linear_relu_fwd(x, w, b)
+    yr = ref.linear_relu_fwd(x, w, b)
+    close(y, yr, atol=1e-4, rtol=1e-5)
+    gy = rnd(M, N, seed=10)
+    gw, gb = rnd(N, Kd, seed=11), rnd(N, seed=12)
+    gw_r, gb_r = gw.clone(), gb.clone()
+    dx = ops.linear_relu_bwd(x, yr, gy, w, gw, gb, True)
+    dx_r = ref.linear_relu_bwd(x, yr, gy, w, gw_r, gb_r, True)
+    close(dx, dx_r, atol=2e-4, rtol=1e-5)
+    close(gw, gw_r, atol=5e-4 * max(1, M / 1000), rtol=1e-5)
+    close(gb, gb_r, atol=5e-4 * max(1, M / 1000), rtol=1e-5)
+
+
+@pytest.mark.parametrize("M", [1, 60, 64, 1000, 70001])
+@pytest.mark.parametrize("Kd,C", [(128, 10), (1024, 10), (50, 10), (128, 3)])
+def test_head_logsoftmax_nll(M, Kd, C):
+    x, w, b = rnd(M, Kd, seed=13), rnd(C, Kd, seed=14) * 0.1, rnd(C, seed=15)
+    t = torch.randint(0, C, (M,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(0))
+    scale = 1.0 / M
+    gw, gb = torch.zeros(C, Kd, device=DEV), torch.zeros(C, device=DEV)
+    gw_r, gb_r = gw.clone(), gb.clone()
+    loss, correct, dx = ops.linear_logsoftmax_nll(x, w, b, t, gw, gb, scale, True)
+    loss_r, correct_r, dx_r = ref.linear_logsoftmax_nll(x, w, b, t, gw_r, gb_r, scale, True)
+    close(loss, loss_r, rtol=2e-5, atol=1e-3)
+    assert int(correct) == int(correct_r)
+    close(dx, dx_r, atol=2e-6, rtol=1e-4)
+    close(gw, gw_r, atol=2e-5, rtol=1e-4)
+    close(gb, gb_r, atol=2e-5, rtol=1e-4)
+    # eval mode: no grads
+    loss_e, correct_e, dx_e = ops.linear_logsoftmax_nll(x, w, b, t, None, None, 1.0, False)
+    assert dx_e is None
+    close(loss_e, loss_r, rtol=2e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("first", [True, False])
+@pytest.mark.parametrize("wd,damp,nest", [(0.0, 0.0, False), (1e-4, 0.1, False), (0.0, 0.0, True)])
+def test_sgd_momentum(first, wd, damp, nest):
+    n = 4096 + 64
+    p, g, buf = rnd(n, seed=16), rnd(n, seed=17), rnd(n, seed=18)
+    p_r, buf_r = p.clone(), buf.clone()
+    if nest:
+        damp = 0.0
+    ops.sgd_momentum_(p, g, buf, 0.1, 0.5, damp, wd, nest, first)
+    ref.sgd_momentum_(p_r, g, buf_r, 0.1, 0.5, damp, wd, nest, first)
+    close(p, p_r, atol=1e-6, rtol=1e-6)
+    close(buf, buf_r, atol=1e-6, rtol=1e-6)
+
+
+def test_synth_device_matches_host():
+    from simple_distributed_machine_learning_amd.data import SyntheticMNIST
+
+    for mode in ("learnable", "random"):
+        a = SyntheticMNIST(777, seed=5, device=DEV, mode=mode, offset=123)
+        b = SyntheticMNIST(777, seed=5, device="cpu", mode=mode, offset=123)
+        assert torch.equal(a.y.cpu(), b.y)
+        assert torch.equal(a.x.cpu(), b.x), (a.x.cpu() - b.x).abs().max()

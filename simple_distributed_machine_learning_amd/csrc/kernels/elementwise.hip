@@ -14,13 +14,14 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // /root/reference/simple_distributed.py:100-104): d = g + wd*p; buf = first ? d :
 // momentum*buf + (1-dampening)*d; d = nesterov ? d + momentum*buf : buf; p -= lr*d.
 // One launch for all parameters of all stages a rank owns; 16 B per lane per stream.
-__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ g,
                                                   float* __restrict__ buf, int64_t n4, float lr, float mom,
-                                                  float damp, float wd, int nesterov, int first) {
+                                                  float damp, float wd, int nesterov, int first, int zero_grad) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
     f32x4 d = reinterpret_cast<const f32x4*>(g)[i];
+    if (zero_grad) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (wd != 0.f) d += wd * pv;
     if (mom != 0.f) {
       f32x4 b;
@@ -53,15 +54,15 @@ __global__ void __launch_bounds__(256) synth_kernel(uint64_t seed, int64_t start
 
 }  // namespace
 
-void sgd_momentum(float* p, const float* g, float* buf, int64_t n, float lr, float momentum, float dampening,
-                  float wd, bool nesterov, bool first, hipStream_t stream) {
+void sgd_momentum(float* p, float* g, float* buf, int64_t n, float lr, float momentum, float dampening,
+                  float wd, bool nesterov, bool first, bool zero_grad, hipStream_t stream) {
   // flat buffers are padded to 64 elements, so n is a multiple of 4
   const int64_t n4 = n / 4;
   int64_t blocks = (n4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, g, buf, n4, lr, momentum, dampening,
-                     wd, nesterov ? 1 : 0, first ? 1 : 0);
+                     wd, nesterov ? 1 : 0, first ? 1 : 0, zero_grad ? 1 : 0);
 }
 
 void synth_mnist(uint64_t seed, int64_t start, int64_t n, int H, int W, int mode, float* x, int64_t* y,

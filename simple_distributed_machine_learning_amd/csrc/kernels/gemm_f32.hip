@@ -286,8 +286,9 @@ bool gemm_f32_supported(const GemmArgs& g) {
 int gemm_f32_pick_splits(int M, int N, int K) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   int splits = 1;
-  // aim for >= 2 blocks per CU (512) while keeping >= 8 K-steps per split
-  while (tiles * splits < 512 && K / (splits * 2) >= 8 * BK) splits *= 2;
+  // fill the chip (<= 2 blocks/CU) but keep >= 32 K-steps per split: every split adds its
+  // whole C tile with fp32 atomics (~1.3 TB/s chip-wide), so splits cost output bandwidth
+  while (tiles * splits * 2 <= 512 && K / (splits * 2) >= 32 * BK) splits *= 2;
   return splits;
 }
 

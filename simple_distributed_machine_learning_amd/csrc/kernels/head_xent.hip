@@ -8,7 +8,8 @@
 //      -> log-sum-exp, NLL, argmax (correct), dz = scale * (softmax - onehot)
 //   3. dx[row][k] = sum_c dz_c W[c][k] written straight from registers (float4)
 //   4. dW partial (C x 128 outputs, 5 per thread for C=10) accumulated in registers across
-//      all chunks of the block, db in LDS; one atomicAdd per output per block at the end.
+//      all chunks of the block; each block writes one partial slab (dW, db, loss, correct)
+//      and a second tiny pass sums the slabs in block order (deterministic, no contention).
 // Memory-bound by design (0.5 KiB read + 0.5 KiB written per sample); all MACs on VALU.
 //
 // head_generic: any K (multiple of 4) / C <= 32: computes loss/dz/dx per row (one wave per
@@ -32,8 +33,7 @@ template <int C>
 __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restrict__ x, const float* __restrict__ W,
                                                           const float* __restrict__ bias,
                                                           const int64_t* __restrict__ target, int M, float scale,
-                                                          float* __restrict__ stats, float* __restrict__ dx,
-                                                          float* __restrict__ gW, float* __restrict__ gb,
+                                                          float* __restrict__ part, float* __restrict__ dx,
                                                           int chunks_per_block) {
   __shared__ __attribute__((aligned(16))) float xs[ROWS * XP];
   __shared__ __attribute__((aligned(16))) float ws[C * HK];
@@ -154,78 +154,139 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
       }
     }
   }
-  // ---- block reductions / global accumulation ----
+  // ---- block partials -> slab (no cross-block atomics: 512 blocks adding into the same
+  // 1.3K addresses serialises at the memory side; a slab + one reduce pass does not) ----
+  float* slab = part + (size_t)blockIdx.x * (C * HK + C + 2);
   if (train) {
 #pragma unroll
     for (int u = 0; u < NOUT; ++u) {
       const int o = t + HTHR * u;
-      if (o < C * HK) atomicAdd(gW + o, gacc[u]);
+      if (o < C * HK) slab[o] = gacc[u];
     }
-    if (t < C) atomicAdd(gb + t, gbacc);
+    if (t < C) slab[C * HK + t] = gbacc;
   }
-  // loss/correct: wave reduce then one atomic per wave
   for (int off = 32; off > 0; off >>= 1) {
     loss_acc += __shfl_xor(loss_acc, off);
     corr_acc += __shfl_xor(corr_acc, off);
   }
   if ((t & 63) == 0) {
-    atomicAdd(stats, loss_acc);
-    atomicAdd(stats + 1, corr_acc);
+    red[2 * (t >> 6)] = loss_acc;
+    red[2 * (t >> 6) + 1] = corr_acc;
+  }
+  __syncthreads();
+  if (t == 0) {
+    float l = 0.f, c = 0.f;
+    for (int w = 0; w < HTHR / 64; ++w) {
+      l += red[2 * w];
+      c += red[2 * w + 1];
+    }
+    slab[C * HK + C] = l;
+    slab[C * HK + C + 1] = c;
   }
 }
 
-// one wave per row, any K (%4 == 0), C <= 32: loss/correct, dz (to dz_out) and dx
+// sum the per-block slabs: out[o] += sum_b part[b][o]   (fixed order -> deterministic).
+// Block = 64 outputs x 16 waves; wave w sums slabs b = w, w+16, ... with 8 loads in flight,
+// then the 16 wave partials are added in LDS in wave order.
+__global__ void __launch_bounds__(1024) head_reduce_kernel(const float* __restrict__ part, int nblocks, int CK, int C,
+                                                           float* __restrict__ gW, float* __restrict__ gb,
+                                                           float* __restrict__ stats, int train) {
+  __shared__ float acc[16][64];
+  const int width = CK + C + 2;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int o = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (o < width) {
+    float v[8];
+    int b = w;
+    for (; b + 16 * 7 < nblocks; b += 16 * 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(b + 16 * u) * width + o];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < nblocks; b += 16) s += part[(size_t)b * width + o];
+  }
+  acc[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && o < width) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += acc[i][lane];
+    if (o < CK) {
+      if (train) gW[o] += t;
+    } else if (o < CK + C) {
+      if (train) gb[o - CK] += t;
+    } else {
+      stats[o - CK - C] += t;
+    }
+  }
+}
+
+// grid-stride, one wave per row at a time, any K / C <= 32: loss/correct, dz (to dz_out) and
+// dx. Loss/correct stay in registers per wave and leave as one atomic pair per block.
 __global__ void __launch_bounds__(256) head_generic_kernel(const float* __restrict__ x, const float* __restrict__ W,
                                                            const float* __restrict__ bias,
                                                            const int64_t* __restrict__ target, int M, int K, int C,
                                                            float scale, float* __restrict__ stats,
                                                            float* __restrict__ dx, float* __restrict__ dz_out) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  const float* xr = x + (size_t)row * K;
-  float z[32];
-  for (int c = 0; c < 32; ++c) z[c] = 0.f;
-  for (int k = lane; k < K; k += 64) {
-    float xv = xr[k];
-    for (int c = 0; c < C; ++c) z[c] += xv * W[(size_t)c * K + k];
-  }
-  for (int c = 0; c < C; ++c) {
-    float v = z[c];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    z[c] = v + bias[c];
-  }
-  float mx = z[0];
-  int am = 0;
-  for (int c = 1; c < C; ++c)
-    if (z[c] > mx) {
-      mx = z[c];
-      am = c;
+  __shared__ float red[8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float loss_acc = 0.f, corr_acc = 0.f;
+  for (int row = blockIdx.x * 4 + wave; row < M; row += gridDim.x * 4) {
+    const float* xr = x + (size_t)row * K;
+    float z[32];
+    for (int c = 0; c < 32; ++c) z[c] = 0.f;
+    for (int k = lane; k < K; k += 64) {
+      float xv = xr[k];
+      for (int c = 0; c < C; ++c) z[c] += xv * W[(size_t)c * K + k];
     }
-  float se = 0.f;
-  for (int c = 0; c < C; ++c) se += __expf(z[c] - mx);
-  const float lse = mx + __logf(se);
-  const int tg = (int)target[row];
-  if (lane == 0) {
+    for (int c = 0; c < C; ++c) {
+      float v = z[c];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      z[c] = v + bias[c];
+    }
+    float mx = z[0];
+    int am = 0;
+    for (int c = 1; c < C; ++c)
+      if (z[c] > mx) {
+        mx = z[c];
+        am = c;
+      }
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += __expf(z[c] - mx);
+    const float lse = mx + __logf(se);
+    const int tg = (int)target[row];
     float zt = 0.f;
     for (int c = 0; c < C; ++c) zt = (c == tg) ? z[c] : zt;
-    atomicAdd(stats, lse - zt);
-    atomicAdd(stats + 1, am == tg ? 1.f : 0.f);
-  }
-  if (dx || dz_out) {
-    float dz[32];
-    for (int c = 0; c < C; ++c) dz[c] = scale * (__expf(z[c] - lse) - (c == tg ? 1.f : 0.f));
-    if (dz_out && lane < C) {
-      float v = 0.f;
-      for (int c = 0; c < C; ++c) v = (c == lane) ? dz[c] : v;
-      dz_out[(size_t)row * C + lane] = v;
-    }
-    if (dx)
-      for (int k = lane; k < K; k += 64) {
-        float o = 0.f;
-        for (int c = 0; c < C; ++c) o += dz[c] * W[(size_t)c * K + k];
-        dx[(size_t)row * K + k] = o;
+    loss_acc += lse - zt;
+    corr_acc += am == tg ? 1.f : 0.f;
+    if (dx || dz_out) {
+      float dz[32];
+      for (int c = 0; c < C; ++c) dz[c] = scale * (__expf(z[c] - lse) - (c == tg ? 1.f : 0.f));
+      if (dz_out && lane < C) {
+        float v = 0.f;
+        for (int c = 0; c < C; ++c) v = (c == lane) ? dz[c] : v;
+        dz_out[(size_t)row * C + lane] = v;
       }
+      if (dx)
+        for (int k = lane; k < K; k += 64) {
+          float o = 0.f;
+          for (int c = 0; c < C; ++c) o += dz[c] * W[(size_t)c * K + k];
+          dx[(size_t)row * K + k] = o;
+        }
+    }
+  }
+  if (lane == 0) {
+    red[2 * wave] = loss_acc;
+    red[2 * wave + 1] = corr_acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float l = red[0] + red[2] + red[4] + red[6];
+    float c = red[1] + red[3] + red[5] + red[7];
+    atomicAdd(stats, l);
+    atomicAdd(stats + 1, c);
   }
 }
 
@@ -233,35 +294,52 @@ __global__ void __launch_bounds__(256) head_generic_kernel(const float* __restri
 
 bool head_fused_supported(int K, int C) { return K == HK && (C == 10 || C == 2 || C == 16); }
 
+// grid of the fused kernel: enough blocks to fill the chip, each keeping its dW partial in
+// registers over several 64-row chunks (fewer slabs to reduce)
+int head_fused_blocks(int M, int* chunks_per_block) {
+  const int chunks = (M + ROWS - 1) / ROWS;
+  int blocks = chunks < 512 ? chunks : 512;
+  int cpb = (chunks + blocks - 1) / blocks;
+  blocks = (chunks + cpb - 1) / cpb;
+  *chunks_per_block = cpb;
+  return blocks;
+}
+
+size_t head_workspace_floats(int M, int K, int C) {
+  if (!head_fused_supported(K, C)) return 0;
+  int cpb;
+  return (size_t)head_fused_blocks(M, &cpb) * (C * K + C + 2);
+}
+
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K, int C,
                          float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
-                         hipStream_t stream) {
+                         float* workspace, hipStream_t stream) {
   if (M <= 0) return;
-  if (head_fused_supported(K, C) && dz_out == nullptr) {
-    const int chunks = (M + ROWS - 1) / ROWS;
-    // enough blocks to fill the chip, but each keeps its dW partial in registers over
-    // several chunks so the final atomics stay small (C*K per block)
-    int blocks = chunks < 512 ? chunks : 512;
-    int cpb = (chunks + blocks - 1) / blocks;
-    blocks = (chunks + cpb - 1) / cpb;
+  if (head_fused_supported(K, C) && dz_out == nullptr && workspace != nullptr) {
+    int cpb = 0, blocks = head_fused_blocks(M, &cpb);
     switch (C) {
       case 10:
         hipLaunchKernelGGL((head_fused_kernel<10>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
-                           stats, dx, gW, gb, cpb);
+                           workspace, dx, cpb);
         break;
       case 2:
         hipLaunchKernelGGL((head_fused_kernel<2>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
-                           stats, dx, gW, gb, cpb);
+                           workspace, dx, cpb);
         break;
       default:
         hipLaunchKernelGGL((head_fused_kernel<16>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
-                           stats, dx, gW, gb, cpb);
+                           workspace, dx, cpb);
         break;
     }
+    const int width = C * K + C + 2;
+    hipLaunchKernelGGL(head_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, stream, workspace, blocks, C * K,
+                       C, gW, gb, stats, dx != nullptr ? 1 : 0);
     return;
   }
-  hipLaunchKernelGGL(head_generic_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, x, W, b, target, M, K, C, scale,
-                     stats, dx, dz_out);
+  int gblocks = (M + 3) / 4;
+  if (gblocks > 1024) gblocks = 1024;
+  hipLaunchKernelGGL(head_generic_kernel, dim3(gblocks), dim3(256), 0, stream, x, W, b, target, M, K, C, scale, stats,
+                     dx, dz_out);
 }
 
 }  // namespace sdml

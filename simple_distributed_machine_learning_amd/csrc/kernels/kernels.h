@@ -45,14 +45,18 @@ int gemm_f32_pick_splits(int M, int N, int K);
 // If dx != nullptr: dx = scale * (softmax - onehot) @ W ; gW += dz^T x ; gb += sum dz.
 // K must be 128 for the fully fused kernel (the 784-128-10 model); head_generic handles others
 // (and writes dz for a follow-up GEMM).
+// The fused path needs a workspace of head_workspace_floats(M, K, C) floats (per-block
+// partial slabs, reduced by a second deterministic pass).
 bool head_fused_supported(int K, int C);
+size_t head_workspace_floats(int M, int K, int C);
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K,
                          int C, float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
-                         hipStream_t stream);
+                         float* workspace, hipStream_t stream);
 
 // ---- SGD with momentum over a flat buffer ------------------------------------------------
-void sgd_momentum(float* p, const float* g, float* buf, int64_t n, float lr, float momentum, float dampening,
-                  float wd, bool nesterov, bool first, hipStream_t stream);
+// zero_grad: also writes g = 0 after reading it (fuses the next step's zero_grad)
+void sgd_momentum(float* p, float* g, float* buf, int64_t n, float lr, float momentum, float dampening,
+                  float wd, bool nesterov, bool first, bool zero_grad, hipStream_t stream);
 
 // ---- synthetic MNIST-shape data (counter-based; bit-identical to the host generator) -----
 void synth_mnist(uint64_t seed, int64_t start, int64_t n, int H, int W, int mode, float* x, int64_t* y,

@@ -167,10 +167,11 @@ void gemm_f32_op(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool a_kmajo
   sdml::gemm_f32(g, cur_stream());
 }
 
-// fused head; returns (stats[2] = {loss_sum, correct}, dx or None)
+// fused head; returns (stats[2] = {loss_sum, correct}, dx or None). If `stats_acc` is given
+// the kernel accumulates into it (and returns it) instead of allocating a new one.
 std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
     torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor target, c10::optional<torch::Tensor> gw,
-    c10::optional<torch::Tensor> gb, double scale, bool need_dx) {
+    c10::optional<torch::Tensor> gb, double scale, bool need_dx, c10::optional<torch::Tensor> stats_acc) {
   check_f32_cuda(x, "x");
   check_f32_cuda(w, "w");
   check_f32_cuda(b, "b");
@@ -182,30 +183,33 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
   TORCH_CHECK(C >= 1 && C <= 32, "head: 1..32 classes supported");
   check_opt(gw, "gw", C * K);
   check_opt(gb, "gb", C);
-  auto stats = torch::zeros({2}, x.options());
+  check_opt(stats_acc, "stats_acc", 2);
+  auto stats = opt_ptr(stats_acc) ? *stats_acc : torch::zeros({2}, x.options());
   const bool train = opt_ptr(gw) != nullptr || opt_ptr(gb) != nullptr || need_dx;
   c10::optional<torch::Tensor> dx;
   if (M == 0) return {stats, need_dx ? c10::optional<torch::Tensor>(torch::empty({0, K}, x.options())) : c10::nullopt};
   hipStream_t s = cur_stream();
-  const bool fused = sdml::head_fused_supported((int)K, (int)C) && opt_ptr(gw) && opt_ptr(gb);
+  const bool fusable = sdml::head_fused_supported((int)K, (int)C);
+  const bool fused = fusable && (!train || (opt_ptr(gw) && opt_ptr(gb)));
+  torch::Tensor ws;
+  if (fused) ws = torch::empty({(int64_t)sdml::head_workspace_floats(M, K, C)}, x.options());
+  float* wsp = fused ? ws.data_ptr<float>() : nullptr;
   if (!train) {
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
                               target.data_ptr<int64_t>(), M, K, C, (float)scale, stats.data_ptr<float>(), nullptr,
-                              nullptr, nullptr, nullptr, s);
+                              nullptr, nullptr, nullptr, wsp, s);
     return {stats, c10::nullopt};
   }
-  // dx is always produced by the kernels in training mode (needed by the fused kernel's
-  // structure); callers that do not need it drop it.
   auto dxt = torch::empty({M, K}, x.options());
   if (fused) {
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
                               target.data_ptr<int64_t>(), M, K, C, (float)scale, stats.data_ptr<float>(),
-                              dxt.data_ptr<float>(), opt_ptr(gw), opt_ptr(gb), nullptr, s);
+                              dxt.data_ptr<float>(), opt_ptr(gw), opt_ptr(gb), nullptr, wsp, s);
   } else {
     auto dz = torch::empty({M, C}, x.options());
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
                               target.data_ptr<int64_t>(), M, K, C, (float)scale, stats.data_ptr<float>(),
-                              dxt.data_ptr<float>(), nullptr, nullptr, dz.data_ptr<float>(), s);
+                              dxt.data_ptr<float>(), nullptr, nullptr, dz.data_ptr<float>(), nullptr, s);
     if (opt_ptr(gw)) {
       sdml::GemmArgs g;  // gw[C,K] += dz^T x ; gb += colsum(dz)
       g.A = dz.data_ptr<float>();
@@ -222,12 +226,8 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
       g.b_kmajor = true;
       g.epi = sdml::EPI_ATOMIC;
       g.splits = sdml::gemm_f32_pick_splits(g.M, g.N, g.K);
-      if (sdml::gemm_f32_supported(g)) {
-        sdml::gemm_f32(g, s);
-      } else {
-        gw->add_(dz.t().mm(x));
-        if (opt_ptr(gb)) gb->add_(dz.sum(0));
-      }
+      TORCH_CHECK(sdml::gemm_f32_supported(g), "head dW: unsupported");
+      sdml::gemm_f32(g, s);
     } else if (opt_ptr(gb)) {
       gb->add_(dz.sum(0));
     }
@@ -237,7 +237,7 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
 }
 
 void sgd_momentum_(torch::Tensor p, torch::Tensor g, torch::Tensor buf, double lr, double momentum, double dampening,
-                   double wd, bool nesterov, bool first) {
+                   double wd, bool nesterov, bool first, bool zero_grad) {
   check_f32_cuda(p, "p");
   check_f32_cuda(g, "g");
   check_f32_cuda(buf, "buf");
@@ -245,7 +245,7 @@ void sgd_momentum_(torch::Tensor p, torch::Tensor g, torch::Tensor buf, double l
   TORCH_CHECK(momentum == 0 || buf.numel() == p.numel(), "sgd: momentum buffer size mismatch");
   TORCH_CHECK(p.numel() % 4 == 0, "sgd: flat buffers must be padded to a multiple of 4");
   sdml::sgd_momentum(p.data_ptr<float>(), g.data_ptr<float>(), buf.data_ptr<float>(), p.numel(), (float)lr,
-                     (float)momentum, (float)dampening, (float)wd, nesterov, first, cur_stream());
+                     (float)momentum, (float)dampening, (float)wd, nesterov, first, zero_grad, cur_stream());
 }
 
 void synth_mnist(int64_t seed, int64_t start, int64_t n, int64_t H, int64_t W, int64_t mode, torch::Tensor x,
@@ -269,7 +269,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f32", &gemm_f32_op, "generic fp32 MFMA GEMM", py::arg("A"), py::arg("B"), py::arg("C"),
         py::arg("a_kmajor"), py::arg("b_kmajor"), py::arg("epi"), py::arg("splits") = 1,
         py::arg("bias") = py::none(), py::arg("rowsum") = py::none());
-  m.def("head_logsoftmax_nll_f32", &head_logsoftmax_nll_f32, "fused fc + log_softmax + NLL (+ backward)");
-  m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer");
+  m.def("head_logsoftmax_nll_f32", &head_logsoftmax_nll_f32, "fused fc + log_softmax + NLL (+ backward)",
+        py::arg("x"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
+        py::arg("need_dx"), py::arg("stats_acc") = py::none());
+  m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer", py::arg("p"), py::arg("g"),
+        py::arg("buf"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"),
+        py::arg("first"), py::arg("zero_grad") = false);
   m.def("synth_mnist", &synth_mnist, "on-device synthetic MNIST-shape data");
 }

@@ -19,7 +19,7 @@ def get_model_spec(name: str, num_stages: int = None, **kw) -> ModelSpec:
     if name == "mlp4x1024":
         return mlp_spec(MLP4X1024_DIMS, n, "mlp4x1024")
     if name == "ref_cnn":
-        return ref_cnn_spec(n, eval_dropout=kw.get("eval_dropout", True))
+        return ref_cnn_spec(n, eval_dropout=kw.get("eval_dropout", True), dropout=kw.get("dropout", 0.5))
     if name == "resnet18":
         return resnet18_spec(n)
     if name == "gpt2":

@@ -70,7 +70,10 @@ class PipelineStage(nn.Module):
         correct = (out.argmax(dim=1) == target).sum()
         return loss, correct, target.numel()
 
-    def head_fwd(self, x: torch.Tensor, target: torch.Tensor, ctx: dict, train: bool, loss_scale: float):
+    def head_fwd(self, x: torch.Tensor, target: torch.Tensor, ctx: dict, train: bool, loss_scale: float,
+                 stats: Optional[torch.Tensor] = None):
+        """Returns (loss_sum, correct, count); a stage may instead accumulate loss/correct into
+        ``stats`` in-kernel and return (None, None, count)."""
         if not train:
             with torch.no_grad():
                 out = self(x)

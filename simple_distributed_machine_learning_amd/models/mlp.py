@@ -104,7 +104,7 @@ class MLPStage(PipelineStage):
             g = ops.linear_relu_bwd(acts[i], acts[i + 1], g, lin.weight, lin.weight.grad, lin.bias.grad, need_dx)
         return g
 
-    def head_fwd(self, x, target, ctx, train, loss_scale):
+    def head_fwd(self, x, target, ctx, train, loss_scale, stats=None):
         if not self._fused(x):
             return super().head_fwd(x, target, ctx, train, loss_scale)
         x = x.reshape(x.shape[0], -1)
@@ -120,7 +120,7 @@ class MLPStage(PipelineStage):
         loss, correct, dx = ops.linear_logsoftmax_nll(
             x, head.weight, head.bias, target,
             head.weight.grad if train else None, head.bias.grad if train else None,
-            loss_scale, need_dx)
+            loss_scale, need_dx, stats=stats)
         if train:
             ctx["acts"] = acts
             ctx["dx"] = dx

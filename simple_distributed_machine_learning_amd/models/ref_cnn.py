@@ -26,11 +26,11 @@ from .base import ModelSpec, PipelineStage
 
 
 class Network1Stage(PipelineStage):
-    def __init__(self):
+    def __init__(self, dropout: float = 0.5):
         super().__init__()
         self.conv1 = nn.Conv2d(1, 10, kernel_size=5)
         self.conv2 = nn.Conv2d(10, 20, kernel_size=5)
-        self.conv2_drop = nn.Dropout2d()
+        self.conv2_drop = nn.Dropout2d(p=dropout)
         self.loss_kind = "nll"
 
     def forward(self, x):
@@ -41,15 +41,16 @@ class Network1Stage(PipelineStage):
 
 
 class Network2Stage(PipelineStage):
-    def __init__(self, eval_dropout: bool = True):
+    def __init__(self, eval_dropout: bool = True, dropout: float = 0.5):
         super().__init__()
         self.fc1 = nn.Linear(320, 50)
         self.fc2 = nn.Linear(50, 10)
         self.eval_dropout = eval_dropout
+        self.p = dropout
         self.loss_kind = "nll"
 
     def forward(self, x):
-        z4 = F.dropout(F.relu(self.fc1(x)), p=0.5, training=self.training or self.eval_dropout)
+        z4 = F.dropout(F.relu(self.fc1(x)), p=self.p, training=self.training or self.eval_dropout)
         z5 = self.fc2(z4)
         return F.log_softmax(z5, dim=1)
 
@@ -65,12 +66,13 @@ class RefCNNSingle(nn.Module):
         return self.s1(self.s0(x))
 
 
-def ref_cnn_spec(num_stages: int = 2, eval_dropout: bool = True) -> ModelSpec:
+def ref_cnn_spec(num_stages: int = 2, eval_dropout: bool = True, dropout: float = 0.5) -> ModelSpec:
+    """``dropout`` = 0.5 is the reference; 0 makes the model deterministic (parity tests)."""
     if num_stages != 2:
         raise ValueError("ref_cnn is defined as the reference's 2-stage split")
 
     def build(s: int) -> PipelineStage:
-        return Network1Stage() if s == 0 else Network2Stage(eval_dropout)
+        return Network1Stage(dropout) if s == 0 else Network2Stage(eval_dropout, dropout)
 
     def shape(s: int, mb: int):
         return (mb, 320)

@@ -38,20 +38,32 @@ def linear_relu_bwd(x, y, gy, w, gw, gb, need_dx: bool):
     return ref.linear_relu_bwd(x, y, gy, w, gw, gb, need_dx)
 
 
-def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool):
+def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool, stats=None):
     """Fused classifier head: z = x @ w.T + b -> log_softmax -> NLL (sum) and, when grads are
     given, the full backward (gw/gb accumulated, dx returned) scaled by ``scale``.
-    Returns (loss_sum, correct, dx) — loss_sum/correct are 0-dim device tensors."""
+
+    Returns (loss_sum, correct, dx). With ``stats`` (a float32 [2] tensor) the loss sum and
+    correct count are ACCUMULATED into it in-kernel and (None, None, dx) is returned."""
     if x.is_cuda:
-        stats, dx = _k().head_logsoftmax_nll_f32(x, w, b, target, gw, gb, float(scale), need_dx)
-        return stats[0], stats[1], dx
-    return ref.linear_logsoftmax_nll(x, w, b, target, gw, gb, scale, need_dx)
+        st, dx = _k().head_logsoftmax_nll_f32(x, w, b, target, gw, gb, float(scale), need_dx, stats)
+        if stats is not None:
+            return None, None, dx
+        return st[0], st[1], dx
+    loss, correct, dx = ref.linear_logsoftmax_nll(x, w, b, target, gw, gb, scale, need_dx)
+    if stats is not None:
+        stats[0] += loss
+        stats[1] += correct
+        return None, None, dx
+    return loss, correct, dx
 
 
 def sgd_momentum_(p, g, buf, lr: float, momentum: float, dampening: float = 0.0, weight_decay: float = 0.0,
-                  nesterov: bool = False, first: bool = False):
+                  nesterov: bool = False, first: bool = False, zero_grad: bool = False):
+    """In-place SGD step; with ``zero_grad`` the kernel also clears ``g`` after reading it."""
     if p.is_cuda:
         _k().sgd_momentum_(p, g, buf, float(lr), float(momentum), float(dampening), float(weight_decay),
-                           bool(nesterov), bool(first))
+                           bool(nesterov), bool(first), bool(zero_grad))
         return
     ref.sgd_momentum_(p, g, buf, lr, momentum, dampening, weight_decay, nesterov, first)
+    if zero_grad:
+        g.zero_()

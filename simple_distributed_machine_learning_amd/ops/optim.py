@@ -26,9 +26,13 @@ class FusedSGD:
         self.momentum_buffer = torch.zeros_like(flat.params) if momentum != 0 else flat.params.new_zeros(64)
         self.steps = 0
 
-    def step(self):
+    def step(self, zero_grad: bool = True):
+        """One update. ``zero_grad`` clears the gradients inside the same kernel (the engine
+        then skips its own zero_grad at the next step: one launch, one pass over memory)."""
         sgd_momentum_(self.flat.params, self.flat.grads, self.momentum_buffer, self.lr, self.momentum,
-                      self.dampening, self.weight_decay, self.nesterov, self.steps == 0)
+                      self.dampening, self.weight_decay, self.nesterov, self.steps == 0, zero_grad)
+        if zero_grad:
+            self.flat.grads_zero = True
         self.steps += 1
 
     def zero_grad(self):

@@ -47,8 +47,8 @@ def split_sizes(n: int, m: int) -> List[int]:
 
 @dataclass
 class StepResult:
-    loss_sum: torch.Tensor  # summed over the samples this rank's last stage(s) saw
-    correct: torch.Tensor
+    loss_sum: torch.Tensor  # 0-dim, summed over the samples this rank's last stage(s) saw
+    correct: torch.Tensor   # 0-dim (float32 count)
     count: int
     wall_s: float = 0.0
 
@@ -178,8 +178,8 @@ class PipelineEngine:
                 if step_optimizer:
                     self.optimizer.step()
                     self.global_step += 1
-            z = torch.zeros((), device=dev, dtype=torch.float32)
-            return StepResult(z, torch.zeros((), device=dev, dtype=torch.int64), 0, time.perf_counter() - t0)
+            z = torch.zeros(2, device=dev, dtype=torch.float32)
+            return StepResult(z[0], z[1], 0, time.perf_counter() - t0)
         sizes = split_sizes(batch_size, self.M)
         M = len(sizes)
         offs = [start]
@@ -193,7 +193,8 @@ class PipelineEngine:
             scale = scale / float(dataset.seq_len)
 
         if train:
-            self.flat.zero_grad()
+            self.flat.zero_grad()  # no-op when the previous optimizer step already cleared them
+            self.flat.grads_zero = False
             self.grad_sync.reset()
         last_bwd = {}
         if train:
@@ -205,8 +206,7 @@ class PipelineEngine:
         local: Dict[Tuple[int, int, int, int], torch.Tensor] = {}
         outbox: Dict[Tuple[int, int, int, int], torch.Tensor] = {}
         inbox: Dict[Tuple[int, int, int, int], Tuple[object, torch.Tensor]] = {}
-        loss_sum = torch.zeros((), device=dev, dtype=torch.float32)
-        correct = torch.zeros((), device=dev, dtype=torch.int64)
+        stats = torch.zeros(2, device=dev, dtype=torch.float32)  # [loss_sum, correct]
         count = 0
 
         def take(key, peer_rank_is_local: bool):
@@ -246,9 +246,10 @@ class PipelineEngine:
                     tgt = dataset.targets(off, mbsz)
                     if tgt.device != dev:
                         tgt = tgt.to(dev, non_blocking=True)
-                    l, c, n = mod.head_fwd(x, tgt, ctx, train, scale)
-                    loss_sum += l.float()
-                    correct += c.to(torch.int64)
+                    l, c, n = mod.head_fwd(x, tgt, ctx, train, scale, stats=stats)
+                    if l is not None:  # stage did not accumulate in-kernel
+                        stats[0] += l.float()
+                        stats[1] += c.float()
                     count += n
                 else:
                     y = mod.fwd(x, ctx, train)
@@ -288,13 +289,13 @@ class PipelineEngine:
             if step_optimizer:
                 self.optimizer.step()
                 self.global_step += 1
-        return StepResult(loss_sum, correct, count, time.perf_counter() - t0)
+        return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
 
     # ---------------------------------------------------------------------------------------
     def reduce_metrics(self, res: StepResult, group=None) -> Tuple[float, int, int]:
         """Sum (loss, correct, count) over all last-stage holders (world). Host-syncs."""
         v = torch.stack([res.loss_sum.double(), res.correct.double(),
-                         torch.tensor(float(res.count), device=res.loss_sum.device, dtype=torch.float64)])
+                         torch.tensor(float(res.count), dtype=torch.float64).to(res.loss_sum.device)])
         if self.mesh.world_size > 1:
             # every pipeline's last stage contributes once; the other ranks contribute zeros
             dist.all_reduce(v, group=group)

@@ -68,9 +68,12 @@ class FlatParams:
             p.data = view
             p.grad = self.grads[seg.offset:seg.offset + seg.numel].view(seg.shape)
         self._plist = plist
+        self.grads_zero = True  # grads known to be all-zero (skip the next zero_grad launch)
 
-    def zero_grad(self):
-        self.grads.zero_()
+    def zero_grad(self, force: bool = False):
+        if force or not self.grads_zero:
+            self.grads.zero_()
+        self.grads_zero = True
 
     def stage_slice(self, stage: int, which: str = "grads") -> torch.Tensor:
         a, b = self.stage_ranges[stage]

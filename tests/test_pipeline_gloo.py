@@ -1,0 +1,95 @@
+"""Multi-process parity on Gloo/CPU: an N-rank pipeline (and dp x pp mesh) must train to the
+same weights and losses as one process running the whole model on the same data and seeds.
+This is the framework's stand-in for "multi-node without a cluster" (SURVEY.md §4)."""
+import pytest
+import torch
+
+from dist_util import run_ranks
+from dist_workers import train_worker
+
+pytestmark = pytest.mark.slow
+
+
+def _single(model, M, steps, B, kind="1f1b", kw=None):
+    # world 1: every stage on the one rank, global batch = B*dp of the multi-rank run
+    return train_worker(0, 1, model, kind, M, 1, steps, B, 3, kw)
+
+
+def _stage_states(results):
+    out = {}
+    for r in results:
+        for s, sd in r["state"].items():
+            if s in out:  # replicas (dp / chimera mirrors) must agree exactly
+                for k in sd:
+                    torch.testing.assert_close(sd[k], out[s][k], rtol=0, atol=0)
+            else:
+                out[s] = sd
+    return out
+
+
+def _compare(results, ref, rtol=1e-5, atol=1e-6):
+    st = _stage_states(results)
+    assert sorted(st) == sorted(ref["state"])
+    for s in st:
+        for k in st[s]:
+            torch.testing.assert_close(st[s][k], ref["state"][s][k], rtol=rtol, atol=atol, msg=f"stage {s} {k}")
+    for a, b in zip(results[0]["losses"], ref["losses"]):
+        assert a == pytest.approx(b, rel=1e-5, abs=1e-6)
+    assert results[0]["eval"][2] == ref["eval"][2]
+    assert results[0]["eval"][0] == pytest.approx(ref["eval"][0], rel=1e-5)
+
+
+@pytest.mark.parametrize("kind,M", [("1f1b", 1), ("1f1b", 3), ("gpipe", 4), ("chimera", 4), ("chimera", 2)])
+def test_mlp_two_ranks_matches_single_process(kind, M):
+    B, steps = 48, 3
+    res = run_ranks(train_worker, 2, "mlp", kind, M, 2, steps, B)
+    ref = _single("mlp", M, steps, B, kind)
+    _compare(res, ref)
+    assert all(r["bytes_sent"] > 0 for r in res)  # the boundary really crossed processes
+
+
+def test_mlp_dp2_pp2_matches_single_process():
+    B, steps = 24, 3
+    res = run_ranks(train_worker, 4, "mlp", "1f1b", 2, 2, steps, B)
+    ref = _single("mlp", 2, steps, 2 * B)
+    # dp changes the micro-batch boundaries of the summed loss only through fp rounding
+    _compare(res, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_mlp_chimera_dp2_matches_single_process():
+    B, steps = 32, 2
+    res = run_ranks(train_worker, 4, "mlp", "chimera", 4, 2, steps, B)
+    ref = _single("mlp", 4, steps, 2 * B, "chimera")
+    _compare(res, ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("kind", ["gpipe", "1f1b"])
+def test_mlp4x1024_four_stages_four_ranks(kind):
+    B, steps = 16, 2
+    res = run_ranks(train_worker, 4, "mlp4x1024", kind, 4, 4, steps, B)
+    ref = _single("mlp4x1024", 4, steps, B, kind)
+    _compare(res, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_ref_cnn_two_ranks_no_dropout():
+    B, steps = 30, 2
+    kw = {"dropout": 0.0, "eval_dropout": False}
+    res = run_ranks(train_worker, 2, "ref_cnn", "1f1b", 2, 2, steps, B, 3, kw)
+    ref = _single("ref_cnn", 2, steps, B, "1f1b", kw)
+    _compare(res, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_resnet18_eight_stages_on_four_ranks():
+    B, steps = 4, 1
+    kw = {"stages": 8}
+    res = run_ranks(train_worker, 4, "resnet18", "1f1b", 2, 4, steps, B, 3, kw)
+    ref = _single("resnet18", 2, steps, B, "1f1b", kw)
+    _compare(res, ref, rtol=1e-3, atol=1e-4)
+
+
+def test_gpt2_tiny_two_ranks():
+    B, steps = 4, 2
+    kw = {"stages": 2, "seq_len": 16}
+    res = run_ranks(train_worker, 2, "gpt2_tiny", "1f1b", 2, 2, steps, B, 3, kw)
+    ref = _single("gpt2_tiny", 2, steps, B, "1f1b", kw)
+    _compare(res, ref, rtol=1e-4, atol=1e-5)

@@ -5,10 +5,15 @@ BASELINE.json metric: "samples/sec (whole node), 2-stage MLP on MNIST-shape synt
 log_softmax + NLL), trained with SGD(lr 0.1, momentum 0.5) in fp32 — the reference's
 optimizer and precision (/root/reference/simple_distributed.py:18-21, :100-104).
 
-Placement by GPU count (weak scaling: per-GPU work is fixed at --batch_per_gpu samples):
-  N=1   both stages on the one GPU (local hand-off, no p2p)
-  N>=2  Chimera bidirectional 2-stage pipeline on each GPU pair (activations/grads over RCCL
-        p2p on the pair's xGMI link) x dp = N/2 replicas (gradient all-reduce over RCCL)
+Placement ("rotate" pipeline; weak scaling: per-GPU work fixed at --batch_per_gpu samples):
+  every GPU owns a data shard and hosts both stages; each step is cut into W waves and in
+  every wave stage 0's output is split R ways and exchanged with ONE RCCL all-to-all (part k
+  -> GPU k), stage 1 (+ loss + its backward) runs on what arrived, the input-gradients go
+  back by the inverse all-to-all, stage 0 runs its backward; stage weights are replicated and
+  their gradients all-reduced over RCCL. On an 8-GPU node every stage boundary therefore
+  fans out over all 7 xGMI links of each GPU instead of one neighbour link. N=1 is the same
+  code with the exchange elided (both stages local).
+  (--schedule chimera / 1f1b select the classic neighbour pipelines instead.)
 
 Timing contract: W untimed warm-up steps; barrier + device sync; K timed steps (each a full
 forward + backward + gradient sync + optimizer step over fresh data); barrier + device sync;
@@ -39,17 +44,50 @@ BASELINE_SAMPLES_PER_S = 413_862.0
 BASELINE_NOTE = "BASELINE.md 2-stage MLP, B=4096 TCP-only: 413,862 samples/s (B=60: 13,704)"
 
 
+class _ShardedSynth:
+    """Per-rank view of the global synthetic dataset: labels for every sample, images only for
+    the samples this rank's stage 0 consumes (``own_len`` samples at ``own_lo`` of each of the
+    ``nbatches`` global batches of ``GB`` samples)."""
+
+    def __init__(self, GB, own_lo, own_len, nbatches, dev):
+        self.n = GB * nbatches
+        self.GB, self.own_lo, self.own_len = GB, own_lo, own_len
+        self.labels = SyntheticMNIST(self.n, seed=1234, device=dev, image_range=(0, 0))
+        self.imgs = [SyntheticMNIST(own_len, seed=1234, device=dev, offset=k * GB + own_lo) for k in range(nbatches)]
+
+    def inputs(self, start, n):
+        k, r = divmod(start, self.GB)
+        r -= self.own_lo
+        assert 0 <= r and r + n <= self.own_len, (start, n)
+        return self.imgs[k].x[r:r + n]
+
+    def targets(self, start, n):
+        return self.labels.y[start:start + n]
+
+    def __len__(self):
+        return self.n
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--batch_per_gpu", type=int, default=int(os.environ.get("SDML_BENCH_BATCH", 65536)))
-    p.add_argument("--microbatches", type=int, default=None, help="per pipeline (default: 1 on N=1, 4 chimera)")
-    p.add_argument("--schedule", default=None, help="default: none on N=1, chimera on N>=2")
-    p.add_argument("--dataset_batches", type=int, default=8, help="distinct batches cycled through")
+    p.add_argument("--batch_per_gpu", type=int, default=int(os.environ.get("SDML_BENCH_BATCH", 131072)))
+    p.add_argument("--waves", type=int, default=None, help="rotate: waves per step (default 1 on N=1, else 2)")
+    p.add_argument("--microbatches", type=int, default=None, help="chimera/1f1b: micro-batches per pipeline")
+    p.add_argument("--schedule", default="rotate", choices=["rotate", "chimera", "1f1b", "gpipe"])
+    p.add_argument("--dataset_batches", type=int, default=4, help="distinct batches cycled through")
     p.add_argument("--model", default="mlp")
     return p.parse_args()
+
+
+def _parallelism(kind, n, mesh):
+    if n == 1:
+        return "single GPU, both pipeline stages local"
+    if kind == "rotate":
+        return f"pp2 rotate: {n} GPUs x (stage0+stage1), all-to-all stage boundary over RCCL/xGMI, grad all-reduce"
+    return f"pp{mesh.pp}-{kind} x dp{mesh.dp}"
 
 
 def main():
@@ -60,27 +98,34 @@ def main():
         if rank == 0:
             print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     n = world
-    if n == 1:
-        kind, pp = (a.schedule or "1f1b"), 1
-        M = a.microbatches or 1
+    kind = a.schedule
+    if kind == "rotate":
+        pp = world
+        W = a.waves or (1 if n == 1 else 2)
+        M = W * pp
+        B = a.batch_per_gpu  # per owner shard
     else:
-        kind = a.schedule or "chimera"
-        pp = 2
-        M = a.microbatches or 4
+        pp = 1 if n == 1 else 2
+        M = a.microbatches or (1 if n == 1 else 4)
+        B = a.batch_per_gpu * pp  # per pipeline replica
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     mesh = init_mesh(pp=pp, schedule_kind=kind, timeout_s=900, rank=rank, world_size=world)
     dev = mesh.device
     spec = get_model_spec(a.model, 2)
     engine = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=1)
     engine.train()
-    # weak scaling: each pipeline replica processes batch_per_gpu * pp samples per step
-    B = a.batch_per_gpu * pp
-    GB = B * mesh.dp
-    ds = SyntheticMNIST(B * a.dataset_batches, seed=1234, device=dev, offset=mesh.dp_rank * B * a.dataset_batches)
+    GB = B * engine.data_shards  # samples per optimizer step, whole node
+    # fresh data every step, cycling over `dataset_batches` global batches; a rank
+    # materialises images only for the shards it feeds into stage 0 (labels for all)
+    if world == 1:
+        ds = SyntheticMNIST(GB * a.dataset_batches, seed=1234, device=dev)
+    else:  # rotate: own shard of the group block; chimera/1f1b: the replica's whole batch
+        own_lo = engine.local_start(0, B) + (mesh.pp_rank * B if kind == "rotate" else 0)
+        ds = _ShardedSynth(GB, own_lo, B, a.dataset_batches, dev)
 
     def step(i):
-        start = (i % a.dataset_batches) * B
-        return engine.run(ds, start, B, train=True, global_batch=GB)
+        start = (i % a.dataset_batches) * GB
+        return engine.run(ds, engine.local_start(start, B), B, train=True, global_batch=GB)
 
     def sync():
         if dev.type == "cuda":
@@ -127,8 +172,8 @@ def main():
                 "model": "mlp-784-128-10 (2 pipeline stages)",
                 "global_batch": GB,
                 "seq_len": None,
-                "parallelism": (f"pp2-chimera x dp{mesh.dp}" if pp == 2 else "single-GPU, both stages local"),
-                "microbatches_per_pipeline": M,
+                "parallelism": _parallelism(kind, n, mesh),
+                "microbatches": M,
                 "batch_per_gpu": a.batch_per_gpu,
                 "optimizer": "SGD lr=0.1 momentum=0.5",
             },

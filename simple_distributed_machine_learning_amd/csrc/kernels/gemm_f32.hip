@@ -153,18 +153,22 @@ __device__ __forceinline__ f32x4 frag(const float* __restrict__ T, int row, int 
 template <bool A_KM, bool B_KM>
 __global__ void __launch_bounds__(NTHR, 2) gemm_f32_kernel(KParams p) {
   __shared__ __attribute__((aligned(16))) float smem[4 * TILE_FLOATS];  // [buf][A|B]
-  // XCD-aware, bijective remap of the (m,n) tile index: consecutive tiles share operands,
-  // so give each XCD a contiguous chunk of the tile order (blocks b and b+8 share an XCD).
-  const int nwg = p.tiles_m * p.tiles_n;
-  int orig = blockIdx.x;
+  // XCD-aware, bijective remap over ALL blocks (tiles x splits): blocks b and b+8 share an
+  // XCD, so hand each XCD a contiguous run of logical ids. Logical id = split * ntiles + tile:
+  // the tiles of one K-split (which stream the SAME A/B K-slices) then sit on one XCD and
+  // read those slices through its L2 instead of once per tile from HBM.
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int nwg = ntiles * gridDim.y;
+  int orig = blockIdx.y * gridDim.x + blockIdx.x;
   int wg = orig;
   if (nwg >= 16) {
     int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
   }
-  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;
+  const int split = wg / ntiles, tile = wg % ntiles;
+  const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.z * p.kps;
+  const int kbeg = split * p.kps;
   const int kend = min(p.K, kbeg + p.kps);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -285,11 +289,13 @@ bool gemm_f32_supported(const GemmArgs& g) {
 
 int gemm_f32_pick_splits(int M, int N, int K) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  int splits = 1;
-  // fill the chip (<= 2 blocks/CU) but keep >= 32 K-steps per split: every split adds its
-  // whole C tile with fp32 atomics (~1.3 TB/s chip-wide), so splits cost output bandwidth
-  while (tiles * splits * 2 <= 512 && K / (splits * 2) >= 32 * BK) splits *= 2;
-  return splits;
+  // fill the chip with one wave of blocks (2 resident per CU = 512 slots) while keeping
+  // >= 32 K-steps per split: every split adds its whole C tile with fp32 atomics
+  // (~1.3 TB/s chip-wide), so splits cost output bandwidth
+  int splits = 512 / tiles;
+  const int max_by_k = K / (32 * BK);
+  if (splits > max_by_k) splits = max_by_k;
+  return splits < 1 ? 1 : splits;
 }
 
 void gemm_f32(const GemmArgs& g, hipStream_t stream) {
@@ -316,7 +322,7 @@ void gemm_f32(const GemmArgs& g, hipStream_t stream) {
   p.kps = kps;
   p.tiles_m = (g.M + BM - 1) / BM;
   p.tiles_n = (g.N + BN - 1) / BN;
-  dim3 grid(p.tiles_m * p.tiles_n, 1, splits);
+  dim3 grid(p.tiles_m * p.tiles_n, splits, 1);
   dim3 block(NTHR);
   if (!g.a_kmajor && !g.b_kmajor)
     hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, block, 0, stream, p);

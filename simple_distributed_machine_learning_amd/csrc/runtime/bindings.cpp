@@ -123,6 +123,9 @@ PYBIND11_MODULE(_runtime, m) {
   m.def("stage_rank", [](const std::string& kind, int P, int M, int R, int pipe, int stage) {
     return sdml::stage_rank(make_spec(kind, P, M, R, 1, 2, false), pipe, stage);
   });
+  m.def("task_rank", [](const std::string& kind, int P, int M, int R, int mb, int stage) {
+    return sdml::task_rank(make_spec(kind, P, M, R, 1, 2, false), mb, stage);
+  });
   m.def("mb_pipe", [](const std::string& kind, int P, int M, int R, int mb) {
     return sdml::mb_pipe(make_spec(kind, P, M, R, 1, 2, false), mb);
   });

@@ -26,10 +26,12 @@ struct Task {
 void check_spec(const ScheduleSpec& s) {
   if (s.num_stages < 1 || s.num_microbatches < 1 || s.num_ranks < 1)
     throw std::invalid_argument("schedule: num_stages, num_microbatches, num_ranks must be >= 1");
-  if (s.num_stages % s.num_ranks != 0)
+  if (s.kind != "rotate" && s.num_stages % s.num_ranks != 0)
     throw std::invalid_argument("schedule: num_stages must be a multiple of num_ranks");
-  if (s.kind != "gpipe" && s.kind != "1f1b" && s.kind != "chimera")
-    throw std::invalid_argument("schedule: unknown kind '" + s.kind + "' (gpipe|1f1b|chimera)");
+  if (s.kind != "gpipe" && s.kind != "1f1b" && s.kind != "chimera" && s.kind != "rotate")
+    throw std::invalid_argument("schedule: unknown kind '" + s.kind + "' (gpipe|1f1b|chimera|rotate)");
+  if (s.kind == "rotate" && s.num_microbatches % s.num_ranks != 0)
+    throw std::invalid_argument("schedule: rotate needs num_microbatches to be a multiple of num_ranks");
   if (!(s.cost_f > 0) || !(s.cost_b > 0)) throw std::invalid_argument("schedule: costs must be > 0");
 }
 
@@ -39,6 +41,7 @@ int rank_pos(const ScheduleSpec& s, int pipe, int rank) {
 }
 
 int mb_index_in_pipe(const ScheduleSpec& s, int mb) {
+  if (s.kind == "rotate") return mb % (s.num_microbatches / s.num_ranks);
   if (num_pipes(s) == 1) return mb;
   int half = (s.num_microbatches + 1) / 2;
   return mb < half ? mb : mb - half;
@@ -54,9 +57,13 @@ using MsgKey = std::tuple<int, int, int, int>;  // payload, pipe, producer stage
 
 }  // namespace
 
-int num_pipes(const ScheduleSpec& s) { return s.kind == "chimera" ? 2 : 1; }
+int num_pipes(const ScheduleSpec& s) {
+  if (s.kind == "rotate") return s.num_ranks;
+  return s.kind == "chimera" ? 2 : 1;
+}
 
 int mb_pipe(const ScheduleSpec& s, int mb) {
+  if (s.kind == "rotate") return mb / (s.num_microbatches / s.num_ranks);  // owner rank
   if (num_pipes(s) == 1) return 0;
   int half = (s.num_microbatches + 1) / 2;
   return mb < half ? 0 : 1;
@@ -65,6 +72,15 @@ int mb_pipe(const ScheduleSpec& s, int mb) {
 int stage_rank(const ScheduleSpec& s, int pipe, int stage) {
   int r = stage / (s.num_stages / s.num_ranks);
   return pipe == 0 ? r : s.num_ranks - 1 - r;
+}
+
+int task_rank(const ScheduleSpec& s, int mb, int stage) {
+  if (s.kind == "rotate") {
+    int per = s.num_microbatches / s.num_ranks;
+    int owner = mb / per, j = mb % per;
+    return (owner + stage * j) % s.num_ranks;
+  }
+  return stage_rank(s, mb_pipe(s, mb), stage);
 }
 
 std::vector<std::vector<Instr>> build_schedule(const ScheduleSpec& spec, SimStats* stats_out) {
@@ -80,10 +96,9 @@ std::vector<std::vector<Instr>> build_schedule(const ScheduleSpec& spec, SimStat
   std::vector<char> started(NT, 0);
   std::vector<std::vector<int>> rank_tasks(R);
   for (int mb = 0; mb < M; ++mb) {
-    int p = mb_pipe(spec, mb);
     for (int s = 0; s < P; ++s) {
-      rank_tasks[stage_rank(spec, p, s)].push_back(tid(s, mb, false));
-      if (!fo) rank_tasks[stage_rank(spec, p, s)].push_back(tid(s, mb, true));
+      rank_tasks[task_rank(spec, mb, s)].push_back(tid(s, mb, false));
+      if (!fo) rank_tasks[task_rank(spec, mb, s)].push_back(tid(s, mb, true));
     }
   }
   auto decode = [&](int t) {
@@ -118,7 +133,7 @@ std::vector<std::vector<Instr>> build_schedule(const ScheduleSpec& spec, SimStat
     for (int t : rank_tasks[r])
       if (!(t & 1)) f_total[r]++;
   // in-flight (F started, B not started) per (pipe, stage)
-  std::vector<int> inflight(2 * P, 0);
+  std::vector<int> inflight((size_t)num_pipes(spec) * P, 0);
   int max_inflight_rank = 0;
   std::vector<int> rank_inflight(R, 0);
 
@@ -150,6 +165,10 @@ std::vector<std::vector<Instr>> build_schedule(const ScheduleSpec& spec, SimStat
         if (spec.kind == "gpipe") {
           if (k.bwd && f_done_started[r] < f_total[r]) continue;  // flush: all F before any B
           key = {k.bwd ? 1 : 0, idx, k.bwd ? -k.stage : k.stage, k.pipe};
+        } else if (spec.kind == "rotate") {
+          // backward first, then the deepest ready forward (frees stashed activations and
+          // keeps every peer fed); own fresh micro-batches last
+          key = {k.bwd ? 0 : 1, -k.stage, idx, (k.pipe - r + R) % R};
         } else {
           if (!k.bwd) {
             int limit = R - pos;  // warm-up depth of this rank along the pipe
@@ -216,7 +235,7 @@ std::vector<std::vector<Instr>> build_schedule(const ScheduleSpec& spec, SimStat
       c.mb = k.mb;
       comp[r].push_back(c);
       if (!k.bwd && k.stage < P - 1) {
-        int dst = stage_rank(spec, k.pipe, k.stage + 1);
+        int dst = task_rank(spec, k.mb, k.stage + 1);
         if (dst != r) {
           Instr s{OP_SEND, k.pipe, k.stage, k.mb, dst, PL_ACT};
           comp[r].push_back(s);
@@ -225,7 +244,7 @@ std::vector<std::vector<Instr>> build_schedule(const ScheduleSpec& spec, SimStat
         }
       }
       if (k.bwd && k.stage > 0) {
-        int dst = stage_rank(spec, k.pipe, k.stage - 1);
+        int dst = task_rank(spec, k.mb, k.stage - 1);
         if (dst != r) {
           Instr s{OP_SEND, k.pipe, k.stage, k.mb, dst, PL_GRAD};
           comp[r].push_back(s);
@@ -245,10 +264,10 @@ std::vector<std::vector<Instr>> build_schedule(const ScheduleSpec& spec, SimStat
         int src = -1;
         MsgKey need;
         if (in.op == OP_FWD && in.stage > 0) {
-          src = stage_rank(spec, in.pipe, in.stage - 1);
+          src = task_rank(spec, in.mb, in.stage - 1);
           need = MsgKey{PL_ACT, in.pipe, in.stage - 1, in.mb};
         } else if (in.op == OP_BWD && in.stage < P - 1) {
-          src = stage_rank(spec, in.pipe, in.stage + 1);
+          src = task_rank(spec, in.mb, in.stage + 1);
           need = MsgKey{PL_GRAD, in.pipe, in.stage + 1, in.mb};
         }
         if (src >= 0 && src != r) {
@@ -291,7 +310,7 @@ SimStats validate_schedule(const ScheduleSpec& spec, const std::vector<std::vect
         throw std::runtime_error("validate: task index out of range");
       int p = mb_pipe(spec, in.mb);
       if (in.pipe != p) throw std::runtime_error("validate: micro-batch on wrong pipe");
-      if (stage_rank(spec, p, in.stage) != r) throw std::runtime_error("validate: task on wrong rank");
+      if (task_rank(spec, in.mb, in.stage) != r) throw std::runtime_error("validate: task on wrong rank");
       seen[{in.stage, in.mb, in.op == OP_BWD}]++;
     }
   }
@@ -389,7 +408,7 @@ SimStats validate_schedule(const ScheduleSpec& spec, const std::vector<std::vect
     for (size_t c = 0; c < comp_idx[r].size(); ++c) {
       const Instr& in = prog[r][comp_idx[r][c]];
       auto add_dep = [&](int payload, int stage_prod, bool prod_bwd) {
-        int pr = stage_rank(spec, in.pipe, stage_prod);
+        int pr = task_rank(spec, in.mb, stage_prod);
         if (pr == r) {
           auto tp = task_pos.at({stage_prod, in.mb, prod_bwd});
           if (tp.second > comp_idx[r][c])

@@ -30,7 +30,7 @@ struct Instr {
 };
 
 struct ScheduleSpec {
-  std::string kind = "1f1b";  // gpipe | 1f1b | chimera
+  std::string kind = "1f1b";  // gpipe | 1f1b | chimera | rotate
   int num_stages = 2;
   int num_microbatches = 1;
   int num_ranks = 2;
@@ -46,8 +46,13 @@ struct SimStats {
   int num_messages = 0;
 };
 
-// rank holding (pipe, stage)
+// rank holding (pipe, stage) — placement-by-pipe kinds (gpipe, 1f1b, chimera)
 int stage_rank(const ScheduleSpec& spec, int pipe, int stage);
+// rank computing stage `stage` of micro-batch `mb` (all kinds). For "rotate": micro-batches
+// are owned by ranks (owner = mb / (M/R)); local index j = mb % (M/R); stage s of it runs on
+// rank (owner + s*j) mod R — every rank hosts every stage, and a stage boundary fans out to
+// all peers (all xGMI links busy) instead of one neighbour.
+int task_rank(const ScheduleSpec& spec, int mb, int stage);
 int num_pipes(const ScheduleSpec& spec);
 int mb_pipe(const ScheduleSpec& spec, int mb);
 

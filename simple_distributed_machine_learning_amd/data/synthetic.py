@@ -42,13 +42,17 @@ class Dataset:
 class SyntheticMNIST(Dataset):
     H = W = 28
 
-    def __init__(self, n: int, seed: int = 1234, device="cpu", mode: str = "learnable", offset: int = 0):
+    def __init__(self, n: int, seed: int = 1234, device="cpu", mode: str = "learnable", offset: int = 0,
+                 image_range=None):
+        """``image_range=(lo, hi)``: materialise images only for samples [lo, hi) (labels for
+        all n) — a rank that runs stage 0 only on its own shard needs no other images."""
         self.n = int(n)
         self.seed = int(seed)
         self.device = torch.device(device)
         self.mode = {"learnable": 0, "random": 1}[mode]
         self.offset = int(offset)  # sample-id offset (train/test splits use disjoint ids)
-        self.x = torch.empty((self.n, 1, self.H, self.W), dtype=torch.float32, device=self.device)
+        self.lo, self.hi = (0, self.n) if image_range is None else (int(image_range[0]), int(image_range[1]))
+        self.x = torch.empty((self.hi - self.lo, 1, self.H, self.W), dtype=torch.float32, device=self.device)
         self.y = torch.empty((self.n,), dtype=torch.int64, device=self.device)
         if self.n:
             self._fill()
@@ -57,13 +61,25 @@ class SyntheticMNIST(Dataset):
         if self.device.type == "cuda":
             from .._native import kernels
 
-            kernels().synth_mnist(self.seed, self.offset, self.n, self.H, self.W, self.mode, self.x, self.y)
+            k = kernels()
+            if (self.lo, self.hi) == (0, self.n):
+                k.synth_mnist(self.seed, self.offset, self.n, self.H, self.W, self.mode, self.x, self.y)
+            else:
+                scratch = torch.empty((self.n, 1, 1, 1), dtype=torch.float32, device=self.device)
+                k.synth_mnist(self.seed, self.offset, self.n, 1, 1, self.mode, scratch, self.y)  # labels only
+                ylo = torch.empty((self.hi - self.lo,), dtype=torch.int64, device=self.device)
+                k.synth_mnist(self.seed, self.offset + self.lo, self.hi - self.lo, self.H, self.W, self.mode, self.x, ylo)
         else:
-            runtime().synth_fill(self.seed, self.offset, self.n, self.H, self.W, self.mode,
-                                 self.x.data_ptr(), self.y.data_ptr())
+            rt = runtime()
+            rt.synth_fill(self.seed, self.offset, self.n, self.H, self.W, self.mode, 0, self.y.data_ptr())
+            rt.synth_fill(self.seed, self.offset + self.lo, self.hi - self.lo, self.H, self.W, self.mode,
+                          self.x.data_ptr(), 0)
 
     def inputs(self, start, n):
-        return self.x[start:start + n]
+        if start < self.lo or start + n > self.hi:
+            raise IndexError(f"images [{start}, {start + n}) not materialised on this rank "
+                             f"(have [{self.lo}, {self.hi}))")
+        return self.x[start - self.lo:start - self.lo + n]
 
     def targets(self, start, n):
         return self.y[start:start + n]

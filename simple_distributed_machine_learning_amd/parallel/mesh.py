@@ -78,6 +78,8 @@ def replica_groups_spec(world_size: int, pp: int, kind: str) -> List[List[int]]:
     dp = world_size // pp
     groups = []
     seen = set()
+    if kind == "rotate":  # every rank hosts every stage: one group over the whole world
+        return [list(range(world_size))]
     for r in range(pp):
         mirror = pp - 1 - r if kind == "chimera" else r
         key = tuple(sorted({r, mirror}))
@@ -137,9 +139,12 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
         g = dist.new_group(ranks, timeout=timeout) if pp > 1 else None
         if d == mesh.dp_rank:
             mesh.pipe_group = g
+    # rotate talks to every peer of the pipeline group; the others only to neighbours
+    pairs = [(r, q) for r in range(pp) for q in range(r + 1, pp)] if schedule_kind == "rotate" else \
+        [(r, r + 1) for r in range(pp - 1)]
     for d in range(mesh.dp):
-        for r in range(pp - 1):
-            a, b = d * pp + r, d * pp + r + 1
+        for r, q in pairs:
+            a, b = d * pp + r, d * pp + q
             for src, dst in ((a, b), (b, a)):
                 g = dist.new_group([a, b], timeout=timeout)
                 if mesh.rank in (a, b):

@@ -107,18 +107,21 @@ class PipelineEngine:
         self.kind = schedule_kind
         self.M = max(1, int(num_microbatches))
         self.P = spec.num_stages
-        if self.P % mesh.pp != 0:
+        if schedule_kind != "rotate" and self.P % mesh.pp != 0:
             raise ValueError(f"{spec.name}: {self.P} stages cannot be placed on {mesh.pp} pipeline ranks")
         self.device = mesh.device
         self.dtype = dtype or spec.param_dtype
         self.debug_sync = debug_sync or os.environ.get("SDML_DEBUG_SYNC") == "1"
         self._sched_cache: Dict[Tuple[int, bool], Schedule] = {}
+        if self.kind == "rotate" and self.M % mesh.pp:
+            raise ValueError(f"rotate: micro-batches ({self.M}) must be a multiple of the ranks ({mesh.pp})")
         sched = self.schedule(self.M, False)
         self.local_pairs = sched.local_stages(mesh.pp_rank)
-        for p in range(sched.num_pipes):
-            for s in range(self.P):
-                if sched.stage_rank(p, s) == mesh.pp_rank and (p, s) not in self.local_pairs:
-                    self.local_pairs.append((p, s))
+        if self.kind != "rotate":
+            for p in range(sched.num_pipes):
+                for s in range(self.P):
+                    if sched.stage_rank(p, s) == mesh.pp_rank and (p, s) not in self.local_pairs:
+                        self.local_pairs.append((p, s))
         self.local_stage_ids = sorted({s for _, s in self.local_pairs})
         mods = build_stages(spec, self.local_stage_ids, base_seed=seed)
         self.stages: Dict[int, PipelineStage] = {}
@@ -133,6 +136,9 @@ class PipelineEngine:
         self.grad_sync = GradSync(self.flat, mesh, self.local_stage_ids)
         self.training = True
         self.global_step = 0
+        # rotate, 2 stages: run each wave's stage boundary as ONE all-to-all collective
+        # (RCCL drives all xGMI links at once; far fewer launches than per-peer p2p)
+        self.use_alltoall = os.environ.get("SDML_ROTATE_P2P") != "1"
 
     # ---------------------------------------------------------------------------------------
     def schedule(self, m: int, forward_only: bool) -> Schedule:
@@ -149,6 +155,19 @@ class PipelineEngine:
 
     def eval(self):
         return self.train(False)
+
+    @property
+    def data_shards(self) -> int:
+        """Number of disjoint per-step data shards (= samples per step / batch_size)."""
+        return self.mesh.dp * (self.mesh.pp if self.kind == "rotate" else 1)
+
+    def local_start(self, step_start: int, batch_size: int) -> int:
+        """The ``start`` to pass to :meth:`run` for a step whose global batch begins at
+        ``step_start`` (``batch_size`` samples per shard). ``rotate`` addresses its owners'
+        shards itself, so it gets the start of its replica group's block."""
+        if self.kind == "rotate":
+            return step_start + self.mesh.dp_rank * self.mesh.pp * batch_size
+        return step_start + self.mesh.dp_rank * batch_size
 
     def holds_first_stage(self) -> bool:
         return 0 in self.stages
@@ -180,14 +199,31 @@ class PipelineEngine:
                     self.global_step += 1
             z = torch.zeros(2, device=dev, dtype=torch.float32)
             return StepResult(z[0], z[1], 0, time.perf_counter() - t0)
-        sizes = split_sizes(batch_size, self.M)
+        if self.kind == "rotate" and self.use_alltoall and self.P == 2:
+            return self._run_rotate_alltoall(dataset, start, batch_size, train, global_batch, step_optimizer, t0)
+        if self.kind == "rotate":
+            # every rank owns a shard of ``batch_size`` samples at start + owner*batch_size,
+            # cut into M/R micro-batches; the schedule sends them around the ring of peers
+            R = self.mesh.pp
+            per = split_sizes(batch_size, self.M // R)
+            if len(per) * R != self.M:
+                raise ValueError(f"rotate: batch {batch_size} too small for {self.M // R} micro-batches per rank")
+            sizes, offs = [], []
+            for owner in range(R):
+                o = start + owner * batch_size
+                for sz in per:
+                    sizes.append(sz)
+                    offs.append(o)
+                    o += sz
+        else:
+            sizes = split_sizes(batch_size, self.M)
+            offs = [start]
+            for s in sizes[:-1]:
+                offs.append(offs[-1] + s)
         M = len(sizes)
-        offs = [start]
-        for s in sizes[:-1]:
-            offs.append(offs[-1] + s)
         sched = self.schedule(M, forward_only=not train)
         prog = sched.program(self.mesh.pp_rank)
-        gb = global_batch if global_batch is not None else batch_size * self.mesh.dp
+        gb = global_batch if global_batch is not None else batch_size * self.data_shards
         scale = 1.0 / float(gb)
         if self.spec.input_kind == "tokens":
             scale = scale / float(dataset.seq_len)
@@ -239,7 +275,7 @@ class PipelineEngine:
                     if x.device != dev:
                         x = x.to(dev, non_blocking=True)
                 else:
-                    prev_local = sched.stage_rank(ins.pipe, ins.stage - 1) == self.mesh.pp_rank
+                    prev_local = sched.task_rank(ins.mb, ins.stage - 1) == self.mesh.pp_rank
                     x = take((PL_ACT, ins.pipe, ins.stage - 1, ins.mb), prev_local)
                 ctx = ctxs.setdefault((ins.pipe, ins.stage, ins.mb), {})
                 if mod.is_last:
@@ -254,7 +290,7 @@ class PipelineEngine:
                 else:
                     y = mod.fwd(x, ctx, train)
                     key = (PL_ACT, ins.pipe, ins.stage, ins.mb)
-                    if sched.stage_rank(ins.pipe, ins.stage + 1) == self.mesh.pp_rank:
+                    if sched.task_rank(ins.mb, ins.stage + 1) == self.mesh.pp_rank:
                         local[key] = y
                     else:
                         outbox[key] = y
@@ -266,12 +302,12 @@ class PipelineEngine:
                 if mod.is_last:
                     gx = mod.head_bwd(ctx)
                 else:
-                    nxt_local = sched.stage_rank(ins.pipe, ins.stage + 1) == self.mesh.pp_rank
+                    nxt_local = sched.task_rank(ins.mb, ins.stage + 1) == self.mesh.pp_rank
                     gy = take((PL_GRAD, ins.pipe, ins.stage + 1, ins.mb), nxt_local)
                     gx = mod.bwd(gy, ctx)
                 if ins.stage > 0:
                     key = (PL_GRAD, ins.pipe, ins.stage, ins.mb)
-                    if sched.stage_rank(ins.pipe, ins.stage - 1) == self.mesh.pp_rank:
+                    if sched.task_rank(ins.mb, ins.stage - 1) == self.mesh.pp_rank:
                         local[key] = gx
                     else:
                         outbox[key] = gx
@@ -292,6 +328,96 @@ class PipelineEngine:
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
 
     # ---------------------------------------------------------------------------------------
+    def _run_rotate_alltoall(self, dataset, start, batch_size, train, global_batch, step_optimizer, t0):
+        """``rotate`` for a 2-stage model, boundary as all-to-all (same math as the p2p form).
+
+        Each rank owns ``batch_size`` samples at ``start + rank*batch_size``, cut into W =
+        M/R waves. Per wave: stage 0 on the own chunk -> the chunk's R parts are exchanged
+        (part k -> rank k) -> stage 1 (+ loss, + its backward) on the R parts received ->
+        input-grads exchanged back -> stage-0 backward. Waves are issued so that wave w's
+        exchange overlaps the compute of its neighbours; the collectives run on the RCCL
+        stream and only the consumer kernels wait for them.
+        """
+        mesh, dev = self.mesh, self.device
+        R, me = mesh.pp, mesh.pp_rank
+        W = max(1, self.M // R)
+        waves = split_sizes(batch_size, W)
+        gb = global_batch if global_batch is not None else batch_size * self.data_shards
+        scale = 1.0 / float(gb)
+        s0, s1 = self.stages[0], self.stages[1]
+        group = mesh.pipe_group
+        stats = torch.zeros(2, device=dev, dtype=torch.float32)
+        count = 0
+        if train:
+            self.flat.zero_grad()
+            self.flat.grads_zero = False
+            self.grad_sync.reset()
+        woff = [0]
+        for w in waves[:-1]:
+            woff.append(woff[-1] + w)
+        parts = [split_sizes(b, R) if b >= R else [b] + [0] * (R - 1) for b in waves]
+
+        def owner_part(o, w, k):  # (start, size) of part k of owner o's wave w
+            pk = parts[w]
+            return start + o * batch_size + woff[w] + sum(pk[:k]), pk[k]
+
+        ctx0 = [dict() for _ in waves]
+        recv, fwork = [None] * W, [None] * W
+        for w, bw in enumerate(waves):  # stage 0 forward + scatter of the boundary activation
+            x = dataset.inputs(start + me * batch_size + woff[w], bw)
+            if x.device != dev:
+                x = x.to(dev, non_blocking=True)
+            h = s0.fwd(x, ctx0[w], train)
+            if R == 1:
+                recv[w] = h
+                continue
+            in_splits = parts[w]
+            out_splits = [parts[w][me] for _ in range(R)]  # every owner sends me its part `me`
+            buf = torch.empty((sum(out_splits),) + tuple(h.shape[1:]), dtype=h.dtype, device=dev)
+            fwork[w] = dist.all_to_all_single(buf, h.contiguous(), out_splits, in_splits, group=group, async_op=True)
+            recv[w] = buf
+        back, bwork = [None] * W, [None] * W
+        for w in range(W):  # stage 1 (+ loss + its backward) on the received parts
+            if fwork[w] is not None:
+                fwork[w].wait()
+            tg = [dataset.targets(*owner_part(o, w, me)) for o in range(R)]
+            tgt = tg[0] if R == 1 else torch.cat(tg)
+            if tgt.device != dev:
+                tgt = tgt.to(dev, non_blocking=True)
+            if tgt.numel() == 0:
+                continue
+            c1 = {}
+            l, c, n = s1.head_fwd(recv[w], tgt, c1, train, scale, stats=stats)
+            if l is not None:
+                stats[0] += l.float()
+                stats[1] += c.float()
+            count += n
+            if not train:
+                continue
+            g = s1.head_bwd(c1)
+            if R == 1:
+                back[w] = g
+                continue
+            out_splits = parts[w]
+            in_splits = [parts[w][me] for _ in range(R)]
+            buf = torch.empty((sum(out_splits),) + tuple(g.shape[1:]), dtype=g.dtype, device=dev)
+            bwork[w] = dist.all_to_all_single(buf, g.contiguous(), out_splits, in_splits, group=group, async_op=True)
+            back[w] = buf
+        if train:
+            self.grad_sync.stage_done(1)
+            for w in range(W):  # stage 0 backward
+                if bwork[w] is not None:
+                    bwork[w].wait()
+                if back[w] is None:  # this wave had no samples for me as stage 1... still owner grads
+                    continue
+                s0.bwd(back[w], ctx0[w])
+            self.grad_sync.stage_done(0)
+            self.grad_sync.finish()
+            if step_optimizer:
+                self.optimizer.step()
+                self.global_step += 1
+        return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
+
     def reduce_metrics(self, res: StepResult, group=None) -> Tuple[float, int, int]:
         """Sum (loss, correct, count) over all last-stage holders (world). Host-syncs."""
         v = torch.stack([res.loss_sum.double(), res.correct.double(),

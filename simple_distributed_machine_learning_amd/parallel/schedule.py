@@ -9,6 +9,11 @@ Kinds:
                 pipe and the mirrored stage of the "up" pipe); fills the bubble and, for
                 a 2-stage split with a heavy first stage (the MNIST MLP: 100k of 101k
                 MACs in fc1), balances the load across both GPUs.
+* ``rotate``  — every rank owns a data shard and hosts every stage; micro-batch j of owner
+                i runs stage s on rank (i + s*j) mod R. Each stage boundary fans out over
+                ALL peers, so on an 8-GPU MI355X node the p2p traffic is spread over the 7
+                xGMI links of every GPU instead of one neighbour link (and 1/R of it stays
+                on-chip). Stage weights are replicated and all-reduced like DP.
 
 The reference is the degenerate case: 2 stages, 1 micro-batch, strictly synchronous
 (/root/reference/simple_distributed.py:108-113).
@@ -22,7 +27,7 @@ from .._native import runtime
 
 OP_FWD, OP_BWD, OP_SEND, OP_RECV = 0, 1, 2, 3
 PL_ACT, PL_GRAD = 0, 1
-KINDS = ("gpipe", "1f1b", "chimera")
+KINDS = ("gpipe", "1f1b", "chimera", "rotate")
 
 
 class Instr(NamedTuple):
@@ -56,12 +61,24 @@ class Schedule:
 
     @property
     def num_pipes(self) -> int:
+        if self.kind == "rotate":
+            return self.num_ranks
         return 2 if self.kind == "chimera" else 1
 
     def stage_rank(self, pipe: int, stage: int) -> int:
         return stage_rank(self.kind, self.num_stages, self.num_ranks, pipe, stage)
 
+    def task_rank(self, mb: int, stage: int) -> int:
+        """Rank that computes ``stage`` of micro-batch ``mb`` (mirror of the C++ rule)."""
+        if self.kind == "rotate":
+            per = self.num_microbatches // self.num_ranks
+            owner, j = divmod(mb, per)
+            return (owner + stage * j) % self.num_ranks
+        return self.stage_rank(self.mb_pipe(mb), stage)
+
     def mb_pipe(self, mb: int) -> int:
+        if self.kind == "rotate":
+            return mb // (self.num_microbatches // self.num_ranks)
         if self.num_pipes == 1:
             return 0
         half = (self.num_microbatches + 1) // 2
@@ -73,7 +90,11 @@ class Schedule:
         for ins in self.programs[pp_rank]:
             if ins.op in (OP_FWD, OP_BWD) and (ins.pipe, ins.stage) not in out:
                 out.append((ins.pipe, ins.stage))
-        if not out:  # a rank can be idle in a forward-only program with few micro-batches
+        if self.kind == "rotate":  # every rank hosts every stage
+            for s in range(self.num_stages):
+                if (pp_rank, s) not in out:
+                    out.append((pp_rank, s))
+        elif not out:  # a rank can be idle in a forward-only program with few micro-batches
             for p in range(self.num_pipes):
                 for s in range(self.num_stages):
                     if self.stage_rank(p, s) == pp_rank:

@@ -79,7 +79,7 @@ def run(args) -> dict:
     metrics = JsonlMetrics(args.metrics if mesh.is_master() else None, mesh.rank)
     master = mesh.is_master()
     B = args.batch_size
-    GB = B * mesh.dp  # one optimizer step consumes dp * B samples
+    GB = B * engine.data_shards  # one optimizer step consumes this many samples
     TB = args.test_batch_size or B
     start_epoch, start_batch = 1, 0
     if args.resume and args.ckpt_dir and os.path.exists(os.path.join(args.ckpt_dir, "stage0.pt")):
@@ -102,9 +102,15 @@ def run(args) -> dict:
         for batch_idx, start, size in batch_ranges(len(train_ds), GB, first_batch):
             if args.max_steps and batch_idx - first_batch >= args.max_steps:
                 break
-            local = min(B, max(0, size - mesh.dp_rank * B))
-            lstart = start + mesh.dp_rank * B
-            res = engine.run(train_ds, lstart, local, train=True, global_batch=size)
+            if engine.data_shards > 1 and size < GB:
+                # ragged last batch: shrink the per-shard batch (rotate needs equal shards)
+                local = size // engine.data_shards
+                if local == 0:
+                    break
+                size = local * engine.data_shards
+            else:
+                local = B
+            res = engine.run(train_ds, engine.local_start(start, local), local, train=True, global_batch=size)
             n_since += size
             last_idx = batch_idx
             if batch_idx % args.log_interval == 0:
@@ -123,9 +129,11 @@ def run(args) -> dict:
     def test():
         engine.eval()
         tot_loss, tot_correct, tot = 0.0, 0, 0
-        for _, start, size in batch_ranges(len(test_ds), TB * mesh.dp):
-            local = min(TB, max(0, size - mesh.dp_rank * TB))
-            res = engine.run(test_ds, start + mesh.dp_rank * TB, local, train=False)
+        for _, start, size in batch_ranges(len(test_ds), TB * engine.data_shards):
+            local = TB if size == TB * engine.data_shards else size // engine.data_shards
+            if local == 0:
+                continue
+            res = engine.run(test_ds, engine.local_start(start, local), local, train=False)
             l, c, n = engine.reduce_metrics(res)
             tot_loss += l
             tot_correct += c

@@ -14,19 +14,19 @@ def train_worker(rank, world, model, kind, M, pp, steps, B, seed=3, kw=None):
                      backend="gloo", timeout_s=120)
     spec = get_model_spec(model, kw.get("stages"), **{k: v for k, v in kw.items() if k != "stages"})
     eng = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=seed)
+    S = eng.data_shards
     if spec.input_kind == "tokens":
-        ds = SyntheticTokens(B * mesh.dp * steps, kw.get("seq_len", 16), 97, seed=7)
+        ds = SyntheticTokens(B * S * steps, kw.get("seq_len", 16), 97, seed=7)
     else:
-        ds = SyntheticMNIST(B * mesh.dp * steps, seed=7)
+        ds = SyntheticMNIST(B * S * steps, seed=7)
     losses = []
     for step in range(steps):
-        start = step * B * mesh.dp + mesh.dp_rank * B
-        res = eng.run(ds, start, B, train=True, global_batch=B * mesh.dp)
+        res = eng.run(ds, eng.local_start(step * B * S, B), B, train=True, global_batch=B * S)
         l, c, n = eng.reduce_metrics(res)
         losses.append(l / n)
     # one forward-only pass (eval schedule)
     eng.eval()
-    res = eng.run(ds, mesh.dp_rank * B, B, train=False)
+    res = eng.run(ds, eng.local_start(0, B), B, train=False)
     el, ec, en = eng.reduce_metrics(res)
     return {"losses": losses, "state": eng.state_dicts(), "dp_rank": mesh.dp_rank, "pp_rank": mesh.pp_rank,
             "eval": (el, ec, en), "bytes_sent": eng.transport.bytes_sent if eng.transport else 0}

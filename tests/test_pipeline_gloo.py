@@ -93,3 +93,17 @@ def test_gpt2_tiny_two_ranks():
     res = run_ranks(train_worker, 2, "gpt2_tiny", "1f1b", 2, 2, steps, B, 3, kw)
     ref = _single("gpt2_tiny", 2, steps, B, "1f1b", kw)
     _compare(res, ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("a2a", [True, False])
+@pytest.mark.parametrize("world,M", [(2, 2), (2, 4), (4, 16), (4, 8)])
+def test_mlp_rotate_matches_single_process(world, M, a2a, monkeypatch):
+    B, steps = 24, 2
+    if not a2a:
+        monkeypatch.setenv("SDML_ROTATE_P2P", "1")
+    res = run_ranks(train_worker, world, "mlp", "rotate", M, world, steps, B)
+    ref = _single("mlp", M, steps, world * B)
+    _compare(res, ref, rtol=1e-4, atol=1e-5)
+    if not a2a:
+        per_owner = M // world  # micro-batch j of an owner goes to rank owner + j: j = 0 stays local
+        assert all((r["bytes_sent"] > 0) == (per_owner > 1) for r in res)

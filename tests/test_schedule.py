@@ -10,6 +10,7 @@ from simple_distributed_machine_learning_amd.parallel.schedule import (OP_BWD, O
 CASES = [(k, P, M, R) for k in ("gpipe", "1f1b", "chimera")
          for (P, R) in [(1, 1), (2, 1), (2, 2), (4, 4), (4, 2), (8, 8), (8, 4), (6, 3)]
          for M in (1, 2, 3, 4, 8, 13)]
+CASES += [("rotate", P, M, R) for (P, R) in [(2, 1), (2, 2), (2, 4), (2, 8), (3, 4), (4, 8)] for M in (R, 2 * R, 4 * R)]
 
 
 @pytest.mark.parametrize("kind,P,M,R", CASES)
@@ -21,7 +22,7 @@ def test_build_and_validate(kind, P, M, R):
     for r, prog in enumerate(s.programs):
         for ins in prog:
             if ins.op in (OP_FWD, OP_BWD):
-                assert s.stage_rank(ins.pipe, ins.stage) == r
+                assert s.task_rank(ins.mb, ins.stage) == r
                 assert ins.pipe == s.mb_pipe(ins.mb)
                 key = (ins.op, ins.stage, ins.mb)
                 assert key not in seen
@@ -108,3 +109,12 @@ def test_bad_specs(args):
 
 def test_instr_str():
     assert str(Instr(OP_SEND, 0, 1, 3, 2, PL_ACT)) == "S0.1.3>2a"
+
+
+def test_rotate_fans_out_over_all_peers():
+    R = 8
+    s = build_schedule("rotate", 2, R * R, R)  # R micro-batches per owner: j -> rank owner+j
+    for r, prog in enumerate(s.programs):
+        peers = {i.peer for i in prog if i.op == OP_SEND and i.payload == PL_ACT}
+        assert peers == set(range(R)) - {r}  # one activation message to each other GPU
+    assert s.bubble_fraction() < 0.2

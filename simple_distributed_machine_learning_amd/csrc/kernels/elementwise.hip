@@ -2,6 +2,8 @@
 // on-device synthetic MNIST-shape data generator.
 #include <hip/hip_runtime.h>
 
+#include <hip/hip_bf16.h>
+
 #include "kernels.h"
 #include "synth_hash.h"
 
@@ -38,6 +40,43 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
   }
 }
 
+// Mixed precision: fp32 master weights + momentum, bf16 gradients in, bf16 model weights out
+// (round-to-nearest-even via the hardware cvt). One pass: 2 B (g) + 8 B (master) + 8 B (buf)
+// read/written + 2 B (p) written per element, 4 elements per lane.
+__device__ __forceinline__ float bf16_to_f32(unsigned short v) { return __uint_as_float(((unsigned)v) << 16); }
+
+__global__ void __launch_bounds__(256) sgd_mixed_kernel(float* __restrict__ master, __hip_bfloat16* __restrict__ p,
+                                                        __hip_bfloat16* __restrict__ g, float* __restrict__ buf,
+                                                        int64_t n4, float lr, float mom, float damp, float wd,
+                                                        int nesterov, int first, int zero_grad) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 mv = reinterpret_cast<f32x4*>(master)[i];
+    ushort4 gr = reinterpret_cast<ushort4*>(g)[i];
+    if (zero_grad) reinterpret_cast<ushort4*>(g)[i] = make_ushort4(0, 0, 0, 0);
+    f32x4 d = {bf16_to_f32(gr.x), bf16_to_f32(gr.y), bf16_to_f32(gr.z), bf16_to_f32(gr.w)};
+    if (wd != 0.f) d += wd * mv;
+    if (mom != 0.f) {
+      f32x4 b;
+      if (first) {
+        b = d;
+      } else {
+        b = reinterpret_cast<f32x4*>(buf)[i];
+        b = mom * b + (1.f - damp) * d;
+      }
+      reinterpret_cast<f32x4*>(buf)[i] = b;
+      d = nesterov ? d + mom * b : b;
+    }
+    mv = mv - lr * d;
+    reinterpret_cast<f32x4*>(master)[i] = mv;
+    __hip_bfloat16* pp = p + 4 * i;
+    pp[0] = __float2bfloat16(mv[0]);
+    pp[1] = __float2bfloat16(mv[1]);
+    pp[2] = __float2bfloat16(mv[2]);
+    pp[3] = __float2bfloat16(mv[3]);
+  }
+}
+
 __global__ void __launch_bounds__(256) synth_kernel(uint64_t seed, int64_t start, int64_t n, int H, int W, int mode,
                                                     float* __restrict__ x, int64_t* __restrict__ y) {
   const int D = H * W;
@@ -63,6 +102,17 @@ void sgd_momentum(float* p, float* g, float* buf, int64_t n, float lr, float mom
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, g, buf, n4, lr, momentum, dampening,
                      wd, nesterov ? 1 : 0, first ? 1 : 0, zero_grad ? 1 : 0);
+}
+
+void sgd_momentum_mixed(float* master, void* p_bf16, void* g_bf16, float* buf, int64_t n, float lr, float momentum,
+                        float dampening, float wd, bool nesterov, bool first, bool zero_grad, hipStream_t stream) {
+  const int64_t n4 = n / 4;
+  int64_t blocks = (n4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(sgd_mixed_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, master,
+                     reinterpret_cast<__hip_bfloat16*>(p_bf16), reinterpret_cast<__hip_bfloat16*>(g_bf16), buf, n4,
+                     lr, momentum, dampening, wd, nesterov ? 1 : 0, first ? 1 : 0, zero_grad ? 1 : 0);
 }
 
 void synth_mnist(uint64_t seed, int64_t start, int64_t n, int H, int W, int mode, float* x, int64_t* y,

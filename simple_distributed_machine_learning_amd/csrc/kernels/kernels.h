@@ -58,6 +58,10 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
 void sgd_momentum(float* p, float* g, float* buf, int64_t n, float lr, float momentum, float dampening,
                   float wd, bool nesterov, bool first, bool zero_grad, hipStream_t stream);
 
+// bf16 model weights with fp32 master weights: master/buf fp32, p/g bf16 (n % 4 == 0)
+void sgd_momentum_mixed(float* master, void* p_bf16, void* g_bf16, float* buf, int64_t n, float lr, float momentum,
+                        float dampening, float wd, bool nesterov, bool first, bool zero_grad, hipStream_t stream);
+
 // ---- synthetic MNIST-shape data (counter-based; bit-identical to the host generator) -----
 void synth_mnist(uint64_t seed, int64_t start, int64_t n, int H, int W, int mode, float* x, int64_t* y,
                  hipStream_t stream);

@@ -248,6 +248,24 @@ void sgd_momentum_(torch::Tensor p, torch::Tensor g, torch::Tensor buf, double l
                      (float)momentum, (float)dampening, (float)wd, nesterov, first, zero_grad, cur_stream());
 }
 
+void sgd_momentum_mixed_(torch::Tensor master, torch::Tensor p, torch::Tensor g, torch::Tensor buf, double lr,
+                         double momentum, double dampening, double wd, bool nesterov, bool first, bool zero_grad) {
+  check_f32_cuda(master, "master");
+  check_f32_cuda(buf, "buf");
+  TORCH_CHECK(p.is_cuda() && g.is_cuda() && p.scalar_type() == torch::kBFloat16 && g.scalar_type() == torch::kBFloat16,
+              "sgd_mixed: p/g must be bf16 device tensors");
+  TORCH_CHECK(p.is_contiguous() && g.is_contiguous(), "sgd_mixed: contiguous");
+  TORCH_CHECK(p.numel() == master.numel() && g.numel() == master.numel() && p.numel() % 4 == 0, "sgd_mixed: sizes");
+  TORCH_CHECK(momentum == 0 || buf.numel() == p.numel(), "sgd_mixed: momentum buffer size");
+  auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  TORCH_CHECK(al(master.data_ptr()) && al(buf.data_ptr()) && (reinterpret_cast<uintptr_t>(p.data_ptr()) & 7) == 0 &&
+                  (reinterpret_cast<uintptr_t>(g.data_ptr()) & 7) == 0,
+              "sgd_mixed: alignment");
+  sdml::sgd_momentum_mixed(master.data_ptr<float>(), p.data_ptr(), g.data_ptr(), buf.data_ptr<float>(), p.numel(),
+                           (float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, first, zero_grad,
+                           cur_stream());
+}
+
 void synth_mnist(int64_t seed, int64_t start, int64_t n, int64_t H, int64_t W, int64_t mode, torch::Tensor x,
                  torch::Tensor y) {
   check_f32_cuda(x, "x");
@@ -275,5 +293,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer", py::arg("p"), py::arg("g"),
         py::arg("buf"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"),
         py::arg("first"), py::arg("zero_grad") = false);
+  m.def("sgd_momentum_mixed_", &sgd_momentum_mixed_, "SGD: fp32 master + momentum, bf16 grads/params");
   m.def("synth_mnist", &synth_mnist, "on-device synthetic MNIST-shape data");
 }

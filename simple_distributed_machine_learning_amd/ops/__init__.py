@@ -67,3 +67,17 @@ def sgd_momentum_(p, g, buf, lr: float, momentum: float, dampening: float = 0.0,
     ref.sgd_momentum_(p, g, buf, lr, momentum, dampening, weight_decay, nesterov, first)
     if zero_grad:
         g.zero_()
+
+
+def sgd_momentum_mixed_(master, p, g, buf, lr: float, momentum: float, dampening: float = 0.0,
+                        weight_decay: float = 0.0, nesterov: bool = False, first: bool = False,
+                        zero_grad: bool = False):
+    """SGD on fp32 ``master`` weights from low-precision grads ``g``; writes ``p`` = bf16(master)."""
+    if master.is_cuda:
+        _k().sgd_momentum_mixed_(master, p, g, buf, float(lr), float(momentum), float(dampening),
+                                 float(weight_decay), bool(nesterov), bool(first), bool(zero_grad))
+        return
+    ref.sgd_momentum_(master, g.float(), buf, lr, momentum, dampening, weight_decay, nesterov, first)
+    p.copy_(master)
+    if zero_grad:
+        g.zero_()

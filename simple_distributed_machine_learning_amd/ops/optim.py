@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import torch
 
-from . import sgd_momentum_
+from . import sgd_momentum_, sgd_momentum_mixed_
 from ..utils.flat import FlatParams
 
 
@@ -23,14 +23,22 @@ class FusedSGD:
         self.flat = flat
         self.lr, self.momentum, self.dampening = lr, momentum, dampening
         self.weight_decay, self.nesterov = weight_decay, nesterov
-        self.momentum_buffer = torch.zeros_like(flat.params) if momentum != 0 else flat.params.new_zeros(64)
+        # low-precision models (bf16 GPT-2) keep fp32 master weights + fp32 momentum here
+        self.master = flat.params.float().clone() if flat.params.dtype != torch.float32 else None
+        ref = self.master if self.master is not None else flat.params
+        self.momentum_buffer = torch.zeros_like(ref) if momentum != 0 else ref.new_zeros(64)
         self.steps = 0
 
     def step(self, zero_grad: bool = True):
         """One update. ``zero_grad`` clears the gradients inside the same kernel (the engine
         then skips its own zero_grad at the next step: one launch, one pass over memory)."""
-        sgd_momentum_(self.flat.params, self.flat.grads, self.momentum_buffer, self.lr, self.momentum,
-                      self.dampening, self.weight_decay, self.nesterov, self.steps == 0, zero_grad)
+        if self.master is not None:
+            sgd_momentum_mixed_(self.master, self.flat.params, self.flat.grads, self.momentum_buffer, self.lr,
+                                self.momentum, self.dampening, self.weight_decay, self.nesterov, self.steps == 0,
+                                zero_grad)
+        else:
+            sgd_momentum_(self.flat.params, self.flat.grads, self.momentum_buffer, self.lr, self.momentum,
+                          self.dampening, self.weight_decay, self.nesterov, self.steps == 0, zero_grad)
         if zero_grad:
             self.flat.grads_zero = True
         self.steps += 1
@@ -44,12 +52,25 @@ class FusedSGD:
         for seg in self.flat.segments:
             if seg.stage == stage and self.momentum != 0:
                 bufs[seg.name] = self.momentum_buffer[seg.offset:seg.offset + seg.numel].view(seg.shape).detach().cpu().clone()
-        return {"momentum_buffer": bufs, "steps": self.steps, "lr": self.lr, "momentum": self.momentum,
-                "dampening": self.dampening, "weight_decay": self.weight_decay, "nesterov": self.nesterov}
+        out = {"momentum_buffer": bufs, "steps": self.steps, "lr": self.lr, "momentum": self.momentum,
+               "dampening": self.dampening, "weight_decay": self.weight_decay, "nesterov": self.nesterov}
+        if self.master is not None:
+            out["master"] = {seg.name: self.master[seg.offset:seg.offset + seg.numel].view(seg.shape).detach().cpu().clone()
+                             for seg in self.flat.segments if seg.stage == stage}
+        return out
 
     def load_state_dict_for_stage(self, stage: int, sd: dict):
         for seg in self.flat.segments:
             if seg.stage == stage and seg.name in sd.get("momentum_buffer", {}):
                 self.momentum_buffer[seg.offset:seg.offset + seg.numel].copy_(
                     sd["momentum_buffer"][seg.name].reshape(-1).to(self.momentum_buffer))
+        if self.master is not None:
+            for seg in self.flat.segments:
+                if seg.stage != stage:
+                    continue
+                src = sd.get("master", {}).get(seg.name)
+                dst = self.master[seg.offset:seg.offset + seg.numel]
+                # without saved master weights fall back to the (rounded) model weights
+                dst.copy_(src.reshape(-1) if src is not None else
+                          self.flat.params[seg.offset:seg.offset + seg.numel].float())
         self.steps = max(self.steps, int(sd.get("steps", 0)))

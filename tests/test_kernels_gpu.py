@@ -127,3 +127,19 @@ def test_synth_device_matches_host():
         b = SyntheticMNIST(777, seed=5, device="cpu", mode=mode, offset=123)
         assert torch.equal(a.y.cpu(), b.y)
         assert torch.equal(a.x.cpu(), b.x), (a.x.cpu() - b.x).abs().max()
+
+
+@pytest.mark.parametrize("first", [True, False])
+def test_sgd_mixed_bf16(first):
+    n = 8192 + 64
+    master = rnd(n, seed=20)
+    p = master.to(torch.bfloat16)
+    g = rnd(n, seed=21).to(torch.bfloat16)
+    buf = rnd(n, seed=22)
+    m_r, b_r, g_r = master.clone(), buf.clone(), g.float()
+    ops.sgd_momentum_mixed_(master, p, g, buf, 0.1, 0.5, 0.0, 0.0, False, first, True)
+    ref.sgd_momentum_(m_r, g_r, b_r, 0.1, 0.5, 0.0, 0.0, False, first)
+    close(master, m_r, atol=1e-6, rtol=1e-6)
+    close(buf, b_r, atol=1e-6, rtol=1e-6)
+    assert torch.equal(p, m_r.to(torch.bfloat16))
+    assert float(g.float().abs().sum()) == 0.0

@@ -58,3 +58,19 @@ def test_fused_sgd_matches_torch_sgd():
         for a, b in zip(m1.parameters(), m2.parameters()):
             torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7)
     assert float(flat.grads.abs().sum()) == 0.0  # step(zero_grad=True) cleared the grads
+
+
+def test_fused_sgd_bf16_keeps_fp32_master():
+    torch.manual_seed(3)
+    m = torch.nn.Linear(8, 8).to(torch.bfloat16)
+    flat = FlatParams([(0, m)], "cpu", dtype=torch.bfloat16)
+    opt = FusedSGD(flat, lr=1e-3, momentum=0.5)
+    assert opt.master is not None and opt.master.dtype == torch.float32
+    w0 = opt.master.clone()
+    for _ in range(3):
+        flat.zero_grad(force=True)
+        m(torch.randn(4, 8, dtype=torch.bfloat16)).float().square().sum().backward()
+        opt.step()
+    # tiny updates accumulate in the fp32 master even when they are below bf16 resolution
+    assert not torch.equal(opt.master, w0)
+    torch.testing.assert_close(flat.params, opt.master.to(torch.bfloat16), rtol=0, atol=0)

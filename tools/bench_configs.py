@@ -1,0 +1,93 @@
+"""Throughput of the BASELINE.json configs through the pipeline engine on the local GPU(s).
+
+    python tools/bench_configs.py --config mlp4x1024|resnet18|gpt2|ref_cnn [--steps N]
+    torchrun --nproc-per-node 4 tools/bench_configs.py --config mlp4x1024   # real pipeline
+
+With one process all stages are local (same schedule, local hand-offs); under torchrun the
+stages are placed on ranks (gpipe for mlp4x1024, 1f1b otherwise). Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from simple_distributed_machine_learning_amd.data import SyntheticMNIST, SyntheticTokens  # noqa: E402
+from simple_distributed_machine_learning_amd.models import DEFAULT_STAGES, get_model_spec  # noqa: E402
+from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh  # noqa: E402
+
+DEFAULTS = {  # model -> (schedule, micro-batches, batch, seq_len)
+    "mlp4x1024": ("gpipe", 8, 65536, None),
+    "resnet18": ("1f1b", 8, 512, None),
+    "gpt2": ("1f1b", 4, 16, 1024),
+    "ref_cnn": ("1f1b", 1, 60, None),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="mlp4x1024", choices=sorted(DEFAULTS))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--microbatches", type=int, default=None)
+    ap.add_argument("--seq_len", type=int, default=None)
+    a = ap.parse_args()
+    kind, M, B, S = DEFAULTS[a.config]
+    M = a.microbatches or M
+    B = a.batch or B
+    S = a.seq_len or S
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    stages = DEFAULT_STAGES[a.config]
+    pp = min(world, stages)
+    mesh = init_mesh(pp=pp, schedule_kind=kind, rank=rank, world_size=world)
+    spec = get_model_spec(a.config, stages, seq_len=S)
+    eng = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.01, momentum=0.5, seed=1)
+    dev = mesh.device
+    nb = 2
+    if spec.input_kind == "tokens":
+        ds = SyntheticTokens(B * eng.data_shards * nb, S, 50257, seed=5, device=dev)
+        unit = "tokens/s"
+        per_sample = S
+    else:
+        ds = SyntheticMNIST(B * eng.data_shards * nb, seed=5, device=dev)
+        unit = "samples/s"
+        per_sample = 1
+    GB = B * eng.data_shards
+
+    def step(i):
+        st = (i % nb) * GB
+        return eng.run(ds, eng.local_start(st, B), B, train=True, global_batch=GB)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for i in range(a.warmup):
+        step(i)
+    sync()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        res = step(i)
+    sync()
+    el = time.perf_counter() - t0
+    l, c, n = eng.reduce_metrics(res)
+    if rank == 0:
+        print(json.dumps({"config": a.config, "schedule": kind, "stages": stages, "ranks": world,
+                          "microbatches": M, "batch": GB, "seq_len": S, "dtype": str(spec.param_dtype),
+                          "value": round(GB * per_sample * a.steps / el, 1), "unit": unit,
+                          "ms_per_step": round(el / a.steps * 1e3, 3), "loss": round(l / max(1, n), 4),
+                          "bubble_model": round(eng.schedule(M, False).bubble_fraction(), 3)}))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -66,4 +66,32 @@ void sgd_momentum_mixed(float* master, void* p_bf16, void* g_bf16, float* buf, i
 void synth_mnist(uint64_t seed, int64_t start, int64_t n, int H, int W, int mode, float* x, int64_t* y,
                  hipStream_t stream);
 
+// ---- transformer (GPT-2) kernels, bf16 ----------------------------------------------------
+// per-row loss / correct (fp32) and, if dlogits != nullptr, dlogits = scale*(softmax-onehot)
+void cross_entropy_bf16(const void* logits, const int64_t* target, int rows, int V, int ld, float scale,
+                        int ignore_index, float* row_loss, float* row_ok, void* dlogits, hipStream_t stream);
+// LayerNorm over the last dim D (D % 8 == 0, D <= 4096); saves fp32 mean/rstd per row
+void layernorm_fwd_bf16(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int rows,
+                        int D, float eps, hipStream_t stream);
+// dx (bf16) and dwdb_acc[0:D] += dw, dwdb_acc[D:2D] += db (fp32); workspace: blocks * 2D floats
+int layernorm_bwd_blocks(int rows);
+void layernorm_bwd_bf16(const void* x, const void* w, const void* gy, const float* mean, const float* rstd, void* dx,
+                        float* workspace, float* dwdb_acc, float* unused, int rows, int D, hipStream_t stream);
+
+// ---- causal flash attention, bf16, head_dim 64 ------------------------------------------
+// q/k/v (and dq/dk/dv) share one strided layout [b][h][s][64] (strides sqb, sqh, sqs; d
+// contiguous) — e.g. views into the fused c_attn output; o/dout share another (sob, soh, sos).
+// lse/delta: fp32 [B*H*S] scratch (lse written by fwd, read by bwd).
+struct AttnShape {
+  const void *q = nullptr, *k = nullptr, *v = nullptr, *o = nullptr, *dout = nullptr;
+  void *out = nullptr, *dq = nullptr, *dk = nullptr, *dv = nullptr;
+  float *lse = nullptr, *delta = nullptr;
+  int B = 0, H = 0, S = 0;
+  long sqb = 0, sqh = 0, sqs = 0, sob = 0, soh = 0, sos = 0;
+  float scale = 1.f;
+  int causal = 1;
+};
+void attention_fwd_bf16(const AttnShape& s, hipStream_t stream);
+void attention_bwd_bf16(const AttnShape& s, hipStream_t stream);
+
 }  // namespace sdml

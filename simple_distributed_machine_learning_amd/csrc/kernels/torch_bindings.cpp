@@ -275,6 +275,137 @@ void synth_mnist(int64_t seed, int64_t start, int64_t n, int64_t H, int64_t W, i
                     cur_stream());
 }
 
+void check_bf16_cuda(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a ROCm device tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16, name, " must be bfloat16");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+// returns (row_loss fp32 [rows], row_correct fp32 [rows], dlogits bf16 or None)
+std::tuple<torch::Tensor, torch::Tensor, c10::optional<torch::Tensor>> cross_entropy_bf16(
+    torch::Tensor logits, torch::Tensor target, double scale, int64_t ignore_index, bool need_grad) {
+  check_bf16_cuda(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2, "logits [rows, V]");
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == torch::kInt64 && target.is_contiguous(), "target int64");
+  const int64_t rows = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(target.numel() == rows, "target size");
+  auto f = logits.options().dtype(torch::kFloat32);
+  auto loss = torch::empty({rows}, f), ok = torch::empty({rows}, f);
+  c10::optional<torch::Tensor> g;
+  if (need_grad) g = torch::empty_like(logits);
+  sdml::cross_entropy_bf16(logits.data_ptr(), target.data_ptr<int64_t>(), rows, V, V, (float)scale, (int)ignore_index,
+                           loss.data_ptr<float>(), ok.data_ptr<float>(), need_grad ? g->data_ptr() : nullptr,
+                           cur_stream());
+  return {loss, ok, g};
+}
+
+// returns (y, mean, rstd)
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> layernorm_fwd_bf16(torch::Tensor x, torch::Tensor w,
+                                                                          torch::Tensor b, double eps) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_bf16_cuda(b, "b");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && D <= 4096 && w.numel() == D && b.numel() == D, "layernorm: D % 8 == 0, D <= 4096");
+  auto y = torch::empty_like(x);
+  auto f = x.options().dtype(torch::kFloat32);
+  auto mean = torch::empty({rows}, f), rstd = torch::empty({rows}, f);
+  sdml::layernorm_fwd_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), mean.data_ptr<float>(),
+                           rstd.data_ptr<float>(), rows, D, (float)eps, cur_stream());
+  return {y, mean, rstd};
+}
+
+// returns (dx bf16, dw fp32 [D], db fp32 [D])
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> layernorm_bwd_bf16(torch::Tensor x, torch::Tensor w,
+                                                                          torch::Tensor gy, torch::Tensor mean,
+                                                                          torch::Tensor rstd) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_bf16_cuda(gy, "gy");
+  check_f32_cuda(mean, "mean");
+  check_f32_cuda(rstd, "rstd");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(gy.sizes() == x.sizes() && mean.numel() == rows && rstd.numel() == rows && w.numel() == D, "ln bwd shapes");
+  auto dx = torch::empty_like(x);
+  auto f = x.options().dtype(torch::kFloat32);
+  auto ws = torch::empty({(int64_t)sdml::layernorm_bwd_blocks(rows) * 2 * D}, f);
+  auto dwdb = torch::zeros({2 * D}, f);
+  sdml::layernorm_bwd_bf16(x.data_ptr(), w.data_ptr(), gy.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                           dx.data_ptr(), ws.data_ptr<float>(), dwdb.data_ptr<float>(), nullptr, rows, D,
+                           cur_stream());
+  return {dx, dwdb.narrow(0, 0, D), dwdb.narrow(0, D, D)};
+}
+
+// q, k, v: [B, S, H, 64] bf16 views sharing strides (d contiguous), e.g. slices of the fused
+// qkv projection. Returns (out [B, S, H, 64] contiguous, lse fp32 [B*H*S]).
+std::tuple<torch::Tensor, torch::Tensor> attention_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, double scale,
+                                                       bool causal) {
+  TORCH_CHECK(q.is_cuda() && q.scalar_type() == torch::kBFloat16, "attention: bf16 device tensors");
+  TORCH_CHECK(q.dim() == 4 && q.size(3) == 64 && q.stride(3) == 1, "attention: [B, S, H, 64] with contiguous d");
+  TORCH_CHECK(k.sizes() == q.sizes() && v.sizes() == q.sizes() && k.strides() == q.strides() &&
+                  v.strides() == q.strides(),
+              "attention: q/k/v must share shape and strides");
+  TORCH_CHECK(q.stride(2) % 8 == 0 && q.stride(1) % 8 == 0 && (reinterpret_cast<uintptr_t>(q.data_ptr()) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(k.data_ptr()) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(v.data_ptr()) & 15) == 0,
+              "attention: 16-B aligned rows required");
+  const int64_t B = q.size(0), S = q.size(1), H = q.size(2);
+  auto out = torch::empty({B, S, H, 64}, q.options());
+  auto lse = torch::empty({B * H * S}, q.options().dtype(torch::kFloat32));
+  sdml::AttnShape a;
+  a.q = q.data_ptr();
+  a.k = k.data_ptr();
+  a.v = v.data_ptr();
+  a.out = out.data_ptr();
+  a.lse = lse.data_ptr<float>();
+  a.B = B;
+  a.H = H;
+  a.S = S;
+  a.sqb = q.stride(0);
+  a.sqs = q.stride(1);
+  a.sqh = q.stride(2);
+  a.sob = out.stride(0);
+  a.sos = out.stride(1);
+  a.soh = out.stride(2);
+  a.scale = (float)scale;
+  a.causal = causal ? 1 : 0;
+  sdml::attention_fwd_bf16(a, cur_stream());
+  return {out, lse};
+}
+
+// grads written into dqkv (same strides as q/k/v views of it: pass dq, dk, dv views)
+void attention_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor out, torch::Tensor dout,
+                   torch::Tensor lse, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv, double scale, bool causal) {
+  TORCH_CHECK(out.is_contiguous() && dout.is_contiguous() && out.sizes() == dout.sizes(), "attention bwd: out/dout");
+  TORCH_CHECK(dq.strides() == q.strides() && dk.strides() == q.strides() && dv.strides() == q.strides(),
+              "attention bwd: grads must use the q/k/v strides");
+  const int64_t B = q.size(0), S = q.size(1), H = q.size(2);
+  auto delta = torch::empty({B * H * S}, q.options().dtype(torch::kFloat32));
+  sdml::AttnShape a;
+  a.q = q.data_ptr();
+  a.k = k.data_ptr();
+  a.v = v.data_ptr();
+  a.o = out.data_ptr();
+  a.dout = dout.data_ptr();
+  a.dq = dq.data_ptr();
+  a.dk = dk.data_ptr();
+  a.dv = dv.data_ptr();
+  a.lse = lse.data_ptr<float>();
+  a.delta = delta.data_ptr<float>();
+  a.B = B;
+  a.H = H;
+  a.S = S;
+  a.sqb = q.stride(0);
+  a.sqs = q.stride(1);
+  a.sqh = q.stride(2);
+  a.sob = out.stride(0);
+  a.sos = out.stride(1);
+  a.soh = out.stride(2);
+  a.scale = (float)scale;
+  a.causal = causal ? 1 : 0;
+  sdml::attention_bwd_bf16(a, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -294,5 +425,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("buf"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"),
         py::arg("first"), py::arg("zero_grad") = false);
   m.def("sgd_momentum_mixed_", &sgd_momentum_mixed_, "SGD: fp32 master + momentum, bf16 grads/params");
+  m.def("cross_entropy_bf16", &cross_entropy_bf16, "vocab cross-entropy on bf16 logits (+ dlogits)");
+  m.def("layernorm_fwd_bf16", &layernorm_fwd_bf16, "LayerNorm forward (bf16, fp32 stats)");
+  m.def("layernorm_bwd_bf16", &layernorm_bwd_bf16, "LayerNorm backward (bf16)");
+  m.def("attention_fwd", &attention_fwd, "causal flash attention forward (bf16, d=64)");
+  m.def("attention_bwd", &attention_bwd, "causal flash attention backward (bf16, d=64)");
   m.def("synth_mnist", &synth_mnist, "on-device synthetic MNIST-shape data");
 }

@@ -1,0 +1,347 @@
+// Transformer-stage kernels for the GPT-2 pipeline config (BASELINE config 5, bf16):
+//
+// * vocab cross-entropy: bf16 logits [rows, V] -> per-row loss, argmax-correct and (training)
+//   dlogits = scale * (softmax - onehot) in bf16. One read pass for max/sum (online softmax),
+//   one read+write pass for the gradient: no fp32 copy of the [rows, 50257] logits.
+// * LayerNorm forward/backward: bf16 I/O, fp32 statistics (mean, rstd saved for backward),
+//   weight/bias grads reduced per block into an fp32 slab and summed by a second pass.
+//
+// One workgroup (256 threads) per row for the vocab kernels (a 50257-wide row is 98 KiB of
+// bf16), grid-stride over rows for LayerNorm (768-wide rows, one wave per row, 16-B loads).
+#include <hip/hip_bf16.h>
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace sdml {
+namespace {
+
+typedef unsigned short u16;
+typedef u16 u16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((unsigned)v) << 16); }
+__device__ __forceinline__ u16 f2bf(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);  // RNE, NaN-preserving (hardware cvt)
+  return *reinterpret_cast<u16*>(&h);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// vocab cross-entropy
+constexpr int CE_T = 256;
+
+__global__ void __launch_bounds__(CE_T) ce_fwd_bwd_kernel(const u16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                          int rows, int V, int ld, float scale, int ignore_index,
+                                                          float* __restrict__ row_loss, float* __restrict__ row_ok,
+                                                          u16* __restrict__ dlogits) {
+  __shared__ float sm[CE_T / 64], ss[CE_T / 64];
+  __shared__ int si[CE_T / 64];
+  const int row = blockIdx.x;
+  if (row >= rows) return;
+  const u16* z = logits + (size_t)row * ld;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // pass 1: online max / sum-exp + argmax (vectorised 8 x bf16 when aligned)
+  float m = -INFINITY, s = 0.f;
+  int am = 0;
+  const bool vec = (V % 8 == 0) && (ld % 8 == 0) && ((reinterpret_cast<uintptr_t>(z) & 15) == 0);
+  auto consume = [&](float v, int idx) {
+    if (v > m) {
+      s = s * __expf(m - v) + 1.f;
+      m = v;
+      am = idx;
+    } else {
+      s += __expf(v - m);
+    }
+  };
+  if (vec) {
+    for (int i = t * 8; i < V; i += CE_T * 8) {
+      u16x8 v = *reinterpret_cast<const u16x8*>(z + i);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) consume(bf2f(v[e]), i + e);
+    }
+  } else {
+    for (int i = t; i < V; i += CE_T) consume(bf2f(z[i]), i);
+  }
+  // combine (m, s, argmax) across the wave, then across waves
+  for (int o = 32; o > 0; o >>= 1) {
+    float m2 = __shfl_xor(m, o), s2 = __shfl_xor(s, o);
+    int a2 = __shfl_xor(am, o);
+    float mn = fmaxf(m, m2);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mn));
+    if (m2 > m || (m2 == m && a2 < am)) am = a2;
+    m = mn;
+  }
+  if (lane == 0) {
+    sm[w] = m;
+    ss[w] = s;
+    si[w] = am;
+  }
+  __syncthreads();
+  float M = sm[0], S = 0.f;
+  int AM = si[0];
+  for (int i = 1; i < CE_T / 64; ++i)
+    if (sm[i] > M || (sm[i] == M && si[i] < AM)) {
+      M = sm[i];
+      AM = si[i];
+    }
+  for (int i = 0; i < CE_T / 64; ++i) S += ss[i] * __expf(sm[i] - M);
+  const float lse = M + __logf(S);
+  const int y = (int)tgt[row];
+  const bool valid = y != ignore_index && y >= 0 && y < V;
+  if (t == 0) {
+    row_loss[row] = valid ? lse - bf2f(z[y]) : 0.f;
+    row_ok[row] = (valid && AM == y) ? 1.f : 0.f;
+  }
+  if (!dlogits) return;
+  u16* g = dlogits + (size_t)row * ld;
+  const float sc = valid ? scale : 0.f;
+  if (vec) {
+    for (int i = t * 8; i < V; i += CE_T * 8) {
+      u16x8 v = *reinterpret_cast<const u16x8*>(z + i);
+      u16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float p = __expf(bf2f(v[e]) - lse);
+        o[e] = f2bf(sc * (p - (i + e == y ? 1.f : 0.f)));
+      }
+      *reinterpret_cast<u16x8*>(g + i) = o;
+    }
+  } else {
+    for (int i = t; i < V; i += CE_T) {
+      float p = __expf(bf2f(z[i]) - lse);
+      g[i] = f2bf(sc * (p - (i == y ? 1.f : 0.f)));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// LayerNorm (row width D <= 4096, D % 8 == 0): one wave per row, fp32 statistics.
+constexpr int LN_T = 256;
+// LN_MAXV = 16-B chunks per lane (template): D <= 64 lanes * 8 elems * LN_MAXV
+
+template <int LN_MAXV>
+__global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ w,
+                                                      const u16* __restrict__ b, u16* __restrict__ y,
+                                                      float* __restrict__ mean, float* __restrict__ rstd, int rows,
+                                                      int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int nch = D / 8;
+  for (int row = blockIdx.x * (LN_T / 64) + (threadIdx.x >> 6); row < rows; row += gridDim.x * (LN_T / 64)) {
+    const u16* xr = x + (size_t)row * D;
+    u16x8 v[LN_MAXV];
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < LN_MAXV; ++c) {
+      int ch = lane + 64 * c;
+      if (ch < nch) {
+        v[c] = *reinterpret_cast<const u16x8*>(xr + 8 * ch);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sum += bf2f(v[c][e]);
+      }
+    }
+    const float mu = wave_sum(sum) / D;
+    float var = 0.f;
+#pragma unroll
+    for (int c = 0; c < LN_MAXV; ++c) {
+      int ch = lane + 64 * c;
+      if (ch < nch)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float d = bf2f(v[c][e]) - mu;
+          var += d * d;
+        }
+    }
+    const float rs = rsqrtf(wave_sum(var) / D + eps);
+    if (lane == 0) {
+      mean[row] = mu;
+      rstd[row] = rs;
+    }
+    u16* yr = y + (size_t)row * D;
+#pragma unroll
+    for (int c = 0; c < LN_MAXV; ++c) {
+      int ch = lane + 64 * c;
+      if (ch < nch) {
+        u16x8 wv = *reinterpret_cast<const u16x8*>(w + 8 * ch);
+        u16x8 bv = *reinterpret_cast<const u16x8*>(b + 8 * ch);
+        u16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf((bf2f(v[c][e]) - mu) * rs * bf2f(wv[e]) + bf2f(bv[e]));
+        *reinterpret_cast<u16x8*>(yr + 8 * ch) = o;
+      }
+    }
+  }
+}
+
+// dx = rstd * (g*w - mean(g*w) - xhat * mean(g*w*xhat)); dw += g*xhat; db += g (per-block slabs)
+template <int LN_MAXV>
+__global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const u16* __restrict__ x, const u16* __restrict__ w,
+                                                      const u16* __restrict__ gy, const float* __restrict__ mean,
+                                                      const float* __restrict__ rstd, u16* __restrict__ dx,
+                                                      float* __restrict__ part, int rows, int D) {
+  const int lane = threadIdx.x & 63, wv_id = threadIdx.x >> 6;
+  const int nch = D / 8;
+  // per-thread partial dW/dB for the chunks this lane owns (reduced over the block's rows)
+  float pw[LN_MAXV][8], pb[LN_MAXV][8];
+#pragma unroll
+  for (int c = 0; c < LN_MAXV; ++c)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pw[c][e] = pb[c][e] = 0.f;
+  for (int row = blockIdx.x * (LN_T / 64) + wv_id; row < rows; row += gridDim.x * (LN_T / 64)) {
+    const u16* xr = x + (size_t)row * D;
+    const u16* gr = gy + (size_t)row * D;
+    const float mu = mean[row], rs = rstd[row];
+    float s1 = 0.f, s2 = 0.f;
+    u16x8 xv[LN_MAXV], gv[LN_MAXV];
+#pragma unroll
+    for (int c = 0; c < LN_MAXV; ++c) {
+      int ch = lane + 64 * c;
+      if (ch < nch) {
+        xv[c] = *reinterpret_cast<const u16x8*>(xr + 8 * ch);
+        gv[c] = *reinterpret_cast<const u16x8*>(gr + 8 * ch);
+        u16x8 wv = *reinterpret_cast<const u16x8*>(w + 8 * ch);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float xh = (bf2f(xv[c][e]) - mu) * rs;
+          float g = bf2f(gv[c][e]);
+          float gw = g * bf2f(wv[e]);
+          s1 += gw;
+          s2 += gw * xh;
+          pw[c][e] += g * xh;
+          pb[c][e] += g;
+        }
+      }
+    }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+    u16* dr = dx + (size_t)row * D;
+#pragma unroll
+    for (int c = 0; c < LN_MAXV; ++c) {
+      int ch = lane + 64 * c;
+      if (ch < nch) {
+        u16x8 wv = *reinterpret_cast<const u16x8*>(w + 8 * ch);
+        u16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float xh = (bf2f(xv[c][e]) - mu) * rs;
+          o[e] = f2bf(rs * (bf2f(gv[c][e]) * bf2f(wv[e]) - s1 - xh * s2));
+        }
+        *reinterpret_cast<u16x8*>(dr + 8 * ch) = o;
+      }
+    }
+  }
+  // block reduction of the 4 waves' partials through LDS, then one slab row per block
+  __shared__ float red[LN_T / 64][2 * 64 * 8];
+  float* slab = part + (size_t)blockIdx.x * 2 * D;
+#pragma unroll
+  for (int c = 0; c < LN_MAXV; ++c) {
+    int ch = lane + 64 * c;
+    if (64 * c >= nch) break;  // uniform
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[wv_id][lane * 8 + e] = pw[c][e];
+      red[wv_id][512 + lane * 8 + e] = pb[c][e];
+    }
+    __syncthreads();
+    if (wv_id == 0 && ch < nch) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float a = 0.f, bsum = 0.f;
+        for (int q = 0; q < LN_T / 64; ++q) {
+          a += red[q][lane * 8 + e];
+          bsum += red[q][512 + lane * 8 + e];
+        }
+        slab[8 * ch + e] = a;
+        slab[D + 8 * ch + e] = bsum;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// out[o] += sum_b part[b][o] (deterministic order). 64 outputs x 16 waves per block; wave w
+// sums slabs w, w+16, ... with 8 loads in flight, partials added in LDS in wave order.
+__global__ void __launch_bounds__(1024) slab_sum_kernel(const float* __restrict__ part, int nblocks, int width,
+                                                        float* __restrict__ out) {
+  __shared__ float acc[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int o = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (o < width) {
+    int b = w;
+    for (; b + 16 * 7 < nblocks; b += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(b + 16 * u) * width + o];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < nblocks; b += 16) s += part[(size_t)b * width + o];
+  }
+  acc[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && o < width) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += acc[i][lane];
+    out[o] += t;
+  }
+}
+
+}  // namespace
+
+void cross_entropy_bf16(const void* logits, const int64_t* target, int rows, int V, int ld, float scale,
+                        int ignore_index, float* row_loss, float* row_ok, void* dlogits, hipStream_t stream) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(ce_fwd_bwd_kernel, dim3(rows), dim3(CE_T), 0, stream, reinterpret_cast<const u16*>(logits),
+                     target, rows, V, ld, scale, ignore_index, row_loss, row_ok, reinterpret_cast<u16*>(dlogits));
+}
+
+int layernorm_bwd_blocks(int rows) {
+  int b = (rows + 3) / 4;
+  return b > 256 ? 256 : (b < 1 ? 1 : b);
+}
+
+void layernorm_fwd_bf16(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int rows,
+                        int D, float eps, hipStream_t stream) {
+  if (rows <= 0) return;
+  int blocks = (rows + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+#define LNF(V)                                                                                                 \
+  hipLaunchKernelGGL((ln_fwd_kernel<V>), dim3(blocks), dim3(LN_T), 0, stream, reinterpret_cast<const u16*>(x), \
+                     reinterpret_cast<const u16*>(w), reinterpret_cast<const u16*>(b), reinterpret_cast<u16*>(y), \
+                     mean, rstd, rows, D, eps)
+  if (D <= 512) LNF(1);
+  else if (D <= 1024) LNF(2);
+  else if (D <= 2048) LNF(4);
+  else LNF(8);
+#undef LNF
+}
+
+void layernorm_bwd_bf16(const void* x, const void* w, const void* gy, const float* mean, const float* rstd, void* dx,
+                        float* workspace, float* dw_acc, float* db_acc, int rows, int D, hipStream_t stream) {
+  if (rows <= 0) return;
+  const int blocks = layernorm_bwd_blocks(rows);
+#define LNB(V)                                                                                                 \
+  hipLaunchKernelGGL((ln_bwd_kernel<V>), dim3(blocks), dim3(LN_T), 0, stream, reinterpret_cast<const u16*>(x), \
+                     reinterpret_cast<const u16*>(w), reinterpret_cast<const u16*>(gy), mean, rstd,             \
+                     reinterpret_cast<u16*>(dx), workspace, rows, D)
+  if (D <= 512) LNB(1);
+  else if (D <= 1024) LNB(2);
+  else if (D <= 2048) LNB(4);
+  else LNB(8);
+#undef LNB
+  // workspace rows are [dw (D) | db (D)]; sum them separately into the two accumulators
+  hipLaunchKernelGGL(slab_sum_kernel, dim3((2 * D + 63) / 64), dim3(1024), 0, stream, workspace, blocks, 2 * D,
+                     dw_acc);
+  (void)db_acc;  // dw_acc is [2*D]: dw followed by db (caller splits)
+}
+
+}  // namespace sdml

@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .base import ModelSpec, PipelineStage
+from ..ops.transformer import LayerNorm, causal_attention, cross_entropy_sum
 
 
 @dataclass
@@ -40,16 +41,8 @@ class CausalSelfAttention(nn.Module):
         self.n_head = cfg.n_head
 
     def forward(self, x):
-        B, S, C = x.shape
-        qkv = self.c_attn(x)
-        q, k, v = qkv.split(C, dim=2)
-        h = self.n_head
-        q = q.view(B, S, h, C // h).transpose(1, 2)
-        k = k.view(B, S, h, C // h).transpose(1, 2)
-        v = v.view(B, S, h, C // h).transpose(1, 2)
-        y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
-        y = y.transpose(1, 2).contiguous().view(B, S, C)
-        return self.c_proj(y)
+        # HIP flash attention (bf16, head_dim 64) on ROCm; PyTorch SDPA elsewhere
+        return self.c_proj(causal_attention(self.c_attn(x), self.n_head))
 
 
 class MLP(nn.Module):
@@ -65,9 +58,9 @@ class MLP(nn.Module):
 class Block(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
-        self.ln_1 = nn.LayerNorm(cfg.n_embd)
+        self.ln_1 = LayerNorm(cfg.n_embd)
         self.attn = CausalSelfAttention(cfg)
-        self.ln_2 = nn.LayerNorm(cfg.n_embd)
+        self.ln_2 = LayerNorm(cfg.n_embd)
         self.mlp = MLP(cfg)
 
     def forward(self, x):
@@ -89,7 +82,7 @@ class GPT2Stage(PipelineStage):
             self.wpe = nn.Embedding(cfg.block_size, cfg.n_embd)
         self.h = nn.ModuleDict({str(i): Block(cfg) for i in range(stage_id * per, (stage_id + 1) * per)})
         if stage_id == num_stages - 1:
-            self.ln_f = nn.LayerNorm(cfg.n_embd)
+            self.ln_f = LayerNorm(cfg.n_embd)
             self.lm_head = nn.Linear(cfg.n_embd, cfg.vocab_size, bias=False)
         self._init()
 
@@ -101,6 +94,27 @@ class GPT2Stage(PipelineStage):
                 nn.init.normal_(p, 0.0, 0.02)
             elif name.endswith("bias"):
                 nn.init.zeros_(p)
+
+    # ---- last stage: fused vocab cross-entropy (no fp32 copy of the [tokens, 50257] logits) --
+    def head_fwd(self, x, target, ctx, train, loss_scale, stats=None):
+        if not train:
+            with torch.no_grad():
+                logits = self(x)
+                l, c, n, _ = cross_entropy_sum(logits.reshape(-1, logits.shape[-1]), target.reshape(-1), 1.0, False)
+            return l, c, n
+        if not self.is_first:
+            x = x.detach().requires_grad_(True)
+        with torch.enable_grad():
+            logits = self(x)
+        l, c, n, g = cross_entropy_sum(logits.detach().reshape(-1, logits.shape[-1]), target.reshape(-1),
+                                       loss_scale, True)
+        ctx["x"], ctx["logits"], ctx["glogits"] = x, logits, g.view_as(logits)
+        return l, c, n
+
+    def head_bwd(self, ctx):
+        x, logits, g = ctx.pop("x"), ctx.pop("logits"), ctx.pop("glogits")
+        torch.autograd.backward(logits, g)
+        return None if self.is_first else x.grad
 
     def forward(self, x):
         if self.stage_id == 0:

@@ -1,0 +1,112 @@
+"""Autograd wrappers of the transformer kernels (csrc/kernels/transformer.hip).
+
+On ROCm bf16 tensors they run the hand-written gfx950 kernels; anything else falls back
+to the plain PyTorch definition (CPU tests, fp32 tiny models).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .._native import kernels
+
+
+def _hip_bf16(*ts) -> bool:
+    return all(t.is_cuda and t.dtype == torch.bfloat16 for t in ts)
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        xc = x.contiguous()
+        y, mean, rstd = kernels().layernorm_fwd_bf16(xc, w, b, eps)
+        ctx.save_for_backward(xc, w, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = kernels().layernorm_bwd_bf16(x, w, gy.contiguous(), mean, rstd)
+        return dx, dw.to(w.dtype), db.to(w.dtype), None
+
+
+def layer_norm(x, w, b, eps: float = 1e-5):
+    if _hip_bf16(x, w, b) and x.shape[-1] % 8 == 0 and x.shape[-1] <= 4096:
+        return _LayerNormFn.apply(x, w, b, eps)
+    return F.layer_norm(x, (x.shape[-1],), w, b, eps)
+
+
+class LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm (same parameter names) backed by the HIP kernel for bf16 on ROCm."""
+
+    def forward(self, x):
+        return layer_norm(x, self.weight, self.bias, self.eps)
+
+
+def cross_entropy_sum(logits, target, scale: float, need_grad: bool, ignore_index: int = -100):
+    """Summed token cross-entropy on [rows, V] logits.
+
+    Returns (loss_sum, correct, count, dlogits): dlogits = scale * d(loss_sum)/dlogits in the
+    logits dtype (None unless ``need_grad``). bf16 on ROCm uses the fused single-row kernel
+    (never materialises fp32 logits)."""
+    if _hip_bf16(logits):
+        loss, ok, g = kernels().cross_entropy_bf16(logits.contiguous(), target.contiguous(), float(scale),
+                                                   ignore_index, need_grad)
+        valid = int((target != ignore_index).sum()) if ignore_index >= 0 else target.numel()
+        return loss.sum(), ok.sum(), valid, g
+    z = logits.float().detach().requires_grad_(need_grad)
+    with torch.enable_grad():
+        loss = F.cross_entropy(z, target, reduction="sum", ignore_index=ignore_index)
+    g = None
+    if need_grad:
+        (g,) = torch.autograd.grad(loss * scale, z)
+        g = g.to(logits.dtype)
+    valid = target != ignore_index
+    correct = ((z.detach().argmax(1) == target) & valid).sum()
+    return loss.detach(), correct, int(valid.sum()), g
+
+
+class _FlashAttnFn(torch.autograd.Function):
+    """Causal attention on a fused qkv projection [B, S, 3C] (HIP kernels, bf16, d = 64)."""
+
+    @staticmethod
+    def forward(ctx, qkv, n_head: int, scale: float):
+        B, S, C3 = qkv.shape
+        C = C3 // 3
+        D = C // n_head
+        qkv = qkv.contiguous()
+        q, k, v = (qkv[..., i * C:(i + 1) * C].view(B, S, n_head, D) for i in range(3))
+        out, lse = kernels().attention_fwd(q, k, v, scale, True)
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.n_head, ctx.scale = n_head, scale
+        return out.view(B, S, C)
+
+    @staticmethod
+    def backward(ctx, gout):
+        qkv, out, lse = ctx.saved_tensors
+        B, S, C3 = qkv.shape
+        C, H = C3 // 3, ctx.n_head
+        D = C // H
+        dqkv = torch.empty_like(qkv)
+        q, k, v = (qkv[..., i * C:(i + 1) * C].view(B, S, H, D) for i in range(3))
+        dq, dk, dv = (dqkv[..., i * C:(i + 1) * C].view(B, S, H, D) for i in range(3))
+        kernels().attention_bwd(q, k, v, out, gout.contiguous().view(B, S, H, D), lse, dq, dk, dv, ctx.scale, True)
+        return dqkv, None, None
+
+
+def causal_attention(qkv, n_head: int):
+    """softmax(q k^T / sqrt(d), causal) v from a fused [B, S, 3C] projection -> [B, S, C]."""
+    B, S, C3 = qkv.shape
+    C = C3 // 3
+    D = C // n_head
+    if _hip_bf16(qkv) and D == 64:
+        return _FlashAttnFn.apply(qkv, n_head, 1.0 / math.sqrt(D))
+    q, k, v = qkv.split(C, dim=2)
+    q = q.view(B, S, n_head, D).transpose(1, 2)
+    k = k.view(B, S, n_head, D).transpose(1, 2)
+    v = v.view(B, S, n_head, D).transpose(1, 2)
+    y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+    return y.transpose(1, 2).contiguous().view(B, S, C)

@@ -143,3 +143,59 @@ def test_sgd_mixed_bf16(first):
     close(buf, b_r, atol=1e-6, rtol=1e-6)
     assert torch.equal(p, m_r.to(torch.bfloat16))
     assert float(g.float().abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("rows,V", [(7, 97), (64, 50257), (33, 1000), (5, 4096)])
+def test_cross_entropy_bf16(rows, V):
+    from simple_distributed_machine_learning_amd.ops.transformer import cross_entropy_sum
+
+    z = (rnd(rows, V, seed=30) * 4).to(torch.bfloat16)
+    t = torch.randint(0, V, (rows,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+    l, c, n, g = cross_entropy_sum(z, t, 0.5, True)
+    zf = z.float().requires_grad_(True)
+    lr_ = torch.nn.functional.cross_entropy(zf, t, reduction="sum")
+    (lr_ * 0.5).backward()
+    close(l, lr_.detach(), rtol=1e-4, atol=1e-3)
+    assert int(c) == int((zf.argmax(1) == t).sum()) and n == rows
+    close(g.float(), zf.grad, rtol=2e-2, atol=2e-3)  # bf16 output rounding
+
+
+@pytest.mark.parametrize("rows,D", [(1, 768), (1000, 768), (37, 64), (8, 3072)])
+def test_layernorm_bf16(rows, D):
+    from simple_distributed_machine_learning_amd.ops.transformer import layer_norm
+
+    x = (rnd(rows, D, seed=31) * 3 + 0.5).to(torch.bfloat16).requires_grad_(True)
+    w = (1 + 0.1 * rnd(D, seed=32)).to(torch.bfloat16).requires_grad_(True)
+    b = (0.1 * rnd(D, seed=33)).to(torch.bfloat16).requires_grad_(True)
+    y = layer_norm(x, w, b)
+    gy = rnd(rows, D, seed=34).to(torch.bfloat16)
+    y.backward(gy)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (D,), wr, br, 1e-5)
+    yr.backward(gy.float())
+    close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    close(x.grad.float(), xr.grad, rtol=2e-2, atol=3e-2)
+    close(w.grad.float(), wr.grad, rtol=2e-2, atol=max(3e-2, 1e-3 * rows))
+    close(b.grad.float(), br.grad, rtol=2e-2, atol=max(3e-2, 1e-3 * rows))
+
+
+@pytest.mark.parametrize("B,S,H", [(1, 64, 1), (2, 128, 2), (1, 200, 3), (2, 1024, 12), (1, 33, 1)])
+def test_flash_attention_fwd_bwd(B, S, H):
+    from simple_distributed_machine_learning_amd.ops.transformer import causal_attention
+
+    C = 64 * H
+    qkv = (rnd(B, S, 3 * C, seed=40) * 1.5).to(torch.bfloat16).requires_grad_(True)
+    y = causal_attention(qkv, H)
+    gy = rnd(B, S, C, seed=41).to(torch.bfloat16)
+    y.backward(gy)
+    # fp32 reference (math path) on the same bf16 inputs
+    x = qkv.detach().float().requires_grad_(True)
+    q, k, v = x.split(C, dim=2)
+    q, k, v = (t.view(B, S, H, 64).transpose(1, 2) for t in (q, k, v))
+    att = (q @ k.transpose(-1, -2)) / 8.0
+    mask = torch.ones(S, S, device=DEV, dtype=torch.bool).tril()
+    att = att.masked_fill(~mask, float("-inf")).softmax(-1)
+    yr = (att @ v).transpose(1, 2).reshape(B, S, C)
+    yr.backward(gy.float())
+    close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    close(qkv.grad.float(), x.grad, rtol=5e-2, atol=5e-2)

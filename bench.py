@@ -109,7 +109,9 @@ def main():
         M = a.microbatches or (1 if n == 1 else 4)
         B = a.batch_per_gpu * pp  # per pipeline replica
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    mesh = init_mesh(pp=pp, schedule_kind=kind, timeout_s=900, rank=rank, world_size=world)
+    # rotate on a 2-stage model runs its boundary as all-to-all collectives: no p2p channels
+    mesh = init_mesh(pp=pp, schedule_kind=kind, timeout_s=900, rank=rank, world_size=world,
+                     p2p_channels=(kind != "rotate"))
     dev = mesh.device
     spec = get_model_spec(a.model, 2)
     engine = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=1)

@@ -93,7 +93,8 @@ def replica_groups_spec(world_size: int, pp: int, kind: str) -> List[List[int]]:
 
 def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = None,
               timeout_s: float = 600.0, rank: Optional[int] = None, world_size: Optional[int] = None,
-              local_rank: Optional[int] = None, device: Optional[torch.device] = None) -> Mesh:
+              local_rank: Optional[int] = None, device: Optional[torch.device] = None,
+              p2p_channels: bool = True) -> Mesh:
     """Join (or reuse) the default process group and build the dp x pp mesh.
 
     Rank/world come from arguments, else torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK).
@@ -142,6 +143,8 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
     # rotate talks to every peer of the pipeline group; the others only to neighbours
     pairs = [(r, q) for r in range(pp) for q in range(r + 1, pp)] if schedule_kind == "rotate" else \
         [(r, r + 1) for r in range(pp - 1)]
+    if not p2p_channels:
+        pairs = []
     for d in range(mesh.dp):
         for r, q in pairs:
             a, b = d * pp + r, d * pp + q

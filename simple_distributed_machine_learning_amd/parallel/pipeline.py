@@ -139,6 +139,8 @@ class PipelineEngine:
         # rotate, 2 stages: run each wave's stage boundary as ONE all-to-all collective
         # (RCCL drives all xGMI links at once; far fewer launches than per-peer p2p)
         self.use_alltoall = os.environ.get("SDML_ROTATE_P2P") != "1"
+        if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
+            raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
 
     # ---------------------------------------------------------------------------------------
     def schedule(self, m: int, forward_only: bool) -> Schedule:

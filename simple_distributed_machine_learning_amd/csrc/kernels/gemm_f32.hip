@@ -31,10 +31,15 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 128, BN = 128, BK = 32, NTHR = 256;
-constexpr int KC_PITCH = BK + 4;            // K-contiguous tile row pitch (floats)
-constexpr int TILE_FLOATS = BM * KC_PITCH;  // >= BK*BM (K-major tile)
-static_assert(BK * BM <= TILE_FLOATS, "tile size");
+constexpr int BM = 128, BN = 128, NTHR = 256;
+constexpr int BK_MAX = 32;
+template <int BK>
+struct TileCfg {
+  static constexpr int KC_PITCH = BK + 4;            // K-contiguous tile row pitch (floats)
+  static constexpr int TILE_FLOATS = BM * KC_PITCH;  // >= BK*BM (K-major tile)
+  static constexpr int NV = BM * BK / 4 / NTHR;      // float4 per thread per operand tile
+  static_assert(BK * BM <= TILE_FLOATS, "tile size");
+};
 
 struct KParams {
   const float* A;
@@ -43,6 +48,7 @@ struct KParams {
   float* C;
   const float* bias;
   float* rowsum;
+  const float* cmask;
   int M, N, K, lda, ldb, ldc;
   int epi;
   int a_vec, b_vec;  // 16-B vector loads legal for the operand
@@ -51,13 +57,14 @@ struct KParams {
 };
 
 // ---- staging ---------------------------------------------------------------------------------
-// K-contiguous operand: tile rows [r0, r0+128), k [k0, k0+32): 1024 float4, 4 per thread.
+// K-contiguous operand: tile rows [r0, r0+128), k [k0, k0+BK): NV float4 per thread.
+template <int BK>
 __device__ __forceinline__ void load_kc(const float* __restrict__ P, const float* __restrict__ mask, int ld,
-                                        int rows, int r0, int k0, int kend, bool vec, f32x4 (&v)[4]) {
+                                        int rows, int r0, int k0, int kend, bool vec, f32x4 (&v)[TileCfg<BK>::NV]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < TileCfg<BK>::NV; ++i) {
     int idx = threadIdx.x + NTHR * i;
-    int r = idx >> 3, k4 = idx & 7;
+    int r = idx / (BK / 4), k4 = idx % (BK / 4);
     int gr = r0 + r, gk = k0 + 4 * k4;
     f32x4 x = {0.f, 0.f, 0.f, 0.f};
     if (!vec) {  // unaligned / K % 4 != 0: element loads (slow path, odd shapes only)
@@ -82,20 +89,22 @@ __device__ __forceinline__ void load_kc(const float* __restrict__ P, const float
   }
 }
 
-__device__ __forceinline__ void store_kc(float* __restrict__ T, const f32x4 (&v)[4]) {
+template <int BK>
+__device__ __forceinline__ void store_kc(float* __restrict__ T, const f32x4 (&v)[TileCfg<BK>::NV]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < TileCfg<BK>::NV; ++i) {
     int idx = threadIdx.x + NTHR * i;
-    int r = idx >> 3, k4 = idx & 7;
-    *reinterpret_cast<f32x4*>(T + r * KC_PITCH + 4 * k4) = v[i];
+    int r = idx / (BK / 4), k4 = idx % (BK / 4);
+    *reinterpret_cast<f32x4*>(T + r * TileCfg<BK>::KC_PITCH + 4 * k4) = v[i];
   }
 }
 
-// K-major operand: tile k [k0, k0+32), rows [r0, r0+128): 1024 float4 along rows.
+// K-major operand: tile k [k0, k0+BK), rows [r0, r0+128): float4 along rows.
+template <int BK>
 __device__ __forceinline__ void load_km(const float* __restrict__ P, const float* __restrict__ mask, int ld,
-                                        int rows, int r0, int k0, int kend, bool vec, f32x4 (&v)[4]) {
+                                        int rows, int r0, int k0, int kend, bool vec, f32x4 (&v)[TileCfg<BK>::NV]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < TileCfg<BK>::NV; ++i) {
     int idx = threadIdx.x + NTHR * i;
     int kk = idx >> 5, r4 = idx & 31;
     int gk = k0 + kk, gr = r0 + 4 * r4;
@@ -125,9 +134,10 @@ __device__ __forceinline__ void load_km(const float* __restrict__ P, const float
   }
 }
 
-__device__ __forceinline__ void store_km(float* __restrict__ T, const f32x4 (&v)[4]) {
+template <int BK>
+__device__ __forceinline__ void store_km(float* __restrict__ T, const f32x4 (&v)[TileCfg<BK>::NV]) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < TileCfg<BK>::NV; ++i) {
     int idx = threadIdx.x + NTHR * i;
     int kk = idx >> 5, r4 = idx & 31;
     *reinterpret_cast<f32x4*>(T + kk * BM + 4 * r4) = v[i];
@@ -135,10 +145,10 @@ __device__ __forceinline__ void store_km(float* __restrict__ T, const f32x4 (&v)
 }
 
 // fragment of a 32-row sub-tile for k-group s: f[j] = X(row, k = 8s + 4h + j)
-template <bool KM>
+template <bool KM, int BK>
 __device__ __forceinline__ f32x4 frag(const float* __restrict__ T, int row, int s, int h) {
   if constexpr (!KM) {
-    return *reinterpret_cast<const f32x4*>(T + row * KC_PITCH + 8 * s + 4 * h);
+    return *reinterpret_cast<const f32x4*>(T + row * TileCfg<BK>::KC_PITCH + 8 * s + 4 * h);
   } else {
     const float* p = T + (8 * s + 4 * h) * BM + row;
     f32x4 f;
@@ -150,8 +160,11 @@ __device__ __forceinline__ f32x4 frag(const float* __restrict__ T, int row, int 
   }
 }
 
-template <bool A_KM, bool B_KM>
+template <bool A_KM, bool B_KM, int BK>
 __global__ void __launch_bounds__(NTHR, 2) gemm_f32_kernel(KParams p) {
+  constexpr int TILE_FLOATS = TileCfg<BK>::TILE_FLOATS;
+  constexpr int KC_PITCH = TileCfg<BK>::KC_PITCH;
+  constexpr int NV = TileCfg<BK>::NV;
   __shared__ __attribute__((aligned(16))) float smem[4 * TILE_FLOATS];  // [buf][A|B]
   // XCD-aware, bijective remap over ALL blocks (tiles x splits): blocks b and b+8 share an
   // XCD, so hand each XCD a contiguous run of logical ids. Logical id = split * ntiles + tile:
@@ -186,20 +199,20 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_f32_kernel(KParams p) {
   const bool do_rowsum = p.rowsum != nullptr && tn == 0;
   float rs = 0.f;  // thread's partial row-sum of A (bias gradient)
 
-  f32x4 va[4], vb[4];
+  f32x4 va[NV], vb[NV];
   auto load = [&](int k0) {
-    if constexpr (A_KM) load_km(p.A, p.amask, p.lda, p.M, m0, k0, kend, p.a_vec, va);
-    else load_kc(p.A, p.amask, p.lda, p.M, m0, k0, kend, p.a_vec, va);
-    if constexpr (B_KM) load_km(p.B, nullptr, p.ldb, p.N, n0, k0, kend, p.b_vec, vb);
-    else load_kc(p.B, nullptr, p.ldb, p.N, n0, k0, kend, p.b_vec, vb);
+    if constexpr (A_KM) load_km<BK>(p.A, p.amask, p.lda, p.M, m0, k0, kend, p.a_vec, va);
+    else load_kc<BK>(p.A, p.amask, p.lda, p.M, m0, k0, kend, p.a_vec, va);
+    if constexpr (B_KM) load_km<BK>(p.B, nullptr, p.ldb, p.N, n0, k0, kend, p.b_vec, vb);
+    else load_kc<BK>(p.B, nullptr, p.ldb, p.N, n0, k0, kend, p.b_vec, vb);
   };
   auto store = [&](int buf) {
     float* As = smem + (2 * buf) * TILE_FLOATS;
     float* Bs = As + TILE_FLOATS;
-    if constexpr (A_KM) store_km(As, va);
-    else store_kc(As, va);
-    if constexpr (B_KM) store_km(Bs, vb);
-    else store_kc(Bs, vb);
+    if constexpr (A_KM) store_km<BK>(As, va);
+    else store_kc<BK>(As, va);
+    if constexpr (B_KM) store_km<BK>(Bs, vb);
+    else store_kc<BK>(Bs, vb);
   };
 
   const int nk = (kend - kbeg + BK - 1) / BK;
@@ -225,9 +238,9 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_f32_kernel(KParams p) {
     for (int s = 0; s < BK / 8; ++s) {
       f32x4 fa[2], fb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = frag<A_KM>(As, wm * 64 + i * 32 + l32, s, h);
+      for (int i = 0; i < 2; ++i) fa[i] = frag<A_KM, BK>(As, wm * 64 + i * 32 + l32, s, h);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) fb[j] = frag<B_KM>(Bs, wn * 64 + j * 32 + l32, s, h);
+      for (int j = 0; j < 2; ++j) fb[j] = frag<B_KM, BK>(Bs, wn * 64 + j * 32 + l32, s, h);
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -260,7 +273,9 @@ __global__ void __launch_bounds__(NTHR, 2) gemm_f32_kernel(KParams p) {
         float v = acc[i][j][r];
         float* dst = p.C + (size_t)row * p.ldc + col;
         switch (p.epi) {
-          case EPI_STORE: *dst = v; break;
+          case EPI_STORE:
+            *dst = (p.cmask && p.cmask[(size_t)row * p.ldc + col] <= 0.f) ? 0.f : v;
+            break;
           case EPI_BIAS: *dst = v + bv; break;
           case EPI_BIAS_RELU: *dst = fmaxf(v + bv, 0.f); break;
           case EPI_ACCUM: *dst += v; break;
@@ -287,7 +302,11 @@ bool gemm_f32_supported(const GemmArgs& g) {
   return true;
 }
 
+static int g_variant = 0;  // 0: auto, 32: BK=32, 16: BK=16 (A/B experiments)
+void gemm_f32_set_variant(int v) { g_variant = v; }
+
 int gemm_f32_pick_splits(int M, int N, int K) {
+  constexpr int BK = BK_MAX;
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   // fill the chip with one wave of blocks (2 resident per CU = 512 slots) while keeping
   // >= 32 K-steps per split: every split adds its whole C tile with fp32 atomics
@@ -306,6 +325,7 @@ void gemm_f32(const GemmArgs& g, hipStream_t stream) {
   p.C = g.C;
   p.bias = g.bias;
   p.rowsum = g.rowsum;
+  p.cmask = g.cmask;
   p.M = g.M;
   p.N = g.N;
   p.K = g.K;
@@ -315,23 +335,31 @@ void gemm_f32(const GemmArgs& g, hipStream_t stream) {
   p.epi = g.epi;
   p.a_vec = vec_ok(g.A, g.amask, g.lda, g.a_kmajor, g.K);
   p.b_vec = vec_ok(g.B, nullptr, g.ldb, g.b_kmajor, g.K);
+  const int BK = (g_variant == 16) ? 16 : 32;
   int splits = g.splits < 1 ? 1 : g.splits;
   int kps = (g.K + splits - 1) / splits;
-  kps = (kps + BK - 1) / BK * BK;
+  kps = (kps + BK_MAX - 1) / BK_MAX * BK_MAX;
   splits = (g.K + kps - 1) / kps;
   p.kps = kps;
   p.tiles_m = (g.M + BM - 1) / BM;
   p.tiles_n = (g.N + BN - 1) / BN;
   dim3 grid(p.tiles_m * p.tiles_n, splits, 1);
   dim3 block(NTHR);
-  if (!g.a_kmajor && !g.b_kmajor)
-    hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, block, 0, stream, p);
-  else if (!g.a_kmajor && g.b_kmajor)
-    hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, block, 0, stream, p);
-  else if (g.a_kmajor && !g.b_kmajor)
-    hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, block, 0, stream, p);
-  else
-    hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, block, 0, stream, p);
+#define GEMM_LAUNCH(BKV)                                                                         \
+  if (!g.a_kmajor && !g.b_kmajor)                                                                \
+    hipLaunchKernelGGL((gemm_f32_kernel<false, false, BKV>), grid, block, 0, stream, p);        \
+  else if (!g.a_kmajor && g.b_kmajor)                                                            \
+    hipLaunchKernelGGL((gemm_f32_kernel<false, true, BKV>), grid, block, 0, stream, p);         \
+  else if (g.a_kmajor && !g.b_kmajor)                                                            \
+    hipLaunchKernelGGL((gemm_f32_kernel<true, false, BKV>), grid, block, 0, stream, p);         \
+  else                                                                                           \
+    hipLaunchKernelGGL((gemm_f32_kernel<true, true, BKV>), grid, block, 0, stream, p);
+  if (BK == 16) {
+    GEMM_LAUNCH(16)
+  } else {
+    GEMM_LAUNCH(32)
+  }
+#undef GEMM_LAUNCH
 }
 
 }  // namespace sdml

@@ -34,7 +34,7 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
                                                           const float* __restrict__ bias,
                                                           const int64_t* __restrict__ target, int M, float scale,
                                                           float* __restrict__ part, float* __restrict__ dx,
-                                                          int chunks_per_block) {
+                                                          int chunks_per_block, int mask_dx) {
   __shared__ __attribute__((aligned(16))) float xs[ROWS * XP];
   __shared__ __attribute__((aligned(16))) float ws[C * HK];
   __shared__ float bs[CMAX];
@@ -130,6 +130,13 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
           for (int c = 0; c < C; ++c) {
             f32x4 wv = *reinterpret_cast<const f32x4*>(ws + c * HK + k);
             o += dz[c] * wv;
+          }
+          if (mask_dx) {  // ReLU backward of the producing stage, fused: x = relu(z) > 0 <=> z > 0
+            f32x4 xv = *reinterpret_cast<const f32x4*>(xs + row_in * XP + k);
+            o[0] = xv[0] > 0.f ? o[0] : 0.f;
+            o[1] = xv[1] > 0.f ? o[1] : 0.f;
+            o[2] = xv[2] > 0.f ? o[2] : 0.f;
+            o[3] = xv[3] > 0.f ? o[3] : 0.f;
           }
           *reinterpret_cast<f32x4*>(dx + (size_t)grow * HK + k) = o;
         }
@@ -229,7 +236,8 @@ __global__ void __launch_bounds__(256) head_generic_kernel(const float* __restri
                                                            const float* __restrict__ bias,
                                                            const int64_t* __restrict__ target, int M, int K, int C,
                                                            float scale, float* __restrict__ stats,
-                                                           float* __restrict__ dx, float* __restrict__ dz_out) {
+                                                           float* __restrict__ dx, float* __restrict__ dz_out,
+                                                           int mask_dx) {
   __shared__ float red[8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float loss_acc = 0.f, corr_acc = 0.f;
@@ -273,7 +281,7 @@ __global__ void __launch_bounds__(256) head_generic_kernel(const float* __restri
         for (int k = lane; k < K; k += 64) {
           float o = 0.f;
           for (int c = 0; c < C; ++c) o += dz[c] * W[(size_t)c * K + k];
-          dx[(size_t)row * K + k] = o;
+          dx[(size_t)row * K + k] = (mask_dx && xr[k] <= 0.f) ? 0.f : o;
         }
     }
   }
@@ -313,22 +321,22 @@ size_t head_workspace_floats(int M, int K, int C) {
 
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K, int C,
                          float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
-                         float* workspace, hipStream_t stream) {
+                         float* workspace, bool mask_dx, hipStream_t stream) {
   if (M <= 0) return;
   if (head_fused_supported(K, C) && dz_out == nullptr && workspace != nullptr) {
     int cpb = 0, blocks = head_fused_blocks(M, &cpb);
     switch (C) {
       case 10:
         hipLaunchKernelGGL((head_fused_kernel<10>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
-                           workspace, dx, cpb);
+                           workspace, dx, cpb, mask_dx ? 1 : 0);
         break;
       case 2:
         hipLaunchKernelGGL((head_fused_kernel<2>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
-                           workspace, dx, cpb);
+                           workspace, dx, cpb, mask_dx ? 1 : 0);
         break;
       default:
         hipLaunchKernelGGL((head_fused_kernel<16>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
-                           workspace, dx, cpb);
+                           workspace, dx, cpb, mask_dx ? 1 : 0);
         break;
     }
     const int width = C * K + C + 2;
@@ -339,7 +347,7 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
   int gblocks = (M + 3) / 4;
   if (gblocks > 1024) gblocks = 1024;
   hipLaunchKernelGGL(head_generic_kernel, dim3(gblocks), dim3(256), 0, stream, x, W, b, target, M, K, C, scale, stats,
-                     dx, dz_out);
+                     dx, dz_out, mask_dx ? 1 : 0);
 }
 
 }  // namespace sdml

@@ -28,6 +28,7 @@ struct GemmArgs {
   float* C = nullptr;
   const float* bias = nullptr;
   float* rowsum = nullptr;  // if set: rowsum[m] += sum_k A(m,k)  (atomic)   — fused bias-grad
+  const float* cmask = nullptr;  // EPI_STORE only: C = acc * (cmask(m,n) > 0), cmask laid out like C
   int M = 0, N = 0, K = 0;
   int lda = 0, ldb = 0, ldc = 0;
   bool a_kmajor = false, b_kmajor = false;
@@ -39,6 +40,7 @@ struct GemmArgs {
 bool gemm_f32_supported(const GemmArgs& g);
 void gemm_f32(const GemmArgs& g, hipStream_t stream);
 int gemm_f32_pick_splits(int M, int N, int K);
+void gemm_f32_set_variant(int v);  // tuning experiments: 0 auto, 16 / 32 = K-step
 
 // ---- fused classifier head: z = x W^T + b; log_softmax; NLL; backward --------------------
 // x [M,K] fp32, W [C,K], b [C], target [M] int64. stats[0] += sum loss, stats[1] += #correct.
@@ -49,9 +51,10 @@ int gemm_f32_pick_splits(int M, int N, int K);
 // partial slabs, reduced by a second deterministic pass).
 bool head_fused_supported(int K, int C);
 size_t head_workspace_floats(int M, int K, int C);
+// mask_dx: dx *= (x > 0) — the producing stage's ReLU backward, fused (x is its output)
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K,
                          int C, float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
-                         float* workspace, hipStream_t stream);
+                         float* workspace, bool mask_dx, hipStream_t stream);
 
 // ---- SGD with momentum over a flat buffer ------------------------------------------------
 // zero_grad: also writes g = 0 after reading it (fuses the next step's zero_grad)

@@ -60,7 +60,8 @@ torch::Tensor linear_fwd_f32(torch::Tensor x, torch::Tensor w, c10::optional<tor
 //   gz = gy * (y > 0);  gw += gz^T x ; gb += colsum(gz) ; returns gz @ w if need_dx
 c10::optional<torch::Tensor> linear_bwd_f32(torch::Tensor x, c10::optional<torch::Tensor> y, torch::Tensor gy,
                                             torch::Tensor w, c10::optional<torch::Tensor> gw,
-                                            c10::optional<torch::Tensor> gb, bool need_dx, bool relu_mask) {
+                                            c10::optional<torch::Tensor> gb, bool need_dx, bool relu_mask,
+                                            bool mask_dx_by_x) {
   check_f32_cuda(x, "x");
   check_f32_cuda(gy, "gy");
   check_f32_cuda(w, "w");
@@ -126,6 +127,7 @@ c10::optional<torch::Tensor> linear_bwd_f32(torch::Tensor x, c10::optional<torch
   g.a_kmajor = false;
   g.b_kmajor = true;
   g.epi = sdml::EPI_STORE;
+  if (mask_dx_by_x) g.cmask = x.data_ptr<float>();  // dx *= (x > 0): ReLU backward of the producer
   TORCH_CHECK(sdml::gemm_f32_supported(g), "linear_bwd_f32(dX): unsupported shape/alignment");
   sdml::gemm_f32(g, s);
   return dx;
@@ -171,7 +173,8 @@ void gemm_f32_op(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool a_kmajo
 // the kernel accumulates into it (and returns it) instead of allocating a new one.
 std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
     torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor target, c10::optional<torch::Tensor> gw,
-    c10::optional<torch::Tensor> gb, double scale, bool need_dx, c10::optional<torch::Tensor> stats_acc) {
+    c10::optional<torch::Tensor> gb, double scale, bool need_dx, c10::optional<torch::Tensor> stats_acc,
+    bool mask_dx) {
   check_f32_cuda(x, "x");
   check_f32_cuda(w, "w");
   check_f32_cuda(b, "b");
@@ -197,19 +200,19 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
   if (!train) {
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
                               target.data_ptr<int64_t>(), M, K, C, (float)scale, stats.data_ptr<float>(), nullptr,
-                              nullptr, nullptr, nullptr, wsp, s);
+                              nullptr, nullptr, nullptr, wsp, false, s);
     return {stats, c10::nullopt};
   }
   auto dxt = torch::empty({M, K}, x.options());
   if (fused) {
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
                               target.data_ptr<int64_t>(), M, K, C, (float)scale, stats.data_ptr<float>(),
-                              dxt.data_ptr<float>(), opt_ptr(gw), opt_ptr(gb), nullptr, wsp, s);
+                              dxt.data_ptr<float>(), opt_ptr(gw), opt_ptr(gb), nullptr, wsp, mask_dx, s);
   } else {
     auto dz = torch::empty({M, C}, x.options());
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
                               target.data_ptr<int64_t>(), M, K, C, (float)scale, stats.data_ptr<float>(),
-                              dxt.data_ptr<float>(), nullptr, nullptr, dz.data_ptr<float>(), nullptr, s);
+                              dxt.data_ptr<float>(), nullptr, nullptr, dz.data_ptr<float>(), nullptr, mask_dx, s);
     if (opt_ptr(gw)) {
       sdml::GemmArgs g;  // gw[C,K] += dz^T x ; gb += colsum(dz)
       g.A = dz.data_ptr<float>();
@@ -414,13 +417,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("b"), py::arg("relu"));
   m.def("linear_bwd_f32", &linear_bwd_f32, "backward of linear(+relu): accumulates gw/gb, returns dx",
         py::arg("x"), py::arg("y"), py::arg("gy"), py::arg("w"), py::arg("gw"), py::arg("gb"), py::arg("need_dx"),
-        py::arg("relu_mask"));
+        py::arg("relu_mask"), py::arg("mask_dx_by_x") = false);
   m.def("gemm_f32", &gemm_f32_op, "generic fp32 MFMA GEMM", py::arg("A"), py::arg("B"), py::arg("C"),
         py::arg("a_kmajor"), py::arg("b_kmajor"), py::arg("epi"), py::arg("splits") = 1,
         py::arg("bias") = py::none(), py::arg("rowsum") = py::none());
   m.def("head_logsoftmax_nll_f32", &head_logsoftmax_nll_f32, "fused fc + log_softmax + NLL (+ backward)",
         py::arg("x"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
-        py::arg("need_dx"), py::arg("stats_acc") = py::none());
+        py::arg("need_dx"), py::arg("stats_acc") = py::none(), py::arg("mask_dx") = false);
   m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer", py::arg("p"), py::arg("g"),
         py::arg("buf"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"),
         py::arg("first"), py::arg("zero_grad") = false);
@@ -430,5 +433,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm_bwd_bf16", &layernorm_bwd_bf16, "LayerNorm backward (bf16)");
   m.def("attention_fwd", &attention_fwd, "causal flash attention forward (bf16, d=64)");
   m.def("attention_bwd", &attention_bwd, "causal flash attention backward (bf16, d=64)");
+  m.def("gemm_f32_set_variant", &sdml::gemm_f32_set_variant, "fp32 GEMM variant (tuning: 0 auto, 16, 32)");
   m.def("synth_mnist", &synth_mnist, "on-device synthetic MNIST-shape data");
 }

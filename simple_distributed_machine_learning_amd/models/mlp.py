@@ -91,6 +91,10 @@ class MLPStage(PipelineStage):
             ctx["acts"] = acts
         return x
 
+    # Fused-path boundary protocol: the gradient an MLP stage sends back is already multiplied
+    # by the ReLU mask of its input (= the previous stage's output), i.e. it is d/dz of the
+    # previous stage's last pre-activation. The mask is applied for free where the input is
+    # already in registers (head kernel, dX epilogue), and the receiving stage skips it.
     def bwd(self, grad_y, ctx):
         if "acts" not in ctx:
             return super().bwd(grad_y, ctx)
@@ -99,9 +103,9 @@ class MLPStage(PipelineStage):
         layers = self.layers()
         for i in range(len(layers) - 1, -1, -1):
             lin = layers[i]
-            # g is dL/d(post-ReLU output); the mask (out > 0) is applied inside the kernels
             need_dx = (i > 0) or (not self.is_first)
-            g = ops.linear_relu_bwd(acts[i], acts[i + 1], g, lin.weight, lin.weight.grad, lin.bias.grad, need_dx)
+            g = ops.linear_relu_bwd(acts[i], acts[i + 1], g, lin.weight, lin.weight.grad, lin.bias.grad, need_dx,
+                                    gy_masked=True, mask_dx=need_dx)
         return g
 
     def head_fwd(self, x, target, ctx, train, loss_scale, stats=None):
@@ -120,7 +124,7 @@ class MLPStage(PipelineStage):
         loss, correct, dx = ops.linear_logsoftmax_nll(
             x, head.weight, head.bias, target,
             head.weight.grad if train else None, head.bias.grad if train else None,
-            loss_scale, need_dx, stats=stats)
+            loss_scale, need_dx, stats=stats, mask_dx=need_dx)
         if train:
             ctx["acts"] = acts
             ctx["dx"] = dx
@@ -135,7 +139,7 @@ class MLPStage(PipelineStage):
         for i in range(len(layers) - 2, -1, -1):
             need_dx = (i > 0) or (not self.is_first)
             g = ops.linear_relu_bwd(acts[i], acts[i + 1], g, layers[i].weight, layers[i].weight.grad,
-                                    layers[i].bias.grad, need_dx)
+                                    layers[i].bias.grad, need_dx, gy_masked=True, mask_dx=need_dx)
         return g
 
 

@@ -30,26 +30,33 @@ def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> t
     return ref.linear_fwd(x, w, b)
 
 
-def linear_relu_bwd(x, y, gy, w, gw, gb, need_dx: bool):
+def linear_relu_bwd(x, y, gy, w, gw, gb, need_dx: bool, gy_masked: bool = False, mask_dx: bool = False):
     """Backward of y = relu(x @ w.T + b): accumulates gw += gz.T @ x, gb += sum(gz) with
-    gz = gy * (y > 0); returns gz @ w when need_dx."""
+    gz = gy * (y > 0) (``gy_masked``: gy already is gz, skip the mask); returns gz @ w when
+    need_dx, times (x > 0) when ``mask_dx`` (the producing layer's ReLU backward, fused)."""
     if x.is_cuda:
-        return _k().linear_bwd_f32(x, y, gy, w, gw, gb, need_dx, True)
-    return ref.linear_relu_bwd(x, y, gy, w, gw, gb, need_dx)
+        return _k().linear_bwd_f32(x, y, gy, w, gw, gb, need_dx, not gy_masked, mask_dx)
+    dx = ref.linear_relu_bwd(x, y, gy, w, gw, gb, need_dx)
+    if dx is not None and mask_dx:
+        dx = dx * (x > 0).to(dx.dtype)
+    return dx
 
 
-def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool, stats=None):
+def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool, stats=None, mask_dx: bool = False):
     """Fused classifier head: z = x @ w.T + b -> log_softmax -> NLL (sum) and, when grads are
     given, the full backward (gw/gb accumulated, dx returned) scaled by ``scale``.
 
     Returns (loss_sum, correct, dx). With ``stats`` (a float32 [2] tensor) the loss sum and
-    correct count are ACCUMULATED into it in-kernel and (None, None, dx) is returned."""
+    correct count are ACCUMULATED into it in-kernel and (None, None, dx) is returned.
+    ``mask_dx``: dx *= (x > 0) (fused ReLU backward of the stage that produced x)."""
     if x.is_cuda:
-        st, dx = _k().head_logsoftmax_nll_f32(x, w, b, target, gw, gb, float(scale), need_dx, stats)
+        st, dx = _k().head_logsoftmax_nll_f32(x, w, b, target, gw, gb, float(scale), need_dx, stats, mask_dx)
         if stats is not None:
             return None, None, dx
         return st[0], st[1], dx
     loss, correct, dx = ref.linear_logsoftmax_nll(x, w, b, target, gw, gb, scale, need_dx)
+    if dx is not None and mask_dx:
+        dx = dx * (x > 0).to(dx.dtype)
     if stats is not None:
         stats[0] += loss
         stats[1] += correct

@@ -199,3 +199,27 @@ def test_flash_attention_fwd_bwd(B, S, H):
     yr.backward(gy.float())
     close(y.float(), yr, rtol=2e-2, atol=2e-2)
     close(qkv.grad.float(), x.grad, rtol=5e-2, atol=5e-2)
+
+
+def test_fused_relu_mask_protocol():
+    # head: dx *= (x > 0); linear bwd: skip the gy mask, mask dx by (x > 0)
+    M, Kd, C = 1000, 128, 10
+    x = torch.relu(rnd(M, Kd, seed=50))
+    w, b = rnd(C, Kd, seed=51) * 0.1, rnd(C, seed=52)
+    t = torch.randint(0, C, (M,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+    gw, gb = torch.zeros(C, Kd, device=DEV), torch.zeros(C, device=DEV)
+    _, _, dx = ops.linear_logsoftmax_nll(x, w, b, t, gw, gb, 1.0 / M, True, mask_dx=True)
+    _, _, dx_r = ref.linear_logsoftmax_nll(x, w, b, t, gw.clone(), gb.clone(), 1.0 / M, True)
+    close(dx, dx_r * (x > 0), atol=2e-6, rtol=1e-4)
+    N, K2 = 256, 512
+    x2 = torch.relu(rnd(M, K2, seed=53))
+    w2 = rnd(N, K2, seed=54) * 0.05
+    y2 = ref.linear_relu_fwd(x2, w2, torch.zeros(N, device=DEV))
+    gz = rnd(M, N, seed=55) * (y2 > 0)
+    gw2, gb2 = torch.zeros_like(w2), torch.zeros(N, device=DEV)
+    dx2 = ops.linear_relu_bwd(x2, y2, gz, w2, gw2, gb2, True, gy_masked=True, mask_dx=True)
+    gw2r, gb2r = torch.zeros_like(w2), torch.zeros(N, device=DEV)
+    dx2r = ref.linear_relu_bwd(x2, y2, gz, w2, gw2r, gb2r, True) * (x2 > 0)
+    close(dx2, dx2r, atol=2e-4, rtol=1e-5)
+    close(gw2, gw2r, atol=5e-4, rtol=1e-5)
+    close(gb2, gb2r, atol=5e-4, rtol=1e-5)

@@ -97,4 +97,17 @@ struct AttnShape {
 void attention_fwd_bf16(const AttnShape& s, hipStream_t stream);
 void attention_bwd_bf16(const AttnShape& s, hipStream_t stream);
 
+// ---- reference CNN (MNIST), fp32, one launch per stage pass (ref_cnn.hip) ------------------
+// Dropout masks: keep iff u(seed, sample0 + n, unit) >= p, scale 1/(1-p) (drop == false: off).
+void ref_cnn_stage0_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2, float* out,
+                        int B, unsigned long long seed, unsigned sample0, float p, bool drop, hipStream_t stream);
+void ref_cnn_stage0_bwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
+                        const float* gout, int B, unsigned long long seed, unsigned sample0, float p, bool drop,
+                        float* gw1, float* gb1, float* gw2, float* gb2, hipStream_t stream);
+// stats[0] += sum NLL, stats[1] += correct; train iff dx != nullptr (then all grads accumulate)
+void ref_cnn_stage1(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
+                    const int64_t* target, int B, unsigned long long seed, unsigned sample0, float p, bool drop,
+                    float scale, float* stats, float* dx, float* gw1, float* gb1, float* gw2, float* gb2,
+                    hipStream_t stream);
+
 }  // namespace sdml

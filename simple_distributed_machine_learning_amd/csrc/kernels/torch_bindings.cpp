@@ -409,6 +409,75 @@ void attention_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Ten
   sdml::attention_bwd_bf16(a, cur_stream());
 }
 
+
+// ---- reference CNN ----------------------------------------------------------------------
+void check_cnn_params(const torch::Tensor& w1, const torch::Tensor& b1, const torch::Tensor& w2,
+                      const torch::Tensor& b2, int64_t n1, int64_t nb1, int64_t n2, int64_t nb2) {
+  check_f32_cuda(w1, "w1");
+  check_f32_cuda(b1, "b1");
+  check_f32_cuda(w2, "w2");
+  check_f32_cuda(b2, "b2");
+  TORCH_CHECK(w1.numel() == n1 && b1.numel() == nb1 && w2.numel() == n2 && b2.numel() == nb2,
+              "ref_cnn: parameter shapes do not match the reference CNN");
+}
+
+torch::Tensor ref_cnn_stage0_fwd(torch::Tensor x, torch::Tensor w1, torch::Tensor b1, torch::Tensor w2,
+                                 torch::Tensor b2, int64_t seed, int64_t sample0, double p, bool drop) {
+  check_f32_cuda(x, "x");
+  TORCH_CHECK(x.numel() % 784 == 0 && x.size(0) * 784 == x.numel(), "ref_cnn stage0: x must be [B,1,28,28]");
+  check_cnn_params(w1, b1, w2, b2, 250, 10, 5000, 20);
+  const int64_t B = x.size(0);
+  auto out = torch::empty({B, 320}, x.options());
+  sdml::ref_cnn_stage0_fwd(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(),
+                           b2.data_ptr<float>(), out.data_ptr<float>(), (int)B, (unsigned long long)seed,
+                           (unsigned)sample0, (float)p, drop, cur_stream());
+  return out;
+}
+
+void ref_cnn_stage0_bwd(torch::Tensor x, torch::Tensor w1, torch::Tensor b1, torch::Tensor w2, torch::Tensor b2,
+                        torch::Tensor gout, int64_t seed, int64_t sample0, double p, bool drop, torch::Tensor gw1,
+                        torch::Tensor gb1, torch::Tensor gw2, torch::Tensor gb2) {
+  check_f32_cuda(x, "x");
+  check_f32_cuda(gout, "gout");
+  const int64_t B = x.size(0);
+  TORCH_CHECK(x.numel() == B * 784 && gout.numel() == B * 320, "ref_cnn stage0 bwd: shape mismatch");
+  check_cnn_params(w1, b1, w2, b2, 250, 10, 5000, 20);
+  check_cnn_params(gw1, gb1, gw2, gb2, 250, 10, 5000, 20);
+  sdml::ref_cnn_stage0_bwd(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(),
+                           b2.data_ptr<float>(), gout.data_ptr<float>(), (int)B, (unsigned long long)seed,
+                           (unsigned)sample0, (float)p, drop, gw1.data_ptr<float>(), gb1.data_ptr<float>(),
+                           gw2.data_ptr<float>(), gb2.data_ptr<float>(), cur_stream());
+}
+
+// returns dx if grads are given (training), else None; loss/correct accumulate into stats[2]
+c10::optional<torch::Tensor> ref_cnn_stage1(torch::Tensor x, torch::Tensor w1, torch::Tensor b1, torch::Tensor w2,
+                                            torch::Tensor b2, torch::Tensor target, int64_t seed, int64_t sample0,
+                                            double p, bool drop, double scale, torch::Tensor stats,
+                                            c10::optional<torch::Tensor> gw1, c10::optional<torch::Tensor> gb1,
+                                            c10::optional<torch::Tensor> gw2, c10::optional<torch::Tensor> gb2) {
+  check_f32_cuda(x, "x");
+  check_f32_cuda(stats, "stats");
+  const int64_t B = x.size(0);
+  TORCH_CHECK(x.dim() == 2 && x.size(1) == 320, "ref_cnn stage1: x must be [B,320]");
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == torch::kInt64 && target.is_contiguous() &&
+                  target.numel() == B,
+              "ref_cnn stage1: target must be a contiguous int64 [B] device tensor");
+  TORCH_CHECK(stats.numel() == 2, "stats must have 2 elements");
+  check_cnn_params(w1, b1, w2, b2, 16000, 50, 500, 10);
+  const bool train = opt_ptr(gw1) != nullptr;
+  c10::optional<torch::Tensor> dx;
+  if (train) {
+    TORCH_CHECK(opt_ptr(gb1) && opt_ptr(gw2) && opt_ptr(gb2), "ref_cnn stage1: all four grads or none");
+    check_cnn_params(*gw1, *gb1, *gw2, *gb2, 16000, 50, 500, 10);
+    dx = torch::empty({B, 320}, x.options());
+  }
+  sdml::ref_cnn_stage1(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(),
+                       b2.data_ptr<float>(), target.data_ptr<int64_t>(), (int)B, (unsigned long long)seed,
+                       (unsigned)sample0, (float)p, drop, (float)scale, stats.data_ptr<float>(),
+                       train ? dx->data_ptr<float>() : nullptr, opt_ptr(gw1), opt_ptr(gb1), opt_ptr(gw2), opt_ptr(gb2),
+                       cur_stream());
+  return dx;
+}
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -434,5 +503,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention_fwd", &attention_fwd, "causal flash attention forward (bf16, d=64)");
   m.def("attention_bwd", &attention_bwd, "causal flash attention backward (bf16, d=64)");
   m.def("gemm_f32_set_variant", &sdml::gemm_f32_set_variant, "fp32 GEMM variant (tuning: 0 auto, 16, 32)");
+  m.def("ref_cnn_stage0_fwd", &ref_cnn_stage0_fwd, "reference CNN stage 0 forward (one launch)");
+  m.def("ref_cnn_stage0_bwd", &ref_cnn_stage0_bwd, "reference CNN stage 0 backward (recompute, one launch)");
+  m.def("ref_cnn_stage1", &ref_cnn_stage1, "reference CNN stage 1 forward+loss+backward (one launch)");
   m.def("synth_mnist", &synth_mnist, "on-device synthetic MNIST-shape data");
 }

@@ -13,8 +13,13 @@ Reference quirk (Appendix B.3): ``F.dropout`` in Network2 has no ``training=`` a
 it stays active during ``test()``. ``eval_dropout=True`` (default) reproduces that;
 ``False`` gives the conventional behaviour.
 
-Ops run through PyTorch (MIOpen convolutions on ROCm) in this round; the stage boundary
-tensor [mb, 320] moves over RCCL exactly like the MLP's.
+On ROCm devices each stage pass is ONE fused HIP launch (csrc/kernels/ref_cnn.hip): stage 0
+forward, stage 0 backward (recompute), and stage 1 forward+NLL+backward. At the reference's
+batch of 60 the model is launch-bound, so fusing ~30 PyTorch/MIOpen launches per step into 3
+is the whole game. Dropout masks there come from a counter hash keyed by a per-pass seed drawn
+from torch's CPU generator (so ``torch.manual_seed`` and the checkpointed RNG state still
+determine them); CPU tensors keep PyTorch's own dropout. The stage boundary tensor
+[mb, 320] moves over RCCL exactly like the MLP's.
 """
 from __future__ import annotations
 
@@ -23,6 +28,11 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .base import ModelSpec, PipelineStage
+from .. import ops
+
+
+def _draw_seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
 class Network1Stage(PipelineStage):
@@ -39,6 +49,26 @@ class Network1Stage(PipelineStage):
         z3 = F.relu(F.max_pool2d(self.conv2_drop(z2), 2))
         return z3.reshape(-1, 320)
 
+    # ---- fused HIP path (one launch each way) ---------------------------------------------
+    def fwd(self, x, ctx, train):
+        if not x.is_cuda:
+            return super().fwd(x, ctx, train)
+        x = x.float().contiguous()
+        p = self.conv2_drop.p
+        drop = train and p > 0
+        seed = _draw_seed() if drop else 0
+        y = ops.ref_cnn_stage0_fwd(x, self.conv1, self.conv2, seed, p, drop)
+        if train:
+            ctx["x"], ctx["seed"], ctx["drop"] = x, seed, drop
+        return y
+
+    def bwd(self, grad_y, ctx):
+        if "seed" not in ctx:
+            return super().bwd(grad_y, ctx)
+        ops.ref_cnn_stage0_bwd(ctx.pop("x"), self.conv1, self.conv2, grad_y, ctx.pop("seed"), self.conv2_drop.p,
+                               ctx.pop("drop"))
+        return None
+
 
 class Network2Stage(PipelineStage):
     def __init__(self, eval_dropout: bool = True, dropout: float = 0.5):
@@ -53,6 +83,26 @@ class Network2Stage(PipelineStage):
         z4 = F.dropout(F.relu(self.fc1(x)), p=self.p, training=self.training or self.eval_dropout)
         z5 = self.fc2(z4)
         return F.log_softmax(z5, dim=1)
+
+    # ---- fused HIP path: forward + NLL + full backward in one launch ------------------------
+    def head_fwd(self, x, target, ctx, train, loss_scale, stats=None):
+        if not x.is_cuda:
+            return super().head_fwd(x, target, ctx, train, loss_scale)
+        x = x.float().contiguous()
+        drop = (train or self.eval_dropout) and self.p > 0
+        seed = _draw_seed() if drop else 0
+        st = stats if stats is not None else torch.zeros(2, device=x.device)
+        dx = ops.ref_cnn_stage1(x, self.fc1, self.fc2, target, seed, self.p, drop, loss_scale, st, train)
+        if train:
+            ctx["dx"] = dx
+        if stats is not None:
+            return None, None, target.numel()
+        return st[0], st[1], target.numel()
+
+    def head_bwd(self, ctx):
+        if "dx" not in ctx:
+            return super().head_bwd(ctx)
+        return ctx.pop("dx")
 
 
 class RefCNNSingle(nn.Module):

@@ -8,6 +8,7 @@ from __future__ import annotations
 from typing import Optional
 
 import torch
+import torch.nn.functional as F
 
 from .._native import kernels
 from . import reference as ref
@@ -88,3 +89,53 @@ def sgd_momentum_mixed_(master, p, g, buf, lr: float, momentum: float, dampening
     p.copy_(master)
     if zero_grad:
         g.zero_()
+
+
+# ---- reference CNN: one launch per stage pass (csrc/kernels/ref_cnn.hip) --------------------
+def ref_cnn_stage0_fwd(x, conv1, conv2, seed: int, p: float, drop: bool, sample0: int = 0):
+    """Network1 (conv1-pool-relu-conv2-dropout2d-pool-relu-flatten) -> [B, 320]."""
+    if x.is_cuda:
+        return _k().ref_cnn_stage0_fwd(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, seed, sample0, p,
+                                       drop)
+    with torch.no_grad():
+        return ref.ref_cnn_stage0(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, seed, sample0, p, drop)
+
+
+def ref_cnn_stage0_bwd(x, conv1, conv2, gout, seed: int, p: float, drop: bool, sample0: int = 0):
+    """Accumulates conv1/conv2 weight and bias grads (recomputes the forward)."""
+    if x.is_cuda:
+        _k().ref_cnn_stage0_bwd(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, gout.contiguous(), seed,
+                                sample0, p, drop, conv1.weight.grad, conv1.bias.grad, conv2.weight.grad,
+                                conv2.bias.grad)
+        return
+    ps = [conv1.weight, conv1.bias, conv2.weight, conv2.bias]
+    leaves = [t.detach().requires_grad_(True) for t in ps]
+    with torch.enable_grad():
+        y = ref.ref_cnn_stage0(x, *leaves, seed, sample0, p, drop)
+        gs = torch.autograd.grad(y, leaves, gout)
+    for t, g in zip(ps, gs):
+        t.grad.add_(g)
+
+
+def ref_cnn_stage1(x, fc1, fc2, target, seed: int, p: float, drop: bool, scale: float, stats, train: bool,
+                   sample0: int = 0):
+    """Network2 + NLL: stats[0] += sum loss, stats[1] += correct; when ``train`` accumulates
+    fc1/fc2 grads of ``scale * sum loss`` and returns dL/dx."""
+    if x.is_cuda:
+        g = (fc1.weight.grad, fc1.bias.grad, fc2.weight.grad, fc2.bias.grad) if train else (None,) * 4
+        return _k().ref_cnn_stage1(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, target, seed, sample0, p, drop,
+                                   scale, stats, *g)
+    ps = [fc1.weight, fc1.bias, fc2.weight, fc2.bias]
+    leaves = [t.detach().requires_grad_(train) for t in ps]
+    xx = x.detach().requires_grad_(train)
+    with torch.set_grad_enabled(train):
+        logp = ref.ref_cnn_stage1_logp(xx, *leaves, seed, sample0, p, drop)
+        loss = F.nll_loss(logp, target, reduction="sum")
+    stats[0] += loss.detach()
+    stats[1] += (logp.argmax(1) == target).sum().to(stats.dtype)
+    if not train:
+        return None
+    gs = torch.autograd.grad(loss * scale, [xx] + leaves)
+    for t, g in zip(ps, gs[1:]):
+        t.grad.add_(g)
+    return gs[0]

@@ -81,3 +81,46 @@ def layernorm_fwd(x, w, b, eps: float = 1e-5):
 
 def gelu_tanh(x):
     return F.gelu(x.float(), approximate="tanh").to(x.dtype)
+
+
+# ---- reference CNN (ref_cnn.hip) ------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def dropout_keep_scale(seed: int, sample0: int, n: int, units: int, p: float) -> torch.Tensor:
+    """[n, units] float32 dropout multipliers, bit-identical to ref_cnn.hip's counter hash:
+    keep iff u(seed, sample0 + i, unit) >= p, kept units scaled by 1/(1-p)."""
+    import numpy as np
+    if p <= 0.0:
+        return torch.ones(n, units)
+    a = (np.arange(n, dtype=np.uint64) + np.uint64(sample0) + np.uint64(1))[:, None]
+    b = np.arange(units, dtype=np.uint64)[None, :] + np.uint64(7)
+    with np.errstate(over="ignore"):
+        x = (np.uint64(seed & _M64) ^ (np.uint64(0x9E3779B97F4A7C15) * a) ^ (np.uint64(0xC2B2AE3D27D4EB4F) * b))
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xFF51AFD7ED558CCD)
+        x ^= x >> np.uint64(33)
+        x *= np.uint64(0xC4CEB9FE1A85EC53)
+        x ^= x >> np.uint64(33)
+    h = (x & np.uint64(0xFFFFFFFF)) >> np.uint64(8)
+    u = h.astype(np.float32) * np.float32(1.0 / 16777216.0)
+    keep = u >= np.float32(p)
+    sc = np.float32(1.0) / (np.float32(1.0) - np.float32(p))
+    return torch.from_numpy(np.where(keep, sc, np.float32(0.0)).astype(np.float32))
+
+
+def ref_cnn_stage0(x, w1, b1, w2, b2, seed: int, sample0: int, p: float, drop: bool):
+    """Network1 forward with hash-based Dropout2d (autograd-capable)."""
+    z1 = F.relu(F.max_pool2d(F.conv2d(x, w1, b1), 2))
+    z2 = F.conv2d(z1, w2, b2)
+    if drop:
+        z2 = z2 * dropout_keep_scale(seed, sample0, x.shape[0], 20, p).to(z2.device)[:, :, None, None]
+    return F.relu(F.max_pool2d(z2, 2)).reshape(-1, 320)
+
+
+def ref_cnn_stage1_logp(x, w1, b1, w2, b2, seed: int, sample0: int, p: float, drop: bool):
+    """Network2 forward (log-probabilities) with hash-based dropout (autograd-capable)."""
+    h = F.relu(F.linear(x, w1, b1))
+    if drop:
+        h = h * dropout_keep_scale(seed, sample0, x.shape[0], 50, p).to(h.device)
+    return F.log_softmax(F.linear(h, w2, b2), dim=1)

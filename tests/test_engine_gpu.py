@@ -15,17 +15,18 @@ from simple_distributed_machine_learning_amd.parallel import PipelineEngine, ini
 DEV = torch.device("cuda", 0)
 
 
-def _engine(model, device, kind="1f1b", M=2, stages=None):
+def _engine(model, device, kind="1f1b", M=2, stages=None, **kw):
     mesh = init_mesh(pp=1, schedule_kind=kind, rank=0, world_size=1, device=device)
-    spec = get_model_spec(model, stages)
+    spec = get_model_spec(model, stages, **kw)
     return PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=3)
 
 
-@pytest.mark.parametrize("model", ["mlp", "mlp4x1024"])
+@pytest.mark.parametrize("model", ["mlp", "mlp4x1024", "ref_cnn"])
 @pytest.mark.parametrize("kind,M", [("1f1b", 1), ("1f1b", 3), ("gpipe", 4), ("chimera", 4)])
 def test_gpu_engine_matches_cpu(model, kind, M):
-    e_gpu = _engine(model, DEV, kind, M)
-    e_cpu = _engine(model, torch.device("cpu"), kind, M)
+    kw = {"dropout": 0.0} if model == "ref_cnn" else {}  # fused CNN kernels vs PyTorch, no RNG
+    e_gpu = _engine(model, DEV, kind, M, **kw)
+    e_cpu = _engine(model, torch.device("cpu"), kind, M, **kw)
     torch.testing.assert_close(e_gpu.flat.params.cpu(), e_cpu.flat.params)
     ds_g = SyntheticMNIST(600, seed=11, device=DEV)
     ds_c = SyntheticMNIST(600, seed=11, device="cpu")

@@ -223,3 +223,70 @@ def test_fused_relu_mask_protocol():
     close(dx2, dx2r, atol=2e-4, rtol=1e-5)
     close(gw2, gw2r, atol=5e-4, rtol=1e-5)
     close(gb2, gb2r, atol=5e-4, rtol=1e-5)
+
+
+# ---- reference CNN fused stages (ref_cnn.hip) vs PyTorch fp32 with the same dropout masks ----
+def _cnn_params(seed=0):
+    torch.manual_seed(seed)
+    c1, c2 = torch.nn.Conv2d(1, 10, 5), torch.nn.Conv2d(10, 20, 5)
+    f1, f2 = torch.nn.Linear(320, 50), torch.nn.Linear(50, 10)
+    mods = [m.to(DEV) for m in (c1, c2, f1, f2)]
+    for m in mods:
+        for p in m.parameters():
+            p.grad = torch.zeros_like(p)
+    return mods
+
+
+@pytest.mark.parametrize("B,drop", [(60, False), (60, True), (7, True), (130, True)])
+def test_ref_cnn_stage0(B, drop):
+    c1, c2, _, _ = _cnn_params(1)
+    x = rnd(B, 1, 28, 28, seed=2).abs()
+    seed, p = 123456789, 0.5
+    y = ops.ref_cnn_stage0_fwd(x, c1, c2, seed, p, drop)
+    ps = [t.detach().clone().requires_grad_(True) for t in (c1.weight, c1.bias, c2.weight, c2.bias)]
+    y_ref = ref.ref_cnn_stage0(x, *ps, seed, 0, p, drop)
+    close(y, y_ref.detach(), rtol=1e-5, atol=1e-5)
+    gout = rnd(B, 320, seed=3)
+    ops.ref_cnn_stage0_bwd(x, c1, c2, gout, seed, p, drop)
+    gs = torch.autograd.grad(y_ref, ps, gout)
+    for got, want in zip((c1.weight.grad, c1.bias.grad, c2.weight.grad, c2.bias.grad), gs):
+        close(got, want, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,drop,train", [(60, True, True), (60, False, True), (200, True, True),
+                                          (33, True, False)])
+def test_ref_cnn_stage1(B, drop, train):
+    _, _, f1, f2 = _cnn_params(4)
+    x = rnd(B, 320, seed=5).relu()
+    tgt = torch.randint(0, 10, (B,), generator=torch.Generator().manual_seed(6)).to(DEV)
+    seed, p, scale = 987654321, 0.5, 1.0 / B
+    stats = torch.zeros(2, device=DEV)
+    dx = ops.ref_cnn_stage1(x, f1, f2, tgt, seed, p, drop, scale, stats, train)
+    xx = x.clone().requires_grad_(True)
+    ps = [t.detach().clone().requires_grad_(True) for t in (f1.weight, f1.bias, f2.weight, f2.bias)]
+    logp = ref.ref_cnn_stage1_logp(xx, *ps, seed, 0, p, drop)
+    loss = torch.nn.functional.nll_loss(logp, tgt, reduction="sum")
+    close(stats[0], loss.detach(), rtol=1e-5, atol=1e-4)
+    assert int(stats[1]) == int((logp.argmax(1) == tgt).sum())
+    if not train:
+        assert dx is None
+        return
+    gs = torch.autograd.grad(loss * scale, [xx] + ps)
+    close(dx, gs[0], rtol=1e-4, atol=1e-6)
+    for got, want in zip((f1.weight.grad, f1.bias.grad, f2.weight.grad, f2.bias.grad), gs[1:]):
+        close(got, want, rtol=1e-4, atol=1e-5)
+
+
+def test_ref_cnn_dropout_mask_statistics():
+    # the kernel's masks: ~p dropped, whole channels in stage 0 (Dropout2d semantics)
+    c1, c2, _, _ = _cnn_params(7)
+    x = rnd(512, 1, 28, 28, seed=8).abs()
+    y0 = ops.ref_cnn_stage0_fwd(x, c1, c2, 1, 0.5, False)
+    y1 = ops.ref_cnn_stage0_fwd(x, c1, c2, 1, 0.5, True)
+    ch0 = y0.view(512, 20, 16)
+    ch1 = y1.view(512, 20, 16)
+    dropped = (ch1.abs().sum(-1) == 0) & (ch0.abs().sum(-1) > 0)
+    frac = dropped.float().sum() / (ch0.abs().sum(-1) > 0).float().sum()
+    assert 0.45 < float(frac) < 0.55
+    kept = ~dropped & (ch0.abs().sum(-1) > 0)
+    close(ch1[kept], 2 * ch0[kept], rtol=1e-5, atol=1e-5)

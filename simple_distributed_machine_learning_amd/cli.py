@@ -78,6 +78,8 @@ def add_engine_args(parser: argparse.ArgumentParser):
     g.add_argument("--no_test", action="store_true")
     g.add_argument("--profile", default=None, help="write a torch.profiler trace of a few steps here")
     g.add_argument("--debug_sync", action="store_true", help="device sync after every pipeline op")
+    g.add_argument("--graph", action="store_true",
+                   help="capture the training step in a hipGraph and replay it (ROCm, one process)")
 
 
 def build_parser() -> argparse.ArgumentParser:

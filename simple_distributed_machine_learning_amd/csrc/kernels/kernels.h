@@ -98,16 +98,23 @@ void attention_fwd_bf16(const AttnShape& s, hipStream_t stream);
 void attention_bwd_bf16(const AttnShape& s, hipStream_t stream);
 
 // ---- reference CNN (MNIST), fp32, one launch per stage pass (ref_cnn.hip) ------------------
-// Dropout masks: keep iff u(seed, sample0 + n, unit) >= p, scale 1/(1-p) (drop == false: off).
+// Dropout masks: keep iff u(seed_eff, sample0 + n, unit) >= p, scale 1/(1-p) (drop == false: off),
+// seed_eff = seed + 0x9E3779B97F4A7C15 * (*ctr) (ctr: optional device step counter).
+// Training forwards save z1 [B,1440] f32 and argmax bytes [B,ref_cnn_idx_bytes()] for the backward
+// (nullptr: inference, nothing saved). The backward takes the forward's output for the ReLU mask.
+int ref_cnn_idx_bytes();
+int ref_cnn_z1_floats();
 void ref_cnn_stage0_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2, float* out,
-                        int B, unsigned long long seed, unsigned sample0, float p, bool drop, hipStream_t stream);
-void ref_cnn_stage0_bwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
-                        const float* gout, int B, unsigned long long seed, unsigned sample0, float p, bool drop,
-                        float* gw1, float* gb1, float* gw2, float* gb2, hipStream_t stream);
+                        float* z1_save, unsigned char* idx_save, int B, unsigned long long seed, const long long* ctr,
+                        unsigned sample0, float p, bool drop, hipStream_t stream);
+void ref_cnn_stage0_bwd(const float* x, const float* w2, const float* out, const float* gout, const float* z1_save,
+                        const unsigned char* idx_save, int B, unsigned long long seed, const long long* ctr,
+                        unsigned sample0, float p, bool drop, float* gw1, float* gb1, float* gw2, float* gb2,
+                        hipStream_t stream);
 // stats[0] += sum NLL, stats[1] += correct; train iff dx != nullptr (then all grads accumulate)
 void ref_cnn_stage1(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
-                    const int64_t* target, int B, unsigned long long seed, unsigned sample0, float p, bool drop,
-                    float scale, float* stats, float* dx, float* gw1, float* gb1, float* gw2, float* gb2,
-                    hipStream_t stream);
+                    const int64_t* target, int B, unsigned long long seed, const long long* ctr, unsigned sample0,
+                    float p, bool drop, float scale, float* stats, float* dx, float* gw1, float* gb1, float* gw2,
+                    float* gb2, hipStream_t stream);
 
 }  // namespace sdml

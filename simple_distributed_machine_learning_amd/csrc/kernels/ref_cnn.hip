@@ -3,21 +3,30 @@
 //
 // Stage 0 (Network1): conv1(1->10,k5) -> maxpool2 -> relu -> conv2(10->20,k5) -> Dropout2d(p)
 //                     -> maxpool2 -> relu -> flatten(320)
-//   * cnn_s0_fwd: ONE launch, one workgroup per sample; the image, both filter banks and the
-//     12x12 intermediate live in LDS; pooling, ReLU and the per-(sample, channel) dropout mask
-//     are fused into the convolution loops (the pool is evaluated on the fly: each pooled output
-//     computes its 2x2 conv window and keeps the max).
-//   * cnn_s0_bwd: ONE launch; recomputes the (cheap) forward in LDS, routes the incoming
-//     gradient through ReLU / max-pool argmax / dropout, and accumulates dW2, db2, dW1, db1
-//     (no dX: the first stage's input is data). Per-block partials go out as one fp32 atomic per
-//     weight per block (60 blocks at the reference batch).
+//   * cnn_s0_fwd: one workgroup (512 threads) per sample. The image, both filter banks and
+//     every intermediate live in LDS. Conv1 is evaluated per pooled output: each one computes
+//     its 2x2 conv window and keeps the max and its argmax. Conv2 is register-blocked: one
+//     thread computes a full 8-wide output row, sliding a 12-value input window over 5 taps.
+//     ReLU and the per-(sample, channel) Dropout2d scale are fused in. For training, the
+//     pooled conv1 activations and both pool argmaxes (1.4K floats + 1.7K bytes per sample)
+//     are saved so that the backward does not recompute.
+//   * cnn_s0_bwd: one workgroup (1024 threads) per sample, in three phases:
+//       1. route the incoming gradient through ReLU, pool argmax and dropout into a dense
+//          conv2-output gradient held in LDS;
+//       2. dW2 over 1000 (c, ci, ky) rows, register-blocked over kx with a sliding input
+//          window; dZ1 as 4-wide strips x 2 channel halves (combined by LDS float atomics),
+//          fused with the ReLU mask;
+//       3. dW1 over the 144 argmax positions per channel (pooling makes conv1's output
+//          gradient 3/4 zeros, so those are never touched), reduced across 4-lane groups.
+//     Per-block partial weight grads go out as one fp32 atomic per weight.
 // Stage 1 (Network2): fc1(320->50) -> relu -> dropout(p) -> fc2(50->10) -> log_softmax -> NLL
 //   * cnn_s1: ONE launch for forward, loss/accuracy and the whole backward (dX, dW1, db1, dW2,
-//     db2); each workgroup handles up to 64 samples, keeps their inputs and dh in LDS and
-//     reduces dW1 = dh^T x over them before a single atomic per weight.
-// Dropout masks come from a counter hash of (seed, sample, unit): the backward regenerates the
-// forward's mask exactly, nothing is stored. At batch 60 these layers are launch-bound, so the
-// design goal is the minimum number of launches per step (3 + the optimizer), not MFMA use.
+//     db2). A workgroup handles ROWS samples (8 at small batch, so the batch spreads over many
+//     CUs) and first stages all of W1 (64 KB) in LDS. Each wave runs one sample at a time: fc1
+//     by lane-per-row dot products, softmax by wave shuffles, dX by lane-per-column walks. dW1 = dh^T x is then reduced over the
+//     block's rows before a single atomic per weight.
+// Dropout masks come from a counter hash of (seed, sample, unit). The backward regenerates the
+// forward's mask exactly, so no mask is stored.
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
@@ -28,7 +37,8 @@ namespace {
 constexpr int IMG = 28, KS = 5, C1 = 10, O1 = 24, P1 = 12, C2 = 20, O2 = 8, P2 = 4;
 constexpr int FLAT = C2 * P2 * P2;  // 320
 constexpr int HID = 50, NCLS = 10;
-constexpr int T = 256;
+constexpr int NZ1 = C1 * P1 * P1;   // 1440 pooled conv1 activations per sample
+constexpr int NIDX = NZ1 + FLAT;    // saved argmax bytes per sample (conv1 pool, conv2 pool)
 
 __device__ __forceinline__ unsigned drop_hash(unsigned long long seed, unsigned a, unsigned b) {
   unsigned long long x = seed ^ (0x9E3779B97F4A7C15ull * (a + 1)) ^ (0xC2B2AE3D27D4EB4Full * (b + 7));
@@ -39,194 +49,281 @@ __device__ __forceinline__ unsigned drop_hash(unsigned long long seed, unsigned 
   x ^= x >> 33;
   return (unsigned)x;
 }
+// per-pass seed + a device step counter (advanced inside captured hipGraphs, so replays
+// draw fresh masks): seed_eff = seed + golden * ctr  (mod 2^64)
+__device__ __forceinline__ unsigned long long eff_seed(unsigned long long seed, const long long* ctr) {
+  return ctr ? seed + 0x9E3779B97F4A7C15ull * (unsigned long long)(*ctr) : seed;
+}
 __device__ __forceinline__ float keep_scale(unsigned long long seed, unsigned a, unsigned b, float p) {
   if (p <= 0.f) return 1.f;
   float u = (float)(drop_hash(seed, a, b) >> 8) * (1.0f / 16777216.0f);
   return u >= p ? 1.f / (1.f - p) : 0.f;
 }
 
-struct S0Smem {
-  float x[IMG * IMG];
-  float w1[C1 * KS * KS];
-  float b1[C1];
-  float w2[C2 * C1 * KS * KS];
-  float b2[C2];
-  float z1[C1 * P1 * P1];      // relu(maxpool(conv1))
-  float dsc[C2];               // dropout2d scale per channel
-  unsigned char a1[C1 * P1 * P1];
-  unsigned char a2[FLAT];
-  float m2[FLAT];              // pre-relu pooled conv2 value (after dropout)
-};
+// ---------------------------------------------------------------------------------------------
+// stage 0 forward
+constexpr int TF = 512;
 
-__device__ void s0_load(S0Smem& s, const float* x, const float* w1, const float* b1, const float* w2,
-                        const float* b2) {
-  for (int i = threadIdx.x; i < IMG * IMG; i += T) s.x[i] = x[i];
-  for (int i = threadIdx.x; i < C1 * KS * KS; i += T) s.w1[i] = w1[i];
-  for (int i = threadIdx.x; i < C2 * C1 * KS * KS; i += T) s.w2[i] = w2[i];
-  if (threadIdx.x < C1) s.b1[threadIdx.x] = b1[threadIdx.x];
-  if (threadIdx.x < C2) s.b2[threadIdx.x] = b2[threadIdx.x];
-}
-
-// forward into LDS (z1, a1, a2, m2); returns nothing, out written by caller from m2
-__device__ void s0_forward(S0Smem& s, unsigned long long seed, unsigned sample, float p, bool drop) {
-  if (threadIdx.x < C2) s.dsc[threadIdx.x] = drop ? keep_scale(seed, sample, threadIdx.x, p) : 1.f;
-  for (int o = threadIdx.x; o < C1 * P1 * P1; o += T) {
+__global__ void __launch_bounds__(TF) cnn_s0_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w1,
+                                                        const float* __restrict__ b1, const float* __restrict__ w2,
+                                                        const float* __restrict__ b2, float* __restrict__ out,
+                                                        float* __restrict__ z1_save, unsigned char* __restrict__ idx_save,
+                                                        unsigned long long seed0, const long long* ctr,
+                                                        unsigned sample0, float p, int drop) {
+  __shared__ float xs[IMG * IMG];
+  __shared__ float w1s[C1 * KS * KS];
+  __shared__ float w2s[C2 * C1 * KS * KS];
+  __shared__ float z1[NZ1];
+  __shared__ float c2[C2 * O2 * O2];
+  __shared__ float dsc[C2];
+  const int n = blockIdx.x, t = threadIdx.x;
+  const float* xn = x + (size_t)n * IMG * IMG;
+  for (int i = t; i < IMG * IMG; i += TF) xs[i] = xn[i];
+  for (int i = t; i < C1 * KS * KS; i += TF) w1s[i] = w1[i];
+  for (int i = t; i < C2 * C1 * KS * KS; i += TF) w2s[i] = w2[i];
+  if (t < C2) dsc[t] = drop ? keep_scale(eff_seed(seed0, ctr), sample0 + n, t, p) : 1.f;
+  __syncthreads();
+  // conv1 -> maxpool2 (argmax) -> relu, one pooled output per item
+  for (int o = t; o < NZ1; o += TF) {
     const int c = o / (P1 * P1), py = (o / P1) % P1, px = o % P1;
-    float best = -INFINITY;
+    float win[6][6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) win[r][q] = xs[(2 * py + r) * IMG + 2 * px + q];
+    float acc[4];
+    const float bias = b1[c];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[d] = bias;
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) {
+        const float w = w1s[(c * KS + ky) * KS + kx];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) acc[d] += w * win[(d >> 1) + ky][(d & 1) + kx];
+      }
+    float best = acc[0];
     int arg = 0;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const int y0 = 2 * py + (d >> 1), x0 = 2 * px + (d & 1);
-      float acc = s.b1[c];
-#pragma unroll
-      for (int ky = 0; ky < KS; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < KS; ++kx) acc += s.w1[(c * KS + ky) * KS + kx] * s.x[(y0 + ky) * IMG + x0 + kx];
-      if (acc > best) {
-        best = acc;
+    for (int d = 1; d < 4; ++d)
+      if (acc[d] > best) {
+        best = acc[d];
         arg = d;
       }
+    const float v = fmaxf(best, 0.f);
+    z1[o] = v;
+    if (z1_save) {
+      z1_save[(size_t)n * NZ1 + o] = v;
+      idx_save[(size_t)n * NIDX + o] = (unsigned char)arg;
     }
-    s.z1[o] = fmaxf(best, 0.f);
-    s.a1[o] = (unsigned char)arg;
   }
   __syncthreads();
-  for (int o = threadIdx.x; o < FLAT; o += T) {
+  // conv2 (+ dropout2d scale): one output row (c, y) of 8 per item, sliding window over kx
+  for (int it = t; it < C2 * O2; it += TF) {
+    const int c = it / O2, y = it % O2;
+    float acc[O2];
+#pragma unroll
+    for (int xo = 0; xo < O2; ++xo) acc[xo] = 0.f;
+    for (int ci = 0; ci < C1; ++ci)
+#pragma unroll
+      for (int ky = 0; ky < KS; ++ky) {
+        const float* zr = z1 + (ci * P1 + y + ky) * P1;
+        const float* wr = w2s + ((c * C1 + ci) * KS + ky) * KS;
+        float zv[P1], wv[KS];
+#pragma unroll
+        for (int q = 0; q < P1; ++q) zv[q] = zr[q];
+#pragma unroll
+        for (int kx = 0; kx < KS; ++kx) wv[kx] = wr[kx];
+#pragma unroll
+        for (int xo = 0; xo < O2; ++xo)
+#pragma unroll
+          for (int kx = 0; kx < KS; ++kx) acc[xo] += wv[kx] * zv[xo + kx];
+      }
+    const float bias = b2[c], sc = dsc[c];
+#pragma unroll
+    for (int xo = 0; xo < O2; ++xo) c2[(c * O2 + y) * O2 + xo] = (acc[xo] + bias) * sc;  // Dropout2d before pool (:45)
+  }
+  __syncthreads();
+  // maxpool2 (argmax) -> relu -> flatten
+  for (int o = t; o < FLAT; o += TF) {
     const int c = o / (P2 * P2), py = (o / P2) % P2, px = o % P2;
-    const float sc = s.dsc[c];
     float best = -INFINITY;
     int arg = 0;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      const int y0 = 2 * py + (d >> 1), x0 = 2 * px + (d & 1);
-      float acc = s.b2[c];
-      for (int ci = 0; ci < C1; ++ci)
-#pragma unroll
-        for (int ky = 0; ky < KS; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < KS; ++kx)
-            acc += s.w2[((c * C1 + ci) * KS + ky) * KS + kx] * s.z1[(ci * P1 + y0 + ky) * P1 + x0 + kx];
-      const float v = acc * sc;  // Dropout2d before the pool (reference order, :45)
+      const float v = c2[(c * O2 + 2 * py + (d >> 1)) * O2 + 2 * px + (d & 1)];
       if (v > best) {
         best = v;
         arg = d;
       }
     }
-    s.m2[o] = best;
-    s.a2[o] = (unsigned char)arg;
+    out[(size_t)n * FLAT + o] = fmaxf(best, 0.f);
+    if (idx_save) idx_save[(size_t)n * NIDX + NZ1 + o] = (unsigned char)arg;
   }
-  __syncthreads();
 }
 
-__global__ void __launch_bounds__(T) cnn_s0_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w1,
-                                                       const float* __restrict__ b1, const float* __restrict__ w2,
-                                                       const float* __restrict__ b2, float* __restrict__ out,
-                                                       unsigned long long seed, unsigned sample0, float p, int drop) {
-  __shared__ S0Smem s;
-  const int n = blockIdx.x;
-  s0_load(s, x + (size_t)n * IMG * IMG, w1, b1, w2, b2);
-  __syncthreads();
-  s0_forward(s, seed, sample0 + n, p, drop != 0);
-  for (int o = threadIdx.x; o < FLAT; o += T) out[(size_t)n * FLAT + o] = fmaxf(s.m2[o], 0.f);
-}
+// ---------------------------------------------------------------------------------------------
+// stage 0 backward (uses the forward's saved z1 / argmaxes and its output for the ReLU mask)
+constexpr int TB = 1024;
 
-__global__ void __launch_bounds__(T) cnn_s0_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w1,
-                                                       const float* __restrict__ b1, const float* __restrict__ w2,
-                                                       const float* __restrict__ b2, const float* __restrict__ gout,
-                                                       unsigned long long seed, unsigned sample0, float p, int drop,
-                                                       float* __restrict__ gw1, float* __restrict__ gb1,
-                                                       float* __restrict__ gw2, float* __restrict__ gb2) {
-  __shared__ S0Smem s;
+__global__ void __launch_bounds__(TB) cnn_s0_bwd_kernel(const float* __restrict__ x, const float* __restrict__ w2,
+                                                        const float* __restrict__ out, const float* __restrict__ gout,
+                                                        const float* __restrict__ z1_save,
+                                                        const unsigned char* __restrict__ idx_save,
+                                                        unsigned long long seed0, const long long* ctr,
+                                                        unsigned sample0, float p, int drop, float* __restrict__ gw1,
+                                                        float* __restrict__ gb1, float* __restrict__ gw2,
+                                                        float* __restrict__ gb2) {
+  __shared__ float xs[IMG * IMG];
+  __shared__ float w2s[C2 * C1 * KS * KS];
+  __shared__ float z1[NZ1];
   __shared__ float G2[C2 * O2 * O2];
-  __shared__ float G1[C1 * O1 * O1];
-  const int n = blockIdx.x;
-  s0_load(s, x + (size_t)n * IMG * IMG, w1, b1, w2, b2);
-  for (int i = threadIdx.x; i < C2 * O2 * O2; i += T) G2[i] = 0.f;
-  for (int i = threadIdx.x; i < C1 * O1 * O1; i += T) G1[i] = 0.f;
+  __shared__ float g1[NZ1];  // d loss / d (pooled conv1 output), ReLU-masked
+  __shared__ unsigned char a1[NZ1];
+  __shared__ float dsc[C2];
+  const int n = blockIdx.x, t = threadIdx.x;
+  const float* xn = x + (size_t)n * IMG * IMG;
+  for (int i = t; i < IMG * IMG; i += TB) xs[i] = xn[i];
+  for (int i = t; i < C2 * C1 * KS * KS; i += TB) w2s[i] = w2[i];
+  for (int i = t; i < NZ1; i += TB) {
+    z1[i] = z1_save[(size_t)n * NZ1 + i];
+    a1[i] = idx_save[(size_t)n * NIDX + i];
+  }
+  for (int i = t; i < C2 * O2 * O2; i += TB) G2[i] = 0.f;
+  for (int i = t; i < NZ1; i += TB) g1[i] = 0.f;
+  if (t < C2) dsc[t] = drop ? keep_scale(eff_seed(seed0, ctr), sample0 + n, t, p) : 1.f;
   __syncthreads();
-  s0_forward(s, seed, sample0 + n, p, drop != 0);
-  // relu -> maxpool2 (argmax) -> dropout2d scale: gradient of the conv2 output
-  for (int o = threadIdx.x; o < FLAT; o += T) {
+  // 1. relu (out > 0 <=> pooled pre-relu > 0) -> pool argmax -> dropout scale
+  for (int o = t; o < FLAT; o += TB) {
     const int c = o / (P2 * P2), py = (o / P2) % P2, px = o % P2;
-    const float g = s.m2[o] > 0.f ? gout[(size_t)n * FLAT + o] * s.dsc[c] : 0.f;
-    const int d = s.a2[o];
+    const float g = out[(size_t)n * FLAT + o] > 0.f ? gout[(size_t)n * FLAT + o] * dsc[c] : 0.f;
+    const int d = idx_save[(size_t)n * NIDX + NZ1 + o];
     G2[(c * O2 + 2 * py + (d >> 1)) * O2 + 2 * px + (d & 1)] = g;
   }
   __syncthreads();
-  // dW2, db2
-  for (int o = threadIdx.x; o < C2 * C1 * KS * KS; o += T) {
-    const int c = o / (C1 * KS * KS), ci = (o / (KS * KS)) % C1, ky = (o / KS) % KS, kx = o % KS;
-    float acc = 0.f;
-    for (int y = 0; y < O2; ++y)
+  // 2a. dW2[c][ci][ky][:] for 1000 (c, ci, ky) rows; db2 on the spare threads
+  if (t < C2 * C1 * KS) {
+    const int c = t / (C1 * KS), ci = (t / KS) % C1, ky = t % KS;
+    float acc[KS] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int y = 0; y < O2; ++y) {
+      const float* zr = z1 + (ci * P1 + y + ky) * P1;
+      const float* gr = G2 + (c * O2 + y) * O2;
+      float zv[P1], gv[O2];
 #pragma unroll
-      for (int xx = 0; xx < O2; ++xx) acc += G2[(c * O2 + y) * O2 + xx] * s.z1[(ci * P1 + y + ky) * P1 + xx + kx];
-    atomicAdd(gw2 + o, acc);
-  }
-  if (threadIdx.x < C2) {
+      for (int q = 0; q < P1; ++q) zv[q] = zr[q];
+#pragma unroll
+      for (int q = 0; q < O2; ++q) gv[q] = gr[q];
+#pragma unroll
+      for (int xo = 0; xo < O2; ++xo)
+#pragma unroll
+        for (int kx = 0; kx < KS; ++kx) acc[kx] += gv[xo] * zv[xo + kx];
+    }
+    float* dst = gw2 + ((c * C1 + ci) * KS + ky) * KS;
+#pragma unroll
+    for (int kx = 0; kx < KS; ++kx) atomicAdd(dst + kx, acc[kx]);
+  } else if (t < C2 * C1 * KS + C2) {
+    const int c = t - C2 * C1 * KS;
     float acc = 0.f;
-    for (int i = 0; i < O2 * O2; ++i) acc += G2[threadIdx.x * O2 * O2 + i];
-    atomicAdd(gb2 + threadIdx.x, acc);
+    for (int i = 0; i < O2 * O2; ++i) acc += G2[c * O2 * O2 + i];
+    atomicAdd(gb2 + c, acc);
   }
-  // dz1 -> relu mask -> maxpool1 argmax -> gradient of the conv1 output
-  for (int o = threadIdx.x; o < C1 * P1 * P1; o += T) {
-    if (s.z1[o] <= 0.f) continue;
-    const int ci = o / (P1 * P1), yy = (o / P1) % P1, xx = o % P1;
-    float acc = 0.f;
-    for (int c = 0; c < C2; ++c)
+  // 2b. dZ1 = full correlation of G2 with W2, 4-wide strips (ci, Y, X0..X0+3) x 2 halves of
+  //     the conv2 channels (720 items: the block's critical path), halves combined by LDS atomics
+  for (int it = t; it < 2 * C1 * P1 * (P1 / 4); it += TB) {
+    const int half = it / (C1 * P1 * 3), r = it % (C1 * P1 * 3);
+    const int ci = r / (P1 * 3), Y = (r / 3) % P1, X0 = (r % 3) * 4;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int c = half * (C2 / 2); c < (half + 1) * (C2 / 2); ++c)
 #pragma unroll
       for (int ky = 0; ky < KS; ++ky) {
-        const int y = yy - ky;
+        const int y = Y - ky;
         if (y < 0 || y >= O2) continue;
+        const float* gr = G2 + (c * O2 + y) * O2;
+        const float* wr = w2s + ((c * C1 + ci) * KS + ky) * KS;
+        float gv[8], wv[KS];
 #pragma unroll
-        for (int kx = 0; kx < KS; ++kx) {
-          const int xo = xx - kx;
-          if (xo < 0 || xo >= O2) continue;
-          acc += G2[(c * O2 + y) * O2 + xo] * s.w2[((c * C1 + ci) * KS + ky) * KS + kx];
+        for (int q = 0; q < 8; ++q) {  // G2 row at x = X0 - 4 + q (zero outside 0..7)
+          const int xx = X0 - 4 + q;
+          gv[q] = (xx >= 0 && xx < O2) ? gr[xx] : 0.f;
         }
+#pragma unroll
+        for (int kx = 0; kx < KS; ++kx) wv[kx] = wr[kx];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int kx = 0; kx < KS; ++kx) acc[j] += wv[kx] * gv[j - kx + 4];
       }
-    const int d = s.a1[o];
-    G1[(ci * O1 + 2 * yy + (d >> 1)) * O1 + 2 * xx + (d & 1)] = acc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int o = (ci * P1 + Y) * P1 + X0 + j;
+      if (z1[o] > 0.f) atomicAdd(&g1[o], acc[j]);  // ReLU mask; g1 pre-zeroed
+    }
   }
   __syncthreads();
-  for (int o = threadIdx.x; o < C1 * KS * KS; o += T) {
-    const int c = o / (KS * KS), ky = (o / KS) % KS, kx = o % KS;
+  // 3. dW1[c][ky][kx] = sum over pooled positions of g1 * x at the argmax tap; 4 lanes per weight
+  if (t < C1 * KS * KS * 4) {
+    const int wi = t >> 2, part = t & 3;
+    const int c = wi / (KS * KS), ky = (wi / KS) % KS, kx = wi % KS;
     float acc = 0.f;
-    for (int y = 0; y < O1; ++y)
-      for (int xx = 0; xx < O1; ++xx) acc += G1[(c * O1 + y) * O1 + xx] * s.x[(y + ky) * IMG + xx + kx];
-    atomicAdd(gw1 + o, acc);
-  }
-  if (threadIdx.x < C1) {
+    for (int q = part; q < P1 * P1; q += 4) {
+      const int o = c * P1 * P1 + q;
+      const int py = q / P1, px = q % P1, d = a1[o];
+      acc += g1[o] * xs[(2 * py + (d >> 1) + ky) * IMG + 2 * px + (d & 1) + kx];
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (part == 0) atomicAdd(gw1 + wi, acc);
+  } else if (t < C1 * KS * KS * 4 + C1) {
+    const int c = t - C1 * KS * KS * 4;
     float acc = 0.f;
-    for (int i = 0; i < O1 * O1; ++i) acc += G1[threadIdx.x * O1 * O1 + i];
-    atomicAdd(gb1 + threadIdx.x, acc);
+    for (int q = 0; q < P1 * P1; ++q) acc += g1[c * P1 * P1 + q];
+    atomicAdd(gb1 + c, acc);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // stage 1
-constexpr int S1_ROWS = 64;
-constexpr int XP1 = FLAT + 1;  // LDS pitch (odd: conflict-free column walks)
+constexpr int T1 = 256;
+constexpr int XP1 = FLAT + 4;  // LDS row pitch of the inputs (16-B aligned rows)
+constexpr int WP1 = FLAT + 1;  // LDS row pitch of W1 (odd: lane-per-row walks are conflict-free)
 
-__global__ void __launch_bounds__(T) cnn_s1_kernel(const float* __restrict__ x, const float* __restrict__ w1,
-                                                   const float* __restrict__ b1, const float* __restrict__ w2,
-                                                   const float* __restrict__ b2, const int64_t* __restrict__ tgt,
-                                                   int B, unsigned long long seed, unsigned sample0, float p,
-                                                   int drop, float scale, float* __restrict__ stats,
-                                                   float* __restrict__ dx, float* __restrict__ gw1,
-                                                   float* __restrict__ gb1, float* __restrict__ gw2,
-                                                   float* __restrict__ gb2) {
-  __shared__ float xs[S1_ROWS * XP1];
-  __shared__ float dhs[S1_ROWS * HID];
+template <int ROWS>
+__global__ void __launch_bounds__(T1) cnn_s1_kernel(const float* __restrict__ x, const float* __restrict__ w1,
+                                                    const float* __restrict__ b1, const float* __restrict__ w2,
+                                                    const float* __restrict__ b2, const int64_t* __restrict__ tgt,
+                                                    int B, unsigned long long seed0, const long long* ctr,
+                                                    unsigned sample0, float p, int drop, float scale,
+                                                    float* __restrict__ stats, float* __restrict__ dx,
+                                                    float* __restrict__ gw1, float* __restrict__ gb1,
+                                                    float* __restrict__ gw2, float* __restrict__ gb2) {
+  __shared__ __attribute__((aligned(16))) float xs[ROWS * XP1];
+  __shared__ float w1s[HID * WP1];  // 64 KB: fc1 and dX read W1 from LDS, not L2
+  __shared__ float dhs[ROWS * HID];
   __shared__ float w2s[NCLS * HID];
   __shared__ float dsh[4][HID];
   __shared__ float lsh[4][NCLS];
   __shared__ float red[4][NCLS * HID + NCLS + 2];
-  const int r0 = blockIdx.x * S1_ROWS;
-  const int nr = min(S1_ROWS, B - r0);
+  const unsigned long long seed = eff_seed(seed0, ctr);
+  const int r0 = blockIdx.x * ROWS;
+  const int nr = min(ROWS, B - r0);
   const bool train = dx != nullptr;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < nr * FLAT; i += T) xs[(i / FLAT) * XP1 + i % FLAT] = x[(size_t)r0 * FLAT + i];
-  for (int i = threadIdx.x; i < NCLS * HID; i += T) w2s[i] = w2[i];
+  for (int i = threadIdx.x; i < nr * (FLAT / 4); i += T1) {
+    const int r = i / (FLAT / 4), k4 = i % (FLAT / 4);
+    *reinterpret_cast<float4*>(xs + r * XP1 + 4 * k4) =
+        *reinterpret_cast<const float4*>(x + (size_t)(r0 + r) * FLAT + 4 * k4);
+  }
+  for (int i = threadIdx.x; i < HID * (FLAT / 4); i += T1) {
+    const int j = i / (FLAT / 4), k4 = i % (FLAT / 4);
+    const float4 v = *reinterpret_cast<const float4*>(w1 + (size_t)j * FLAT + 4 * k4);
+    float* d = w1s + j * WP1 + 4 * k4;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+  }
+  for (int i = threadIdx.x; i < NCLS * HID; i += T1) w2s[i] = w2[i];
   __syncthreads();
   float gw2acc[NCLS];  // lane j < 50: dW2[c][j]
 #pragma unroll
@@ -234,13 +331,21 @@ __global__ void __launch_bounds__(T) cnn_s1_kernel(const float* __restrict__ x, 
   float gb2acc = 0.f, loss_acc = 0.f, ok_acc = 0.f;
   for (int rr = w; rr < nr; rr += 4) {
     const int n = r0 + rr;
-    // fc1 + relu + dropout: lane j < 50
+    // fc1 + relu + dropout: lane j < 50 (W1 row j from LDS, x broadcast as float4)
     float h = 0.f, ms = 0.f;
     if (lane < HID) {
-      float acc = b1[lane];
-      const float* wr = w1 + (size_t)lane * FLAT;
-      for (int k = 0; k < FLAT; ++k) acc += wr[k] * xs[rr * XP1 + k];
-      h = fmaxf(acc, 0.f);
+      float a4[4] = {0.f, 0.f, 0.f, 0.f};
+      const float* wr = w1s + lane * WP1;
+      const float4* xr = reinterpret_cast<const float4*>(xs + rr * XP1);
+#pragma unroll 8
+      for (int k4 = 0; k4 < FLAT / 4; ++k4) {
+        const float4 xv = xr[k4];
+        a4[0] += wr[4 * k4] * xv.x;
+        a4[1] += wr[4 * k4 + 1] * xv.y;
+        a4[2] += wr[4 * k4 + 2] * xv.z;
+        a4[3] += wr[4 * k4 + 3] * xv.w;
+      }
+      h = fmaxf(b1[lane] + ((a4[0] + a4[1]) + (a4[2] + a4[3])), 0.f);
       ms = drop ? keep_scale(seed, sample0 + n, lane, p) : 1.f;
       dsh[w][lane] = h * ms;
     }
@@ -255,13 +360,11 @@ __global__ void __launch_bounds__(T) cnn_s1_kernel(const float* __restrict__ x, 
     }
     float mx = z;
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    float e = lane < NCLS ? __expf(z - mx) : 0.f;
-    float se = e;
+    float se = lane < NCLS ? __expf(z - mx) : 0.f;
     for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
     const float lse = mx + __logf(se);
     const int y = (int)tgt[n];
-    // argmax (first max) among lanes 0..9
-    unsigned long long bal = __ballot(lane < NCLS && z == mx);
+    const unsigned long long bal = __ballot(lane < NCLS && z == mx);  // first max = torch argmax
     const int am = __ffsll((long long)bal) - 1;
     const float zy = __shfl(z, y);
     if (lane == 0) {
@@ -273,7 +376,6 @@ __global__ void __launch_bounds__(T) cnn_s1_kernel(const float* __restrict__ x, 
     if (lane < NCLS) lsh[w][lane] = dl;
     __builtin_amdgcn_wave_barrier();
     gb2acc += dl;
-    float dh = 0.f;
     if (lane < HID) {
       float dd = 0.f;
 #pragma unroll
@@ -282,30 +384,30 @@ __global__ void __launch_bounds__(T) cnn_s1_kernel(const float* __restrict__ x, 
         dd += w2s[c * HID + lane] * lc;
         gw2acc[c] += lc * dsh[w][lane];
       }
-      dh = (h > 0.f) ? dd * ms : 0.f;
-      dhs[rr * HID + lane] = dh;
+      dhs[rr * HID + lane] = (h > 0.f) ? dd * ms : 0.f;
     }
     __builtin_amdgcn_wave_barrier();
-    // dx[n][k] = sum_j W1[j][k] dh_j  (lanes over k: coalesced W1 reads)
+    // dx[n][k] = sum_j W1[j][k] dh_j  (lanes over k)
     for (int k = lane; k < FLAT; k += 64) {
       float acc = 0.f;
-      for (int j = 0; j < HID; ++j) acc += w1[(size_t)j * FLAT + k] * dhs[rr * HID + j];
+#pragma unroll 10
+      for (int j = 0; j < HID; ++j) acc += w1s[j * WP1 + k] * dhs[rr * HID + j];
       dx[(size_t)n * FLAT + k] = acc;
     }
     __builtin_amdgcn_wave_barrier();
   }
   // per-wave partials -> LDS -> one atomic per output per block
-  if (train && lane < HID) {
+  if (lane < HID) {
 #pragma unroll
     for (int c = 0; c < NCLS; ++c) red[w][c * HID + lane] = gw2acc[c];
   }
-  if (lane < NCLS) red[w][NCLS * HID + lane] = train ? gb2acc : 0.f;
+  if (lane < NCLS) red[w][NCLS * HID + lane] = gb2acc;
   if (lane == 0) {
     red[w][NCLS * HID + NCLS] = loss_acc;
     red[w][NCLS * HID + NCLS + 1] = ok_acc;
   }
   __syncthreads();
-  for (int o = threadIdx.x; o < NCLS * HID + NCLS + 2; o += T) {
+  for (int o = threadIdx.x; o < NCLS * HID + NCLS + 2; o += T1) {
     const float v = red[0][o] + red[1][o] + red[2][o] + red[3][o];
     if (o < NCLS * HID) {
       if (train) atomicAdd(gw2 + o, v);
@@ -317,9 +419,10 @@ __global__ void __launch_bounds__(T) cnn_s1_kernel(const float* __restrict__ x, 
   }
   if (!train) return;
   // dW1[j][k] = sum_rows dh[r][j] x[r][k]; db1[j] = sum_rows dh[r][j]
-  for (int o = threadIdx.x; o < HID * FLAT; o += T) {
+  for (int o = threadIdx.x; o < HID * FLAT; o += T1) {
     const int j = o / FLAT, k = o % FLAT;
     float acc = 0.f;
+#pragma unroll 4
     for (int r = 0; r < nr; ++r) acc += dhs[r * HID + j] * xs[r * XP1 + k];
     atomicAdd(gw1 + o, acc);
   }
@@ -332,28 +435,39 @@ __global__ void __launch_bounds__(T) cnn_s1_kernel(const float* __restrict__ x, 
 
 }  // namespace
 
+int ref_cnn_idx_bytes() { return NIDX; }
+int ref_cnn_z1_floats() { return NZ1; }
+
 void ref_cnn_stage0_fwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2, float* out,
-                        int B, unsigned long long seed, unsigned sample0, float p, bool drop, hipStream_t stream) {
+                        float* z1_save, unsigned char* idx_save, int B, unsigned long long seed, const long long* ctr,
+                        unsigned sample0, float p, bool drop, hipStream_t stream) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(cnn_s0_fwd_kernel, dim3(B), dim3(T), 0, stream, x, w1, b1, w2, b2, out, seed, sample0, p,
-                     drop ? 1 : 0);
+  hipLaunchKernelGGL(cnn_s0_fwd_kernel, dim3(B), dim3(TF), 0, stream, x, w1, b1, w2, b2, out, z1_save, idx_save,
+                     seed, ctr, sample0, p, drop ? 1 : 0);
 }
 
-void ref_cnn_stage0_bwd(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
-                        const float* gout, int B, unsigned long long seed, unsigned sample0, float p, bool drop,
-                        float* gw1, float* gb1, float* gw2, float* gb2, hipStream_t stream) {
+void ref_cnn_stage0_bwd(const float* x, const float* w2, const float* out, const float* gout, const float* z1_save,
+                        const unsigned char* idx_save, int B, unsigned long long seed, const long long* ctr,
+                        unsigned sample0, float p, bool drop, float* gw1, float* gb1, float* gw2, float* gb2,
+                        hipStream_t stream) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(cnn_s0_bwd_kernel, dim3(B), dim3(T), 0, stream, x, w1, b1, w2, b2, gout, seed, sample0, p,
-                     drop ? 1 : 0, gw1, gb1, gw2, gb2);
+  hipLaunchKernelGGL(cnn_s0_bwd_kernel, dim3(B), dim3(TB), 0, stream, x, w2, out, gout, z1_save, idx_save, seed, ctr,
+                     sample0, p, drop ? 1 : 0, gw1, gb1, gw2, gb2);
 }
 
 void ref_cnn_stage1(const float* x, const float* w1, const float* b1, const float* w2, const float* b2,
-                    const int64_t* target, int B, unsigned long long seed, unsigned sample0, float p, bool drop,
-                    float scale, float* stats, float* dx, float* gw1, float* gb1, float* gw2, float* gb2,
-                    hipStream_t stream) {
+                    const int64_t* target, int B, unsigned long long seed, const long long* ctr, unsigned sample0,
+                    float p, bool drop, float scale, float* stats, float* dx, float* gw1, float* gb1, float* gw2,
+                    float* gb2, hipStream_t stream) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(cnn_s1_kernel, dim3((B + S1_ROWS - 1) / S1_ROWS), dim3(T), 0, stream, x, w1, b1, w2, b2, target,
-                     B, seed, sample0, p, drop ? 1 : 0, scale, stats, dx, gw1, gb1, gw2, gb2);
+  // small batches: 8 rows per block (spread over CUs); large: 32 (fewer dW1 atomics per sample)
+  if (B <= 4096) {
+    hipLaunchKernelGGL(cnn_s1_kernel<8>, dim3((B + 7) / 8), dim3(T1), 0, stream, x, w1, b1, w2, b2, target, B, seed,
+                       ctr, sample0, p, drop ? 1 : 0, scale, stats, dx, gw1, gb1, gw2, gb2);
+  } else {
+    hipLaunchKernelGGL(cnn_s1_kernel<32>, dim3((B + 31) / 32), dim3(T1), 0, stream, x, w1, b1, w2, b2, target, B,
+                       seed, ctr, sample0, p, drop ? 1 : 0, scale, stats, dx, gw1, gb1, gw2, gb2);
+  }
 }
 
 }  // namespace sdml

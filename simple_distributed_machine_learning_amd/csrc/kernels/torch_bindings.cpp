@@ -421,38 +421,59 @@ void check_cnn_params(const torch::Tensor& w1, const torch::Tensor& b1, const to
               "ref_cnn: parameter shapes do not match the reference CNN");
 }
 
-torch::Tensor ref_cnn_stage0_fwd(torch::Tensor x, torch::Tensor w1, torch::Tensor b1, torch::Tensor w2,
-                                 torch::Tensor b2, int64_t seed, int64_t sample0, double p, bool drop) {
+const long long* ctr_ptr(const c10::optional<torch::Tensor>& c) {
+  if (!c.has_value() || !c->defined()) return nullptr;
+  TORCH_CHECK(c->is_cuda() && c->scalar_type() == torch::kInt64 && c->numel() >= 1, "ctr must be an int64 device tensor");
+  return reinterpret_cast<const long long*>(c->data_ptr<int64_t>());
+}
+
+// returns (out [B,320], z1 [B,1440] or None, idx [B,NIDX] uint8 or None); save = training
+std::tuple<torch::Tensor, c10::optional<torch::Tensor>, c10::optional<torch::Tensor>> ref_cnn_stage0_fwd(
+    torch::Tensor x, torch::Tensor w1, torch::Tensor b1, torch::Tensor w2, torch::Tensor b2, int64_t seed,
+    c10::optional<torch::Tensor> ctr, int64_t sample0, double p, bool drop, bool save) {
   check_f32_cuda(x, "x");
   TORCH_CHECK(x.numel() % 784 == 0 && x.size(0) * 784 == x.numel(), "ref_cnn stage0: x must be [B,1,28,28]");
   check_cnn_params(w1, b1, w2, b2, 250, 10, 5000, 20);
   const int64_t B = x.size(0);
   auto out = torch::empty({B, 320}, x.options());
+  c10::optional<torch::Tensor> z1, idx;
+  if (save) {
+    z1 = torch::empty({B, (int64_t)sdml::ref_cnn_z1_floats()}, x.options());
+    idx = torch::empty({B, (int64_t)sdml::ref_cnn_idx_bytes()}, x.options().dtype(torch::kUInt8));
+  }
   sdml::ref_cnn_stage0_fwd(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(),
-                           b2.data_ptr<float>(), out.data_ptr<float>(), (int)B, (unsigned long long)seed,
+                           b2.data_ptr<float>(), out.data_ptr<float>(), save ? z1->data_ptr<float>() : nullptr,
+                           save ? idx->data_ptr<uint8_t>() : nullptr, (int)B, (unsigned long long)seed, ctr_ptr(ctr),
                            (unsigned)sample0, (float)p, drop, cur_stream());
-  return out;
+  return {out, z1, idx};
 }
 
-void ref_cnn_stage0_bwd(torch::Tensor x, torch::Tensor w1, torch::Tensor b1, torch::Tensor w2, torch::Tensor b2,
-                        torch::Tensor gout, int64_t seed, int64_t sample0, double p, bool drop, torch::Tensor gw1,
-                        torch::Tensor gb1, torch::Tensor gw2, torch::Tensor gb2) {
+void ref_cnn_stage0_bwd(torch::Tensor x, torch::Tensor w2, torch::Tensor out, torch::Tensor gout, torch::Tensor z1,
+                        torch::Tensor idx, int64_t seed, c10::optional<torch::Tensor> ctr, int64_t sample0, double p,
+                        bool drop, torch::Tensor gw1, torch::Tensor gb1, torch::Tensor gw2, torch::Tensor gb2) {
   check_f32_cuda(x, "x");
+  check_f32_cuda(w2, "w2");
+  check_f32_cuda(out, "out");
   check_f32_cuda(gout, "gout");
+  check_f32_cuda(z1, "z1");
   const int64_t B = x.size(0);
-  TORCH_CHECK(x.numel() == B * 784 && gout.numel() == B * 320, "ref_cnn stage0 bwd: shape mismatch");
-  check_cnn_params(w1, b1, w2, b2, 250, 10, 5000, 20);
+  TORCH_CHECK(x.numel() == B * 784 && out.numel() == B * 320 && gout.numel() == B * 320 && w2.numel() == 5000 &&
+                  z1.numel() == B * sdml::ref_cnn_z1_floats(),
+              "ref_cnn stage0 bwd: shape mismatch");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == torch::kUInt8 && idx.is_contiguous() &&
+                  idx.numel() == B * sdml::ref_cnn_idx_bytes(),
+              "ref_cnn stage0 bwd: idx must be the forward's uint8 argmax tensor");
   check_cnn_params(gw1, gb1, gw2, gb2, 250, 10, 5000, 20);
-  sdml::ref_cnn_stage0_bwd(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(),
-                           b2.data_ptr<float>(), gout.data_ptr<float>(), (int)B, (unsigned long long)seed,
-                           (unsigned)sample0, (float)p, drop, gw1.data_ptr<float>(), gb1.data_ptr<float>(),
-                           gw2.data_ptr<float>(), gb2.data_ptr<float>(), cur_stream());
+  sdml::ref_cnn_stage0_bwd(x.data_ptr<float>(), w2.data_ptr<float>(), out.data_ptr<float>(), gout.data_ptr<float>(),
+                           z1.data_ptr<float>(), idx.data_ptr<uint8_t>(), (int)B, (unsigned long long)seed,
+                           ctr_ptr(ctr), (unsigned)sample0, (float)p, drop, gw1.data_ptr<float>(),
+                           gb1.data_ptr<float>(), gw2.data_ptr<float>(), gb2.data_ptr<float>(), cur_stream());
 }
 
 // returns dx if grads are given (training), else None; loss/correct accumulate into stats[2]
 c10::optional<torch::Tensor> ref_cnn_stage1(torch::Tensor x, torch::Tensor w1, torch::Tensor b1, torch::Tensor w2,
-                                            torch::Tensor b2, torch::Tensor target, int64_t seed, int64_t sample0,
-                                            double p, bool drop, double scale, torch::Tensor stats,
+                                            torch::Tensor b2, torch::Tensor target, int64_t seed,
+                                            c10::optional<torch::Tensor> ctr, int64_t sample0, double p, bool drop, double scale, torch::Tensor stats,
                                             c10::optional<torch::Tensor> gw1, c10::optional<torch::Tensor> gb1,
                                             c10::optional<torch::Tensor> gw2, c10::optional<torch::Tensor> gb2) {
   check_f32_cuda(x, "x");
@@ -473,7 +494,7 @@ c10::optional<torch::Tensor> ref_cnn_stage1(torch::Tensor x, torch::Tensor w1, t
   }
   sdml::ref_cnn_stage1(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(),
                        b2.data_ptr<float>(), target.data_ptr<int64_t>(), (int)B, (unsigned long long)seed,
-                       (unsigned)sample0, (float)p, drop, (float)scale, stats.data_ptr<float>(),
+                       ctr_ptr(ctr), (unsigned)sample0, (float)p, drop, (float)scale, stats.data_ptr<float>(),
                        train ? dx->data_ptr<float>() : nullptr, opt_ptr(gw1), opt_ptr(gb1), opt_ptr(gw2), opt_ptr(gb2),
                        cur_stream());
   return dx;
@@ -504,7 +525,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention_bwd", &attention_bwd, "causal flash attention backward (bf16, d=64)");
   m.def("gemm_f32_set_variant", &sdml::gemm_f32_set_variant, "fp32 GEMM variant (tuning: 0 auto, 16, 32)");
   m.def("ref_cnn_stage0_fwd", &ref_cnn_stage0_fwd, "reference CNN stage 0 forward (one launch)");
-  m.def("ref_cnn_stage0_bwd", &ref_cnn_stage0_bwd, "reference CNN stage 0 backward (recompute, one launch)");
+  m.def("ref_cnn_stage0_bwd", &ref_cnn_stage0_bwd, "reference CNN stage 0 backward (one launch)");
   m.def("ref_cnn_stage1", &ref_cnn_stage1, "reference CNN stage 1 forward+loss+backward (one launch)");
   m.def("synth_mnist", &synth_mnist, "on-device synthetic MNIST-shape data");
 }

@@ -35,7 +35,18 @@ def _draw_seed() -> int:
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
-class Network1Stage(PipelineStage):
+class _RngStage(PipelineStage):
+    """Stage whose fused kernels draw dropout masks; ``rng_step`` is an int64 device counter
+    (the engine attaches its own; a non-persistent buffer keeps the reference's state_dict
+    keys)."""
+    uses_rng_step = True
+
+    def _ctr(self, x):
+        ctr = getattr(self, "rng_step", None)
+        return ctr if ctr is not None and ctr.device == x.device else None
+
+
+class Network1Stage(_RngStage):
     def __init__(self, dropout: float = 0.5):
         super().__init__()
         self.conv1 = nn.Conv2d(1, 10, kernel_size=5)
@@ -57,20 +68,21 @@ class Network1Stage(PipelineStage):
         p = self.conv2_drop.p
         drop = train and p > 0
         seed = _draw_seed() if drop else 0
-        y = ops.ref_cnn_stage0_fwd(x, self.conv1, self.conv2, seed, p, drop)
+        ctr = self._ctr(x)
+        y, saved = ops.ref_cnn_stage0_fwd(x, self.conv1, self.conv2, seed, p, drop, ctr=ctr, save=train)
         if train:
-            ctx["x"], ctx["seed"], ctx["drop"] = x, seed, drop
+            ctx.update(x=x, y=y, saved=saved, seed=seed, drop=drop, ctr=ctr)
         return y
 
     def bwd(self, grad_y, ctx):
         if "seed" not in ctx:
             return super().bwd(grad_y, ctx)
-        ops.ref_cnn_stage0_bwd(ctx.pop("x"), self.conv1, self.conv2, grad_y, ctx.pop("seed"), self.conv2_drop.p,
-                               ctx.pop("drop"))
+        ops.ref_cnn_stage0_bwd(ctx.pop("x"), self.conv1, self.conv2, ctx.pop("y"), grad_y, ctx.pop("saved"),
+                               ctx.pop("seed"), self.conv2_drop.p, ctx.pop("drop"), ctr=ctx.pop("ctr"))
         return None
 
 
-class Network2Stage(PipelineStage):
+class Network2Stage(_RngStage):
     def __init__(self, eval_dropout: bool = True, dropout: float = 0.5):
         super().__init__()
         self.fc1 = nn.Linear(320, 50)
@@ -92,7 +104,8 @@ class Network2Stage(PipelineStage):
         drop = (train or self.eval_dropout) and self.p > 0
         seed = _draw_seed() if drop else 0
         st = stats if stats is not None else torch.zeros(2, device=x.device)
-        dx = ops.ref_cnn_stage1(x, self.fc1, self.fc2, target, seed, self.p, drop, loss_scale, st, train)
+        dx = ops.ref_cnn_stage1(x, self.fc1, self.fc2, target, seed, self.p, drop, loss_scale, st, train,
+                                ctr=self._ctr(x))
         if train:
             ctx["dx"] = dx
         if stats is not None:

@@ -92,22 +92,31 @@ def sgd_momentum_mixed_(master, p, g, buf, lr: float, momentum: float, dampening
 
 
 # ---- reference CNN: one launch per stage pass (csrc/kernels/ref_cnn.hip) --------------------
-def ref_cnn_stage0_fwd(x, conv1, conv2, seed: int, p: float, drop: bool, sample0: int = 0):
-    """Network1 (conv1-pool-relu-conv2-dropout2d-pool-relu-flatten) -> [B, 320]."""
+# Dropout seeds: ``seed`` (host, per pass) combined with ``ctr`` (optional int64 device step
+# counter, advanced inside captured hipGraphs) as ops.reference.effective_seed.
+def ref_cnn_stage0_fwd(x, conv1, conv2, seed: int, p: float, drop: bool, sample0: int = 0, ctr=None,
+                       save: bool = False):
+    """Network1 (conv1-pool-relu-conv2-dropout2d-pool-relu-flatten) -> (out [B, 320], saved).
+    ``save`` (training) also returns what :func:`ref_cnn_stage0_bwd` needs."""
     if x.is_cuda:
-        return _k().ref_cnn_stage0_fwd(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, seed, sample0, p,
-                                       drop)
+        out, z1, idx = _k().ref_cnn_stage0_fwd(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, seed, ctr,
+                                               sample0, p, drop, save)
+        return out, ((z1, idx) if save else None)
+    seed_e = ref.effective_seed(seed, ctr)
     with torch.no_grad():
-        return ref.ref_cnn_stage0(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, seed, sample0, p, drop)
+        out = ref.ref_cnn_stage0(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, seed_e, sample0, p, drop)
+    return out, (None if not save else ())
 
 
-def ref_cnn_stage0_bwd(x, conv1, conv2, gout, seed: int, p: float, drop: bool, sample0: int = 0):
-    """Accumulates conv1/conv2 weight and bias grads (recomputes the forward)."""
+def ref_cnn_stage0_bwd(x, conv1, conv2, out, gout, saved, seed: int, p: float, drop: bool, sample0: int = 0,
+                       ctr=None):
+    """Accumulates conv1/conv2 weight and bias grads from the forward's output/saved state."""
     if x.is_cuda:
-        _k().ref_cnn_stage0_bwd(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, gout.contiguous(), seed,
-                                sample0, p, drop, conv1.weight.grad, conv1.bias.grad, conv2.weight.grad,
-                                conv2.bias.grad)
+        z1, idx = saved
+        _k().ref_cnn_stage0_bwd(x, conv2.weight, out, gout.contiguous(), z1, idx, seed, ctr, sample0, p, drop,
+                                conv1.weight.grad, conv1.bias.grad, conv2.weight.grad, conv2.bias.grad)
         return
+    seed = ref.effective_seed(seed, ctr)
     ps = [conv1.weight, conv1.bias, conv2.weight, conv2.bias]
     leaves = [t.detach().requires_grad_(True) for t in ps]
     with torch.enable_grad():
@@ -118,13 +127,14 @@ def ref_cnn_stage0_bwd(x, conv1, conv2, gout, seed: int, p: float, drop: bool, s
 
 
 def ref_cnn_stage1(x, fc1, fc2, target, seed: int, p: float, drop: bool, scale: float, stats, train: bool,
-                   sample0: int = 0):
+                   sample0: int = 0, ctr=None):
     """Network2 + NLL: stats[0] += sum loss, stats[1] += correct; when ``train`` accumulates
     fc1/fc2 grads of ``scale * sum loss`` and returns dL/dx."""
     if x.is_cuda:
         g = (fc1.weight.grad, fc1.bias.grad, fc2.weight.grad, fc2.bias.grad) if train else (None,) * 4
-        return _k().ref_cnn_stage1(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, target, seed, sample0, p, drop,
-                                   scale, stats, *g)
+        return _k().ref_cnn_stage1(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, target, seed, ctr, sample0, p,
+                                   drop, scale, stats, *g)
+    seed = ref.effective_seed(seed, ctr)
     ps = [fc1.weight, fc1.bias, fc2.weight, fc2.bias]
     leaves = [t.detach().requires_grad_(train) for t in ps]
     xx = x.detach().requires_grad_(train)

@@ -109,6 +109,12 @@ def dropout_keep_scale(seed: int, sample0: int, n: int, units: int, p: float) ->
     return torch.from_numpy(np.where(keep, sc, np.float32(0.0)).astype(np.float32))
 
 
+def effective_seed(seed: int, ctr=None) -> int:
+    """ref_cnn.hip's eff_seed: seed + 0x9E3779B97F4A7C15 * step_counter (mod 2^64)."""
+    c = 0 if ctr is None else int(ctr.reshape(-1)[0])
+    return (seed + 0x9E3779B97F4A7C15 * c) & _M64
+
+
 def ref_cnn_stage0(x, w1, b1, w2, b2, seed: int, sample0: int, p: float, drop: bool):
     """Network1 forward with hash-based Dropout2d (autograd-capable)."""
     z1 = F.relu(F.max_pool2d(F.conv2d(x, w1, b1), 2))

@@ -1,0 +1,148 @@
+"""hipGraph capture of a whole training step.
+
+At the reference's batch of 60 a step is a few microseconds of GPU work, and the host
+cannot keep up. Python dispatch and ~10 kernel launches cost hundreds of microseconds, and
+the reference's RPC round trips cost milliseconds (/root/reference/simple_distributed.py:108-113).
+:class:`GraphedStep` records the engine's step once into a HIP graph and then replays it.
+The recorded step covers data reads, every stage's forward and backward, the loss and
+metrics, the fused SGD update, and the device step counter. A replay is one host call.
+
+What changes between replays, and how it gets into the graph:
+
+* data: the graph reads from static buffers, one per slice the engine asks for. A first,
+  discarded capture discovers the slices, and the buffers are allocated outside the graph's
+  pool. A buffer allocated inside the pool could alias memory that earlier nodes of the
+  same graph reuse. Before each replay the step's real slices are copied into the buffers.
+  These are device-to-device copies, because the datasets already live in HBM.
+* dropout: the fused kernels mix the engine's device step counter into their seeds. The
+  graph increments that counter, so each replay draws fresh masks.
+* the optimizer: the first step (momentum-buffer initialisation) runs eagerly, so the
+  captured SGD launch is the steady-state update.
+
+Constraints (checked): a CUDA/ROCm engine; a training step with an optimizer update; and
+one process, unless ``allow_collectives``. RCCL collectives can be captured, but that path
+is opt-in until it has been validated on multi-GPU hardware. The returned
+:class:`StepResult` tensors belong to the graph and are overwritten by the next replay, so
+read them first. The ragged last batch of an epoch has a different shape and gets its own
+graph. A failed capture falls back to eager execution and emits a warning.
+"""
+from __future__ import annotations
+
+import time
+import warnings
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from .pipeline import PipelineEngine, StepResult
+
+
+class _StaticWindow:
+    """Dataset seen by the engine during capture: every (kind, offset, n) slice it reads maps
+    to a persistent buffer; :meth:`load` fills them from the real dataset for one step.
+
+    ``discover`` mode (first capture) only records the slices and hands out placeholders;
+    :meth:`freeze` then allocates the real buffers OUTSIDE any graph pool."""
+
+    def __init__(self, real):
+        self.real = real
+        self.bufs: Dict[Tuple[str, int, int], torch.Tensor] = {}
+        self.keys = []
+        self.discover = True
+        self.seq_len = getattr(real, "seq_len", None)
+        self.n = len(real)
+
+    def __len__(self):
+        return self.n
+
+    def _src(self, kind, start, n):
+        return self.real.inputs(start, n) if kind == "x" else self.real.targets(start, n)
+
+    def _buf(self, kind: str, start: int, n: int) -> torch.Tensor:
+        key = (kind, start, n)
+        if self.discover:
+            if key not in self.keys:
+                self.keys.append(key)
+            return torch.empty_like(self._src(*key), memory_format=torch.contiguous_format)
+        if key not in self.bufs:
+            raise RuntimeError(f"graph capture read an undiscovered slice {key}")
+        return self.bufs[key]
+
+    def freeze(self):
+        self.discover = False
+        for key in self.keys:
+            self.bufs[key] = torch.empty_like(self._src(*key), memory_format=torch.contiguous_format)
+
+    def inputs(self, start: int, n: int) -> torch.Tensor:
+        return self._buf("x", start, n)
+
+    def targets(self, start: int, n: int) -> torch.Tensor:
+        return self._buf("y", start, n)
+
+    def load(self, dataset, delta: int):
+        """Copy the slices at (offset + delta) of ``dataset`` into the static buffers."""
+        for (kind, start, n), buf in self.bufs.items():
+            src = dataset.inputs(start + delta, n) if kind == "x" else dataset.targets(start + delta, n)
+            buf.copy_(src, non_blocking=True)
+
+
+class GraphedStep:
+    """``step(dataset, start, batch_size, global_batch)`` == ``engine.run(..., train=True)``
+    replayed from a captured HIP graph (one graph per (batch_size, global_batch))."""
+
+    def __init__(self, engine: PipelineEngine, allow_collectives: bool = False):
+        if engine.device.type != "cuda":
+            raise ValueError("GraphedStep needs a ROCm device engine")
+        if engine.mesh.world_size > 1 and not allow_collectives:
+            raise ValueError("GraphedStep: multi-process capture (RCCL in the graph) is opt-in: "
+                             "pass allow_collectives=True")
+        self.engine = engine
+        self.graphs: Dict[Tuple[int, Optional[int]], Tuple[torch.cuda.CUDAGraph, _StaticWindow, StepResult, int]] = {}
+        self.pool = None
+        self.disabled = False
+        self.replays = 0
+
+    def _record(self, win, start, batch_size, global_batch, pool):
+        eng = self.engine
+        gs, steps, zero = eng.global_step, eng.optimizer.steps, eng.flat.grads_zero
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(eng.device)
+        with torch.cuda.graph(g, pool=pool):
+            res = eng.run(win, start, batch_size, train=True, global_batch=global_batch)
+        # capture recorded but did not execute the step: restore the host-side state
+        eng.global_step, eng.optimizer.steps, eng.flat.grads_zero = gs, steps, zero
+        return g, res
+
+    def _capture(self, dataset, start: int, batch_size: int, global_batch: Optional[int]):
+        win = _StaticWindow(dataset)
+        g, _ = self._record(win, start, batch_size, global_batch, None)  # discover the data slices
+        del g
+        win.freeze()
+        g, res = self._record(win, start, batch_size, global_batch, self.pool)
+        if self.pool is None:
+            self.pool = g.pool()
+        # the graph ends with the optimizer's fused zero_grad, like the eager step
+        self.engine.flat.grads_zero = True
+        return g, win, res, start
+
+    def __call__(self, dataset, start: int, batch_size: int, global_batch: Optional[int] = None) -> StepResult:
+        eng = self.engine
+        if self.disabled or eng.optimizer.steps == 0:
+            return eng.run(dataset, start, batch_size, train=True, global_batch=global_batch)
+        key = (batch_size, global_batch)
+        t0 = time.perf_counter()
+        if key not in self.graphs:
+            try:
+                self.graphs[key] = self._capture(dataset, start, batch_size, global_batch)
+            except Exception as e:  # noqa: BLE001 - any capture failure: run eagerly from now on
+                warnings.warn(f"hipGraph capture failed ({type(e).__name__}: {e}); running eagerly")
+                self.disabled = True
+                torch.cuda.synchronize(eng.device)
+                return eng.run(dataset, start, batch_size, train=True, global_batch=global_batch)
+        g, win, res, cap_start = self.graphs[key]
+        win.load(dataset, start - cap_start)
+        g.replay()
+        eng.global_step += 1
+        eng.optimizer.steps += 1
+        self.replays += 1
+        return StepResult(res.loss_sum, res.correct, res.count, time.perf_counter() - t0)

@@ -131,6 +131,13 @@ class PipelineEngine:
                 m.to(self.dtype)
             self.stages[s] = m
         self.flat = FlatParams([(s, m) for s, m in self.stages.items()], self.device, self.dtype)
+        # device-side training-step counter: fused dropout kernels mix it into their seeds, and
+        # it is advanced by a (capturable) device op at the end of every training step, so a
+        # replayed hipGraph draws fresh masks each step (see parallel/graphs.py)
+        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
+        for m in self.stages.values():
+            if getattr(m, "uses_rng_step", False):
+                m.rng_step = self.step_ctr
         self.optimizer = FusedSGD(self.flat, lr=lr, momentum=momentum, weight_decay=weight_decay)
         self.transport = Transport(mesh) if mesh.pp > 1 else None
         self.grad_sync = GradSync(self.flat, mesh, self.local_stage_ids)
@@ -199,6 +206,7 @@ class PipelineEngine:
                 if step_optimizer:
                     self.optimizer.step()
                     self.global_step += 1
+                self.step_ctr.add_(1)
             z = torch.zeros(2, device=dev, dtype=torch.float32)
             return StepResult(z[0], z[1], 0, time.perf_counter() - t0)
         if self.kind == "rotate" and self.use_alltoall and self.P == 2:
@@ -327,6 +335,7 @@ class PipelineEngine:
             if step_optimizer:
                 self.optimizer.step()
                 self.global_step += 1
+            self.step_ctr.add_(1)
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
 
     # ---------------------------------------------------------------------------------------
@@ -418,6 +427,7 @@ class PipelineEngine:
             if step_optimizer:
                 self.optimizer.step()
                 self.global_step += 1
+            self.step_ctr.add_(1)
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
 
     def reduce_metrics(self, res: StepResult, group=None) -> Tuple[float, int, int]:

@@ -93,6 +93,15 @@ def run(args) -> dict:
             print(f"[sdml] resumed from {args.ckpt_dir}: epoch {start_epoch} batch {start_batch}", flush=True)
 
     history = {"train": [], "test": []}
+    graphed = None
+    if getattr(args, "graph", False) and device.type == "cuda" and not args.debug_sync:
+        from .parallel.graphs import GraphedStep
+
+        try:
+            graphed = GraphedStep(engine, allow_collectives=os.environ.get("SDML_GRAPH_COLLECTIVES") == "1")
+        except ValueError as e:
+            if master:
+                print(f"[sdml] --graph ignored: {e}", flush=True)
 
     def train(epoch: int, first_batch: int):
         engine.train()
@@ -110,7 +119,10 @@ def run(args) -> dict:
                 size = local * engine.data_shards
             else:
                 local = B
-            res = engine.run(train_ds, engine.local_start(start, local), local, train=True, global_batch=size)
+            if graphed is not None:
+                res = graphed(train_ds, engine.local_start(start, local), local, global_batch=size)
+            else:
+                res = engine.run(train_ds, engine.local_start(start, local), local, train=True, global_batch=size)
             n_since += size
             last_idx = batch_idx
             if batch_idx % args.log_interval == 0:

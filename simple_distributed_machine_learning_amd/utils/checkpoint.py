@@ -46,7 +46,7 @@ def save_checkpoint(engine: PipelineEngine, ckpt_dir: str, epoch: int, batch: in
         if extra:
             obj.update(extra)
         _atomic_save(obj, d / f"stage{s}.pt")
-    rng = {"cpu": torch.get_rng_state()}
+    rng = {"cpu": torch.get_rng_state(), "step_ctr": engine.step_ctr.detach().cpu()}
     if engine.device.type == "cuda":
         rng["cuda"] = torch.cuda.get_rng_state(engine.device)
     _atomic_save(rng, d / f"rng_rank{mesh.rank}.pt")
@@ -72,5 +72,7 @@ def load_checkpoint(engine: PipelineEngine, ckpt_dir: str, strict: bool = True) 
         torch.set_rng_state(rng["cpu"])
         if "cuda" in rng and engine.device.type == "cuda":
             torch.cuda.set_rng_state(rng["cuda"], engine.device)
+        if "step_ctr" in rng:
+            engine.step_ctr.copy_(rng["step_ctr"])
     engine.global_step = meta["global_step"]
     return meta

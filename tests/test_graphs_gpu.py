@@ -1,0 +1,54 @@
+"""hipGraph-captured training step (parallel/graphs.py) == eager engine step (GPU only)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():
+    pytest.skip("no ROCm GPU", allow_module_level=True)
+
+from simple_distributed_machine_learning_amd.data import SyntheticMNIST  # noqa: E402
+from simple_distributed_machine_learning_amd.models import get_model_spec  # noqa: E402
+from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh  # noqa: E402
+from simple_distributed_machine_learning_amd.parallel.graphs import GraphedStep  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def _engine(model, kind="1f1b", M=2, **kw):
+    mesh = init_mesh(pp=1, schedule_kind=kind, rank=0, world_size=1, device=DEV)
+    return PipelineEngine(get_model_spec(model, None, **kw), mesh, schedule_kind=kind, num_microbatches=M, lr=0.1,
+                          momentum=0.5, seed=5)
+
+
+@pytest.mark.parametrize("model,kw,kind,M", [("mlp", {}, "1f1b", 1), ("mlp", {}, "gpipe", 3),
+                                             ("mlp4x1024", {}, "1f1b", 2), ("ref_cnn", {"dropout": 0.0}, "1f1b", 1),
+                                             ("ref_cnn", {"dropout": 0.0}, "chimera", 2)])
+def test_graphed_step_matches_eager(model, kw, kind, M):
+    ds = SyntheticMNIST(600, seed=3, device=DEV)
+    e1, e2 = _engine(model, kind, M, **kw), _engine(model, kind, M, **kw)
+    g = GraphedStep(e2)
+    sizes = [60, 60, 60, 60, 40, 60]  # the 40 is a ragged last batch: its own graph
+    start = 0
+    for B in sizes:
+        r1 = e1.run(ds, start, B, train=True)
+        l1, c1 = float(r1.loss_sum), int(r1.correct)
+        r2 = g(ds, start, B)
+        l2, c2 = float(r2.loss_sum), int(r2.correct)
+        assert abs(l1 - l2) <= 1e-4 * max(1.0, abs(l1))
+        assert c1 == c2 and r1.count == r2.count == B
+        start += B
+    assert g.replays == len(sizes) - 1 and len(g.graphs) == 2 and not g.disabled
+    torch.testing.assert_close(e1.flat.params, e2.flat.params, rtol=1e-5, atol=1e-6)
+    assert e1.global_step == e2.global_step
+    assert int(e1.step_ctr) == int(e2.step_ctr) == len(sizes)
+
+
+def test_graphed_dropout_draws_fresh_masks():
+    ds = SyntheticMNIST(120, seed=4, device=DEV)
+    e = _engine("ref_cnn", "1f1b", 1, dropout=0.5)
+    e.optimizer.lr = 0.0  # weights fixed: loss differences come from the masks alone
+    g = GraphedStep(e)
+    losses = [float(g(ds, 0, 60).loss_sum) for _ in range(4)]
+    assert g.replays == 3
+    assert len(set(losses[1:])) == 3  # every replay saw different dropout masks
+    assert int(e.step_ctr) == 4

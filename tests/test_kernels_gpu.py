@@ -242,12 +242,14 @@ def test_ref_cnn_stage0(B, drop):
     c1, c2, _, _ = _cnn_params(1)
     x = rnd(B, 1, 28, 28, seed=2).abs()
     seed, p = 123456789, 0.5
-    y = ops.ref_cnn_stage0_fwd(x, c1, c2, seed, p, drop)
+    y, saved = ops.ref_cnn_stage0_fwd(x, c1, c2, seed, p, drop, save=True)
+    y_eval, none = ops.ref_cnn_stage0_fwd(x, c1, c2, seed, p, drop)
+    assert none is None and torch.equal(y, y_eval)
     ps = [t.detach().clone().requires_grad_(True) for t in (c1.weight, c1.bias, c2.weight, c2.bias)]
     y_ref = ref.ref_cnn_stage0(x, *ps, seed, 0, p, drop)
     close(y, y_ref.detach(), rtol=1e-5, atol=1e-5)
     gout = rnd(B, 320, seed=3)
-    ops.ref_cnn_stage0_bwd(x, c1, c2, gout, seed, p, drop)
+    ops.ref_cnn_stage0_bwd(x, c1, c2, y, gout, saved, seed, p, drop)
     gs = torch.autograd.grad(y_ref, ps, gout)
     for got, want in zip((c1.weight.grad, c1.bias.grad, c2.weight.grad, c2.bias.grad), gs):
         close(got, want, rtol=1e-4, atol=1e-4)
@@ -281,8 +283,8 @@ def test_ref_cnn_dropout_mask_statistics():
     # the kernel's masks: ~p dropped, whole channels in stage 0 (Dropout2d semantics)
     c1, c2, _, _ = _cnn_params(7)
     x = rnd(512, 1, 28, 28, seed=8).abs()
-    y0 = ops.ref_cnn_stage0_fwd(x, c1, c2, 1, 0.5, False)
-    y1 = ops.ref_cnn_stage0_fwd(x, c1, c2, 1, 0.5, True)
+    y0, _ = ops.ref_cnn_stage0_fwd(x, c1, c2, 1, 0.5, False)
+    y1, _ = ops.ref_cnn_stage0_fwd(x, c1, c2, 1, 0.5, True)
     ch0 = y0.view(512, 20, 16)
     ch1 = y1.view(512, 20, 16)
     dropped = (ch1.abs().sum(-1) == 0) & (ch0.abs().sum(-1) > 0)

@@ -86,7 +86,7 @@ def test_ref_cnn_cpu_ops_match_modules_without_dropout():
         p.grad = torch.zeros_like(p)
     x = torch.rand(9, 1, 28, 28)
     t = torch.randint(0, 10, (9,))
-    y = ops.ref_cnn_stage0_fwd(x, s0.conv1, s0.conv2, 5, 0.0, False)
+    y, _ = ops.ref_cnn_stage0_fwd(x, s0.conv1, s0.conv2, 5, 0.0, False)
     torch.testing.assert_close(y, s0(x))
     st = torch.zeros(2)
     dx = ops.ref_cnn_stage1(y, s1.fc1, s1.fc2, t, 5, 0.0, False, 0.5, st, True)

@@ -25,6 +25,7 @@ DEFAULTS = {  # model -> (schedule, micro-batches, batch, seq_len)
     "resnet18": ("1f1b", 8, 512, None),
     "gpt2": ("1f1b", 4, 16, 1024),
     "ref_cnn": ("1f1b", 1, 60, None),
+    "mlp": ("1f1b", 1, 60, None),  # the reference's own batch (13,704 samples/s at B=60)
 }
 
 
@@ -36,6 +37,7 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--seq_len", type=int, default=None)
+    ap.add_argument("--graph", action="store_true", help="replay the step from a captured hipGraph")
     a = ap.parse_args()
     kind, M, B, S = DEFAULTS[a.config]
     M = a.microbatches or M
@@ -60,8 +62,16 @@ def main():
         per_sample = 1
     GB = B * eng.data_shards
 
+    graphed = None
+    if a.graph:
+        from simple_distributed_machine_learning_amd.parallel.graphs import GraphedStep
+
+        graphed = GraphedStep(eng)
+
     def step(i):
         st = (i % nb) * GB
+        if graphed is not None:
+            return graphed(ds, eng.local_start(st, B), B, global_batch=GB)
         return eng.run(ds, eng.local_start(st, B), B, train=True, global_batch=GB)
 
     def sync():
@@ -81,7 +91,7 @@ def main():
     l, c, n = eng.reduce_metrics(res)
     if rank == 0:
         print(json.dumps({"config": a.config, "schedule": kind, "stages": stages, "ranks": world,
-                          "microbatches": M, "batch": GB, "seq_len": S, "dtype": str(spec.param_dtype),
+                          "microbatches": M, "batch": GB, "seq_len": S, "dtype": str(spec.param_dtype), "graph": bool(a.graph),
                           "value": round(GB * per_sample * a.steps / el, 1), "unit": unit,
                           "ms_per_step": round(el / a.steps * 1e3, 3), "loss": round(l / max(1, n), 4),
                           "bubble_model": round(eng.schedule(M, False).bubble_fraction(), 3)}))

@@ -23,6 +23,8 @@
 // MFMA C/D map (gfx950, dtype-independent): col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace sdml {
@@ -317,7 +319,183 @@ int gemm_f32_pick_splits(int M, int N, int K) {
   return splits < 1 ? 1 : splits;
 }
 
+namespace {
+// skinny-GEMM helpers: C rows <- bias (or 0) before a split-K atomic GEMM; relu / x>0 mask after
+__global__ void __launch_bounds__(256) rows_init_kernel(float* __restrict__ C, const float* __restrict__ bias, int M,
+                                                        int N, int ldc) {
+  const int64_t n = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int m = (int)(i / N), c = (int)(i % N);
+    C[(int64_t)m * ldc + c] = bias ? bias[c] : 0.f;
+  }
+}
+__global__ void __launch_bounds__(256) post_epi_kernel(float* __restrict__ C, const float* __restrict__ cmask, int M,
+                                                       int N, int ldc, int relu) {
+  const int64_t n = (int64_t)M * N;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int m = (int)(i / N), c = (int)(i % N);
+    float v = C[(int64_t)m * ldc + c];
+    if (relu) v = fmaxf(v, 0.f);
+    if (cmask && !(cmask[(int64_t)m * ldc + c] > 0.f)) v = 0.f;
+    C[(int64_t)m * ldc + c] = v;
+  }
+}
+// dW for a SMALL batch (the GEMM's K): gw[n][k] += sum_m gz(m,n) x[m][k], gb[n] += sum_m gz(m,n),
+// gz(m,n) = gy[m][n] * (mask[m][n] > 0). One thread owns DW_NG n x 4 k outputs (plain
+// read-modify-write: deterministic, no atomics, no 128x128 tile epilogue funnelled through a
+// few CUs); gy values are wave-broadcast. DW_NG = 1 maximises the wave count: with ~100
+// waves (DW_NG = 4) the kernel was VALU-issue bound on a quarter of the CUs.
+constexpr int DW_NG = 1;
+__global__ void __launch_bounds__(256) dw_smallk_kernel(const float* __restrict__ gy, const float* __restrict__ mask,
+                                                        const float* __restrict__ x, float* __restrict__ gw,
+                                                        float* __restrict__ gb, int M, int N, int K, int vec) {
+  const int K4 = (K + 3) / 4;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const int ng = idx / K4, k4 = idx % K4;
+  const int n0 = ng * DW_NG;
+  if (n0 >= N) return;
+  float acc[DW_NG][4] = {};
+  float gs[DW_NG] = {};
+  const int k0 = 4 * k4;
+  // batches of DW_MB rows: all their loads are issued before the FMAs (latency, not
+  // bandwidth, bounds this kernel: a few hundred waves, L2-resident operands)
+  constexpr int DW_MB = 8;
+  for (int mb = 0; mb < M; mb += DW_MB) {
+    float xv[DW_MB][4], gv[DW_MB][DW_NG];
+#pragma unroll
+    for (int u = 0; u < DW_MB; ++u) {
+      const int m = mb + u;
+      const bool ok = m < M;
+      const float* xr = x + (size_t)m * K + k0;
+      if (vec && ok) {
+        const float4 v = *reinterpret_cast<const float4*>(xr);
+        xv[u][0] = v.x;
+        xv[u][1] = v.y;
+        xv[u][2] = v.z;
+        xv[u][3] = v.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xv[u][j] = (ok && k0 + j < K) ? xr[j] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < DW_NG; ++i) {
+        const int n = n0 + i;
+        float g = 0.f;
+        if (ok && n < N) {
+          g = gy[(size_t)m * N + n];
+          if (mask && !(mask[(size_t)m * N + n] > 0.f)) g = 0.f;
+        }
+        gv[u][i] = g;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < DW_MB; ++u)
+#pragma unroll
+      for (int i = 0; i < DW_NG; ++i) {
+        gs[i] += gv[u][i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += gv[u][i] * xv[u][j];
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < DW_NG; ++i) {
+    const int n = n0 + i;
+    if (n >= N) break;
+    float* dst = gw + (size_t)n * K + k0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (k0 + j < K) dst[j] += acc[i][j];
+    if (gb && k4 == 0) gb[n] += gs[i];
+  }
+}
+// Forward GEMM for a SMALL batch: C[m][n] = epi(sum_k A[m][k] B[n][k] + bias[n]), both operands
+// k-contiguous (x @ W^T). A workgroup owns one row m and 64 outputs n (one per lane); its 4 waves
+// split K into quarters (float4 steps: the x row is wave-broadcast, every lane streams its own
+// W row from L2) and meet in LDS for the bias/ReLU epilogue. Grid M x N/64 (120 WGs at the
+// reference's 60 x 784 -> 128), versus a single 128x128 MFMA tile walking all of K.
+__global__ void __launch_bounds__(256) fwd_smallm_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                         const float* __restrict__ bias, float* __restrict__ C, int N,
+                                                         int K, int lda, int ldb, int ldc, int relu) {
+  __shared__ float red[4][64];
+  const int m = blockIdx.x, n0 = blockIdx.y * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n = n0 + lane;
+  const int K4 = K / 4, q = (K4 + 3) / 4;
+  const int kb = w * q, ke = min(K4, kb + q);
+  const float4* a = reinterpret_cast<const float4*>(A + (size_t)m * lda);
+  const float4* b = reinterpret_cast<const float4*>(B + (size_t)(n < N ? n : 0) * ldb);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int k4 = kb; k4 < ke; ++k4) {
+    const float4 av = a[k4], bv = b[k4];
+    acc[0] += av.x * bv.x;
+    acc[1] += av.y * bv.y;
+    acc[2] += av.z * bv.z;
+    acc[3] += av.w * bv.w;
+  }
+  red[w][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (w == 0 && n < N) {
+    float v = ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane])) + (bias ? bias[n] : 0.f);
+    if (relu) v = fmaxf(v, 0.f);
+    C[(size_t)m * ldc + n] = v;
+  }
+}
+
+}  // namespace
+
+void dw_smallk(const float* gy, const float* mask, const float* x, float* gw, float* gb, int M, int N, int K,
+               hipStream_t stream) {
+  const bool vec = (K % 4 == 0) && al16(x);
+  const int64_t threads = (int64_t)((N + DW_NG - 1) / DW_NG) * ((K + 3) / 4);
+  hipLaunchKernelGGL(dw_smallk_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, gy, mask, x, gw,
+                     gb, M, N, K, vec ? 1 : 0);
+}
+
+// Few output tiles and a long K (e.g. a batch-60 forward: ONE 128x128 tile, K = 784) leave
+// the chip idle and run one block through the whole K. Split K instead and accumulate with
+// fp32 atomics into C pre-set to the bias, then apply ReLU / the x>0 mask in a light pass:
+// three short launches instead of one long serial one. 0 = not worth it.
+int gemm_f32_skinny_splits(int M, int N, int K, int epi) {
+  if (epi == EPI_ATOMIC) return 0;
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (tiles > 32 || K < 256) return 0;
+  int splits = 256 / tiles;
+  const int max_by_k = K / (2 * BK_MAX);  // >= 2 K-steps per split
+  if (splits > max_by_k) splits = max_by_k;
+  return splits >= 4 ? splits : 0;
+}
+
 void gemm_f32(const GemmArgs& g, hipStream_t stream) {
+  if (g.M <= FWD_SMALLM_MAX_M && !g.a_kmajor && !g.b_kmajor && g.splits <= 1 && !g.amask && !g.rowsum &&
+      (g.epi == EPI_BIAS || g.epi == EPI_BIAS_RELU || (g.epi == EPI_STORE && !g.cmask)) && g.K % 4 == 0 &&
+      al16(g.A) && al16(g.B) && g.lda % 4 == 0 && g.ldb % 4 == 0) {
+    hipLaunchKernelGGL(fwd_smallm_kernel, dim3(g.M, (g.N + 63) / 64), dim3(256), 0, stream, g.A, g.B,
+                       g.epi == EPI_STORE ? nullptr : g.bias, g.C, g.N, g.K, g.lda, g.ldb, g.ldc,
+                       g.epi == EPI_BIAS_RELU ? 1 : 0);
+    return;
+  }
+  if (g.splits <= 1 && g.epi != EPI_ATOMIC) {
+    const int sk = gemm_f32_skinny_splits(g.M, g.N, g.K, g.epi);
+    if (sk > 0) {
+      const int64_t n = (int64_t)g.M * g.N;
+      const int eb = (int)std::min<int64_t>((n + 255) / 256, 1024);
+      if (g.epi != EPI_ACCUM)
+        hipLaunchKernelGGL(rows_init_kernel, dim3(eb), dim3(256), 0, stream, g.C,
+                           (g.epi == EPI_BIAS || g.epi == EPI_BIAS_RELU) ? g.bias : nullptr, g.M, g.N, g.ldc);
+      GemmArgs a = g;
+      a.epi = EPI_ATOMIC;
+      a.splits = sk;
+      a.bias = nullptr;
+      a.cmask = nullptr;  // rowsum (bias grad) is split-K safe: it stays
+      gemm_f32(a, stream);
+      const bool relu = g.epi == EPI_BIAS_RELU;
+      if (relu || (g.cmask && g.epi == EPI_STORE))
+        hipLaunchKernelGGL(post_epi_kernel, dim3(eb), dim3(256), 0, stream, g.C,
+                           g.epi == EPI_STORE ? g.cmask : nullptr, g.M, g.N, g.ldc, relu ? 1 : 0);
+      return;
+    }
+  }
   KParams p;
   p.A = g.A;
   p.amask = g.amask;

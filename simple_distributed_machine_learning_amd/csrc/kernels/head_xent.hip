@@ -11,6 +11,7 @@
 //      all chunks of the block; each block writes one partial slab (dW, db, loss, correct)
 //      and a second tiny pass sums the slabs in block order (deterministic, no contention).
 // Memory-bound by design (0.5 KiB read + 0.5 KiB written per sample); all MACs on VALU.
+// Small batches (<= 2048 rows) use 16-row chunks with 16 threads per row instead.
 //
 // head_generic: any K (multiple of 4) / C <= 32: computes loss/dz/dx per row (one wave per
 // row); dW/db are then done by the MFMA GEMM (gemm_f32 with fused row-sum).
@@ -25,20 +26,22 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int HK = 128;     // fused kernel: hidden width
 constexpr int CMAX = 16;    // fused kernel: max classes
-constexpr int ROWS = 64;    // rows per chunk
 constexpr int HTHR = 256;
 constexpr int XP = HK + 4;  // LDS row pitch of the x chunk
 
-template <int C>
+// TPR threads per row: 4 (64-row chunks) for large batches, 16 (16-row chunks) for small ones,
+// so a batch of 60 spreads over 4 workgroups instead of serialising through one.
+template <int C, int TPR>
 __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restrict__ x, const float* __restrict__ W,
                                                           const float* __restrict__ bias,
                                                           const int64_t* __restrict__ target, int M, float scale,
                                                           float* __restrict__ part, float* __restrict__ dx,
                                                           int chunks_per_block, int mask_dx) {
-  __shared__ __attribute__((aligned(16))) float xs[ROWS * XP];
+  constexpr int RWS = HTHR / TPR;  // rows per chunk
+  __shared__ __attribute__((aligned(16))) float xs[RWS * XP];
   __shared__ __attribute__((aligned(16))) float ws[C * HK];
   __shared__ float bs[CMAX];
-  __shared__ float dzs[ROWS * C];
+  __shared__ float dzs[RWS * C];
   __shared__ float red[2 * HTHR / 64];
   const int t = threadIdx.x;
   const bool train = dx != nullptr;
@@ -53,14 +56,14 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
   float gbacc = 0.f;
   float loss_acc = 0.f, corr_acc = 0.f;
 
-  const int row_in = t >> 2, q = t & 3;  // 4 threads per row, 32 k each
+  const int row_in = t / TPR, q = t % TPR;  // TPR threads per row, HK / TPR k each
   for (int ch = 0; ch < chunks_per_block; ++ch) {
-    const int r0 = (blockIdx.x * chunks_per_block + ch) * ROWS;
+    const int r0 = (blockIdx.x * chunks_per_block + ch) * RWS;
     if (r0 >= M) break;
     __syncthreads();  // previous chunk fully consumed (and ws/bs visible on first pass)
     // stage x chunk
 #pragma unroll
-    for (int i = 0; i < ROWS * HK / 4 / HTHR; ++i) {
+    for (int i = 0; i < RWS * HK / 4 / HTHR; ++i) {
       int idx = t + HTHR * i;
       int r = idx >> 5, k4 = idx & 31;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -73,10 +76,10 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
     float z[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) z[c] = 0.f;
-    // thread q covers k = 4*(q + 4*j) .. +3, j = 0..7 (interleaved -> conflict-light LDS reads)
+    // thread q covers k = 4*(q + TPR*j) .. +3 (interleaved -> conflict-light LDS reads)
 #pragma unroll
-    for (int j = 0; j < HK / 16; ++j) {
-      const int k = 4 * (q + 4 * j);
+    for (int j = 0; j < HK / (4 * TPR); ++j) {
+      const int k = 4 * (q + TPR * j);
       f32x4 xv = *reinterpret_cast<const f32x4*>(xs + row_in * XP + k);
 #pragma unroll
       for (int c = 0; c < C; ++c) {
@@ -86,8 +89,8 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      z[c] += __shfl_xor(z[c], 1);
-      z[c] += __shfl_xor(z[c], 2);
+#pragma unroll
+      for (int off = 1; off < TPR; off <<= 1) z[c] += __shfl_xor(z[c], off);
       z[c] += bs[c];
     }
     float mx = z[0];
@@ -123,8 +126,8 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
       }
       if (valid) {
 #pragma unroll
-        for (int j = 0; j < HK / 16; ++j) {
-          const int k = 4 * (q + 4 * j);
+        for (int j = 0; j < HK / (4 * TPR); ++j) {
+          const int k = 4 * (q + TPR * j);
           f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int c = 0; c < C; ++c) {
@@ -150,13 +153,13 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
           const int c = o / HK, k = o % HK;
           float s = 0.f;
 #pragma unroll 8
-          for (int r = 0; r < ROWS; ++r) s += dzs[r * C + c] * xs[r * XP + k];
+          for (int r = 0; r < RWS; ++r) s += dzs[r * C + c] * xs[r * XP + k];
           gacc[u] += s;
         }
       }
       if (t < C) {
         float s = 0.f;
-        for (int r = 0; r < ROWS; ++r) s += dzs[r * C + t];
+        for (int r = 0; r < RWS; ++r) s += dzs[r * C + t];
         gbacc += s;
       }
     }
@@ -304,8 +307,12 @@ bool head_fused_supported(int K, int C) { return K == HK && (C == 10 || C == 2 |
 
 // grid of the fused kernel: enough blocks to fill the chip, each keeping its dW partial in
 // registers over several 64-row chunks (fewer slabs to reduce)
+constexpr int SMALL_BATCH = 2048;  // <= this many rows: 16-row chunks (TPR = 16)
+int head_rows_per_chunk(int M) { return M <= SMALL_BATCH ? HTHR / 16 : HTHR / 4; }
+
 int head_fused_blocks(int M, int* chunks_per_block) {
-  const int chunks = (M + ROWS - 1) / ROWS;
+  const int rows = head_rows_per_chunk(M);
+  const int chunks = (M + rows - 1) / rows;
   int blocks = chunks < 512 ? chunks : 512;
   int cpb = (chunks + blocks - 1) / blocks;
   blocks = (chunks + cpb - 1) / cpb;
@@ -325,20 +332,22 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
   if (M <= 0) return;
   if (head_fused_supported(K, C) && dz_out == nullptr && workspace != nullptr) {
     int cpb = 0, blocks = head_fused_blocks(M, &cpb);
+#define HEAD_LAUNCH(CC, TT)                                                                             \
+  hipLaunchKernelGGL((head_fused_kernel<CC, TT>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale, \
+                     workspace, dx, cpb, mask_dx ? 1 : 0)
+    const bool small = M <= SMALL_BATCH;
     switch (C) {
       case 10:
-        hipLaunchKernelGGL((head_fused_kernel<10>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
-                           workspace, dx, cpb, mask_dx ? 1 : 0);
+        if (small) HEAD_LAUNCH(10, 16); else HEAD_LAUNCH(10, 4);
         break;
       case 2:
-        hipLaunchKernelGGL((head_fused_kernel<2>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
-                           workspace, dx, cpb, mask_dx ? 1 : 0);
+        if (small) HEAD_LAUNCH(2, 16); else HEAD_LAUNCH(2, 4);
         break;
       default:
-        hipLaunchKernelGGL((head_fused_kernel<16>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale,
-                           workspace, dx, cpb, mask_dx ? 1 : 0);
+        if (small) HEAD_LAUNCH(16, 16); else HEAD_LAUNCH(16, 4);
         break;
     }
+#undef HEAD_LAUNCH
     const int width = C * K + C + 2;
     hipLaunchKernelGGL(head_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, stream, workspace, blocks, C * K,
                        C, gW, gb, stats, dx != nullptr ? 1 : 0);

@@ -40,6 +40,16 @@ struct GemmArgs {
 bool gemm_f32_supported(const GemmArgs& g);
 void gemm_f32(const GemmArgs& g, hipStream_t stream);
 int gemm_f32_pick_splits(int M, int N, int K);
+// gemm_f32 internally splits K for few-tile/long-K shapes with non-atomic epilogues
+// (bias-init + atomic split-K + ReLU/mask pass); this is its split count, 0 = not used.
+int gemm_f32_skinny_splits(int M, int N, int K, int epi);
+// small-batch weight gradient (VALU, deterministic): gw[N,K] += (gy*(mask>0))^T[N,M] x[M,K];
+// gb[N] += column sums (gb/mask optional); gy/mask are [M,N], x is [M,K], all row-major
+constexpr int DW_SMALLK_MAX_M = 128;
+// gemm_f32 runs x @ W^T forwards with M <= this many rows on a VALU small-batch kernel
+constexpr int FWD_SMALLM_MAX_M = 64;
+void dw_smallk(const float* gy, const float* mask, const float* x, float* gw, float* gb, int M, int N, int K,
+               hipStream_t stream);
 void gemm_f32_set_variant(int v);  // tuning experiments: 0 auto, 16 / 32 = K-step
 
 // ---- fused classifier head: z = x W^T + b; log_softmax; NLL; backward --------------------

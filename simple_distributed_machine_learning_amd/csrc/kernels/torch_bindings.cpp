@@ -78,7 +78,12 @@ c10::optional<torch::Tensor> linear_bwd_f32(torch::Tensor x, c10::optional<torch
   check_opt(gw, "gw", N * K);
   check_opt(gb, "gb", N);
   hipStream_t s = cur_stream();
-  if (M > 0 && (opt_ptr(gw) || opt_ptr(gb))) {
+  if (M > 0 && M <= sdml::DW_SMALLK_MAX_M && opt_ptr(gw)) {
+    // small batch: one deterministic VALU pass (the MFMA GEMM would run K=M in a handful of
+    // blocks and spend its time in the 128x128-tile epilogue)
+    sdml::dw_smallk(gy.data_ptr<float>(), mask, x.data_ptr<float>(), opt_ptr(gw), opt_ptr(gb), (int)M, (int)N, (int)K,
+                    s);
+  } else if (M > 0 && (opt_ptr(gw) || opt_ptr(gb))) {
     // gw[N,K] += sum_m gz[m,n] x[m,k]: A(n,m) = gy[m*N + n] (k-major), B(k,m) = x[m*K + k] (k-major)
     sdml::GemmArgs g;
     g.A = gy.data_ptr<float>();

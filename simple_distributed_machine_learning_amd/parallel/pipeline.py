@@ -135,9 +135,11 @@ class PipelineEngine:
         # it is advanced by a (capturable) device op at the end of every training step, so a
         # replayed hipGraph draws fresh masks each step (see parallel/graphs.py)
         self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._uses_rng = False
         for m in self.stages.values():
             if getattr(m, "uses_rng_step", False):
                 m.rng_step = self.step_ctr
+                self._uses_rng = True
         self.optimizer = FusedSGD(self.flat, lr=lr, momentum=momentum, weight_decay=weight_decay)
         self.transport = Transport(mesh) if mesh.pp > 1 else None
         self.grad_sync = GradSync(self.flat, mesh, self.local_stage_ids)
@@ -148,6 +150,10 @@ class PipelineEngine:
         self.use_alltoall = os.environ.get("SDML_ROTATE_P2P") != "1"
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
+
+    def _advance_rng(self):
+        if self._uses_rng:  # one tiny launch per step, only for models with fused dropout
+            self.step_ctr.add_(1)
 
     # ---------------------------------------------------------------------------------------
     def schedule(self, m: int, forward_only: bool) -> Schedule:
@@ -206,7 +212,7 @@ class PipelineEngine:
                 if step_optimizer:
                     self.optimizer.step()
                     self.global_step += 1
-                self.step_ctr.add_(1)
+                self._advance_rng()
             z = torch.zeros(2, device=dev, dtype=torch.float32)
             return StepResult(z[0], z[1], 0, time.perf_counter() - t0)
         if self.kind == "rotate" and self.use_alltoall and self.P == 2:
@@ -335,7 +341,7 @@ class PipelineEngine:
             if step_optimizer:
                 self.optimizer.step()
                 self.global_step += 1
-            self.step_ctr.add_(1)
+            self._advance_rng()
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
 
     # ---------------------------------------------------------------------------------------
@@ -427,7 +433,7 @@ class PipelineEngine:
             if step_optimizer:
                 self.optimizer.step()
                 self.global_step += 1
-            self.step_ctr.add_(1)
+            self._advance_rng()
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
 
     def reduce_metrics(self, res: StepResult, group=None) -> Tuple[float, int, int]:

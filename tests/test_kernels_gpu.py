@@ -67,8 +67,8 @@ def test_gemm_epilogues_and_splitk():
         close(rs, A.sum(1), atol=2e-4, rtol=1e-5)
 
 
-@pytest.mark.parametrize("M", [60, 1000, 4096])
-@pytest.mark.parametrize("N,Kd", [(128, 784), (1024, 1024), (50, 320)])
+@pytest.mark.parametrize("M", [1, 7, 60, 128, 129, 1000, 4096])
+@pytest.mark.parametrize("N,Kd", [(128, 784), (1024, 1024), (50, 320), (50, 322)])
 def test_linear_relu_fwd_bwd(M, N, Kd):
     x, w, b = rnd(M, Kd, seed=7), rnd(N, Kd, seed=8) * 0.05, rnd(N, seed=9) * 0.1
     y = ops.linear_relu_fwd(x, w, b)
@@ -82,6 +82,17 @@ def test_linear_relu_fwd_bwd(M, N, Kd):
     close(dx, dx_r, atol=2e-4, rtol=1e-5)
     close(gw, gw_r, atol=5e-4 * max(1, M / 1000), rtol=1e-5)
     close(gb, gb_r, atol=5e-4 * max(1, M / 1000), rtol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(60, 1024, 1024), (1, 1024, 1024), (60, 784, 1024), (200, 512, 2048)])
+def test_skinny_split_k_epilogues(M, N, Kd):
+    # few output tiles + long K: split-K (bias init / atomics / ReLU-or-mask pass) path
+    x, w, b = rnd(M, Kd, seed=31).relu(), rnd(N, Kd, seed=32) * 0.05, rnd(N, seed=33) * 0.1
+    close(ops.linear_relu_fwd(x, w, b), torch.relu(x @ w.t() + b), atol=1e-4, rtol=1e-5)
+    close(ops.linear_fwd(x, w, b), x @ w.t() + b, atol=1e-4, rtol=1e-5)
+    gz = rnd(M, N, seed=34)
+    dx = ops.linear_relu_bwd(x, None, gz, w, None, None, True, gy_masked=True, mask_dx=True)
+    close(dx, (gz @ w) * (x > 0), atol=2e-4, rtol=1e-5)
 
 
 @pytest.mark.parametrize("M", [1, 60, 64, 1000, 70001])

@@ -91,6 +91,15 @@ int layernorm_bwd_blocks(int rows);
 void layernorm_bwd_bf16(const void* x, const void* w, const void* gy, const float* mean, const float* rstd, void* dx,
                         float* workspace, float* dwdb_acc, float* unused, int rows, int D, hipStream_t stream);
 
+// same, but dw/db are added straight into the bf16 parameter gradients gw/gb (no fp32 copy,
+// no separate accumulate kernel)
+void layernorm_bwd_bf16_accum(const void* x, const void* w, const void* gy, const float* mean, const float* rstd,
+                              void* dx, float* workspace, void* gw, void* gb, int rows, int D, hipStream_t stream);
+// bias gradient of a bf16 linear layer: gb[n] (bf16) += sum_m gy[m][n]; workspace fp32
+// [bias_grad_blocks(M) * N]. Deterministic (fixed-order partial sums).
+int bias_grad_blocks(int M);
+void bias_grad_bf16(const void* gy, int M, int N, int ld, void* gb, float* workspace, hipStream_t stream);
+
 // ---- causal flash attention, bf16, head_dim 64 ------------------------------------------
 // q/k/v (and dq/dk/dv) share one strided layout [b][h][s][64] (strides sqb, sqh, sqs; d
 // contiguous) — e.g. views into the fused c_attn output; o/dout share another (sob, soh, sos).

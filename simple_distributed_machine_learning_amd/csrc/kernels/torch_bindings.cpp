@@ -344,6 +344,44 @@ std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> layernorm_bwd_bf16(torch
   return {dx, dwdb.narrow(0, 0, D), dwdb.narrow(0, D, D)};
 }
 
+// layernorm backward accumulating dw/db into bf16 parameter grads; returns dx
+torch::Tensor layernorm_bwd_bf16_accum(torch::Tensor x, torch::Tensor w, torch::Tensor gy, torch::Tensor mean,
+                                       torch::Tensor rstd, torch::Tensor gw, torch::Tensor gb) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(w, "w");
+  check_bf16_cuda(gy, "gy");
+  check_bf16_cuda(gw, "gw");
+  check_bf16_cuda(gb, "gb");
+  check_f32_cuda(mean, "mean");
+  check_f32_cuda(rstd, "rstd");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(gy.sizes() == x.sizes() && mean.numel() == rows && rstd.numel() == rows && w.numel() == D &&
+                  gw.numel() == D && gb.numel() == D,
+              "ln bwd shapes");
+  auto dx = torch::empty_like(x);
+  auto ws = torch::empty({(int64_t)sdml::layernorm_bwd_blocks(rows) * 2 * D}, x.options().dtype(torch::kFloat32));
+  sdml::layernorm_bwd_bf16_accum(x.data_ptr(), w.data_ptr(), gy.data_ptr(), mean.data_ptr<float>(),
+                                 rstd.data_ptr<float>(), dx.data_ptr(), ws.data_ptr<float>(), gw.data_ptr(),
+                                 gb.data_ptr(), rows, D, cur_stream());
+  return dx;
+}
+
+// gb (bf16 [N]) += column sums of gy (bf16 [..., N], last dim contiguous)
+void bias_grad_bf16_(torch::Tensor gy, torch::Tensor gb) {
+  TORCH_CHECK(gy.is_cuda() && gy.scalar_type() == torch::kBFloat16 && gy.stride(-1) == 1,
+              "bias_grad: gy must be a bf16 device tensor with a contiguous last dim");
+  check_bf16_cuda(gb, "gb");
+  const int64_t N = gy.size(-1);
+  TORCH_CHECK(gb.numel() == N, "bias_grad: gb size");
+  auto g2 = gy.reshape({-1, N});
+  TORCH_CHECK(g2.stride(1) == 1, "bias_grad: rows must be addressable with one stride");
+  const int64_t M = g2.size(0);
+  if (M == 0) return;
+  auto ws = torch::empty({(int64_t)sdml::bias_grad_blocks(M) * N}, gy.options().dtype(torch::kFloat32));
+  sdml::bias_grad_bf16(g2.data_ptr(), (int)M, (int)N, (int)g2.stride(0), gb.data_ptr(), ws.data_ptr<float>(),
+                       cur_stream());
+}
+
 // q, k, v: [B, S, H, 64] bf16 views sharing strides (d contiguous), e.g. slices of the fused
 // qkv projection. Returns (out [B, S, H, 64] contiguous, lse fp32 [B*H*S]).
 std::tuple<torch::Tensor, torch::Tensor> attention_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, double scale,
@@ -526,6 +564,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cross_entropy_bf16", &cross_entropy_bf16, "vocab cross-entropy on bf16 logits (+ dlogits)");
   m.def("layernorm_fwd_bf16", &layernorm_fwd_bf16, "LayerNorm forward (bf16, fp32 stats)");
   m.def("layernorm_bwd_bf16", &layernorm_bwd_bf16, "LayerNorm backward (bf16)");
+  m.def("layernorm_bwd_bf16_accum", &layernorm_bwd_bf16_accum, "LayerNorm backward, dw/db added into bf16 grads");
+  m.def("bias_grad_bf16_", &bias_grad_bf16_, "gb += column sums of gy (bf16, deterministic)");
   m.def("attention_fwd", &attention_fwd, "causal flash attention forward (bf16, d=64)");
   m.def("attention_bwd", &attention_bwd, "causal flash attention backward (bf16, d=64)");
   m.def("gemm_f32_set_variant", &sdml::gemm_f32_set_variant, "fp32 GEMM variant (tuning: 0 auto, 16, 32)");

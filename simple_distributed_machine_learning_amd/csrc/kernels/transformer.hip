@@ -295,7 +295,76 @@ __global__ void __launch_bounds__(1024) slab_sum_kernel(const float* __restrict_
   }
 }
 
+// same reduction, accumulated straight into bf16 parameter gradients: outputs [0, split) go to
+// lo[o], [split, width) to hi[o - split] (hi may be null when split == width)
+__global__ void __launch_bounds__(1024) slab_sum_bf16_kernel(const float* __restrict__ part, int nblocks, int width,
+                                                             int split, u16* __restrict__ lo, u16* __restrict__ hi) {
+  __shared__ float acc[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int o = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (o < width) {
+    int b = w;
+    for (; b + 16 * 7 < nblocks; b += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(b + 16 * u) * width + o];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < nblocks; b += 16) s += part[(size_t)b * width + o];
+  }
+  acc[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && o < width) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += acc[i][lane];
+    u16* dst = o < split ? lo + o : hi + (o - split);
+    *dst = f2bf(bf2f(*dst) + t);
+  }
+}
+
+// bias gradient partials: part[blockIdx.y][n] = sum over this block's rows of gy[m][n] (fp32).
+// Block = 64 columns x 4 row lanes; rows of the block's range are strided by 4.
+constexpr int CS_T = 256;
+__global__ void __launch_bounds__(CS_T) colsum_partial_kernel(const u16* __restrict__ gy, int M, int N, int ld,
+                                                              int rows_per_block, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  float s = 0.f;
+  if (n < N) {
+    int r = r0 + rl;
+    for (; r + 12 < r1; r += 16) {
+      const float a = bf2f(gy[(size_t)r * ld + n]), b = bf2f(gy[(size_t)(r + 4) * ld + n]);
+      const float c = bf2f(gy[(size_t)(r + 8) * ld + n]), d = bf2f(gy[(size_t)(r + 12) * ld + n]);
+      s += (a + b) + (c + d);
+    }
+    for (; r < r1; r += 4) s += bf2f(gy[(size_t)r * ld + n]);
+  }
+  red[rl][lane] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) part[(size_t)blockIdx.y * N + n] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
 }  // namespace
+
+int bias_grad_blocks(int M) {
+  int r = (M + 63) / 64;
+  return r > 64 ? 64 : (r < 1 ? 1 : r);
+}
+
+void bias_grad_bf16(const void* gy, int M, int N, int ld, void* gb, float* workspace, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return;
+  const int R = bias_grad_blocks(M);
+  const int rpb = (M + R - 1) / R;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3((N + 63) / 64, R), dim3(CS_T), 0, stream,
+                     reinterpret_cast<const u16*>(gy), M, N, ld, rpb, workspace);
+  hipLaunchKernelGGL(slab_sum_bf16_kernel, dim3((N + 63) / 64), dim3(1024), 0, stream, workspace, R, N, N,
+                     reinterpret_cast<u16*>(gb), nullptr);
+}
 
 void cross_entropy_bf16(const void* logits, const int64_t* target, int rows, int V, int ld, float scale,
                         int ignore_index, float* row_loss, float* row_ok, void* dlogits, hipStream_t stream) {
@@ -342,6 +411,23 @@ void layernorm_bwd_bf16(const void* x, const void* w, const void* gy, const floa
   hipLaunchKernelGGL(slab_sum_kernel, dim3((2 * D + 63) / 64), dim3(1024), 0, stream, workspace, blocks, 2 * D,
                      dw_acc);
   (void)db_acc;  // dw_acc is [2*D]: dw followed by db (caller splits)
+}
+
+void layernorm_bwd_bf16_accum(const void* x, const void* w, const void* gy, const float* mean, const float* rstd,
+                              void* dx, float* workspace, void* gw, void* gb, int rows, int D, hipStream_t stream) {
+  if (rows <= 0) return;
+  const int blocks = layernorm_bwd_blocks(rows);
+#define LNB(V)                                                                                                 \
+  hipLaunchKernelGGL((ln_bwd_kernel<V>), dim3(blocks), dim3(LN_T), 0, stream, reinterpret_cast<const u16*>(x), \
+                     reinterpret_cast<const u16*>(w), reinterpret_cast<const u16*>(gy), mean, rstd,             \
+                     reinterpret_cast<u16*>(dx), workspace, rows, D)
+  if (D <= 512) LNB(1);
+  else if (D <= 1024) LNB(2);
+  else if (D <= 2048) LNB(4);
+  else LNB(8);
+#undef LNB
+  hipLaunchKernelGGL(slab_sum_bf16_kernel, dim3((2 * D + 63) / 64), dim3(1024), 0, stream, workspace, blocks, 2 * D, D,
+                     reinterpret_cast<u16*>(gw), reinterpret_cast<u16*>(gb));
 }
 
 }  // namespace sdml

@@ -7,7 +7,9 @@ at S=1024) — the large-activation send that RCCL p2p overlaps with compute.
 
 The output projection is untied from ``wte`` because the two live on different ranks
 (documented deviation from the 124M tied checkpoint; +38.6M parameters on the last stage).
-Parameter names follow the common GPT-2 layout (wte, wpe, h.{i}.ln_1, h.{i}.attn.c_attn,
+Linear layers (ops/linear.py) and LayerNorms accumulate their weight/bias gradients straight
+into the flat gradient buffer (GEMM beta = 1, in-place bf16 reductions) instead of
+materialise-then-add. Parameter names follow the common GPT-2 layout (wte, wpe, h.{i}.ln_1, h.{i}.attn.c_attn,
 h.{i}.attn.c_proj, h.{i}.ln_2, h.{i}.mlp.c_fc, h.{i}.mlp.c_proj, ln_f, lm_head).
 """
 from __future__ import annotations
@@ -20,6 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .base import ModelSpec, PipelineStage
+from ..ops.linear import Linear
 from ..ops.transformer import LayerNorm, causal_attention, cross_entropy_sum
 
 
@@ -36,8 +39,8 @@ class GPT2Config:
 class CausalSelfAttention(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
-        self.c_attn = nn.Linear(cfg.n_embd, 3 * cfg.n_embd)
-        self.c_proj = nn.Linear(cfg.n_embd, cfg.n_embd)
+        self.c_attn = Linear(cfg.n_embd, 3 * cfg.n_embd)
+        self.c_proj = Linear(cfg.n_embd, cfg.n_embd)
         self.n_head = cfg.n_head
 
     def forward(self, x):
@@ -48,8 +51,8 @@ class CausalSelfAttention(nn.Module):
 class MLP(nn.Module):
     def __init__(self, cfg: GPT2Config):
         super().__init__()
-        self.c_fc = nn.Linear(cfg.n_embd, 4 * cfg.n_embd)
-        self.c_proj = nn.Linear(4 * cfg.n_embd, cfg.n_embd)
+        self.c_fc = Linear(cfg.n_embd, 4 * cfg.n_embd)
+        self.c_proj = Linear(4 * cfg.n_embd, cfg.n_embd)
 
     def forward(self, x):
         return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
@@ -83,7 +86,7 @@ class GPT2Stage(PipelineStage):
         self.h = nn.ModuleDict({str(i): Block(cfg) for i in range(stage_id * per, (stage_id + 1) * per)})
         if stage_id == num_stages - 1:
             self.ln_f = LayerNorm(cfg.n_embd)
-            self.lm_head = nn.Linear(cfg.n_embd, cfg.vocab_size, bias=False)
+            self.lm_head = Linear(cfg.n_embd, cfg.vocab_size, bias=False)
         self._init()
 
     def _init(self):

@@ -24,11 +24,17 @@ class _LayerNormFn(torch.autograd.Function):
         xc = x.contiguous()
         y, mean, rstd = kernels().layernorm_fwd_bf16(xc, w, b, eps)
         ctx.save_for_backward(xc, w, mean, rstd)
+        ctx.params = (w, b)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w, mean, rstd = ctx.saved_tensors
+        wp, bp = ctx.params
+        if wp.grad is not None and bp.grad is not None and wp.grad.is_contiguous() and bp.grad.is_contiguous():
+            # flat-buffer gradients: dw/db are added in place by the reduction kernel
+            dx = kernels().layernorm_bwd_bf16_accum(x, w, gy.contiguous(), mean, rstd, wp.grad, bp.grad)
+            return dx, None, None, None
         dx, dw, db = kernels().layernorm_bwd_bf16(x, w, gy.contiguous(), mean, rstd)
         return dx, dw.to(w.dtype), db.to(w.dtype), None
 

@@ -303,3 +303,64 @@ def test_ref_cnn_dropout_mask_statistics():
     assert 0.45 < float(frac) < 0.55
     kept = ~dropped & (ch0.abs().sum(-1) > 0)
     close(ch1[kept], 2 * ch0[kept], rtol=1e-5, atol=1e-5)
+
+
+# ---- gradient-accumulating Linear / LayerNorm (ops/linear.py, transformer.hip) -------------
+@pytest.mark.parametrize("M,N", [(4096, 768), (5, 50), (1000, 3072), (64, 50257)])
+def test_bias_grad_bf16(M, N):
+    gy = rnd(M, N, seed=41).to(torch.bfloat16)
+    gb = rnd(N, seed=42).to(torch.bfloat16)
+    want = gb.float() + gy.float().sum(0)
+    K.bias_grad_bf16_(gy, gb)
+    close(gb.float(), want, rtol=1e-2, atol=2e-2 * max(1.0, (M / 1000) ** 0.5))
+
+
+@pytest.mark.parametrize("with_bias", [True, False])
+def test_fused_linear_accumulates_into_grad(with_bias):
+    from simple_distributed_machine_learning_amd.ops.linear import Linear
+
+    torch.manual_seed(3)
+    lin = Linear(96, 200, bias=with_bias).to(DEV, torch.bfloat16)
+    ref_lin = torch.nn.Linear(96, 200, bias=with_bias).to(DEV, torch.float32)
+    ref_lin.load_state_dict({k: v.float() for k, v in lin.state_dict().items()})
+    for p in lin.parameters():  # pre-existing (flat-buffer style) grads get ADDED to
+        p.grad = torch.full_like(p, 0.25)
+    for mb in range(2):  # two micro-batches accumulate
+        x = rnd(3, 40, 96, seed=50 + mb).to(torch.bfloat16).requires_grad_(True)
+        gy = rnd(3, 40, 200, seed=60 + mb).to(torch.bfloat16)
+        y = lin(x)
+        y.backward(gy)
+        xr = x.detach().float().requires_grad_(True)
+        yr = ref_lin(xr)
+        yr.backward(gy.float())
+        close(y.float(), yr.detach(), rtol=2e-2, atol=3e-2)
+        close(x.grad.float(), xr.grad, rtol=2e-2, atol=3e-2)
+    close(lin.weight.grad.float(), 0.25 + ref_lin.weight.grad, rtol=2e-2, atol=1e-1)
+    if with_bias:
+        close(lin.bias.grad.float(), 0.25 + ref_lin.bias.grad, rtol=2e-2, atol=1e-1)
+    # no pre-existing grads: ordinary autograd accumulation
+    lin2 = Linear(96, 200, bias=with_bias).to(DEV, torch.bfloat16)
+    x = rnd(7, 96, seed=70).to(torch.bfloat16)
+    lin2(x).float().sum().backward()
+    assert lin2.weight.grad is not None and torch.isfinite(lin2.weight.grad.float()).all()
+
+
+def test_layernorm_accumulates_into_grad():
+    from simple_distributed_machine_learning_amd.ops.transformer import LayerNorm
+
+    ln = LayerNorm(768).to(DEV, torch.bfloat16)
+    with torch.no_grad():
+        ln.weight.copy_(rnd(768, seed=80).to(torch.bfloat16))
+        ln.bias.copy_(rnd(768, seed=81).to(torch.bfloat16))
+    ln.weight.grad = torch.full_like(ln.weight, 0.5)
+    ln.bias.grad = torch.full_like(ln.bias, -0.5)
+    x = rnd(4, 64, 768, seed=82).to(torch.bfloat16).requires_grad_(True)
+    gy = rnd(4, 64, 768, seed=83).to(torch.bfloat16)
+    ln(x).backward(gy)
+    xr = x.detach().float().requires_grad_(True)
+    wr = ln.weight.detach().float().requires_grad_(True)
+    br = ln.bias.detach().float().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr, (768,), wr, br, 1e-5).backward(gy.float())
+    close(x.grad.float(), xr.grad, rtol=3e-2, atol=5e-2)
+    close(ln.weight.grad.float(), 0.5 + wr.grad, rtol=2e-2, atol=2e-1)
+    close(ln.bias.grad.float(), -0.5 + br.grad, rtol=2e-2, atol=2e-1)

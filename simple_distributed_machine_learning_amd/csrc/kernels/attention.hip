@@ -20,6 +20,19 @@
 //        scalar multiply. LSE (log2 domain) is saved for the backward pass.
 // Backward: dK/dV kernel (workgroup = 128 keys; loops over query blocks) and dQ kernel
 // (workgroup = 128 queries; loops over key blocks) — no atomics, P recomputed from LSE.
+//
+// Tiles (64 rows x 64 d, bf16) live in LDS as ONE swizzled row-major image each, read two ways:
+//   * by rows with ds_read_b128 (operands whose MFMA k is d: S = K Q^T, dP = dO V^T, ...)
+//   * by columns with ds_read_b64_tr_b16 (operands whose MFMA k is the key/query axis:
+//     V^T P^T, dO^T P, Q^T dS, K^T dS^T) — the hardware transpose read replaces a transposed
+//     second copy written element by element.
+//   Chunk c (16 B) of row r is stored at chunk c ^ f(r), f(r) = ((r>>1)&1)<<2 | ((r>>2)&3):
+//   both read kinds are bank-conflict-free on 128-B rows (the row reads' 16-lane groups hit
+//   16 distinct 16-B slots; each 32-lane half of a transposed read covers 4 rows x 4 chunks in
+//   16 distinct slots).
+// Every loop double-buffers its tiles: the next tile's global loads are issued into registers
+// before the current tile's MFMAs and written to the other LDS buffer after them, so the HBM/L2
+// latency hides behind compute and each iteration has one barrier.
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 
@@ -40,8 +53,6 @@ constexpr int QW = 32;             // queries per wave
 constexpr int NW = 4;              // waves per workgroup
 constexpr int QB = QW * NW;        // queries per workgroup
 constexpr int KB = 64;             // keys per iteration
-constexpr int KP = HD + 8;         // LDS pitch (bf16) of row-major [key][d] tiles: 144 B rows
-constexpr int TP = KB + 8;         // LDS pitch (bf16) of transposed [d][key] tiles
 constexpr float LOG2E = 1.4426950408889634f;
 
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((unsigned)v) << 16); }
@@ -70,21 +81,53 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int s) {
   return r;
 }
 
-// fragment in the accumulator k-order from a transposed image T[row][key]:
-// element j = T[row][k0 + 8(j>>2) + 4h + (j&3)]  (two 8-byte reads)
-__device__ __forceinline__ bf16x8 tr_frag(const u16* T, int pitch, int row, int k0, int h) {
-  const u16* p = T + row * pitch + k0 + 4 * h;
-  bf16x4 lo = *reinterpret_cast<const bf16x4*>(p);
-  bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + 8);
+// ---- swizzled tile image ----------------------------------------------------------------------
+constexpr int TR = 64;  // rows per staged tile (KB keys or BQ queries)
+__device__ __forceinline__ int swz(int r, int ch) {
+  return r * HD + 8 * (ch ^ ((((r >> 1) & 1) << 2) | ((r >> 2) & 3)));
+}
+// row fragment (A/B operand with k = d): element j = X[row][16t + 8h + j]
+__device__ __forceinline__ bf16x8 rowf(const u16* X, int row, int t, int h) {
+  return *reinterpret_cast<const bf16x8*>(X + swz(row, 2 * t + h));
+}
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+__device__ __forceinline__ s16x4 ds_tr16(const u16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+// transposed fragment in the accumulator k-order: element j = X[k0 + 8(j>>2) + 4h + (j&3)][c0 + (lane&31)]
+// (k0 % 8 == 0, c0 % 32 == 0). Two ds_read_b64_tr_b16: each 16-lane group g reads rows
+// k0 + 4(g>>1) + q (q = 0..3) at columns c0 + 16(g&1) + 0..15; lane 4q+p supplies row q, cols 4p..4p+3.
+// Must run with all 64 lanes active.
+__device__ __forceinline__ bf16x8 trf(const u16* X, int k0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int R = k0 + 4 * (g >> 1) + q;
+  const int col = c0 + 16 * (g & 1) + 4 * p;
+  const s16x4 lo = ds_tr16(X + swz(R, col >> 3) + (col & 7));
+  const s16x4 hi = ds_tr16(X + swz(R + 8, col >> 3) + (col & 7));
   bf16x8 r;
   r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
 }
-
-// natural-order fragment of row `row` of a row-major [row][d] image: element j = X[row][k0 + 8h + j]
-__device__ __forceinline__ bf16x8 row_frag(const u16* X, int pitch, int row, int k0, int h) {
-  return *reinterpret_cast<const bf16x8*>(X + row * pitch + k0 + 8 * h);
+// a 64-row tile in registers (2 x 16 B per thread) on its way from global memory to LDS
+struct TileRegs {
+  u16x8 v[2];
+};
+__device__ __forceinline__ void tile_load(TileRegs& t, const u16* G, long srow, int r0, int S) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int idx = threadIdx.x + 256 * u, r = idx >> 3, ch = idx & 7;
+    u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r0 + r < S) v = *reinterpret_cast<const u16x8*>(G + (long)(r0 + r) * srow + 8 * ch);
+    t.v[u] = v;
+  }
+}
+__device__ __forceinline__ void tile_store(u16* L, const TileRegs& t) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int idx = threadIdx.x + 256 * u, r = idx >> 3, ch = idx & 7;
+    *reinterpret_cast<u16x8*>(L + swz(r, ch)) = t.v[u];
+  }
 }
 
 struct AttnArgs {
@@ -98,33 +141,11 @@ struct AttnArgs {
   int causal;
 };
 
-// cooperative copy of `rows` rows x 64 d (bf16) starting at global row r0 into a row-major
-// LDS image [row][KP]; rows beyond S are zero-filled. 256 threads, 16 B each.
-__device__ __forceinline__ void stage_rows(u16* L, const u16* G, long srow, int r0, int rows, int S) {
-  for (int c = threadIdx.x; c < rows * 8; c += 256) {
-    int r = c >> 3, ch = c & 7;
-    u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (r0 + r < S) v = *reinterpret_cast<const u16x8*>(G + (long)(r0 + r) * srow + 8 * ch);
-    *reinterpret_cast<u16x8*>(L + r * KP + 8 * ch) = v;
-  }
-}
-
-// same rows stored transposed: T[d][row] with pitch TP
-__device__ __forceinline__ void stage_rows_tr(u16* T, const u16* G, long srow, int r0, int rows, int S) {
-  for (int c = threadIdx.x; c < rows * 8; c += 256) {
-    int r = c >> 3, ch = c & 7;
-    u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (r0 + r < S) v = *reinterpret_cast<const u16x8*>(G + (long)(r0 + r) * srow + 8 * ch);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) T[(8 * ch + e) * TP + r] = v[e];
-  }
-}
-
 // ============================================================================================
 // forward
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 Ks[KB * KP];
-  __shared__ __attribute__((aligned(16))) u16 Vt[HD * TP];
+  __shared__ __attribute__((aligned(16))) u16 Ks[2][TR * HD];
+  __shared__ __attribute__((aligned(16))) u16 Vs[2][TR * HD];
   const int nqb = (a.S + QB - 1) / QB;
   const int bh = blockIdx.x / nqb;
   const int qb = nqb - 1 - (blockIdx.x % nqb);  // heaviest (causal) blocks first
@@ -147,59 +168,78 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   float m = -INFINITY, l = 0.f;
   f32x16 o[2] = {zero16(), zero16()};  // O^T[d][q]: d tile 0..1
   const int kend = a.causal ? min(a.S, qb * QB + QB) : a.S;
-  for (int k0 = 0; k0 < kend; k0 += KB) {
-    __syncthreads();
-    stage_rows(Ks, K, a.sqs, k0, KB, a.S);
-    stage_rows_tr(Vt, V, a.sqs, k0, KB, a.S);
-    __syncthreads();
-    if (a.causal && k0 > q0w + QW - 1) continue;  // this wave's queries are all before k0
-    // S^T for two 32-key sub-blocks
-    f32x16 s[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      s[c] = zero16();
-#pragma unroll
-      for (int t = 0; t < 4; ++t) s[c] = mfma(row_frag(Ks, KP, 32 * c + r, 16 * t, h), qf[t], s[c]);
+  TileRegs kr, vr;
+  tile_load(kr, K, a.sqs, 0, a.S);
+  tile_load(vr, V, a.sqs, 0, a.S);
+  tile_store(Ks[0], kr);
+  tile_store(Vs[0], vr);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < kend; k0 += KB, buf ^= 1) {
+    const bool more = k0 + KB < kend;
+    if (more) {  // next tile's loads fly during this tile's MFMAs
+      tile_load(kr, K, a.sqs, k0 + KB, a.S);
+      tile_load(vr, V, a.sqs, k0 + KB, a.S);
     }
-    // scale, mask, running max
-    float mx = m;
+    if (!(a.causal && k0 > q0w + QW - 1)) {  // else: all this wave's queries precede k0
+      const u16* Kt = Ks[buf];
+      const u16* Vt = Vs[buf];
+      // S^T for two 32-key sub-blocks
+      f32x16 s[2];
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < 2; ++c) {
+        s[c] = zero16();
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int kj = k0 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
-        float v = s[c][i] * sl2;
-        if (kj >= a.S || (a.causal && kj > qi)) v = -INFINITY;
-        s[c][i] = v;
-        mx = fmaxf(mx, v);
+        for (int t = 0; t < 4; ++t) s[c] = mfma(rowf(Kt, 32 * c + r, t, h), qf[t], s[c]);
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float alpha = (m == -INFINITY) ? 0.f : exp2f(m - mx);
-    float rs = 0.f;
+      // scale (+ mask on the diagonal / ragged tiles only), running max
+      const bool edge = (a.causal && k0 + KB - 1 > q0w) || k0 + KB > a.S;
+      float mx = m;
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p = (mx == -INFINITY) ? 0.f : exp2f(s[c][i] - mx);
-        s[c][i] = p;
-        rs += p;
-      }
-    rs += __shfl_xor(rs, 32);
-    l = l * alpha + rs;
-    m = mx;
+        for (int i = 0; i < 16; ++i) {
+          float v = s[c][i] * sl2;
+          if (edge) {
+            const int kj = k0 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (kj >= a.S || (a.causal && kj > qi)) v = -INFINITY;
+          }
+          s[c][i] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float alpha = (m == -INFINITY) ? 0.f : exp2f(m - mx);
+      float rs = 0.f;
 #pragma unroll
-    for (int d = 0; d < 2; ++d)
+      for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
-    // O^T[d][q] += sum_k V^T[d][k] P^T[k][q]
+        for (int i = 0; i < 16; ++i) {
+          float p = (mx == -INFINITY) ? 0.f : exp2f(s[c][i] - mx);
+          s[c][i] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 32);
+      l = l * alpha + rs;
+      m = mx;
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+      for (int d = 0; d < 2; ++d)
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        bf16x8 pb = pack8(s[c], st);
+        for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+      // O^T[d][q] += sum_k V^T[d][k] P^T[k][q]   (V^T by transposed reads of the V image)
 #pragma unroll
-        for (int d = 0; d < 2; ++d) o[d] = mfma(tr_frag(Vt, TP, 32 * d + r, 32 * c + 16 * st, h), pb, o[d]);
-      }
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          bf16x8 pb = pack8(s[c], st);
+#pragma unroll
+          for (int d = 0; d < 2; ++d) o[d] = mfma(trf(Vt, 32 * c + 16 * st, 32 * d, lane), pb, o[d]);
+        }
+    }
+    if (more) {
+      tile_store(Ks[buf ^ 1], kr);
+      tile_store(Vs[buf ^ 1], vr);
+    }
+    __syncthreads();
   }
   if (qi >= a.S) return;
   const float inv = l > 0.f ? 1.f / l : 0.f;
@@ -217,7 +257,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 }
 
 // ============================================================================================
-// backward, part 0: delta[q] = sum_d dO[q][d] * O[q][d]   (one wave per 64 queries... per row)
+// backward, part 0: delta[q] = sum_d dO[q][d] * O[q][d]   (one thread per query row)
 __global__ void __launch_bounds__(256) attn_delta_kernel(AttnArgs a) {
   const long rows = (long)a.B * a.H * a.S;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < rows; i += (long)gridDim.x * 256) {
@@ -238,23 +278,21 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(AttnArgs a) {
 }
 
 // backward, part 1: dK, dV. Workgroup = 128 keys (wave = 32 keys); loop over query blocks of 64.
-//   S  = Q K^T      (A = Q rows from LDS, B = K rows of this wave -> registers); C: key on lane
+//   S  = Q K^T      (A = Q rows, B = K rows of this wave -> registers); C: key on lane
 //   P  = exp2(S*c - lse[q])                       (lse per register row, from LDS)
-//   dV^T[d][k] += dO^T[d][q] P[q][k]              (A = dO^T transposed image, B = P registers)
-//   dP = dO V^T     (A = dO rows from LDS, B = V rows of this wave -> registers)
+//   dV^T[d][k] += dO^T[d][q] P[q][k]              (A = dO^T by transposed reads, B = P registers)
+//   dP = dO V^T     (A = dO rows, B = V rows of this wave -> registers)
 //   dS = P (dP - delta[q])
-//   dK^T[d][k] += Q^T[d][q] dS[q][k]              (A = Q^T transposed image, B = dS registers)
+//   dK^T[d][k] += Q^T[d][q] dS[q][k]              (A = Q^T by transposed reads, B = dS registers)
 constexpr int BQ = 64;  // queries per iteration (backward)
 
 __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 Qs[BQ * KP];
-  __shared__ __attribute__((aligned(16))) u16 Qt[HD * TP];
-  __shared__ __attribute__((aligned(16))) u16 Ds[BQ * KP];
-  __shared__ __attribute__((aligned(16))) u16 Dt[HD * TP];
-  __shared__ float Ls[BQ], Dl[BQ];
+  __shared__ __attribute__((aligned(16))) u16 Qs[2][TR * HD];
+  __shared__ __attribute__((aligned(16))) u16 Ds[2][TR * HD];
+  __shared__ float Ls[2][BQ], Dl[2][BQ];
   const int nkb = (a.S + QB - 1) / QB;
   const int bh = blockIdx.x / nkb;
-  const int kb = blockIdx.x % nkb;  // light blocks (early keys see many queries) first... any order
+  const int kb = blockIdx.x % nkb;
   const int b = bh / a.H, hh = bh % a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const long off = (long)b * a.sqb + (long)hh * a.sqh;
@@ -274,47 +312,73 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
   const float sl2 = a.scale * LOG2E;
   f32x16 dv[2] = {zero16(), zero16()}, dk[2] = {zero16(), zero16()};
   const int qstart = a.causal ? (kb * QB) / BQ * BQ : 0;
-  for (int q0 = qstart; q0 < a.S; q0 += BQ) {
-    __syncthreads();
-    stage_rows(Qs, a.q + off, a.sqs, q0, BQ, a.S);
-    stage_rows_tr(Qt, a.q + off, a.sqs, q0, BQ, a.S);
-    stage_rows(Ds, a.dout + ooff, a.sos, q0, BQ, a.S);
-    stage_rows_tr(Dt, a.dout + ooff, a.sos, q0, BQ, a.S);
+  const float* LSE = a.lse + (long)bh * a.S;
+  const float* DEL = a.delta + (long)bh * a.S;
+  TileRegs qr, dr;
+  float lr = 0.f, dlr = 0.f;
+  auto load = [&](int q0) {
+    tile_load(qr, a.q + off, a.sqs, q0, a.S);
+    tile_load(dr, a.dout + ooff, a.sos, q0, a.S);
     if (threadIdx.x < BQ) {
       const int qi = q0 + threadIdx.x;
-      Ls[threadIdx.x] = qi < a.S ? a.lse[(long)bh * a.S + qi] : 0.f;
-      Dl[threadIdx.x] = qi < a.S ? a.delta[(long)bh * a.S + qi] : 0.f;
+      lr = qi < a.S ? LSE[qi] : 0.f;
+      dlr = qi < a.S ? DEL[qi] : 0.f;
     }
-    __syncthreads();
-    if (a.causal && q0 + BQ - 1 < k0w) continue;  // all these queries precede this wave's keys
+  };
+  auto store = [&](int bi) {
+    tile_store(Qs[bi], qr);
+    tile_store(Ds[bi], dr);
+    if (threadIdx.x < BQ) {
+      Ls[bi][threadIdx.x] = lr;
+      Dl[bi][threadIdx.x] = dlr;
+    }
+  };
+  if (qstart < a.S) {
+    load(qstart);
+    store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int q0 = qstart; q0 < a.S; q0 += BQ, buf ^= 1) {
+    const bool more = q0 + BQ < a.S;
+    if (more) load(q0 + BQ);
+    if (!(a.causal && q0 + BQ - 1 < k0w)) {  // else: all these queries precede this wave's keys
+      const u16* Qt = Qs[buf];
+      const u16* Dt = Ds[buf];
+      const bool edge = (a.causal && q0 < k0w + QW - 1) || q0 + BQ > a.S || kj >= a.S;
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {  // 32-query sub-blocks
-      f32x16 s = zero16(), dp = zero16();
+      for (int c = 0; c < 2; ++c) {  // 32-query sub-blocks
+        f32x16 s = zero16(), dp = zero16();
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        s = mfma(row_frag(Qs, KP, 32 * c + r, 16 * t, h), kf[t], s);
-        dp = mfma(row_frag(Ds, KP, 32 * c + r, 16 * t, h), vf[t], dp);
-      }
-      // rows of s/dp are queries: q = q0 + 32c + (i&3) + 8(i>>2) + 4h
+        for (int t = 0; t < 4; ++t) {
+          s = mfma(rowf(Qt, 32 * c + r, t, h), kf[t], s);
+          dp = mfma(rowf(Dt, 32 * c + r, t, h), vf[t], dp);
+        }
+        // rows of s/dp are queries: q = q0 + 32c + (i&3) + 8(i>>2) + 4h
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int ql = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
-        const int qi = q0 + ql;
-        float p = exp2f(s[i] * sl2 - Ls[ql]);
-        if (qi >= a.S || kj >= a.S || (a.causal && kj > qi)) p = 0.f;
-        s[i] = p;
-        dp[i] = p * (dp[i] - Dl[ql]);  // dS (scale applied to dK at the end)
-      }
+        for (int i = 0; i < 16; ++i) {
+          const int ql = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
+          float p = exp2f(s[i] * sl2 - Ls[buf][ql]);
+          if (edge) {
+            const int qi = q0 + ql;
+            if (qi >= a.S || kj >= a.S || (a.causal && kj > qi)) p = 0.f;
+          }
+          s[i] = p;
+          dp[i] = p * (dp[i] - Dl[buf][ql]);  // dS (scale applied to dK at the end)
+        }
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        bf16x8 pb = pack8(s, st), db = pack8(dp, st);
+        for (int st = 0; st < 2; ++st) {
+          bf16x8 pb = pack8(s, st), db = pack8(dp, st);
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          dv[d] = mfma(tr_frag(Dt, TP, 32 * d + r, 32 * c + 16 * st, h), pb, dv[d]);
-          dk[d] = mfma(tr_frag(Qt, TP, 32 * d + r, 32 * c + 16 * st, h), db, dk[d]);
+          for (int d = 0; d < 2; ++d) {
+            dv[d] = mfma(trf(Dt, 32 * c + 16 * st, 32 * d, lane), pb, dv[d]);
+            dk[d] = mfma(trf(Qt, 32 * c + 16 * st, 32 * d, lane), db, dk[d]);
+          }
         }
       }
     }
+    if (more) store(buf ^ 1);
+    __syncthreads();
   }
   if (kj >= a.S) return;
   // dV^T / dK^T: lane = key, register rows = d
@@ -336,15 +400,14 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
 }
 
 // backward, part 2: dQ. Workgroup = 128 queries (wave = 32); loop over key blocks of 64.
-//   S^T  = K Q^T     (A = K rows from LDS, B = Q rows of this wave -> registers); lane = query
+//   S^T  = K Q^T     (A = K rows, B = Q rows of this wave -> registers); lane = query
 //   P^T  = exp2(S^T c - lse[q])      (lse per lane)
-//   dP^T = V dO^T    (A = V rows from LDS, B = dO rows of this wave -> registers)
+//   dP^T = V dO^T    (A = V rows, B = dO rows of this wave -> registers)
 //   dS^T = P^T (dP^T - delta[q])
-//   dQ^T[d][q] += K^T[d][k] dS^T[k][q]   (A = K^T transposed image, B = dS^T registers)
+//   dQ^T[d][q] += K^T[d][k] dS^T[k][q]   (A = K^T by transposed reads, B = dS^T registers)
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 Ks[KB * KP];
-  __shared__ __attribute__((aligned(16))) u16 Kt[HD * TP];
-  __shared__ __attribute__((aligned(16))) u16 Vs[KB * KP];
+  __shared__ __attribute__((aligned(16))) u16 Ks[2][TR * HD];
+  __shared__ __attribute__((aligned(16))) u16 Vs[2][TR * HD];
   const int nqb = (a.S + QB - 1) / QB;
   const int bh = blockIdx.x / nqb;
   const int qb = nqb - 1 - (blockIdx.x % nqb);
@@ -369,35 +432,53 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   const float sl2 = a.scale * LOG2E;
   f32x16 dq[2] = {zero16(), zero16()};
   const int kend = a.causal ? min(a.S, qb * QB + QB) : a.S;
-  for (int k0 = 0; k0 < kend; k0 += KB) {
-    __syncthreads();
-    stage_rows(Ks, a.k + off, a.sqs, k0, KB, a.S);
-    stage_rows_tr(Kt, a.k + off, a.sqs, k0, KB, a.S);
-    stage_rows(Vs, a.v + off, a.sqs, k0, KB, a.S);
-    __syncthreads();
-    if (a.causal && k0 > q0w + QW - 1) continue;
+  TileRegs kr, vr;
+  tile_load(kr, a.k + off, a.sqs, 0, a.S);
+  tile_load(vr, a.v + off, a.sqs, 0, a.S);
+  tile_store(Ks[0], kr);
+  tile_store(Vs[0], vr);
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = 0; k0 < kend; k0 += KB, buf ^= 1) {
+    const bool more = k0 + KB < kend;
+    if (more) {
+      tile_load(kr, a.k + off, a.sqs, k0 + KB, a.S);
+      tile_load(vr, a.v + off, a.sqs, k0 + KB, a.S);
+    }
+    if (!(a.causal && k0 > q0w + QW - 1)) {
+      const u16* Kt = Ks[buf];
+      const u16* Vt = Vs[buf];
+      const bool edge = (a.causal && k0 + KB - 1 > q0w) || k0 + KB > a.S || qi >= a.S;
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      f32x16 s = zero16(), dp = zero16();
+      for (int c = 0; c < 2; ++c) {
+        f32x16 s = zero16(), dp = zero16();
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        s = mfma(row_frag(Ks, KP, 32 * c + r, 16 * t, h), qf[t], s);
-        dp = mfma(row_frag(Vs, KP, 32 * c + r, 16 * t, h), df[t], dp);
-      }
+        for (int t = 0; t < 4; ++t) {
+          s = mfma(rowf(Kt, 32 * c + r, t, h), qf[t], s);
+          dp = mfma(rowf(Vt, 32 * c + r, t, h), df[t], dp);
+        }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int kj = k0 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
-        float p = exp2f(s[i] * sl2 - lse);
-        if (qi >= a.S || kj >= a.S || (a.causal && kj > qi)) p = 0.f;
-        dp[i] = p * (dp[i] - dl);
-      }
+        for (int i = 0; i < 16; ++i) {
+          float p = exp2f(s[i] * sl2 - lse);
+          if (edge) {
+            const int kj = k0 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (qi >= a.S || kj >= a.S || (a.causal && kj > qi)) p = 0.f;
+          }
+          dp[i] = p * (dp[i] - dl);
+        }
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        bf16x8 db = pack8(dp, st);
+        for (int st = 0; st < 2; ++st) {
+          bf16x8 db = pack8(dp, st);
 #pragma unroll
-        for (int d = 0; d < 2; ++d) dq[d] = mfma(tr_frag(Kt, TP, 32 * d + r, 32 * c + 16 * st, h), db, dq[d]);
+          for (int d = 0; d < 2; ++d) dq[d] = mfma(trf(Kt, 32 * c + 16 * st, 32 * d, lane), db, dq[d]);
+        }
       }
     }
+    if (more) {
+      tile_store(Ks[buf ^ 1], kr);
+      tile_store(Vs[buf ^ 1], vr);
+    }
+    __syncthreads();
   }
   if (qi >= a.S) return;
   u16* DQ = a.dq + off + (long)qi * a.sqs;

@@ -66,6 +66,10 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// v_exp_f32 directly (exp2f adds denormal range fix-ups we do not need: arguments are <= 0 or
+// -inf, and flushing tiny probabilities to 0 is harmless)
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -109,22 +113,25 @@ __device__ __forceinline__ bf16x8 trf(const u16* X, int k0, int c0, int lane) {
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
 }
-// a 64-row tile in registers (2 x 16 B per thread) on its way from global memory to LDS
+// a tile of ROWS rows in registers (ROWS/32 x 16 B per thread) on its way from global memory to LDS
+template <int ROWS>
 struct TileRegs {
-  u16x8 v[2];
+  u16x8 v[ROWS / 32];
 };
-__device__ __forceinline__ void tile_load(TileRegs& t, const u16* G, long srow, int r0, int S) {
+template <int ROWS>
+__device__ __forceinline__ void tile_load(TileRegs<ROWS>& t, const u16* G, long srow, int r0, int S) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < ROWS / 32; ++u) {
     const int idx = threadIdx.x + 256 * u, r = idx >> 3, ch = idx & 7;
     u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
     if (r0 + r < S) v = *reinterpret_cast<const u16x8*>(G + (long)(r0 + r) * srow + 8 * ch);
     t.v[u] = v;
   }
 }
-__device__ __forceinline__ void tile_store(u16* L, const TileRegs& t) {
+template <int ROWS>
+__device__ __forceinline__ void tile_store(u16* L, const TileRegs<ROWS>& t) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < ROWS / 32; ++u) {
     const int idx = threadIdx.x + 256 * u, r = idx >> 3, ch = idx & 7;
     *reinterpret_cast<u16x8*>(L + swz(r, ch)) = t.v[u];
   }
@@ -143,14 +150,17 @@ struct AttnArgs {
 
 // ============================================================================================
 // forward
+template <int KBT>  // keys per tile (64 or 128)
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(16))) u16 Ks[2][TR * HD];
-  __shared__ __attribute__((aligned(16))) u16 Vs[2][TR * HD];
+  constexpr int NC = KBT / 32;  // 32-key sub-blocks per tile
+  __shared__ __attribute__((aligned(16))) u16 Ks[2][KBT * HD];
+  __shared__ __attribute__((aligned(16))) u16 Vs[2][KBT * HD];
   const int nqb = (a.S + QB - 1) / QB;
   const int bh = blockIdx.x / nqb;
   const int qb = nqb - 1 - (blockIdx.x % nqb);  // heaviest (causal) blocks first
   const int b = bh / a.H, hh = bh % a.H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31,
+            h = lane >> 5;
   const long qoff = (long)b * a.sqb + (long)hh * a.sqh;
   const u16* Q = a.q + qoff;
   const u16* K = a.k + qoff;
@@ -168,35 +178,35 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   float m = -INFINITY, l = 0.f;
   f32x16 o[2] = {zero16(), zero16()};  // O^T[d][q]: d tile 0..1
   const int kend = a.causal ? min(a.S, qb * QB + QB) : a.S;
-  TileRegs kr, vr;
+  TileRegs<KBT> kr, vr;
   tile_load(kr, K, a.sqs, 0, a.S);
   tile_load(vr, V, a.sqs, 0, a.S);
   tile_store(Ks[0], kr);
   tile_store(Vs[0], vr);
   __syncthreads();
   int buf = 0;
-  for (int k0 = 0; k0 < kend; k0 += KB, buf ^= 1) {
-    const bool more = k0 + KB < kend;
+  for (int k0 = 0; k0 < kend; k0 += KBT, buf ^= 1) {
+    const bool more = k0 + KBT < kend;
     if (more) {  // next tile's loads fly during this tile's MFMAs
-      tile_load(kr, K, a.sqs, k0 + KB, a.S);
-      tile_load(vr, V, a.sqs, k0 + KB, a.S);
+      tile_load(kr, K, a.sqs, k0 + KBT, a.S);
+      tile_load(vr, V, a.sqs, k0 + KBT, a.S);
     }
     if (!(a.causal && k0 > q0w + QW - 1)) {  // else: all this wave's queries precede k0
       const u16* Kt = Ks[buf];
       const u16* Vt = Vs[buf];
       // S^T for two 32-key sub-blocks
-      f32x16 s[2];
+      f32x16 s[NC];
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < NC; ++c) {
         s[c] = zero16();
 #pragma unroll
         for (int t = 0; t < 4; ++t) s[c] = mfma(rowf(Kt, 32 * c + r, t, h), qf[t], s[c]);
       }
       // scale (+ mask on the diagonal / ragged tiles only), running max
-      const bool edge = (a.causal && k0 + KB - 1 > q0w) || k0 + KB > a.S;
+      const bool edge = (a.causal && k0 + KBT - 1 > q0w) || k0 + KBT > a.S;
       float mx = m;
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           float v = s[c][i] * sl2;
@@ -208,13 +218,14 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
           mx = fmaxf(mx, v);
         }
       mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float alpha = (m == -INFINITY) ? 0.f : exp2f(m - mx);
+      const float alpha = (m == -INFINITY) ? 0.f : ex2(m - mx);
+      const float msub = (mx == -INFINITY) ? 0.f : mx;  // all-masked so far: exp2(-inf) = 0
       float rs = 0.f;
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float p = (mx == -INFINITY) ? 0.f : exp2f(s[c][i] - mx);
+          const float p = ex2(s[c][i] - msub);
           s[c][i] = p;
           rs += p;
         }
@@ -227,7 +238,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
         for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
       // O^T[d][q] += sum_k V^T[d][k] P^T[k][q]   (V^T by transposed reads of the V image)
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
           bf16x8 pb = pack8(s[c], st);
@@ -294,7 +305,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
   const int bh = blockIdx.x / nkb;
   const int kb = blockIdx.x % nkb;
   const int b = bh / a.H, hh = bh % a.H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31,
+            h = lane >> 5;
   const long off = (long)b * a.sqb + (long)hh * a.sqh;
   const long ooff = (long)b * a.sob + (long)hh * a.soh;
   const int k0w = kb * QB + w * QW;
@@ -314,7 +326,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
   const int qstart = a.causal ? (kb * QB) / BQ * BQ : 0;
   const float* LSE = a.lse + (long)bh * a.S;
   const float* DEL = a.delta + (long)bh * a.S;
-  TileRegs qr, dr;
+  TileRegs<TR> qr, dr;
   float lr = 0.f, dlr = 0.f;
   auto load = [&](int q0) {
     tile_load(qr, a.q + off, a.sqs, q0, a.S);
@@ -345,7 +357,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
     if (!(a.causal && q0 + BQ - 1 < k0w)) {  // else: all these queries precede this wave's keys
       const u16* Qt = Qs[buf];
       const u16* Dt = Ds[buf];
-      const bool edge = (a.causal && q0 < k0w + QW - 1) || q0 + BQ > a.S || kj >= a.S;
+      // only the causal diagonal needs a mask: rows past S are zero-filled Q/dO (their P and dS
+      // terms multiply zero rows), and lanes with kj >= S are never stored
+      const bool edge = a.causal && q0 < k0w + QW - 1;
 #pragma unroll
       for (int c = 0; c < 2; ++c) {  // 32-query sub-blocks
         f32x16 s = zero16(), dp = zero16();
@@ -358,11 +372,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int ql = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
-          float p = exp2f(s[i] * sl2 - Ls[buf][ql]);
-          if (edge) {
-            const int qi = q0 + ql;
-            if (qi >= a.S || kj >= a.S || (a.causal && kj > qi)) p = 0.f;
-          }
+          float p = ex2(s[i] * sl2 - Ls[buf][ql]);
+          if (edge && kj > q0 + ql) p = 0.f;
           s[i] = p;
           dp[i] = p * (dp[i] - Dl[buf][ql]);  // dS (scale applied to dK at the end)
         }
@@ -412,7 +423,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   const int bh = blockIdx.x / nqb;
   const int qb = nqb - 1 - (blockIdx.x % nqb);
   const int b = bh / a.H, hh = bh % a.H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31,
+            h = lane >> 5;
   const long off = (long)b * a.sqb + (long)hh * a.sqh;
   const long ooff = (long)b * a.sob + (long)hh * a.soh;
   const int q0w = qb * QB + w * QW;
@@ -432,7 +444,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   const float sl2 = a.scale * LOG2E;
   f32x16 dq[2] = {zero16(), zero16()};
   const int kend = a.causal ? min(a.S, qb * QB + QB) : a.S;
-  TileRegs kr, vr;
+  TileRegs<TR> kr, vr;
   tile_load(kr, a.k + off, a.sqs, 0, a.S);
   tile_load(vr, a.v + off, a.sqs, 0, a.S);
   tile_store(Ks[0], kr);
@@ -448,7 +460,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
     if (!(a.causal && k0 > q0w + QW - 1)) {
       const u16* Kt = Ks[buf];
       const u16* Vt = Vs[buf];
-      const bool edge = (a.causal && k0 + KB - 1 > q0w) || k0 + KB > a.S || qi >= a.S;
+      // causal diagonal only: keys past S have zero K/V rows (their dS^T terms multiply zero
+      // K^T columns) and lanes with qi >= S are never stored
+      const bool edge = a.causal && k0 + KB - 1 > q0w;
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         f32x16 s = zero16(), dp = zero16();
@@ -459,11 +473,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float p = exp2f(s[i] * sl2 - lse);
-          if (edge) {
-            const int kj = k0 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (qi >= a.S || kj >= a.S || (a.causal && kj > qi)) p = 0.f;
-          }
+          float p = ex2(s[i] * sl2 - lse);
+          if (edge && k0 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p = 0.f;
           dp[i] = p * (dp[i] - dl);
         }
 #pragma unroll
@@ -522,10 +533,16 @@ AttnArgs make_args(const AttnShape& s) {
 
 }  // namespace
 
+static int g_fwd_kb = 0;  // 0: default; 64 / 128 (A/B experiments)
+void attention_set_fwd_kb(int kb) { g_fwd_kb = kb; }
+
 void attention_fwd_bf16(const AttnShape& s, hipStream_t stream) {
   AttnArgs a = make_args(s);
   const int nqb = (s.S + QB - 1) / QB;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
+  if (g_fwd_kb == 128)
+    hipLaunchKernelGGL(attn_fwd_kernel<128>, dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<64>, dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
 }
 
 void attention_bwd_bf16(const AttnShape& s, hipStream_t stream) {

@@ -114,6 +114,7 @@ struct AttnShape {
   int causal = 1;
 };
 void attention_fwd_bf16(const AttnShape& s, hipStream_t stream);
+void attention_set_fwd_kb(int kb);  // tuning: keys per forward tile (0 = default, 64, 128)
 void attention_bwd_bf16(const AttnShape& s, hipStream_t stream);
 
 // ---- reference CNN (MNIST), fp32, one launch per stage pass (ref_cnn.hip) ------------------

@@ -568,6 +568,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_grad_bf16_", &bias_grad_bf16_, "gb += column sums of gy (bf16, deterministic)");
   m.def("attention_fwd", &attention_fwd, "causal flash attention forward (bf16, d=64)");
   m.def("attention_bwd", &attention_bwd, "causal flash attention backward (bf16, d=64)");
+  m.def("attention_set_fwd_kb", &sdml::attention_set_fwd_kb, "attention forward keys per tile (tuning)");
   m.def("gemm_f32_set_variant", &sdml::gemm_f32_set_variant, "fp32 GEMM variant (tuning: 0 auto, 16, 32)");
   m.def("ref_cnn_stage0_fwd", &ref_cnn_stage0_fwd, "reference CNN stage 0 forward (one launch)");
   m.def("ref_cnn_stage0_bwd", &ref_cnn_stage0_bwd, "reference CNN stage 0 backward (one launch)");

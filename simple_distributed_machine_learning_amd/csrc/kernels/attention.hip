@@ -202,22 +202,22 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) s[c] = mfma(rowf(Kt, 32 * c + r, t, h), qf[t], s[c]);
       }
-      // scale (+ mask on the diagonal / ragged tiles only), running max
+      // mask (diagonal / ragged tiles only) and running max on the RAW scores; the softmax scale
+      // is folded into one FMA per score: p = exp2(s * c - max * c), c = scale * log2(e) > 0
       const bool edge = (a.causal && k0 + KBT - 1 > q0w) || k0 + KBT > a.S;
-      float mx = m;
+      float mr = -INFINITY;
 #pragma unroll
       for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float v = s[c][i] * sl2;
           if (edge) {
             const int kj = k0 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (kj >= a.S || (a.causal && kj > qi)) v = -INFINITY;
+            if (kj >= a.S || (a.causal && kj > qi)) s[c][i] = -INFINITY;
           }
-          s[c][i] = v;
-          mx = fmaxf(mx, v);
+          mr = fmaxf(mr, s[c][i]);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      mr = fmaxf(mr, __shfl_xor(mr, 32));
+      const float mx = fmaxf(m, mr * sl2);  // running max, log2 domain
       const float alpha = (m == -INFINITY) ? 0.f : ex2(m - mx);
       const float msub = (mx == -INFINITY) ? 0.f : mx;  // all-masked so far: exp2(-inf) = 0
       float rs = 0.f;
@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
       for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = ex2(s[c][i] - msub);
+          const float p = ex2(__builtin_fmaf(s[c][i], sl2, -msub));
           s[c][i] = p;
           rs += p;
         }

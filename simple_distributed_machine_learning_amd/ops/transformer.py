@@ -72,7 +72,9 @@ def cross_entropy_sum(logits, target, scale: float, need_grad: bool, ignore_inde
         g = g.to(logits.dtype)
     valid = target != ignore_index
     correct = ((z.detach().argmax(1) == target) & valid).sum()
-    return loss.detach(), correct, int(valid.sum()), g
+    # no host sync unless an ignore_index can actually occur (keeps the step graph-capturable)
+    count = target.numel() if ignore_index < 0 else int(valid.sum())
+    return loss.detach(), correct, count, g
 
 
 class _FlashAttnFn(torch.autograd.Function):

@@ -101,13 +101,17 @@ class GraphedStep:
         self.pool = None
         self.disabled = False
         self.replays = 0
+        # eager warm-up steps and captures share one side stream: autograd's AccumulateGrad
+        # nodes remember the stream they were created on, and a capture on a different stream
+        # would make them synchronise with it (not permitted while capturing)
+        self.stream = torch.cuda.Stream(device=engine.device)
 
     def _record(self, win, start, batch_size, global_batch, pool):
         eng = self.engine
         gs, steps, zero = eng.global_step, eng.optimizer.steps, eng.flat.grads_zero
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(eng.device)
-        with torch.cuda.graph(g, pool=pool):
+        with torch.cuda.graph(g, pool=pool, stream=self.stream):
             res = eng.run(win, start, batch_size, train=True, global_batch=global_batch)
         # capture recorded but did not execute the step: restore the host-side state
         eng.global_step, eng.optimizer.steps, eng.flat.grads_zero = gs, steps, zero
@@ -125,10 +129,18 @@ class GraphedStep:
         self.engine.flat.grads_zero = True
         return g, win, res, start
 
+    def _eager(self, dataset, start, batch_size, global_batch):
+        cur = torch.cuda.current_stream(self.engine.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            res = self.engine.run(dataset, start, batch_size, train=True, global_batch=global_batch)
+        cur.wait_stream(self.stream)
+        return res
+
     def __call__(self, dataset, start: int, batch_size: int, global_batch: Optional[int] = None) -> StepResult:
         eng = self.engine
         if self.disabled or eng.optimizer.steps == 0:
-            return eng.run(dataset, start, batch_size, train=True, global_batch=global_batch)
+            return self._eager(dataset, start, batch_size, global_batch)
         key = (batch_size, global_batch)
         t0 = time.perf_counter()
         if key not in self.graphs:
@@ -138,7 +150,7 @@ class GraphedStep:
                 warnings.warn(f"hipGraph capture failed ({type(e).__name__}: {e}); running eagerly")
                 self.disabled = True
                 torch.cuda.synchronize(eng.device)
-                return eng.run(dataset, start, batch_size, train=True, global_batch=global_batch)
+                return self._eager(dataset, start, batch_size, global_batch)
         g, win, res, cap_start = self.graphs[key]
         win.load(dataset, start - cap_start)
         g.replay()

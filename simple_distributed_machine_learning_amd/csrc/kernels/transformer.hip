@@ -122,6 +122,110 @@ __global__ void __launch_bounds__(CE_T) ce_fwd_bwd_kernel(const u16* __restrict_
   }
 }
 
+// Register-resident variant (V <= 512 threads * 8 * CE_NVMAX): the row is read from HBM ONCE
+// into registers (16-B loads over the row's 16-B aligned body; the unaligned head/tail elements of
+// an odd vocabulary like GPT-2's 50257 go one per thread), then max/argmax, sum-exp and dlogits
+// are all computed from registers: one read and one write of the logits per row (the online
+// kernel above reads them twice and, for odd V, element by element).
+constexpr int CER_T = 512;  // 2 waves/SIMD per workgroup: up to 256 VGPRs for the resident row
+constexpr int CE_NVMAX = 16;
+constexpr u16 BF16_NEG_INF = 0xFF80;
+
+template <int NV>
+__global__ void __launch_bounds__(CER_T) ce_reg_kernel(const u16* __restrict__ logits, const int64_t* __restrict__ tgt,
+                                                       int rows, int V, int ld, float scale, int ignore_index,
+                                                       float* __restrict__ row_loss, float* __restrict__ row_ok,
+                                                       u16* __restrict__ dlogits) {
+  __shared__ float red_m[CER_T / 64], red_s[CER_T / 64];
+  __shared__ int red_i[CER_T / 64];
+  const int row = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const u16* z = logits + (size_t)row * ld;
+  int head = (int)(((16 - (reinterpret_cast<uintptr_t>(z) & 15)) & 15) >> 1);
+  if (head > V) head = V;
+  const int nvec = (V - head) >> 3;
+  const int tail0 = head + 8 * nvec, ntail = V - tail0;
+  u16x8 v[NV];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int vi = t + u * CER_T;
+    if (vi < nvec) {
+      v[u] = *reinterpret_cast<const u16x8*>(z + head + 8 * vi);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[u][e] = BF16_NEG_INF;
+    }
+  }
+  // unaligned head (t < head) and tail (t < ntail) elements, one each per thread
+  const float xh = t < head ? bf2f(z[t]) : -INFINITY;
+  const float xt = t < ntail ? bf2f(z[tail0 + t]) : -INFINITY;
+  // block max (values stay packed bf16 in registers; unpacking is one shift)
+  float mx = fmaxf(xh, xt);
+#pragma unroll
+  for (int u = 0; u < NV; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mx = fmaxf(mx, bf2f(v[u][e]));
+  mx = wave_max(mx);
+  if (lane == 0) red_m[w] = mx;
+  __syncthreads();
+  float M = red_m[0];
+#pragma unroll
+  for (int i = 1; i < CER_T / 64; ++i) M = fmaxf(M, red_m[i]);
+  // first index holding the max (torch.argmax semantics)
+  int am = 0x7fffffff;
+  if (xh == M) am = t;
+#pragma unroll
+  for (int u = 0; u < NV; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (bf2f(v[u][e]) == M) am = min(am, head + 8 * (t + u * CER_T) + e);
+  if (xt == M) am = min(am, tail0 + t);
+  for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o));
+  if (lane == 0) red_i[w] = am;
+  __syncthreads();
+  int AM = red_i[0];
+#pragma unroll
+  for (int i = 1; i < CER_T / 64; ++i) AM = min(AM, red_i[i]);
+  // sum of exp from registers
+  float se = 0.f;
+#pragma unroll
+  for (int u = 0; u < NV; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) se += __expf(bf2f(v[u][e]) - M);
+  se += __expf(xh - M) + __expf(xt - M);
+  se = wave_sum(se);
+  if (lane == 0) red_s[w] = se;
+  __syncthreads();
+  float S = 0.f;
+#pragma unroll
+  for (int i = 0; i < CER_T / 64; ++i) S += red_s[i];
+  const float lse = M + __logf(S);
+  const int y = (int)tgt[row];
+  const bool valid = y != ignore_index && y >= 0 && y < V;
+  if (t == 0) {
+    row_loss[row] = valid ? lse - bf2f(z[y]) : 0.f;
+    row_ok[row] = (valid && AM == y) ? 1.f : 0.f;
+  }
+  if (!dlogits) return;
+  u16* g = dlogits + (size_t)row * ld;  // same alignment as the logits row (same ld)
+  const float sc = valid ? scale : 0.f;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int vi = t + u * CER_T;
+    if (vi < nvec) {
+      u16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int idx = head + 8 * vi + e;
+        o[e] = f2bf(sc * (__expf(bf2f(v[u][e]) - lse) - (idx == y ? 1.f : 0.f)));
+      }
+      *reinterpret_cast<u16x8*>(g + head + 8 * vi) = o;
+    }
+  }
+  if (t < head) g[t] = f2bf(sc * (__expf(xh - lse) - (t == y ? 1.f : 0.f)));
+  if (t < ntail) g[tail0 + t] = f2bf(sc * (__expf(xt - lse) - (tail0 + t == y ? 1.f : 0.f)));
+}
+
 // ---------------------------------------------------------------------------------------------
 // LayerNorm (row width D <= 4096, D % 8 == 0): one wave per row, fp32 statistics.
 constexpr int LN_T = 256;
@@ -369,6 +473,23 @@ void bias_grad_bf16(const void* gy, int M, int N, int ld, void* gb, float* works
 void cross_entropy_bf16(const void* logits, const int64_t* target, int rows, int V, int ld, float scale,
                         int ignore_index, float* row_loss, float* row_ok, void* dlogits, hipStream_t stream) {
   if (rows <= 0) return;
+  // register-resident kernel when the row fits (and dlogits shares the logits' alignment)
+  const int nvec = (V + 7) / 8;
+  const int nv = (nvec + CER_T - 1) / CER_T;
+  const bool same_align = !dlogits || ((reinterpret_cast<uintptr_t>(logits) ^ reinterpret_cast<uintptr_t>(dlogits)) & 15) == 0;
+  if (nv <= CE_NVMAX && same_align) {
+    const u16* L = reinterpret_cast<const u16*>(logits);
+    u16* G = reinterpret_cast<u16*>(dlogits);
+#define CER(NVV)                                                                                                   \
+  hipLaunchKernelGGL(ce_reg_kernel<NVV>, dim3(rows), dim3(CER_T), 0, stream, L, target, rows, V, ld, scale, \
+                     ignore_index, row_loss, row_ok, G)
+    if (nv <= 4) CER(4);
+    else if (nv <= 8) CER(8);
+    else if (nv <= 13) CER(13);  // GPT-2: V = 50257 -> 13 vectors of 8 per thread
+    else CER(16);
+#undef CER
+    return;
+  }
   hipLaunchKernelGGL(ce_fwd_bwd_kernel, dim3(rows), dim3(CE_T), 0, stream, reinterpret_cast<const u16*>(logits),
                      target, rows, V, ld, scale, ignore_index, row_loss, row_ok, reinterpret_cast<u16*>(dlogits));
 }

@@ -156,7 +156,7 @@ def test_sgd_mixed_bf16(first):
     assert float(g.float().abs().sum()) == 0.0
 
 
-@pytest.mark.parametrize("rows,V", [(7, 97), (64, 50257), (33, 1000), (5, 4096)])
+@pytest.mark.parametrize("rows,V", [(7, 97), (64, 50257), (33, 1000), (5, 4096), (3, 131073), (2, 7), (9, 50257 * 2)])
 def test_cross_entropy_bf16(rows, V):
     from simple_distributed_machine_learning_amd.ops.transformer import cross_entropy_sum
 

@@ -50,6 +50,11 @@ def main():
     mesh = init_mesh(pp=pp, schedule_kind=kind, rank=rank, world_size=world)
     spec = get_model_spec(a.config, stages, seq_len=S)
     eng = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.01, momentum=0.5, seed=1)
+    tuned = False
+    if spec.input_kind == "tokens" and mesh.device.type == "cuda":
+        from simple_distributed_machine_learning_amd.utils.tuned_gemm import use_tuned_gemms
+
+        tuned = use_tuned_gemms()
     dev = mesh.device
     nb = 2
     if spec.input_kind == "tokens":
@@ -91,7 +96,7 @@ def main():
     l, c, n = eng.reduce_metrics(res)
     if rank == 0:
         print(json.dumps({"config": a.config, "schedule": kind, "stages": stages, "ranks": world,
-                          "microbatches": M, "batch": GB, "seq_len": S, "dtype": str(spec.param_dtype), "graph": bool(a.graph),
+                          "microbatches": M, "batch": GB, "seq_len": S, "dtype": str(spec.param_dtype), "graph": bool(a.graph), "tuned_gemms": tuned,
                           "value": round(GB * per_sample * a.steps / el, 1), "unit": unit,
                           "ms_per_step": round(el / a.steps * 1e3, 3), "loss": round(l / max(1, n), 4),
                           "bubble_model": round(eng.schedule(M, False).bubble_fraction(), 3)}))

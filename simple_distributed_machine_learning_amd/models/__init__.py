@@ -21,7 +21,7 @@ def get_model_spec(name: str, num_stages: int = None, **kw) -> ModelSpec:
     if name == "ref_cnn":
         return ref_cnn_spec(n, eval_dropout=kw.get("eval_dropout", True), dropout=kw.get("dropout", 0.5))
     if name == "resnet18":
-        return resnet18_spec(n)
+        return resnet18_spec(n, dtype=kw.get("dtype", None) or __import__("torch").float32)
     if name == "gpt2":
         return gpt2_spec(n, seq_len=kw.get("seq_len"))
     if name == "gpt2_tiny":  # test-sized transformer with the same code path

@@ -7,10 +7,12 @@ The 8 BasicBlocks are the cut units: stage k gets ``8 / num_stages`` consecutive
 the stem rides with the first stage and pool+fc with the last.
 
 BatchNorm runs per micro-batch (GPipe semantics). Convolutions use MIOpen through
-PyTorch in this round.
+PyTorch in this round. ``dtype=bf16`` runs
+the stages in bf16 (fp32 master weights in the optimizer); the default is fp32.
 """
 from __future__ import annotations
 
+import os
 from typing import List
 
 import torch
@@ -20,6 +22,7 @@ import torch.nn.functional as F
 from .base import ModelSpec, PipelineStage
 
 WIDTHS = (64, 128, 256, 512)
+CHANNELS_LAST = os.environ.get("SDML_RESNET_NHWC", "0") == "1"  # measured slower with MIOpen fp32
 
 
 class BasicBlock(nn.Module):
@@ -72,6 +75,13 @@ class ResNetStage(PipelineStage):
             self.fc = nn.Linear(512, num_classes)
 
     def forward(self, x):
+        # optional NHWC inside the stage (SDML_RESNET_NHWC=1). Measured on MI355X (8 stages on one
+        # GPU, batch 512, 8 micro-batches): MIOpen picks slower solutions for channels-last fp32
+        # (9.6K vs 14.6K samples/s), so NCHW is the default. The boundary tensor is always NCHW.
+        if self.stage_id == 0:
+            x = x.to(self.stem_conv.weight.dtype)
+        if x.is_cuda and CHANNELS_LAST:
+            x = x.contiguous(memory_format=torch.channels_last)
         if self.stage_id == 0:
             x = F.relu(self.stem_bn(self.stem_conv(x)))
         for n in self.block_names:
@@ -79,7 +89,8 @@ class ResNetStage(PipelineStage):
         if self.stage_id == self.num_stages - 1:
             x = F.adaptive_avg_pool2d(x, 1).flatten(1)
             x = self.fc(x)
-        return x
+            return x
+        return x.contiguous()
 
 
 def _out_shape(stage: int, num_stages: int, hw: int = 28):
@@ -94,7 +105,7 @@ def _out_shape(stage: int, num_stages: int, hw: int = 28):
     return c, size
 
 
-def resnet18_spec(num_stages: int = 8) -> ModelSpec:
+def resnet18_spec(num_stages: int = 8, dtype=torch.float32) -> ModelSpec:
     def build(s):
         return ResNetStage(s, num_stages)
 
@@ -103,4 +114,4 @@ def resnet18_spec(num_stages: int = 8) -> ModelSpec:
         return (mb, c, hw, hw)
 
     return ModelSpec(name="resnet18", num_stages=num_stages, build_stage=build, boundary_shape=shape,
-                     boundary_dtype=torch.float32, input_kind="image")
+                     boundary_dtype=dtype, input_kind="image", param_dtype=dtype)

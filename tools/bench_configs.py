@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--seq_len", type=int, default=None)
     ap.add_argument("--graph", action="store_true", help="replay the step from a captured hipGraph")
+    ap.add_argument("--dtype", default=None, choices=[None, "fp32", "bf16"], help="resnet18: compute dtype")
     a = ap.parse_args()
     kind, M, B, S = DEFAULTS[a.config]
     M = a.microbatches or M
@@ -48,7 +49,8 @@ def main():
     stages = DEFAULT_STAGES[a.config]
     pp = min(world, stages)
     mesh = init_mesh(pp=pp, schedule_kind=kind, rank=rank, world_size=world)
-    spec = get_model_spec(a.config, stages, seq_len=S)
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16}.get(a.dtype)
+    spec = get_model_spec(a.config, stages, seq_len=S, **({"dtype": dt} if dt is not None else {}))
     eng = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.01, momentum=0.5, seed=1)
     tuned = False
     if spec.input_kind == "tokens" and mesh.device.type == "cuda":

@@ -80,6 +80,10 @@ def add_engine_args(parser: argparse.ArgumentParser):
     g.add_argument("--debug_sync", action="store_true", help="device sync after every pipeline op")
     g.add_argument("--graph", action="store_true",
                    help="capture the training step in a hipGraph and replay it (ROCm, one process)")
+    g.add_argument("--timing", action="store_true",
+                   help="per-stage/phase device timers (fwd, bwd, recv_wait, grad_sync, optim) in the metrics")
+    g.add_argument("--dtype", default="auto", choices=["auto", "fp32", "bf16"],
+                   help="parameter/compute dtype (auto: the model's default; gpt2 is bf16, the rest fp32)")
 
 
 def build_parser() -> argparse.ArgumentParser:

@@ -33,6 +33,7 @@ import torch.distributed as dist
 from ..models.base import ModelSpec, PipelineStage, build_stages
 from ..ops.optim import FusedSGD
 from ..utils.flat import FlatParams
+from ..utils.timing import PhaseTimer
 from .mesh import Mesh
 from .p2p import Transport, message_tag
 from .schedule import OP_BWD, OP_FWD, OP_RECV, OP_SEND, PL_ACT, PL_GRAD, Schedule, build_schedule
@@ -102,7 +103,7 @@ class GradSync:
 class PipelineEngine:
     def __init__(self, spec: ModelSpec, mesh: Mesh, schedule_kind: str = "1f1b", num_microbatches: int = 1,
                  lr: float = 0.1, momentum: float = 0.5, weight_decay: float = 0.0, seed: int = 0,
-                 dtype: Optional[torch.dtype] = None, debug_sync: bool = False):
+                 dtype: Optional[torch.dtype] = None, debug_sync: bool = False, timing: bool = False):
         self.spec, self.mesh = spec, mesh
         self.kind = schedule_kind
         self.M = max(1, int(num_microbatches))
@@ -112,6 +113,8 @@ class PipelineEngine:
         self.device = mesh.device
         self.dtype = dtype or spec.param_dtype
         self.debug_sync = debug_sync or os.environ.get("SDML_DEBUG_SYNC") == "1"
+        self.timing = timing
+        self.last_timing: Dict[str, float] = {}  # per-stage/phase ms of the last step (timing=True)
         self._sched_cache: Dict[Tuple[int, bool], Schedule] = {}
         if self.kind == "rotate" and self.M % mesh.pp:
             raise ValueError(f"rotate: micro-batches ({self.M}) must be a multiple of the ranks ({mesh.pp})")
@@ -261,11 +264,14 @@ class PipelineEngine:
         stats = torch.zeros(2, device=dev, dtype=torch.float32)  # [loss_sum, correct]
         count = 0
 
+        tm = PhaseTimer(dev, self.timing)
+
         def take(key, peer_rank_is_local: bool):
             if peer_rank_is_local:
                 return local.pop(key)
             w, buf = inbox.pop(key)
-            w.wait()
+            with tm.span("recv_wait", key[2]):
+                w.wait()
             return buf
 
         for i, ins in enumerate(prog):
@@ -298,13 +304,15 @@ class PipelineEngine:
                     tgt = dataset.targets(off, mbsz)
                     if tgt.device != dev:
                         tgt = tgt.to(dev, non_blocking=True)
-                    l, c, n = mod.head_fwd(x, tgt, ctx, train, scale, stats=stats)
+                    with tm.span("fwd", ins.stage):
+                        l, c, n = mod.head_fwd(x, tgt, ctx, train, scale, stats=stats)
                     if l is not None:  # stage did not accumulate in-kernel
                         stats[0] += l.float()
                         stats[1] += c.float()
                     count += n
                 else:
-                    y = mod.fwd(x, ctx, train)
+                    with tm.span("fwd", ins.stage):
+                        y = mod.fwd(x, ctx, train)
                     key = (PL_ACT, ins.pipe, ins.stage, ins.mb)
                     if sched.task_rank(ins.mb, ins.stage + 1) == self.mesh.pp_rank:
                         local[key] = y
@@ -316,11 +324,13 @@ class PipelineEngine:
                 mod = self.stages[ins.stage]
                 ctx = ctxs.pop((ins.pipe, ins.stage, ins.mb))
                 if mod.is_last:
-                    gx = mod.head_bwd(ctx)
+                    with tm.span("bwd", ins.stage):
+                        gx = mod.head_bwd(ctx)
                 else:
                     nxt_local = sched.task_rank(ins.mb, ins.stage + 1) == self.mesh.pp_rank
                     gy = take((PL_GRAD, ins.pipe, ins.stage + 1, ins.mb), nxt_local)
-                    gx = mod.bwd(gy, ctx)
+                    with tm.span("bwd", ins.stage):
+                        gx = mod.bwd(gy, ctx)
                 if ins.stage > 0:
                     key = (PL_GRAD, ins.pipe, ins.stage, ins.mb)
                     if sched.task_rank(ins.mb, ins.stage - 1) == self.mesh.pp_rank:
@@ -335,13 +345,17 @@ class PipelineEngine:
             raise RuntimeError(f"pipeline step left undelivered tensors: out={list(outbox)} "
                                f"in={list(inbox)} local={list(local)}")
         if self.transport is not None:
-            self.transport.drain_sends()
+            with tm.span("send_drain"):
+                self.transport.drain_sends()
         if train:
-            self.grad_sync.finish()
+            with tm.span("grad_sync"):
+                self.grad_sync.finish()
             if step_optimizer:
-                self.optimizer.step()
+                with tm.span("optim"):
+                    self.optimizer.step()
                 self.global_step += 1
             self._advance_rng()
+        self.last_timing = tm.result()
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
 
     # ---------------------------------------------------------------------------------------
@@ -378,13 +392,15 @@ class PipelineEngine:
             pk = parts[w]
             return start + o * batch_size + woff[w] + sum(pk[:k]), pk[k]
 
+        tm = PhaseTimer(dev, self.timing)
         ctx0 = [dict() for _ in waves]
         recv, fwork = [None] * W, [None] * W
         for w, bw in enumerate(waves):  # stage 0 forward + scatter of the boundary activation
             x = dataset.inputs(start + me * batch_size + woff[w], bw)
             if x.device != dev:
                 x = x.to(dev, non_blocking=True)
-            h = s0.fwd(x, ctx0[w], train)
+            with tm.span("fwd", 0):
+                h = s0.fwd(x, ctx0[w], train)
             if R == 1:
                 recv[w] = h
                 continue
@@ -396,7 +412,8 @@ class PipelineEngine:
         back, bwork = [None] * W, [None] * W
         for w in range(W):  # stage 1 (+ loss + its backward) on the received parts
             if fwork[w] is not None:
-                fwork[w].wait()
+                with tm.span("recv_wait", 0):
+                    fwork[w].wait()
             tg = [dataset.targets(*owner_part(o, w, me)) for o in range(R)]
             tgt = tg[0] if R == 1 else torch.cat(tg)
             if tgt.device != dev:
@@ -404,14 +421,16 @@ class PipelineEngine:
             if tgt.numel() == 0:
                 continue
             c1 = {}
-            l, c, n = s1.head_fwd(recv[w], tgt, c1, train, scale, stats=stats)
+            with tm.span("fwd", 1):
+                l, c, n = s1.head_fwd(recv[w], tgt, c1, train, scale, stats=stats)
             if l is not None:
                 stats[0] += l.float()
                 stats[1] += c.float()
             count += n
             if not train:
                 continue
-            g = s1.head_bwd(c1)
+            with tm.span("bwd", 1):
+                g = s1.head_bwd(c1)
             if R == 1:
                 back[w] = g
                 continue
@@ -424,16 +443,21 @@ class PipelineEngine:
             self.grad_sync.stage_done(1)
             for w in range(W):  # stage 0 backward
                 if bwork[w] is not None:
-                    bwork[w].wait()
+                    with tm.span("recv_wait", 1):
+                        bwork[w].wait()
                 if back[w] is None:  # this wave had no samples for me as stage 1... still owner grads
                     continue
-                s0.bwd(back[w], ctx0[w])
+                with tm.span("bwd", 0):
+                    s0.bwd(back[w], ctx0[w])
             self.grad_sync.stage_done(0)
-            self.grad_sync.finish()
+            with tm.span("grad_sync"):
+                self.grad_sync.finish()
             if step_optimizer:
-                self.optimizer.step()
+                with tm.span("optim"):
+                    self.optimizer.step()
                 self.global_step += 1
             self._advance_rng()
+        self.last_timing = tm.result()
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
 
     def reduce_metrics(self, res: StepResult, group=None) -> Tuple[float, int, int]:

@@ -70,10 +70,14 @@ def run(args) -> dict:
     hb = None
     if args.heartbeat > 0 and mesh.world_size > 1:
         hb = Heartbeat(mesh.rank, range(mesh.world_size), timeout_s=args.heartbeat).start()
-    spec = get_model_spec(args.model, stages, eval_dropout=bool(args.eval_dropout), seq_len=args.seq_len or 64)
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16}.get(getattr(args, "dtype", "auto"))
+    kw = {"dtype": dt} if dt is not None and args.model in ("resnet18", "gpt2_tiny") else {}
+    spec = get_model_spec(args.model, stages, eval_dropout=bool(args.eval_dropout), seq_len=args.seq_len or 64, **kw)
+    if dt is not None and spec.param_dtype != dt:
+        raise SystemExit(f"--dtype {args.dtype} is not supported for --model {args.model}")
     engine = PipelineEngine(spec, mesh, schedule_kind=args.schedule, num_microbatches=args.microbatches,
                             lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay, seed=args.seed,
-                            debug_sync=args.debug_sync)
+                            debug_sync=args.debug_sync, timing=getattr(args, "timing", False))
     torch.manual_seed(args.seed * 7 + mesh.rank)  # dropout streams (reference: unseeded)
     if spec.input_kind == "tokens" and device.type == "cuda":
         from .utils.tuned_gemm import use_tuned_gemms
@@ -138,7 +142,8 @@ def run(args) -> dict:
                 if master:
                     print(train_line(epoch, batch_idx, size, len(train_ds), nb, loss),
                           flush=True)
-                    metrics.log(event="train", epoch=epoch, batch=batch_idx, loss=loss, samples_per_s=sps)
+                    extra = {"timing_ms": engine.last_timing} if engine.timing else {}
+                    metrics.log(event="train", epoch=epoch, batch=batch_idx, loss=loss, samples_per_s=sps, **extra)
                 history["train"].append((epoch, batch_idx, loss))
         return last_idx
 

@@ -50,3 +50,11 @@ def test_env_export(monkeypatch):
 
 def test_rccl_alias():
     assert cli.parse_args(["--rank", "0", "--backend", "rccl"]).backend == "nccl"
+
+
+def test_dtype_and_timing_flags():
+    from simple_distributed_machine_learning_amd import cli
+
+    a = cli.parse_args(["--rank=0", "--dtype=bf16", "--timing", "--model=resnet18"])
+    assert a.dtype == "bf16" and a.timing and a.model == "resnet18"
+    assert cli.parse_args(["--rank=0"]).dtype == "auto"

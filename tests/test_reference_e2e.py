@@ -54,3 +54,16 @@ def test_reference_command_line_two_ranks(tmp_path):
     outs = _launch(["--epochs=3", "--train_size=1200", "--test_size=200", f"--ckpt_dir={tmp_path}", "--resume"])
     assert "resumed from" in outs[0]
     assert sum(1 for l in outs[0].splitlines() if TRAIN_RE.match(l)) == 2  # only epoch 3
+
+
+def test_timing_metrics_two_ranks(tmp_path):
+    # --timing: per-stage/phase times of the logged steps land in the JSONL metrics
+    import json
+
+    _launch(["--epochs=1", "--train_size=240", "--test_size=60", "--model=mlp", "--timing", "--no_test",
+             f"--metrics={tmp_path}/m.jsonl"])
+    recs = [json.loads(l) for l in open(f"{tmp_path}/m.jsonl")]
+    t = [r["timing_ms"] for r in recs if r.get("event") == "train"]
+    assert t and all(v >= 0 for v in t[0].values())
+    # rank 0 holds stage 0 of the 2-stage pipeline: forward, backward, the wait for stage 1's gradient
+    assert {"fwd/stage0", "bwd/stage0", "recv_wait/stage1", "optim"} <= set(t[0])

@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 
 #include "kernels.h"
 
@@ -307,6 +309,16 @@ bool gemm_f32_supported(const GemmArgs& g) {
 static int g_variant = 0;  // 0: auto, 32: BK=32, 16: BK=16 (A/B experiments)
 void gemm_f32_set_variant(int v) { g_variant = v; }
 
+static int g_mode = -1;  // -1: not yet read from the environment
+void gemm_f32_set_mode(int mode) { g_mode = mode; }
+int gemm_f32_mode() {
+  if (g_mode < 0) {
+    const char* e = getenv("SDML_F32_GEMM");
+    g_mode = (e && std::string(e) == "mfma") ? 0 : 1;
+  }
+  return g_mode;
+}
+
 int gemm_f32_pick_splits(int M, int N, int K) {
   constexpr int BK = BK_MAX;
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
@@ -473,6 +485,11 @@ void gemm_f32(const GemmArgs& g, hipStream_t stream) {
     hipLaunchKernelGGL(fwd_smallm_kernel, dim3(g.M, (g.N + 63) / 64), dim3(256), 0, stream, g.A, g.B,
                        g.epi == EPI_STORE ? nullptr : g.bias, g.C, g.N, g.K, g.lda, g.ldb, g.ldc,
                        g.epi == EPI_BIAS_RELU ? 1 : 0);
+    return;
+  }
+  // large shapes: fp32 via the bf16x3 split on the bf16 matrix cores (2.67x the fp32 MFMA rate)
+  if (gemm_f32_mode() == 1 && (int64_t)g.M * g.N * g.K >= (int64_t(1) << 26) && gemm_f32x3_eligible(g)) {
+    gemm_f32x3(g, stream);
     return;
   }
   if (g.splits <= 1 && g.epi != EPI_ATOMIC) {

@@ -1,0 +1,463 @@
+// fp32 GEMM on the bf16 matrix cores: every fp32 operand is split into three bf16 terms
+// x = hi + mid + lo (round-to-nearest at each step; the split is EXACT: 8 + 8 + 8 significant
+// bits = the fp32 mantissa) and the product is formed from the six terms that matter,
+//   a*b ~= hi*hi + (hi*mid + mid*hi) + (hi*lo + lo*hi + mid*mid),
+// each term an exact bf16 x bf16 product accumulated in fp32 by v_mfma_f32_32x32x16_bf16.
+// The dropped terms (mid*lo, lo*mid, lo*lo) are below 2^-24 |a*b|: the result has fp32
+// accuracy (tests/test_kernels_gpu.py compares its error against an fp64 reference with the
+// error of the exact-fp32 v_mfma_f32_32x32x2_f32 path), at 6 bf16 MFMAs per fp32 product:
+// bf16 MFMA runs 16x the fp32-input MFMA rate on gfx950, so this is 2.67x the fp32 matrix
+// peak and turns the MLP GEMMs (K = 784, 128-wide) from MFMA-bound into HBM-bound.
+//
+// Same contract as gemm_f32.hip (C[M,N] op= sum_k A(m,k) B(n,k), any of the four operand
+// layouts, the same epilogues, ReLU masks and fused bias-gradient row sums); it replaces the
+// ATen fc-layer GEMMs of the reference (/root/reference/simple_distributed.py:63-64, :75-77).
+//
+// Geometry (gfx950, wave64): 512 threads = 8 waves, K-step 32, one workgroup per CU.
+//   A k-contiguous: block tile 256 x 128, waves 4 x 2, 64 x 64 per wave (2 x 2 MFMA tiles)
+//   A k-major     : block tile 128 x 128, waves 2 x 4, 64 x 32 per wave (2 x 1 MFMA tiles)
+// LDS holds each operand as three bf16 planes (hi/mid/lo), double-buffered: 144 KiB / 96 KiB.
+//   * k-contiguous operand: image [rows][32 k], 64-B rows, 16-B chunk c of row r stored at
+//     chunk c ^ ((r >> 2) & 3): the ds_read_b128 fragment reads (8 consecutive k of one row per
+//     lane) hit 16 distinct 16-B slots per lane group -> conflict-free.
+//   * k-major operand (rows contiguous in memory, e.g. dZ^T or X in the weight gradient):
+//     image [32 k][128 rows], 256-B rows, chunk c of row k at c ^ (((k&3)<<2) | ((k>>2)&3));
+//     written straight from float4 loads (no transpose in registers) and read by two
+//     ds_read_b64_tr_b16 per fragment (hardware transpose), conflict-free on both sides.
+// Global -> registers -> (split) -> LDS staging is prefetched one K-step ahead; one barrier
+// per K-step (the split of tile t+1 is written to the other buffer after tile t's MFMAs).
+// MFMA maps (gfx950): A lane (r = l&31, h = l>>5) holds A[r][k = 8h + j]; B lane holds
+// B[k = 8h + j][col r]; C/D: col = l&31, row = (i&3) + 8(i>>2) + 4h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kernels.h"
+
+namespace sdml {
+namespace {
+
+typedef unsigned short u16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef u16 u16x8 __attribute__((ext_vector_type(8)));
+typedef u16 u16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int NT = 512;  // threads per workgroup
+constexpr int BK = 32;   // k per K-step
+constexpr int BN = 128;  // block tile columns (B operand rows)
+
+struct X3Params {
+  const float* A;
+  const float* amask;
+  const float* B;
+  float* C;
+  const float* bias;
+  float* rowsum;
+  const float* cmask;
+  int M, N, K, lda, ldb, ldc;
+  int epi;
+  int kps;  // K per split (multiple of BK)
+  int tiles_m, tiles_n;
+};
+
+// ---- the split ---------------------------------------------------------------------------------
+__device__ __forceinline__ u16 bf16_bits(float f) {
+  __bf16 h = static_cast<__bf16>(f);  // round-to-nearest-even (v_cvt_pk_bf16_f32)
+  return __builtin_bit_cast(u16, h);
+}
+__device__ __forceinline__ float bf16_val(u16 b) { return __uint_as_float(((unsigned)b) << 16); }
+
+// x -> (hi, mid, lo), x == hi + mid + lo exactly for normal-range x
+template <int N>
+__device__ __forceinline__ void split3(const float (&x)[N], u16 (&h)[N], u16 (&m)[N], u16 (&l)[N]) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    h[j] = bf16_bits(x[j]);
+    const float r1 = x[j] - bf16_val(h[j]);
+    m[j] = bf16_bits(r1);
+    const float r2 = r1 - bf16_val(m[j]);
+    l[j] = bf16_bits(r2);
+  }
+}
+
+// ---- LDS images (offsets in u16 elements) ------------------------------------------------------
+// k-contiguous image [rows][32]: chunk ch (8 k) of row r
+__device__ __forceinline__ int kc_off(int r, int ch) { return r * BK + 8 * (ch ^ ((r >> 2) & 3)); }
+// k-major image [32][128]: 16-B chunk ch (8 rows) of k-row k
+__device__ __forceinline__ int km_off(int k, int ch) {
+  return k * 128 + 8 * (ch ^ (((k & 3) << 2) | ((k >> 2) & 3)));
+}
+
+__device__ __forceinline__ s16x4 ds_tr16(const u16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+// A/B fragment of the 32-row sub-tile at r0, k-substep s (k = 16s + 8h + j), natural k order
+template <bool KM>
+__device__ __forceinline__ bf16x8 frag(const u16* P, int r0, int s, int lane) {
+  if constexpr (!KM) {
+    const int r = r0 + (lane & 31), h = lane >> 5;
+    return *reinterpret_cast<const bf16x8*>(P + kc_off(r, 2 * s + h));
+  } else {
+    // two ds_read_b64_tr_b16: 16-lane group g reads k-rows 16s + 8(g>>1) + q (+4), q = 0..3, at
+    // rows r0 + 16(g&1) + 4p .. +3; lane i of the group receives row r0 + 16(g&1) + i.
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int k = 16 * s + 8 * (g >> 1) + q;
+    const int col = r0 + 16 * (g & 1) + 4 * p;
+    const s16x4 lo = ds_tr16(P + km_off(k, col >> 3) + (col & 7));
+    const s16x4 hi = ds_tr16(P + km_off(k + 4, col >> 3) + (col & 7));
+    bf16x8 f;
+    f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+    f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+    return f;
+  }
+}
+
+__device__ __forceinline__ f32x4 mask4(f32x4 x, f32x4 mk) {
+  x[0] = mk[0] > 0.f ? x[0] : 0.f;
+  x[1] = mk[1] > 0.f ? x[1] : 0.f;
+  x[2] = mk[2] > 0.f ? x[2] : 0.f;
+  x[3] = mk[3] > 0.f ? x[3] : 0.f;
+  return x;
+}
+
+// ---- staging of one operand tile (ROWS x BK) ---------------------------------------------------
+// k-contiguous: ROWS*4 chunks of 8 k; a thread owns NC = ROWS*4/NT chunks (2 float4 each).
+// k-major (ROWS == 128): 32 k-rows x 32 float4; a thread owns 2 float4 (4 rows at one k each).
+template <bool KM, int ROWS>
+struct Stage {
+  static constexpr int NV = ROWS * BK / 4 / NT;  // float4 per thread
+  f32x4 v[NV];
+
+  __device__ __forceinline__ void load(const float* __restrict__ P, const float* __restrict__ mask, int ld,
+                                       int rows, int r0, int k0, int kend) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      int gr, gk;
+      if constexpr (!KM) {
+        const int id = t + NT * (u >> 1);  // chunk
+        gr = r0 + (id >> 2);
+        gk = k0 + 8 * (id & 3) + 4 * (u & 1);
+        if (gr < rows && gk < kend) {
+          const size_t o = (size_t)gr * ld + gk;
+          x = *reinterpret_cast<const f32x4*>(P + o);
+          if (mask) x = mask4(x, *reinterpret_cast<const f32x4*>(mask + o));
+        }
+      } else {
+        const int id = t + NT * u;
+        gk = k0 + (id >> 5);
+        gr = r0 + 4 * (id & 31);
+        if (gk < kend && gr < rows) {  // rows % 4 == 0 (host check): whole float4 in or out
+          const size_t o = (size_t)gk * ld + gr;
+          x = *reinterpret_cast<const f32x4*>(P + o);
+          if (mask) x = mask4(x, *reinterpret_cast<const f32x4*>(mask + o));
+        }
+      }
+      v[u] = x;
+    }
+  }
+
+  // fp32 row sums of the staged values (bias gradient): k-contiguous -> one row per chunk,
+  // k-major -> 4 rows per float4
+  __device__ __forceinline__ void accum_rowsum(float (&rs)[4]) const {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      if constexpr (!KM) {
+        rs[u >> 1] += (v[u][0] + v[u][1]) + (v[u][2] + v[u][3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) rs[e] += v[u][e];
+      }
+    }
+  }
+
+  // split into hi/mid/lo and write the three planes (plane stride PL u16)
+  template <int PL>
+  __device__ __forceinline__ void store(u16* L) const {
+    const int t = threadIdx.x;
+    if constexpr (!KM) {
+#pragma unroll
+      for (int c = 0; c < NV / 2; ++c) {
+        const int id = t + NT * c;
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x[e] = v[2 * c][e];
+          x[4 + e] = v[2 * c + 1][e];
+        }
+        u16 h[8], m[8], l[8];
+        split3<8>(x, h, m, l);
+        const int o = kc_off(id >> 2, id & 3);
+        u16x8 H, Mi, Lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          H[e] = h[e];
+          Mi[e] = m[e];
+          Lo[e] = l[e];
+        }
+        *reinterpret_cast<u16x8*>(L + o) = H;
+        *reinterpret_cast<u16x8*>(L + PL + o) = Mi;
+        *reinterpret_cast<u16x8*>(L + 2 * PL + o) = Lo;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        const int id = t + NT * u;
+        const int k = id >> 5, row = 4 * (id & 31);
+        float x[4] = {v[u][0], v[u][1], v[u][2], v[u][3]};
+        u16 h[4], m[4], l[4];
+        split3<4>(x, h, m, l);
+        const int o = km_off(k, row >> 3) + (row & 7);
+        u16x4 H = {h[0], h[1], h[2], h[3]}, Mi = {m[0], m[1], m[2], m[3]}, Lo = {l[0], l[1], l[2], l[3]};
+        *reinterpret_cast<u16x4*>(L + o) = H;
+        *reinterpret_cast<u16x4*>(L + PL + o) = Mi;
+        *reinterpret_cast<u16x4*>(L + 2 * PL + o) = Lo;
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// FRESH: each K-step's 12 MFMAs accumulate into a zeroed partial tile that is then added to the
+// fp32 accumulator with one round-to-nearest VALU add: the matrix core's internal accumulation
+// then only ever sees a 32-deep partial sum (its rounding error scales with that magnitude, not
+// with the running total's).
+template <bool A_KM, bool B_KM, bool FRESH>
+__global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
+  constexpr int BM = A_KM ? 128 : 256;
+  constexpr int WGM = BM / 64, WGN = 8 / WGM;  // wave grid
+  constexpr int TN = BN / WGN / 32;             // 32-col MFMA tiles per wave (TM = 2)
+  constexpr int AP = BM * BK, BP = BN * BK;     // u16 per plane
+  constexpr int BUF = 3 * (AP + BP);
+  __shared__ __attribute__((aligned(16))) u16 smem[2 * BUF];
+
+  // XCD-aware bijective remap over tiles x splits (blocks b, b+8 share an XCD): each XCD gets a
+  // contiguous run of logical ids; logical id = split * ntiles + tile, so the tiles that stream
+  // the same K-slice of the shared operand read it through one L2.
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int nwg = ntiles * gridDim.y;
+  const int orig = blockIdx.y * gridDim.x + blockIdx.x;
+  int wg = orig;
+  if (nwg >= 16) {
+    const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  }
+  const int split = wg / ntiles, tile = wg % ntiles;
+  const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = split * p.kps;
+  const int kend = min(p.K, kbeg + p.kps);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % WGM, wn = wave / WGM;
+  const int h = lane >> 5;
+
+  f32x16 acc[2][TN];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  f32x16 part[2][TN];  // FRESH: the K-step's partial tile
+  const bool do_rowsum = p.rowsum != nullptr && tn == 0;
+  float rs[4] = {0.f, 0.f, 0.f, 0.f};
+
+  Stage<A_KM, BM> sa;
+  Stage<B_KM, BN> sb;
+  auto load = [&](int k0) {
+    sa.load(p.A, p.amask, p.lda, p.M, m0, k0, kend);
+    sb.load(p.B, nullptr, p.ldb, p.N, n0, k0, kend);
+  };
+  auto store = [&](int buf) {
+    u16* L = smem + buf * BUF;
+    sa.template store<AP>(L);
+    sb.template store<BP>(L + 3 * AP);
+  };
+
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    load(kbeg);
+    if (do_rowsum) sa.accum_rowsum(rs);
+    store(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) load(kbeg + (t + 1) * BK);  // next tile -> registers (latency under the MFMAs)
+    const u16* As = smem + cur * BUF;
+    const u16* Bs = As + 3 * AP;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 a[2][3], b[TN][3];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) a[i][pl] = frag<A_KM>(As + pl * AP, wm * 64 + i * 32, s, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) b[j][pl] = frag<B_KM>(Bs + pl * BP, wn * (32 * TN) + j * 32, s, lane);
+      // small terms first, the leading hi*hi term last
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          f32x16 c = (FRESH && s == 0) ? f32x16{} : (FRESH ? part[i][j] : acc[i][j]);
+          c = mfma(a[i][1], b[j][1], c);  // mid*mid
+          c = mfma(a[i][2], b[j][0], c);  // lo*hi
+          c = mfma(a[i][0], b[j][2], c);  // hi*lo
+          c = mfma(a[i][1], b[j][0], c);  // mid*hi
+          c = mfma(a[i][0], b[j][1], c);  // hi*mid
+          c = mfma(a[i][0], b[j][0], c);  // hi*hi
+          if constexpr (FRESH) {
+            if (s == BK / 16 - 1) acc[i][j] += c;
+            else part[i][j] = c;
+          } else {
+            acc[i][j] = c;
+          }
+        }
+    }
+    if (t + 1 < nk) {
+      if (do_rowsum) sa.accum_rowsum(rs);
+      store(cur ^ 1);
+    }
+    __syncthreads();
+  }
+
+  if (do_rowsum) {
+    if constexpr (!A_KM) {
+      // thread's chunks: rows (t + NT*c) >> 2; the 4 threads of a row are adjacent lanes
+#pragma unroll
+      for (int c = 0; c < Stage<A_KM, BM>::NV / 2; ++c) {
+        float v = rs[c];
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        const int row = m0 + ((threadIdx.x + NT * c) >> 2);
+        if ((lane & 3) == 0 && row < p.M) atomicAdd(p.rowsum + row, v);
+      }
+    } else {
+      // rows m0 + 4*(t & 31) + e: lanes l and l^32 share them
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = rs[e] + __shfl_xor(rs[e], 32);
+        const int row = m0 + 4 * (threadIdx.x & 31) + e;
+        if (lane < 32 && row < p.M) atomicAdd(p.rowsum + row, v);
+      }
+    }
+  }
+
+  // ---- epilogue ----
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * (32 * TN) + j * 32 + (lane & 31);
+      if (col >= p.N) continue;
+      const float bv = (p.epi == EPI_BIAS || p.epi == EPI_BIAS_RELU) ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= p.M) continue;
+        const float v = acc[i][j][r];
+        float* dst = p.C + (size_t)row * p.ldc + col;
+        switch (p.epi) {
+          case EPI_STORE:
+            *dst = (p.cmask && p.cmask[(size_t)row * p.ldc + col] <= 0.f) ? 0.f : v;
+            break;
+          case EPI_BIAS: *dst = v + bv; break;
+          case EPI_BIAS_RELU: *dst = fmaxf(v + bv, 0.f); break;
+          case EPI_ACCUM: *dst += v; break;
+          default: atomicAdd(dst, v); break;
+        }
+      }
+    }
+}
+
+bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+
+// operand staging needs whole, aligned float4s: a k-contiguous operand K % 4 == 0, a k-major
+// one rows % 4 == 0, and ld % 4 == 0 with 16-B aligned bases (masks laid out like the operand)
+bool operand_ok(const float* P, const float* mask, int ld, bool kmajor, int rows, int K) {
+  if (!P || !al16(P) || (mask && !al16(mask)) || ld % 4) return false;
+  return kmajor ? rows % 4 == 0 : K % 4 == 0;
+}
+
+}  // namespace
+
+static int g_x3_variant = 0;  // 0: per-K-step fresh partials (default), 1: one running accumulator
+
+bool gemm_f32x3_eligible(const GemmArgs& g) {
+  if (g.M <= 0 || g.N <= 0 || g.K <= 0) return false;
+  if (g.epi == EPI_ATOMIC ? false : g.splits > 1) return false;
+  return operand_ok(g.A, g.amask, g.lda, g.a_kmajor, g.M, g.K) && operand_ok(g.B, nullptr, g.ldb, g.b_kmajor, g.N, g.K);
+}
+
+int gemm_f32x3_pick_splits(int M, int N, int K, bool a_kmajor) {
+  const int bm = a_kmajor ? 128 : 256;
+  const int tiles = ((M + bm - 1) / bm) * ((N + BN - 1) / BN);
+  // one 512-thread workgroup per CU (LDS): aim at one full wave of 256 workgroups, with at
+  // least 16 K-steps per split (each split adds a whole C tile with fp32 atomics)
+  int splits = 256 / tiles;
+  const int max_by_k = K / (16 * BK);
+  if (splits > max_by_k) splits = max_by_k;
+  return splits < 1 ? 1 : splits;
+}
+
+void gemm_f32x3(const GemmArgs& g, hipStream_t stream) {
+  X3Params p;
+  p.A = g.A;
+  p.amask = g.amask;
+  p.B = g.B;
+  p.C = g.C;
+  p.bias = g.bias;
+  p.rowsum = g.rowsum;
+  p.cmask = g.cmask;
+  p.M = g.M;
+  p.N = g.N;
+  p.K = g.K;
+  p.lda = g.lda;
+  p.ldb = g.ldb;
+  p.ldc = g.ldc;
+  p.epi = g.epi;
+  const int bm = g.a_kmajor ? 128 : 256;
+  // atomic epilogues are split-invariant: pick the split count for THIS kernel's geometry
+  int splits = g.epi == EPI_ATOMIC ? gemm_f32x3_pick_splits(g.M, g.N, g.K, g.a_kmajor) : 1;
+  int kps = (g.K + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = (g.K + kps - 1) / kps;
+  p.kps = kps;
+  p.tiles_m = (g.M + bm - 1) / bm;
+  p.tiles_n = (g.N + BN - 1) / BN;
+  dim3 grid(p.tiles_m * p.tiles_n, splits, 1);
+  dim3 block(NT);
+#define X3_LAUNCH(F)                                                                      \
+  if (!g.a_kmajor && !g.b_kmajor)                                                         \
+    hipLaunchKernelGGL((gemm_x3_kernel<false, false, F>), grid, block, 0, stream, p);     \
+  else if (!g.a_kmajor && g.b_kmajor)                                                     \
+    hipLaunchKernelGGL((gemm_x3_kernel<false, true, F>), grid, block, 0, stream, p);      \
+  else if (g.a_kmajor && !g.b_kmajor)                                                     \
+    hipLaunchKernelGGL((gemm_x3_kernel<true, false, F>), grid, block, 0, stream, p);      \
+  else                                                                                    \
+    hipLaunchKernelGGL((gemm_x3_kernel<true, true, F>), grid, block, 0, stream, p);
+  if (g_x3_variant == 1) {
+    X3_LAUNCH(false)
+  } else {
+    X3_LAUNCH(true)
+  }
+#undef X3_LAUNCH
+}
+
+void gemm_f32x3_set_variant(int v) { g_x3_variant = v; }
+
+}  // namespace sdml

@@ -51,6 +51,14 @@ constexpr int FWD_SMALLM_MAX_M = 64;
 void dw_smallk(const float* gy, const float* mask, const float* x, float* gw, float* gb, int M, int N, int K,
                hipStream_t stream);
 void gemm_f32_set_variant(int v);  // tuning experiments: 0 auto, 16 / 32 = K-step
+// fp32 GEMM engine for large shapes: 1 = bf16x3 split on bf16 MFMA (gemm_f32x3.hip, fp32
+// accuracy, default), 0 = exact fp32-input MFMA (gemm_f32.hip). Env SDML_F32_GEMM=x3|mfma.
+void gemm_f32_set_mode(int mode);
+int gemm_f32_mode();
+bool gemm_f32x3_eligible(const GemmArgs& g);
+int gemm_f32x3_pick_splits(int M, int N, int K, bool a_kmajor);
+void gemm_f32x3(const GemmArgs& g, hipStream_t stream);
+void gemm_f32x3_set_variant(int v);  // 0: fresh per-K-step partials (default), 1: running accumulator
 
 // ---- fused classifier head: z = x W^T + b; log_softmax; NLL; backward --------------------
 // x [M,K] fp32, W [C,K], b [C], target [M] int64. stats[0] += sum loss, stats[1] += #correct.

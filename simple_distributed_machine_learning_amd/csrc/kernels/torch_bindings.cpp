@@ -174,6 +174,46 @@ void gemm_f32_op(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool a_kmajo
   sdml::gemm_f32(g, cur_stream());
 }
 
+// the bf16x3-split engine called directly (tests, any size): same contract as gemm_f32_op
+void gemm_f32x3_op(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool a_kmajor, bool b_kmajor, int64_t epi,
+                   c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> rowsum,
+                   c10::optional<torch::Tensor> amask, c10::optional<torch::Tensor> cmask) {
+  check_f32_cuda(A, "A");
+  check_f32_cuda(B, "B");
+  check_f32_cuda(C, "C");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "2-D operands");
+  const int64_t M = C.size(0), N = C.size(1);
+  const int64_t K = a_kmajor ? A.size(0) : A.size(1);
+  TORCH_CHECK((a_kmajor ? A.size(1) : A.size(0)) == M, "A rows != M");
+  TORCH_CHECK((b_kmajor ? B.size(0) : B.size(1)) == K, "B k-extent != K");
+  TORCH_CHECK((b_kmajor ? B.size(1) : B.size(0)) == N, "B rows != N");
+  check_opt(bias, "bias", N);
+  check_opt(rowsum, "rowsum", M);
+  check_opt(amask, "amask", A.numel());
+  check_opt(cmask, "cmask", C.numel());
+  TORCH_CHECK(epi >= 0 && epi <= 4, "bad epilogue");
+  sdml::GemmArgs g;
+  g.A = A.data_ptr<float>();
+  g.B = B.data_ptr<float>();
+  g.C = C.data_ptr<float>();
+  g.bias = opt_ptr(bias);
+  g.rowsum = opt_ptr(rowsum);
+  g.amask = opt_ptr(amask);
+  g.cmask = opt_ptr(cmask);
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.lda = A.size(1);
+  g.ldb = B.size(1);
+  g.ldc = N;
+  g.a_kmajor = a_kmajor;
+  g.b_kmajor = b_kmajor;
+  g.epi = (int)epi;
+  TORCH_CHECK(!(epi == 1 || epi == 2) || g.bias, "bias epilogue needs bias");
+  TORCH_CHECK(sdml::gemm_f32x3_eligible(g), "gemm_f32x3: unsupported shape/alignment");
+  sdml::gemm_f32x3(g, cur_stream());
+}
+
 // fused head; returns (stats[2] = {loss_sum, correct}, dx or None). If `stats_acc` is given
 // the kernel accumulates into it (and returns it) instead of allocating a new one.
 std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
@@ -569,6 +609,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention_fwd", &attention_fwd, "causal flash attention forward (bf16, d=64)");
   m.def("attention_bwd", &attention_bwd, "causal flash attention backward (bf16, d=64)");
   m.def("attention_set_fwd_kb", &sdml::attention_set_fwd_kb, "attention forward keys per tile (tuning)");
+  m.def("gemm_f32x3", &gemm_f32x3_op, "fp32 GEMM via the bf16x3 split on bf16 MFMA", py::arg("A"), py::arg("B"),
+        py::arg("C"), py::arg("a_kmajor"), py::arg("b_kmajor"), py::arg("epi") = 0, py::arg("bias") = py::none(),
+        py::arg("rowsum") = py::none(), py::arg("amask") = py::none(), py::arg("cmask") = py::none());
+  m.def("gemm_f32x3_set_variant", &sdml::gemm_f32x3_set_variant, "x3 engine accumulation variant (A/B)");
+  m.def("gemm_f32_set_mode", &sdml::gemm_f32_set_mode, "fp32 GEMM engine: 1 = bf16x3 split (default), 0 = fp32 MFMA");
+  m.def("gemm_f32_mode", &sdml::gemm_f32_mode, "current fp32 GEMM engine");
   m.def("gemm_f32_set_variant", &sdml::gemm_f32_set_variant, "fp32 GEMM variant (tuning: 0 auto, 16, 32)");
   m.def("ref_cnn_stage0_fwd", &ref_cnn_stage0_fwd, "reference CNN stage 0 forward (one launch)");
   m.def("ref_cnn_stage0_bwd", &ref_cnn_stage0_bwd, "reference CNN stage 0 backward (one launch)");

@@ -1,0 +1,140 @@
+"""The bf16x3-split fp32 GEMM engine (csrc/kernels/gemm_f32x3.hip) against fp32/fp64 PyTorch
+references: every operand layout, every epilogue, the fused bias-gradient row sums and ReLU
+masks, and an accuracy comparison with the exact-fp32 MFMA engine (gemm_f32.hip)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no ROCm GPU", allow_module_level=True)
+
+from simple_distributed_machine_learning_amd import _native, ops  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+K = _native.kernels()
+
+
+def rnd(*shape, seed=0, lo=-1.0, hi=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.empty(shape).uniform_(lo, hi, generator=g).to(DEV)
+
+
+def ref64(A, B):
+    return (A.double() @ B.double().t())
+
+
+def layout(A, km):
+    return A.t().contiguous() if km else A
+
+
+def test_x3_identity_asymmetric():
+    # A = I with an asymmetric B: a transposed C/D map or a wrong fragment k order fails
+    n = 256
+    A = torch.eye(n, device=DEV)
+    B = torch.arange(n * n, device=DEV, dtype=torch.float32).reshape(n, n) / (n * n)
+    for a_km in (False, True):
+        for b_km in (False, True):
+            C = torch.empty(n, n, device=DEV)
+            K.gemm_f32x3(layout(A, a_km), layout(B, b_km), C, a_km, b_km, 0)
+            torch.testing.assert_close(C, B.t().contiguous(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("a_km,b_km", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,Kd", [(256, 128, 784), (300, 132, 100), (1000, 260, 68), (64, 784, 2048), (8, 4, 4)])
+def test_x3_layouts_fp32_accuracy(a_km, b_km, M, N, Kd):
+    A, B = rnd(M, Kd, seed=1), rnd(N, Kd, seed=2)
+    C = torch.full((M, N), float("nan"), device=DEV)
+    K.gemm_f32x3(layout(A, a_km), layout(B, b_km), C, a_km, b_km, 0)
+    want = ref64(A, B)
+    err = (C.double() - want).abs()
+    # fp32-level accuracy: bounded like an fp32 dot product, |err| <~ K * 2^-24 * sum|a||b|
+    bound = Kd * 2.0 ** -24 * (A.abs().double() @ B.abs().double().t()) + 1e-30
+    assert torch.isfinite(C).all()
+    assert (err <= bound).all(), float((err / bound).max())
+
+
+@pytest.mark.parametrize("Kd", [784, 4096])
+def test_x3_error_matches_fp32_mfma(Kd):
+    """Error vs fp64 of the split engine is within 2x of the exact fp32-input MFMA engine."""
+    M, N = 512, 256
+    A, B = rnd(M, Kd, seed=3), rnd(N, Kd, seed=4)
+    C3 = torch.empty(M, N, device=DEV)
+    Cf = torch.empty(M, N, device=DEV)
+    K.gemm_f32x3(A, B, C3, False, False, 0)
+    mode = K.gemm_f32_mode()
+    try:
+        K.gemm_f32_set_mode(0)
+        K.gemm_f32(A, B, Cf, False, False, 0)
+    finally:
+        K.gemm_f32_set_mode(mode)
+    want = ref64(A, B)
+    e3 = (C3.double() - want).abs()
+    ef = (Cf.double() - want).abs()
+    assert e3.max() <= 2.0 * ef.max() + 1e-7, (float(e3.max()), float(ef.max()))
+    assert e3.mean() <= 2.0 * ef.mean() + 1e-8, (float(e3.mean()), float(ef.mean()))
+
+
+def test_x3_wide_dynamic_range():
+    # terms spanning many binades: the split is exact for any normal-range value
+    M, N, Kd = 256, 128, 512
+    A = rnd(M, Kd, seed=5) * torch.exp2(rnd(M, Kd, seed=6, lo=-30, hi=30).round())
+    B = rnd(N, Kd, seed=7) * torch.exp2(rnd(N, Kd, seed=8, lo=-30, hi=30).round())
+    C = torch.empty(M, N, device=DEV)
+    K.gemm_f32x3(A, B, C, False, False, 0)
+    want = ref64(A, B)
+    bound = Kd * 2.0 ** -24 * (A.abs().double() @ B.abs().double().t()) + 1e-30
+    assert ((C.double() - want).abs() <= bound).all()
+
+
+def test_x3_epilogues():
+    M, N, Kd = 512, 256, 320
+    A, B, bias = rnd(M, Kd, seed=9), rnd(N, Kd, seed=10), rnd(N, seed=11)
+    want = (A.double() @ B.double().t()).float()
+    C = torch.empty(M, N, device=DEV)
+    K.gemm_f32x3(A, B, C, False, False, 1, bias)
+    torch.testing.assert_close(C, want + bias, rtol=1e-5, atol=1e-5)
+    K.gemm_f32x3(A, B, C, False, False, 2, bias)
+    torch.testing.assert_close(C, torch.relu(want + bias), rtol=1e-5, atol=1e-5)
+    C0 = rnd(M, N, seed=12)
+    C = C0.clone()
+    K.gemm_f32x3(A, B, C, False, False, 3)
+    torch.testing.assert_close(C, C0 + want, rtol=1e-5, atol=1e-5)
+    cm = rnd(M, N, seed=13)
+    K.gemm_f32x3(A, B, C, False, False, 0, None, None, None, cm)
+    torch.testing.assert_close(C, want * (cm > 0), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("a_km", [False, True])
+def test_x3_splitk_atomic_rowsum_amask(a_km):
+    # the weight-gradient shape: gW[N, K] += (gy*mask)^T x, gb += colsum(gy*mask), split over M
+    Mb, N, Kd = 20000, 128, 784
+    gy, x, mask = rnd(Mb, N, seed=14), rnd(Mb, Kd, seed=15), rnd(Mb, N, seed=16)
+    gz = gy * (mask > 0)
+    gw0, gb0 = rnd(N, Kd, seed=17), rnd(N, seed=18)
+    gw, gb = gw0.clone(), gb0.clone()
+    if a_km:  # A(n, m) = gy[m][n] (k-major), B(k, m) = x[m][k] (k-major)
+        K.gemm_f32x3(gy, x, gw, True, True, 4, None, gb, mask)
+    else:
+        K.gemm_f32x3(gy.t().contiguous(), x, gw, False, True, 4, None, gb, mask.t().contiguous())
+    want_w = (gz.double().t() @ x.double()).float() + gw0
+    want_b = gz.double().sum(0).float() + gb0
+    torch.testing.assert_close(gw, want_w, rtol=1e-5, atol=2e-4)
+    torch.testing.assert_close(gb, want_b, rtol=1e-5, atol=2e-4)
+
+
+def test_linear_ops_route_to_x3_at_bench_shape():
+    """ops.linear_relu_fwd / linear_relu_bwd at the headline shape run on the split engine and
+    agree with an fp64 reference to fp32 accuracy."""
+    assert K.gemm_f32_mode() == 1
+    M, Kd, N = 16384, 784, 128
+    x, w, b = rnd(M, Kd, seed=19, lo=0, hi=1), rnd(N, Kd, seed=20) * 0.05, rnd(N, seed=21) * 0.1
+    y = ops.linear_relu_fwd(x, w, b)
+    want = torch.relu(x.double() @ w.double().t() + b.double())
+    assert ((y.double() - want).abs() <= 1e-5 * (1 + want.abs())).all()
+    gy = rnd(M, N, seed=22) * 1e-3 * (y > 0)
+    gw, gb = torch.zeros_like(w), torch.zeros_like(b)
+    dx = ops.linear_relu_bwd(x, y, gy, w, gw, gb, need_dx=True, gy_masked=True, mask_dx=False)
+    torch.testing.assert_close(gw, (gy.double().t() @ x.double()).float(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(gb, gy.double().sum(0).float(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dx, (gy.double() @ w.double()).float(), rtol=1e-5, atol=1e-7)

@@ -67,19 +67,22 @@ def main():
     rep("dX_gemm_masked", timeit(lambda: ops.linear_relu_bwd(x, h, gy, w, None, None, True)), fl)
     rep("head_fused_fwd_bwd", timeit(lambda: ops.linear_logsoftmax_nll(h, w2, b2, t, gw2, gb2, 1.0 / B, True, stats)),
         bytes_=B * N * 4 * 2 + B * 8)
-    # A/B of the fp32 GEMM K-step, interleaved rounds in one process (guide §5.4 rule 24)
+    # A/B of the two fp32 GEMM engines (bf16x3 split vs exact fp32-input MFMA), interleaved
+    # rounds in one process (guide §5.4 rule 24)
     K_ = _native.kernels()
-    ab = {16: {"fwd": [], "dW": []}, 32: {"fwd": [], "dW": []}}
+    ab = {1: {"fwd": [], "dW": [], "dX": []}, 0: {"fwd": [], "dW": [], "dX": []}}
     for _ in range(5):
-        for v in (32, 16):
-            K_.gemm_f32_set_variant(v)
+        for v in (1, 0):
+            K_.gemm_f32_set_mode(v)
             ab[v]["fwd"].append(timeit(lambda: ops.linear_relu_fwd(x, w, b), iters=10))
             ab[v]["dW"].append(timeit(lambda: ops.linear_relu_bwd(x, h, gy, w, gw, gb, False), iters=10))
-    K_.gemm_f32_set_variant(0)
+            ab[v]["dX"].append(timeit(lambda: ops.linear_relu_bwd(x, h, gy, w, None, None, True), iters=10))
+    K_.gemm_f32_set_mode(1)
     for v in ab:
         for k in ab[v]:
             t_ = sorted(ab[v][k])
-            rep(f"variant BK={v} {k} (median of 5 rounds)", t_[2], fl)
+            rep(f"engine {'bf16x3' if v else 'fp32-mfma'} {k} (median of 5 rounds)", t_[2], fl,
+                bytes_=B * K * 4 + B * N * 4)
     p = torch.zeros(101888, device=dev)
     gg, mb = torch.randn_like(p), torch.zeros_like(p)
     rep("sgd", timeit(lambda: ops.sgd_momentum_(p, gg, mb, 0.1, 0.5)), bytes_=p.numel() * 4 * 5)

@@ -478,6 +478,10 @@ int gemm_f32_skinny_splits(int M, int N, int K, int epi) {
   return splits >= 4 ? splits : 0;
 }
 
+bool gemm_f32_uses_x3(const GemmArgs& g) {
+  return gemm_f32_mode() == 1 && (int64_t)g.M * g.N * g.K >= (int64_t(1) << 26) && gemm_f32x3_eligible(g);
+}
+
 void gemm_f32(const GemmArgs& g, hipStream_t stream) {
   if (g.M <= FWD_SMALLM_MAX_M && !g.a_kmajor && !g.b_kmajor && g.splits <= 1 && !g.amask && !g.rowsum &&
       (g.epi == EPI_BIAS || g.epi == EPI_BIAS_RELU || (g.epi == EPI_STORE && !g.cmask)) && g.K % 4 == 0 &&
@@ -488,7 +492,7 @@ void gemm_f32(const GemmArgs& g, hipStream_t stream) {
     return;
   }
   // large shapes: fp32 via the bf16x3 split on the bf16 matrix cores (2.67x the fp32 MFMA rate)
-  if (gemm_f32_mode() == 1 && (int64_t)g.M * g.N * g.K >= (int64_t(1) << 26) && gemm_f32x3_eligible(g)) {
+  if (gemm_f32_uses_x3(g)) {
     gemm_f32x3(g, stream);
     return;
   }

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -53,6 +54,7 @@ struct X3Params {
   const float* A;
   const float* amask;
   const float* B;
+  const u16* Bp;  // B pre-split into bf16 planes [3][N][ldb] (k-contiguous B only) or nullptr
   float* C;
   const float* bias;
   float* rowsum;
@@ -132,33 +134,44 @@ struct Stage {
   static constexpr int NV = ROWS * BK / 4 / NT;  // float4 per thread
   f32x4 v[NV];
 
+  // Branch-free and select-free: indices are clamped into the operand (rows past the end re-read
+  // the last row / float4 and only feed outputs that are never stored; k past kend is zeroed at
+  // split time by store()), so the loads' results are not needed until the split and the whole
+  // K-step stays one basic block the scheduler can interleave.
+  template <bool MASK>
   __device__ __forceinline__ void load(const float* __restrict__ P, const float* __restrict__ mask, int ld,
-                                       int rows, int r0, int k0, int kend) {
+                                       int rows, int r0, int k0, int K) {
     const int t = threadIdx.x;
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
-      f32x4 x = {0.f, 0.f, 0.f, 0.f};
-      int gr, gk;
+      size_t o;
       if constexpr (!KM) {
         const int id = t + NT * (u >> 1);  // chunk
-        gr = r0 + (id >> 2);
-        gk = k0 + 8 * (id & 3) + 4 * (u & 1);
-        if (gr < rows && gk < kend) {
-          const size_t o = (size_t)gr * ld + gk;
-          x = *reinterpret_cast<const f32x4*>(P + o);
-          if (mask) x = mask4(x, *reinterpret_cast<const f32x4*>(mask + o));
-        }
+        const int gr = min(r0 + (id >> 2), rows - 1);
+        const int gk = min(k0 + 8 * (id & 3) + 4 * (u & 1), K - 4);
+        o = (size_t)gr * ld + gk;
       } else {
         const int id = t + NT * u;
-        gk = k0 + (id >> 5);
-        gr = r0 + 4 * (id & 31);
-        if (gk < kend && gr < rows) {  // rows % 4 == 0 (host check): whole float4 in or out
-          const size_t o = (size_t)gk * ld + gr;
-          x = *reinterpret_cast<const f32x4*>(P + o);
-          if (mask) x = mask4(x, *reinterpret_cast<const f32x4*>(mask + o));
-        }
+        const int gk = min(k0 + (id >> 5), K - 1);
+        const int gr = min(r0 + 4 * (id & 31), rows - 4);  // rows % 4 == 0 (host check)
+        o = (size_t)gk * ld + gr;
       }
+      f32x4 x = *reinterpret_cast<const f32x4*>(P + o);
+      if constexpr (MASK) x = mask4(x, *reinterpret_cast<const f32x4*>(mask + o));
       v[u] = x;
+    }
+  }
+
+  // zero the k >= kend part of the tile staged for k0 (the K tail / past the end of a split)
+  __device__ __forceinline__ void zero_tail(int k0, int kend) {
+    const int t = threadIdx.x;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      int gk;
+      if constexpr (!KM) gk = k0 + 8 * ((t + NT * (u >> 1)) & 3) + 4 * (u & 1);
+      else gk = k0 + ((t + NT * u) >> 5);
+      v[u] = gk < kend ? v[u] : z;
     }
   }
 
@@ -222,6 +235,59 @@ struct Stage {
   }
 };
 
+// k-contiguous operand already split into bf16 planes in global memory ([3][rows][ld] u16, ld %
+// 8 == 0): a plain copy into the LDS image, no VALU split. A thread owns one 8-k chunk per plane.
+template <int ROWS>
+struct StagePre {
+  static constexpr int NC = ROWS * 4 / NT;  // chunks per thread per plane
+  u16x8 v[3][NC];
+
+  __device__ __forceinline__ void load(const u16* __restrict__ P, int ld, int rows, int r0, int k0, int K) {
+    const size_t plane = (size_t)rows * ld;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int id = threadIdx.x + NT * c;
+      const int gr = min(r0 + (id >> 2), rows - 1);
+      const int gk = min(k0 + 8 * (id & 3), K - 8);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) v[pl][c] = *reinterpret_cast<const u16x8*>(P + pl * plane + (size_t)gr * ld + gk);
+    }
+  }
+  __device__ __forceinline__ void zero_tail(int k0, int kend) {
+    const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const bool ok = k0 + 8 * ((threadIdx.x + NT * c) & 3) < kend;  // K % 8 == 0: chunk all in or out
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) v[pl][c] = ok ? v[pl][c] : z;
+    }
+  }
+  template <int PL>
+  __device__ __forceinline__ void store(u16* L) const {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int id = threadIdx.x + NT * c;
+      const int o = kc_off(id >> 2, id & 3);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u16x8*>(L + pl * PL + o) = v[pl][c];
+    }
+  }
+};
+
+// fp32 -> three bf16 planes (hi, mid, lo), 4 elements per thread (n % 4 == 0)
+__global__ void __launch_bounds__(256) split3_planes_kernel(const float* __restrict__ x, u16* __restrict__ out,
+                                                            int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  const f32x4 v = *reinterpret_cast<const f32x4*>(x + i);
+  float a[4] = {v[0], v[1], v[2], v[3]};
+  u16 h[4], m[4], l[4];
+  split3<4>(a, h, m, l);
+  *reinterpret_cast<u16x4*>(out + i) = u16x4{h[0], h[1], h[2], h[3]};
+  *reinterpret_cast<u16x4*>(out + n + i) = u16x4{m[0], m[1], m[2], m[3]};
+  *reinterpret_cast<u16x4*>(out + 2 * n + i) = u16x4{l[0], l[1], l[2], l[3]};
+}
+
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -230,8 +296,13 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 // fp32 accumulator with one round-to-nearest VALU add: the matrix core's internal accumulation
 // then only ever sees a 32-deep partial sum (its rounding error scales with that magnitude, not
 // with the running total's).
-template <bool A_KM, bool B_KM, bool FRESH>
+// EARLY: the split + LDS write of tile t+1 and the global loads of tile t+2 are issued in the
+// same basic block as tile t's MFMAs (the scheduler interleaves the VALU/LDS work into the
+// matrix-core shadow); otherwise they follow the MFMAs (tile t+1 loaded during tile t).
+// BPRE: B arrives pre-split (p.Bp; k-contiguous B only)
+template <bool A_KM, bool B_KM, bool AMASK, bool EARLY, bool BPRE = false>
 __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
+  constexpr bool FRESH = true;
   constexpr int BM = A_KM ? 128 : 256;
   constexpr int WGM = BM / 64, WGN = 8 / WGM;  // wave grid
   constexpr int TN = BN / WGN / 32;             // 32-col MFMA tiles per wave (TM = 2)
@@ -274,12 +345,18 @@ __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
 
   Stage<A_KM, BM> sa;
-  Stage<B_KM, BN> sb;
+  typedef typename std::conditional<BPRE, StagePre<BN>, Stage<B_KM, BN>>::type SB;
+  SB sb;
   auto load = [&](int k0) {
-    sa.load(p.A, p.amask, p.lda, p.M, m0, k0, kend);
-    sb.load(p.B, nullptr, p.ldb, p.N, n0, k0, kend);
+    sa.template load<AMASK>(p.A, p.amask, p.lda, p.M, m0, k0, p.K);
+    if constexpr (BPRE) sb.load(p.Bp, p.ldb, p.N, n0, k0, p.K);
+    else sb.template load<false>(p.B, nullptr, p.ldb, p.N, n0, k0, p.K);
   };
-  auto store = [&](int buf) {
+  // tile staged for k0 -> K-tail zeroing -> bias-grad row sums -> split -> LDS buffer `buf`
+  auto store = [&](int buf, int k0) {
+    sa.zero_tail(k0, kend);
+    sb.zero_tail(k0, kend);
+    sa.accum_rowsum(rs);
     u16* L = smem + buf * BUF;
     sa.template store<AP>(L);
     sb.template store<BP>(L + 3 * AP);
@@ -288,15 +365,17 @@ __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
   const int nk = (kend - kbeg + BK - 1) / BK;
   if (nk > 0) {
     load(kbeg);
-    if (do_rowsum) sa.accum_rowsum(rs);
-    store(0);
+    store(0, kbeg);
+    if (EARLY) load(kbeg + BK);  // zeroed at split time past kend
   }
   __syncthreads();
   for (int t = 0; t < nk; ++t) {
     const int cur = t & 1;
-    if (t + 1 < nk) load(kbeg + (t + 1) * BK);  // next tile -> registers (latency under the MFMAs)
     const u16* As = smem + cur * BUF;
     const u16* Bs = As + 3 * AP;
+    if constexpr (!EARLY) {
+      if (t + 1 < nk) load(kbeg + (t + 1) * BK);  // next tile -> registers (latency under the MFMAs)
+    }
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       bf16x8 a[2][3], b[TN][3];
@@ -308,6 +387,15 @@ __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) b[j][pl] = frag<B_KM>(Bs + pl * BP, wn * (32 * TN) + j * 32, s, lane);
+      if constexpr (EARLY) {
+        if (s == 0) {
+          // tile t+1 (in registers since the previous K-step) -> split -> the other buffer, whose
+          // last readers passed the previous barrier; then tile t+2 -> registers. Past the end
+          // both are harmless: zero tiles written to a buffer nobody reads again.
+          store(cur ^ 1, kbeg + (t + 1) * BK);
+          load(kbeg + (t + 2) * BK);
+        }
+      }
       // small terms first, the leading hi*hi term last
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -328,12 +416,12 @@ __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
           }
         }
     }
-    if (t + 1 < nk) {
-      if (do_rowsum) sa.accum_rowsum(rs);
-      store(cur ^ 1);
+    if constexpr (!EARLY) {
+      if (t + 1 < nk) store(cur ^ 1, kbeg + (t + 1) * BK);
     }
     __syncthreads();
   }
+  // EARLY staged one tile past the end in the last iteration: zeroed, row sums unaffected
 
   if (do_rowsum) {
     if constexpr (!A_KM) {
@@ -395,7 +483,7 @@ bool operand_ok(const float* P, const float* mask, int ld, bool kmajor, int rows
 
 }  // namespace
 
-static int g_x3_variant = 0;  // 0: per-K-step fresh partials (default), 1: one running accumulator
+static int g_x3_variant = 0;  // pipeline A/B: 0 = EARLY split (default), 1 = split after the MFMAs
 
 bool gemm_f32x3_eligible(const GemmArgs& g) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0) return false;
@@ -441,23 +529,49 @@ void gemm_f32x3(const GemmArgs& g, hipStream_t stream) {
   p.tiles_n = (g.N + BN - 1) / BN;
   dim3 grid(p.tiles_m * p.tiles_n, splits, 1);
   dim3 block(NT);
-#define X3_LAUNCH(F)                                                                      \
-  if (!g.a_kmajor && !g.b_kmajor)                                                         \
-    hipLaunchKernelGGL((gemm_x3_kernel<false, false, F>), grid, block, 0, stream, p);     \
-  else if (!g.a_kmajor && g.b_kmajor)                                                     \
-    hipLaunchKernelGGL((gemm_x3_kernel<false, true, F>), grid, block, 0, stream, p);      \
-  else if (g.a_kmajor && !g.b_kmajor)                                                     \
-    hipLaunchKernelGGL((gemm_x3_kernel<true, false, F>), grid, block, 0, stream, p);      \
-  else                                                                                    \
-    hipLaunchKernelGGL((gemm_x3_kernel<true, true, F>), grid, block, 0, stream, p);
-  if (g_x3_variant == 1) {
-    X3_LAUNCH(false)
+#define X3_LAUNCH(AM, E)                                                                      \
+  if (!g.a_kmajor && !g.b_kmajor)                                                             \
+    hipLaunchKernelGGL((gemm_x3_kernel<false, false, AM, E>), grid, block, 0, stream, p);     \
+  else if (!g.a_kmajor && g.b_kmajor)                                                         \
+    hipLaunchKernelGGL((gemm_x3_kernel<false, true, AM, E>), grid, block, 0, stream, p);      \
+  else if (g.a_kmajor && !g.b_kmajor)                                                         \
+    hipLaunchKernelGGL((gemm_x3_kernel<true, false, AM, E>), grid, block, 0, stream, p);      \
+  else                                                                                        \
+    hipLaunchKernelGGL((gemm_x3_kernel<true, true, AM, E>), grid, block, 0, stream, p);
+  p.Bp = reinterpret_cast<const u16*>(g.b_split);
+  const bool early = g_x3_variant != 1;
+  if (p.Bp) {  // the forward of a Linear layer: W pre-split once per call (split3_planes)
+    if (g.a_kmajor || g.b_kmajor || g.ldb % 8 || g.K % 8) abort();  // host contract, checked by callers
+    if (g.amask) hipLaunchKernelGGL((gemm_x3_kernel<false, false, true, true, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true>), grid, block, 0, stream, p);
+    return;
+  }
+  if (g.amask) {
+    if (early) {
+      X3_LAUNCH(true, true)
+    } else {
+      X3_LAUNCH(true, false)
+    }
   } else {
-    X3_LAUNCH(true)
+    if (early) {
+      X3_LAUNCH(false, true)
+    } else {
+      X3_LAUNCH(false, false)
+    }
   }
 #undef X3_LAUNCH
 }
 
 void gemm_f32x3_set_variant(int v) { g_x3_variant = v; }
+
+void split3_planes(const float* x, unsigned short* out, int64_t n, hipStream_t stream) {
+  if (n <= 0) return;
+  const int64_t blocks = (n / 4 + 255) / 256;
+  hipLaunchKernelGGL(split3_planes_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, out, n);
+}
+
+bool gemm_f32x3_can_presplit_b(const GemmArgs& g) {
+  return !g.a_kmajor && !g.b_kmajor && g.ldb % 8 == 0 && g.K % 8 == 0 && (size_t)g.N * g.ldb % 4 == 0;
+}
 
 }  // namespace sdml

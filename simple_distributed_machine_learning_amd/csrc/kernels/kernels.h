@@ -34,6 +34,9 @@ struct GemmArgs {
   bool a_kmajor = false, b_kmajor = false;
   int epi = EPI_STORE;
   int splits = 1;  // split-K factor (EPI_ATOMIC only)
+  // bf16x3 engine only: B already split into bf16 planes [3][N][ldb] (split3_planes of B);
+  // k-contiguous B, K % 8 == 0, ldb % 8 == 0 (gemm_f32x3_can_presplit_b)
+  const unsigned short* b_split = nullptr;
 };
 
 // returns false if the shape/alignment is not supported by the MFMA path
@@ -58,7 +61,12 @@ int gemm_f32_mode();
 bool gemm_f32x3_eligible(const GemmArgs& g);
 int gemm_f32x3_pick_splits(int M, int N, int K, bool a_kmajor);
 void gemm_f32x3(const GemmArgs& g, hipStream_t stream);
-void gemm_f32x3_set_variant(int v);  // 0: fresh per-K-step partials (default), 1: running accumulator
+// true iff gemm_f32 will run this shape on the bf16x3 engine
+bool gemm_f32_uses_x3(const GemmArgs& g);
+bool gemm_f32x3_can_presplit_b(const GemmArgs& g);
+// x[n] fp32 -> out[3][n] bf16 bits (hi, mid, lo; x == hi + mid + lo), n % 4 == 0, 16-B aligned
+void split3_planes(const float* x, unsigned short* out, int64_t n, hipStream_t stream);
+void gemm_f32x3_set_variant(int v);  // pipeline A/B: 0 = early split (default), 1 = split after MFMAs
 
 // ---- fused classifier head: z = x W^T + b; log_softmax; NLL; backward --------------------
 // x [M,K] fp32, W [C,K], b [C], target [M] int64. stats[0] += sum loss, stats[1] += #correct.

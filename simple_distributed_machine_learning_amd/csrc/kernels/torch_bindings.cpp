@@ -52,6 +52,14 @@ torch::Tensor linear_fwd_f32(torch::Tensor x, torch::Tensor w, c10::optional<tor
   g.epi = g.bias ? (relu ? sdml::EPI_BIAS_RELU : sdml::EPI_BIAS) : sdml::EPI_STORE;
   TORCH_CHECK(!relu || g.bias, "relu epilogue requires a bias in this kernel");
   TORCH_CHECK(sdml::gemm_f32_supported(g), "linear_fwd_f32: unsupported shape/alignment (K % 4 != 0?)");
+  torch::Tensor wsplit;
+  if (sdml::gemm_f32_uses_x3(g) && sdml::gemm_f32x3_can_presplit_b(g)) {
+    // the weight is shared by every row block: split it into bf16 planes once per call
+    wsplit = torch::empty({3, N, K}, x.options().dtype(torch::kInt16));
+    sdml::split3_planes(w.data_ptr<float>(), reinterpret_cast<unsigned short*>(wsplit.data_ptr<int16_t>()), N * K,
+                        cur_stream());
+    g.b_split = reinterpret_cast<const unsigned short*>(wsplit.data_ptr<int16_t>());
+  }
   sdml::gemm_f32(g, cur_stream());
   return y;
 }

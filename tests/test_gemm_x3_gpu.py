@@ -138,3 +138,16 @@ def test_linear_ops_route_to_x3_at_bench_shape():
     torch.testing.assert_close(gw, (gy.double().t() @ x.double()).float(), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(gb, gy.double().sum(0).float(), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(dx, (gy.double() @ w.double()).float(), rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("M,N", [(20000, 100), (4096, 128), (70000, 1024)])
+def test_linear_fwd_presplit_weight(M, N):
+    """x @ W^T with W pre-split into bf16 planes once per call (ragged row/column tiles)."""
+    Kd = 784 if N != 1024 else 1024
+    x, w, b = rnd(M, Kd, seed=23), rnd(N, Kd, seed=24) * 0.05, rnd(N, seed=25)
+    y = ops.linear_relu_fwd(x, w, b)
+    want = torch.relu(x.double() @ w.double().t() + b.double())
+    bound = Kd * 2.0 ** -24 * (x.abs().double() @ w.abs().double().t() + b.double().abs()) + 1e-30
+    assert ((y.double() - want).abs() <= bound).all()
+    y2 = ops.linear_fwd(x, w, b)
+    assert ((y2.double() - (x.double() @ w.double().t() + b.double())).abs() <= bound).all()

@@ -1,5 +1,6 @@
-"""Accuracy/speed probe of the bf16x3 fp32 GEMM engine variants (fresh per-K-step partials vs
-one running accumulator) against the exact fp32-input MFMA engine and fp64.
+"""Accuracy/speed probe of the bf16x3 fp32 GEMM engine pipeline variants (0: split of tile t+1
+interleaved with tile t's MFMAs, 1: split after the MFMAs) against the exact fp32-input MFMA
+engine and fp64.
 
     python tools/x3_probe.py
 """

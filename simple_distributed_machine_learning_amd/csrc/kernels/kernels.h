@@ -116,6 +116,15 @@ void layernorm_bwd_bf16_accum(const void* x, const void* w, const void* gy, cons
 int bias_grad_blocks(int M);
 void bias_grad_bf16(const void* gy, int M, int N, int ld, void* gb, float* workspace, hipStream_t stream);
 
+// ---- weight gradient of a bf16 Linear: gw[M,N] (bf16) += gy[T,M]^T x[T,N] -------------------
+// fp32 accumulation, token range split over workgroups, deterministic slab reduction.
+// workspace: wgrad_bf16_workspace_floats(M, N, T) fp32 (0 = none needed)
+bool wgrad_bf16_supported(int M, int N, int T, int lda, int ldb, int ldc);
+int wgrad_bf16_splits(int M, int N, int T);
+size_t wgrad_bf16_workspace_floats(int M, int N, int T);
+void wgrad_bf16(const void* gy, const void* x, void* gw, float* workspace, int M, int N, int T, int lda, int ldb,
+                int ldc, hipStream_t stream);
+
 // ---- causal flash attention, bf16, head_dim 64 ------------------------------------------
 // q/k/v (and dq/dk/dv) share one strided layout [b][h][s][64] (strides sqb, sqh, sqs; d
 // contiguous) — e.g. views into the fused c_attn output; o/dout share another (sob, soh, sos).

@@ -6,14 +6,16 @@ materialises each gradient and then launches an AccumulateGrad add (``grad += ne
 every weight and bias costs an extra full read and write per micro-batch. It also reduces
 the bias gradient with a generic reduction. This module avoids both:
 
-* dW: ``param.grad.addmm_(gy^T, x)``. The hipBLASLt GEMM accumulates in its epilogue
-  (beta = 1), so there is no temporary and no add kernel.
+* dW (bf16 on ROCm): ``wgrad_bf16_``, a hand-written MFMA GEMM (csrc/kernels/gemm_bf16_wgrad.hip)
+  that splits the token reduction over workgroups and adds the result into the bf16 gradient
+  in place. hipBLASLt runs these small-output / long-reduction shapes at 180-470 TF/s
+  (tools/bench_gpt2_gemms.py). Other dtypes: ``param.grad.addmm_(gy^T, x)`` (beta = 1).
 * db (bf16 on ROCm): ``bias_grad_bf16_``, a deterministic two-pass column sum that adds
   into the bf16 gradient in place (csrc/kernels/transformer.hip).
 
 When a parameter has no ``.grad`` yet (standalone use), the gradients are returned to
 autograd in the usual way. CPU tensors and non-bf16 dtypes keep the plain ``F.linear``
-path. The GEMMs themselves are plain library GEMMs (hipBLASLt), per the design rules.
+path. The GEMMs themselves are plain library GEMMs (hipBLASLt) for the forward and input gradient.
 """
 from __future__ import annotations
 
@@ -42,7 +44,9 @@ class _LinearFn(torch.autograd.Function):
         dx = (g2 @ w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
         gw = gb = None
         if ctx.needs_input_grad[1]:
-            if w.grad is not None:
+            if w.grad is not None and _wgrad_ok(g2, x2, w.grad):
+                kernels().wgrad_bf16_(g2, x2, w.grad)
+            elif w.grad is not None:
                 w.grad.addmm_(g2.t(), x2)
             else:
                 gw = g2.t() @ x2
@@ -52,6 +56,13 @@ class _LinearFn(torch.autograd.Function):
             else:
                 gb = g2.sum(0)
         return dx, gw, gb
+
+
+def _wgrad_ok(g2, x2, gw) -> bool:
+    return (g2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and gw.dtype == torch.bfloat16
+            and g2.stride(-1) == 1 and x2.stride(-1) == 1 and gw.is_contiguous()
+            and g2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0
+            and kernels().wgrad_bf16_supported(gw.shape[0], gw.shape[1], g2.shape[0]))
 
 
 def linear(x, w, b=None):

@@ -364,3 +364,21 @@ def test_layernorm_accumulates_into_grad():
     close(x.grad.float(), xr.grad, rtol=3e-2, atol=5e-2)
     close(ln.weight.grad.float(), 0.5 + wr.grad, rtol=2e-2, atol=2e-1)
     close(ln.bias.grad.float(), -0.5 + br.grad, rtol=2e-2, atol=2e-1)
+
+
+@pytest.mark.parametrize("T,M,N", [(16384, 3072, 768), (4096, 768, 768), (1000, 2304, 776), (64, 8, 16), (300, 520, 136)])
+def test_wgrad_bf16(T, M, N):
+    """gw (bf16) += gy^T x, split-token MFMA GEMM vs an fp64 reference of the same bf16 inputs."""
+    g = torch.Generator(device="cpu").manual_seed(T + M)
+    gy = torch.randn(T, M, generator=g).to(DEV, torch.bfloat16)
+    x = torch.randn(T, N, generator=g).to(DEV, torch.bfloat16)
+    gw0 = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    gw = gw0.clone()
+    K.wgrad_bf16_(gy, x, gw)
+    want = gw0.double() + gy.double().t() @ x.double()
+    scale = (gy.double().abs().t() @ x.double().abs()) + gw0.double().abs()
+    err = (gw.double() - want).abs()
+    assert (err <= 2 ** -7 * scale + 1e-6).all(), float((err / scale).max())
+    gw2 = gw0.clone()
+    K.wgrad_bf16_(gy, x, gw2)
+    assert torch.equal(gw, gw2)  # deterministic (fixed-order slab reduction, no atomics)

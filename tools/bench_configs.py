@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--dtype", default=None, choices=[None, "fp32", "bf16"], help="resnet18: compute dtype")
     a = ap.parse_args()
     kind, M, B, S = DEFAULTS[a.config]
+    world0 = int(os.environ.get("WORLD_SIZE", "1"))
+    if world0 == 1 and a.config == "gpt2":
+        M = 1  # all stages local: micro-batching only shrinks the GEMMs (614K vs 438K tokens/s at M=4)
     M = a.microbatches or M
     B = a.batch or B
     S = a.seq_len or S

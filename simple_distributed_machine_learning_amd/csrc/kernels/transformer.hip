@@ -495,8 +495,11 @@ void cross_entropy_bf16(const void* logits, const int64_t* target, int rows, int
 }
 
 int layernorm_bwd_blocks(int rows) {
+  // one wave per row in flight: 1024 blocks x 4 waves = 16 waves per CU keep enough loads in
+  // flight (256 blocks left 4 waves per CU latency-bound: 43 us -> see profiles/); the dW/dB
+  // slabs this adds (blocks x 2D fp32) are summed by one extra 6 MB pass
   int b = (rows + 3) / 4;
-  return b > 256 ? 256 : (b < 1 ? 1 : b);
+  return b > 1024 ? 1024 : (b < 1 ? 1 : b);
 }
 
 void layernorm_fwd_bf16(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int rows,

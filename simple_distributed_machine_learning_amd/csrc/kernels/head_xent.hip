@@ -38,10 +38,13 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
                                                           float* __restrict__ part, float* __restrict__ dx,
                                                           int chunks_per_block, int mask_dx) {
   constexpr int RWS = HTHR / TPR;  // rows per chunk
-  __shared__ __attribute__((aligned(16))) float xs[RWS * XP];
+  // x chunk; reused at the end for the dW partial reduction ([4 waves][C * HK])
+  constexpr int XS = RWS * XP > (HTHR / 64) * C * HK ? RWS * XP : (HTHR / 64) * C * HK;
+  __shared__ __attribute__((aligned(16))) float xs[XS];
   __shared__ __attribute__((aligned(16))) float ws[C * HK];
   __shared__ float bs[CMAX];
-  __shared__ float dzs[RWS * C];
+  constexpr int DZP = (C + 3) / 4 * 4;  // dz row pitch (16-B aligned rows for b128 broadcasts)
+  __shared__ __attribute__((aligned(16))) float dzs[RWS * DZP];
   __shared__ float red[2 * HTHR / 64];
   const int t = threadIdx.x;
   const bool train = dx != nullptr;
@@ -49,10 +52,14 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
     reinterpret_cast<f32x4*>(ws)[i] = reinterpret_cast<const f32x4*>(W)[i];
   if (t < C) bs[t] = bias[t];
 
-  constexpr int NOUT = (C * HK + HTHR - 1) / HTHR;  // dW outputs per thread
-  float gacc[NOUT];
+  constexpr int NOUT = (C * HK + HTHR - 1) / HTHR;  // dW outputs per thread (slab write)
+  // dW partial: thread owns k = 4*kq .. 4*kq+3 for every class c, over rows rq, rq+RG, ...
+  // of each chunk (one float4 of x and one broadcast dz row per row: 40 FMAs per 4 LDS reads)
+  constexpr int RG = HTHR / (HK / 4);  // row groups (8)
+  const int kq = t % (HK / 4), rq = t / (HK / 4);
+  f32x4 gacc[C];
 #pragma unroll
-  for (int o = 0; o < NOUT; ++o) gacc[o] = 0.f;
+  for (int c = 0; c < C; ++c) gacc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
   float gbacc = 0.f;
   float loss_acc = 0.f, corr_acc = 0.f;
 
@@ -122,7 +129,7 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
       }
       if (q == 0) {
 #pragma unroll
-        for (int c = 0; c < C; ++c) dzs[row_in * C + c] = dz[c];
+        for (int c = 0; c < C; ++c) dzs[row_in * DZP + c] = dz[c];
       }
       if (valid) {
 #pragma unroll
@@ -145,21 +152,24 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
         }
       }
       __syncthreads();  // dzs complete
-      // dW partial: output o = t + HTHR*u -> (c = o / HK, k = o % HK), sum over chunk rows
+#pragma unroll 2
+      for (int r = rq; r < RWS; r += RG) {
+        const f32x4 xv = *reinterpret_cast<const f32x4*>(xs + r * XP + 4 * kq);
+        float d[DZP];
 #pragma unroll
-      for (int u = 0; u < NOUT; ++u) {
-        const int o = t + HTHR * u;
-        if (o < C * HK) {
-          const int c = o / HK, k = o % HK;
-          float s = 0.f;
-#pragma unroll 8
-          for (int r = 0; r < RWS; ++r) s += dzs[r * C + c] * xs[r * XP + k];
-          gacc[u] += s;
+        for (int c4 = 0; c4 < DZP / 4; ++c4) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(dzs + r * DZP + 4 * c4);
+          d[4 * c4] = v[0];
+          d[4 * c4 + 1] = v[1];
+          d[4 * c4 + 2] = v[2];
+          d[4 * c4 + 3] = v[3];
         }
+#pragma unroll
+        for (int c = 0; c < C; ++c) gacc[c] += d[c] * xv;
       }
       if (t < C) {
         float s = 0.f;
-        for (int r = 0; r < RWS; ++r) s += dzs[r * C + t];
+        for (int r = 0; r < RWS; ++r) s += dzs[r * DZP + t];
         gbacc += s;
       }
     }
@@ -168,10 +178,25 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
   // 1.3K addresses serialises at the memory side; a slab + one reduce pass does not) ----
   float* slab = part + (size_t)blockIdx.x * (C * HK + C + 2);
   if (train) {
+    // row groups rq and rq^1 are lanes l and l^32 of one wave; the 4 waves meet in LDS (the x
+    // chunk buffer is free now) in wave order
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gacc[c][e] += __shfl_xor(gacc[c][e], 32);
+    static_assert(RG == 8 && HTHR == 256, "dW partial reduction assumes 8 row groups in 4 waves");
+    __syncthreads();  // everyone done reading xs
+    float* red4 = xs;  // [4 waves][C * HK]
+    if ((t & 63) < 32) {
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        *reinterpret_cast<f32x4*>(red4 + (t >> 6) * C * HK + c * HK + 4 * kq) = gacc[c];
+    }
+    __syncthreads();
 #pragma unroll
     for (int u = 0; u < NOUT; ++u) {
       const int o = t + HTHR * u;
-      if (o < C * HK) slab[o] = gacc[u];
+      if (o < C * HK) slab[o] = (red4[o] + red4[C * HK + o]) + (red4[2 * C * HK + o] + red4[3 * C * HK + o]);
     }
     if (t < C) slab[C * HK + t] = gbacc;
   }

@@ -42,8 +42,10 @@ def main():
     a = ap.parse_args()
     kind, M, B, S = DEFAULTS[a.config]
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
-    if world0 == 1 and a.config == "gpt2":
-        M = 1  # all stages local: micro-batching only shrinks the GEMMs (614K vs 438K tokens/s at M=4)
+    if world0 == 1 and a.config in ("gpt2", "resnet18"):
+        # all stages local: micro-batching only shrinks the GEMMs / convolutions
+        # (measured: GPT-2 614K vs 438K tokens/s at M=4; ResNet-18 27.2K vs 15.6K samples/s at M=8)
+        M = 1
     M = a.microbatches or M
     B = a.batch or B
     S = a.seq_len or S

@@ -1,0 +1,52 @@
+"""Summaries of rocprofv3 output for profiles/ (kernel stats -> per-step table; PMC -> per-kernel
+averages with derived utilisations).
+
+    python tools/summarize_profile.py stats <kernel_stats.csv> <steps>
+    python tools/summarize_profile.py pmc <counter_collection.csv> [more.csv ...]
+"""
+import collections
+import csv
+import sys
+
+
+def stats(path, steps):
+    rows = list(csv.DictReader(open(path)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    print(f"kernel time per step: {tot / 1e6 / steps:.3f} ms over {steps} steps (incl. warm-up/setup kernels)")
+    print(f"{'ms/step':>8} {'calls/step':>10} {'avg us':>9} {'%':>6}  kernel")
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:30]:
+        t = float(r["TotalDurationNs"])
+        print(f"{t / 1e6 / steps:8.3f} {int(r['Calls']) / steps:10.1f} {float(r['AverageNs']) / 1e3:9.1f} "
+              f"{100 * t / tot:6.2f}  {r['Name'][:120]}")
+
+
+def pmc(paths):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    dur = collections.defaultdict(list)
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            n = r["Kernel_Name"]
+            if "sdml" not in n:
+                continue
+            key = n.replace("sdml::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+            agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            dur[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    for k, d in agg.items():
+        m = {c: sum(v) / len(v) for c, v in d.items()}
+        print(f"== {k}  (dispatch {sorted(dur[k])[len(dur[k]) // 2]:.1f} us median, profiled)")
+        for c in sorted(m):
+            print(f"   {c:28s} {m[c]:.4g}")
+        wc = m.get("SQ_WAVE_CYCLES")
+        if wc:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if c in m:
+                    print(f"   {c + ' / WAVE_CYCLES':28s} {100 * m[c] / wc:.1f} %")
+        if "FETCH_SIZE" in m:
+            print(f"   {'HBM bytes read (2 x FETCH_SIZE KB)':28s} {2 * m['FETCH_SIZE'] / 1e3:.1f} MB")
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2], int(sys.argv[3]))
+    else:
+        pmc(sys.argv[2:])

@@ -13,6 +13,8 @@
 // The token range is split over workgroups until the grid covers the chip; each split writes
 // an fp32 slab and a second pass adds the slabs, in a fixed order, to the bf16 gradient
 // (deterministic: no float atomics). With one split the block adds its tile directly.
+// The bias gradient (column sums of gy) is fused: the first column tile's blocks sum the gy tile
+// they stage anyway, so the separate bias reduction pass over gy disappears.
 // Replaces the autograd weight gradient of the GPT-2 stages' projections (ops/linear.py).
 #include <hip/hip_runtime.h>
 
@@ -37,7 +39,8 @@ struct WgParams {
   const u16* A;  // gy [T][lda]
   const u16* B;  // x  [T][ldb]
   u16* C;        // gW [M][ldc] (bf16, accumulated)
-  float* slab;   // [splits][M][N] fp32 (splits > 1)
+  u16* gb;       // bias gradient [M] (bf16, accumulated) or nullptr: column sums of gy
+  float* slab;   // [splits][M][N] fp32, then [splits][M] bias partials (splits > 1)
   int M, N, T, lda, ldb, ldc;
   int tps;  // tokens per split (multiple of BK)
   int tiles_m, tiles_n, splits;
@@ -81,13 +84,21 @@ struct KmTile {
       v[u] = *reinterpret_cast<const u16x8*>(P + (size_t)k * ld + c);
     }
   }
-  __device__ __forceinline__ void store(u16* L, int k0, int kend) const {
+  // ROWSUM: colsum[e] += the 8 staged values of this thread's column chunk (every u of a
+  // thread has the same chunk index: NT is a multiple of CPR), k >= kend excluded
+  template <bool ROWSUM>
+  __device__ __forceinline__ void store(u16* L, int k0, int kend, float (&colsum)[8]) const {
     const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
       const int id = threadIdx.x + NT * u;
       const int k = id / CPR, ch = id % CPR;
-      *reinterpret_cast<u16x8*>(L + (ch >> 4) * IMG + km_off(k, ch & 15)) = (k0 + k < kend) ? v[u] : z;
+      const u16x8 val = (k0 + k < kend) ? v[u] : z;
+      *reinterpret_cast<u16x8*>(L + (ch >> 4) * IMG + km_off(k, ch & 15)) = val;
+      if constexpr (ROWSUM) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) colsum[e] += bf2f(val[e]);
+      }
     }
   }
 };
@@ -96,6 +107,8 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// BIAS: the tn == 0 blocks also reduce the staged gy tile over tokens (the bias gradient)
+template <bool BIAS>
 __global__ void __launch_bounds__(NT) wgrad_kernel(WgParams p) {
   constexpr int BUF = 3 * IMG;  // A: two 128-col images, B: one
   __shared__ __attribute__((aligned(16))) u16 smem[2 * BUF];
@@ -127,12 +140,16 @@ __global__ void __launch_bounds__(NT) wgrad_kernel(WgParams p) {
 
   KmTile<BM> ta;
   KmTile<BN> tb;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // bias partials (BIAS, tn == 0)
+  float dummy[8];
+  const bool do_bias = BIAS && tn == 0;
   const int nk = (kend - kbeg + BK - 1) / BK;
   if (nk > 0) {
     ta.load(p.A, p.lda, p.M, m0, kbeg, p.T);
     tb.load(p.B, p.ldb, p.N, n0, kbeg, p.T);
-    ta.store(smem, kbeg, kend);
-    tb.store(smem + 2 * IMG, kbeg, kend);
+    if (do_bias) ta.template store<true>(smem, kbeg, kend, cs);
+    else ta.template store<false>(smem, kbeg, kend, dummy);
+    tb.template store<false>(smem + 2 * IMG, kbeg, kend, dummy);
     ta.load(p.A, p.lda, p.M, m0, kbeg + BK, p.T);
     tb.load(p.B, p.ldb, p.N, n0, kbeg + BK, p.T);
   }
@@ -149,8 +166,9 @@ __global__ void __launch_bounds__(NT) wgrad_kernel(WgParams p) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) b[j] = trfrag(L + 2 * IMG, wn * 64 + 32 * j, s, lane);
       if (s == 0) {  // tile t+1 (registers) -> the other buffer; tile t+2 -> registers
-        ta.store(Ln, kbeg + (t + 1) * BK, kend);
-        tb.store(Ln + 2 * IMG, kbeg + (t + 1) * BK, kend);
+        if (do_bias) ta.template store<true>(Ln, kbeg + (t + 1) * BK, kend, cs);
+        else ta.template store<false>(Ln, kbeg + (t + 1) * BK, kend, dummy);
+        tb.template store<false>(Ln + 2 * IMG, kbeg + (t + 1) * BK, kend, dummy);
         ta.load(p.A, p.lda, p.M, m0, kbeg + (t + 2) * BK, p.T);
         tb.load(p.B, p.ldb, p.N, n0, kbeg + (t + 2) * BK, p.T);
       }
@@ -160,6 +178,25 @@ __global__ void __launch_bounds__(NT) wgrad_kernel(WgParams p) {
         for (int j = 0; j < 2; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
     }
     __syncthreads();
+  }
+
+  if (do_bias) {
+    // the 16 threads t, t+32, ..., t+480 own the same 8 columns m0 + 8*(t&31) + e: meet in LDS
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [16][256]
+    const int ch = threadIdx.x & 31, part = threadIdx.x >> 5;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[part * 256 + 8 * ch + e] = cs[e];
+    __syncthreads();
+    if (threadIdx.x < BM) {
+      float sum = 0.f;
+      for (int q = 0; q < 16; ++q) sum += red[q * 256 + threadIdx.x];
+      const int m = m0 + threadIdx.x;
+      if (m < p.M) {
+        if (p.splits == 1) p.gb[m] = f2bf(bf2f(p.gb[m]) + sum);
+        else p.slab[(size_t)p.splits * p.M * p.N + (size_t)split * p.M + m] = sum;
+      }
+    }
   }
 
   // epilogue: C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
@@ -184,11 +221,20 @@ __global__ void __launch_bounds__(NT) wgrad_kernel(WgParams p) {
     }
 }
 
-// C[m][n] (bf16) += sum_s slab[s][m][n], fixed order; 4 elements per thread (N % 4 == 0)
+// C[m][n] (bf16) += sum_s slab[s][m][n], fixed order; 4 elements per thread (N % 4 == 0);
+// gb[m] += sum_s bias_slab[s][m] when gb is given
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N,
-                                                           u16* __restrict__ C, int ldc) {
+                                                           u16* __restrict__ C, int ldc, u16* __restrict__ gb) {
   const int64_t n4 = (int64_t)M * N / 4;
   const int64_t MN = (int64_t)M * N;
+  if (gb) {
+    const float* bs = slab + (size_t)splits * MN;
+    for (int64_t m = blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
+      float s = 0.f;
+      for (int k = 0; k < splits; ++k) s += bs[(size_t)k * M + m];
+      gb[m] = f2bf(bf2f(gb[m]) + s);
+    }
+  }
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     f32x4 s = *reinterpret_cast<const f32x4*>(slab + 4 * i);
     for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(slab + k * MN + 4 * i);
@@ -217,15 +263,16 @@ int wgrad_bf16_splits(int M, int N, int T) {
 
 size_t wgrad_bf16_workspace_floats(int M, int N, int T) {
   const int s = wgrad_bf16_splits(M, N, T);
-  return s > 1 ? (size_t)s * M * N : 0;
+  return s > 1 ? (size_t)s * M * N + (size_t)s * M : 0;
 }
 
-void wgrad_bf16(const void* gy, const void* x, void* gw, float* workspace, int M, int N, int T, int lda, int ldb,
-                int ldc, hipStream_t stream) {
+void wgrad_bf16(const void* gy, const void* x, void* gw, void* gb, float* workspace, int M, int N, int T, int lda,
+                int ldb, int ldc, hipStream_t stream) {
   WgParams p;
   p.A = static_cast<const u16*>(gy);
   p.B = static_cast<const u16*>(x);
   p.C = static_cast<u16*>(gw);
+  p.gb = static_cast<u16*>(gb);
   p.slab = workspace;
   p.M = M;
   p.N = N;
@@ -241,12 +288,13 @@ void wgrad_bf16(const void* gy, const void* x, void* gw, float* workspace, int M
   p.splits = s;
   p.tiles_m = (M + BM - 1) / BM;
   p.tiles_n = (N + BN - 1) / BN;
-  hipLaunchKernelGGL(wgrad_kernel, dim3(p.tiles_m * p.tiles_n * s), dim3(NT), 0, stream, p);
+  if (gb) hipLaunchKernelGGL(wgrad_kernel<true>, dim3(p.tiles_m * p.tiles_n * s), dim3(NT), 0, stream, p);
+  else hipLaunchKernelGGL(wgrad_kernel<false>, dim3(p.tiles_m * p.tiles_n * s), dim3(NT), 0, stream, p);
   if (s > 1) {
     const int64_t n4 = (int64_t)M * N / 4;
     const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, workspace, s, M, N,
-                       static_cast<u16*>(gw), ldc);
+                       static_cast<u16*>(gw), ldc, static_cast<u16*>(gb));
   }
 }
 

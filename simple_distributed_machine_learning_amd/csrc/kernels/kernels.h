@@ -122,8 +122,9 @@ void bias_grad_bf16(const void* gy, int M, int N, int ld, void* gb, float* works
 bool wgrad_bf16_supported(int M, int N, int T, int lda, int ldb, int ldc);
 int wgrad_bf16_splits(int M, int N, int T);
 size_t wgrad_bf16_workspace_floats(int M, int N, int T);
-void wgrad_bf16(const void* gy, const void* x, void* gw, float* workspace, int M, int N, int T, int lda, int ldb,
-                int ldc, hipStream_t stream);
+// gb (optional, bf16 [M]) += column sums of gy (the bias gradient), fused
+void wgrad_bf16(const void* gy, const void* x, void* gw, void* gb, float* workspace, int M, int N, int T, int lda,
+                int ldb, int ldc, hipStream_t stream);
 
 // ---- causal flash attention, bf16, head_dim 64 ------------------------------------------
 // q/k/v (and dq/dk/dv) share one strided layout [b][h][s][64] (strides sqb, sqh, sqs; d

@@ -223,7 +223,7 @@ void gemm_f32x3_op(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool a_kma
 }
 
 // gw (bf16 [M, N], in place) += gy[T, M]^T @ x[T, N] (bf16), hand-written MFMA split-token GEMM
-void wgrad_bf16_(torch::Tensor gy, torch::Tensor x, torch::Tensor gw) {
+void wgrad_bf16_(torch::Tensor gy, torch::Tensor x, torch::Tensor gw, c10::optional<torch::Tensor> gb) {
   for (auto* t : {&gy, &x, &gw}) {
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kBFloat16, "wgrad_bf16_: bf16 ROCm tensors expected");
     TORCH_CHECK(t->dim() == 2 && t->stride(1) == 1, "wgrad_bf16_: 2-D row-major operands expected");
@@ -232,11 +232,17 @@ void wgrad_bf16_(torch::Tensor gy, torch::Tensor x, torch::Tensor gw) {
   TORCH_CHECK(x.size(0) == T && gw.size(0) == M && gw.size(1) == N, "wgrad_bf16_: shape mismatch");
   TORCH_CHECK(sdml::wgrad_bf16_supported(M, N, T, gy.stride(0), x.stride(0), gw.stride(0)),
               "wgrad_bf16_: unsupported shape/alignment");
+  void* gbp = nullptr;
+  if (gb.has_value() && gb->defined()) {
+    TORCH_CHECK(gb->is_cuda() && gb->scalar_type() == torch::kBFloat16 && gb->is_contiguous() && gb->numel() == M,
+                "wgrad_bf16_: gb must be a contiguous bf16 [M] tensor");
+    gbp = gb->data_ptr();
+  }
   if (T == 0) return;
   const size_t ws = sdml::wgrad_bf16_workspace_floats(M, N, T);
   torch::Tensor w;
   if (ws) w = torch::empty({(int64_t)ws}, gy.options().dtype(torch::kFloat32));
-  sdml::wgrad_bf16(gy.data_ptr(), x.data_ptr(), gw.data_ptr(), ws ? w.data_ptr<float>() : nullptr, M, N, T,
+  sdml::wgrad_bf16(gy.data_ptr(), x.data_ptr(), gw.data_ptr(), gbp, ws ? w.data_ptr<float>() : nullptr, M, N, T,
                    gy.stride(0), x.stride(0), gw.stride(0), cur_stream());
 }
 
@@ -643,7 +649,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("C"), py::arg("a_kmajor"), py::arg("b_kmajor"), py::arg("epi") = 0, py::arg("bias") = py::none(),
         py::arg("rowsum") = py::none(), py::arg("amask") = py::none(), py::arg("cmask") = py::none());
   m.def("gemm_f32x3_set_variant", &sdml::gemm_f32x3_set_variant, "x3 engine accumulation variant (A/B)");
-  m.def("wgrad_bf16_", &wgrad_bf16_, "gw += gy^T x (bf16 Linear weight gradient, MFMA split-token GEMM)");
+  m.def("wgrad_bf16_", &wgrad_bf16_, "gw += gy^T x, gb += colsum(gy) (bf16 Linear weight/bias gradient)",
+        py::arg("gy"), py::arg("x"), py::arg("gw"), py::arg("gb") = py::none());
   m.def("wgrad_bf16_supported", &wgrad_bf16_supported_op, "shape check for wgrad_bf16_ (contiguous operands)");
   m.def("gemm_f32_set_mode", &sdml::gemm_f32_set_mode, "fp32 GEMM engine: 1 = bf16x3 split (default), 0 = fp32 MFMA");
   m.def("gemm_f32_mode", &sdml::gemm_f32_mode, "current fp32 GEMM engine");

@@ -10,8 +10,9 @@ the bias gradient with a generic reduction. This module avoids both:
   that splits the token reduction over workgroups and adds the result into the bf16 gradient
   in place. hipBLASLt runs these small-output / long-reduction shapes at 180-470 TF/s
   (tools/bench_gpt2_gemms.py). Other dtypes: ``param.grad.addmm_(gy^T, x)`` (beta = 1).
-* db (bf16 on ROCm): ``bias_grad_bf16_``, a deterministic two-pass column sum that adds
-  into the bf16 gradient in place (csrc/kernels/transformer.hip).
+* db (bf16 on ROCm): fused into ``wgrad_bf16_`` (the weight-gradient GEMM already stages every
+  gy tile; its first column tile sums them); otherwise ``bias_grad_bf16_``, a deterministic
+  two-pass column sum that adds into the bf16 gradient in place (csrc/kernels/transformer.hip).
 
 When a parameter has no ``.grad`` yet (standalone use), the gradients are returned to
 autograd in the usual way. CPU tensors and non-bf16 dtypes keep the plain ``F.linear``
@@ -43,14 +44,18 @@ class _LinearFn(torch.autograd.Function):
         g2 = gy.reshape(-1, gy.shape[-1])
         dx = (g2 @ w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
         gw = gb = None
+        bias_done = False
         if ctx.needs_input_grad[1]:
             if w.grad is not None and _wgrad_ok(g2, x2, w.grad):
-                kernels().wgrad_bf16_(g2, x2, w.grad)
+                fuse_b = (b is not None and ctx.needs_input_grad[2] and b.grad is not None
+                          and b.grad.is_contiguous() and b.grad.dtype == torch.bfloat16)
+                kernels().wgrad_bf16_(g2, x2, w.grad, b.grad if fuse_b else None)
+                bias_done = fuse_b
             elif w.grad is not None:
                 w.grad.addmm_(g2.t(), x2)
             else:
                 gw = g2.t() @ x2
-        if b is not None and ctx.needs_input_grad[2]:
+        if b is not None and ctx.needs_input_grad[2] and not bias_done:
             if b.grad is not None and b.grad.is_contiguous() and g2.stride(-1) == 1:
                 kernels().bias_grad_bf16_(g2, b.grad)
             else:

@@ -382,3 +382,11 @@ def test_wgrad_bf16(T, M, N):
     gw2 = gw0.clone()
     K.wgrad_bf16_(gy, x, gw2)
     assert torch.equal(gw, gw2)  # deterministic (fixed-order slab reduction, no atomics)
+    # fused bias gradient: gb += column sums of gy
+    gb0 = torch.randn(M, generator=g).to(DEV, torch.bfloat16)
+    gw3, gb = gw0.clone(), gb0.clone()
+    K.wgrad_bf16_(gy, x, gw3, gb)
+    assert torch.equal(gw3, gw)
+    want_b = gb0.double() + gy.double().sum(0)
+    scale_b = gy.double().abs().sum(0) + gb0.double().abs()
+    assert ((gb.double() - want_b).abs() <= 2 ** -7 * scale_b + 1e-6).all()

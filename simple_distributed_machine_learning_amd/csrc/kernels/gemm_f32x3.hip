@@ -4,8 +4,8 @@
 //   a*b ~= hi*hi + (hi*mid + mid*hi) + (hi*lo + lo*hi + mid*mid),
 // each term an exact bf16 x bf16 product accumulated in fp32 by v_mfma_f32_32x32x16_bf16.
 // The dropped terms (mid*lo, lo*mid, lo*lo) are below 2^-24 |a*b|: the result has fp32
-// accuracy (tests/test_kernels_gpu.py compares its error against an fp64 reference with the
-// error of the exact-fp32 v_mfma_f32_32x32x2_f32 path), at 6 bf16 MFMAs per fp32 product:
+// accuracy (compared against an fp64 reference together with the
+// error of the exact-fp32 v_mfma_f32_32x32x2_f32 path; tests/test_gemm_x3_gpu.py), at 6 bf16 MFMAs per fp32 product:
 // bf16 MFMA runs 16x the fp32-input MFMA rate on gfx950, so this is 2.67x the fp32 matrix
 // peak and turns the MLP GEMMs (K = 784, 128-wide) from MFMA-bound into HBM-bound.
 //
@@ -16,6 +16,8 @@
 // Geometry (gfx950, wave64): 512 threads = 8 waves, K-step 32, one workgroup per CU.
 //   A k-contiguous: block tile 256 x 128, waves 4 x 2, 64 x 64 per wave (2 x 2 MFMA tiles)
 //   A k-major     : block tile 128 x 128, waves 2 x 4, 64 x 32 per wave (2 x 1 MFMA tiles)
+//   (a 128 x 256 tile for the weight gradient, B = X widened to 256 columns, measured slower:
+//    784 columns -> 4 tiles with 31 % padding; 250 vs 217 us at the headline shape)
 // LDS holds each operand as three bf16 planes (hi/mid/lo), double-buffered: 144 KiB / 96 KiB.
 //   * k-contiguous operand: image [rows][32 k], 64-B rows, 16-B chunk c of row r stored at
 //     chunk c ^ ((r >> 2) & 3): the ds_read_b128 fragment reads (8 consecutive k of one row per

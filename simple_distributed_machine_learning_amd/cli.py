@@ -47,6 +47,8 @@ def add_engine_args(parser: argparse.ArgumentParser):
     g.add_argument("--stages", type=int, default=None, help="pipeline stages (default per model)")
     g.add_argument("--pp", type=int, default=None,
                    help="ranks per pipeline (default: min(stages, world_size); chimera: 2)")
+    g.add_argument("--tp", type=int, default=1,
+                   help="tensor-parallel ranks per stage (GPT-2 models; gpipe/1f1b schedules)")
     g.add_argument("--schedule", default="1f1b", choices=["gpipe", "1f1b", "chimera", "rotate"])
     g.add_argument("--microbatches", type=int, default=1)
     g.add_argument("--batch_size", type=int, default=60, help="per-replica batch (reference: 60)")

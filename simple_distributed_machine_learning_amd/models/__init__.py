@@ -26,7 +26,8 @@ def get_model_spec(name: str, num_stages: int = None, **kw) -> ModelSpec:
         return gpt2_spec(n, seq_len=kw.get("seq_len"))
     if name == "gpt2_tiny":  # test-sized transformer with the same code path
         cfg = GPT2Config(n_layer=2 * n, n_head=2, n_embd=32, vocab_size=97, block_size=32)
-        return gpt2_spec(n, cfg=cfg, seq_len=kw.get("seq_len", 16), dtype=kw.get("dtype", None) or __import__("torch").float32)
+        return gpt2_spec(n, cfg=cfg, seq_len=kw.get("seq_len") or 16,
+                         dtype=kw.get("dtype", None) or __import__("torch").float32, name="gpt2_tiny")
     raise ValueError(f"unknown model {name!r}; choose from {MODELS}")
 
 

@@ -105,6 +105,8 @@ class ModelSpec:
     boundary_dtype: torch.dtype = torch.float32
     input_kind: str = "image"   # image | tokens
     param_dtype: torch.dtype = torch.float32
+    vocab_size: int = 0         # token models: vocabulary size
+    seq_len: int = 0            # token models: sequence length of the boundary tensors
 
 
 def stage_seed(base_seed: int, stage: int) -> int:

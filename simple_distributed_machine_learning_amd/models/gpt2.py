@@ -22,8 +22,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .base import ModelSpec, PipelineStage
-from ..ops.linear import Linear
+from ..ops.linear import Linear, linear
 from ..ops.transformer import LayerNorm, causal_attention, cross_entropy_sum
+from ..parallel.tp import TPContext, column_slice, copy_to_tp, reduce_from_tp, shard_parameter
 
 
 @dataclass
@@ -42,10 +43,26 @@ class CausalSelfAttention(nn.Module):
         self.c_attn = Linear(cfg.n_embd, 3 * cfg.n_embd)
         self.c_proj = Linear(cfg.n_embd, cfg.n_embd)
         self.n_head = cfg.n_head
+        self.tp: TPContext = None
+
+    def shard_tp(self, tp: TPContext):
+        """Keep this rank's heads: the q/k/v columns of c_attn (column-parallel) and the matching
+        input features of c_proj (row-parallel; its bias stays whole, added after the reduce)."""
+        C = self.c_proj.weight.shape[0]
+        cols = column_slice(C, tp)
+        idx = torch.cat([torch.arange(cols.start, cols.stop) + i * C for i in range(3)])
+        shard_parameter(self.c_attn, "weight", 0, idx)
+        shard_parameter(self.c_attn, "bias", 0, idx)
+        shard_parameter(self.c_proj, "weight", 1, cols)
+        self.n_head //= tp.size
+        self.tp = tp
 
     def forward(self, x):
         # HIP flash attention (bf16, head_dim 64) on ROCm; PyTorch SDPA elsewhere
-        return self.c_proj(causal_attention(self.c_attn(x), self.n_head))
+        if self.tp is None:
+            return self.c_proj(causal_attention(self.c_attn(x), self.n_head))
+        a = causal_attention(self.c_attn(copy_to_tp(x, self.tp)), self.n_head)
+        return reduce_from_tp(linear(a, self.c_proj.weight), self.tp) + self.c_proj.bias
 
 
 class MLP(nn.Module):
@@ -53,9 +70,20 @@ class MLP(nn.Module):
         super().__init__()
         self.c_fc = Linear(cfg.n_embd, 4 * cfg.n_embd)
         self.c_proj = Linear(4 * cfg.n_embd, cfg.n_embd)
+        self.tp: TPContext = None
+
+    def shard_tp(self, tp: TPContext):
+        cols = column_slice(self.c_fc.weight.shape[0], tp)
+        shard_parameter(self.c_fc, "weight", 0, cols)
+        shard_parameter(self.c_fc, "bias", 0, cols)
+        shard_parameter(self.c_proj, "weight", 1, cols)
+        self.tp = tp
 
     def forward(self, x):
-        return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
+        if self.tp is None:
+            return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
+        h = F.gelu(self.c_fc(copy_to_tp(x, self.tp)), approximate="tanh")
+        return reduce_from_tp(linear(h, self.c_proj.weight), self.tp) + self.c_proj.bias
 
 
 class Block(nn.Module):
@@ -88,6 +116,18 @@ class GPT2Stage(PipelineStage):
             self.ln_f = LayerNorm(cfg.n_embd)
             self.lm_head = Linear(cfg.n_embd, cfg.vocab_size, bias=False)
         self._init()
+
+    supports_tp = True
+
+    def shard_tp(self, tp: TPContext):
+        """Tensor-parallel split of every block (parallel/tp.py); embeddings, LayerNorms and the
+        vocabulary head stay replicated."""
+        if self.cfg.n_head % tp.size:
+            raise ValueError(f"n_head={self.cfg.n_head} is not divisible by tp={tp.size}")
+        for blk in self.h.values():
+            blk.attn.shard_tp(tp)
+            blk.mlp.shard_tp(tp)
+        self.tp = tp
 
     def _init(self):
         for name, p in self.named_parameters():
@@ -131,9 +171,10 @@ class GPT2Stage(PipelineStage):
         return x
 
 
-def gpt2_spec(num_stages: int = 2, cfg: GPT2Config = None, seq_len: int = None, dtype=torch.bfloat16) -> ModelSpec:
+def gpt2_spec(num_stages: int = 2, cfg: GPT2Config = None, seq_len: int = None, dtype=torch.bfloat16,
+              name: str = "gpt2") -> ModelSpec:
     cfg = cfg or GPT2Config()
-    S = seq_len or cfg.block_size
+    S = min(seq_len or cfg.block_size, cfg.block_size)
 
     def build(s):
         return GPT2Stage(cfg, s, num_stages)
@@ -141,5 +182,6 @@ def gpt2_spec(num_stages: int = 2, cfg: GPT2Config = None, seq_len: int = None, 
     def shape(s, mb):
         return (mb, S, cfg.n_embd)
 
-    return ModelSpec(name="gpt2", num_stages=num_stages, build_stage=build, boundary_shape=shape,
-                     boundary_dtype=dtype, input_kind="tokens", param_dtype=dtype)
+    return ModelSpec(name=name, num_stages=num_stages, build_stage=build, boundary_shape=shape,
+                     boundary_dtype=dtype, input_kind="tokens", param_dtype=dtype, vocab_size=cfg.vocab_size,
+                     seq_len=S)

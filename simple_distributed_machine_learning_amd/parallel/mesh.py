@@ -5,9 +5,11 @@ Replaces the reference's RPC bootstrap (``rpc.init_rpc`` / ``rpc.shutdown``,
 modules, every rank joins ONE ``torch.distributed`` process group (RCCL — PyTorch-ROCm's
 ``"nccl"`` backend — on MI355X, Gloo on the CPU test path) and runs the same SPMD program.
 
-Rank layout: ``rank = dp_rank * pp + pp_rank`` — the ranks of one pipeline are adjacent,
-so on an 8-GPU node the stage pairs (0,1), (2,3), ... each talk over their own direct xGMI
-link and DP replicas of a stage all-reduce over the other links.
+Rank layout: ``rank = (dp_rank * pp + pp_rank) * tp + tp_rank`` — the tensor-parallel ranks of
+a stage (parallel/tp.py) are adjacent, then the stages of one pipeline, then the replicas. On an
+8-GPU node the stage pairs (0,1), (2,3), ... (tp = 1) each talk over their own direct xGMI link
+and DP replicas of a stage all-reduce over the other links. A pipeline's stage-to-stage
+messages go between ranks with the same ``tp_rank``.
 
 Point-to-point traffic uses one 2-rank process group per *ordered* neighbour pair
 (direction). Each group owns its own RCCL communicator and HIP stream, so every
@@ -44,15 +46,24 @@ class Mesh:
     grad_group_ranks: List[int] = field(default_factory=list)
     pipe_group: Optional[object] = None
     initialized_here: bool = False
+    tp: int = 1  # tensor-parallel ranks per stage
+    tp_rank: int = 0
+    tp_group: Optional[object] = None
 
     @property
     def distributed(self) -> bool:
         return self.world_size > 1
 
     def global_rank(self, dp_rank: int, pp_rank: int) -> int:
-        return dp_rank * self.pp + pp_rank
+        """Global rank of pipeline position (dp_rank, pp_rank) in THIS rank's tensor-parallel slice."""
+        return (dp_rank * self.pp + pp_rank) * self.tp + self.tp_rank
 
-    def pipe_ranks(self) -> List[int]:
+    def tp_context(self):
+        from .tp import TPContext
+
+        return TPContext(self.tp, self.tp_rank, self.tp_group)
+
+    def pipe_ranks(self) -> List[int]:  # this rank's pipeline (same dp_rank, same tp_rank)
         return [self.global_rank(self.dp_rank, r) for r in range(self.pp)]
 
     def is_master(self) -> bool:
@@ -73,21 +84,23 @@ def default_backend(device: torch.device) -> str:
     return "nccl" if device.type == "cuda" else "gloo"
 
 
-def replica_groups_spec(world_size: int, pp: int, kind: str) -> List[List[int]]:
-    """Lists of ranks that hold replicas of the same stage set (gradient all-reduce groups)."""
-    dp = world_size // pp
+def replica_groups_spec(world_size: int, pp: int, kind: str, tp: int = 1) -> List[List[int]]:
+    """Lists of ranks that hold replicas of the same parameters (gradient all-reduce groups):
+    the same stage set at the same tensor-parallel position."""
+    dp = world_size // (pp * tp)
     groups = []
-    seen = set()
     if kind == "rotate":  # every rank hosts every stage: one group over the whole world
         return [list(range(world_size))]
-    for r in range(pp):
-        mirror = pp - 1 - r if kind == "chimera" else r
-        key = tuple(sorted({r, mirror}))
-        if key in seen:
-            continue
-        seen.add(key)
-        ranks = sorted(d * pp + x for d in range(dp) for x in key)
-        groups.append(ranks)
+    for t in range(tp):
+        seen = set()
+        for r in range(pp):
+            mirror = pp - 1 - r if kind == "chimera" else r
+            key = tuple(sorted({r, mirror}))
+            if key in seen:
+                continue
+            seen.add(key)
+            ranks = sorted((d * pp + x) * tp + t for d in range(dp) for x in key)
+            groups.append(ranks)
     return groups
 
 
@@ -111,7 +124,7 @@ def _pg_options(backend: str):
 def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = None,
               timeout_s: float = 600.0, rank: Optional[int] = None, world_size: Optional[int] = None,
               local_rank: Optional[int] = None, device: Optional[torch.device] = None,
-              p2p_channels: bool = True) -> Mesh:
+              p2p_channels: bool = True, tp: int = 1) -> Mesh:
     """Join (or reuse) the default process group and build the dp x pp mesh.
 
     Rank/world come from arguments, else torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK).
@@ -130,13 +143,19 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
         device = select_device(local_rank)
     if backend is None:
         backend = default_backend(device)
-    pp = max(1, min(pp, world_size))
-    if world_size % pp != 0:
-        raise ValueError(f"world_size={world_size} is not a multiple of pipeline ranks pp={pp}")
-    mesh = Mesh(rank=rank, world_size=world_size, local_rank=local_rank, pp=pp, dp=world_size // pp,
-                schedule_kind=schedule_kind, device=device, backend=backend)
-    mesh.pp_rank = rank % pp
-    mesh.dp_rank = rank // pp
+    tp = max(1, int(tp))
+    if world_size % tp != 0:
+        raise ValueError(f"world_size={world_size} is not a multiple of tensor-parallel ranks tp={tp}")
+    if tp > 1 and schedule_kind in ("rotate", "chimera"):
+        raise ValueError(f"tensor parallelism runs with the gpipe / 1f1b schedules, not {schedule_kind!r}")
+    pp = max(1, min(pp, world_size // tp))
+    if world_size % (pp * tp) != 0:
+        raise ValueError(f"world_size={world_size} is not a multiple of pp={pp} x tp={tp}")
+    mesh = Mesh(rank=rank, world_size=world_size, local_rank=local_rank, pp=pp, dp=world_size // (pp * tp),
+                schedule_kind=schedule_kind, device=device, backend=backend, tp=tp)
+    mesh.tp_rank = rank % tp
+    mesh.pp_rank = (rank // tp) % pp
+    mesh.dp_rank = rank // (tp * pp)
     if world_size == 1:
         return mesh
 
@@ -161,27 +180,36 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
         return dist.new_group(ranks, timeout=timeout, pg_options=opts)
 
     for d in range(mesh.dp):
-        ranks = [d * pp + r for r in range(pp)]
-        g = new_group(ranks) if pp > 1 else None
-        if d == mesh.dp_rank:
-            mesh.pipe_group = g
+        for t in range(tp):
+            ranks = [(d * pp + r) * tp + t for r in range(pp)]
+            g = new_group(ranks) if pp > 1 else None
+            if d == mesh.dp_rank and t == mesh.tp_rank:
+                mesh.pipe_group = g
     # rotate talks to every peer of the pipeline group; the others only to neighbours
     pairs = [(r, q) for r in range(pp) for q in range(r + 1, pp)] if schedule_kind == "rotate" else \
         [(r, r + 1) for r in range(pp - 1)]
     if not p2p_channels:
         pairs = []
     for d in range(mesh.dp):
-        for r, q in pairs:
-            a, b = d * pp + r, d * pp + q
-            for src, dst in ((a, b), (b, a)):
-                g = new_group([a, b])
-                if mesh.rank in (a, b):
-                    mesh.p2p_groups[(src, dst)] = g
-    for ranks in replica_groups_spec(world_size, pp, schedule_kind):
+        for t in range(tp):
+            for r, q in pairs:
+                a, b = (d * pp + r) * tp + t, (d * pp + q) * tp + t
+                for src, dst in ((a, b), (b, a)):
+                    g = new_group([a, b])
+                    if mesh.rank in (a, b):
+                        mesh.p2p_groups[(src, dst)] = g
+    for ranks in replica_groups_spec(world_size, pp, schedule_kind, tp):
         g = new_group(ranks) if len(ranks) > 1 else None
         if rank in ranks and len(ranks) > 1:
             mesh.grad_group = g
             mesh.grad_group_ranks = ranks
+    if tp > 1:
+        for d in range(mesh.dp):
+            for r in range(pp):
+                ranks = [(d * pp + r) * tp + t for t in range(tp)]
+                g = new_group(ranks)
+                if rank in ranks:
+                    mesh.tp_group = g
     return mesh
 
 

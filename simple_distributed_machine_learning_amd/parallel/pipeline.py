@@ -127,6 +127,12 @@ class PipelineEngine:
                         self.local_pairs.append((p, s))
         self.local_stage_ids = sorted({s for _, s in self.local_pairs})
         mods = build_stages(spec, self.local_stage_ids, base_seed=seed)
+        if mesh.tp > 1:  # tensor-parallel split of each local stage (parallel/tp.py)
+            tpc = mesh.tp_context()
+            for m in mods:
+                if not getattr(m, "supports_tp", False):
+                    raise ValueError(f"{spec.name} has no tensor-parallel implementation (tp={mesh.tp})")
+                m.shard_tp(tpc)
         self.stages: Dict[int, PipelineStage] = {}
         for s, m in zip(self.local_stage_ids, mods):
             m.to(self.device)
@@ -464,6 +470,8 @@ class PipelineEngine:
         """Sum (loss, correct, count) over all last-stage holders (world). Host-syncs."""
         v = torch.stack([res.loss_sum.double(), res.correct.double(),
                          torch.tensor(float(res.count), dtype=torch.float64).to(res.loss_sum.device)])
+        if self.mesh.tp_rank != 0:  # a tensor-parallel stage computes the loss on every tp rank
+            v.zero_()
         if self.mesh.world_size > 1:
             # every pipeline's last stage contributes once; the other ranks contribute zeros
             dist.all_reduce(v, group=group)

@@ -42,8 +42,8 @@ def _device(args) -> torch.device:
 
 def make_datasets(args, spec, device):
     if spec.input_kind == "tokens":
-        S = args.seq_len or 64
-        vocab = 97 if spec.name == "gpt2_tiny" else 50257
+        S = spec.seq_len or args.seq_len or 64
+        vocab = spec.vocab_size or 50257
         tr = SyntheticTokens(args.train_size, S, vocab, seed=args.data_seed, device=device)
         te = SyntheticTokens(args.test_size, S, vocab, seed=args.data_seed + 1, device=device)
         return tr, te
@@ -60,19 +60,20 @@ def run(args) -> dict:
     cli.export_env(args)
     device = _device(args)
     stages = args.stages or DEFAULT_STAGES[args.model]
-    pp = args.pp or (2 if args.schedule == "chimera" else min(stages, args.world_size))
-    pp = max(1, min(pp, args.world_size))
+    tp = max(1, getattr(args, "tp", 1))
+    pp = args.pp or (2 if args.schedule == "chimera" else min(stages, args.world_size // tp))
+    pp = max(1, min(pp, args.world_size // tp))
     while stages % pp:
         pp -= 1
     backend = None if args.backend == "auto" else args.backend
     mesh = init_mesh(pp=pp, schedule_kind=args.schedule, backend=backend, timeout_s=args.timeout,
-                     rank=args.rank, world_size=args.world_size, device=device)
+                     rank=args.rank, world_size=args.world_size, device=device, tp=tp)
     hb = None
     if args.heartbeat > 0 and mesh.world_size > 1:
         hb = Heartbeat(mesh.rank, range(mesh.world_size), timeout_s=args.heartbeat).start()
     dt = {"fp32": torch.float32, "bf16": torch.bfloat16}.get(getattr(args, "dtype", "auto"))
     kw = {"dtype": dt} if dt is not None and args.model in ("resnet18", "gpt2_tiny") else {}
-    spec = get_model_spec(args.model, stages, eval_dropout=bool(args.eval_dropout), seq_len=args.seq_len or 64, **kw)
+    spec = get_model_spec(args.model, stages, eval_dropout=bool(args.eval_dropout), seq_len=args.seq_len, **kw)
     if dt is not None and spec.param_dtype != dt:
         raise SystemExit(f"--dtype {args.dtype} is not supported for --model {args.model}")
     engine = PipelineEngine(spec, mesh, schedule_kind=args.schedule, num_microbatches=args.microbatches,

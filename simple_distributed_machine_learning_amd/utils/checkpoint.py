@@ -8,6 +8,7 @@ these files keep verbatim:
                          "optim": {"momentum_buffer": {name: tensor}, "steps": n, ...},
                          "epoch", "batch", "global_step", "stage", "num_stages", "model_name"}
     <dir>/rng_rank{r}.pt = per-rank RNG states (bit-identical resume of dropout)
+    with tensor parallelism (tp > 1) every tp rank writes its shard: stage{k}_tp{t}.pt
 
 Exactly one rank writes each stage file (the dp-rank-0 holder of the stage in pipe 0); all
 holders of a stage (DP replicas, Chimera mirrors) load the same file. Loading uses
@@ -30,6 +31,10 @@ def _atomic_save(obj, path: Path):
     os.replace(tmp, path)
 
 
+def _stage_file(d: Path, s: int, mesh) -> Path:
+    return d / (f"stage{s}.pt" if mesh.tp == 1 else f"stage{s}_tp{mesh.tp_rank}.pt")
+
+
 def save_checkpoint(engine: PipelineEngine, ckpt_dir: str, epoch: int, batch: int, extra: Optional[dict] = None):
     d = Path(ckpt_dir)
     d.mkdir(parents=True, exist_ok=True)
@@ -45,7 +50,9 @@ def save_checkpoint(engine: PipelineEngine, ckpt_dir: str, epoch: int, batch: in
                "num_stages": int(engine.P), "model_name": engine.spec.name}
         if extra:
             obj.update(extra)
-        _atomic_save(obj, d / f"stage{s}.pt")
+        if mesh.tp > 1:
+            obj["tp"], obj["tp_rank"] = int(mesh.tp), int(mesh.tp_rank)
+        _atomic_save(obj, _stage_file(d, s, mesh))
     rng = {"cpu": torch.get_rng_state(), "step_ctr": engine.step_ctr.detach().cpu()}
     if engine.device.type == "cuda":
         rng["cuda"] = torch.cuda.get_rng_state(engine.device)
@@ -57,8 +64,10 @@ def load_checkpoint(engine: PipelineEngine, ckpt_dir: str, strict: bool = True) 
     d = Path(ckpt_dir)
     meta = {"epoch": 0, "batch": -1, "global_step": 0}
     for s, mod in engine.stages.items():
-        path = d / f"stage{s}.pt"
+        path = _stage_file(d, s, engine.mesh)
         obj = torch.load(path, map_location="cpu", weights_only=True)
+        if int(obj.get("tp", 1)) != engine.mesh.tp:
+            raise ValueError(f"{path}: saved with tp={obj.get('tp', 1)}, running with tp={engine.mesh.tp}")
         if obj.get("model_name") not in (None, engine.spec.name):
             raise ValueError(f"{path}: checkpoint is for model {obj.get('model_name')!r}, not {engine.spec.name!r}")
         with torch.no_grad():

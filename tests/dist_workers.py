@@ -4,14 +4,14 @@ from __future__ import annotations
 import torch
 
 
-def train_worker(rank, world, model, kind, M, pp, steps, B, seed=3, kw=None):
+def train_worker(rank, world, model, kind, M, pp, steps, B, seed=3, kw=None, tp=1):
     from simple_distributed_machine_learning_amd.data import SyntheticMNIST, SyntheticTokens
     from simple_distributed_machine_learning_amd.models import get_model_spec
     from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh
 
     kw = kw or {}
     mesh = init_mesh(pp=pp, schedule_kind=kind, rank=rank, world_size=world, device=torch.device("cpu"),
-                     backend="gloo", timeout_s=120)
+                     backend="gloo", timeout_s=120, tp=tp)
     spec = get_model_spec(model, kw.get("stages"), **{k: v for k, v in kw.items() if k != "stages"})
     eng = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=seed)
     S = eng.data_shards
@@ -29,4 +29,5 @@ def train_worker(rank, world, model, kind, M, pp, steps, B, seed=3, kw=None):
     res = eng.run(ds, eng.local_start(0, B), B, train=False)
     el, ec, en = eng.reduce_metrics(res)
     return {"losses": losses, "state": eng.state_dicts(), "dp_rank": mesh.dp_rank, "pp_rank": mesh.pp_rank,
+            "tp_rank": mesh.tp_rank,
             "eval": (el, ec, en), "bytes_sent": eng.transport.bytes_sent if eng.transport else 0}

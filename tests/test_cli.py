@@ -58,3 +58,11 @@ def test_dtype_and_timing_flags():
     a = cli.parse_args(["--rank=0", "--dtype=bf16", "--timing", "--model=resnet18"])
     assert a.dtype == "bf16" and a.timing and a.model == "resnet18"
     assert cli.parse_args(["--rank=0"]).dtype == "auto"
+
+
+def test_tp_flag_parses():
+    from simple_distributed_machine_learning_amd import cli
+
+    args = cli.build_parser().parse_args(["--rank", "0", "--model", "gpt2_tiny", "--tp", "2"])
+    assert args.tp == 2
+    assert cli.build_parser().parse_args(["--rank", "0"]).tp == 1

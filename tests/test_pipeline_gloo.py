@@ -107,3 +107,47 @@ def test_mlp_rotate_matches_single_process(world, M, a2a, monkeypatch):
     if not a2a:
         per_owner = M // world  # micro-batch j of an owner goes to rank owner + j: j = 0 stays local
         assert all((r["bytes_sent"] > 0) == (per_owner > 1) for r in res)
+
+
+def _merge_tp(results, tp, n_embd):
+    """Reassemble full stage state dicts from tensor-parallel shards (parallel/tp.py layout)."""
+    by_stage = {}
+    for r in results:
+        for s, sd in r["state"].items():
+            by_stage.setdefault(s, {})[r["tp_rank"]] = sd
+    C = n_embd
+    out = {}
+    for s, shards in by_stage.items():
+        full = {}
+        for k in shards[0]:
+            parts = [shards[t][k] for t in range(tp)]
+            if "attn.c_attn" in k:  # q, k, v column blocks of every rank's heads
+                per = C // tp
+                full[k] = torch.cat([parts[t][i * per:(i + 1) * per] for i in range(3) for t in range(tp)])
+            elif k.endswith("attn.c_proj.weight") or k.endswith("mlp.c_proj.weight"):
+                full[k] = torch.cat(parts, dim=1)
+            elif "mlp.c_fc" in k:
+                full[k] = torch.cat(parts, dim=0)
+            else:  # replicated: identical on every tp rank
+                for t in range(1, tp):
+                    torch.testing.assert_close(parts[t], parts[0], rtol=0, atol=0, msg=k)
+                full[k] = parts[0]
+        out[s] = full
+    return out
+
+
+@pytest.mark.parametrize("world,pp,M", [(2, 1, 2), (4, 2, 2)])
+def test_gpt2_tiny_tensor_parallel_matches_single_process(world, pp, M):
+    """tp=2 (x pp) GPT-2: column/row-parallel blocks over Gloo train to the single-process weights."""
+    B, steps = 4, 2
+    kw = {"stages": 2, "seq_len": 16}
+    res = run_ranks(train_worker, world, "gpt2_tiny", "1f1b", M, pp, steps, B, 3, kw, 2)
+    ref = _single("gpt2_tiny", M, steps, B, "1f1b", kw)
+    st = _merge_tp(res, 2, 32)
+    assert sorted(st) == sorted(ref["state"])
+    for s in st:
+        for k in ref["state"][s]:
+            torch.testing.assert_close(st[s][k], ref["state"][s][k], rtol=1e-4, atol=1e-5, msg=f"stage {s} {k}")
+    for a, b in zip(res[0]["losses"], ref["losses"]):
+        assert a == pytest.approx(b, rel=1e-5, abs=1e-6)
+    assert res[0]["eval"][2] == ref["eval"][2]

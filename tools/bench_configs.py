@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--seq_len", type=int, default=None)
     ap.add_argument("--graph", action="store_true", help="replay the step from a captured hipGraph")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel ranks per stage (gpt2)")
     ap.add_argument("--dtype", default=None, choices=[None, "fp32", "bf16"], help="resnet18: compute dtype")
     a = ap.parse_args()
     kind, M, B, S = DEFAULTS[a.config]
@@ -52,8 +53,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     stages = DEFAULT_STAGES[a.config]
-    pp = min(world, stages)
-    mesh = init_mesh(pp=pp, schedule_kind=kind, rank=rank, world_size=world)
+    pp = min(world // a.tp, stages)
+    mesh = init_mesh(pp=pp, schedule_kind=kind, rank=rank, world_size=world, tp=a.tp)
     dt = {"fp32": torch.float32, "bf16": torch.bfloat16}.get(a.dtype)
     spec = get_model_spec(a.config, stages, seq_len=S, **({"dtype": dt} if dt is not None else {}))
     eng = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.01, momentum=0.5, seed=1)
@@ -102,7 +103,7 @@ def main():
     el = time.perf_counter() - t0
     l, c, n = eng.reduce_metrics(res)
     if rank == 0:
-        print(json.dumps({"config": a.config, "schedule": kind, "stages": stages, "ranks": world,
+        print(json.dumps({"config": a.config, "schedule": kind, "stages": stages, "ranks": world, "tp": a.tp,
                           "microbatches": M, "batch": GB, "seq_len": S, "dtype": str(spec.param_dtype), "graph": bool(a.graph), "tuned_gemms": tuned,
                           "value": round(GB * per_sample * a.steps / el, 1), "unit": unit,
                           "ms_per_step": round(el / a.steps * 1e3, 3), "loss": round(l / max(1, n), 4),

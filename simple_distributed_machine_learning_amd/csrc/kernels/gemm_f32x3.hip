@@ -14,6 +14,8 @@
 // ATen fc-layer GEMMs of the reference (/root/reference/simple_distributed.py:63-64, :75-77).
 //
 // Geometry (gfx950, wave64): 512 threads = 8 waves, K-step 32, one workgroup per CU.
+// (Measured alternative: 256-thread 128 x 128 workgroups with one LDS buffer, two per CU so one's
+//  barrier/split phases run under the other's MFMAs: 205 vs 182 us for the headline forward.)
 //   A k-contiguous: block tile 256 x 128, waves 4 x 2, 64 x 64 per wave (2 x 2 MFMA tiles)
 //   A k-major     : block tile 128 x 128, waves 2 x 4, 64 x 32 per wave (2 x 1 MFMA tiles)
 //   (a 128 x 256 tile for the weight gradient, B = X widened to 256 columns, measured slower:
@@ -48,7 +50,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef u16 u16x8 __attribute__((ext_vector_type(8)));
 typedef u16 u16x4 __attribute__((ext_vector_type(4)));
 
-constexpr int NT = 512;  // threads per workgroup
+constexpr int NT = 512;  // threads per workgroup (main kernel)
 constexpr int BK = 32;   // k per K-step
 constexpr int BN = 128;  // block tile columns (B operand rows)
 
@@ -131,7 +133,7 @@ __device__ __forceinline__ f32x4 mask4(f32x4 x, f32x4 mk) {
 // ---- staging of one operand tile (ROWS x BK) ---------------------------------------------------
 // k-contiguous: ROWS*4 chunks of 8 k; a thread owns NC = ROWS*4/NT chunks (2 float4 each).
 // k-major (ROWS == 128): 32 k-rows x 32 float4; a thread owns 2 float4 (4 rows at one k each).
-template <bool KM, int ROWS>
+template <bool KM, int ROWS, int NT = ::sdml::NT>
 struct Stage {
   static constexpr int NV = ROWS * BK / 4 / NT;  // float4 per thread
   f32x4 v[NV];
@@ -239,7 +241,7 @@ struct Stage {
 
 // k-contiguous operand already split into bf16 planes in global memory ([3][rows][ld] u16, ld %
 // 8 == 0): a plain copy into the LDS image, no VALU split. A thread owns one 8-k chunk per plane.
-template <int ROWS>
+template <int ROWS, int NT = ::sdml::NT>
 struct StagePre {
   static constexpr int NC = ROWS * 4 / NT;  // chunks per thread per plane
   u16x8 v[3][NC];

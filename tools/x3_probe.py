@@ -56,7 +56,14 @@ h = ops.linear_relu_fwd(x, w, b)
 gy = rnd(Bt, N, seed=4) * 1e-3 * (h > 0)
 gw, gb = torch.zeros_like(w), torch.zeros_like(b)
 fl = 2.0 * Bt * Kd * N
-for v in (0, 1, 0, 1):
+variants = [int(v) for v in os.environ.get("X3_VARIANTS", "0,1").split(",")]
+outs = {}
+for v in variants:
+    K.gemm_f32x3_set_variant(v)
+    outs[v] = ops.linear_relu_fwd(x, w, b)
+for v in variants[1:]:
+    print(f"variant {v} fwd vs variant {variants[0]}: max |diff| {(outs[v] - outs[variants[0]]).abs().max():.3e}")
+for v in variants + variants:
     K.gemm_f32x3_set_variant(v)
     tf = timeit(lambda: ops.linear_relu_fwd(x, w, b))
     tw = timeit(lambda: ops.linear_relu_bwd(x, h, gy, w, gw, gb, False, gy_masked=True))

@@ -1,0 +1,267 @@
+// Training-mode BatchNorm (+ residual add) (+ ReLU) on channels-last bf16 activations, for the
+// ResNet-18-style stages (models/resnet.py). x is viewed as [M = N*H*W][C] (channels contiguous).
+//
+// forward : stats   per-channel sum / sum of squares -> per-block fp32 partials
+//           finalize fixed-order fp64 reduction of the partials -> mean, rstd, the folded
+//                    scale = gamma * rstd and shift = beta - mean * scale, running-stat update
+//           apply    y = relu?(x * scale + shift (+ residual))        (one read, one write)
+// backward: partial  per-channel sums of g and g * xhat, g = dy * (y > 0 if relu)
+//           finalize dgamma / dbeta added into the bf16 parameter gradients, the two means
+//           apply    dx = gamma * rstd * (g - mean(g) - xhat * mean(g * xhat)); dres = g
+// Every pass streams 16 B per thread (8 channels); reductions are deterministic (per-block
+// partials summed in block order). PyTorch's channels-last BatchNorm kernels ran 100-800 us per
+// call on these shapes (0.1-0.5 TB/s, profiles/r1_resnet_bf16_kernel_stats.txt).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kernels.h"
+
+namespace sdml {
+namespace {
+
+typedef unsigned short u16;
+typedef u16 u16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((unsigned)v) << 16); }
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, static_cast<__bf16>(f)); }
+
+constexpr int BT = 256;
+
+// rows of this block: [blockIdx.x * rpb, +rpb); thread = (row lane, 8-channel group)
+template <bool BWD>
+__global__ void __launch_bounds__(BT) bn_partial_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
+                                                        const u16* __restrict__ y, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, int M, int C, int rpb,
+                                                        int relu, float* __restrict__ part) {
+  __shared__ float red[BT * 16];
+  const int G = C / 8;  // channel groups
+  const int lanes = BT / G;
+  const int cg = threadIdx.x % G, rl = threadIdx.x / G;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  float mu[8], rs[8];
+  if (BWD) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mu[e] = mean[8 * cg + e];
+      rs[e] = rstd[8 * cg + e];
+    }
+  }
+  const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
+  if (rl < lanes) {
+    for (int r = r0 + rl; r < r1; r += lanes) {
+      const size_t o = (size_t)r * C + 8 * cg;
+      const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
+      if (!BWD) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = bf2f(xv[e]);
+          s1[e] += v;
+          s2[e] += v * v;
+        }
+      } else {
+        const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
+        u16x8 yv = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (relu) yv = *reinterpret_cast<const u16x8*>(y + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float g = bf2f(gv[e]);
+          if (relu && !(bf2f(yv[e]) > 0.f)) g = 0.f;
+          s1[e] += g;
+          s2[e] += g * (bf2f(xv[e]) - mu[e]) * rs[e];
+        }
+      }
+    }
+  }
+  // block reduction over the row lanes (fixed order)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[(rl * G + cg) * 16 + e] = s1[e];
+    red[(rl * G + cg) * 16 + 8 + e] = s2[e];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < G * 16; i += BT) {
+    const int g = i / 16, e = i % 16;
+    float a = 0.f;
+    for (int l = 0; l < lanes; ++l) a += red[(l * G + g) * 16 + e];
+    const int c = 8 * g + (e & 7);
+    part[(size_t)blockIdx.x * 2 * C + (e < 8 ? c : C + c)] = a;
+  }
+}
+
+// one wave per channel: lane l sums partials l, l+64, ... in order (fp64), then a fixed shuffle tree
+__device__ __forceinline__ void wave_sum2(const float* __restrict__ part, int nblk, int C, int c, double& s1,
+                                          double& s2) {
+  const int lane = threadIdx.x & 63;
+  s1 = 0.0;
+  s2 = 0.0;
+  for (int b = lane; b < nblk; b += 64) {
+    s1 += part[(size_t)b * 2 * C + c];
+    s2 += part[(size_t)b * 2 * C + C + c];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
+  }
+}
+
+__global__ void __launch_bounds__(BT) bn_fwd_finalize_kernel(const float* __restrict__ part, int nblk, int C, int M,
+                                                             float eps, float momentum, const u16* __restrict__ gamma,
+                                                             const u16* __restrict__ beta, u16* __restrict__ rmean,
+                                                             u16* __restrict__ rvar, float* __restrict__ mean,
+                                                             float* __restrict__ rstd, float* __restrict__ scale,
+                                                             float* __restrict__ shift) {
+  const int c = blockIdx.x * (BT / 64) + (threadIdx.x >> 6);
+  if (c >= C) return;
+  double s1, s2;
+  wave_sum2(part, nblk, C, c, s1, s2);
+  if ((threadIdx.x & 63) != 0) return;
+  const double mu = s1 / M;
+  double var = s2 / M - mu * mu;
+  if (var < 0.0) var = 0.0;
+  const float r = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = bf2f(gamma[c]), bta = bf2f(beta[c]);
+  mean[c] = (float)mu;
+  rstd[c] = r;
+  scale[c] = g * r;
+  shift[c] = bta - (float)mu * g * r;
+  if (rmean) {
+    const double unb = M > 1 ? var * M / (M - 1) : var;
+    rmean[c] = f2bf((1.f - momentum) * bf2f(rmean[c]) + momentum * (float)mu);
+    rvar[c] = f2bf((1.f - momentum) * bf2f(rvar[c]) + momentum * (float)unb);
+  }
+}
+
+// y = relu?(x * scale + shift (+ res)), 8 channels per thread, grid-stride
+__global__ void __launch_bounds__(BT) bn_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
+                                                      const float* __restrict__ scale, const float* __restrict__ shift,
+                                                      int64_t n8, int C, int relu, u16* __restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * BT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * BT) {
+    const int c0 = (int)((8 * i) % C);
+    const u16x8 xv = reinterpret_cast<const u16x8*>(x)[i];
+    u16x8 rv = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (res) rv = reinterpret_cast<const u16x8*>(res)[i];
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = bf2f(xv[e]) * scale[c0 + e] + shift[c0 + e];
+      if (res) v += bf2f(rv[e]);
+      if (relu) v = fmaxf(v, 0.f);
+      o[e] = f2bf(v);
+    }
+    reinterpret_cast<u16x8*>(y)[i] = o;
+  }
+}
+
+// per channel: dbeta = sum g, dgamma = sum g*xhat (added into the bf16 grads), and the two means
+__global__ void __launch_bounds__(BT) bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C, int M,
+                                                             u16* __restrict__ ggamma, u16* __restrict__ gbeta,
+                                                             float* __restrict__ mg, float* __restrict__ mgx) {
+  const int c = blockIdx.x * (BT / 64) + (threadIdx.x >> 6);
+  if (c >= C) return;
+  double s1, s2;
+  wave_sum2(part, nblk, C, c, s1, s2);
+  if ((threadIdx.x & 63) != 0) return;
+  mg[c] = (float)(s1 / M);
+  mgx[c] = (float)(s2 / M);
+  if (gbeta) gbeta[c] = f2bf(bf2f(gbeta[c]) + (float)s1);
+  if (ggamma) ggamma[c] = f2bf(bf2f(ggamma[c]) + (float)s2);
+}
+
+// dx = gamma * rstd * (g - mg - xhat * mgx); dres = g (optional)
+__global__ void __launch_bounds__(BT) bn_bwd_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
+                                                          const u16* __restrict__ y, const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          const u16* __restrict__ gamma, const float* __restrict__ mg,
+                                                          const float* __restrict__ mgx, int64_t n8, int C, int relu,
+                                                          u16* __restrict__ dx, u16* __restrict__ dres) {
+  for (int64_t i = (int64_t)blockIdx.x * BT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * BT) {
+    const int c0 = (int)((8 * i) % C);
+    const u16x8 xv = reinterpret_cast<const u16x8*>(x)[i];
+    const u16x8 gv = reinterpret_cast<const u16x8*>(dy)[i];
+    u16x8 yv = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (relu) yv = reinterpret_cast<const u16x8*>(y)[i];
+    u16x8 o, og;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      float g = bf2f(gv[e]);
+      if (relu && !(bf2f(yv[e]) > 0.f)) g = 0.f;
+      const float xh = (bf2f(xv[e]) - mean[c]) * rstd[c];
+      o[e] = f2bf(bf2f(gamma[c]) * rstd[c] * (g - mg[c] - xh * mgx[c]));
+      og[e] = f2bf(g);
+    }
+    reinterpret_cast<u16x8*>(dx)[i] = o;
+    if (dres) reinterpret_cast<u16x8*>(dres)[i] = og;
+  }
+}
+
+int bn_blocks(int M, int C, int* rpb) {
+  // one partial row per block, at most 512 of them (>= 2 blocks per CU for the streaming pass)
+  int blocks = std::min(512, std::max(1, M / 64));
+  *rpb = (M + blocks - 1) / blocks;
+  blocks = (M + *rpb - 1) / *rpb;
+  return blocks;
+}
+
+int elem_blocks(int64_t n8) { return (int)std::min<int64_t>((n8 + BT - 1) / BT, 8192); }
+
+}  // namespace
+
+bool bn_nhwc_supported(int C) { return C % 8 == 0 && C >= 8 && C <= 2048; }
+
+size_t bn_nhwc_workspace_floats(int M, int C) {
+  int rpb;
+  return (size_t)bn_blocks(M, C, &rpb) * 2 * C + 8 * (size_t)C;
+}
+
+void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const void* beta, void* rmean, void* rvar,
+                      int M, int C, float eps, float momentum, bool relu, void* y, float* mean, float* rstd,
+                      float* workspace, hipStream_t stream) {
+  int rpb;
+  const int nblk = bn_blocks(M, C, &rpb);
+  float* part = workspace;
+  float* scale = workspace + (size_t)nblk * 2 * C;
+  float* shift = scale + C;
+  hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(nblk), dim3(BT), 0, stream, static_cast<const u16*>(x), nullptr,
+                     nullptr, nullptr, nullptr, M, C, rpb, 0, part);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + BT / 64 - 1) / (BT / 64)), dim3(BT), 0, stream, part, nblk, C, M, eps,
+                     momentum, static_cast<const u16*>(gamma), static_cast<const u16*>(beta), static_cast<u16*>(rmean),
+                     static_cast<u16*>(rvar), mean, rstd, scale, shift);
+  const int64_t n8 = (int64_t)M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(elem_blocks(n8)), dim3(BT), 0, stream, static_cast<const u16*>(x),
+                     static_cast<const u16*>(res), scale, shift, n8, C, relu ? 1 : 0, static_cast<u16*>(y));
+}
+
+void bn_nhwc_bwd_bf16(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
+                      const void* gamma, int M, int C, bool relu, void* dx, void* dres, void* ggamma, void* gbeta,
+                      float* workspace, hipStream_t stream) {
+  int rpb;
+  const int nblk = bn_blocks(M, C, &rpb);
+  float* part = workspace;
+  float* mg = workspace + (size_t)nblk * 2 * C;
+  float* mgx = mg + C;
+  hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(nblk), dim3(BT), 0, stream, static_cast<const u16*>(x),
+                     static_cast<const u16*>(dy), static_cast<const u16*>(y), mean, rstd, M, C, rpb, relu ? 1 : 0,
+                     part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + BT / 64 - 1) / (BT / 64)), dim3(BT), 0, stream, part, nblk, C, M,
+                     static_cast<u16*>(ggamma), static_cast<u16*>(gbeta), mg, mgx);
+  const int64_t n8 = (int64_t)M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(elem_blocks(n8)), dim3(BT), 0, stream, static_cast<const u16*>(x),
+                     static_cast<const u16*>(dy), static_cast<const u16*>(y), mean, rstd,
+                     static_cast<const u16*>(gamma), mg, mgx, n8, C, relu ? 1 : 0, static_cast<u16*>(dx),
+                     static_cast<u16*>(dres));
+}
+
+// eval mode: y = relu?(x * scale + shift (+ res)) from the running statistics
+void bn_nhwc_eval_bf16(const void* x, const void* res, const float* scale, const float* shift, int M, int C, bool relu,
+                       void* y, hipStream_t stream) {
+  const int64_t n8 = (int64_t)M * C / 8;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(elem_blocks(n8)), dim3(BT), 0, stream, static_cast<const u16*>(x),
+                     static_cast<const u16*>(res), scale, shift, n8, C, relu ? 1 : 0, static_cast<u16*>(y));
+}
+
+}  // namespace sdml

@@ -126,6 +126,34 @@ size_t wgrad_bf16_workspace_floats(int M, int N, int T);
 void wgrad_bf16(const void* gy, const void* x, void* gw, void* gb, float* workspace, int M, int N, int T, int lda,
                 int ldb, int ldc, hipStream_t stream);
 
+// ---- 3x3 stride-1 pad-1 convolution, bf16 NHWC (conv_bf16.hip) ---------------------------
+// C (input channels) and Co multiples of 64. Weights in torch layout [Co][C][3][3] are first
+// transformed: forward [Co][9][C]; dgrad (flipped, transposed) [C][9][Co] — the dgrad is the
+// forward kernel on dy with the dgrad weights.
+bool conv3x3_bf16_supported(int C, int Co);
+void conv3x3_weight_transform_bf16(const void* w_torch, void* out, int Co, int C, bool dgrad, hipStream_t stream);
+void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co, hipStream_t stream);
+// gw_torch [Co][C][3][3] bf16 += dw; workspace: conv3x3_wgrad_workspace_floats(...) fp32
+size_t conv3x3_wgrad_workspace_floats(int Nb, int H, int W, int C, int Co);
+void conv3x3_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* workspace, int Nb, int H, int W, int C,
+                        int Co, hipStream_t stream);
+
+// ---- BatchNorm (+ residual) (+ ReLU), channels-last bf16 [M = N*H*W][C] (batchnorm_nhwc.hip) ---
+// training forward: batch statistics, optional running-stat update (rmean/rvar may be null),
+// y = relu?(bn(x) + res?); mean/rstd (fp32 [C]) saved for the backward.
+// workspace: bn_nhwc_workspace_floats(M, C) fp32
+bool bn_nhwc_supported(int C);
+size_t bn_nhwc_workspace_floats(int M, int C);
+void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const void* beta, void* rmean, void* rvar,
+                      int M, int C, float eps, float momentum, bool relu, void* y, float* mean, float* rstd,
+                      float* workspace, hipStream_t stream);
+// backward: g = dy * (y > 0 if relu); dx, dres = g (optional), ggamma/gbeta (bf16, accumulated; optional)
+void bn_nhwc_bwd_bf16(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
+                      const void* gamma, int M, int C, bool relu, void* dx, void* dres, void* ggamma, void* gbeta,
+                      float* workspace, hipStream_t stream);
+void bn_nhwc_eval_bf16(const void* x, const void* res, const float* scale, const float* shift, int M, int C, bool relu,
+                       void* y, hipStream_t stream);
+
 // ---- causal flash attention, bf16, head_dim 64 ------------------------------------------
 // q/k/v (and dq/dk/dv) share one strided layout [b][h][s][64] (strides sqb, sqh, sqs; d
 // contiguous) — e.g. views into the fused c_attn output; o/dout share another (sob, soh, sos).

@@ -250,6 +250,132 @@ bool wgrad_bf16_supported_op(int64_t M, int64_t N, int64_t T) {
   return sdml::wgrad_bf16_supported(M, N, T, M, N, N);
 }
 
+// ---- 3x3 / stride 1 / pad 1 convolutions on channels-last bf16 tensors ----
+static void check_cl_bf16(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kBFloat16 && t.dim() == 4, name,
+              ": 4-D bf16 ROCm tensor expected");
+  TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name, ": channels-last (NHWC) memory expected");
+}
+
+// weight [Co][C][3][3] -> [Co][9][C] (dgrad = false) or [C][9][Co] flipped (dgrad = true)
+torch::Tensor conv3x3_weight_bf16(torch::Tensor w, bool dgrad) {
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.dim() == 4 && w.size(2) == 3 &&
+              w.size(3) == 3 && w.is_contiguous(), "conv3x3_weight_bf16: contiguous [Co][C][3][3] bf16 weight");
+  const int64_t Co = w.size(0), C = w.size(1);
+  auto out = dgrad ? torch::empty({C, 9, Co}, w.options()) : torch::empty({Co, 9, C}, w.options());
+  sdml::conv3x3_weight_transform_bf16(w.data_ptr(), out.data_ptr(), Co, C, dgrad, cur_stream());
+  return out;
+}
+
+// y (channels-last [N][Co][H][W]) = conv3x3(x, w) with wt from conv3x3_weight_bf16(w, dgrad=false)
+torch::Tensor conv3x3_fwd_bf16(torch::Tensor x, torch::Tensor wt) {
+  check_cl_bf16(x, "x");
+  TORCH_CHECK(wt.dim() == 3 && wt.size(1) == 9 && wt.size(2) == x.size(1) && wt.is_contiguous() &&
+              wt.scalar_type() == torch::kBFloat16, "conv3x3_fwd_bf16: wt must be [Co][9][C] bf16");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), Co = wt.size(0);
+  TORCH_CHECK(sdml::conv3x3_bf16_supported(C, Co), "conv3x3_fwd_bf16: channels must be multiples of 64");
+  auto y = torch::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (N * H * W > 0) sdml::conv3x3_fwd_bf16(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, C, Co, cur_stream());
+  return y;
+}
+
+// gw ([Co][C][3][3] bf16, in place) += dW of y = conv3x3(x, w) for output gradient dy
+void conv3x3_wgrad_bf16_(torch::Tensor dy, torch::Tensor x, torch::Tensor gw) {
+  check_cl_bf16(dy, "dy");
+  check_cl_bf16(x, "x");
+  TORCH_CHECK(gw.is_contiguous() && gw.scalar_type() == torch::kBFloat16 && gw.dim() == 4 &&
+              gw.size(0) == dy.size(1) && gw.size(1) == x.size(1), "conv3x3_wgrad_bf16_: gw [Co][C][3][3] bf16");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), Co = dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W, "conv3x3_wgrad_bf16_: shape mismatch");
+  TORCH_CHECK(sdml::conv3x3_bf16_supported(C, Co), "conv3x3_wgrad_bf16_: channels must be multiples of 64");
+  if (N * H * W == 0) return;
+  auto ws = torch::empty({(int64_t)sdml::conv3x3_wgrad_workspace_floats(N, H, W, C, Co)},
+                         x.options().dtype(torch::kFloat32).memory_format(at::MemoryFormat::Contiguous));
+  sdml::conv3x3_wgrad_bf16(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), ws.data_ptr<float>(), N, H, W, C, Co,
+                           cur_stream());
+}
+
+// ---- BatchNorm (+ residual) (+ ReLU) on channels-last bf16 activations ----
+static void* opt_data(const c10::optional<torch::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr;
+}
+static void check_bn_vec(const c10::optional<torch::Tensor>& t, int64_t C, const char* name) {
+  if (t.has_value() && t->defined())
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kBFloat16 && t->is_contiguous() && t->numel() == C, name,
+                ": contiguous bf16 [C] expected");
+}
+
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> bn_nhwc_fwd(
+    torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor gamma, torch::Tensor beta,
+    c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar, double eps, double momentum, bool relu) {
+  check_cl_bf16(x, "x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), M = N * H * W;
+  TORCH_CHECK(sdml::bn_nhwc_supported(C), "bn_nhwc_fwd: C must be a multiple of 8 and <= 2048");
+  if (res.has_value() && res->defined()) {
+    check_cl_bf16(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes(), "bn_nhwc_fwd: residual shape mismatch");
+  }
+  check_bn_vec(gamma, C, "gamma");
+  check_bn_vec(beta, C, "beta");
+  check_bn_vec(rmean, C, "running_mean");
+  check_bn_vec(rvar, C, "running_var");
+  auto y = torch::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto f = x.options().dtype(torch::kFloat32).memory_format(at::MemoryFormat::Contiguous);
+  auto mean = torch::empty({C}, f), rstd = torch::empty({C}, f);
+  auto ws = torch::empty({(int64_t)sdml::bn_nhwc_workspace_floats(M, C)}, f);
+  if (M > 0)
+    sdml::bn_nhwc_fwd_bf16(x.data_ptr(), opt_data(res), gamma.data_ptr(), beta.data_ptr(), opt_data(rmean),
+                           opt_data(rvar), M, C, (float)eps, (float)momentum, relu, y.data_ptr(), mean.data_ptr<float>(),
+                           rstd.data_ptr<float>(), ws.data_ptr<float>(), cur_stream());
+  return {y, mean, rstd};
+}
+
+// returns (dx, dres or None); ggamma/gbeta (bf16) are accumulated in place
+std::tuple<torch::Tensor, c10::optional<torch::Tensor>> bn_nhwc_bwd(
+    torch::Tensor x, torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor mean, torch::Tensor rstd,
+    torch::Tensor gamma, bool relu, bool need_dres, c10::optional<torch::Tensor> ggamma,
+    c10::optional<torch::Tensor> gbeta) {
+  check_cl_bf16(x, "x");
+  check_cl_bf16(dy, "dy");
+  TORCH_CHECK(dy.sizes() == x.sizes(), "bn_nhwc_bwd: dy shape mismatch");
+  if (relu) {
+    TORCH_CHECK(y.has_value() && y->defined(), "bn_nhwc_bwd: relu needs the forward output");
+    check_cl_bf16(*y, "y");
+  }
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), M = N * H * W;
+  check_bn_vec(gamma, C, "gamma");
+  check_bn_vec(ggamma, C, "ggamma");
+  check_bn_vec(gbeta, C, "gbeta");
+  TORCH_CHECK(mean.numel() == C && rstd.numel() == C && mean.scalar_type() == torch::kFloat32, "bn_nhwc_bwd: stats");
+  auto cl = x.options().memory_format(at::MemoryFormat::ChannelsLast);
+  auto dx = torch::empty_like(x, cl);
+  c10::optional<torch::Tensor> dres;
+  if (need_dres) dres = torch::empty_like(x, cl);
+  auto ws = torch::empty({(int64_t)sdml::bn_nhwc_workspace_floats(M, C)},
+                         x.options().dtype(torch::kFloat32).memory_format(at::MemoryFormat::Contiguous));
+  if (M > 0)
+    sdml::bn_nhwc_bwd_bf16(x.data_ptr(), dy.data_ptr(), relu ? y->data_ptr() : nullptr, mean.data_ptr<float>(),
+                           rstd.data_ptr<float>(), gamma.data_ptr(), M, C, relu, dx.data_ptr(),
+                           need_dres ? dres->data_ptr() : nullptr, opt_data(ggamma), opt_data(gbeta),
+                           ws.data_ptr<float>(), cur_stream());
+  return {dx, dres};
+}
+
+torch::Tensor bn_nhwc_eval(torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor scale, torch::Tensor shift,
+                           bool relu) {
+  check_cl_bf16(x, "x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), M = N * H * W;
+  TORCH_CHECK(scale.numel() == C && shift.numel() == C && scale.scalar_type() == torch::kFloat32 &&
+              shift.scalar_type() == torch::kFloat32 && scale.is_contiguous() && shift.is_contiguous(),
+              "bn_nhwc_eval: fp32 [C] scale/shift");
+  if (res.has_value() && res->defined()) check_cl_bf16(*res, "res");
+  auto y = torch::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (M > 0)
+    sdml::bn_nhwc_eval_bf16(x.data_ptr(), opt_data(res), scale.data_ptr<float>(), shift.data_ptr<float>(), M, C, relu,
+                            y.data_ptr(), cur_stream());
+  return y;
+}
+
 // fused head; returns (stats[2] = {loss_sum, correct}, dx or None). If `stats_acc` is given
 // the kernel accumulates into it (and returns it) instead of allocating a new one.
 std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
@@ -652,6 +778,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bf16_", &wgrad_bf16_, "gw += gy^T x, gb += colsum(gy) (bf16 Linear weight/bias gradient)",
         py::arg("gy"), py::arg("x"), py::arg("gw"), py::arg("gb") = py::none());
   m.def("wgrad_bf16_supported", &wgrad_bf16_supported_op, "shape check for wgrad_bf16_ (contiguous operands)");
+  m.def("conv3x3_weight_bf16", &conv3x3_weight_bf16, "3x3 conv weight -> kernel layout (forward / dgrad)");
+  m.def("conv3x3_fwd_bf16", &conv3x3_fwd_bf16, "3x3 stride-1 pad-1 conv, channels-last bf16 (implicit GEMM)");
+  m.def("conv3x3_wgrad_bf16_", &conv3x3_wgrad_bf16_, "3x3 conv weight gradient, accumulated into bf16 grad");
+  m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm (+residual)(+ReLU), channels-last bf16");
+  m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "BatchNorm (+residual)(+ReLU) backward, channels-last bf16");
+  m.def("bn_nhwc_eval", &bn_nhwc_eval, "BatchNorm with running statistics (+residual)(+ReLU)");
   m.def("gemm_f32_set_mode", &sdml::gemm_f32_set_mode, "fp32 GEMM engine: 1 = bf16x3 split (default), 0 = fp32 MFMA");
   m.def("gemm_f32_mode", &sdml::gemm_f32_mode, "current fp32 GEMM engine");
   m.def("gemm_f32_set_variant", &sdml::gemm_f32_set_variant, "fp32 GEMM variant (tuning: 0 auto, 16, 32)");

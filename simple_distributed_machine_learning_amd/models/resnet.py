@@ -6,9 +6,11 @@ Architecture (CIFAR-style stem for 28x28 inputs): conv3x3(1->64)+BN+ReLU, then 4
 The 8 BasicBlocks are the cut units: stage k gets ``8 / num_stages`` consecutive blocks;
 the stem rides with the first stage and pool+fc with the last.
 
-BatchNorm runs per micro-batch (GPipe semantics). Convolutions use MIOpen through
-PyTorch in this round. ``dtype=bf16`` runs
-the stages in bf16 (fp32 master weights in the optimizer); the default is fp32.
+BatchNorm runs per micro-batch (GPipe semantics). ``dtype=bf16`` runs the stages in bf16
+channels-last (fp32 master weights in the optimizer): the twelve stride-1 3x3 convolutions (88 %
+of the MACs) then run on the hand-written implicit-GEMM kernels of csrc/kernels/conv_bf16.hip
+(forward, input and weight gradients); the stem, the stride-2 and the 1x1 shortcut convolutions
+and the fp32 default use MIOpen through PyTorch.
 """
 from __future__ import annotations
 
@@ -20,9 +22,12 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .base import ModelSpec, PipelineStage
+from ..ops import conv as conv_ops
 
 WIDTHS = (64, 128, 256, 512)
-CHANNELS_LAST = os.environ.get("SDML_RESNET_NHWC", "0") == "1"  # measured slower with MIOpen fp32
+# fp32 runs NCHW on MIOpen (channels-last fp32 measured slower there); bf16 runs channels-last so
+# the stride-1 3x3 convolutions take the hand-written implicit-GEMM kernels (ops/conv.py)
+CHANNELS_LAST = os.environ.get("SDML_RESNET_NHWC", "auto")
 
 
 class BasicBlock(nn.Module):
@@ -37,10 +42,11 @@ class BasicBlock(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x):
-        out = F.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        sc = x if self.shortcut is None else self.shortcut(x)
-        return F.relu(out + sc)
+        # conv (HIP implicit GEMM when stride-1 bf16 NHWC) -> BN+ReLU / BN+residual+ReLU in one
+        # pass each (ops/conv.py; PyTorch ops elsewhere)
+        out = conv_ops.batch_norm(self.bn1, conv_ops.conv2d(self.conv1, x), relu=True)
+        sc = x if self.shortcut is None else conv_ops.batch_norm(self.shortcut[1], self.shortcut[0](x))
+        return conv_ops.batch_norm(self.bn2, conv_ops.conv2d(self.conv2, out), res=sc, relu=True)
 
 
 def block_defs(in_ch: int = 1):
@@ -75,15 +81,17 @@ class ResNetStage(PipelineStage):
             self.fc = nn.Linear(512, num_classes)
 
     def forward(self, x):
-        # optional NHWC inside the stage (SDML_RESNET_NHWC=1). Measured on MI355X (8 stages on one
-        # GPU, batch 512, 8 micro-batches): MIOpen picks slower solutions for channels-last fp32
-        # (9.6K vs 14.6K samples/s), so NCHW is the default. The boundary tensor is always NCHW.
+        # NHWC inside the stage for bf16 (SDML_RESNET_NHWC=auto; 1/0 force it on/off). Measured on
+        # MI355X (8 stages on one GPU, batch 512, 8 micro-batches): MIOpen picks slower solutions
+        # for channels-last fp32 (9.6K vs 14.6K samples/s), so fp32 stays NCHW. The boundary
+        # tensor is always NCHW.
         if self.stage_id == 0:
             x = x.to(self.stem_conv.weight.dtype)
-        if x.is_cuda and CHANNELS_LAST:
+        nhwc = CHANNELS_LAST == "1" or (CHANNELS_LAST == "auto" and x.dtype == torch.bfloat16)
+        if x.is_cuda and nhwc:
             x = x.contiguous(memory_format=torch.channels_last)
         if self.stage_id == 0:
-            x = F.relu(self.stem_bn(self.stem_conv(x)))
+            x = conv_ops.batch_norm(self.stem_bn, self.stem_conv(x), relu=True)
         for n in self.block_names:
             x = getattr(self, n)(x)
         if self.stage_id == self.num_stages - 1:

@@ -1,0 +1,117 @@
+"""3x3 / stride 1 / pad 1 convolution on channels-last bf16 tensors, backed by the hand-written
+implicit-GEMM kernels of csrc/kernels/conv_bf16.hip (forward, input gradient = the forward kernel
+with flipped/transposed weights, weight gradient accumulated into ``weight.grad`` in place).
+
+Used by the ResNet-18-style stages (models/resnet.py) for their twelve stride-1 3x3 convolutions
+when they run in bf16 channels-last; every other convolution (and every other dtype/layout) goes
+through ``F.conv2d``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .._native import kernels
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        K = kernels()
+        y = K.conv3x3_fwd_bf16(x, K.conv3x3_weight_bf16(w, False))
+        ctx.save_for_backward(x)
+        ctx.w = w
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        w = ctx.w
+        K = kernels()
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = K.conv3x3_fwd_bf16(dy, K.conv3x3_weight_bf16(w, True)) if ctx.needs_input_grad[0] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
+                K.conv3x3_wgrad_bf16_(dy, x, w.grad)  # straight into the flat gradient buffer
+            else:
+                gw = torch.zeros_like(w)
+                K.conv3x3_wgrad_bf16_(dy, x, gw)
+        return dx, gw
+
+
+def hip_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    w = conv.weight
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and conv.bias is None
+            and tuple(conv.kernel_size) == (3, 3) and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1)
+            and tuple(conv.dilation) == (1, 1) and conv.groups == 1
+            and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
+
+
+def conv2d(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+    """``conv(x)``, on the HIP implicit-GEMM kernels where they apply."""
+    if hip_eligible(x, conv):
+        return _Conv3x3Fn.apply(x, conv.weight)
+    return conv(x)
+
+
+# ---- BatchNorm (+ residual) (+ ReLU), channels-last bf16 (csrc/kernels/batchnorm_nhwc.hip) -----
+class _BNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, gamma, beta, bn: torch.nn.BatchNorm2d, relu: bool):
+        momentum = 0.1 if bn.momentum is None else bn.momentum
+        y, mean, rstd = kernels().bn_nhwc_fwd(x, res, gamma, beta, bn.running_mean, bn.running_var, bn.eps,
+                                              momentum, relu)
+        if bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+        ctx.save_for_backward(x, y, mean, rstd)
+        ctx.gamma, ctx.beta, ctx.relu, ctx.has_res = gamma, beta, relu, res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, rstd = ctx.saved_tensors
+        gamma, beta = ctx.gamma, ctx.beta
+        dy = dy.contiguous(memory_format=torch.channels_last)
+
+        def acc(p):  # the flat-buffer gradient (accumulated in place) or a fresh zero tensor
+            if p.grad is not None and p.grad.is_contiguous() and p.grad.dtype == torch.bfloat16:
+                return p.grad, False
+            return torch.zeros_like(p), True
+
+        gg, own_g = acc(gamma)
+        gb, own_b = acc(beta)
+        dx, dres = kernels().bn_nhwc_bwd(x, dy, y if ctx.relu else None, mean, rstd, gamma, ctx.relu, ctx.has_res,
+                                          gg, gb)
+        return dx, dres, (gg if own_g else None), (gb if own_b else None), None, None
+
+
+def bn_eligible(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res=None) -> bool:
+    ok = (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and bn.affine and bn.track_running_stats
+          and bn.weight.dtype == torch.bfloat16 and x.shape[1] % 8 == 0 and x.shape[1] <= 2048
+          and x.is_contiguous(memory_format=torch.channels_last))
+    if ok and res is not None:
+        ok = res.shape == x.shape and res.dtype == x.dtype and res.is_contiguous(memory_format=torch.channels_last)
+    return ok
+
+
+def batch_norm(bn: torch.nn.BatchNorm2d, x: torch.Tensor, res=None, relu: bool = False) -> torch.Tensor:
+    """``relu?(bn(x) (+ res))`` — one pass per direction on the HIP kernels where they apply."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4:
+        # MIOpen may hand back NCHW (e.g. the 1-channel stem): one copy beats PyTorch's NCHW
+        # BatchNorm backward (~0.8 ms per call at batch 512)
+        x = x.contiguous(memory_format=torch.channels_last)
+        if res is not None:
+            res = res.contiguous(memory_format=torch.channels_last)
+    if bn_eligible(x, bn, res):
+        if bn.training:
+            return _BNFn.apply(x, res, bn.weight, bn.bias, bn, relu)
+        with torch.no_grad():
+            scale = (bn.weight.float() * torch.rsqrt(bn.running_var.float() + bn.eps)).contiguous()
+            shift = (bn.bias.float() - bn.running_mean.float() * scale).contiguous()
+        return kernels().bn_nhwc_eval(x, res, scale, shift, relu)
+    y = bn(x)
+    if res is not None:
+        y = y + res
+    return F.relu(y) if relu else y

@@ -1,0 +1,114 @@
+"""Hand-written 3x3 convolution kernels (csrc/kernels/conv_bf16.hip) vs an fp32 PyTorch reference
+computed on the same bf16 values: forward, input gradient and weight gradient."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no ROCm GPU", allow_module_level=True)
+
+from simple_distributed_machine_learning_amd import _native  # noqa: E402
+from simple_distributed_machine_learning_amd.ops import conv as conv_ops  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+K = _native.kernels()
+
+
+def cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("N,C,Co,H,W", [(4, 64, 128, 14, 14), (3, 128, 64, 7, 7), (2, 64, 64, 28, 28),
+                                        (5, 256, 256, 4, 4), (1, 128, 192, 9, 11)])
+def test_conv3x3_fwd_dgrad_wgrad(N, C, Co, H, W):
+    g = torch.Generator(device="cpu").manual_seed(N * 1000 + C + Co + H)
+    x = torch.randn(N, C, H, W, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(Co, C, 3, 3, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    dy = torch.randn(N, Co, H, W, generator=g).to(DEV, torch.bfloat16)
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, padding=1)
+    yr.backward(dy.float())
+    # forward
+    y = K.conv3x3_fwd_bf16(cl(x), K.conv3x3_weight_bf16(w, False))
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    scale = F.conv2d(x.float().abs(), w.float().abs(), padding=1) + 1e-3
+    assert ((y.float() - yr.detach()).abs() <= 2 ** -7 * scale).all()
+    # input gradient: the forward kernel with flipped, transposed weights
+    dx = K.conv3x3_fwd_bf16(cl(dy), K.conv3x3_weight_bf16(w, True))
+    sdx = F.conv_transpose2d(dy.float().abs(), w.float().abs(), padding=1) + 1e-3
+    assert ((dx.float() - xr.grad).abs() <= 2 ** -7 * sdx).all()
+    # weight gradient, accumulated into an existing bf16 gradient
+    gw0 = (torch.randn(Co, C, 3, 3, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    gw = gw0.clone()
+    K.conv3x3_wgrad_bf16_(cl(dy), cl(x), gw)
+    want = gw0.float() + wr.grad
+    sw = torch.nn.grad.conv2d_weight(x.float().abs(), w.shape, dy.float().abs(), padding=1) + gw0.float().abs() + 1e-3
+    assert ((gw.float() - want).abs() <= 2 ** -7 * sw).all()
+
+
+def test_conv_autograd_function_matches_torch():
+    conv = torch.nn.Conv2d(64, 128, 3, 1, 1, bias=False).to(DEV, torch.bfloat16)
+    x = cl(torch.randn(2, 64, 8, 8, device=DEV, dtype=torch.bfloat16)).requires_grad_(True)
+    assert conv_ops.hip_eligible(x, conv)
+    y = conv_ops.conv2d(conv, x)
+    y.float().square().sum().backward()
+    gx, gw = x.grad.clone(), conv.weight.grad.clone()
+    x2 = x.detach().float().requires_grad_(True)
+    w2 = conv.weight.detach().float().requires_grad_(True)
+    F.conv2d(x2, w2, padding=1).square().sum().backward()
+    torch.testing.assert_close(gx.float(), x2.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(gw.float(), w2.grad, rtol=3e-2, atol=5e-1)
+
+
+@pytest.mark.parametrize("relu,res", [(True, False), (False, False), (True, True)])
+@pytest.mark.parametrize("N,C,H,W", [(8, 64, 14, 14), (4, 512, 4, 4), (3, 24, 5, 7)])
+def test_batchnorm_nhwc_train_matches_torch(N, C, H, W, relu, res):
+    g = torch.Generator(device="cpu").manual_seed(N + C + H)
+    x = cl(torch.randn(N, C, H, W, generator=g).mul(2).add(0.5).to(DEV, torch.bfloat16))
+    r = cl(torch.randn(N, C, H, W, generator=g).to(DEV, torch.bfloat16)) if res else None
+    dy = cl(torch.randn(N, C, H, W, generator=g).to(DEV, torch.bfloat16))
+    bn = torch.nn.BatchNorm2d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, generator=g) * 0.1)
+    ref = torch.nn.BatchNorm2d(C).to(DEV)
+    ref.load_state_dict(bn.state_dict())
+    bn = bn.to(torch.bfloat16)
+    ref_w = ref.weight.detach().to(torch.bfloat16).float()  # same (bf16-rounded) parameters
+    with torch.no_grad():
+        ref.weight.copy_(ref_w)
+        ref.bias.copy_(ref.bias.detach().to(torch.bfloat16).float())
+    xr = x.float().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if res else None
+    yr = ref(xr)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    yr.backward(dy.float())
+    xx = x.clone().requires_grad_(True)
+    rx = r.clone().requires_grad_(True) if res else None
+    y = conv_ops.batch_norm(bn, xx, res=rx, relu=relu)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), yr.detach(), rtol=2e-2, atol=3e-2)
+    y.backward(dy)
+    torch.testing.assert_close(xx.grad.float(), xr.grad, rtol=3e-2, atol=3e-2)
+    if res:
+        torch.testing.assert_close(rx.grad.float(), rr.grad, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(bn.weight.grad.float(), ref.weight.grad, rtol=2e-2, atol=0.5)
+    torch.testing.assert_close(bn.bias.grad.float(), ref.bias.grad, rtol=2e-2, atol=0.5)
+    torch.testing.assert_close(bn.running_mean.float(), ref.running_mean, rtol=2e-2, atol=1e-2)
+    torch.testing.assert_close(bn.running_var.float(), ref.running_var, rtol=2e-2, atol=1e-2)
+    assert int(bn.num_batches_tracked) == 1
+    # eval mode: running statistics
+    bn.eval()
+    ref.eval()
+    with torch.no_grad():
+        ye = conv_ops.batch_norm(bn, x, res=r, relu=relu)
+        yre = ref(x.float()) + (r.float() if res else 0)
+        if relu:
+            yre = torch.relu(yre)
+    torch.testing.assert_close(ye.float(), yre, rtol=2e-2, atol=3e-2)

@@ -60,9 +60,17 @@ def block_defs(in_ch: int = 1):
     return defs
 
 
+def _nhwc(dtype) -> bool:
+    return CHANNELS_LAST == "1" or (CHANNELS_LAST == "auto" and dtype == torch.bfloat16)
+
+
 class ResNetStage(PipelineStage):
-    def __init__(self, stage_id: int, num_stages: int, in_ch: int = 1, num_classes: int = 10):
+    def __init__(self, stage_id: int, num_stages: int, in_ch: int = 1, num_classes: int = 10,
+                 boundary_nhwc: bool = False):
         super().__init__()
+        # channels-last runs hand the boundary tensor over as a contiguous [N, H, W, C] array (the
+        # same bytes as the channels-last activation): no NCHW <-> NHWC copy at each stage cut
+        self.boundary_nhwc = boundary_nhwc
         if 8 % num_stages:
             raise ValueError("resnet18 splits into 1, 2, 4 or 8 stages")
         self.stage_id, self.num_stages = stage_id, num_stages
@@ -84,10 +92,12 @@ class ResNetStage(PipelineStage):
         # NHWC inside the stage for bf16 (SDML_RESNET_NHWC=auto; 1/0 force it on/off). Measured on
         # MI355X (8 stages on one GPU, batch 512, 8 micro-batches): MIOpen picks slower solutions
         # for channels-last fp32 (9.6K vs 14.6K samples/s), so fp32 stays NCHW. The boundary
-        # tensor is always NCHW.
+        # tensor is NCHW, or [N, H, W, C] in channels-last runs (boundary_nhwc).
         if self.stage_id == 0:
             x = x.to(self.stem_conv.weight.dtype)
-        nhwc = CHANNELS_LAST == "1" or (CHANNELS_LAST == "auto" and x.dtype == torch.bfloat16)
+        elif self.boundary_nhwc:
+            x = x.permute(0, 3, 1, 2)  # [N, H, W, C] boundary -> channels-last NCHW view, no copy
+        nhwc = _nhwc(x.dtype)
         if x.is_cuda and nhwc:
             x = x.contiguous(memory_format=torch.channels_last)
         if self.stage_id == 0:
@@ -98,6 +108,8 @@ class ResNetStage(PipelineStage):
             x = F.adaptive_avg_pool2d(x, 1).flatten(1)
             x = self.fc(x)
             return x
+        if self.boundary_nhwc:
+            return x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
         return x.contiguous()
 
 
@@ -114,12 +126,14 @@ def _out_shape(stage: int, num_stages: int, hw: int = 28):
 
 
 def resnet18_spec(num_stages: int = 8, dtype=torch.float32) -> ModelSpec:
+    nhwc = _nhwc(dtype) and torch.cuda.is_available()
+
     def build(s):
-        return ResNetStage(s, num_stages)
+        return ResNetStage(s, num_stages, boundary_nhwc=nhwc)
 
     def shape(s, mb):
         c, hw = _out_shape(s, num_stages)
-        return (mb, c, hw, hw)
+        return (mb, hw, hw, c) if nhwc else (mb, c, hw, hw)
 
     return ModelSpec(name="resnet18", num_stages=num_stages, build_stage=build, boundary_shape=shape,
                      boundary_dtype=dtype, input_kind="image", param_dtype=dtype)

@@ -48,8 +48,8 @@ def test_gpu_eval_and_ref_cnn_runs():
     assert r.count == 40
 
 
-@pytest.mark.parametrize("model,B,kw", [("resnet18", 16, {}), ("gpt2_tiny", 8, {"seq_len": 16}),
-                                        ("gpt2", 2, {"seq_len": 64})])
+@pytest.mark.parametrize("model,B,kw", [("resnet18", 16, {}), ("resnet18", 16, {"dtype": torch.bfloat16}),
+                                        ("gpt2_tiny", 8, {"seq_len": 16}), ("gpt2", 2, {"seq_len": 64})])
 def test_gpu_models_train(model, B, kw):
     from simple_distributed_machine_learning_amd.data import SyntheticTokens
 
@@ -69,3 +69,26 @@ def test_gpu_models_train(model, B, kw):
     assert all(l == l for l in losses)  # finite
     assert not torch.equal(p0, e.flat.params)
     assert losses[-1] < losses[0]  # same batch thrice: loss must drop
+
+
+def test_resnet_bf16_hip_kernels_match_library_path(monkeypatch):
+    """8-stage ResNet, bf16 channels-last: the hand-written conv/BatchNorm kernels train like the
+    MIOpen/PyTorch path (same init, same data, 3 steps)."""
+    from simple_distributed_machine_learning_amd.ops import conv as conv_ops
+
+    def run():
+        mesh = init_mesh(pp=1, schedule_kind="1f1b", rank=0, world_size=1, device=DEV)
+        spec = get_model_spec("resnet18", 8, dtype=torch.bfloat16)
+        e = PipelineEngine(spec, mesh, schedule_kind="1f1b", num_microbatches=1, lr=0.05, momentum=0.5, seed=3)
+        ds = SyntheticMNIST(64, seed=1, device=DEV)
+        out = [float(e.run(ds, 0, 64, train=True).loss_sum) / 64 for _ in range(3)]
+        return out, e.flat.params.float().clone()
+
+    hip_losses, hip_p = run()
+    monkeypatch.setattr(conv_ops, "hip_eligible", lambda x, conv: False)
+    monkeypatch.setattr(conv_ops, "bn_eligible", lambda x, bn, res=None: False)
+    lib_losses, lib_p = run()
+    for a, b in zip(hip_losses, lib_losses):
+        assert abs(a - b) <= 0.02 * abs(b) + 0.02, (hip_losses, lib_losses)
+    rel = (hip_p - lib_p).norm() / lib_p.norm()
+    assert rel < 0.02, float(rel)

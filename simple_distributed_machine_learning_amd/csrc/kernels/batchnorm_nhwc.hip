@@ -8,6 +8,7 @@
 // backward: partial  per-channel sums of g and g * xhat, g = dy * (y > 0 if relu)
 //           finalize dgamma / dbeta added into the bf16 parameter gradients, the two means
 //           apply    dx = gamma * rstd * (g - mean(g) - xhat * mean(g * xhat)); dres = g
+//                    (folded per channel into dx = a * (g - mean(g)) + b * (x - mean))
 // Every pass streams 16 B per thread (8 channels); reductions are deterministic (per-block
 // partials summed in block order). PyTorch's channels-last BatchNorm kernels ran 100-800 us per
 // call on these shapes (0.1-0.5 TB/s, profiles/r1_resnet_bf16_kernel_stats.txt).
@@ -135,67 +136,91 @@ __global__ void __launch_bounds__(BT) bn_fwd_finalize_kernel(const float* __rest
   }
 }
 
-// y = relu?(x * scale + shift (+ res)), 8 channels per thread, grid-stride
+// y = relu?(x * scale + shift (+ res)), 8 channels per thread, grid-stride. The block size (and so
+// the grid stride) is a multiple of C / 8 (apply_threads), so a thread's channel group never changes: the folded
+// coefficients live in registers and the loop is a pure 16 B-per-tensor stream (the first version
+// re-loaded them per element and ran at ~1.6 TB/s).
+template <bool RES, bool RELU>
 __global__ void __launch_bounds__(BT) bn_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
                                                       const float* __restrict__ scale, const float* __restrict__ shift,
-                                                      int64_t n8, int C, int relu, u16* __restrict__ y) {
-  for (int64_t i = (int64_t)blockIdx.x * BT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * BT) {
-    const int c0 = (int)((8 * i) % C);
+                                                      int64_t n8, int C, u16* __restrict__ y) {
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = 8 * (threadIdx.x % (C / 8));
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = scale[c0 + e];
+    sh[e] = shift[c0 + e];
+  }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = i0; i < n8; i += stride) {
     const u16x8 xv = reinterpret_cast<const u16x8*>(x)[i];
     u16x8 rv = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (res) rv = reinterpret_cast<const u16x8*>(res)[i];
+    if (RES) rv = reinterpret_cast<const u16x8*>(res)[i];
     u16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float v = bf2f(xv[e]) * scale[c0 + e] + shift[c0 + e];
-      if (res) v += bf2f(rv[e]);
-      if (relu) v = fmaxf(v, 0.f);
+      float v = fmaf(bf2f(xv[e]), sc[e], sh[e]);
+      if (RES) v += bf2f(rv[e]);
+      if (RELU) v = fmaxf(v, 0.f);
       o[e] = f2bf(v);
     }
     reinterpret_cast<u16x8*>(y)[i] = o;
   }
 }
 
-// per channel: dbeta = sum g, dgamma = sum g*xhat (added into the bf16 grads), and the two means
+// per channel: dbeta = sum g, dgamma = sum g*xhat (added into the bf16 grads), and the folded
+// input-gradient coefficients dx = a * (g - mg) + b * (x - mean) with a = gamma * rstd,
+// b = -a * rstd * mean(g * xhat)
 __global__ void __launch_bounds__(BT) bn_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int C, int M,
-                                                             u16* __restrict__ ggamma, u16* __restrict__ gbeta,
-                                                             float* __restrict__ mg, float* __restrict__ mgx) {
+                                                             const float* __restrict__ rstd,
+                                                             const u16* __restrict__ gamma, u16* __restrict__ ggamma,
+                                                             u16* __restrict__ gbeta, float* __restrict__ coef) {
   const int c = blockIdx.x * (BT / 64) + (threadIdx.x >> 6);
   if (c >= C) return;
   double s1, s2;
   wave_sum2(part, nblk, C, c, s1, s2);
   if ((threadIdx.x & 63) != 0) return;
-  mg[c] = (float)(s1 / M);
-  mgx[c] = (float)(s2 / M);
+  const float a = bf2f(gamma[c]) * rstd[c];
+  coef[c] = a;
+  coef[C + c] = (float)(s1 / M);
+  coef[2 * C + c] = -a * rstd[c] * (float)(s2 / M);
   if (gbeta) gbeta[c] = f2bf(bf2f(gbeta[c]) + (float)s1);
   if (ggamma) ggamma[c] = f2bf(bf2f(ggamma[c]) + (float)s2);
 }
 
-// dx = gamma * rstd * (g - mg - xhat * mgx); dres = g (optional)
+// dx = a * (g - mg) + b * (x - mean); dres = g (optional). Coefficients in registers (see apply).
+template <bool RELU, bool DRES>
 __global__ void __launch_bounds__(BT) bn_bwd_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
                                                           const u16* __restrict__ y, const float* __restrict__ mean,
-                                                          const float* __restrict__ rstd,
-                                                          const u16* __restrict__ gamma, const float* __restrict__ mg,
-                                                          const float* __restrict__ mgx, int64_t n8, int C, int relu,
+                                                          const float* __restrict__ coef, int64_t n8, int C,
                                                           u16* __restrict__ dx, u16* __restrict__ dres) {
-  for (int64_t i = (int64_t)blockIdx.x * BT + threadIdx.x; i < n8; i += (int64_t)gridDim.x * BT) {
-    const int c0 = (int)((8 * i) % C);
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = 8 * (threadIdx.x % (C / 8));
+  float ca[8], cm[8], cb[8], mu[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    ca[e] = coef[c0 + e];
+    cm[e] = coef[C + c0 + e];
+    cb[e] = coef[2 * C + c0 + e];
+    mu[e] = mean[c0 + e];
+  }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = i0; i < n8; i += stride) {
     const u16x8 xv = reinterpret_cast<const u16x8*>(x)[i];
     const u16x8 gv = reinterpret_cast<const u16x8*>(dy)[i];
     u16x8 yv = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (relu) yv = reinterpret_cast<const u16x8*>(y)[i];
+    if (RELU) yv = reinterpret_cast<const u16x8*>(y)[i];
     u16x8 o, og;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int c = c0 + e;
       float g = bf2f(gv[e]);
-      if (relu && !(bf2f(yv[e]) > 0.f)) g = 0.f;
-      const float xh = (bf2f(xv[e]) - mean[c]) * rstd[c];
-      o[e] = f2bf(bf2f(gamma[c]) * rstd[c] * (g - mg[c] - xh * mgx[c]));
+      if (RELU && !(bf2f(yv[e]) > 0.f)) g = 0.f;
+      o[e] = f2bf(fmaf(ca[e], g - cm[e], cb[e] * (bf2f(xv[e]) - mu[e])));
       og[e] = f2bf(g);
     }
     reinterpret_cast<u16x8*>(dx)[i] = o;
-    if (dres) reinterpret_cast<u16x8*>(dres)[i] = og;
+    if (DRES) reinterpret_cast<u16x8*>(dres)[i] = og;
   }
 }
 
@@ -207,7 +232,24 @@ int bn_blocks(int M, int C, int* rpb) {
   return blocks;
 }
 
-int elem_blocks(int64_t n8) { return (int)std::min<int64_t>((n8 + BT - 1) / BT, 8192); }
+// largest multiple of the channel-group count C / 8 that fits a BT-thread block
+int apply_threads(int C) { return (BT / (C / 8)) * (C / 8); }
+int elem_blocks(int64_t n8, int nt) { return (int)std::min<int64_t>((n8 + nt - 1) / nt, 8192); }
+
+void launch_apply(const void* x, const void* res, const float* scale, const float* shift, int64_t n8, int C, bool relu,
+                  void* y, hipStream_t stream) {
+  const dim3 g(elem_blocks(n8, apply_threads(C))), b(apply_threads(C));
+  const u16 *xp = static_cast<const u16*>(x), *rp = static_cast<const u16*>(res);
+  u16* yp = static_cast<u16*>(y);
+  if (res && relu)
+    hipLaunchKernelGGL((bn_apply_kernel<true, true>), g, b, 0, stream, xp, rp, scale, shift, n8, C, yp);
+  else if (res)
+    hipLaunchKernelGGL((bn_apply_kernel<true, false>), g, b, 0, stream, xp, rp, scale, shift, n8, C, yp);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_kernel<false, true>), g, b, 0, stream, xp, rp, scale, shift, n8, C, yp);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<false, false>), g, b, 0, stream, xp, rp, scale, shift, n8, C, yp);
+}
 
 }  // namespace
 
@@ -232,8 +274,7 @@ void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const v
                      momentum, static_cast<const u16*>(gamma), static_cast<const u16*>(beta), static_cast<u16*>(rmean),
                      static_cast<u16*>(rvar), mean, rstd, scale, shift);
   const int64_t n8 = (int64_t)M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(elem_blocks(n8)), dim3(BT), 0, stream, static_cast<const u16*>(x),
-                     static_cast<const u16*>(res), scale, shift, n8, C, relu ? 1 : 0, static_cast<u16*>(y));
+  launch_apply(x, res, scale, shift, n8, C, relu, y, stream);
 }
 
 void bn_nhwc_bwd_bf16(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
@@ -242,26 +283,31 @@ void bn_nhwc_bwd_bf16(const void* x, const void* dy, const void* y, const float*
   int rpb;
   const int nblk = bn_blocks(M, C, &rpb);
   float* part = workspace;
-  float* mg = workspace + (size_t)nblk * 2 * C;
-  float* mgx = mg + C;
+  float* coef = workspace + (size_t)nblk * 2 * C;  // [3][C]
   hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(nblk), dim3(BT), 0, stream, static_cast<const u16*>(x),
                      static_cast<const u16*>(dy), static_cast<const u16*>(y), mean, rstd, M, C, rpb, relu ? 1 : 0,
                      part);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + BT / 64 - 1) / (BT / 64)), dim3(BT), 0, stream, part, nblk, C, M,
-                     static_cast<u16*>(ggamma), static_cast<u16*>(gbeta), mg, mgx);
+                     rstd, static_cast<const u16*>(gamma), static_cast<u16*>(ggamma), static_cast<u16*>(gbeta), coef);
   const int64_t n8 = (int64_t)M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(elem_blocks(n8)), dim3(BT), 0, stream, static_cast<const u16*>(x),
-                     static_cast<const u16*>(dy), static_cast<const u16*>(y), mean, rstd,
-                     static_cast<const u16*>(gamma), mg, mgx, n8, C, relu ? 1 : 0, static_cast<u16*>(dx),
-                     static_cast<u16*>(dres));
+  const dim3 g(elem_blocks(n8, apply_threads(C))), b(apply_threads(C));
+  const u16 *xp = static_cast<const u16*>(x), *dyp = static_cast<const u16*>(dy), *yp = static_cast<const u16*>(y);
+  u16 *dxp = static_cast<u16*>(dx), *drp = static_cast<u16*>(dres);
+  if (relu && dres)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), g, b, 0, stream, xp, dyp, yp, mean, coef, n8, C, dxp, drp);
+  else if (relu)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), g, b, 0, stream, xp, dyp, yp, mean, coef, n8, C, dxp, drp);
+  else if (dres)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), g, b, 0, stream, xp, dyp, yp, mean, coef, n8, C, dxp, drp);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), g, b, 0, stream, xp, dyp, yp, mean, coef, n8, C, dxp, drp);
 }
 
 // eval mode: y = relu?(x * scale + shift (+ res)) from the running statistics
 void bn_nhwc_eval_bf16(const void* x, const void* res, const float* scale, const float* shift, int M, int C, bool relu,
                        void* y, hipStream_t stream) {
   const int64_t n8 = (int64_t)M * C / 8;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(elem_blocks(n8)), dim3(BT), 0, stream, static_cast<const u16*>(x),
-                     static_cast<const u16*>(res), scale, shift, n8, C, relu ? 1 : 0, static_cast<u16*>(y));
+  launch_apply(x, res, scale, shift, n8, C, relu, y, stream);
 }
 
 }  // namespace sdml

@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -168,6 +171,170 @@ __global__ void __launch_bounds__(NT) conv3x3_fwd_kernel(ConvArgs a) {
     }
 }
 
+// ---- forward / dgrad, halo-staged ("direct") variant ------------------------------------------
+// The im2col kernel above re-reads every input pixel once per tap (9x the input bytes through L2
+// per output tile). This one stages, per 64-channel chunk, the block's BM output pixels plus a
+// halo of W + 1 flattened pixels on either side ([m0 - W - 1, m0 + BM + W + 1), the only input
+// rows any tap of the tile touches) in LDS once; the nine taps are then row-shifted reads of that
+// image (row = pixel + dh * W + dw), zeroed per lane where the shifted pixel leaves the image.
+// Steps run chunk-major, tap-minor; the weight tile of step st + 1 is stored (and st + 2 loaded)
+// during step st, the halo of chunk cc + 1 is stored at tap 4 of chunk cc (its buffer's readers
+// finished with chunk cc - 1) and chunk cc + 2's halo loaded into registers then.
+// HL = 16-B halo chunks per thread: 5 covers W <= 31 (halo rows <= 320), 7 covers W <= 95 (448).
+// The 64-channel-tile, HL = 5 form fits 128 VGPRs: two workgroups (4 waves per SIMD) per CU.
+constexpr int HALO_MAX_W = 95;
+constexpr int halo_hl(int W) { return (BM + 2 * W + 2) * 8 <= 5 * NT ? 5 : 7; }
+constexpr int halo_occ(int BN, int HL) { return BN == 64 && HL == 5 ? 4 : 2; }
+
+template <int BN, int HL>
+__global__ void __launch_bounds__(NT, halo_occ(BN, HL)) conv3x3_halo_kernel(ConvArgs a) {
+  constexpr int WGN = BN / 64;
+  constexpr int WGM = 8 / WGN;
+  constexpr int WTM = BM / WGM;
+  constexpr int TM = WTM / 32;
+  constexpr int BI = BN * BK;
+  constexpr int NB = BN * 8 / NT;
+  extern __shared__ __attribute__((aligned(16))) u16 dsm[];
+  const int HR = BM + 2 * a.W + 2;  // halo rows
+  // one halo buffer when C == 64 (a single chunk): 56 KB at W = 28, two workgroups per CU
+  const int nhb = a.C > 64 ? 2 : 1;
+  u16* const HB[2] = {dsm, dsm + (nhb - 1) * HR * 64};
+  u16* const BB[2] = {dsm + nhb * HR * 64, dsm + nhb * HR * 64 + BI};
+  const int ntiles = a.tiles_m * a.tiles_n;
+  const int orig = blockIdx.x;
+  int wg = orig;
+  if (ntiles >= 16) {
+    const int q = ntiles / 8, r = ntiles % 8, xcd = orig % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  }
+  const int tn = wg % a.tiles_n, tm = wg / a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int K = 9 * a.C;
+  const int nch = a.C / 64, NS = 9 * nch;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % WGM, wn = wave / WGM;
+  const int t = threadIdx.x, ch = t & 7;
+
+  // this lane's A rows: local row lr[i]; vm[i] bit tap = shifted pixel inside the image
+  int lr[TM];
+  unsigned vm[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    lr[i] = wm * WTM + 32 * i + (lane & 31);
+    const int p = min(m0 + lr[i], a.M - 1);
+    const int pw = p % a.W, q = p / a.W, ph = q % a.H;
+    unsigned m = 0;
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+      const int ih = ph + tp / 3 - 1, iw = pw + tp % 3 - 1;
+      m |= (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) ? (1u << tp) : 0u;
+    }
+    vm[i] = m;
+  }
+
+  u16x8 vh[HL], vb[2][NB];  // weight tiles: two register sets, loaded 2 steps before their store
+  const int hbase = m0 - a.W - 1;
+  auto load_halo = [&](int cc) {
+#pragma unroll
+    for (int u = 0; u < HL; ++u) {
+      const int id = t + NT * u;
+      // clamped rows (outside [0, M) or past the halo) load valid memory that no unmasked tap reads;
+      // unconditional, so the compiler does not wait on each load separately
+      const int q = min(max(hbase + (id >> 3), 0), a.M - 1);
+      vh[u] = *reinterpret_cast<const u16x8*>(a.x + (size_t)q * a.C + cc * 64 + 8 * (id & 7));
+    }
+  };
+  auto store_halo = [&](u16* L) {
+#pragma unroll
+    for (int u = 0; u < HL; ++u) {
+      const int id = t + NT * u;
+      if (id < HR * 8) *reinterpret_cast<u16x8*>(L + swz(id >> 3, id & 7)) = vh[u];
+    }
+  };
+  auto load_b = [&](u16x8* v, int st) {
+    st = min(st, NS - 1);
+    const int cc = st / 9, tap = st % 9;
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int n = n0 + (t >> 3) + 64 * u;
+      v[u] = *reinterpret_cast<const u16x8*>(a.w + (size_t)n * K + tap * a.C + cc * 64 + 8 * ch);
+    }
+  };
+  auto store_b = [&](u16* L, const u16x8* v) {
+#pragma unroll
+    for (int u = 0; u < NB; ++u) *reinterpret_cast<u16x8*>(L + swz((t >> 3) + 64 * u, ch)) = v[u];
+  };
+
+  f32x16 acc[TM][2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  load_halo(0);
+  load_b(vb[0], 0);
+  store_halo(HB[0]);
+  store_b(BB[0], vb[0]);
+  load_b(vb[1], 1);
+  load_b(vb[0], 2);
+  if (nch > 1) load_halo(1);
+  __syncthreads();
+  const bf16x8 zf = {0, 0, 0, 0, 0, 0, 0, 0};
+  // step st stores weight tile st + 1 (register set (st + 1) & 1) and refills that set with
+  // tile st + 3; the parity is a template constant so the register sets stay in registers
+  auto step = [&](auto parity, int st) {
+    constexpr int P = decltype(parity)::value;
+    const int cc = st / 9, tap = st % 9;
+    const u16* HA = HB[cc & 1];
+    const u16* L = BB[P];
+    const int shift = (tap / 3) * a.W + tap % 3;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 af[TM], bf[2];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bf16x8 v = rowf(HA, lr[i] + shift, s, h);
+        af[i] = ((vm[i] >> tap) & 1) ? v : zf;
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = rowf(L, wn * 64 + 32 * j + (lane & 31), s, h);
+      if (s == 0) {
+        store_b(BB[P ^ 1], vb[P ^ 1]);
+        load_b(vb[P ^ 1], st + 3);
+        if (tap == 4 && cc + 1 < nch) {
+          store_halo(HB[(cc + 1) & 1]);
+          if (cc + 2 < nch) load_halo(cc + 2);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(af[i], bf[j], acc[i][j]);
+    }
+    __syncthreads();
+  };
+  int st = 0;
+  for (; st + 1 < NS; st += 2) {  // NS = 9 * nch is odd for odd nch: one tail step
+    step(std::integral_constant<int, 0>(), st);
+    step(std::integral_constant<int, 1>(), st + 1);
+  }
+  if (st < NS) step(std::integral_constant<int, 0>(), st);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int co = n0 + wn * 64 + 32 * j + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int p = m0 + wm * WTM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (p < a.M) a.y[(size_t)p * a.Co + co] = f2bf(acc[i][j][r]);
+      }
+    }
+}
+
 // ---- weight gradient: dw[co][tap][ci] (fp32 slabs) = sum_p dy[p][co] x[p + off(tap)][ci] ---------
 // tile 128 (co) x 128 (tap, ci), K-step 64 pixels; both operands k-major images [64][128] read by
 // ds_read_b64_tr_b16 (same image/swizzle as gemm_bf16_wgrad.hip)
@@ -196,8 +363,12 @@ struct WgArgs {
   int tiles_m, tiles_n, splits;
 };
 
+template <int TMR>  // output-channel rows per tile: 128 (waves 64 x 32) or 64 (waves 32 x 32; Cout = 64)
 __global__ void __launch_bounds__(NT) conv3x3_wgrad_kernel(WgArgs a) {
   constexpr int IMG = 64 * 128;
+  constexpr int TI = TMR / 64;       // 32-row blocks per wave
+  constexpr int ACPR = TMR / 8;      // dy chunks per pixel row of the tile
+  constexpr int NA = 64 * ACPR / NT;  // dy chunks per thread per K-step
   __shared__ __attribute__((aligned(16))) u16 smem[2 * 2 * IMG];
   const int ntiles = a.tiles_m * a.tiles_n;
   const int nwg = ntiles * a.splits;
@@ -209,46 +380,76 @@ __global__ void __launch_bounds__(NT) conv3x3_wgrad_kernel(WgArgs a) {
   }
   const int split = wg / ntiles, tile = wg % ntiles;
   const int tm = tile % a.tiles_m, tn = tile / a.tiles_m;
-  const int m0 = tm * 128, n0 = tn * 128;  // m: co, n: tap*C + ci
+  const int m0 = tm * TMR, n0 = tn * 128;  // m: co, n: tap*C + ci
   const int K9 = 9 * a.C;
   const int pbeg = split * a.pps, pend = min(a.M, pbeg + a.pps);
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave & 1, wn = wave >> 1;  // 2 x 4 waves: 64 (co) x 32 (n) each
+  const int wm = wave & 1, wn = wave >> 1;  // 2 x 4 waves: TMR / 2 (co) x 32 (n) each
   const int t = threadIdx.x;
-  // per K-step each operand tile is 64 pixels x 128 columns = 1024 16-B chunks: 2 per thread
-  // (pixel row kk = id >> 4, 8-column chunk c = id & 15)
-  u16x8 va[2], vb[2];
+  // per K-step: the dy tile is 64 pixels x TMR channels, the x tile 64 pixels x 128 columns (2 16-B
+  // chunks per thread: pixel row kk = id >> 4, 8-column chunk c = id & 15)
+  u16x8 va[NA], vb[2];
   unsigned okb = 0;  // bit u: chunk u of vb is inside the image (zeroed at store time otherwise)
+  // this thread's x chunks: one column chunk (tap, ci fixed) on pixel rows kk0 and kk0 + 32; the
+  // pixel coordinates advance by 64 pixels per K-step incrementally (no integer division in the loop)
+  const int kk0 = t >> 4, cb = t & 15;
+  const int nb_col = min(n0 + 8 * cb, K9 - 8);
+  const int tap = nb_col / a.C, ci = nb_col % a.C, dh = tap / 3 - 1, dw = tap % 3 - 1;
+  const int HW = a.H * a.W;
+  const int st_n = 64 / HW, st_h = (64 % HW) / a.W, st_w = 64 % a.W;
+  int pn[2], ph[2], pw[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int p = pbeg + kk0 + 32 * u;
+    pw[u] = p % a.W;
+    ph[u] = (p / a.W) % a.H;
+    pn[u] = p / HW;
+  }
   auto load = [&](int p0) {
     okb = 0;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int id = t + NT * u, kk = id >> 4, c = id & 15;
+    for (int u = 0; u < NA; ++u) {
+      const int id = t + NT * u, kk = id / ACPR, c = id % ACPR;
       const int p = min(p0 + kk, a.M - 1);
       va[u] = *reinterpret_cast<const u16x8*>(a.dy + (size_t)p * a.Co + min(m0 + 8 * c, a.Co - 8));
-      const int n = n0 + 8 * c;
-      const int tap = min(n, K9 - 8) / a.C, ci = min(n, K9 - 8) % a.C;
-      const int ow = p % a.W, q = p / a.W, oh = q % a.H, nb = q / a.H;
-      const int ih = oh + tap / 3 - 1, iw = ow + tap % 3 - 1;
-      const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      vb[u] = *reinterpret_cast<const u16x8*>(a.x + (ok ? (((size_t)nb * a.H + ih) * a.W + iw) * a.C + ci : 0));
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int ih = ph[u] + dh, iw = pw[u] + dw;
+      const bool ok = pn[u] < a.Nb && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      vb[u] = *reinterpret_cast<const u16x8*>(a.x + (ok ? (((size_t)pn[u] * a.H + ih) * a.W + iw) * a.C + ci : 0));
       okb |= ok ? (1u << u) : 0u;
+      pw[u] += st_w;  // next call loads the rows 64 pixels further
+      if (pw[u] >= a.W) {
+        pw[u] -= a.W;
+        ++ph[u];
+      }
+      ph[u] += st_h;
+      if (ph[u] >= a.H) {
+        ph[u] -= a.H;
+        ++pn[u];
+      }
+      pn[u] += st_n;
     }
   };
   auto store = [&](u16* L, int p0) {
     const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      const int id = t + NT * u, kk = id / ACPR, c = id % ACPR;
+      *reinterpret_cast<u16x8*>(L + km_off(kk, c)) = p0 + kk < pend ? va[u] : z;
+    }
+#pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int id = t + NT * u, kk = id >> 4, c = id & 15;
       const bool in = p0 + kk < pend;
-      *reinterpret_cast<u16x8*>(L + km_off(kk, c)) = in ? va[u] : z;
       *reinterpret_cast<u16x8*>(L + IMG + km_off(kk, c)) = (in && ((okb >> u) & 1)) ? vb[u] : z;
     }
   };
-  f32x16 acc[2];
+  f32x16 acc[TI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
   const int nk = (pend - pbeg + 63) / 64;
@@ -263,16 +464,16 @@ __global__ void __launch_bounds__(NT) conv3x3_wgrad_kernel(WgArgs a) {
     u16* Ln = smem + ((it + 1) & 1) * 2 * IMG;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      bf16x8 af[2], bfr;
+      bf16x8 af[TI], bfr;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = trfrag(L, wm * 64 + 32 * i, s, lane);
+      for (int i = 0; i < TI; ++i) af[i] = trfrag(L, wm * (TMR / 2) + 32 * i, s, lane);
       bfr = trfrag(L + IMG, wn * 32, s, lane);
       if (s == 0) {
         store(Ln, pbeg + (it + 1) * 64);
         load(pbeg + (it + 2) * 64);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i) acc[i] = mfma(af[i], bfr, acc[i]);
+      for (int i = 0; i < TI; ++i) acc[i] = mfma(af[i], bfr, acc[i]);
     }
     __syncthreads();
   }
@@ -280,10 +481,10 @@ __global__ void __launch_bounds__(NT) conv3x3_wgrad_kernel(WgArgs a) {
   if (col >= K9) return;
   float* S = a.slab + (size_t)split * a.Co * K9;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int co = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int co = m0 + wm * (TMR / 2) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (co < a.Co) S[(size_t)co * K9 + col] = acc[i][r];
     }
 }
@@ -341,6 +542,36 @@ void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int
   a.Co = Co;
   a.M = Nb * H * W;
   a.tiles_m = (a.M + BM - 1) / BM;
+  static const int engine = [] {  // SDML_CONV_FWD=im2col forces the im2col kernel (A/B tuning)
+    const char* e = std::getenv("SDML_CONV_FWD");
+    return (e && std::string(e) == "im2col") ? 0 : 1;
+  }();
+  static const int bn128_min = [] {  // BN 128 needs this many tiles, else BN 64 (more workgroups)
+    const char* e = std::getenv("SDML_CONV_BN128_MIN");
+    return e ? std::atoi(e) : 160;
+  }();
+  if (engine == 1 && W <= HALO_MAX_W) {
+    const bool big = Co % 128 == 0 && a.tiles_m * (Co / 128) >= bn128_min;
+    const int bn = big ? 128 : 64;
+    a.tiles_n = Co / bn;
+    const size_t lds = (size_t)((C > 64 ? 2 : 1) * (BM + 2 * W + 2) * 64 + 2 * bn * BK) * sizeof(u16);
+    static bool attr = [] {
+      for (const void* f : {reinterpret_cast<const void*>(conv3x3_halo_kernel<128, 5>),
+                             reinterpret_cast<const void*>(conv3x3_halo_kernel<128, 7>),
+                             reinterpret_cast<const void*>(conv3x3_halo_kernel<64, 5>),
+                             reinterpret_cast<const void*>(conv3x3_halo_kernel<64, 7>)})
+        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      return true;
+    }();
+    (void)attr;
+    const dim3 grid(a.tiles_m * a.tiles_n), block(NT);
+    const bool h5 = halo_hl(W) == 5;
+    if (big && h5) hipLaunchKernelGGL((conv3x3_halo_kernel<128, 5>), grid, block, lds, stream, a);
+    else if (big) hipLaunchKernelGGL((conv3x3_halo_kernel<128, 7>), grid, block, lds, stream, a);
+    else if (h5) hipLaunchKernelGGL((conv3x3_halo_kernel<64, 5>), grid, block, lds, stream, a);
+    else hipLaunchKernelGGL((conv3x3_halo_kernel<64, 7>), grid, block, lds, stream, a);
+    return;
+  }
   if (Co % 128 == 0) {
     a.tiles_n = Co / 128;
     hipLaunchKernelGGL(conv3x3_fwd_kernel<128>, dim3(a.tiles_m * a.tiles_n), dim3(NT), 0, stream, a);
@@ -350,11 +581,25 @@ void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int
   }
 }
 
+static int wgrad_rows(int Co) {
+  static const bool rows64 = [] {  // SDML_CONV_WG_ROWS64=0: 128-row tiles (half idle) for Cout = 64 too
+    const char* e = std::getenv("SDML_CONV_WG_ROWS64");
+    return !(e && std::string(e) == "0");
+  }();
+  return Co % 128 == 0 || !rows64 ? 128 : 64;
+}
+
 int conv3x3_wgrad_splits(int Nb, int H, int W, int C, int Co) {
-  const int tiles = ((Co + 127) / 128) * ((9 * C + 127) / 128);
+  // the pixel range is split until the grid reaches ~two workgroups per CU (64 KB LDS, <= 128 VGPRs)
+  static const int target = [] {
+    const char* e = std::getenv("SDML_CONV_WG_BLOCKS");
+    return e ? std::max(1, std::atoi(e)) : 512;
+  }();
+  const int tr = wgrad_rows(Co);
+  const int tiles = ((Co + tr - 1) / tr) * ((9 * C + 127) / 128);
   const int M = Nb * H * W;
-  int s = 256 / tiles;
-  const int max_by_m = M / (8 * 64);
+  int s = target / tiles;
+  const int max_by_m = M / (8 * 64);  // >= 8 K-steps per workgroup
   if (s > max_by_m) s = max_by_m;
   return s < 1 ? 1 : s;
 }
@@ -381,9 +626,13 @@ void conv3x3_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* wo
   s = (a.M + pps - 1) / pps;
   a.pps = pps;
   a.splits = s;
-  a.tiles_m = (Co + 127) / 128;
+  const int tr = wgrad_rows(Co);
+  a.tiles_m = (Co + tr - 1) / tr;
   a.tiles_n = (9 * C + 127) / 128;
-  hipLaunchKernelGGL(conv3x3_wgrad_kernel, dim3(a.tiles_m * a.tiles_n * s), dim3(NT), 0, stream, a);
+  if (tr == 128)
+    hipLaunchKernelGGL(conv3x3_wgrad_kernel<128>, dim3(a.tiles_m * a.tiles_n * s), dim3(NT), 0, stream, a);
+  else
+    hipLaunchKernelGGL(conv3x3_wgrad_kernel<64>, dim3(a.tiles_m * a.tiles_n * s), dim3(NT), 0, stream, a);
   const int64_t n = (int64_t)Co * 9 * C;
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, workspace, s, Co, C,

@@ -489,32 +489,45 @@ __global__ void __launch_bounds__(NT) conv3x3_wgrad_kernel(WgArgs a) {
     }
 }
 
-// gw[co][ci][kh][kw] (bf16, torch layout, accumulated) += sum_s slab[s][co][tap][ci]
+// gw[co][ci][kh][kw] (bf16, torch layout, accumulated) += sum_s slab[s][co][tap][ci]: the slabs are
+// read in their own order, 4 channels per thread (coalesced 16-B loads), the 4 results scattered
 __global__ void __launch_bounds__(256) conv_wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Co,
                                                                 int C, u16* __restrict__ gw) {
-  const int64_t n = (int64_t)Co * 9 * C;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    // i indexes the torch layout [co][ci][tap]
-    const int tap = (int)(i % 9);
-    const int64_t r = i / 9;
-    const int ci = (int)(r % C), co = (int)(r / C);
-    const int64_t src = ((int64_t)co * 9 + tap) * C + ci;
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += slab[(size_t)k * n + src];
-    gw[i] = f2bf(bf2f(gw[i]) + s);
+  const int64_t n = (int64_t)Co * 9 * C, n4 = n / 4;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 acc = reinterpret_cast<const float4*>(slab)[i];
+    for (int k = 1; k < splits; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(slab + (size_t)k * n)[i];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    const int64_t e = 4 * i;  // slab layout [co][tap][ci]
+    const int ci = (int)(e % C);
+    const int64_t r = e / C;
+    const int tap = (int)(r % 9), co = (int)(r / 9);
+    const float sv[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t dst = ((int64_t)co * C + ci + j) * 9 + tap;
+      gw[dst] = f2bf(bf2f(gw[dst]) + sv[j]);
+    }
   }
 }
 
-// torch weight [co][ci][3][3] -> [co][tap][ci] (forward) or the dgrad weight [ci][8 - tap][co]
-__global__ void __launch_bounds__(256) conv_weight_transform_kernel(const u16* __restrict__ w, u16* __restrict__ out,
-                                                                    int Co, int C, int dgrad) {
+// torch weight [co][ci][3][3] -> the forward layout [co][tap][ci] and/or the dgrad layout
+// [ci][8 - tap][co] (either output may be null)
+__global__ void __launch_bounds__(256) conv_weight_transform_kernel(const u16* __restrict__ w, u16* __restrict__ fwd,
+                                                                    u16* __restrict__ dgrad, int Co, int C) {
   const int64_t n = (int64_t)Co * C * 9;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int tap = (int)(i % 9);
     const int64_t r = i / 9;
     const int ci = (int)(r % C), co = (int)(r / C);
-    const int64_t dst = dgrad ? ((int64_t)ci * 9 + (8 - tap)) * Co + co : ((int64_t)co * 9 + tap) * C + ci;
-    out[dst] = w[i];
+    const u16 v = w[i];
+    if (fwd) fwd[((int64_t)co * 9 + tap) * C + ci] = v;
+    if (dgrad) dgrad[((int64_t)ci * 9 + (8 - tap)) * Co + co] = v;
   }
 }
 
@@ -522,11 +535,11 @@ __global__ void __launch_bounds__(256) conv_weight_transform_kernel(const u16* _
 
 bool conv3x3_bf16_supported(int C, int Co) { return C >= 64 && Co >= 64 && C % 64 == 0 && Co % 64 == 0; }
 
-void conv3x3_weight_transform_bf16(const void* w_torch, void* out, int Co, int C, bool dgrad, hipStream_t stream) {
+void conv3x3_weight_transform_bf16(const void* w_torch, void* fwd, void* dgrad, int Co, int C, hipStream_t stream) {
   const int64_t n = (int64_t)Co * C * 9;
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(conv_weight_transform_kernel, dim3(blocks), dim3(256), 0, stream,
-                     static_cast<const u16*>(w_torch), static_cast<u16*>(out), Co, C, dgrad ? 1 : 0);
+                     static_cast<const u16*>(w_torch), static_cast<u16*>(fwd), static_cast<u16*>(dgrad), Co, C);
 }
 
 void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co,
@@ -633,8 +646,8 @@ void conv3x3_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* wo
     hipLaunchKernelGGL(conv3x3_wgrad_kernel<128>, dim3(a.tiles_m * a.tiles_n * s), dim3(NT), 0, stream, a);
   else
     hipLaunchKernelGGL(conv3x3_wgrad_kernel<64>, dim3(a.tiles_m * a.tiles_n * s), dim3(NT), 0, stream, a);
-  const int64_t n = (int64_t)Co * 9 * C;
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  const int64_t n4 = (int64_t)Co * 9 * C / 4;
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, workspace, s, Co, C,
                      static_cast<u16*>(gw_torch));
 }

@@ -131,7 +131,8 @@ void wgrad_bf16(const void* gy, const void* x, void* gw, void* gb, float* worksp
 // transformed: forward [Co][9][C]; dgrad (flipped, transposed) [C][9][Co] — the dgrad is the
 // forward kernel on dy with the dgrad weights.
 bool conv3x3_bf16_supported(int C, int Co);
-void conv3x3_weight_transform_bf16(const void* w_torch, void* out, int Co, int C, bool dgrad, hipStream_t stream);
+// torch [Co][C][3][3] weight -> forward layout [Co][9][C] and/or dgrad layout [C][9][Co] (flipped taps); either may be null
+void conv3x3_weight_transform_bf16(const void* w_torch, void* fwd, void* dgrad, int Co, int C, hipStream_t stream);
 void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co, hipStream_t stream);
 // gw_torch [Co][C][3][3] bf16 += dw; workspace: conv3x3_wgrad_workspace_floats(...) fp32
 size_t conv3x3_wgrad_workspace_floats(int Nb, int H, int W, int C, int Co);

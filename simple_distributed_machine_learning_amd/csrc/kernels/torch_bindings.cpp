@@ -258,13 +258,28 @@ static void check_cl_bf16(const torch::Tensor& t, const char* name) {
 }
 
 // weight [Co][C][3][3] -> [Co][9][C] (dgrad = false) or [C][9][Co] flipped (dgrad = true)
-torch::Tensor conv3x3_weight_bf16(torch::Tensor w, bool dgrad) {
+static void check_conv_w(const torch::Tensor& w) {
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.dim() == 4 && w.size(2) == 3 &&
-              w.size(3) == 3 && w.is_contiguous(), "conv3x3_weight_bf16: contiguous [Co][C][3][3] bf16 weight");
+              w.size(3) == 3 && w.is_contiguous(), "conv3x3 weight: contiguous [Co][C][3][3] bf16");
+}
+
+torch::Tensor conv3x3_weight_bf16(torch::Tensor w, bool dgrad) {
+  check_conv_w(w);
   const int64_t Co = w.size(0), C = w.size(1);
   auto out = dgrad ? torch::empty({C, 9, Co}, w.options()) : torch::empty({Co, 9, C}, w.options());
-  sdml::conv3x3_weight_transform_bf16(w.data_ptr(), out.data_ptr(), Co, C, dgrad, cur_stream());
+  sdml::conv3x3_weight_transform_bf16(w.data_ptr(), dgrad ? nullptr : out.data_ptr(), dgrad ? out.data_ptr() : nullptr,
+                                      Co, C, cur_stream());
   return out;
+}
+
+// both kernel layouts of one weight in one pass: (forward [Co][9][C], dgrad [C][9][Co])
+std::tuple<torch::Tensor, torch::Tensor> conv3x3_weights_bf16(torch::Tensor w) {
+  check_conv_w(w);
+  const int64_t Co = w.size(0), C = w.size(1);
+  auto f = torch::empty({Co, 9, C}, w.options());
+  auto d = torch::empty({C, 9, Co}, w.options());
+  sdml::conv3x3_weight_transform_bf16(w.data_ptr(), f.data_ptr(), d.data_ptr(), Co, C, cur_stream());
+  return {f, d};
 }
 
 // y (channels-last [N][Co][H][W]) = conv3x3(x, w) with wt from conv3x3_weight_bf16(w, dgrad=false)
@@ -779,6 +794,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gy"), py::arg("x"), py::arg("gw"), py::arg("gb") = py::none());
   m.def("wgrad_bf16_supported", &wgrad_bf16_supported_op, "shape check for wgrad_bf16_ (contiguous operands)");
   m.def("conv3x3_weight_bf16", &conv3x3_weight_bf16, "3x3 conv weight -> kernel layout (forward / dgrad)");
+  m.def("conv3x3_weights_bf16", &conv3x3_weights_bf16, "3x3 conv weight -> (forward, dgrad) kernel layouts");
   m.def("conv3x3_fwd_bf16", &conv3x3_fwd_bf16, "3x3 stride-1 pad-1 conv, channels-last bf16 (implicit GEMM)");
   m.def("conv3x3_wgrad_bf16_", &conv3x3_wgrad_bf16_, "3x3 conv weight gradient, accumulated into bf16 grad");
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm (+residual)(+ReLU), channels-last bf16");

@@ -18,7 +18,11 @@ class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w):
         K = kernels()
-        y = K.conv3x3_fwd_bf16(x, K.conv3x3_weight_bf16(w, False))
+        if ctx.needs_input_grad[0]:  # both layouts in one pass; the dgrad one waits for backward
+            wt, ctx.wd = K.conv3x3_weights_bf16(w)
+        else:
+            wt, ctx.wd = K.conv3x3_weight_bf16(w, False), None
+        y = K.conv3x3_fwd_bf16(x, wt)
         ctx.save_for_backward(x)
         ctx.w = w
         return y
@@ -29,7 +33,8 @@ class _Conv3x3Fn(torch.autograd.Function):
         w = ctx.w
         K = kernels()
         dy = dy.contiguous(memory_format=torch.channels_last)
-        dx = K.conv3x3_fwd_bf16(dy, K.conv3x3_weight_bf16(w, True)) if ctx.needs_input_grad[0] else None
+        dx = K.conv3x3_fwd_bf16(dy, ctx.wd) if ctx.needs_input_grad[0] else None
+        ctx.wd = None
         gw = None
         if ctx.needs_input_grad[1]:
             if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:

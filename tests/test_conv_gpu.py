@@ -20,8 +20,10 @@ def cl(t):
     return t.contiguous(memory_format=torch.channels_last)
 
 
+# W <= 31: halo kernel, 5 halo chunks per thread; W 32..95: 7 chunks; W > 95: im2col kernel
 @pytest.mark.parametrize("N,C,Co,H,W", [(4, 64, 128, 14, 14), (3, 128, 64, 7, 7), (2, 64, 64, 28, 28),
-                                        (5, 256, 256, 4, 4), (1, 128, 192, 9, 11)])
+                                        (5, 256, 256, 4, 4), (1, 128, 192, 9, 11), (2, 128, 64, 3, 40),
+                                        (1, 64, 128, 2, 100)])
 def test_conv3x3_fwd_dgrad_wgrad(N, C, Co, H, W):
     g = torch.Generator(device="cpu").manual_seed(N * 1000 + C + Co + H)
     x = torch.randn(N, C, H, W, generator=g).to(DEV, torch.bfloat16)
@@ -31,8 +33,10 @@ def test_conv3x3_fwd_dgrad_wgrad(N, C, Co, H, W):
     wr = w.float().requires_grad_(True)
     yr = F.conv2d(xr, wr, padding=1)
     yr.backward(dy.float())
-    # forward
-    y = K.conv3x3_fwd_bf16(cl(x), K.conv3x3_weight_bf16(w, False))
+    # forward; the fused two-layout transform matches the single ones
+    wf, wd = K.conv3x3_weights_bf16(w)
+    assert torch.equal(wf, K.conv3x3_weight_bf16(w, False)) and torch.equal(wd, K.conv3x3_weight_bf16(w, True))
+    y = K.conv3x3_fwd_bf16(cl(x), wf)
     assert y.is_contiguous(memory_format=torch.channels_last)
     scale = F.conv2d(x.float().abs(), w.float().abs(), padding=1) + 1e-3
     assert ((y.float() - yr.detach()).abs() <= 2 ** -7 * scale).all()

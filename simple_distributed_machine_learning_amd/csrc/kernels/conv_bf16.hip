@@ -531,6 +531,112 @@ __global__ void __launch_bounds__(256) conv_weight_transform_kernel(const u16* _
   }
 }
 
+// ---- stem: one input channel (MNIST), 3x3 / stride 1 / pad 1 -----------------------------------
+// K = 9 is far too short for the matrix cores: both passes are plain streaming kernels at the
+// output/gradient bandwidth. Forward: a thread owns 16 output channels of one pixel (weights in
+// LDS as fp32 [tap][co]); it writes NHWC directly, so no layout copy follows (MIOpen produced NCHW
+// here, 68 us + a 24 us channels-last copy at batch 512).
+constexpr int STEM_T = 256;
+
+__global__ void __launch_bounds__(STEM_T) conv_c1_fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ w,
+                                                             u16* __restrict__ y, int Nb, int H, int W, int Co) {
+  __shared__ float ws[9 * 512];
+  for (int i = threadIdx.x; i < 9 * Co; i += STEM_T) {  // w [co][tap] -> ws [tap][co]
+    const int co = i / 9, tap = i % 9;
+    ws[tap * Co + co] = bf2f(w[i]);
+  }
+  __syncthreads();
+  const int G = Co / 16;
+  const int64_t M = (int64_t)Nb * H * W, total = M * G;
+  for (int64_t idx = (int64_t)blockIdx.x * STEM_T + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * STEM_T) {
+    const int64_t p = idx / G;
+    const int c0 = 16 * (int)(idx % G);
+    const int pw = (int)(p % W);
+    const int64_t q = p / W;
+    const int ph = (int)(q % H);
+    float acc[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ih = ph + tap / 3 - 1, iw = pw + tap % 3 - 1;
+      if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
+      const float xv = bf2f(x[p + (int64_t)(tap / 3 - 1) * W + (tap % 3 - 1)]);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = fmaf(xv, ws[tap * Co + c0 + e], acc[e]);
+    }
+    u16x8 o0, o1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o0[e] = f2bf(acc[e]);
+      o1[e] = f2bf(acc[8 + e]);
+    }
+    u16x8* dst = reinterpret_cast<u16x8*>(y + p * Co + c0);
+    dst[0] = o0;
+    dst[1] = o1;
+  }
+}
+
+// weight gradient: per-block partial [9][Co] over a pixel range; thread = (pixel lane, 8 channels),
+// 72 fp32 accumulators; block reduction over the pixel lanes in fixed order
+__global__ void __launch_bounds__(STEM_T) conv_c1_wgrad_kernel(const u16* __restrict__ dy, const u16* __restrict__ x,
+                                                               int Nb, int H, int W, int Co, int ppb,
+                                                               float* __restrict__ part) {
+  __shared__ float red[STEM_T * 8];
+  const int G = Co / 8, lanes = STEM_T / G;
+  const int g = threadIdx.x % G, rl = threadIdx.x / G;
+  const int64_t M = (int64_t)Nb * H * W;
+  const int64_t p0 = (int64_t)blockIdx.x * ppb, p1 = min(M, p0 + ppb);
+  float acc[9][8];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[t][e] = 0.f;
+  if (rl < lanes) {
+    for (int64_t p = p0 + rl; p < p1; p += lanes) {
+      const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + p * Co + 8 * g);
+      const int pw = (int)(p % W), ph = (int)((p / W) % H);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ih = ph + tap / 3 - 1, iw = pw + tap % 3 - 1;
+        const bool ok = ih >= 0 && ih < H && iw >= 0 && iw < W;
+        const float xv = ok ? bf2f(x[p + (int64_t)(tap / 3 - 1) * W + (tap % 3 - 1)]) : 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[tap][e] = fmaf(bf2f(gv[e]), xv, acc[tap][e]);
+      }
+    }
+  }
+  // reduce over the row lanes, one tap at a time through LDS (fixed order)
+  for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = acc[tap][e];
+    __syncthreads();
+    for (int i = threadIdx.x; i < Co; i += STEM_T) {
+      const int gg = i / 8, e = i % 8;
+      float s2 = 0.f;
+      for (int l = 0; l < lanes; ++l) s2 += red[(l * G + gg) * 8 + e];
+      part[((size_t)blockIdx.x * 9 + tap) * Co + i] = s2;
+    }
+    __syncthreads();
+  }
+}
+
+// gw[co][0][tap] (bf16, accumulated) += sum over blocks of part[b][tap][co]: one wave per output,
+// lane l sums blocks l, l + 64, ... in order, then a fixed shuffle tree (deterministic)
+__global__ void __launch_bounds__(STEM_T) conv_c1_wgrad_reduce_kernel(const float* __restrict__ part, int nblk, int Co,
+                                                                      u16* __restrict__ gw) {
+  const int i = blockIdx.x * (STEM_T / 64) + (threadIdx.x >> 6);  // over [tap][co]
+  if (i >= 9 * Co) return;
+  const int lane = threadIdx.x & 63;
+  float s2 = 0.f;
+  for (int b = lane; b < nblk; b += 64) s2 += part[(size_t)b * 9 * Co + i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s2 += __shfl_xor(s2, off);
+  if (lane != 0) return;
+  const int tap = i / Co, co = i % Co;
+  gw[co * 9 + tap] = f2bf(bf2f(gw[co * 9 + tap]) + s2);
+}
+
 }  // namespace
 
 bool conv3x3_bf16_supported(int C, int Co) { return C >= 64 && Co >= 64 && C % 64 == 0 && Co % 64 == 0; }
@@ -650,6 +756,37 @@ void conv3x3_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* wo
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, workspace, s, Co, C,
                      static_cast<u16*>(gw_torch));
+}
+
+// ---- stem (one input channel) ----------------------------------------------------------------
+bool conv_c1_supported(int Co) { return Co % 16 == 0 && Co <= 512; }
+
+void conv_c1_fwd_bf16(const void* x, const void* w, void* y, int Nb, int H, int W, int Co, hipStream_t stream) {
+  const int64_t total = (int64_t)Nb * H * W * (Co / 16);
+  const int blocks = (int)std::min<int64_t>((total + STEM_T - 1) / STEM_T, 8192);
+  hipLaunchKernelGGL(conv_c1_fwd_kernel, dim3(blocks), dim3(STEM_T), 0, stream, static_cast<const u16*>(x),
+                     static_cast<const u16*>(w), static_cast<u16*>(y), Nb, H, W, Co);
+}
+
+static int c1_wgrad_blocks(int64_t M, int* ppb) {
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(1024, M / 64));
+  *ppb = (int)((M + blocks - 1) / blocks);
+  return (int)((M + *ppb - 1) / *ppb);
+}
+
+size_t conv_c1_wgrad_workspace_floats(int Nb, int H, int W, int Co) {
+  int ppb;
+  return (size_t)c1_wgrad_blocks((int64_t)Nb * H * W, &ppb) * 9 * Co;
+}
+
+void conv_c1_wgrad_bf16(const void* dy, const void* x, void* gw, float* workspace, int Nb, int H, int W, int Co,
+                        hipStream_t stream) {
+  int ppb;
+  const int nblk = c1_wgrad_blocks((int64_t)Nb * H * W, &ppb);
+  hipLaunchKernelGGL(conv_c1_wgrad_kernel, dim3(nblk), dim3(STEM_T), 0, stream, static_cast<const u16*>(dy),
+                     static_cast<const u16*>(x), Nb, H, W, Co, ppb, workspace);
+  hipLaunchKernelGGL(conv_c1_wgrad_reduce_kernel, dim3((9 * Co + STEM_T / 64 - 1) / (STEM_T / 64)), dim3(STEM_T), 0, stream,
+                     workspace, nblk, Co, static_cast<u16*>(gw));
 }
 
 }  // namespace sdml

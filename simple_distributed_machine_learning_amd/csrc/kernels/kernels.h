@@ -135,6 +135,13 @@ bool conv3x3_bf16_supported(int C, int Co);
 void conv3x3_weight_transform_bf16(const void* w_torch, void* fwd, void* dgrad, int Co, int C, hipStream_t stream);
 void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co, hipStream_t stream);
 // gw_torch [Co][C][3][3] bf16 += dw; workspace: conv3x3_wgrad_workspace_floats(...) fp32
+// stem convolution with ONE input channel, 3x3 / stride 1 / pad 1, bf16: x [N][H][W], w [Co][1][3][3],
+// y NHWC [N][H][W][Co]; weight gradient accumulated into the bf16 [Co][1][3][3] gradient
+bool conv_c1_supported(int Co);
+void conv_c1_fwd_bf16(const void* x, const void* w, void* y, int Nb, int H, int W, int Co, hipStream_t stream);
+size_t conv_c1_wgrad_workspace_floats(int Nb, int H, int W, int Co);
+void conv_c1_wgrad_bf16(const void* dy, const void* x, void* gw, float* workspace, int Nb, int H, int W, int Co,
+                        hipStream_t stream);
 size_t conv3x3_wgrad_workspace_floats(int Nb, int H, int W, int C, int Co);
 void conv3x3_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* workspace, int Nb, int H, int W, int C,
                         int Co, hipStream_t stream);

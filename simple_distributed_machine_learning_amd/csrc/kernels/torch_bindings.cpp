@@ -320,6 +320,34 @@ static void check_bn_vec(const c10::optional<torch::Tensor>& t, int64_t C, const
                 ": contiguous bf16 [C] expected");
 }
 
+// stem convolution, one input channel: y (channels-last [N][Co][H][W]) = conv3x3(x [N][1][H][W], w)
+torch::Tensor conv_c1_fwd_bf16(torch::Tensor x, torch::Tensor w) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 4 && x.size(1) == 1 && x.is_contiguous(),
+              "conv_c1_fwd_bf16: x must be contiguous [N][1][H][W] bf16");
+  TORCH_CHECK(w.is_cuda() && w.scalar_type() == torch::kBFloat16 && w.dim() == 4 && w.size(1) == 1 && w.size(2) == 3 &&
+              w.size(3) == 3 && w.is_contiguous() && sdml::conv_c1_supported(w.size(0)),
+              "conv_c1_fwd_bf16: w must be contiguous [Co][1][3][3] bf16, Co % 16 == 0, Co <= 512");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3), Co = w.size(0);
+  auto y = torch::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (N * H * W > 0) sdml::conv_c1_fwd_bf16(x.data_ptr(), w.data_ptr(), y.data_ptr(), N, H, W, Co, cur_stream());
+  return y;
+}
+
+// gw ([Co][1][3][3] bf16, in place) += dW of the stem convolution for output gradient dy (channels-last)
+void conv_c1_wgrad_bf16_(torch::Tensor dy, torch::Tensor x, torch::Tensor gw) {
+  check_cl_bf16(dy, "dy");
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 4 && x.size(1) == 1 && x.is_contiguous(),
+              "conv_c1_wgrad_bf16_: x must be contiguous [N][1][H][W] bf16");
+  TORCH_CHECK(gw.is_contiguous() && gw.scalar_type() == torch::kBFloat16 && gw.dim() == 4 && gw.size(0) == dy.size(1) &&
+              gw.size(1) == 1 && sdml::conv_c1_supported(gw.size(0)), "conv_c1_wgrad_bf16_: gw [Co][1][3][3] bf16");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3), Co = dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W, "conv_c1_wgrad_bf16_: shape mismatch");
+  if (N * H * W == 0) return;
+  auto ws = torch::empty({(int64_t)sdml::conv_c1_wgrad_workspace_floats(N, H, W, Co)},
+                         x.options().dtype(torch::kFloat32));
+  sdml::conv_c1_wgrad_bf16(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), ws.data_ptr<float>(), N, H, W, Co, cur_stream());
+}
+
 std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> bn_nhwc_fwd(
     torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor gamma, torch::Tensor beta,
     c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar, double eps, double momentum, bool relu) {
@@ -797,6 +825,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_weights_bf16", &conv3x3_weights_bf16, "3x3 conv weight -> (forward, dgrad) kernel layouts");
   m.def("conv3x3_fwd_bf16", &conv3x3_fwd_bf16, "3x3 stride-1 pad-1 conv, channels-last bf16 (implicit GEMM)");
   m.def("conv3x3_wgrad_bf16_", &conv3x3_wgrad_bf16_, "3x3 conv weight gradient, accumulated into bf16 grad");
+  m.def("conv_c1_fwd_bf16", &conv_c1_fwd_bf16, "stem 3x3 conv with one input channel -> channels-last bf16");
+  m.def("conv_c1_wgrad_bf16_", &conv_c1_wgrad_bf16_, "stem conv weight gradient, accumulated into bf16 grad");
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm (+residual)(+ReLU), channels-last bf16");
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "BatchNorm (+residual)(+ReLU) backward, channels-last bf16");
   m.def("bn_nhwc_eval", &bn_nhwc_eval, "BatchNorm with running statistics (+residual)(+ReLU)");

@@ -101,7 +101,7 @@ class ResNetStage(PipelineStage):
         if x.is_cuda and nhwc:
             x = x.contiguous(memory_format=torch.channels_last)
         if self.stage_id == 0:
-            x = conv_ops.batch_norm(self.stem_bn, self.stem_conv(x), relu=True)
+            x = conv_ops.batch_norm(self.stem_bn, conv_ops.conv2d(self.stem_conv, x), relu=True)
         for n in self.block_names:
             x = getattr(self, n)(x)
         if self.stage_id == self.num_stages - 1:

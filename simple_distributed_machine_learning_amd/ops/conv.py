@@ -3,8 +3,8 @@ implicit-GEMM kernels of csrc/kernels/conv_bf16.hip (forward, input gradient = t
 with flipped/transposed weights, weight gradient accumulated into ``weight.grad`` in place).
 
 Used by the ResNet-18-style stages (models/resnet.py) for their twelve stride-1 3x3 convolutions
-when they run in bf16 channels-last; every other convolution (and every other dtype/layout) goes
-through ``F.conv2d``.
+and the one-channel stem when they run in bf16 channels-last; the stride-2 and 1x1 shortcut
+convolutions (and every other dtype/layout) go through ``F.conv2d``.
 """
 from __future__ import annotations
 
@@ -54,10 +54,49 @@ def hip_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
 
 
+class _StemConvFn(torch.autograd.Function):
+    """3x3 convolution of a one-channel image (the MNIST stem): streaming kernels, NHWC output."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        x = x.contiguous()
+        ctx.save_for_backward(x)
+        ctx.w = w
+        return kernels().conv_c1_fwd_bf16(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        w = ctx.w
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = None
+        if ctx.needs_input_grad[0]:  # the stem's input is data; kept for completeness
+            dx = torch.nn.grad.conv2d_input(x.shape, w, dy, padding=1)
+        gw = None
+        if ctx.needs_input_grad[1]:
+            if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
+                kernels().conv_c1_wgrad_bf16_(dy, x, w.grad)
+            else:
+                gw = torch.zeros_like(w)
+                kernels().conv_c1_wgrad_bf16_(dy, x, gw)
+        return dx, gw
+
+
+def stem_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    w = conv.weight
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
+            and conv.in_channels == 1 and conv.bias is None and tuple(conv.kernel_size) == (3, 3)
+            and tuple(conv.stride) == (1, 1) and tuple(conv.padding) == (1, 1) and tuple(conv.dilation) == (1, 1)
+            and conv.groups == 1 and conv.out_channels % 16 == 0 and conv.out_channels <= 512)
+
+
 def conv2d(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
-    """``conv(x)``, on the HIP implicit-GEMM kernels where they apply."""
+    """``conv(x)``, on the HIP kernels where they apply (implicit GEMM for 64-multiple channel
+    counts, the streaming stem kernels for a one-channel input)."""
     if hip_eligible(x, conv):
         return _Conv3x3Fn.apply(x, conv.weight)
+    if stem_eligible(x, conv):
+        return _StemConvFn.apply(x, conv.weight)
     return conv(x)
 
 

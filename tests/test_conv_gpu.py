@@ -53,6 +53,26 @@ def test_conv3x3_fwd_dgrad_wgrad(N, C, Co, H, W):
     assert ((gw.float() - want).abs() <= 2 ** -7 * sw).all()
 
 
+@pytest.mark.parametrize("N,Co,H,W", [(4, 64, 28, 28), (3, 32, 5, 9)])
+def test_stem_conv_one_channel(N, Co, H, W):
+    g = torch.Generator(device="cpu").manual_seed(N + Co + H)
+    x = torch.randn(N, 1, H, W, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(Co, 1, 3, 3, generator=g) * 0.3).to(DEV, torch.bfloat16)
+    dy = cl(torch.randn(N, Co, H, W, generator=g).to(DEV, torch.bfloat16))
+    y = K.conv_c1_fwd_bf16(x, w)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    yr = F.conv2d(x.float(), w.float(), padding=1)
+    torch.testing.assert_close(y.float(), yr, rtol=1e-2, atol=1e-2)
+    gw0 = (torch.randn(Co, 1, 3, 3, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    gw = gw0.clone()
+    K.conv_c1_wgrad_bf16_(dy, x, gw)
+    want = gw0.float() + torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), padding=1)
+    sw = torch.nn.grad.conv2d_weight(x.float().abs(), w.shape, dy.float().abs(), padding=1) + gw0.float().abs()
+    assert ((gw.float() - want).abs() <= 2 ** -7 * sw + 1e-3).all()
+    conv = torch.nn.Conv2d(1, Co, 3, 1, 1, bias=False).to(DEV, torch.bfloat16)
+    assert conv_ops.stem_eligible(x, conv)
+
+
 def test_conv_autograd_function_matches_torch():
     conv = torch.nn.Conv2d(64, 128, 3, 1, 1, bias=False).to(DEV, torch.bfloat16)
     x = cl(torch.randn(2, 64, 8, 8, device=DEV, dtype=torch.bfloat16)).requires_grad_(True)

@@ -50,11 +50,12 @@ __device__ __forceinline__ bf16x8 rowf(const u16* X, int row, int s, int h) {
 
 struct ConvArgs {
   const u16* x;  // NHWC input [Nb][H][W][C]
-  const u16* w;  // [Co][9][C]
-  u16* y;        // NHWC output [Nb][H][W][Co]
+  const u16* w;  // [Co][KS*KS][C]
+  u16* y;        // NHWC output [Nb][OH][OW][Co]
   int Nb, H, W, C, Co;
-  int M;         // Nb*H*W
+  int M;         // Nb*OH*OW
   int tiles_m, tiles_n;
+  int OH, OW, S, KS, P;  // output size, stride, kernel size (3 or 1), padding (the halo kernel: 1 / 3 / 1)
 };
 
 template <int BN>
@@ -75,7 +76,7 @@ __global__ void __launch_bounds__(NT) conv3x3_fwd_kernel(ConvArgs a) {
   }
   const int tn = wg % a.tiles_n, tm = wg / a.tiles_n;  // the Cout tiles of a pixel tile are adjacent
   const int m0 = tm * BM, n0 = tn * BN;
-  const int K = 9 * a.C;
+  const int K = a.KS * a.KS * a.C;
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave % WGM, wn = wave / WGM;
@@ -89,22 +90,22 @@ __global__ void __launch_bounds__(NT) conv3x3_fwd_kernel(ConvArgs a) {
     const int p = m0 + (t >> 3) + 64 * u;
     pv[u] = p < a.M;
     const int pp = pv[u] ? p : 0;
-    pw[u] = pp % a.W;
-    const int q = pp / a.W;
-    ph[u] = q % a.H;
-    pn[u] = q / a.H;
+    pw[u] = pp % a.OW;
+    const int q = pp / a.OW;
+    ph[u] = q % a.OH;
+    pn[u] = q / a.OH;
   }
   u16x8 va[4], vb[NB];
   auto inb = [&](int u, int k0) {  // is row u's shifted pixel inside the image for tap(k0)?
     const int tap = k0 / a.C;
-    const int ih = ph[u] + tap / 3 - 1, iw = pw[u] + tap % 3 - 1;
+    const int ih = ph[u] * a.S + tap / a.KS - a.P, iw = pw[u] * a.S + tap % a.KS - a.P;
     return pv[u] && k0 < K && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
   };
   auto load = [&](int k0) {
     const int tap = min(k0, K - BK) / a.C, ci0 = min(k0, K - BK) % a.C;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int ih = ph[u] + tap / 3 - 1, iw = pw[u] + tap % 3 - 1;
+      const int ih = ph[u] * a.S + tap / a.KS - a.P, iw = pw[u] * a.S + tap % a.KS - a.P;
       const bool ok = pv[u] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
       const size_t off = ok ? (((size_t)pn[u] * a.H + ih) * a.W + iw) * a.C + ci0 + 8 * ch : 0;
       va[u] = *reinterpret_cast<const u16x8*>(a.x + off);
@@ -355,10 +356,11 @@ __device__ __forceinline__ bf16x8 trfrag(const u16* P, int c0, int s, int lane) 
 }
 
 struct WgArgs {
-  const u16* dy;  // [M][Co]
-  const u16* x;   // [M][C] (NHWC)
-  float* slab;    // [splits][Co][9C]
+  const u16* dy;  // [M][Co] (NHWC output gradient, M = Nb*OH*OW)
+  const u16* x;   // [Nb][H][W][C] (NHWC)
+  float* slab;    // [splits][Co][KS*KS*C]
   int Nb, H, W, C, Co, M;
+  int OH, OW, S, KS, P;
   int pps;        // pixels per split (multiple of 64)
   int tiles_m, tiles_n, splits;
 };
@@ -381,7 +383,7 @@ __global__ void __launch_bounds__(NT) conv3x3_wgrad_kernel(WgArgs a) {
   const int split = wg / ntiles, tile = wg % ntiles;
   const int tm = tile % a.tiles_m, tn = tile / a.tiles_m;
   const int m0 = tm * TMR, n0 = tn * 128;  // m: co, n: tap*C + ci
-  const int K9 = 9 * a.C;
+  const int K9 = a.KS * a.KS * a.C;  // GEMM N: (tap, ci)
   const int pbeg = split * a.pps, pend = min(a.M, pbeg + a.pps);
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -395,15 +397,15 @@ __global__ void __launch_bounds__(NT) conv3x3_wgrad_kernel(WgArgs a) {
   // pixel coordinates advance by 64 pixels per K-step incrementally (no integer division in the loop)
   const int kk0 = t >> 4, cb = t & 15;
   const int nb_col = min(n0 + 8 * cb, K9 - 8);
-  const int tap = nb_col / a.C, ci = nb_col % a.C, dh = tap / 3 - 1, dw = tap % 3 - 1;
-  const int HW = a.H * a.W;
-  const int st_n = 64 / HW, st_h = (64 % HW) / a.W, st_w = 64 % a.W;
+  const int tap = nb_col / a.C, ci = nb_col % a.C, dh = tap / a.KS - a.P, dw = tap % a.KS - a.P;
+  const int HW = a.OH * a.OW;  // output-pixel coordinates (the GEMM's K axis)
+  const int st_n = 64 / HW, st_h = (64 % HW) / a.OW, st_w = 64 % a.OW;
   int pn[2], ph[2], pw[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int p = pbeg + kk0 + 32 * u;
-    pw[u] = p % a.W;
-    ph[u] = (p / a.W) % a.H;
+    pw[u] = p % a.OW;
+    ph[u] = (p / a.OW) % a.OH;
     pn[u] = p / HW;
   }
   auto load = [&](int p0) {
@@ -416,18 +418,18 @@ __global__ void __launch_bounds__(NT) conv3x3_wgrad_kernel(WgArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int ih = ph[u] + dh, iw = pw[u] + dw;
+      const int ih = ph[u] * a.S + dh, iw = pw[u] * a.S + dw;
       const bool ok = pn[u] < a.Nb && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
       vb[u] = *reinterpret_cast<const u16x8*>(a.x + (ok ? (((size_t)pn[u] * a.H + ih) * a.W + iw) * a.C + ci : 0));
       okb |= ok ? (1u << u) : 0u;
       pw[u] += st_w;  // next call loads the rows 64 pixels further
-      if (pw[u] >= a.W) {
-        pw[u] -= a.W;
+      if (pw[u] >= a.OW) {
+        pw[u] -= a.OW;
         ++ph[u];
       }
       ph[u] += st_h;
-      if (ph[u] >= a.H) {
-        ph[u] -= a.H;
+      if (ph[u] >= a.OH) {
+        ph[u] -= a.OH;
         ++pn[u];
       }
       pn[u] += st_n;
@@ -492,8 +494,8 @@ __global__ void __launch_bounds__(NT) conv3x3_wgrad_kernel(WgArgs a) {
 // gw[co][ci][kh][kw] (bf16, torch layout, accumulated) += sum_s slab[s][co][tap][ci]: the slabs are
 // read in their own order, 4 channels per thread (coalesced 16-B loads), the 4 results scattered
 __global__ void __launch_bounds__(256) conv_wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Co,
-                                                                int C, u16* __restrict__ gw) {
-  const int64_t n = (int64_t)Co * 9 * C, n4 = n / 4;
+                                                                int C, int T, u16* __restrict__ gw) {
+  const int64_t n = (int64_t)Co * T * C, n4 = n / 4;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 acc = reinterpret_cast<const float4*>(slab)[i];
     for (int k = 1; k < splits; ++k) {
@@ -506,11 +508,11 @@ __global__ void __launch_bounds__(256) conv_wgrad_reduce_kernel(const float* __r
     const int64_t e = 4 * i;  // slab layout [co][tap][ci]
     const int ci = (int)(e % C);
     const int64_t r = e / C;
-    const int tap = (int)(r % 9), co = (int)(r / 9);
+    const int tap = (int)(r % T), co = (int)(r / T);
     const float sv[4] = {acc.x, acc.y, acc.z, acc.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int64_t dst = ((int64_t)co * C + ci + j) * 9 + tap;
+      const int64_t dst = ((int64_t)co * C + ci + j) * T + tap;
       gw[dst] = f2bf(bf2f(gw[dst]) + sv[j]);
     }
   }
@@ -660,6 +662,11 @@ void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int
   a.C = C;
   a.Co = Co;
   a.M = Nb * H * W;
+  a.OH = H;
+  a.OW = W;
+  a.S = 1;
+  a.KS = 3;
+  a.P = 1;
   a.tiles_m = (a.M + BM - 1) / BM;
   static const int engine = [] {  // SDML_CONV_FWD=im2col forces the im2col kernel (A/B tuning)
     const char* e = std::getenv("SDML_CONV_FWD");
@@ -700,6 +707,40 @@ void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int
   }
 }
 
+int conv_out_size(int in, int ks, int stride, int pad) { return (in + 2 * pad - ks) / stride + 1; }
+
+bool conv_general_supported(int C, int Co, int ks, int stride, int pad) {
+  return C >= 64 && Co >= 64 && C % 64 == 0 && Co % 64 == 0 && ((ks == 3 && pad == 1) || (ks == 1 && pad == 0)) &&
+         (stride == 1 || stride == 2);
+}
+
+void conv_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co, int ks, int stride,
+                   int pad, hipStream_t stream) {
+  ConvArgs a;
+  a.x = static_cast<const u16*>(x);
+  a.w = static_cast<const u16*>(wt);
+  a.y = static_cast<u16*>(y);
+  a.Nb = Nb;
+  a.H = H;
+  a.W = W;
+  a.C = C;
+  a.Co = Co;
+  a.OH = conv_out_size(H, ks, stride, pad);
+  a.OW = conv_out_size(W, ks, stride, pad);
+  a.S = stride;
+  a.KS = ks;
+  a.P = pad;
+  a.M = Nb * a.OH * a.OW;
+  a.tiles_m = (a.M + BM - 1) / BM;
+  if (Co % 128 == 0 && a.tiles_m * (Co / 128) >= 160) {
+    a.tiles_n = Co / 128;
+    hipLaunchKernelGGL(conv3x3_fwd_kernel<128>, dim3(a.tiles_m * a.tiles_n), dim3(NT), 0, stream, a);
+  } else {
+    a.tiles_n = Co / 64;
+    hipLaunchKernelGGL(conv3x3_fwd_kernel<64>, dim3(a.tiles_m * a.tiles_n), dim3(NT), 0, stream, a);
+  }
+}
+
 static int wgrad_rows(int Co) {
   static const bool rows64 = [] {  // SDML_CONV_WG_ROWS64=0: 128-row tiles (half idle) for Cout = 64 too
     const char* e = std::getenv("SDML_CONV_WG_ROWS64");
@@ -708,27 +749,33 @@ static int wgrad_rows(int Co) {
   return Co % 128 == 0 || !rows64 ? 128 : 64;
 }
 
-int conv3x3_wgrad_splits(int Nb, int H, int W, int C, int Co) {
+static int wgrad_splits(int M, int KT, int Co) {
   // the pixel range is split until the grid reaches ~two workgroups per CU (64 KB LDS, <= 128 VGPRs)
   static const int target = [] {
     const char* e = std::getenv("SDML_CONV_WG_BLOCKS");
     return e ? std::max(1, std::atoi(e)) : 512;
   }();
   const int tr = wgrad_rows(Co);
-  const int tiles = ((Co + tr - 1) / tr) * ((9 * C + 127) / 128);
-  const int M = Nb * H * W;
+  const int tiles = ((Co + tr - 1) / tr) * ((KT + 127) / 128);
   int s = target / tiles;
   const int max_by_m = M / (8 * 64);  // >= 8 K-steps per workgroup
   if (s > max_by_m) s = max_by_m;
   return s < 1 ? 1 : s;
 }
 
-size_t conv3x3_wgrad_workspace_floats(int Nb, int H, int W, int C, int Co) {
-  return (size_t)conv3x3_wgrad_splits(Nb, H, W, C, Co) * Co * 9 * C;
+int conv3x3_wgrad_splits(int Nb, int H, int W, int C, int Co) { return wgrad_splits(Nb * H * W, 9 * C, Co); }
+
+size_t conv_wgrad_workspace_floats(int Nb, int H, int W, int C, int Co, int ks, int stride, int pad) {
+  const int M = Nb * conv_out_size(H, ks, stride, pad) * conv_out_size(W, ks, stride, pad);
+  return (size_t)wgrad_splits(M, ks * ks * C, Co) * Co * ks * ks * C;
 }
 
-void conv3x3_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* workspace, int Nb, int H, int W, int C,
-                        int Co, hipStream_t stream) {
+size_t conv3x3_wgrad_workspace_floats(int Nb, int H, int W, int C, int Co) {
+  return conv_wgrad_workspace_floats(Nb, H, W, C, Co, 3, 1, 1);
+}
+
+void conv_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* workspace, int Nb, int H, int W, int C,
+                     int Co, int ks, int stride, int pad, hipStream_t stream) {
   WgArgs a;
   a.dy = static_cast<const u16*>(dy);
   a.x = static_cast<const u16*>(x);
@@ -738,8 +785,14 @@ void conv3x3_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* wo
   a.W = W;
   a.C = C;
   a.Co = Co;
-  a.M = Nb * H * W;
-  int s = conv3x3_wgrad_splits(Nb, H, W, C, Co);
+  a.OH = conv_out_size(H, ks, stride, pad);
+  a.OW = conv_out_size(W, ks, stride, pad);
+  a.S = stride;
+  a.KS = ks;
+  a.P = pad;
+  a.M = Nb * a.OH * a.OW;
+  const int T = ks * ks;
+  int s = wgrad_splits(a.M, T * C, Co);
   int pps = (a.M + s - 1) / s;
   pps = (pps + 63) / 64 * 64;
   s = (a.M + pps - 1) / pps;
@@ -747,15 +800,20 @@ void conv3x3_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* wo
   a.splits = s;
   const int tr = wgrad_rows(Co);
   a.tiles_m = (Co + tr - 1) / tr;
-  a.tiles_n = (9 * C + 127) / 128;
+  a.tiles_n = (T * C + 127) / 128;
   if (tr == 128)
     hipLaunchKernelGGL(conv3x3_wgrad_kernel<128>, dim3(a.tiles_m * a.tiles_n * s), dim3(NT), 0, stream, a);
   else
     hipLaunchKernelGGL(conv3x3_wgrad_kernel<64>, dim3(a.tiles_m * a.tiles_n * s), dim3(NT), 0, stream, a);
-  const int64_t n4 = (int64_t)Co * 9 * C / 4;
+  const int64_t n4 = (int64_t)Co * T * C / 4;
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, workspace, s, Co, C,
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, workspace, s, Co, C, T,
                      static_cast<u16*>(gw_torch));
+}
+
+void conv3x3_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* workspace, int Nb, int H, int W, int C,
+                        int Co, hipStream_t stream) {
+  conv_wgrad_bf16(dy, x, gw_torch, workspace, Nb, H, W, C, Co, 3, 1, 1, stream);
 }
 
 // ---- stem (one input channel) ----------------------------------------------------------------

@@ -135,6 +135,17 @@ bool conv3x3_bf16_supported(int C, int Co);
 void conv3x3_weight_transform_bf16(const void* w_torch, void* fwd, void* dgrad, int Co, int C, hipStream_t stream);
 void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co, hipStream_t stream);
 // gw_torch [Co][C][3][3] bf16 += dw; workspace: conv3x3_wgrad_workspace_floats(...) fp32
+// general bf16 NHWC convolution on the implicit-GEMM kernels: kernel 3 (pad 1) or 1 (pad 0), stride 1
+// or 2, C and Co multiples of 64. Forward (im2col kernel; wt = [Co][ks*ks][C]) and weight gradient
+// (accumulated into the bf16 torch-layout [Co][C][ks][ks] gradient); the input gradient of strided
+// convolutions stays with MIOpen.
+int conv_out_size(int in, int ks, int stride, int pad);
+bool conv_general_supported(int C, int Co, int ks, int stride, int pad);
+void conv_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co, int ks, int stride,
+                   int pad, hipStream_t stream);
+size_t conv_wgrad_workspace_floats(int Nb, int H, int W, int C, int Co, int ks, int stride, int pad);
+void conv_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* workspace, int Nb, int H, int W, int C,
+                     int Co, int ks, int stride, int pad, hipStream_t stream);
 // stem convolution with ONE input channel, 3x3 / stride 1 / pad 1, bf16: x [N][H][W], w [Co][1][3][3],
 // y NHWC [N][H][W][Co]; weight gradient accumulated into the bf16 [Co][1][3][3] gradient
 bool conv_c1_supported(int Co);

@@ -320,6 +320,37 @@ static void check_bn_vec(const c10::optional<torch::Tensor>& t, int64_t C, const
                 ": contiguous bf16 [C] expected");
 }
 
+// general convolution (kernel 3 pad 1 / kernel 1 pad 0, stride 1 or 2), channels-last bf16; wt from
+// conv3x3_weight_bf16(w, false) for 3x3 or the [Co][C][1][1] weight itself for 1x1
+torch::Tensor conv_fwd_bf16(torch::Tensor x, torch::Tensor wt, int64_t ks, int64_t stride, int64_t pad) {
+  check_cl_bf16(x, "x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), Co = wt.size(0);
+  TORCH_CHECK(wt.is_contiguous() && wt.scalar_type() == torch::kBFloat16 && wt.numel() == Co * ks * ks * C,
+              "conv_fwd_bf16: wt must be a contiguous [Co][ks*ks][C] bf16 tensor");
+  TORCH_CHECK(sdml::conv_general_supported(C, Co, ks, stride, pad), "conv_fwd_bf16: unsupported geometry");
+  const int64_t OH = sdml::conv_out_size(H, ks, stride, pad), OW = sdml::conv_out_size(W, ks, stride, pad);
+  auto y = torch::empty({N, Co, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (N * OH * OW > 0)
+    sdml::conv_fwd_bf16(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, C, Co, ks, stride, pad, cur_stream());
+  return y;
+}
+
+void conv_wgrad_bf16_(torch::Tensor dy, torch::Tensor x, torch::Tensor gw, int64_t stride, int64_t pad) {
+  check_cl_bf16(dy, "dy");
+  check_cl_bf16(x, "x");
+  TORCH_CHECK(gw.is_contiguous() && gw.scalar_type() == torch::kBFloat16 && gw.dim() == 4 && gw.size(2) == gw.size(3) &&
+              gw.size(0) == dy.size(1) && gw.size(1) == x.size(1), "conv_wgrad_bf16_: gw [Co][C][k][k] bf16");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), Co = dy.size(1), ks = gw.size(2);
+  TORCH_CHECK(sdml::conv_general_supported(C, Co, ks, stride, pad), "conv_wgrad_bf16_: unsupported geometry");
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == sdml::conv_out_size(H, ks, stride, pad) &&
+              dy.size(3) == sdml::conv_out_size(W, ks, stride, pad), "conv_wgrad_bf16_: shape mismatch");
+  if (dy.numel() == 0) return;
+  auto ws = torch::empty({(int64_t)sdml::conv_wgrad_workspace_floats(N, H, W, C, Co, ks, stride, pad)},
+                         x.options().dtype(torch::kFloat32).memory_format(at::MemoryFormat::Contiguous));
+  sdml::conv_wgrad_bf16(dy.data_ptr(), x.data_ptr(), gw.data_ptr(), ws.data_ptr<float>(), N, H, W, C, Co, ks, stride,
+                        pad, cur_stream());
+}
+
 // stem convolution, one input channel: y (channels-last [N][Co][H][W]) = conv3x3(x [N][1][H][W], w)
 torch::Tensor conv_c1_fwd_bf16(torch::Tensor x, torch::Tensor w) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 4 && x.size(1) == 1 && x.is_contiguous(),
@@ -825,6 +856,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_weights_bf16", &conv3x3_weights_bf16, "3x3 conv weight -> (forward, dgrad) kernel layouts");
   m.def("conv3x3_fwd_bf16", &conv3x3_fwd_bf16, "3x3 stride-1 pad-1 conv, channels-last bf16 (implicit GEMM)");
   m.def("conv3x3_wgrad_bf16_", &conv3x3_wgrad_bf16_, "3x3 conv weight gradient, accumulated into bf16 grad");
+  m.def("conv_fwd_bf16", &conv_fwd_bf16, "conv (3x3 pad 1 / 1x1, stride 1|2), channels-last bf16 (implicit GEMM)");
+  m.def("conv_wgrad_bf16_", &conv_wgrad_bf16_, "conv weight gradient (3x3 / 1x1, stride 1|2), accumulated");
   m.def("conv_c1_fwd_bf16", &conv_c1_fwd_bf16, "stem 3x3 conv with one input channel -> channels-last bf16");
   m.def("conv_c1_wgrad_bf16_", &conv_c1_wgrad_bf16_, "stem conv weight gradient, accumulated into bf16 grad");
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm (+residual)(+ReLU), channels-last bf16");

@@ -7,10 +7,11 @@ The 8 BasicBlocks are the cut units: stage k gets ``8 / num_stages`` consecutive
 the stem rides with the first stage and pool+fc with the last.
 
 BatchNorm runs per micro-batch (GPipe semantics). ``dtype=bf16`` runs the stages in bf16
-channels-last (fp32 master weights in the optimizer): the twelve stride-1 3x3 convolutions (88 %
-of the MACs) then run on the hand-written implicit-GEMM kernels of csrc/kernels/conv_bf16.hip
-(forward, input and weight gradients); the stem, the stride-2 and the 1x1 shortcut convolutions
-and the fp32 default use MIOpen through PyTorch.
+channels-last (fp32 master weights in the optimizer): every convolution then runs on the
+hand-written kernels of csrc/kernels/conv_bf16.hip — the twelve stride-1 3x3 convolutions (88 % of
+the MACs: forward, input and weight gradients), the stride-2 3x3 and 1x1 shortcut convolutions
+(forward and weight gradient; input gradient on MIOpen) and the one-channel stem — and every
+BatchNorm(+residual)(+ReLU) on csrc/kernels/batchnorm_nhwc.hip. The fp32 default uses MIOpen.
 """
 from __future__ import annotations
 
@@ -45,7 +46,7 @@ class BasicBlock(nn.Module):
         # conv (HIP implicit GEMM when stride-1 bf16 NHWC) -> BN+ReLU / BN+residual+ReLU in one
         # pass each (ops/conv.py; PyTorch ops elsewhere)
         out = conv_ops.batch_norm(self.bn1, conv_ops.conv2d(self.conv1, x), relu=True)
-        sc = x if self.shortcut is None else conv_ops.batch_norm(self.shortcut[1], self.shortcut[0](x))
+        sc = x if self.shortcut is None else conv_ops.batch_norm(self.shortcut[1], conv_ops.conv2d(self.shortcut[0], x))
         return conv_ops.batch_norm(self.bn2, conv_ops.conv2d(self.conv2, out), res=sc, relu=True)
 
 

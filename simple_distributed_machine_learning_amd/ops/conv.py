@@ -2,9 +2,10 @@
 implicit-GEMM kernels of csrc/kernels/conv_bf16.hip (forward, input gradient = the forward kernel
 with flipped/transposed weights, weight gradient accumulated into ``weight.grad`` in place).
 
-Used by the ResNet-18-style stages (models/resnet.py) for their twelve stride-1 3x3 convolutions
-and the one-channel stem when they run in bf16 channels-last; the stride-2 and 1x1 shortcut
-convolutions (and every other dtype/layout) go through ``F.conv2d``.
+Used by the ResNet-18-style stages (models/resnet.py) when they run in bf16 channels-last: the
+twelve stride-1 3x3 convolutions, the one-channel stem, and the stride-2 3x3 / 1x1 shortcut
+convolutions (forward and weight gradient; their input gradient stays on MIOpen). Every other
+dtype/layout goes through ``F.conv2d``.
 """
 from __future__ import annotations
 
@@ -54,6 +55,49 @@ def hip_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
 
 
+class _ConvGeneralFn(torch.autograd.Function):
+    """Strided 3x3 / 1x1 convolution (the downsampling blocks): forward and weight gradient on the
+    im2col implicit-GEMM kernels; the input gradient (a transposed strided convolution) on MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, pad):
+        K = kernels()
+        ks = w.shape[2]
+        wt = K.conv3x3_weight_bf16(w, False) if ks == 3 else w  # [Co][C][1][1] is already [Co][1][C]
+        y = K.conv_fwd_bf16(x, wt, ks, stride, pad)
+        ctx.save_for_backward(x)
+        ctx.w, ctx.stride, ctx.pad = w, stride, pad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        w, st, pd = ctx.w, ctx.stride, ctx.pad
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(dy, x, w, None, [st, st], [pd, pd], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        gw = None
+        if ctx.needs_input_grad[1]:
+            if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
+                kernels().conv_wgrad_bf16_(dy, x, w.grad, st, pd)
+            else:
+                gw = torch.zeros_like(w)
+                kernels().conv_wgrad_bf16_(dy, x, gw, st, pd)
+        return dx, gw, None, None
+
+
+def general_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    w = conv.weight
+    ks, st, pd = tuple(conv.kernel_size), tuple(conv.stride), tuple(conv.padding)
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and conv.bias is None and w.is_contiguous()
+            and ks in ((3, 3), (1, 1)) and pd == ((ks[0] - 1) // 2,) * 2 and st in ((1, 1), (2, 2))
+            and tuple(conv.dilation) == (1, 1) and conv.groups == 1
+            and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
+
+
 class _StemConvFn(torch.autograd.Function):
     """3x3 convolution of a one-channel image (the MNIST stem): streaming kernels, NHWC output."""
 
@@ -91,10 +135,13 @@ def stem_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
 
 
 def conv2d(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
-    """``conv(x)``, on the HIP kernels where they apply (implicit GEMM for 64-multiple channel
-    counts, the streaming stem kernels for a one-channel input)."""
+    """``conv(x)``, on the HIP kernels where they apply: stride-1 3x3 on the halo kernel, strided
+    3x3 / 1x1 on the im2col kernel (input gradient on MIOpen), the streaming stem kernels for a
+    one-channel input."""
     if hip_eligible(x, conv):
         return _Conv3x3Fn.apply(x, conv.weight)
+    if general_eligible(x, conv):
+        return _ConvGeneralFn.apply(x, conv.weight, conv.stride[0], conv.padding[0])
     if stem_eligible(x, conv):
         return _StemConvFn.apply(x, conv.weight)
     return conv(x)

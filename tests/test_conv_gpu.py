@@ -53,6 +53,31 @@ def test_conv3x3_fwd_dgrad_wgrad(N, C, Co, H, W):
     assert ((gw.float() - want).abs() <= 2 ** -7 * sw).all()
 
 
+@pytest.mark.parametrize("N,C,Co,H,W,ks,st", [(4, 64, 128, 28, 28, 3, 2), (3, 128, 256, 14, 14, 3, 2),
+                                               (2, 256, 512, 7, 7, 3, 2), (4, 64, 128, 28, 28, 1, 2),
+                                               (2, 256, 512, 7, 7, 1, 2), (3, 64, 64, 9, 11, 1, 1),
+                                               (2, 128, 64, 9, 7, 3, 2)])
+def test_strided_and_pointwise_conv(N, C, Co, H, W, ks, st):
+    g = torch.Generator(device="cpu").manual_seed(N + C + Co + H + ks + st)
+    pd = (ks - 1) // 2
+    conv = torch.nn.Conv2d(C, Co, ks, st, pd, bias=False).to(DEV, torch.bfloat16)
+    x = cl(torch.randn(N, C, H, W, generator=g).to(DEV, torch.bfloat16)).requires_grad_(True)
+    assert conv_ops.general_eligible(x, conv)
+    y = conv_ops.conv2d(conv, x)
+    yr = F.conv2d(x.detach().float(), conv.weight.detach().float(), stride=st, padding=pd)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    scale = F.conv2d(x.detach().float().abs(), conv.weight.detach().float().abs(), stride=st, padding=pd) + 1e-3
+    assert ((y.float() - yr).abs() <= 2 ** -7 * scale).all()
+    dy = cl(torch.randn(yr.shape, generator=g).to(DEV, torch.bfloat16))
+    y.backward(dy)
+    gwr = torch.nn.grad.conv2d_weight(x.detach().float(), conv.weight.shape, dy.float(), stride=st, padding=pd)
+    sw = torch.nn.grad.conv2d_weight(x.detach().float().abs(), conv.weight.shape, dy.float().abs(), stride=st,
+                                     padding=pd) + 1e-3
+    assert ((conv.weight.grad.float() - gwr).abs() <= 2 ** -7 * sw).all()
+    dxr = torch.nn.grad.conv2d_input(x.shape, conv.weight.detach().float(), dy.float(), stride=st, padding=pd)
+    torch.testing.assert_close(x.grad.float(), dxr, rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("N,Co,H,W", [(4, 64, 28, 28), (3, 32, 5, 9)])
 def test_stem_conv_one_channel(N, Co, H, W):
     g = torch.Generator(device="cpu").manual_seed(N + Co + H)

@@ -491,30 +491,51 @@ __global__ void __launch_bounds__(NT) conv3x3_wgrad_kernel(WgArgs a) {
     }
 }
 
-// gw[co][ci][kh][kw] (bf16, torch layout, accumulated) += sum_s slab[s][co][tap][ci]: the slabs are
-// read in their own order, 4 channels per thread (coalesced 16-B loads), the 4 results scattered
-__global__ void __launch_bounds__(256) conv_wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Co,
-                                                                int C, int T, u16* __restrict__ gw) {
+// gw[co][ci][kh][kw] (bf16, torch layout, accumulated) += sum_s slab[s][co][tap][ci]. A block is 32
+// float4 outputs (slab order, coalesced) x 8 split groups: group g sums splits g, g + 8, ... in
+// order, then the 8 partials are added in fixed order through LDS (deterministic); the 4 results
+// of a thread are scattered to the torch layout.
+constexpr int RD_OUT = 32, RD_GRP = 8;
+
+__global__ void __launch_bounds__(RD_OUT * RD_GRP) conv_wgrad_reduce_kernel(const float* __restrict__ slab, int splits,
+                                                                           int Co, int C, int T, u16* __restrict__ gw) {
+  __shared__ float4 red[RD_GRP][RD_OUT];
   const int64_t n = (int64_t)Co * T * C, n4 = n / 4;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    float4 acc = reinterpret_cast<const float4*>(slab)[i];
-    for (int k = 1; k < splits; ++k) {
-      const float4 v = reinterpret_cast<const float4*>(slab + (size_t)k * n)[i];
-      acc.x += v.x;
-      acc.y += v.y;
-      acc.z += v.z;
-      acc.w += v.w;
-    }
-    const int64_t e = 4 * i;  // slab layout [co][tap][ci]
-    const int ci = (int)(e % C);
-    const int64_t r = e / C;
-    const int tap = (int)(r % T), co = (int)(r / T);
-    const float sv[4] = {acc.x, acc.y, acc.z, acc.w};
+  const int o = threadIdx.x % RD_OUT, g = threadIdx.x / RD_OUT;
+  for (int64_t base = (int64_t)blockIdx.x * RD_OUT; base < n4; base += (int64_t)gridDim.x * RD_OUT) {
+    const int64_t i = base + o;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < n4)
+      for (int k = g; k < splits; k += RD_GRP) {
+        const float4 v = reinterpret_cast<const float4*>(slab + (size_t)k * n)[i];
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+    red[g][o] = acc;
+    __syncthreads();
+    if (g == 0 && i < n4) {
+      float4 t = red[0][o];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t dst = ((int64_t)co * C + ci + j) * T + tap;
-      gw[dst] = f2bf(bf2f(gw[dst]) + sv[j]);
+      for (int gg = 1; gg < RD_GRP; ++gg) {
+        t.x += red[gg][o].x;
+        t.y += red[gg][o].y;
+        t.z += red[gg][o].z;
+        t.w += red[gg][o].w;
+      }
+      const int64_t e = 4 * i;  // slab layout [co][tap][ci]
+      const int ci = (int)(e % C);
+      const int64_t r = e / C;
+      const int tap = (int)(r % T), co = (int)(r / T);
+      const float sv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t dst = ((int64_t)co * C + ci + j) * T + tap;
+        gw[dst] = f2bf(bf2f(gw[dst]) + sv[j]);
+      }
     }
+    __syncthreads();
   }
 }
 
@@ -806,8 +827,8 @@ void conv_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* works
   else
     hipLaunchKernelGGL(conv3x3_wgrad_kernel<64>, dim3(a.tiles_m * a.tiles_n * s), dim3(NT), 0, stream, a);
   const int64_t n4 = (int64_t)Co * T * C / 4;
-  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, workspace, s, Co, C, T,
+  const int blocks = (int)std::min<int64_t>((n4 + RD_OUT - 1) / RD_OUT, 8192);
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(RD_OUT * RD_GRP), 0, stream, workspace, s, Co, C, T,
                      static_cast<u16*>(gw_torch));
 }
 

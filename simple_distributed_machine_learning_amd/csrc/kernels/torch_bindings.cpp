@@ -539,12 +539,12 @@ void sgd_momentum_mixed_(torch::Tensor master, torch::Tensor p, torch::Tensor g,
   TORCH_CHECK(p.is_cuda() && g.is_cuda() && p.scalar_type() == torch::kBFloat16 && g.scalar_type() == torch::kBFloat16,
               "sgd_mixed: p/g must be bf16 device tensors");
   TORCH_CHECK(p.is_contiguous() && g.is_contiguous(), "sgd_mixed: contiguous");
-  TORCH_CHECK(p.numel() == master.numel() && g.numel() == master.numel() && p.numel() % 4 == 0, "sgd_mixed: sizes");
+  TORCH_CHECK(p.numel() == master.numel() && g.numel() == master.numel() && p.numel() % 8 == 0,
+              "sgd_mixed: sizes (a multiple of 8: the flat buffers pad every view to 64 elements)");
   TORCH_CHECK(momentum == 0 || buf.numel() == p.numel(), "sgd_mixed: momentum buffer size");
   auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  TORCH_CHECK(al(master.data_ptr()) && al(buf.data_ptr()) && (reinterpret_cast<uintptr_t>(p.data_ptr()) & 7) == 0 &&
-                  (reinterpret_cast<uintptr_t>(g.data_ptr()) & 7) == 0,
-              "sgd_mixed: alignment");
+  TORCH_CHECK(al(master.data_ptr()) && al(buf.data_ptr()) && al(p.data_ptr()) && al(g.data_ptr()),
+              "sgd_mixed: 16-B alignment");
   sdml::sgd_momentum_mixed(master.data_ptr<float>(), p.data_ptr(), g.data_ptr(), buf.data_ptr<float>(), p.numel(),
                            (float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, first, zero_grad,
                            cur_stream());

@@ -100,8 +100,9 @@ void synth_mnist(uint64_t seed, int64_t start, int64_t n, int H, int W, int mode
 void cross_entropy_bf16(const void* logits, const int64_t* target, int rows, int V, int ld, float scale,
                         int ignore_index, float* row_loss, float* row_ok, void* dlogits, hipStream_t stream);
 // LayerNorm over the last dim D (D % 8 == 0, D <= 4096); saves fp32 mean/rstd per row
+// res/xs non-null: fused residual add, xs = x + res is stored and normalised (one pass)
 void layernorm_fwd_bf16(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int rows,
-                        int D, float eps, hipStream_t stream);
+                        int D, float eps, hipStream_t stream, const void* res = nullptr, void* xs = nullptr);
 // dx (bf16) and dwdb_acc[0:D] += dw, dwdb_acc[D:2D] += db (fp32); workspace: blocks * 2D floats
 int layernorm_bwd_blocks(int rows);
 void layernorm_bwd_bf16(const void* x, const void* w, const void* gy, const float* mean, const float* rstd, void* dx,
@@ -109,8 +110,10 @@ void layernorm_bwd_bf16(const void* x, const void* w, const void* gy, const floa
 
 // same, but dw/db are added straight into the bf16 parameter gradients gw/gb (no fp32 copy,
 // no separate accumulate kernel)
+// gadd non-null: dx also gets the residual-path gradient of a fused add + LayerNorm
 void layernorm_bwd_bf16_accum(const void* x, const void* w, const void* gy, const float* mean, const float* rstd,
-                              void* dx, float* workspace, void* gw, void* gb, int rows, int D, hipStream_t stream);
+                              void* dx, float* workspace, void* gw, void* gb, int rows, int D, hipStream_t stream,
+                              const void* gadd = nullptr);
 // bias gradient of a bf16 linear layer: gb[n] (bf16) += sum_m gy[m][n]; workspace fp32
 // [bias_grad_blocks(M) * N]. Deterministic (fixed-order partial sums).
 int bias_grad_blocks(int M);

@@ -599,6 +599,26 @@ std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> layernorm_fwd_bf16(torch
   return {y, mean, rstd};
 }
 
+// fused residual add + LayerNorm: xs = x + h (bf16, exactly the unfused add), y = LN(xs);
+// returns (xs, y, mean, rstd)
+std::tuple<torch::Tensor, torch::Tensor, torch::Tensor, torch::Tensor> add_layernorm_fwd_bf16(
+    torch::Tensor x, torch::Tensor h, torch::Tensor w, torch::Tensor b, double eps) {
+  check_bf16_cuda(x, "x");
+  check_bf16_cuda(h, "h");
+  check_bf16_cuda(w, "w");
+  check_bf16_cuda(b, "b");
+  TORCH_CHECK(x.sizes() == h.sizes(), "add_layernorm: x / h shape mismatch");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && D <= 4096 && w.numel() == D && b.numel() == D, "layernorm: D % 8 == 0, D <= 4096");
+  auto xs = torch::empty_like(x);
+  auto y = torch::empty_like(x);
+  auto f = x.options().dtype(torch::kFloat32);
+  auto mean = torch::empty({rows}, f), rstd = torch::empty({rows}, f);
+  sdml::layernorm_fwd_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), mean.data_ptr<float>(),
+                           rstd.data_ptr<float>(), rows, D, (float)eps, cur_stream(), h.data_ptr(), xs.data_ptr());
+  return {xs, y, mean, rstd};
+}
+
 // returns (dx bf16, dw fp32 [D], db fp32 [D])
 std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> layernorm_bwd_bf16(torch::Tensor x, torch::Tensor w,
                                                                           torch::Tensor gy, torch::Tensor mean,
@@ -622,7 +642,8 @@ std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> layernorm_bwd_bf16(torch
 
 // layernorm backward accumulating dw/db into bf16 parameter grads; returns dx
 torch::Tensor layernorm_bwd_bf16_accum(torch::Tensor x, torch::Tensor w, torch::Tensor gy, torch::Tensor mean,
-                                       torch::Tensor rstd, torch::Tensor gw, torch::Tensor gb) {
+                                       torch::Tensor rstd, torch::Tensor gw, torch::Tensor gb,
+                                       c10::optional<torch::Tensor> gadd) {
   check_bf16_cuda(x, "x");
   check_bf16_cuda(w, "w");
   check_bf16_cuda(gy, "gy");
@@ -634,11 +655,17 @@ torch::Tensor layernorm_bwd_bf16_accum(torch::Tensor x, torch::Tensor w, torch::
   TORCH_CHECK(gy.sizes() == x.sizes() && mean.numel() == rows && rstd.numel() == rows && w.numel() == D &&
                   gw.numel() == D && gb.numel() == D,
               "ln bwd shapes");
+  const void* ga = nullptr;
+  if (gadd.has_value() && gadd->defined()) {
+    check_bf16_cuda(*gadd, "gadd");
+    TORCH_CHECK(gadd->sizes() == x.sizes() && gadd->is_contiguous(), "ln bwd: gadd must match x (contiguous)");
+    ga = gadd->data_ptr();
+  }
   auto dx = torch::empty_like(x);
   auto ws = torch::empty({(int64_t)sdml::layernorm_bwd_blocks(rows) * 2 * D}, x.options().dtype(torch::kFloat32));
   sdml::layernorm_bwd_bf16_accum(x.data_ptr(), w.data_ptr(), gy.data_ptr(), mean.data_ptr<float>(),
                                  rstd.data_ptr<float>(), dx.data_ptr(), ws.data_ptr<float>(), gw.data_ptr(),
-                                 gb.data_ptr(), rows, D, cur_stream());
+                                 gb.data_ptr(), rows, D, cur_stream(), ga);
   return dx;
 }
 
@@ -840,7 +867,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cross_entropy_bf16", &cross_entropy_bf16, "vocab cross-entropy on bf16 logits (+ dlogits)");
   m.def("layernorm_fwd_bf16", &layernorm_fwd_bf16, "LayerNorm forward (bf16, fp32 stats)");
   m.def("layernorm_bwd_bf16", &layernorm_bwd_bf16, "LayerNorm backward (bf16)");
-  m.def("layernorm_bwd_bf16_accum", &layernorm_bwd_bf16_accum, "LayerNorm backward, dw/db added into bf16 grads");
+  m.def("layernorm_bwd_bf16_accum", &layernorm_bwd_bf16_accum, "LayerNorm backward, dw/db added into bf16 grads",
+        py::arg("x"), py::arg("w"), py::arg("gy"), py::arg("mean"), py::arg("rstd"), py::arg("gw"), py::arg("gb"),
+        py::arg("gadd") = py::none());
+  m.def("add_layernorm_fwd_bf16", &add_layernorm_fwd_bf16, "fused residual add + LayerNorm forward (bf16)");
   m.def("bias_grad_bf16_", &bias_grad_bf16_, "gb += column sums of gy (bf16, deterministic)");
   m.def("attention_fwd", &attention_fwd, "causal flash attention forward (bf16, d=64)");
   m.def("attention_bwd", &attention_bwd, "causal flash attention backward (bf16, d=64)");

@@ -231,9 +231,12 @@ __global__ void __launch_bounds__(CER_T) ce_reg_kernel(const u16* __restrict__ l
 constexpr int LN_T = 256;
 // LN_MAXV = 16-B chunks per lane (template): D <= 64 lanes * 8 elems * LN_MAXV
 
+// res != nullptr: the row is first the residual sum xs = bf16(x + res) (stored to xs, exactly the
+// unfused bf16 add), and the statistics are those of xs — one pass instead of add + LayerNorm
 template <int LN_MAXV>
-__global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ w,
-                                                      const u16* __restrict__ b, u16* __restrict__ y,
+__global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const u16* __restrict__ x, const u16* __restrict__ res,
+                                                      const u16* __restrict__ w, const u16* __restrict__ b,
+                                                      u16* __restrict__ xs, u16* __restrict__ y,
                                                       float* __restrict__ mean, float* __restrict__ rstd, int rows,
                                                       int D, float eps) {
   const int lane = threadIdx.x & 63;
@@ -247,6 +250,12 @@ __global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const u16* __restrict__ x,
       int ch = lane + 64 * c;
       if (ch < nch) {
         v[c] = *reinterpret_cast<const u16x8*>(xr + 8 * ch);
+        if (res) {
+          const u16x8 rv = *reinterpret_cast<const u16x8*>(res + (size_t)row * D + 8 * ch);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[c][e] = f2bf(bf2f(v[c][e]) + bf2f(rv[e]));
+          *reinterpret_cast<u16x8*>(xs + (size_t)row * D + 8 * ch) = v[c];
+        }
 #pragma unroll
         for (int e = 0; e < 8; ++e) sum += bf2f(v[c][e]);
       }
@@ -284,12 +293,13 @@ __global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const u16* __restrict__ x,
   }
 }
 
-// dx = rstd * (g*w - mean(g*w) - xhat * mean(g*w*xhat)); dw += g*xhat; db += g (per-block slabs)
+// dx = rstd * (g*w - mean(g*w) - xhat * mean(g*w*xhat)) (+ gadd: the residual-path gradient of
+// a fused add + LayerNorm, summed in fp32 and rounded once); dw += g*xhat; db += g (per-block slabs)
 template <int LN_MAXV>
 __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const u16* __restrict__ x, const u16* __restrict__ w,
                                                       const u16* __restrict__ gy, const float* __restrict__ mean,
-                                                      const float* __restrict__ rstd, u16* __restrict__ dx,
-                                                      float* __restrict__ part, int rows, int D) {
+                                                      const float* __restrict__ rstd, const u16* __restrict__ gadd,
+                                                      u16* __restrict__ dx, float* __restrict__ part, int rows, int D) {
   const int lane = threadIdx.x & 63, wv_id = threadIdx.x >> 6;
   const int nch = D / 8;
   // per-thread partial dW/dB for the chunks this lane owns (reduced over the block's rows)
@@ -331,11 +341,13 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const u16* __restrict__ x,
       int ch = lane + 64 * c;
       if (ch < nch) {
         u16x8 wv = *reinterpret_cast<const u16x8*>(w + 8 * ch);
+        u16x8 av = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (gadd) av = *reinterpret_cast<const u16x8*>(gadd + (size_t)row * D + 8 * ch);
         u16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float xh = (bf2f(xv[c][e]) - mu) * rs;
-          o[e] = f2bf(rs * (bf2f(gv[c][e]) * bf2f(wv[e]) - s1 - xh * s2));
+          o[e] = f2bf(rs * (bf2f(gv[c][e]) * bf2f(wv[e]) - s1 - xh * s2) + bf2f(av[e]));
         }
         *reinterpret_cast<u16x8*>(dr + 8 * ch) = o;
       }
@@ -503,13 +515,14 @@ int layernorm_bwd_blocks(int rows) {
 }
 
 void layernorm_fwd_bf16(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int rows,
-                        int D, float eps, hipStream_t stream) {
+                        int D, float eps, hipStream_t stream, const void* res, void* xs) {
   if (rows <= 0) return;
   int blocks = (rows + 3) / 4;
   if (blocks > 4096) blocks = 4096;
 #define LNF(V)                                                                                                 \
   hipLaunchKernelGGL((ln_fwd_kernel<V>), dim3(blocks), dim3(LN_T), 0, stream, reinterpret_cast<const u16*>(x), \
-                     reinterpret_cast<const u16*>(w), reinterpret_cast<const u16*>(b), reinterpret_cast<u16*>(y), \
+                     reinterpret_cast<const u16*>(res), reinterpret_cast<const u16*>(w),                         \
+                     reinterpret_cast<const u16*>(b), reinterpret_cast<u16*>(xs), reinterpret_cast<u16*>(y),     \
                      mean, rstd, rows, D, eps)
   if (D <= 512) LNF(1);
   else if (D <= 1024) LNF(2);
@@ -524,7 +537,7 @@ void layernorm_bwd_bf16(const void* x, const void* w, const void* gy, const floa
   const int blocks = layernorm_bwd_blocks(rows);
 #define LNB(V)                                                                                                 \
   hipLaunchKernelGGL((ln_bwd_kernel<V>), dim3(blocks), dim3(LN_T), 0, stream, reinterpret_cast<const u16*>(x), \
-                     reinterpret_cast<const u16*>(w), reinterpret_cast<const u16*>(gy), mean, rstd,             \
+                     reinterpret_cast<const u16*>(w), reinterpret_cast<const u16*>(gy), mean, rstd, nullptr,    \
                      reinterpret_cast<u16*>(dx), workspace, rows, D)
   if (D <= 512) LNB(1);
   else if (D <= 1024) LNB(2);
@@ -538,13 +551,14 @@ void layernorm_bwd_bf16(const void* x, const void* w, const void* gy, const floa
 }
 
 void layernorm_bwd_bf16_accum(const void* x, const void* w, const void* gy, const float* mean, const float* rstd,
-                              void* dx, float* workspace, void* gw, void* gb, int rows, int D, hipStream_t stream) {
+                              void* dx, float* workspace, void* gw, void* gb, int rows, int D, hipStream_t stream,
+                              const void* gadd) {
   if (rows <= 0) return;
   const int blocks = layernorm_bwd_blocks(rows);
 #define LNB(V)                                                                                                 \
   hipLaunchKernelGGL((ln_bwd_kernel<V>), dim3(blocks), dim3(LN_T), 0, stream, reinterpret_cast<const u16*>(x), \
                      reinterpret_cast<const u16*>(w), reinterpret_cast<const u16*>(gy), mean, rstd,             \
-                     reinterpret_cast<u16*>(dx), workspace, rows, D)
+                     reinterpret_cast<const u16*>(gadd), reinterpret_cast<u16*>(dx), workspace, rows, D)
   if (D <= 512) LNB(1);
   else if (D <= 1024) LNB(2);
   else if (D <= 2048) LNB(4);

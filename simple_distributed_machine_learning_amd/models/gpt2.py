@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from .base import ModelSpec, PipelineStage
 from ..ops.linear import Linear, linear
-from ..ops.transformer import LayerNorm, causal_attention, cross_entropy_sum
+from ..ops.transformer import LayerNorm, add_layer_norm, causal_attention, cross_entropy_sum
 from ..parallel.tp import TPContext, column_slice, copy_to_tp, reduce_from_tp, shard_parameter
 
 
@@ -164,11 +164,22 @@ class GPT2Stage(PipelineStage):
             S = x.shape[1]
             pos = torch.arange(S, device=x.device)
             x = self.wte(x) + self.wpe(pos)[None]
-        for blk in self.h.values():
-            x = blk(x)
-        if self.stage_id == self.num_stages - 1:
-            x = self.lm_head(self.ln_f(x))
-        return x
+        last = self.stage_id == self.num_stages - 1
+        blocks = list(self.h.values())
+        if not blocks:
+            return self.lm_head(self.ln_f(x)) if last else x
+        # each residual add is fused into the LayerNorm that reads its sum (ln_2 of the same block,
+        # ln_1 of the next, ln_f at the end); the block maths is exactly Block.forward
+        y = blocks[0].ln_1(x)
+        for i, blk in enumerate(blocks):
+            x, y = add_layer_norm(x, blk.attn(y), blk.ln_2)
+            m = blk.mlp(y)
+            nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else (self.ln_f if last else None)
+            if nxt is None:
+                x = x + m
+            else:
+                x, y = add_layer_norm(x, m, nxt)
+        return self.lm_head(y) if last else x
 
 
 def gpt2_spec(num_stages: int = 2, cfg: GPT2Config = None, seq_len: int = None, dtype=torch.bfloat16,

@@ -45,6 +45,40 @@ def layer_norm(x, w, b, eps: float = 1e-5):
     return F.layer_norm(x, (x.shape[-1],), w, b, eps)
 
 
+class _AddLayerNormFn(torch.autograd.Function):
+    """xs = x + h; y = LayerNorm(xs) in one pass. Backward: dxs = g_xs + LN_bwd(g_y), added inside
+    the LayerNorm backward kernel; both addends of the residual get dxs."""
+
+    @staticmethod
+    def forward(ctx, x, h, w, b, eps):
+        xs, y, mean, rstd = kernels().add_layernorm_fwd_bf16(x.contiguous(), h.contiguous(), w, b, eps)
+        ctx.save_for_backward(xs, w, mean, rstd)
+        ctx.params = (w, b)
+        return xs, y
+
+    @staticmethod
+    def backward(ctx, g_xs, g_y):
+        xs, w, mean, rstd = ctx.saved_tensors
+        wp, bp = ctx.params
+        g_xs = None if g_xs is None else g_xs.contiguous()
+        if wp.grad is not None and bp.grad is not None and wp.grad.is_contiguous() and bp.grad.is_contiguous():
+            d = kernels().layernorm_bwd_bf16_accum(xs, w, g_y.contiguous(), mean, rstd, wp.grad, bp.grad, g_xs)
+            return d, d, None, None, None
+        d, dw, db = kernels().layernorm_bwd_bf16(xs, w, g_y.contiguous(), mean, rstd)
+        if g_xs is not None:
+            d = d + g_xs
+        return d, d, dw.to(w.dtype), db.to(w.dtype), None
+
+
+def add_layer_norm(x, h, ln: nn.LayerNorm):
+    """(x + h, ln(x + h)): the residual add fused into the LayerNorm pass on ROCm bf16."""
+    w, b = ln.weight, ln.bias
+    if _hip_bf16(x, h, w, b) and x.shape[-1] % 8 == 0 and x.shape[-1] <= 4096 and x.shape == h.shape:
+        return _AddLayerNormFn.apply(x, h, w, b, ln.eps)
+    xs = x + h
+    return xs, ln(xs)
+
+
 class LayerNorm(nn.LayerNorm):
     """nn.LayerNorm (same parameter names) backed by the HIP kernel for bf16 on ROCm."""
 

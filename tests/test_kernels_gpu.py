@@ -366,6 +366,37 @@ def test_layernorm_accumulates_into_grad():
     close(ln.bias.grad.float(), -0.5 + br.grad, rtol=2e-2, atol=2e-1)
 
 
+@pytest.mark.parametrize("flat_grads", [True, False])
+def test_add_layernorm_fused_matches_unfused(flat_grads):
+    """(x + h, LN(x + h)) in one pass; backward adds the residual-path gradient inside the LN kernel."""
+    from simple_distributed_machine_learning_amd.ops.transformer import LayerNorm, add_layer_norm
+
+    ln = LayerNorm(768).to(DEV, torch.bfloat16)
+    with torch.no_grad():
+        ln.weight.copy_(rnd(768, seed=84).to(torch.bfloat16))
+        ln.bias.copy_(rnd(768, seed=85).to(torch.bfloat16))
+    if flat_grads:
+        ln.weight.grad = torch.zeros_like(ln.weight)
+        ln.bias.grad = torch.zeros_like(ln.bias)
+    x = rnd(3, 50, 768, seed=86).to(torch.bfloat16).requires_grad_(True)
+    h = rnd(3, 50, 768, seed=87).to(torch.bfloat16).requires_grad_(True)
+    g_xs = rnd(3, 50, 768, seed=88).to(torch.bfloat16)
+    g_y = rnd(3, 50, 768, seed=89).to(torch.bfloat16)
+    xs, y = add_layer_norm(x, h, ln)
+    assert torch.equal(xs, x.detach() + h.detach())  # the unfused bf16 add, bit for bit
+    torch.autograd.backward([xs, y], [g_xs, g_y])
+    xr = (x.detach().float() + h.detach().float()).to(torch.bfloat16).float().requires_grad_(True)
+    wr = ln.weight.detach().float().requires_grad_(True)
+    br = ln.bias.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (768,), wr, br, 1e-5)
+    torch.autograd.backward([xr, yr], [g_xs.float(), g_y.float()])
+    close(y.float(), yr.detach(), rtol=2e-2, atol=3e-2)
+    close(x.grad.float(), xr.grad, rtol=3e-2, atol=5e-2)
+    assert torch.equal(x.grad, h.grad)
+    gw = ln.weight.grad
+    close(gw.float(), wr.grad, rtol=2e-2, atol=2e-1)
+
+
 @pytest.mark.parametrize("T,M,N", [(16384, 3072, 768), (4096, 768, 768), (1000, 2304, 776), (64, 8, 16), (300, 520, 136)])
 def test_wgrad_bf16(T, M, N):
     """gw (bf16) += gy^T x, split-token MFMA GEMM vs an fp64 reference of the same bf16 inputs."""

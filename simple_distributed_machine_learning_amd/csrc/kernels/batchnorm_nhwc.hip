@@ -114,7 +114,8 @@ __global__ void __launch_bounds__(BT) bn_fwd_finalize_kernel(const float* __rest
                                                              const u16* __restrict__ beta, u16* __restrict__ rmean,
                                                              u16* __restrict__ rvar, float* __restrict__ mean,
                                                              float* __restrict__ rstd, float* __restrict__ scale,
-                                                             float* __restrict__ shift) {
+                                                             float* __restrict__ shift, int64_t* __restrict__ nbt) {
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) ++*nbt;  // BatchNorm2d.num_batches_tracked (one launch less)
   const int c = blockIdx.x * (BT / 64) + (threadIdx.x >> 6);
   if (c >= C) return;
   double s1, s2;
@@ -262,7 +263,7 @@ size_t bn_nhwc_workspace_floats(int M, int C) {
 
 void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const void* beta, void* rmean, void* rvar,
                       int M, int C, float eps, float momentum, bool relu, void* y, float* mean, float* rstd,
-                      float* workspace, hipStream_t stream) {
+                      float* workspace, hipStream_t stream, int64_t* num_batches_tracked) {
   int rpb;
   const int nblk = bn_blocks(M, C, &rpb);
   float* part = workspace;
@@ -272,7 +273,7 @@ void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const v
                      nullptr, nullptr, nullptr, M, C, rpb, 0, part);
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + BT / 64 - 1) / (BT / 64)), dim3(BT), 0, stream, part, nblk, C, M, eps,
                      momentum, static_cast<const u16*>(gamma), static_cast<const u16*>(beta), static_cast<u16*>(rmean),
-                     static_cast<u16*>(rvar), mean, rstd, scale, shift);
+                     static_cast<u16*>(rvar), mean, rstd, scale, shift, num_batches_tracked);
   const int64_t n8 = (int64_t)M * C / 8;
   launch_apply(x, res, scale, shift, n8, C, relu, y, stream);
 }

@@ -168,7 +168,7 @@ bool bn_nhwc_supported(int C);
 size_t bn_nhwc_workspace_floats(int M, int C);
 void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const void* beta, void* rmean, void* rvar,
                       int M, int C, float eps, float momentum, bool relu, void* y, float* mean, float* rstd,
-                      float* workspace, hipStream_t stream);
+                      float* workspace, hipStream_t stream, int64_t* num_batches_tracked = nullptr);
 // backward: g = dy * (y > 0 if relu); dx, dres = g (optional), ggamma/gbeta (bf16, accumulated; optional)
 void bn_nhwc_bwd_bf16(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
                       const void* gamma, int M, int C, bool relu, void* dx, void* dres, void* ggamma, void* gbeta,

@@ -381,8 +381,15 @@ void conv_c1_wgrad_bf16_(torch::Tensor dy, torch::Tensor x, torch::Tensor gw) {
 
 std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> bn_nhwc_fwd(
     torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor gamma, torch::Tensor beta,
-    c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar, double eps, double momentum, bool relu) {
+    c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar, double eps, double momentum, bool relu,
+    c10::optional<torch::Tensor> num_batches_tracked) {
   check_cl_bf16(x, "x");
+  int64_t* nbt = nullptr;
+  if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
+    TORCH_CHECK(num_batches_tracked->is_cuda() && num_batches_tracked->scalar_type() == torch::kLong &&
+                    num_batches_tracked->numel() == 1, "bn_nhwc_fwd: num_batches_tracked must be a device int64 scalar");
+    nbt = num_batches_tracked->data_ptr<int64_t>();
+  }
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), M = N * H * W;
   TORCH_CHECK(sdml::bn_nhwc_supported(C), "bn_nhwc_fwd: C must be a multiple of 8 and <= 2048");
   if (res.has_value() && res->defined()) {
@@ -400,7 +407,7 @@ std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> bn_nhwc_fwd(
   if (M > 0)
     sdml::bn_nhwc_fwd_bf16(x.data_ptr(), opt_data(res), gamma.data_ptr(), beta.data_ptr(), opt_data(rmean),
                            opt_data(rvar), M, C, (float)eps, (float)momentum, relu, y.data_ptr(), mean.data_ptr<float>(),
-                           rstd.data_ptr<float>(), ws.data_ptr<float>(), cur_stream());
+                           rstd.data_ptr<float>(), ws.data_ptr<float>(), cur_stream(), nbt);
   return {y, mean, rstd};
 }
 
@@ -890,7 +897,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad_bf16_", &conv_wgrad_bf16_, "conv weight gradient (3x3 / 1x1, stride 1|2), accumulated");
   m.def("conv_c1_fwd_bf16", &conv_c1_fwd_bf16, "stem 3x3 conv with one input channel -> channels-last bf16");
   m.def("conv_c1_wgrad_bf16_", &conv_c1_wgrad_bf16_, "stem conv weight gradient, accumulated into bf16 grad");
-  m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm (+residual)(+ReLU), channels-last bf16");
+  m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm (+residual)(+ReLU), channels-last bf16", py::arg("x"),
+        py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("eps"),
+        py::arg("momentum"), py::arg("relu"), py::arg("num_batches_tracked") = py::none());
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "BatchNorm (+residual)(+ReLU) backward, channels-last bf16");
   m.def("bn_nhwc_eval", &bn_nhwc_eval, "BatchNorm with running statistics (+residual)(+ReLU)");
   m.def("gemm_f32_set_mode", &sdml::gemm_f32_set_mode, "fp32 GEMM engine: 1 = bf16x3 split (default), 0 = fp32 MFMA");

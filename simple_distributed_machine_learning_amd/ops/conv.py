@@ -152,10 +152,11 @@ class _BNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, gamma, beta, bn: torch.nn.BatchNorm2d, relu: bool):
         momentum = 0.1 if bn.momentum is None else bn.momentum
+        nbt = bn.num_batches_tracked  # incremented inside the statistics kernel
         y, mean, rstd = kernels().bn_nhwc_fwd(x, res, gamma, beta, bn.running_mean, bn.running_var, bn.eps,
-                                              momentum, relu)
-        if bn.num_batches_tracked is not None:
-            bn.num_batches_tracked.add_(1)
+                                              momentum, relu, nbt if nbt is not None and nbt.is_cuda else None)
+        if nbt is not None and not nbt.is_cuda:
+            nbt.add_(1)
         ctx.save_for_backward(x, y, mean, rstd)
         ctx.gamma, ctx.beta, ctx.relu, ctx.has_res = gamma, beta, relu, res is not None
         return y

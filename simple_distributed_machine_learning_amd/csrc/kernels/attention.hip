@@ -33,6 +33,10 @@
 // Every loop double-buffers its tiles: the next tile's global loads are issued into registers
 // before the current tile's MFMAs and written to the other LDS buffer after them, so the HBM/L2
 // latency hides behind compute and each iteration has one barrier.
+// Measured and rejected (forward, GPT-2 shape, tools/attn_prof.py): the softmax denominator on the
+// matrix core (an all-ones d tile) plus FA4-style lazy rescaling removed 34 VALU adds and 16
+// packed multiplies per tile but ran 93 vs 87 us: the loop is not VALU-issue bound; at ~12 % MFMA
+// busy (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES) it waits on the one-tile-deep K/V prefetch.
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 

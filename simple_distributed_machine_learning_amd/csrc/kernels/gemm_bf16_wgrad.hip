@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -254,8 +255,15 @@ bool wgrad_bf16_supported(int M, int N, int T, int lda, int ldb, int ldc) {
 
 int wgrad_bf16_splits(int M, int N, int T) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  // one 512-thread workgroup per CU: cover the 256 CUs once, >= 8 K-steps per split
-  int s = 256 / tiles;
+  // one 512-thread workgroup per CU (96 KB LDS): SDML_WGRAD_WAVES = how many times the grid may
+  // cover the 256 CUs (default 1: floor(256 / tiles) splits); >= 8 K-steps per split. Measured on
+  // the GPT-2 shapes (tools/bench_gpt2_gemms.py): 2 or 3 grid waves are 5-25 % slower — the larger
+  // fp32 slab reduction costs more than the idle CUs of one partial wave.
+  static const int waves = [] {
+    const char* e = std::getenv("SDML_WGRAD_WAVES");
+    return e ? std::max(1, std::atoi(e)) : 1;
+  }();
+  int s = 256 * waves / tiles;
   const int max_by_t = T / (8 * BK);
   if (s > max_by_t) s = max_by_t;
   return s < 1 ? 1 : s;

@@ -36,7 +36,10 @@
 // Measured and rejected (forward, GPT-2 shape, tools/attn_prof.py): the softmax denominator on the
 // matrix core (an all-ones d tile) plus FA4-style lazy rescaling removed 34 VALU adds and 16
 // packed multiplies per tile but ran 93 vs 87 us: the loop is not VALU-issue bound; at ~12 % MFMA
-// busy (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES) it waits on the one-tile-deep K/V prefetch.
+// busy (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES). A two-tile-deep prefetch (K/V by global_load_lds into
+// a 3-buffer ring, counted vmcnt + raw barriers, the V^T reads as inline-asm ds_read_b64_tr_b16 so
+// hipcc stops draining the DMA before them) ran 90-91 vs 88 us as well: neither VALU issue nor the
+// tile prefetch depth is what bounds this loop.
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 

@@ -326,6 +326,137 @@ __global__ void __launch_bounds__(256) head_generic_kernel(const float* __restri
   }
 }
 
+// wide-K heads (the 4x1024 MLP: K = 1024, C = 10, 65536 rows): W [C][K] staged in LDS once per
+// block and every W chunk read serves two rows; x and dx move as float4. The per-row generic
+// kernel above re-read W through the cache for every row (twice): 1.25 ms at 65536 x 1024.
+constexpr int HL_MAXJ = 4;  // float4 chunks per lane: K <= 64 * 4 * HL_MAXJ = 1024
+
+template <int C>
+__global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                       const float* __restrict__ bias,
+                                                       const int64_t* __restrict__ target, int M, int K, float scale,
+                                                       float* __restrict__ stats, float* __restrict__ dx,
+                                                       float* __restrict__ dz_out, int mask_dx) {
+  extern __shared__ float4 Ws4[];  // [C][K / 4]
+  __shared__ float red[8];
+  const int nch = K / 4;
+  for (int i = threadIdx.x; i < C * nch; i += 256) Ws4[i] = reinterpret_cast<const float4*>(W)[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float bv[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) bv[c] = bias[c];
+  float loss_acc = 0.f, corr_acc = 0.f;
+  for (int row0 = (blockIdx.x * 4 + wave) * 2; row0 < M; row0 += gridDim.x * 8) {
+    float4 xv[2][HL_MAXJ];
+    float z[2][C];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) z[rr][c] = 0.f;
+#pragma unroll
+      for (int j = 0; j < HL_MAXJ; ++j) {
+        const int ch = lane + 64 * j;
+        xv[rr][j] = (row0 + rr < M && ch < nch) ? reinterpret_cast<const float4*>(x + (size_t)(row0 + rr) * K)[ch]
+                                                : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < HL_MAXJ; ++j) {
+      const int ch = lane + 64 * j;
+      if (ch < nch)
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const float4 w = Ws4[c * nch + ch];
+#pragma unroll
+          for (int rr = 0; rr < 2; ++rr)
+            z[rr][c] += xv[rr][j].x * w.x + xv[rr][j].y * w.y + xv[rr][j].z * w.z + xv[rr][j].w * w.w;
+        }
+    }
+    float dz[2][C];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float v = z[rr][c];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        z[rr][c] = v + bv[c];
+      }
+      const int row = row0 + rr;
+      if (row >= M) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) dz[rr][c] = 0.f;
+        continue;
+      }
+      float mx = z[rr][0];
+      int am = 0;
+#pragma unroll
+      for (int c = 1; c < C; ++c)
+        if (z[rr][c] > mx) {
+          mx = z[rr][c];
+          am = c;
+        }
+      float se = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) se += __expf(z[rr][c] - mx);
+      const float lse = mx + __logf(se);
+      const int tg = (int)target[row];
+      float zt = 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) zt = (c == tg) ? z[rr][c] : zt;
+      loss_acc += lse - zt;
+      corr_acc += am == tg ? 1.f : 0.f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) dz[rr][c] = scale * (__expf(z[rr][c] - lse) - (c == tg ? 1.f : 0.f));
+      if (dz_out && lane < C) {
+        float v = 0.f;
+#pragma unroll
+        for (int c = 0; c < C; ++c) v = (c == lane) ? dz[rr][c] : v;
+        dz_out[(size_t)row * C + lane] = v;
+      }
+    }
+    if (dx)
+#pragma unroll
+      for (int j = 0; j < HL_MAXJ; ++j) {
+        const int ch = lane + 64 * j;
+        if (ch >= nch) continue;
+        float4 o[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+          const float4 w = Ws4[c * nch + ch];
+#pragma unroll
+          for (int rr = 0; rr < 2; ++rr) {
+            o[rr].x += dz[rr][c] * w.x;
+            o[rr].y += dz[rr][c] * w.y;
+            o[rr].z += dz[rr][c] * w.z;
+            o[rr].w += dz[rr][c] * w.w;
+          }
+        }
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+          if (row0 + rr >= M) continue;
+          if (mask_dx) {
+            o[rr].x = xv[rr][j].x <= 0.f ? 0.f : o[rr].x;
+            o[rr].y = xv[rr][j].y <= 0.f ? 0.f : o[rr].y;
+            o[rr].z = xv[rr][j].z <= 0.f ? 0.f : o[rr].z;
+            o[rr].w = xv[rr][j].w <= 0.f ? 0.f : o[rr].w;
+          }
+          reinterpret_cast<float4*>(dx + (size_t)(row0 + rr) * K)[ch] = o[rr];
+        }
+      }
+  }
+  if (lane == 0) {
+    red[2 * wave] = loss_acc;
+    red[2 * wave + 1] = corr_acc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(stats, red[0] + red[2] + red[4] + red[6]);
+    atomicAdd(stats + 1, red[1] + red[3] + red[5] + red[7]);
+  }
+}
+
 }  // namespace
 
 bool head_fused_supported(int K, int C) { return K == HK && (C == 10 || C == 2 || C == 16); }
@@ -376,6 +507,13 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
     const int width = C * K + C + 2;
     hipLaunchKernelGGL(head_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, stream, workspace, blocks, C * K,
                        C, gW, gb, stats, dx != nullptr ? 1 : 0);
+    return;
+  }
+  if (C == 10 && K % 4 == 0 && K <= 64 * 4 * HL_MAXJ && M >= 4096) {
+    int lblocks = (M + 7) / 8;
+    if (lblocks > 1024) lblocks = 1024;
+    hipLaunchKernelGGL(head_lds_kernel<10>, dim3(lblocks), dim3(256), (size_t)C * K * sizeof(float), stream, x, W, b,
+                       target, M, K, scale, stats, dx, dz_out, mask_dx ? 1 : 0);
     return;
   }
   int gblocks = (M + 3) / 4;

@@ -43,9 +43,10 @@ def main():
     a = ap.parse_args()
     kind, M, B, S = DEFAULTS[a.config]
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
-    if world0 == 1 and a.config in ("gpt2", "resnet18"):
-        # all stages local: micro-batching only shrinks the GEMMs / convolutions
-        # (measured: GPT-2 614K vs 438K tokens/s at M=4; ResNet-18 27.2K vs 15.6K samples/s at M=8)
+    if world0 == 1 and a.config in ("gpt2", "resnet18", "mlp4x1024"):
+        # all stages local: micro-batching only shrinks the GEMMs / convolutions (measured: GPT-2
+        # 614K vs 438K tokens/s at M=4; ResNet-18 27.2K vs 15.6K samples/s at M=8; 4x1024 MLP
+        # 6.27M vs 5.61M samples/s at M=8)
         M = 1
     M = a.microbatches or M
     B = a.batch or B

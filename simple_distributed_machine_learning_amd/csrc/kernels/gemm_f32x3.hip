@@ -292,6 +292,42 @@ __global__ void __launch_bounds__(256) split3_planes_kernel(const float* __restr
   *reinterpret_cast<u16x4*>(out + 2 * n + i) = u16x4{l[0], l[1], l[2], l[3]};
 }
 
+// transposed split: w [R][Cc] fp32 -> planes [3][Cc][R] (the dX GEMM's B = W^T, k-contiguous, so
+// the input gradient takes the same pre-split path as the forward). 64 x 64 tiles through LDS:
+// coalesced float4 reads of w rows, coalesced u16 writes of the transposed plane rows.
+__global__ void __launch_bounds__(256) split3_planes_t_kernel(const float* __restrict__ w, u16* __restrict__ out,
+                                                              int R, int Cc) {
+  __shared__ u16 t[3][64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int i = threadIdx.x; i < 64 * 16; i += 256) {  // 64 rows x 16 float4
+    const int rr = i / 16, c4 = (i % 16) * 4;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r0 + rr < R && c0 + c4 + 3 < Cc) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(w + (size_t)(r0 + rr) * Cc + c0 + c4);
+      a[0] = v[0];
+      a[1] = v[1];
+      a[2] = v[2];
+      a[3] = v[3];
+    } else {
+      for (int e = 0; e < 4; ++e)
+        if (r0 + rr < R && c0 + c4 + e < Cc) a[e] = w[(size_t)(r0 + rr) * Cc + c0 + c4 + e];
+    }
+    u16 h[4], m[4], l[4];
+    split3<4>(a, h, m, l);
+    for (int e = 0; e < 4; ++e) {
+      t[0][c4 + e][rr] = h[e];
+      t[1][c4 + e][rr] = m[e];
+      t[2][c4 + e][rr] = l[e];
+    }
+  }
+  __syncthreads();
+  const size_t plane = (size_t)R * Cc;
+  for (int i = threadIdx.x; i < 3 * 64 * 64; i += 256) {
+    const int pl = i / 4096, cc = (i / 64) % 64, rr = i % 64;
+    if (c0 + cc < Cc && r0 + rr < R) out[pl * plane + (size_t)(c0 + cc) * R + r0 + rr] = t[pl][cc][rr];
+  }
+}
+
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -572,6 +608,11 @@ void split3_planes(const float* x, unsigned short* out, int64_t n, hipStream_t s
   if (n <= 0) return;
   const int64_t blocks = (n / 4 + 255) / 256;
   hipLaunchKernelGGL(split3_planes_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, out, n);
+}
+
+void split3_planes_t(const float* w, unsigned short* out, int R, int C, hipStream_t stream) {
+  if (R <= 0 || C <= 0) return;
+  hipLaunchKernelGGL(split3_planes_t_kernel, dim3((C + 63) / 64, (R + 63) / 64), dim3(256), 0, stream, w, out, R, C);
 }
 
 bool gemm_f32x3_can_presplit_b(const GemmArgs& g) {

@@ -331,12 +331,17 @@ __global__ void __launch_bounds__(256) head_generic_kernel(const float* __restri
 // kernel above re-read W through the cache for every row (twice): 1.25 ms at 65536 x 1024.
 constexpr int HL_MAXJ = 4;  // float4 chunks per lane: K <= 64 * 4 * HL_MAXJ = 1024
 
-template <int C>
+// DW: the weight/bias gradients are accumulated per lane (dW[c][its 16 k] += dz[c] x[k]) over the
+// block's rows, reduced over the 4 waves through LDS in wave order and written, with the loss and
+// correct count, as one slab row [dW | db | loss, correct] per block for head_reduce_kernel (no
+// separate dz^T x GEMM re-reading x: 250 us at 65536 x 1024)
+template <int C, bool DW>
 __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__ x, const float* __restrict__ W,
                                                        const float* __restrict__ bias,
                                                        const int64_t* __restrict__ target, int M, int K, float scale,
                                                        float* __restrict__ stats, float* __restrict__ dx,
-                                                       float* __restrict__ dz_out, int mask_dx) {
+                                                       float* __restrict__ dz_out, int mask_dx,
+                                                       float* __restrict__ part) {
   extern __shared__ float4 Ws4[];  // [C][K / 4]
   __shared__ float red[8];
   const int nch = K / 4;
@@ -346,12 +351,23 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
   float bv[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) bv[c] = bias[c];
+  constexpr int R = 2;  // rows per W read (1 row with DW measured no better: hipcc keeps ~300 registers either way)
   float loss_acc = 0.f, corr_acc = 0.f;
-  for (int row0 = (blockIdx.x * 4 + wave) * 2; row0 < M; row0 += gridDim.x * 8) {
-    float4 xv[2][HL_MAXJ];
-    float z[2][C];
+  float4 gacc[DW ? C : 1][HL_MAXJ];
+  float gbacc[DW ? C : 1];
+  if constexpr (DW) {
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
+    for (int c = 0; c < C; ++c) {
+      gbacc[c] = 0.f;
+#pragma unroll
+      for (int j = 0; j < HL_MAXJ; ++j) gacc[c][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  for (int row0 = (blockIdx.x * 4 + wave) * R; row0 < M; row0 += gridDim.x * 4 * R) {
+    float4 xv[R][HL_MAXJ];
+    float z[R][C];
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
 #pragma unroll
       for (int c = 0; c < C; ++c) z[rr][c] = 0.f;
 #pragma unroll
@@ -369,13 +385,13 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
         for (int c = 0; c < C; ++c) {
           const float4 w = Ws4[c * nch + ch];
 #pragma unroll
-          for (int rr = 0; rr < 2; ++rr)
+          for (int rr = 0; rr < R; ++rr)
             z[rr][c] += xv[rr][j].x * w.x + xv[rr][j].y * w.y + xv[rr][j].z * w.z + xv[rr][j].w * w.w;
         }
     }
-    float dz[2][C];
+    float dz[R][C];
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr) {
+    for (int rr = 0; rr < R; ++rr) {
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         float v = z[rr][c];
@@ -416,17 +432,35 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
         dz_out[(size_t)row * C + lane] = v;
       }
     }
+    if constexpr (DW) {  // rows past M have dz = 0 and zero x: they add nothing
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        #pragma unroll
+        for (int rr = 0; rr < R; ++rr) gbacc[c] += dz[rr][c];
+#pragma unroll
+        for (int j = 0; j < HL_MAXJ; ++j)
+#pragma unroll
+          for (int rr = 0; rr < R; ++rr) {
+            gacc[c][j].x += dz[rr][c] * xv[rr][j].x;
+            gacc[c][j].y += dz[rr][c] * xv[rr][j].y;
+            gacc[c][j].z += dz[rr][c] * xv[rr][j].z;
+            gacc[c][j].w += dz[rr][c] * xv[rr][j].w;
+          }
+      }
+    }
     if (dx)
 #pragma unroll
       for (int j = 0; j < HL_MAXJ; ++j) {
         const int ch = lane + 64 * j;
         if (ch >= nch) continue;
-        float4 o[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+        float4 o[R];
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) o[rr] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int c = 0; c < C; ++c) {
           const float4 w = Ws4[c * nch + ch];
 #pragma unroll
-          for (int rr = 0; rr < 2; ++rr) {
+          for (int rr = 0; rr < R; ++rr) {
             o[rr].x += dz[rr][c] * w.x;
             o[rr].y += dz[rr][c] * w.y;
             o[rr].z += dz[rr][c] * w.z;
@@ -434,7 +468,7 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
           }
         }
 #pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
+        for (int rr = 0; rr < R; ++rr) {
           if (row0 + rr >= M) continue;
           if (mask_dx) {
             o[rr].x = xv[rr][j].x <= 0.f ? 0.f : o[rr].x;
@@ -450,6 +484,44 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
     red[2 * wave] = loss_acc;
     red[2 * wave + 1] = corr_acc;
   }
+  if constexpr (DW) {
+    __shared__ float gbs[4][C];
+    if (lane == 0)
+#pragma unroll
+      for (int c = 0; c < C; ++c) gbs[wave][c] = gbacc[c];
+    // the W image is dead: reuse it for the dW partial, the waves adding in order 0, 1, 2, 3
+    for (int wv = 0; wv < 4; ++wv) {
+      __syncthreads();
+      if (wave == wv)
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+          for (int j = 0; j < HL_MAXJ; ++j) {
+            const int ch = lane + 64 * j;
+            if (ch >= nch) continue;
+            float4 v = gacc[c][j];
+            if (wv > 0) {
+              const float4 q = Ws4[c * nch + ch];
+              v.x += q.x;
+              v.y += q.y;
+              v.z += q.z;
+              v.w += q.w;
+            }
+            Ws4[c * nch + ch] = v;
+          }
+    }
+    __syncthreads();
+    const int width = C * K + C + 2;
+    float* slab = part + (size_t)blockIdx.x * width;
+    for (int i = threadIdx.x; i < C * nch; i += 256) reinterpret_cast<float4*>(slab)[i] = Ws4[i];
+    if (threadIdx.x < C) slab[C * K + threadIdx.x] = gbs[0][threadIdx.x] + gbs[1][threadIdx.x] +
+                                                     gbs[2][threadIdx.x] + gbs[3][threadIdx.x];
+    if (threadIdx.x == 0) {
+      slab[C * K + C] = red[0] + red[2] + red[4] + red[6];
+      slab[C * K + C + 1] = red[1] + red[3] + red[5] + red[7];
+    }
+    return;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     atomicAdd(stats, red[0] + red[2] + red[4] + red[6]);
@@ -460,6 +532,10 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
 }  // namespace
 
 bool head_fused_supported(int K, int C) { return K == HK && (C == 10 || C == 2 || C == 16); }
+
+// the LDS-staged wide-K head (C = 10, K % 4 == 0, K <= 1024, large batches)
+bool head_lds_supported(int M, int K, int C) { return C == 10 && K % 4 == 0 && K <= 64 * 4 * HL_MAXJ && M >= 4096; }
+int head_lds_blocks(int M) { return (int)std::min<int64_t>(((int64_t)M + 7) / 8, 1024); }
 
 // grid of the fused kernel: enough blocks to fill the chip, each keeping its dW partial in
 // registers over several 64-row chunks (fewer slabs to reduce)
@@ -477,6 +553,7 @@ int head_fused_blocks(int M, int* chunks_per_block) {
 }
 
 size_t head_workspace_floats(int M, int K, int C) {
+  if (head_lds_supported(M, K, C)) return (size_t)head_lds_blocks(M) * (C * K + C + 2);
   if (!head_fused_supported(K, C)) return 0;
   int cpb;
   return (size_t)head_fused_blocks(M, &cpb) * (C * K + C + 2);
@@ -509,11 +586,19 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
                        C, gW, gb, stats, dx != nullptr ? 1 : 0);
     return;
   }
-  if (C == 10 && K % 4 == 0 && K <= 64 * 4 * HL_MAXJ && M >= 4096) {
-    int lblocks = (M + 7) / 8;
-    if (lblocks > 1024) lblocks = 1024;
-    hipLaunchKernelGGL(head_lds_kernel<10>, dim3(lblocks), dim3(256), (size_t)C * K * sizeof(float), stream, x, W, b,
-                       target, M, K, scale, stats, dx, dz_out, mask_dx ? 1 : 0);
+  if (head_lds_supported(M, K, C)) {
+    const int lblocks = head_lds_blocks(M);
+    const size_t lds = (size_t)C * K * sizeof(float);
+    if (gW && gb && workspace && dz_out == nullptr) {
+      hipLaunchKernelGGL((head_lds_kernel<10, true>), dim3(lblocks), dim3(256), lds, stream, x, W, b, target, M, K,
+                         scale, stats, dx, nullptr, mask_dx ? 1 : 0, workspace);
+      const int width = C * K + C + 2;
+      hipLaunchKernelGGL(head_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, stream, workspace, lblocks, C * K,
+                         C, gW, gb, stats, 1);
+    } else {
+      hipLaunchKernelGGL((head_lds_kernel<10, false>), dim3(lblocks), dim3(256), lds, stream, x, W, b, target, M, K,
+                         scale, stats, dx, dz_out, mask_dx ? 1 : 0, nullptr);
+    }
     return;
   }
   int gblocks = (M + 3) / 4;

@@ -66,6 +66,8 @@ bool gemm_f32_uses_x3(const GemmArgs& g);
 bool gemm_f32x3_can_presplit_b(const GemmArgs& g);
 // x[n] fp32 -> out[3][n] bf16 bits (hi, mid, lo; x == hi + mid + lo), n % 4 == 0, 16-B aligned
 void split3_planes(const float* x, unsigned short* out, int64_t n, hipStream_t stream);
+// transposed split: w [R][C] fp32 -> bf16 planes [3][C][R] (pre-split B = W^T of an input-gradient GEMM)
+void split3_planes_t(const float* w, unsigned short* out, int R, int C, hipStream_t stream);
 void gemm_f32x3_set_variant(int v);  // pipeline A/B: 0 = early split (default), 1 = split after MFMAs
 
 // ---- fused classifier head: z = x W^T + b; log_softmax; NLL; backward --------------------
@@ -76,6 +78,8 @@ void gemm_f32x3_set_variant(int v);  // pipeline A/B: 0 = early split (default),
 // The fused path needs a workspace of head_workspace_floats(M, K, C) floats (per-block
 // partial slabs, reduced by a second deterministic pass).
 bool head_fused_supported(int K, int C);
+// wide-K LDS-staged head (C = 10, K <= 1024): with gW/gb and a workspace it also produces dW/db
+bool head_lds_supported(int M, int K, int C);
 size_t head_workspace_floats(int M, int K, int C);
 // mask_dx: dx *= (x > 0) — the producing stage's ReLU backward, fused (x is its output)
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K,

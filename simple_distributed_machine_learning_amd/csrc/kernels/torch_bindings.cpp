@@ -142,6 +142,20 @@ c10::optional<torch::Tensor> linear_bwd_f32(torch::Tensor x, c10::optional<torch
   g.epi = sdml::EPI_STORE;
   if (mask_dx_by_x) g.cmask = x.data_ptr<float>();  // dx *= (x > 0): ReLU backward of the producer
   TORCH_CHECK(sdml::gemm_f32_supported(g), "linear_bwd_f32(dX): unsupported shape/alignment");
+  // on the bf16x3 engine, take B = W^T pre-split (one transposed split of the weight per call)
+  // like the forward instead of splitting the k-major weight tile in every workgroup
+  sdml::GemmArgs gt = g;
+  gt.b_kmajor = false;
+  gt.ldb = N;
+  torch::Tensor wsplit;
+  if (sdml::gemm_f32_uses_x3(gt) && sdml::gemm_f32x3_can_presplit_b(gt)) {
+    wsplit = torch::empty({3, K, N}, x.options().dtype(torch::kInt16));
+    sdml::split3_planes_t(w.data_ptr<float>(), reinterpret_cast<unsigned short*>(wsplit.data_ptr<int16_t>()), (int)N,
+                          (int)K, s);
+    gt.b_split = reinterpret_cast<const unsigned short*>(wsplit.data_ptr<int16_t>());
+    sdml::gemm_f32(gt, s);
+    return dx;
+  }
   sdml::gemm_f32(g, s);
   return dx;
 }
@@ -480,7 +494,7 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
   c10::optional<torch::Tensor> dx;
   if (M == 0) return {stats, need_dx ? c10::optional<torch::Tensor>(torch::empty({0, K}, x.options())) : c10::nullopt};
   hipStream_t s = cur_stream();
-  const bool fusable = sdml::head_fused_supported((int)K, (int)C);
+  const bool fusable = sdml::head_fused_supported((int)K, (int)C) || sdml::head_lds_supported((int)M, (int)K, (int)C);
   const bool fused = fusable && (!train || (opt_ptr(gw) && opt_ptr(gb)));
   torch::Tensor ws;
   if (fused) ws = torch::empty({(int64_t)sdml::head_workspace_floats(M, K, C)}, x.options());

@@ -151,3 +151,14 @@ def test_linear_fwd_presplit_weight(M, N):
     assert ((y.double() - want).abs() <= bound).all()
     y2 = ops.linear_fwd(x, w, b)
     assert ((y2.double() - (x.double() @ w.double().t() + b.double())).abs() <= bound).all()
+
+
+@pytest.mark.parametrize("M,N,Kd", [(70000, 1024, 1024), (20000, 136, 520)])
+def test_linear_bwd_dx_presplit_transposed_weight(M, N, Kd):
+    """dX = gz @ W with W^T pre-split into bf16 planes by the transposed split (ragged 64-tiles)."""
+    x, w = rnd(M, Kd, seed=26), rnd(N, Kd, seed=27) * 0.05
+    gy = rnd(M, N, seed=28) * 1e-2
+    dx = ops.linear_relu_bwd(x, None, gy, w, None, None, need_dx=True, gy_masked=True, mask_dx=False)
+    want = gy.double() @ w.double()
+    bound = N * 2.0 ** -24 * (gy.abs().double() @ w.abs().double()) + 1e-30
+    assert ((dx.double() - want).abs() <= bound).all()

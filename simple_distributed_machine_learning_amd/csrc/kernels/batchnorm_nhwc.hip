@@ -30,10 +30,14 @@ __device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, st
 constexpr int BT = 256;
 
 // rows of this block: [blockIdx.x * rpb, +rpb); thread = (row lane, 8-channel group)
+// relu (backward): 0 none, 1 mask from the saved output y > 0, 2 mask recomputed from the input
+// (x * gamma * rstd + beta - mean * gamma * rstd > 0: BatchNorm + ReLU without a residual, so the
+// output need not be kept or re-read)
 template <bool BWD>
 __global__ void __launch_bounds__(BT) bn_partial_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
                                                         const u16* __restrict__ y, const float* __restrict__ mean,
-                                                        const float* __restrict__ rstd, int M, int C, int rpb,
+                                                        const float* __restrict__ rstd, const u16* __restrict__ gamma,
+                                                        const u16* __restrict__ beta, int M, int C, int rpb,
                                                         int relu, float* __restrict__ part) {
   __shared__ float red[BT * 16];
   const int G = C / 8;  // channel groups
@@ -42,12 +46,16 @@ __global__ void __launch_bounds__(BT) bn_partial_kernel(const u16* __restrict__ 
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
-  float mu[8], rs[8];
+  float mu[8], rs[8], sc[8], sh[8];
   if (BWD) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       mu[e] = mean[8 * cg + e];
       rs[e] = rstd[8 * cg + e];
+      if (relu == 2) {
+        sc[e] = bf2f(gamma[8 * cg + e]) * rs[e];
+        sh[e] = bf2f(beta[8 * cg + e]) - mu[e] * sc[e];
+      }
     }
   }
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
@@ -65,11 +73,12 @@ __global__ void __launch_bounds__(BT) bn_partial_kernel(const u16* __restrict__ 
       } else {
         const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
         u16x8 yv = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (relu) yv = *reinterpret_cast<const u16x8*>(y + o);
+        if (relu == 1) yv = *reinterpret_cast<const u16x8*>(y + o);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float g = bf2f(gv[e]);
-          if (relu && !(bf2f(yv[e]) > 0.f)) g = 0.f;
+          if (relu == 1 && !(bf2f(yv[e]) > 0.f)) g = 0.f;
+          if (relu == 2 && !(fmaf(bf2f(xv[e]), sc[e], sh[e]) > 0.f)) g = 0.f;
           s1[e] += g;
           s2[e] += g * (bf2f(xv[e]) - mu[e]) * rs[e];
         }
@@ -129,7 +138,7 @@ __global__ void __launch_bounds__(BT) bn_fwd_finalize_kernel(const float* __rest
   mean[c] = (float)mu;
   rstd[c] = r;
   scale[c] = g * r;
-  shift[c] = bta - (float)mu * g * r;
+  shift[c] = bta - (float)mu * (g * r);  // bit-identical to the backward's recomputed ReLU mask
   if (rmean) {
     const double unb = M > 1 ? var * M / (M - 1) : var;
     rmean[c] = f2bf((1.f - momentum) * bf2f(rmean[c]) + momentum * (float)mu);
@@ -190,33 +199,41 @@ __global__ void __launch_bounds__(BT) bn_bwd_finalize_kernel(const float* __rest
   if (ggamma) ggamma[c] = f2bf(bf2f(ggamma[c]) + (float)s2);
 }
 
-// dx = a * (g - mg) + b * (x - mean); dres = g (optional). Coefficients in registers (see apply).
-template <bool RELU, bool DRES>
+// dx = a * (g - mg) + b * (x - mean); dres = g (optional). Coefficients in registers (see apply);
+// RELU as in bn_partial_kernel (2: the mask from x, with the forward's folded scale/shift)
+template <int RELU, bool DRES>
 __global__ void __launch_bounds__(BT) bn_bwd_apply_kernel(const u16* __restrict__ x, const u16* __restrict__ dy,
                                                           const u16* __restrict__ y, const float* __restrict__ mean,
-                                                          const float* __restrict__ coef, int64_t n8, int C,
+                                                          const float* __restrict__ coef, const u16* __restrict__ gamma,
+                                                          const u16* __restrict__ beta, int64_t n8, int C,
                                                           u16* __restrict__ dx, u16* __restrict__ dres) {
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int c0 = 8 * (threadIdx.x % (C / 8));
-  float ca[8], cm[8], cb[8], mu[8];
+  float ca[8], cm[8], cb[8], mu[8], fs[8], fh[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     ca[e] = coef[c0 + e];
     cm[e] = coef[C + c0 + e];
     cb[e] = coef[2 * C + c0 + e];
     mu[e] = mean[c0 + e];
+    if (RELU == 2) {  // a = gamma * rstd is the forward scale
+      fs[e] = ca[e];
+      fh[e] = bf2f(beta[c0 + e]) - mu[e] * ca[e];
+    }
   }
+  (void)gamma;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = i0; i < n8; i += stride) {
     const u16x8 xv = reinterpret_cast<const u16x8*>(x)[i];
     const u16x8 gv = reinterpret_cast<const u16x8*>(dy)[i];
     u16x8 yv = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (RELU) yv = reinterpret_cast<const u16x8*>(y)[i];
+    if (RELU == 1) yv = reinterpret_cast<const u16x8*>(y)[i];
     u16x8 o, og;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float g = bf2f(gv[e]);
-      if (RELU && !(bf2f(yv[e]) > 0.f)) g = 0.f;
+      if (RELU == 1 && !(bf2f(yv[e]) > 0.f)) g = 0.f;
+      if (RELU == 2 && !(fmaf(bf2f(xv[e]), fs[e], fh[e]) > 0.f)) g = 0.f;
       o[e] = f2bf(fmaf(ca[e], g - cm[e], cb[e] * (bf2f(xv[e]) - mu[e])));
       og[e] = f2bf(g);
     }
@@ -270,7 +287,7 @@ void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const v
   float* scale = workspace + (size_t)nblk * 2 * C;
   float* shift = scale + C;
   hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(nblk), dim3(BT), 0, stream, static_cast<const u16*>(x), nullptr,
-                     nullptr, nullptr, nullptr, M, C, rpb, 0, part);
+                     nullptr, nullptr, nullptr, nullptr, nullptr, M, C, rpb, 0, part);
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + BT / 64 - 1) / (BT / 64)), dim3(BT), 0, stream, part, nblk, C, M, eps,
                      momentum, static_cast<const u16*>(gamma), static_cast<const u16*>(beta), static_cast<u16*>(rmean),
                      static_cast<u16*>(rvar), mean, rstd, scale, shift, num_batches_tracked);
@@ -280,28 +297,32 @@ void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const v
 
 void bn_nhwc_bwd_bf16(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
                       const void* gamma, int M, int C, bool relu, void* dx, void* dres, void* ggamma, void* gbeta,
-                      float* workspace, hipStream_t stream) {
+                      float* workspace, hipStream_t stream, const void* beta) {
   int rpb;
   const int nblk = bn_blocks(M, C, &rpb);
   float* part = workspace;
   float* coef = workspace + (size_t)nblk * 2 * C;  // [3][C]
+  // ReLU mask: from y when given, else recomputed from x (needs beta; BatchNorm + ReLU, no residual)
+  const int rmode = !relu ? 0 : (y ? 1 : 2);
+  const u16 *gp = static_cast<const u16*>(gamma), *bp = static_cast<const u16*>(beta);
   hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(nblk), dim3(BT), 0, stream, static_cast<const u16*>(x),
-                     static_cast<const u16*>(dy), static_cast<const u16*>(y), mean, rstd, M, C, rpb, relu ? 1 : 0,
+                     static_cast<const u16*>(dy), static_cast<const u16*>(y), mean, rstd, gp, bp, M, C, rpb, rmode,
                      part);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + BT / 64 - 1) / (BT / 64)), dim3(BT), 0, stream, part, nblk, C, M,
-                     rstd, static_cast<const u16*>(gamma), static_cast<u16*>(ggamma), static_cast<u16*>(gbeta), coef);
+                     rstd, gp, static_cast<u16*>(ggamma), static_cast<u16*>(gbeta), coef);
   const int64_t n8 = (int64_t)M * C / 8;
   const dim3 g(elem_blocks(n8, apply_threads(C))), b(apply_threads(C));
   const u16 *xp = static_cast<const u16*>(x), *dyp = static_cast<const u16*>(dy), *yp = static_cast<const u16*>(y);
   u16 *dxp = static_cast<u16*>(dx), *drp = static_cast<u16*>(dres);
-  if (relu && dres)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, true>), g, b, 0, stream, xp, dyp, yp, mean, coef, n8, C, dxp, drp);
-  else if (relu)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<true, false>), g, b, 0, stream, xp, dyp, yp, mean, coef, n8, C, dxp, drp);
-  else if (dres)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, true>), g, b, 0, stream, xp, dyp, yp, mean, coef, n8, C, dxp, drp);
-  else
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<false, false>), g, b, 0, stream, xp, dyp, yp, mean, coef, n8, C, dxp, drp);
+#define BNB(R, D) \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<R, D>), g, b, 0, stream, xp, dyp, yp, mean, coef, gp, bp, n8, C, dxp, drp)
+  if (rmode == 1 && dres) BNB(1, true);
+  else if (rmode == 1) BNB(1, false);
+  else if (rmode == 2 && dres) BNB(2, true);
+  else if (rmode == 2) BNB(2, false);
+  else if (dres) BNB(0, true);
+  else BNB(0, false);
+#undef BNB
 }
 
 // eval mode: y = relu?(x * scale + shift (+ res)) from the running statistics

@@ -176,7 +176,7 @@ void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const v
 // backward: g = dy * (y > 0 if relu); dx, dres = g (optional), ggamma/gbeta (bf16, accumulated; optional)
 void bn_nhwc_bwd_bf16(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
                       const void* gamma, int M, int C, bool relu, void* dx, void* dres, void* ggamma, void* gbeta,
-                      float* workspace, hipStream_t stream);
+                      float* workspace, hipStream_t stream, const void* beta = nullptr);
 void bn_nhwc_eval_bf16(const void* x, const void* res, const float* scale, const float* shift, int M, int C, bool relu,
                        void* y, hipStream_t stream);
 

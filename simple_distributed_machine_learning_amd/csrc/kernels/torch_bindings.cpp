@@ -429,18 +429,20 @@ std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> bn_nhwc_fwd(
 std::tuple<torch::Tensor, c10::optional<torch::Tensor>> bn_nhwc_bwd(
     torch::Tensor x, torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor mean, torch::Tensor rstd,
     torch::Tensor gamma, bool relu, bool need_dres, c10::optional<torch::Tensor> ggamma,
-    c10::optional<torch::Tensor> gbeta) {
+    c10::optional<torch::Tensor> gbeta, c10::optional<torch::Tensor> beta) {
   check_cl_bf16(x, "x");
   check_cl_bf16(dy, "dy");
   TORCH_CHECK(dy.sizes() == x.sizes(), "bn_nhwc_bwd: dy shape mismatch");
-  if (relu) {
-    TORCH_CHECK(y.has_value() && y->defined(), "bn_nhwc_bwd: relu needs the forward output");
-    check_cl_bf16(*y, "y");
+  const bool have_y = y.has_value() && y->defined();
+  if (relu) {  // the mask comes from y, or is recomputed from x with beta (no residual)
+    TORCH_CHECK(have_y || (beta.has_value() && beta->defined()), "bn_nhwc_bwd: relu needs y or beta");
+    if (have_y) check_cl_bf16(*y, "y");
   }
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), M = N * H * W;
   check_bn_vec(gamma, C, "gamma");
   check_bn_vec(ggamma, C, "ggamma");
   check_bn_vec(gbeta, C, "gbeta");
+  check_bn_vec(beta, C, "beta");
   TORCH_CHECK(mean.numel() == C && rstd.numel() == C && mean.scalar_type() == torch::kFloat32, "bn_nhwc_bwd: stats");
   auto cl = x.options().memory_format(at::MemoryFormat::ChannelsLast);
   auto dx = torch::empty_like(x, cl);
@@ -449,10 +451,10 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> bn_nhwc_bwd(
   auto ws = torch::empty({(int64_t)sdml::bn_nhwc_workspace_floats(M, C)},
                          x.options().dtype(torch::kFloat32).memory_format(at::MemoryFormat::Contiguous));
   if (M > 0)
-    sdml::bn_nhwc_bwd_bf16(x.data_ptr(), dy.data_ptr(), relu ? y->data_ptr() : nullptr, mean.data_ptr<float>(),
-                           rstd.data_ptr<float>(), gamma.data_ptr(), M, C, relu, dx.data_ptr(),
+    sdml::bn_nhwc_bwd_bf16(x.data_ptr(), dy.data_ptr(), (relu && have_y) ? y->data_ptr() : nullptr,
+                           mean.data_ptr<float>(), rstd.data_ptr<float>(), gamma.data_ptr(), M, C, relu, dx.data_ptr(),
                            need_dres ? dres->data_ptr() : nullptr, opt_data(ggamma), opt_data(gbeta),
-                           ws.data_ptr<float>(), cur_stream());
+                           ws.data_ptr<float>(), cur_stream(), opt_data(beta));
   return {dx, dres};
 }
 
@@ -914,7 +916,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm (+residual)(+ReLU), channels-last bf16", py::arg("x"),
         py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("eps"),
         py::arg("momentum"), py::arg("relu"), py::arg("num_batches_tracked") = py::none());
-  m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "BatchNorm (+residual)(+ReLU) backward, channels-last bf16");
+  m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "BatchNorm (+residual)(+ReLU) backward, channels-last bf16", py::arg("x"),
+        py::arg("dy"), py::arg("y"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("relu"),
+        py::arg("need_dres"), py::arg("ggamma"), py::arg("gbeta"), py::arg("beta") = py::none());
   m.def("bn_nhwc_eval", &bn_nhwc_eval, "BatchNorm with running statistics (+residual)(+ReLU)");
   m.def("gemm_f32_set_mode", &sdml::gemm_f32_set_mode, "fp32 GEMM engine: 1 = bf16x3 split (default), 0 = fp32 MFMA");
   m.def("gemm_f32_mode", &sdml::gemm_f32_mode, "current fp32 GEMM engine");

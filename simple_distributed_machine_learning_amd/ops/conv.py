@@ -157,7 +157,10 @@ class _BNFn(torch.autograd.Function):
                                               momentum, relu, nbt if nbt is not None and nbt.is_cuda else None)
         if nbt is not None and not nbt.is_cuda:
             nbt.add_(1)
-        ctx.save_for_backward(x, y, mean, rstd)
+        # BatchNorm + ReLU without a residual: the backward recomputes the mask from x, so y is
+        # neither kept alive nor re-read
+        keep_y = relu and res is not None
+        ctx.save_for_backward(x, y if keep_y else None, mean, rstd)
         ctx.gamma, ctx.beta, ctx.relu, ctx.has_res = gamma, beta, relu, res is not None
         return y
 
@@ -175,7 +178,7 @@ class _BNFn(torch.autograd.Function):
         gg, own_g = acc(gamma)
         gb, own_b = acc(beta)
         dx, dres = kernels().bn_nhwc_bwd(x, dy, y if ctx.relu else None, mean, rstd, gamma, ctx.relu, ctx.has_res,
-                                          gg, gb)
+                                          gg, gb, beta)
         return dx, dres, (gg if own_g else None), (gb if own_b else None), None, None
 
 

@@ -49,11 +49,12 @@ class _ShardedSynth:
     the samples this rank's stage 0 consumes (``own_len`` samples at ``own_lo`` of each of the
     ``nbatches`` global batches of ``GB`` samples)."""
 
-    def __init__(self, GB, own_lo, own_len, nbatches, dev):
+    def __init__(self, GB, own_lo, own_len, nbatches, dev, pixels="u8"):
         self.n = GB * nbatches
         self.GB, self.own_lo, self.own_len = GB, own_lo, own_len
         self.labels = SyntheticMNIST(self.n, seed=1234, device=dev, image_range=(0, 0))
-        self.imgs = [SyntheticMNIST(own_len, seed=1234, device=dev, offset=k * GB + own_lo) for k in range(nbatches)]
+        self.imgs = [SyntheticMNIST(own_len, seed=1234, device=dev, offset=k * GB + own_lo, pixels=pixels)
+                     for k in range(nbatches)]
 
     def inputs(self, start, n):
         k, r = divmod(start, self.GB)
@@ -79,6 +80,8 @@ def parse():
     p.add_argument("--schedule", default="rotate", choices=["rotate", "chimera", "1f1b", "gpipe"])
     p.add_argument("--dataset_batches", type=int, default=4, help="distinct batches cycled through")
     p.add_argument("--model", default="mlp")
+    p.add_argument("--pixels", default="u8", choices=["u8", "f32"],
+                   help="image storage: MNIST's uint8 bytes (ToTensor's /255 fused into fc1) or float32")
     return p.parse_args()
 
 
@@ -120,10 +123,10 @@ def main():
     # fresh data every step, cycling over `dataset_batches` global batches; a rank
     # materialises images only for the shards it feeds into stage 0 (labels for all)
     if world == 1:
-        ds = SyntheticMNIST(GB * a.dataset_batches, seed=1234, device=dev)
+        ds = SyntheticMNIST(GB * a.dataset_batches, seed=1234, device=dev, pixels=a.pixels)
     else:  # rotate: own shard of the group block; chimera/1f1b: the replica's whole batch
         own_lo = engine.local_start(0, B) + (mesh.pp_rank * B if kind == "rotate" else 0)
-        ds = _ShardedSynth(GB, own_lo, B, a.dataset_batches, dev)
+        ds = _ShardedSynth(GB, own_lo, B, a.dataset_batches, dev, pixels=a.pixels)
 
     def step(i):
         start = (i % a.dataset_batches) * GB
@@ -169,7 +172,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(sps / BASELINE_SAMPLES_PER_S, 2),
             "dtype": "fp32",
-            "data": "synthetic (on-device MNIST-shape, random-init weights)",
+            "data": ("synthetic (on-device MNIST-shape, random-init weights; "
+                     + ("uint8 pixels as MNIST ships them, ToTensor /255 fused into fc1's fp32-accurate GEMM)"
+                        if a.pixels == "u8" else "float32 pixels)")),
             "config": {
                 "model": "mlp-784-128-10 (2 pipeline stages)",
                 "global_batch": GB,

@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "kernels.h"
@@ -67,7 +68,13 @@ struct X3Params {
   int epi;
   int kps;  // K per split (multiple of BK)
   int tiles_m, tiles_n;
+  const unsigned char* X8;  // U8 kernels: the uint8 pixel operand (A for U8_A, B for U8_B)
+  float scale;              // U8 kernels: C = scale * acc (+ bias); 1/255 = ToTensor's scaling
 };
+
+// which operand (if any) is a uint8 pixel matrix: integers 0..255 have at most 8 significant
+// bits, so the operand is EXACT in one bf16 plane and each product needs 3 MFMAs, not 6
+enum { U8_NONE = 0, U8_A = 1, U8_B = 2 };
 
 // ---- the split ---------------------------------------------------------------------------------
 __device__ __forceinline__ u16 bf16_bits(float f) {
@@ -278,6 +285,79 @@ struct StagePre {
   }
 };
 
+// uint8 pixel operand -> one exact bf16 plane.
+//   k-contiguous (ROWS x 32 bytes per K-step): a thread owns one 16-B chunk = 16 k of one row
+//   (rows r0 + id/2, k0 + 16*(id&1)); host contract K % 16 == 0, ld % 16 == 0, 16-B aligned base.
+//   k-major (32 k-rows x ROWS bytes): a thread owns 8 bytes = 8 rows at one k (k0 + id/16, rows
+//   r0 + 8*(id&15)); host contract rows % 8 == 0, ld % 8 == 0, 8-B aligned base.
+// Same clamped, branch-free loads as Stage; past-the-end k is zeroed by zero_tail.
+template <bool KM, int ROWS, int NT = ::sdml::NT>
+struct StageU8 {
+  static constexpr int NC = KM ? (BK * ROWS / 8) / NT : (ROWS * 2) / NT;
+  static_assert(NC >= 1, "tile too small for the thread count");
+  typedef typename std::conditional<KM, uint2, uint4>::type V;
+  V v[NC];
+
+  __device__ __forceinline__ void load(const unsigned char* __restrict__ P, int ld, int rows, int r0, int k0, int K) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int id = threadIdx.x + NT * c;
+      size_t o;
+      if constexpr (!KM) {
+        const int gr = min(r0 + (id >> 1), rows - 1);
+        const int gk = min(k0 + 16 * (id & 1), K - 16);
+        o = (size_t)gr * ld + gk;
+      } else {
+        const int gk = min(k0 + (id >> 4), K - 1);
+        const int gr = min(r0 + 8 * (id & 15), rows - 8);
+        o = (size_t)gk * ld + gr;
+      }
+      v[c] = *reinterpret_cast<const V*>(P + o);
+    }
+  }
+  __device__ __forceinline__ void zero_tail(int k0, int kend) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int id = threadIdx.x + NT * c;
+      const int gk = KM ? k0 + (id >> 4) : k0 + 16 * (id & 1);
+      if constexpr (!KM) {
+        const uint4 z = {0u, 0u, 0u, 0u};
+        v[c] = gk < kend ? v[c] : z;
+      } else {
+        const uint2 z = {0u, 0u};
+        v[c] = gk < kend ? v[c] : z;
+      }
+    }
+  }
+  __device__ __forceinline__ void accum_rowsum(float (&)[4]) const {}
+
+  // bytes -> bf16 bit patterns: (float)b has its significant bits in the upper half
+  __device__ __forceinline__ static u16x8 widen8(unsigned lo, unsigned hi) {
+    u16x8 r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      r[e] = (u16)(__float_as_uint((float)((lo >> (8 * e)) & 0xffu)) >> 16);
+      r[4 + e] = (u16)(__float_as_uint((float)((hi >> (8 * e)) & 0xffu)) >> 16);
+    }
+    return r;
+  }
+  template <int PL>
+  __device__ __forceinline__ void store(u16* L) const {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int id = threadIdx.x + NT * c;
+      if constexpr (!KM) {
+        const int r = id >> 1, h = id & 1;
+        *reinterpret_cast<u16x8*>(L + kc_off(r, 2 * h)) = widen8(v[c].x, v[c].y);
+        *reinterpret_cast<u16x8*>(L + kc_off(r, 2 * h + 1)) = widen8(v[c].z, v[c].w);
+      } else {
+        const int k = id >> 4, row = 8 * (id & 15);
+        *reinterpret_cast<u16x8*>(L + km_off(k, row >> 3)) = widen8(v[c].x, v[c].y);
+      }
+    }
+  }
+};
+
 // fp32 -> three bf16 planes (hi, mid, lo), 4 elements per thread (n % 4 == 0)
 __global__ void __launch_bounds__(256) split3_planes_kernel(const float* __restrict__ x, u16* __restrict__ out,
                                                             int64_t n) {
@@ -340,14 +420,21 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 // same basic block as tile t's MFMAs (the scheduler interleaves the VALU/LDS work into the
 // matrix-core shadow); otherwise they follow the MFMAs (tile t+1 loaded during tile t).
 // BPRE: B arrives pre-split (p.Bp; k-contiguous B only)
-template <bool A_KM, bool B_KM, bool AMASK, bool EARLY, bool BPRE = false>
+// U8: U8_A = A is a k-contiguous uint8 matrix (p.X8), U8_B = B is a k-major uint8 matrix; that
+// operand takes one LDS plane and each product 3 MFMAs; the epilogue scales by p.scale.
+// DEEP (EARLY only): two tiles in flight in registers instead of one (LEAD = 2 K-steps of load
+// latency cover instead of 1)
+template <bool A_KM, bool B_KM, bool AMASK, bool EARLY, bool BPRE = false, int U8 = U8_NONE, bool DEEP = false>
 __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
   constexpr bool FRESH = true;
   constexpr int BM = A_KM ? 128 : 256;
   constexpr int WGM = BM / 64, WGN = 8 / WGM;  // wave grid
   constexpr int TN = BN / WGN / 32;             // 32-col MFMA tiles per wave (TM = 2)
   constexpr int AP = BM * BK, BP = BN * BK;     // u16 per plane
-  constexpr int BUF = 3 * (AP + BP);
+  constexpr int NPA = U8 == U8_A ? 1 : 3, NPB = U8 == U8_B ? 1 : 3;  // bf16 planes per operand
+  static_assert(U8 != U8_A || (!A_KM && !AMASK), "uint8 A: k-contiguous, unmasked");
+  static_assert(U8 != U8_B || (B_KM && !BPRE), "uint8 B: k-major");
+  constexpr int BUF = NPA * AP + NPB * BP;
   __shared__ __attribute__((aligned(16))) u16 smem[2 * BUF];
 
   // XCD-aware bijective remap over tiles x splits (blocks b, b+8 share an XCD): each XCD gets a
@@ -384,56 +471,56 @@ __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
   const bool do_rowsum = p.rowsum != nullptr && tn == 0;
   float rs[4] = {0.f, 0.f, 0.f, 0.f};
 
-  Stage<A_KM, BM> sa;
-  typedef typename std::conditional<BPRE, StagePre<BN>, Stage<B_KM, BN>>::type SB;
-  SB sb;
-  auto load = [&](int k0) {
-    sa.template load<AMASK>(p.A, p.amask, p.lda, p.M, m0, k0, p.K);
-    if constexpr (BPRE) sb.load(p.Bp, p.ldb, p.N, n0, k0, p.K);
-    else sb.template load<false>(p.B, nullptr, p.ldb, p.N, n0, k0, p.K);
+  typedef typename std::conditional<U8 == U8_A, StageU8<false, BM>, Stage<A_KM, BM>>::type SA;
+  typedef typename std::conditional<BPRE, StagePre<BN>,
+                                    typename std::conditional<U8 == U8_B, StageU8<true, BN>, Stage<B_KM, BN>>::type>::type SB;
+  SA sa, sa2;  // register stages (sa2: second in-flight tile of the DEEP pipeline)
+  SB sb, sb2;
+  auto load = [&](SA& ra, SB& rb, int k0) {
+    if constexpr (U8 == U8_A) ra.load(p.X8, p.lda, p.M, m0, k0, p.K);
+    else ra.template load<AMASK>(p.A, p.amask, p.lda, p.M, m0, k0, p.K);
+    if constexpr (BPRE) rb.load(p.Bp, p.ldb, p.N, n0, k0, p.K);
+    else if constexpr (U8 == U8_B) rb.load(p.X8, p.ldb, p.N, n0, k0, p.K);
+    else rb.template load<false>(p.B, nullptr, p.ldb, p.N, n0, k0, p.K);
   };
   // tile staged for k0 -> K-tail zeroing -> bias-grad row sums -> split -> LDS buffer `buf`
-  auto store = [&](int buf, int k0) {
-    sa.zero_tail(k0, kend);
-    sb.zero_tail(k0, kend);
-    sa.accum_rowsum(rs);
+  auto store = [&](SA& ra, SB& rb, int buf, int k0) {
+    ra.zero_tail(k0, kend);
+    rb.zero_tail(k0, kend);
+    ra.accum_rowsum(rs);
     u16* L = smem + buf * BUF;
-    sa.template store<AP>(L);
-    sb.template store<BP>(L + 3 * AP);
+    ra.template store<AP>(L);
+    rb.template store<BP>(L + NPA * AP);
   };
 
+  // one K-step on LDS buffer t & 1. EARLY: (ra, rb) hold tile t+1 (loaded LEAD K-steps ago); it is
+  // split into the other buffer, whose last readers passed the previous barrier, and tile
+  // t+1+LEAD is loaded in its place. Past the end both are harmless: zero tiles written to a
+  // buffer nobody reads again.
+  constexpr int LEAD = DEEP ? 2 : 1;
   const int nk = (kend - kbeg + BK - 1) / BK;
-  if (nk > 0) {
-    load(kbeg);
-    store(0, kbeg);
-    if (EARLY) load(kbeg + BK);  // zeroed at split time past kend
-  }
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
+  auto kstep = [&](int t, SA& ra, SB& rb) {
     const int cur = t & 1;
     const u16* As = smem + cur * BUF;
-    const u16* Bs = As + 3 * AP;
+    const u16* Bs = As + NPA * AP;
     if constexpr (!EARLY) {
-      if (t + 1 < nk) load(kbeg + (t + 1) * BK);  // next tile -> registers (latency under the MFMAs)
+      if (t + 1 < nk) load(ra, rb, kbeg + (t + 1) * BK);  // next tile -> registers (latency under the MFMAs)
     }
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
-      bf16x8 a[2][3], b[TN][3];
+      bf16x8 a[2][NPA], b[TN][NPB];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) a[i][pl] = frag<A_KM>(As + pl * AP, wm * 64 + i * 32, s, lane);
+        for (int pl = 0; pl < NPA; ++pl) a[i][pl] = frag<A_KM>(As + pl * AP, wm * 64 + i * 32, s, lane);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) b[j][pl] = frag<B_KM>(Bs + pl * BP, wn * (32 * TN) + j * 32, s, lane);
+        for (int pl = 0; pl < NPB; ++pl) b[j][pl] = frag<B_KM>(Bs + pl * BP, wn * (32 * TN) + j * 32, s, lane);
       if constexpr (EARLY) {
         if (s == 0) {
-          // tile t+1 (in registers since the previous K-step) -> split -> the other buffer, whose
-          // last readers passed the previous barrier; then tile t+2 -> registers. Past the end
-          // both are harmless: zero tiles written to a buffer nobody reads again.
-          store(cur ^ 1, kbeg + (t + 1) * BK);
-          load(kbeg + (t + 2) * BK);
+          store(ra, rb, cur ^ 1, kbeg + (t + 1) * BK);
+          load(ra, rb, kbeg + (t + 1 + LEAD) * BK);
         }
       }
       // small terms first, the leading hi*hi term last
@@ -442,12 +529,22 @@ __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           f32x16 c = (FRESH && s == 0) ? f32x16{} : (FRESH ? part[i][j] : acc[i][j]);
-          c = mfma(a[i][1], b[j][1], c);  // mid*mid
-          c = mfma(a[i][2], b[j][0], c);  // lo*hi
-          c = mfma(a[i][0], b[j][2], c);  // hi*lo
-          c = mfma(a[i][1], b[j][0], c);  // mid*hi
-          c = mfma(a[i][0], b[j][1], c);  // hi*mid
-          c = mfma(a[i][0], b[j][0], c);  // hi*hi
+          if constexpr (U8 == U8_A) {  // exact A: a*b = a*(hi + mid + lo)
+            c = mfma(a[i][0], b[j][NPB - 1], c);
+            c = mfma(a[i][0], b[j][NPB > 1 ? 1 : 0], c);
+            c = mfma(a[i][0], b[j][0], c);
+          } else if constexpr (U8 == U8_B) {
+            c = mfma(a[i][NPA - 1], b[j][0], c);
+            c = mfma(a[i][NPA > 1 ? 1 : 0], b[j][0], c);
+            c = mfma(a[i][0], b[j][0], c);
+          } else {
+            c = mfma(a[i][1], b[j][1], c);  // mid*mid
+            c = mfma(a[i][2], b[j][0], c);  // lo*hi
+            c = mfma(a[i][0], b[j][2], c);  // hi*lo
+            c = mfma(a[i][1], b[j][0], c);  // mid*hi
+            c = mfma(a[i][0], b[j][1], c);  // hi*mid
+            c = mfma(a[i][0], b[j][0], c);  // hi*hi
+          }
           if constexpr (FRESH) {
             if (s == BK / 16 - 1) acc[i][j] += c;
             else part[i][j] = c;
@@ -457,11 +554,32 @@ __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
         }
     }
     if constexpr (!EARLY) {
-      if (t + 1 < nk) store(cur ^ 1, kbeg + (t + 1) * BK);
+      if (t + 1 < nk) store(ra, rb, cur ^ 1, kbeg + (t + 1) * BK);
     }
     __syncthreads();
+  };
+
+  if (nk > 0) {
+    load(sa, sb, kbeg);
+    store(sa, sb, 0, kbeg);
+    if constexpr (DEEP) {
+      load(sa2, sb2, kbeg + BK);  // tiles 1 and 2 in flight (zeroed at split time past kend)
+      load(sa, sb, kbeg + 2 * BK);
+    } else if constexpr (EARLY) {
+      load(sa, sb, kbeg + BK);
+    }
   }
-  // EARLY staged one tile past the end in the last iteration: zeroed, row sums unaffected
+  __syncthreads();
+  if constexpr (DEEP) {
+    // two register stages alternate: K-step t splits the stage holding tile t+1
+    for (int t = 0; t < nk; t += 2) {
+      kstep(t, sa2, sb2);
+      if (t + 1 < nk) kstep(t + 1, sa, sb);
+    }
+  } else {
+    for (int t = 0; t < nk; ++t) kstep(t, sa, sb);
+  }
+  // EARLY staged LEAD tiles past the end: zeroed, row sums unaffected
 
   if (do_rowsum) {
     if constexpr (!A_KM) {
@@ -497,7 +615,7 @@ __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (row >= p.M) continue;
-        const float v = acc[i][j][r];
+        const float v = U8 != U8_NONE ? acc[i][j][r] * p.scale : acc[i][j][r];
         float* dst = p.C + (size_t)row * p.ldc + col;
         switch (p.epi) {
           case EPI_STORE:
@@ -524,6 +642,17 @@ bool operand_ok(const float* P, const float* mask, int ld, bool kmajor, int rows
 }  // namespace
 
 static int g_x3_variant = 0;  // pipeline A/B: 0 = EARLY split (default), 1 = split after the MFMAs
+
+// DEEP register pipeline (two tiles in flight) for the uint8 kernels. Measured at 131072 x 784 -> 128
+// (tools/bench_u8.py): forward 144 us 1-deep vs 153 us DEEP; weight gradient 172 us 1-deep
+// (167 us with 2 workgroups/CU) vs 154 us DEEP. SDML_X3_DEEP=0/1 forces one for both (A/B).
+static bool x3_deep(bool dflt) {
+  static const int force = [] {
+    const char* e = getenv("SDML_X3_DEEP");
+    return e ? (e[0] == '0' ? 0 : 1) : -1;
+  }();
+  return force < 0 ? dflt : force == 1;
+}
 
 bool gemm_f32x3_eligible(const GemmArgs& g) {
   if (g.M <= 0 || g.N <= 0 || g.K <= 0) return false;
@@ -558,6 +687,8 @@ void gemm_f32x3(const GemmArgs& g, hipStream_t stream) {
   p.ldb = g.ldb;
   p.ldc = g.ldc;
   p.epi = g.epi;
+  p.X8 = nullptr;
+  p.scale = 1.f;
   const int bm = g.a_kmajor ? 128 : 256;
   // atomic epilogues are split-invariant: pick the split count for THIS kernel's geometry
   int splits = g.epi == EPI_ATOMIC ? gemm_f32x3_pick_splits(g.M, g.N, g.K, g.a_kmajor) : 1;
@@ -617,6 +748,69 @@ void split3_planes_t(const float* w, unsigned short* out, int R, int C, hipStrea
 
 bool gemm_f32x3_can_presplit_b(const GemmArgs& g) {
   return !g.a_kmajor && !g.b_kmajor && g.ldb % 8 == 0 && g.K % 8 == 0 && (size_t)g.N * g.ldb % 4 == 0;
+}
+
+// ---- uint8 pixel GEMMs (first layer fed straight from MNIST bytes) ----------------------------
+void gemm_u8x3_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_split, int N,
+                   const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream) {
+  X3Params p{};
+  p.X8 = X;
+  p.Bp = w_split;
+  p.C = C;
+  p.bias = bias;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = ldx;
+  p.ldb = K;
+  p.ldc = ldc;
+  p.epi = bias ? (relu ? EPI_BIAS_RELU : EPI_BIAS) : EPI_STORE;
+  p.scale = scale;
+  p.kps = (K + BK - 1) / BK * BK;
+  p.tiles_m = (M + 255) / 256;
+  p.tiles_n = (N + BN - 1) / BN;
+  if (x3_deep(false))
+    hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A, true>), dim3(p.tiles_m * p.tiles_n, 1, 1),
+                       dim3(NT), 0, stream, p);
+  else
+    hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A>), dim3(p.tiles_m * p.tiles_n, 1, 1),
+                       dim3(NT), 0, stream, p);
+}
+
+// gw[N,K] += scale * sum_m gz[m,n] X[m,k]; gb[n] += sum_m gz[m,n] (gb optional)
+void gemm_u8x3_wgrad(const float* gz, const unsigned char* X, int M, int N, int K, int ldx, float* gw, float* gb,
+                     float scale, hipStream_t stream) {
+  X3Params p{};
+  p.A = gz;
+  p.X8 = X;
+  p.C = gw;
+  p.rowsum = gb;
+  p.M = N;
+  p.N = K;
+  p.K = M;
+  p.lda = N;
+  p.ldb = ldx;
+  p.ldc = K;
+  p.epi = EPI_ATOMIC;
+  p.scale = scale;
+  // workgroups per CU the split count aims at (the 1-deep kernel fits 2 per CU: 125 VGPRs, 64 KiB LDS)
+  static const int wg_per_cu = [] {
+    const char* e = getenv("SDML_U8_WGRAD_WG_PER_CU");
+    return e ? std::max(1, atoi(e)) : 1;
+  }();
+  int splits = gemm_f32x3_pick_splits(N, K, M, true) * wg_per_cu;
+  int kps = (M + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = (M + kps - 1) / kps;
+  p.kps = kps;
+  p.tiles_m = (N + 127) / 128;
+  p.tiles_n = (K + BN - 1) / BN;
+  if (x3_deep(true))
+    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true>),
+                       dim3(p.tiles_m * p.tiles_n, splits, 1), dim3(NT), 0, stream, p);
+  else
+    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B>), dim3(p.tiles_m * p.tiles_n, splits, 1),
+                       dim3(NT), 0, stream, p);
 }
 
 }  // namespace sdml

@@ -69,6 +69,16 @@ void split3_planes(const float* x, unsigned short* out, int64_t n, hipStream_t s
 // transposed split: w [R][C] fp32 -> bf16 planes [3][C][R] (pre-split B = W^T of an input-gradient GEMM)
 void split3_planes_t(const float* w, unsigned short* out, int R, int C, hipStream_t stream);
 void gemm_f32x3_set_variant(int v);  // pipeline A/B: 0 = early split (default), 1 = split after MFMAs
+// uint8-pixel first layer on the bf16x3 engine (the pixel operand is exact in one bf16 plane:
+// 3 MFMAs per product, 1 byte per element read). X [M][ldx] uint8.
+//   fwd  : C[M,N] = act(scale * X W^T + b), W given pre-split (split3_planes, [3][N][K]);
+//          K % 16 == 0, ldx % 16 == 0, X 16-B aligned, ldc >= N
+//   wgrad: gw[N,K] += scale * gz^T X, gb[N] += colsum(gz) (gb may be null); gz [M,N] fp32;
+//          K % 8 == 0, ldx % 8 == 0, X 8-B aligned, N % 4 == 0
+void gemm_u8x3_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_split, int N,
+                   const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream);
+void gemm_u8x3_wgrad(const float* gz, const unsigned char* X, int M, int N, int K, int ldx, float* gw, float* gb,
+                     float scale, hipStream_t stream);
 
 // ---- fused classifier head: z = x W^T + b; log_softmax; NLL; backward --------------------
 // x [M,K] fp32, W [C,K], b [C], target [M] int64. stats[0] += sum loss, stats[1] += #correct.

@@ -160,6 +160,53 @@ c10::optional<torch::Tensor> linear_bwd_f32(torch::Tensor x, c10::optional<torch
   return dx;
 }
 
+// first layer fed by uint8 pixels (MNIST's native bytes): y = act(scale * x_u8 @ w.T + b), with
+// scale = 1/255 this is ToTensor() fused into the GEMM's operand load. Shapes the uint8 kernel
+// does not take (small batches, unaligned K) go through an fp32 copy of x * scale.
+torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> b, bool relu,
+                            double scale) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
+              "linear_fwd_u8: x must be a contiguous 2-D uint8 ROCm tensor");
+  check_f32_cuda(w, "w");
+  TORCH_CHECK(w.dim() == 2 && x.size(1) == w.size(1), "linear_fwd_u8: shape mismatch ", x.sizes(), " vs ", w.sizes());
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  check_opt(b, "b", N);
+  TORCH_CHECK(!relu || opt_ptr(b), "relu epilogue requires a bias");
+  const bool direct = M >= 4096 && K % 16 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
+                      M * K < (int64_t(1) << 31);
+  if (!direct) return linear_fwd_f32(x.to(torch::kFloat32).mul_(scale), w, b, relu);
+  auto y = torch::empty({M, N}, w.options());
+  auto wsplit = torch::empty({3, N, K}, w.options().dtype(torch::kInt16));
+  sdml::split3_planes(w.data_ptr<float>(), reinterpret_cast<unsigned short*>(wsplit.data_ptr<int16_t>()), N * K,
+                      cur_stream());
+  sdml::gemm_u8x3_fwd(x.data_ptr<uint8_t>(), (int)M, (int)K, (int)K,
+                      reinterpret_cast<const unsigned short*>(wsplit.data_ptr<int16_t>()), (int)N, opt_ptr(b),
+                      y.data_ptr<float>(), (int)N, relu, (float)scale, cur_stream());
+  return y;
+}
+
+// weight/bias gradient of the uint8-fed first layer: gw += scale * gz^T x_u8, gb += colsum(gz)
+void linear_wgrad_u8(torch::Tensor x, torch::Tensor gz, torch::Tensor gw, c10::optional<torch::Tensor> gb,
+                     double scale) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
+              "linear_wgrad_u8: x must be a contiguous 2-D uint8 ROCm tensor");
+  check_f32_cuda(gz, "gz");
+  check_f32_cuda(gw, "gw");
+  const int64_t M = x.size(0), K = x.size(1), N = gz.size(1);
+  TORCH_CHECK(gz.dim() == 2 && gz.size(0) == M && gw.size(0) == N && gw.size(1) == K, "linear_wgrad_u8: shape mismatch");
+  check_opt(gb, "gb", N);
+  const bool direct = M >= 4096 && K % 8 == 0 && N % 4 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 7) == 0 &&
+                      M * K < (int64_t(1) << 31);
+  if (!direct) {
+    auto xf = x.to(torch::kFloat32).mul_(scale);
+    linear_bwd_f32(xf, c10::nullopt, gz, gw, gw, gb, false, false, false);
+    return;
+  }
+  sdml::gemm_u8x3_wgrad(gz.data_ptr<float>(), x.data_ptr<uint8_t>(), (int)M, (int)N, (int)K, (int)K,
+                        gw.data_ptr<float>(), opt_ptr(gb), (float)scale, cur_stream());
+}
+
+
 // generic GEMM entry (tests/benchmarks): C = A(m,k) B(n,k) with layout flags
 void gemm_f32_op(torch::Tensor A, torch::Tensor B, torch::Tensor C, bool a_kmajor, bool b_kmajor, int64_t epi,
                  int64_t splits, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> rowsum) {
@@ -872,6 +919,10 @@ c10::optional<torch::Tensor> ref_cnn_stage1(torch::Tensor x, torch::Tensor w1, t
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "sdml gfx950 HIP kernels";
+  m.def("linear_fwd_u8", &linear_fwd_u8, "act(scale * x_u8 @ w.T + b): uint8-pixel first layer", py::arg("x"),
+        py::arg("w"), py::arg("b"), py::arg("relu"), py::arg("scale"));
+  m.def("linear_wgrad_u8", &linear_wgrad_u8, "gw += scale * gz^T x_u8, gb += colsum(gz)", py::arg("x"), py::arg("gz"),
+        py::arg("gw"), py::arg("gb"), py::arg("scale"));
   m.def("linear_fwd_f32", &linear_fwd_f32, "relu?(x @ w.T + b) on fp32 MFMA", py::arg("x"), py::arg("w"),
         py::arg("b"), py::arg("relu"));
   m.def("linear_bwd_f32", &linear_bwd_f32, "backward of linear(+relu): accumulates gw/gb, returns dx",

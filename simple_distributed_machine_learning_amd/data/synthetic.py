@@ -7,7 +7,10 @@ Neither the network nor torchvision exists here, so:
 * :class:`SyntheticMNIST` — counter-based, seed-deterministic MNIST-shape data
   ([N,1,28,28] float32 in [0,1], int64 labels in [0,10)), generated directly in HBM by a
   HIP kernel (or on the host by the bit-identical C++ twin). Every rank builds the same
-  dataset locally, so labels never cross the wire.
+  dataset locally, so labels never cross the wire. ``pixels="u8"`` stores the images the way
+  MNIST ships them, as uint8 bytes k = round(255 x); ``ToTensor()`` (k / 255) is then applied
+  by the consuming stage (fused into the first GEMM for the MLPs, ``ops.pixels_to_float``
+  otherwise), which reads a quarter of the bytes.
 * :class:`IdxMNIST` — reads real MNIST ``*-idx?-ubyte`` files if the user has them locally
   (no download), ``ToTensor()`` scaling like the reference.
 * :class:`SyntheticTokens` — GPT-2 style token sequences for the transformer configs.
@@ -43,7 +46,7 @@ class SyntheticMNIST(Dataset):
     H = W = 28
 
     def __init__(self, n: int, seed: int = 1234, device="cpu", mode: str = "learnable", offset: int = 0,
-                 image_range=None):
+                 image_range=None, pixels: str = "f32"):
         """``image_range=(lo, hi)``: materialise images only for samples [lo, hi) (labels for
         all n) — a rank that runs stage 0 only on its own shard needs no other images."""
         self.n = int(n)
@@ -56,6 +59,12 @@ class SyntheticMNIST(Dataset):
         self.y = torch.empty((self.n,), dtype=torch.int64, device=self.device)
         if self.n:
             self._fill()
+        if pixels == "u8":
+            # MNIST's storage format: bytes k = round(255 x) (deterministic fp32 ops: the same
+            # bytes on every device); the float32 view of a sample is k / 255 (ToTensor)
+            self.x = self.x.mul_(255.0).round_().to(torch.uint8)
+        elif pixels != "f32":
+            raise ValueError(f"pixels must be 'f32' or 'u8', got {pixels!r}")
 
     def _fill(self):
         if self.device.type == "cuda":

@@ -30,6 +30,9 @@ class PipelineStage(nn.Module):
     # "nll": stage output is log-probabilities (reference: log_softmax + nll_loss, :79, :111)
     # "ce": stage output is logits (cross-entropy)
     loss_kind: str = "nll"
+    # True if stage 0 takes uint8 pixel batches itself (ToTensor's /255 fused into its first
+    # kernel); otherwise the engine converts them with ops.pixels_to_float first
+    accepts_u8_pixels: bool = False
 
     @property
     def is_first(self) -> bool:

@@ -55,6 +55,8 @@ class MLPStage(PipelineStage):
             setattr(self, name, nn.Linear(dims[i], dims[i + 1]))
         self.loss_kind = "nll"
         self.in_features = dims[self.layer_ids[0]]
+        # stage 0 reads MNIST's uint8 pixels directly (ToTensor fused into fc1's GEMM)
+        self.accepts_u8_pixels = self.layer_ids[0] == 0
 
     def layers(self) -> List[nn.Linear]:
         return [getattr(self, n) for n in self.names]
@@ -63,7 +65,7 @@ class MLPStage(PipelineStage):
         return self.layer_ids[i] == self.n_total - 1
 
     def forward(self, x):
-        x = x.reshape(x.shape[0], -1)
+        x = ops.pixels_to_float(x.reshape(x.shape[0], -1))
         for i, lin in enumerate(self.layers()):
             x = lin(x)
             if self._is_classifier(i):
@@ -80,12 +82,17 @@ class MLPStage(PipelineStage):
         if not self._fused(x):
             return super().fwd(x, ctx, train)
         x = x.reshape(x.shape[0], -1)
-        if x.dtype != torch.float32 or not x.is_contiguous():
+        if x.dtype == torch.uint8:
+            x = x.contiguous()
+        elif x.dtype != torch.float32 or not x.is_contiguous():
             x = x.float().contiguous()
         acts = [x]
         for i, lin in enumerate(self.layers()):
             assert not self._is_classifier(i), "classifier layers run in head_fwd"
-            x = ops.linear_relu_fwd(x, lin.weight, lin.bias)
+            if x.dtype == torch.uint8:
+                x = ops.linear_relu_fwd_u8(x, lin.weight, lin.bias)
+            else:
+                x = ops.linear_relu_fwd(x, lin.weight, lin.bias)
             acts.append(x)
         if train:
             ctx["acts"] = acts
@@ -103,6 +110,9 @@ class MLPStage(PipelineStage):
         layers = self.layers()
         for i in range(len(layers) - 1, -1, -1):
             lin = layers[i]
+            if acts[i].dtype == torch.uint8:  # uint8 pixels: first layer, no input gradient
+                ops.linear_wgrad_u8(acts[i], g, lin.weight.grad, lin.bias.grad)
+                return None
             need_dx = (i > 0) or (not self.is_first)
             g = ops.linear_relu_bwd(acts[i], acts[i + 1], g, lin.weight, lin.weight.grad, lin.bias.grad, need_dx,
                                     gy_masked=True, mask_dx=need_dx)
@@ -111,7 +121,7 @@ class MLPStage(PipelineStage):
     def head_fwd(self, x, target, ctx, train, loss_scale, stats=None):
         if not self._fused(x):
             return super().head_fwd(x, target, ctx, train, loss_scale)
-        x = x.reshape(x.shape[0], -1)
+        x = ops.pixels_to_float(x.reshape(x.shape[0], -1))
         if x.dtype != torch.float32 or not x.is_contiguous():
             x = x.float().contiguous()
         layers = self.layers()

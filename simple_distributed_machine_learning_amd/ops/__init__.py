@@ -25,6 +25,33 @@ def linear_relu_fwd(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.
     return ref.linear_relu_fwd(x, w, b)
 
 
+PIXEL_SCALE = 1.0 / 255.0  # torchvision ToTensor(): uint8 pixel k -> k / 255
+
+
+def pixels_to_float(x: torch.Tensor) -> torch.Tensor:
+    """uint8 pixels -> float32 in [0, 1] exactly as ``ToTensor()`` (the reference's transform,
+    /root/reference/simple_distributed.py:87-88); float input passes through."""
+    return x.to(torch.float32).div_(255.0) if x.dtype == torch.uint8 else x
+
+
+def linear_relu_fwd_u8(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """relu(ToTensor(x) @ w.T + b) for uint8 pixels x [M,K]: on ROCm the /255 is folded into the
+    bf16x3 GEMM's epilogue and each pixel byte is an exact single bf16 plane (3 MFMAs/product)."""
+    if x.is_cuda:
+        return _k().linear_fwd_u8(x, w, b, True, PIXEL_SCALE)
+    return ref.linear_relu_fwd(pixels_to_float(x), w, b)
+
+
+def linear_wgrad_u8(x: torch.Tensor, gz: torch.Tensor, gw: torch.Tensor, gb: Optional[torch.Tensor]) -> None:
+    """gw += gz.T @ ToTensor(x), gb += sum(gz) for uint8 pixels x (first layer: no input grad)."""
+    if x.is_cuda:
+        _k().linear_wgrad_u8(x, gz, gw, gb, PIXEL_SCALE)
+        return
+    gw += gz.t() @ pixels_to_float(x)
+    if gb is not None:
+        gb += gz.sum(0)
+
+
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
     if x.is_cuda:
         return _k().linear_fwd_f32(x, w, b, False)

@@ -31,6 +31,7 @@ import torch
 import torch.distributed as dist
 
 from ..models.base import ModelSpec, PipelineStage, build_stages
+from ..ops import pixels_to_float
 from ..ops.optim import FusedSGD
 from ..utils.flat import FlatParams
 from ..utils.timing import PhaseTimer
@@ -302,6 +303,8 @@ class PipelineEngine:
                     x = dataset.inputs(off, mbsz)
                     if x.device != dev:
                         x = x.to(dev, non_blocking=True)
+                    if x.dtype == torch.uint8 and not mod.accepts_u8_pixels:
+                        x = pixels_to_float(x)
                 else:
                     prev_local = sched.task_rank(ins.mb, ins.stage - 1) == self.mesh.pp_rank
                     x = take((PL_ACT, ins.pipe, ins.stage - 1, ins.mb), prev_local)
@@ -405,6 +408,8 @@ class PipelineEngine:
             x = dataset.inputs(start + me * batch_size + woff[w], bw)
             if x.device != dev:
                 x = x.to(dev, non_blocking=True)
+            if x.dtype == torch.uint8 and not s0.accepts_u8_pixels:
+                x = pixels_to_float(x)
             with tm.span("fwd", 0):
                 h = s0.fwd(x, ctx0[w], train)
             if R == 1:

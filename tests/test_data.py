@@ -62,3 +62,39 @@ def test_idx_mnist(tmp_path):
     assert torch.allclose(tr.x[0, 0], torch.tensor(imgs[0], dtype=torch.float32) / 255)
     te = IdxMNIST(str(tmp_path), False, fraction=1.0)
     assert len(te) == 20 and te.y.tolist() == lbls[:20].tolist()
+
+
+def test_synthetic_u8_pixels_are_mnist_bytes():
+    f = SyntheticMNIST(50, seed=3)
+    u = SyntheticMNIST(50, seed=3, pixels="u8")
+    assert u.x.dtype == torch.uint8 and u.x.shape == f.x.shape
+    assert torch.equal(u.x, (f.x * 255.0).round().to(torch.uint8))
+    assert torch.equal(u.y, f.y)
+    from simple_distributed_machine_learning_amd.ops import pixels_to_float
+
+    assert torch.equal(pixels_to_float(u.x), u.x.float() / 255.0)
+
+
+def test_cpu_engine_u8_pixels_equal_totensor_floats():
+    from simple_distributed_machine_learning_amd.models import get_model_spec
+    from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh
+
+    def eng(model):
+        mesh = init_mesh(pp=1, schedule_kind="1f1b", rank=0, world_size=1, device=torch.device("cpu"))
+        return PipelineEngine(get_model_spec(model, None), mesh, schedule_kind="1f1b", num_microbatches=2, lr=0.1,
+                              momentum=0.5, seed=2)
+
+    for model in ("mlp", "ref_cnn"):
+        a, b = eng(model), eng(model)
+        du = SyntheticMNIST(240, seed=4, pixels="u8")
+        df = SyntheticMNIST(240, seed=4)
+        df.x = du.x.float() / 255.0
+        for s in range(2):
+            if model == "ref_cnn":
+                torch.manual_seed(s)
+            ra = a.run(du, s * 120, 120, train=True)
+            if model == "ref_cnn":
+                torch.manual_seed(s)
+            rb = b.run(df, s * 120, 120, train=True)
+            assert float(ra.loss_sum) == float(rb.loss_sum)
+        assert torch.equal(a.flat.params, b.flat.params)

@@ -92,3 +92,23 @@ def test_resnet_bf16_hip_kernels_match_library_path(monkeypatch):
         assert abs(a - b) <= 0.02 * abs(b) + 0.02, (hip_losses, lib_losses)
     rel = (hip_p - lib_p).norm() / lib_p.norm()
     assert rel < 0.02, float(rel)
+
+
+@pytest.mark.parametrize("model,kind", [("mlp", "1f1b"), ("mlp", "rotate"), ("mlp4x1024", "gpipe"), ("ref_cnn", "1f1b")])
+def test_gpu_u8_pixels_match_cpu_float(model, kind):
+    """uint8 pixel batches (ToTensor fused into the MLPs' first GEMM on the GPU, converted by the
+    engine for other models) train like float32 k/255 images on the CPU engine. 8192-sample
+    batches put the MLP's first layer on the uint8 bf16x3 kernels."""
+    kw = {"dropout": 0.0} if model == "ref_cnn" else {}
+    B = 120 if model == "ref_cnn" else 8192
+    e_gpu = _engine(model, DEV, kind, 2, **kw)
+    e_cpu = _engine(model, torch.device("cpu"), kind, 2, **kw)
+    ds_g = SyntheticMNIST(2 * B, seed=5, device=DEV, pixels="u8")
+    ds_c = SyntheticMNIST(2 * B, seed=5, device="cpu")
+    assert ds_g.x.dtype == torch.uint8
+    ds_c.x = ds_g.x.cpu().float().div_(255.0)
+    for step in range(2):
+        rg = e_gpu.run(ds_g, step * B, B, train=True)
+        rc = e_cpu.run(ds_c, step * B, B, train=True)
+        torch.testing.assert_close(float(rg.loss_sum), float(rc.loss_sum), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(e_gpu.flat.params.cpu(), e_cpu.flat.params, rtol=1e-4, atol=5e-5)

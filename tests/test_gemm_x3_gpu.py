@@ -162,3 +162,50 @@ def test_linear_bwd_dx_presplit_transposed_weight(M, N, Kd):
     want = gy.double() @ w.double()
     bound = N * 2.0 ** -24 * (gy.abs().double() @ w.abs().double()) + 1e-30
     assert ((dx.double() - want).abs() <= bound).all()
+
+
+# ---- uint8-pixel first layer (ToTensor fused into the GEMM) ----------------------------------
+
+def pixels(M, Kd, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randint(0, 256, (M, Kd), generator=g, dtype=torch.uint8).to(DEV)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(131072, 128, 784), (4096 + 77, 128, 784), (5000, 1024, 784), (8192, 36, 96)])
+def test_linear_fwd_u8_matches_fp32_reference(M, N, Kd):
+    x8 = pixels(M, Kd, 3)
+    w, b = rnd(N, Kd, seed=4, lo=-0.05, hi=0.05), rnd(N, seed=5)
+    y = K.linear_fwd_u8(x8, w, b, True, 1.0 / 255.0)
+    xf = x8.double() / 255.0
+    want = torch.relu(xf @ w.double().t() + b.double())
+    bound = Kd * 2.0 ** -24 * (xf @ w.double().abs().t() + b.double().abs()) + 1e-30
+    assert ((y.double() - want).abs() <= 2 * bound).all()
+    # the fp32 ToTensor path (x.float() / 255 through the fp32 GEMM) agrees to fp32 rounding
+    torch.testing.assert_close(y, ops.linear_relu_fwd(x8.float().div(255.0), w, b), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(131072, 128, 784), (4096 + 33, 128, 784), (6000, 1024, 784), (8192, 36, 96)])
+def test_linear_wgrad_u8_matches_fp32_reference(M, N, Kd):
+    x8 = pixels(M, Kd, 6)
+    gz = rnd(M, N, seed=7) * (rnd(M, N, seed=8) > 0).float()
+    gw0, gb0 = rnd(N, Kd, seed=9), rnd(N, seed=10)
+    gw, gb = gw0.clone(), gb0.clone()
+    K.linear_wgrad_u8(x8, gz, gw, gb, 1.0 / 255.0)
+    xf = x8.double() / 255.0
+    want_w = gw0.double() + gz.double().t() @ xf
+    want_b = gb0.double() + gz.double().sum(0)
+    bound = M * 2.0 ** -24 * (gz.double().abs().t() @ xf + gw0.double().abs()) + 1e-30
+    assert ((gw.double() - want_w).abs() <= 2 * bound).all(), float(((gw.double() - want_w).abs() / bound).max())
+    torch.testing.assert_close(gb.double(), want_b, rtol=1e-5, atol=1e-3)
+
+
+def test_u8_small_batch_falls_back_to_fp32():
+    x8 = pixels(60, 784, 11)
+    w, b = rnd(128, 784, seed=12, lo=-0.05, hi=0.05), rnd(128, seed=13)
+    y = K.linear_fwd_u8(x8, w, b, True, 1.0 / 255.0)
+    torch.testing.assert_close(y, ops.linear_relu_fwd(x8.float().div(255.0), w, b), rtol=1e-5, atol=1e-5)
+    gz = rnd(60, 128, seed=14)
+    gw, gb = torch.zeros(128, 784, device=DEV), torch.zeros(128, device=DEV)
+    K.linear_wgrad_u8(x8, gz, gw, gb, 1.0 / 255.0)
+    torch.testing.assert_close(gw, gz.t() @ (x8.float() / 255.0), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(gb, gz.sum(0), rtol=1e-5, atol=1e-5)

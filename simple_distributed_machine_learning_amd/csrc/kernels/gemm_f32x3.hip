@@ -295,6 +295,17 @@ template <bool KM, int ROWS, int NT = ::sdml::NT>
 struct StageU8 {
   static constexpr int NC = KM ? (BK * ROWS / 8) / NT : (ROWS * 2) / NT;
   static_assert(NC >= 1, "tile too small for the thread count");
+
+  // k-contiguous: row of the 16-k chunk pair owned by thread id (h = id & 1 picks the half).
+  // ds_write_b128 banks 8 contiguous lanes over 32 banks (128 B): lanes 2j, 2j+1 of an 8-lane
+  // group take rows base + {0, 1, 4, 5} (base = 8*(id>>4) + 2*((id>>3)&1)), so the two rows of
+  // each parity have swizzles differing in bit 0 and the group's 8 chunks land in 8 distinct
+  // 16-B bank slots (rows id>>1 put 2 rows of one parity on the same slots: 2-way conflicts,
+  // 1.7M SQ_LDS_BANK_CONFLICT cycles per forward at the headline shape).
+  __device__ __forceinline__ static int kc_row(int id) {
+    const int rr = (id >> 1) & 3;
+    return 8 * (id >> 4) + 2 * ((id >> 3) & 1) + (rr & 1) + 4 * (rr >> 1);
+  }
   typedef typename std::conditional<KM, uint2, uint4>::type V;
   V v[NC];
 
@@ -304,7 +315,7 @@ struct StageU8 {
       const int id = threadIdx.x + NT * c;
       size_t o;
       if constexpr (!KM) {
-        const int gr = min(r0 + (id >> 1), rows - 1);
+        const int gr = min(r0 + kc_row(id), rows - 1);
         const int gk = min(k0 + 16 * (id & 1), K - 16);
         o = (size_t)gr * ld + gk;
       } else {
@@ -347,7 +358,7 @@ struct StageU8 {
     for (int c = 0; c < NC; ++c) {
       const int id = threadIdx.x + NT * c;
       if constexpr (!KM) {
-        const int r = id >> 1, h = id & 1;
+        const int r = kc_row(id), h = id & 1;
         *reinterpret_cast<u16x8*>(L + kc_off(r, 2 * h)) = widen8(v[c].x, v[c].y);
         *reinterpret_cast<u16x8*>(L + kc_off(r, 2 * h + 1)) = widen8(v[c].z, v[c].w);
       } else {

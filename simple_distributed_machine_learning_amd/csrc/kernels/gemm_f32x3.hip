@@ -50,6 +50,8 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef u16 u16x8 __attribute__((ext_vector_type(8)));
 typedef u16 u16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int NT = 512;  // threads per workgroup (main kernel)
 constexpr int BK = 32;   // k per K-step
@@ -306,7 +308,9 @@ struct StageU8 {
     const int rr = (id >> 1) & 3;
     return 8 * (id >> 4) + 2 * ((id >> 3) & 1) + (rr & 1) + 4 * (rr >> 1);
   }
-  typedef typename std::conditional<KM, uint2, uint4>::type V;
+  // native vectors: a ?: select on HIP's uint4/uint2 structs is lowered through scratch memory
+  // (a scratch store + load and an s_waitcnt vmcnt(0) per K-step)
+  typedef typename std::conditional<KM, u32x2, u32x4>::type V;
   V v[NC];
 
   __device__ __forceinline__ void load(const unsigned char* __restrict__ P, int ld, int rows, int r0, int k0, int K) {
@@ -331,13 +335,8 @@ struct StageU8 {
     for (int c = 0; c < NC; ++c) {
       const int id = threadIdx.x + NT * c;
       const int gk = KM ? k0 + (id >> 4) : k0 + 16 * (id & 1);
-      if constexpr (!KM) {
-        const uint4 z = {0u, 0u, 0u, 0u};
-        v[c] = gk < kend ? v[c] : z;
-      } else {
-        const uint2 z = {0u, 0u};
-        v[c] = gk < kend ? v[c] : z;
-      }
+      const V z = {};
+      v[c] = gk < kend ? v[c] : z;
     }
   }
   __device__ __forceinline__ void accum_rowsum(float (&)[4]) const {}
@@ -359,11 +358,11 @@ struct StageU8 {
       const int id = threadIdx.x + NT * c;
       if constexpr (!KM) {
         const int r = kc_row(id), h = id & 1;
-        *reinterpret_cast<u16x8*>(L + kc_off(r, 2 * h)) = widen8(v[c].x, v[c].y);
-        *reinterpret_cast<u16x8*>(L + kc_off(r, 2 * h + 1)) = widen8(v[c].z, v[c].w);
+        *reinterpret_cast<u16x8*>(L + kc_off(r, 2 * h)) = widen8(v[c][0], v[c][1]);
+        *reinterpret_cast<u16x8*>(L + kc_off(r, 2 * h + 1)) = widen8(v[c][2], v[c][3]);
       } else {
         const int k = id >> 4, row = 8 * (id & 15);
-        *reinterpret_cast<u16x8*>(L + km_off(k, row >> 3)) = widen8(v[c].x, v[c].y);
+        *reinterpret_cast<u16x8*>(L + km_off(k, row >> 3)) = widen8(v[c][0], v[c][1]);
       }
     }
   }
@@ -655,8 +654,9 @@ bool operand_ok(const float* P, const float* mask, int ld, bool kmajor, int rows
 static int g_x3_variant = 0;  // pipeline A/B: 0 = EARLY split (default), 1 = split after the MFMAs
 
 // DEEP register pipeline (two tiles in flight) for the uint8 kernels. Measured at 131072 x 784 -> 128
-// (tools/bench_u8.py): forward 144 us 1-deep vs 153 us DEEP; weight gradient 172 us 1-deep
-// (167 us with 2 workgroups/CU) vs 154 us DEEP. SDML_X3_DEEP=0/1 forces one for both (A/B).
+// (tools/bench_u8.py, profiles/r1_u8_gemm_ab.txt): forward 114 us 1-deep vs 111 us DEEP; weight
+// gradient 161 us 1-deep (167 us with 2 workgroups/CU) vs 154 us DEEP. SDML_X3_DEEP=0/1 forces one
+// for both (A/B).
 static bool x3_deep(bool dflt) {
   static const int force = [] {
     const char* e = getenv("SDML_X3_DEEP");
@@ -780,7 +780,7 @@ void gemm_u8x3_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned
   p.kps = (K + BK - 1) / BK * BK;
   p.tiles_m = (M + 255) / 256;
   p.tiles_n = (N + BN - 1) / BN;
-  if (x3_deep(false))
+  if (x3_deep(true))
     hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A, true>), dim3(p.tiles_m * p.tiles_n, 1, 1),
                        dim3(NT), 0, stream, p);
   else

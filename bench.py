@@ -15,6 +15,11 @@ Placement ("rotate" pipeline; weak scaling: per-GPU work fixed at --batch_per_gp
   code with the exchange elided (both stages local).
   (--schedule chimera / 1f1b select the classic neighbour pipelines instead.)
 
+Data: synthetic MNIST-shape images stored as uint8 bytes, the way MNIST ships them (``--pixels u8``,
+default). ToTensor's /255, which the reference runs on the host per batch
+(/root/reference/simple_distributed.py:87-88), is folded into fc1's fp32-accurate GEMM (the bytes
+are exact in one bf16 plane; README "uint8 pixels"). ``--pixels f32`` stores float32 images instead.
+
 Timing contract: W untimed warm-up steps; barrier + device sync; K timed steps (each a full
 forward + backward + gradient sync + optimizer step over fresh data); barrier + device sync;
 the MAX elapsed over ranks; rank 0 prints one JSON line.

@@ -61,6 +61,9 @@ def add_engine_args(parser: argparse.ArgumentParser):
     g.add_argument("--data", default="auto", choices=["auto", "synthetic", "random", "mnist"],
                    help="auto: MNIST idx files under --data_dir if present, else synthetic")
     g.add_argument("--data_dir", default="data")
+    g.add_argument("--pixels", default="f32", choices=["f32", "u8"],
+                   help="image storage on the device: float32 (ToTensor applied at load) or MNIST's uint8 bytes "
+                        "(ToTensor's /255 applied by stage 0: fused into the first GEMM for the MLPs)")
     g.add_argument("--train_size", type=int, default=6000, help="reference keeps len(MNIST)//10")
     g.add_argument("--test_size", type=int, default=1000)
     g.add_argument("--seq_len", type=int, default=None, help="token models: sequence length")

@@ -112,7 +112,7 @@ class IdxMNIST(Dataset):
     FILES = {True: ("train-images-idx3-ubyte", "train-labels-idx1-ubyte"),
              False: ("t10k-images-idx3-ubyte", "t10k-labels-idx1-ubyte")}
 
-    def __init__(self, root: str, train: bool, device="cpu", fraction: float = 0.1):
+    def __init__(self, root: str, train: bool, device="cpu", fraction: float = 0.1, pixels: str = "f32"):
         root = Path(root)
         img_name, lbl_name = self.FILES[train]
 
@@ -123,7 +123,11 @@ class IdxMNIST(Dataset):
                     return cand
             raise FileNotFoundError(f"{name} not found under {root}")
 
-        x = _read_idx(find(img_name)).float().div_(255.0).unsqueeze(1)
+        x = _read_idx(find(img_name)).unsqueeze(1)  # uint8, as stored
+        if pixels == "f32":
+            x = x.float().div_(255.0)  # ToTensor()
+        elif pixels != "u8":
+            raise ValueError(f"pixels must be 'f32' or 'u8', got {pixels!r}")
         y = _read_idx(find(lbl_name)).long()
         n = int(len(x) * fraction) if fraction < 1 else len(x)
         self.n = n

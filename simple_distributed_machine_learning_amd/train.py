@@ -49,10 +49,12 @@ def make_datasets(args, spec, device):
         return tr, te
     use_mnist = args.data == "mnist" or (args.data == "auto" and IdxMNIST.available(args.data_dir))
     if use_mnist:
-        return (IdxMNIST(args.data_dir, True, device), IdxMNIST(args.data_dir, False, device))
+        px = getattr(args, "pixels", "f32")
+        return (IdxMNIST(args.data_dir, True, device, pixels=px), IdxMNIST(args.data_dir, False, device, pixels=px))
     mode = "random" if args.data == "random" else "learnable"
-    tr = SyntheticMNIST(args.train_size, seed=args.data_seed, device=device, mode=mode, offset=0)
-    te = SyntheticMNIST(args.test_size, seed=args.data_seed, device=device, mode=mode, offset=10_000_000)
+    px = getattr(args, "pixels", "f32")
+    tr = SyntheticMNIST(args.train_size, seed=args.data_seed, device=device, mode=mode, offset=0, pixels=px)
+    te = SyntheticMNIST(args.test_size, seed=args.data_seed, device=device, mode=mode, offset=10_000_000, pixels=px)
     return tr, te
 
 

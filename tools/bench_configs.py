@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay the step from a captured hipGraph")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel ranks per stage (gpt2)")
     ap.add_argument("--dtype", default=None, choices=[None, "fp32", "bf16"], help="resnet18: compute dtype")
+    ap.add_argument("--pixels", default="f32", choices=["f32", "u8"], help="image models: pixel storage")
     a = ap.parse_args()
     kind, M, B, S = DEFAULTS[a.config]
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
@@ -75,7 +76,7 @@ def main():
         unit = "tokens/s"
         per_sample = S
     else:
-        ds = SyntheticMNIST(B * eng.data_shards * nb, seed=5, device=dev)
+        ds = SyntheticMNIST(B * eng.data_shards * nb, seed=5, device=dev, pixels=a.pixels)
         unit = "samples/s"
         per_sample = 1
     GB = B * eng.data_shards
@@ -110,6 +111,7 @@ def main():
     if rank == 0:
         print(json.dumps({"config": a.config, "schedule": kind, "stages": stages, "ranks": world, "tp": a.tp,
                           "microbatches": M, "batch": GB, "seq_len": S, "dtype": str(spec.param_dtype), "graph": bool(a.graph), "tuned_gemms": tuned,
+                          "pixels": a.pixels,
                           "value": round(GB * per_sample * a.steps / el, 1), "unit": unit,
                           "ms_per_step": round(el / a.steps * 1e3, 3), "loss": round(l / max(1, n), 4),
                           "bubble_model": round(eng.schedule(M, False).bubble_fraction(), 3)}))

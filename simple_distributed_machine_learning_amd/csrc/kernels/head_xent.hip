@@ -17,6 +17,9 @@
 // row); dW/db are then done by the MFMA GEMM (gemm_f32 with fused row-sum).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace sdml {
@@ -545,7 +548,11 @@ int head_rows_per_chunk(int M) { return M <= SMALL_BATCH ? HTHR / 16 : HTHR / 4;
 int head_fused_blocks(int M, int* chunks_per_block) {
   const int rows = head_rows_per_chunk(M);
   const int chunks = (M + rows - 1) / rows;
-  int blocks = chunks < 512 ? chunks : 512;
+  static const int max_blocks = [] {  // A/B knob (SDML_HEAD_MAX_BLOCKS)
+    const char* e = getenv("SDML_HEAD_MAX_BLOCKS");
+    return e ? std::max(1, atoi(e)) : 512;
+  }();
+  int blocks = chunks < max_blocks ? chunks : max_blocks;
   int cpb = (chunks + blocks - 1) / blocks;
   blocks = (chunks + cpb - 1) / cpb;
   *chunks_per_block = cpb;

@@ -3,6 +3,7 @@
 // (a kernel must never see operands its grid does not assume) and launches on the current
 // PyTorch HIP stream, so the ops compose with torch streams, events and hipGraph capture.
 #include <ATen/hip/HIPContext.h>
+#include <cmath>
 #include <torch/extension.h>
 
 #include "kernels.h"
@@ -160,6 +161,13 @@ c10::optional<torch::Tensor> linear_bwd_f32(torch::Tensor x, c10::optional<torch
   return dx;
 }
 
+// uint8 pixels -> float32 the way ToTensor() does it (k / 255 for scale = 1/255, a true division)
+torch::Tensor pixels_f32(const torch::Tensor& x, double scale) {
+  const double d = 1.0 / scale, r = std::round(d);
+  auto xf = x.to(torch::kFloat32);
+  return std::abs(d - r) < 1e-9 * r ? xf.div_(r) : xf.mul_(scale);
+}
+
 // first layer fed by uint8 pixels (MNIST's native bytes): y = act(scale * x_u8 @ w.T + b), with
 // scale = 1/255 this is ToTensor() fused into the GEMM's operand load. Shapes the uint8 kernel
 // does not take (small batches, unaligned K) go through an fp32 copy of x * scale.
@@ -174,7 +182,7 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
   TORCH_CHECK(!relu || opt_ptr(b), "relu epilogue requires a bias");
   const bool direct = M >= 4096 && K % 16 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
                       M * K < (int64_t(1) << 31);
-  if (!direct) return linear_fwd_f32(x.to(torch::kFloat32).mul_(scale), w, b, relu);
+  if (!direct) return linear_fwd_f32(pixels_f32(x, scale), w, b, relu);
   auto y = torch::empty({M, N}, w.options());
   auto wsplit = torch::empty({3, N, K}, w.options().dtype(torch::kInt16));
   sdml::split3_planes(w.data_ptr<float>(), reinterpret_cast<unsigned short*>(wsplit.data_ptr<int16_t>()), N * K,
@@ -198,8 +206,8 @@ void linear_wgrad_u8(torch::Tensor x, torch::Tensor gz, torch::Tensor gw, c10::o
   const bool direct = M >= 4096 && K % 8 == 0 && N % 4 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 7) == 0 &&
                       M * K < (int64_t(1) << 31);
   if (!direct) {
-    auto xf = x.to(torch::kFloat32).mul_(scale);
-    linear_bwd_f32(xf, c10::nullopt, gz, gw, gw, gb, false, false, false);
+    // fp32 path: linear_bwd_f32 only reads w's shape when no input gradient is asked for
+    linear_bwd_f32(pixels_f32(x, scale), c10::nullopt, gz, /*w=*/gw, gw, gb, false, false, false);
     return;
   }
   sdml::gemm_u8x3_wgrad(gz.data_ptr<float>(), x.data_ptr<uint8_t>(), (int)M, (int)N, (int)K, (int)K,

@@ -188,6 +188,7 @@ def main():
                 "microbatches": M,
                 "batch_per_gpu": a.batch_per_gpu,
                 "optimizer": "SGD lr=0.1 momentum=0.5",
+                "pixels": a.pixels,
             },
             "baseline": BASELINE_NOTE,
             "final_loss": None if loss is None else round(loss, 5),

@@ -67,19 +67,33 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
   float loss_acc = 0.f, corr_acc = 0.f;
 
   const int row_in = t / TPR, q = t % TPR;  // TPR threads per row, HK / TPR k each
+  // x chunks are prefetched one ahead into registers: chunk ch+1's loads are in flight while
+  // chunk ch is computed (the loop is otherwise load -> barrier -> compute, memory idle meanwhile)
+  constexpr int NPRE = RWS * HK / 4 / HTHR;
+  f32x4 pre[NPRE];
+  auto gload = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < NPRE; ++i) {
+      const int idx = t + HTHR * i;
+      const int r = idx >> 5, k4 = idx & 31;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (r0 + r < M) v = *reinterpret_cast<const f32x4*>(x + (size_t)(r0 + r) * HK + 4 * k4);
+      pre[i] = v;
+    }
+  };
+  gload(blockIdx.x * chunks_per_block * RWS);
   for (int ch = 0; ch < chunks_per_block; ++ch) {
     const int r0 = (blockIdx.x * chunks_per_block + ch) * RWS;
     if (r0 >= M) break;
     __syncthreads();  // previous chunk fully consumed (and ws/bs visible on first pass)
     // stage x chunk
 #pragma unroll
-    for (int i = 0; i < RWS * HK / 4 / HTHR; ++i) {
-      int idx = t + HTHR * i;
-      int r = idx >> 5, k4 = idx & 31;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (r0 + r < M) v = *reinterpret_cast<const f32x4*>(x + (size_t)(r0 + r) * HK + 4 * k4);
-      *reinterpret_cast<f32x4*>(xs + r * XP + 4 * k4) = v;
+    for (int i = 0; i < NPRE; ++i) {
+      const int idx = t + HTHR * i;
+      const int r = idx >> 5, k4 = idx & 31;
+      *reinterpret_cast<f32x4*>(xs + r * XP + 4 * k4) = pre[i];
     }
+    if (ch + 1 < chunks_per_block) gload(r0 + RWS);
     __syncthreads();
     const int grow = r0 + row_in;
     const bool valid = grow < M;

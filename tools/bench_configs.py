@@ -40,7 +40,8 @@ def main():
     ap.add_argument("--graph", action="store_true", help="replay the step from a captured hipGraph")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel ranks per stage (gpt2)")
     ap.add_argument("--dtype", default=None, choices=[None, "fp32", "bf16"], help="resnet18: compute dtype")
-    ap.add_argument("--pixels", default="f32", choices=["f32", "u8"], help="image models: pixel storage")
+    ap.add_argument("--pixels", default="auto", choices=["auto", "f32", "u8"],
+                    help="image models: pixel storage (auto: uint8 for the MLPs at batches the uint8 kernels take)")
     a = ap.parse_args()
     kind, M, B, S = DEFAULTS[a.config]
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
@@ -51,6 +52,8 @@ def main():
         M = 1
     M = a.microbatches or M
     B = a.batch or B
+    if a.pixels == "auto":
+        a.pixels = "u8" if a.config in ("mlp", "mlp4x1024") and B >= 4096 else "f32"
     S = a.seq_len or S
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

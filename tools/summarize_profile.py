@@ -3,6 +3,7 @@ averages with derived utilisations).
 
     python tools/summarize_profile.py stats <kernel_stats.csv> <steps>
     python tools/summarize_profile.py pmc <counter_collection.csv> [more.csv ...]
+    python tools/summarize_profile.py trace <kernel_trace.csv> <steps>   (rocpd2csv output of a .db run)
 """
 import collections
 import csv
@@ -18,6 +19,21 @@ def stats(path, steps):
         t = float(r["TotalDurationNs"])
         print(f"{t / 1e6 / steps:8.3f} {int(r['Calls']) / steps:10.1f} {float(r['AverageNs']) / 1e3:9.1f} "
               f"{100 * t / tot:6.2f}  {r['Name'][:120]}")
+
+
+def trace(path, steps):
+    """Per-kernel stats from a kernel-trace CSV (rocprofv3's default .db output, exported with
+    rocpd2csv) in the same layout as `stats`."""
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        agg[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    tot = sum(sum(v) for v in agg.values())
+    print(f"kernel time per step: {tot / 1e6 / steps:.3f} ms over {steps} steps (incl. warm-up/setup kernels)")
+    print(f"{'ms/step':>8} {'calls/step':>10} {'avg us':>9} {'%':>6}  kernel")
+    for name, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:30]:
+        t = sum(v)
+        print(f"{t / 1e6 / steps:8.3f} {len(v) / steps:10.1f} {t / len(v) / 1e3:9.1f} "
+              f"{100 * t / tot:6.2f}  {name[:120]}")
 
 
 def pmc(paths):
@@ -48,5 +64,7 @@ def pmc(paths):
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], int(sys.argv[3]))
+    elif sys.argv[1] == "trace":
+        trace(sys.argv[2], int(sys.argv[3]))
     else:
         pmc(sys.argv[2:])

@@ -204,6 +204,16 @@ class PipelineEngine:
     def _boundary(self, producer_stage: int, mb: int):
         return self.spec.boundary_shape(producer_stage, mb), self.spec.boundary_dtype
 
+    def _loss_scale(self, dataset, batch_size: int, global_batch: Optional[int]) -> float:
+        """Per-sample (per-token for token models) loss weight: the summed gradients then equal
+        d(mean loss over the global batch)/dθ, as ``nll_loss(reduction='mean')`` on one
+        process (/root/reference/simple_distributed.py:111). Every schedule uses this."""
+        gb = global_batch if global_batch is not None else batch_size * self.data_shards
+        scale = 1.0 / float(gb)
+        if self.spec.input_kind == "tokens":
+            scale = scale / float(dataset.seq_len)
+        return scale
+
     def run(self, dataset, start: int, batch_size: int, train: bool, global_batch: Optional[int] = None,
             step_optimizer: bool = True) -> StepResult:
         """One pipeline step over samples [start, start+batch_size) of ``dataset``.
@@ -249,10 +259,7 @@ class PipelineEngine:
         M = len(sizes)
         sched = self.schedule(M, forward_only=not train)
         prog = sched.program(self.mesh.pp_rank)
-        gb = global_batch if global_batch is not None else batch_size * self.data_shards
-        scale = 1.0 / float(gb)
-        if self.spec.input_kind == "tokens":
-            scale = scale / float(dataset.seq_len)
+        scale = self._loss_scale(dataset, batch_size, global_batch)
 
         if train:
             self.flat.zero_grad()  # no-op when the previous optimizer step already cleared them
@@ -380,10 +387,11 @@ class PipelineEngine:
         """
         mesh, dev = self.mesh, self.device
         R, me = mesh.pp, mesh.pp_rank
-        W = max(1, self.M // R)
-        waves = split_sizes(batch_size, W)
-        gb = global_batch if global_batch is not None else batch_size * self.data_shards
-        scale = 1.0 / float(gb)
+        # every owner holds the same ``batch_size``, so every rank derives the same wave count
+        # (fewer waves than M/R when the batch is smaller) and issues the same collectives
+        waves = split_sizes(batch_size, max(1, self.M // R))
+        W = len(waves)
+        scale = self._loss_scale(dataset, batch_size, global_batch)
         s0, s1 = self.stages[0], self.stages[1]
         group = mesh.pipe_group
         stats = torch.zeros(2, device=dev, dtype=torch.float32)
@@ -395,7 +403,8 @@ class PipelineEngine:
         woff = [0]
         for w in waves[:-1]:
             woff.append(woff[-1] + w)
-        parts = [split_sizes(b, R) if b >= R else [b] + [0] * (R - 1) for b in waves]
+        # part k of a wave goes to rank k; a wave smaller than R leaves some parts empty
+        parts = [split_sizes(b, R) + [0] * (R - min(b, R)) for b in waves]
 
         def owner_part(o, w, k):  # (start, size) of part k of owner o's wave w
             pk = parts[w]
@@ -429,19 +438,22 @@ class PipelineEngine:
             tgt = tg[0] if R == 1 else torch.cat(tg)
             if tgt.device != dev:
                 tgt = tgt.to(dev, non_blocking=True)
-            if tgt.numel() == 0:
-                continue
-            c1 = {}
-            with tm.span("fwd", 1):
-                l, c, n = s1.head_fwd(recv[w], tgt, c1, train, scale, stats=stats)
-            if l is not None:
-                stats[0] += l.float()
-                stats[1] += c.float()
-            count += n
+            if tgt.numel() > 0:
+                c1 = {}
+                with tm.span("fwd", 1):
+                    l, c, n = s1.head_fwd(recv[w], tgt, c1, train, scale, stats=stats)
+                if l is not None:
+                    stats[0] += l.float()
+                    stats[1] += c.float()
+                count += n
+                if train:
+                    with tm.span("bwd", 1):
+                        g = s1.head_bwd(c1)
+            elif train:  # no rows for me in this wave: still join the backward exchange
+                shape, dt = self._boundary(0, 0)
+                g = torch.empty(shape, dtype=dt, device=dev)
             if not train:
                 continue
-            with tm.span("bwd", 1):
-                g = s1.head_bwd(c1)
             if R == 1:
                 back[w] = g
                 continue
@@ -456,9 +468,7 @@ class PipelineEngine:
                 if bwork[w] is not None:
                     with tm.span("recv_wait", 1):
                         bwork[w].wait()
-                if back[w] is None:  # this wave had no samples for me as stage 1... still owner grads
-                    continue
-                with tm.span("bwd", 0):
+                with tm.span("bwd", 0):  # every wave holds >= 1 owned row
                     s0.bwd(back[w], ctx0[w])
             self.grad_sync.stage_done(0)
             with tm.span("grad_sync"):

@@ -162,7 +162,10 @@ def run(args) -> dict:
             tot_loss += l
             tot_correct += c
             tot += n
-        n_ds = len(test_ds) if spec.input_kind != "tokens" else tot
+        # divide by what was evaluated: with several data shards a ragged last test batch can
+        # leave up to shards-1 samples out (the reference divides by len(test_ds) = the count
+        # it evaluated, /root/reference/simple_distributed.py:129-132)
+        n_ds = tot
         avg = tot_loss / max(1, n_ds)
         if master:
             print(test_line(avg, tot_correct, n_ds), flush=True)
@@ -176,6 +179,7 @@ def run(args) -> dict:
         acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if device.type == "cuda" else [])
         prof = profile(activities=acts)
         prof.__enter__()
+    finished = False
     try:
         for epoch in range(start_epoch, args.epochs + 1):
             last = train(epoch, start_batch if epoch == start_epoch else 0)
@@ -183,13 +187,14 @@ def run(args) -> dict:
                 test()
             if args.ckpt_dir and (args.save_every and epoch % args.save_every == 0 or epoch == args.epochs):
                 save_checkpoint(engine, args.ckpt_dir, epoch, last)
+        finished = True
     finally:
         if prof is not None:
             prof.__exit__(None, None, None)
             if master:
                 prof.export_chrome_trace(args.profile)
         if hb is not None:
-            hb.stop()
+            hb.stop(clean=finished)  # a rank that raised stays silent, so its peers abort
     history["engine"] = engine
     history["mesh"] = mesh
     return history

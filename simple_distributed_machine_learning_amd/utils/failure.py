@@ -18,6 +18,9 @@ from typing import Callable, Optional, Sequence
 import torch.distributed as dist
 
 
+DONE = "done"
+
+
 class Heartbeat:
     def __init__(self, rank: int, peers: Sequence[int], interval_s: float = 2.0, timeout_s: float = 60.0,
                  store=None, on_failure: Optional[Callable[[int, float], None]] = None):
@@ -54,7 +57,10 @@ class Heartbeat:
                                 self._fail(p, now - t_start)
                                 return
                             continue
-                        last = float(self.store.get(key).decode())
+                        val = self.store.get(key).decode()
+                        if val == DONE:  # the peer finished cleanly: never a failure
+                            continue
+                        last = float(val)
                     except Exception:  # noqa: BLE001  store gone: master died
                         self._fail(p, -1.0)
                         return
@@ -73,10 +79,17 @@ class Heartbeat:
         self.failed_peer = peer
         self.on_failure(peer, age)
 
-    def stop(self):
+    def stop(self, clean: bool = True):
+        """Stop beating. ``clean`` publishes ``hb/<rank> = done`` afterwards, so a slower peer
+        (e.g. one still writing its checkpoint) does not read this rank's silence as death."""
         self._stop.set()
         if self._thread is not None:
             self._thread.join(timeout=self.interval_s * 2)
+        if clean and self.store is not None:
+            try:
+                self.store.set(f"hb/{self.rank}", DONE)
+            except Exception:  # noqa: BLE001  store already torn down
+                pass
 
 
 def _default_store():

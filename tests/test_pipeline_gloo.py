@@ -151,3 +151,24 @@ def test_gpt2_tiny_tensor_parallel_matches_single_process(world, pp, M):
     for a, b in zip(res[0]["losses"], ref["losses"]):
         assert a == pytest.approx(b, rel=1e-5, abs=1e-6)
     assert res[0]["eval"][2] == ref["eval"][2]
+
+
+def test_gpt2_tiny_rotate_alltoall_matches_single_process():
+    """Token models under rotate: the all-to-all path must scale the loss per token, as the
+    generic path does (a missing 1/seq_len would make the gradients seq_len times too large
+    while the reported loss stays right)."""
+    B, steps = 2, 2
+    kw = {"stages": 2, "seq_len": 16}
+    res = run_ranks(train_worker, 2, "gpt2_tiny", "rotate", 2, 2, steps, B, 3, kw)
+    ref = _single("gpt2_tiny", 2, steps, 2 * B, "1f1b", kw)
+    _compare(res, ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("B,M", [(3, 4), (1, 4), (5, 8)])
+def test_mlp_rotate_alltoall_ragged_small_batches(B, M):
+    """Batches smaller than waves x ranks: fewer waves, empty all-to-all parts; every rank
+    must still join every collective and run its stage-0 backward."""
+    steps = 2
+    res = run_ranks(train_worker, 2, "mlp", "rotate", M, 2, steps, B)
+    ref = _single("mlp", 1, steps, 2 * B)
+    _compare(res, ref, rtol=1e-4, atol=1e-5)

@@ -4,6 +4,7 @@ averages with derived utilisations).
     python tools/summarize_profile.py stats <kernel_stats.csv> <steps>
     python tools/summarize_profile.py pmc <counter_collection.csv> [more.csv ...]
     python tools/summarize_profile.py trace <kernel_trace.csv> <steps>   (rocpd2csv output of a .db run)
+    python tools/summarize_profile.py db <run_results.db> <steps>        (rocprofv3's default rocpd output)
 """
 import collections
 import csv
@@ -27,6 +28,22 @@ def trace(path, steps):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         agg[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    tot = sum(sum(v) for v in agg.values())
+    print(f"kernel time per step: {tot / 1e6 / steps:.3f} ms over {steps} steps (incl. warm-up/setup kernels)")
+    print(f"{'ms/step':>8} {'calls/step':>10} {'avg us':>9} {'%':>6}  kernel")
+    for name, v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[:30]:
+        t = sum(v)
+        print(f"{t / 1e6 / steps:8.3f} {len(v) / steps:10.1f} {t / len(v) / 1e3:9.1f} "
+              f"{100 * t / tot:6.2f}  {name[:120]}")
+
+
+def db(path, steps):
+    """Per-kernel stats straight from a rocpd SQLite database (rocprofv3's default output)."""
+    import sqlite3
+
+    agg = collections.defaultdict(list)
+    for name, d in sqlite3.connect(path).execute("select name, duration from kernels"):
+        agg[name].append(int(d))
     tot = sum(sum(v) for v in agg.values())
     print(f"kernel time per step: {tot / 1e6 / steps:.3f} ms over {steps} steps (incl. warm-up/setup kernels)")
     print(f"{'ms/step':>8} {'calls/step':>10} {'avg us':>9} {'%':>6}  kernel")
@@ -64,6 +81,8 @@ def pmc(paths):
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], int(sys.argv[3]))
+    elif sys.argv[1] == "db":
+        db(sys.argv[2], int(sys.argv[3]))
     elif sys.argv[1] == "trace":
         trace(sys.argv[2], int(sys.argv[3]))
     else:

@@ -434,9 +434,9 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 // operand takes one LDS plane and each product 3 MFMAs; the epilogue scales by p.scale.
 // DEEP (EARLY only): two tiles in flight in registers instead of one (LEAD = 2 K-steps of load
 // latency cover instead of 1)
-template <bool A_KM, bool B_KM, bool AMASK, bool EARLY, bool BPRE = false, int U8 = U8_NONE, bool DEEP = false>
+template <bool A_KM, bool B_KM, bool AMASK, bool EARLY, bool BPRE = false, int U8 = U8_NONE, bool DEEP = false,
+          bool FRESH = true, bool NOEPI = false>
 __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
-  constexpr bool FRESH = true;
   constexpr int BM = A_KM ? 128 : 256;
   constexpr int WGM = BM / 64, WGN = 8 / WGM;  // wave grid
   constexpr int TN = BN / WGN / 32;             // 32-col MFMA tiles per wave (TM = 2)
@@ -614,6 +614,15 @@ __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
   }
 
   // ---- epilogue ----
+  if constexpr (NOEPI) {  // timing experiments only: keep the accumulators live, store nothing
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) z += acc[i][j][0] + acc[i][j][15];
+    if (z == 1234.5f) p.C[0] = z;
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -663,6 +672,16 @@ static bool x3_deep(bool dflt) {
     return e ? (e[0] == '0' ? 0 : 1) : -1;
   }();
   return force < 0 ? dflt : force == 1;
+}
+
+// experiment selector for the uint8 kernels (SDML_U8_VARIANT): 1 = no FRESH partials, 2 = no epilogue
+// (timing only), 3 = both
+static int u8_variant() {
+  static const int v = [] {
+    const char* e = getenv("SDML_U8_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 bool gemm_f32x3_eligible(const GemmArgs& g) {
@@ -780,12 +799,18 @@ void gemm_u8x3_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned
   p.kps = (K + BK - 1) / BK * BK;
   p.tiles_m = (M + 255) / 256;
   p.tiles_n = (N + BN - 1) / BN;
-  if (x3_deep(true))
-    hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A, true>), dim3(p.tiles_m * p.tiles_n, 1, 1),
-                       dim3(NT), 0, stream, p);
+  const dim3 grid(p.tiles_m * p.tiles_n, 1, 1);
+  const int v = u8_variant();
+  if (v == 1)
+    hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A, true, false>), grid, dim3(NT), 0, stream, p);
+  else if (v == 2)
+    hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A, true, true, true>), grid, dim3(NT), 0, stream, p);
+  else if (v == 3)
+    hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A, true, false, true>), grid, dim3(NT), 0, stream, p);
+  else if (x3_deep(true))
+    hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A, true>), grid, dim3(NT), 0, stream, p);
   else
-    hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A>), dim3(p.tiles_m * p.tiles_n, 1, 1),
-                       dim3(NT), 0, stream, p);
+    hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A>), grid, dim3(NT), 0, stream, p);
 }
 
 // gw[N,K] += scale * sum_m gz[m,n] X[m,k]; gb[n] += sum_m gz[m,n] (gb optional)
@@ -816,9 +841,16 @@ void gemm_u8x3_wgrad(const float* gz, const unsigned char* X, int M, int N, int 
   p.kps = kps;
   p.tiles_m = (N + 127) / 128;
   p.tiles_n = (K + BN - 1) / BN;
-  if (x3_deep(true))
-    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true>),
-                       dim3(p.tiles_m * p.tiles_n, splits, 1), dim3(NT), 0, stream, p);
+  const dim3 grid(p.tiles_m * p.tiles_n, splits, 1);
+  const int v = u8_variant();
+  if (v == 1)
+    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true, false>), grid, dim3(NT), 0, stream, p);
+  else if (v == 2)
+    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true, true, true>), grid, dim3(NT), 0, stream, p);
+  else if (v == 3)
+    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true, false, true>), grid, dim3(NT), 0, stream, p);
+  else if (x3_deep(true))
+    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true>), grid, dim3(NT), 0, stream, p);
   else
     hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B>), dim3(p.tiles_m * p.tiles_n, splits, 1),
                        dim3(NT), 0, stream, p);

@@ -79,6 +79,13 @@ void gemm_u8x3_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned
                    const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream);
 void gemm_u8x3_wgrad(const float* gz, const unsigned char* X, int M, int N, int K, int ldx, float* gw, float* gb,
                      float scale, hipStream_t stream);
+// mlp_u8.hip: LDS-DMA pipelined forward of the uint8-fed first layer (N % 128 == 0). W is given as
+// zero-padded bf16 planes [3][N][Kp], Kp = u8_fwd_kpad(K), written by split3_pad.
+int u8_fwd_kpad(int K);
+bool u8_fwd_supported(int M, int N, int K, int ldx, const void* X);
+void split3_pad(const float* w, unsigned short* out, int N, int K, int Kp, hipStream_t stream);
+void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
+            const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream);
 
 // ---- fused classifier head: z = x W^T + b; log_softmax; NLL; backward --------------------
 // x [M,K] fp32, W [C,K], b [C], target [M] int64. stats[0] += sum loss, stats[1] += #correct.

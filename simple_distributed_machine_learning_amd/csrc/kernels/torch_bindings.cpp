@@ -184,6 +184,19 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
                       M * K < (int64_t(1) << 31);
   if (!direct) return linear_fwd_f32(pixels_f32(x, scale), w, b, relu);
   auto y = torch::empty({M, N}, w.options());
+  static const bool legacy = [] {
+    const char* e = getenv("SDML_U8_FWD");
+    return e && std::string(e) == "x3";
+  }();
+  if (!legacy && sdml::u8_fwd_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr())) {
+    const int Kp = sdml::u8_fwd_kpad((int)K);
+    auto wp = torch::empty({3, N, Kp}, w.options().dtype(torch::kInt16));
+    auto* wpp = reinterpret_cast<unsigned short*>(wp.data_ptr<int16_t>());
+    sdml::split3_pad(w.data_ptr<float>(), wpp, (int)N, (int)K, Kp, cur_stream());
+    sdml::u8_fwd(x.data_ptr<uint8_t>(), (int)M, (int)K, (int)K, wpp, (int)N, Kp, opt_ptr(b), y.data_ptr<float>(),
+                 (int)N, relu, (float)scale, cur_stream());
+    return y;
+  }
   auto wsplit = torch::empty({3, N, K}, w.options().dtype(torch::kInt16));
   sdml::split3_planes(w.data_ptr<float>(), reinterpret_cast<unsigned short*>(wsplit.data_ptr<int16_t>()), N * K,
                       cur_stream());

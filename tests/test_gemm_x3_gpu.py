@@ -171,7 +171,8 @@ def pixels(M, Kd, seed):
     return torch.randint(0, 256, (M, Kd), generator=g, dtype=torch.uint8).to(DEV)
 
 
-@pytest.mark.parametrize("M,N,Kd", [(131072, 128, 784), (4096 + 77, 128, 784), (5000, 1024, 784), (8192, 36, 96)])
+@pytest.mark.parametrize("M,N,Kd", [(131072, 128, 784), (4096 + 77, 128, 784), (5000, 1024, 784), (8192, 36, 96),
+                                    (4096 + 77, 256, 816), (5000, 128, 96), (300, 128, 784)])
 def test_linear_fwd_u8_matches_fp32_reference(M, N, Kd):
     x8 = pixels(M, Kd, 3)
     w, b = rnd(N, Kd, seed=4, lo=-0.05, hi=0.05), rnd(N, seed=5)

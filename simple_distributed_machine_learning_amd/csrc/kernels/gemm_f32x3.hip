@@ -72,6 +72,8 @@ struct X3Params {
   int tiles_m, tiles_n;
   const unsigned char* X8;  // U8 kernels: the uint8 pixel operand (A for U8_A, B for U8_B)
   float scale;              // U8 kernels: C = scale * acc (+ bias); 1/255 = ToTensor's scaling
+  float* slab;              // split-K partials: split s writes slab + s * slab_stride ([M][ldc]) with
+  int64_t slab_stride;      // plain stores instead of atomics (reduced in fixed order afterwards)
 };
 
 // which operand (if any) is a uint8 pixel matrix: integers 0..255 have at most 8 significant
@@ -635,6 +637,10 @@ __global__ void __launch_bounds__(NT) gemm_x3_kernel(X3Params p) {
         const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (row >= p.M) continue;
         const float v = U8 != U8_NONE ? acc[i][j][r] * p.scale : acc[i][j][r];
+        if (p.slab) {
+          p.slab[split * p.slab_stride + (size_t)row * p.ldc + col] = v;
+          continue;
+        }
         float* dst = p.C + (size_t)row * p.ldc + col;
         switch (p.epi) {
           case EPI_STORE:
@@ -674,8 +680,8 @@ static bool x3_deep(bool dflt) {
   return force < 0 ? dflt : force == 1;
 }
 
-// experiment selector for the uint8 kernels (SDML_U8_VARIANT): 1 = no FRESH partials, 2 = no epilogue
-// (timing only), 3 = both
+// experiment selector for the uint8 kernels (SDML_U8_VARIANT). Forward (engine path, SDML_U8_FWD=x3):
+// 1 = no FRESH partials, 2 = no epilogue (timing only), 3 = both. Weight gradient: 1 = FRESH partials.
 static int u8_variant() {
   static const int v = [] {
     const char* e = getenv("SDML_U8_VARIANT");
@@ -702,7 +708,7 @@ int gemm_f32x3_pick_splits(int M, int N, int K, bool a_kmajor) {
 }
 
 void gemm_f32x3(const GemmArgs& g, hipStream_t stream) {
-  X3Params p;
+  X3Params p{};
   p.A = g.A;
   p.amask = g.amask;
   p.B = g.B;
@@ -813,9 +819,41 @@ void gemm_u8x3_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned
     hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A>), grid, dim3(NT), 0, stream, p);
 }
 
-// gw[N,K] += scale * sum_m gz[m,n] X[m,k]; gb[n] += sum_m gz[m,n] (gb optional)
+// deterministic split-K reduction: out[i] += sum_s slab[s][i], s in order (n % 4 == 0). 64-thread
+// blocks (n = 100K floats is only ~390 blocks of float4 lanes) with 4 independent partial sums per
+// lane, so ~8 loads per lane are in flight instead of one dependent chain; the partials are
+// combined in a fixed order.
+__global__ void __launch_bounds__(64) slab_reduce_kernel(const float* __restrict__ slab, int64_t stride, int splits,
+                                                         float* __restrict__ out, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * 64 + threadIdx.x) * 4;
+  if (i >= n) return;
+  f32x4 a[4] = {};
+  int s = 0;
+  for (; s + 8 <= splits; s += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u & 3] += *reinterpret_cast<const f32x4*>(slab + (s + u) * stride + i);
+  }
+  for (; s < splits; ++s) a[0] += *reinterpret_cast<const f32x4*>(slab + s * stride + i);
+  f32x4 acc = *reinterpret_cast<const f32x4*>(out + i);
+  acc += (a[0] + a[1]) + (a[2] + a[3]);
+  *reinterpret_cast<f32x4*>(out + i) = acc;
+}
+
+int u8x3_wgrad_splits(int M, int N, int K) {
+  int splits = gemm_f32x3_pick_splits(N, K, M, true);
+  int kps = (M + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  return (M + kps - 1) / kps;
+}
+
+// gw[N,K] += scale * sum_m gz[m,n] X[m,k]; gb[n] += sum_m gz[m,n] (gb optional).
+// Split-K partial tiles go to `slab` ([splits][N][K] fp32, u8x3_wgrad_splits(M, N, K) splits) with
+// plain stores and are summed in split order by slab_reduce_kernel: deterministic, and cheaper than
+// fp32 atomics (measured: the atomic epilogue cost ~14 us of 153 at the headline shape). With
+// slab == nullptr the partials are added atomically. Straight MFMA accumulation (no per-K-step
+// fp32 partials: tools/probes/mfma_acc_probe.hip) - measured 153 -> 142 us.
 void gemm_u8x3_wgrad(const float* gz, const unsigned char* X, int M, int N, int K, int ldx, float* gw, float* gb,
-                     float scale, hipStream_t stream) {
+                     float scale, float* slab, hipStream_t stream) {
   X3Params p{};
   p.A = gz;
   p.X8 = X;
@@ -829,31 +867,25 @@ void gemm_u8x3_wgrad(const float* gz, const unsigned char* X, int M, int N, int 
   p.ldc = K;
   p.epi = EPI_ATOMIC;
   p.scale = scale;
-  // workgroups per CU the split count aims at (the 1-deep kernel fits 2 per CU: 125 VGPRs, 64 KiB LDS)
-  static const int wg_per_cu = [] {
-    const char* e = getenv("SDML_U8_WGRAD_WG_PER_CU");
-    return e ? std::max(1, atoi(e)) : 1;
-  }();
-  int splits = gemm_f32x3_pick_splits(N, K, M, true) * wg_per_cu;
+  p.slab = slab;
+  p.slab_stride = (int64_t)N * K;
+  const int splits = u8x3_wgrad_splits(M, N, K);
   int kps = (M + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
-  splits = (M + kps - 1) / kps;
   p.kps = kps;
   p.tiles_m = (N + 127) / 128;
   p.tiles_n = (K + BN - 1) / BN;
-  const dim3 grid(p.tiles_m * p.tiles_n, splits, 1);
+  const dim3 grid(p.tiles_m * p.tiles_n, (M + kps - 1) / kps, 1);
   const int v = u8_variant();
-  if (v == 1)
-    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true, false>), grid, dim3(NT), 0, stream, p);
-  else if (v == 2)
-    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true, true, true>), grid, dim3(NT), 0, stream, p);
-  else if (v == 3)
-    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true, false, true>), grid, dim3(NT), 0, stream, p);
-  else if (x3_deep(true))
-    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true>), grid, dim3(NT), 0, stream, p);
+  if (v == 1)  // A/B: per-K-step fp32 partials (FRESH), as in round 1
+    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true, true>), grid, dim3(NT), 0, stream, p);
   else
-    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B>), dim3(p.tiles_m * p.tiles_n, splits, 1),
-                       dim3(NT), 0, stream, p);
+    hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true, false>), grid, dim3(NT), 0, stream, p);
+  if (slab) {
+    const int64_t n = (int64_t)N * K;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n / 4 + 63) / 64)), dim3(64), 0, stream, slab,
+                       p.slab_stride, (int)grid.y, gw, n);
+  }
 }
 
 }  // namespace sdml

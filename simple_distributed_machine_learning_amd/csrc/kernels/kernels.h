@@ -77,8 +77,11 @@ void gemm_f32x3_set_variant(int v);  // pipeline A/B: 0 = early split (default),
 //          K % 8 == 0, ldx % 8 == 0, X 8-B aligned, N % 4 == 0
 void gemm_u8x3_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_split, int N,
                    const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream);
+//          slab: optional [u8x3_wgrad_splits(M, N, K)][N][K] fp32 workspace -> deterministic
+//          split-K reduction (nullptr: fp32 atomics); needs (N * K) % 4 == 0 and 16-B aligned gw
+int u8x3_wgrad_splits(int M, int N, int K);
 void gemm_u8x3_wgrad(const float* gz, const unsigned char* X, int M, int N, int K, int ldx, float* gw, float* gb,
-                     float scale, hipStream_t stream);
+                     float scale, float* slab, hipStream_t stream);
 // mlp_u8.hip: LDS-DMA pipelined forward of the uint8-fed first layer (N % 128 == 0). W is given as
 // zero-padded bf16 planes [3][N][Kp], Kp = u8_fwd_kpad(K), written by split3_pad.
 int u8_fwd_kpad(int K);

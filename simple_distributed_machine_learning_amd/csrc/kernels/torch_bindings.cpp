@@ -223,8 +223,14 @@ void linear_wgrad_u8(torch::Tensor x, torch::Tensor gz, torch::Tensor gw, c10::o
     linear_bwd_f32(pixels_f32(x, scale), c10::nullopt, gz, /*w=*/gw, gw, gb, false, false, false);
     return;
   }
+  float* slab = nullptr;
+  torch::Tensor ws;
+  if ((N * K) % 4 == 0 && (reinterpret_cast<uintptr_t>(gw.data_ptr()) & 15) == 0 && gw.is_contiguous()) {
+    ws = torch::empty({(int64_t)sdml::u8x3_wgrad_splits((int)M, (int)N, (int)K), N, K}, gw.options());
+    slab = ws.data_ptr<float>();
+  }
   sdml::gemm_u8x3_wgrad(gz.data_ptr<float>(), x.data_ptr<uint8_t>(), (int)M, (int)N, (int)K, (int)K,
-                        gw.data_ptr<float>(), opt_ptr(gb), (float)scale, cur_stream());
+                        gw.data_ptr<float>(), opt_ptr(gb), (float)scale, slab, cur_stream());
 }
 
 

@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
                                                           const float* __restrict__ bias,
                                                           const int64_t* __restrict__ target, int M, float scale,
                                                           float* __restrict__ part, float* __restrict__ dx,
-                                                          int chunks_per_block, int mask_dx) {
+                                                          int chunks_per_block, int mask_dx, float* __restrict__ dl) {
   constexpr int RWS = HTHR / TPR;  // rows per chunk
   // x chunk; reused at the end for the dW partial reduction ([4 waves][C * HK])
   constexpr int XS = RWS * XP > (HTHR / 64) * C * HK ? RWS * XP : (HTHR / 64) * C * HK;
@@ -50,7 +50,9 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
   __shared__ __attribute__((aligned(16))) float dzs[RWS * DZP];
   __shared__ float red[2 * HTHR / 64];
   const int t = threadIdx.x;
-  const bool train = dx != nullptr;
+  // dl: the row's scaled dlogits dz [M][C] instead of (or besides) dx = dz @ W, the factor form of
+  // the boundary gradient (head_dx_from_dl rebuilds dx from it bit for bit)
+  const bool train = dx != nullptr || dl != nullptr;
   for (int i = t; i < C * HK / 4; i += HTHR)
     reinterpret_cast<f32x4*>(ws)[i] = reinterpret_cast<const f32x4*>(W)[i];
   if (t < C) bs[t] = bias[t];
@@ -147,8 +149,12 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
       if (q == 0) {
 #pragma unroll
         for (int c = 0; c < C; ++c) dzs[row_in * DZP + c] = dz[c];
+        if (dl && valid) {
+#pragma unroll
+          for (int c = 0; c < C; ++c) dl[(size_t)grow * C + c] = dz[c];
+        }
       }
-      if (valid) {
+      if (valid && dx) {
 #pragma unroll
         for (int j = 0; j < HK / (4 * TPR); ++j) {
           const int k = 4 * (q + TPR * j);
@@ -580,15 +586,63 @@ size_t head_workspace_floats(int M, int K, int C) {
   return (size_t)head_fused_blocks(M, &cpb) * (C * K + C + 2);
 }
 
+// dx[m][k] = (sum_c dl[m][c] W[c][k]) * (mask ? x[m][k] > 0 : 1): the fused head's dx, rebuilt from its
+// factor with the SAME operations in the same order (f32x4 accumulation over c from zero), so the
+// result is bit-identical to the dx the head would have written. K == HK (128).
+template <int C>
+__global__ void __launch_bounds__(256) head_dx_from_dl_kernel(const float* __restrict__ dl, const float* __restrict__ W,
+                                                              const float* __restrict__ x, float* __restrict__ dx,
+                                                              int M, int mask) {
+  __shared__ __attribute__((aligned(16))) float ws[C * HK];
+  for (int i = threadIdx.x; i < C * HK / 4; i += 256)
+    reinterpret_cast<f32x4*>(ws)[i] = reinterpret_cast<const f32x4*>(W)[i];
+  __syncthreads();
+  const int q = threadIdx.x & 31;  // float4 column of the row
+  for (int row = blockIdx.x * 8 + (threadIdx.x >> 5); row < M; row += gridDim.x * 8) {
+    float dz[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) dz[c] = dl[(size_t)row * C + c];
+    const int k = 4 * q;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      f32x4 wv = *reinterpret_cast<const f32x4*>(ws + c * HK + k);
+      o += dz[c] * wv;
+    }
+    if (mask) {
+      f32x4 xv = *reinterpret_cast<const f32x4*>(x + (size_t)row * HK + k);
+      o[0] = xv[0] > 0.f ? o[0] : 0.f;
+      o[1] = xv[1] > 0.f ? o[1] : 0.f;
+      o[2] = xv[2] > 0.f ? o[2] : 0.f;
+      o[3] = xv[3] > 0.f ? o[3] : 0.f;
+    }
+    *reinterpret_cast<f32x4*>(dx + (size_t)row * HK + k) = o;
+  }
+}
+
+void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx, int M, int K, int C, bool mask,
+                     hipStream_t stream) {
+  if (M <= 0) return;
+  if (K != HK) abort();  // host contract (checked by the binding)
+  int blocks = (M + 7) / 8;
+  if (blocks > 2048) blocks = 2048;
+  switch (C) {
+    case 10: hipLaunchKernelGGL(head_dx_from_dl_kernel<10>, dim3(blocks), dim3(256), 0, stream, dl, W, x, dx, M, mask ? 1 : 0); break;
+    case 2: hipLaunchKernelGGL(head_dx_from_dl_kernel<2>, dim3(blocks), dim3(256), 0, stream, dl, W, x, dx, M, mask ? 1 : 0); break;
+    case 16: hipLaunchKernelGGL(head_dx_from_dl_kernel<16>, dim3(blocks), dim3(256), 0, stream, dl, W, x, dx, M, mask ? 1 : 0); break;
+    default: abort();  // host contract: C in {2, 10, 16} (head_fused_supported)
+  }
+}
+
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K, int C,
                          float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
-                         float* workspace, bool mask_dx, hipStream_t stream) {
+                         float* workspace, bool mask_dx, hipStream_t stream, float* dl) {
   if (M <= 0) return;
   if (head_fused_supported(K, C) && dz_out == nullptr && workspace != nullptr) {
     int cpb = 0, blocks = head_fused_blocks(M, &cpb);
 #define HEAD_LAUNCH(CC, TT)                                                                             \
   hipLaunchKernelGGL((head_fused_kernel<CC, TT>), dim3(blocks), dim3(HTHR), 0, stream, x, W, b, target, M, scale, \
-                     workspace, dx, cpb, mask_dx ? 1 : 0)
+                     workspace, dx, cpb, mask_dx ? 1 : 0, dl)
     const bool small = M <= SMALL_BATCH;
     switch (C) {
       case 10:
@@ -604,9 +658,10 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
 #undef HEAD_LAUNCH
     const int width = C * K + C + 2;
     hipLaunchKernelGGL(head_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, stream, workspace, blocks, C * K,
-                       C, gW, gb, stats, dx != nullptr ? 1 : 0);
+                       C, gW, gb, stats, (dx != nullptr || dl != nullptr) ? 1 : 0);
     return;
   }
+  if (dl) abort();  // host contract: the dlogits output exists on the fused path only (head_fused_supported)
   if (head_lds_supported(M, K, C)) {
     const int lblocks = head_lds_blocks(M);
     const size_t lds = (size_t)C * K * sizeof(float);

@@ -102,9 +102,15 @@ bool head_fused_supported(int K, int C);
 bool head_lds_supported(int M, int K, int C);
 size_t head_workspace_floats(int M, int K, int C);
 // mask_dx: dx *= (x > 0) — the producing stage's ReLU backward, fused (x is its output)
+// dl (fused path only, may be null): also/instead write the scaled dlogits dz [M][C] — the rank-C
+// factor of dx = dz @ W (with dx == nullptr the dx pass is skipped; gW/gb/stats as usual)
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K,
                          int C, float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
-                         float* workspace, bool mask_dx, hipStream_t stream);
+                         float* workspace, bool mask_dx, hipStream_t stream, float* dl = nullptr);
+// dx = (dl @ W) * (x > 0 if mask): the fused head's dx rebuilt bit-identically from its factor dl
+// (K == 128, C in {2, 10, 16}: head_fused_supported)
+void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx, int M, int K, int C, bool mask,
+                     hipStream_t stream);
 
 // ---- SGD with momentum over a flat buffer ------------------------------------------------
 // zero_grad: also writes g = 0 after reading it (fuses the next step's zero_grad)

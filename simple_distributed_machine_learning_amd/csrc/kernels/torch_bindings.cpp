@@ -617,6 +617,49 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
   return {stats, dx};
 }
 
+// training head that returns its boundary gradient as the factor dl = scale * (softmax - onehot) [M, C]
+// (dx = dl @ w, rebuilt by head_dx_from_dl wherever w is held); gw/gb accumulated, loss and correct
+// count accumulated into stats_acc [2]
+torch::Tensor head_logsoftmax_nll_dl_f32(torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor target,
+                                         torch::Tensor gw, torch::Tensor gb, double scale, torch::Tensor stats_acc) {
+  check_f32_cuda(x, "x");
+  check_f32_cuda(w, "w");
+  check_f32_cuda(b, "b");
+  check_f32_cuda(gw, "gw");
+  check_f32_cuda(gb, "gb");
+  check_f32_cuda(stats_acc, "stats_acc");
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == torch::kInt64 && target.is_contiguous(),
+              "target must be a contiguous int64 device tensor");
+  const int64_t M = x.size(0), K = x.size(1), C = w.size(0);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && w.size(1) == K && b.numel() == C && target.numel() == M &&
+                  gw.numel() == C * K && gb.numel() == C && stats_acc.numel() == 2,
+              "head_dl: shape mismatch");
+  TORCH_CHECK(sdml::head_fused_supported((int)K, (int)C), "head_dl: needs the fused head (K == 128, C in {2, 10, 16})");
+  auto dl = torch::empty({M, C}, x.options());
+  if (M == 0) return dl;
+  auto ws = torch::empty({(int64_t)sdml::head_workspace_floats(M, K, C)}, x.options());
+  sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), target.data_ptr<int64_t>(),
+                            M, K, C, (float)scale, stats_acc.data_ptr<float>(), nullptr, gw.data_ptr<float>(),
+                            gb.data_ptr<float>(), nullptr, ws.data_ptr<float>(), false, cur_stream(),
+                            dl.data_ptr<float>());
+  return dl;
+}
+
+// dx = (dl @ w) * (x > 0 if mask): the fused head's boundary gradient rebuilt from its factor
+torch::Tensor head_dx_from_dl(torch::Tensor dl, torch::Tensor w, torch::Tensor x, bool mask) {
+  check_f32_cuda(dl, "dl");
+  check_f32_cuda(w, "w");
+  check_f32_cuda(x, "x");
+  const int64_t M = dl.size(0), C = dl.size(1), K = w.size(1);
+  TORCH_CHECK(dl.dim() == 2 && w.dim() == 2 && w.size(0) == C && x.dim() == 2 && x.size(0) == M && x.size(1) == K,
+              "head_dx_from_dl: shape mismatch");
+  TORCH_CHECK(sdml::head_fused_supported((int)K, (int)C), "head_dx_from_dl: K == 128, C in {2, 10, 16}");
+  auto dx = torch::empty({M, K}, x.options());
+  sdml::head_dx_from_dl(dl.data_ptr<float>(), w.data_ptr<float>(), x.data_ptr<float>(), dx.data_ptr<float>(), (int)M,
+                        (int)K, (int)C, mask, cur_stream());
+  return dx;
+}
+
 void sgd_momentum_(torch::Tensor p, torch::Tensor g, torch::Tensor buf, double lr, double momentum, double dampening,
                    double wd, bool nesterov, bool first, bool zero_grad) {
   check_f32_cuda(p, "p");
@@ -961,6 +1004,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("head_logsoftmax_nll_f32", &head_logsoftmax_nll_f32, "fused fc + log_softmax + NLL (+ backward)",
         py::arg("x"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
         py::arg("need_dx"), py::arg("stats_acc") = py::none(), py::arg("mask_dx") = false);
+  m.def("head_logsoftmax_nll_dl_f32", &head_logsoftmax_nll_dl_f32,
+        "fused head returning the boundary gradient as its factor dl = scale * (softmax - onehot)", py::arg("x"),
+        py::arg("w"), py::arg("b"), py::arg("target"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
+        py::arg("stats_acc"));
+  m.def("head_dx_from_dl", &head_dx_from_dl, "dx = (dl @ w) * (x > 0): boundary gradient from its factor",
+        py::arg("dl"), py::arg("w"), py::arg("x"), py::arg("mask"));
   m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer", py::arg("p"), py::arg("g"),
         py::arg("buf"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"),
         py::arg("first"), py::arg("zero_grad") = false);

@@ -140,6 +140,31 @@ class MLPStage(PipelineStage):
             ctx["dx"] = dx
         return loss, correct, target.numel()
 
+    # Factored boundary gradient (rotate placement): the gradient this single-Linear head sends back,
+    # (dl @ W) * (x > 0), has rank <= C per sample; the head returns the factor dl [M, C] and the
+    # rank that owns the boundary activation x rebuilds the gradient with ITS replica of W
+    # (boundary_grad_from_factor). 40 bytes per sample cross the boundary instead of 512 for
+    # 784-128-10, with a bit-identical result (ops.head_dx_from_dlogits).
+    @property
+    def supports_factored_grad(self) -> bool:
+        return self.is_last and not self.is_first and len(self.layer_ids) == 1
+
+    def head_fwd_factored(self, x, target, loss_scale, stats):
+        """Training head_fwd + head_bwd in one call: returns (dl, count); loss/correct go to stats."""
+        head = self.layers()[-1]
+        x = x.reshape(x.shape[0], -1)
+        if x.dtype != torch.float32 or not x.is_contiguous():
+            x = x.float().contiguous()
+        dl = ops.linear_logsoftmax_nll_dl(x, head.weight, head.bias, target, head.weight.grad, head.bias.grad,
+                                          loss_scale, stats)
+        return dl, target.numel()
+
+    def boundary_grad_from_factor(self, dl, x):
+        """d(loss)/d(pre-activation of the producing stage) from the head's factor ``dl`` and the
+        boundary activation ``x`` (the producer's ReLU output)."""
+        head = self.layers()[-1]
+        return ops.head_dx_from_dlogits(dl, head.weight.detach(), x.reshape(x.shape[0], -1), mask=True)
+
     def head_bwd(self, ctx):
         if "dx" not in ctx:
             return super().head_bwd(ctx)

@@ -92,6 +92,30 @@ def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool, 
     return loss, correct, dx
 
 
+def linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale: float, stats):
+    """Training head (fc -> log_softmax -> NLL, backward) whose boundary gradient is returned as its
+    rank-C factor ``dl = scale * (softmax - onehot)`` [M, C] instead of ``dx = dl @ w`` [M, K]
+    (:func:`head_dx_from_dlogits` rebuilds dx bit-identically wherever ``w`` is held). gw/gb are
+    accumulated; loss sum and correct count are accumulated into ``stats`` [2]."""
+    if x.is_cuda:
+        return _k().head_logsoftmax_nll_dl_f32(x, w, b, target, gw, gb, float(scale), stats)
+    with torch.no_grad():
+        loss, correct, dl = ref.linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale)
+    stats[0] += loss
+    stats[1] += correct
+    return dl
+
+
+def head_dx_from_dlogits(dl, w, x, mask: bool = True):
+    """Boundary gradient from its factor: ``(dl @ w) * (x > 0)`` (the ReLU backward of the stage
+    that produced ``x``, fused), with the fused head's exact arithmetic on ROCm."""
+    if dl.is_cuda:
+        return _k().head_dx_from_dl(dl, w, x, bool(mask))
+    with torch.no_grad():
+        dx = dl @ w
+    return dx * (x > 0).to(dx.dtype) if mask else dx
+
+
 def sgd_momentum_(p, g, buf, lr: float, momentum: float, dampening: float = 0.0, weight_decay: float = 0.0,
                   nesterov: bool = False, first: bool = False, zero_grad: bool = False):
     """In-place SGD step; with ``zero_grad`` the kernel also clears ``g`` after reading it."""

@@ -47,6 +47,21 @@ def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool):
     return loss, correct, dx
 
 
+def linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale: float):
+    """Training head whose boundary gradient is returned as its factor dl = scale * (softmax - onehot)
+    (dx = dl @ w); gw/gb accumulated. Returns (loss_sum, correct, dl)."""
+    z = x @ w.t() + b
+    lp = F.log_softmax(z, dim=1)
+    loss = -lp.gather(1, target.view(-1, 1)).sum()
+    correct = (lp.argmax(1) == target).sum()
+    dl = lp.exp()
+    dl[torch.arange(z.shape[0]), target] -= 1.0
+    dl *= scale
+    gw += dl.t() @ x
+    gb += dl.sum(0)
+    return loss, correct, dl
+
+
 def sgd_momentum_(p, g, buf, lr: float, momentum: float, dampening: float = 0.0, weight_decay: float = 0.0,
                   nesterov: bool = False, first: bool = False):
     """torch.optim.SGD semantics (first step: buf = g, no dampening)."""

@@ -158,6 +158,9 @@ class PipelineEngine:
         # rotate, 2 stages: run each wave's stage boundary as ONE all-to-all collective
         # (RCCL drives all xGMI links at once; far fewer launches than per-peer p2p)
         self.use_alltoall = os.environ.get("SDML_ROTATE_P2P") != "1"
+        # rotate all-to-all, 2-stage models with a single-Linear head: send the boundary gradient
+        # as its rank-C factor (see _run_rotate_alltoall); SDML_ROTATE_FACTORED=0 sends it whole
+        self.factored_boundary_grad = os.environ.get("SDML_ROTATE_FACTORED", "1") != "0"
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
 
@@ -384,15 +387,26 @@ class PipelineEngine:
         input-grads exchanged back -> stage-0 backward. Waves are issued so that wave w's
         exchange overlaps the compute of its neighbours; the collectives run on the RCCL
         stream and only the consumer kernels wait for them.
+
+        Factored boundary gradient (stage 1 a single Linear + log_softmax, e.g. 784-128-10): the
+        gradient stage 1 returns, (dl @ W) * (h > 0), has rank <= C per sample. Every rank holds
+        W (stage weights are replicated here), so the head returns dl [n, C] and the OWNER
+        rebuilds the gradient from its own copy of h -- bit-identical to the head's own dx
+        (tests/test_kernels_gpu.py), and 40 instead of 512 bytes per sample on the return
+        all-to-all. Stage 1's forward, loss, dW/db and optimizer step stay where they were.
         """
         mesh, dev = self.mesh, self.device
         R, me = mesh.pp, mesh.pp_rank
+        s0, s1 = self.stages[0], self.stages[1]
+        # factored boundary gradient: every rank holds stage 1's weights (they are replicated in
+        # this placement), so the head sends back only its rank-C factor dl [n, C] and the owner
+        # rebuilds d(loss)/dz0 = (dl @ W1) * (h > 0) from its own boundary activation h
+        factored = (train and R > 1 and self.factored_boundary_grad and getattr(s1, "supports_factored_grad", False))
         # every owner holds the same ``batch_size``, so every rank derives the same wave count
         # (fewer waves than M/R when the batch is smaller) and issues the same collectives
         waves = split_sizes(batch_size, max(1, self.M // R))
         W = len(waves)
         scale = self._loss_scale(dataset, batch_size, global_batch)
-        s0, s1 = self.stages[0], self.stages[1]
         group = mesh.pipe_group
         stats = torch.zeros(2, device=dev, dtype=torch.float32)
         count = 0
@@ -412,6 +426,7 @@ class PipelineEngine:
 
         tm = PhaseTimer(dev, self.timing)
         ctx0 = [dict() for _ in waves]
+        hkeep = [None] * W  # factored: the owner's boundary activation per wave (ReLU mask source)
         recv, fwork = [None] * W, [None] * W
         for w, bw in enumerate(waves):  # stage 0 forward + scatter of the boundary activation
             x = dataset.inputs(start + me * batch_size + woff[w], bw)
@@ -421,6 +436,8 @@ class PipelineEngine:
                 x = pixels_to_float(x)
             with tm.span("fwd", 0):
                 h = s0.fwd(x, ctx0[w], train)
+            if factored:
+                hkeep[w] = h
             if R == 1:
                 recv[w] = h
                 continue
@@ -438,7 +455,11 @@ class PipelineEngine:
             tgt = tg[0] if R == 1 else torch.cat(tg)
             if tgt.device != dev:
                 tgt = tgt.to(dev, non_blocking=True)
-            if tgt.numel() > 0:
+            if tgt.numel() > 0 and factored:
+                with tm.span("fwd", 1):
+                    g, n = s1.head_fwd_factored(recv[w], tgt, scale, stats)
+                count += n
+            elif tgt.numel() > 0:
                 c1 = {}
                 with tm.span("fwd", 1):
                     l, c, n = s1.head_fwd(recv[w], tgt, c1, train, scale, stats=stats)
@@ -450,8 +471,11 @@ class PipelineEngine:
                     with tm.span("bwd", 1):
                         g = s1.head_bwd(c1)
             elif train:  # no rows for me in this wave: still join the backward exchange
-                shape, dt = self._boundary(0, 0)
-                g = torch.empty(shape, dtype=dt, device=dev)
+                if factored:
+                    g = torch.empty((0, s1.layers()[-1].out_features), dtype=torch.float32, device=dev)
+                else:
+                    shape, dt = self._boundary(0, 0)
+                    g = torch.empty(shape, dtype=dt, device=dev)
             if not train:
                 continue
             if R == 1:
@@ -468,8 +492,13 @@ class PipelineEngine:
                 if bwork[w] is not None:
                     with tm.span("recv_wait", 1):
                         bwork[w].wait()
+                gz = back[w]
+                if factored:
+                    with tm.span("bwd", 1):
+                        gz = s1.boundary_grad_from_factor(gz, hkeep[w])
+                        hkeep[w] = None
                 with tm.span("bwd", 0):  # every wave holds >= 1 owned row
-                    s0.bwd(back[w], ctx0[w])
+                    s0.bwd(gz, ctx0[w])
             self.grad_sync.stage_done(0)
             with tm.span("grad_sync"):
                 self.grad_sync.finish()

@@ -116,6 +116,28 @@ def test_head_logsoftmax_nll(M, Kd, C):
     close(loss_e, loss_r, rtol=2e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("M", [60, 3000, 131072])
+@pytest.mark.parametrize("C", [10, 2])
+def test_head_factored_boundary_grad_bit_identical(M, C):
+    """The factored head (dlogits out) + head_dx_from_dl rebuild the masked boundary gradient bit for
+    bit, with the same loss/correct/dW/db as the fused head that writes dx itself."""
+    Kd = 128
+    x, w, b = rnd(M, Kd, seed=41).relu(), rnd(C, Kd, seed=42) * 0.1, rnd(C, seed=43)
+    t = torch.randint(0, C, (M,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+    scale = 1.0 / M
+    gw, gb, st = torch.zeros(C, Kd, device=DEV), torch.zeros(C, device=DEV), torch.zeros(2, device=DEV)
+    gw2, gb2, st2 = gw.clone(), gb.clone(), st.clone()
+    _, _, dx = ops.linear_logsoftmax_nll(x, w, b, t, gw, gb, scale, True, stats=st, mask_dx=True)
+    dl = ops.linear_logsoftmax_nll_dl(x, w, b, t, gw2, gb2, scale, st2)
+    assert dl.shape == (M, C)
+    dx2 = ops.head_dx_from_dlogits(dl, w, x, mask=True)
+    assert torch.equal(dx, dx2)
+    assert torch.equal(gw, gw2) and torch.equal(gb, gb2) and torch.equal(st, st2)
+    # and the factor is the reference dlogits
+    _, _, dl_r = ref.linear_logsoftmax_nll_dl(x, w, b, t, torch.zeros_like(gw), torch.zeros_like(gb), scale)
+    close(dl, dl_r, atol=1e-7, rtol=1e-4)
+
+
 @pytest.mark.parametrize("first", [True, False])
 @pytest.mark.parametrize("wd,damp,nest", [(0.0, 0.0, False), (1e-4, 0.1, False), (0.0, 0.0, True)])
 def test_sgd_momentum(first, wd, damp, nest):

@@ -95,12 +95,17 @@ def test_gpt2_tiny_two_ranks():
     _compare(res, ref, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("a2a", [True, False])
+@pytest.mark.parametrize("a2a", [True, False, "whole_grad"])
 @pytest.mark.parametrize("world,M", [(2, 2), (2, 4), (4, 16), (4, 8)])
 def test_mlp_rotate_matches_single_process(world, M, a2a, monkeypatch):
+    """a2a=True: all-to-all boundary with the factored gradient (the head's dlogits cross, the owner
+    rebuilds the boundary gradient); "whole_grad": all-to-all sending the full boundary gradient;
+    False: per-peer p2p transfers."""
     B, steps = 24, 2
     if not a2a:
         monkeypatch.setenv("SDML_ROTATE_P2P", "1")
+    if a2a == "whole_grad":
+        monkeypatch.setenv("SDML_ROTATE_FACTORED", "0")
     res = run_ranks(train_worker, world, "mlp", "rotate", M, world, steps, B)
     ref = _single("mlp", M, steps, world * B)
     _compare(res, ref, rtol=1e-4, atol=1e-5)

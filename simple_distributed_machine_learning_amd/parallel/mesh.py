@@ -49,6 +49,9 @@ class Mesh:
     tp: int = 1  # tensor-parallel ranks per stage
     tp_rank: int = 0
     tp_group: Optional[object] = None
+    # rotate: a second communicator over the pipeline ranks for the backward boundary exchange, so
+    # it does not queue behind the next wave's forward exchange on one RCCL stream
+    pipe_group_bwd: Optional[object] = None
 
     @property
     def distributed(self) -> bool:
@@ -183,8 +186,10 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
         for t in range(tp):
             ranks = [(d * pp + r) * tp + t for r in range(pp)]
             g = new_group(ranks) if pp > 1 else None
+            gb = new_group(ranks) if pp > 1 and schedule_kind == "rotate" else None
             if d == mesh.dp_rank and t == mesh.tp_rank:
                 mesh.pipe_group = g
+                mesh.pipe_group_bwd = gb
     # rotate talks to every peer of the pipeline group; the others only to neighbours
     pairs = [(r, q) for r in range(pp) for q in range(r + 1, pp)] if schedule_kind == "rotate" else \
         [(r, r + 1) for r in range(pp - 1)]

@@ -447,6 +447,25 @@ class PipelineEngine:
             fwork[w] = dist.all_to_all_single(buf, h.contiguous(), out_splits, in_splits, group=group, async_op=True)
             recv[w] = buf
         back, bwork = [None] * W, [None] * W
+        bgroup = mesh.pipe_group_bwd or group
+
+        def stage0_bwd(w):
+            if bwork[w] is not None:
+                with tm.span("recv_wait", 1):
+                    bwork[w].wait()
+            gz = back[w]
+            if factored:
+                with tm.span("bwd", 1):
+                    gz = s1.boundary_grad_from_factor(gz, hkeep[w])
+                    hkeep[w] = None
+            with tm.span("bwd", 0):  # every wave holds >= 1 owned row
+                s0.bwd(gz, ctx0[w])
+            back[w] = None
+
+        # R > 1: wave w's stage-0 backward is issued right after its head, ahead of wave w+1's head:
+        # the compute stream then has work while wave w+1's activations are still on the links
+        # (the backward exchange runs on its own communicator and, factored, is small)
+        interleave = train and R > 1
         for w in range(W):  # stage 1 (+ loss + its backward) on the received parts
             if fwork[w] is not None:
                 with tm.span("recv_wait", 0):
@@ -484,21 +503,16 @@ class PipelineEngine:
             out_splits = parts[w]
             in_splits = [parts[w][me] for _ in range(R)]
             buf = torch.empty((sum(out_splits),) + tuple(g.shape[1:]), dtype=g.dtype, device=dev)
-            bwork[w] = dist.all_to_all_single(buf, g.contiguous(), out_splits, in_splits, group=group, async_op=True)
+            bwork[w] = dist.all_to_all_single(buf, g.contiguous(), out_splits, in_splits, group=bgroup,
+                                              async_op=True)
             back[w] = buf
+            if interleave:
+                stage0_bwd(w)
         if train:
             self.grad_sync.stage_done(1)
-            for w in range(W):  # stage 0 backward
-                if bwork[w] is not None:
-                    with tm.span("recv_wait", 1):
-                        bwork[w].wait()
-                gz = back[w]
-                if factored:
-                    with tm.span("bwd", 1):
-                        gz = s1.boundary_grad_from_factor(gz, hkeep[w])
-                        hkeep[w] = None
-                with tm.span("bwd", 0):  # every wave holds >= 1 owned row
-                    s0.bwd(gz, ctx0[w])
+            if not interleave:
+                for w in range(W):
+                    stage0_bwd(w)
             self.grad_sync.stage_done(0)
             with tm.span("grad_sync"):
                 self.grad_sync.finish()

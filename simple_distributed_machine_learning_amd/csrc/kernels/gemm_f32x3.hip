@@ -839,6 +839,12 @@ __global__ void __launch_bounds__(64) slab_reduce_kernel(const float* __restrict
   *reinterpret_cast<f32x4*>(out + i) = acc;
 }
 
+void slab_reduce(const float* slab, int64_t stride, int splits, float* out, int64_t n, hipStream_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n / 4 + 63) / 64)), dim3(64), 0, stream, slab, stride, splits,
+                     out, n);
+}
+
 int u8x3_wgrad_splits(int M, int N, int K) {
   int splits = gemm_f32x3_pick_splits(N, K, M, true);
   int kps = (M + splits - 1) / splits;

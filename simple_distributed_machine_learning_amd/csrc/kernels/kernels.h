@@ -89,6 +89,16 @@ bool u8_fwd_supported(int M, int N, int K, int ldx, const void* X);
 void split3_pad(const float* w, unsigned short* out, int N, int K, int Kp, hipStream_t stream);
 void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
             const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream);
+// mlp_u8.hip: weight + bias gradient of the uint8-fed first layer (K = 784 pixel columns, N % 64 == 0,
+// M % 32 == 0): gw[N][784] += scale * dz^T X, gb[N] += colsum(dz), where gb MUST directly follow gw in
+// memory (gwb = gw, gwb + N * 784 = gb: the flat gradient buffer's layout). slab: workspace of
+// u8_wgrad_slab_floats(M, N) floats; deterministic (fixed-order reduction).
+bool u8_wgrad_supported(int M, int N, int K, int ldx, const void* X, const void* dz);
+int64_t u8_wgrad_slab_floats(int M, int N);
+void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
+              hipStream_t stream);
+// out[i] += sum_s slab[s * stride + i] in split order (n % 4 == 0, 16-B aligned)
+void slab_reduce(const float* slab, int64_t stride, int splits, float* out, int64_t n, hipStream_t stream);
 
 // ---- fused classifier head: z = x W^T + b; log_softmax; NLL; backward --------------------
 // x [M,K] fp32, W [C,K], b [C], target [M] int64. stats[0] += sum loss, stats[1] += #correct.

@@ -27,6 +27,7 @@
 // Measured at 131072 x 784 -> 128 (tools/bench_u8.py): see README "uint8 pixels".
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -290,6 +291,189 @@ __global__ void __launch_bounds__(256) split3_pad_kernel(const float* __restrict
   out[2 * n + i] = lo;
 }
 
+
+// ==== weight gradient of the uint8-fed first layer =============================================
+// gW[n][k] += scale * sum_m dz[m][n] X[m][k]   and   gb[n] += sum_m dz[m][n]
+// (dz [M][N] fp32 = the boundary gradient, already ReLU-masked; X [M][784] uint8 pixels).
+//
+// Why this shape: the reduction runs over the batch (K = 131072 rows), so the work is split over
+// row ranges and every workgroup leaves one partial tile. dz must be split into 3 bf16 planes on
+// the VALU; in a 128 x 128 output tile (gemm_f32x3's kernel) every dz element is split 7 times
+// (once per 128-column tile), which made that kernel VALU-issue-bound (~90 VALU per 12 MFMAs).
+// Here a workgroup owns 64 hidden units x ALL 784 columns: each dz element is split exactly once
+// and each pixel byte widened twice (once per hidden half), at the price of larger partial tiles
+// (written with plain stores, reduced in fixed order by slab_reduce).
+//
+// Geometry: v_mfma_f32_16x16x32_bf16 (784 = 49 16-column tiles); 8 waves: waves 0..6 each own 64
+// hidden x 112 columns (4 x 7 MFMA tiles, 28 f32x4 accumulators), wave 7 only stages. All 8 waves
+// stage the next 32-row K-step (dz float4 -> 3 bf16 planes, 16 pixel bytes -> 16 bf16) into the
+// other LDS buffer while the current one is consumed. Both operands are k-major in memory (the
+// reduction index is the row), so fragments come from [row][col] LDS images through
+// ds_read_b64_tr_b16 (a 16-lane group reads 4 rows x 16 columns and receives them transposed).
+constexpr int GT = 512;             // threads
+constexpr int GHN = 64;             // hidden units per workgroup
+constexpr int GBK = 32;             // rows per K-step (one 16x16x32 MFMA k-step)
+constexpr int GKC = 784;            // pixel columns (MNIST)
+constexpr int GXP = GKC + 8;        // LDS pitch (bf16) of the pixel image rows
+constexpr int GDP = GHN + 8;        // LDS pitch (bf16) of the dz plane rows
+constexpr int GX_U16 = GBK * GXP;   // pixel image per buffer (u16)
+constexpr int GD_U16 = GBK * GDP;   // one dz plane per buffer (u16)
+constexpr int GBUF_U16 = GX_U16 + 3 * GD_U16;
+constexpr int GXCH = GBK * GKC / 16;  // 16-byte pixel chunks per K-step (1568)
+static_assert(2 * GBUF_U16 * 2 <= 160 * 1024, "LDS");
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ s16x4 tr16(const u16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+// 16-lane group g reads rows 8g + 0..3 and 8g + 4..7 of columns c0 .. c0 + 15 of a [row][pitch]
+// image; lane i of the group receives column c0 + i: elements j = 0..7 <-> row 8g + j
+template <int PITCH>
+__device__ __forceinline__ bf16x8 frag_tr(const u16* img, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const u16* p = img + (8 * g + (i >> 2)) * PITCH + c0 + 4 * (i & 3);
+  const s16x4 lo = tr16(p), hi = tr16(p + 4 * PITCH);
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+
+struct WgradParams {
+  const float* dz;           // [M][N]
+  const unsigned char* X;    // [M][ldx]
+  float* slab;               // [splits][N * 784 + N]: gW partial (scaled) then gb partial
+  int M, N, ldx;
+  int rows_per_split;        // multiple of GBK
+  float scale;
+};
+
+__global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
+  __shared__ __attribute__((aligned(16))) u16 smem[2 * GBUF_U16];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int n0 = blockIdx.x * GHN;
+  const int split = blockIdx.y;
+  const int r0 = split * p.rows_per_split;
+  const int nk = min(p.rows_per_split, p.M - r0) / GBK;  // host: M % GBK == 0
+
+  // ---- staging: thread t owns dz float4 (row t >> 4, hidden 4 (t & 15)) and pixel chunks
+  // t, t + 512, t + 1024 (+ t + 1536 for t < 32) (chunk c: row c / 49, columns 16 (c % 49)) ----
+  const float* dzp = p.dz + (size_t)(r0 + (t >> 4)) * p.N + n0 + 4 * (t & 15);
+  const size_t dz_step = (size_t)GBK * p.N;
+  const unsigned char* xp[4];
+  int xoff[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c = min(t + GT * u, GXCH - 1);  // the 4th round: threads >= 32 redo the last chunk
+    xp[u] = p.X + (size_t)(r0 + c / 49) * p.ldx + 16 * (c % 49);
+    xoff[u] = (c / 49) * GXP + 16 * (c % 49);
+  }
+  const bool x4 = t + 3 * GT < GXCH;
+  const size_t x_step = (size_t)GBK * p.ldx;
+  f32x4v dv;
+  u32x4 xv[4];
+  f32x4v bsum = {0.f, 0.f, 0.f, 0.f};
+  auto gload = [&](int kt) {
+    dv = *reinterpret_cast<const f32x4v*>(dzp + kt * dz_step);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xv[u] = *reinterpret_cast<const u32x4*>(xp[u] + kt * x_step);
+  };
+  auto stage = [&](int buf) {
+    u16* B = smem + buf * GBUF_U16;
+    bsum += dv;
+    u16x4 hi, mi, lo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x = dv[e];
+      const u16 h = bf16_bits(x);
+      const float r1 = x - bf16_val(h);
+      const u16 m = bf16_bits(r1);
+      hi[e] = h;
+      mi[e] = m;
+      lo[e] = bf16_bits(r1 - bf16_val(m));
+    }
+    const int doff = GX_U16 + (t >> 4) * GDP + 4 * (t & 15);
+    *reinterpret_cast<u16x4*>(B + doff) = hi;
+    *reinterpret_cast<u16x4*>(B + doff + GD_U16) = mi;
+    *reinterpret_cast<u16x4*>(B + doff + 2 * GD_U16) = lo;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u == 3 && !x4) break;
+      *reinterpret_cast<bf16x8*>(B + xoff[u]) = widen8(xv[u][0], xv[u][1]);
+      *reinterpret_cast<bf16x8*>(B + xoff[u] + 8) = widen8(xv[u][2], xv[u][3]);
+    }
+  };
+
+  // ---- compute: wave w < 7 owns columns 112 w .. 112 w + 111 (7 tiles) x all 64 hidden (4 tiles)
+  f32x4v acc[4][7];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  const bool computes = wave < 7;
+  const int c0 = 112 * (wave < 7 ? wave : 0);
+  auto compute = [&](int buf) {
+    const u16* B = smem + buf * GBUF_U16;
+    bf16x8 a[4][3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) a[i][pl] = frag_tr<GDP>(B + GX_U16 + pl * GD_U16, 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const bf16x8 b = frag_tr<GXP>(B, c0 + 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b, acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  if (nk > 0) {
+    gload(0);
+    stage(0);
+    if (nk > 1) gload(1);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (computes) compute(kt & 1);  // wave-uniform
+    if (kt + 1 < nk) {
+      stage((kt + 1) & 1);  // the other buffer: its last readers passed the previous barrier
+      if (kt + 2 < nk) gload(kt + 2);
+    }
+    __syncthreads();
+  }
+
+  // ---- partial tile -> slab (plain stores); C map: column = lane & 15, row = 4 (lane >> 4) + r
+  float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
+  if (computes) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + 16 * i + 4 * (lane >> 4) + r;
+          out[(size_t)n * GKC + c0 + 16 * j + (lane & 15)] = acc[i][j][r] * p.scale;
+        }
+  }
+  // bias-gradient partial: the 32 threads of each hidden float4 meet in LDS (buffers are free)
+  float* red = reinterpret_cast<float*>(smem);
+  *reinterpret_cast<f32x4v*>(red + 4 * t) = bsum;
+  __syncthreads();
+  if (t < GHN) {
+    float sacc = 0.f;
+    for (int rr = 0; rr < GBK; ++rr) sacc += red[4 * (rr * 16 + (t >> 2)) + (t & 3)];
+    out[(size_t)p.N * GKC + n0 + t] = sacc;
+  }
+}
+
 }  // namespace
 
 int u8_fwd_kpad(int K) { return (K + FBK - 1) / FBK * FBK; }  // zero-padded W planes
@@ -298,6 +482,41 @@ bool u8_fwd_supported(int M, int N, int K, int ldx, const void* X) {
   // (the epilogue stores 16-B row pieces: C 16-B aligned with ldc % 4 == 0, checked by the caller)
   return M >= FBM && N % FBN == 0 && K >= 16 && K % 16 == 0 && ldx % 16 == 0 &&
          (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (int64_t)M * ldx < (int64_t(1) << 31);
+}
+
+bool u8_wgrad_supported(int M, int N, int K, int ldx, const void* X, const void* dz) {
+  return K == GKC && N % GHN == 0 && M % GBK == 0 && M >= GBK && ldx % 16 == 0 &&
+         (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (reinterpret_cast<uintptr_t>(dz) & 15) == 0 &&
+         (int64_t)M * ldx < (int64_t(1) << 31);
+}
+
+int u8_wgrad_splits(int M, int N) {
+  // one workgroup per CU: (N / 64) hidden groups x splits ~ 256 workgroups, >= 4 K-steps each
+  const int groups = N / GHN;
+  int splits = std::max(1, 256 / std::max(1, groups));
+  splits = std::min(splits, std::max(1, M / (4 * GBK)));
+  const int rps = ((M + splits - 1) / splits + GBK - 1) / GBK * GBK;
+  return (M + rps - 1) / rps;
+}
+
+int64_t u8_wgrad_slab_floats(int M, int N) {
+  return (int64_t)u8_wgrad_splits(M, N) * ((int64_t)N * GKC + N);
+}
+
+void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
+              hipStream_t stream) {
+  WgradParams p;
+  p.dz = dz;
+  p.X = X;
+  p.slab = slab;
+  p.M = M;
+  p.N = N;
+  p.ldx = ldx;
+  p.scale = scale;
+  const int splits = u8_wgrad_splits(M, N);
+  p.rows_per_split = ((M + splits - 1) / splits + GBK - 1) / GBK * GBK;
+  hipLaunchKernelGGL(u8_wgrad_kernel, dim3(N / GHN, splits), dim3(GT), 0, stream, p);
+  slab_reduce(slab, (int64_t)N * GKC + N, splits, gwb, (int64_t)N * GKC + N, stream);
 }
 
 void split3_pad(const float* w, unsigned short* out, int N, int K, int Kp, hipStream_t stream) {

@@ -223,6 +223,20 @@ void linear_wgrad_u8(torch::Tensor x, torch::Tensor gz, torch::Tensor gw, c10::o
     linear_bwd_f32(pixels_f32(x, scale), c10::nullopt, gz, /*w=*/gw, gw, gb, false, false, false);
     return;
   }
+  static const bool legacy_wgrad = [] {
+    const char* e = getenv("SDML_U8_WGRAD");
+    return e && std::string(e) == "x3";
+  }();
+  // mlp_u8.hip's kernel writes gw and gb through one [N * K + N] span: gb must follow gw
+  const bool gb_follows = opt_ptr(gb) && gw.is_contiguous() && gb->is_contiguous() &&
+                          opt_ptr(gb) == gw.data_ptr<float>() + N * K;
+  if (!legacy_wgrad && gb_follows && sdml::u8_wgrad_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr(),
+                                                               gz.data_ptr())) {
+    auto ws = torch::empty({sdml::u8_wgrad_slab_floats((int)M, (int)N)}, gw.options());
+    sdml::u8_wgrad(gz.data_ptr<float>(), x.data_ptr<uint8_t>(), (int)M, (int)N, (int)K, ws.data_ptr<float>(),
+                   gw.data_ptr<float>(), (float)scale, cur_stream());
+    return;
+  }
   float* slab = nullptr;
   torch::Tensor ws;
   if ((N * K) % 4 == 0 && (reinterpret_cast<uintptr_t>(gw.data_ptr()) & 15) == 0 && gw.is_contiguous()) {

@@ -185,12 +185,20 @@ def test_linear_fwd_u8_matches_fp32_reference(M, N, Kd):
     torch.testing.assert_close(y, ops.linear_relu_fwd(x8.float().div(255.0), w, b), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("M,N,Kd", [(131072, 128, 784), (4096 + 33, 128, 784), (6000, 1024, 784), (8192, 36, 96)])
-def test_linear_wgrad_u8_matches_fp32_reference(M, N, Kd):
+@pytest.mark.parametrize("flat", [False, True])
+@pytest.mark.parametrize("M,N,Kd", [(131072, 128, 784), (4096 + 33, 128, 784), (6000, 1024, 784), (8192, 36, 96),
+                                    (4096, 128, 784), (65536, 64, 784)])
+def test_linear_wgrad_u8_matches_fp32_reference(M, N, Kd, flat):
+    """flat: gw and gb adjacent in one buffer (the flat gradient layout), which selects mlp_u8.hip's
+    one-split-per-dz-element kernel when M % 32 == 0; otherwise the bf16x3 engine kernel."""
     x8 = pixels(M, Kd, 6)
     gz = rnd(M, N, seed=7) * (rnd(M, N, seed=8) > 0).float()
     gw0, gb0 = rnd(N, Kd, seed=9), rnd(N, seed=10)
-    gw, gb = gw0.clone(), gb0.clone()
+    if flat:
+        buf = torch.cat([gw0.reshape(-1), gb0])
+        gw, gb = buf[:N * Kd].view(N, Kd), buf[N * Kd:]
+    else:
+        gw, gb = gw0.clone(), gb0.clone()
     K.linear_wgrad_u8(x8, gz, gw, gb, 1.0 / 255.0)
     xf = x8.double() / 255.0
     want_w = gw0.double() + gz.double().t() @ xf

@@ -1,5 +1,5 @@
 """Micro-benchmark of the uint8-pixel first-layer GEMMs at the headline shape (131072 x 784 -> 128).
-Env knobs (read once per process): SDML_X3_DEEP, SDML_U8_WGRAD_WG_PER_CU."""
+Env knobs (read once per process): SDML_X3_DEEP, SDML_U8_WGRAD_WG_PER_CU, SDML_U8_FWD=x3, SDML_U8_WGRAD=x3."""
 import json
 import os
 import sys
@@ -16,7 +16,8 @@ x8 = torch.randint(0, 256, (M, Kd), dtype=torch.uint8, device=dev)
 w = torch.randn(N, Kd, device=dev) * 0.05
 b = torch.randn(N, device=dev)
 gz = torch.randn(M, N, device=dev)
-gw, gb = torch.zeros(N, Kd, device=dev), torch.zeros(N, device=dev)
+_g = torch.zeros(N * Kd + N, device=dev)  # flat layout: gb right after gw (as in the engine's grad buffer)
+gw, gb = _g[:N * Kd].view(N, Kd), _g[N * Kd:]
 
 
 def timeit(fn, n=50):

@@ -212,7 +212,9 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
     if (t < nk) issue_stage(p, smem + t * STAGE, m0, n0, t * FBK, wave, lane);
-  auto sync_step = [&](int t) {  // stage t % NS landed and visible; stage (t - 1) % NS free
+  // stage t % NS landed and visible; stage (t - 1) % NS free; ISSUE: refill it with K-step t+NS-1
+  // (the main loop passes a compile-time true so its body stays one basic block)
+  auto sync_step = [&](int t, auto issue_c) {
     const int ahead = min(NS - 2, nk - 1 - t);  // K-steps issued after t that may stay in flight
     if constexpr (NS >= 4) {
       if (ahead >= 2) wait_vmcnt<2 * GLDS_PER_STAGE>();
@@ -227,16 +229,17 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");  // no LDS access moves across the barrier
-    if constexpr (MODE != 2) {
-      if (t + NS - 1 < nk) issue_stage(p, smem + ((t + NS - 1) % NS) * STAGE, m0, n0, (t + NS - 1) * FBK, wave, lane);
+    if constexpr (MODE != 2 && decltype(issue_c)::value) {
+      if (NS == 2 || t + NS - 1 < nk)
+        issue_stage(p, smem + ((t + NS - 1) % NS) * STAGE, m0, n0, (t + NS - 1) * FBK, wave, lane);
     }
   };
-  for (int t = 0; t + 1 < nk; ++t) {
-    sync_step(t);
+  for (int t = 0; t + 1 < nk; ++t) {  // NS == 2: K-step t + 1 always exists here
+    sync_step(t, std::true_type{});
     kstep(smem + (t % NS) * STAGE, std::integral_constant<int, NSUB>{});
   }
   {  // last K-step: only the substeps holding k < K (lane half 0 covers the first FBK / 2 k)
-    sync_step(nk - 1);
+    sync_step(nk - 1, std::integral_constant<bool, (NS > 2)>{});
     const unsigned char* st = smem + ((nk - 1) % NS) * STAGE;
     const int v = p.K - (nk - 1) * FBK;
     if (v > FBK / 2 - 8) kstep(st, std::integral_constant<int, NSUB>{});
@@ -304,37 +307,46 @@ __global__ void __launch_bounds__(256) split3_pad_kernel(const float* __restrict
 // and each pixel byte widened twice (once per hidden half), at the price of larger partial tiles
 // (written with plain stores, reduced in fixed order by slab_reduce).
 //
-// Geometry: v_mfma_f32_16x16x32_bf16 (784 = 49 16-column tiles); 8 waves: waves 0..6 each own 64
-// hidden x 112 columns (4 x 7 MFMA tiles, 28 f32x4 accumulators), wave 7 only stages. All 8 waves
-// stage the next 32-row K-step (dz float4 -> 3 bf16 planes, 16 pixel bytes -> 16 bf16) into the
-// other LDS buffer while the current one is consumed. Both operands are k-major in memory (the
-// reduction index is the row), so fragments come from [row][col] LDS images through
-// ds_read_b64_tr_b16 (a 16-lane group reads 4 rows x 16 columns and receives them transposed).
+// Geometry: v_mfma_f32_32x32x16_bf16 (an MFMA holds the SIMD's vector issue 8 of its 32 cycles;
+// the 16x16x32 form holds 8 of 16, which left a first version of this kernel issue-bound), the 784
+// columns padded to 25 tiles of 32. 8 waves, all computing: wave 0 owns columns 0..127, waves
+// 1..7 three 32-column tiles each, every wave all 64 hidden (2 x {4,3} tiles, <= 8 f32x16
+// accumulators). All 8 waves stage the next 32-row K-step (dz float4 -> 3 bf16 planes, 16 pixel
+// bytes -> 16 bf16) into the other LDS buffer while the current one is consumed. Both operands
+// are k-major in memory (the reduction index is the row), so fragments come from [row][col] LDS
+// images through ds_read_b64_tr_b16 (a 16-lane group reads 4 rows x 16 columns, transposed).
 constexpr int GT = 512;             // threads
 constexpr int GHN = 64;             // hidden units per workgroup
-constexpr int GBK = 32;             // rows per K-step (one 16x16x32 MFMA k-step)
+constexpr int GBK = 32;             // rows per K-step (two 32x32x16 MFMA k-substeps)
 constexpr int GKC = 784;            // pixel columns (MNIST)
-constexpr int GXP = GKC + 8;        // LDS pitch (bf16) of the pixel image rows
-constexpr int GDP = GHN + 8;        // LDS pitch (bf16) of the dz plane rows
+constexpr int GKP = 800;            // padded to 25 column tiles of 32
+// LDS row pitches: a transposed read of a 32x32x16 operand has a 32-lane half read 4 consecutive
+// rows x 64 B (16 banks each), conflict-free when the row pitch is 16 dwords mod 64 (rows land on
+// bank offsets 0, 16, 32, 48 in some order): 1600 B (400 dwords) and 192 B (48 dwords).
+// Measured before: pitches 1616 / 144 B -> SQ_LDS_BANK_CONFLICT 47% of LDS-active cycles.
+constexpr int GXP = GKP;            // LDS pitch (bf16) of the pixel image rows
+constexpr int GDP = GHN + 32;       // LDS pitch (bf16) of the dz plane rows
+static_assert((GXP * 2 / 4) % 64 == 16 && (GDP * 2 / 4) % 64 == 48, "conflict-free transposed-read pitches");
 constexpr int GX_U16 = GBK * GXP;   // pixel image per buffer (u16)
 constexpr int GD_U16 = GBK * GDP;   // one dz plane per buffer (u16)
 constexpr int GBUF_U16 = GX_U16 + 3 * GD_U16;
-constexpr int GXCH = GBK * GKC / 16;  // 16-byte pixel chunks per K-step (1568)
+constexpr int GXCH = GBK * (GKP / 16);  // 16-byte pixel chunks per K-step incl. the zero pad (1600)
 static_assert(2 * GBUF_U16 * 2 <= 160 * 1024, "LDS");
 
-typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ s16x4 tr16(const u16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
 }
 
-// 16-lane group g reads rows 8g + 0..3 and 8g + 4..7 of columns c0 .. c0 + 15 of a [row][pitch]
-// image; lane i of the group receives column c0 + i: elements j = 0..7 <-> row 8g + j
+// 32x32x16 operand of the 32 columns c0.. of a [k-row][PITCH] image at k-substep s: lane l
+// (r = l & 31, h = l >> 5) gets column c0 + r, k-rows 16 s + 8 h + j (j = 0..7). Two tr16 reads:
+// 16-lane group g covers k-rows 16 s + 8 (g >> 1) + q (+4), lane 4q + p addressing columns
+// c0 + 16 (g & 1) + 4p .. +3, lane i receiving column c0 + 16 (g & 1) + i.
 template <int PITCH>
-__device__ __forceinline__ bf16x8 frag_tr(const u16* img, int c0, int lane) {
+__device__ __forceinline__ bf16x8 frag_tr(const u16* img, int c0, int s, int lane) {
   const int g = lane >> 4, i = lane & 15;
-  const u16* p = img + (8 * g + (i >> 2)) * PITCH + c0 + 4 * (i & 3);
+  const u16* p = img + (16 * s + 8 * (g >> 1) + (i >> 2)) * PITCH + c0 + 16 * (g & 1) + 4 * (i & 3);
   const s16x4 lo = tr16(p), hi = tr16(p + 4 * PITCH);
   bf16x8 f;
   f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
@@ -361,26 +373,31 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   const int nk = min(p.rows_per_split, p.M - r0) / GBK;  // host: M % GBK == 0
 
   // ---- staging: thread t owns dz float4 (row t >> 4, hidden 4 (t & 15)) and pixel chunks
-  // t, t + 512, t + 1024 (+ t + 1536 for t < 32) (chunk c: row c / 49, columns 16 (c % 49)) ----
+  // t + 512 u (chunk c: row c / 50, columns 16 (c % 50); c % 50 == 49 is the zero pad). The 4th
+  // round covers chunks 1536..1599: threads >= 64 repeat chunk 1599 (same bytes to the same
+  // place), so staging has no lane-dependent branches ----
   const float* dzp = p.dz + (size_t)(r0 + (t >> 4)) * p.N + n0 + 4 * (t & 15);
   const size_t dz_step = (size_t)GBK * p.N;
-  const unsigned char* xp[4];
-  int xoff[4];
+  constexpr int XU = (GXCH + GT - 1) / GT;  // 4 rounds
+  const unsigned char* xp[XU];
+  int xoff[XU];
+  bool xload[XU];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int c = min(t + GT * u, GXCH - 1);  // the 4th round: threads >= 32 redo the last chunk
-    xp[u] = p.X + (size_t)(r0 + c / 49) * p.ldx + 16 * (c % 49);
-    xoff[u] = (c / 49) * GXP + 16 * (c % 49);
+  for (int u = 0; u < XU; ++u) {
+    const int c = min(t + GT * u, GXCH - 1);
+    const int row = c / 50, cc = c % 50;
+    xload[u] = cc < 49;
+    xp[u] = p.X + (size_t)(r0 + row) * p.ldx + 16 * min(cc, 48);
+    xoff[u] = row * GXP + 16 * cc;
   }
-  const bool x4 = t + 3 * GT < GXCH;
   const size_t x_step = (size_t)GBK * p.ldx;
-  f32x4v dv;
-  u32x4 xv[4];
-  f32x4v bsum = {0.f, 0.f, 0.f, 0.f};
+  f32x4 dv;
+  u32x4 xv[XU];
+  f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
   auto gload = [&](int kt) {
-    dv = *reinterpret_cast<const f32x4v*>(dzp + kt * dz_step);
+    dv = *reinterpret_cast<const f32x4*>(dzp + kt * dz_step);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) xv[u] = *reinterpret_cast<const u32x4*>(xp[u] + kt * x_step);
+    for (int u = 0; u < XU; ++u) xv[u] = *reinterpret_cast<const u32x4*>(xp[u] + kt * x_step);
   };
   auto stage = [&](int buf) {
     u16* B = smem + buf * GBUF_U16;
@@ -401,71 +418,90 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     *reinterpret_cast<u16x4*>(B + doff + GD_U16) = mi;
     *reinterpret_cast<u16x4*>(B + doff + 2 * GD_U16) = lo;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (u == 3 && !x4) break;
-      *reinterpret_cast<bf16x8*>(B + xoff[u]) = widen8(xv[u][0], xv[u][1]);
-      *reinterpret_cast<bf16x8*>(B + xoff[u] + 8) = widen8(xv[u][2], xv[u][3]);
+    for (int u = 0; u < XU; ++u) {
+      const u32x4 v = xload[u] ? xv[u] : u32x4{0u, 0u, 0u, 0u};
+      *reinterpret_cast<bf16x8*>(B + xoff[u]) = widen8(v[0], v[1]);
+      *reinterpret_cast<bf16x8*>(B + xoff[u] + 8) = widen8(v[2], v[3]);
     }
   };
 
-  // ---- compute: wave w < 7 owns columns 112 w .. 112 w + 111 (7 tiles) x all 64 hidden (4 tiles)
-  f32x4v acc[4][7];
+  // ---- compute: wave 0 columns 0..127, wave w >= 1 columns 128 + 96 (w - 1) .. +95; all 64 hidden.
+  // The K loop is instantiated per column count, and its body has no branches: the compiler can
+  // then interleave the staging VALU work into the MFMA shadows of the same wave.
+  auto run = [&](auto nct_c) {
+    constexpr int NCT = decltype(nct_c)::value;
+    const int ct0 = NCT == 4 ? 0 : 4 + 3 * (wave - 1);  // first 32-column tile
+    f32x16 acc[2][NCT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 7; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  const bool computes = wave < 7;
-  const int c0 = 112 * (wave < 7 ? wave : 0);
-  auto compute = [&](int buf) {
-    const u16* B = smem + buf * GBUF_U16;
-    bf16x8 a[4][3];
+      for (int j = 0; j < NCT; ++j) acc[i][j] = f32x16{};
+    auto compute = [&](int buf) {
+      const u16* B = smem + buf * GBUF_U16;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 a[2][3];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) a[i][pl] = frag_tr<GDP>(B + GX_U16 + pl * GD_U16, 16 * i, lane);
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      const bf16x8 b = frag_tr<GXP>(B, c0 + 16 * j, lane);
+          for (int pl = 0; pl < 3; ++pl) a[i][pl] = frag_tr<GDP>(B + GX_U16 + pl * GD_U16, 32 * i, s, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b, acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b, acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b, acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NCT; ++j) {
+          const bf16x8 b = frag_tr<GXP>(B, 32 * (ct0 + j), s, lane);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            acc[i][j] = mfma(a[i][2], b, acc[i][j]);
+            acc[i][j] = mfma(a[i][1], b, acc[i][j]);
+            acc[i][j] = mfma(a[i][0], b, acc[i][j]);
+          }
+        }
       }
-    }
-  };
-
-  if (nk > 0) {
+    };
+    // buffer kt & 1 is consumed in step kt while step kt+1 is staged into the other one (its last
+    // readers passed the previous barrier) and step kt+2's global loads fly
     gload(0);
     stage(0);
     if (nk > 1) gload(1);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 2 < nk; ++kt) {
+      compute(kt & 1);
+      stage((kt + 1) & 1);
+      gload(kt + 2);
+      __syncthreads();
+    }
+    if (kt + 1 < nk) {
+      compute(kt & 1);
+      stage((kt + 1) & 1);
+      __syncthreads();
+      ++kt;
+    }
+    compute(kt & 1);
+
+    // partial tile -> slab (plain stores); C map: column = lane & 31, row = (r&3) + 8(r>>2) + 4h
+    float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) {
+      const int col = 32 * (ct0 + j) + (lane & 31);
+      if (col >= GKC) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int n = n0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          out[(size_t)n * GKC + col] = acc[i][j][r] * p.scale;
+        }
+    }
+  };
+  if (nk > 0) {
+    if (wave == 0) run(std::integral_constant<int, 4>{});
+    else run(std::integral_constant<int, 3>{});
   }
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (computes) compute(kt & 1);  // wave-uniform
-    if (kt + 1 < nk) {
-      stage((kt + 1) & 1);  // the other buffer: its last readers passed the previous barrier
-      if (kt + 2 < nk) gload(kt + 2);
-    }
-    __syncthreads();
-  }
-
-  // ---- partial tile -> slab (plain stores); C map: column = lane & 15, row = 4 (lane >> 4) + r
   float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
-  if (computes) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 7; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int n = n0 + 16 * i + 4 * (lane >> 4) + r;
-          out[(size_t)n * GKC + c0 + 16 * j + (lane & 15)] = acc[i][j][r] * p.scale;
-        }
-  }
   // bias-gradient partial: the 32 threads of each hidden float4 meet in LDS (buffers are free)
   float* red = reinterpret_cast<float*>(smem);
-  *reinterpret_cast<f32x4v*>(red + 4 * t) = bsum;
+  *reinterpret_cast<f32x4*>(red + 4 * t) = bsum;
   __syncthreads();
   if (t < GHN) {
     float sacc = 0.f;

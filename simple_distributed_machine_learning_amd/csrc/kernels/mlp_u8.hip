@@ -15,8 +15,10 @@
 // wave tile 64 x 64 = 2 x 2 tiles of v_mfma_f32_32x32x16_bf16, K-step 64 (4 MFMA k-substeps).
 // Both operands reach LDS by LDS-DMA (global_load_lds_dwordx4, 16 B per lane, no VGPR staging)
 // into a ring of NS stages (2 x 64 KiB; the DMA of K-step t+1 flies under K-step t's 48 MFMAs per
-// wave). Measured alternative: 32-deep K-steps in a 4-stage ring (3 K-steps in flight), slower
-// (102.6 vs 93.8 us at the headline shape: half the MFMAs per barrier).
+// wave). Measured alternatives: 32-deep K-steps in a 4-stage ring (3 K-steps in flight), slower
+// (102.6 vs 93.8 us at the headline shape: half the MFMAs per barrier); weight fragments of
+// substep s+1 pinned ahead of substep s's MFMAs with sched_barrier (register double buffer),
+// 2-3 % slower than the compiler's own placement.
 // The LDS images are swizzled on the DMA's per-lane source address (the DMA writes 1 KiB
 // lane-linearly) so the fragment ds_read_b128s are conflict-free; k order inside a K-step is
 // permuted identically for both operands (lane half h, substep s, element j <-> k = 32h + 8s + j),

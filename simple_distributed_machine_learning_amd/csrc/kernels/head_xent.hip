@@ -12,6 +12,9 @@
 //      and a second tiny pass sums the slabs in block order (deterministic, no contention).
 // Memory-bound by design (0.5 KiB read + 0.5 KiB written per sample); all MACs on VALU.
 // Small batches (<= 2048 rows) use 16-row chunks with 16 threads per row instead.
+// Measured and rejected (round 2): 32 lanes per row with W and the dW partial in registers and no
+// LDS in the row loop - 75 us vs 49 us at 131072 rows: every lane of a row then redoes the
+// row's reduction and softmax, ~2.8x the VALU work per row of this 4-lanes-per-row layout.
 //
 // head_generic: any K (multiple of 4) / C <= 32: computes loss/dz/dx per row (one wave per
 // row); dW/db are then done by the MFMA GEMM (gemm_f32 with fused row-sum).

@@ -18,7 +18,8 @@
 // wave). Measured alternatives: 32-deep K-steps in a 4-stage ring (3 K-steps in flight), slower
 // (102.6 vs 93.8 us at the headline shape: half the MFMAs per barrier); weight fragments of
 // substep s+1 pinned ahead of substep s's MFMAs with sched_barrier (register double buffer),
-// 2-3 % slower than the compiler's own placement.
+// 2-3 % slower than the compiler's own placement; 1024-thread blocks of 512 rows (W staged once
+// per CU instead of twice) do not fit 4 waves per SIMD: 128 VGPRs with ~400 spilled.
 // The LDS images are swizzled on the DMA's per-lane source address (the DMA writes 1 KiB
 // lane-linearly) so the fragment ds_read_b128s are conflict-free; k order inside a K-step is
 // permuted identically for both operands (lane half h, substep s, element j <-> k = 32h + 8s + j),

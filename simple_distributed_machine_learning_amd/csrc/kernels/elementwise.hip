@@ -16,9 +16,22 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // /root/reference/simple_distributed.py:100-104): d = g + wd*p; buf = first ? d :
 // momentum*buf + (1-dampening)*d; d = nesterov ? d + momentum*buf : buf; p -= lr*d.
 // One launch for all parameters of all stages a rank owns; 16 B per lane per stream.
+// split of an updated fp32 value into bf16 planes hi + mid + lo (exact; same arithmetic as
+// gemm_f32x3.hip / mlp_u8.hip's split kernels)
+__device__ __forceinline__ unsigned short sgd_bf16_bits(float f) {
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));
+}
+__device__ __forceinline__ float sgd_bf16_val(unsigned short b) { return __uint_as_float(((unsigned)b) << 16); }
+typedef unsigned short u16x4s __attribute__((ext_vector_type(4)));
+
+// pl: optional weight-plane cache written from the UPDATED weights (the uint8 first layer's
+// forward reads W as zero-padded bf16 planes [3][rows][Kp]; writing them here saves a separate
+// split launch per step). pl.n4 float4 of the flat buffer starting at float4 pl.off4 form a
+// [rows][K] matrix, K % 4 == 0.
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ g,
                                                   float* __restrict__ buf, int64_t n4, float lr, float mom,
-                                                  float damp, float wd, int nesterov, int first, int zero_grad) {
+                                                  float damp, float wd, int nesterov, int first, int zero_grad,
+                                                  SgdPlanes pl) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
@@ -36,7 +49,24 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
       reinterpret_cast<f32x4*>(buf)[i] = b;
       d = nesterov ? d + mom * b : b;
     }
-    reinterpret_cast<f32x4*>(p)[i] = pv - lr * d;
+    const f32x4 nv = pv - lr * d;
+    reinterpret_cast<f32x4*>(p)[i] = nv;
+    if (pl.planes && i >= pl.off4 && i < pl.off4 + pl.n4) {
+      const int64_t e = 4 * (i - pl.off4);
+      const int64_t r = e / pl.K, k = e % pl.K;
+      u16x4s h, m, l;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        h[j] = sgd_bf16_bits(nv[j]);
+        const float r1 = nv[j] - sgd_bf16_val(h[j]);
+        m[j] = sgd_bf16_bits(r1);
+        l[j] = sgd_bf16_bits(r1 - sgd_bf16_val(m[j]));
+      }
+      unsigned short* q = pl.planes + r * pl.Kp + k;
+      *reinterpret_cast<u16x4s*>(q) = h;
+      *reinterpret_cast<u16x4s*>(q + pl.plane_stride) = m;
+      *reinterpret_cast<u16x4s*>(q + 2 * pl.plane_stride) = l;
+    }
   }
 }
 
@@ -101,14 +131,14 @@ __global__ void __launch_bounds__(256) synth_kernel(uint64_t seed, int64_t start
 }  // namespace
 
 void sgd_momentum(float* p, float* g, float* buf, int64_t n, float lr, float momentum, float dampening,
-                  float wd, bool nesterov, bool first, bool zero_grad, hipStream_t stream) {
+                  float wd, bool nesterov, bool first, bool zero_grad, hipStream_t stream, SgdPlanes planes) {
   // flat buffers are padded to 64 elements, so n is a multiple of 4
   const int64_t n4 = n / 4;
   int64_t blocks = (n4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, g, buf, n4, lr, momentum, dampening,
-                     wd, nesterov ? 1 : 0, first ? 1 : 0, zero_grad ? 1 : 0);
+                     wd, nesterov ? 1 : 0, first ? 1 : 0, zero_grad ? 1 : 0, planes);
 }
 
 void sgd_momentum_mixed(float* master, void* p_bf16, void* g_bf16, float* buf, int64_t n, float lr, float momentum,

@@ -124,8 +124,15 @@ void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx,
 
 // ---- SGD with momentum over a flat buffer ------------------------------------------------
 // zero_grad: also writes g = 0 after reading it (fuses the next step's zero_grad)
+// optional bf16 weight-plane cache written from the updated weights (see sgd_kernel)
+struct SgdPlanes {
+  unsigned short* planes = nullptr;  // [3][rows][Kp], plane_stride = rows * Kp
+  int64_t off4 = 0, n4 = 0;          // float4 range of the flat buffer holding the [rows][K] weight
+  int64_t K = 0, Kp = 0, plane_stride = 0;
+};
 void sgd_momentum(float* p, float* g, float* buf, int64_t n, float lr, float momentum, float dampening,
-                  float wd, bool nesterov, bool first, bool zero_grad, hipStream_t stream);
+                  float wd, bool nesterov, bool first, bool zero_grad, hipStream_t stream,
+                  SgdPlanes planes = SgdPlanes());
 
 // bf16 model weights with fp32 master weights: master/buf fp32, p/g bf16 (n % 4 == 0)
 void sgd_momentum_mixed(float* master, void* p_bf16, void* g_bf16, float* buf, int64_t n, float lr, float momentum,

@@ -172,7 +172,7 @@ torch::Tensor pixels_f32(const torch::Tensor& x, double scale) {
 // scale = 1/255 this is ToTensor() fused into the GEMM's operand load. Shapes the uint8 kernel
 // does not take (small batches, unaligned K) go through an fp32 copy of x * scale.
 torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> b, bool relu,
-                            double scale) {
+                            double scale, c10::optional<torch::Tensor> planes, bool planes_valid) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
               "linear_fwd_u8: x must be a contiguous 2-D uint8 ROCm tensor");
   check_f32_cuda(w, "w");
@@ -190,9 +190,16 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
   }();
   if (!legacy && sdml::u8_fwd_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr())) {
     const int Kp = sdml::u8_fwd_kpad((int)K);
-    auto wp = torch::empty({3, N, Kp}, w.options().dtype(torch::kInt16));
+    // planes: a caller-owned cache [3][N][Kp] (zero padding columns; kept current by the fused SGD
+    // step, ops/optim.py); planes_valid == false -> (re)split into it
+    const bool cache = planes.has_value() && planes->defined();
+    if (cache)
+      TORCH_CHECK(planes->is_cuda() && planes->scalar_type() == torch::kInt16 && planes->is_contiguous() &&
+                      planes->dim() == 3 && planes->size(0) == 3 && planes->size(1) == N && planes->size(2) == Kp,
+                  "linear_fwd_u8: planes must be a [3][N][u8_fwd_kpad(K)] int16 device tensor");
+    auto wp = cache ? *planes : torch::empty({3, N, Kp}, w.options().dtype(torch::kInt16));
     auto* wpp = reinterpret_cast<unsigned short*>(wp.data_ptr<int16_t>());
-    sdml::split3_pad(w.data_ptr<float>(), wpp, (int)N, (int)K, Kp, cur_stream());
+    if (!cache || !planes_valid) sdml::split3_pad(w.data_ptr<float>(), wpp, (int)N, (int)K, Kp, cur_stream());
     sdml::u8_fwd(x.data_ptr<uint8_t>(), (int)M, (int)K, (int)K, wpp, (int)N, Kp, opt_ptr(b), y.data_ptr<float>(),
                  (int)N, relu, (float)scale, cur_stream());
     return y;
@@ -675,15 +682,33 @@ torch::Tensor head_dx_from_dl(torch::Tensor dl, torch::Tensor w, torch::Tensor x
 }
 
 void sgd_momentum_(torch::Tensor p, torch::Tensor g, torch::Tensor buf, double lr, double momentum, double dampening,
-                   double wd, bool nesterov, bool first, bool zero_grad) {
+                   double wd, bool nesterov, bool first, bool zero_grad, c10::optional<torch::Tensor> planes,
+                   int64_t plane_offset, int64_t plane_rows, int64_t plane_k) {
   check_f32_cuda(p, "p");
   check_f32_cuda(g, "g");
   check_f32_cuda(buf, "buf");
   TORCH_CHECK(p.numel() == g.numel(), "sgd: p/g size mismatch");
   TORCH_CHECK(momentum == 0 || buf.numel() == p.numel(), "sgd: momentum buffer size mismatch");
   TORCH_CHECK(p.numel() % 4 == 0, "sgd: flat buffers must be padded to a multiple of 4");
+  sdml::SgdPlanes pl;
+  if (planes.has_value() && planes->defined()) {
+    // planes [3][rows][Kp] int16 (bf16 bits) of the [rows][K] weight at float offset plane_offset
+    TORCH_CHECK(planes->is_cuda() && planes->scalar_type() == torch::kInt16 && planes->is_contiguous() &&
+                    planes->dim() == 3 && planes->size(0) == 3 && planes->size(1) == plane_rows,
+                "sgd planes: [3][rows][Kp] int16 device tensor");
+    const int64_t Kp = planes->size(2);
+    TORCH_CHECK(plane_k % 4 == 0 && plane_offset % 4 == 0 && Kp % 4 == 0 && Kp >= plane_k &&
+                    plane_offset + plane_rows * plane_k <= p.numel(),
+                "sgd planes: K, offset and Kp must be multiples of 4 and the weight inside the buffer");
+    pl.planes = reinterpret_cast<unsigned short*>(planes->data_ptr<int16_t>());
+    pl.off4 = plane_offset / 4;
+    pl.n4 = plane_rows * plane_k / 4;
+    pl.K = plane_k;
+    pl.Kp = Kp;
+    pl.plane_stride = plane_rows * Kp;
+  }
   sdml::sgd_momentum(p.data_ptr<float>(), g.data_ptr<float>(), buf.data_ptr<float>(), p.numel(), (float)lr,
-                     (float)momentum, (float)dampening, (float)wd, nesterov, first, zero_grad, cur_stream());
+                     (float)momentum, (float)dampening, (float)wd, nesterov, first, zero_grad, cur_stream(), pl);
 }
 
 void sgd_momentum_mixed_(torch::Tensor master, torch::Tensor p, torch::Tensor g, torch::Tensor buf, double lr,
@@ -1004,7 +1029,10 @@ c10::optional<torch::Tensor> ref_cnn_stage1(torch::Tensor x, torch::Tensor w1, t
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "sdml gfx950 HIP kernels";
   m.def("linear_fwd_u8", &linear_fwd_u8, "act(scale * x_u8 @ w.T + b): uint8-pixel first layer", py::arg("x"),
-        py::arg("w"), py::arg("b"), py::arg("relu"), py::arg("scale"));
+        py::arg("w"), py::arg("b"), py::arg("relu"), py::arg("scale"), py::arg("planes") = py::none(),
+        py::arg("planes_valid") = false);
+  m.def("u8_fwd_kpad", [](int64_t K) { return (int64_t)sdml::u8_fwd_kpad((int)K); },
+        "padded K of the uint8 forward's weight planes");
   m.def("linear_wgrad_u8", &linear_wgrad_u8, "gw += scale * gz^T x_u8, gb += colsum(gz)", py::arg("x"), py::arg("gz"),
         py::arg("gw"), py::arg("gb"), py::arg("scale"));
   m.def("linear_fwd_f32", &linear_fwd_f32, "relu?(x @ w.T + b) on fp32 MFMA", py::arg("x"), py::arg("w"),
@@ -1024,9 +1052,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stats_acc"));
   m.def("head_dx_from_dl", &head_dx_from_dl, "dx = (dl @ w) * (x > 0): boundary gradient from its factor",
         py::arg("dl"), py::arg("w"), py::arg("x"), py::arg("mask"));
-  m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer", py::arg("p"), py::arg("g"),
-        py::arg("buf"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"),
-        py::arg("first"), py::arg("zero_grad") = false);
+  m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer (optionally also writing a "
+        "weight's bf16 plane cache)", py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"), py::arg("momentum"),
+        py::arg("dampening"), py::arg("wd"), py::arg("nesterov"), py::arg("first"), py::arg("zero_grad") = false,
+        py::arg("planes") = py::none(), py::arg("plane_offset") = 0, py::arg("plane_rows") = 0,
+        py::arg("plane_k") = 0);
   m.def("sgd_momentum_mixed_", &sgd_momentum_mixed_, "SGD: fp32 master + momentum, bf16 grads/params");
   m.def("cross_entropy_bf16", &cross_entropy_bf16, "vocab cross-entropy on bf16 logits (+ dlogits)");
   m.def("layernorm_fwd_bf16", &layernorm_fwd_bf16, "LayerNorm forward (bf16, fp32 stats)");

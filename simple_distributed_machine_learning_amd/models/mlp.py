@@ -57,6 +57,21 @@ class MLPStage(PipelineStage):
         self.in_features = dims[self.layer_ids[0]]
         # stage 0 reads MNIST's uint8 pixels directly (ToTensor fused into fc1's GEMM)
         self.accepts_u8_pixels = self.layer_ids[0] == 0
+        # fc1's bf16 weight planes, kept current by the fused SGD step (attach_plane_cache)
+        self.plane_cache = None
+        self.flat_ref = None
+
+    def attach_plane_cache(self, flat, optimizer) -> bool:
+        """ROCm, uint8-fed first layer: let ``optimizer``'s step write fc1's weight planes, so the
+        forward skips its per-step split launch (ops.PlaneCache)."""
+        if not self.accepts_u8_pixels or not flat.params.is_cuda:
+            return False
+        w = self.layers()[0].weight
+        cache = ops.PlaneCache(w)
+        if not optimizer.add_plane_cache(cache, w):
+            return False
+        self.plane_cache, self.flat_ref = cache, flat
+        return True
 
     def layers(self) -> List[nn.Linear]:
         return [getattr(self, n) for n in self.names]
@@ -90,7 +105,9 @@ class MLPStage(PipelineStage):
         for i, lin in enumerate(self.layers()):
             assert not self._is_classifier(i), "classifier layers run in head_fwd"
             if x.dtype == torch.uint8:
-                x = ops.linear_relu_fwd_u8(x, lin.weight, lin.bias)
+                cache = self.plane_cache
+                epoch = self.flat_ref.param_epoch if self.flat_ref is not None else 0
+                x = ops.linear_relu_fwd_u8(x, lin.weight, lin.bias, cache, epoch)
             else:
                 x = ops.linear_relu_fwd(x, lin.weight, lin.bias)
             acts.append(x)

@@ -34,11 +34,37 @@ def pixels_to_float(x: torch.Tensor) -> torch.Tensor:
     return x.to(torch.float32).div_(255.0) if x.dtype == torch.uint8 else x
 
 
-def linear_relu_fwd_u8(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+class PlaneCache:
+    """The uint8 first layer's weight as zero-padded bf16 planes [3][N][Kp] (hi + mid + lo == W).
+
+    The forward needs them every step; instead of a split launch per step, the fused SGD step
+    writes them from the weights it has just updated (ops/optim.py, ``add_plane_cache``). The
+    cache is valid for the parameter values identified by ``(weight._version, flat.param_epoch)``:
+    an optimizer step bumps the epoch and re-validates it, any torch in-place write to the weight
+    (checkpoint load, ...) bumps the version and invalidates it (the forward then re-splits)."""
+
+    def __init__(self, weight: torch.Tensor):
+        n, k = weight.shape
+        self.planes = torch.zeros(3, n, int(_k().u8_fwd_kpad(k)), dtype=torch.int16, device=weight.device)
+        self.token = None
+
+    @staticmethod
+    def token_of(weight: torch.Tensor, epoch: int):
+        return (weight.data_ptr(), weight._version, epoch)
+
+
+def linear_relu_fwd_u8(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, cache: Optional[PlaneCache] = None,
+                       epoch: int = 0) -> torch.Tensor:
     """relu(ToTensor(x) @ w.T + b) for uint8 pixels x [M,K]: on ROCm the /255 is folded into the
-    bf16x3 GEMM's epilogue and each pixel byte is an exact single bf16 plane (3 MFMAs/product)."""
+    GEMM's epilogue and each pixel byte is an exact single bf16 plane (3 MFMAs/product). With a
+    ``cache`` (and the flat buffer's ``epoch``) the weight planes are reused when still current."""
     if x.is_cuda:
-        return _k().linear_fwd_u8(x, w, b, True, PIXEL_SCALE)
+        if cache is None:
+            return _k().linear_fwd_u8(x, w, b, True, PIXEL_SCALE)
+        tok = PlaneCache.token_of(w, epoch)
+        y = _k().linear_fwd_u8(x, w, b, True, PIXEL_SCALE, cache.planes, cache.token == tok)
+        cache.token = tok
+        return y
     return ref.linear_relu_fwd(pixels_to_float(x), w, b)
 
 
@@ -117,11 +143,18 @@ def head_dx_from_dlogits(dl, w, x, mask: bool = True):
 
 
 def sgd_momentum_(p, g, buf, lr: float, momentum: float, dampening: float = 0.0, weight_decay: float = 0.0,
-                  nesterov: bool = False, first: bool = False, zero_grad: bool = False):
-    """In-place SGD step; with ``zero_grad`` the kernel also clears ``g`` after reading it."""
+                  nesterov: bool = False, first: bool = False, zero_grad: bool = False, planes=None):
+    """In-place SGD step; with ``zero_grad`` the kernel also clears ``g`` after reading it.
+    ``planes = (cache_tensor, offset, rows, K)``: also write that weight's bf16 plane cache from the
+    updated values (ROCm only)."""
     if p.is_cuda:
-        _k().sgd_momentum_(p, g, buf, float(lr), float(momentum), float(dampening), float(weight_decay),
-                           bool(nesterov), bool(first), bool(zero_grad))
+        if planes is not None:
+            t, off, rows, k = planes
+            _k().sgd_momentum_(p, g, buf, float(lr), float(momentum), float(dampening), float(weight_decay),
+                               bool(nesterov), bool(first), bool(zero_grad), t, int(off), int(rows), int(k))
+        else:
+            _k().sgd_momentum_(p, g, buf, float(lr), float(momentum), float(dampening), float(weight_decay),
+                               bool(nesterov), bool(first), bool(zero_grad))
         return
     ref.sgd_momentum_(p, g, buf, lr, momentum, dampening, weight_decay, nesterov, first)
     if zero_grad:

@@ -28,6 +28,18 @@ class FusedSGD:
         ref = self.master if self.master is not None else flat.params
         self.momentum_buffer = torch.zeros_like(ref) if momentum != 0 else ref.new_zeros(64)
         self.steps = 0
+        self.plane_cache = None  # (PlaneCache, weight, flat offset): written by the step kernel
+
+    def add_plane_cache(self, cache, weight: torch.Tensor) -> bool:
+        """Have the fp32 step kernel also write ``cache`` (ops.PlaneCache) from ``weight``'s updated
+        values. One cache per optimizer (the kernel takes one); returns False if not taken."""
+        if self.master is not None or self.plane_cache is not None or not self.flat.params.is_cuda:
+            return False
+        off = (weight.data_ptr() - self.flat.params.data_ptr()) // self.flat.params.element_size()
+        if not (0 <= off < self.flat.numel) or off % 4 or weight.shape[1] % 4:
+            return False
+        self.plane_cache = (cache, weight, off)
+        return True
 
     def step(self, zero_grad: bool = True):
         """One update. ``zero_grad`` clears the gradients inside the same kernel (the engine
@@ -37,11 +49,21 @@ class FusedSGD:
                                 self.momentum, self.dampening, self.weight_decay, self.nesterov, self.steps == 0,
                                 zero_grad)
         else:
+            planes = None
+            if self.plane_cache is not None:
+                cache, w, off = self.plane_cache
+                planes = (cache.planes, off, w.shape[0], w.shape[1])
             sgd_momentum_(self.flat.params, self.flat.grads, self.momentum_buffer, self.lr, self.momentum,
-                          self.dampening, self.weight_decay, self.nesterov, self.steps == 0, zero_grad)
+                          self.dampening, self.weight_decay, self.nesterov, self.steps == 0, zero_grad, planes)
         if zero_grad:
             self.flat.grads_zero = True
         self.steps += 1
+        self.flat.param_epoch += 1
+        if self.plane_cache is not None:
+            from . import PlaneCache
+
+            cache, w, _ = self.plane_cache
+            cache.token = PlaneCache.token_of(w, self.flat.param_epoch)
 
     def zero_grad(self):
         self.flat.zero_grad()

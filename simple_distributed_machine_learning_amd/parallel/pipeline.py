@@ -151,6 +151,9 @@ class PipelineEngine:
                 m.rng_step = self.step_ctr
                 self._uses_rng = True
         self.optimizer = FusedSGD(self.flat, lr=lr, momentum=momentum, weight_decay=weight_decay)
+        for m in self.stages.values():  # derived weight caches the step kernel keeps current
+            if hasattr(m, "attach_plane_cache"):
+                m.attach_plane_cache(self.flat, self.optimizer)
         self.transport = Transport(mesh) if mesh.pp > 1 else None
         self.grad_sync = GradSync(self.flat, mesh, self.local_stage_ids)
         self.training = True

@@ -69,6 +69,10 @@ class FlatParams:
             p.grad = self.grads[seg.offset:seg.offset + seg.numel].view(seg.shape)
         self._plist = plist
         self.grads_zero = True  # grads known to be all-zero (skip the next zero_grad launch)
+        # bumped by every optimizer step (whose kernels write the parameters through raw pointers,
+        # which torch's per-tensor version counters do not see); with ``param._version`` it
+        # identifies the parameter values a derived cache (ops.PlaneCache) was computed from
+        self.param_epoch = 0
 
     def zero_grad(self, force: bool = False):
         if force or not self.grads_zero:

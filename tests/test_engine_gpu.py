@@ -112,3 +112,33 @@ def test_gpu_u8_pixels_match_cpu_float(model, kind):
         rc = e_cpu.run(ds_c, step * B, B, train=True)
         torch.testing.assert_close(float(rg.loss_sum), float(rc.loss_sum), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(e_gpu.flat.params.cpu(), e_cpu.flat.params, rtol=1e-4, atol=5e-5)
+
+
+def test_gpu_u8_weight_plane_cache_follows_the_weights():
+    """fc1's bf16 weight planes are written by the SGD step kernel (no split launch per step) and
+    stay current: after steps, after an in-place weight change (a checkpoint load), after more steps,
+    the forward equals a forward without the cache."""
+    from simple_distributed_machine_learning_amd import ops
+
+    B = 8192
+    e = _engine("mlp", DEV, "1f1b", 1)
+    s0 = e.stages[0]
+    assert s0.plane_cache is not None and e.optimizer.plane_cache is not None
+    ds = SyntheticMNIST(3 * B, seed=9, device=DEV, pixels="u8")
+    fc1 = s0.fc1
+    x = ds.x[:B].reshape(B, -1).contiguous()
+
+    def check():
+        got = ops.linear_relu_fwd_u8(x, fc1.weight, fc1.bias, s0.plane_cache, e.flat.param_epoch)
+        want = ops.linear_relu_fwd_u8(x, fc1.weight, fc1.bias)  # fresh split
+        assert torch.equal(got, want)
+
+    for step in range(2):
+        e.run(ds, step * B, B, train=True)
+    check()
+    assert s0.plane_cache.token == ops.PlaneCache.token_of(fc1.weight, e.flat.param_epoch)
+    with torch.no_grad():
+        fc1.weight.mul_(0.5)  # e.g. load_state_dict: bumps the version, the cache must re-split
+    check()
+    e.run(ds, 2 * B, B, train=True)
+    check()

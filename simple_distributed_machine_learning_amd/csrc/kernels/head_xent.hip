@@ -251,7 +251,9 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
 // then the 16 wave partials are added in LDS in wave order.
 __global__ void __launch_bounds__(1024) head_reduce_kernel(const float* __restrict__ part, int nblocks, int CK, int C,
                                                            float* __restrict__ gW, float* __restrict__ gb,
-                                                           float* __restrict__ stats, int train) {
+                                                           float* __restrict__ stats, int flags) {
+  // flags: bit 0 = training (accumulate gW/gb), bit 1 = overwrite stats instead of adding
+  const int train = flags & 1;
   __shared__ float acc[16][64];
   const int width = CK + C + 2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -278,6 +280,8 @@ __global__ void __launch_bounds__(1024) head_reduce_kernel(const float* __restri
       if (train) gW[o] += t;
     } else if (o < CK + C) {
       if (train) gb[o - CK] += t;
+    } else if (flags & 2) {
+      stats[o - CK - C] = t;
     } else {
       stats[o - CK - C] += t;
     }
@@ -555,6 +559,252 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
   }
 }
 
+
+// ==== MFMA head (K = 128, C <= 16) =============================================================
+// The whole head as fp32 MFMAs (v_mfma_f32_16x16x4_f32: fp32 operands and accumulation, the
+// same product precision as the VALU path), one wave per 16-row tile, no block-level barriers in
+// the row loop. Lane l = (r = l % 16, g = l / 16):
+//   logits^T = W x^T : A = W (lane: class r), B = x^T (lane: row r), k = 16u + 4g + e over 32 MFMAs;
+//     D leaves lane (r, g) with row r's logits of classes 4g .. 4g+3 (bias as the initial value),
+//     so softmax/NLL/argmax reduce 4 values in-lane plus two xor-shuffles (symmetric: every lane
+//     of a row ends with bitwise the same max / sum)
+//   dx^T = W^T dz^T : MFMA kk feeds each lane's own dz[row r][4g + kk] (the k index is the class,
+//     permuted so no shuffle is needed), A = W^T fragments held in registers for the whole kernel;
+//     D = dx[row r][16 t + 4g .. +3], exactly the x elements lane (r, g) loaded -> fused ReLU mask
+//   dW^T += x^T dz : needs row-indexed K and hidden-/class-indexed lanes, so the tile and its dz
+//     go through a wave-private LDS transpose (8 + 1 ds_write_b128, 36 ds_read_b32; pitches keep
+//     the reads conflict-free); the dW^T accumulators stay in registers across the wave's tiles.
+// x of the next tile is loaded while the current one is computed. Per block (4 waves) the dW, db,
+// loss and correct partials meet in LDS in wave order and leave as one slab row (head_reduce_kernel
+// sums the slabs in block order: deterministic).
+typedef float f32x4m __attribute__((ext_vector_type(4)));
+constexpr int MW = 4;          // waves per block
+constexpr int XTP = HK + 16;   // transpose pitch: (16 g + r) distinct banks for the column reads
+constexpr int DTP = 16;        // dz tile pitch
+
+__device__ __forceinline__ f32x4m mfma4(float a, float b, f32x4m c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// dx tile t of one 16-row tile: dx[row r][16 t + 4 g + v] = sum_c dz[r][c] W[c][16 t + 4 g + v]
+__device__ __forceinline__ f32x4m dx_tile(const float (&wd)[8][4], const float (&dz)[4], int t) {
+  f32x4m o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) o = mfma4(wd[t][kk], dz[kk], o);
+  return o;
+}
+
+// wd[t][kk] = W[class 4 g + kk][hidden 16 t + r] (zero for classes >= C)
+__device__ __forceinline__ void load_wd(const float* ws, int r, int g, float (&wd)[8][4]) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) wd[t][kk] = ws[(4 * g + kk) * HK + 16 * t + r];
+}
+
+__device__ __forceinline__ void load_x_tile(const float* __restrict__ x, int row, bool valid, int g, f32x4m (&xv)[8]) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    xv[u] = valid ? *reinterpret_cast<const f32x4m*>(x + (size_t)row * HK + 16 * u + 4 * g) : f32x4m{0.f, 0.f, 0.f, 0.f};
+}
+
+// (MFMAs run wave-wide: only the stores are predicated on the row)
+__device__ __forceinline__ void store_dx(float* __restrict__ dx, int row, bool valid, int g, const float (&wd)[8][4],
+                                         const float (&dz)[4], const f32x4m (&xv)[8], int mask) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    f32x4m o = dx_tile(wd, dz, t);
+    if (mask) {  // ReLU backward of the producing stage: x = relu(z) > 0 <=> z > 0
+#pragma unroll
+      for (int v = 0; v < 4; ++v) o[v] = xv[t][v] > 0.f ? o[v] : 0.f;
+    }
+    if (valid) *reinterpret_cast<f32x4m*>(dx + (size_t)row * HK + 16 * t + 4 * g) = o;
+  }
+}
+
+template <int C>
+__global__ void __launch_bounds__(64 * MW) head_mfma_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                            const float* __restrict__ bias,
+                                                            const int64_t* __restrict__ target, int M, float scale,
+                                                            float* __restrict__ part, float* __restrict__ dx,
+                                                            int tiles_per_wave, int mask_dx, float* __restrict__ dl) {
+  static_assert(C <= 16, "one 16-class MFMA tile");
+  __shared__ __attribute__((aligned(16))) float ws[16 * HK];             // W, zero-padded to 16 classes
+  __shared__ __attribute__((aligned(16))) float xt[MW][16 * XTP];        // per-wave transposes / final reduce
+  __shared__ __attribute__((aligned(16))) float dzt[MW][16 * DTP];
+  __shared__ float red[MW][2 + 16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const bool train = dx != nullptr || dl != nullptr;
+  for (int i = tid; i < 16 * HK / 4; i += 64 * MW)
+    reinterpret_cast<f32x4m*>(ws)[i] = (i / (HK / 4)) < C ? reinterpret_cast<const f32x4m*>(W)[i] : f32x4m{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  f32x4m wl[8];  // wl[u][e] = W[class r][16 u + 4 g + e]
+#pragma unroll
+  for (int u = 0; u < 8; ++u) wl[u] = *reinterpret_cast<const f32x4m*>(ws + r * HK + 16 * u + 4 * g);
+  float wd[8][4];
+  if (train) load_wd(ws, r, g, wd);
+  f32x4m bv;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) bv[v] = (4 * g + v) < C ? bias[4 * g + v] : 0.f;
+
+  f32x4m gw[8];  // dW^T tiles: gw[t][v] = dW[class r][hidden 16 t + 4 g + v]
+#pragma unroll
+  for (int t = 0; t < 8; ++t) gw[t] = f32x4m{0.f, 0.f, 0.f, 0.f};
+  float gbp = 0.f, loss_acc = 0.f, corr_acc = 0.f;
+  float* xw = xt[wave];
+  float* dw = dzt[wave];
+
+  const int tile0 = (blockIdx.x * MW + wave) * tiles_per_wave;
+  f32x4m xv[8];
+  {
+    const int row = tile0 * 16 + r;
+    load_x_tile(x, row, row < M, g, xv);
+  }
+  for (int it = 0; it < tiles_per_wave; ++it) {
+    const int row0 = (tile0 + it) * 16;
+    if (row0 >= M) break;
+    const int row = row0 + r;
+    const bool valid = row < M;
+    f32x4m xn[8];  // next tile, in flight during this one
+    {
+      const int nrow = row0 + 16 + r;
+      load_x_tile(x, nrow, it + 1 < tiles_per_wave && nrow < M, g, xn);
+    }
+    f32x4m z = bv;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) z = mfma4(wl[u][e], xv[u][e], z);
+    float zc[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) zc[v] = (4 * g + v) < C ? z[v] : -INFINITY;
+    // row max and first argmax over the 4 lane groups (symmetric combines)
+    float mx = zc[0];
+    int am = 4 * g;
+#pragma unroll
+    for (int v = 1; v < 4; ++v)
+      if (zc[v] > mx) {
+        mx = zc[v];
+        am = 4 * g + v;
+      }
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+      const float om = __shfl_xor(mx, off);
+      const int oa = __shfl_xor(am, off);
+      if (om > mx || (om == mx && oa < am)) {
+        mx = om;
+        am = oa;
+      }
+    }
+    float se = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) se += __expf(zc[v] - mx);
+    se += __shfl_xor(se, 16);
+    se += __shfl_xor(se, 32);
+    const float lse = mx + __logf(se);
+    const int tg = valid ? (int)target[row] : -1;
+    if (valid && (tg >> 2) == g) {
+      float zt = zc[0];
+#pragma unroll
+      for (int v = 1; v < 4; ++v) zt = (tg & 3) == v ? zc[v] : zt;
+      loss_acc += lse - zt;
+    }
+    if (valid && g == 0) corr_acc += (am == tg) ? 1.f : 0.f;
+    if (train) {
+      float dz[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int c = 4 * g + v;
+        dz[v] = (valid && c < C) ? scale * (__expf(zc[v] - lse) - (c == tg ? 1.f : 0.f)) : 0.f;
+      }
+      if (dl && valid) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (4 * g + v < C) dl[(size_t)row * C + 4 * g + v] = dz[v];
+      }
+      if (dx) store_dx(dx, row, valid, g, wd, dz, xv, mask_dx);
+      // dW^T += x^T dz through the wave-private transpose
+#pragma unroll
+      for (int u = 0; u < 8; ++u) *reinterpret_cast<f32x4m*>(xw + r * XTP + 16 * u + 4 * g) = xv[u];
+      *reinterpret_cast<f32x4m*>(dw + r * DTP + 4 * g) = f32x4m{dz[0], dz[1], dz[2], dz[3]};
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      float db[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        db[kk] = dw[(4 * kk + g) * DTP + r];
+        gbp += db[kk];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) gw[t] = mfma4(xw[(4 * kk + g) * XTP + 16 * t + r], db[kk], gw[t]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next tile's writes
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xv[u] = xn[u];
+  }
+
+  // ---- block partials -> slab row ----
+  float* slab = part + (size_t)blockIdx.x * (C * HK + C + 2);
+  if (train) {
+    __syncthreads();  // all waves done with their transposes: xt holds the wave partials now
+    float* mine = xt[wave];  // [C][HK] of this wave (C * HK <= 16 * XTP)
+    if (r < C) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) *reinterpret_cast<f32x4m*>(mine + r * HK + 16 * t + 4 * g) = gw[t];
+    }
+    gbp += __shfl_xor(gbp, 16);
+    gbp += __shfl_xor(gbp, 32);
+    if (g == 0) red[wave][2 + r] = gbp;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    loss_acc += __shfl_xor(loss_acc, off);
+    corr_acc += __shfl_xor(corr_acc, off);
+  }
+  if (lane == 0) {
+    red[wave][0] = loss_acc;
+    red[wave][1] = corr_acc;
+  }
+  __syncthreads();
+  if (train) {
+    for (int o = tid; o < C * HK; o += 64 * MW)
+      slab[o] = (xt[0][o] + xt[1][o]) + (xt[2][o] + xt[3][o]);
+    if (tid < C) slab[C * HK + tid] = (red[0][2 + tid] + red[1][2 + tid]) + (red[2][2 + tid] + red[3][2 + tid]);
+  }
+  if (tid == 0) {
+    slab[C * HK + C] = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
+    slab[C * HK + C + 1] = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+  }
+}
+
+// dx from the factor dl with the MFMA head's exact operations (bit-identical to its dx)
+template <int C>
+__global__ void __launch_bounds__(256) head_mfma_dx_from_dl_kernel(const float* __restrict__ dl, const float* __restrict__ W,
+                                                                   const float* __restrict__ x, float* __restrict__ dx,
+                                                                   int M, int mask) {
+  __shared__ __attribute__((aligned(16))) float ws[16 * HK];
+  for (int i = threadIdx.x; i < 16 * HK / 4; i += 256)
+    reinterpret_cast<f32x4m*>(ws)[i] = (i / (HK / 4)) < C ? reinterpret_cast<const f32x4m*>(W)[i] : f32x4m{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  float wd[8][4];
+  load_wd(ws, r, g, wd);
+  const int tiles = (M + 15) / 16;
+  for (int tile = blockIdx.x * 4 + (threadIdx.x >> 6); tile < tiles; tile += gridDim.x * 4) {
+    const int row = tile * 16 + r;
+    const bool valid = row < M;
+    f32x4m xv[8];
+    load_x_tile(x, row, valid && mask, g, xv);
+    float dz[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) dz[v] = (valid && 4 * g + v < C) ? dl[(size_t)row * C + 4 * g + v] : 0.f;
+    store_dx(dx, row, valid, g, wd, dz, xv, mask);
+  }
+}
+
 }  // namespace
 
 bool head_fused_supported(int K, int C) { return K == HK && (C == 10 || C == 2 || C == 16); }
@@ -568,7 +818,28 @@ int head_lds_blocks(int M) { return (int)std::min<int64_t>(((int64_t)M + 7) / 8,
 constexpr int SMALL_BATCH = 2048;  // <= this many rows: 16-row chunks (TPR = 16)
 int head_rows_per_chunk(int M) { return M <= SMALL_BATCH ? HTHR / 16 : HTHR / 4; }
 
+// the MFMA head (default) or the 4-lanes-per-row VALU head (SDML_HEAD=v1, A/B only)
+static bool head_use_mfma() {
+  static const bool v = [] {
+    const char* e = getenv("SDML_HEAD");
+    return !(e && e[0] == 'v' && e[1] == '1');
+  }();
+  return v;
+}
+
+// MFMA head grid: 16-row tiles, ~2 waves per SIMD, each wave several tiles (its dW partial stays
+// in registers across them)
+static int head_mfma_blocks(int M, int* tiles_per_wave) {
+  const int tiles = (M + 15) / 16;
+  int blocks = std::min(512, (tiles + MW - 1) / MW);
+  const int tpw = (tiles + blocks * MW - 1) / (blocks * MW);
+  blocks = (tiles + MW * tpw - 1) / (MW * tpw);
+  *tiles_per_wave = tpw;
+  return blocks;
+}
+
 int head_fused_blocks(int M, int* chunks_per_block) {
+  if (head_use_mfma()) return head_mfma_blocks(M, chunks_per_block);
   const int rows = head_rows_per_chunk(M);
   const int chunks = (M + rows - 1) / rows;
   static const int max_blocks = [] {  // A/B knob (SDML_HEAD_MAX_BLOCKS)
@@ -627,6 +898,19 @@ void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx,
                      hipStream_t stream) {
   if (M <= 0) return;
   if (K != HK) abort();  // host contract (checked by the binding)
+  if (head_use_mfma()) {
+    const int blocks = std::min(2048, (M + 63) / 64);
+#define DX_MFMA(CC) \
+  hipLaunchKernelGGL((head_mfma_dx_from_dl_kernel<CC>), dim3(blocks), dim3(256), 0, stream, dl, W, x, dx, M, mask ? 1 : 0)
+    switch (C) {
+      case 10: DX_MFMA(10); break;
+      case 2: DX_MFMA(2); break;
+      case 16: DX_MFMA(16); break;
+      default: abort();  // host contract: C in {2, 10, 16} (head_fused_supported)
+    }
+#undef DX_MFMA
+    return;
+  }
   int blocks = (M + 7) / 8;
   if (blocks > 2048) blocks = 2048;
   switch (C) {
@@ -639,8 +923,29 @@ void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx,
 
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K, int C,
                          float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
-                         float* workspace, bool mask_dx, hipStream_t stream, float* dl) {
-  if (M <= 0) return;
+                         float* workspace, bool mask_dx, hipStream_t stream, float* dl, bool stats_overwrite) {
+  if (M <= 0) {
+    if (stats_overwrite) (void)hipMemsetAsync(stats, 0, 2 * sizeof(float), stream);
+    return;
+  }
+  const int rflags = ((dx != nullptr || dl != nullptr) ? 1 : 0) | (stats_overwrite ? 2 : 0);
+  if (head_fused_supported(K, C) && dz_out == nullptr && workspace != nullptr && head_use_mfma()) {
+    int tpw = 0;
+    const int blocks = head_mfma_blocks(M, &tpw);
+#define HEAD_MFMA(CC)                                                                                              \
+  hipLaunchKernelGGL((head_mfma_kernel<CC>), dim3(blocks), dim3(64 * MW), 0, stream, x, W, b, target, M, scale, workspace, \
+                     dx, tpw, mask_dx ? 1 : 0, dl)
+    switch (C) {
+      case 10: HEAD_MFMA(10); break;
+      case 2: HEAD_MFMA(2); break;
+      default: HEAD_MFMA(16); break;
+    }
+#undef HEAD_MFMA
+    const int width = C * K + C + 2;
+    hipLaunchKernelGGL(head_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, stream, workspace, blocks, C * K,
+                       C, gW, gb, stats, rflags);
+    return;
+  }
   if (head_fused_supported(K, C) && dz_out == nullptr && workspace != nullptr) {
     int cpb = 0, blocks = head_fused_blocks(M, &cpb);
 #define HEAD_LAUNCH(CC, TT)                                                                             \
@@ -661,7 +966,7 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
 #undef HEAD_LAUNCH
     const int width = C * K + C + 2;
     hipLaunchKernelGGL(head_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, stream, workspace, blocks, C * K,
-                       C, gW, gb, stats, (dx != nullptr || dl != nullptr) ? 1 : 0);
+                       C, gW, gb, stats, rflags);
     return;
   }
   if (dl) abort();  // host contract: the dlogits output exists on the fused path only (head_fused_supported)
@@ -673,13 +978,15 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
                          scale, stats, dx, nullptr, mask_dx ? 1 : 0, workspace);
       const int width = C * K + C + 2;
       hipLaunchKernelGGL(head_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, stream, workspace, lblocks, C * K,
-                         C, gW, gb, stats, 1);
+                         C, gW, gb, stats, 1 | (stats_overwrite ? 2 : 0));
     } else {
+      if (stats_overwrite) (void)hipMemsetAsync(stats, 0, 2 * sizeof(float), stream);  // this variant adds
       hipLaunchKernelGGL((head_lds_kernel<10, false>), dim3(lblocks), dim3(256), lds, stream, x, W, b, target, M, K,
                          scale, stats, dx, dz_out, mask_dx ? 1 : 0, nullptr);
     }
     return;
   }
+  if (stats_overwrite) (void)hipMemsetAsync(stats, 0, 2 * sizeof(float), stream);  // the generic kernel adds
   int gblocks = (M + 3) / 4;
   if (gblocks > 1024) gblocks = 1024;
   hipLaunchKernelGGL(head_generic_kernel, dim3(gblocks), dim3(256), 0, stream, x, W, b, target, M, K, C, scale, stats,

@@ -116,7 +116,8 @@ size_t head_workspace_floats(int M, int K, int C);
 // factor of dx = dz @ W (with dx == nullptr the dx pass is skipped; gW/gb/stats as usual)
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K,
                          int C, float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
-                         float* workspace, bool mask_dx, hipStream_t stream, float* dl = nullptr);
+                         float* workspace, bool mask_dx, hipStream_t stream, float* dl = nullptr,
+                         bool stats_overwrite = false);  // stats_overwrite: stats = this call's totals
 // dx = (dl @ W) * (x > 0 if mask): the fused head's dx rebuilt bit-identically from its factor dl
 // (K == 128, C in {2, 10, 16}: head_fused_supported)
 void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx, int M, int K, int C, bool mask,

@@ -47,21 +47,27 @@ typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int FT = 512;                       // threads
-constexpr int FBM = 256;                      // rows per block
 constexpr int FBN = 128;                      // columns per block
 constexpr int FBK = 64;                       // k per K-step (FBK / 16 MFMA k-substeps)
 constexpr int NS = 2;                         // LDS stages
 constexpr int NSUB = FBK / 16;
-constexpr int A_BYTES = FBM * FBK;            // raw pixel bytes per stage
 constexpr int B_PLANE = FBN * FBK * 2;        // bytes per bf16 plane per stage
-constexpr int STAGE = A_BYTES + 3 * B_PLANE;
 constexpr int XCH = FBK / 16;                 // 16-B chunks per pixel row (2 or 4)
 constexpr int WCH = FBK / 8;                  // 16-B chunks per weight row (4 or 8)
-constexpr int GLDS_X = A_BYTES / 1024 / (FT / 64), GLDS_W = 3 * B_PLANE / 1024 / (FT / 64);
-constexpr int GLDS_PER_STAGE = GLDS_X + GLDS_W;  // DMA instructions per wave per stage
+constexpr int GLDS_W = 3 * B_PLANE / 1024 / (FT / 64);
 static_assert(FBK == 32 || FBK == 64, "swizzles below are written for 32- and 64-deep K-steps");
-static_assert(NS * STAGE <= 160 * 1024, "LDS");
-static_assert(NS * STAGE >= (FT / 64) * 64 * 64 * 4, "the epilogue transposes each wave's 64 x 64 fp32 tile in the stage buffers");
+
+// block geometry per WMT = 32-row MFMA tiles per wave (wave tile 32 WMT x 64, block 128 WMT x 128)
+template <int WMT>
+struct Geo {
+  static constexpr int BM = 4 * 32 * WMT;           // rows per block
+  static constexpr int A_BYTES = BM * FBK;          // raw pixel bytes per stage
+  static constexpr int STAGE = A_BYTES + 3 * B_PLANE;
+  static constexpr int GLDS_X = A_BYTES / 1024 / (FT / 64);
+  static constexpr int GLDS_PER_STAGE = GLDS_X + GLDS_W;  // DMA instructions per wave per stage
+  static_assert(NS * STAGE <= 160 * 1024, "LDS");
+  static_assert(NS * STAGE >= (FT / 64) * 64 * 64 * 4, "the epilogue transposes 64 x 64 fp32 per wave in the stage buffers");
+};
 
 // swizzled 16-B chunk positions: every 16-lane group of a fragment ds_read_b128 (16 rows, one
 // logical chunk) hits 16 distinct bank groups
@@ -109,11 +115,13 @@ struct FwdParams {
 // LDS images of one stage: X [256 rows][FBK bytes], W [3 planes][128 rows][FBK bf16], chunks at
 // xpos / wpos. The DMA writes 1 KiB per wave-instruction lane-linearly (lane i -> bytes 16i..), so
 // the swizzle goes on the per-lane SOURCE address.
+template <int WMT>
 __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* st, int m0, int n0, int k0, int wave,
                                            int lane) {
+  using G = Geo<WMT>;
   constexpr int XROWS = 1024 / FBK;  // pixel rows per DMA instruction
 #pragma unroll
-  for (int u = 0; u < GLDS_X; ++u) {
+  for (int u = 0; u < G::GLDS_X; ++u) {
     const int q = wave + (FT / 64) * u;
     const int row = XROWS * q + lane / XCH;
     const int pos = lane % XCH;
@@ -131,77 +139,106 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
     const int pl = q / WINST;
     const int row = WROWS * (q % WINST) + lane / WCH;
     const int ch = wpos(row, lane % WCH);
-    glds16(p.Wp + pl * plane + (size_t)(n0 + row) * p.Kp + k0 + 8 * ch, st + A_BYTES + 1024 * q);
+    glds16(p.Wp + pl * plane + (size_t)(n0 + row) * p.Kp + k0 + 8 * ch, st + G::A_BYTES + 1024 * q);
   }
 }
 
 // MODE (timing experiments only): 0 = normal, 1 = no MFMA/LDS reads (DMA pipeline alone),
+// 4 = no DMA and no barrier in the K loop, 5 = no byte widening (MFMA on raw bytes),
 // 2 = no DMA in the K loop (compute on stale LDS), 3 = no LDS reads (MFMA on register data)
-template <int MODE = 0>
+// TAIL = MFMA substeps of the last K-step (tail_substeps: only those holding k < K; chosen on the
+// host so the kernel carries one straight-line tail)
+template <int MODE, int WMT, int TAIL, bool PF>
 __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
+  using G = Geo<WMT>;
+  constexpr int STAGE = G::STAGE, GLDS_PER_STAGE = G::GLDS_PER_STAGE;
   __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STAGE];
-  const int m0 = blockIdx.x * FBM, n0 = blockIdx.y * FBN;
+  const int m0 = blockIdx.x * G::BM, n0 = blockIdx.y * FBN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave & 3, wn = wave >> 2;
   const int h = lane >> 5, r32 = lane & 31;
 
-  f32x16 acc[2][2];
+  f32x16 acc[WMT][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WMT; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
 
   // per-lane LDS read offsets (bytes, within a stage). k order inside a K-step, identical for both
   // operands: lane half h, substep s, element j <-> k = (FBK / 2) h + 8 s + j, so the lane's
   // FBK / 2 contiguous pixel bytes of a row feed all substeps of the X operand.
-  int aoff[2][XCH / 2], boff[2][NSUB];
+  // (the swizzles use row bits below 5 only, so tiles 32 rows apart differ by a constant offset)
+  int aoff[XCH / 2], boff[NSUB];
+  {
+    const int row = wm * 32 * WMT + r32;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = wm * 64 + 32 * i + r32;
-#pragma unroll
-    for (int c = 0; c < XCH / 2; ++c) aoff[i][c] = row * FBK + 16 * xpos(row, (XCH / 2) * h + c);
+    for (int c = 0; c < XCH / 2; ++c) aoff[c] = row * FBK + 16 * xpos(row, (XCH / 2) * h + c);
   }
+  {
+    const int row = wn * 64 + r32;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = wn * 64 + 32 * j + r32;
-#pragma unroll
-    for (int s = 0; s < NSUB; ++s) boff[j][s] = A_BYTES + row * (2 * FBK) + 16 * wpos(row, NSUB * h + s);
+    for (int s = 0; s < NSUB; ++s) boff[s] = G::A_BYTES + row * (2 * FBK) + 16 * wpos(row, NSUB * h + s);
   }
 
   // NS_ = substeps to run: NSUB, or fewer in the last K-step when only lane half 0's first
   // substeps hold k < K (the rest multiply zero-padded weights)
+  auto load_a = [&](const unsigned char* st, int s2, u32x4 (&ar)[WMT]) {  // 16 B = substeps 2 s2, 2 s2 + 1
+#pragma unroll
+    for (int i = 0; i < WMT; ++i) {
+      if constexpr (MODE == 3) ar[i] = u32x4{(unsigned)aoff[s2], 1u, 2u, 3u};
+      else ar[i] = *reinterpret_cast<const u32x4*>(st + aoff[s2] + 32 * FBK * i);
+    }
+  };
+  auto load_b = [&](const unsigned char* st, int s, bf16x8 (&b)[2][3]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        if constexpr (MODE == 3) b[j][pl] = bf16x8{(short)boff[s], (short)pl, (short)j, 2, 3, 4, 5, 6};
+        else b[j][pl] = *reinterpret_cast<const bf16x8*>(st + boff[s] + 64 * FBK * j + pl * B_PLANE);
+      }
+  };
+  auto compute = [&](int s, const u32x4 (&ar)[WMT], const bf16x8 (&b)[2][3]) {
+#pragma unroll
+    for (int i = 0; i < WMT; ++i) {
+      const u32x4 v = ar[i];
+      bf16x8 a;
+      if constexpr (MODE == 5) a = __builtin_bit_cast(bf16x8, v);  // timing only: no widening
+      else a = (s & 1) ? widen8(v[2], v[3]) : widen8(v[0], v[1]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc[i][j] = mfma(a, b[j][2], acc[i][j]);  // lo
+        acc[i][j] = mfma(a, b[j][1], acc[i][j]);  // mid
+        acc[i][j] = mfma(a, b[j][0], acc[i][j]);  // hi
+      }
+    }
+  };
   auto kstep = [&](const unsigned char* st, auto ns_c) {
     constexpr int NS_ = decltype(ns_c)::value;
     if constexpr (MODE == 1) return;
-    u32x4 araw[2][XCH / 2];
+    if constexpr (PF) {  // substep s+1's fragments are read ahead of substep s's MFMAs
+      u32x4 ar[2][WMT];
+      bf16x8 b[2][2][3];
+      load_a(st, 0, ar[0]);
+      load_b(st, 0, b[0]);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int c = 0; c < XCH / 2; ++c) {
-        if constexpr (MODE == 3) araw[i][c] = u32x4{(unsigned)aoff[i][c], 1u, 2u, 3u};
-        else araw[i][c] = *reinterpret_cast<const u32x4*>(st + aoff[i][c]);
+      for (int s = 0; s < NS_; ++s) {
+        if (s + 1 < NS_) {
+          if ((s + 1) % 2 == 0) load_a(st, (s + 1) >> 1, ar[((s + 1) >> 1) & 1]);
+          load_b(st, s + 1, b[(s + 1) & 1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of this substep's MFMAs
+        compute(s, ar[(s >> 1) & 1], b[s & 1]);
       }
-#pragma unroll
-    for (int s = 0; s < NS_; ++s) {
+    } else {
+      u32x4 ar[WMT];
       bf16x8 b[2][3];
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          if constexpr (MODE == 3) b[j][pl] = bf16x8{(short)boff[j][s], (short)pl, 1, 2, 3, 4, 5, 6};
-          else b[j][pl] = *reinterpret_cast<const bf16x8*>(st + boff[j][s] + pl * B_PLANE);
-        }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const u32x4 v = araw[i][s >> 1];
-        const bf16x8 a = (s & 1) ? widen8(v[2], v[3]) : widen8(v[0], v[1]);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[i][j] = mfma(a, b[j][2], acc[i][j]);  // lo
-          acc[i][j] = mfma(a, b[j][1], acc[i][j]);  // mid
-          acc[i][j] = mfma(a, b[j][0], acc[i][j]);  // hi
-        }
+      for (int s = 0; s < NS_; ++s) {
+        if (s % 2 == 0) load_a(st, s >> 1, ar);
+        load_b(st, s, b);
+        compute(s, ar, b);
       }
     }
   };
@@ -214,7 +251,7 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
   const int nk = p.Kp / FBK;
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
-    if (t < nk) issue_stage(p, smem + t * STAGE, m0, n0, t * FBK, wave, lane);
+    if (t < nk) issue_stage<WMT>(p, smem + t * STAGE, m0, n0, t * FBK, wave, lane);
   // stage t % NS landed and visible; stage (t - 1) % NS free; ISSUE: refill it with K-step t+NS-1
   // (the main loop passes a compile-time true so its body stays one basic block)
   auto sync_step = [&](int t, auto issue_c) {
@@ -229,12 +266,14 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
     } else {
       wait_vmcnt<0>();
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr (MODE != 4) {  // (MODE 4, timing only: no DMA and no barrier)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
     asm volatile("" ::: "memory");  // no LDS access moves across the barrier
-    if constexpr (MODE != 2 && decltype(issue_c)::value) {
+    if constexpr (MODE != 2 && MODE != 4 && decltype(issue_c)::value) {
       if (NS == 2 || t + NS - 1 < nk)
-        issue_stage(p, smem + ((t + NS - 1) % NS) * STAGE, m0, n0, (t + NS - 1) * FBK, wave, lane);
+        issue_stage<WMT>(p, smem + ((t + NS - 1) % NS) * STAGE, m0, n0, (t + NS - 1) * FBK, wave, lane);
     }
   };
   for (int t = 0; t + 1 < nk; ++t) {  // NS == 2: K-step t + 1 always exists here
@@ -243,40 +282,39 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
   }
   {  // last K-step: only the substeps holding k < K (lane half 0 covers the first FBK / 2 k)
     sync_step(nk - 1, std::integral_constant<bool, (NS > 2)>{});
-    const unsigned char* st = smem + ((nk - 1) % NS) * STAGE;
-    const int v = p.K - (nk - 1) * FBK;
-    if (v > FBK / 2 - 8) kstep(st, std::integral_constant<int, NSUB>{});
-    else if (NSUB == 4 && v > 16) kstep(st, std::integral_constant<int, 3>{});
-    else if (NSUB == 4 && v > 8) kstep(st, std::integral_constant<int, 2>{});
-    else kstep(st, std::integral_constant<int, 1>{});
+    kstep(smem + ((nk - 1) % NS) * STAGE, std::integral_constant<int, TAIL>{});
   }
 
   // epilogue: relu(scale * acc + bias), transposed through LDS so that every lane stores whole
-  // 16-byte row pieces (a wave's 64 x 64 fp32 tile = 16 KiB; the 8 tiles reuse the 128 KiB of
-  // stage buffers, free after the barrier that ended the last K-step)
+  // 16-byte row pieces, 64 rows of the wave tile at a time (64 x 64 fp32 = 16 KiB per wave; the 8
+  // waves' pieces reuse 128 KiB of stage buffers, free after the barrier that ended the last K-step)
   __syncthreads();
   float* T = reinterpret_cast<float*>(smem) + wave * 64 * 64;
+  float bv[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn * 64 + 32 * j + r32;
-    const float bv = p.bias ? p.bias[col] : 0.f;
+  for (int j = 0; j < 2; ++j) bv[j] = p.bias ? p.bias[n0 + wn * 64 + 32 * j + r32] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+  for (int ip = 0; ip < WMT / 2; ++ip) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous piece's reads are done
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float y = acc[i][j][r] * p.scale + bv;
-        if (p.relu) y = fmaxf(y, 0.f);
-        T[(32 * i + (r & 3) + 8 * (r >> 2) + 4 * h) * 64 + 32 * j + r32] = y;
-      }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile is in LDS (wave-private region)
-  __builtin_amdgcn_wave_barrier();
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int rr = 4 * q + (lane >> 4);
-    const int row = m0 + wm * 64 + rr;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(T + rr * 64 + 4 * (lane & 15));
-    if (row < p.M) *reinterpret_cast<f32x4*>(p.C + (size_t)row * p.ldc + n0 + wn * 64 + 4 * (lane & 15)) = v;
+      for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float y = acc[2 * ip + i2][j][r] * p.scale + bv[j];
+          if (p.relu) y = fmaxf(y, 0.f);
+          T[(32 * i2 + (r & 3) + 8 * (r >> 2) + 4 * h) * 64 + 32 * j + r32] = y;
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's piece is in LDS (wave-private region)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int rr = 4 * q + (lane >> 4);
+      const int row = m0 + wm * 32 * WMT + 64 * ip + rr;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(T + rr * 64 + 4 * (lane & 15));
+      if (row < p.M) *reinterpret_cast<f32x4*>(p.C + (size_t)row * p.ldc + n0 + wn * 64 + 4 * (lane & 15)) = v;
+    }
   }
 }
 
@@ -515,11 +553,21 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
 
 }  // namespace
 
+// substeps of the last K-step that hold k < K (lane half 0 covers its first FBK / 2 k; the rest
+// multiply zero-padded weights)
+static int tail_substeps(int K) {
+  const int v = K - ((K + FBK - 1) / FBK - 1) * FBK;
+  if (v > FBK / 2 - 8) return NSUB;
+  if (NSUB == 4 && v > 16) return 3;
+  if (NSUB == 4 && v > 8) return 2;
+  return 1;
+}
+
 int u8_fwd_kpad(int K) { return (K + FBK - 1) / FBK * FBK; }  // zero-padded W planes
 
 bool u8_fwd_supported(int M, int N, int K, int ldx, const void* X) {
   // (the epilogue stores 16-B row pieces: C 16-B aligned with ldc % 4 == 0, checked by the caller)
-  return M >= FBM && N % FBN == 0 && K >= 16 && K % 16 == 0 && ldx % 16 == 0 &&
+  return M >= 256 && N % FBN == 0 && K >= 16 && K % 16 == 0 && ldx % 16 == 0 &&
          (reinterpret_cast<uintptr_t>(X) & 15) == 0 && (int64_t)M * ldx < (int64_t(1) << 31);
 }
 
@@ -582,11 +630,48 @@ void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short*
     const char* e = getenv("SDML_U8_FWD_MODE");
     return e ? atoi(e) : 0;
   }();
-  const dim3 grid((M + FBM - 1) / FBM, N / FBN);
-  if (mode == 1) hipLaunchKernelGGL(u8_fwd_kernel<1>, grid, dim3(FT), 0, stream, p);
-  else if (mode == 2) hipLaunchKernelGGL(u8_fwd_kernel<2>, grid, dim3(FT), 0, stream, p);
-  else if (mode == 3) hipLaunchKernelGGL(u8_fwd_kernel<3>, grid, dim3(FT), 0, stream, p);
-  else hipLaunchKernelGGL(u8_fwd_kernel<0>, grid, dim3(FT), 0, stream, p);
+  static const int wmt_env = [] {
+    const char* e = getenv("SDML_U8_FWD_WMT");
+    return e ? atoi(e) : 0;
+  }();
+  // 512-row blocks (half the LDS weight traffic per MFMA) once they still cover every CU
+  const int wmt = wmt_env ? wmt_env : (M >= 256 * Geo<4>::BM ? 4 : 2);
+  const int bm = wmt == 4 ? Geo<4>::BM : Geo<2>::BM;
+  const dim3 grid((M + bm - 1) / bm, N / FBN);
+  const int tail = tail_substeps(K);
+  static const bool pf = [] {
+    const char* e = getenv("SDML_U8_FWD_PF");
+    return e && atoi(e) != 0;
+  }();
+#define FWD_LAUNCH(MD, W, T)                                                                   \
+  do {                                                                                         \
+    if (pf) hipLaunchKernelGGL((u8_fwd_kernel<MD, W, T, true>), grid, dim3(FT), 0, stream, p);  \
+    else hipLaunchKernelGGL((u8_fwd_kernel<MD, W, T, false>), grid, dim3(FT), 0, stream, p);    \
+  } while (0)
+#define FWD_TAILS(W)                  \
+  do {                                \
+    switch (tail) {                   \
+      case 1: FWD_LAUNCH(0, W, 1); break; \
+      case 2: FWD_LAUNCH(0, W, 2); break; \
+      case 3: FWD_LAUNCH(0, W, 3); break; \
+      default: FWD_LAUNCH(0, W, NSUB);    \
+    }                                 \
+  } while (0)
+#define FWD_MODE(MD)                           \
+  do {                                         \
+    if (wmt == 4) FWD_LAUNCH(MD, 4, NSUB);     \
+    else FWD_LAUNCH(MD, 2, NSUB);              \
+  } while (0)  // timing modes: full last K-step
+  if (mode == 1) FWD_MODE(1);
+  else if (mode == 2) FWD_MODE(2);
+  else if (mode == 3) FWD_MODE(3);
+  else if (mode == 4) FWD_MODE(4);
+  else if (mode == 5) FWD_MODE(5);
+  else if (wmt == 4) FWD_TAILS(4);
+  else FWD_TAILS(2);
+#undef FWD_TAILS
+#undef FWD_MODE
+#undef FWD_LAUNCH
 }
 
 }  // namespace sdml

@@ -569,11 +569,12 @@ torch::Tensor bn_nhwc_eval(torch::Tensor x, c10::optional<torch::Tensor> res, to
 }
 
 // fused head; returns (stats[2] = {loss_sum, correct}, dx or None). If `stats_acc` is given
-// the kernel accumulates into it (and returns it) instead of allocating a new one.
+// the kernel accumulates into it (and returns it) instead of allocating a new one; with
+// `stats_init` it overwrites it (stats_acc may then hold anything: no zero-fill launch).
 std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
     torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor target, c10::optional<torch::Tensor> gw,
     c10::optional<torch::Tensor> gb, double scale, bool need_dx, c10::optional<torch::Tensor> stats_acc,
-    bool mask_dx) {
+    bool mask_dx, bool stats_init) {
   check_f32_cuda(x, "x");
   check_f32_cuda(w, "w");
   check_f32_cuda(b, "b");
@@ -586,10 +587,15 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
   check_opt(gw, "gw", C * K);
   check_opt(gb, "gb", C);
   check_opt(stats_acc, "stats_acc", 2);
-  auto stats = opt_ptr(stats_acc) ? *stats_acc : torch::zeros({2}, x.options());
+  const bool fresh = !opt_ptr(stats_acc);
+  auto stats = fresh ? torch::empty({2}, x.options()) : *stats_acc;
+  const bool overwrite = fresh || stats_init;
   const bool train = opt_ptr(gw) != nullptr || opt_ptr(gb) != nullptr || need_dx;
   c10::optional<torch::Tensor> dx;
-  if (M == 0) return {stats, need_dx ? c10::optional<torch::Tensor>(torch::empty({0, K}, x.options())) : c10::nullopt};
+  if (M == 0) {
+    if (overwrite) stats.zero_();
+    return {stats, need_dx ? c10::optional<torch::Tensor>(torch::empty({0, K}, x.options())) : c10::nullopt};
+  }
   hipStream_t s = cur_stream();
   const bool fusable = sdml::head_fused_supported((int)K, (int)C) || sdml::head_lds_supported((int)M, (int)K, (int)C);
   const bool fused = fusable && (!train || (opt_ptr(gw) && opt_ptr(gb)));
@@ -599,19 +605,21 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
   if (!train) {
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
                               target.data_ptr<int64_t>(), M, K, C, (float)scale, stats.data_ptr<float>(), nullptr,
-                              nullptr, nullptr, nullptr, wsp, false, s);
+                              nullptr, nullptr, nullptr, wsp, false, s, nullptr, overwrite);
     return {stats, c10::nullopt};
   }
   auto dxt = torch::empty({M, K}, x.options());
   if (fused) {
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
                               target.data_ptr<int64_t>(), M, K, C, (float)scale, stats.data_ptr<float>(),
-                              dxt.data_ptr<float>(), opt_ptr(gw), opt_ptr(gb), nullptr, wsp, mask_dx, s);
+                              dxt.data_ptr<float>(), opt_ptr(gw), opt_ptr(gb), nullptr, wsp, mask_dx, s, nullptr,
+                              overwrite);
   } else {
     auto dz = torch::empty({M, C}, x.options());
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
                               target.data_ptr<int64_t>(), M, K, C, (float)scale, stats.data_ptr<float>(),
-                              dxt.data_ptr<float>(), nullptr, nullptr, dz.data_ptr<float>(), nullptr, mask_dx, s);
+                              dxt.data_ptr<float>(), nullptr, nullptr, dz.data_ptr<float>(), nullptr, mask_dx, s, nullptr,
+                              overwrite);
     if (opt_ptr(gw)) {
       sdml::GemmArgs g;  // gw[C,K] += dz^T x ; gb += colsum(dz)
       g.A = dz.data_ptr<float>();
@@ -640,9 +648,10 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
 
 // training head that returns its boundary gradient as the factor dl = scale * (softmax - onehot) [M, C]
 // (dx = dl @ w, rebuilt by head_dx_from_dl wherever w is held); gw/gb accumulated, loss and correct
-// count accumulated into stats_acc [2]
+// count accumulated into stats_acc [2] (overwritten with stats_init)
 torch::Tensor head_logsoftmax_nll_dl_f32(torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor target,
-                                         torch::Tensor gw, torch::Tensor gb, double scale, torch::Tensor stats_acc) {
+                                         torch::Tensor gw, torch::Tensor gb, double scale, torch::Tensor stats_acc,
+                                         bool stats_init) {
   check_f32_cuda(x, "x");
   check_f32_cuda(w, "w");
   check_f32_cuda(b, "b");
@@ -657,12 +666,15 @@ torch::Tensor head_logsoftmax_nll_dl_f32(torch::Tensor x, torch::Tensor w, torch
               "head_dl: shape mismatch");
   TORCH_CHECK(sdml::head_fused_supported((int)K, (int)C), "head_dl: needs the fused head (K == 128, C in {2, 10, 16})");
   auto dl = torch::empty({M, C}, x.options());
-  if (M == 0) return dl;
+  if (M == 0) {
+    if (stats_init) stats_acc.zero_();
+    return dl;
+  }
   auto ws = torch::empty({(int64_t)sdml::head_workspace_floats(M, K, C)}, x.options());
   sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), target.data_ptr<int64_t>(),
                             M, K, C, (float)scale, stats_acc.data_ptr<float>(), nullptr, gw.data_ptr<float>(),
                             gb.data_ptr<float>(), nullptr, ws.data_ptr<float>(), false, cur_stream(),
-                            dl.data_ptr<float>());
+                            dl.data_ptr<float>(), stats_init);
   return dl;
 }
 
@@ -1045,11 +1057,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias") = py::none(), py::arg("rowsum") = py::none());
   m.def("head_logsoftmax_nll_f32", &head_logsoftmax_nll_f32, "fused fc + log_softmax + NLL (+ backward)",
         py::arg("x"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
-        py::arg("need_dx"), py::arg("stats_acc") = py::none(), py::arg("mask_dx") = false);
+        py::arg("need_dx"), py::arg("stats_acc") = py::none(), py::arg("mask_dx") = false,
+        py::arg("stats_init") = false);
   m.def("head_logsoftmax_nll_dl_f32", &head_logsoftmax_nll_dl_f32,
         "fused head returning the boundary gradient as its factor dl = scale * (softmax - onehot)", py::arg("x"),
         py::arg("w"), py::arg("b"), py::arg("target"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
-        py::arg("stats_acc"));
+        py::arg("stats_acc"), py::arg("stats_init") = false);
   m.def("head_dx_from_dl", &head_dx_from_dl, "dx = (dl @ w) * (x > 0): boundary gradient from its factor",
         py::arg("dl"), py::arg("w"), py::arg("x"), py::arg("mask"));
   m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer (optionally also writing a "

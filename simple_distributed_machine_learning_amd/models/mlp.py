@@ -135,9 +135,17 @@ class MLPStage(PipelineStage):
                                     gy_masked=True, mask_dx=need_dx)
         return g
 
-    def head_fwd(self, x, target, ctx, train, loss_scale, stats=None):
+    # head_fwd(stats=..., stats_init=True) overwrites ``stats`` instead of adding to it (an engine
+    # then allocates its per-step [loss, correct] without a zero-fill launch)
+    supports_stats_init = True
+
+    def head_fwd(self, x, target, ctx, train, loss_scale, stats=None, stats_init: bool = False):
         if not self._fused(x):
-            return super().head_fwd(x, target, ctx, train, loss_scale)
+            loss, correct, n = super().head_fwd(x, target, ctx, train, loss_scale)
+            if stats is not None:
+                ops._put_stats(stats, loss.float(), correct.float(), stats_init)
+                return None, None, n
+            return loss, correct, n
         x = ops.pixels_to_float(x.reshape(x.shape[0], -1))
         if x.dtype != torch.float32 or not x.is_contiguous():
             x = x.float().contiguous()
@@ -151,7 +159,7 @@ class MLPStage(PipelineStage):
         loss, correct, dx = ops.linear_logsoftmax_nll(
             x, head.weight, head.bias, target,
             head.weight.grad if train else None, head.bias.grad if train else None,
-            loss_scale, need_dx, stats=stats, mask_dx=need_dx)
+            loss_scale, need_dx, stats=stats, mask_dx=need_dx, stats_init=stats_init)
         if train:
             ctx["acts"] = acts
             ctx["dx"] = dx
@@ -166,14 +174,14 @@ class MLPStage(PipelineStage):
     def supports_factored_grad(self) -> bool:
         return self.is_last and not self.is_first and len(self.layer_ids) == 1
 
-    def head_fwd_factored(self, x, target, loss_scale, stats):
+    def head_fwd_factored(self, x, target, loss_scale, stats, stats_init: bool = False):
         """Training head_fwd + head_bwd in one call: returns (dl, count); loss/correct go to stats."""
         head = self.layers()[-1]
         x = x.reshape(x.shape[0], -1)
         if x.dtype != torch.float32 or not x.is_contiguous():
             x = x.float().contiguous()
         dl = ops.linear_logsoftmax_nll_dl(x, head.weight, head.bias, target, head.weight.grad, head.bias.grad,
-                                          loss_scale, stats)
+                                          loss_scale, stats, stats_init)
         return dl, target.numel()
 
     def boundary_grad_from_factor(self, dl, x):

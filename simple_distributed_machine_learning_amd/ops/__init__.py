@@ -96,15 +96,27 @@ def linear_relu_bwd(x, y, gy, w, gw, gb, need_dx: bool, gy_masked: bool = False,
     return dx
 
 
-def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool, stats=None, mask_dx: bool = False):
+def _put_stats(stats, loss, correct, init: bool):
+    if init:
+        stats[0] = loss
+        stats[1] = correct
+    else:
+        stats[0] += loss
+        stats[1] += correct
+
+
+def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool, stats=None, mask_dx: bool = False,
+                          stats_init: bool = False):
     """Fused classifier head: z = x @ w.T + b -> log_softmax -> NLL (sum) and, when grads are
     given, the full backward (gw/gb accumulated, dx returned) scaled by ``scale``.
 
     Returns (loss_sum, correct, dx). With ``stats`` (a float32 [2] tensor) the loss sum and
-    correct count are ACCUMULATED into it in-kernel and (None, None, dx) is returned.
+    correct count are ACCUMULATED into it in-kernel (``stats_init``: overwrite it, so it needs no
+    zero-fill beforehand) and (None, None, dx) is returned.
     ``mask_dx``: dx *= (x > 0) (fused ReLU backward of the stage that produced x)."""
     if x.is_cuda:
-        st, dx = _k().head_logsoftmax_nll_f32(x, w, b, target, gw, gb, float(scale), need_dx, stats, mask_dx)
+        st, dx = _k().head_logsoftmax_nll_f32(x, w, b, target, gw, gb, float(scale), need_dx, stats, mask_dx,
+                                              bool(stats_init))
         if stats is not None:
             return None, None, dx
         return st[0], st[1], dx
@@ -112,23 +124,22 @@ def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool, 
     if dx is not None and mask_dx:
         dx = dx * (x > 0).to(dx.dtype)
     if stats is not None:
-        stats[0] += loss
-        stats[1] += correct
+        _put_stats(stats, loss, correct, stats_init)
         return None, None, dx
     return loss, correct, dx
 
 
-def linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale: float, stats):
+def linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale: float, stats, stats_init: bool = False):
     """Training head (fc -> log_softmax -> NLL, backward) whose boundary gradient is returned as its
     rank-C factor ``dl = scale * (softmax - onehot)`` [M, C] instead of ``dx = dl @ w`` [M, K]
     (:func:`head_dx_from_dlogits` rebuilds dx bit-identically wherever ``w`` is held). gw/gb are
-    accumulated; loss sum and correct count are accumulated into ``stats`` [2]."""
+    accumulated; loss sum and correct count are accumulated into ``stats`` [2] (overwritten with
+    ``stats_init``)."""
     if x.is_cuda:
-        return _k().head_logsoftmax_nll_dl_f32(x, w, b, target, gw, gb, float(scale), stats)
+        return _k().head_logsoftmax_nll_dl_f32(x, w, b, target, gw, gb, float(scale), stats, bool(stats_init))
     with torch.no_grad():
         loss, correct, dl = ref.linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale)
-    stats[0] += loss
-    stats[1] += correct
+    _put_stats(stats, loss, correct, stats_init)
     return dl
 
 

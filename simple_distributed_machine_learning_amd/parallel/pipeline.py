@@ -411,7 +411,10 @@ class PipelineEngine:
         W = len(waves)
         scale = self._loss_scale(dataset, batch_size, global_batch)
         group = mesh.pipe_group
-        stats = torch.zeros(2, device=dev, dtype=torch.float32)
+        # [loss_sum, correct]; a head that can overwrite it (supports_stats_init) initialises it on
+        # its first call of the step, so no zero-fill is launched
+        fresh = bool(getattr(s1, "supports_stats_init", False))
+        stats = (torch.empty if fresh else torch.zeros)(2, device=dev, dtype=torch.float32)
         count = 0
         if train:
             self.flat.zero_grad()
@@ -479,12 +482,15 @@ class PipelineEngine:
                 tgt = tgt.to(dev, non_blocking=True)
             if tgt.numel() > 0 and factored:
                 with tm.span("fwd", 1):
-                    g, n = s1.head_fwd_factored(recv[w], tgt, scale, stats)
+                    g, n = s1.head_fwd_factored(recv[w], tgt, scale, stats, stats_init=fresh)
+                fresh = False
                 count += n
             elif tgt.numel() > 0:
                 c1 = {}
+                kw = {"stats_init": True} if fresh else {}
                 with tm.span("fwd", 1):
-                    l, c, n = s1.head_fwd(recv[w], tgt, c1, train, scale, stats=stats)
+                    l, c, n = s1.head_fwd(recv[w], tgt, c1, train, scale, stats=stats, **kw)
+                fresh = False
                 if l is not None:
                     stats[0] += l.float()
                     stats[1] += c.float()
@@ -524,6 +530,8 @@ class PipelineEngine:
                     self.optimizer.step()
                 self.global_step += 1
             self._advance_rng()
+        if fresh:  # no head ran on this rank this step
+            stats.zero_()
         self.last_timing = tm.result()
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
 

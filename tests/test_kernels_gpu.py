@@ -443,3 +443,23 @@ def test_wgrad_bf16(T, M, N):
     want_b = gb0.double() + gy.double().sum(0)
     scale_b = gy.double().abs().sum(0) + gb0.double().abs()
     assert ((gb.double() - want_b).abs() <= 2 ** -7 * scale_b + 1e-6).all()
+
+
+@pytest.mark.parametrize("M", [60, 70001])
+def test_head_stats_init_overwrites(M):
+    """stats_init: the head overwrites a garbage-filled stats tensor with its own totals (the engine's
+    per-step stats then need no zero-fill launch), on both the dx and the factored head."""
+    Kd, C = 128, 10
+    x, w, b = rnd(M, Kd, seed=51).relu(), rnd(C, Kd, seed=52) * 0.1, rnd(C, seed=53)
+    t = torch.randint(0, C, (M,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(2))
+    want = torch.zeros(2, device=DEV)
+    ops.linear_logsoftmax_nll(x, w, b, t, torch.zeros(C, Kd, device=DEV), torch.zeros(C, device=DEV), 1.0 / M, True,
+                              stats=want, mask_dx=True)
+    got = torch.full((2,), float("nan"), device=DEV)
+    ops.linear_logsoftmax_nll(x, w, b, t, torch.zeros(C, Kd, device=DEV), torch.zeros(C, device=DEV), 1.0 / M, True,
+                              stats=got, mask_dx=True, stats_init=True)
+    assert torch.equal(got, want)
+    got2 = torch.full((2,), float("nan"), device=DEV)
+    ops.linear_logsoftmax_nll_dl(x, w, b, t, torch.zeros(C, Kd, device=DEV), torch.zeros(C, device=DEV), 1.0 / M,
+                                 got2, stats_init=True)
+    assert torch.equal(got2, want)

@@ -819,29 +819,37 @@ void gemm_u8x3_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned
     hipLaunchKernelGGL((gemm_x3_kernel<false, false, false, true, true, U8_A>), grid, dim3(NT), 0, stream, p);
 }
 
-// deterministic split-K reduction: out[i] += sum_s slab[s][i], s in order (n % 4 == 0). 64-thread
-// blocks (n = 100K floats is only ~390 blocks of float4 lanes) with 4 independent partial sums per
-// lane, so ~8 loads per lane are in flight instead of one dependent chain; the partials are
-// combined in a fixed order.
-__global__ void __launch_bounds__(64) slab_reduce_kernel(const float* __restrict__ slab, int64_t stride, int splits,
-                                                         float* __restrict__ out, int64_t n) {
-  const int64_t i = ((int64_t)blockIdx.x * 64 + threadIdx.x) * 4;
-  if (i >= n) return;
+// deterministic split-K reduction: out[i] += sum_s slab[s][i] in a fixed order (n % 4 == 0). A block
+// owns 256 outputs (64 float4 lanes) and its 4 waves take every 4th split (n = 100K floats is only
+// ~390 float4 lane groups: one wave each left the memory system underfed, 13.6 us for 51 MB at the
+// headline shape), each lane with 4 independent partial sums and 8 loads in flight; the wave
+// partials meet in LDS in wave order.
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, int64_t stride, int splits,
+                                                          float* __restrict__ out, int64_t n) {
+  __shared__ f32x4 part[4][64];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t i = ((int64_t)blockIdx.x * 64 + l) * 4;
   f32x4 a[4] = {};
-  int s = 0;
-  for (; s + 8 <= splits; s += 8) {
+  if (i < n) {
+    int s = w;  // wave w: splits w, w + 4, ...
+    for (; s + 4 * 7 < splits; s += 4 * 8) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) a[u & 3] += *reinterpret_cast<const f32x4*>(slab + (s + u) * stride + i);
+      for (int u = 0; u < 8; ++u) a[u & 3] += *reinterpret_cast<const f32x4*>(slab + (int64_t)(s + 4 * u) * stride + i);
+    }
+    for (; s < splits; s += 4) a[0] += *reinterpret_cast<const f32x4*>(slab + (int64_t)s * stride + i);
   }
-  for (; s < splits; ++s) a[0] += *reinterpret_cast<const f32x4*>(slab + s * stride + i);
-  f32x4 acc = *reinterpret_cast<const f32x4*>(out + i);
-  acc += (a[0] + a[1]) + (a[2] + a[3]);
-  *reinterpret_cast<f32x4*>(out + i) = acc;
+  part[w][l] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (w == 0 && i < n) {
+    f32x4 acc = *reinterpret_cast<const f32x4*>(out + i);
+    acc += (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
+    *reinterpret_cast<f32x4*>(out + i) = acc;
+  }
 }
 
 void slab_reduce(const float* slab, int64_t stride, int splits, float* out, int64_t n, hipStream_t stream) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n / 4 + 63) / 64)), dim3(64), 0, stream, slab, stride, splits,
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n / 4 + 63) / 64)), dim3(256), 0, stream, slab, stride, splits,
                      out, n);
 }
 

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -569,29 +570,39 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
 //     so softmax/NLL/argmax reduce 4 values in-lane plus two xor-shuffles (symmetric: every lane
 //     of a row ends with bitwise the same max / sum)
 //   dx^T = W^T dz^T : MFMA kk feeds each lane's own dz[row r][4g + kk] (the k index is the class,
-//     permuted so no shuffle is needed), A = W^T fragments held in registers for the whole kernel;
-//     D = dx[row r][16 t + 4g .. +3], exactly the x elements lane (r, g) loaded -> fused ReLU mask
+//     permuted so no shuffle is needed); D = dx[row r][16 t + 4g .. +3], exactly the x elements
+//     lane (r, g) loaded -> fused ReLU mask
 //   dW^T += x^T dz : needs row-indexed K and hidden-/class-indexed lanes, so the tile and its dz
-//     go through a wave-private LDS transpose (8 + 1 ds_write_b128, 36 ds_read_b32; pitches keep
-//     the reads conflict-free); the dW^T accumulators stay in registers across the wave's tiles.
-// x of the next tile is loaded while the current one is computed. Per block (4 waves) the dW, db,
-// loss and correct partials meet in LDS in wave order and leave as one slab row (head_reduce_kernel
-// sums the slabs in block order: deterministic).
+//     go through a wave-private LDS transpose (8 + 1 ds_write_b128, 36 ds_read_b32, swizzled so
+//     both sides are bank-conflict-free); the dW^T accumulators stay in registers across the
+//     wave's tiles.
+// Both W fragment sets live in registers for the whole kernel (2 waves per SIMD); the next tile's
+// x and targets are loaded while the current one is computed (ping-pong registers, no copies).
+// Loads are unpredicated (rows clamped); a full tile stores without per-lane predicates, so its
+// loop body is one basic block. Measured and rejected: 16-wave blocks at <= 128 VGPRs (W re-read
+// from LDS per tile, 4 waves per SIMD) - spills, and its scratch reloads wait on every outstanding
+// store (40.9 vs 38.2 us). Per block (4 waves) the dW, db, loss and correct partials meet in LDS
+// in wave order and leave as one slab row (head_reduce_kernel sums the slabs in block order).
 typedef float f32x4m __attribute__((ext_vector_type(4)));
 constexpr int MW = 4;          // waves per block
-constexpr int XTP = HK + 16;   // transpose pitch: (16 g + r) distinct banks for the column reads
+constexpr int WSP = HK + 4;    // W pitch in LDS: the per-wave fragment reads hit distinct banks
 constexpr int DTP = 16;        // dz tile pitch
+// transposes: 16-B chunk c of row rho's 16-float group sits at c ^ swz(rho), and x's 16-float
+// group q of row rho at q ^ (rho & 3): rows r and r+4 of a ds_write_b128 phase land in different
+// banks, and the column reads (rows 4kk + g, columns 16t + r) cover 64 distinct banks
+__device__ __forceinline__ int swz(int rho) { return 4 * ((rho >> 2) & 3); }
+__device__ __forceinline__ int xt_at(int rho, int q, int j) { return rho * HK + 16 * (q ^ (rho & 3)) + (j ^ swz(rho)); }
+
+__device__ __forceinline__ void stage_w16(const float* __restrict__ W, int C, float* ws, int tid, int nthr) {
+  for (int i = tid; i < 16 * HK / 4; i += nthr) {
+    const int c = i / (HK / 4), k4 = i % (HK / 4);
+    *reinterpret_cast<f32x4m*>(ws + c * WSP + 4 * k4) =
+        c < C ? reinterpret_cast<const f32x4m*>(W)[i] : f32x4m{0.f, 0.f, 0.f, 0.f};
+  }
+}
 
 __device__ __forceinline__ f32x4m mfma4(float a, float b, f32x4m c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-// dx tile t of one 16-row tile: dx[row r][16 t + 4 g + v] = sum_c dz[r][c] W[c][16 t + 4 g + v]
-__device__ __forceinline__ f32x4m dx_tile(const float (&wd)[8][4], const float (&dz)[4], int t) {
-  f32x4m o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) o = mfma4(wd[t][kk], dz[kk], o);
-  return o;
 }
 
 // wd[t][kk] = W[class 4 g + kk][hidden 16 t + r] (zero for classes >= C)
@@ -599,51 +610,50 @@ __device__ __forceinline__ void load_wd(const float* ws, int r, int g, float (&w
 #pragma unroll
   for (int t = 0; t < 8; ++t)
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) wd[t][kk] = ws[(4 * g + kk) * HK + 16 * t + r];
+    for (int kk = 0; kk < 4; ++kk) wd[t][kk] = ws[(4 * g + kk) * WSP + 16 * t + r];
 }
 
-__device__ __forceinline__ void load_x_tile(const float* __restrict__ x, int row, bool valid, int g, f32x4m (&xv)[8]) {
+// row clamped into [0, M): past-the-end rows of a partial tile read (and compute on) real data,
+// their results are never stored or counted
+__device__ __forceinline__ void load_x_tile(const float* __restrict__ x, int row, int g, f32x4m (&xv)[8]) {
 #pragma unroll
-  for (int u = 0; u < 8; ++u)
-    xv[u] = valid ? *reinterpret_cast<const f32x4m*>(x + (size_t)row * HK + 16 * u + 4 * g) : f32x4m{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < 8; ++u) xv[u] = *reinterpret_cast<const f32x4m*>(x + (size_t)row * HK + 16 * u + 4 * g);
 }
 
-// (MFMAs run wave-wide: only the stores are predicated on the row)
-__device__ __forceinline__ void store_dx(float* __restrict__ dx, int row, bool valid, int g, const float (&wd)[8][4],
-                                         const float (&dz)[4], const f32x4m (&xv)[8], int mask) {
+// dx columns 16 t + 4 g .. +3 of row r: dx = sum_c dz[r][c] W[c][.], then the ReLU mask. The head
+// and head_mfma_dx_from_dl_kernel both go through here, so their dx agree bit for bit.
+__device__ __forceinline__ f32x4m dx_t(const float (&w4)[4], const float (&dz)[4], const f32x4m& xv, int mask) {
+  f32x4m o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    f32x4m o = dx_tile(wd, dz, t);
-    if (mask) {  // ReLU backward of the producing stage: x = relu(z) > 0 <=> z > 0
+  for (int kk = 0; kk < 4; ++kk) o = mfma4(w4[kk], dz[kk], o);
+  if (mask) {  // ReLU backward of the producing stage: x = relu(z) > 0 <=> z > 0
 #pragma unroll
-      for (int v = 0; v < 4; ++v) o[v] = xv[t][v] > 0.f ? o[v] : 0.f;
-    }
-    if (valid) *reinterpret_cast<f32x4m*>(dx + (size_t)row * HK + 16 * t + 4 * g) = o;
+    for (int v = 0; v < 4; ++v) o[v] = xv[v] > 0.f ? o[v] : 0.f;
   }
+  return o;
 }
 
 template <int C>
-__global__ void __launch_bounds__(64 * MW) head_mfma_kernel(const float* __restrict__ x, const float* __restrict__ W,
+__global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __restrict__ x, const float* __restrict__ W,
                                                             const float* __restrict__ bias,
                                                             const int64_t* __restrict__ target, int M, float scale,
                                                             float* __restrict__ part, float* __restrict__ dx,
                                                             int tiles_per_wave, int mask_dx, float* __restrict__ dl) {
   static_assert(C <= 16, "one 16-class MFMA tile");
-  __shared__ __attribute__((aligned(16))) float ws[16 * HK];             // W, zero-padded to 16 classes
-  __shared__ __attribute__((aligned(16))) float xt[MW][16 * XTP];        // per-wave transposes / final reduce
+  __shared__ __attribute__((aligned(16))) float ws[16 * WSP];            // W, zero-padded to 16 classes
+  __shared__ __attribute__((aligned(16))) float xt[MW][16 * HK];         // per-wave transposes / final reduce
   __shared__ __attribute__((aligned(16))) float dzt[MW][16 * DTP];
   __shared__ float red[MW][2 + 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const bool train = dx != nullptr || dl != nullptr;
-  for (int i = tid; i < 16 * HK / 4; i += 64 * MW)
-    reinterpret_cast<f32x4m*>(ws)[i] = (i / (HK / 4)) < C ? reinterpret_cast<const f32x4m*>(W)[i] : f32x4m{0.f, 0.f, 0.f, 0.f};
+  stage_w16(W, C, ws, tid, 64 * MW);
   __syncthreads();
   f32x4m wl[8];  // wl[u][e] = W[class r][16 u + 4 g + e]
 #pragma unroll
-  for (int u = 0; u < 8; ++u) wl[u] = *reinterpret_cast<const f32x4m*>(ws + r * HK + 16 * u + 4 * g);
+  for (int u = 0; u < 8; ++u) wl[u] = *reinterpret_cast<const f32x4m*>(ws + r * WSP + 16 * u + 4 * g);
   float wd[8][4];
-  if (train) load_wd(ws, r, g, wd);
+  load_wd(ws, r, g, wd);
   f32x4m bv;
 #pragma unroll
   for (int v = 0; v < 4; ++v) bv[v] = (4 * g + v) < C ? bias[4 * g + v] : 0.f;
@@ -655,22 +665,11 @@ __global__ void __launch_bounds__(64 * MW) head_mfma_kernel(const float* __restr
   float* xw = xt[wave];
   float* dw = dzt[wave];
 
-  const int tile0 = (blockIdx.x * MW + wave) * tiles_per_wave;
-  f32x4m xv[8];
-  {
-    const int row = tile0 * 16 + r;
-    load_x_tile(x, row, row < M, g, xv);
-  }
-  for (int it = 0; it < tiles_per_wave; ++it) {
-    const int row0 = (tile0 + it) * 16;
-    if (row0 >= M) break;
+  // one 16-row tile; FULL: all 16 rows < M (wave-uniform), stores unpredicated
+  auto tile = [&](auto full_c, int row0, const f32x4m (&xv)[8], int tg_raw) {
+    constexpr bool FULL = decltype(full_c)::value;
     const int row = row0 + r;
-    const bool valid = row < M;
-    f32x4m xn[8];  // next tile, in flight during this one
-    {
-      const int nrow = row0 + 16 + r;
-      load_x_tile(x, nrow, it + 1 < tiles_per_wave && nrow < M, g, xn);
-    }
+    const bool valid = FULL || row < M;
     f32x4m z = bv;
 #pragma unroll
     for (int u = 0; u < 8; ++u)
@@ -692,10 +691,9 @@ __global__ void __launch_bounds__(64 * MW) head_mfma_kernel(const float* __restr
     for (int off = 16; off <= 32; off <<= 1) {
       const float om = __shfl_xor(mx, off);
       const int oa = __shfl_xor(am, off);
-      if (om > mx || (om == mx && oa < am)) {
-        mx = om;
-        am = oa;
-      }
+      const bool take = om > mx || (om == mx && oa < am);
+      mx = take ? om : mx;
+      am = take ? oa : am;
     }
     float se = 0.f;
 #pragma unroll
@@ -703,55 +701,78 @@ __global__ void __launch_bounds__(64 * MW) head_mfma_kernel(const float* __restr
     se += __shfl_xor(se, 16);
     se += __shfl_xor(se, 32);
     const float lse = mx + __logf(se);
-    const int tg = valid ? (int)target[row] : -1;
-    if (valid && (tg >> 2) == g) {
-      float zt = zc[0];
+    const int tg = valid ? tg_raw : -1;
+    float zt = zc[0];
 #pragma unroll
-      for (int v = 1; v < 4; ++v) zt = (tg & 3) == v ? zc[v] : zt;
-      loss_acc += lse - zt;
+    for (int v = 1; v < 4; ++v) zt = (tg & 3) == v ? zc[v] : zt;
+    loss_acc += (valid && (tg >> 2) == g) ? lse - zt : 0.f;
+    corr_acc += (valid && g == 0 && am == tg) ? 1.f : 0.f;
+    if (!train) return;
+    float dz[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int c = 4 * g + v;
+      dz[v] = (valid && c < C) ? scale * (__expf(zc[v] - lse) - (c == tg ? 1.f : 0.f)) : 0.f;
     }
-    if (valid && g == 0) corr_acc += (am == tg) ? 1.f : 0.f;
-    if (train) {
-      float dz[4];
+    if (dl) {
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int c = 4 * g + v;
-        dz[v] = (valid && c < C) ? scale * (__expf(zc[v] - lse) - (c == tg ? 1.f : 0.f)) : 0.f;
+      for (int v = 0; v < 4; ++v)
+        if (valid && 4 * g + v < C) dl[(size_t)row * C + 4 * g + v] = dz[v];
+    }
+    if (dx) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const f32x4m o = dx_t(wd[t], dz, xv[t], mask_dx);
+        if (valid) *reinterpret_cast<f32x4m*>(dx + (size_t)row * HK + 16 * t + 4 * g) = o;
       }
-      if (dl && valid) {
+    }
+    // dW^T += x^T dz through the wave-private transpose
 #pragma unroll
-        for (int v = 0; v < 4; ++v)
-          if (4 * g + v < C) dl[(size_t)row * C + 4 * g + v] = dz[v];
-      }
-      if (dx) store_dx(dx, row, valid, g, wd, dz, xv, mask_dx);
-      // dW^T += x^T dz through the wave-private transpose
+    for (int u = 0; u < 8; ++u) *reinterpret_cast<f32x4m*>(xw + xt_at(r, u, 4 * g)) = xv[u];
+    *reinterpret_cast<f32x4m*>(dw + r * DTP + ((4 * g) ^ swz(r))) = f32x4m{dz[0], dz[1], dz[2], dz[3]};
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float db[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) *reinterpret_cast<f32x4m*>(xw + r * XTP + 16 * u + 4 * g) = xv[u];
-      *reinterpret_cast<f32x4m*>(dw + r * DTP + 4 * g) = f32x4m{dz[0], dz[1], dz[2], dz[3]};
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      float db[4];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        db[kk] = dw[(4 * kk + g) * DTP + r];
-        gbp += db[kk];
-      }
-#pragma unroll
-      for (int t = 0; t < 8; ++t)
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) gw[t] = mfma4(xw[(4 * kk + g) * XTP + 16 * t + r], db[kk], gw[t]);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next tile's writes
-      __builtin_amdgcn_wave_barrier();
+    for (int kk = 0; kk < 4; ++kk) {
+      db[kk] = dw[(4 * kk + g) * DTP + (r ^ swz(4 * kk + g))];
+      gbp += db[kk];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) xv[u] = xn[u];
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) gw[t] = mfma4(xw[xt_at(4 * kk + g, t, r)], db[kk], gw[t]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next tile's writes
+    __builtin_amdgcn_wave_barrier();
+  };
+  auto run = [&](int row0, const f32x4m (&xv)[8], int tg) {
+    if (row0 + 16 <= M) tile(std::true_type{}, row0, xv, tg);
+    else tile(std::false_type{}, row0, xv, tg);
+  };
+  const int tile0 = (blockIdx.x * MW + wave) * tiles_per_wave;
+  auto fetch = [&](int row0, f32x4m (&xv)[8], int& tg) {
+    const int row = min(row0 + r, M - 1);
+    load_x_tile(x, row, g, xv);
+    tg = (int)target[row];
+  };
+  f32x4m xa[8], xb[8];
+  int ta = 0, tb = 0;
+  fetch(tile0 * 16, xa, ta);
+  for (int it = 0; it < tiles_per_wave; it += 2) {
+    const int row0 = (tile0 + it) * 16;
+    if (row0 >= M) break;
+    if (it + 1 < tiles_per_wave) fetch(row0 + 16, xb, tb);
+    run(row0, xa, ta);
+    if (it + 1 >= tiles_per_wave || row0 + 16 >= M) break;
+    if (it + 2 < tiles_per_wave) fetch(row0 + 32, xa, ta);
+    run(row0 + 16, xb, tb);
   }
 
   // ---- block partials -> slab row ----
   float* slab = part + (size_t)blockIdx.x * (C * HK + C + 2);
   if (train) {
     __syncthreads();  // all waves done with their transposes: xt holds the wave partials now
-    float* mine = xt[wave];  // [C][HK] of this wave (C * HK <= 16 * XTP)
+    float* mine = xt[wave];  // [C][HK] of this wave
     if (r < C) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) *reinterpret_cast<f32x4m*>(mine + r * HK + 16 * t + 4 * g) = gw[t];
@@ -769,9 +790,9 @@ __global__ void __launch_bounds__(64 * MW) head_mfma_kernel(const float* __restr
     red[wave][1] = corr_acc;
   }
   __syncthreads();
+  static_assert(MW == 4, "wave-partial sums below are written for 4 waves");
   if (train) {
-    for (int o = tid; o < C * HK; o += 64 * MW)
-      slab[o] = (xt[0][o] + xt[1][o]) + (xt[2][o] + xt[3][o]);
+    for (int o = tid; o < C * HK; o += 64 * MW) slab[o] = (xt[0][o] + xt[1][o]) + (xt[2][o] + xt[3][o]);
     if (tid < C) slab[C * HK + tid] = (red[0][2 + tid] + red[1][2 + tid]) + (red[2][2 + tid] + red[3][2 + tid]);
   }
   if (tid == 0) {
@@ -785,9 +806,8 @@ template <int C>
 __global__ void __launch_bounds__(256) head_mfma_dx_from_dl_kernel(const float* __restrict__ dl, const float* __restrict__ W,
                                                                    const float* __restrict__ x, float* __restrict__ dx,
                                                                    int M, int mask) {
-  __shared__ __attribute__((aligned(16))) float ws[16 * HK];
-  for (int i = threadIdx.x; i < 16 * HK / 4; i += 256)
-    reinterpret_cast<f32x4m*>(ws)[i] = (i / (HK / 4)) < C ? reinterpret_cast<const f32x4m*>(W)[i] : f32x4m{0.f, 0.f, 0.f, 0.f};
+  __shared__ __attribute__((aligned(16))) float ws[16 * WSP];
+  stage_w16(W, C, ws, threadIdx.x, 256);
   __syncthreads();
   const int lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   float wd[8][4];
@@ -796,12 +816,17 @@ __global__ void __launch_bounds__(256) head_mfma_dx_from_dl_kernel(const float* 
   for (int tile = blockIdx.x * 4 + (threadIdx.x >> 6); tile < tiles; tile += gridDim.x * 4) {
     const int row = tile * 16 + r;
     const bool valid = row < M;
+    const int crow = min(row, M - 1);
     f32x4m xv[8];
-    load_x_tile(x, row, valid && mask, g, xv);
+    if (mask) load_x_tile(x, crow, g, xv);
     float dz[4];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) dz[v] = (valid && 4 * g + v < C) ? dl[(size_t)row * C + 4 * g + v] : 0.f;
-    store_dx(dx, row, valid, g, wd, dz, xv, mask);
+    for (int v = 0; v < 4; ++v) dz[v] = (valid && 4 * g + v < C) ? dl[(size_t)crow * C + 4 * g + v] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const f32x4m o = dx_t(wd[t], dz, xv[t], mask);
+      if (valid) *reinterpret_cast<f32x4m*>(dx + (size_t)row * HK + 16 * t + 4 * g) = o;
+    }
   }
 }
 

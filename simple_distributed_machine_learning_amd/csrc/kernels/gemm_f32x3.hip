@@ -896,9 +896,7 @@ void gemm_u8x3_wgrad(const float* gz, const unsigned char* X, int M, int N, int 
   else
     hipLaunchKernelGGL((gemm_x3_kernel<true, true, false, true, false, U8_B, true, false>), grid, dim3(NT), 0, stream, p);
   if (slab) {
-    const int64_t n = (int64_t)N * K;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((n / 4 + 63) / 64)), dim3(64), 0, stream, slab,
-                       p.slab_stride, (int)grid.y, gw, n);
+    slab_reduce(slab, p.slab_stride, (int)grid.y, gw, (int64_t)N * K, stream);
   }
 }
 

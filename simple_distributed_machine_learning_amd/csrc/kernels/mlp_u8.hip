@@ -352,7 +352,10 @@ __global__ void __launch_bounds__(256) split3_pad_kernel(const float* __restrict
 // the 16x16x32 form holds 8 of 16, which left a first version of this kernel issue-bound), the 784
 // columns padded to 25 tiles of 32. 8 waves, all computing: wave 0 owns columns 0..127, waves
 // 1..7 three 32-column tiles each, every wave all 64 hidden (2 x {4,3} tiles, <= 8 f32x16
-// accumulators). All 8 waves stage the next 32-row K-step (dz float4 -> 3 bf16 planes, 16 pixel
+// accumulators; measured and rejected: the 25th tile split by hidden half over waves 0 and 1 so no
+// SIMD carries more than 13 of the 50 tile pairs, with or without double-buffered staging
+// registers - 91-93 vs 85 us, the extra fragment reads and register pressure (spills) outweigh the
+// balance). All 8 waves stage the next 32-row K-step (dz float4 -> 3 bf16 planes, 16 pixel
 // bytes -> 16 bf16) into the other LDS buffer while the current one is consumed. Both operands
 // are k-major in memory (the reduction index is the row), so fragments come from [row][col] LDS
 // images through ds_read_b64_tr_b16 (a 16-lane group reads 4 rows x 16 columns, transposed).

@@ -97,6 +97,11 @@ bool u8_wgrad_supported(int M, int N, int K, int ldx, const void* X, const void*
 int64_t u8_wgrad_slab_floats(int M, int N);
 void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
               hipStream_t stream);
+// the same with the factored boundary gradient: dz = (dl @ w2) * (h > 0) (dl [M][C], w2 [C][N],
+// h [M][N]) expanded in the kernel's staging, bit-identical to head_dx_from_dl + u8_wgrad
+bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const void* h, int C);
+void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const unsigned char* X, int M, int N, int ldx,
+                 float* slab, float* gwb, float scale, hipStream_t stream);
 // out[i] += sum_s slab[s * stride + i] in split order (n % 4 == 0, 16-B aligned)
 void slab_reduce(const float* slab, int64_t stride, int splits, float* out, int64_t n, hipStream_t stream);
 

@@ -144,7 +144,7 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
 }
 
 // MODE (timing experiments only): 0 = normal, 1 = no MFMA/LDS reads (DMA pipeline alone),
-// 4 = no DMA and no barrier in the K loop, 5 = no byte widening (MFMA on raw bytes),
+// 4 = no DMA and no barrier in the K loop, 5 = no byte widening (MFMA on raw bytes), 6 = no output stores,
 // 2 = no DMA in the K loop (compute on stale LDS), 3 = no LDS reads (MFMA on register data)
 // TAIL = MFMA substeps of the last K-step (tail_substeps: only those holding k < K; chosen on the
 // host so the kernel carries one straight-line tail)
@@ -313,7 +313,11 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
       const int rr = 4 * q + (lane >> 4);
       const int row = m0 + wm * 32 * WMT + 64 * ip + rr;
       const f32x4 v = *reinterpret_cast<const f32x4*>(T + rr * 64 + 4 * (lane & 15));
-      if (row < p.M) *reinterpret_cast<f32x4*>(p.C + (size_t)row * p.ldc + n0 + wn * 64 + 4 * (lane & 15)) = v;
+      if constexpr (MODE == 6) {  // timing only: no global stores (keep the values alive)
+        if (v[0] == 12345.f && row < 0) *reinterpret_cast<f32x4*>(p.C) = v;
+      } else if (row < p.M) {
+        *reinterpret_cast<f32x4*>(p.C + (size_t)row * p.ldc + n0 + wn * 64 + 4 * (lane & 15)) = v;
+      }
     }
   }
 }
@@ -405,8 +409,29 @@ struct WgradParams {
   int M, N, ldx;
   int rows_per_split;        // multiple of GBK
   float scale;
+  // FD (factored boundary gradient): dz = (dl @ W2) * (h > 0) rebuilt in the staging
+  const float* dl;           // [M][C]
+  const float* w2;           // [C][N]
+  const float* h;            // [M][N]
+  int C;                     // <= 16
 };
 
+// dx tile of head_xent.hip's MFMA head (dx_t / head_mfma_dx_from_dl_kernel), reproduced operation
+// for operation: lane (r, g) of a 16-row tile gets dz[row r][16 t + 4 g + v] =
+// sum over the 4 MFMAs kk of W2[4 g + kk][16 t + r] * dl[row r][4 g + kk], then the ReLU mask of h.
+__device__ __forceinline__ f32x4 fd_dz(const float (&w4)[4], const float (&d4)[4], const f32x4& hv) {
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) o = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[kk], d4[kk], o, 0, 0, 0);
+#pragma unroll
+  for (int v = 0; v < 4; ++v) o[v] = hv[v] > 0.f ? o[v] : 0.f;
+  return o;
+}
+
+// FD = false: dz read as [M][N]. FD = true: the factored boundary gradient (rotate placement)
+// is expanded here instead of by a separate kernel that writes dz to memory and reads it back -
+// with head_xent.hip's exact operations, so gW / gb are bit-identical to the unfused pair.
+template <bool FD>
 __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) u16 smem[2 * GBUF_U16];
   const int t = threadIdx.x, lane = t & 63;
@@ -420,8 +445,22 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   // t + 512 u (chunk c: row c / 50, columns 16 (c % 50); c % 50 == 49 is the zero pad). The 4th
   // round covers chunks 1536..1599: threads >= 64 repeat chunk 1599 (same bytes to the same
   // place), so staging has no lane-dependent branches ----
-  const float* dzp = p.dz + (size_t)(r0 + (t >> 4)) * p.N + n0 + 4 * (t & 15);
+  // FD: wave w builds the 16 x 16 dz tile (rows 16 (w >> 2) .., hidden 16 (w & 3) ..) of each
+  // K-step with 4 fp32 MFMAs, lane (r, g) holding row r, hidden 4 g .. 4 g + 3 of it
+  const int fr = 16 * (wave >> 2) + (lane & 15), fc = 16 * (wave & 3) + 4 * (lane >> 4);
+  const int drow = FD ? fr : (t >> 4), dcol = FD ? fc : 4 * (t & 15);  // this thread's dz float4
+  const float* dzp = (FD ? p.h : p.dz) + (size_t)(r0 + drow) * p.N + n0 + dcol;
   const size_t dz_step = (size_t)GBK * p.N;
+  float w4[4] = {0.f, 0.f, 0.f, 0.f};  // FD: W2[4 g + kk][n0 + 16 (w & 3) + r]
+  const float* dlp = nullptr;
+  if constexpr (FD) {
+    const int g = lane >> 4;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      if (4 * g + kk < p.C) w4[kk] = p.w2[(size_t)(4 * g + kk) * p.N + n0 + 16 * (wave & 3) + (lane & 15)];
+    dlp = p.dl + (size_t)(r0 + fr) * p.C;
+  }
+  float d4[4] = {0.f, 0.f, 0.f, 0.f};
   constexpr int XU = (GXCH + GT - 1) / GT;  // 4 rounds
   const unsigned char* xp[XU];
   int xoff[XU];
@@ -439,12 +478,19 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   u32x4 xv[XU];
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
   auto gload = [&](int kt) {
-    dv = *reinterpret_cast<const f32x4*>(dzp + kt * dz_step);
+    dv = *reinterpret_cast<const f32x4*>(dzp + kt * dz_step);  // FD: h (the ReLU mask source)
+    if constexpr (FD) {
+      const int g = lane >> 4;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        d4[kk] = 4 * g + kk < p.C ? dlp[(size_t)kt * GBK * p.C + 4 * g + kk] : 0.f;
+    }
 #pragma unroll
     for (int u = 0; u < XU; ++u) xv[u] = *reinterpret_cast<const u32x4*>(xp[u] + kt * x_step);
   };
   auto stage = [&](int buf) {
     u16* B = smem + buf * GBUF_U16;
+    if constexpr (FD) dv = fd_dz(w4, d4, dv);
     bsum += dv;
     u16x4 hi, mi, lo;
 #pragma unroll
@@ -457,7 +503,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
       mi[e] = m;
       lo[e] = bf16_bits(r1 - bf16_val(m));
     }
-    const int doff = GX_U16 + (t >> 4) * GDP + 4 * (t & 15);
+    const int doff = GX_U16 + drow * GDP + dcol;
     *reinterpret_cast<u16x4*>(B + doff) = hi;
     *reinterpret_cast<u16x4*>(B + doff + GD_U16) = mi;
     *reinterpret_cast<u16x4*>(B + doff + 2 * GD_U16) = lo;
@@ -547,9 +593,12 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   float* red = reinterpret_cast<float*>(smem);
   *reinterpret_cast<f32x4*>(red + 4 * t) = bsum;
   __syncthreads();
-  if (t < GHN) {
+  if (t < GHN) {  // rows rr = 0 .. 31 in order, whichever thread staged them
     float sacc = 0.f;
-    for (int rr = 0; rr < GBK; ++rr) sacc += red[4 * (rr * 16 + (t >> 2)) + (t & 3)];
+    for (int rr = 0; rr < GBK; ++rr) {
+      const int owner = FD ? 64 * ((rr >> 4) * 4 + (t >> 4)) + 16 * ((t >> 2) & 3) + (rr & 15) : rr * 16 + (t >> 2);
+      sacc += red[4 * owner + (t & 3)];
+    }
     out[(size_t)p.N * GKC + n0 + t] = sacc;
   }
 }
@@ -595,7 +644,7 @@ int64_t u8_wgrad_slab_floats(int M, int N) {
 
 void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
               hipStream_t stream) {
-  WgradParams p;
+  WgradParams p{};
   p.dz = dz;
   p.X = X;
   p.slab = slab;
@@ -605,7 +654,30 @@ void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, fl
   p.scale = scale;
   const int splits = u8_wgrad_splits(M, N);
   p.rows_per_split = ((M + splits - 1) / splits + GBK - 1) / GBK * GBK;
-  hipLaunchKernelGGL(u8_wgrad_kernel, dim3(N / GHN, splits), dim3(GT), 0, stream, p);
+  hipLaunchKernelGGL(u8_wgrad_kernel<false>, dim3(N / GHN, splits), dim3(GT), 0, stream, p);
+  slab_reduce(slab, (int64_t)N * GKC + N, splits, gwb, (int64_t)N * GKC + N, stream);
+}
+
+bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const void* h, int C) {
+  return u8_wgrad_supported(M, N, K, ldx, X, h) && C >= 1 && C <= 16;
+}
+
+void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const unsigned char* X, int M, int N, int ldx,
+                 float* slab, float* gwb, float scale, hipStream_t stream) {
+  WgradParams p{};
+  p.X = X;
+  p.slab = slab;
+  p.M = M;
+  p.N = N;
+  p.ldx = ldx;
+  p.scale = scale;
+  p.dl = dl;
+  p.w2 = w2;
+  p.h = h;
+  p.C = C;
+  const int splits = u8_wgrad_splits(M, N);
+  p.rows_per_split = ((M + splits - 1) / splits + GBK - 1) / GBK * GBK;
+  hipLaunchKernelGGL(u8_wgrad_kernel<true>, dim3(N / GHN, splits), dim3(GT), 0, stream, p);
   slab_reduce(slab, (int64_t)N * GKC + N, splits, gwb, (int64_t)N * GKC + N, stream);
 }
 
@@ -670,6 +742,7 @@ void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short*
   else if (mode == 3) FWD_MODE(3);
   else if (mode == 4) FWD_MODE(4);
   else if (mode == 5) FWD_MODE(5);
+  else if (mode == 6) FWD_MODE(6);
   else if (wmt == 4) FWD_TAILS(4);
   else FWD_TAILS(2);
 #undef FWD_TAILS

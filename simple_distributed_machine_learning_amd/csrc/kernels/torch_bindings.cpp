@@ -693,6 +693,35 @@ torch::Tensor head_dx_from_dl(torch::Tensor dl, torch::Tensor w, torch::Tensor x
   return dx;
 }
 
+// first layer's weight gradient from the FACTORED boundary gradient: gw += scale * dz^T x_u8,
+// gb += colsum(dz) with dz = (dl @ w2) * (h > 0) - expanded inside mlp_u8.hip's wgrad kernel when
+// it applies (bit-identical to head_dx_from_dl followed by linear_wgrad_u8), else those two
+void linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, torch::Tensor h, torch::Tensor gw,
+                        torch::Tensor gb, double scale) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
+              "linear_wgrad_u8_dl: x must be a contiguous 2-D uint8 ROCm tensor");
+  check_f32_cuda(dl, "dl");
+  check_f32_cuda(w2, "w2");
+  check_f32_cuda(h, "h");
+  check_f32_cuda(gw, "gw");
+  check_f32_cuda(gb, "gb");
+  const int64_t M = x.size(0), K = x.size(1), N = h.size(1), C = dl.size(1);
+  TORCH_CHECK(dl.dim() == 2 && dl.size(0) == M && w2.dim() == 2 && w2.size(0) == C && w2.size(1) == N &&
+                  h.dim() == 2 && h.size(0) == M && gw.size(0) == N && gw.size(1) == K && gb.numel() == N,
+              "linear_wgrad_u8_dl: shape mismatch");
+  const bool gb_follows = gw.is_contiguous() && gb.is_contiguous() && gb.data_ptr<float>() == gw.data_ptr<float>() + N * K;
+  if (gb_follows && sdml::head_fused_supported((int)N, (int)C) &&
+      sdml::u8_wgrad_dl_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr(), h.data_ptr(), (int)C)) {
+    auto ws = torch::empty({sdml::u8_wgrad_slab_floats((int)M, (int)N)}, gw.options());
+    sdml::u8_wgrad_dl(dl.data_ptr<float>(), w2.data_ptr<float>(), h.data_ptr<float>(), (int)C, x.data_ptr<uint8_t>(),
+                      (int)M, (int)N, (int)K, ws.data_ptr<float>(), gw.data_ptr<float>(), (float)scale, cur_stream());
+    return;
+  }
+  torch::Tensor dz = sdml::head_fused_supported((int)N, (int)C) ? head_dx_from_dl(dl, w2, h, true)
+                                                                  : at::matmul(dl, w2).mul_((h > 0).to(h.scalar_type()));
+  linear_wgrad_u8(x, dz, gw, gb, scale);
+}
+
 void sgd_momentum_(torch::Tensor p, torch::Tensor g, torch::Tensor buf, double lr, double momentum, double dampening,
                    double wd, bool nesterov, bool first, bool zero_grad, c10::optional<torch::Tensor> planes,
                    int64_t plane_offset, int64_t plane_rows, int64_t plane_k) {
@@ -1063,6 +1092,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "fused head returning the boundary gradient as its factor dl = scale * (softmax - onehot)", py::arg("x"),
         py::arg("w"), py::arg("b"), py::arg("target"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
         py::arg("stats_acc"), py::arg("stats_init") = false);
+  m.def("linear_wgrad_u8_dl", &linear_wgrad_u8_dl,
+        "gw += scale * dz^T x_u8, gb += colsum(dz), dz = (dl @ w2) * (h > 0) (factored boundary gradient)",
+        py::arg("x"), py::arg("dl"), py::arg("w2"), py::arg("h"), py::arg("gw"), py::arg("gb"), py::arg("scale"));
   m.def("head_dx_from_dl", &head_dx_from_dl, "dx = (dl @ w) * (x > 0): boundary gradient from its factor",
         py::arg("dl"), py::arg("w"), py::arg("x"), py::arg("mask"));
   m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer (optionally also writing a "

@@ -190,6 +190,23 @@ class MLPStage(PipelineStage):
         head = self.layers()[-1]
         return ops.head_dx_from_dlogits(dl, head.weight.detach(), x.reshape(x.shape[0], -1), mask=True)
 
+    def factor_weight(self):
+        """The weight the factored boundary gradient is expanded with (dx = dl @ W)."""
+        return self.layers()[-1].weight.detach()
+
+    def bwd_from_factor(self, dl, w2, ctx) -> bool:
+        """Stage-0 backward fed by the factored boundary gradient dl (dz = (dl @ w2) * (h > 0), h this
+        stage's output). A single uint8-fed layer takes it straight into its weight-gradient kernel
+        (dz never materialised); returns False (nothing done) for other stages."""
+        acts = ctx.get("acts")
+        layers = self.layers()
+        if acts is None or len(layers) != 1 or acts[0].dtype != torch.uint8:
+            return False
+        ctx.pop("acts")
+        lin = layers[0]
+        ops.linear_wgrad_u8_dl(acts[0], dl, w2, acts[1], lin.weight.grad, lin.bias.grad)
+        return True
+
     def head_bwd(self, ctx):
         if "dx" not in ctx:
             return super().head_bwd(ctx)

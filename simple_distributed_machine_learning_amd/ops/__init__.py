@@ -78,6 +78,20 @@ def linear_wgrad_u8(x: torch.Tensor, gz: torch.Tensor, gw: torch.Tensor, gb: Opt
         gb += gz.sum(0)
 
 
+def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb) -> None:
+    """First-layer weight gradient from the FACTORED boundary gradient: with dz = (dl @ w2) * (h > 0)
+    (dl [M, C] the head's factor, w2 [C, N] the head weight, h [M, N] this layer's ReLU output),
+    gw += dz.T @ ToTensor(x), gb += sum(dz). On ROCm dz is expanded inside the weight-gradient kernel
+    (never written to memory), bit-identical to :func:`head_dx_from_dlogits` + :func:`linear_wgrad_u8`."""
+    if x.is_cuda:
+        _k().linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, PIXEL_SCALE)
+        return
+    with torch.no_grad():
+        dz = (dl @ w2) * (h > 0).to(dl.dtype)
+        gw += dz.t() @ pixels_to_float(x)
+        gb += dz.sum(0)
+
+
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
     if x.is_cuda:
         return _k().linear_fwd_f32(x, w, b, False)

@@ -454,12 +454,20 @@ class PipelineEngine:
             recv[w] = buf
         back, bwork = [None] * W, [None] * W
         bgroup = mesh.pipe_group_bwd or group
+        # stage 0 expands the factor itself when it can (MLP first layer on uint8 pixels)
+        fuse0 = factored and hasattr(s0, "bwd_from_factor") and hasattr(s1, "factor_weight")
 
         def stage0_bwd(w):
             if bwork[w] is not None:
                 with tm.span("recv_wait", 1):
                     bwork[w].wait()
             gz = back[w]
+            if factored and fuse0:  # the factor goes straight into stage 0's weight-gradient kernel
+                with tm.span("bwd", 0):
+                    done = s0.bwd_from_factor(gz, s1.factor_weight(), ctx0[w])
+                if done:
+                    hkeep[w] = back[w] = None
+                    return
             if factored:
                 with tm.span("bwd", 1):
                     gz = s1.boundary_grad_from_factor(gz, hkeep[w])

@@ -12,13 +12,13 @@ def train_worker(rank, world, model, kind, M, pp, steps, B, seed=3, kw=None, tp=
     kw = kw or {}
     mesh = init_mesh(pp=pp, schedule_kind=kind, rank=rank, world_size=world, device=torch.device("cpu"),
                      backend="gloo", timeout_s=120, tp=tp)
-    spec = get_model_spec(model, kw.get("stages"), **{k: v for k, v in kw.items() if k != "stages"})
+    spec = get_model_spec(model, kw.get("stages"), **{k: v for k, v in kw.items() if k not in ("stages", "pixels")})
     eng = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=seed)
     S = eng.data_shards
     if spec.input_kind == "tokens":
         ds = SyntheticTokens(B * S * steps, kw.get("seq_len", 16), 97, seed=7)
     else:
-        ds = SyntheticMNIST(B * S * steps, seed=7)
+        ds = SyntheticMNIST(B * S * steps, seed=7, pixels=kw.get("pixels", "f32"))
     losses = []
     for step in range(steps):
         res = eng.run(ds, eng.local_start(step * B * S, B), B, train=True, global_batch=B * S)

@@ -218,3 +218,31 @@ def test_u8_small_batch_falls_back_to_fp32():
     K.linear_wgrad_u8(x8, gz, gw, gb, 1.0 / 255.0)
     torch.testing.assert_close(gw, gz.t() @ (x8.float() / 255.0), rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(gb, gz.sum(0), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M", [4096, 65536, 131072])
+@pytest.mark.parametrize("C", [10, 2])
+def test_wgrad_u8_from_factor_bit_identical(M, C):
+    """The factored boundary gradient expanded inside the weight-gradient kernel (rotate placement,
+    R > 1) gives bit for bit the gw/gb of head_dx_from_dl followed by linear_wgrad_u8."""
+    N, Kd = 128, 784
+    x8 = pixels(M, Kd, 21)
+    h = rnd(M, N, seed=22).relu()
+    dl = rnd(M, C, seed=23) * 1e-3
+    w2 = rnd(C, N, seed=24) * 0.1
+    g0 = rnd(N * Kd + N, seed=25)
+
+    def flat():
+        buf = g0.clone()
+        return buf, buf[:N * Kd].view(N, Kd), buf[N * Kd:]
+
+    b1, gw1, gb1 = flat()
+    ops.linear_wgrad_u8_dl(x8, dl, w2, h, gw1, gb1)
+    b2, gw2, gb2 = flat()
+    ops.linear_wgrad_u8(x8, ops.head_dx_from_dlogits(dl, w2, h, mask=True), gw2, gb2)
+    assert torch.equal(b1, b2)
+    # and against the fp64 reference
+    dz = (dl.double() @ w2.double()) * (h > 0).double()
+    want = g0.double()[:N * Kd].view(N, Kd) + dz.t() @ (x8.double() / 255.0)
+    torch.testing.assert_close(gw1.double(), want, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(gb1.double(), g0.double()[N * Kd:] + dz.sum(0), rtol=1e-4, atol=1e-6)

@@ -95,13 +95,20 @@ def test_gpt2_tiny_two_ranks():
     _compare(res, ref, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("a2a", [True, False, "whole_grad"])
+@pytest.mark.parametrize("a2a", [True, False, "whole_grad", "u8"])
 @pytest.mark.parametrize("world,M", [(2, 2), (2, 4), (4, 16), (4, 8)])
 def test_mlp_rotate_matches_single_process(world, M, a2a, monkeypatch):
     """a2a=True: all-to-all boundary with the factored gradient (the head's dlogits cross, the owner
     rebuilds the boundary gradient); "whole_grad": all-to-all sending the full boundary gradient;
-    False: per-peer p2p transfers."""
+    False: per-peer p2p transfers; "u8": uint8 pixels, the factor going straight into stage 0's
+    weight gradient (MLPStage.bwd_from_factor)."""
     B, steps = 24, 2
+    if a2a == "u8":
+        kw = {"pixels": "u8"}
+        res = run_ranks(train_worker, world, "mlp", "rotate", M, world, steps, B, 3, kw)
+        ref = _single("mlp", M, steps, world * B, "rotate", kw)
+        _compare(res, ref, rtol=1e-4, atol=1e-5)
+        return
     if not a2a:
         monkeypatch.setenv("SDML_ROTATE_P2P", "1")
     if a2a == "whole_grad":

@@ -581,7 +581,8 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
 // Loads are unpredicated (rows clamped); a full tile stores without per-lane predicates, so its
 // loop body is one basic block. Measured and rejected: 16-wave blocks at <= 128 VGPRs (W re-read
 // from LDS per tile, 4 waves per SIMD) - spills, and its scratch reloads wait on every outstanding
-// store (40.9 vs 38.2 us). Per block (4 waves) the dW, db, loss and correct partials meet in LDS
+// store (40.9 vs 38.2 us); 3 waves per SIMD (W re-read from LDS per tile, no register prefetch,
+// 158 VGPRs, 512-1024 blocks) - 38.6 vs 36.5 us. Per block (4 waves) the dW, db, loss and correct partials meet in LDS
 // in wave order and leave as one slab row (head_reduce_kernel sums the slabs in block order).
 typedef float f32x4m __attribute__((ext_vector_type(4)));
 constexpr int MW = 4;          // waves per block

@@ -218,7 +218,8 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
     constexpr int NS_ = decltype(ns_c)::value;
     if constexpr (MODE == 1) return;
     // (reading substep s+1's fragments ahead of substep s's MFMAs, pinned with sched_barrier,
-    // measured no faster at either geometry: 87.2 vs 87.5 us)
+    // measured no faster at either geometry: 87.2 vs 87.5 us; neither did s_setprio 1 around
+    // each substep's MFMAs: 92.3-92.9 vs 91.5-93.4 us)
     u32x4 ar[WMT];
     bf16x8 b[2][3];
 #pragma unroll

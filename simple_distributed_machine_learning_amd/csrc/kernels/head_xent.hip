@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
 }
 
 // sum the per-block slabs: out[o] += sum_b part[b][o]   (fixed order -> deterministic).
-// Block = 64 outputs x 16 waves; wave w sums slabs b = w, w+16, ... with 8 loads in flight,
+// Block = 64 outputs x 16 waves; wave w sums slabs b = w, w+16, ... with 16 loads in flight,
 // then the 16 wave partials are added in LDS in wave order.
 __global__ void __launch_bounds__(1024) head_reduce_kernel(const float* __restrict__ part, int nblocks, int CK, int C,
                                                            float* __restrict__ gW, float* __restrict__ gb,
@@ -260,14 +260,14 @@ __global__ void __launch_bounds__(1024) head_reduce_kernel(const float* __restri
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int o = blockIdx.x * 64 + lane;
   float s = 0.f;
-  if (o < width) {
-    float v[8];
+  if (o < width) {  // 16 loads in flight per lane (512 slabs: two round trips per wave)
+    float v[16];
     int b = w;
-    for (; b + 16 * 7 < nblocks; b += 16 * 8) {
+    for (; b + 16 * 15 < nblocks; b += 16 * 16) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(b + 16 * u) * width + o];
+      for (int u = 0; u < 16; ++u) v[u] = part[(size_t)(b + 16 * u) * width + o];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
+      for (int u = 0; u < 16; ++u) s += v[u];
     }
     for (; b < nblocks; b += 16) s += part[(size_t)b * width + o];
   }

@@ -6,6 +6,7 @@
 
 #include "kernels.h"
 #include "synth_hash.h"
+#include "u8_planes.h"
 
 namespace sdml {
 namespace {
@@ -16,16 +17,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // /root/reference/simple_distributed.py:100-104): d = g + wd*p; buf = first ? d :
 // momentum*buf + (1-dampening)*d; d = nesterov ? d + momentum*buf : buf; p -= lr*d.
 // One launch for all parameters of all stages a rank owns; 16 B per lane per stream.
-// split of an updated fp32 value into bf16 planes hi + mid + lo (exact; same arithmetic as
-// gemm_f32x3.hip / mlp_u8.hip's split kernels)
-__device__ __forceinline__ unsigned short sgd_bf16_bits(float f) {
-  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));
-}
-__device__ __forceinline__ float sgd_bf16_val(unsigned short b) { return __uint_as_float(((unsigned)b) << 16); }
 typedef unsigned short u16x4s __attribute__((ext_vector_type(4)));
 
 // pl: optional weight-plane cache written from the UPDATED weights (the uint8 first layer's
-// forward reads W as zero-padded bf16 planes [3][rows][Kp]; writing them here saves a separate
+// forward reads W as zero-padded fp16 planes [2][rows][Kp], u8_planes.h - the same function as
+// mlp_u8.hip's split kernel, so both writers agree bit for bit; writing them here saves a separate
 // split launch per step). pl.n4 float4 of the flat buffer starting at float4 pl.off4 form a
 // [rows][K] matrix, K % 4 == 0.
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ g,
@@ -54,18 +50,17 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
     if (pl.planes && i >= pl.off4 && i < pl.off4 + pl.n4) {
       const int64_t e = 4 * (i - pl.off4);
       const int64_t r = e / pl.K, k = e % pl.K;
-      u16x4s h, m, l;
+      u16x4s h, l;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        h[j] = sgd_bf16_bits(nv[j]);
-        const float r1 = nv[j] - sgd_bf16_val(h[j]);
-        m[j] = sgd_bf16_bits(r1);
-        l[j] = sgd_bf16_bits(r1 - sgd_bf16_val(m[j]));
+        unsigned short hj, lj;
+        u8_fwd_planes_of(nv[j], hj, lj);
+        h[j] = hj;
+        l[j] = lj;
       }
       unsigned short* q = pl.planes + r * pl.Kp + k;
       *reinterpret_cast<u16x4s*>(q) = h;
-      *reinterpret_cast<u16x4s*>(q + pl.plane_stride) = m;
-      *reinterpret_cast<u16x4s*>(q + 2 * pl.plane_stride) = l;
+      *reinterpret_cast<u16x4s*>(q + pl.plane_stride) = l;
     }
   }
 }

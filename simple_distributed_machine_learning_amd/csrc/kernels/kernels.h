@@ -83,10 +83,12 @@ int u8x3_wgrad_splits(int M, int N, int K);
 void gemm_u8x3_wgrad(const float* gz, const unsigned char* X, int M, int N, int K, int ldx, float* gw, float* gb,
                      float scale, float* slab, hipStream_t stream);
 // mlp_u8.hip: LDS-DMA pipelined forward of the uint8-fed first layer (N % 128 == 0). W is given as
-// zero-padded bf16 planes [3][N][Kp], Kp = u8_fwd_kpad(K), written by split3_pad.
+// zero-padded fp16 planes [2][N][Kp] of W * 2^8 (u8_planes.h), Kp = u8_fwd_kpad(K), written by
+// split_planes_pad or by the fused SGD step.
+constexpr int kU8FwdPlanes = 2;
 int u8_fwd_kpad(int K);
 bool u8_fwd_supported(int M, int N, int K, int ldx, const void* X);
-void split3_pad(const float* w, unsigned short* out, int N, int K, int Kp, hipStream_t stream);
+void split_planes_pad(const float* w, unsigned short* out, int N, int K, int Kp, hipStream_t stream);
 void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
             const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream);
 // mlp_u8.hip: weight + bias gradient of the uint8-fed first layer (K = 784 pixel columns, N % 64 == 0,
@@ -132,7 +134,7 @@ void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx,
 // zero_grad: also writes g = 0 after reading it (fuses the next step's zero_grad)
 // optional bf16 weight-plane cache written from the updated weights (see sgd_kernel)
 struct SgdPlanes {
-  unsigned short* planes = nullptr;  // [3][rows][Kp], plane_stride = rows * Kp
+  unsigned short* planes = nullptr;  // [2][rows][Kp] (u8_planes.h), plane_stride = rows * Kp
   int64_t off4 = 0, n4 = 0;          // float4 range of the flat buffer holding the [rows][K] weight
   int64_t K = 0, Kp = 0, plane_stride = 0;
 };

@@ -1,22 +1,23 @@
 // First layer of the MNIST MLPs fed straight from uint8 pixels (BASELINE configs 1-3): the
 // forward GEMM y = relu(scale * X W^T + b) with X [M][K] uint8 and W [N][K] fp32.
 //
-// Numerics (same contract as gemm_f32x3.hip's uint8 path): a pixel byte is exact in one bf16, W is
-// split exactly into three bf16 planes (hi + mid + lo = W), so every product is 3 exact bf16 MFMA
-// products accumulated in fp32; ToTensor's 1/255 is applied in the epilogue. The reference does the
-// same layer in fp32 on the CPU (/root/reference/simple_distributed.py:63, :75 for its fc layers,
-// :87-88 for ToTensor).
+// Numerics: a pixel byte is exact in one fp16, and W is held as two fp16 planes of W * 2^8
+// (u8_planes.h: hi + lo is W to within one fp32 ulp), so every product is 2 exact
+// fp16 MFMA products accumulated in fp32; ToTensor's 1/255 and the 2^-8 are applied in the
+// epilogue. (Round 1 and the first half of round 2 used 3 exact bf16 planes, 3 MFMAs per product;
+// the pair of fp16 planes carries the same 24 bits in 2.) The reference does the same layer in fp32
+// on the CPU (/root/reference/simple_distributed.py:63, :75 for its fc layers, :87-88 for ToTensor).
 //
 // Accumulation: straight MFMA chains (no per-K-step fp32 partials). tools/probes/mfma_acc_probe.hip
 // measured v_mfma_f32_32x32x16_bf16's accumulation on gfx950 as unbiased and more accurate than a
 // k-ordered fp32 fmaf chain (K = 4096: 2.7e-7 vs 7.6e-7 mean relative error, bias 4e-9).
 //
-// Structure (gfx950, wave64): 512 threads = 8 waves as 4 (rows) x 2 (cols), block tile 256 x 128,
-// wave tile 64 x 64 = 2 x 2 tiles of v_mfma_f32_32x32x16_bf16, K-step 64 (4 MFMA k-substeps).
+// Structure (gfx950, wave64): 512 threads = 8 waves as 4 (rows) x 2 (cols), block tile 128 WMT x 128,
+// wave tile 32 WMT x 64 = WMT x 2 tiles of v_mfma_f32_32x32x16_f16, K-step 64 (4 MFMA k-substeps).
 // Both operands reach LDS by LDS-DMA (global_load_lds_dwordx4, 16 B per lane, no VGPR staging)
-// into a ring of NS stages (2 x 64 KiB; the DMA of K-step t+1 flies under K-step t's 48 MFMAs per
-// wave). Measured alternatives: 32-deep K-steps in a 4-stage ring (3 K-steps in flight), slower
-// (102.6 vs 93.8 us at the headline shape: half the MFMAs per barrier); weight fragments of
+// into a ring of NS stages (the DMA of K-step t+1 flies under K-step t's MFMAs). Measured
+// alternatives (on the 3-plane bf16 form): 32-deep K-steps in a 4-stage ring (3 K-steps in flight),
+// slower (102.6 vs 93.8 us at the headline shape: half the MFMAs per barrier); weight fragments of
 // substep s+1 pinned ahead of substep s's MFMAs with sched_barrier (register double buffer),
 // 2-3 % slower than the compiler's own placement; 1024-thread blocks of 512 rows (W staged once
 // per CU instead of twice) do not fit 4 waves per SIMD: 128 VGPRs with ~400 spilled.
@@ -24,8 +25,9 @@
 // lane-linearly) so the fragment ds_read_b128s are conflict-free; k order inside a K-step is
 // permuted identically for both operands (lane half h, substep s, element j <-> k = 32h + 8s + j),
 // so one 32-byte read per row tile feeds all four substeps of the pixel operand. Bytes are widened to
-// bf16 in registers. The epilogue goes through LDS so every lane stores whole 16-byte row pieces.
-// W is pre-split into zero-padded planes [3][N][Kp] (Kp = K rounded up to FBK), so the K tail needs
+// fp16 in registers (a byte permute builds 1024 + b, one packed subtract removes the 1024). The
+// epilogue goes through LDS so every lane stores whole 16-byte row pieces.
+// W is pre-split into zero-padded planes [2][N][Kp] (Kp = K rounded up to FBK), so the K tail needs
 // no masking: past-the-end pixel bytes (clamped, finite) meet zero weights.
 // Measured at 131072 x 784 -> 128 (tools/bench_u8.py): see README "uint8 pixels".
 #include <hip/hip_runtime.h>
@@ -35,6 +37,7 @@
 #include <type_traits>
 
 #include "kernels.h"
+#include "u8_planes.h"
 
 namespace sdml {
 namespace {
@@ -45,16 +48,19 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int FT = 512;                       // threads
 constexpr int FBN = 128;                      // columns per block
 constexpr int FBK = 64;                       // k per K-step (FBK / 16 MFMA k-substeps)
 constexpr int NS = 2;                         // LDS stages
 constexpr int NSUB = FBK / 16;
-constexpr int B_PLANE = FBN * FBK * 2;        // bytes per bf16 plane per stage
+constexpr int NPL = kU8FwdPlanes;            // fp16 weight planes
+constexpr int B_PLANE = FBN * FBK * 2;        // bytes per fp16 plane per stage
 constexpr int XCH = FBK / 16;                 // 16-B chunks per pixel row (2 or 4)
 constexpr int WCH = FBK / 8;                  // 16-B chunks per weight row (4 or 8)
-constexpr int GLDS_W = 3 * B_PLANE / 1024 / (FT / 64);
+constexpr int GLDS_W = NPL * B_PLANE / 1024 / (FT / 64);
 static_assert(FBK == 32 || FBK == 64, "swizzles below are written for 32- and 64-deep K-steps");
 
 // block geometry per WMT = 32-row MFMA tiles per wave (wave tile 32 WMT x 64, block 128 WMT x 128)
@@ -62,11 +68,12 @@ template <int WMT>
 struct Geo {
   static constexpr int BM = 4 * 32 * WMT;           // rows per block
   static constexpr int A_BYTES = BM * FBK;          // raw pixel bytes per stage
-  static constexpr int STAGE = A_BYTES + 3 * B_PLANE;
+  static constexpr int STAGE = A_BYTES + NPL * B_PLANE;
   static constexpr int GLDS_X = A_BYTES / 1024 / (FT / 64);
   static constexpr int GLDS_PER_STAGE = GLDS_X + GLDS_W;  // DMA instructions per wave per stage
-  static_assert(NS * STAGE <= 160 * 1024, "LDS");
-  static_assert(NS * STAGE >= (FT / 64) * 64 * 64 * 4, "the epilogue transposes 64 x 64 fp32 per wave in the stage buffers");
+  // the epilogue transposes 64 x 64 fp32 per wave through the (then free) stage buffers
+  static constexpr int SMEM = std::max(NS * STAGE, (FT / 64) * 64 * 64 * 4);
+  static_assert(SMEM <= 160 * 1024, "LDS");
 };
 
 // swizzled 16-B chunk positions: every 16-lane group of a fragment ds_read_b128 (16 rows, one
@@ -87,6 +94,18 @@ __device__ __forceinline__ void wait_vmcnt() {
 __device__ __forceinline__ u16 bf16_bits(float f) { return __builtin_bit_cast(u16, static_cast<__bf16>(f)); }
 __device__ __forceinline__ float bf16_val(u16 b) { return __uint_as_float(((unsigned)b) << 16); }
 
+// 8 bytes -> 8 fp16 (exact): a byte permute puts b under the exponent of 1024 (fp16 0x6400 | b ==
+// 1024 + b), one packed subtract per pair removes the 1024
+__device__ __forceinline__ f16x2 h2_of(unsigned v, unsigned sel) {
+  const unsigned t = __builtin_amdgcn_perm(0x64646464u, v, sel);
+  return __builtin_bit_cast(f16x2, t) - f16x2{(_Float16)1024.f, (_Float16)1024.f};
+}
+__device__ __forceinline__ f16x8 widen8h(unsigned lo, unsigned hi) {
+  const f16x2 a = h2_of(lo, 0x04010400u), b = h2_of(lo, 0x04030402u);
+  const f16x2 c = h2_of(hi, 0x04010400u), d = h2_of(hi, 0x04030402u);
+  return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
 // 8 bytes -> 8 bf16 (exact: (float)b has its significant bits in the upper half)
 __device__ __forceinline__ bf16x8 widen8(unsigned lo, unsigned hi) {
   bf16x8 r;
@@ -101,10 +120,13 @@ __device__ __forceinline__ bf16x8 widen8(unsigned lo, unsigned hi) {
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
 
 struct FwdParams {
   const unsigned char* X;
-  const u16* Wp;  // [3][N][Kp]
+  const u16* Wp;  // [NPL][N][Kp] fp16 bits
   const float* bias;
   float* C;
   int M, N, K, Kp, ldx, ldc;
@@ -112,7 +134,7 @@ struct FwdParams {
   int relu;
 };
 
-// LDS images of one stage: X [256 rows][FBK bytes], W [3 planes][128 rows][FBK bf16], chunks at
+// LDS images of one stage: X [BM rows][FBK bytes], W [NPL planes][128 rows][FBK fp16], chunks at
 // xpos / wpos. The DMA writes 1 KiB per wave-instruction lane-linearly (lane i -> bytes 16i..), so
 // the swizzle goes on the per-lane SOURCE address.
 template <int WMT>
@@ -152,7 +174,7 @@ template <int MODE, int WMT, int TAIL>
 __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
   using G = Geo<WMT>;
   constexpr int STAGE = G::STAGE, GLDS_PER_STAGE = G::GLDS_PER_STAGE;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STAGE];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[G::SMEM];
   const int m0 = blockIdx.x * G::BM, n0 = blockIdx.y * FBN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -190,28 +212,26 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
       else ar[i] = *reinterpret_cast<const u32x4*>(st + aoff[s2] + 32 * FBK * i);
     }
   };
-  auto load_b = [&](const unsigned char* st, int s, bf16x8 (&b)[2][3]) {
+  auto load_b = [&](const unsigned char* st, int s, f16x8 (&b)[2][NPL]) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
-        if constexpr (MODE == 3) b[j][pl] = bf16x8{(short)boff[s], (short)pl, (short)j, 2, 3, 4, 5, 6};
-        else b[j][pl] = *reinterpret_cast<const bf16x8*>(st + boff[s] + 64 * FBK * j + pl * B_PLANE);
+      for (int pl = 0; pl < NPL; ++pl) {
+        if constexpr (MODE == 3) b[j][pl] = __builtin_bit_cast(f16x8, bf16x8{(short)boff[s], (short)pl, (short)j, 2, 3, 4, 5, 6});
+        else b[j][pl] = *reinterpret_cast<const f16x8*>(st + boff[s] + 64 * FBK * j + pl * B_PLANE);
       }
   };
-  auto compute = [&](int s, const u32x4 (&ar)[WMT], const bf16x8 (&b)[2][3]) {
+  auto compute = [&](int s, const u32x4 (&ar)[WMT], const f16x8 (&b)[2][NPL]) {
 #pragma unroll
     for (int i = 0; i < WMT; ++i) {
       const u32x4 v = ar[i];
-      bf16x8 a;
-      if constexpr (MODE == 5) a = __builtin_bit_cast(bf16x8, v);  // timing only: no widening
-      else a = (s & 1) ? widen8(v[2], v[3]) : widen8(v[0], v[1]);
+      f16x8 a;
+      if constexpr (MODE == 5) a = __builtin_bit_cast(f16x8, v);  // timing only: no widening
+      else a = (s & 1) ? widen8h(v[2], v[3]) : widen8h(v[0], v[1]);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        acc[i][j] = mfma(a, b[j][2], acc[i][j]);  // lo
-        acc[i][j] = mfma(a, b[j][1], acc[i][j]);  // mid
-        acc[i][j] = mfma(a, b[j][0], acc[i][j]);  // hi
-      }
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int pl = NPL - 1; pl >= 0; --pl) acc[i][j] = mfma(a, b[j][pl], acc[i][j]);  // lo first
     }
   };
   auto kstep = [&](const unsigned char* st, auto ns_c) {
@@ -221,7 +241,7 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
     // measured no faster at either geometry: 87.2 vs 87.5 us; neither did s_setprio 1 around
     // each substep's MFMAs: 92.3-92.9 vs 91.5-93.4 us)
     u32x4 ar[WMT];
-    bf16x8 b[2][3];
+    f16x8 b[2][NPL];
 #pragma unroll
     for (int s = 0; s < NS_; ++s) {
       if (s % 2 == 0) load_a(st, s >> 1, ar);
@@ -309,21 +329,18 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
   }
 }
 
-// fp32 [N][K] -> three zero-padded bf16 planes [3][N][Kp] (hi + mid + lo == w exactly)
-__global__ void __launch_bounds__(256) split3_pad_kernel(const float* __restrict__ w, u16* __restrict__ out, int N,
-                                                         int K, int Kp) {
+// fp32 [N][K] -> zero-padded fp16 planes [NPL][N][Kp] of W * 2^8 (u8_planes.h)
+__global__ void __launch_bounds__(256) split_planes_pad_kernel(const float* __restrict__ w, u16* __restrict__ out,
+                                                               int N, int K, int Kp) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // element of the padded [N][Kp]
   const int64_t n = (int64_t)N * Kp;
   if (i >= n) return;
   const int r = (int)(i / Kp), k = (int)(i % Kp);
   const float x = k < K ? w[(size_t)r * K + k] : 0.f;
-  const u16 hi = bf16_bits(x);
-  const float r1 = x - bf16_val(hi);
-  const u16 mi = bf16_bits(r1);
-  const u16 lo = bf16_bits(r1 - bf16_val(mi));
+  u16 hi, lo;
+  u8_fwd_planes_of(x, hi, lo);
   out[i] = hi;
-  out[n + i] = mi;
-  out[2 * n + i] = lo;
+  out[n + i] = lo;
 }
 
 
@@ -668,9 +685,9 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const 
   slab_reduce(slab, (int64_t)N * GKC + N, splits, gwb, (int64_t)N * GKC + N, stream);
 }
 
-void split3_pad(const float* w, unsigned short* out, int N, int K, int Kp, hipStream_t stream) {
+void split_planes_pad(const float* w, unsigned short* out, int N, int K, int Kp, hipStream_t stream) {
   const int64_t n = (int64_t)N * Kp;
-  hipLaunchKernelGGL(split3_pad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, w, out, N, K, Kp);
+  hipLaunchKernelGGL(split_planes_pad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, w, out, N, K, Kp);
 }
 
 void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
@@ -686,7 +703,7 @@ void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short*
   p.Kp = Kp;
   p.ldx = ldx;
   p.ldc = ldc;
-  p.scale = scale;
+  p.scale = scale / kU8FwdWScale;  // the planes hold W * 2^8 (exact power of two)
   p.relu = relu ? 1 : 0;
   static const int mode = [] {
     const char* e = getenv("SDML_U8_FWD_MODE");

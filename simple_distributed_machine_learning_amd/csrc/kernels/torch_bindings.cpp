@@ -190,16 +190,17 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
   }();
   if (!legacy && sdml::u8_fwd_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr())) {
     const int Kp = sdml::u8_fwd_kpad((int)K);
-    // planes: a caller-owned cache [3][N][Kp] (zero padding columns; kept current by the fused SGD
-    // step, ops/optim.py); planes_valid == false -> (re)split into it
+    // planes: a caller-owned cache [2][N][Kp] (fp16 bits of W * 2^8, zero padding columns; kept
+    // current by the fused SGD step, ops/optim.py); planes_valid == false -> (re)split into it
     const bool cache = planes.has_value() && planes->defined();
     if (cache)
       TORCH_CHECK(planes->is_cuda() && planes->scalar_type() == torch::kInt16 && planes->is_contiguous() &&
-                      planes->dim() == 3 && planes->size(0) == 3 && planes->size(1) == N && planes->size(2) == Kp,
-                  "linear_fwd_u8: planes must be a [3][N][u8_fwd_kpad(K)] int16 device tensor");
-    auto wp = cache ? *planes : torch::empty({3, N, Kp}, w.options().dtype(torch::kInt16));
+                      planes->dim() == 3 && planes->size(0) == sdml::kU8FwdPlanes && planes->size(1) == N &&
+                      planes->size(2) == Kp,
+                  "linear_fwd_u8: planes must be a [u8_fwd_planes()][N][u8_fwd_kpad(K)] int16 device tensor");
+    auto wp = cache ? *planes : torch::empty({sdml::kU8FwdPlanes, N, Kp}, w.options().dtype(torch::kInt16));
     auto* wpp = reinterpret_cast<unsigned short*>(wp.data_ptr<int16_t>());
-    if (!cache || !planes_valid) sdml::split3_pad(w.data_ptr<float>(), wpp, (int)N, (int)K, Kp, cur_stream());
+    if (!cache || !planes_valid) sdml::split_planes_pad(w.data_ptr<float>(), wpp, (int)N, (int)K, Kp, cur_stream());
     sdml::u8_fwd(x.data_ptr<uint8_t>(), (int)M, (int)K, (int)K, wpp, (int)N, Kp, opt_ptr(b), y.data_ptr<float>(),
                  (int)N, relu, (float)scale, cur_stream());
     return y;
@@ -733,10 +734,10 @@ void sgd_momentum_(torch::Tensor p, torch::Tensor g, torch::Tensor buf, double l
   TORCH_CHECK(p.numel() % 4 == 0, "sgd: flat buffers must be padded to a multiple of 4");
   sdml::SgdPlanes pl;
   if (planes.has_value() && planes->defined()) {
-    // planes [3][rows][Kp] int16 (bf16 bits) of the [rows][K] weight at float offset plane_offset
+    // planes [2][rows][Kp] int16 (fp16 bits, u8_planes.h) of the [rows][K] weight at float offset plane_offset
     TORCH_CHECK(planes->is_cuda() && planes->scalar_type() == torch::kInt16 && planes->is_contiguous() &&
-                    planes->dim() == 3 && planes->size(0) == 3 && planes->size(1) == plane_rows,
-                "sgd planes: [3][rows][Kp] int16 device tensor");
+                    planes->dim() == 3 && planes->size(0) == sdml::kU8FwdPlanes && planes->size(1) == plane_rows,
+                "sgd planes: [u8_fwd_planes()][rows][Kp] int16 device tensor");
     const int64_t Kp = planes->size(2);
     TORCH_CHECK(plane_k % 4 == 0 && plane_offset % 4 == 0 && Kp % 4 == 0 && Kp >= plane_k &&
                     plane_offset + plane_rows * plane_k <= p.numel(),
@@ -1074,6 +1075,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("planes_valid") = false);
   m.def("u8_fwd_kpad", [](int64_t K) { return (int64_t)sdml::u8_fwd_kpad((int)K); },
         "padded K of the uint8 forward's weight planes");
+  m.def("u8_fwd_planes", []() { return (int64_t)sdml::kU8FwdPlanes; }, "number of the uint8 forward's weight planes");
   m.def("linear_wgrad_u8", &linear_wgrad_u8, "gw += scale * gz^T x_u8, gb += colsum(gz)", py::arg("x"), py::arg("gz"),
         py::arg("gw"), py::arg("gb"), py::arg("scale"));
   m.def("linear_fwd_f32", &linear_fwd_f32, "relu?(x @ w.T + b) on fp32 MFMA", py::arg("x"), py::arg("w"),
@@ -1098,7 +1100,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("head_dx_from_dl", &head_dx_from_dl, "dx = (dl @ w) * (x > 0): boundary gradient from its factor",
         py::arg("dl"), py::arg("w"), py::arg("x"), py::arg("mask"));
   m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer (optionally also writing a "
-        "weight's bf16 plane cache)", py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"), py::arg("momentum"),
+        "weight's fp16 plane cache)", py::arg("p"), py::arg("g"), py::arg("buf"), py::arg("lr"), py::arg("momentum"),
         py::arg("dampening"), py::arg("wd"), py::arg("nesterov"), py::arg("first"), py::arg("zero_grad") = false,
         py::arg("planes") = py::none(), py::arg("plane_offset") = 0, py::arg("plane_rows") = 0,
         py::arg("plane_k") = 0);

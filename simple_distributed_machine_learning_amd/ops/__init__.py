@@ -35,7 +35,8 @@ def pixels_to_float(x: torch.Tensor) -> torch.Tensor:
 
 
 class PlaneCache:
-    """The uint8 first layer's weight as zero-padded bf16 planes [3][N][Kp] (hi + mid + lo == W).
+    """The uint8 first layer's weight as zero-padded fp16 planes [2][N][Kp] of W * 2^8 (hi + lo
+    is W to within one fp32 ulp, csrc/kernels/u8_planes.h).
 
     The forward needs them every step; instead of a split launch per step, the fused SGD step
     writes them from the weights it has just updated (ops/optim.py, ``add_plane_cache``). The
@@ -45,7 +46,8 @@ class PlaneCache:
 
     def __init__(self, weight: torch.Tensor):
         n, k = weight.shape
-        self.planes = torch.zeros(3, n, int(_k().u8_fwd_kpad(k)), dtype=torch.int16, device=weight.device)
+        self.planes = torch.zeros(int(_k().u8_fwd_planes()), n, int(_k().u8_fwd_kpad(k)), dtype=torch.int16,
+                                  device=weight.device)
         self.token = None
 
     @staticmethod
@@ -56,7 +58,7 @@ class PlaneCache:
 def linear_relu_fwd_u8(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, cache: Optional[PlaneCache] = None,
                        epoch: int = 0) -> torch.Tensor:
     """relu(ToTensor(x) @ w.T + b) for uint8 pixels x [M,K]: on ROCm the /255 is folded into the
-    GEMM's epilogue and each pixel byte is an exact single bf16 plane (3 MFMAs/product). With a
+    GEMM's epilogue and each pixel byte is exact in fp16 against two fp16 weight planes (2 MFMAs/product). With a
     ``cache`` (and the flat buffer's ``epoch``) the weight planes are reused when still current."""
     if x.is_cuda:
         if cache is None:
@@ -170,7 +172,7 @@ def head_dx_from_dlogits(dl, w, x, mask: bool = True):
 def sgd_momentum_(p, g, buf, lr: float, momentum: float, dampening: float = 0.0, weight_decay: float = 0.0,
                   nesterov: bool = False, first: bool = False, zero_grad: bool = False, planes=None):
     """In-place SGD step; with ``zero_grad`` the kernel also clears ``g`` after reading it.
-    ``planes = (cache_tensor, offset, rows, K)``: also write that weight's bf16 plane cache from the
+    ``planes = (cache_tensor, offset, rows, K)``: also write that weight's fp16 plane cache from the
     updated values (ROCm only)."""
     if p.is_cuda:
         if planes is not None:

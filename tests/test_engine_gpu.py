@@ -115,7 +115,7 @@ def test_gpu_u8_pixels_match_cpu_float(model, kind):
 
 
 def test_gpu_u8_weight_plane_cache_follows_the_weights():
-    """fc1's bf16 weight planes are written by the SGD step kernel (no split launch per step) and
+    """fc1's fp16 weight planes are written by the SGD step kernel (no split launch per step) and
     stay current: after steps, after an in-place weight change (a checkpoint load), after more steps,
     the forward equals a forward without the cache."""
     from simple_distributed_machine_learning_amd import ops

@@ -208,6 +208,41 @@ def test_linear_wgrad_u8_matches_fp32_reference(M, N, Kd, flat):
     torch.testing.assert_close(gb.double(), want_b, rtol=1e-5, atol=1e-3)
 
 
+def test_u8_fwd_weight_planes_reproduce_w():
+    """The forward's two fp16 planes of W * 2^8 (csrc/kernels/u8_planes.h) give W back to within one
+    fp32 ulp for |W| >= 2^-9, to 2^-33 absolute below that, and overflow to inf (loudly) past
+    the fp16 range; the SGD step's plane writer agrees with the split kernel."""
+    N, Kd = 128, 784
+    g = torch.Generator(device="cpu").manual_seed(31)
+    mag = torch.pow(2.0, torch.empty(N, Kd).uniform_(-20, 7, generator=g))
+    sign = torch.where(torch.rand(N, Kd, generator=g) < 0.5, -1.0, 1.0)
+    w = (mag * sign).float().to(DEV)
+    w[0, :4] = torch.tensor([0.0, -0.0, 255.0, -2.0 ** -9])
+    kp = int(K.u8_fwd_kpad(Kd))
+    planes = torch.zeros(int(K.u8_fwd_planes()), N, kp, dtype=torch.int16, device=DEV)
+    x8 = pixels(4096, Kd, 32)
+    K.linear_fwd_u8(x8, w, torch.zeros(N, device=DEV), False, 1.0 / 255.0, planes, False)
+    hi = planes[0].view(torch.float16).double()
+    lo = planes[1].view(torch.float16).double()
+    assert torch.all(hi[:, Kd:] == 0) and torch.all(lo[:, Kd:] == 0)
+    back = (hi + lo)[:, :Kd] / 256.0
+    wd = w.double()
+    err = (back - wd).abs()
+    big = wd.abs() >= 2.0 ** -9
+    assert torch.all(err[big] <= 2.0 ** -23 * wd.abs()[big])
+    assert torch.all(err[~big] <= 2.0 ** -33)
+    # the fused SGD step writes the same bits (lr = 0: the weights stay as they are)
+    flat = torch.cat([w.reshape(-1), torch.zeros(4, device=DEV)])
+    grad, buf = torch.zeros_like(flat), torch.zeros_like(flat)
+    planes2 = torch.zeros_like(planes)
+    ops.sgd_momentum_(flat, grad, buf, 0.0, 0.5, first=True, planes=(planes2, 0, N, Kd))
+    assert torch.equal(planes.view(torch.float16), planes2.view(torch.float16))  # (the sign of a zero lo may differ)
+    # past the fp16 range: a non-finite output, not a silent error
+    w[3, 5] = 300.0
+    y = K.linear_fwd_u8(x8, w, torch.zeros(N, device=DEV), False, 1.0 / 255.0)
+    assert not torch.isfinite(y[:, 3]).all()
+
+
 def test_u8_small_batch_falls_back_to_fp32():
     x8 = pixels(60, 784, 11)
     w, b = rnd(128, 784, seed=12, lo=-0.05, hi=0.05), rnd(128, seed=13)

@@ -639,12 +639,18 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
                                                             const float* __restrict__ bias,
                                                             const int64_t* __restrict__ target, int M, float scale,
                                                             float* __restrict__ part, float* __restrict__ dx,
-                                                            int tiles_per_wave, int mask_dx, float* __restrict__ dl) {
+                                                            int tiles_per_wave, int mask_dx, float* __restrict__ dl,
+                                                            float* __restrict__ dxmax) {
+  // dxmax (optional, [gridDim.x]): a bound on the block's |dx|, 2 max_row sum_c |dz_c| * max |W|
+  // (|dx_k| = |sum_c dz_c W_ck| <= sum_c |dz_c| max |W|; the 2 covers fp32 rounding), which the uint8
+  // weight-gradient kernel scales its fp16 dz planes with (mlp_u8.hip). The row sums cost a few
+  // VALU ops per tile; an exact max over the dx values measured 4 us more per step (40 vs 36 us).
   static_assert(C <= 16, "one 16-class MFMA tile");
   __shared__ __attribute__((aligned(16))) float ws[16 * WSP];            // W, zero-padded to 16 classes
   __shared__ __attribute__((aligned(16))) float xt[MW][16 * HK];         // per-wave transposes / final reduce
   __shared__ __attribute__((aligned(16))) float dzt[MW][16 * DTP];
   __shared__ float red[MW][2 + 16];
+  __shared__ float redm[MW];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const bool train = dx != nullptr || dl != nullptr;
@@ -662,7 +668,7 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
   f32x4m gw[8];  // dW^T tiles: gw[t][v] = dW[class r][hidden 16 t + 4 g + v]
 #pragma unroll
   for (int t = 0; t < 8; ++t) gw[t] = f32x4m{0.f, 0.f, 0.f, 0.f};
-  float gbp = 0.f, loss_acc = 0.f, corr_acc = 0.f;
+  float gbp = 0.f, loss_acc = 0.f, corr_acc = 0.f, amx = 0.f;
   float* xw = xt[wave];
   float* dw = dzt[wave];
 
@@ -721,6 +727,12 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
         if (valid && 4 * g + v < C) dl[(size_t)row * C + 4 * g + v] = dz[v];
     }
     if (dx) {
+      if (dxmax) {  // (invalid rows and classes >= C hold dz == 0)
+        float sa = (fabsf(dz[0]) + fabsf(dz[1])) + (fabsf(dz[2]) + fabsf(dz[3]));
+        sa += __shfl_xor(sa, 16);
+        sa += __shfl_xor(sa, 32);
+        amx = fmaxf(amx, sa);
+      }
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const f32x4m o = dx_t(wd[t], dz, xv[t], mask_dx);
@@ -785,13 +797,24 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
   for (int off = 32; off > 0; off >>= 1) {
     loss_acc += __shfl_xor(loss_acc, off);
     corr_acc += __shfl_xor(corr_acc, off);
+    amx = fmaxf(amx, __shfl_xor(amx, off));
   }
   if (lane == 0) {
     red[wave][0] = loss_acc;
     red[wave][1] = corr_acc;
+    redm[wave] = amx;
   }
   __syncthreads();
   static_assert(MW == 4, "wave-partial sums below are written for 4 waves");
+  if (dxmax && wave == 0) {  // times max |W| over the staged classes (wd: every class and hidden unit)
+    float wm = 0.f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) wm = fmaxf(wm, fabsf(wd[t][kk]));
+    for (int off = 32; off > 0; off >>= 1) wm = fmaxf(wm, __shfl_xor(wm, off));
+    if (tid == 0) dxmax[blockIdx.x] = 2.f * fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3])) * wm;
+  }
   if (train) {
     for (int o = tid; o < C * HK; o += 64 * MW) slab[o] = (xt[0][o] + xt[1][o]) + (xt[2][o] + xt[3][o]);
     if (tid < C) slab[C * HK + tid] = (red[0][2 + tid] + red[1][2 + tid]) + (red[2][2 + tid] + red[3][2 + tid]);
@@ -857,7 +880,7 @@ static bool head_use_mfma() {
 // in registers across them)
 static int head_mfma_blocks(int M, int* tiles_per_wave) {
   const int tiles = (M + 15) / 16;
-  int blocks = std::min(512, (tiles + MW - 1) / MW);
+  int blocks = std::min(kHeadAmaxMax, (tiles + MW - 1) / MW);  // (<= 512: one dx max per block)
   const int tpw = (tiles + blocks * MW - 1) / (blocks * MW);
   blocks = (tiles + MW * tpw - 1) / (MW * tpw);
   *tiles_per_wave = tpw;
@@ -949,7 +972,9 @@ void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx,
 
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K, int C,
                          float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
-                         float* workspace, bool mask_dx, hipStream_t stream, float* dl, bool stats_overwrite) {
+                         float* workspace, bool mask_dx, hipStream_t stream, float* dl, bool stats_overwrite,
+                         float* dx_amax, int* n_amax) {
+  if (n_amax) *n_amax = 0;
   if (M <= 0) {
     if (stats_overwrite) (void)hipMemsetAsync(stats, 0, 2 * sizeof(float), stream);
     return;
@@ -958,9 +983,11 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
   if (head_fused_supported(K, C) && dz_out == nullptr && workspace != nullptr && head_use_mfma()) {
     int tpw = 0;
     const int blocks = head_mfma_blocks(M, &tpw);
+    float* amx = (dx && dx_amax && n_amax) ? dx_amax : nullptr;
+    if (amx) *n_amax = blocks;
 #define HEAD_MFMA(CC)                                                                                              \
   hipLaunchKernelGGL((head_mfma_kernel<CC>), dim3(blocks), dim3(64 * MW), 0, stream, x, W, b, target, M, scale, workspace, \
-                     dx, tpw, mask_dx ? 1 : 0, dl)
+                     dx, tpw, mask_dx ? 1 : 0, dl, amx)
     switch (C) {
       case 10: HEAD_MFMA(10); break;
       case 2: HEAD_MFMA(2); break;

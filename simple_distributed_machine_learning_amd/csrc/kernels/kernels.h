@@ -97,13 +97,17 @@ void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short*
 // u8_wgrad_slab_floats(M, N) floats; deterministic (fixed-order reduction).
 bool u8_wgrad_supported(int M, int N, int K, int ldx, const void* X, const void* dz);
 int64_t u8_wgrad_slab_floats(int M, int N);
+// dz enters as two fp16 planes scaled by a power of two chosen from a bound: amax [namax] with
+// |dz| <= max(amax) (required here: the fused head's per-block maxima or a torch amax).
 void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
-              hipStream_t stream);
+              const float* amax, int namax, hipStream_t stream);
 // the same with the factored boundary gradient: dz = (dl @ w2) * (h > 0) (dl [M][C], w2 [C][N],
-// h [M][N]) expanded in the kernel's staging, bit-identical to head_dx_from_dl + u8_wgrad
+// h [M][N]) expanded in the kernel's staging with head_dx_from_dl's exact arithmetic; without amax
+// (namax == 0) each workgroup bounds its dz by max_row sum_c |dl| * max |w2|. With the same amax the
+// result is bit-identical to head_dx_from_dl + u8_wgrad.
 bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const void* h, int C);
 void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const unsigned char* X, int M, int N, int ldx,
-                 float* slab, float* gwb, float scale, hipStream_t stream);
+                 float* slab, float* gwb, float scale, const float* amax, int namax, hipStream_t stream);
 // out[i] += sum_s slab[s * stride + i] in split order (n % 4 == 0, 16-B aligned)
 void slab_reduce(const float* slab, int64_t stride, int splits, float* out, int64_t n, hipStream_t stream);
 
@@ -124,7 +128,11 @@ size_t head_workspace_floats(int M, int K, int C);
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K,
                          int C, float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
                          float* workspace, bool mask_dx, hipStream_t stream, float* dl = nullptr,
-                         bool stats_overwrite = false);  // stats_overwrite: stats = this call's totals
+                         bool stats_overwrite = false,  // stats_overwrite: stats = this call's totals
+                         float* dx_amax = nullptr, int* n_amax = nullptr);
+// dx_amax (capacity kHeadAmaxMax floats): where the MFMA head path writes per-block bounds on |dx|
+// (*n_amax of them; 0 when another head variant ran) - the uint8 weight gradient's dz bound
+constexpr int kHeadAmaxMax = 512;
 // dx = (dl @ W) * (x > 0 if mask): the fused head's dx rebuilt bit-identically from its factor dl
 // (K == 128, C in {2, 10, 16}: head_fused_supported)
 void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx, int M, int K, int C, bool mask,

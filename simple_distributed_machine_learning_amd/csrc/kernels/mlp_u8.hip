@@ -348,6 +348,15 @@ __global__ void __launch_bounds__(256) split_planes_pad_kernel(const float* __re
 // gW[n][k] += scale * sum_m dz[m][n] X[m][k]   and   gb[n] += sum_m dz[m][n]
 // (dz [M][N] fp32 = the boundary gradient, already ReLU-masked; X [M][784] uint8 pixels).
 //
+// Numerics: a pixel byte is exact in fp16; dz is split into two fp16 planes of dz * 2^s, hi =
+// fp16(dz 2^s) and lo = fp16(dz 2^s - hi) (each dz to within one fp32 ulp, as the forward's weight
+// planes in u8_planes.h), so every product is 2 fp16 MFMA products accumulated in fp32 and the 2^-s
+// is folded into the partial tile's scale. The power of two 2^s = 2^(14 - E) is chosen from a bound
+// |dz| < 2^E: the max of the head's per-block bounds when the gradient comes from the fused head
+// (head_xent.hip writes them next to dx: 2 max_row sum_c |dl_c| * max |W2|), a torch amax otherwise, and for the factored gradient (FD)
+// the workgroup's own bound max_row sum_c |dl| * max |W2| (hidden columns of the workgroup). dz
+// elements above 2^(E-15) keep the one-ulp split; smaller ones an absolute error below 2^(E-39).
+//
 // Why this shape: the reduction runs over the batch (K = 131072 rows), so the work is split over
 // row ranges and every workgroup leaves one partial tile. dz must be split into 3 bf16 planes on
 // the VALU; in a 128 x 128 output tile (gemm_f32x3's kernel) every dz element is split 7 times
@@ -381,7 +390,8 @@ constexpr int GDP = GHN + 32;       // LDS pitch (bf16) of the dz plane rows
 static_assert((GXP * 2 / 4) % 64 == 16 && (GDP * 2 / 4) % 64 == 48, "conflict-free transposed-read pitches");
 constexpr int GX_U16 = GBK * GXP;   // pixel image per buffer (u16)
 constexpr int GD_U16 = GBK * GDP;   // one dz plane per buffer (u16)
-constexpr int GBUF_U16 = GX_U16 + 3 * GD_U16;
+constexpr int GNPL = 2;              // fp16 planes of dz
+constexpr int GBUF_U16 = GX_U16 + GNPL * GD_U16;
 constexpr int GXCH = GBK * (GKP / 16);  // 16-byte pixel chunks per K-step incl. the zero pad (1600)
 static_assert(2 * GBUF_U16 * 2 <= 160 * 1024, "LDS");
 
@@ -396,15 +406,24 @@ __device__ __forceinline__ s16x4 tr16(const u16* p) {
 // 16-lane group g covers k-rows 16 s + 8 (g >> 1) + q (+4), lane 4q + p addressing columns
 // c0 + 16 (g & 1) + 4p .. +3, lane i receiving column c0 + 16 (g & 1) + i.
 template <int PITCH>
-__device__ __forceinline__ bf16x8 frag_tr(const u16* img, int c0, int s, int lane) {
+__device__ __forceinline__ f16x8 frag_tr(const u16* img, int c0, int s, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const u16* p = img + (16 * s + 8 * (g >> 1) + (i >> 2)) * PITCH + c0 + 16 * (g & 1) + 4 * (i & 3);
   const s16x4 lo = tr16(p), hi = tr16(p + 4 * PITCH);
   bf16x8 f;
   f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
   f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
-  return f;
+  return __builtin_bit_cast(f16x8, f);
 }
+
+// exponent E with |v| < 2^E for a finite v >= 0 (v = m 2^E, m in [0.5, 1)), clamped so 2^(14 - E)
+// and 2^(E - 14) stay normal floats
+__device__ __forceinline__ int bound_exp(float v) {
+  const unsigned b = __float_as_uint(v);
+  const int e = (int)((b >> 23) & 0xffu) - 126;
+  return (b & 0x7fffffffu) == 0u ? -100 : min(max(e, -100), 120);
+}
+__device__ __forceinline__ float pow2f(int e) { return __uint_as_float((unsigned)(e + 127) << 23); }
 
 struct WgradParams {
   const float* dz;           // [M][N]
@@ -413,6 +432,8 @@ struct WgradParams {
   int M, N, ldx;
   int rows_per_split;        // multiple of GBK
   float scale;
+  const float* amax;         // optional [namax]: |dz| <= max(amax) (the head's per-block maxima)
+  int namax;
   // FD (factored boundary gradient): dz = (dl @ W2) * (h > 0) rebuilt in the staging
   const float* dl;           // [M][C]
   const float* w2;           // [C][N]
@@ -455,6 +476,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   const int drow = FD ? fr : (t >> 4), dcol = FD ? fc : 4 * (t & 15);  // this thread's dz float4
   const float* dzp = (FD ? p.h : p.dz) + (size_t)(r0 + drow) * p.N + n0 + dcol;
   const size_t dz_step = (size_t)GBK * p.N;
+  float dz_up = 1.f, out_scale = p.scale;  // 2^(14 - E) and scale * 2^(E - 14), set below
   float w4[4] = {0.f, 0.f, 0.f, 0.f};  // FD: W2[4 g + kk][n0 + 16 (w & 3) + r]
   const float* dlp = nullptr;
   if constexpr (FD) {
@@ -465,6 +487,49 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     dlp = p.dl + (size_t)(r0 + fr) * p.C;
   }
   float d4[4] = {0.f, 0.f, 0.f, 0.f};
+
+  // ---- dz bound -> plane scale 2^(14 - E): block max through LDS (the buffers are free here) ----
+  {
+    float bnd = 0.f;
+    if (p.amax) {
+      for (int i = t; i < p.namax; i += GT) bnd = fmaxf(bnd, p.amax[i]);
+    } else if constexpr (FD) {  // max_row sum_c |dl| over this workgroup's rows, times max |W2| here
+      const int nrows = min(p.rows_per_split, p.M - r0);
+      for (int i = t; i < nrows; i += GT) {
+        const float* d = p.dl + (size_t)(r0 + i) * p.C;
+        float sa = 0.f;
+        for (int c = 0; c < p.C; ++c) sa += fabsf(d[c]);
+        bnd = fmaxf(bnd, sa);
+      }
+    }
+    float* red = reinterpret_cast<float*>(smem);
+    float wmx = 0.f;
+    if constexpr (FD) {
+      if (!p.amax)
+        for (int i = t; i < p.C * GHN; i += GT) wmx = fmaxf(wmx, fabsf(p.w2[(size_t)(i / GHN) * p.N + n0 + i % GHN]));
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      bnd = fmaxf(bnd, __shfl_xor(bnd, off));
+      wmx = fmaxf(wmx, __shfl_xor(wmx, off));
+    }
+    if (lane == 0) {
+      red[wave] = bnd;
+      red[8 + wave] = wmx;
+    }
+    __syncthreads();
+    bnd = red[0];
+    wmx = red[8];
+#pragma unroll
+    for (int w = 1; w < GT / 64; ++w) {
+      bnd = fmaxf(bnd, red[w]);
+      wmx = fmaxf(wmx, red[8 + w]);
+    }
+    __syncthreads();
+    // FD without amax: |dz_n| <= sum_c |dl_c| |W2_cn|; the product is rounded, so bound it by 2x
+    const int E = bound_exp((FD && !p.amax) ? 2.f * bnd * wmx : bnd);
+    dz_up = pow2f(14 - E);
+    out_scale = p.scale * pow2f(E - 14);
+  }
   constexpr int XU = (GXCH + GT - 1) / GT;  // 4 rounds
   const unsigned char* xp[XU];
   int xoff[XU];
@@ -496,26 +561,22 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     u16* B = smem + buf * GBUF_U16;
     if constexpr (FD) dv = fd_dz(w4, d4, dv);
     bsum += dv;
-    u16x4 hi, mi, lo;
+    u16x4 hi, lo;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float x = dv[e];
-      const u16 h = bf16_bits(x);
-      const float r1 = x - bf16_val(h);
-      const u16 m = bf16_bits(r1);
-      hi[e] = h;
-      mi[e] = m;
-      lo[e] = bf16_bits(r1 - bf16_val(m));
+      const float x = dv[e] * dz_up;  // exact (power of two), |x| < 2^14
+      const _Float16 h = static_cast<_Float16>(x);
+      hi[e] = __builtin_bit_cast(u16, h);
+      lo[e] = __builtin_bit_cast(u16, static_cast<_Float16>(x - static_cast<float>(h)));
     }
     const int doff = GX_U16 + drow * GDP + dcol;
     *reinterpret_cast<u16x4*>(B + doff) = hi;
-    *reinterpret_cast<u16x4*>(B + doff + GD_U16) = mi;
-    *reinterpret_cast<u16x4*>(B + doff + 2 * GD_U16) = lo;
+    *reinterpret_cast<u16x4*>(B + doff + GD_U16) = lo;
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
       const u32x4 v = xload[u] ? xv[u] : u32x4{0u, 0u, 0u, 0u};
-      *reinterpret_cast<bf16x8*>(B + xoff[u]) = widen8(v[0], v[1]);
-      *reinterpret_cast<bf16x8*>(B + xoff[u] + 8) = widen8(v[2], v[3]);
+      *reinterpret_cast<f16x8*>(B + xoff[u]) = widen8h(v[0], v[1]);
+      *reinterpret_cast<f16x8*>(B + xoff[u] + 8) = widen8h(v[2], v[3]);
     }
   };
 
@@ -534,19 +595,18 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
       const u16* B = smem + buf * GBUF_U16;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        bf16x8 a[2][3];
+        f16x8 a[2][GNPL];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int pl = 0; pl < 3; ++pl) a[i][pl] = frag_tr<GDP>(B + GX_U16 + pl * GD_U16, 32 * i, s, lane);
+          for (int pl = 0; pl < GNPL; ++pl) a[i][pl] = frag_tr<GDP>(B + GX_U16 + pl * GD_U16, 32 * i, s, lane);
 #pragma unroll
         for (int j = 0; j < NCT; ++j) {
-          const bf16x8 b = frag_tr<GXP>(B, 32 * (ct0 + j), s, lane);
+          const f16x8 b = frag_tr<GXP>(B, 32 * (ct0 + j), s, lane);
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
-            acc[i][j] = mfma(a[i][2], b, acc[i][j]);
-            acc[i][j] = mfma(a[i][1], b, acc[i][j]);
-            acc[i][j] = mfma(a[i][0], b, acc[i][j]);
+            acc[i][j] = mfma(a[i][1], b, acc[i][j]);  // lo
+            acc[i][j] = mfma(a[i][0], b, acc[i][j]);  // hi
           }
         }
       }
@@ -583,7 +643,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int n = n0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          out[(size_t)n * GKC + col] = acc[i][j][r] * p.scale;
+          out[(size_t)n * GKC + col] = acc[i][j][r] * out_scale;
         }
     }
   };
@@ -647,9 +707,12 @@ int64_t u8_wgrad_slab_floats(int M, int N) {
 }
 
 void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
-              hipStream_t stream) {
+              const float* amax, int namax, hipStream_t stream) {
+  if (!amax || namax < 1) abort();  // host contract: the dz bound is given
   WgradParams p{};
   p.dz = dz;
+  p.amax = amax;
+  p.namax = namax;
   p.X = X;
   p.slab = slab;
   p.M = M;
@@ -667,8 +730,10 @@ bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const vo
 }
 
 void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const unsigned char* X, int M, int N, int ldx,
-                 float* slab, float* gwb, float scale, hipStream_t stream) {
+                 float* slab, float* gwb, float scale, const float* amax, int namax, hipStream_t stream) {
   WgradParams p{};
+  p.amax = namax > 0 ? amax : nullptr;
+  p.namax = namax;
   p.X = X;
   p.slab = slab;
   p.M = M;

@@ -215,8 +215,10 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
 }
 
 // weight/bias gradient of the uint8-fed first layer: gw += scale * gz^T x_u8, gb += colsum(gz)
+// amax: optional float tensor with |gz| <= max(amax) (the fused head's per-block |dx| maxima); the
+// uint8 kernel scales gz's fp16 planes from it (computed here with a torch amax when absent)
 void linear_wgrad_u8(torch::Tensor x, torch::Tensor gz, torch::Tensor gw, c10::optional<torch::Tensor> gb,
-                     double scale) {
+                     double scale, c10::optional<torch::Tensor> amax) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
               "linear_wgrad_u8: x must be a contiguous 2-D uint8 ROCm tensor");
   check_f32_cuda(gz, "gz");
@@ -241,8 +243,11 @@ void linear_wgrad_u8(torch::Tensor x, torch::Tensor gz, torch::Tensor gw, c10::o
   if (!legacy_wgrad && gb_follows && sdml::u8_wgrad_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr(),
                                                                gz.data_ptr())) {
     auto ws = torch::empty({sdml::u8_wgrad_slab_floats((int)M, (int)N)}, gw.options());
+    torch::Tensor am = amax.has_value() && amax->defined() ? *amax : gz.abs().amax().reshape({1});
+    check_f32_cuda(am, "amax");
+    TORCH_CHECK(am.numel() >= 1 && am.is_contiguous(), "linear_wgrad_u8: amax must be a non-empty contiguous tensor");
     sdml::u8_wgrad(gz.data_ptr<float>(), x.data_ptr<uint8_t>(), (int)M, (int)N, (int)K, ws.data_ptr<float>(),
-                   gw.data_ptr<float>(), (float)scale, cur_stream());
+                   gw.data_ptr<float>(), (float)scale, am.data_ptr<float>(), (int)am.numel(), cur_stream());
     return;
   }
   float* slab = nullptr;
@@ -569,10 +574,13 @@ torch::Tensor bn_nhwc_eval(torch::Tensor x, c10::optional<torch::Tensor> res, to
   return y;
 }
 
-// fused head; returns (stats[2] = {loss_sum, correct}, dx or None). If `stats_acc` is given
+using HeadOut = std::tuple<torch::Tensor, c10::optional<torch::Tensor>, c10::optional<torch::Tensor>>;
+
+// fused head; returns (stats[2] = {loss_sum, correct}, dx or None, dx_amax or None), dx_amax = the
+// MFMA head's per-block bounds on |dx| (what linear_wgrad_u8 takes for dz). If `stats_acc` is given
 // the kernel accumulates into it (and returns it) instead of allocating a new one; with
 // `stats_init` it overwrites it (stats_acc may then hold anything: no zero-fill launch).
-std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
+HeadOut head_logsoftmax_nll_f32(
     torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor target, c10::optional<torch::Tensor> gw,
     c10::optional<torch::Tensor> gb, double scale, bool need_dx, c10::optional<torch::Tensor> stats_acc,
     bool mask_dx, bool stats_init) {
@@ -595,7 +603,8 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
   c10::optional<torch::Tensor> dx;
   if (M == 0) {
     if (overwrite) stats.zero_();
-    return {stats, need_dx ? c10::optional<torch::Tensor>(torch::empty({0, K}, x.options())) : c10::nullopt};
+    return {stats, need_dx ? c10::optional<torch::Tensor>(torch::empty({0, K}, x.options())) : c10::nullopt,
+            c10::nullopt};
   }
   hipStream_t s = cur_stream();
   const bool fusable = sdml::head_fused_supported((int)K, (int)C) || sdml::head_lds_supported((int)M, (int)K, (int)C);
@@ -607,14 +616,18 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
                               target.data_ptr<int64_t>(), M, K, C, (float)scale, stats.data_ptr<float>(), nullptr,
                               nullptr, nullptr, nullptr, wsp, false, s, nullptr, overwrite);
-    return {stats, c10::nullopt};
+    return {stats, c10::nullopt, c10::nullopt};
   }
   auto dxt = torch::empty({M, K}, x.options());
+  c10::optional<torch::Tensor> amax;
   if (fused) {
+    auto am = torch::empty({sdml::kHeadAmaxMax}, x.options());
+    int n_am = 0;
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
                               target.data_ptr<int64_t>(), M, K, C, (float)scale, stats.data_ptr<float>(),
                               dxt.data_ptr<float>(), opt_ptr(gw), opt_ptr(gb), nullptr, wsp, mask_dx, s, nullptr,
-                              overwrite);
+                              overwrite, am.data_ptr<float>(), &n_am);
+    if (n_am > 0) amax = am.narrow(0, 0, n_am);
   } else {
     auto dz = torch::empty({M, C}, x.options());
     sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(),
@@ -644,7 +657,7 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_f32(
     }
   }
   if (need_dx) dx = dxt;
-  return {stats, dx};
+  return {stats, dx, need_dx ? amax : c10::nullopt};
 }
 
 // training head that returns its boundary gradient as the factor dl = scale * (softmax - onehot) [M, C]
@@ -698,7 +711,7 @@ torch::Tensor head_dx_from_dl(torch::Tensor dl, torch::Tensor w, torch::Tensor x
 // gb += colsum(dz) with dz = (dl @ w2) * (h > 0) - expanded inside mlp_u8.hip's wgrad kernel when
 // it applies (bit-identical to head_dx_from_dl followed by linear_wgrad_u8), else those two
 void linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, torch::Tensor h, torch::Tensor gw,
-                        torch::Tensor gb, double scale) {
+                        torch::Tensor gb, double scale, c10::optional<torch::Tensor> amax) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
               "linear_wgrad_u8_dl: x must be a contiguous 2-D uint8 ROCm tensor");
   check_f32_cuda(dl, "dl");
@@ -714,13 +727,19 @@ void linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, tor
   if (gb_follows && sdml::head_fused_supported((int)N, (int)C) &&
       sdml::u8_wgrad_dl_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr(), h.data_ptr(), (int)C)) {
     auto ws = torch::empty({sdml::u8_wgrad_slab_floats((int)M, (int)N)}, gw.options());
+    const bool has_am = amax.has_value() && amax->defined();
+    if (has_am) {
+      check_f32_cuda(*amax, "amax");
+      TORCH_CHECK(amax->numel() >= 1 && amax->is_contiguous(), "linear_wgrad_u8_dl: amax must be non-empty");
+    }
     sdml::u8_wgrad_dl(dl.data_ptr<float>(), w2.data_ptr<float>(), h.data_ptr<float>(), (int)C, x.data_ptr<uint8_t>(),
-                      (int)M, (int)N, (int)K, ws.data_ptr<float>(), gw.data_ptr<float>(), (float)scale, cur_stream());
+                      (int)M, (int)N, (int)K, ws.data_ptr<float>(), gw.data_ptr<float>(), (float)scale,
+                      has_am ? amax->data_ptr<float>() : nullptr, has_am ? (int)amax->numel() : 0, cur_stream());
     return;
   }
   torch::Tensor dz = sdml::head_fused_supported((int)N, (int)C) ? head_dx_from_dl(dl, w2, h, true)
                                                                   : at::matmul(dl, w2).mul_((h > 0).to(h.scalar_type()));
-  linear_wgrad_u8(x, dz, gw, gb, scale);
+  linear_wgrad_u8(x, dz, gw, gb, scale, amax);
 }
 
 void sgd_momentum_(torch::Tensor p, torch::Tensor g, torch::Tensor buf, double lr, double momentum, double dampening,
@@ -1077,7 +1096,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "padded K of the uint8 forward's weight planes");
   m.def("u8_fwd_planes", []() { return (int64_t)sdml::kU8FwdPlanes; }, "number of the uint8 forward's weight planes");
   m.def("linear_wgrad_u8", &linear_wgrad_u8, "gw += scale * gz^T x_u8, gb += colsum(gz)", py::arg("x"), py::arg("gz"),
-        py::arg("gw"), py::arg("gb"), py::arg("scale"));
+        py::arg("gw"), py::arg("gb"), py::arg("scale"), py::arg("amax") = py::none());
   m.def("linear_fwd_f32", &linear_fwd_f32, "relu?(x @ w.T + b) on fp32 MFMA", py::arg("x"), py::arg("w"),
         py::arg("b"), py::arg("relu"));
   m.def("linear_bwd_f32", &linear_bwd_f32, "backward of linear(+relu): accumulates gw/gb, returns dx",
@@ -1096,7 +1115,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stats_acc"), py::arg("stats_init") = false);
   m.def("linear_wgrad_u8_dl", &linear_wgrad_u8_dl,
         "gw += scale * dz^T x_u8, gb += colsum(dz), dz = (dl @ w2) * (h > 0) (factored boundary gradient)",
-        py::arg("x"), py::arg("dl"), py::arg("w2"), py::arg("h"), py::arg("gw"), py::arg("gb"), py::arg("scale"));
+        py::arg("x"), py::arg("dl"), py::arg("w2"), py::arg("h"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
+        py::arg("amax") = py::none());
   m.def("head_dx_from_dl", &head_dx_from_dl, "dx = (dl @ w) * (x > 0): boundary gradient from its factor",
         py::arg("dl"), py::arg("w"), py::arg("x"), py::arg("mask"));
   m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer (optionally also writing a "

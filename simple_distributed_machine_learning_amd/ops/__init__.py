@@ -70,23 +70,32 @@ def linear_relu_fwd_u8(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, cache:
     return ref.linear_relu_fwd(pixels_to_float(x), w, b)
 
 
-def linear_wgrad_u8(x: torch.Tensor, gz: torch.Tensor, gw: torch.Tensor, gb: Optional[torch.Tensor]) -> None:
-    """gw += gz.T @ ToTensor(x), gb += sum(gz) for uint8 pixels x (first layer: no input grad)."""
+def linear_wgrad_u8(x: torch.Tensor, gz: torch.Tensor, gw: torch.Tensor, gb: Optional[torch.Tensor],
+                    amax: Optional[torch.Tensor] = None) -> None:
+    """gw += gz.T @ ToTensor(x), gb += sum(gz) for uint8 pixels x (first layer: no input grad).
+
+    ROCm: gz enters the kernel as fp16 planes scaled from a bound on |gz|: ``amax`` (any float
+    tensor whose max bounds |gz|), else the bounds the fused head attached to the dx it returned
+    (:func:`linear_logsoftmax_nll`), else a torch amax of gz."""
     if x.is_cuda:
-        _k().linear_wgrad_u8(x, gz, gw, gb, PIXEL_SCALE)
+        if amax is None:
+            amax = getattr(gz, "_sdml_amax", None)
+        _k().linear_wgrad_u8(x, gz, gw, gb, PIXEL_SCALE, amax)
         return
     gw += gz.t() @ pixels_to_float(x)
     if gb is not None:
         gb += gz.sum(0)
 
 
-def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb) -> None:
+def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, amax: Optional[torch.Tensor] = None) -> None:
     """First-layer weight gradient from the FACTORED boundary gradient: with dz = (dl @ w2) * (h > 0)
     (dl [M, C] the head's factor, w2 [C, N] the head weight, h [M, N] this layer's ReLU output),
     gw += dz.T @ ToTensor(x), gb += sum(dz). On ROCm dz is expanded inside the weight-gradient kernel
-    (never written to memory), bit-identical to :func:`head_dx_from_dlogits` + :func:`linear_wgrad_u8`."""
+    (never written to memory); with the same ``amax`` (a bound on |dz|, see :func:`linear_wgrad_u8`)
+    bit-identical to :func:`head_dx_from_dlogits` + :func:`linear_wgrad_u8`, without it each workgroup
+    bounds dz by its rows' max sum |dl| times max |w2|."""
     if x.is_cuda:
-        _k().linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, PIXEL_SCALE)
+        _k().linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, PIXEL_SCALE, amax)
         return
     with torch.no_grad():
         dz = (dl @ w2) * (h > 0).to(dl.dtype)
@@ -131,8 +140,10 @@ def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool, 
     zero-fill beforehand) and (None, None, dx) is returned.
     ``mask_dx``: dx *= (x > 0) (fused ReLU backward of the stage that produced x)."""
     if x.is_cuda:
-        st, dx = _k().head_logsoftmax_nll_f32(x, w, b, target, gw, gb, float(scale), need_dx, stats, mask_dx,
-                                              bool(stats_init))
+        st, dx, amax = _k().head_logsoftmax_nll_f32(x, w, b, target, gw, gb, float(scale), need_dx, stats, mask_dx,
+                                                    bool(stats_init))
+        if dx is not None and amax is not None:
+            dx._sdml_amax = amax  # per-block bounds on |dx|, which linear_wgrad_u8 scales dz's fp16 planes with
         if stats is not None:
             return None, None, dx
         return st[0], st[1], dx

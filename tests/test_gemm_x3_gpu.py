@@ -259,7 +259,7 @@ def test_u8_small_batch_falls_back_to_fp32():
 @pytest.mark.parametrize("C", [10, 2])
 def test_wgrad_u8_from_factor_bit_identical(M, C):
     """The factored boundary gradient expanded inside the weight-gradient kernel (rotate placement,
-    R > 1) gives bit for bit the gw/gb of head_dx_from_dl followed by linear_wgrad_u8."""
+    R > 1) gives bit for bit the gw/gb of head_dx_from_dl followed by linear_wgrad_u8 (same dz bound)."""
     N, Kd = 128, 784
     x8 = pixels(M, Kd, 21)
     h = rnd(M, N, seed=22).relu()
@@ -271,13 +271,19 @@ def test_wgrad_u8_from_factor_bit_identical(M, C):
         buf = g0.clone()
         return buf, buf[:N * Kd].view(N, Kd), buf[N * Kd:]
 
+    dz_dev = ops.head_dx_from_dlogits(dl, w2, h, mask=True)
+    amax = dz_dev.abs().amax().reshape(1)
     b1, gw1, gb1 = flat()
-    ops.linear_wgrad_u8_dl(x8, dl, w2, h, gw1, gb1)
+    ops.linear_wgrad_u8_dl(x8, dl, w2, h, gw1, gb1, amax=amax)
     b2, gw2, gb2 = flat()
-    ops.linear_wgrad_u8(x8, ops.head_dx_from_dlogits(dl, w2, h, mask=True), gw2, gb2)
+    ops.linear_wgrad_u8(x8, dz_dev, gw2, gb2, amax=amax)
     assert torch.equal(b1, b2)
+    # the workgroup-local bound (rotate placement: no amax) agrees with the fp64 reference as well
+    b3, gw3, gb3 = flat()
+    ops.linear_wgrad_u8_dl(x8, dl, w2, h, gw3, gb3)
     # and against the fp64 reference
     dz = (dl.double() @ w2.double()) * (h > 0).double()
     want = g0.double()[:N * Kd].view(N, Kd) + dz.t() @ (x8.double() / 255.0)
-    torch.testing.assert_close(gw1.double(), want, rtol=1e-4, atol=1e-6)
-    torch.testing.assert_close(gb1.double(), g0.double()[N * Kd:] + dz.sum(0), rtol=1e-4, atol=1e-6)
+    for gwi, gbi in ((gw1, gb1), (gw3, gb3)):
+        torch.testing.assert_close(gwi.double(), want, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(gbi.double(), g0.double()[N * Kd:] + dz.sum(0), rtol=1e-4, atol=1e-6)

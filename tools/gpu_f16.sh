@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out/f16
 export TMPDIR=/tmp
 L=gpurun_out/f16/log.txt
-timeout -k 10 400 python -u -m pytest tests/test_gemm_x3_gpu.py tests/test_engine_gpu.py tests/test_graphs_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/f16/pytest.log 2>&1 || { tail -40 gpurun_out/f16/pytest.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/f16/pytest.log 2>&1 || { tail -40 gpurun_out/f16/pytest.log; exit 1; }
 tail -1 gpurun_out/f16/pytest.log
 timeout -k 10 120 python tools/bench_u8.py > $L 2>&1 || { tail $L; exit 1; }
 timeout -k 10 200 python bench.py >> $L 2>&1 || { tail $L; exit 1; }

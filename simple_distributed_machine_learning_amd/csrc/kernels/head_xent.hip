@@ -641,7 +641,8 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
                                                             float* __restrict__ part, float* __restrict__ dx,
                                                             int tiles_per_wave, int mask_dx, float* __restrict__ dl,
                                                             float* __restrict__ dxmax) {
-  // dxmax (optional, [gridDim.x]): a bound on the block's |dx|, 2 max_row sum_c |dz_c| * max |W|
+  // dxmax (optional, [gridDim.x]): a bound on the block's |dx| (dx = dl @ W, whether dx itself or
+  // its factor dl is written), 2 max_row sum_c |dz_c| * max |W|
   // (|dx_k| = |sum_c dz_c W_ck| <= sum_c |dz_c| max |W|; the 2 covers fp32 rounding), which the uint8
   // weight-gradient kernel scales its fp16 dz planes with (mlp_u8.hip). The row sums cost a few
   // VALU ops per tile; an exact max over the dx values measured 4 us more per step (40 vs 36 us).
@@ -726,13 +727,13 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
       for (int v = 0; v < 4; ++v)
         if (valid && 4 * g + v < C) dl[(size_t)row * C + 4 * g + v] = dz[v];
     }
+    if (dxmax) {  // (invalid rows and classes >= C hold dz == 0)
+      float sa = (fabsf(dz[0]) + fabsf(dz[1])) + (fabsf(dz[2]) + fabsf(dz[3]));
+      sa += __shfl_xor(sa, 16);
+      sa += __shfl_xor(sa, 32);
+      amx = fmaxf(amx, sa);
+    }
     if (dx) {
-      if (dxmax) {  // (invalid rows and classes >= C hold dz == 0)
-        float sa = (fabsf(dz[0]) + fabsf(dz[1])) + (fabsf(dz[2]) + fabsf(dz[3]));
-        sa += __shfl_xor(sa, 16);
-        sa += __shfl_xor(sa, 32);
-        amx = fmaxf(amx, sa);
-      }
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const f32x4m o = dx_t(wd[t], dz, xv[t], mask_dx);
@@ -983,7 +984,7 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
   if (head_fused_supported(K, C) && dz_out == nullptr && workspace != nullptr && head_use_mfma()) {
     int tpw = 0;
     const int blocks = head_mfma_blocks(M, &tpw);
-    float* amx = (dx && dx_amax && n_amax) ? dx_amax : nullptr;
+    float* amx = ((dx || dl) && dx_amax && n_amax) ? dx_amax : nullptr;
     if (amx) *n_amax = blocks;
 #define HEAD_MFMA(CC)                                                                                              \
   hipLaunchKernelGGL((head_mfma_kernel<CC>), dim3(blocks), dim3(64 * MW), 0, stream, x, W, b, target, M, scale, workspace, \

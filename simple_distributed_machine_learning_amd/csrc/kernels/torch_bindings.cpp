@@ -662,8 +662,9 @@ HeadOut head_logsoftmax_nll_f32(
 
 // training head that returns its boundary gradient as the factor dl = scale * (softmax - onehot) [M, C]
 // (dx = dl @ w, rebuilt by head_dx_from_dl wherever w is held); gw/gb accumulated, loss and correct
-// count accumulated into stats_acc [2] (overwritten with stats_init)
-torch::Tensor head_logsoftmax_nll_dl_f32(torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor target,
+// count accumulated into stats_acc [2] (overwritten with stats_init). Returns (dl, bound or None):
+// the MFMA head's per-block bounds on |dl @ w| (what linear_wgrad_u8_dl takes as amax)
+std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_dl_f32(torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor target,
                                          torch::Tensor gw, torch::Tensor gb, double scale, torch::Tensor stats_acc,
                                          bool stats_init) {
   check_f32_cuda(x, "x");
@@ -682,14 +683,17 @@ torch::Tensor head_logsoftmax_nll_dl_f32(torch::Tensor x, torch::Tensor w, torch
   auto dl = torch::empty({M, C}, x.options());
   if (M == 0) {
     if (stats_init) stats_acc.zero_();
-    return dl;
+    return {dl, c10::nullopt};
   }
   auto ws = torch::empty({(int64_t)sdml::head_workspace_floats(M, K, C)}, x.options());
+  auto am = torch::empty({sdml::kHeadAmaxMax}, x.options());
+  int n_am = 0;
   sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), target.data_ptr<int64_t>(),
                             M, K, C, (float)scale, stats_acc.data_ptr<float>(), nullptr, gw.data_ptr<float>(),
                             gb.data_ptr<float>(), nullptr, ws.data_ptr<float>(), false, cur_stream(),
-                            dl.data_ptr<float>(), stats_init);
-  return dl;
+                            dl.data_ptr<float>(), stats_init, am.data_ptr<float>(), &n_am);
+  if (n_am > 0) return {dl, am.narrow(0, 0, n_am)};
+  return {dl, c10::nullopt};
 }
 
 // dx = (dl @ w) * (x > 0 if mask): the fused head's boundary gradient rebuilt from its factor

@@ -92,9 +92,12 @@ def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, amax: Optional[torch.Tensor] = None
     (dl [M, C] the head's factor, w2 [C, N] the head weight, h [M, N] this layer's ReLU output),
     gw += dz.T @ ToTensor(x), gb += sum(dz). On ROCm dz is expanded inside the weight-gradient kernel
     (never written to memory); with the same ``amax`` (a bound on |dz|, see :func:`linear_wgrad_u8`)
-    bit-identical to :func:`head_dx_from_dlogits` + :func:`linear_wgrad_u8`, without it each workgroup
-    bounds dz by its rows' max sum |dl| times max |w2|."""
+    bit-identical to :func:`head_dx_from_dlogits` + :func:`linear_wgrad_u8`; without it the bounds the
+    fused head attached to the ``dl`` it returned, else each workgroup bounds dz by its rows'
+    max sum |dl| times max |w2| (a dl received over the network carries no attribute)."""
     if x.is_cuda:
+        if amax is None:
+            amax = getattr(dl, "_sdml_amax", None)
         _k().linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, PIXEL_SCALE, amax)
         return
     with torch.no_grad():
@@ -163,7 +166,10 @@ def linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale: float, stats, stats
     accumulated; loss sum and correct count are accumulated into ``stats`` [2] (overwritten with
     ``stats_init``)."""
     if x.is_cuda:
-        return _k().head_logsoftmax_nll_dl_f32(x, w, b, target, gw, gb, float(scale), stats, bool(stats_init))
+        dl, amax = _k().head_logsoftmax_nll_dl_f32(x, w, b, target, gw, gb, float(scale), stats, bool(stats_init))
+        if amax is not None:
+            dl._sdml_amax = amax  # per-block bounds on |dl @ w| (linear_wgrad_u8_dl's dz bound)
+        return dl
     with torch.no_grad():
         loss, correct, dl = ref.linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale)
     _put_stats(stats, loss, correct, stats_init)

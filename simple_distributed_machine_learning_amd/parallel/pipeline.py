@@ -164,6 +164,9 @@ class PipelineEngine:
         # rotate all-to-all, 2-stage models with a single-Linear head: send the boundary gradient
         # as its rank-C factor (see _run_rotate_alltoall); SDML_ROTATE_FACTORED=0 sends it whole
         self.factored_boundary_grad = os.environ.get("SDML_ROTATE_FACTORED", "1") != "0"
+        # ... also with both stages on one rank (R == 1): the head then skips its dx pass and stage 0
+        # reads h + dl instead of dx (SDML_FACTORED_R1=0: the head returns dx)
+        self.factored_r1 = os.environ.get("SDML_FACTORED_R1", "1") != "0"
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
 
@@ -404,7 +407,8 @@ class PipelineEngine:
         # factored boundary gradient: every rank holds stage 1's weights (they are replicated in
         # this placement), so the head sends back only its rank-C factor dl [n, C] and the owner
         # rebuilds d(loss)/dz0 = (dl @ W1) * (h > 0) from its own boundary activation h
-        factored = (train and R > 1 and self.factored_boundary_grad and getattr(s1, "supports_factored_grad", False))
+        factored = (train and (R > 1 or self.factored_r1) and self.factored_boundary_grad
+                    and getattr(s1, "supports_factored_grad", False))
         # every owner holds the same ``batch_size``, so every rank derives the same wave count
         # (fewer waves than M/R when the batch is smaller) and issues the same collectives
         waves = split_sizes(batch_size, max(1, self.M // R))

@@ -1,5 +1,7 @@
 """Time the rotate placement's stage-0 backward from the factored boundary gradient: head_dx_from_dl
-+ linear_wgrad_u8 (dz written and read back) vs linear_wgrad_u8_dl (dz expanded in the kernel)."""
++ linear_wgrad_u8 (dz written and read back) vs linear_wgrad_u8_dl (dz expanded in the kernel), and
+the weight-gradient kernels alone (each including the slab reduction): dz given with a bound,
+dl given with a bound (what the fused head attaches), dl without (workgroup-local bound)."""
 import json
 import os
 import sys
@@ -37,6 +39,10 @@ def main():
         out[f"M{M}_unfused_us"] = round(timed(lambda: ops.linear_wgrad_u8(
             x8, ops.head_dx_from_dlogits(dl, w2, h, mask=True), gw, gb)), 1)
         out[f"M{M}_fused_us"] = round(timed(lambda: ops.linear_wgrad_u8_dl(x8, dl, w2, h, gw, gb)), 1)
+        dz = ops.head_dx_from_dlogits(dl, w2, h, mask=True)
+        am = dz.abs().amax().reshape(1)
+        out[f"M{M}_dz_bound_us"] = round(timed(lambda: ops.linear_wgrad_u8(x8, dz, gw, gb, amax=am)), 1)
+        out[f"M{M}_dl_bound_us"] = round(timed(lambda: ops.linear_wgrad_u8_dl(x8, dl, w2, h, gw, gb, amax=am)), 1)
     print(json.dumps(out))
 
 

@@ -142,3 +142,22 @@ def test_gpu_u8_weight_plane_cache_follows_the_weights():
     check()
     e.run(ds, 2 * B, B, train=True)
     check()
+
+
+@pytest.mark.parametrize("factored", [True, False])
+def test_gpu_rotate_one_rank_factored_and_whole_gradient(factored):
+    """Rotate on one rank: the head returns its factor dl (stage 0's weight-gradient kernel expands
+    it, dz bounded by the head's per-block bounds) or dx (bounds attached to dx); both train like
+    the CPU engine on the same images."""
+    B = 8192
+    e_gpu = _engine("mlp", DEV, "rotate", 1)
+    e_gpu.factored_r1 = factored
+    e_cpu = _engine("mlp", torch.device("cpu"), "rotate", 1)
+    ds_g = SyntheticMNIST(2 * B, seed=7, device=DEV, pixels="u8")
+    ds_c = SyntheticMNIST(2 * B, seed=7, device="cpu")
+    ds_c.x = ds_g.x.cpu().float().div_(255.0)
+    for step in range(2):
+        rg = e_gpu.run(ds_g, step * B, B, train=True)
+        rc = e_cpu.run(ds_c, step * B, B, train=True)
+        torch.testing.assert_close(float(rg.loss_sum), float(rc.loss_sum), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(e_gpu.flat.params.cpu(), e_cpu.flat.params, rtol=1e-4, atol=5e-5)

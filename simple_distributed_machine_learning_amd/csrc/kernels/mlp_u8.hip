@@ -12,8 +12,9 @@
 // measured v_mfma_f32_32x32x16_bf16's accumulation on gfx950 as unbiased and more accurate than a
 // k-ordered fp32 fmaf chain (K = 4096: 2.7e-7 vs 7.6e-7 mean relative error, bias 4e-9).
 //
-// Structure (gfx950, wave64): 512 threads = 8 waves as 4 (rows) x 2 (cols), block tile 128 WMT x 128,
-// wave tile 32 WMT x 64 = WMT x 2 tiles of v_mfma_f32_32x32x16_f16, K-step 64 (4 MFMA k-substeps).
+// Structure (gfx950, wave64): NWR x 2 waves (4 x 2 = 512 threads, or 8 x 2 = 1024 threads for the
+// 512-row blocks of large batches, 4 waves per SIMD), wave tile 32 WMT x 64 = WMT x 2 tiles of
+// v_mfma_f32_32x32x16_f16, block tile 32 WMT NWR x 128, K-step 64 (4 MFMA k-substeps).
 // Both operands reach LDS by LDS-DMA (global_load_lds_dwordx4, 16 B per lane, no VGPR staging)
 // into a ring of NS stages (the DMA of K-step t+1 flies under K-step t's MFMAs). Measured
 // alternatives (on the 3-plane bf16 form): 32-deep K-steps in a 4-stage ring (3 K-steps in flight),
@@ -51,7 +52,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-constexpr int FT = 512;                       // threads
 constexpr int FBN = 128;                      // columns per block
 constexpr int FBK = 64;                       // k per K-step (FBK / 16 MFMA k-substeps)
 constexpr int NS = 2;                         // LDS stages
@@ -60,19 +60,25 @@ constexpr int NPL = kU8FwdPlanes;            // fp16 weight planes
 constexpr int B_PLANE = FBN * FBK * 2;        // bytes per fp16 plane per stage
 constexpr int XCH = FBK / 16;                 // 16-B chunks per pixel row (2 or 4)
 constexpr int WCH = FBK / 8;                  // 16-B chunks per weight row (4 or 8)
-constexpr int GLDS_W = NPL * B_PLANE / 1024 / (FT / 64);
 static_assert(FBK == 32 || FBK == 64, "swizzles below are written for 32- and 64-deep K-steps");
 
-// block geometry per WMT = 32-row MFMA tiles per wave (wave tile 32 WMT x 64, block 128 WMT x 128)
-template <int WMT>
+// block geometry per WMT = 32-row MFMA tiles per wave and NWR = row waves (the block is NWR x 2
+// waves; wave tile 32 WMT x 64, block 32 WMT NWR x 128). NWR = 4: 512 threads (2 waves per SIMD);
+// NWR = 8: 1024 threads (4 waves per SIMD, <= 128 VGPRs)
+template <int WMT, int NWR = 4>
 struct Geo {
-  static constexpr int BM = 4 * 32 * WMT;           // rows per block
+  static constexpr int THREADS = 128 * NWR;
+  static constexpr int WAVES = THREADS / 64;
+  static constexpr int BM = NWR * 32 * WMT;         // rows per block
   static constexpr int A_BYTES = BM * FBK;          // raw pixel bytes per stage
   static constexpr int STAGE = A_BYTES + NPL * B_PLANE;
-  static constexpr int GLDS_X = A_BYTES / 1024 / (FT / 64);
+  static constexpr int GLDS_X = A_BYTES / 1024 / WAVES;
+  static constexpr int GLDS_W = NPL * B_PLANE / 1024 / WAVES;
   static constexpr int GLDS_PER_STAGE = GLDS_X + GLDS_W;  // DMA instructions per wave per stage
-  // the epilogue transposes 64 x 64 fp32 per wave through the (then free) stage buffers
-  static constexpr int SMEM = std::max(NS * STAGE, (FT / 64) * 64 * 64 * 4);
+  static_assert(GLDS_X * 1024 * WAVES == A_BYTES && GLDS_W * 1024 * WAVES == NPL * B_PLANE, "DMA split");
+  // the epilogue transposes EPR x 64 fp32 per wave through the (then free) stage buffers
+  static constexpr int EPR = WAVES * 64 * 64 * 4 <= 128 * 1024 ? 64 : 32;
+  static constexpr int SMEM = std::max(NS * STAGE, WAVES * EPR * 64 * 4);
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
 
@@ -137,14 +143,14 @@ struct FwdParams {
 // LDS images of one stage: X [BM rows][FBK bytes], W [NPL planes][128 rows][FBK fp16], chunks at
 // xpos / wpos. The DMA writes 1 KiB per wave-instruction lane-linearly (lane i -> bytes 16i..), so
 // the swizzle goes on the per-lane SOURCE address.
-template <int WMT>
+template <int WMT, int NWR>
 __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* st, int m0, int n0, int k0, int wave,
                                            int lane) {
-  using G = Geo<WMT>;
+  using G = Geo<WMT, NWR>;
   constexpr int XROWS = 1024 / FBK;  // pixel rows per DMA instruction
 #pragma unroll
   for (int u = 0; u < G::GLDS_X; ++u) {
-    const int q = wave + (FT / 64) * u;
+    const int q = wave + G::WAVES * u;
     const int row = XROWS * q + lane / XCH;
     const int pos = lane % XCH;
     const int ch = xpos(row, pos);  // xpos is an involution: the chunk stored at `pos`
@@ -156,8 +162,8 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
   constexpr int WINST = FBN / WROWS;       // instructions per plane
   const size_t plane = (size_t)p.N * p.Kp;
 #pragma unroll
-  for (int u = 0; u < GLDS_W; ++u) {
-    const int q = wave + (FT / 64) * u;
+  for (int u = 0; u < G::GLDS_W; ++u) {
+    const int q = wave + G::WAVES * u;
     const int pl = q / WINST;
     const int row = WROWS * (q % WINST) + lane / WCH;
     const int ch = wpos(row, lane % WCH);
@@ -170,15 +176,15 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
 // 2 = no DMA in the K loop (compute on stale LDS), 3 = no LDS reads (MFMA on register data)
 // TAIL = MFMA substeps of the last K-step (tail_substeps: only those holding k < K; chosen on the
 // host so the kernel carries one straight-line tail)
-template <int MODE, int WMT, int TAIL>
-__global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
-  using G = Geo<WMT>;
+template <int MODE, int WMT, int TAIL, int NWR>
+__global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
+  using G = Geo<WMT, NWR>;
   constexpr int STAGE = G::STAGE, GLDS_PER_STAGE = G::GLDS_PER_STAGE;
   __shared__ __attribute__((aligned(16))) unsigned char smem[G::SMEM];
   const int m0 = blockIdx.x * G::BM, n0 = blockIdx.y * FBN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave & 3, wn = wave >> 2;
+  const int wm = wave % NWR, wn = wave / NWR;
   const int h = lane >> 5, r32 = lane & 31;
 
   f32x16 acc[WMT][2];
@@ -258,7 +264,7 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
   const int nk = p.Kp / FBK;
 #pragma unroll
   for (int t = 0; t < NS - 1; ++t)
-    if (t < nk) issue_stage<WMT>(p, smem + t * STAGE, m0, n0, t * FBK, wave, lane);
+    if (t < nk) issue_stage<WMT, NWR>(p, smem + t * STAGE, m0, n0, t * FBK, wave, lane);
   // stage t % NS landed and visible; stage (t - 1) % NS free; ISSUE: refill it with K-step t+NS-1
   // (the main loop passes a compile-time true so its body stays one basic block)
   auto sync_step = [&](int t, auto issue_c) {
@@ -280,7 +286,7 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
     asm volatile("" ::: "memory");  // no LDS access moves across the barrier
     if constexpr (MODE != 2 && MODE != 4 && decltype(issue_c)::value) {
       if (NS == 2 || t + NS - 1 < nk)
-        issue_stage<WMT>(p, smem + ((t + NS - 1) % NS) * STAGE, m0, n0, (t + NS - 1) * FBK, wave, lane);
+        issue_stage<WMT, NWR>(p, smem + ((t + NS - 1) % NS) * STAGE, m0, n0, (t + NS - 1) * FBK, wave, lane);
     }
   };
   for (int t = 0; t + 1 < nk; ++t) {  // NS == 2: K-step t + 1 always exists here
@@ -293,32 +299,33 @@ __global__ void __launch_bounds__(FT) u8_fwd_kernel(FwdParams p) {
   }
 
   // epilogue: relu(scale * acc + bias), transposed through LDS so that every lane stores whole
-  // 16-byte row pieces, 64 rows of the wave tile at a time (64 x 64 fp32 = 16 KiB per wave; the 8
-  // waves' pieces reuse 128 KiB of stage buffers, free after the barrier that ended the last K-step)
+  // 16-byte row pieces, EPR rows of the wave tile at a time (EPR x 64 fp32 per wave; the waves'
+  // pieces reuse the stage buffers, free after the barrier that ended the last K-step)
   __syncthreads();
-  float* T = reinterpret_cast<float*>(smem) + wave * 64 * 64;
+  constexpr int EPR = G::EPR, NI2 = EPR / 32;
+  float* T = reinterpret_cast<float*>(smem) + wave * EPR * 64;
   float bv[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bv[j] = p.bias ? p.bias[n0 + wn * 64 + 32 * j + r32] : 0.f;
 #pragma unroll
-  for (int ip = 0; ip < WMT / 2; ++ip) {
+  for (int ip = 0; ip < WMT / NI2; ++ip) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous piece's reads are done
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int i2 = 0; i2 < 2; ++i2)
+      for (int i2 = 0; i2 < NI2; ++i2)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float y = acc[2 * ip + i2][j][r] * p.scale + bv[j];
+          float y = acc[NI2 * ip + i2][j][r] * p.scale + bv[j];
           if (p.relu) y = fmaxf(y, 0.f);
           T[(32 * i2 + (r & 3) + 8 * (r >> 2) + 4 * h) * 64 + 32 * j + r32] = y;
         }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's piece is in LDS (wave-private region)
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < EPR / 4; ++q) {
       const int rr = 4 * q + (lane >> 4);
-      const int row = m0 + wm * 32 * WMT + 64 * ip + rr;
+      const int row = m0 + wm * 32 * WMT + EPR * ip + rr;
       const f32x4 v = *reinterpret_cast<const f32x4*>(T + rr * 64 + 4 * (lane & 15));
       if constexpr (MODE == 6) {  // timing only: no global stores (keep the values alive)
         if (v[0] == 12345.f && row < 0) *reinterpret_cast<f32x4*>(p.C) = v;
@@ -778,25 +785,36 @@ void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short*
     const char* e = getenv("SDML_U8_FWD_WMT");
     return e ? atoi(e) : 0;
   }();
-  // 512-row blocks (half the LDS weight traffic per MFMA) once they still cover every CU
-  const int wmt = wmt_env ? wmt_env : (M >= 256 * Geo<4>::BM ? 4 : 2);
-  const int bm = wmt == 4 ? Geo<4>::BM : Geo<2>::BM;
+  static const int waves_env = [] {  // 8 (512 threads) or 16 (1024 threads, 4 waves per SIMD)
+    const char* e = getenv("SDML_U8_FWD_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  // 512-row blocks (half the LDS weight traffic per MFMA) once they still cover every CU, as 16
+  // waves of 64 x 64 (4 waves per SIMD at 115 VGPRs; 8 waves of 128 x 64 need 199: 63.9-65.3 vs
+  // 66.5-67.3 us at 131072 rows, tools/gpu_fwd16.sh); smaller batches: 256-row blocks of 8 waves
+  const bool big = M >= 256 * Geo<4>::BM;
+  const bool w16 = waves_env ? waves_env == 16 : (big && !wmt_env);
+  int wmt = wmt_env ? wmt_env : (big ? 4 : 2);
+  if (w16) wmt = 2;
+  const int bm = w16 ? Geo<2, 8>::BM : (wmt == 4 ? Geo<4>::BM : Geo<2>::BM);
   const dim3 grid((M + bm - 1) / bm, N / FBN);
   const int tail = tail_substeps(K);
-#define FWD_LAUNCH(MD, W, T) hipLaunchKernelGGL((u8_fwd_kernel<MD, W, T>), grid, dim3(FT), 0, stream, p)
-#define FWD_TAILS(W)                  \
-  do {                                \
-    switch (tail) {                   \
-      case 1: FWD_LAUNCH(0, W, 1); break; \
-      case 2: FWD_LAUNCH(0, W, 2); break; \
-      case 3: FWD_LAUNCH(0, W, 3); break; \
-      default: FWD_LAUNCH(0, W, NSUB);    \
-    }                                 \
+#define FWD_LAUNCH(MD, W, T, R) \
+  hipLaunchKernelGGL((u8_fwd_kernel<MD, W, T, R>), grid, dim3(Geo<W, R>::THREADS), 0, stream, p)
+#define FWD_TAILS(W, R)                          \
+  do {                                           \
+    switch (tail) {                              \
+      case 1: FWD_LAUNCH(0, W, 1, R); break;     \
+      case 2: FWD_LAUNCH(0, W, 2, R); break;     \
+      case 3: FWD_LAUNCH(0, W, 3, R); break;     \
+      default: FWD_LAUNCH(0, W, NSUB, R);        \
+    }                                            \
   } while (0)
-#define FWD_MODE(MD)                           \
-  do {                                         \
-    if (wmt == 4) FWD_LAUNCH(MD, 4, NSUB);     \
-    else FWD_LAUNCH(MD, 2, NSUB);              \
+#define FWD_MODE(MD)                                \
+  do {                                              \
+    if (w16) FWD_LAUNCH(MD, 2, NSUB, 8);            \
+    else if (wmt == 4) FWD_LAUNCH(MD, 4, NSUB, 4);  \
+    else FWD_LAUNCH(MD, 2, NSUB, 4);                \
   } while (0)  // timing modes: full last K-step
   if (mode == 1) FWD_MODE(1);
   else if (mode == 2) FWD_MODE(2);
@@ -804,8 +822,9 @@ void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short*
   else if (mode == 4) FWD_MODE(4);
   else if (mode == 5) FWD_MODE(5);
   else if (mode == 6) FWD_MODE(6);
-  else if (wmt == 4) FWD_TAILS(4);
-  else FWD_TAILS(2);
+  else if (w16) FWD_TAILS(2, 8);
+  else if (wmt == 4) FWD_TAILS(4, 4);
+  else FWD_TAILS(2, 4);
 #undef FWD_TAILS
 #undef FWD_MODE
 #undef FWD_LAUNCH

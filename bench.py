@@ -18,7 +18,8 @@ Placement ("rotate" pipeline; weak scaling: per-GPU work fixed at --batch_per_gp
 Data: synthetic MNIST-shape images stored as uint8 bytes, the way MNIST ships them (``--pixels u8``,
 default). ToTensor's /255, which the reference runs on the host per batch
 (/root/reference/simple_distributed.py:87-88), is folded into fc1's fp32-accurate GEMM (the bytes
-are exact in one bf16 plane; README "uint8 pixels"). ``--pixels f32`` stores float32 images instead.
+are exact in fp16, the weights two fp16 planes within one fp32 ulp; README "uint8 pixels").
+``--pixels f32`` stores float32 images instead.
 
 Timing contract: W untimed warm-up steps; barrier + device sync; K timed steps (each a full
 forward + backward + gradient sync + optimizer step over fresh data); barrier + device sync;
@@ -189,6 +190,8 @@ def main():
                 "batch_per_gpu": a.batch_per_gpu,
                 "optimizer": "SGD lr=0.1 momentum=0.5",
                 "pixels": a.pixels,
+                "gemm_numerics": ("fp32-accurate: fp32 operands as exact hi+lo fp16 planes (within one fp32 ulp) "
+                                  "or 3 bf16 planes, fp32 accumulation (README 'Two fp16 planes')"),
             },
             "baseline": BASELINE_NOTE,
             "final_loss": None if loss is None else round(loss, 5),

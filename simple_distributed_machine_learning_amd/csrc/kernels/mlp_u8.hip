@@ -446,6 +446,8 @@ struct WgradParams {
   const float* w2;           // [C][N]
   const float* h;            // [M][N]
   int C;                     // <= 16
+  int groups, splits;        // N / GHN hidden groups x row splits (1-D grid, XCD-aware order)
+  int xcd;                   // 0: plain order (split-major), A/B only (SDML_U8_WGRAD_XCD=0)
 };
 
 // dx tile of head_xent.hip's MFMA head (dx_t / head_mfma_dx_from_dl_kernel), reproduced operation
@@ -468,8 +470,13 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) u16 smem[2 * GBUF_U16];
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int n0 = blockIdx.x * GHN;
-  const int split = blockIdx.y;
+  // XCD-aware order: the hidden groups of one row split read the same pixel rows, so they are given
+  // block ids 8 apart (same XCD under the round-robin dispatch, one L2) and run side by side:
+  // L = 8 G (s / 8) + 8 g + s % 8. Ids past the last split (splits rounded up to 8) exit here.
+  const int L = blockIdx.x, G8 = 8 * p.groups;
+  const int split = p.xcd ? (L / G8) * 8 + L % 8 : L / p.groups;
+  if (split >= p.splits) return;
+  const int n0 = (p.xcd ? (L % G8) / 8 : L % p.groups) * GHN;
   const int r0 = split * p.rows_per_split;
   const int nk = min(p.rows_per_split, p.M - r0) / GBK;  // host: M % GBK == 0
 
@@ -678,6 +685,14 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
 
 // substeps of the last K-step that hold k < K (lane half 0 covers its first FBK / 2 k; the rest
 // multiply zero-padded weights)
+static int wgrad_xcd() {
+  static const int v = [] {
+    const char* e = getenv("SDML_U8_WGRAD_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 static int tail_substeps(int K) {
   const int v = K - ((K + FBK - 1) / FBK - 1) * FBK;
   if (v > FBK / 2 - 8) return NSUB;
@@ -728,7 +743,10 @@ void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, fl
   p.scale = scale;
   const int splits = u8_wgrad_splits(M, N);
   p.rows_per_split = ((M + splits - 1) / splits + GBK - 1) / GBK * GBK;
-  hipLaunchKernelGGL(u8_wgrad_kernel<false>, dim3(N / GHN, splits), dim3(GT), 0, stream, p);
+  p.groups = N / GHN;
+  p.splits = splits;
+  p.xcd = wgrad_xcd();
+  hipLaunchKernelGGL(u8_wgrad_kernel<false>, dim3(((splits + 7) / 8) * 8 * p.groups), dim3(GT), 0, stream, p);
   slab_reduce(slab, (int64_t)N * GKC + N, splits, gwb, (int64_t)N * GKC + N, stream);
 }
 
@@ -753,7 +771,10 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const 
   p.C = C;
   const int splits = u8_wgrad_splits(M, N);
   p.rows_per_split = ((M + splits - 1) / splits + GBK - 1) / GBK * GBK;
-  hipLaunchKernelGGL(u8_wgrad_kernel<true>, dim3(N / GHN, splits), dim3(GT), 0, stream, p);
+  p.groups = N / GHN;
+  p.splits = splits;
+  p.xcd = wgrad_xcd();
+  hipLaunchKernelGGL(u8_wgrad_kernel<true>, dim3(((splits + 7) / 8) * 8 * p.groups), dim3(GT), 0, stream, p);
   slab_reduce(slab, (int64_t)N * GKC + N, splits, gwb, (int64_t)N * GKC + N, stream);
 }
 

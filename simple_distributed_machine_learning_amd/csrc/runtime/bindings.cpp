@@ -2,12 +2,14 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
 #include <vector>
 
 #include "schedule.h"
+#include "synth_fill.h"
 #include "synth_hash.h"
 
 namespace py = pybind11;
@@ -62,24 +64,11 @@ py::dict stats_dict(const SimStats& s) {
 // [start, start+n) — host twin of the HIP generator (bit-identical).
 void synth_fill(uint64_t seed, int64_t start, int64_t n, int H, int W, int mode, uintptr_t x_ptr,
                 uintptr_t y_ptr) {
-  float* x = reinterpret_cast<float*>(x_ptr);
-  int64_t* y = reinterpret_cast<int64_t*>(y_ptr);
-  const int D = H * W;
   unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
   if (n < 4096) nt = 1;
-  std::vector<std::thread> th;
-  auto work = [&](unsigned t) {
-    for (int64_t i = t; i < n; i += nt) {
-      uint64_t smp = (uint64_t)(start + i);
-      if (y) y[i] = sdml::synth_label(seed, smp);
-      if (x)
-        for (int p = 0; p < D; ++p) x[i * D + p] = sdml::synth_pixel(seed, smp, p, H, W, mode);
-    }
-  };
   py::gil_scoped_release nogil;
-  for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
-  work(0);
-  for (auto& t : th) t.join();
+  sdml::synth_fill_host(seed, start, n, H, W, mode, reinterpret_cast<float*>(x_ptr), reinterpret_cast<int64_t*>(y_ptr),
+                        nt);
 }
 
 }  // namespace

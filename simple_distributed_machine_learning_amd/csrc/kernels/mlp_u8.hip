@@ -20,8 +20,9 @@
 // alternatives (on the 3-plane bf16 form): 32-deep K-steps in a 4-stage ring (3 K-steps in flight),
 // slower (102.6 vs 93.8 us at the headline shape: half the MFMAs per barrier); weight fragments of
 // substep s+1 pinned ahead of substep s's MFMAs with sched_barrier (register double buffer),
-// 2-3 % slower than the compiler's own placement; 1024-thread blocks of 512 rows (W staged once
-// per CU instead of twice) do not fit 4 waves per SIMD: 128 VGPRs with ~400 spilled.
+// 2-3 % slower than the compiler's own placement; 1024-thread blocks of 512 rows did not fit 4 waves
+// per SIMD with 3 planes (~400 VGPRs spilled at 128) - with 2 planes they need 115 and are the
+// default for large batches (62-65 vs 66.5-67.3 us for 8 waves of 128 x 64).
 // The LDS images are swizzled on the DMA's per-lane source address (the DMA writes 1 KiB
 // lane-linearly) so the fragment ds_read_b128s are conflict-free; k order inside a K-step is
 // permuted identically for both operands (lane half h, substep s, element j <-> k = 32h + 8s + j),
@@ -97,9 +98,6 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-__device__ __forceinline__ u16 bf16_bits(float f) { return __builtin_bit_cast(u16, static_cast<__bf16>(f)); }
-__device__ __forceinline__ float bf16_val(u16 b) { return __uint_as_float(((unsigned)b) << 16); }
-
 // 8 bytes -> 8 fp16 (exact): a byte permute puts b under the exponent of 1024 (fp16 0x6400 | b ==
 // 1024 + b), one packed subtract per pair removes the 1024
 __device__ __forceinline__ f16x2 h2_of(unsigned v, unsigned sel) {
@@ -112,20 +110,6 @@ __device__ __forceinline__ f16x8 widen8h(unsigned lo, unsigned hi) {
   return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
 }
 
-// 8 bytes -> 8 bf16 (exact: (float)b has its significant bits in the upper half)
-__device__ __forceinline__ bf16x8 widen8(unsigned lo, unsigned hi) {
-  bf16x8 r;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    r[e] = (short)(__float_as_uint((float)((lo >> (8 * e)) & 0xffu)) >> 16);
-    r[4 + e] = (short)(__float_as_uint((float)((hi >> (8 * e)) & 0xffu)) >> 16);
-  }
-  return r;
-}
-
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
 __device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }

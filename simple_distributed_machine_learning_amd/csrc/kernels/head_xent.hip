@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "head_reduce.h"
 #include "kernels.h"
 
 namespace sdml {
@@ -247,46 +248,10 @@ __global__ void __launch_bounds__(HTHR) head_fused_kernel(const float* __restric
   }
 }
 
-// sum the per-block slabs: out[o] += sum_b part[b][o]   (fixed order -> deterministic).
-// Block = 64 outputs x 16 waves; wave w sums slabs b = w, w+16, ... with 16 loads in flight,
-// then the 16 wave partials are added in LDS in wave order.
-__global__ void __launch_bounds__(1024) head_reduce_kernel(const float* __restrict__ part, int nblocks, int CK, int C,
-                                                           float* __restrict__ gW, float* __restrict__ gb,
-                                                           float* __restrict__ stats, int flags) {
-  // flags: bit 0 = training (accumulate gW/gb), bit 1 = overwrite stats instead of adding
-  const int train = flags & 1;
+// sum the per-block slabs: out[o] += sum_b part[b][o] (fixed order -> deterministic), head_reduce.h
+__global__ void __launch_bounds__(1024) head_reduce_kernel(HeadReduceArgs a) {
   __shared__ float acc[16][64];
-  const int width = CK + C + 2;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int o = blockIdx.x * 64 + lane;
-  float s = 0.f;
-  if (o < width) {  // 16 loads in flight per lane (512 slabs: two round trips per wave)
-    float v[16];
-    int b = w;
-    for (; b + 16 * 15 < nblocks; b += 16 * 16) {
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = part[(size_t)(b + 16 * u) * width + o];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) s += v[u];
-    }
-    for (; b < nblocks; b += 16) s += part[(size_t)b * width + o];
-  }
-  acc[w][lane] = s;
-  __syncthreads();
-  if (w == 0 && o < width) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t += acc[i][lane];
-    if (o < CK) {
-      if (train) gW[o] += t;
-    } else if (o < CK + C) {
-      if (train) gb[o - CK] += t;
-    } else if (flags & 2) {
-      stats[o - CK - C] = t;
-    } else {
-      stats[o - CK - C] += t;
-    }
-  }
+  head_reduce_block(a, blockIdx.x, acc);
 }
 
 // grid-stride, one wave per row at a time, any K / C <= 32: loss/correct, dz (to dz_out) and
@@ -971,11 +936,17 @@ void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx,
   }
 }
 
+void head_reduce_run(const HeadReduceArgs& a, hipStream_t stream) {
+  if (!a.part) return;
+  hipLaunchKernelGGL(head_reduce_kernel, dim3(head_reduce_blocks(a)), dim3(1024), 0, stream, a);
+}
+
 void head_logsoftmax_nll(const float* x, const float* W, const float* b, const int64_t* target, int M, int K, int C,
                          float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
                          float* workspace, bool mask_dx, hipStream_t stream, float* dl, bool stats_overwrite,
-                         float* dx_amax, int* n_amax) {
+                         float* dx_amax, int* n_amax, HeadReduceArgs* defer) {
   if (n_amax) *n_amax = 0;
+  if (defer) *defer = HeadReduceArgs();
   if (M <= 0) {
     if (stats_overwrite) (void)hipMemsetAsync(stats, 0, 2 * sizeof(float), stream);
     return;
@@ -995,9 +966,17 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
       default: HEAD_MFMA(16); break;
     }
 #undef HEAD_MFMA
-    const int width = C * K + C + 2;
-    hipLaunchKernelGGL(head_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, stream, workspace, blocks, C * K,
-                       C, gW, gb, stats, rflags);
+    HeadReduceArgs ra;
+    ra.part = workspace;
+    ra.nblocks = blocks;
+    ra.CK = C * K;
+    ra.C = C;
+    ra.gW = gW;
+    ra.gb = gb;
+    ra.stats = stats;
+    ra.flags = rflags;
+    if (defer) *defer = ra;  // the caller runs it (u8_wgrad_dl's reduction, or head_reduce_run)
+    else head_reduce_run(ra, stream);
     return;
   }
   if (head_fused_supported(K, C) && dz_out == nullptr && workspace != nullptr) {
@@ -1018,9 +997,16 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
         break;
     }
 #undef HEAD_LAUNCH
-    const int width = C * K + C + 2;
-    hipLaunchKernelGGL(head_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, stream, workspace, blocks, C * K,
-                       C, gW, gb, stats, rflags);
+    HeadReduceArgs ra;
+    ra.part = workspace;
+    ra.nblocks = blocks;
+    ra.CK = C * K;
+    ra.C = C;
+    ra.gW = gW;
+    ra.gb = gb;
+    ra.stats = stats;
+    ra.flags = rflags;
+    head_reduce_run(ra, stream);
     return;
   }
   if (dl) abort();  // host contract: the dlogits output exists on the fused path only (head_fused_supported)
@@ -1030,9 +1016,16 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
     if (gW && gb && workspace && dz_out == nullptr) {
       hipLaunchKernelGGL((head_lds_kernel<10, true>), dim3(lblocks), dim3(256), lds, stream, x, W, b, target, M, K,
                          scale, stats, dx, nullptr, mask_dx ? 1 : 0, workspace);
-      const int width = C * K + C + 2;
-      hipLaunchKernelGGL(head_reduce_kernel, dim3((width + 63) / 64), dim3(1024), 0, stream, workspace, lblocks, C * K,
-                         C, gW, gb, stats, 1 | (stats_overwrite ? 2 : 0));
+      HeadReduceArgs ra;
+      ra.part = workspace;
+      ra.nblocks = lblocks;
+      ra.CK = C * K;
+      ra.C = C;
+      ra.gW = gW;
+      ra.gb = gb;
+      ra.stats = stats;
+      ra.flags = 1 | (stats_overwrite ? 2 : 0);
+      head_reduce_run(ra, stream);
     } else {
       if (stats_overwrite) (void)hipMemsetAsync(stats, 0, 2 * sizeof(float), stream);  // this variant adds
       hipLaunchKernelGGL((head_lds_kernel<10, false>), dim3(lblocks), dim3(256), lds, stream, x, W, b, target, M, K,

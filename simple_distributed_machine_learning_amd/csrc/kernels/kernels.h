@@ -7,6 +7,19 @@
 
 namespace sdml {
 
+// The head's deferred slab reduction (head_logsoftmax_nll with `defer`): the per-block slabs and where
+// they sum to. head_reduce_run launches it alone; u8_wgrad_dl runs it in the same launch as its own
+// slab reduction.
+struct HeadReduceArgs {
+  const float* part = nullptr;  // [nblocks][CK + C + 2]; nullptr: nothing deferred
+  int nblocks = 0, CK = 0, C = 0;
+  float* gW = nullptr;
+  float* gb = nullptr;
+  float* stats = nullptr;
+  int flags = 0;  // bit 0 = training (accumulate gW/gb), bit 1 = overwrite stats
+};
+void head_reduce_run(const HeadReduceArgs& a, hipStream_t stream);
+
 // ---- fp32 MFMA GEMM ------------------------------------------------------------------------
 // C[M,N] (op)= sum_k A(m,k) * B(n,k)
 //   A(m,k) = A[m*lda + k]        (a_kmajor = false)   or A[k*lda + m]   (a_kmajor = true)
@@ -106,8 +119,10 @@ void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, fl
 // (namax == 0) each workgroup bounds its dz by max_row sum_c |dl| * max |w2|. With the same amax the
 // result is bit-identical to head_dx_from_dl + u8_wgrad.
 bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const void* h, int C);
+// head (optional): a deferred head reduction run in the same launch as this one's slab reduction
 void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const unsigned char* X, int M, int N, int ldx,
-                 float* slab, float* gwb, float scale, const float* amax, int namax, hipStream_t stream);
+                 float* slab, float* gwb, float scale, const float* amax, int namax, hipStream_t stream,
+                 const HeadReduceArgs* head = nullptr);
 // out[i] += sum_s slab[s * stride + i] in split order (n % 4 == 0, 16-B aligned)
 void slab_reduce(const float* slab, int64_t stride, int splits, float* out, int64_t n, hipStream_t stream);
 
@@ -129,7 +144,7 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
                          int C, float scale, float* stats, float* dx, float* gW, float* gb, float* dz_out,
                          float* workspace, bool mask_dx, hipStream_t stream, float* dl = nullptr,
                          bool stats_overwrite = false,  // stats_overwrite: stats = this call's totals
-                         float* dx_amax = nullptr, int* n_amax = nullptr);
+                         float* dx_amax = nullptr, int* n_amax = nullptr, HeadReduceArgs* defer = nullptr);
 // dx_amax (capacity kHeadAmaxMax floats): where the MFMA head path writes per-block bounds on |dx|
 // (*n_amax of them; 0 when another head variant ran) - the uint8 weight gradient's dz bound
 constexpr int kHeadAmaxMax = 512;

@@ -38,6 +38,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "head_reduce.h"
 #include "kernels.h"
 #include "u8_planes.h"
 
@@ -665,6 +666,40 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   }
 }
 
+// The step's two deterministic reductions in one launch: blocks [0, nslab) sum the weight
+// gradient's split slabs (64 float4 columns per block, 16 waves over the splits w, w + 16, ..., wave
+// partials added in wave order), the blocks after them run the fused head's reduction (head_reduce.h).
+// Saves the head reduction's own launch (~5 us of latency-bound work) on the one-rank MLP step.
+__global__ void __launch_bounds__(1024) slab_head_reduce_kernel(const float* __restrict__ slab, int64_t stride,
+                                                                int splits, float* __restrict__ out, int64_t n,
+                                                                int nslab, HeadReduceArgs head) {
+  __shared__ f32x4 part[16][64];
+  if ((int)blockIdx.x >= nslab) {
+    head_reduce_block(head, blockIdx.x - nslab, reinterpret_cast<float(*)[64]>(&part[0][0]));
+    return;
+  }
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t i = ((int64_t)blockIdx.x * 64 + l) * 4;
+  f32x4 a[4] = {};
+  if (i < n) {
+    int s = w;  // wave w: splits w, w + 16, ...
+    for (; s + 16 * 7 < splits; s += 16 * 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u & 3] += *reinterpret_cast<const f32x4*>(slab + (int64_t)(s + 16 * u) * stride + i);
+    }
+    for (; s < splits; s += 16) a[0] += *reinterpret_cast<const f32x4*>(slab + (int64_t)s * stride + i);
+  }
+  part[w][l] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (w == 0 && i < n) {
+    f32x4 acc = *reinterpret_cast<const f32x4*>(out + i);
+    f32x4 t = part[0][l];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) t += part[q][l];
+    *reinterpret_cast<f32x4*>(out + i) = acc + t;
+  }
+}
+
 }  // namespace
 
 // substeps of the last K-step that hold k < K (lane half 0 covers its first FBK / 2 k; the rest
@@ -739,7 +774,8 @@ bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const vo
 }
 
 void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const unsigned char* X, int M, int N, int ldx,
-                 float* slab, float* gwb, float scale, const float* amax, int namax, hipStream_t stream) {
+                 float* slab, float* gwb, float scale, const float* amax, int namax, hipStream_t stream,
+                 const HeadReduceArgs* head) {
   WgradParams p{};
   p.amax = namax > 0 ? amax : nullptr;
   p.namax = namax;
@@ -759,7 +795,14 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const 
   p.splits = splits;
   p.xcd = wgrad_xcd();
   hipLaunchKernelGGL(u8_wgrad_kernel<true>, dim3(((splits + 7) / 8) * 8 * p.groups), dim3(GT), 0, stream, p);
-  slab_reduce(slab, (int64_t)N * GKC + N, splits, gwb, (int64_t)N * GKC + N, stream);
+  const int64_t n = (int64_t)N * GKC + N;
+  if (head && head->part) {
+    const int nslab = (int)((n / 4 + 63) / 64);
+    hipLaunchKernelGGL(slab_head_reduce_kernel, dim3(nslab + head_reduce_blocks(*head)), dim3(1024), 0, stream, slab, n,
+                       splits, gwb, n, nslab, *head);
+  } else {
+    slab_reduce(slab, n, splits, gwb, n, stream);
+  }
 }
 
 void split_planes_pad(const float* w, unsigned short* out, int N, int K, int Kp, hipStream_t stream) {

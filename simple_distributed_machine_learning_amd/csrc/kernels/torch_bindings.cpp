@@ -664,9 +664,27 @@ HeadOut head_logsoftmax_nll_f32(
 // (dx = dl @ w, rebuilt by head_dx_from_dl wherever w is held); gw/gb accumulated, loss and correct
 // count accumulated into stats_acc [2] (overwritten with stats_init). Returns (dl, bound or None):
 // the MFMA head's per-block bounds on |dl @ w| (what linear_wgrad_u8_dl takes as amax)
-std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_dl_f32(torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor target,
-                                         torch::Tensor gw, torch::Tensor gb, double scale, torch::Tensor stats_acc,
-                                         bool stats_init) {
+// A head reduction deferred by head_logsoftmax_nll_dl_f32(defer_reduce=True): keeps the slab workspace
+// (and the outputs) alive until it runs - inside linear_wgrad_u8_dl's reduction launch, or alone via
+// run() - exactly once.
+struct HeadPending {
+  sdml::HeadReduceArgs args;
+  torch::Tensor ws, gw, gb, stats;
+  bool pending() const { return args.part != nullptr; }
+  void run() {
+    if (!pending()) return;
+    sdml::head_reduce_run(args, cur_stream());
+    done();
+  }
+  void done() {
+    args = sdml::HeadReduceArgs();
+    ws = torch::Tensor();
+  }
+};
+
+std::tuple<torch::Tensor, c10::optional<torch::Tensor>, std::shared_ptr<HeadPending>> head_logsoftmax_nll_dl_f32(
+    torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor target, torch::Tensor gw, torch::Tensor gb,
+    double scale, torch::Tensor stats_acc, bool stats_init, bool defer_reduce) {
   check_f32_cuda(x, "x");
   check_f32_cuda(w, "w");
   check_f32_cuda(b, "b");
@@ -683,17 +701,26 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> head_logsoftmax_nll_dl_f
   auto dl = torch::empty({M, C}, x.options());
   if (M == 0) {
     if (stats_init) stats_acc.zero_();
-    return {dl, c10::nullopt};
+    return {dl, c10::nullopt, nullptr};
   }
   auto ws = torch::empty({(int64_t)sdml::head_workspace_floats(M, K, C)}, x.options());
   auto am = torch::empty({sdml::kHeadAmaxMax}, x.options());
   int n_am = 0;
+  auto pend = std::make_shared<HeadPending>();
   sdml::head_logsoftmax_nll(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), target.data_ptr<int64_t>(),
                             M, K, C, (float)scale, stats_acc.data_ptr<float>(), nullptr, gw.data_ptr<float>(),
                             gb.data_ptr<float>(), nullptr, ws.data_ptr<float>(), false, cur_stream(),
-                            dl.data_ptr<float>(), stats_init, am.data_ptr<float>(), &n_am);
-  if (n_am > 0) return {dl, am.narrow(0, 0, n_am)};
-  return {dl, c10::nullopt};
+                            dl.data_ptr<float>(), stats_init, am.data_ptr<float>(), &n_am,
+                            defer_reduce ? &pend->args : nullptr);
+  std::shared_ptr<HeadPending> out;
+  if (pend->pending()) {
+    pend->ws = ws;
+    pend->gw = gw;
+    pend->gb = gb;
+    pend->stats = stats_acc;
+    out = pend;
+  }
+  return {dl, n_am > 0 ? c10::optional<torch::Tensor>(am.narrow(0, 0, n_am)) : c10::nullopt, out};
 }
 
 // dx = (dl @ w) * (x > 0 if mask): the fused head's boundary gradient rebuilt from its factor
@@ -714,8 +741,10 @@ torch::Tensor head_dx_from_dl(torch::Tensor dl, torch::Tensor w, torch::Tensor x
 // first layer's weight gradient from the FACTORED boundary gradient: gw += scale * dz^T x_u8,
 // gb += colsum(dz) with dz = (dl @ w2) * (h > 0) - expanded inside mlp_u8.hip's wgrad kernel when
 // it applies (bit-identical to head_dx_from_dl followed by linear_wgrad_u8), else those two
+// head: a deferred head reduction (HeadPending) to run in this call's reduction launch (or before it)
 void linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, torch::Tensor h, torch::Tensor gw,
-                        torch::Tensor gb, double scale, c10::optional<torch::Tensor> amax) {
+                        torch::Tensor gb, double scale, c10::optional<torch::Tensor> amax,
+                        std::shared_ptr<HeadPending> head) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
               "linear_wgrad_u8_dl: x must be a contiguous 2-D uint8 ROCm tensor");
   check_f32_cuda(dl, "dl");
@@ -736,11 +765,15 @@ void linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, tor
       check_f32_cuda(*amax, "amax");
       TORCH_CHECK(amax->numel() >= 1 && amax->is_contiguous(), "linear_wgrad_u8_dl: amax must be non-empty");
     }
+    const bool fuse_head = head && head->pending();
     sdml::u8_wgrad_dl(dl.data_ptr<float>(), w2.data_ptr<float>(), h.data_ptr<float>(), (int)C, x.data_ptr<uint8_t>(),
                       (int)M, (int)N, (int)K, ws.data_ptr<float>(), gw.data_ptr<float>(), (float)scale,
-                      has_am ? amax->data_ptr<float>() : nullptr, has_am ? (int)amax->numel() : 0, cur_stream());
+                      has_am ? amax->data_ptr<float>() : nullptr, has_am ? (int)amax->numel() : 0, cur_stream(),
+                      fuse_head ? &head->args : nullptr);
+    if (fuse_head) head->done();
     return;
   }
+  if (head) head->run();
   torch::Tensor dz = sdml::head_fused_supported((int)N, (int)C) ? head_dx_from_dl(dl, w2, h, true)
                                                                   : at::matmul(dl, w2).mul_((h > 0).to(h.scalar_type()));
   linear_wgrad_u8(x, dz, gw, gb, scale, amax);
@@ -1116,11 +1149,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("head_logsoftmax_nll_dl_f32", &head_logsoftmax_nll_dl_f32,
         "fused head returning the boundary gradient as its factor dl = scale * (softmax - onehot)", py::arg("x"),
         py::arg("w"), py::arg("b"), py::arg("target"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
-        py::arg("stats_acc"), py::arg("stats_init") = false);
+        py::arg("stats_acc"), py::arg("stats_init") = false, py::arg("defer_reduce") = false);
+  py::class_<HeadPending, std::shared_ptr<HeadPending>>(m, "HeadPending")
+      .def("run", &HeadPending::run, "launch the deferred head reduction now (once)")
+      .def_property_readonly("pending", &HeadPending::pending);
   m.def("linear_wgrad_u8_dl", &linear_wgrad_u8_dl,
         "gw += scale * dz^T x_u8, gb += colsum(dz), dz = (dl @ w2) * (h > 0) (factored boundary gradient)",
         py::arg("x"), py::arg("dl"), py::arg("w2"), py::arg("h"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
-        py::arg("amax") = py::none());
+        py::arg("amax") = py::none(), py::arg("head") = nullptr);
   m.def("head_dx_from_dl", &head_dx_from_dl, "dx = (dl @ w) * (x > 0): boundary gradient from its factor",
         py::arg("dl"), py::arg("w"), py::arg("x"), py::arg("mask"));
   m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer (optionally also writing a "

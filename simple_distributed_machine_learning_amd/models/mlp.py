@@ -174,15 +174,19 @@ class MLPStage(PipelineStage):
     def supports_factored_grad(self) -> bool:
         return self.is_last and not self.is_first and len(self.layer_ids) == 1
 
-    def head_fwd_factored(self, x, target, loss_scale, stats, stats_init: bool = False):
-        """Training head_fwd + head_bwd in one call: returns (dl, count); loss/correct go to stats."""
+    def head_fwd_factored(self, x, target, loss_scale, stats, stats_init: bool = False, defer_reduce: bool = False):
+        """Training head_fwd + head_bwd in one call: returns (dl, count); loss/correct go to stats.
+        ``defer_reduce``: returns (dl, count, pending) with the head's gradient/stats reduction left to
+        ``pending`` (ops.linear_logsoftmax_nll_dl), which must reach :meth:`bwd_from_factor` or be run."""
         head = self.layers()[-1]
         x = x.reshape(x.shape[0], -1)
         if x.dtype != torch.float32 or not x.is_contiguous():
             x = x.float().contiguous()
-        dl = ops.linear_logsoftmax_nll_dl(x, head.weight, head.bias, target, head.weight.grad, head.bias.grad,
-                                          loss_scale, stats, stats_init)
-        return dl, target.numel()
+        out = ops.linear_logsoftmax_nll_dl(x, head.weight, head.bias, target, head.weight.grad, head.bias.grad,
+                                           loss_scale, stats, stats_init, defer_reduce=defer_reduce)
+        if defer_reduce:
+            return out[0], target.numel(), out[1]
+        return out, target.numel()
 
     def boundary_grad_from_factor(self, dl, x):
         """d(loss)/d(pre-activation of the producing stage) from the head's factor ``dl`` and the
@@ -194,17 +198,18 @@ class MLPStage(PipelineStage):
         """The weight the factored boundary gradient is expanded with (dx = dl @ W)."""
         return self.layers()[-1].weight.detach()
 
-    def bwd_from_factor(self, dl, w2, ctx) -> bool:
+    def bwd_from_factor(self, dl, w2, ctx, head_pending=None) -> bool:
         """Stage-0 backward fed by the factored boundary gradient dl (dz = (dl @ w2) * (h > 0), h this
         stage's output). A single uint8-fed layer takes it straight into its weight-gradient kernel
-        (dz never materialised); returns False (nothing done) for other stages."""
+        (dz never materialised; a deferred head reduction ``head_pending`` shares its reduction
+        launch); returns False (nothing done, ``head_pending`` untouched) for other stages."""
         acts = ctx.get("acts")
         layers = self.layers()
         if acts is None or len(layers) != 1 or acts[0].dtype != torch.uint8:
             return False
         ctx.pop("acts")
         lin = layers[0]
-        ops.linear_wgrad_u8_dl(acts[0], dl, w2, acts[1], lin.weight.grad, lin.bias.grad)
+        ops.linear_wgrad_u8_dl(acts[0], dl, w2, acts[1], lin.weight.grad, lin.bias.grad, head_pending=head_pending)
         return True
 
     def head_bwd(self, ctx):

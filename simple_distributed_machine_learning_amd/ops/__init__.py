@@ -87,19 +87,23 @@ def linear_wgrad_u8(x: torch.Tensor, gz: torch.Tensor, gw: torch.Tensor, gb: Opt
         gb += gz.sum(0)
 
 
-def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, amax: Optional[torch.Tensor] = None) -> None:
+def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, amax: Optional[torch.Tensor] = None, head_pending=None) -> None:
     """First-layer weight gradient from the FACTORED boundary gradient: with dz = (dl @ w2) * (h > 0)
     (dl [M, C] the head's factor, w2 [C, N] the head weight, h [M, N] this layer's ReLU output),
     gw += dz.T @ ToTensor(x), gb += sum(dz). On ROCm dz is expanded inside the weight-gradient kernel
     (never written to memory); with the same ``amax`` (a bound on |dz|, see :func:`linear_wgrad_u8`)
     bit-identical to :func:`head_dx_from_dlogits` + :func:`linear_wgrad_u8`; without it the bounds the
     fused head attached to the ``dl`` it returned, else each workgroup bounds dz by its rows'
-    max sum |dl| times max |w2| (a dl received over the network carries no attribute)."""
+    max sum |dl| times max |w2| (a dl received over the network carries no attribute).
+    ``head_pending``: a head reduction deferred by :func:`linear_logsoftmax_nll_dl`, run in the same
+    launch as this one's slab reduction (or before it, on the paths without one)."""
     if x.is_cuda:
         if amax is None:
             amax = getattr(dl, "_sdml_amax", None)
-        _k().linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, PIXEL_SCALE, amax)
+        _k().linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, PIXEL_SCALE, amax, head_pending)
         return
+    if head_pending is not None:
+        head_pending.run()
     with torch.no_grad():
         dz = (dl @ w2) * (h > 0).to(dl.dtype)
         gw += dz.t() @ pixels_to_float(x)
@@ -159,21 +163,28 @@ def linear_logsoftmax_nll(x, w, b, target, gw, gb, scale: float, need_dx: bool, 
     return loss, correct, dx
 
 
-def linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale: float, stats, stats_init: bool = False):
+def linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale: float, stats, stats_init: bool = False,
+                             defer_reduce: bool = False):
     """Training head (fc -> log_softmax -> NLL, backward) whose boundary gradient is returned as its
     rank-C factor ``dl = scale * (softmax - onehot)`` [M, C] instead of ``dx = dl @ w`` [M, K]
     (:func:`head_dx_from_dlogits` rebuilds dx bit-identically wherever ``w`` is held). gw/gb are
     accumulated; loss sum and correct count are accumulated into ``stats`` [2] (overwritten with
-    ``stats_init``)."""
+    ``stats_init``).
+
+    ``defer_reduce``: return ``(dl, pending)``; on ROCm the head's slab reduction (gw/gb/stats) is
+    then left to ``pending`` (None when nothing was deferred), which the caller MUST hand to
+    :func:`linear_wgrad_u8_dl` (``head_pending``: both reductions in one launch) or run itself
+    (``pending.run()``) before it reads gw/gb/stats."""
     if x.is_cuda:
-        dl, amax = _k().head_logsoftmax_nll_dl_f32(x, w, b, target, gw, gb, float(scale), stats, bool(stats_init))
+        dl, amax, pending = _k().head_logsoftmax_nll_dl_f32(x, w, b, target, gw, gb, float(scale), stats,
+                                                             bool(stats_init), bool(defer_reduce))
         if amax is not None:
             dl._sdml_amax = amax  # per-block bounds on |dl @ w| (linear_wgrad_u8_dl's dz bound)
-        return dl
+        return (dl, pending) if defer_reduce else dl
     with torch.no_grad():
         loss, correct, dl = ref.linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale)
     _put_stats(stats, loss, correct, stats_init)
-    return dl
+    return (dl, None) if defer_reduce else dl
 
 
 def head_dx_from_dlogits(dl, w, x, mask: bool = True):

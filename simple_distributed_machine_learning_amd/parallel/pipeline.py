@@ -460,6 +460,15 @@ class PipelineEngine:
         bgroup = mesh.pipe_group_bwd or group
         # stage 0 expands the factor itself when it can (MLP first layer on uint8 pixels)
         fuse0 = factored and hasattr(s0, "bwd_from_factor") and hasattr(s1, "factor_weight")
+        # one rank: the head's gradient/stats reduction is deferred into stage 0's weight-gradient
+        # reduction launch (one launch instead of two per wave); `pend[w]` must be consumed or run
+        defer = fuse0 and R == 1
+        pend = [None] * W
+
+        def run_pending(w):
+            if pend[w] is not None:
+                pend[w].run()
+                pend[w] = None
 
         def stage0_bwd(w):
             if bwork[w] is not None:
@@ -468,10 +477,15 @@ class PipelineEngine:
             gz = back[w]
             if factored and fuse0:  # the factor goes straight into stage 0's weight-gradient kernel
                 with tm.span("bwd", 0):
-                    done = s0.bwd_from_factor(gz, s1.factor_weight(), ctx0[w])
+                    if pend[w] is not None:
+                        done = s0.bwd_from_factor(gz, s1.factor_weight(), ctx0[w], head_pending=pend[w])
+                    else:
+                        done = s0.bwd_from_factor(gz, s1.factor_weight(), ctx0[w])
                 if done:
+                    pend[w] = None  # consumed (run inside the weight-gradient reduction)
                     hkeep[w] = back[w] = None
                     return
+                run_pending(w)
             if factored:
                 with tm.span("bwd", 1):
                     gz = s1.boundary_grad_from_factor(gz, hkeep[w])
@@ -494,7 +508,11 @@ class PipelineEngine:
                 tgt = tgt.to(dev, non_blocking=True)
             if tgt.numel() > 0 and factored:
                 with tm.span("fwd", 1):
-                    g, n = s1.head_fwd_factored(recv[w], tgt, scale, stats, stats_init=fresh)
+                    if defer:
+                        g, n, pend[w] = s1.head_fwd_factored(recv[w], tgt, scale, stats, stats_init=fresh,
+                                                             defer_reduce=True)
+                    else:
+                        g, n = s1.head_fwd_factored(recv[w], tgt, scale, stats, stats_init=fresh)
                 fresh = False
                 count += n
             elif tgt.numel() > 0:
@@ -534,6 +552,8 @@ class PipelineEngine:
             if not interleave:
                 for w in range(W):
                     stage0_bwd(w)
+            for w in range(W):  # (nothing is left unless a stage-0 backward was skipped)
+                run_pending(w)
             self.grad_sync.stage_done(0)
             with tm.span("grad_sync"):
                 self.grad_sync.finish()

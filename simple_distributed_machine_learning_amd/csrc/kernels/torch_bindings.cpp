@@ -243,7 +243,9 @@ void linear_wgrad_u8(torch::Tensor x, torch::Tensor gz, torch::Tensor gw, c10::o
   if (!legacy_wgrad && gb_follows && sdml::u8_wgrad_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr(),
                                                                gz.data_ptr())) {
     auto ws = torch::empty({sdml::u8_wgrad_slab_floats((int)M, (int)N)}, gw.options());
-    torch::Tensor am = amax.has_value() && amax->defined() ? *amax : gz.abs().amax().reshape({1});
+    // (no bound given: one reduction pass over gz, its inf-norm; abs().amax() would also write |gz|)
+    torch::Tensor am =
+        amax.has_value() && amax->defined() ? *amax : at::linalg_vector_norm(gz, INFINITY).reshape({1});
     check_f32_cuda(am, "amax");
     TORCH_CHECK(am.numel() >= 1 && am.is_contiguous(), "linear_wgrad_u8: amax must be a non-empty contiguous tensor");
     sdml::u8_wgrad(gz.data_ptr<float>(), x.data_ptr<uint8_t>(), (int)M, (int)N, (int)K, ws.data_ptr<float>(),

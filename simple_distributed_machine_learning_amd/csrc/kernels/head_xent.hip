@@ -599,7 +599,9 @@ __device__ __forceinline__ f32x4m dx_t(const float (&w4)[4], const float (&dz)[4
   return o;
 }
 
-template <int C>
+// DXP = false: no dx pass (the factored form writes dl instead, or evaluation): the dx operands
+// (wd, 32 VGPRs) are not loaded
+template <int C, bool DXP>
 __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __restrict__ x, const float* __restrict__ W,
                                                             const float* __restrict__ bias,
                                                             const int64_t* __restrict__ target, int M, float scale,
@@ -626,7 +628,7 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
 #pragma unroll
   for (int u = 0; u < 8; ++u) wl[u] = *reinterpret_cast<const f32x4m*>(ws + r * WSP + 16 * u + 4 * g);
   float wd[8][4];
-  load_wd(ws, r, g, wd);
+  if constexpr (DXP) load_wd(ws, r, g, wd);
   f32x4m bv;
 #pragma unroll
   for (int v = 0; v < 4; ++v) bv[v] = (4 * g + v) < C ? bias[4 * g + v] : 0.f;
@@ -698,7 +700,7 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
       sa += __shfl_xor(sa, 32);
       amx = fmaxf(amx, sa);
     }
-    if (dx) {
+    if (DXP && dx) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const f32x4m o = dx_t(wd[t], dz, xv[t], mask_dx);
@@ -772,12 +774,12 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
   }
   __syncthreads();
   static_assert(MW == 4, "wave-partial sums below are written for 4 waves");
-  if (dxmax && wave == 0) {  // times max |W| over the staged classes (wd: every class and hidden unit)
+  if (dxmax && wave == 0) {  // times max |W| over the staged classes (wl: every class and hidden unit)
     float wm = 0.f;
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+    for (int u = 0; u < 8; ++u)
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) wm = fmaxf(wm, fabsf(wd[t][kk]));
+      for (int e = 0; e < 4; ++e) wm = fmaxf(wm, fabsf(wl[u][e]));
     for (int off = 32; off > 0; off >>= 1) wm = fmaxf(wm, __shfl_xor(wm, off));
     if (tid == 0) dxmax[blockIdx.x] = 2.f * fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3])) * wm;
   }
@@ -957,9 +959,15 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
     const int blocks = head_mfma_blocks(M, &tpw);
     float* amx = ((dx || dl) && dx_amax && n_amax) ? dx_amax : nullptr;
     if (amx) *n_amax = blocks;
-#define HEAD_MFMA(CC)                                                                                              \
-  hipLaunchKernelGGL((head_mfma_kernel<CC>), dim3(blocks), dim3(64 * MW), 0, stream, x, W, b, target, M, scale, workspace, \
-                     dx, tpw, mask_dx ? 1 : 0, dl, amx)
+#define HEAD_MFMA(CC)                                                                                          \
+  do {                                                                                                     \
+    if (dx)                                                                                                \
+      hipLaunchKernelGGL((head_mfma_kernel<CC, true>), dim3(blocks), dim3(64 * MW), 0, stream, x, W, b, target, M, \
+                         scale, workspace, dx, tpw, mask_dx ? 1 : 0, dl, amx);                              \
+    else                                                                                                   \
+      hipLaunchKernelGGL((head_mfma_kernel<CC, false>), dim3(blocks), dim3(64 * MW), 0, stream, x, W, b, target, M, \
+                         scale, workspace, dx, tpw, mask_dx ? 1 : 0, dl, amx);                              \
+  } while (0)
     switch (C) {
       case 10: HEAD_MFMA(10); break;
       case 2: HEAD_MFMA(2); break;

@@ -6,6 +6,7 @@
 
 #include "kernels.h"
 #include "synth_hash.h"
+#include "sgd_rule.h"
 #include "u8_planes.h"
 
 namespace sdml {
@@ -29,38 +30,15 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
                                                   float damp, float wd, int nesterov, int first, int zero_grad,
                                                   SgdPlanes pl) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const SgdRule rule{lr, mom, damp, wd, nesterov, first};
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
-    f32x4 d = reinterpret_cast<const f32x4*>(g)[i];
+    const f32x4 d = reinterpret_cast<const f32x4*>(g)[i];
     if (zero_grad) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (wd != 0.f) d += wd * pv;
-    if (mom != 0.f) {
-      f32x4 b;
-      if (first) {
-        b = d;
-      } else {
-        b = reinterpret_cast<f32x4*>(buf)[i];
-        b = mom * b + (1.f - damp) * d;
-      }
-      reinterpret_cast<f32x4*>(buf)[i] = b;
-      d = nesterov ? d + mom * b : b;
-    }
-    const f32x4 nv = pv - lr * d;
-    reinterpret_cast<f32x4*>(p)[i] = nv;
+    const f32x4 nv = sgd_update4(p + 4 * i, buf + 4 * i, d, rule);
     if (pl.planes && i >= pl.off4 && i < pl.off4 + pl.n4) {
       const int64_t e = 4 * (i - pl.off4);
       const int64_t r = e / pl.K, k = e % pl.K;
-      u16x4s h, l;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        unsigned short hj, lj;
-        u8_fwd_planes_of(nv[j], hj, lj);
-        h[j] = hj;
-        l[j] = lj;
-      }
-      unsigned short* q = pl.planes + r * pl.Kp + k;
-      *reinterpret_cast<u16x4s*>(q) = h;
-      *reinterpret_cast<u16x4s*>(q + pl.plane_stride) = l;
+      sgd_write_planes4(pl.planes + r * pl.Kp + k, pl.plane_stride, nv);
     }
   }
 }

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
+#include "sgd_rule.h"
 
 namespace sdml {
 
@@ -13,7 +14,10 @@ namespace sdml {
 // 1024 threads = 64 outputs x 16 waves; wave w sums slabs b = w, w+16, ... with 16 loads in flight,
 // then the 16 wave partials are added in LDS (acc, 16 x 64 floats) in wave order.
 // flags: bit 0 = training (accumulate gW/gb), bit 1 = overwrite stats instead of adding.
-__device__ __forceinline__ void head_reduce_block(const HeadReduceArgs& a, int bx, float (*acc)[64]) {
+// sg (optional, sg->hp set): apply the optimizer step to gW / gb's parameters right here (the
+// step's last gradient contribution), with the same rule as the SGD kernel.
+__device__ __forceinline__ void head_reduce_block(const HeadReduceArgs& a, int bx, float (*acc)[64],
+                                                  const SgdFuse* sg = nullptr) {
   const int train = a.flags & 1;
   const int width = a.CK + a.C + 2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -32,6 +36,48 @@ __device__ __forceinline__ void head_reduce_block(const HeadReduceArgs& a, int b
   }
   acc[w][lane] = s;
   __syncthreads();
+  if (sg && sg->hp && (a.flags & 1)) {  // fused step: 4 consecutive outputs per lane (gb follows gW)
+    __syncthreads();
+    if (w == 0 && o < width) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t += acc[i][lane];
+      acc[0][lane] = t;  // (row 0 was wave 0's own partial: read above)
+    }
+    __syncthreads();
+    const int o4 = bx * 64 + 4 * lane;
+    if (w == 0 && lane < 16 && o4 < a.CK + a.C) {
+      const int n4 = min(4, a.CK + a.C - o4);  // the last group may hold the 2 stats or padding
+      float* gp = a.gW + o4;
+      sgd_f32x4 d;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = j < n4 ? gp[j] + acc[0][4 * lane + j] : 0.f;
+      if (n4 == 4) {
+        sgd_update4(sg->hp + o4, sg->hbuf + o4, d, SgdRule{sg->lr, sg->mom, sg->damp, sg->wd, sg->nesterov, sg->first});
+        *reinterpret_cast<sgd_f32x4*>(gp) = sg->zero_grad ? sgd_f32x4{0.f, 0.f, 0.f, 0.f} : d;
+      } else {  // ragged tail (CK + C not a multiple of 4): the padding after gb is zero in every buffer
+        float pt[4], bt[4];  // (hbuf is null without momentum: the rule then never reads it)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pt[j] = j < n4 ? sg->hp[o4 + j] : 0.f;
+          bt[j] = (j < n4 && sg->hbuf) ? sg->hbuf[o4 + j] : 0.f;
+        }
+        sgd_update4(pt, bt, d, SgdRule{sg->lr, sg->mom, sg->damp, sg->wd, sg->nesterov, sg->first});
+        for (int j = 0; j < n4; ++j) {
+          sg->hp[o4 + j] = pt[j];
+          if (sg->hbuf) sg->hbuf[o4 + j] = bt[j];
+          gp[j] = sg->zero_grad ? 0.f : d[j];
+        }
+      }
+    }
+    if (w == 1 && lane < 2 && bx * 64 <= a.CK + a.C + lane && a.CK + a.C + lane < bx * 64 + 64) {  // stats
+      const int so = a.CK + a.C + lane;
+      float t = acc[0][so - bx * 64];
+      if (a.flags & 2) a.stats[lane] = t;
+      else a.stats[lane] += t;
+    }
+    return;
+  }
   if (w == 0 && o < width) {
     float t = 0.f;
 #pragma unroll

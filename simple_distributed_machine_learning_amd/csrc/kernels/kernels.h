@@ -20,6 +20,22 @@ struct HeadReduceArgs {
 };
 void head_reduce_run(const HeadReduceArgs& a, hipStream_t stream);
 
+// The optimizer step applied by the reduction that produces the last gradients of a step (the one-rank
+// MLP step: u8_wgrad_dl's slab + head reduction), instead of a separate SGD launch. p/buf are the
+// parameters and momentum aligned with the reduced gradient (p[i] <-> gw[i]), hp/hbuf with the head's
+// gW (gb must follow gW). planes: the uint8 forward's fp16 weight planes of the weight at float
+// offset pl_off (relative to gw), [rows][K] (SgdPlanes' layout).
+struct SgdFuse {
+  float* p = nullptr;  // nullptr: no update
+  float* buf = nullptr;
+  float* hp = nullptr;
+  float* hbuf = nullptr;
+  float lr = 0.f, mom = 0.f, damp = 0.f, wd = 0.f;
+  int nesterov = 0, first = 0, zero_grad = 0;
+  unsigned short* planes = nullptr;
+  int64_t pl_off4 = 0, pl_n4 = 0, K = 0, Kp = 0, plane_stride = 0;
+};
+
 // ---- fp32 MFMA GEMM ------------------------------------------------------------------------
 // C[M,N] (op)= sum_k A(m,k) * B(n,k)
 //   A(m,k) = A[m*lda + k]        (a_kmajor = false)   or A[k*lda + m]   (a_kmajor = true)
@@ -122,7 +138,7 @@ bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const vo
 // head (optional): a deferred head reduction run in the same launch as this one's slab reduction
 void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const unsigned char* X, int M, int N, int ldx,
                  float* slab, float* gwb, float scale, const float* amax, int namax, hipStream_t stream,
-                 const HeadReduceArgs* head = nullptr);
+                 const HeadReduceArgs* head = nullptr, const SgdFuse* sgd = nullptr);
 // out[i] += sum_s slab[s * stride + i] in split order (n % 4 == 0, 16-B aligned)
 void slab_reduce(const float* slab, int64_t stride, int splits, float* out, int64_t n, hipStream_t stream);
 

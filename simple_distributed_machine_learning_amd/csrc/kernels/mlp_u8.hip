@@ -40,6 +40,7 @@
 
 #include "head_reduce.h"
 #include "kernels.h"
+#include "sgd_rule.h"
 #include "u8_planes.h"
 
 namespace sdml {
@@ -670,12 +671,14 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
 // gradient's split slabs (64 float4 columns per block, 16 waves over the splits w, w + 16, ..., wave
 // partials added in wave order), the blocks after them run the fused head's reduction (head_reduce.h).
 // Saves the head reduction's own launch (~5 us of latency-bound work) on the one-rank MLP step.
+// sg.p set: these are the step's last gradients, and the optimizer step is applied here (sgd_rule.h)
+// instead of by a separate SGD launch over the flat buffer.
 __global__ void __launch_bounds__(1024) slab_head_reduce_kernel(const float* __restrict__ slab, int64_t stride,
                                                                 int splits, float* __restrict__ out, int64_t n,
-                                                                int nslab, HeadReduceArgs head) {
+                                                                int nslab, HeadReduceArgs head, SgdFuse sg) {
   __shared__ f32x4 part[16][64];
   if ((int)blockIdx.x >= nslab) {
-    head_reduce_block(head, blockIdx.x - nslab, reinterpret_cast<float(*)[64]>(&part[0][0]));
+    head_reduce_block(head, blockIdx.x - nslab, reinterpret_cast<float(*)[64]>(&part[0][0]), sg.p ? &sg : nullptr);
     return;
   }
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -696,7 +699,17 @@ __global__ void __launch_bounds__(1024) slab_head_reduce_kernel(const float* __r
     f32x4 t = part[0][l];
 #pragma unroll
     for (int q = 1; q < 16; ++q) t += part[q][l];
-    *reinterpret_cast<f32x4*>(out + i) = acc + t;
+    acc += t;
+    if (sg.p) {
+      const f32x4 nv = sgd_update4(sg.p + i, sg.buf + i, acc, SgdRule{sg.lr, sg.mom, sg.damp, sg.wd, sg.nesterov, sg.first});
+      const int64_t i4 = i / 4;
+      if (sg.planes && i4 >= sg.pl_off4 && i4 < sg.pl_off4 + sg.pl_n4) {
+        const int64_t e = i - 4 * sg.pl_off4;
+        sgd_write_planes4(sg.planes + (e / sg.K) * sg.Kp + e % sg.K, sg.plane_stride, nv);
+      }
+      if (sg.zero_grad) acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    *reinterpret_cast<f32x4*>(out + i) = acc;
   }
 }
 
@@ -775,7 +788,7 @@ bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const vo
 
 void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const unsigned char* X, int M, int N, int ldx,
                  float* slab, float* gwb, float scale, const float* amax, int namax, hipStream_t stream,
-                 const HeadReduceArgs* head) {
+                 const HeadReduceArgs* head, const SgdFuse* sgd) {
   WgradParams p{};
   p.amax = namax > 0 ? amax : nullptr;
   p.namax = namax;
@@ -799,8 +812,9 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const 
   if (head && head->part) {
     const int nslab = (int)((n / 4 + 63) / 64);
     hipLaunchKernelGGL(slab_head_reduce_kernel, dim3(nslab + head_reduce_blocks(*head)), dim3(1024), 0, stream, slab, n,
-                       splits, gwb, n, nslab, *head);
+                       splits, gwb, n, nslab, *head, sgd ? *sgd : SgdFuse());
   } else {
+    if (sgd && sgd->p) abort();  // host contract: the fused step needs the head reduction in the same launch
     slab_reduce(slab, n, splits, gwb, n, stream);
   }
 }

@@ -743,10 +743,14 @@ torch::Tensor head_dx_from_dl(torch::Tensor dl, torch::Tensor w, torch::Tensor x
 // first layer's weight gradient from the FACTORED boundary gradient: gw += scale * dz^T x_u8,
 // gb += colsum(dz) with dz = (dl @ w2) * (h > 0) - expanded inside mlp_u8.hip's wgrad kernel when
 // it applies (bit-identical to head_dx_from_dl followed by linear_wgrad_u8), else those two
-// head: a deferred head reduction (HeadPending) to run in this call's reduction launch (or before it)
-void linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, torch::Tensor h, torch::Tensor gw,
+// head: a deferred head reduction (HeadPending) to run in this call's reduction launch (or before it).
+// sgd (optional, with head): (params, grads, momentum_buffer, lr, momentum, dampening, weight_decay,
+// nesterov, first, zero_grad, planes | None, plane_offset, plane_rows, plane_k) of the flat buffers
+// gw/gb and the head's gW/gb live in - when these are the step's last gradients, the optimizer step is
+// applied inside the same reduction launch. Returns whether it was (else the caller steps).
+bool linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, torch::Tensor h, torch::Tensor gw,
                         torch::Tensor gb, double scale, c10::optional<torch::Tensor> amax,
-                        std::shared_ptr<HeadPending> head) {
+                        std::shared_ptr<HeadPending> head, c10::optional<py::tuple> sgd) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
               "linear_wgrad_u8_dl: x must be a contiguous 2-D uint8 ROCm tensor");
   check_f32_cuda(dl, "dl");
@@ -768,17 +772,60 @@ void linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, tor
       TORCH_CHECK(amax->numel() >= 1 && amax->is_contiguous(), "linear_wgrad_u8_dl: amax must be non-empty");
     }
     const bool fuse_head = head && head->pending();
+    sdml::SgdFuse sg;
+    if (fuse_head && sgd.has_value() && (head->args.flags & 1) &&
+        head->args.gb == head->args.gW + head->args.CK) {
+      const py::tuple& t = *sgd;
+      TORCH_CHECK(t.size() == 14, "linear_wgrad_u8_dl: sgd tuple of 14");
+      auto P = t[0].cast<torch::Tensor>(), G = t[1].cast<torch::Tensor>(), B = t[2].cast<torch::Tensor>();
+      check_f32_cuda(P, "params");
+      check_f32_cuda(G, "grads");
+      const int64_t nflat = G.numel();
+      const int64_t off_w = gw.data_ptr<float>() - G.data_ptr<float>();
+      const int64_t off_h = head->args.gW - G.data_ptr<float>();
+      const float mom = (float)t[4].cast<double>();
+      TORCH_CHECK(P.numel() == nflat && off_w >= 0 && off_w % 4 == 0 && off_w + N * K + N <= nflat && off_h >= 0 &&
+                      off_h % 4 == 0 && off_h + head->args.CK + head->args.C <= nflat &&
+                      (mom == 0.f || B.numel() == nflat),
+                  "linear_wgrad_u8_dl: gradients outside the flat buffers");
+      sg.p = P.data_ptr<float>() + off_w;
+      sg.hp = P.data_ptr<float>() + off_h;
+      sg.buf = mom != 0.f ? B.data_ptr<float>() + off_w : nullptr;
+      sg.hbuf = mom != 0.f ? B.data_ptr<float>() + off_h : nullptr;
+      sg.lr = (float)t[3].cast<double>();
+      sg.mom = mom;
+      sg.damp = (float)t[5].cast<double>();
+      sg.wd = (float)t[6].cast<double>();
+      sg.nesterov = t[7].cast<bool>() ? 1 : 0;
+      sg.first = t[8].cast<bool>() ? 1 : 0;
+      sg.zero_grad = t[9].cast<bool>() ? 1 : 0;
+      if (!t[10].is_none()) {
+        auto planes = t[10].cast<torch::Tensor>();
+        const int64_t poff = t[11].cast<int64_t>(), prows = t[12].cast<int64_t>(), pk = t[13].cast<int64_t>();
+        TORCH_CHECK(planes.is_cuda() && planes.scalar_type() == torch::kInt16 && planes.is_contiguous() &&
+                        planes.dim() == 3 && planes.size(0) == sdml::kU8FwdPlanes && planes.size(1) == prows &&
+                        poff >= off_w && (poff - off_w) % 4 == 0 && pk % 4 == 0 && poff + prows * pk <= off_w + N * K,
+                    "linear_wgrad_u8_dl: planes must cover a weight inside gw");
+        sg.planes = reinterpret_cast<unsigned short*>(planes.data_ptr<int16_t>());
+        sg.pl_off4 = (poff - off_w) / 4;
+        sg.pl_n4 = prows * pk / 4;
+        sg.K = pk;
+        sg.Kp = planes.size(2);
+        sg.plane_stride = prows * planes.size(2);
+      }
+    }
     sdml::u8_wgrad_dl(dl.data_ptr<float>(), w2.data_ptr<float>(), h.data_ptr<float>(), (int)C, x.data_ptr<uint8_t>(),
                       (int)M, (int)N, (int)K, ws.data_ptr<float>(), gw.data_ptr<float>(), (float)scale,
                       has_am ? amax->data_ptr<float>() : nullptr, has_am ? (int)amax->numel() : 0, cur_stream(),
-                      fuse_head ? &head->args : nullptr);
+                      fuse_head ? &head->args : nullptr, sg.p ? &sg : nullptr);
     if (fuse_head) head->done();
-    return;
+    return sg.p != nullptr;
   }
   if (head) head->run();
   torch::Tensor dz = sdml::head_fused_supported((int)N, (int)C) ? head_dx_from_dl(dl, w2, h, true)
                                                                   : at::matmul(dl, w2).mul_((h > 0).to(h.scalar_type()));
   linear_wgrad_u8(x, dz, gw, gb, scale, amax);
+  return false;
 }
 
 void sgd_momentum_(torch::Tensor p, torch::Tensor g, torch::Tensor buf, double lr, double momentum, double dampening,
@@ -1158,7 +1205,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_wgrad_u8_dl", &linear_wgrad_u8_dl,
         "gw += scale * dz^T x_u8, gb += colsum(dz), dz = (dl @ w2) * (h > 0) (factored boundary gradient)",
         py::arg("x"), py::arg("dl"), py::arg("w2"), py::arg("h"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
-        py::arg("amax") = py::none(), py::arg("head") = nullptr);
+        py::arg("amax") = py::none(), py::arg("head") = nullptr, py::arg("sgd") = py::none());
   m.def("head_dx_from_dl", &head_dx_from_dl, "dx = (dl @ w) * (x > 0): boundary gradient from its factor",
         py::arg("dl"), py::arg("w"), py::arg("x"), py::arg("mask"));
   m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer (optionally also writing a "

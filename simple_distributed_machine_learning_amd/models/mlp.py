@@ -198,18 +198,32 @@ class MLPStage(PipelineStage):
         """The weight the factored boundary gradient is expanded with (dx = dl @ W)."""
         return self.layers()[-1].weight.detach()
 
-    def bwd_from_factor(self, dl, w2, ctx, head_pending=None) -> bool:
+    def grad_span(self):
+        """(first gradient tensor, numel) of this stage's parameters in the flat gradient buffer, if
+        they are one contiguous range (their flat segments are back to back), else None."""
+        ps = [p for lin in self.layers() for p in (lin.weight, lin.bias)]
+        if any(p.grad is None for p in ps):
+            return None
+        for a, b in zip(ps, ps[1:]):
+            if a.grad.data_ptr() + a.numel() * a.grad.element_size() != b.grad.data_ptr():
+                return None
+        return ps[0].grad, sum(p.numel() for p in ps)
+
+    def bwd_from_factor(self, dl, w2, ctx, head_pending=None, sgd=None) -> bool:
         """Stage-0 backward fed by the factored boundary gradient dl (dz = (dl @ w2) * (h > 0), h this
         stage's output). A single uint8-fed layer takes it straight into its weight-gradient kernel
         (dz never materialised; a deferred head reduction ``head_pending`` shares its reduction
-        launch); returns False (nothing done, ``head_pending`` untouched) for other stages."""
+        launch, and with ``sgd`` so does the optimizer step: ``self.sgd_fused`` tells whether it
+        ran); returns False (nothing done, ``head_pending`` untouched) for other stages."""
+        self.sgd_fused = False
         acts = ctx.get("acts")
         layers = self.layers()
         if acts is None or len(layers) != 1 or acts[0].dtype != torch.uint8:
             return False
         ctx.pop("acts")
         lin = layers[0]
-        ops.linear_wgrad_u8_dl(acts[0], dl, w2, acts[1], lin.weight.grad, lin.bias.grad, head_pending=head_pending)
+        self.sgd_fused = ops.linear_wgrad_u8_dl(acts[0], dl, w2, acts[1], lin.weight.grad, lin.bias.grad,
+                                                head_pending=head_pending, sgd=sgd)
         return True
 
     def head_bwd(self, ctx):

@@ -87,7 +87,8 @@ def linear_wgrad_u8(x: torch.Tensor, gz: torch.Tensor, gw: torch.Tensor, gb: Opt
         gb += gz.sum(0)
 
 
-def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, amax: Optional[torch.Tensor] = None, head_pending=None) -> None:
+def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, amax: Optional[torch.Tensor] = None, head_pending=None,
+                       sgd=None) -> bool:
     """First-layer weight gradient from the FACTORED boundary gradient: with dz = (dl @ w2) * (h > 0)
     (dl [M, C] the head's factor, w2 [C, N] the head weight, h [M, N] this layer's ReLU output),
     gw += dz.T @ ToTensor(x), gb += sum(dz). On ROCm dz is expanded inside the weight-gradient kernel
@@ -96,18 +97,21 @@ def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, amax: Optional[torch.Tensor] = None
     fused head attached to the ``dl`` it returned, else each workgroup bounds dz by its rows'
     max sum |dl| times max |w2| (a dl received over the network carries no attribute).
     ``head_pending``: a head reduction deferred by :func:`linear_logsoftmax_nll_dl`, run in the same
-    launch as this one's slab reduction (or before it, on the paths without one)."""
+    launch as this one's slab reduction (or before it, on the paths without one).
+    ``sgd`` (with ``head_pending``; ops.optim.FusedSGD.fused_args): these are the step's last
+    gradients - apply the optimizer step inside the same launch. Returns True if it was applied (the
+    caller then commits it with FusedSGD.commit_fused instead of stepping)."""
     if x.is_cuda:
         if amax is None:
             amax = getattr(dl, "_sdml_amax", None)
-        _k().linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, PIXEL_SCALE, amax, head_pending)
-        return
+        return bool(_k().linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, PIXEL_SCALE, amax, head_pending, sgd))
     if head_pending is not None:
         head_pending.run()
     with torch.no_grad():
         dz = (dl @ w2) * (h > 0).to(dl.dtype)
         gw += dz.t() @ pixels_to_float(x)
         gb += dz.sum(0)
+    return False
 
 
 def linear_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:

@@ -65,6 +65,39 @@ class FusedSGD:
             cache, w, _ = self.plane_cache
             cache.token = PlaneCache.token_of(w, self.flat.param_epoch)
 
+    def fused_args(self, spans, zero_grad: bool = True):
+        """Arguments for applying this optimizer's step inside the reduction that produces the step's
+        last gradients (ops.linear_wgrad_u8_dl ``sgd``), or None when that cannot cover the whole step:
+        ``spans`` = [(first grad tensor, numel)] of the flat gradient ranges that reduction writes;
+        every parameter segment must lie inside them (the padding between segments stays zero)."""
+        if self.master is not None or not self.flat.params.is_cuda:
+            return None
+        base, es = self.flat.grads.data_ptr(), self.flat.grads.element_size()
+        ranges = [((t.data_ptr() - base) // es, n) for t, n in spans]
+        for seg in self.flat.segments:
+            if not any(o <= seg.offset and seg.offset + seg.numel <= o + n for o, n in ranges):
+                return None
+        planes, poff, prows, pk = None, 0, 0, 0
+        if self.plane_cache is not None:
+            cache, w, poff = self.plane_cache
+            planes, prows, pk = cache.planes, w.shape[0], w.shape[1]
+        return (self.flat.params, self.flat.grads, self.momentum_buffer, float(self.lr), float(self.momentum),
+                float(self.dampening), float(self.weight_decay), bool(self.nesterov), self.steps == 0,
+                bool(zero_grad), planes, int(poff), int(prows), int(pk))
+
+    def commit_fused(self, zero_grad: bool = True):
+        """Book-keeping of a step that ``fused_args`` let a reduction kernel apply (what step() does
+        after its kernel)."""
+        if zero_grad:
+            self.flat.grads_zero = True
+        self.steps += 1
+        self.flat.param_epoch += 1
+        if self.plane_cache is not None:
+            from . import PlaneCache
+
+            cache, w, _ = self.plane_cache
+            cache.token = PlaneCache.token_of(w, self.flat.param_epoch)
+
     def zero_grad(self):
         self.flat.zero_grad()
 

@@ -464,6 +464,12 @@ class PipelineEngine:
         # reduction launch (one launch instead of two per wave); `pend[w]` must be consumed or run
         defer = fuse0 and R == 1
         pend = [None] * W
+        # ... and when nothing else touches the gradients before the optimizer (one rank, no gradient
+        # all-reduce, stepping this call), the last wave's reduction applies the optimizer step too
+        fuse_step = (defer and train and step_optimizer and not self.grad_sync.enabled
+                     and hasattr(self.optimizer, "fused_args") and hasattr(s0, "grad_span")
+                     and hasattr(s1, "grad_span"))
+        step_fused = [False]
 
         def run_pending(w):
             if pend[w] is not None:
@@ -478,7 +484,13 @@ class PipelineEngine:
             if factored and fuse0:  # the factor goes straight into stage 0's weight-gradient kernel
                 with tm.span("bwd", 0):
                     if pend[w] is not None:
-                        done = s0.bwd_from_factor(gz, s1.factor_weight(), ctx0[w], head_pending=pend[w])
+                        sgd = None
+                        if fuse_step and w == W - 1:
+                            spans = [s0.grad_span(), s1.grad_span()]
+                            if all(sp is not None for sp in spans):
+                                sgd = self.optimizer.fused_args(spans)
+                        done = s0.bwd_from_factor(gz, s1.factor_weight(), ctx0[w], head_pending=pend[w], sgd=sgd)
+                        step_fused[0] = bool(done and sgd is not None and getattr(s0, "sgd_fused", False))
                     else:
                         done = s0.bwd_from_factor(gz, s1.factor_weight(), ctx0[w])
                 if done:
@@ -559,7 +571,10 @@ class PipelineEngine:
                 self.grad_sync.finish()
             if step_optimizer:
                 with tm.span("optim"):
-                    self.optimizer.step()
+                    if step_fused[0]:  # applied by the last weight-gradient reduction
+                        self.optimizer.commit_fused()
+                    else:
+                        self.optimizer.step()
                 self.global_step += 1
             self._advance_rng()
         if fresh:  # no head ran on this rank this step

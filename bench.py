@@ -5,15 +5,19 @@ BASELINE.json metric: "samples/sec (whole node), 2-stage MLP on MNIST-shape synt
 log_softmax + NLL), trained with SGD(lr 0.1, momentum 0.5) in fp32 — the reference's
 optimizer and precision (/root/reference/simple_distributed.py:18-21, :100-104).
 
-Placement ("rotate" pipeline; weak scaling: per-GPU work fixed at --batch_per_gpu samples):
-  every GPU owns a data shard and hosts both stages; each step is cut into W waves and in
-  every wave stage 0's output is split R ways and exchanged with ONE RCCL all-to-all (part k
-  -> GPU k), stage 1 (+ loss + its backward) runs on what arrived, the input-gradients go
-  back by the inverse all-to-all, stage 0 runs its backward; stage weights are replicated and
-  their gradients all-reduced over RCCL. On an 8-GPU node every stage boundary therefore
-  fans out over all 7 xGMI links of each GPU instead of one neighbour link. N=1 is the same
-  code with the exchange elided (both stages local).
-  (--schedule chimera / 1f1b select the classic neighbour pipelines instead.)
+Placement (``--placement``, parallel/placement.py; weak scaling: per-GPU work fixed at
+--batch_per_gpu samples): N = 1 runs both stages on the one GPU. For N > 1 the placement is a
+decision of the link/compute cost model, not a default:
+  pp2dp     the reference's cut replicated: GPU pairs (stage 0 | stage 1), Chimera schedule,
+            boundary tensors by RCCL isend/irecv over the pair's xGMI link, dp over the pairs
+  rotate    every GPU owns a shard and hosts both stages; an equal share of each wave's boundary
+            goes to every peer with ONE RCCL all-to-all per wave and direction (all 7 links)
+  balanced  rotate with the cross-GPU fraction sized so the links stay under the compute
+  dp        rows stay on their owner (nothing crosses); gradients all-reduced
+  auto      (default) the fastest predicted placement; within 2 %, the one moving the most
+            boundary bytes across GPUs
+The JSON ``config`` carries the placement, the boundary bytes that crossed GPUs per step
+(measured by the transport), the link model and every placement's prediction.
 
 Data: synthetic MNIST-shape images stored as uint8 bytes, the way MNIST ships them (``--pixels u8``,
 default). ToTensor's /255, which the reference runs on the host per batch
@@ -42,6 +46,7 @@ import torch.distributed as dist
 from simple_distributed_machine_learning_amd.data import SyntheticMNIST
 from simple_distributed_machine_learning_amd.models import get_model_spec
 from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh
+from simple_distributed_machine_learning_amd.parallel import placement as plc
 
 # reference RPC mechanism with the same 2-stage MLP on 8 vCPUs; the best number
 # it reports for this model is 413,862 samples/s (B=4096, TCP-only transport). The headline
@@ -81,9 +86,15 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch_per_gpu", type=int, default=int(os.environ.get("SDML_BENCH_BATCH", 131072)))
-    p.add_argument("--waves", type=int, default=None, help="rotate: waves per step (default 1 on N=1, else 2)")
-    p.add_argument("--microbatches", type=int, default=None, help="chimera/1f1b: micro-batches per pipeline")
-    p.add_argument("--schedule", default="rotate", choices=["rotate", "chimera", "1f1b", "gpipe"])
+    p.add_argument("--placement", default="auto", choices=plc.PLACEMENTS,
+                   help="where the two stages run on N GPUs (parallel/placement.py)")
+    p.add_argument("--cross_fraction", type=float, default=None,
+                   help="rotate family: fraction of each wave whose stage 1 runs on a peer (overrides the model)")
+    p.add_argument("--waves", type=int, default=None,
+                   help="rotate family: waves per step (default 1 when nothing crosses GPUs, else 2)")
+    p.add_argument("--microbatches", type=int, default=None, help="pp2dp: micro-batches per pipeline")
+    p.add_argument("--schedule", default=None, choices=["chimera", "1f1b", "gpipe"],
+                   help="pp2dp: pipeline schedule (default chimera)")
     p.add_argument("--dataset_batches", type=int, default=4, help="distinct batches cycled through")
     p.add_argument("--model", default="mlp")
     p.add_argument("--pixels", default="u8", choices=["u8", "f32"],
@@ -91,12 +102,16 @@ def parse():
     return p.parse_args()
 
 
-def _parallelism(kind, n, mesh):
+def _parallelism(placement, n, mesh, phi, kind):
     if n == 1:
         return "single GPU, both pipeline stages local"
-    if kind == "rotate":
-        return f"pp2 rotate: {n} GPUs x (stage0+stage1), all-to-all stage boundary over RCCL/xGMI, grad all-reduce"
-    return f"pp{mesh.pp}-{kind} x dp{mesh.dp}"
+    if placement == "pp2dp":
+        return f"pp2 x dp{mesh.dp}: GPU pairs (stage0 | stage1), {kind} schedule, RCCL isend/irecv over xGMI"
+    if phi == 0:
+        return f"dp{n}: both stages on every GPU, no boundary crosses GPUs, RCCL gradient all-reduce"
+    share = "equal shares" if phi is None else f"{phi:.4g} of each wave"
+    return (f"pp2 {placement}: {n} GPUs x (stage0+stage1), stage-1 rows on peers ({share}) by RCCL all-to-all "
+            f"over xGMI, gradient all-reduce")
 
 
 def main():
@@ -107,23 +122,45 @@ def main():
         if rank == 0:
             print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     n = world
-    kind = a.schedule
-    if kind == "rotate":
+    place = a.placement
+    predicted = plc.table(n, a.batch_per_gpu)
+    phi = None
+    if n == 1:
+        place = "dp"
+    elif place == "auto":
+        place, phi, _ = plc.choose(n, a.batch_per_gpu)
+    if a.schedule is not None and n > 1:
+        place = "pp2dp"
+    if place == "pp2dp" and n % 2:
+        raise SystemExit(f"pp2dp needs an even number of GPUs, got {n}")
+    if place == "pp2dp":
+        kind = a.schedule or "chimera"
+        pp = 2
+        M = a.microbatches or 4
+        B = a.batch_per_gpu * pp  # per pipeline replica
+        phi = 1.0
+    else:
+        kind = "rotate"
         pp = world
-        W = a.waves or (1 if n == 1 else 2)
+        if place == "dp":
+            phi = 0.0
+        elif place == "balanced":
+            phi = plc.balanced_fraction(n, a.batch_per_gpu)
+        elif place == "rotate":
+            phi = None
+        if a.cross_fraction is not None:
+            phi = a.cross_fraction
+        W = a.waves or (1 if (n == 1 or phi == 0) else 2)
         M = W * pp
         B = a.batch_per_gpu  # per owner shard
-    else:
-        pp = 1 if n == 1 else 2
-        M = a.microbatches or (1 if n == 1 else 4)
-        B = a.batch_per_gpu * pp  # per pipeline replica
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     # rotate on a 2-stage model runs its boundary as all-to-all collectives: no p2p channels
     mesh = init_mesh(pp=pp, schedule_kind=kind, timeout_s=900, rank=rank, world_size=world,
                      p2p_channels=(kind != "rotate"))
     dev = mesh.device
     spec = get_model_spec(a.model, 2)
-    engine = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=1)
+    engine = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=1,
+                            cross_fraction=phi if kind == "rotate" else None)
     engine.train()
     GB = B * engine.data_shards  # samples per optimizer step, whole node
     # fresh data every step, cycling over `dataset_batches` global batches; a rank
@@ -141,15 +178,13 @@ def main():
     def sync():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
-        if world > 1:
-            if dev.type == "cuda":
-                dist.barrier(device_ids=[dev.index])
-            else:
-                dist.barrier()
+        mesh.barrier()
 
     for i in range(a.warmup):
         step(i)
     sync()
+    if engine.transport is not None:
+        engine.transport.reset_counters()
     t0 = time.perf_counter()
     res = None
     for i in range(a.steps):
@@ -157,9 +192,13 @@ def main():
     sync()
     el = time.perf_counter() - t0
     t = torch.tensor([el], dtype=torch.float64, device=dev)
+    sent = torch.tensor([float(engine.transport.bytes_sent if engine.transport else 0)], dtype=torch.float64,
+                        device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        engine.transport.all_reduce(t, channel="world", op=dist.ReduceOp.MAX, async_op=False)
+        engine.transport.all_reduce(sent, channel="world", async_op=False)
     el = float(t.item())
+    cross_bytes = float(sent.item()) / a.steps
     loss = None
     if res is not None:
         l, c, cnt = engine.reduce_metrics(res)
@@ -185,7 +224,13 @@ def main():
                 "model": "mlp-784-128-10 (2 pipeline stages)",
                 "global_batch": GB,
                 "seq_len": None,
-                "parallelism": _parallelism(kind, n, mesh),
+                "parallelism": _parallelism(place, n, mesh, phi, kind),
+                "placement": place,
+                "cross_fraction": phi if place != "rotate" else round((n - 1) / n, 4),
+                "boundary_bytes_across_gpus_per_step": int(cross_bytes),
+                "transport": engine.transport.name if engine.transport else None,
+                "link_model": plc.model_dict(),
+                "predicted": predicted,
                 "microbatches": M,
                 "batch_per_gpu": a.batch_per_gpu,
                 "optimizer": "SGD lr=0.1 momentum=0.5",

@@ -52,6 +52,26 @@ class Mesh:
     # rotate: a second communicator over the pipeline ranks for the backward boundary exchange, so
     # it does not queue behind the next wave's forward exchange on one RCCL stream
     pipe_group_bwd: Optional[object] = None
+    # how cross-rank bytes move (parallel/p2p.py): "direct" = torch.distributed on the tensors
+    # themselves (RCCL for device tensors, Gloo for CPU ones); "host" = device tensors staged
+    # through host memory over Gloo (several ranks sharing one GPU)
+    transport_kind: str = "direct"
+    _transport: Optional[object] = None
+
+    @property
+    def transport(self):
+        """The rank's :class:`~.p2p.Transport` (None on a 1-rank mesh)."""
+        if self.world_size == 1:
+            return None
+        if self._transport is None:
+            from .p2p import make_transport
+
+            self._transport = make_transport(self)
+        return self._transport
+
+    def barrier(self):
+        if self.world_size > 1:
+            self.transport.barrier()
 
     @property
     def distributed(self) -> bool:
@@ -64,7 +84,7 @@ class Mesh:
     def tp_context(self):
         from .tp import TPContext
 
-        return TPContext(self.tp, self.tp_rank, self.tp_group)
+        return TPContext(self.tp, self.tp_rank, self.tp_group, self.transport)
 
     def pipe_ranks(self) -> List[int]:  # this rank's pipeline (same dp_rank, same tp_rank)
         return [self.global_rank(self.dp_rank, r) for r in range(self.pp)]
@@ -127,7 +147,7 @@ def _pg_options(backend: str):
 def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = None,
               timeout_s: float = 600.0, rank: Optional[int] = None, world_size: Optional[int] = None,
               local_rank: Optional[int] = None, device: Optional[torch.device] = None,
-              p2p_channels: bool = True, tp: int = 1) -> Mesh:
+              p2p_channels: bool = True, tp: int = 1, transport: Optional[str] = None) -> Mesh:
     """Join (or reuse) the default process group and build the dp x pp mesh.
 
     Rank/world come from arguments, else torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK).
@@ -135,6 +155,10 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
     same store the reference's ``init_rpc`` used). The timeout is finite:
     the reference's ``rpc_timeout=0`` means "wait forever" and, on torch 2.10, an instant
     rendezvous failure.
+
+    ``transport`` (default: env ``SDML_TRANSPORT``, else ``"direct"``): ``"host"`` stages device
+    tensors through host memory over Gloo, so several ranks can share one GPU (RCCL refuses
+    that); the process group is then Gloo even on a ROCm device.
     """
     if rank is None:
         rank = int(os.environ.get("RANK", "0"))
@@ -144,8 +168,13 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
         local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
     if device is None:
         device = select_device(local_rank)
+    transport = transport or os.environ.get("SDML_TRANSPORT", "direct")
+    if transport not in ("direct", "host"):
+        raise ValueError(f"unknown transport {transport!r} (direct | host)")
     if backend is None:
-        backend = default_backend(device)
+        backend = "gloo" if transport == "host" else default_backend(device)
+    if backend == "gloo" and device.type == "cuda":
+        transport = "host"  # Gloo cannot run the engine's collectives on device tensors
     tp = max(1, int(tp))
     if world_size % tp != 0:
         raise ValueError(f"world_size={world_size} is not a multiple of tensor-parallel ranks tp={tp}")
@@ -155,7 +184,7 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
     if world_size % (pp * tp) != 0:
         raise ValueError(f"world_size={world_size} is not a multiple of pp={pp} x tp={tp}")
     mesh = Mesh(rank=rank, world_size=world_size, local_rank=local_rank, pp=pp, dp=world_size // (pp * tp),
-                schedule_kind=schedule_kind, device=device, backend=backend, tp=tp)
+                schedule_kind=schedule_kind, device=device, backend=backend, tp=tp, transport_kind=transport)
     mesh.tp_rank = rank % tp
     mesh.pp_rank = (rank // tp) % pp
     mesh.dp_rank = rank // (tp * pp)
@@ -223,8 +252,8 @@ def shutdown(mesh: Optional[Mesh] = None):
     blocks until every rank arrives, simple_distributed.py:186)."""
     if dist.is_initialized():
         try:
-            if mesh is not None and mesh.device.type == "cuda":
-                dist.barrier(device_ids=[mesh.device.index])
+            if mesh is not None and mesh.world_size > 1:
+                mesh.barrier()
             else:
                 dist.barrier()
         finally:

@@ -28,7 +28,6 @@ from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
-import torch.distributed as dist
 
 from ..models.base import ModelSpec, PipelineStage, build_stages
 from ..ops import pixels_to_float
@@ -36,7 +35,7 @@ from ..ops.optim import FusedSGD
 from ..utils.flat import FlatParams
 from ..utils.timing import PhaseTimer
 from .mesh import Mesh
-from .p2p import Transport, message_tag
+from .p2p import BufferPool, message_tag
 from .schedule import OP_BWD, OP_FWD, OP_RECV, OP_SEND, PL_ACT, PL_GRAD, Schedule, build_schedule
 
 
@@ -68,6 +67,7 @@ class GradSync:
 
     def __init__(self, flat: FlatParams, mesh: Mesh, local_stages: Sequence[int]):
         self.flat, self.mesh = flat, mesh
+        self.transport = mesh.transport
         self.order = sorted(set(local_stages), reverse=True)
         self.enabled = mesh.grad_group is not None
         self._done = set()
@@ -88,8 +88,17 @@ class GradSync:
         while self._ptr < len(self.order) and self.order[self._ptr] in self._done:
             s = self.order[self._ptr]
             t = self.flat.stage_slice(s, "grads")
-            self._works.append(dist.all_reduce(t, group=self.group, async_op=True))
+            self._works.append(self.transport.all_reduce(t, channel="grad"))
             self._ptr += 1
+
+    def finish_all(self):
+        """ONE all-reduce over the whole flat gradient buffer (every local stage at once): fewer
+        collectives when nothing is left to overlap them with (rotate / dp placements)."""
+        if not self.enabled:
+            return
+        if self._ptr:
+            raise RuntimeError("GradSync.finish_all after per-stage all-reduces were issued")
+        self.transport.all_reduce(self.flat.grads, channel="grad").wait()
 
     def finish(self):
         if not self.enabled:
@@ -104,7 +113,8 @@ class GradSync:
 class PipelineEngine:
     def __init__(self, spec: ModelSpec, mesh: Mesh, schedule_kind: str = "1f1b", num_microbatches: int = 1,
                  lr: float = 0.1, momentum: float = 0.5, weight_decay: float = 0.0, seed: int = 0,
-                 dtype: Optional[torch.dtype] = None, debug_sync: bool = False, timing: bool = False):
+                 dtype: Optional[torch.dtype] = None, debug_sync: bool = False, timing: bool = False,
+                 cross_fraction: Optional[float] = None):
         self.spec, self.mesh = spec, mesh
         self.kind = schedule_kind
         self.M = max(1, int(num_microbatches))
@@ -154,7 +164,10 @@ class PipelineEngine:
         for m in self.stages.values():  # derived weight caches the step kernel keeps current
             if hasattr(m, "attach_plane_cache"):
                 m.attach_plane_cache(self.flat, self.optimizer)
-        self.transport = Transport(mesh) if mesh.pp > 1 else None
+        # every cross-rank byte goes through the mesh's transport seam (parallel/p2p.py); boundary
+        # buffers come from a persistent pool (no per-step communication allocations)
+        self.transport = mesh.transport
+        self.bufs = BufferPool(self.device)
         self.grad_sync = GradSync(self.flat, mesh, self.local_stage_ids)
         self.training = True
         self.global_step = 0
@@ -167,6 +180,14 @@ class PipelineEngine:
         # ... also with both stages on one rank (R == 1): the head then skips its dx pass and stage 0
         # reads h + dl instead of dx (SDML_FACTORED_R1=0: the head returns dx)
         self.factored_r1 = os.environ.get("SDML_FACTORED_R1", "1") != "0"
+        # rotate (2 stages): fraction of every wave whose stage 1 runs on a peer (rotate_parts);
+        # None = classic equal shares. SDML_CROSS_FRACTION overrides.
+        env_phi = os.environ.get("SDML_CROSS_FRACTION")
+        if env_phi is not None:
+            cross_fraction = float(env_phi)
+        if cross_fraction is not None and not 0.0 <= cross_fraction <= 1.0:
+            raise ValueError(f"cross_fraction must be in [0, 1], got {cross_fraction}")
+        self.cross_fraction = cross_fraction
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
 
@@ -303,7 +324,7 @@ class PipelineEngine:
                 mbsz = sizes[ins.mb]
                 prod = ins.stage if ins.payload == PL_ACT else ins.stage - 1
                 shape, dt = self._boundary(prod, mbsz)
-                buf = torch.empty(shape, dtype=dt, device=dev)
+                buf = self.bufs.get(("recv", ins.payload, ins.pipe, ins.stage, ins.mb), shape, dt)
                 src = self.mesh.global_rank(self.mesh.dp_rank, ins.peer)
                 w = self.transport.irecv(buf, src, message_tag(ins.payload, ins.pipe, ins.stage, ins.mb))
                 inbox[(ins.payload, ins.pipe, ins.stage, ins.mb)] = (w, buf)
@@ -384,15 +405,48 @@ class PipelineEngine:
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
 
     # ---------------------------------------------------------------------------------------
+    def rotate_parts(self, waves: Sequence[int], R: int) -> List[List[List[int]]]:
+        """``P[w][o][k]``: rows of owner ``o``'s wave ``w`` whose stage 1 runs on rank ``k``
+        (``k == o``: the rows that stay on their owner). Every rank derives the same matrix, so all
+        of them issue the same collectives. An owner's wave rows are laid out
+        ``[local | to peer k1 | to peer k2 | ...]`` (peers ascending).
+
+        ``cross_fraction`` None: classic rotate, an equal 1/R share per rank (the owner keeps the
+        largest); else that fraction of every wave crosses to the peers (0: nothing crosses, pure
+        data parallelism over replicated stages; parallel/placement.py chooses it from a link
+        model)."""
+        P = []
+        phi = self.cross_fraction
+        for b in waves:
+            if R == 1:
+                c = 0
+            elif phi is None:
+                c = b - split_sizes(b, R)[0]
+            else:
+                c = min(b, int(round(phi * b)))
+            cs = split_sizes(c, R - 1) if c > 0 else []
+            cs += [0] * (R - 1 - len(cs))
+            rows = []
+            for o in range(R):
+                row = [0] * R
+                row[o] = b - c
+                for i, k in enumerate(k for k in range(R) if k != o):
+                    row[k] = cs[i]
+                rows.append(row)
+            P.append(rows)
+        return P
+
     def _run_rotate_alltoall(self, dataset, start, batch_size, train, global_batch, step_optimizer, t0):
         """``rotate`` for a 2-stage model, boundary as all-to-all (same math as the p2p form).
 
         Each rank owns ``batch_size`` samples at ``start + rank*batch_size``, cut into W =
-        M/R waves. Per wave: stage 0 on the own chunk -> the chunk's R parts are exchanged
-        (part k -> rank k) -> stage 1 (+ loss, + its backward) on the R parts received ->
-        input-grads exchanged back -> stage-0 backward. Waves are issued so that wave w's
-        exchange overlaps the compute of its neighbours; the collectives run on the RCCL
-        stream and only the consumer kernels wait for them.
+        M/R waves. Per wave: stage 0 on the own chunk -> the rows assigned to peers
+        (:meth:`rotate_parts`) are exchanged with ONE all-to-all on the transport's forward
+        channel -> stage 1 (+ loss, + its backward) on the rows that stayed local and on the rows
+        received -> their input-grads go back by the inverse all-to-all on the backward channel ->
+        stage-0 backward over all own rows. The local rows never enter a collective (no self
+        copy). Waves are issued so that wave w's exchange overlaps the compute of its neighbours;
+        with RCCL the collectives run on their own streams and only the consumer kernels wait.
 
         Factored boundary gradient (stage 1 a single Linear + log_softmax, e.g. 784-128-10): the
         gradient stage 1 returns, (dl @ W) * (h > 0), has rank <= C per sample. Every rank holds
@@ -414,7 +468,6 @@ class PipelineEngine:
         waves = split_sizes(batch_size, max(1, self.M // R))
         W = len(waves)
         scale = self._loss_scale(dataset, batch_size, global_batch)
-        group = mesh.pipe_group
         # [loss_sum, correct]; a head that can overwrite it (supports_stats_init) initialises it on
         # its first call of the step, so no zero-fill is launched
         fresh = bool(getattr(s1, "supports_stats_init", False))
@@ -427,17 +480,19 @@ class PipelineEngine:
         woff = [0]
         for w in waves[:-1]:
             woff.append(woff[-1] + w)
-        # part k of a wave goes to rank k; a wave smaller than R leaves some parts empty
-        parts = [split_sizes(b, R) + [0] * (R - min(b, R)) for b in waves]
+        P = self.rotate_parts(waves, R)
+        # rows crossing a link in wave w (all owners): 0 -> every rank skips that wave's collectives
+        crossing = [sum(P[w][o][k] for o in range(R) for k in range(R) if k != o) for w in range(W)]
 
-        def owner_part(o, w, k):  # (start, size) of part k of owner o's wave w
-            pk = parts[w]
-            return start + o * batch_size + woff[w] + sum(pk[:k]), pk[k]
+        def owner_part(o, w, k):  # (dataset start, size) of the rows of owner o's wave w that go to k
+            row = P[w][o]
+            off = 0 if k == o else row[o] + sum(row[j] for j in range(k) if j != o)
+            return start + o * batch_size + woff[w] + off, row[k]
 
         tm = PhaseTimer(dev, self.timing)
         ctx0 = [dict() for _ in waves]
         hkeep = [None] * W  # factored: the owner's boundary activation per wave (ReLU mask source)
-        recv, fwork = [None] * W, [None] * W
+        hloc, recv, fwork = [None] * W, [None] * W, [None] * W
         for w, bw in enumerate(waves):  # stage 0 forward + scatter of the boundary activation
             x = dataset.inputs(start + me * batch_size + woff[w], bw)
             if x.device != dev:
@@ -448,21 +503,21 @@ class PipelineEngine:
                 h = s0.fwd(x, ctx0[w], train)
             if factored:
                 hkeep[w] = h
-            if R == 1:
-                recv[w] = h
+            L = P[w][me][me]
+            hloc[w] = h if L == bw else h[:L]
+            if crossing[w] == 0:
                 continue
-            in_splits = parts[w]
-            out_splits = [parts[w][me] for _ in range(R)]  # every owner sends me its part `me`
-            buf = torch.empty((sum(out_splits),) + tuple(h.shape[1:]), dtype=h.dtype, device=dev)
-            fwork[w] = dist.all_to_all_single(buf, h.contiguous(), out_splits, in_splits, group=group, async_op=True)
+            in_splits = [0 if k == me else P[w][me][k] for k in range(R)]
+            out_splits = [0 if o == me else P[w][o][me] for o in range(R)]
+            buf = self.bufs.get(("a2a_fwd", w), (sum(out_splits),) + tuple(h.shape[1:]), h.dtype)
+            fwork[w] = self.transport.all_to_all(buf, h[L:], out_splits, in_splits, channel="fwd")
             recv[w] = buf
         back, bwork = [None] * W, [None] * W
-        bgroup = mesh.pipe_group_bwd or group
         # stage 0 expands the factor itself when it can (MLP first layer on uint8 pixels)
         fuse0 = factored and hasattr(s0, "bwd_from_factor") and hasattr(s1, "factor_weight")
         # one rank: the head's gradient/stats reduction is deferred into stage 0's weight-gradient
         # reduction launch (one launch instead of two per wave); `pend[w]` must be consumed or run
-        defer = fuse0 and R == 1
+        defer = fuse0 and not any(crossing)
         pend = [None] * W
         # ... and when nothing else touches the gradients before the optimizer (one rank, no gradient
         # all-reduce, stepping this call), the last wave's reduction applies the optimizer step too
@@ -470,11 +525,43 @@ class PipelineEngine:
                      and hasattr(self.optimizer, "fused_args") and hasattr(s0, "grad_span")
                      and hasattr(s1, "grad_span"))
         step_fused = [False]
+        if factored:
+            gshape, gdt = (s1.layers()[-1].out_features,), torch.float32
+        else:
+            gshape, gdt = tuple(self._boundary(0, 1)[0][1:]), self.spec.boundary_dtype
 
         def run_pending(w):
             if pend[w] is not None:
                 pend[w].run()
                 pend[w] = None
+
+        def head(xin, tgt, w):  # stage 1 forward + loss (+ its backward) on one block of rows
+            nonlocal fresh, count
+            if tgt.device != dev:
+                tgt = tgt.to(dev, non_blocking=True)
+            if factored:
+                with tm.span("fwd", 1):
+                    if defer:
+                        g, n, pend[w] = s1.head_fwd_factored(xin, tgt, scale, stats, stats_init=fresh,
+                                                             defer_reduce=True)
+                    else:
+                        g, n = s1.head_fwd_factored(xin, tgt, scale, stats, stats_init=fresh)
+                fresh = False
+                count += n
+                return g
+            c1 = {}
+            kw = {"stats_init": True} if fresh else {}
+            with tm.span("fwd", 1):
+                l, c, n = s1.head_fwd(xin, tgt, c1, train, scale, stats=stats, **kw)
+            fresh = False
+            if l is not None:
+                stats[0] += l.float()
+                stats[1] += c.float()
+            count += n
+            if not train:
+                return None
+            with tm.span("bwd", 1):
+                return s1.head_bwd(c1)
 
         def stage0_bwd(w):
             if bwork[w] is not None:
@@ -510,65 +597,47 @@ class PipelineEngine:
         # the compute stream then has work while wave w+1's activations are still on the links
         # (the backward exchange runs on its own communicator and, factored, is small)
         interleave = train and R > 1
-        for w in range(W):  # stage 1 (+ loss + its backward) on the received parts
+        for w, bw in enumerate(waves):  # stage 1 (+ loss + its backward): local rows, then received rows
+            L = P[w][me][me]
+            gloc = head(hloc[w], dataset.targets(*owner_part(me, w, me)), w) if L > 0 else None
+            hloc[w] = None
+            if crossing[w] == 0:
+                back[w] = gloc
+                if interleave:
+                    stage0_bwd(w)
+                continue
             if fwork[w] is not None:
                 with tm.span("recv_wait", 0):
                     fwork[w].wait()
-            tg = [dataset.targets(*owner_part(o, w, me)) for o in range(R)]
-            tgt = tg[0] if R == 1 else torch.cat(tg)
-            if tgt.device != dev:
-                tgt = tgt.to(dev, non_blocking=True)
-            if tgt.numel() > 0 and factored:
-                with tm.span("fwd", 1):
-                    if defer:
-                        g, n, pend[w] = s1.head_fwd_factored(recv[w], tgt, scale, stats, stats_init=fresh,
-                                                             defer_reduce=True)
-                    else:
-                        g, n = s1.head_fwd_factored(recv[w], tgt, scale, stats, stats_init=fresh)
-                fresh = False
-                count += n
-            elif tgt.numel() > 0:
-                c1 = {}
-                kw = {"stats_init": True} if fresh else {}
-                with tm.span("fwd", 1):
-                    l, c, n = s1.head_fwd(recv[w], tgt, c1, train, scale, stats=stats, **kw)
-                fresh = False
-                if l is not None:
-                    stats[0] += l.float()
-                    stats[1] += c.float()
-                count += n
-                if train:
-                    with tm.span("bwd", 1):
-                        g = s1.head_bwd(c1)
-            elif train:  # no rows for me in this wave: still join the backward exchange
-                if factored:
-                    g = torch.empty((0, s1.layers()[-1].out_features), dtype=torch.float32, device=dev)
-                else:
-                    shape, dt = self._boundary(0, 0)
-                    g = torch.empty(shape, dtype=dt, device=dev)
+            srcs = [o for o in range(R) if o != me and P[w][o][me] > 0]
+            grecv = None
+            if srcs:
+                tg = [dataset.targets(*owner_part(o, w, me)) for o in srcs]
+                grecv = head(recv[w], tg[0] if len(tg) == 1 else torch.cat(tg), w)
+            recv[w] = None
             if not train:
                 continue
-            if R == 1:
-                back[w] = g
-                continue
-            out_splits = parts[w]
-            in_splits = [parts[w][me] for _ in range(R)]
-            buf = torch.empty((sum(out_splits),) + tuple(g.shape[1:]), dtype=g.dtype, device=dev)
-            bwork[w] = dist.all_to_all_single(buf, g.contiguous(), out_splits, in_splits, group=bgroup,
-                                              async_op=True)
-            back[w] = buf
+            # the received rows' gradients go back to their owners, into the own-rows gradient
+            # buffer right after the local rows' part: [local | from peer k1 | from peer k2 ...]
+            if grecv is None:  # nothing received this wave: still join the backward exchange
+                grecv = torch.empty((0,) + gshape, dtype=gdt, device=dev)
+            out_splits = [0 if k == me else P[w][me][k] for k in range(R)]
+            in_splits = [0 if o == me else P[w][o][me] for o in range(R)]
+            G = self.bufs.get(("grad_own", w), (bw,) + gshape, gdt)
+            if L > 0:
+                G[:L].copy_(gloc)
+            bwork[w] = self.transport.all_to_all(G[L:], grecv, out_splits, in_splits, channel="bwd")
+            back[w] = G
             if interleave:
                 stage0_bwd(w)
         if train:
-            self.grad_sync.stage_done(1)
             if not interleave:
                 for w in range(W):
                     stage0_bwd(w)
             for w in range(W):  # (nothing is left unless a stage-0 backward was skipped)
                 run_pending(w)
-            self.grad_sync.stage_done(0)
-            with tm.span("grad_sync"):
-                self.grad_sync.finish()
+            with tm.span("grad_sync"):  # both stages' gradients in one collective
+                self.grad_sync.finish_all()
             if step_optimizer:
                 with tm.span("optim"):
                     if step_fused[0]:  # applied by the last weight-gradient reduction
@@ -590,7 +659,7 @@ class PipelineEngine:
             v.zero_()
         if self.mesh.world_size > 1:
             # every pipeline's last stage contributes once; the other ranks contribute zeros
-            dist.all_reduce(v, group=group)
+            self.transport.all_reduce(v, group=group, async_op=False)
         v = v.cpu()
         return float(v[0]), int(v[1]), int(v[2])
 

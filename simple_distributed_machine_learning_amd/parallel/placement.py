@@ -1,0 +1,148 @@
+"""Where the two stages of the headline MLP run on an N-GPU node: a link/compute cost model.
+
+The reference places stage 0 on rank 0 and stage 1 on rank 1 and moves every boundary tensor
+between them (/root/reference/simple_distributed.py:33-37, :47-49, :71, :112). On MI355X the
+784-128-10 MLP computes a sample in ~1.4 ns, while its boundary costs 512 B forward plus 40 B back
+(factored gradient, parallel/pipeline.py) — ~11 ns on one xGMI link. So where the boundary goes is
+the main decision of a multi-GPU run, and it is made here from a model instead of by default:
+
+``pp2dp``     the reference's placement, replicated: GPU pairs (stage 0 | stage 1) with the
+              Chimera schedule (both directions, so both GPUs do equal work), data-parallel over
+              N/2 pairs; every boundary byte goes over the pair's ONE link.
+``rotate``    every GPU owns a data shard and hosts both stages; an equal share of every wave's
+              rows runs stage 1 on each peer, so the boundary fans out over all N-1 links.
+``dp``        both stages on every GPU, nothing crosses (rows stay on their owner); only the
+              gradient all-reduce uses the links.
+``balanced``  rotate with the cross-GPU fraction phi chosen so that the boundary traffic the
+              links carry stays under the compute it overlaps (``link_budget`` of the step).
+
+The model (documented in README "Multi-GPU placement") is deliberately simple:
+
+* compute per GPU = rows x ns/row of each stage it runs + a fixed per-step cost (measured on one
+  MI355X, ``ComputeModel``);
+* link time = the busiest link's bytes / ``LinkModel.gbps`` + one launch latency per collective;
+* the exchange overlaps compute (the transfers run on RCCL streams beside the kernels of other
+  waves and of the local rows): step = max(compute, link) + the part that cannot overlap (the
+  first wave's forward exchange when nothing local is left to compute, a fixed ``exposed``
+  fraction of the link time);
+* gradient all-reduce: ring over N GPUs of the parameter bytes, after the last backward.
+
+``choose`` returns the placement with the smallest predicted step; among placements within 2% of
+it, the one that moves the most boundary bytes across GPUs (the split the benchmark is about).
+"""
+from __future__ import annotations
+
+from dataclasses import asdict, dataclass
+from typing import Dict, Optional, Tuple
+
+PLACEMENTS = ("auto", "balanced", "rotate", "dp", "pp2dp")
+
+
+@dataclass
+class LinkModel:
+    # sustained RCCL bytes/s per xGMI link and direction while kernels share the GPU (MI355X: 7 links
+    # of 153.6 GB/s bidirectional peak each; RCCL all-to-all reaches roughly 2/3 of a direction's peak)
+    gbps: float = 50.0
+    links: int = 7
+    collective_us: float = 12.0   # launch + handshake per collective
+    exposed: float = 0.15         # fraction of the link time that cannot hide under compute
+    link_budget: float = 0.75     # balanced: keep the busiest link busy at most this share of the step
+
+
+@dataclass
+class ComputeModel:
+    """Per-row costs of the 784-128-10 stages on one MI355X at 131072 rows per GPU
+    (profiles/r2_fused_step_bench_n1_kernel_stats.txt: uint8 forward 61 us + weight gradient 78 us
+    + reduction/SGD 12 us for stage 0; fused head 25.6 us for stage 1)."""
+    s0_ns: float = 1.06
+    s1_ns: float = 0.195
+    fixed_us: float = 12.0
+    act_bytes: int = 512          # boundary activation per row (128 fp32)
+    grad_bytes: int = 40          # factored boundary gradient per row (10 fp32)
+    param_bytes: int = 101_770 * 4
+
+
+def predict(placement: str, n: int, batch_per_gpu: int, waves: int = 2, phi: Optional[float] = None,
+            link: LinkModel = LinkModel(), comp: ComputeModel = ComputeModel()) -> Dict[str, float]:
+    """Predicted step of ``placement`` at ``n`` GPUs (weak scaling: ``batch_per_gpu`` rows per GPU)."""
+    B = float(batch_per_gpu)
+    row = comp.act_bytes + comp.grad_bytes
+    if n == 1:
+        placement, phi = "dp", 0.0
+    if placement == "rotate":
+        phi = (n - 1) / n
+    if placement == "dp":
+        phi = 0.0
+    compute_us = B * (comp.s0_ns + comp.s1_ns) / 1e3 + comp.fixed_us
+    if placement == "pp2dp":
+        if n % 2:
+            raise ValueError("pp2dp needs an even number of GPUs")
+        # Chimera: each GPU runs stage 0 for its own B rows and stage 1 for its partner's B rows;
+        # all B rows' boundary crosses the pair's single link in each direction
+        link_bytes = B * row
+        ncoll = 4 * waves  # per micro-batch: act + grad, both directions
+        phi = 1.0
+        cross_bytes = B * row
+    else:
+        phi = float(phi or 0.0)
+        cross_bytes = phi * B * row
+        link_bytes = cross_bytes / max(1, n - 1)
+        ncoll = 2 * waves if phi > 0 else 0
+    link_us = link_bytes / (link.gbps * 1e3) + ncoll * link.collective_us
+    if n > 1:  # ring all-reduce of the gradients (2 (n-1)/n of the bytes per GPU, over 2 ring links)
+        ar_us = 2 * (n - 1) / n * comp.param_bytes / (2 * link.gbps * 1e3) + link.collective_us
+    else:
+        ar_us = 0.0
+    if link_bytes > 0:
+        step_us = max(compute_us, link_us) + link.exposed * link_us + ar_us
+    else:
+        step_us = compute_us + ar_us
+    return {
+        "placement": placement, "n_gpus": n, "cross_fraction": round(phi, 4),
+        "compute_ms": round(compute_us / 1e3, 4), "link_ms": round(link_us / 1e3, 4),
+        "allreduce_ms": round(ar_us / 1e3, 4), "step_ms": round(step_us / 1e3, 4),
+        "samples_per_s": round(n * B / (step_us / 1e6), 1),
+        "boundary_bytes_per_gpu": int(cross_bytes), "busiest_link_bytes": int(link_bytes),
+    }
+
+
+def balanced_fraction(n: int, batch_per_gpu: int, link: LinkModel = LinkModel(),
+                      comp: ComputeModel = ComputeModel(), waves: int = 2) -> float:
+    """Largest phi whose busiest-link time stays within ``link_budget`` of the compute it overlaps."""
+    if n == 1:
+        return 0.0
+    B = float(batch_per_gpu)
+    compute_us = B * (comp.s0_ns + comp.s1_ns) / 1e3 + comp.fixed_us
+    budget_us = link.link_budget * compute_us - 2 * waves * link.collective_us
+    if budget_us <= 0:
+        return 0.0
+    per_link_bytes = budget_us * link.gbps * 1e3
+    phi = per_link_bytes * (n - 1) / (B * (comp.act_bytes + comp.grad_bytes))
+    phi = min(phi, (n - 1) / n)
+    return max(0.0, round(phi * 64) / 64)  # a 1/64 grid: the same phi on every rank, readable in logs
+
+
+def table(n: int, batch_per_gpu: int, waves: int = 2, link: LinkModel = LinkModel(),
+          comp: ComputeModel = ComputeModel()) -> Dict[str, Dict[str, float]]:
+    out = {}
+    for p in ("balanced", "rotate", "dp", "pp2dp"):
+        if p == "pp2dp" and (n % 2 or n == 1):
+            continue
+        phi = balanced_fraction(n, batch_per_gpu, link, comp, waves) if p == "balanced" else None
+        out[p] = predict(p, n, batch_per_gpu, waves, phi, link, comp)
+    return out
+
+
+def choose(n: int, batch_per_gpu: int, waves: int = 2, link: LinkModel = LinkModel(),
+           comp: ComputeModel = ComputeModel()) -> Tuple[str, float, Dict[str, Dict[str, float]]]:
+    """(placement, cross_fraction, predictions): the fastest predicted placement; within 2% of it,
+    the one that sends the most boundary bytes across GPUs."""
+    t = table(n, batch_per_gpu, waves, link, comp)
+    best = min(v["step_ms"] for v in t.values())
+    near = [p for p, v in t.items() if v["step_ms"] <= best * 1.02]
+    pick = max(near, key=lambda p: (t[p]["boundary_bytes_per_gpu"], -t[p]["step_ms"]))
+    return pick, t[pick]["cross_fraction"], t
+
+
+def model_dict(link: LinkModel = LinkModel(), comp: ComputeModel = ComputeModel()) -> Dict[str, Dict[str, float]]:
+    return {"link": asdict(link), "compute": asdict(comp)}

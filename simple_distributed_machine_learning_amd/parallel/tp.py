@@ -27,7 +27,6 @@ from dataclasses import dataclass
 from typing import Optional
 
 import torch
-import torch.distributed as dist
 
 
 @dataclass
@@ -35,13 +34,14 @@ class TPContext:
     size: int
     rank: int
     group: Optional[object]  # None when size == 1
+    transport: Optional[object] = None  # parallel/p2p.py Transport of the rank
 
 
 def _all_reduce(x: torch.Tensor, ctx: TPContext) -> torch.Tensor:
     if ctx.size == 1:
         return x
     x = x.contiguous()
-    dist.all_reduce(x, group=ctx.group)
+    ctx.transport.all_reduce(x, group=ctx.group, async_op=False)
     return x
 
 

@@ -11,11 +11,24 @@ import torch.multiprocessing as mp
 
 
 def free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A free TCP port; under pytest-xdist each worker draws from its own range, so two tests that
+    run at once cannot pick the same rendezvous port between its probe and its use."""
+    import random
+
+    wid = os.environ.get("PYTEST_XDIST_WORKER", "gw0")
+    slot = int(wid[2:]) if wid[2:].isdigit() else 0
+    lo = 20000 + (slot % 16) * 2500
+    for _ in range(200):
+        p = random.randint(lo, lo + 2499)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    raise RuntimeError("no free port")
 
 
 def _entry(rank, world, port, fn, args, outdir):

@@ -9,18 +9,26 @@ def train_worker(rank, world, model, kind, M, pp, steps, B, seed=3, kw=None, tp=
     from simple_distributed_machine_learning_amd.models import get_model_spec
     from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh
 
-    kw = kw or {}
-    mesh = init_mesh(pp=pp, schedule_kind=kind, rank=rank, world_size=world, device=torch.device("cpu"),
-                     backend="gloo", timeout_s=120, tp=tp)
+    kw = dict(kw or {})
+    # engine/mesh options (not model options): device ("cpu" | "cuda"), transport, cross_fraction
+    dev = torch.device(kw.pop("device", "cpu"))
+    transport = kw.pop("transport", None)
+    eng_kw = {k: kw.pop(k) for k in ("cross_fraction",) if k in kw}
+    mesh = init_mesh(pp=pp, schedule_kind=kind, rank=rank, world_size=world, device=dev,
+                     backend="gloo", timeout_s=120, tp=tp, transport=transport)
     spec = get_model_spec(model, kw.get("stages"), **{k: v for k, v in kw.items() if k not in ("stages", "pixels")})
-    eng = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=seed)
+    eng = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=seed,
+                         **eng_kw)
     S = eng.data_shards
     if spec.input_kind == "tokens":
-        ds = SyntheticTokens(B * S * steps, kw.get("seq_len", 16), 97, seed=7)
+        ds = SyntheticTokens(B * S * steps, kw.get("seq_len", 16), 97, seed=7, device=dev)
     else:
-        ds = SyntheticMNIST(B * S * steps, seed=7, pixels=kw.get("pixels", "f32"))
+        ds = SyntheticMNIST(B * S * steps, seed=7, pixels=kw.get("pixels", "f32"), device=dev)
     losses = []
+    allocs_first = None
     for step in range(steps):
+        if step == 1:
+            allocs_first = eng.bufs.allocations
         res = eng.run(ds, eng.local_start(step * B * S, B), B, train=True, global_batch=B * S)
         l, c, n = eng.reduce_metrics(res)
         losses.append(l / n)
@@ -30,4 +38,6 @@ def train_worker(rank, world, model, kind, M, pp, steps, B, seed=3, kw=None, tp=
     el, ec, en = eng.reduce_metrics(res)
     return {"losses": losses, "state": eng.state_dicts(), "dp_rank": mesh.dp_rank, "pp_rank": mesh.pp_rank,
             "tp_rank": mesh.tp_rank,
-            "eval": (el, ec, en), "bytes_sent": eng.transport.bytes_sent if eng.transport else 0}
+            "eval": (el, ec, en), "bytes_sent": eng.transport.bytes_sent if eng.transport else 0,
+            "transport": eng.transport.name if eng.transport else None,
+            "pool_allocs": eng.bufs.allocations, "pool_allocs_first": allocs_first}

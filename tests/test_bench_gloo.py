@@ -1,10 +1,12 @@
-"""bench.py's multi-rank path (rotate schedule, all-to-all stage boundary, sharded synthetic data,
-MAX-over-ranks timing, one JSON line from rank 0) rehearsed on Gloo/CPU with 4 ranks."""
+"""bench.py's multi-rank paths (every placement, sharded synthetic data, MAX-over-ranks timing, the
+measured boundary bytes, one JSON line from rank 0) rehearsed on Gloo/CPU with 2 and 4 ranks."""
 import contextlib
 import io
 import json
 import os
 import sys
+
+import pytest
 
 from dist_util import run_ranks
 
@@ -23,11 +25,33 @@ def _bench_worker(rank, world, argv):
     return buf.getvalue()
 
 
-def test_bench_rotate_four_ranks_one_json_line():
-    outs = run_ranks(_bench_worker, 4, ["--gpus", "4", "--steps", "2", "--warmup", "1"], timeout=300)
+def _run(world, extra=()):
+    outs = run_ranks(_bench_worker, world, ["--gpus", str(world), "--steps", "2", "--warmup", "1", *extra],
+                     timeout=300)
     lines = [l for l in outs[0].splitlines() if l.startswith("{")]
     assert len(lines) == 1 and all(not o.strip() for o in outs[1:])
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 4 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
-    assert d["config"]["global_batch"] == 4 * 256 and d["value"] > 0 and d["higher_is_better"] is True
+    assert d["n_gpus"] == world and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
+    assert d["config"]["global_batch"] == world * 256 and d["value"] > 0 and d["higher_is_better"] is True
     assert d["final_loss"] is not None and d["final_loss"] == d["final_loss"]  # finite
+    return d
+
+
+@pytest.mark.parametrize("placement", ["auto", "rotate", "balanced", "pp2dp"])
+def test_bench_four_ranks_one_json_line(placement):
+    d = _run(4, ["--placement", placement])
+    c = d["config"]
+    assert set(c["predicted"]) >= {"rotate", "dp", "balanced", "pp2dp"}
+    assert c["placement"] == (placement if placement != "auto" else c["placement"])
+    rows = 256
+    if c["placement"] == "rotate":  # 3/4 of every owner's rows cross: 512 B forward + 40 B back each
+        assert c["boundary_bytes_across_gpus_per_step"] == 4 * (rows - rows // 4) * (512 + 40)
+    if c["placement"] == "dp":
+        assert c["boundary_bytes_across_gpus_per_step"] == 0
+    if c["placement"] == "pp2dp":  # every row's activation and full gradient cross the pair's link
+        assert c["boundary_bytes_across_gpus_per_step"] == 4 * rows * (512 + 512)
+
+
+def test_bench_two_ranks_cross_fraction_override():
+    d = _run(2, ["--placement", "rotate", "--cross_fraction", "0.25"])
+    assert d["config"]["boundary_bytes_across_gpus_per_step"] == 2 * 64 * (512 + 40)

@@ -184,3 +184,36 @@ def test_mlp_rotate_alltoall_ragged_small_batches(B, M):
     res = run_ranks(train_worker, 2, "mlp", "rotate", M, 2, steps, B)
     ref = _single("mlp", 1, steps, 2 * B)
     _compare(res, ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("world,phi", [(2, 0.0), (2, 0.25), (2, 1.0), (4, 0.5)])
+@pytest.mark.parametrize("pixels", ["f32", "u8"])
+def test_mlp_rotate_cross_fraction_matches_single_process(world, phi, pixels):
+    """rotate with a chosen cross-GPU fraction (parallel/placement.py): phi = 0 is data parallelism over
+    replicated stages (no boundary collective at all), 1.0 sends every row to a peer; every split trains
+    to the single-process weights."""
+    B, steps, M = 24, 2, 2 * world
+    kw = {"cross_fraction": phi, "pixels": pixels}
+    res = run_ranks(train_worker, world, "mlp", "rotate", M, world, steps, B, 3, kw)
+    ref = _single("mlp", M, steps, world * B, "rotate", {"pixels": pixels})
+    _compare(res, ref, rtol=1e-4, atol=1e-5)
+    assert all((r["bytes_sent"] > 0) == (phi > 0) for r in res)
+
+
+@pytest.mark.parametrize("kind,world,pp,M", [("rotate", 2, 2, 4), ("1f1b", 2, 2, 3), ("1f1b", 4, 2, 2),
+                                             ("chimera", 2, 2, 4)])
+def test_host_staged_transport_matches_direct(kind, world, pp, M):
+    """The host-staged transport (what multi-rank runs on ONE GPU use) is interchangeable with the
+    direct one: same weights, same losses, same bytes."""
+    B, steps = 16, 3
+    direct = run_ranks(train_worker, world, "mlp", kind, M, pp, steps, B, 3, {"transport": "direct"})
+    host = run_ranks(train_worker, world, "mlp", kind, M, pp, steps, B, 3, {"transport": "host"})
+    assert {r["transport"] for r in host} == {"host"} and {r["transport"] for r in direct} == {"direct"}
+    for a, b in zip(host, direct):
+        assert a["bytes_sent"] == b["bytes_sent"]
+        for s in a["state"]:
+            for k in a["state"][s]:
+                torch.testing.assert_close(a["state"][s][k], b["state"][s][k], rtol=0, atol=0)
+        assert a["losses"] == b["losses"]
+        # persistent boundary buffers: nothing new after the first step
+        assert a["pool_allocs"] == a["pool_allocs_first"]

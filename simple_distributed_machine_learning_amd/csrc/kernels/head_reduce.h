@@ -56,13 +56,14 @@ __device__ __forceinline__ void head_reduce_block(const HeadReduceArgs& a, int b
         sgd_update4(sg->hp + o4, sg->hbuf + o4, d, SgdRule{sg->lr, sg->mom, sg->damp, sg->wd, sg->nesterov, sg->first});
         *reinterpret_cast<sgd_f32x4*>(gp) = sg->zero_grad ? sgd_f32x4{0.f, 0.f, 0.f, 0.f} : d;
       } else {  // ragged tail (CK + C not a multiple of 4): the padding after gb is zero in every buffer
-        float pt[4], bt[4];  // (hbuf is null without momentum: the rule then never reads it)
+        sgd_f32x4 pt, bt;  // 16-B aligned locals (hbuf is null without momentum: the rule then never reads it)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           pt[j] = j < n4 ? sg->hp[o4 + j] : 0.f;
           bt[j] = (j < n4 && sg->hbuf) ? sg->hbuf[o4 + j] : 0.f;
         }
-        sgd_update4(pt, bt, d, SgdRule{sg->lr, sg->mom, sg->damp, sg->wd, sg->nesterov, sg->first});
+        sgd_update4(reinterpret_cast<float*>(&pt), reinterpret_cast<float*>(&bt), d,
+                    SgdRule{sg->lr, sg->mom, sg->damp, sg->wd, sg->nesterov, sg->first});
         for (int j = 0; j < n4; ++j) {
           sg->hp[o4 + j] = pt[j];
           if (sg->hbuf) sg->hbuf[o4 + j] = bt[j];

@@ -1,0 +1,132 @@
+// One 16-row tile of the MFMA classifier head (K = 128 hidden, C <= 16 classes), shared by
+// head_xent.hip's head_mfma_kernel (h read from HBM) and mlp_u8.hip's fused uint8 forward + head
+// (h never leaves the workgroup: it is staged in LDS straight from the forward's accumulators).
+// Both call the same two device functions, so their logits, dlogits and dW^T products are the same
+// operations in the same order (the fused kernel's dl is bit-identical to the standalone head's).
+//
+// Lane l = (r = l % 16, g = l / 16), fp32 MFMAs (v_mfma_f32_16x16x4_f32):
+//   logits^T = W x^T : A = W (lane: class r), B = x^T (lane: row r), k = 16u + 4g + e over 32 MFMAs;
+//     lane (r, g) ends with row r's logits of classes 4g .. 4g+3 (bias as the initial value), so
+//     softmax / NLL / argmax reduce 4 values in-lane plus two symmetric xor-shuffles
+//   dW^T += x^T dz : x read back transposed from the tile's LDS image (xt_at layout) and dz through a
+//     wave-private 16 x 16 transpose; dW^T stays in registers across the wave's tiles.
+// Reference op: /root/reference/simple_distributed.py:77-79 (fc2, log_softmax), :111 (nll_loss).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace sdml {
+namespace headtile {
+
+typedef float f32x4m __attribute__((ext_vector_type(4)));
+constexpr int HKT = 128;  // hidden width
+constexpr int DTP = 16;   // dz transpose pitch
+
+// x tile image [16 rows][128] with the 16-B chunk c of row rho's 16-float group at c ^ swz(rho) and
+// group q at q ^ (rho & 3): rows r and r + 4 of a ds_write_b128 phase land in different banks, and
+// the column reads (rows 4kk + g, columns 16t + r) cover 64 distinct banks
+__device__ __forceinline__ int swz(int rho) { return 4 * ((rho >> 2) & 3); }
+__device__ __forceinline__ int xt_at(int rho, int q, int j) {
+  return rho * HKT + 16 * (q ^ (rho & 3)) + (j ^ swz(rho));
+}
+
+__device__ __forceinline__ f32x4m mfma4(float a, float b, f32x4m c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+struct TileAcc {
+  f32x4m gw[8];  // dW^T: gw[t][v] = dW[class r][hidden 16 t + 4 g + v]
+  float gbp, loss, corr, amx;
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) gw[t] = f32x4m{0.f, 0.f, 0.f, 0.f};
+    gbp = loss = corr = amx = 0.f;
+  }
+};
+
+// logits, log_softmax, NLL (loss accumulated for valid rows), argmax (correct), and when `train`
+// dz = scale (softmax - onehot) for the lane's 4 classes (0 for invalid rows / classes >= C),
+// optionally stored to dl [row][C]; amx tracks max_row sum_c |dz_c| (the |dl @ W| bound).
+// wl[u][e] = W[class r][16u + 4g + e]; xv[u][e] = x[row r][16u + 4g + e]; bv = bias of classes 4g..
+template <int C>
+__device__ __forceinline__ void logits_dz(const f32x4m (&wl)[8], const f32x4m& bv, const f32x4m (&xv)[8], int tg_raw,
+                                          bool valid, bool train, float scale, int g, TileAcc& a, float (&dz)[4],
+                                          float* dl_row, bool track_amax) {
+  f32x4m z = bv;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) z = mfma4(wl[u][e], xv[u][e], z);
+  float zc[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) zc[v] = (4 * g + v) < C ? z[v] : -INFINITY;
+  // row max and first argmax over the 4 lane groups (symmetric combines)
+  float mx = zc[0];
+  int am = 4 * g;
+#pragma unroll
+  for (int v = 1; v < 4; ++v)
+    if (zc[v] > mx) {
+      mx = zc[v];
+      am = 4 * g + v;
+    }
+#pragma unroll
+  for (int off = 16; off <= 32; off <<= 1) {
+    const float om = __shfl_xor(mx, off);
+    const int oa = __shfl_xor(am, off);
+    const bool take = om > mx || (om == mx && oa < am);
+    mx = take ? om : mx;
+    am = take ? oa : am;
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) se += __expf(zc[v] - mx);
+  se += __shfl_xor(se, 16);
+  se += __shfl_xor(se, 32);
+  const float lse = mx + __logf(se);
+  const int tg = valid ? tg_raw : -1;
+  float zt = zc[0];
+#pragma unroll
+  for (int v = 1; v < 4; ++v) zt = (tg & 3) == v ? zc[v] : zt;
+  a.loss += (valid && (tg >> 2) == g) ? lse - zt : 0.f;
+  a.corr += (valid && g == 0 && am == tg) ? 1.f : 0.f;
+  if (!train) return;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int c = 4 * g + v;
+    dz[v] = (valid && c < C) ? scale * (__expf(zc[v] - lse) - (c == tg ? 1.f : 0.f)) : 0.f;
+  }
+  if (dl_row) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      if (valid && 4 * g + v < C) dl_row[4 * g + v] = dz[v];
+  }
+  if (track_amax) {  // (invalid rows and classes >= C hold dz == 0)
+    float sa = (fabsf(dz[0]) + fabsf(dz[1])) + (fabsf(dz[2]) + fabsf(dz[3]));
+    sa += __shfl_xor(sa, 16);
+    sa += __shfl_xor(sa, 32);
+    a.amx = fmaxf(a.amx, sa);
+  }
+}
+
+// dW^T += x^T dz, db += dz: xw = this tile's x image (xt_at layout, complete and visible to the wave),
+// dw = the wave's 16 x DTP dz transpose scratch
+__device__ __forceinline__ void dw_accum(const float* xw, float* dw, const float (&dz)[4], int r, int g, TileAcc& a) {
+  *reinterpret_cast<f32x4m*>(dw + r * DTP + ((4 * g) ^ swz(r))) = f32x4m{dz[0], dz[1], dz[2], dz[3]};
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  float db[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    db[kk] = dw[(4 * kk + g) * DTP + (r ^ swz(4 * kk + g))];
+    a.gbp += db[kk];
+  }
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) a.gw[t] = mfma4(xw[xt_at(4 * kk + g, t, r)], db[kk], a.gw[t]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next tile's writes
+  __builtin_amdgcn_wave_barrier();
+}
+
+}  // namespace headtile
+}  // namespace sdml

@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "head_reduce.h"
+#include "head_tile.h"
 #include "kernels.h"
 
 namespace sdml {
@@ -549,15 +550,13 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
 // store (40.9 vs 38.2 us); 3 waves per SIMD (W re-read from LDS per tile, no register prefetch,
 // 158 VGPRs, 512-1024 blocks) - 38.6 vs 36.5 us. Per block (4 waves) the dW, db, loss and correct partials meet in LDS
 // in wave order and leave as one slab row (head_reduce_kernel sums the slabs in block order).
-typedef float f32x4m __attribute__((ext_vector_type(4)));
+using headtile::f32x4m;
+using headtile::mfma4;
+using headtile::swz;
+using headtile::xt_at;
 constexpr int MW = 4;          // waves per block
 constexpr int WSP = HK + 4;    // W pitch in LDS: the per-wave fragment reads hit distinct banks
-constexpr int DTP = 16;        // dz tile pitch
-// transposes: 16-B chunk c of row rho's 16-float group sits at c ^ swz(rho), and x's 16-float
-// group q of row rho at q ^ (rho & 3): rows r and r+4 of a ds_write_b128 phase land in different
-// banks, and the column reads (rows 4kk + g, columns 16t + r) cover 64 distinct banks
-__device__ __forceinline__ int swz(int rho) { return 4 * ((rho >> 2) & 3); }
-__device__ __forceinline__ int xt_at(int rho, int q, int j) { return rho * HK + 16 * (q ^ (rho & 3)) + (j ^ swz(rho)); }
+constexpr int DTP = headtile::DTP;  // dz tile pitch
 
 __device__ __forceinline__ void stage_w16(const float* __restrict__ W, int C, float* ws, int tid, int nthr) {
   for (int i = tid; i < 16 * HK / 4; i += nthr) {
@@ -565,10 +564,6 @@ __device__ __forceinline__ void stage_w16(const float* __restrict__ W, int C, fl
     *reinterpret_cast<f32x4m*>(ws + c * WSP + 4 * k4) =
         c < C ? reinterpret_cast<const f32x4m*>(W)[i] : f32x4m{0.f, 0.f, 0.f, 0.f};
   }
-}
-
-__device__ __forceinline__ f32x4m mfma4(float a, float b, f32x4m c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 // wd[t][kk] = W[class 4 g + kk][hidden 16 t + r] (zero for classes >= C)
@@ -633,10 +628,8 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
 #pragma unroll
   for (int v = 0; v < 4; ++v) bv[v] = (4 * g + v) < C ? bias[4 * g + v] : 0.f;
 
-  f32x4m gw[8];  // dW^T tiles: gw[t][v] = dW[class r][hidden 16 t + 4 g + v]
-#pragma unroll
-  for (int t = 0; t < 8; ++t) gw[t] = f32x4m{0.f, 0.f, 0.f, 0.f};
-  float gbp = 0.f, loss_acc = 0.f, corr_acc = 0.f, amx = 0.f;
+  headtile::TileAcc acc;  // dW^T tiles, db, loss, correct and |dx| bound partials of this wave
+  acc.zero();
   float* xw = xt[wave];
   float* dw = dzt[wave];
 
@@ -645,61 +638,10 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
     constexpr bool FULL = decltype(full_c)::value;
     const int row = row0 + r;
     const bool valid = FULL || row < M;
-    f32x4m z = bv;
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) z = mfma4(wl[u][e], xv[u][e], z);
-    float zc[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) zc[v] = (4 * g + v) < C ? z[v] : -INFINITY;
-    // row max and first argmax over the 4 lane groups (symmetric combines)
-    float mx = zc[0];
-    int am = 4 * g;
-#pragma unroll
-    for (int v = 1; v < 4; ++v)
-      if (zc[v] > mx) {
-        mx = zc[v];
-        am = 4 * g + v;
-      }
-#pragma unroll
-    for (int off = 16; off <= 32; off <<= 1) {
-      const float om = __shfl_xor(mx, off);
-      const int oa = __shfl_xor(am, off);
-      const bool take = om > mx || (om == mx && oa < am);
-      mx = take ? om : mx;
-      am = take ? oa : am;
-    }
-    float se = 0.f;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) se += __expf(zc[v] - mx);
-    se += __shfl_xor(se, 16);
-    se += __shfl_xor(se, 32);
-    const float lse = mx + __logf(se);
-    const int tg = valid ? tg_raw : -1;
-    float zt = zc[0];
-#pragma unroll
-    for (int v = 1; v < 4; ++v) zt = (tg & 3) == v ? zc[v] : zt;
-    loss_acc += (valid && (tg >> 2) == g) ? lse - zt : 0.f;
-    corr_acc += (valid && g == 0 && am == tg) ? 1.f : 0.f;
-    if (!train) return;
     float dz[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int c = 4 * g + v;
-      dz[v] = (valid && c < C) ? scale * (__expf(zc[v] - lse) - (c == tg ? 1.f : 0.f)) : 0.f;
-    }
-    if (dl) {
-#pragma unroll
-      for (int v = 0; v < 4; ++v)
-        if (valid && 4 * g + v < C) dl[(size_t)row * C + 4 * g + v] = dz[v];
-    }
-    if (dxmax) {  // (invalid rows and classes >= C hold dz == 0)
-      float sa = (fabsf(dz[0]) + fabsf(dz[1])) + (fabsf(dz[2]) + fabsf(dz[3]));
-      sa += __shfl_xor(sa, 16);
-      sa += __shfl_xor(sa, 32);
-      amx = fmaxf(amx, sa);
-    }
+    headtile::logits_dz<C>(wl, bv, xv, tg_raw, valid, train, scale, g, acc, dz, dl ? dl + (size_t)row * C : nullptr,
+                           dxmax != nullptr);
+    if (!train) return;
     if (DXP && dx) {
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
@@ -710,21 +652,7 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
     // dW^T += x^T dz through the wave-private transpose
 #pragma unroll
     for (int u = 0; u < 8; ++u) *reinterpret_cast<f32x4m*>(xw + xt_at(r, u, 4 * g)) = xv[u];
-    *reinterpret_cast<f32x4m*>(dw + r * DTP + ((4 * g) ^ swz(r))) = f32x4m{dz[0], dz[1], dz[2], dz[3]};
-    __builtin_amdgcn_wave_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    float db[4];
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      db[kk] = dw[(4 * kk + g) * DTP + (r ^ swz(4 * kk + g))];
-      gbp += db[kk];
-    }
-#pragma unroll
-    for (int t = 0; t < 8; ++t)
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) gw[t] = mfma4(xw[xt_at(4 * kk + g, t, r)], db[kk], gw[t]);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next tile's writes
-    __builtin_amdgcn_wave_barrier();
+    headtile::dw_accum(xw, dw, dz, r, g, acc);
   };
   auto run = [&](int row0, const f32x4m (&xv)[8], int tg) {
     if (row0 + 16 <= M) tile(std::true_type{}, row0, xv, tg);
@@ -756,21 +684,21 @@ __global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __re
     float* mine = xt[wave];  // [C][HK] of this wave
     if (r < C) {
 #pragma unroll
-      for (int t = 0; t < 8; ++t) *reinterpret_cast<f32x4m*>(mine + r * HK + 16 * t + 4 * g) = gw[t];
+      for (int t = 0; t < 8; ++t) *reinterpret_cast<f32x4m*>(mine + r * HK + 16 * t + 4 * g) = acc.gw[t];
     }
-    gbp += __shfl_xor(gbp, 16);
-    gbp += __shfl_xor(gbp, 32);
-    if (g == 0) red[wave][2 + r] = gbp;
+    acc.gbp += __shfl_xor(acc.gbp, 16);
+    acc.gbp += __shfl_xor(acc.gbp, 32);
+    if (g == 0) red[wave][2 + r] = acc.gbp;
   }
   for (int off = 32; off > 0; off >>= 1) {
-    loss_acc += __shfl_xor(loss_acc, off);
-    corr_acc += __shfl_xor(corr_acc, off);
-    amx = fmaxf(amx, __shfl_xor(amx, off));
+    acc.loss += __shfl_xor(acc.loss, off);
+    acc.corr += __shfl_xor(acc.corr, off);
+    acc.amx = fmaxf(acc.amx, __shfl_xor(acc.amx, off));
   }
   if (lane == 0) {
-    red[wave][0] = loss_acc;
-    red[wave][1] = corr_acc;
-    redm[wave] = amx;
+    red[wave][0] = acc.loss;
+    red[wave][1] = acc.corr;
+    redm[wave] = acc.amx;
   }
   __syncthreads();
   static_assert(MW == 4, "wave-partial sums below are written for 4 waves");

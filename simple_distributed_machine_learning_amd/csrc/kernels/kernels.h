@@ -118,8 +118,32 @@ constexpr int kU8FwdPlanes = 2;
 int u8_fwd_kpad(int K);
 bool u8_fwd_supported(int M, int N, int K, int ldx, const void* X);
 void split_planes_pad(const float* w, unsigned short* out, int N, int K, int Kp, hipStream_t stream);
+// mask (optional, relu only): [M][N / 32] words, bit n % 32 of word n / 32 = (y[m][n] > 0), the ReLU
+// mask the factored weight gradient (u8_wgrad_dl) reads instead of y itself
 void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
-            const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream);
+            const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream,
+            unsigned* mask = nullptr);
+// The uint8 first layer and the classifier head in ONE kernel (N = 128 hidden, C in {2, 10, 16}, training):
+// h = relu(scale X W^T + b) stays in the workgroup (LDS, from the MFMA accumulators), the head
+// (head_tile.h: logits, log_softmax, NLL, argmax, dl = loss_scale (softmax - onehot), dW2^T/db2 partials)
+// runs on it, and only dl [M][C], the ReLU bits mask [M][4], one head slab row per block
+// ([C*128 dW2 | C db2 | loss, correct], reduced by head_reduce_run / u8_wgrad_dl) and one |dl @ W2|
+// bound per block leave the chip. h is never written.
+struct U8HeadArgs {
+  const float* w2 = nullptr;      // [C][128]
+  const float* b2 = nullptr;      // [C]
+  const int64_t* target = nullptr;
+  int C = 0;
+  float loss_scale = 0.f;
+  float* dl = nullptr;            // [M][C]
+  unsigned* mask = nullptr;       // [M][4]
+  float* part = nullptr;          // [u8_fwd_head_blocks(M)][C * 128 + C + 2]
+  float* bound = nullptr;         // [u8_fwd_head_blocks(M)]
+};
+bool u8_fwd_head_supported(int M, int N, int K, int ldx, const void* X, int C);
+int u8_fwd_head_blocks(int M);
+void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
+                 const float* bias, float scale, const U8HeadArgs& head, hipStream_t stream);
 // mlp_u8.hip: weight + bias gradient of the uint8-fed first layer (K = 784 pixel columns, N % 64 == 0,
 // M % 32 == 0): gw[N][784] += scale * dz^T X, gb[N] += colsum(dz), where gb MUST directly follow gw in
 // memory (gwb = gw, gwb + N * 784 = gb: the flat gradient buffer's layout). slab: workspace of
@@ -133,12 +157,14 @@ void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, fl
 // the same with the factored boundary gradient: dz = (dl @ w2) * (h > 0) (dl [M][C], w2 [C][N],
 // h [M][N]) expanded in the kernel's staging with head_dx_from_dl's exact arithmetic; without amax
 // (namax == 0) each workgroup bounds its dz by max_row sum_c |dl| * max |w2|. With the same amax the
-// result is bit-identical to head_dx_from_dl + u8_wgrad.
+// result is bit-identical to head_dx_from_dl + u8_wgrad. The ReLU mask comes from h [M][N] OR from
+// its bits (mask [M][N / 32], u8_fwd / u8_fwd_head): exactly one of h / mask is non-null.
 bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const void* h, int C);
 // head (optional): a deferred head reduction run in the same launch as this one's slab reduction
-void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const unsigned char* X, int M, int N, int ldx,
-                 float* slab, float* gwb, float scale, const float* amax, int namax, hipStream_t stream,
-                 const HeadReduceArgs* head = nullptr, const SgdFuse* sgd = nullptr);
+void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigned* mask, int C,
+                 const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
+                 const float* amax, int namax, hipStream_t stream, const HeadReduceArgs* head = nullptr,
+                 const SgdFuse* sgd = nullptr);
 // out[i] += sum_s slab[s * stride + i] in split order (n % 4 == 0, 16-B aligned)
 void slab_reduce(const float* slab, int64_t stride, int splits, float* out, int64_t n, hipStream_t stream);
 

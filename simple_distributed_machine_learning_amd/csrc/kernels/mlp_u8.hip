@@ -39,6 +39,7 @@
 #include <type_traits>
 
 #include "head_reduce.h"
+#include "head_tile.h"
 #include "kernels.h"
 #include "sgd_rule.h"
 #include "u8_planes.h"
@@ -124,7 +125,20 @@ struct FwdParams {
   int M, N, K, Kp, ldx, ldc;
   float scale;
   int relu;
+  unsigned* mask;  // optional [M][N / 32] ReLU bits (plain epilogue)
+  U8HeadArgs head;  // fused head epilogue (HEADC > 0)
 };
+
+// ---- fused classifier-head epilogue (HEADC > 0; NWR = 4, WMT = 2: 8 waves, 256 rows x 128 hidden per
+// block). LDS (floats): the block's h as 16 x-tile images of head_tile.h's xt_at layout [16][2048],
+// W2 zero-padded to 16 classes [16][FH_WSP], per-wave dz transposes [8][256], wave partials.
+constexpr int FH_ROWS = 256;
+constexpr int FH_WSP = 128 + 4;
+constexpr int FH_WS = FH_ROWS * 128;
+constexpr int FH_DZT = FH_WS + 16 * FH_WSP;
+constexpr int FH_RED = FH_DZT + 8 * 256;
+constexpr int FH_FLOATS = FH_RED + 8 * 18 + 8;
+static_assert(FH_FLOATS * 4 <= 160 * 1024, "LDS");
 
 // LDS images of one stage: X [BM rows][FBK bytes], W [NPL planes][128 rows][FBK fp16], chunks at
 // xpos / wpos. The DMA writes 1 KiB per wave-instruction lane-linearly (lane i -> bytes 16i..), so
@@ -162,11 +176,19 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
 // 2 = no DMA in the K loop (compute on stale LDS), 3 = no LDS reads (MFMA on register data)
 // TAIL = MFMA substeps of the last K-step (tail_substeps: only those holding k < K; chosen on the
 // host so the kernel carries one straight-line tail)
-template <int MODE, int WMT, int TAIL, int NWR>
+template <int C>
+__device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
+                                                    int m0, int wave, int lane, int wm, int wn);
+
+// HEADC = 0: store h = act(scale acc + b) (+ its ReLU bits when p.mask); HEADC = C > 0: the fused
+// classifier head on h (fused_head_epilogue), h is never stored
+template <int MODE, int WMT, int TAIL, int NWR, int HEADC = 0>
 __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
   using G = Geo<WMT, NWR>;
+  static_assert(HEADC == 0 || (WMT == 2 && NWR == 4), "the fused head epilogue is written for 8 waves of 64 x 64");
   constexpr int STAGE = G::STAGE, GLDS_PER_STAGE = G::GLDS_PER_STAGE;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[G::SMEM];
+  constexpr int SMEM_BYTES = HEADC ? std::max(G::SMEM, FH_FLOATS * 4) : G::SMEM;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
   const int m0 = blockIdx.x * G::BM, n0 = blockIdx.y * FBN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -284,6 +306,10 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
     kstep(smem + ((nk - 1) % NS) * STAGE, std::integral_constant<int, TAIL>{});
   }
 
+  if constexpr (HEADC > 0) {
+    fused_head_epilogue<HEADC>(p, acc, smem, m0, wave, lane, wm, wn);
+    return;
+  }
   // epilogue: relu(scale * acc + bias), transposed through LDS so that every lane stores whole
   // 16-byte row pieces, EPR rows of the wave tile at a time (EPR x 64 fp32 per wave; the waves'
   // pieces reuse the stage buffers, free after the barrier that ended the last K-step)
@@ -318,7 +344,129 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
       } else if (row < p.M) {
         *reinterpret_cast<f32x4*>(p.C + (size_t)row * p.ldc + n0 + wn * 64 + 4 * (lane & 15)) = v;
       }
+      if (p.mask) {  // ReLU bits: the 8 lanes holding 32 columns of the row OR their nibbles into one word
+        unsigned w = ((v[0] > 0.f ? 1u : 0u) | (v[1] > 0.f ? 2u : 0u) | (v[2] > 0.f ? 4u : 0u) |
+                      (v[3] > 0.f ? 8u : 0u)) << (4 * (lane & 7));
+        w |= __shfl_xor(w, 1);
+        w |= __shfl_xor(w, 2);
+        w |= __shfl_xor(w, 4);
+        if ((lane & 7) == 0 && row < p.M)
+          p.mask[(size_t)row * (p.N / 32) + (n0 + wn * 64) / 32 + ((lane & 15) >> 3)] = w;
+      }
     }
+  }
+}
+
+// The classifier head on the block's h, straight from the forward's accumulators (no HBM round trip):
+//  1. h = relu(scale acc + b1) into the block's LDS x-tile images (the K loop's stage buffers are free);
+//     the ReLU bits leave by one 8-byte store per lane (lane = row of the wave, bits from ballots)
+//  2. every wave runs 2 of the block's 16 row tiles through head_tile.h (bit-identical dl to the
+//     standalone MFMA head on the same h); dW2^T, db2, loss, correct stay in registers
+//  3. wave partials meet in LDS in wave order -> one slab row + one |dl @ W2| bound per block
+template <int C>
+__device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
+                                                    int m0, int wave, int lane, int wm, int wn) {
+  using namespace headtile;
+  const U8HeadArgs& hd = p.head;
+  float* F = reinterpret_cast<float*>(smem);
+  float* himg = F;
+  float* ws = F + FH_WS;
+  float* dzt = F + FH_DZT + wave * 256;
+  float* red = F + FH_RED;  // [8][2 + 16] (loss, correct, db) then [8] dz bounds
+  const int tid = threadIdx.x, h2 = lane >> 5, r32 = lane & 31;
+  __syncthreads();  // every wave's last K-step reads are done: the stage buffers are free
+  for (int i = tid; i < 16 * 32; i += 512) {  // W2, zero-padded to 16 classes
+    const int c = i >> 5, k4 = i & 31;
+    *reinterpret_cast<f32x4m*>(ws + c * FH_WSP + 4 * k4) =
+        c < C ? reinterpret_cast<const f32x4m*>(hd.w2)[c * 32 + k4] : f32x4m{0.f, 0.f, 0.f, 0.f};
+  }
+  float bv1[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bv1[j] = p.bias[wn * 64 + 32 * j + r32];
+  unsigned mw[2] = {0u, 0u};  // lane L: mask words 2 wn + j of the wave's row L
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float y = fmaxf(acc[i][j][r] * p.scale + bv1[j], 0.f);  // the plain epilogue's arithmetic
+        const int rw = 32 * i + (r & 3) + 8 * (r >> 2);               // + 4 h2: row within the wave tile
+        const int row = wm * 64 + rw + 4 * h2, col = wn * 64 + 32 * j + r32;
+        himg[(row >> 4) * 2048 + xt_at(row & 15, col >> 4, col & 15)] = y;
+        const unsigned long long b = __ballot(y > 0.f);
+        if (lane == rw) mw[j] = (unsigned)b;
+        if (lane == rw + 4) mw[j] = (unsigned)(b >> 32);
+      }
+  {
+    const int row = m0 + wm * 64 + lane;
+    if (row < p.M) *reinterpret_cast<uint2*>(hd.mask + (size_t)row * 4 + 2 * wn) = uint2{mw[0], mw[1]};
+  }
+  __syncthreads();
+
+  const int r = lane & 15, g = lane >> 4;
+  f32x4m wl[8];  // wl[u][e] = W2[class r][16 u + 4 g + e]
+#pragma unroll
+  for (int u = 0; u < 8; ++u) wl[u] = *reinterpret_cast<const f32x4m*>(ws + r * FH_WSP + 16 * u + 4 * g);
+  f32x4m bv;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) bv[v] = (4 * g + v) < C ? hd.b2[4 * g + v] : 0.f;
+  TileAcc a;
+  a.zero();
+  int tg[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) tg[it] = (int)hd.target[min(m0 + 16 * (wave + 8 * it) + r, p.M - 1)];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int T = wave + 8 * it, row = m0 + 16 * T + r;
+    const float* xw = himg + T * 2048;
+    f32x4m xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xv[u] = *reinterpret_cast<const f32x4m*>(xw + xt_at(r, u, 4 * g));
+    float dz[4];
+    logits_dz<C>(wl, bv, xv, tg[it], row < p.M, true, hd.loss_scale, g, a, dz, hd.dl + (size_t)row * C, true);
+    dw_accum(xw, dzt, dz, r, g, a);
+  }
+
+  __syncthreads();  // every tile done: the x images are free for the wave partials
+  float* mine = F + wave * (C * 128);
+  if (r < C) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) *reinterpret_cast<f32x4m*>(mine + r * 128 + 16 * t + 4 * g) = a.gw[t];
+  }
+  a.gbp += __shfl_xor(a.gbp, 16);
+  a.gbp += __shfl_xor(a.gbp, 32);
+  if (g == 0) red[wave * 18 + 2 + r] = a.gbp;
+  for (int off = 32; off > 0; off >>= 1) {
+    a.loss += __shfl_xor(a.loss, off);
+    a.corr += __shfl_xor(a.corr, off);
+    a.amx = fmaxf(a.amx, __shfl_xor(a.amx, off));
+  }
+  if (lane == 0) {
+    red[wave * 18] = a.loss;
+    red[wave * 18 + 1] = a.corr;
+    red[8 * 18 + wave] = a.amx;
+  }
+  __syncthreads();
+  float* slab = hd.part + (size_t)blockIdx.x * (C * 128 + C + 2);
+  auto sum8 = [&](auto at) {  // wave partials in wave order
+    return ((at(0) + at(1)) + (at(2) + at(3))) + ((at(4) + at(5)) + (at(6) + at(7)));
+  };
+  for (int o = tid; o < C * 128; o += 512) slab[o] = sum8([&](int w) { return F[w * (C * 128) + o]; });
+  if (tid < C) slab[C * 128 + tid] = sum8([&](int w) { return red[w * 18 + 2 + tid]; });
+  if (tid == 64) slab[C * 128 + C] = sum8([&](int w) { return red[w * 18]; });
+  if (tid == 128) slab[C * 128 + C + 1] = sum8([&](int w) { return red[w * 18 + 1]; });
+  if (wave == 7) {  // the |dl @ W2| bound: 2 max_row sum_c |dl_c| * max |W2| (head_xent.hip's formula)
+    float wm2 = 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wm2 = fmaxf(wm2, fabsf(wl[u][e]));
+    for (int off = 32; off > 0; off >>= 1) wm2 = fmaxf(wm2, __shfl_xor(wm2, off));
+    float am = red[8 * 18];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) am = fmaxf(am, red[8 * 18 + w]);
+    if (lane == 0) hd.bound[blockIdx.x] = 2.f * am * wm2;
   }
 }
 
@@ -430,7 +578,8 @@ struct WgradParams {
   // FD (factored boundary gradient): dz = (dl @ W2) * (h > 0) rebuilt in the staging
   const float* dl;           // [M][C]
   const float* w2;           // [C][N]
-  const float* h;            // [M][N]
+  const float* h;            // [M][N] (FD == 1)
+  const unsigned* mask;      // [M][N / 32] ReLU bits (FD == 2)
   int C;                     // <= 16
   int groups, splits;        // N / GHN hidden groups x row splits (1-D grid, XCD-aware order)
   int xcd;                   // 0: plain order (split-major), A/B only (SDML_U8_WGRAD_XCD=0)
@@ -447,11 +596,21 @@ __device__ __forceinline__ f32x4 fd_dz(const float (&w4)[4], const float (&d4)[4
   for (int v = 0; v < 4; ++v) o[v] = hv[v] > 0.f ? o[v] : 0.f;
   return o;
 }
+// the same with the ReLU mask as 4 bits (bit v <=> h[.][column v] > 0): bit-identical dz
+__device__ __forceinline__ f32x4 fd_dz_bits(const float (&w4)[4], const float (&d4)[4], unsigned bits) {
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) o = __builtin_amdgcn_mfma_f32_16x16x4f32(w4[kk], d4[kk], o, 0, 0, 0);
+#pragma unroll
+  for (int v = 0; v < 4; ++v) o[v] = (bits >> v) & 1u ? o[v] : 0.f;
+  return o;
+}
 
-// FD = false: dz read as [M][N]. FD = true: the factored boundary gradient (rotate placement)
+// FD = 0: dz read as [M][N]. FD > 0: the factored boundary gradient (rotate placement, one-rank step)
 // is expanded here instead of by a separate kernel that writes dz to memory and reads it back -
-// with head_xent.hip's exact operations, so gW / gb are bit-identical to the unfused pair.
-template <bool FD>
+// with head_xent.hip's exact operations, so gW / gb are bit-identical to the unfused pair; the ReLU
+// mask comes from h (FD = 1, 16 B per thread and K-step) or from its bits (FD = 2, 4 B).
+template <int FD>
 __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) u16 smem[2 * GBUF_U16];
   const int t = threadIdx.x, lane = t & 63;
@@ -474,12 +633,15 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   // K-step with 4 fp32 MFMAs, lane (r, g) holding row r, hidden 4 g .. 4 g + 3 of it
   const int fr = 16 * (wave >> 2) + (lane & 15), fc = 16 * (wave & 3) + 4 * (lane >> 4);
   const int drow = FD ? fr : (t >> 4), dcol = FD ? fc : 4 * (t & 15);  // this thread's dz float4
-  const float* dzp = (FD ? p.h : p.dz) + (size_t)(r0 + drow) * p.N + n0 + dcol;
+  const float* dzp = (FD == 1 ? p.h : p.dz) + (size_t)(r0 + drow) * p.N + n0 + dcol;
   const size_t dz_step = (size_t)GBK * p.N;
+  const unsigned* mkp = p.mask + (size_t)(r0 + drow) * (p.N / 32) + (n0 + dcol) / 32;  // FD == 2
+  const int mshift = (n0 + dcol) & 31;
+  unsigned mbits = 0u;
   float dz_up = 1.f, out_scale = p.scale;  // 2^(14 - E) and scale * 2^(E - 14), set below
   float w4[4] = {0.f, 0.f, 0.f, 0.f};  // FD: W2[4 g + kk][n0 + 16 (w & 3) + r]
   const float* dlp = nullptr;
-  if constexpr (FD) {
+  if constexpr (FD != 0) {
     const int g = lane >> 4;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
@@ -493,7 +655,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     float bnd = 0.f;
     if (p.amax) {
       for (int i = t; i < p.namax; i += GT) bnd = fmaxf(bnd, p.amax[i]);
-    } else if constexpr (FD) {  // max_row sum_c |dl| over this workgroup's rows, times max |W2| here
+    } else if constexpr (FD != 0) {  // max_row sum_c |dl| over this workgroup's rows, times max |W2| here
       const int nrows = min(p.rows_per_split, p.M - r0);
       for (int i = t; i < nrows; i += GT) {
         const float* d = p.dl + (size_t)(r0 + i) * p.C;
@@ -504,7 +666,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     }
     float* red = reinterpret_cast<float*>(smem);
     float wmx = 0.f;
-    if constexpr (FD) {
+    if constexpr (FD != 0) {
       if (!p.amax)
         for (int i = t; i < p.C * GHN; i += GT) wmx = fmaxf(wmx, fabsf(p.w2[(size_t)(i / GHN) * p.N + n0 + i % GHN]));
     }
@@ -526,7 +688,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     }
     __syncthreads();
     // FD without amax: |dz_n| <= sum_c |dl_c| |W2_cn|; the product is rounded, so bound it by 2x
-    const int E = bound_exp((FD && !p.amax) ? 2.f * bnd * wmx : bnd);
+    const int E = bound_exp((FD != 0 && !p.amax) ? 2.f * bnd * wmx : bnd);
     dz_up = pow2f(14 - E);
     out_scale = p.scale * pow2f(E - 14);
   }
@@ -547,8 +709,9 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   u32x4 xv[XU];
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
   auto gload = [&](int kt) {
-    dv = *reinterpret_cast<const f32x4*>(dzp + kt * dz_step);  // FD: h (the ReLU mask source)
-    if constexpr (FD) {
+    if constexpr (FD == 2) mbits = mkp[(size_t)kt * GBK * (p.N / 32)];  // the ReLU bits
+    else dv = *reinterpret_cast<const f32x4*>(dzp + kt * dz_step);      // dz, or FD == 1: h (the ReLU mask source)
+    if constexpr (FD != 0) {
       const int g = lane >> 4;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
@@ -559,7 +722,8 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   };
   auto stage = [&](int buf) {
     u16* B = smem + buf * GBUF_U16;
-    if constexpr (FD) dv = fd_dz(w4, d4, dv);
+    if constexpr (FD == 1) dv = fd_dz(w4, d4, dv);
+    if constexpr (FD == 2) dv = fd_dz_bits(w4, d4, (mbits >> mshift) & 15u);
     bsum += dv;
     u16x4 hi, lo;
 #pragma unroll
@@ -660,7 +824,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   if (t < GHN) {  // rows rr = 0 .. 31 in order, whichever thread staged them
     float sacc = 0.f;
     for (int rr = 0; rr < GBK; ++rr) {
-      const int owner = FD ? 64 * ((rr >> 4) * 4 + (t >> 4)) + 16 * ((t >> 2) & 3) + (rr & 15) : rr * 16 + (t >> 2);
+      const int owner = FD != 0 ? 64 * ((rr >> 4) * 4 + (t >> 4)) + 16 * ((t >> 2) & 3) + (rr & 15) : rr * 16 + (t >> 2);
       sacc += red[4 * owner + (t & 3)];
     }
     out[(size_t)p.N * GKC + n0 + t] = sacc;
@@ -778,7 +942,7 @@ void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, fl
   p.groups = N / GHN;
   p.splits = splits;
   p.xcd = wgrad_xcd();
-  hipLaunchKernelGGL(u8_wgrad_kernel<false>, dim3(((splits + 7) / 8) * 8 * p.groups), dim3(GT), 0, stream, p);
+  hipLaunchKernelGGL(u8_wgrad_kernel<0>, dim3(((splits + 7) / 8) * 8 * p.groups), dim3(GT), 0, stream, p);
   slab_reduce(slab, (int64_t)N * GKC + N, splits, gwb, (int64_t)N * GKC + N, stream);
 }
 
@@ -786,9 +950,10 @@ bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const vo
   return u8_wgrad_supported(M, N, K, ldx, X, h) && C >= 1 && C <= 16;
 }
 
-void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const unsigned char* X, int M, int N, int ldx,
-                 float* slab, float* gwb, float scale, const float* amax, int namax, hipStream_t stream,
-                 const HeadReduceArgs* head, const SgdFuse* sgd) {
+void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigned* mask, int C,
+                 const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
+                 const float* amax, int namax, hipStream_t stream, const HeadReduceArgs* head, const SgdFuse* sgd) {
+  if ((h == nullptr) == (mask == nullptr)) abort();  // host contract: exactly one ReLU-mask source
   WgradParams p{};
   p.amax = namax > 0 ? amax : nullptr;
   p.namax = namax;
@@ -801,13 +966,16 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, int C, const 
   p.dl = dl;
   p.w2 = w2;
   p.h = h;
+  p.mask = mask;
   p.C = C;
   const int splits = u8_wgrad_splits(M, N);
   p.rows_per_split = ((M + splits - 1) / splits + GBK - 1) / GBK * GBK;
   p.groups = N / GHN;
   p.splits = splits;
   p.xcd = wgrad_xcd();
-  hipLaunchKernelGGL(u8_wgrad_kernel<true>, dim3(((splits + 7) / 8) * 8 * p.groups), dim3(GT), 0, stream, p);
+  const dim3 wgrid(((splits + 7) / 8) * 8 * p.groups);
+  if (mask) hipLaunchKernelGGL(u8_wgrad_kernel<2>, wgrid, dim3(GT), 0, stream, p);
+  else hipLaunchKernelGGL(u8_wgrad_kernel<1>, wgrid, dim3(GT), 0, stream, p);
   const int64_t n = (int64_t)N * GKC + N;
   if (head && head->part) {
     const int nslab = (int)((n / 4 + 63) / 64);
@@ -825,8 +993,10 @@ void split_planes_pad(const float* w, unsigned short* out, int N, int K, int Kp,
 }
 
 void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
-            const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream) {
-  FwdParams p;
+            const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream, unsigned* mask) {
+  if (mask && !relu) abort();  // host contract: the ReLU bits need the ReLU epilogue
+  FwdParams p{};
+  p.mask = mask;
   p.X = X;
   p.Wp = w_planes;
   p.bias = bias;
@@ -839,10 +1009,14 @@ void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short*
   p.ldc = ldc;
   p.scale = scale / kU8FwdWScale;  // the planes hold W * 2^8 (exact power of two)
   p.relu = relu ? 1 : 0;
+#ifdef SDML_KERNEL_EXPERIMENTS  // timing-experiment variants (tools/bench_u8.py): not in production builds
   static const int mode = [] {
     const char* e = getenv("SDML_U8_FWD_MODE");
     return e ? atoi(e) : 0;
   }();
+#else
+  constexpr int mode = 0;
+#endif
   static const int wmt_env = [] {
     const char* e = getenv("SDML_U8_FWD_WMT");
     return e ? atoi(e) : 0;
@@ -878,18 +1052,65 @@ void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short*
     else if (wmt == 4) FWD_LAUNCH(MD, 4, NSUB, 4);  \
     else FWD_LAUNCH(MD, 2, NSUB, 4);                \
   } while (0)  // timing modes: full last K-step
+#ifdef SDML_KERNEL_EXPERIMENTS
   if (mode == 1) FWD_MODE(1);
   else if (mode == 2) FWD_MODE(2);
   else if (mode == 3) FWD_MODE(3);
   else if (mode == 4) FWD_MODE(4);
   else if (mode == 5) FWD_MODE(5);
   else if (mode == 6) FWD_MODE(6);
-  else if (w16) FWD_TAILS(2, 8);
+  else
+#endif
+  if (w16) FWD_TAILS(2, 8);
   else if (wmt == 4) FWD_TAILS(4, 4);
   else FWD_TAILS(2, 4);
 #undef FWD_TAILS
 #undef FWD_MODE
 #undef FWD_LAUNCH
+}
+
+bool u8_fwd_head_supported(int M, int N, int K, int ldx, const void* X, int C) {
+  return u8_fwd_supported(M, N, K, ldx, X) && N == FBN && (C == 2 || C == 10 || C == 16);
+}
+
+int u8_fwd_head_blocks(int M) { return (M + FH_ROWS - 1) / FH_ROWS; }
+
+void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
+                 const float* bias, float scale, const U8HeadArgs& head, hipStream_t stream) {
+  if (N != FBN || !head.dl || !head.mask || !head.part || !head.bound || !bias) abort();  // host contract
+  static_assert(Geo<2, 4>::BM == FH_ROWS, "one fused-head block = 256 rows");
+  FwdParams p{};
+  p.X = X;
+  p.Wp = w_planes;
+  p.bias = bias;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.Kp = Kp;
+  p.ldx = ldx;
+  p.scale = scale / kU8FwdWScale;
+  p.relu = 1;
+  p.head = head;
+  const dim3 grid(u8_fwd_head_blocks(M), 1);
+  const int tail = tail_substeps(K);
+#define FH_LAUNCH(T, CC) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC>), grid, dim3(512), 0, stream, p)
+#define FH_TAILS(CC)                      \
+  do {                                    \
+    switch (tail) {                       \
+      case 1: FH_LAUNCH(1, CC); break;    \
+      case 2: FH_LAUNCH(2, CC); break;    \
+      case 3: FH_LAUNCH(3, CC); break;    \
+      default: FH_LAUNCH(NSUB, CC);       \
+    }                                     \
+  } while (0)
+  switch (head.C) {
+    case 10: FH_TAILS(10); break;
+    case 2: FH_TAILS(2); break;
+    case 16: FH_TAILS(16); break;
+    default: abort();  // host contract: u8_fwd_head_supported
+  }
+#undef FH_TAILS
+#undef FH_LAUNCH
 }
 
 }  // namespace sdml

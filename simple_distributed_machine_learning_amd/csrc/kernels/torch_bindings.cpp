@@ -171,8 +171,34 @@ torch::Tensor pixels_f32(const torch::Tensor& x, double scale) {
 // first layer fed by uint8 pixels (MNIST's native bytes): y = act(scale * x_u8 @ w.T + b), with
 // scale = 1/255 this is ToTensor() fused into the GEMM's operand load. Shapes the uint8 kernel
 // does not take (small batches, unaligned K) go through an fp32 copy of x * scale.
+// ReLU bits of y [M][N] (N % 32 == 0): int32 [M][N / 32], bit n % 32 of word n / 32 = (y[m][n] > 0) -
+// the layout u8_fwd / u8_fwd_head write (for the paths that do not go through them)
+torch::Tensor relu_bits(const torch::Tensor& y) {
+  const int64_t M = y.size(0), N = y.size(1);
+  TORCH_CHECK(N % 32 == 0, "relu_bits: N % 32 == 0");
+  auto sh = torch::arange(32, y.options().dtype(torch::kInt64));
+  auto b = (y > 0).view({M, N / 32, 32}).to(torch::kInt64);
+  return b.bitwise_left_shift(sh).sum(-1).to(torch::kInt32);
+}
+
+// the inverse: float 0/1 [M][32 * words]
+torch::Tensor relu_bits_unpack(const torch::Tensor& mask) {
+  auto sh = torch::arange(32, mask.options().dtype(torch::kInt64));
+  auto w = mask.to(torch::kInt64).bitwise_and(0xffffffffLL).unsqueeze(-1);
+  return w.bitwise_right_shift(sh).bitwise_and(1).view({mask.size(0), mask.size(1) * 32}).to(torch::kFloat32);
+}
+
+void check_mask_out(const c10::optional<torch::Tensor>& m, int64_t M, int64_t N) {
+  if (!m.has_value() || !m->defined()) return;
+  TORCH_CHECK(m->is_cuda() && m->scalar_type() == torch::kInt32 && m->is_contiguous() && m->dim() == 2 &&
+                  m->size(0) == M && N % 32 == 0 && m->size(1) == N / 32,
+              "mask_out must be a contiguous int32 [M, N / 32] device tensor");
+}
+
+// mask_out (optional, relu): also write the ReLU bits of y (relu_bits' layout)
 torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> b, bool relu,
-                            double scale, c10::optional<torch::Tensor> planes, bool planes_valid) {
+                            double scale, c10::optional<torch::Tensor> planes, bool planes_valid,
+                            c10::optional<torch::Tensor> mask_out) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
               "linear_fwd_u8: x must be a contiguous 2-D uint8 ROCm tensor");
   check_f32_cuda(w, "w");
@@ -180,9 +206,16 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   check_opt(b, "b", N);
   TORCH_CHECK(!relu || opt_ptr(b), "relu epilogue requires a bias");
+  check_mask_out(mask_out, M, N);
+  const bool want_mask = mask_out.has_value() && mask_out->defined();
+  TORCH_CHECK(!want_mask || relu, "linear_fwd_u8: mask_out needs the relu epilogue");
   const bool direct = M >= 4096 && K % 16 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
                       M * K < (int64_t(1) << 31);
-  if (!direct) return linear_fwd_f32(pixels_f32(x, scale), w, b, relu);
+  auto with_mask = [&](torch::Tensor y) {
+    if (want_mask) mask_out->copy_(relu_bits(y));
+    return y;
+  };
+  if (!direct) return with_mask(linear_fwd_f32(pixels_f32(x, scale), w, b, relu));
   auto y = torch::empty({M, N}, w.options());
   static const bool legacy = [] {
     const char* e = getenv("SDML_U8_FWD");
@@ -202,7 +235,8 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
     auto* wpp = reinterpret_cast<unsigned short*>(wp.data_ptr<int16_t>());
     if (!cache || !planes_valid) sdml::split_planes_pad(w.data_ptr<float>(), wpp, (int)N, (int)K, Kp, cur_stream());
     sdml::u8_fwd(x.data_ptr<uint8_t>(), (int)M, (int)K, (int)K, wpp, (int)N, Kp, opt_ptr(b), y.data_ptr<float>(),
-                 (int)N, relu, (float)scale, cur_stream());
+                 (int)N, relu, (float)scale, cur_stream(),
+                 want_mask ? reinterpret_cast<unsigned*>(mask_out->data_ptr<int32_t>()) : nullptr);
     return y;
   }
   auto wsplit = torch::empty({3, N, K}, w.options().dtype(torch::kInt16));
@@ -211,7 +245,7 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
   sdml::gemm_u8x3_fwd(x.data_ptr<uint8_t>(), (int)M, (int)K, (int)K,
                       reinterpret_cast<const unsigned short*>(wsplit.data_ptr<int16_t>()), (int)N, opt_ptr(b),
                       y.data_ptr<float>(), (int)N, relu, (float)scale, cur_stream());
-  return y;
+  return with_mask(y);
 }
 
 // weight/bias gradient of the uint8-fed first layer: gw += scale * gz^T x_u8, gb += colsum(gz)
@@ -748,23 +782,30 @@ torch::Tensor head_dx_from_dl(torch::Tensor dl, torch::Tensor w, torch::Tensor x
 // nesterov, first, zero_grad, planes | None, plane_offset, plane_rows, plane_k) of the flat buffers
 // gw/gb and the head's gW/gb live in - when these are the step's last gradients, the optimizer step is
 // applied inside the same reduction launch. Returns whether it was (else the caller steps).
-bool linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, torch::Tensor h, torch::Tensor gw,
+// act: the layer's output h [M][N] fp32, or its ReLU bits [M][N / 32] int32 (linear_fwd_u8's mask_out /
+// linear_relu_head_u8) - only the mask is used
+bool linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, torch::Tensor act, torch::Tensor gw,
                         torch::Tensor gb, double scale, c10::optional<torch::Tensor> amax,
                         std::shared_ptr<HeadPending> head, c10::optional<py::tuple> sgd) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
               "linear_wgrad_u8_dl: x must be a contiguous 2-D uint8 ROCm tensor");
   check_f32_cuda(dl, "dl");
   check_f32_cuda(w2, "w2");
-  check_f32_cuda(h, "h");
   check_f32_cuda(gw, "gw");
   check_f32_cuda(gb, "gb");
-  const int64_t M = x.size(0), K = x.size(1), N = h.size(1), C = dl.size(1);
+  const bool bits = act.scalar_type() == torch::kInt32;
+  if (bits) {
+    TORCH_CHECK(act.is_cuda() && act.is_contiguous() && act.dim() == 2, "linear_wgrad_u8_dl: bad mask");
+  } else {
+    check_f32_cuda(act, "h");
+  }
+  const int64_t M = x.size(0), K = x.size(1), N = bits ? act.size(1) * 32 : act.size(1), C = dl.size(1);
   TORCH_CHECK(dl.dim() == 2 && dl.size(0) == M && w2.dim() == 2 && w2.size(0) == C && w2.size(1) == N &&
-                  h.dim() == 2 && h.size(0) == M && gw.size(0) == N && gw.size(1) == K && gb.numel() == N,
+                  act.dim() == 2 && act.size(0) == M && gw.size(0) == N && gw.size(1) == K && gb.numel() == N,
               "linear_wgrad_u8_dl: shape mismatch");
   const bool gb_follows = gw.is_contiguous() && gb.is_contiguous() && gb.data_ptr<float>() == gw.data_ptr<float>() + N * K;
   if (gb_follows && sdml::head_fused_supported((int)N, (int)C) &&
-      sdml::u8_wgrad_dl_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr(), h.data_ptr(), (int)C)) {
+      sdml::u8_wgrad_dl_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr(), act.data_ptr(), (int)C)) {
     auto ws = torch::empty({sdml::u8_wgrad_slab_floats((int)M, (int)N)}, gw.options());
     const bool has_am = amax.has_value() && amax->defined();
     if (has_am) {
@@ -814,18 +855,88 @@ bool linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, tor
         sg.plane_stride = prows * planes.size(2);
       }
     }
-    sdml::u8_wgrad_dl(dl.data_ptr<float>(), w2.data_ptr<float>(), h.data_ptr<float>(), (int)C, x.data_ptr<uint8_t>(),
-                      (int)M, (int)N, (int)K, ws.data_ptr<float>(), gw.data_ptr<float>(), (float)scale,
+    sdml::u8_wgrad_dl(dl.data_ptr<float>(), w2.data_ptr<float>(), bits ? nullptr : act.data_ptr<float>(),
+                      bits ? reinterpret_cast<const unsigned*>(act.data_ptr<int32_t>()) : nullptr, (int)C,
+                      x.data_ptr<uint8_t>(), (int)M, (int)N, (int)K, ws.data_ptr<float>(), gw.data_ptr<float>(), (float)scale,
                       has_am ? amax->data_ptr<float>() : nullptr, has_am ? (int)amax->numel() : 0, cur_stream(),
                       fuse_head ? &head->args : nullptr, sg.p ? &sg : nullptr);
     if (fuse_head) head->done();
     return sg.p != nullptr;
   }
   if (head) head->run();
-  torch::Tensor dz = sdml::head_fused_supported((int)N, (int)C) ? head_dx_from_dl(dl, w2, h, true)
-                                                                  : at::matmul(dl, w2).mul_((h > 0).to(h.scalar_type()));
+  torch::Tensor dz;
+  if (bits) dz = at::matmul(dl, w2).mul_(relu_bits_unpack(act));
+  else dz = sdml::head_fused_supported((int)N, (int)C) ? head_dx_from_dl(dl, w2, act, true)
+                                                       : at::matmul(dl, w2).mul_((act > 0).to(act.scalar_type()));
   linear_wgrad_u8(x, dz, gw, gb, scale, amax);
   return false;
+}
+
+// The uint8 first layer + classifier head in one launch (mlp_u8.hip u8_fwd_head, training): h =
+// relu(scale x @ w1.T + b1) never leaves the chip; writes dl = loss_scale (softmax - onehot) into
+// dl_out [M, C] and the ReLU bits into mask_out [M, 4]; loss sum / correct count go to stats (overwritten
+// with stats_init), dW2/db2 to gw2/gb2 through a slab reduction - deferred (returned as HeadPending, for
+// linear_wgrad_u8_dl's reduction launch) with `defer`, else run here. Returns (dl bounds, pending).
+std::tuple<torch::Tensor, std::shared_ptr<HeadPending>> linear_relu_head_u8(
+    torch::Tensor x, torch::Tensor w1, torch::Tensor b1, double scale, torch::Tensor planes, bool planes_valid,
+    torch::Tensor w2, torch::Tensor b2, torch::Tensor target, torch::Tensor gw2, torch::Tensor gb2, double loss_scale,
+    torch::Tensor stats, bool stats_init, torch::Tensor dl_out, torch::Tensor mask_out, bool defer) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
+              "linear_relu_head_u8: x must be a contiguous 2-D uint8 ROCm tensor");
+  for (auto* t : {&w1, &b1, &w2, &b2, &gw2, &gb2, &stats, &dl_out}) check_f32_cuda(*t, "linear_relu_head_u8");
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == torch::kInt64 && target.is_contiguous(),
+              "target must be a contiguous int64 device tensor");
+  const int64_t M = x.size(0), K = x.size(1), N = w1.size(0), C = w2.size(0);
+  TORCH_CHECK(w1.dim() == 2 && w1.size(1) == K && b1.numel() == N && w2.dim() == 2 && w2.size(1) == N &&
+                  b2.numel() == C && target.numel() == M && gw2.numel() == C * N && gb2.numel() == C &&
+                  stats.numel() == 2 && dl_out.dim() == 2 && dl_out.size(0) == M && dl_out.size(1) == C,
+              "linear_relu_head_u8: shape mismatch");
+  check_mask_out(mask_out, M, N);
+  TORCH_CHECK(sdml::u8_fwd_head_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr(), (int)C),
+              "linear_relu_head_u8: unsupported shape (u8_fwd_head_supported)");
+  const int Kp = sdml::u8_fwd_kpad((int)K);
+  TORCH_CHECK(planes.is_cuda() && planes.scalar_type() == torch::kInt16 && planes.is_contiguous() &&
+                  planes.dim() == 3 && planes.size(0) == sdml::kU8FwdPlanes && planes.size(1) == N && planes.size(2) == Kp,
+              "linear_relu_head_u8: planes must be a [u8_fwd_planes()][N][u8_fwd_kpad(K)] int16 device tensor");
+  auto* wpp = reinterpret_cast<unsigned short*>(planes.data_ptr<int16_t>());
+  if (!planes_valid) sdml::split_planes_pad(w1.data_ptr<float>(), wpp, (int)N, (int)K, Kp, cur_stream());
+  const int blocks = sdml::u8_fwd_head_blocks((int)M);
+  auto ws = torch::empty({(int64_t)blocks * (C * N + C + 2)}, w1.options());
+  auto bound = torch::empty({blocks}, w1.options());
+  sdml::U8HeadArgs h;
+  h.w2 = w2.data_ptr<float>();
+  h.b2 = b2.data_ptr<float>();
+  h.target = target.data_ptr<int64_t>();
+  h.C = (int)C;
+  h.loss_scale = (float)loss_scale;
+  h.dl = dl_out.data_ptr<float>();
+  h.mask = reinterpret_cast<unsigned*>(mask_out.data_ptr<int32_t>());
+  h.part = ws.data_ptr<float>();
+  h.bound = bound.data_ptr<float>();
+  sdml::u8_fwd_head(x.data_ptr<uint8_t>(), (int)M, (int)K, (int)K, wpp, (int)N, Kp, b1.data_ptr<float>(), (float)scale, h,
+                    cur_stream());
+  auto pend = std::make_shared<HeadPending>();
+  pend->args.part = ws.data_ptr<float>();
+  pend->args.nblocks = blocks;
+  pend->args.CK = (int)(C * N);
+  pend->args.C = (int)C;
+  pend->args.gW = gw2.data_ptr<float>();
+  pend->args.gb = gb2.data_ptr<float>();
+  pend->args.stats = stats.data_ptr<float>();
+  pend->args.flags = 1 | (stats_init ? 2 : 0);
+  pend->ws = ws;
+  pend->gw = gw2;
+  pend->gb = gb2;
+  pend->stats = stats;
+  if (!defer) {
+    pend->run();
+    return {bound, nullptr};
+  }
+  return {bound, pend};
+}
+
+bool u8_fwd_head_supported_op(int64_t M, int64_t N, int64_t K, int64_t C) {
+  return sdml::u8_fwd_head_supported((int)M, (int)N, (int)K, (int)K, nullptr, (int)C);
 }
 
 void sgd_momentum_(torch::Tensor p, torch::Tensor g, torch::Tensor buf, double lr, double momentum, double dampening,
@@ -1177,7 +1288,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "sdml gfx950 HIP kernels";
   m.def("linear_fwd_u8", &linear_fwd_u8, "act(scale * x_u8 @ w.T + b): uint8-pixel first layer", py::arg("x"),
         py::arg("w"), py::arg("b"), py::arg("relu"), py::arg("scale"), py::arg("planes") = py::none(),
-        py::arg("planes_valid") = false);
+        py::arg("planes_valid") = false, py::arg("mask_out") = py::none());
+  m.def("linear_relu_head_u8", &linear_relu_head_u8,
+        "uint8 first layer + classifier head in one launch (h stays on chip): dl, ReLU bits, head slab");
+  m.def("u8_fwd_head_supported", &u8_fwd_head_supported_op, "shape check for linear_relu_head_u8 (M, N, K, C)");
+  m.def("relu_bits", &relu_bits, "int32 [M, N/32] ReLU bits of y (the uint8 kernels' mask layout)");
   m.def("u8_fwd_kpad", [](int64_t K) { return (int64_t)sdml::u8_fwd_kpad((int)K); },
         "padded K of the uint8 forward's weight planes");
   m.def("u8_fwd_planes", []() { return (int64_t)sdml::kU8FwdPlanes; }, "number of the uint8 forward's weight planes");

@@ -93,8 +93,15 @@ class MLPStage(PipelineStage):
     def _fused(self, x) -> bool:
         return x.is_cuda
 
-    def fwd(self, x, ctx, train):
+    def fwd(self, x, ctx, train, mask_out=None):
+        """``mask_out`` (int32 [M, N/32], uint8-fed single-layer stage): also write the output's ReLU bits
+        there (ops.relu_bits layout) - all :meth:`bwd_from_factor` needs of the output."""
         if not self._fused(x):
+            if mask_out is not None:
+                y = super().fwd(x, ctx, train)
+                mask_out.copy_(ops.relu_bits(y))
+                ctx["mask"] = mask_out
+                return y
             return super().fwd(x, ctx, train)
         x = x.reshape(x.shape[0], -1)
         if x.dtype == torch.uint8:
@@ -107,7 +114,10 @@ class MLPStage(PipelineStage):
             if x.dtype == torch.uint8:
                 cache = self.plane_cache
                 epoch = self.flat_ref.param_epoch if self.flat_ref is not None else 0
-                x = ops.linear_relu_fwd_u8(x, lin.weight, lin.bias, cache, epoch)
+                m = mask_out if len(self.layers()) == 1 else None
+                x = ops.linear_relu_fwd_u8(x, lin.weight, lin.bias, cache, epoch, mask_out=m)
+                if m is not None:
+                    ctx["mask"] = m
             else:
                 x = ops.linear_relu_fwd(x, lin.weight, lin.bias)
             acts.append(x)
@@ -221,10 +231,34 @@ class MLPStage(PipelineStage):
         if acts is None or len(layers) != 1 or acts[0].dtype != torch.uint8:
             return False
         ctx.pop("acts")
+        mask = ctx.pop("mask", None)  # the output's ReLU bits (fwd(mask_out=) / fwd_head_fused), else h itself
         lin = layers[0]
-        self.sgd_fused = ops.linear_wgrad_u8_dl(acts[0], dl, w2, acts[1], lin.weight.grad, lin.bias.grad,
-                                                head_pending=head_pending, sgd=sgd)
+        self.sgd_fused = ops.linear_wgrad_u8_dl(acts[0], dl, w2, mask if mask is not None else acts[1],
+                                                lin.weight.grad, lin.bias.grad, head_pending=head_pending, sgd=sgd)
         return True
+
+    # ---- stage 0 + stage 1 in ONE launch (both stages on this rank) -------------------------
+    def can_fuse_head(self, head: "MLPStage", x: torch.Tensor) -> bool:
+        """A uint8-fed single hidden layer followed by a single-Linear head (784-128-10) fuse into one
+        kernel on ROCm (ops.linear_relu_head_u8): the boundary activation never reaches HBM."""
+        if len(self.layers()) != 1 or self.plane_cache is None or not getattr(head, "supports_factored_grad", False):
+            return False
+        return ops.relu_head_u8_supported(x, self.layers()[0].weight, head.layers()[-1].weight)
+
+    def fwd_head_fused(self, x, head: "MLPStage", target, loss_scale, stats, stats_init, dl_out, mask_out, ctx,
+                       defer=False):
+        """Training forward of this stage AND ``head``'s forward + loss + backward (its factored boundary
+        gradient dl into ``dl_out``, the ReLU bits into ``mask_out``; ctx then serves
+        :meth:`bwd_from_factor`). Returns (dl bounds, deferred head reduction or None)."""
+        lin, hl = self.layers()[0], head.layers()[-1]
+        epoch = self.flat_ref.param_epoch if self.flat_ref is not None else 0
+        out = ops.linear_relu_head_u8(x, lin.weight, lin.bias, self.plane_cache, epoch, hl.weight.detach(),
+                                      hl.bias.detach(), target, hl.weight.grad, hl.bias.grad, loss_scale, stats,
+                                      stats_init, dl_out, mask_out, defer)
+        if ctx is not None:
+            ctx["acts"] = [x]
+            ctx["mask"] = mask_out
+        return out
 
     def head_bwd(self, ctx):
         if "dx" not in ctx:

@@ -55,19 +55,70 @@ class PlaneCache:
         return (weight.data_ptr(), weight._version, epoch)
 
 
+def relu_bits(y: torch.Tensor) -> torch.Tensor:
+    """int32 [M, N/32] ReLU mask of y [M, N]: bit n % 32 of word n // 32 is (y[m, n] > 0) - the layout the
+    uint8 kernels write (mask_out) and the factored weight gradient reads."""
+    M, N = y.shape
+    sh = torch.arange(32, device=y.device, dtype=torch.int64)
+    w = ((y > 0).view(M, N // 32, 32).to(torch.int64) << sh).sum(-1)
+    return torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32)
+
+
+def relu_bits_unpack(mask: torch.Tensor) -> torch.Tensor:
+    """float 0/1 [M, 32 * words] from :func:`relu_bits`' layout."""
+    sh = torch.arange(32, device=mask.device, dtype=torch.int64)
+    w = mask.to(torch.int64) & 0xFFFFFFFF
+    return ((w.unsqueeze(-1) >> sh) & 1).view(mask.shape[0], -1).to(torch.float32)
+
+
 def linear_relu_fwd_u8(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, cache: Optional[PlaneCache] = None,
-                       epoch: int = 0) -> torch.Tensor:
+                       epoch: int = 0, mask_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """relu(ToTensor(x) @ w.T + b) for uint8 pixels x [M,K]: on ROCm the /255 is folded into the
     GEMM's epilogue and each pixel byte is exact in fp16 against two fp16 weight planes (2 MFMAs/product). With a
-    ``cache`` (and the flat buffer's ``epoch``) the weight planes are reused when still current."""
+    ``cache`` (and the flat buffer's ``epoch``) the weight planes are reused when still current.
+    ``mask_out`` (int32 [M, N/32]): also receives the output's ReLU bits (:func:`relu_bits`)."""
     if x.is_cuda:
         if cache is None:
-            return _k().linear_fwd_u8(x, w, b, True, PIXEL_SCALE)
+            return _k().linear_fwd_u8(x, w, b, True, PIXEL_SCALE, None, False, mask_out)
         tok = PlaneCache.token_of(w, epoch)
-        y = _k().linear_fwd_u8(x, w, b, True, PIXEL_SCALE, cache.planes, cache.token == tok)
+        y = _k().linear_fwd_u8(x, w, b, True, PIXEL_SCALE, cache.planes, cache.token == tok, mask_out)
         cache.token = tok
         return y
-    return ref.linear_relu_fwd(pixels_to_float(x), w, b)
+    y = ref.linear_relu_fwd(pixels_to_float(x), w, b)
+    if mask_out is not None:
+        mask_out.copy_(relu_bits(y))
+    return y
+
+
+def relu_head_u8_supported(x: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor) -> bool:
+    """Whether :func:`linear_relu_head_u8` runs as ONE fused launch for these shapes (ROCm)."""
+    return bool(x.is_cuda and x.dtype == torch.uint8 and x.dim() == 2 and x.is_contiguous()
+                and x.data_ptr() % 16 == 0
+                and _k().u8_fwd_head_supported(x.shape[0], w1.shape[0], x.shape[1], w2.shape[0]))
+
+
+def linear_relu_head_u8(x, w1, b1, cache: PlaneCache, epoch: int, w2, b2, target, gw2, gb2, loss_scale: float, stats,
+                        stats_init: bool, dl_out, mask_out, defer: bool = False):
+    """Training step of a uint8-fed hidden layer AND the classifier head in one launch (ROCm:
+    mlp_u8.hip u8_fwd_head; h = relu(ToTensor(x) @ w1.T + b1) never leaves the chip). Writes the head's
+    factored boundary gradient dl = loss_scale (softmax - onehot) into ``dl_out`` [M, C] and h's ReLU
+    bits into ``mask_out`` [M, N/32]; accumulates gw2/gb2 and (loss sum, correct) into ``stats``
+    (overwritten with ``stats_init``). Returns (dl bounds, pending): ``pending`` (with ``defer``) is the
+    head's deferred slab reduction for :func:`linear_wgrad_u8_dl`'s ``head_pending``. The bounds
+    bound |dl @ w2| per block (the weight gradient's dz scale)."""
+    if x.is_cuda:
+        tok = PlaneCache.token_of(w1, epoch)
+        out = _k().linear_relu_head_u8(x, w1, b1, PIXEL_SCALE, cache.planes, cache.token == tok, w2, b2, target,
+                                       gw2, gb2, float(loss_scale), stats, bool(stats_init), dl_out, mask_out,
+                                       bool(defer))
+        cache.token = tok
+        return out
+    h = linear_relu_fwd_u8(x, w1, b1, mask_out=mask_out)
+    with torch.no_grad():
+        loss, correct, dl = ref.linear_logsoftmax_nll_dl(h, w2, b2, target, gw2, gb2, loss_scale)
+    _put_stats(stats, loss, correct, stats_init)
+    dl_out.copy_(dl)
+    return None, None
 
 
 def linear_wgrad_u8(x: torch.Tensor, gz: torch.Tensor, gw: torch.Tensor, gb: Optional[torch.Tensor],
@@ -90,7 +141,8 @@ def linear_wgrad_u8(x: torch.Tensor, gz: torch.Tensor, gw: torch.Tensor, gb: Opt
 def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, amax: Optional[torch.Tensor] = None, head_pending=None,
                        sgd=None) -> bool:
     """First-layer weight gradient from the FACTORED boundary gradient: with dz = (dl @ w2) * (h > 0)
-    (dl [M, C] the head's factor, w2 [C, N] the head weight, h [M, N] this layer's ReLU output),
+    (dl [M, C] the head's factor, w2 [C, N] the head weight, h [M, N] this layer's ReLU output - or its
+    ReLU bits, int32 [M, N/32] (:func:`relu_bits`), which is all that is read),
     gw += dz.T @ ToTensor(x), gb += sum(dz). On ROCm dz is expanded inside the weight-gradient kernel
     (never written to memory); with the same ``amax`` (a bound on |dz|, see :func:`linear_wgrad_u8`)
     bit-identical to :func:`head_dx_from_dlogits` + :func:`linear_wgrad_u8`; without it the bounds the
@@ -108,7 +160,8 @@ def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, amax: Optional[torch.Tensor] = None
     if head_pending is not None:
         head_pending.run()
     with torch.no_grad():
-        dz = (dl @ w2) * (h > 0).to(dl.dtype)
+        mask = relu_bits_unpack(h) if h.dtype == torch.int32 else (h > 0).to(dl.dtype)
+        dz = (dl @ w2) * mask
         gw += dz.t() @ pixels_to_float(x)
         gb += dz.sum(0)
     return False

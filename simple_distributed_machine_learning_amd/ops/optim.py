@@ -9,6 +9,8 @@ update rule is torch.optim.SGD's (dampening 0, no nesterov, no weight decay by d
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import sgd_momentum_, sgd_momentum_mixed_
@@ -70,7 +72,7 @@ class FusedSGD:
         last gradients (ops.linear_wgrad_u8_dl ``sgd``), or None when that cannot cover the whole step:
         ``spans`` = [(first grad tensor, numel)] of the flat gradient ranges that reduction writes;
         every parameter segment must lie inside them (the padding between segments stays zero)."""
-        if self.master is not None or not self.flat.params.is_cuda:
+        if self.master is not None or not self.flat.params.is_cuda or os.environ.get("SDML_FUSED_STEP", "1") == "0":
             return None
         base, es = self.flat.grads.data_ptr(), self.flat.grads.element_size()
         ranges = [((t.data_ptr() - base) // es, n) for t, n in spans]

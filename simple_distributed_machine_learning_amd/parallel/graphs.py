@@ -106,15 +106,33 @@ class GraphedStep:
         # would make them synchronise with it (not permitted while capturing)
         self.stream = torch.cuda.Stream(device=engine.device)
 
+    def _plane_caches(self):
+        """(cache, weight) of every derived weight cache a captured step relies on (ops.PlaneCache)."""
+        return [(m.plane_cache, m.layers()[0].weight) for m in self.engine.stages.values()
+                if getattr(m, "plane_cache", None) is not None]
+
+    def _caches_current(self) -> bool:
+        """A replay reuses the plane caches the way they were at capture (valid, kept current by the
+        captured SGD step); a torch in-place write to a weight since (checkpoint load, user edit) bumps
+        its version and makes them stale."""
+        from ..ops import PlaneCache
+
+        ep = self.engine.flat.param_epoch
+        return all(c.token == PlaneCache.token_of(w, ep) for c, w in self._plane_caches())
+
     def _record(self, win, start, batch_size, global_batch, pool):
         eng = self.engine
         gs, steps, zero = eng.global_step, eng.optimizer.steps, eng.flat.grads_zero
+        epoch, tokens = eng.flat.param_epoch, [c.token for c, _ in self._plane_caches()]
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(eng.device)
         with torch.cuda.graph(g, pool=pool, stream=self.stream):
             res = eng.run(win, start, batch_size, train=True, global_batch=global_batch)
         # capture recorded but did not execute the step: restore the host-side state
         eng.global_step, eng.optimizer.steps, eng.flat.grads_zero = gs, steps, zero
+        eng.flat.param_epoch = epoch
+        for (c, _), t in zip(self._plane_caches(), tokens):
+            c.token = t
         return g, res
 
     def _capture(self, dataset, start: int, batch_size: int, global_batch: Optional[int]):
@@ -143,6 +161,11 @@ class GraphedStep:
             return self._eager(dataset, start, batch_size, global_batch)
         key = (batch_size, global_batch)
         t0 = time.perf_counter()
+        if self.graphs and not self._caches_current():
+            # weights changed outside the captured step: the graphs would read stale weight planes.
+            # Drop them; this step runs eagerly (re-splitting the planes) and the next one recaptures.
+            self.graphs.clear()
+            return self._eager(dataset, start, batch_size, global_batch)
         if key not in self.graphs:
             try:
                 self.graphs[key] = self._capture(dataset, start, batch_size, global_batch)
@@ -155,6 +178,6 @@ class GraphedStep:
         win.load(dataset, start - cap_start)
         g.replay()
         eng.global_step += 1
-        eng.optimizer.steps += 1
+        eng.optimizer.commit_fused(zero_grad=True)  # the captured step's update: steps, epoch, cache tokens
         self.replays += 1
         return StepResult(res.loss_sum, res.correct, res.count, time.perf_counter() - t0)

@@ -188,6 +188,9 @@ class PipelineEngine:
         if cross_fraction is not None and not 0.0 <= cross_fraction <= 1.0:
             raise ValueError(f"cross_fraction must be in [0, 1], got {cross_fraction}")
         self.cross_fraction = cross_fraction
+        # rotate: stage 0's forward and stage 1's forward+loss+backward in one kernel for the rows that
+        # stay on their owner (models/mlp.py fwd_head_fused); SDML_FUSE_HEAD=0 keeps them separate
+        self.fuse_head = os.environ.get("SDML_FUSE_HEAD", "1") != "0"
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
 
@@ -493,42 +496,76 @@ class PipelineEngine:
         ctx0 = [dict() for _ in waves]
         hkeep = [None] * W  # factored: the owner's boundary activation per wave (ReLU mask source)
         hloc, recv, fwork = [None] * W, [None] * W, [None] * W
+        # stage 0 expands the factor itself when it can (MLP first layer on uint8 pixels)
+        fuse0 = factored and hasattr(s0, "bwd_from_factor") and hasattr(s1, "factor_weight")
+        # nothing crosses GPUs: the head's gradient/stats reduction is deferred into stage 0's
+        # weight-gradient reduction launch (one launch instead of two per wave); `pend[w]` must be
+        # consumed or run
+        defer = fuse0 and not any(crossing)
+        pend = [None] * W
+        if factored:
+            gshape, gdt = (s1.layers()[-1].out_features,), torch.float32
+        else:
+            gshape, gdt = tuple(self._boundary(0, 1)[0][1:]), self.spec.boundary_dtype
+        # both stages on this rank for the wave's local rows: ONE kernel runs stage 0's forward and
+        # stage 1's forward + loss + backward (models/mlp.py fwd_head_fused; the boundary activation of
+        # those rows never reaches HBM). SDML_FUSE_HEAD=0 runs them as separate kernels.
+        fuse_fh = (train and fuse0 and self.fuse_head and hasattr(s0, "can_fuse_head"))
+        gfused = [None] * W  # fused waves: the own-rows gradient buffer, local part written by the kernel
         for w, bw in enumerate(waves):  # stage 0 forward + scatter of the boundary activation
             x = dataset.inputs(start + me * batch_size + woff[w], bw)
             if x.device != dev:
                 x = x.to(dev, non_blocking=True)
             if x.dtype == torch.uint8 and not s0.accepts_u8_pixels:
                 x = pixels_to_float(x)
-            with tm.span("fwd", 0):
-                h = s0.fwd(x, ctx0[w], train)
-            if factored:
-                hkeep[w] = h
             L = P[w][me][me]
-            hloc[w] = h if L == bw else h[:L]
-            if crossing[w] == 0:
-                continue
+            if fuse_fh and L > 0 and s0.can_fuse_head(s1, x[:L]):
+                mask = torch.empty((bw, s0.layers()[0].out_features // 32), dtype=torch.int32, device=dev)
+                G = self.bufs.get(("grad_own", w), (bw,) + gshape, gdt)
+                h = None
+                if L < bw:  # the rows whose stage 1 runs on peers: plain forward, h is sent
+                    with tm.span("fwd", 0):
+                        h = s0.fwd(x[L:], {}, train, mask_out=mask[L:])
+                tgt = dataset.targets(*owner_part(me, w, me))
+                if tgt.device != dev:
+                    tgt = tgt.to(dev, non_blocking=True)
+                with tm.span("fwd", 1):
+                    bound, pw = s0.fwd_head_fused(x[:L], s1, tgt, scale, stats, fresh, G[:L], mask[:L], None,
+                                                  defer=defer)
+                fresh = False
+                count += L
+                pend[w] = pw
+                if bound is not None and L == bw:
+                    G._sdml_amax = bound  # per-block bounds on |dl @ W2| (the weight gradient's dz scale)
+                ctx0[w] = {"acts": [x], "mask": mask}
+                gfused[w] = G
+                if crossing[w] == 0:
+                    continue
+                hx = h
+            else:
+                mask = None
+                if fuse0 and x.dtype == torch.uint8 and s0.layers()[0].out_features % 32 == 0:
+                    mask = torch.empty((bw, s0.layers()[0].out_features // 32), dtype=torch.int32, device=dev)
+                with tm.span("fwd", 0):
+                    h = s0.fwd(x, ctx0[w], train, mask_out=mask) if mask is not None else s0.fwd(x, ctx0[w], train)
+                if factored:
+                    hkeep[w] = h
+                hloc[w] = h if L == bw else h[:L]
+                if crossing[w] == 0:
+                    continue
+                hx = h[L:]
             in_splits = [0 if k == me else P[w][me][k] for k in range(R)]
             out_splits = [0 if o == me else P[w][o][me] for o in range(R)]
-            buf = self.bufs.get(("a2a_fwd", w), (sum(out_splits),) + tuple(h.shape[1:]), h.dtype)
-            fwork[w] = self.transport.all_to_all(buf, h[L:], out_splits, in_splits, channel="fwd")
+            buf = self.bufs.get(("a2a_fwd", w), (sum(out_splits),) + tuple(hx.shape[1:]), hx.dtype)
+            fwork[w] = self.transport.all_to_all(buf, hx, out_splits, in_splits, channel="fwd")
             recv[w] = buf
         back, bwork = [None] * W, [None] * W
-        # stage 0 expands the factor itself when it can (MLP first layer on uint8 pixels)
-        fuse0 = factored and hasattr(s0, "bwd_from_factor") and hasattr(s1, "factor_weight")
-        # one rank: the head's gradient/stats reduction is deferred into stage 0's weight-gradient
-        # reduction launch (one launch instead of two per wave); `pend[w]` must be consumed or run
-        defer = fuse0 and not any(crossing)
-        pend = [None] * W
         # ... and when nothing else touches the gradients before the optimizer (one rank, no gradient
         # all-reduce, stepping this call), the last wave's reduction applies the optimizer step too
         fuse_step = (defer and train and step_optimizer and not self.grad_sync.enabled
                      and hasattr(self.optimizer, "fused_args") and hasattr(s0, "grad_span")
                      and hasattr(s1, "grad_span"))
         step_fused = [False]
-        if factored:
-            gshape, gdt = (s1.layers()[-1].out_features,), torch.float32
-        else:
-            gshape, gdt = tuple(self._boundary(0, 1)[0][1:]), self.spec.boundary_dtype
 
         def run_pending(w):
             if pend[w] is not None:
@@ -599,10 +636,12 @@ class PipelineEngine:
         interleave = train and R > 1
         for w, bw in enumerate(waves):  # stage 1 (+ loss + its backward): local rows, then received rows
             L = P[w][me][me]
-            gloc = head(hloc[w], dataset.targets(*owner_part(me, w, me)), w) if L > 0 else None
+            gloc = None
+            if L > 0 and gfused[w] is None:  # (fused waves: the local rows' head already ran)
+                gloc = head(hloc[w], dataset.targets(*owner_part(me, w, me)), w)
             hloc[w] = None
             if crossing[w] == 0:
-                back[w] = gloc
+                back[w] = gfused[w] if gfused[w] is not None else gloc
                 if interleave:
                     stage0_bwd(w)
                 continue
@@ -623,9 +662,11 @@ class PipelineEngine:
                 grecv = torch.empty((0,) + gshape, dtype=gdt, device=dev)
             out_splits = [0 if k == me else P[w][me][k] for k in range(R)]
             in_splits = [0 if o == me else P[w][o][me] for o in range(R)]
-            G = self.bufs.get(("grad_own", w), (bw,) + gshape, gdt)
-            if L > 0:
-                G[:L].copy_(gloc)
+            G = gfused[w]
+            if G is None:
+                G = self.bufs.get(("grad_own", w), (bw,) + gshape, gdt)
+                if L > 0:
+                    G[:L].copy_(gloc)
             bwork[w] = self.transport.all_to_all(G[L:], grecv, out_splits, in_splits, channel="bwd")
             back[w] = G
             if interleave:

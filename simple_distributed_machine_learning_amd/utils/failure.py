@@ -29,6 +29,8 @@ class Heartbeat:
         self.store = store if store is not None else _default_store()
         self.on_failure = on_failure or _exit_on_failure
         self._stop = threading.Event()
+        self._clean = False
+        self._done_sent = False
         self._thread = None
         self.failed_peer = None
 
@@ -44,6 +46,22 @@ class Heartbeat:
         self.store.set(f"hb/{self.rank}", repr(time.time()))
 
     def _loop(self):
+        try:
+            self._watch()
+        finally:
+            # the clean-exit marker comes from THIS thread, after its last beat: a beat still in flight
+            # can no longer land after it and make a finished rank look alive-but-stale
+            if self._stop.is_set() and self._clean:
+                self._publish_done()
+
+    def _publish_done(self):
+        self._done_sent = True
+        try:
+            self.store.set(f"hb/{self.rank}", DONE)
+        except Exception:  # noqa: BLE001  store already torn down
+            pass
+
+    def _watch(self):
         t_start = time.time()
         while not self._stop.wait(self.interval_s):
             try:
@@ -82,14 +100,14 @@ class Heartbeat:
     def stop(self, clean: bool = True):
         """Stop beating. ``clean`` publishes ``hb/<rank> = done`` afterwards, so a slower peer
         (e.g. one still writing its checkpoint) does not read this rank's silence as death."""
+        self._clean = clean
         self._stop.set()
         if self._thread is not None:
-            self._thread.join(timeout=self.interval_s * 2)
-        if clean and self.store is not None:
-            try:
-                self.store.set(f"hb/{self.rank}", DONE)
-            except Exception:  # noqa: BLE001  store already torn down
-                pass
+            self._thread.join(timeout=max(10.0, self.interval_s * 4))
+            if not self._thread.is_alive() and (self._done_sent or not clean):
+                return  # the thread published the marker (if clean) as its last action
+        if clean and self.store is not None and not self._done_sent:  # no thread / stuck / exited early
+            self._publish_done()
 
 
 def _default_store():

@@ -1,0 +1,180 @@
+"""The uint8 first layer and the classifier head fused into one kernel (mlp_u8.hip u8_fwd_head) and the
+weight gradient reading ReLU bits instead of h: bit-identity with the unfused kernels where the
+arithmetic is the same (dl, the mask, gW1/gb1), fp32 agreement where only the summation blocking
+differs (gW2/gb2, loss), engine-level agreement of the fused and unfused steps, the fused optimizer step
+against optimizer.step() (bitwise, every SGD option), and the documented error bound of the weight
+gradient's fp16 dz planes on adversarial data (one row dominating its block). Reference ops:
+/root/reference/simple_distributed.py:63-64, :75-79 (fc1, relu, fc2, log_softmax), :111 (nll_loss),
+:100-104 (SGD)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no ROCm GPU", allow_module_level=True)
+
+from simple_distributed_machine_learning_amd import ops  # noqa: E402
+from simple_distributed_machine_learning_amd.data import SyntheticMNIST  # noqa: E402
+from simple_distributed_machine_learning_amd.models import get_model_spec  # noqa: E402
+from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+N, KD = 128, 784
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.rand(shape, generator=g) * 2 - 1).mul_(scale).to(DEV)
+
+
+def pixels(M, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randint(0, 256, (M, KD), generator=g, dtype=torch.uint8).to(DEV)
+
+
+def _problem(M, C, seed=0):
+    x8 = pixels(M, seed)
+    w1, b1 = rnd(N, KD, seed=seed + 1, scale=0.05), rnd(N, seed=seed + 2, scale=0.1)
+    w2, b2 = rnd(C, N, seed=seed + 3, scale=0.2), rnd(C, seed=seed + 4, scale=0.1)
+    g = torch.Generator(device="cpu").manual_seed(seed + 5)
+    tgt = torch.randint(0, C, (M,), generator=g).to(DEV)
+    return x8, w1, b1, w2, b2, tgt
+
+
+@pytest.mark.parametrize("M", [4096, 4096 + 100, 131072])
+@pytest.mark.parametrize("C", [10, 2])
+@pytest.mark.parametrize("defer", [False, True])
+def test_fused_forward_head_matches_unfused(M, C, defer):
+    x8, w1, b1, w2, b2, tgt = _problem(M, C)
+    scale = 1.0 / M
+    # unfused: forward (h + its bits) -> standalone MFMA head returning dl
+    mask_u = torch.empty(M, N // 32, dtype=torch.int32, device=DEV)
+    h = ops.linear_relu_fwd_u8(x8, w1, b1, None, 0, mask_out=mask_u)
+    gw_u, gb_u = torch.zeros(C, N, device=DEV), torch.zeros(C, device=DEV)
+    st_u = torch.empty(2, device=DEV)
+    dl_u = ops.linear_logsoftmax_nll_dl(h, w2, b2, tgt, gw_u, gb_u, scale, st_u, stats_init=True)
+    # fused
+    cache = ops.PlaneCache(w1)
+    dl_f = torch.full((M, C), float("nan"), device=DEV)
+    mask_f = torch.zeros(M, N // 32, dtype=torch.int32, device=DEV)
+    gw_f, gb_f = torch.zeros(C, N, device=DEV), torch.zeros(C, device=DEV)
+    st_f = torch.full((2,), 123.0, device=DEV)
+    bound, pend = ops.linear_relu_head_u8(x8, w1, b1, cache, 0, w2, b2, tgt, gw_f, gb_f, scale, st_f, True, dl_f,
+                                          mask_f, defer=defer)
+    if defer:
+        assert pend is not None and pend.pending
+        pend.run()
+    torch.cuda.synchronize()
+    assert torch.equal(mask_u, ops.relu_bits(h))
+    assert torch.equal(mask_f, mask_u)
+    assert torch.equal(dl_f, dl_u)  # same h, same MFMA sequence (head_tile.h)
+    torch.testing.assert_close(gw_f, gw_u, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(gb_f, gb_u, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(st_f[0], st_u[0], rtol=1e-5, atol=1e-3)
+    assert float(st_f[1]) == float(st_u[1])
+    assert float(bound.max()) >= float((dl_f.double() @ w2.double()).abs().max())
+    # and against an fp64 reference of the whole head
+    z = (x8.double() / 255.0) @ w1.double().t() + b1.double()
+    hr = z.clamp_min(0)
+    logits = hr @ w2.double().t() + b2.double()
+    p = torch.softmax(logits, 1)
+    want = (p - torch.nn.functional.one_hot(tgt, C).double()) * scale
+    torch.testing.assert_close(dl_f.double(), want, rtol=1e-4, atol=1e-9)
+    torch.testing.assert_close(gw_f.double(), want.t() @ hr, rtol=1e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("M", [4096, 65536])
+def test_wgrad_from_relu_bits_bit_identical_to_h(M):
+    C = 10
+    x8 = pixels(M, 31)
+    h = rnd(M, N, seed=32).relu()
+    dl = rnd(M, C, seed=33, scale=1e-3)
+    w2 = rnd(C, N, seed=34, scale=0.1)
+    g0 = rnd(N * KD + N, seed=35)
+    bits = ops.relu_bits(h)
+    for amax in (None, (dl.abs().sum(1).max() * w2.abs().max() * 2).reshape(1)):
+        bufs = []
+        for act in (h, bits):
+            b = g0.clone()
+            ops.linear_wgrad_u8_dl(x8, dl, w2, act, b[:N * KD].view(N, KD), b[N * KD:], amax=amax)
+            bufs.append(b)
+        assert torch.equal(bufs[0], bufs[1])
+
+
+def test_wgrad_dz_planes_error_bound_with_a_dominating_row():
+    """One row's |dl| is 2^20 times its neighbours': the block's dz bound (hence the fp16 plane scale)
+    is set by that row, and the small rows' dz fall to the planes' absolute floor. The documented bound
+    (README "Two fp16 planes"): each dz element keeps one fp32 ulp above 2^(E-15) and an absolute error
+    below 2^(E-39) otherwise, |dz| < 2^E. The weight gradient must stay within that, plus fp32
+    accumulation."""
+    M, C = 8192, 10
+    x8 = pixels(M, 41)
+    h = rnd(M, N, seed=42).relu()
+    dl = rnd(M, C, seed=43, scale=2.0 ** -20)
+    dl[1234] = rnd(C, seed=44)  # ~2^20 x the others
+    w2 = rnd(C, N, seed=45, scale=0.5)
+    g = torch.zeros(N * KD + N, device=DEV)
+    ops.linear_wgrad_u8_dl(x8, dl, w2, ops.relu_bits(h), g[:N * KD].view(N, KD), g[N * KD:])
+    dz = (dl.double() @ w2.double()) * (h > 0).double()
+    xf = x8.double() / 255.0
+    want = dz.t() @ xf
+    E = torch.ceil(torch.log2(2 * dl.abs().sum(1).max().double() * w2.abs().max().double())) + 1
+    per_elem = torch.maximum(dz.abs() * 2.0 ** -23, torch.full_like(dz, float(2.0 ** (E - 39))))
+    bound = per_elem.t() @ xf + 1e-5 * (dz.abs().t() @ xf) + 1e-30
+    err = (g[:N * KD].view(N, KD).double() - want).abs()
+    assert bool((err <= bound).all()), float((err / bound).max())
+    # the small rows still contribute: without them the result would be visibly different
+    only_big = dz[1234:1235].t() @ xf[1234:1235]
+    assert float((want - only_big).abs().max()) > 10 * float(bound.max())
+
+
+def _engine(M, lr=0.1, momentum=0.5, wd=0.0, damp=0.0, nesterov=False):
+    mesh = init_mesh(pp=1, schedule_kind="rotate", rank=0, world_size=1, device=DEV)
+    spec = get_model_spec("mlp", 2)
+    e = PipelineEngine(spec, mesh, schedule_kind="rotate", num_microbatches=M, lr=lr, momentum=momentum,
+                       weight_decay=wd, seed=3)
+    e.optimizer.dampening, e.optimizer.nesterov = damp, nesterov
+    return e
+
+
+def _train(e, steps=3, B=16384):
+    ds = SyntheticMNIST(B * steps, seed=5, device=DEV, pixels="u8")
+    losses = []
+    for s in range(steps):
+        r = e.run(ds, s * B, B, train=True)
+        losses.append(float(r.loss_sum) / r.count)
+    torch.cuda.synchronize()
+    return losses
+
+
+@pytest.mark.parametrize("M", [1, 2])
+def test_engine_fused_head_step_matches_unfused(M, monkeypatch):
+    monkeypatch.setenv("SDML_FUSE_HEAD", "0")
+    e0 = _engine(M)
+    l0 = _train(e0)
+    monkeypatch.setenv("SDML_FUSE_HEAD", "1")
+    e1 = _engine(M)
+    l1 = _train(e1)
+    assert l1 == pytest.approx(l0, rel=1e-5)
+    torch.testing.assert_close(e1.flat.params, e0.flat.params, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("opt", [dict(), dict(momentum=0.0), dict(wd=1e-4), dict(damp=0.1), dict(nesterov=True)])
+def test_fused_optimizer_step_bitwise_equals_optimizer_step(M, opt, monkeypatch):
+    """the SGD update applied inside the last reduction launch (FusedSGD.fused_args) against
+    the separate optimizer.step() launch - same fp32 operations in the same order, so bitwise equal
+    parameters, momentum buffers and uint8 forward weight planes."""
+    runs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("SDML_FUSED_STEP", fused)
+        e = _engine(M, **opt)
+        _train(e)
+        cache = e.stages[0].plane_cache
+        runs.append((e.flat.params.clone(), e.optimizer.momentum_buffer.clone() if e.optimizer.momentum else None,
+                     cache.planes.clone()))
+    (p0, b0, c0), (p1, b1, c1) = runs
+    assert torch.equal(p0, p1)
+    assert (b0 is None and b1 is None) or torch.equal(b0, b1)
+    assert torch.equal(c0, c1)

@@ -239,6 +239,18 @@ void layernorm_bwd_bf16_accum(const void* x, const void* w, const void* gy, cons
 int bias_grad_blocks(int M);
 void bias_grad_bf16(const void* gy, int M, int N, int ld, void* gb, float* workspace, hipStream_t stream);
 
+// ---- GPT-2 elementwise / embedding kernels (gpt2_ops.hip) ------------------------------------
+// tanh-GELU (n % 8 == 0, 16-B aligned): y = gelu(x); gx = gy * gelu'(x) (gx may alias gy)
+void gelu_fwd_bf16(const void* x, void* y, int64_t n, hipStream_t stream);
+void gelu_bwd_bf16(const void* gy, const void* x, void* gx, int64_t n, hipStream_t stream);
+// out[r] = wte[tok[r]] + wpe[r % S]  (rows = B * S, C % 4 == 0)
+void embedding_fwd_bf16(const int64_t* tok, const void* wte, const void* wpe, void* out, int rows, int S, int C, int V,
+                        hipStream_t stream);
+// gwpe[s] += sum_b g[b][s]; gwte[v] += sum over positions of token v (sorted_tok / perm: the tokens sorted
+// stably, with their positions) - deterministic, either gradient may be null
+void embedding_bwd_bf16(const void* g, const int64_t* sorted_tok, const int64_t* perm, void* gwte, void* gwpe, int B,
+                        int S, int C, int V, hipStream_t stream);
+
 // ---- weight gradient of a bf16 Linear: gw[M,N] (bf16) += gy[T,M]^T x[T,N] -------------------
 // fp32 accumulation, token range split over workgroups, deterministic slab reduction.
 // workspace: wgrad_bf16_workspace_floats(M, N, T) fp32 (0 = none needed)

@@ -935,6 +935,65 @@ std::tuple<torch::Tensor, std::shared_ptr<HeadPending>> linear_relu_head_u8(
   return {bound, pend};
 }
 
+void check_bf16_cuda(const torch::Tensor& t, const char* name);  // (defined with the transformer ops)
+
+torch::Tensor gelu_fwd_bf16(torch::Tensor x) {
+  check_bf16_cuda(x, "x");
+  TORCH_CHECK(x.numel() % 8 == 0, "gelu: numel % 8 == 0");
+  auto y = torch::empty_like(x);
+  sdml::gelu_fwd_bf16(x.data_ptr(), y.data_ptr(), x.numel(), cur_stream());
+  return y;
+}
+
+// gx = gy * gelu'(x); in place into gy when `inplace`
+torch::Tensor gelu_bwd_bf16(torch::Tensor gy, torch::Tensor x, bool inplace) {
+  check_bf16_cuda(gy, "gy");
+  check_bf16_cuda(x, "x");
+  TORCH_CHECK(gy.numel() == x.numel() && x.numel() % 8 == 0, "gelu_bwd: shape mismatch");
+  auto gx = inplace ? gy : torch::empty_like(gy);
+  sdml::gelu_bwd_bf16(gy.data_ptr(), x.data_ptr(), gx.data_ptr(), x.numel(), cur_stream());
+  return gx;
+}
+
+torch::Tensor embedding_fwd_bf16(torch::Tensor tok, torch::Tensor wte, torch::Tensor wpe) {
+  TORCH_CHECK(tok.is_cuda() && tok.scalar_type() == torch::kInt64 && tok.is_contiguous() && tok.dim() == 2,
+              "embedding: tokens must be a contiguous int64 [B, S] device tensor");
+  check_bf16_cuda(wte, "wte");
+  check_bf16_cuda(wpe, "wpe");
+  const int64_t B = tok.size(0), S = tok.size(1), C = wte.size(1);
+  TORCH_CHECK(wpe.size(1) == C && wpe.size(0) >= S && C % 4 == 0, "embedding: shape mismatch");
+  auto out = torch::empty({B, S, C}, wte.options());
+  sdml::embedding_fwd_bf16(tok.data_ptr<int64_t>(), wte.data_ptr(), wpe.data_ptr(), out.data_ptr(), (int)(B * S),
+                           (int)S, (int)C, (int)wte.size(0), cur_stream());
+  return out;
+}
+
+void embedding_bwd_bf16(torch::Tensor g, torch::Tensor sorted_tok, torch::Tensor perm,
+                        c10::optional<torch::Tensor> gwte, c10::optional<torch::Tensor> gwpe) {
+  check_bf16_cuda(g, "g");
+  TORCH_CHECK(g.dim() == 3 && sorted_tok.is_cuda() && perm.is_cuda() && sorted_tok.scalar_type() == torch::kInt64 &&
+                  perm.scalar_type() == torch::kInt64 && sorted_tok.numel() == g.size(0) * g.size(1) &&
+                  perm.numel() == sorted_tok.numel() && sorted_tok.is_contiguous() && perm.is_contiguous(),
+              "embedding_bwd: shape mismatch");
+  const int64_t B = g.size(0), S = g.size(1), C = g.size(2);
+  int64_t V = 0;
+  void* pw = nullptr;
+  void* pp = nullptr;
+  if (gwte.has_value() && gwte->defined()) {
+    check_bf16_cuda(*gwte, "gwte");
+    TORCH_CHECK(gwte->size(1) == C, "embedding_bwd: wte grad shape");
+    V = gwte->size(0);
+    pw = gwte->data_ptr();
+  }
+  if (gwpe.has_value() && gwpe->defined()) {
+    check_bf16_cuda(*gwpe, "gwpe");
+    TORCH_CHECK(gwpe->size(1) == C && gwpe->size(0) >= S, "embedding_bwd: wpe grad shape");
+    pp = gwpe->data_ptr();
+  }
+  sdml::embedding_bwd_bf16(g.data_ptr(), sorted_tok.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), pw, pp, (int)B,
+                           (int)S, (int)C, (int)V, cur_stream());
+}
+
 bool u8_fwd_head_supported_op(int64_t M, int64_t N, int64_t K, int64_t C) {
   return sdml::u8_fwd_head_supported((int)M, (int)N, (int)K, (int)K, nullptr, (int)C);
 }
@@ -1293,6 +1352,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "uint8 first layer + classifier head in one launch (h stays on chip): dl, ReLU bits, head slab");
   m.def("u8_fwd_head_supported", &u8_fwd_head_supported_op, "shape check for linear_relu_head_u8 (M, N, K, C)");
   m.def("relu_bits", &relu_bits, "int32 [M, N/32] ReLU bits of y (the uint8 kernels' mask layout)");
+  m.def("gelu_fwd_bf16", &gelu_fwd_bf16, "tanh-GELU forward (bf16)");
+  m.def("gelu_bwd_bf16", &gelu_bwd_bf16, "tanh-GELU backward (bf16): gy * gelu'(x)", py::arg("gy"), py::arg("x"),
+        py::arg("inplace") = false);
+  m.def("embedding_fwd_bf16", &embedding_fwd_bf16, "token + position embedding (bf16)");
+  m.def("embedding_bwd_bf16", &embedding_bwd_bf16, "deterministic embedding backward into bf16 grads",
+        py::arg("g"), py::arg("sorted_tok"), py::arg("perm"), py::arg("gwte") = py::none(),
+        py::arg("gwpe") = py::none());
   m.def("u8_fwd_kpad", [](int64_t K) { return (int64_t)sdml::u8_fwd_kpad((int)K); },
         "padded K of the uint8 forward's weight planes");
   m.def("u8_fwd_planes", []() { return (int64_t)sdml::kU8FwdPlanes; }, "number of the uint8 forward's weight planes");

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from .base import ModelSpec, PipelineStage
 from ..ops.linear import Linear, linear
-from ..ops.transformer import LayerNorm, add_layer_norm, causal_attention, cross_entropy_sum
+from ..ops.transformer import LayerNorm, add_layer_norm, causal_attention, cross_entropy_sum, embedding, gelu
 from ..parallel.tp import TPContext, column_slice, copy_to_tp, reduce_from_tp, shard_parameter
 
 
@@ -81,8 +81,8 @@ class MLP(nn.Module):
 
     def forward(self, x):
         if self.tp is None:
-            return self.c_proj(F.gelu(self.c_fc(x), approximate="tanh"))
-        h = F.gelu(self.c_fc(copy_to_tp(x, self.tp)), approximate="tanh")
+            return self.c_proj(gelu(self.c_fc(x)))
+        h = gelu(self.c_fc(copy_to_tp(x, self.tp)))
         return reduce_from_tp(linear(h, self.c_proj.weight), self.tp) + self.c_proj.bias
 
 
@@ -160,10 +160,8 @@ class GPT2Stage(PipelineStage):
         return None if self.is_first else x.grad
 
     def forward(self, x):
-        if self.stage_id == 0:
-            S = x.shape[1]
-            pos = torch.arange(S, device=x.device)
-            x = self.wte(x) + self.wpe(pos)[None]
+        if self.stage_id == 0:  # token + position embedding (HIP gather, deterministic backward)
+            x = embedding(x, self.wte.weight, self.wpe.weight)
         last = self.stage_id == self.num_stages - 1
         blocks = list(self.h.values())
         if not blocks:

@@ -152,3 +152,60 @@ def causal_attention(qkv, n_head: int):
     v = v.view(B, S, n_head, D).transpose(1, 2)
     y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
     return y.transpose(1, 2).contiguous().view(B, S, C)
+
+
+class _GeluFn(torch.autograd.Function):
+    """tanh-GELU on the HIP kernels (gpt2_ops.hip); the backward multiplies in place."""
+
+    @staticmethod
+    def forward(ctx, x):
+        xc = x.contiguous()
+        ctx.save_for_backward(xc)
+        return kernels().gelu_fwd_bf16(xc)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        return kernels().gelu_bwd_bf16(gy.contiguous(), x, False)
+
+
+def gelu(x):
+    """GELU with the tanh approximation (GPT-2's activation)."""
+    if _hip_bf16(x) and x.numel() % 8 == 0:
+        return _GeluFn.apply(x)
+    return F.gelu(x, approximate="tanh")
+
+
+class _EmbeddingFn(torch.autograd.Function):
+    """wte[tok] + wpe[:S] (HIP gather). The backward adds into wte.grad / wpe.grad in place (flat
+    gradient buffer) with a deterministic segmented sum over the stably sorted tokens."""
+
+    @staticmethod
+    def forward(ctx, tok, wte, wpe):
+        tok = tok.contiguous()
+        out = kernels().embedding_fwd_bf16(tok, wte, wpe)
+        ctx.tok = tok
+        ctx.params = (wte, wpe)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        wte, wpe = ctx.params
+        g = g.contiguous()
+        sorted_tok, perm = torch.sort(ctx.tok.reshape(-1), stable=True)
+        direct = all(p.grad is not None and p.grad.is_contiguous() and p.grad.dtype == torch.bfloat16
+                     for p in (wte, wpe))
+        if direct:
+            kernels().embedding_bwd_bf16(g, sorted_tok, perm, wte.grad, wpe.grad)
+            return None, None, None
+        gwte, gwpe = torch.zeros_like(wte), torch.zeros_like(wpe)
+        kernels().embedding_bwd_bf16(g, sorted_tok, perm, gwte, gwpe)
+        return None, gwte, gwpe
+
+
+def embedding(tok, wte, wpe):
+    """GPT-2 input embedding: wte[tok] + wpe[position] for tok [B, S]."""
+    if _hip_bf16(wte, wpe) and tok.is_cuda and wte.shape[1] % 4 == 0:
+        return _EmbeddingFn.apply(tok, wte, wpe)
+    S = tok.shape[1]
+    return F.embedding(tok, wte) + F.embedding(torch.arange(S, device=tok.device), wpe)[None]

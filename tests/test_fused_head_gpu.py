@@ -124,9 +124,9 @@ def test_wgrad_dz_planes_error_bound_with_a_dominating_row():
     bound = per_elem.t() @ xf + 1e-5 * (dz.abs().t() @ xf) + 1e-30
     err = (g[:N * KD].view(N, KD).double() - want).abs()
     assert bool((err <= bound).all()), float((err / bound).max())
-    # the small rows still contribute: without them the result would be visibly different
+    # the small rows' contribution survives: the error is far below what they add
     only_big = dz[1234:1235].t() @ xf[1234:1235]
-    assert float((want - only_big).abs().max()) > 10 * float(bound.max())
+    assert float(err.max()) < 0.05 * float((want - only_big).abs().max())
 
 
 def _engine(M, lr=0.1, momentum=0.5, wd=0.0, damp=0.0, nesterov=False):

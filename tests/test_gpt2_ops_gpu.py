@@ -1,0 +1,75 @@
+"""GPT-2 elementwise / embedding HIP kernels (gpt2_ops.hip) against PyTorch fp32 references: tanh-GELU
+forward and backward, the token + position embedding gather, and its deterministic backward (bitwise
+repeatable, equal to an fp64 scatter-add within bf16 rounding of the accumulation)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no ROCm GPU", allow_module_level=True)
+
+from simple_distributed_machine_learning_amd import _native  # noqa: E402
+from simple_distributed_machine_learning_amd.ops.transformer import embedding, gelu  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+K = _native.kernels()
+
+
+@pytest.mark.parametrize("n", [8, 4096 * 3072, 1000 * 8])
+def test_gelu_fwd_bwd_match_torch(n):
+    g = torch.Generator(device="cpu").manual_seed(n % 97)
+    x = (torch.randn(n, generator=g) * 3).to(DEV, torch.bfloat16)
+    gy = torch.randn(n, generator=g).to(DEV, torch.bfloat16)
+    y = K.gelu_fwd_bf16(x)
+    ref = F.gelu(x.float(), approximate="tanh")
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+    # the same formula as PyTorch's bf16 kernels: at most one bf16 ulp apart
+    yt = F.gelu(x, approximate="tanh")
+    assert float((y.float() - yt.float()).abs().max()) <= float(yt.float().abs().max()) * 2 ** -7 + 1e-6
+    xr = x.float().requires_grad_(True)
+    F.gelu(xr, approximate="tanh").backward(gy.float())
+    gx = K.gelu_bwd_bf16(gy, x, False)
+    torch.testing.assert_close(gx.float(), xr.grad, rtol=1e-2, atol=1e-2)
+    gx2 = gy.clone()
+    K.gelu_bwd_bf16(gx2, x, True)
+    assert torch.equal(gx2, gx)
+
+
+def test_gelu_autograd_wrapper():
+    x = torch.randn(64, 3072, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = gelu(x)
+    y.sum().backward()
+    xr = x.detach().float().requires_grad_(True)
+    F.gelu(xr, approximate="tanh").sum().backward()
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("B,S,C,V", [(16, 1024, 768, 50257), (4, 16, 32, 97), (3, 7, 64, 5)])
+def test_embedding_fwd_bwd(B, S, C, V):
+    g = torch.Generator(device="cpu").manual_seed(B * S)
+    tok = torch.randint(0, V, (B, S), generator=g).to(DEV)
+    if V > 50:  # a heavily repeated token: one long segment
+        tok[:, ::3] = 11
+    wte = (torch.randn(V, C, generator=g) * 0.02).to(DEV, torch.bfloat16).requires_grad_(True)
+    wpe = (torch.randn(S + 5, C, generator=g) * 0.02).to(DEV, torch.bfloat16).requires_grad_(True)
+    out = embedding(tok, wte, wpe)
+    want = F.embedding(tok, wte.detach()) + wpe.detach()[:S][None]
+    assert torch.equal(out, want)
+    gout = torch.randn(B, S, C, generator=g).to(DEV, torch.bfloat16)
+    # flat-buffer style: the backward adds into preset bf16 grads in place
+    wte.grad = torch.zeros_like(wte)
+    wpe.grad = torch.zeros_like(wpe)
+    out.backward(gout)
+    gw1, gp1 = wte.grad.clone(), wpe.grad.clone()
+    wte.grad.zero_()
+    wpe.grad.zero_()
+    embedding(tok, wte, wpe).backward(gout)
+    assert torch.equal(wte.grad, gw1) and torch.equal(wpe.grad, gp1)  # deterministic
+    ref_w = torch.zeros(V, C, dtype=torch.float64, device=DEV).index_add_(0, tok.reshape(-1),
+                                                                        gout.reshape(-1, C).double())
+    ref_p = gout.double().sum(0)
+    torch.testing.assert_close(gw1.double(), ref_w, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(gp1[:S].double(), ref_p, rtol=2e-2, atol=2e-2)
+    assert float(gp1[S:].abs().max()) == 0.0

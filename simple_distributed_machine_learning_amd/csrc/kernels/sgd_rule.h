@@ -18,22 +18,38 @@ struct SgdRule {
   int nesterov, first;
 };
 
-// p4 / buf4: the 4 parameters and their momentum (16-B aligned); returns the updated parameters
+// p4 / buf4: the 4 parameters and their momentum (16-B aligned); returns the updated parameters.
+// Every multiply-add is an explicit fma and contraction is off, so each kernel that inlines this rule
+// (the SGD kernel, the reductions that apply the step themselves) produces the same bits: left to the
+// compiler, "mom * b + (1 - damp) * d" may be fused around either product depending on the context.
 __device__ __forceinline__ sgd_f32x4 sgd_update4(float* p4, float* buf4, sgd_f32x4 d, const SgdRule& r) {
+#pragma clang fp contract(off)
   const sgd_f32x4 pv = *reinterpret_cast<const sgd_f32x4*>(p4);
-  if (r.wd != 0.f) d += r.wd * pv;
+  if (r.wd != 0.f) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = __builtin_fmaf(r.wd, pv[j], d[j]);
+  }
   if (r.mom != 0.f) {
     sgd_f32x4 b;
     if (r.first) {
       b = d;
     } else {
       b = *reinterpret_cast<const sgd_f32x4*>(buf4);
-      b = r.mom * b + (1.f - r.damp) * d;
+      const float keep = 1.f - r.damp;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = __builtin_fmaf(r.mom, b[j], keep * d[j]);
     }
     *reinterpret_cast<sgd_f32x4*>(buf4) = b;
-    d = r.nesterov ? d + r.mom * b : b;
+    if (r.nesterov) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) d[j] = __builtin_fmaf(r.mom, b[j], d[j]);
+    } else {
+      d = b;
+    }
   }
-  const sgd_f32x4 nv = pv - r.lr * d;
+  sgd_f32x4 nv;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) nv[j] = __builtin_fmaf(-r.lr, d[j], pv[j]);
   *reinterpret_cast<sgd_f32x4*>(p4) = nv;
   return nv;
 }

@@ -243,7 +243,7 @@ class MLPStage(PipelineStage):
         kernel on ROCm (ops.linear_relu_head_u8): the boundary activation never reaches HBM."""
         if len(self.layers()) != 1 or self.plane_cache is None or not getattr(head, "supports_factored_grad", False):
             return False
-        return ops.relu_head_u8_supported(x, self.layers()[0].weight, head.layers()[-1].weight)
+        return ops.relu_head_u8_supported(x.reshape(x.shape[0], -1), self.layers()[0].weight, head.layers()[-1].weight)
 
     def fwd_head_fused(self, x, head: "MLPStage", target, loss_scale, stats, stats_init, dl_out, mask_out, ctx,
                        defer=False):
@@ -251,6 +251,8 @@ class MLPStage(PipelineStage):
         gradient dl into ``dl_out``, the ReLU bits into ``mask_out``; ctx then serves
         :meth:`bwd_from_factor`). Returns (dl bounds, deferred head reduction or None)."""
         lin, hl = self.layers()[0], head.layers()[-1]
+        x = x.reshape(x.shape[0], -1)
+        self.fused_head_calls = getattr(self, "fused_head_calls", 0) + 1
         epoch = self.flat_ref.param_epoch if self.flat_ref is not None else 0
         out = ops.linear_relu_head_u8(x, lin.weight, lin.bias, self.plane_cache, epoch, hl.weight.detach(),
                                       hl.bias.detach(), target, hl.weight.grad, hl.bias.grad, loss_scale, stats,

@@ -537,7 +537,7 @@ class PipelineEngine:
                 pend[w] = pw
                 if bound is not None and L == bw:
                     G._sdml_amax = bound  # per-block bounds on |dl @ W2| (the weight gradient's dz scale)
-                ctx0[w] = {"acts": [x], "mask": mask}
+                ctx0[w] = {"acts": [x.reshape(bw, -1)], "mask": mask}
                 gfused[w] = G
                 if crossing[w] == 0:
                     continue

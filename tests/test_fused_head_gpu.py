@@ -156,6 +156,8 @@ def test_engine_fused_head_step_matches_unfused(M, monkeypatch):
     monkeypatch.setenv("SDML_FUSE_HEAD", "1")
     e1 = _engine(M)
     l1 = _train(e1)
+    assert getattr(e1.stages[0], "fused_head_calls", 0) == 3 * M  # every wave went through the fused kernel
+    assert getattr(e0.stages[0], "fused_head_calls", 0) == 0
     assert l1 == pytest.approx(l0, rel=1e-5)
     torch.testing.assert_close(e1.flat.params, e0.flat.params, rtol=1e-5, atol=1e-7)
 

@@ -1,0 +1,242 @@
+// The whole training step of the 784-128-10 MLP at the reference's batch sizes (B <= 128; the
+// reference trains at B = 60: /root/reference/simple_distributed.py:18) as ONE cooperative launch:
+// stage 0 forward, stage 1 forward + log_softmax + NLL + backward, stage 0 backward and the SGD update
+// of all four parameter tensors (:63-64, :75-79, :111-113). At this size every kernel is a few
+// microseconds of work and the step is launch-bound (8 launches: ~53 us); here the dependency chain
+// runs inside one grid with one grid-wide barrier:
+//
+//   phase A (block g owns hidden units 2g, 2g+1; 64 blocks): h[:, own] = relu(x W1[own]^T + b1[own])
+//            -> HBM scratch; W2, b2 and the own W1 rows are copied to LDS before anyone updates them
+//   grid barrier (cooperative launch: the runtime guarantees every block is resident)
+//   phase B (every block, redundantly): logits of all rows from the full h, log_softmax, NLL,
+//            dl = scale (softmax - onehot) (identical bits in every block: same operations, same order)
+//            own part: dz = (dl W2[:, own]) * (h > 0); gW1[own] = dz^T x; gb1[own]; gW2[:, own]; block 0:
+//            gb2, loss, correct; then torch.optim.SGD's update of exactly the parameters the block owns
+//            (sgd_rule.h's fma sequence per element) - no other block reads them in this launch.
+// fp32 throughout (VALU fmas, fixed summation orders: deterministic). The flat gradient buffer is not
+// touched: the gradients are consumed where they are produced (it stays zero, as after a fused
+// zero_grad step).
+#include <hip/hip_cooperative_groups.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "kernels.h"
+
+namespace sdml {
+namespace {
+
+constexpr int SK = 784, SH = 128, SC = 10;
+constexpr int ST = 256;            // threads per block
+constexpr int SG = SH / 2;         // blocks: 2 hidden units each
+constexpr int SMAXB = 128;         // rows
+
+struct SmallArgs {
+  const void* x;  // [B][784] fp32 pixels, or uint8 (x8 = 1; scaled by 1/255)
+  int x8;
+  const int64_t* target;
+  int B;
+  float scale;
+  float* w1;  // [128][784]
+  float* b1;
+  float* w2;  // [10][128]
+  float* b2;
+  float* m1;  // momentum buffers aligned with the parameters (null without momentum)
+  float* mb1;
+  float* m2;
+  float* mb2;
+  float lr, mom, damp, wd;
+  int nesterov, first;
+  float* h;      // scratch [B][128]
+  float* stats;  // [2] loss sum, correct (overwritten)
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float xval(const SmallArgs& a, int b, int k) {
+  if (a.x8) return static_cast<float>(static_cast<const unsigned char*>(a.x)[(size_t)b * SK + k]) * (1.f / 255.f);
+  return static_cast<const float*>(a.x)[(size_t)b * SK + k];
+}
+
+// torch.optim.SGD on one parameter, with sgd_rule.h's operation sequence (explicit fmas)
+__device__ __forceinline__ void sgd1(float* p, float* buf, float d, const SmallArgs& a) {
+#pragma clang fp contract(off)
+  const float pv = *p;
+  if (a.wd != 0.f) d = __builtin_fmaf(a.wd, pv, d);
+  if (a.mom != 0.f) {
+    const float b = a.first ? d : __builtin_fmaf(a.mom, *buf, (1.f - a.damp) * d);
+    *buf = b;
+    d = a.nesterov ? __builtin_fmaf(a.mom, b, d) : b;
+  }
+  *p = __builtin_fmaf(-a.lr, d, pv);
+}
+
+__global__ void __launch_bounds__(ST) mlp_small_step_kernel(SmallArgs a) {
+  namespace cg = cooperative_groups;
+  __shared__ float w1s[2][SK];
+  __shared__ float w2s[SC][SH];
+  __shared__ float b2s[SC];
+  __shared__ float hs[SMAXB][SH + 1];
+  __shared__ float dls[SMAXB][SC];
+  __shared__ float dzs[SMAXB][2];
+  __shared__ float red[ST / 64][2];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int j0 = 2 * blockIdx.x;
+  const int B = a.B;
+
+  // ---- phase A ----
+  for (int i = t; i < 2 * SK; i += ST) w1s[i / SK][i % SK] = a.w1[(size_t)(j0 + i / SK) * SK + i % SK];
+  for (int i = t; i < SC * SH; i += ST) w2s[i / SH][i % SH] = a.w2[i];
+  if (t < SC) b2s[t] = a.b2[t];
+  const float bj0 = a.b1[j0], bj1 = a.b1[j0 + 1];
+  __syncthreads();
+  for (int b = wave; b < B; b += ST / 64) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int k = lane; k < SK; k += 64) {
+      const float xv = xval(a, b, k);
+      s0 = __builtin_fmaf(xv, w1s[0][k], s0);
+      s1 = __builtin_fmaf(xv, w1s[1][k], s1);
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if (lane == 0) {
+      a.h[(size_t)b * SH + j0] = fmaxf(s0 + bj0, 0.f);
+      a.h[(size_t)b * SH + j0 + 1] = fmaxf(s1 + bj1, 0.f);
+    }
+  }
+  cg::this_grid().sync();  // every block's h columns are in HBM (the sync orders global memory)
+
+  // ---- phase B: the head, redundantly in every block ----
+  for (int i = t; i < B * SH; i += ST) hs[i / SH][i % SH] = a.h[i];
+  __syncthreads();
+  float lsum = 0.f, csum = 0.f;
+  for (int b = wave; b < B; b += ST / 64) {
+    float z[SC];
+#pragma unroll
+    for (int c = 0; c < SC; ++c) {
+      float p = 0.f;
+      p = __builtin_fmaf(hs[b][2 * lane], w2s[c][2 * lane], p);
+      p = __builtin_fmaf(hs[b][2 * lane + 1], w2s[c][2 * lane + 1], p);
+      z[c] = wave_sum(p) + b2s[c];
+    }
+    float mx = z[0];
+    int am = 0;
+#pragma unroll
+    for (int c = 1; c < SC; ++c)
+      if (z[c] > mx) {
+        mx = z[c];
+        am = c;
+      }
+    float se = 0.f;
+#pragma unroll
+    for (int c = 0; c < SC; ++c) se += __expf(z[c] - mx);
+    const float lse = mx + __logf(se);
+    const int tg = (int)a.target[b];
+    float zt = 0.f;
+#pragma unroll
+    for (int c = 0; c < SC; ++c) zt = c == tg ? z[c] : zt;
+    lsum += lse - zt;
+    csum += am == tg ? 1.f : 0.f;
+    if (lane < SC) {
+      float zl = z[0];
+#pragma unroll
+      for (int c = 1; c < SC; ++c) zl = lane == c ? z[c] : zl;
+      dls[b][lane] = a.scale * (__expf(zl - lse) - (lane == tg ? 1.f : 0.f));
+    }
+  }
+  if (lane == 0) {
+    red[wave][0] = lsum;
+    red[wave][1] = csum;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && t == 0) {
+    float l = 0.f, c = 0.f;
+    for (int w = 0; w < ST / 64; ++w) {
+      l += red[w][0];
+      c += red[w][1];
+    }
+    a.stats[0] = l;
+    a.stats[1] = c;
+  }
+  // dz of the own hidden units (the ReLU backward from h > 0)
+  for (int i = t; i < 2 * B; i += ST) {
+    const int b = i >> 1, jj = i & 1;
+    float d = 0.f;
+#pragma unroll
+    for (int c = 0; c < SC; ++c) d = __builtin_fmaf(dls[b][c], w2s[c][j0 + jj], d);
+    dzs[b][jj] = hs[b][j0 + jj] > 0.f ? d : 0.f;
+  }
+  __syncthreads();
+  // gW1[own rows] = dz^T x, then the update of those rows (each element by the thread that reduced it)
+  for (int k = t; k < SK; k += ST) {
+    float g0 = 0.f, g1 = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float xv = xval(a, b, k);
+      g0 = __builtin_fmaf(dzs[b][0], xv, g0);
+      g1 = __builtin_fmaf(dzs[b][1], xv, g1);
+    }
+    const size_t o0 = (size_t)j0 * SK + k, o1 = o0 + SK;
+    sgd1(a.w1 + o0, a.m1 ? a.m1 + o0 : nullptr, g0, a);
+    sgd1(a.w1 + o1, a.m1 ? a.m1 + o1 : nullptr, g1, a);
+  }
+  if (t < 2) {  // gb1[own]
+    float g = 0.f;
+    for (int b = 0; b < B; ++b) g += dzs[b][t];
+    sgd1(a.b1 + j0 + t, a.mb1 ? a.mb1 + j0 + t : nullptr, g, a);
+  } else if (t >= 64 && t < 64 + 2 * SC) {  // gW2[:, own]
+    const int c = (t - 64) >> 1, jj = (t - 64) & 1;
+    float g = 0.f;
+    for (int b = 0; b < B; ++b) g = __builtin_fmaf(dls[b][c], hs[b][j0 + jj], g);
+    const size_t o = (size_t)c * SH + j0 + jj;
+    sgd1(a.w2 + o, a.m2 ? a.m2 + o : nullptr, g, a);
+  } else if (blockIdx.x == 0 && t >= 128 && t < 128 + SC) {  // gb2
+    const int c = t - 128;
+    float g = 0.f;
+    for (int b = 0; b < B; ++b) g += dls[b][c];
+    sgd1(a.b2 + c, a.mb2 ? a.mb2 + c : nullptr, g, a);
+  }
+}
+
+}  // namespace
+
+int mlp_small_step_max_batch() { return SMAXB; }
+
+bool mlp_small_step(const void* x, bool x_u8, const int64_t* target, int B, float scale, float* w1, float* b1,
+                    float* w2, float* b2, float* m1, float* mb1, float* m2, float* mb2, float lr, float mom,
+                    float damp, float wd, bool nesterov, bool first, float* h_scratch, float* stats,
+                    hipStream_t stream) {
+  if (B < 1 || B > SMAXB) return false;
+  SmallArgs a;
+  a.x = x;
+  a.x8 = x_u8 ? 1 : 0;
+  a.target = target;
+  a.B = B;
+  a.scale = scale;
+  a.w1 = w1;
+  a.b1 = b1;
+  a.w2 = w2;
+  a.b2 = b2;
+  a.m1 = m1;
+  a.mb1 = mb1;
+  a.m2 = m2;
+  a.mb2 = mb2;
+  a.lr = lr;
+  a.mom = mom;
+  a.damp = damp;
+  a.wd = wd;
+  a.nesterov = nesterov ? 1 : 0;
+  a.first = first ? 1 : 0;
+  a.h = h_scratch;
+  a.stats = stats;
+  void* args[] = {&a};
+  // cooperative: the launch fails (instead of deadlocking at the grid barrier) if the 64 blocks
+  // cannot all be resident at once
+  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(mlp_small_step_kernel), dim3(SG), dim3(ST), args,
+                                    0, stream) == hipSuccess;
+}
+
+}  // namespace sdml

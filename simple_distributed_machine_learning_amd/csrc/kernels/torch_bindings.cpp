@@ -994,6 +994,39 @@ void embedding_bwd_bf16(torch::Tensor g, torch::Tensor sorted_tok, torch::Tensor
                            (int)S, (int)C, (int)V, cur_stream());
 }
 
+// the whole 784-128-10 training step in one cooperative launch (mlp_small.hip); params/momentum are
+// views into the flat buffers (momentum views None without momentum). Returns False if not launched.
+bool mlp_small_step(torch::Tensor x, torch::Tensor target, torch::Tensor w1, torch::Tensor b1, torch::Tensor w2,
+                    torch::Tensor b2, c10::optional<torch::Tensor> m1, c10::optional<torch::Tensor> mb1,
+                    c10::optional<torch::Tensor> m2, c10::optional<torch::Tensor> mb2, double lr, double mom,
+                    double damp, double wd, bool nesterov, bool first, double scale, torch::Tensor stats) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 2 && x.size(1) == 784 &&
+                  (x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kUInt8),
+              "mlp_small_step: x must be a contiguous [B, 784] fp32 or uint8 device tensor");
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == torch::kInt64 && target.is_contiguous() &&
+                  target.numel() == x.size(0),
+              "mlp_small_step: target");
+  for (auto* t : {&w1, &b1, &w2, &b2, &stats}) check_f32_cuda(*t, "mlp_small_step");
+  TORCH_CHECK(w1.numel() == 128 * 784 && b1.numel() == 128 && w2.numel() == 10 * 128 && b2.numel() == 10 &&
+                  stats.numel() == 2,
+              "mlp_small_step: the 784-128-10 MLP only");
+  const bool has_m = m1.has_value() && m1->defined();
+  if (has_m) {
+    TORCH_CHECK(mb1 && m2 && mb2 && m1->numel() == w1.numel() && mb1->numel() == 128 && m2->numel() == 1280 &&
+                    mb2->numel() == 10,
+                "mlp_small_step: momentum buffers");
+  }
+  const int64_t B = x.size(0);
+  if (B < 1 || B > sdml::mlp_small_step_max_batch()) return false;
+  auto h = torch::empty({B, 128}, w1.options());
+  auto mp = [&](c10::optional<torch::Tensor>& t) { return has_m ? t->data_ptr<float>() : nullptr; };
+  return sdml::mlp_small_step(x.data_ptr(), x.scalar_type() == torch::kUInt8, target.data_ptr<int64_t>(), (int)B,
+                              (float)scale, w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(),
+                              b2.data_ptr<float>(), mp(m1), mp(mb1), mp(m2), mp(mb2), (float)lr, (float)mom,
+                              (float)damp, (float)wd, nesterov, first, h.data_ptr<float>(), stats.data_ptr<float>(),
+                              cur_stream());
+}
+
 bool u8_fwd_head_supported_op(int64_t M, int64_t N, int64_t K, int64_t C) {
   return sdml::u8_fwd_head_supported((int)M, (int)N, (int)K, (int)K, nullptr, (int)C);
 }
@@ -1352,6 +1385,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "uint8 first layer + classifier head in one launch (h stays on chip): dl, ReLU bits, head slab");
   m.def("u8_fwd_head_supported", &u8_fwd_head_supported_op, "shape check for linear_relu_head_u8 (M, N, K, C)");
   m.def("relu_bits", &relu_bits, "int32 [M, N/32] ReLU bits of y (the uint8 kernels' mask layout)");
+  m.def("mlp_small_step", &mlp_small_step, "784-128-10 MLP training step (fwd, loss, bwd, SGD) in one launch");
+  m.def("mlp_small_step_max_batch", &sdml::mlp_small_step_max_batch);
   m.def("gelu_fwd_bf16", &gelu_fwd_bf16, "tanh-GELU forward (bf16)");
   m.def("gelu_bwd_bf16", &gelu_bwd_bf16, "tanh-GELU backward (bf16): gy * gelu'(x)", py::arg("gy"), py::arg("x"),
         py::arg("inplace") = false);

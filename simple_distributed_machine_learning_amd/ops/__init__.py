@@ -345,3 +345,18 @@ def ref_cnn_stage1(x, fc1, fc2, target, seed: int, p: float, drop: bool, scale: 
     for t, g in zip(ps, gs[1:]):
         t.grad.add_(g)
     return gs[0]
+
+
+def mlp_small_step(x, target, fc1, fc2, optimizer, scale: float, stats) -> bool:
+    """ROCm: the whole 784-128-10 training step (both stages' forward, loss, backward and the SGD update
+    of fc1/fc2, torch.optim.SGD semantics) in ONE cooperative launch (mlp_small.hip) for batches of up
+    to ``mlp_small_step_max_batch()`` rows. ``stats`` [2] receives (loss sum, correct). Returns False
+    when it did not run (the caller then takes the multi-kernel path)."""
+    k = _k()
+    if x.shape[0] > k.mlp_small_step_max_batch():
+        return False
+    o = optimizer
+    mv = [o.buffer_view(p) for p in (fc1.weight, fc1.bias, fc2.weight, fc2.bias)]
+    return bool(k.mlp_small_step(x, target, fc1.weight, fc1.bias, fc2.weight, fc2.bias, *mv, float(o.lr),
+                                 float(o.momentum), float(o.dampening), float(o.weight_decay), bool(o.nesterov),
+                                 o.steps == 0, float(scale), stats))

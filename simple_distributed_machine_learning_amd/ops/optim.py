@@ -87,9 +87,10 @@ class FusedSGD:
                 float(self.dampening), float(self.weight_decay), bool(self.nesterov), self.steps == 0,
                 bool(zero_grad), planes, int(poff), int(prows), int(pk))
 
-    def commit_fused(self, zero_grad: bool = True):
-        """Book-keeping of a step that ``fused_args`` let a reduction kernel apply (what step() does
-        after its kernel)."""
+    def commit_fused(self, zero_grad: bool = True, planes_current: bool = True):
+        """Book-keeping of a step that a fused kernel applied (what step() does after its kernel):
+        ``fused_args``' reductions, or the whole-step kernel (``planes_current=False``: it did not
+        write the weight-plane cache, which the next uint8 forward then re-splits)."""
         if zero_grad:
             self.flat.grads_zero = True
         self.steps += 1
@@ -98,7 +99,15 @@ class FusedSGD:
             from . import PlaneCache
 
             cache, w, _ = self.plane_cache
-            cache.token = PlaneCache.token_of(w, self.flat.param_epoch)
+            cache.token = PlaneCache.token_of(w, self.flat.param_epoch) if planes_current else None
+
+    def buffer_view(self, param: torch.Tensor):
+        """The momentum buffer's view aligned with ``param`` (a view into the flat parameter buffer), or
+        None without momentum."""
+        if self.momentum == 0:
+            return None
+        off = (param.data_ptr() - self.flat.params.data_ptr()) // self.flat.params.element_size()
+        return self.momentum_buffer[off:off + param.numel()].view(param.shape)
 
     def zero_grad(self):
         self.flat.zero_grad()

@@ -30,6 +30,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..models.base import ModelSpec, PipelineStage, build_stages
+from .. import ops
 from ..ops import pixels_to_float
 from ..ops.optim import FusedSGD
 from ..utils.flat import FlatParams
@@ -191,6 +192,7 @@ class PipelineEngine:
         # rotate: stage 0's forward and stage 1's forward+loss+backward in one kernel for the rows that
         # stay on their owner (models/mlp.py fwd_head_fused); SDML_FUSE_HEAD=0 keeps them separate
         self.fuse_head = os.environ.get("SDML_FUSE_HEAD", "1") != "0"
+        self._small_step = None  # one-launch reference-size MLP step available (decided on first use)
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
 
@@ -268,6 +270,10 @@ class PipelineEngine:
                 self._advance_rng()
             z = torch.zeros(2, device=dev, dtype=torch.float32)
             return StepResult(z[0], z[1], 0, time.perf_counter() - t0)
+        if train and step_optimizer and self._small_step_ok(batch_size):
+            res = self._run_small_mlp_step(dataset, start, batch_size, global_batch, t0)
+            if res is not None:
+                return res
         if self.kind == "rotate" and self.use_alltoall and self.P == 2:
             return self._run_rotate_alltoall(dataset, start, batch_size, train, global_batch, step_optimizer, t0)
         if self.kind == "rotate":
@@ -691,6 +697,47 @@ class PipelineEngine:
             stats.zero_()
         self.last_timing = tm.result()
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
+
+    # ---------------------------------------------------------------------------------------
+    def _small_step_ok(self, batch_size: int) -> bool:
+        """Both stages of the 784-128-10 MLP on this (only) rank, fp32 weights, a batch the one-launch
+        step kernel takes, and no gradients pending from an earlier step_optimizer=False call."""
+        if self._small_step is None:
+            s = self.stages
+            self._small_step = bool(
+                self.device.type == "cuda" and self.mesh.world_size == 1 and self.P == 2 and 0 in s and 1 in s
+                and os.environ.get("SDML_SMALL_STEP", "1") != "0" and not self.timing and not self.debug_sync
+                and self.optimizer.master is None and hasattr(s[0], "layers") and hasattr(s[1], "layers")
+                and [tuple(l.weight.shape) for l in s[0].layers()] == [(128, 784)]
+                and [tuple(l.weight.shape) for l in s[1].layers()] == [(10, 128)])
+        # (not inside a hipGraph capture: a cooperative launch is not captured; graphs/replays already
+        # remove the launch overhead the one-launch step exists for)
+        return (self._small_step and batch_size <= 128 and self.flat.grads_zero
+                and not torch.cuda.is_current_stream_capturing())
+
+    def _run_small_mlp_step(self, dataset, start, batch_size, global_batch, t0):
+        """The reference-size training step (B <= 128, e.g. its B = 60) as ONE kernel launch (ops.mlp_small_step):
+        at this size the multi-kernel step is launch-bound."""
+        dev = self.device
+        x = dataset.inputs(start, batch_size)
+        if x.device != dev:
+            x = x.to(dev, non_blocking=True)
+        x = x.reshape(batch_size, -1)
+        if x.dtype not in (torch.float32, torch.uint8):
+            x = x.float()
+        tgt = dataset.targets(start, batch_size)
+        if tgt.device != dev:
+            tgt = tgt.to(dev, non_blocking=True)
+        stats = torch.empty(2, device=dev, dtype=torch.float32)
+        fc1, fc2 = self.stages[0].layers()[0], self.stages[1].layers()[0]
+        scale = self._loss_scale(dataset, batch_size, global_batch)
+        if not ops.mlp_small_step(x.contiguous(), tgt.contiguous(), fc1, fc2, self.optimizer, scale, stats):
+            return None
+        self.optimizer.commit_fused(zero_grad=True, planes_current=False)
+        self.global_step += 1
+        self._advance_rng()
+        self.last_timing = {}
+        return StepResult(stats[0], stats[1], batch_size, time.perf_counter() - t0)
 
     def reduce_metrics(self, res: StepResult, group=None) -> Tuple[float, int, int]:
         """Sum (loss, correct, count) over all last-stage holders (world). Host-syncs."""

@@ -1,0 +1,288 @@
+// bf16 GEMMs of the GPT-2 stages (BASELINE config 5) with fused epilogues: the forward of every
+// Linear (Y = X W^T + b, optionally Y = gelu(X W^T + b) writing the pre-activation too) and the input
+// gradient (dX = dY W, optionally times gelu'(u) of the layer below: the MLP's activation backward).
+// They replace the hipBLASLt GEMMs of the forward and input-gradient passes and the two GELU kernels
+// (the weight gradient is gemm_bf16_wgrad.hip's).
+//
+//   C[M][N] = A[M][K] . op(B)   A row-major (the activations / incoming gradient, k contiguous)
+//     BL = 0 ("NT"): B stored [N][K] (nn.Linear's weight; forward)       -> C = A B^T
+//     BL = 1 ("NN"): B stored [K][N] (the same weight; input gradient)   -> C = A B
+//
+// Geometry (gfx950): 256 x 256 output tile per 512-thread workgroup, 8 waves as 2 (M) x 4 (N), wave tile
+// 128 x 64 = 8 x 4 v_mfma_f32_16x16x32_bf16 accumulators (128 VGPRs), K-step 64 (two 32-deep substeps).
+// Both operands go HBM -> LDS by LDS-DMA (global_load_lds_dwordx4, 16 B per lane, no VGPR staging) into
+// two 64 KiB stages: K-step t+1's DMA is issued before K-step t's fragment reads + MFMAs, then one
+// counted wait + barrier per K-step ("2-phase" form of the guide's T3/T4 schedule).
+// LDS images are lane-linear per DMA instruction, so the bank swizzles live on the per-lane SOURCE
+// address (an involution applied again on the read):
+//   [rows][64 k] images (A, NT B): 16-B chunk c of row r stored at c ^ ((r >> 1) & 7): the 16 rows of a
+//     ds_read_b128 lane group land in 16 distinct 16-B bank slots (conflict-free)
+//   [64 k][256 n] image (NN B): chunk c of k-row r at c ^ (((r & 3) | ((r >> 1) & 4)) << 1): the 8 rows of
+//     a 32-lane half of the ds_read_b64_tr_b16 pair (k-rows q, q + 8 of the block) hit distinct 32-B slots
+// The grid is remapped XCD-aware (bijective): consecutive tiles of one M panel run on one XCD's L2.
+// Epilogue through LDS (the stage buffers are free then): each wave stores its 128 x 64 tile as bf16 rows,
+// then every lane moves whole 16-B row pieces, where the elementwise epilogue runs:
+//   EPI_BIAS        C = bf16(acc + b)
+//   EPI_BIAS_GELU   U = bf16(acc + b) -> aux, C = bf16(gelu(U))            (exactly the unfused pair)
+//   EPI_DGELU       C = bf16(gelu'(U) * bf16(acc)), U read from aux       (exactly the unfused pair)
+#include <hip/hip_bf16.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "kernels.h"
+
+namespace sdml {
+namespace {
+
+typedef unsigned short u16;
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef u16 u16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int GT = 512, TM = 256, TN = 256, TK = 64;
+constexpr int A_BYTES = TM * TK * 2;     // 32 KiB
+constexpr int STAGE = 2 * A_BYTES;       // A + B
+constexpr int SMEM = 2 * STAGE;          // 128 KiB
+constexpr int GLDS = STAGE / 1024 / 8;   // DMA instructions per wave per stage (8)
+
+struct GP {
+  const u16* A;
+  const u16* B;
+  u16* C;
+  const u16* bias;  // [N] bf16 (EPI_BIAS, EPI_BIAS_GELU)
+  u16* aux;         // EPI_BIAS_GELU: U out; EPI_DGELU: U in ([M][ldaux])
+  int M, N, K, lda, ldb, ldc, ldaux;
+  int tiles_m, tiles_n;
+};
+
+__device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((unsigned)v) << 16); }
+__device__ __forceinline__ u16 f2bf(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);  // RNE, NaN-preserving
+  return *reinterpret_cast<u16*>(&h);
+}
+
+constexpr float kBeta = 0.7978845608028654f, kKappa = 0.044715f;  // gpt2_ops.hip's tanh-GELU
+__device__ __forceinline__ float gelu_f(float x) {
+  const float inner = kBeta * (x + kKappa * (x * x * x));
+  return 0.5f * x * (1.f + tanhf(inner));
+}
+__device__ __forceinline__ float gelu_grad_f(float dy, float x) {
+  const float x_sq = x * x, x_cube = x_sq * x;
+  const float t = tanhf(kBeta * (x + kKappa * x_cube));
+  const float left = 0.5f * x, right = 1.f + t;
+  return dy * (0.5f * right + left * (1.f - t * t) * kBeta * (1.f + 3.f * kKappa * x_sq));
+}
+
+__device__ __forceinline__ void glds16(const void* src, unsigned char* lds_block) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_block, 16, 0, 0);
+}
+
+__device__ __forceinline__ int rk_swz(int r) { return (r >> 1) & 7; }                          // [rows][64]
+__device__ __forceinline__ int kn_swz(int r) { return ((r & 3) | ((r >> 1) & 4)) << 1; }       // [64][256]
+
+// one stage: A tile rows m0.., k0..k0+63; B tile (NT: rows n0.., NN: k-rows k0.., columns n0..)
+template <int BL>
+__device__ __forceinline__ void issue_stage(const GP& p, unsigned char* st, int m0, int n0, int k0, int wave,
+                                            int lane) {
+#pragma unroll
+  for (int u = 0; u < GLDS / 2; ++u) {  // A: 32 instructions of 8 rows x 128 B
+    const int q = wave + 8 * u;
+    const int r = 8 * q + (lane >> 3);
+    const int c = (lane & 7) ^ rk_swz(r);
+    const int gr = min(m0 + r, p.M - 1);
+    glds16(p.A + (size_t)gr * p.lda + k0 + 8 * c, st + 1024 * q);
+  }
+#pragma unroll
+  for (int u = 0; u < GLDS / 2; ++u) {
+    const int q = wave + 8 * u;
+    if constexpr (BL == 0) {  // B [N][K]: like A
+      const int r = 8 * q + (lane >> 3);
+      const int c = (lane & 7) ^ rk_swz(r);
+      const int gr = min(n0 + r, p.N - 1);
+      glds16(p.B + (size_t)gr * p.ldb + k0 + 8 * c, st + A_BYTES + 1024 * q);
+    } else {  // B [K][N]: 2 k-rows x 512 B
+      const int r = 2 * q + (lane >> 5);
+      const int c = (lane & 31) ^ kn_swz(r);
+      const int gc = min(n0 + 8 * c, p.N - 8);
+      glds16(p.B + (size_t)(k0 + r) * p.ldb + gc, st + A_BYTES + 1024 * q);
+    }
+  }
+}
+
+__device__ __forceinline__ bf16x8 ld_b128(const unsigned char* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ s16x4 ds_tr16(const unsigned char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+template <int BL, int EPI>
+__global__ void __launch_bounds__(GT) gemm_bf16_kernel(GP p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  const int nwg = p.tiles_m * p.tiles_n;
+  int wg = blockIdx.x;
+  if (nwg >= 16) {  // XCD-aware bijective remap: blocks sharing an XCD get consecutive tile ids
+    const int q = nwg / 8, r = nwg % 8, xcd = wg % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
+  }
+  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;  // M fastest: neighbours share the B panel
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane LDS byte offsets of the fragments (stage-relative)
+  const int g = lane >> 4, l16 = lane & 15;
+  int aoff[2][8];  // [substep][m-tile]: A row wm*128 + 16 i + l16, chunk 4 s + g
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = wm * 128 + 16 * i + l16;
+      aoff[s][i] = r * 128 + 16 * ((4 * s + g) ^ rk_swz(r));
+    }
+  int boff[2][4][2];  // NT: [s][j][0]; NN: the two transposed reads
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (BL == 0) {
+        const int r = wn * 64 + 16 * j + l16;
+        boff[s][j][0] = A_BYTES + r * 128 + 16 * ((4 * s + g) ^ rk_swz(r));
+        boff[s][j][1] = 0;
+      } else {
+        const int q = l16 >> 2, pp = l16 & 3;
+        const int n = wn * 64 + 16 * j + 4 * pp;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int r = 32 * s + 8 * g + 4 * h + q;
+          boff[s][j][h] = A_BYTES + r * 512 + 16 * ((n >> 3) ^ kn_swz(r)) + 2 * (n & 7);
+        }
+      }
+    }
+
+  const int nk = p.K / TK;
+  issue_stage<BL>(p, smem, m0, n0, 0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const unsigned char* st = smem + (t & 1) * STAGE;
+    if (t + 1 < nk) issue_stage<BL>(p, smem + ((t + 1) & 1) * STAGE, m0, n0, (t + 1) * TK, wave, lane);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (BL == 0) {
+          b[j] = ld_b128(st + boff[s][j][0]);
+        } else {
+          const s16x4 lo = ds_tr16(st + boff[s][j][0]), hi = ds_tr16(st + boff[s][j][1]);
+          b[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 a = ld_b128(st + aoff[s][i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  // ---- epilogue: bf16 rows through the (free) stage buffers, 16-B row pieces to HBM ----
+  // wave image [128 rows][64 cols] bf16 (128 B rows, 16-B chunks swizzled like the A image)
+  unsigned char* W = smem + wave * (128 * 128);
+  float bj[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = min(n0 + wn * 64 + 16 * j + l16, p.N - 1);
+      bj[j] = bf2f(p.bias[col]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * i + 4 * g + r, col = 16 * j + l16;
+        const float v = acc[i][j][r] + bj[j];
+        *reinterpret_cast<u16*>(W + row * 128 + 16 * ((col >> 3) ^ rk_swz(row)) + 2 * (col & 7)) = f2bf(v);
+      }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+  for (int it = 0; it < 16; ++it) {
+    const int row = 8 * it + (lane >> 3), ch = lane & 7;
+    const u16x8 v = *reinterpret_cast<const u16x8*>(W + row * 128 + 16 * (ch ^ rk_swz(row)));
+    const int grow = m0 + wm * 128 + row, gcol = n0 + wn * 64 + 8 * ch;
+    if (grow >= p.M || gcol >= p.N) continue;  // (N % 8 == 0: a chunk is all in or all out)
+    u16x8 o = v;
+    if constexpr (EPI == EPI_BIAS_GELU) {
+      *reinterpret_cast<u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol) = v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_f(bf2f(v[e])));
+    } else if constexpr (EPI == EPI_DGELU) {
+      const u16x8 u = *reinterpret_cast<const u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_grad_f(bf2f(v[e]), bf2f(u[e])));
+    }
+    *reinterpret_cast<u16x8*>(p.C + (size_t)grow * p.ldc + gcol) = o;
+  }
+}
+
+}  // namespace
+
+bool gemm_bf16_supported(int M, int N, int K, int lda, int ldb, int ldc, bool b_kn) {
+  // K whole K-steps; 16-B aligned rows for the DMA and the row-piece stores
+  return M >= 1 && N >= 8 && K >= TK && K % TK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+         ldc % 8 == 0 && (b_kn ? ldb >= N : ldb >= K) && lda >= K && ldc >= N;
+}
+
+void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool b_kn,
+               int epi, const void* bias, void* aux, int ldaux, hipStream_t stream) {
+  GP p;
+  p.A = static_cast<const u16*>(A);
+  p.B = static_cast<const u16*>(B);
+  p.C = static_cast<u16*>(C);
+  p.bias = static_cast<const u16*>(bias);
+  p.aux = static_cast<u16*>(aux);
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = ldb;
+  p.ldc = ldc;
+  p.ldaux = ldaux;
+  p.tiles_m = (M + TM - 1) / TM;
+  p.tiles_n = (N + TN - 1) / TN;
+  const dim3 grid(p.tiles_m * p.tiles_n);
+#define GB_LAUNCH(BLV, E) hipLaunchKernelGGL((gemm_bf16_kernel<BLV, E>), grid, dim3(GT), 0, stream, p)
+#define GB_EPI(BLV)                                       \
+  do {                                                    \
+    switch (epi) {                                        \
+      case EPI_BIAS: GB_LAUNCH(BLV, EPI_BIAS); break;      \
+      case EPI_BIAS_GELU: GB_LAUNCH(BLV, EPI_BIAS_GELU); break; \
+      case EPI_DGELU: GB_LAUNCH(BLV, EPI_DGELU); break;    \
+      default: GB_LAUNCH(BLV, EPI_STORE); break;           \
+    }                                                     \
+  } while (0)
+  if (b_kn) GB_EPI(1);
+  else GB_EPI(0);
+#undef GB_EPI
+#undef GB_LAUNCH
+}
+
+}  // namespace sdml

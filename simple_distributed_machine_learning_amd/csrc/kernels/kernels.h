@@ -48,6 +48,8 @@ enum GemmEpi : int {
   EPI_BIAS_RELU = 2,      // C = relu(acc + bias[n])
   EPI_ACCUM = 3,          // C += acc
   EPI_ATOMIC = 4,         // atomicAdd(C, acc)           (split-K capable)
+  EPI_BIAS_GELU = 5,      // gemm_bf16 only: U = acc + bias -> aux, C = gelu(U)
+  EPI_DGELU = 6,          // gemm_bf16 only: C = acc * gelu'(U), U read from aux
 };
 
 struct GemmArgs {
@@ -259,6 +261,13 @@ void embedding_fwd_bf16(const int64_t* tok, const void* wte, const void* wpe, vo
 // stably, with their positions) - deterministic, either gradient may be null
 void embedding_bwd_bf16(const void* g, const int64_t* sorted_tok, const int64_t* perm, void* gwte, void* gwpe, int B,
                         int S, int C, int V, hipStream_t stream);
+
+// ---- bf16 GEMM with fused epilogues (gemm_bf16.hip): C[M][N] = A[M][K] . (b_kn ? B[K][N] : B[N][K]^T) ----
+// epi: EPI_STORE, EPI_BIAS (bias [N] bf16), EPI_BIAS_GELU (aux = pre-activation out), EPI_DGELU (aux =
+// pre-activation in). K % 64 == 0, N % 8 == 0, leading dimensions % 8 == 0 (gemm_bf16_supported).
+bool gemm_bf16_supported(int M, int N, int K, int lda, int ldb, int ldc, bool b_kn);
+void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool b_kn,
+               int epi, const void* bias, void* aux, int ldaux, hipStream_t stream);
 
 // ---- weight gradient of a bf16 Linear: gw[M,N] (bf16) += gy[T,M]^T x[T,N] -------------------
 // fp32 accumulation, token range split over workgroups, deterministic slab reduction.

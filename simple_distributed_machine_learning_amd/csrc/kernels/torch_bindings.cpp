@@ -1027,6 +1027,51 @@ bool mlp_small_step(torch::Tensor x, torch::Tensor target, torch::Tensor w1, tor
                               cur_stream());
 }
 
+// C = A . (b_kn ? B : B^T) with a fused epilogue (gemm_bf16.hip); A [M, K] (row stride lda), B [N, K] or
+// [K, N]; returns C [M, N] bf16. epi: 0 store, 1 bias, 5 bias+GELU (aux out, allocated here and returned),
+// 6 gelu' (aux in).
+std::tuple<torch::Tensor, c10::optional<torch::Tensor>> gemm_bf16_op(torch::Tensor A, torch::Tensor B,
+                                                                     c10::optional<torch::Tensor> bias, bool b_kn,
+                                                                     int64_t epi, c10::optional<torch::Tensor> aux) {
+  TORCH_CHECK(A.is_cuda() && A.scalar_type() == torch::kBFloat16 && A.dim() == 2 && A.stride(1) == 1,
+              "gemm_bf16: A must be a 2-D bf16 device tensor with unit column stride");
+  check_bf16_cuda(B, "B");
+  TORCH_CHECK(B.dim() == 2, "gemm_bf16: B must be 2-D");
+  const int64_t M = A.size(0), K = A.size(1), N = b_kn ? B.size(1) : B.size(0);
+  TORCH_CHECK((b_kn ? B.size(0) : B.size(1)) == K, "gemm_bf16: inner dimensions ", A.sizes(), " vs ", B.sizes());
+  TORCH_CHECK(sdml::gemm_bf16_supported((int)M, (int)N, (int)K, (int)A.stride(0), (int)B.stride(0), (int)N, b_kn),
+              "gemm_bf16: unsupported shape (gemm_bf16_supported)");
+  auto C = torch::empty({M, N}, A.options());
+  c10::optional<torch::Tensor> u;
+  const void* bp = nullptr;
+  if (epi == sdml::EPI_BIAS || epi == sdml::EPI_BIAS_GELU) {
+    TORCH_CHECK(bias.has_value() && bias->defined(), "gemm_bf16: bias required");
+    check_bf16_cuda(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N, "gemm_bf16: bias shape");
+    bp = bias->data_ptr();
+  }
+  void* ap = nullptr;
+  int64_t ldaux = N;
+  if (epi == sdml::EPI_BIAS_GELU) {
+    u = torch::empty({M, N}, A.options());
+    ap = u->data_ptr();
+  } else if (epi == sdml::EPI_DGELU) {
+    TORCH_CHECK(aux.has_value() && aux->defined(), "gemm_bf16: pre-activation required");
+    check_bf16_cuda(*aux, "aux");
+    TORCH_CHECK(aux->numel() == M * N, "gemm_bf16: pre-activation shape");
+    ap = aux->data_ptr();
+  } else {
+    TORCH_CHECK(epi == sdml::EPI_STORE || epi == sdml::EPI_BIAS, "gemm_bf16: unknown epilogue ", epi);
+  }
+  sdml::gemm_bf16(A.data_ptr(), B.data_ptr(), C.data_ptr(), (int)M, (int)N, (int)K, (int)A.stride(0),
+                  (int)B.stride(0), (int)N, b_kn, (int)epi, bp, ap, (int)ldaux, cur_stream());
+  return {C, u};
+}
+
+bool gemm_bf16_supported_op(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, bool b_kn) {
+  return sdml::gemm_bf16_supported((int)M, (int)N, (int)K, (int)lda, (int)ldb, (int)N, b_kn);
+}
+
 bool u8_fwd_head_supported_op(int64_t M, int64_t N, int64_t K, int64_t C) {
   return sdml::u8_fwd_head_supported((int)M, (int)N, (int)K, (int)K, nullptr, (int)C);
 }
@@ -1385,6 +1430,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "uint8 first layer + classifier head in one launch (h stays on chip): dl, ReLU bits, head slab");
   m.def("u8_fwd_head_supported", &u8_fwd_head_supported_op, "shape check for linear_relu_head_u8 (M, N, K, C)");
   m.def("relu_bits", &relu_bits, "int32 [M, N/32] ReLU bits of y (the uint8 kernels' mask layout)");
+  m.def("gemm_bf16", &gemm_bf16_op, "bf16 GEMM with fused bias / bias+GELU / GELU-backward epilogues",
+        py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("b_kn") = false, py::arg("epi") = 0,
+        py::arg("aux") = py::none());
+  m.def("gemm_bf16_supported", &gemm_bf16_supported_op, "shape check for gemm_bf16 (M, N, K, lda, ldb, b_kn)");
   m.def("mlp_small_step", &mlp_small_step, "784-128-10 MLP training step (fwd, loss, bwd, SGD) in one launch");
   m.def("mlp_small_step_max_batch", &sdml::mlp_small_step_max_batch);
   m.def("gelu_fwd_bf16", &gelu_fwd_bf16, "tanh-GELU forward (bf16)");

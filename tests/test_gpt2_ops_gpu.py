@@ -73,3 +73,52 @@ def test_embedding_fwd_bwd(B, S, C, V):
     torch.testing.assert_close(gw1.double(), ref_w, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(gp1[:S].double(), ref_p, rtol=2e-2, atol=2e-2)
     assert float(gp1[S:].abs().max()) == 0.0
+
+
+def _ref_gelu(u):
+    return F.gelu(u.float(), approximate="tanh")
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 776, 192), (4096, 2304, 768), (1000, 768, 3072)])
+@pytest.mark.parametrize("b_kn", [False, True])
+def test_gemm_bf16_layouts_match_fp32(M, N, Kd, b_kn):
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(Kd, N, generator=g) if b_kn else torch.randn(N, Kd, generator=g)).to(DEV, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    Wf = W.float() if b_kn else W.float().t()
+    ref = A.float() @ Wf
+    C, _ = K.gemm_bf16(A, W, None, b_kn, 0)
+    torch.testing.assert_close(C.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+    if not b_kn:
+        C, _ = K.gemm_bf16(A, W, bias, False, 1)
+        torch.testing.assert_close(C.float(), ref + bias.float(), rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+
+
+def test_gemm_bf16_identity_asymmetric():
+    """A = I and an asymmetric B catch a transposed fragment or C map (guide §3)."""
+    n = 256
+    A = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+    B = (torch.arange(n * n, device=DEV, dtype=torch.float32).reshape(n, n) % 251 / 8).to(torch.bfloat16)
+    C, _ = K.gemm_bf16(A, B, None, False, 0)  # A B^T
+    assert torch.equal(C, B.t().contiguous())
+    C, _ = K.gemm_bf16(A, B, None, True, 0)  # A B
+    assert torch.equal(C, B)
+
+
+def test_gemm_bf16_gelu_epilogues_match_unfused():
+    g = torch.Generator(device="cpu").manual_seed(5)
+    M, N, Kd = 512, 3072, 768
+    x = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, Kd, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    y, u = K.gemm_bf16(x, w, b, False, 5)
+    ub, _ = K.gemm_bf16(x, w, b, False, 1)
+    assert torch.equal(u, ub)  # the pre-activation is the plain bias GEMM's output
+    assert torch.equal(y, K.gelu_fwd_bf16(ub))  # and the activation is the standalone GELU kernel's
+    # backward: dU = (dY W2) * gelu'(U), exactly the unfused GEMM + gelu_bwd pair
+    w2 = (torch.randn(768, N, generator=g) * 0.05).to(DEV, torch.bfloat16)  # c_proj [768, 3072]
+    gy = torch.randn(M, 768, generator=g).to(DEV, torch.bfloat16)
+    du, _ = K.gemm_bf16(gy, w2, None, True, 6, u)
+    da, _ = K.gemm_bf16(gy, w2, None, True, 0)
+    assert torch.equal(du, K.gelu_bwd_bf16(da, u, False))

@@ -27,7 +27,7 @@ namespace sdml {
 namespace {
 
 constexpr int SK = 784, SH = 128, SC = 10;
-constexpr int ST = 256;            // threads per block
+constexpr int ST = 1024;           // threads per block (16 waves: rows spread over more waves)
 constexpr int SG = SH / 2;         // blocks: 2 hidden units each
 constexpr int SMAXB = 128;         // rows
 
@@ -95,11 +95,16 @@ __global__ void __launch_bounds__(ST) mlp_small_step_kernel(SmallArgs a) {
   const float bj0 = a.b1[j0], bj1 = a.b1[j0 + 1];
   __syncthreads();
   for (int b = wave; b < B; b += ST / 64) {
+    // the row's 13 loads are issued together (fully unrolled, the partial 13th masked)
+    float xv[13];
+#pragma unroll
+    for (int i = 0; i < 13; ++i) xv[i] = (lane + 64 * i < SK) ? xval(a, b, lane + 64 * i) : 0.f;
     float s0 = 0.f, s1 = 0.f;
-    for (int k = lane; k < SK; k += 64) {
-      const float xv = xval(a, b, k);
-      s0 = __builtin_fmaf(xv, w1s[0][k], s0);
-      s1 = __builtin_fmaf(xv, w1s[1][k], s1);
+#pragma unroll
+    for (int i = 0; i < 13; ++i) {
+      const int k = min(lane + 64 * i, SK - 1);
+      s0 = __builtin_fmaf(xv[i], w1s[0][k], s0);
+      s1 = __builtin_fmaf(xv[i], w1s[1][k], s1);
     }
     s0 = wave_sum(s0);
     s1 = wave_sum(s1);
@@ -174,7 +179,18 @@ __global__ void __launch_bounds__(ST) mlp_small_step_kernel(SmallArgs a) {
   // gW1[own rows] = dz^T x, then the update of those rows (each element by the thread that reduced it)
   for (int k = t; k < SK; k += ST) {
     float g0 = 0.f, g1 = 0.f;
-    for (int b = 0; b < B; ++b) {
+    int b = 0;
+    for (; b + 16 <= B; b += 16) {  // 16 loads in flight, then the fmas in row order
+      float xv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) xv[u] = xval(a, b + u, k);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        g0 = __builtin_fmaf(dzs[b + u][0], xv[u], g0);
+        g1 = __builtin_fmaf(dzs[b + u][1], xv[u], g1);
+      }
+    }
+    for (; b < B; ++b) {
       const float xv = xval(a, b, k);
       g0 = __builtin_fmaf(dzs[b][0], xv, g0);
       g1 = __builtin_fmaf(dzs[b][1], xv, g1);

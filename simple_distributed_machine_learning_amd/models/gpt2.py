@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .base import ModelSpec, PipelineStage
-from ..ops.linear import Linear, linear
+from ..ops.linear import Linear, linear, mlp_gelu
 from ..ops.transformer import LayerNorm, add_layer_norm, causal_attention, cross_entropy_sum, embedding, gelu
 from ..parallel.tp import TPContext, column_slice, copy_to_tp, reduce_from_tp, shard_parameter
 
@@ -80,8 +80,8 @@ class MLP(nn.Module):
         self.tp = tp
 
     def forward(self, x):
-        if self.tp is None:
-            return self.c_proj(gelu(self.c_fc(x)))
+        if self.tp is None:  # GELU fused into the c_fc forward / c_proj input-gradient GEMM epilogues
+            return mlp_gelu(x, self.c_fc.weight, self.c_fc.bias, self.c_proj.weight, self.c_proj.bias)
         h = gelu(self.c_fc(copy_to_tp(x, self.tp)))
         return reduce_from_tp(linear(h, self.c_proj.weight), self.tp) + self.c_proj.bias
 

@@ -347,7 +347,14 @@ def ref_cnn_stage1(x, fc1, fc2, target, seed: int, p: float, drop: bool, scale: 
     return gs[0]
 
 
-def mlp_small_step(x, target, fc1, fc2, optimizer, scale: float, stats) -> bool:
+def mlp_small_step_args(fc1, fc2, optimizer):
+    """The parameter / momentum views :func:`mlp_small_step` takes, built once per engine (the flat
+    buffers never move): per step only the batch-dependent arguments cross the binding."""
+    mv = [optimizer.buffer_view(p) for p in (fc1.weight, fc1.bias, fc2.weight, fc2.bias)]
+    return (fc1.weight, fc1.bias, fc2.weight, fc2.bias, *mv)
+
+
+def mlp_small_step(x, target, fc1, fc2, optimizer, scale: float, stats, args=None) -> bool:
     """ROCm: the whole 784-128-10 training step (both stages' forward, loss, backward and the SGD update
     of fc1/fc2, torch.optim.SGD semantics) in ONE cooperative launch (mlp_small.hip) for batches of up
     to ``mlp_small_step_max_batch()`` rows. ``stats`` [2] receives (loss sum, correct). Returns False
@@ -356,7 +363,7 @@ def mlp_small_step(x, target, fc1, fc2, optimizer, scale: float, stats) -> bool:
     if x.shape[0] > k.mlp_small_step_max_batch():
         return False
     o = optimizer
-    mv = [o.buffer_view(p) for p in (fc1.weight, fc1.bias, fc2.weight, fc2.bias)]
-    return bool(k.mlp_small_step(x, target, fc1.weight, fc1.bias, fc2.weight, fc2.bias, *mv, float(o.lr),
-                                 float(o.momentum), float(o.dampening), float(o.weight_decay), bool(o.nesterov),
-                                 o.steps == 0, float(scale), stats))
+    if args is None:
+        args = mlp_small_step_args(fc1, fc2, optimizer)
+    return bool(k.mlp_small_step(x, target, *args, float(o.lr), float(o.momentum), float(o.dampening),
+                                 float(o.weight_decay), bool(o.nesterov), o.steps == 0, float(scale), stats))

@@ -16,7 +16,9 @@ the bias gradient with a generic reduction. This module avoids both:
 
 When a parameter has no ``.grad`` yet (standalone use), the gradients are returned to
 autograd in the usual way. CPU tensors and non-bf16 dtypes keep the plain ``F.linear``
-path. The GEMMs themselves are plain library GEMMs (hipBLASLt) for the forward and input gradient.
+path. The forward / input-gradient GEMMs of a plain Linear are library GEMMs (hipBLASLt, faster at these
+shapes than gemm_bf16.hip's current schedule: tools/bench_gemm_bf16.py); the MLP's c_fc forward and c_proj
+input gradient run on gemm_bf16.hip with the GELU fused into their epilogues (:func:`mlp_gelu`).
 """
 from __future__ import annotations
 
@@ -43,24 +45,78 @@ class _LinearFn(torch.autograd.Function):
         w, b = ctx.w, ctx.b
         g2 = gy.reshape(-1, gy.shape[-1])
         dx = (g2 @ w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
-        gw = gb = None
-        bias_done = False
-        if ctx.needs_input_grad[1]:
-            if w.grad is not None and _wgrad_ok(g2, x2, w.grad):
-                fuse_b = (b is not None and ctx.needs_input_grad[2] and b.grad is not None
-                          and b.grad.is_contiguous() and b.grad.dtype == torch.bfloat16)
-                kernels().wgrad_bf16_(g2, x2, w.grad, b.grad if fuse_b else None)
-                bias_done = fuse_b
-            elif w.grad is not None:
-                w.grad.addmm_(g2.t(), x2)
-            else:
-                gw = g2.t() @ x2
-        if b is not None and ctx.needs_input_grad[2] and not bias_done:
-            if b.grad is not None and b.grad.is_contiguous() and g2.stride(-1) == 1:
-                kernels().bias_grad_bf16_(g2, b.grad)
-            else:
-                gb = g2.sum(0)
+        gw, gb = _param_grads(g2, x2, w, b, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         return dx, gw, gb
+
+
+def _param_grads(g2, x2, w, b, need_w: bool, need_b: bool):
+    """Weight / bias gradients of y = x w^T + b from g2 = dy: added in place into the flat-buffer .grad
+    (returns None for those) or returned for autograd to accumulate."""
+    gw = gb = None
+    bias_done = False
+    if need_w:
+        if w.grad is not None and _wgrad_ok(g2, x2, w.grad):
+            fuse_b = (b is not None and need_b and b.grad is not None
+                      and b.grad.is_contiguous() and b.grad.dtype == torch.bfloat16)
+            kernels().wgrad_bf16_(g2, x2, w.grad, b.grad if fuse_b else None)
+            bias_done = fuse_b
+        elif w.grad is not None:
+            w.grad.addmm_(g2.t(), x2)
+        else:
+            gw = g2.t() @ x2
+    if b is not None and need_b and not bias_done:
+        if b.grad is not None and b.grad.is_contiguous() and g2.stride(-1) == 1:
+            kernels().bias_grad_bf16_(g2, b.grad)
+        else:
+            gb = g2.sum(0)
+    return gw, gb
+
+
+EPI_BIAS_GELU, EPI_DGELU = 5, 6  # csrc/kernels/kernels.h GemmEpi
+
+
+class _MLPFn(torch.autograd.Function):
+    """GPT-2's MLP, y = c_proj(gelu(c_fc(x))), with the activation fused into the GEMMs on both sides
+    (gemm_bf16.hip): the c_fc forward writes the pre-activation U and gelu(U) from its epilogue, and the
+    c_proj input-gradient GEMM multiplies by gelu'(U) in its epilogue - no standalone GELU passes over
+    the [tokens, 3072] activations. The remaining GEMMs (c_proj forward, c_fc input gradient) stay on the
+    library path, which is faster at these shapes (tools/bench_gemm_bf16.py); weight gradients as Linear."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        x2 = x.reshape(-1, x.shape[-1])
+        a, u = kernels().gemm_bf16(x2, w1, b1, False, EPI_BIAS_GELU)
+        y = torch.addmm(b2, a, w2.t())
+        ctx.save_for_backward(x2, u, a)
+        ctx.params = (w1, b1, w2, b2)
+        ctx.in_shape = x.shape
+        return y.view(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, u, a = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.params
+        g2 = gy.reshape(-1, gy.shape[-1])
+        du, _ = kernels().gemm_bf16(g2, w2, None, True, EPI_DGELU, u)  # (dY W2) * gelu'(U)
+        gw2, gb2 = _param_grads(g2, a, w2, b2, ctx.needs_input_grad[3], ctx.needs_input_grad[4])
+        dx = (du @ w1).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        gw1, gb1 = _param_grads(du, x2, w1, b1, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        return dx, gw1, gb1, gw2, gb2
+
+
+def mlp_gelu(x, w1, b1, w2, b2):
+    """c_proj(gelu_tanh(c_fc(x))) with the fused-epilogue GEMMs on ROCm bf16 (else the composed ops)."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16 and b1 is not None
+            and b2 is not None):
+        T, C = x.numel() // x.shape[-1], x.shape[-1]
+        k = kernels()
+        if (k.gemm_bf16_supported(T, w1.shape[0], C, C, C, False)
+                and k.gemm_bf16_supported(T, w2.shape[1], w2.shape[0], w2.shape[0], w2.shape[1], True)
+                and x.stride(-1) == 1):
+            return _MLPFn.apply(x, w1, b1, w2, b2)
+    from .transformer import gelu
+
+    return linear(gelu(linear(x, w1, b1)), w2, b2)
 
 
 def _wgrad_ok(g2, x2, gw) -> bool:

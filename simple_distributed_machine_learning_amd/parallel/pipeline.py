@@ -193,6 +193,7 @@ class PipelineEngine:
         # stay on their owner (models/mlp.py fwd_head_fused); SDML_FUSE_HEAD=0 keeps them separate
         self.fuse_head = os.environ.get("SDML_FUSE_HEAD", "1") != "0"
         self._small_step = None  # one-launch reference-size MLP step available (decided on first use)
+        self._small_args = None
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
 
@@ -730,8 +731,11 @@ class PipelineEngine:
             tgt = tgt.to(dev, non_blocking=True)
         stats = torch.empty(2, device=dev, dtype=torch.float32)
         fc1, fc2 = self.stages[0].layers()[0], self.stages[1].layers()[0]
+        if self._small_args is None:
+            self._small_args = ops.mlp_small_step_args(fc1, fc2, self.optimizer)
         scale = self._loss_scale(dataset, batch_size, global_batch)
-        if not ops.mlp_small_step(x.contiguous(), tgt.contiguous(), fc1, fc2, self.optimizer, scale, stats):
+        if not ops.mlp_small_step(x.contiguous(), tgt.contiguous(), fc1, fc2, self.optimizer, scale, stats,
+                                  self._small_args):
             return None
         self.optimizer.commit_fused(zero_grad=True, planes_current=False)
         self.global_step += 1

@@ -122,3 +122,28 @@ def test_gemm_bf16_gelu_epilogues_match_unfused():
     du, _ = K.gemm_bf16(gy, w2, None, True, 6, u)
     da, _ = K.gemm_bf16(gy, w2, None, True, 0)
     assert torch.equal(du, K.gelu_bwd_bf16(da, u, False))
+
+
+def test_mlp_gelu_fused_matches_composed():
+    """GPT-2's MLP with the GELU fused into the GEMM epilogues (ops.linear.mlp_gelu) against
+    c_proj(gelu(c_fc(x))) composed from separate kernels: forward and every gradient."""
+    from simple_distributed_machine_learning_amd.ops.linear import _MLPFn, linear
+
+    g = torch.Generator(device="cpu").manual_seed(9)
+    T, C = 1024, 768
+    x0 = torch.randn(2, T // 2, C, generator=g).to(DEV, torch.bfloat16)
+    ps = [(torch.randn(4 * C, C, generator=g) * 0.02), (torch.randn(4 * C, generator=g) * 0.02),
+          (torch.randn(C, 4 * C, generator=g) * 0.02), (torch.randn(C, generator=g) * 0.02)]
+    ps = [p.to(DEV, torch.bfloat16) for p in ps]
+    gy = torch.randn(2, T // 2, C, generator=g).to(DEV, torch.bfloat16)
+
+    def run(fused):
+        x = x0.clone().requires_grad_(True)
+        w = [p.clone().requires_grad_(True) for p in ps]
+        y = _MLPFn.apply(x, *w) if fused else linear(gelu(linear(x, w[0], w[1])), w[2], w[3])
+        y.backward(gy)
+        return [y] + [x.grad] + [t.grad for t in w]
+
+    for a, b in zip(run(True), run(False)):
+        scale = float(b.float().abs().max())
+        torch.testing.assert_close(a.float(), b.float(), rtol=3e-2, atol=3e-2 * scale)

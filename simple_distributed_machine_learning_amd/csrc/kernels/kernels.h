@@ -241,14 +241,14 @@ void layernorm_bwd_bf16_accum(const void* x, const void* w, const void* gy, cons
 int bias_grad_blocks(int M);
 void bias_grad_bf16(const void* gy, int M, int N, int ld, void* gb, float* workspace, hipStream_t stream);
 
-// ---- the whole 784-128-10 MLP training step in one cooperative launch (mlp_small.hip, B <= 128) --
+// ---- the whole 784-128-10 MLP training step in two launches (mlp_small.hip, B <= 128) ----------------
 // x [B][784] fp32 (or uint8 pixels, x_u8: scaled by 1/255), parameters and momentum buffers updated in
-// place (torch.optim.SGD), stats = {loss sum, correct}. Returns false if the launch was refused.
+// place (torch.optim.SGD), stats = {loss sum, correct}; scratch: h [B][128], snap [10 * 128 + 10].
 int mlp_small_step_max_batch();
 bool mlp_small_step(const void* x, bool x_u8, const int64_t* target, int B, float scale, float* w1, float* b1,
                     float* w2, float* b2, float* m1, float* mb1, float* m2, float* mb2, float lr, float mom,
-                    float damp, float wd, bool nesterov, bool first, float* h_scratch, float* stats,
-                    hipStream_t stream);
+                    float damp, float wd, bool nesterov, bool first, float* h_scratch, float* snap_scratch,
+                    float* stats, hipStream_t stream);
 
 // ---- GPT-2 elementwise / embedding kernels (gpt2_ops.hip) ------------------------------------
 // tanh-GELU (n % 8 == 0, 16-B aligned): y = gelu(x); gx = gy * gelu'(x) (gx may alias gy)

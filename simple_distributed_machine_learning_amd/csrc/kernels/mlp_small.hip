@@ -1,22 +1,21 @@
 // The whole training step of the 784-128-10 MLP at the reference's batch sizes (B <= 128; the
-// reference trains at B = 60: /root/reference/simple_distributed.py:18) as ONE cooperative launch:
-// stage 0 forward, stage 1 forward + log_softmax + NLL + backward, stage 0 backward and the SGD update
-// of all four parameter tensors (:63-64, :75-79, :111-113). At this size every kernel is a few
-// microseconds of work and the step is launch-bound (8 launches: ~53 us); here the dependency chain
-// runs inside one grid with one grid-wide barrier:
+// reference trains at B = 60: /root/reference/simple_distributed.py:18) as TWO launches: stage 0
+// forward, stage 1 forward + log_softmax + NLL + backward, stage 0 backward and the SGD update of all
+// four parameter tensors (:63-64, :75-79, :111-113). At this size every kernel is a few microseconds
+// of work and the multi-kernel step (6 launches + the host work between them) is launch-bound:
 //
-//   phase A (block g owns hidden units 2g, 2g+1; 64 blocks): h[:, own] = relu(x W1[own]^T + b1[own])
-//            -> HBM scratch; W2, b2 and the own W1 rows are copied to LDS before anyone updates them
-//   grid barrier (cooperative launch: the runtime guarantees every block is resident)
-//   phase B (every block, redundantly): logits of all rows from the full h, log_softmax, NLL,
+//   kernel A (block g owns hidden units 2g, 2g+1; 64 blocks): h[:, own] = relu(x W1[own]^T + b1[own])
+//   kernel B (every block, redundantly): logits of all rows from the full h, log_softmax, NLL,
 //            dl = scale (softmax - onehot) (identical bits in every block: same operations, same order)
 //            own part: dz = (dl W2[:, own]) * (h > 0); gW1[own] = dz^T x; gb1[own]; gW2[:, own]; block 0:
 //            gb2, loss, correct; then torch.optim.SGD's update of exactly the parameters the block owns
-//            (sgd_rule.h's fma sequence per element) - no other block reads them in this launch.
+//            (sgd_rule.h's fma sequence per element). W2 / b2 are read into LDS before a __syncthreads
+//            that precedes every update, and no block reads another block's updated parameters.
+// (A first version ran both phases in one cooperative launch with a grid barrier: 29.6 us of kernel
+// time, but the cooperative launch API alone held the step at ~50 us of host time.)
 // fp32 throughout (VALU fmas, fixed summation orders: deterministic). The flat gradient buffer is not
 // touched: the gradients are consumed where they are produced (it stays zero, as after a fused
 // zero_grad step).
-#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -48,6 +47,7 @@ struct SmallArgs {
   float lr, mom, damp, wd;
   int nesterov, first;
   float* h;      // scratch [B][128]
+  float* snap;   // scratch [10 * 128 + 10]: W2 and b2 as kernel B must read them (before any update)
   float* stats;  // [2] loss sum, correct (overwritten)
 };
 
@@ -75,24 +75,17 @@ __device__ __forceinline__ void sgd1(float* p, float* buf, float d, const SmallA
   *p = __builtin_fmaf(-a.lr, d, pv);
 }
 
-__global__ void __launch_bounds__(ST) mlp_small_step_kernel(SmallArgs a) {
-  namespace cg = cooperative_groups;
+__global__ void __launch_bounds__(ST) mlp_small_fwd_kernel(SmallArgs a) {
   __shared__ float w1s[2][SK];
-  __shared__ float w2s[SC][SH];
-  __shared__ float b2s[SC];
-  __shared__ float hs[SMAXB][SH + 1];
-  __shared__ float dls[SMAXB][SC];
-  __shared__ float dzs[SMAXB][2];
-  __shared__ float red[ST / 64][2];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int j0 = 2 * blockIdx.x;
   const int B = a.B;
-
-  // ---- phase A ----
   for (int i = t; i < 2 * SK; i += ST) w1s[i / SK][i % SK] = a.w1[(size_t)(j0 + i / SK) * SK + i % SK];
-  for (int i = t; i < SC * SH; i += ST) w2s[i / SH][i % SH] = a.w2[i];
-  if (t < SC) b2s[t] = a.b2[t];
   const float bj0 = a.b1[j0], bj1 = a.b1[j0 + 1];
+  // snapshot of W2 / b2 for kernel B: its blocks update W2's columns (and block 0 b2) while other blocks
+  // may still be starting, so they read the values of this step from here (stream order: A before B)
+  if (t < 2 * SC) a.snap[(t >> 1) * SH + j0 + (t & 1)] = a.w2[(t >> 1) * SH + j0 + (t & 1)];
+  if (blockIdx.x == 0 && t >= 64 && t < 64 + SC) a.snap[SC * SH + t - 64] = a.b2[t - 64];
   __syncthreads();
   for (int b = wave; b < B; b += ST / 64) {
     // the row's 13 loads are issued together (fully unrolled, the partial 13th masked)
@@ -113,9 +106,20 @@ __global__ void __launch_bounds__(ST) mlp_small_step_kernel(SmallArgs a) {
       a.h[(size_t)b * SH + j0 + 1] = fmaxf(s1 + bj1, 0.f);
     }
   }
-  cg::this_grid().sync();  // every block's h columns are in HBM (the sync orders global memory)
+}
 
-  // ---- phase B: the head, redundantly in every block ----
+__global__ void __launch_bounds__(ST) mlp_small_bwd_kernel(SmallArgs a) {
+  __shared__ float w2s[SC][SH];
+  __shared__ float b2s[SC];
+  __shared__ float hs[SMAXB][SH + 1];
+  __shared__ float dls[SMAXB][SC];
+  __shared__ float dzs[SMAXB][2];
+  __shared__ float red[ST / 64][2];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int j0 = 2 * blockIdx.x;
+  const int B = a.B;
+  for (int i = t; i < SC * SH; i += ST) w2s[i / SH][i % SH] = a.snap[i];
+  if (t < SC) b2s[t] = a.snap[SC * SH + t];
   for (int i = t; i < B * SH; i += ST) hs[i / SH][i % SH] = a.h[i];
   __syncthreads();
   float lsum = 0.f, csum = 0.f;
@@ -223,8 +227,8 @@ int mlp_small_step_max_batch() { return SMAXB; }
 
 bool mlp_small_step(const void* x, bool x_u8, const int64_t* target, int B, float scale, float* w1, float* b1,
                     float* w2, float* b2, float* m1, float* mb1, float* m2, float* mb2, float lr, float mom,
-                    float damp, float wd, bool nesterov, bool first, float* h_scratch, float* stats,
-                    hipStream_t stream) {
+                    float damp, float wd, bool nesterov, bool first, float* h_scratch, float* snap_scratch,
+                    float* stats, hipStream_t stream) {
   if (B < 1 || B > SMAXB) return false;
   SmallArgs a;
   a.x = x;
@@ -247,12 +251,11 @@ bool mlp_small_step(const void* x, bool x_u8, const int64_t* target, int B, floa
   a.nesterov = nesterov ? 1 : 0;
   a.first = first ? 1 : 0;
   a.h = h_scratch;
+  a.snap = snap_scratch;
   a.stats = stats;
-  void* args[] = {&a};
-  // cooperative: the launch fails (instead of deadlocking at the grid barrier) if the 64 blocks
-  // cannot all be resident at once
-  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(mlp_small_step_kernel), dim3(SG), dim3(ST), args,
-                                    0, stream) == hipSuccess;
+  hipLaunchKernelGGL(mlp_small_fwd_kernel, dim3(SG), dim3(ST), 0, stream, a);
+  hipLaunchKernelGGL(mlp_small_bwd_kernel, dim3(SG), dim3(ST), 0, stream, a);
+  return true;
 }
 
 }  // namespace sdml

@@ -994,7 +994,7 @@ void embedding_bwd_bf16(torch::Tensor g, torch::Tensor sorted_tok, torch::Tensor
                            (int)S, (int)C, (int)V, cur_stream());
 }
 
-// the whole 784-128-10 training step in one cooperative launch (mlp_small.hip); params/momentum are
+// the whole 784-128-10 training step in two launches (mlp_small.hip); params/momentum are
 // views into the flat buffers (momentum views None without momentum). Returns False if not launched.
 bool mlp_small_step(torch::Tensor x, torch::Tensor target, torch::Tensor w1, torch::Tensor b1, torch::Tensor w2,
                     torch::Tensor b2, c10::optional<torch::Tensor> m1, c10::optional<torch::Tensor> mb1,
@@ -1018,13 +1018,13 @@ bool mlp_small_step(torch::Tensor x, torch::Tensor target, torch::Tensor w1, tor
   }
   const int64_t B = x.size(0);
   if (B < 1 || B > sdml::mlp_small_step_max_batch()) return false;
-  auto h = torch::empty({B, 128}, w1.options());
+  auto h = torch::empty({B * 128 + 10 * 128 + 10}, w1.options());  // h, then the W2/b2 snapshot
   auto mp = [&](c10::optional<torch::Tensor>& t) { return has_m ? t->data_ptr<float>() : nullptr; };
   return sdml::mlp_small_step(x.data_ptr(), x.scalar_type() == torch::kUInt8, target.data_ptr<int64_t>(), (int)B,
                               (float)scale, w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(),
                               b2.data_ptr<float>(), mp(m1), mp(mb1), mp(m2), mp(mb2), (float)lr, (float)mom,
-                              (float)damp, (float)wd, nesterov, first, h.data_ptr<float>(), stats.data_ptr<float>(),
-                              cur_stream());
+                              (float)damp, (float)wd, nesterov, first, h.data_ptr<float>(),
+                              h.data_ptr<float>() + B * 128, stats.data_ptr<float>(), cur_stream());
 }
 
 // C = A . (b_kn ? B : B^T) with a fused epilogue (gemm_bf16.hip); A [M, K] (row stride lda), B [N, K] or

@@ -356,7 +356,7 @@ def mlp_small_step_args(fc1, fc2, optimizer):
 
 def mlp_small_step(x, target, fc1, fc2, optimizer, scale: float, stats, args=None) -> bool:
     """ROCm: the whole 784-128-10 training step (both stages' forward, loss, backward and the SGD update
-    of fc1/fc2, torch.optim.SGD semantics) in ONE cooperative launch (mlp_small.hip) for batches of up
+    of fc1/fc2, torch.optim.SGD semantics) in two launches (mlp_small.hip) for batches of up
     to ``mlp_small_step_max_batch()`` rows. ``stats`` [2] receives (loss sum, correct). Returns False
     when it did not run (the caller then takes the multi-kernel path)."""
     k = _k()

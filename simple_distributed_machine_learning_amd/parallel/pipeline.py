@@ -711,13 +711,10 @@ class PipelineEngine:
                 and self.optimizer.master is None and hasattr(s[0], "layers") and hasattr(s[1], "layers")
                 and [tuple(l.weight.shape) for l in s[0].layers()] == [(128, 784)]
                 and [tuple(l.weight.shape) for l in s[1].layers()] == [(10, 128)])
-        # (not inside a hipGraph capture: a cooperative launch is not captured; graphs/replays already
-        # remove the launch overhead the one-launch step exists for)
-        return (self._small_step and batch_size <= 128 and self.flat.grads_zero
-                and not torch.cuda.is_current_stream_capturing())
+        return self._small_step and batch_size <= 128 and self.flat.grads_zero
 
     def _run_small_mlp_step(self, dataset, start, batch_size, global_batch, t0):
-        """The reference-size training step (B <= 128, e.g. its B = 60) as ONE kernel launch (ops.mlp_small_step):
+        """The reference-size training step (B <= 128, e.g. its B = 60) in two kernel launches (ops.mlp_small_step):
         at this size the multi-kernel step is launch-bound."""
         dev = self.device
         x = dataset.inputs(start, batch_size)

@@ -1,4 +1,4 @@
-"""The reference-size MLP step as ONE cooperative launch (mlp_small.hip) against the multi-kernel engine
+"""The reference-size MLP step in two launches (mlp_small.hip) against the multi-kernel engine
 step it replaces (SDML_SMALL_STEP=0): same data, same seeds, every SGD option; fp32 agreement (the
 summation orders differ), equal correct counts. Reference: /root/reference/simple_distributed.py:18
 (B = 60), :100-113 (one training step)."""

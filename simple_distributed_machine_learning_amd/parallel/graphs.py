@@ -20,8 +20,9 @@ What changes between replays, and how it gets into the graph:
   captured SGD launch is the steady-state update.
 
 Constraints (checked): a CUDA/ROCm engine; a training step with an optimizer update; and
-one process, unless ``allow_collectives``. RCCL collectives can be captured, but that path
-is opt-in until it has been validated on multi-GPU hardware. The returned
+one process, unless ``allow_collectives``: RCCL collectives are captured then (the gradient
+all-reduce, boundary all-to-alls); tests/test_graphs_gpu.py replays a step whose all-reduce runs on a
+one-rank RCCL communicator. The returned
 :class:`StepResult` tensors belong to the graph and are overwritten by the next replay, so
 read them first. The ragged last batch of an epoch has a different shape and gets its own
 graph. A failed capture falls back to eager execution and emits a warning.
@@ -97,7 +98,8 @@ class GraphedStep:
             raise ValueError("GraphedStep: multi-process capture (RCCL in the graph) is opt-in: "
                              "pass allow_collectives=True")
         self.engine = engine
-        self.graphs: Dict[Tuple[int, Optional[int]], Tuple[torch.cuda.CUDAGraph, _StaticWindow, StepResult, int]] = {}
+        self.graphs: Dict[Tuple[int, Optional[int]], tuple] = {}  # (graph, window, result, start, planes_current)
+        self._planes_current = True
         self.pool = None
         self.disabled = False
         self.replays = 0
@@ -128,6 +130,9 @@ class GraphedStep:
         torch.cuda.synchronize(eng.device)
         with torch.cuda.graph(g, pool=pool, stream=self.stream):
             res = eng.run(win, start, batch_size, train=True, global_batch=global_batch)
+        # whether the captured step keeps the weight planes current (the one-launch small-batch step
+        # does not write them: its replays must leave the caches invalid, as the eager step does)
+        self._planes_current = all(c.token is not None for c, _ in self._plane_caches())
         # capture recorded but did not execute the step: restore the host-side state
         eng.global_step, eng.optimizer.steps, eng.flat.grads_zero = gs, steps, zero
         eng.flat.param_epoch = epoch
@@ -145,7 +150,7 @@ class GraphedStep:
             self.pool = g.pool()
         # the graph ends with the optimizer's fused zero_grad, like the eager step
         self.engine.flat.grads_zero = True
-        return g, win, res, start
+        return g, win, res, start, self._planes_current
 
     def _eager(self, dataset, start, batch_size, global_batch):
         cur = torch.cuda.current_stream(self.engine.device)
@@ -174,10 +179,11 @@ class GraphedStep:
                 self.disabled = True
                 torch.cuda.synchronize(eng.device)
                 return self._eager(dataset, start, batch_size, global_batch)
-        g, win, res, cap_start = self.graphs[key]
+        g, win, res, cap_start, planes_current = self.graphs[key]
         win.load(dataset, start - cap_start)
         g.replay()
         eng.global_step += 1
-        eng.optimizer.commit_fused(zero_grad=True)  # the captured step's update: steps, epoch, cache tokens
+        # the captured step's update: steps, epoch, cache tokens
+        eng.optimizer.commit_fused(zero_grad=True, planes_current=planes_current)
         self.replays += 1
         return StepResult(res.loss_sum, res.correct, res.count, time.perf_counter() - t0)

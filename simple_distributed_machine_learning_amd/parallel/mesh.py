@@ -58,10 +58,14 @@ class Mesh:
     transport_kind: str = "direct"
     _transport: Optional[object] = None
 
+    # a one-rank mesh that still builds its communicators and runs its collectives (graph-capture
+    # and RCCL checks on one GPU: init_mesh(force_collectives=True) inside a 1-rank process group)
+    force_collectives: bool = False
+
     @property
     def transport(self):
         """The rank's :class:`~.p2p.Transport` (None on a 1-rank mesh)."""
-        if self.world_size == 1:
+        if self.world_size == 1 and not self.force_collectives:
             return None
         if self._transport is None:
             from .p2p import make_transport
@@ -147,7 +151,8 @@ def _pg_options(backend: str):
 def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = None,
               timeout_s: float = 600.0, rank: Optional[int] = None, world_size: Optional[int] = None,
               local_rank: Optional[int] = None, device: Optional[torch.device] = None,
-              p2p_channels: bool = True, tp: int = 1, transport: Optional[str] = None) -> Mesh:
+              p2p_channels: bool = True, tp: int = 1, transport: Optional[str] = None,
+              force_collectives: bool = False) -> Mesh:
     """Join (or reuse) the default process group and build the dp x pp mesh.
 
     Rank/world come from arguments, else torchrun-style env (RANK, WORLD_SIZE, LOCAL_RANK).
@@ -188,7 +193,8 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
     mesh.tp_rank = rank % tp
     mesh.pp_rank = (rank // tp) % pp
     mesh.dp_rank = rank // (tp * pp)
-    if world_size == 1:
+    mesh.force_collectives = bool(force_collectives and world_size == 1 and dist.is_initialized())
+    if world_size == 1 and not mesh.force_collectives:
         return mesh
 
     if not dist.is_initialized():
@@ -233,8 +239,9 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
                     if mesh.rank in (a, b):
                         mesh.p2p_groups[(src, dst)] = g
     for ranks in replica_groups_spec(world_size, pp, schedule_kind, tp):
-        g = new_group(ranks) if len(ranks) > 1 else None
-        if rank in ranks and len(ranks) > 1:
+        real = len(ranks) > 1 or mesh.force_collectives
+        g = new_group(ranks) if real else None
+        if rank in ranks and real:
             mesh.grad_group = g
             mesh.grad_group_ranks = ranks
     if tp > 1:

@@ -62,3 +62,50 @@ def test_graphed_dropout_draws_fresh_masks():
     assert g.replays == 3
     assert len(set(losses[1:])) == 3  # every replay saw different dropout masks
     assert int(e.step_ctr) == 4
+
+
+def test_graphed_step_with_rccl_allreduce_on_one_rank():
+    """A captured step that contains an RCCL collective: a one-rank "nccl" (RCCL) process group, a mesh
+    that keeps its gradient all-reduce (force_collectives), GraphedStep(allow_collectives=True); the
+    replays must match the eager engine without any process group. Runs in a subprocess (process-group
+    state stays out of the test session)."""
+    import os
+    import subprocess
+    import sys
+    import textwrap
+
+    from conftest import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent("""
+        import datetime, torch, torch.distributed as dist
+        from simple_distributed_machine_learning_amd.data import SyntheticMNIST
+        from simple_distributed_machine_learning_amd.models import get_model_spec
+        from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh
+        from simple_distributed_machine_learning_amd.parallel.graphs import GraphedStep
+        dev = torch.device("cuda", 0)
+        ds = SyntheticMNIST(8192 * 6, seed=3, device=dev, pixels="u8")
+        def engine(mesh):
+            return PipelineEngine(get_model_spec("mlp", 2), mesh, schedule_kind="rotate", num_microbatches=1,
+                                  lr=0.1, momentum=0.5, seed=5)
+        e1 = engine(init_mesh(pp=1, schedule_kind="rotate", rank=0, world_size=1, device=dev))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, timeout=datetime.timedelta(seconds=60))
+        m2 = init_mesh(pp=1, schedule_kind="rotate", rank=0, world_size=1, device=dev, force_collectives=True)
+        e2 = engine(m2)
+        assert e2.grad_sync.enabled and e2.transport is not None
+        g = GraphedStep(e2, allow_collectives=True)
+        ops0 = e2.transport.ops
+        for i in range(6):
+            r1 = e1.run(ds, i * 8192, 8192, train=True)
+            r2 = g(ds, i * 8192, 8192)
+            assert abs(float(r1.loss_sum) - float(r2.loss_sum)) <= 1e-4 * abs(float(r1.loss_sum))
+        torch.cuda.synchronize()
+        assert g.replays == 5 and not g.disabled, (g.replays, g.disabled)
+        assert e2.transport.ops > ops0  # the all-reduce was issued (eager step + capture)
+        torch.testing.assert_close(e1.flat.params, e2.flat.params, rtol=1e-5, atol=1e-6)
+        dist.destroy_process_group()
+        print("graph+rccl ok")
+    """)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0 and "graph+rccl ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

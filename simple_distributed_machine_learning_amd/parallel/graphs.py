@@ -98,8 +98,10 @@ class GraphedStep:
             raise ValueError("GraphedStep: multi-process capture (RCCL in the graph) is opt-in: "
                              "pass allow_collectives=True")
         self.engine = engine
-        self.graphs: Dict[Tuple[int, Optional[int]], tuple] = {}  # (graph, window, result, start, planes_current)
+        # (graph, window, result, start, planes_current, relies_on_planes) per (batch, global batch)
+        self.graphs: Dict[Tuple[int, Optional[int]], tuple] = {}
         self._planes_current = True
+        self._relies_on_planes = False
         self.pool = None
         self.disabled = False
         self.replays = 0
@@ -126,6 +128,9 @@ class GraphedStep:
         eng = self.engine
         gs, steps, zero = eng.global_step, eng.optimizer.steps, eng.flat.grads_zero
         epoch, tokens = eng.flat.param_epoch, [c.token for c, _ in self._plane_caches()]
+        # a graph captured while the caches were current reads them without re-splitting: its replays
+        # are only valid while they stay current (see __call__)
+        self._relies_on_planes = bool(self._plane_caches()) and self._caches_current()
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(eng.device)
         with torch.cuda.graph(g, pool=pool, stream=self.stream):
@@ -150,7 +155,7 @@ class GraphedStep:
             self.pool = g.pool()
         # the graph ends with the optimizer's fused zero_grad, like the eager step
         self.engine.flat.grads_zero = True
-        return g, win, res, start, self._planes_current
+        return g, win, res, start, self._planes_current, self._relies_on_planes
 
     def _eager(self, dataset, start, batch_size, global_batch):
         cur = torch.cuda.current_stream(self.engine.device)
@@ -166,10 +171,10 @@ class GraphedStep:
             return self._eager(dataset, start, batch_size, global_batch)
         key = (batch_size, global_batch)
         t0 = time.perf_counter()
-        if self.graphs and not self._caches_current():
-            # weights changed outside the captured step: the graphs would read stale weight planes.
-            # Drop them; this step runs eagerly (re-splitting the planes) and the next one recaptures.
-            self.graphs.clear()
+        if any(gr[5] for gr in self.graphs.values()) and not self._caches_current():
+            # weights changed outside the captured step: graphs that read the cached weight planes would
+            # use stale ones. Drop them; this step runs eagerly (re-splitting) and the next one recaptures.
+            self.graphs = {k: gr for k, gr in self.graphs.items() if not gr[5]}
             return self._eager(dataset, start, batch_size, global_batch)
         if key not in self.graphs:
             try:
@@ -179,7 +184,7 @@ class GraphedStep:
                 self.disabled = True
                 torch.cuda.synchronize(eng.device)
                 return self._eager(dataset, start, batch_size, global_batch)
-        g, win, res, cap_start, planes_current = self.graphs[key]
+        g, win, res, cap_start, planes_current, _ = self.graphs[key]
         win.load(dataset, start - cap_start)
         g.replay()
         eng.global_step += 1

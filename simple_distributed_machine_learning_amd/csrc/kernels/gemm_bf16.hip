@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "gelu.h"
 #include "kernels.h"
 
 namespace sdml {
@@ -62,18 +63,6 @@ __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((unsigned
 __device__ __forceinline__ u16 f2bf(float f) {
   __hip_bfloat16 h = __float2bfloat16(f);  // RNE, NaN-preserving
   return *reinterpret_cast<u16*>(&h);
-}
-
-constexpr float kBeta = 0.7978845608028654f, kKappa = 0.044715f;  // gpt2_ops.hip's tanh-GELU
-__device__ __forceinline__ float gelu_f(float x) {
-  const float inner = kBeta * (x + kKappa * (x * x * x));
-  return 0.5f * x * (1.f + tanhf(inner));
-}
-__device__ __forceinline__ float gelu_grad_f(float dy, float x) {
-  const float x_sq = x * x, x_cube = x_sq * x;
-  const float t = tanhf(kBeta * (x + kKappa * x_cube));
-  const float left = 0.5f * x, right = 1.f + t;
-  return dy * (0.5f * right + left * (1.f - t * t) * kBeta * (1.f + 3.f * kKappa * x_sq));
 }
 
 __device__ __forceinline__ void glds16(const void* src, unsigned char* lds_block) {

@@ -1,7 +1,7 @@
 // GPT-2 stage kernels outside the GEMMs/attention/LayerNorm (BASELINE config 5, bf16):
 //
-// * tanh-GELU forward and backward (the MLP activation, models/gpt2.py MLP): fp32 math on bf16 I/O,
-//   the same formulas as PyTorch's approximate="tanh" kernels, 8 elements (16 B) per lane.
+// * tanh-GELU forward and backward (the MLP activation, models/gpt2.py MLP; gelu.h): fp32 math on bf16 I/O,
+//   PyTorch's approximate="tanh" functions in sigmoid form (one __expf), 8 elements (16 B) per lane.
 // * token + position embedding: out[b][s] = wte[tok[b][s]] + wpe[s], one wave per token row.
 // * embedding backward, deterministic: wpe.grad[s] += sum_b g[b][s] in batch order; wte.grad[v] +=
 //   sum of g over the positions holding token v, in position order - the tokens arrive stably sorted
@@ -11,6 +11,7 @@
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 
+#include "gelu.h"
 #include "kernels.h"
 
 namespace sdml {
@@ -25,24 +26,6 @@ __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((unsigned
 __device__ __forceinline__ u16 f2bf(float f) {
   __hip_bfloat16 h = __float2bfloat16(f);  // RNE, NaN-preserving
   return *reinterpret_cast<u16*>(&h);
-}
-
-constexpr float kBeta = 0.7978845608028654f;  // sqrt(2 / pi)
-constexpr float kKappa = 0.044715f;
-
-__device__ __forceinline__ float gelu_f(float x) {
-  const float inner = kBeta * (x + kKappa * (x * x * x));
-  return 0.5f * x * (1.f + tanhf(inner));
-}
-
-__device__ __forceinline__ float gelu_grad_f(float dy, float x) {
-  const float x_sq = x * x, x_cube = x_sq * x;
-  const float inner = kBeta * (x + kKappa * x_cube);
-  const float t = tanhf(inner);
-  const float left = 0.5f * x, right = 1.f + t;
-  const float left_d = 0.5f * right;
-  const float right_d = left * (1.f - t * t) * kBeta * (1.f + 3.f * kKappa * x_sq);
-  return dy * (left_d + right_d);
 }
 
 __global__ void __launch_bounds__(256) gelu_fwd_kernel(const u16x8* __restrict__ x, u16x8* __restrict__ y,

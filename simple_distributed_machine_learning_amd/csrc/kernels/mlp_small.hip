@@ -57,9 +57,12 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// X8 is a template parameter: a runtime "uint8 or float" select inside the unrolled load batches makes
+// hipcc branch around every load and wait for each one (no loads in flight)
+template <bool X8>
 __device__ __forceinline__ float xval(const SmallArgs& a, int b, int k) {
-  if (a.x8) return static_cast<float>(static_cast<const unsigned char*>(a.x)[(size_t)b * SK + k]) * (1.f / 255.f);
-  return static_cast<const float*>(a.x)[(size_t)b * SK + k];
+  if constexpr (X8) return static_cast<float>(static_cast<const unsigned char*>(a.x)[(size_t)b * SK + k]) * (1.f / 255.f);
+  else return static_cast<const float*>(a.x)[(size_t)b * SK + k];
 }
 
 // torch.optim.SGD on one parameter, with sgd_rule.h's operation sequence (explicit fmas)
@@ -75,6 +78,7 @@ __device__ __forceinline__ void sgd1(float* p, float* buf, float d, const SmallA
   *p = __builtin_fmaf(-a.lr, d, pv);
 }
 
+template <bool X8>
 __global__ void __launch_bounds__(ST) mlp_small_fwd_kernel(SmallArgs a) {
   __shared__ float w1s[2][SK];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -91,7 +95,7 @@ __global__ void __launch_bounds__(ST) mlp_small_fwd_kernel(SmallArgs a) {
     // the row's 13 loads are issued together (fully unrolled, the partial 13th masked)
     float xv[13];
 #pragma unroll
-    for (int i = 0; i < 13; ++i) xv[i] = (lane + 64 * i < SK) ? xval(a, b, lane + 64 * i) : 0.f;
+    for (int i = 0; i < 13; ++i) xv[i] = (lane + 64 * i < SK) ? xval<X8>(a, b, lane + 64 * i) : 0.f;
     float s0 = 0.f, s1 = 0.f;
 #pragma unroll
     for (int i = 0; i < 13; ++i) {
@@ -108,6 +112,7 @@ __global__ void __launch_bounds__(ST) mlp_small_fwd_kernel(SmallArgs a) {
   }
 }
 
+template <bool X8>
 __global__ void __launch_bounds__(ST) mlp_small_bwd_kernel(SmallArgs a) {
   __shared__ float w2s[SC][SH];
   __shared__ float b2s[SC];
@@ -187,7 +192,7 @@ __global__ void __launch_bounds__(ST) mlp_small_bwd_kernel(SmallArgs a) {
     for (; b + 16 <= B; b += 16) {  // 16 loads in flight, then the fmas in row order
       float xv[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) xv[u] = xval(a, b + u, k);
+      for (int u = 0; u < 16; ++u) xv[u] = xval<X8>(a, b + u, k);
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         g0 = __builtin_fmaf(dzs[b + u][0], xv[u], g0);
@@ -195,7 +200,7 @@ __global__ void __launch_bounds__(ST) mlp_small_bwd_kernel(SmallArgs a) {
       }
     }
     for (; b < B; ++b) {
-      const float xv = xval(a, b, k);
+      const float xv = xval<X8>(a, b, k);
       g0 = __builtin_fmaf(dzs[b][0], xv, g0);
       g1 = __builtin_fmaf(dzs[b][1], xv, g1);
     }
@@ -253,8 +258,13 @@ bool mlp_small_step(const void* x, bool x_u8, const int64_t* target, int B, floa
   a.h = h_scratch;
   a.snap = snap_scratch;
   a.stats = stats;
-  hipLaunchKernelGGL(mlp_small_fwd_kernel, dim3(SG), dim3(ST), 0, stream, a);
-  hipLaunchKernelGGL(mlp_small_bwd_kernel, dim3(SG), dim3(ST), 0, stream, a);
+  if (x_u8) {
+    hipLaunchKernelGGL(mlp_small_fwd_kernel<true>, dim3(SG), dim3(ST), 0, stream, a);
+    hipLaunchKernelGGL(mlp_small_bwd_kernel<true>, dim3(SG), dim3(ST), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(mlp_small_fwd_kernel<false>, dim3(SG), dim3(ST), 0, stream, a);
+    hipLaunchKernelGGL(mlp_small_bwd_kernel<false>, dim3(SG), dim3(ST), 0, stream, a);
+  }
   return true;
 }
 

@@ -17,10 +17,13 @@ the bias gradient with a generic reduction. This module avoids both:
 When a parameter has no ``.grad`` yet (standalone use), the gradients are returned to
 autograd in the usual way. CPU tensors and non-bf16 dtypes keep the plain ``F.linear``
 path. The forward / input-gradient GEMMs of a plain Linear are library GEMMs (hipBLASLt, faster at these
-shapes than gemm_bf16.hip's current schedule: tools/bench_gemm_bf16.py); the MLP's c_fc forward and c_proj
-input gradient run on gemm_bf16.hip with the GELU fused into their epilogues (:func:`mlp_gelu`).
+shapes than gemm_bf16.hip's current schedule: tools/bench_gemm_bf16.py); with SDML_FUSED_GELU_GEMM=1 the MLP's
+c_fc forward and c_proj input gradient run on gemm_bf16.hip with the GELU fused into their epilogues
+(:func:`mlp_gelu`).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn as nn
@@ -105,9 +108,12 @@ class _MLPFn(torch.autograd.Function):
 
 
 def mlp_gelu(x, w1, b1, w2, b2):
-    """c_proj(gelu_tanh(c_fc(x))) with the fused-epilogue GEMMs on ROCm bf16 (else the composed ops)."""
+    """c_proj(gelu_tanh(c_fc(x))). SDML_FUSED_GELU_GEMM=1: the fused-epilogue GEMMs (gemm_bf16.hip) on ROCm
+    bf16; default: library GEMMs + the standalone GELU kernels (gpt2_ops.hip), measured faster on one MI355X
+    at 16 x 1024 tokens (fused c_fc 124.5 us vs 77 + GELU; fused c_proj dX 160 us vs 78 + GELU':
+    profiles/r3_gpt2_kernel_stats.txt), because the GEMM mainloop still trails hipBLASLt's."""
     if (x.is_cuda and x.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16 and b1 is not None
-            and b2 is not None):
+            and b2 is not None and os.environ.get("SDML_FUSED_GELU_GEMM", "0") == "1"):
         T, C = x.numel() // x.shape[-1], x.shape[-1]
         k = kernels()
         if (k.gemm_bf16_supported(T, w1.shape[0], C, C, C, False)

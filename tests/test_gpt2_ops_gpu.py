@@ -125,7 +125,7 @@ def test_gemm_bf16_gelu_epilogues_match_unfused():
 
 
 def test_mlp_gelu_fused_matches_composed():
-    """GPT-2's MLP with the GELU fused into the GEMM epilogues (ops.linear.mlp_gelu) against
+    """GPT-2's MLP with the GELU fused into the GEMM epilogues (ops.linear._MLPFn) against
     c_proj(gelu(c_fc(x))) composed from separate kernels: forward and every gradient."""
     from simple_distributed_machine_learning_amd.ops.linear import _MLPFn, linear
 

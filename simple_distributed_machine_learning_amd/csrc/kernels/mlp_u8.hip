@@ -557,6 +557,26 @@ __device__ __forceinline__ f16x8 frag_tr(const u16* img, int c0, int s, int lane
   return __builtin_bit_cast(f16x8, f);
 }
 
+// dz plane images: the 8-byte granule g (4 hidden units) of k-row r is stored at g ^ dz_swz(r). The
+// factored staging writes one 16-row x 4-column block per 16 lanes (the fd_dz MFMA layout); on the
+// 48-dword pitch those rows repeat every 4 rows in the banks (4-way conflicts, SQ_LDS_BANK_CONFLICT
+// 7.1e6 for this kernel). The XOR by (r >> 2) & 3 (doubled) spreads them; the transposed reads keep
+// whole 4-row blocks under one XOR value, so they stay conflict-free.
+__device__ __forceinline__ int dz_swz(int r) { return ((r >> 2) & 3) << 1; }
+
+template <int PITCH>
+__device__ __forceinline__ f16x8 frag_tr_dz(const u16* img, int c0, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int r = 16 * s + 8 * (g >> 1) + (i >> 2);  // the 4 rows of one transposed read share dz_swz
+  const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
+  const s16x4 lo = tr16(img + r * PITCH + (((col >> 2) ^ dz_swz(r)) << 2));
+  const s16x4 hi = tr16(img + (r + 4) * PITCH + (((col >> 2) ^ dz_swz(r + 4)) << 2));
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return __builtin_bit_cast(f16x8, f);
+}
+
 // exponent E with |v| < 2^E for a finite v >= 0 (v = m 2^E, m in [0.5, 1)), clamped so 2^(14 - E)
 // and 2^(E - 14) stay normal floats
 __device__ __forceinline__ int bound_exp(float v) {
@@ -733,7 +753,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
       hi[e] = __builtin_bit_cast(u16, h);
       lo[e] = __builtin_bit_cast(u16, static_cast<_Float16>(x - static_cast<float>(h)));
     }
-    const int doff = GX_U16 + drow * GDP + dcol;
+    const int doff = GX_U16 + drow * GDP + (((dcol >> 2) ^ dz_swz(drow)) << 2);
     *reinterpret_cast<u16x4*>(B + doff) = hi;
     *reinterpret_cast<u16x4*>(B + doff + GD_U16) = lo;
 #pragma unroll
@@ -763,7 +783,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int pl = 0; pl < GNPL; ++pl) a[i][pl] = frag_tr<GDP>(B + GX_U16 + pl * GD_U16, 32 * i, s, lane);
+          for (int pl = 0; pl < GNPL; ++pl) a[i][pl] = frag_tr_dz<GDP>(B + GX_U16 + pl * GD_U16, 32 * i, s, lane);
 #pragma unroll
         for (int j = 0; j < NCT; ++j) {
           const f16x8 b = frag_tr<GXP>(B, 32 * (ct0 + j), s, lane);

@@ -280,14 +280,20 @@ size_t bn_nhwc_workspace_floats(int M, int C) {
 
 void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const void* beta, void* rmean, void* rvar,
                       int M, int C, float eps, float momentum, bool relu, void* y, float* mean, float* rstd,
-                      float* workspace, hipStream_t stream, int64_t* num_batches_tracked) {
+                      float* workspace, hipStream_t stream, int64_t* num_batches_tracked, const float* part_in,
+                      int part_rows) {
   int rpb;
-  const int nblk = bn_blocks(M, C, &rpb);
-  float* part = workspace;
+  int nblk = bn_blocks(M, C, &rpb);
+  const float* part = workspace;
   float* scale = workspace + (size_t)nblk * 2 * C;
   float* shift = scale + C;
-  hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(nblk), dim3(BT), 0, stream, static_cast<const u16*>(x), nullptr,
-                     nullptr, nullptr, nullptr, nullptr, nullptr, M, C, rpb, 0, part);
+  if (part_in) {  // the producing convolution's epilogue already summed y per tile (conv_bf16.hip)
+    part = part_in;
+    nblk = part_rows;
+  } else {
+    hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(nblk), dim3(BT), 0, stream, static_cast<const u16*>(x), nullptr,
+                       nullptr, nullptr, nullptr, nullptr, nullptr, M, C, rpb, 0, workspace);
+  }
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + BT / 64 - 1) / (BT / 64)), dim3(BT), 0, stream, part, nblk, C, M, eps,
                      momentum, static_cast<const u16*>(gamma), static_cast<const u16*>(beta), static_cast<u16*>(rmean),
                      static_cast<u16*>(rvar), mean, rstd, scale, shift, num_batches_tracked);

@@ -56,9 +56,104 @@ struct ConvArgs {
   int M;         // Nb*OH*OW
   int tiles_m, tiles_n;
   int OH, OW, S, KS, P;  // output size, stride, kernel size (3 or 1), padding (the halo kernel: 1 / 3 / 1)
+  const u16* add;  // optional addend in y's layout: y = bf16(acc + add) (the residual branch's input gradient)
+  float* part;     // optional BatchNorm partials [tiles_m][2][Co]: per-tile sums of y and y^2 (bf16-rounded y)
 };
 
-template <int BN>
+// Output tile store shared by the im2col, halo and strided-dgrad kernels. The MFMA accumulators
+// (C/D map: col = lane&31, row = (r&3) + 8(r>>2) + 4h) are rounded to bf16 into an LDS image
+// [BM][BN + 8] (padded rows), then written out as 16-B row chunks: a thread owns one 8-channel chunk of
+// BM / (NT / (BN / 8)) rows, so every global access is a full 16-B vector and the output row's address
+// (rowoff: element offset of channel n0 of tile row r in y, < 0 = no such row) is decoded once per row,
+// not once per element. EPI = 1 adds the optional addend (same layout as y; y = bf16(bf16(acc) + add),
+// the rounding of the separate add it replaces) and the optional BatchNorm partials of the stored y:
+// per channel, sums of y and y^2 over the tile's rows in a fixed order (the thread's rows, then the
+// row groups through LDS), written to part_row[0][0..BN) and part_row[0][Co..Co+BN) - the forward
+// BatchNorm (batchnorm_nhwc.hip) then finalizes these rows instead of re-reading y.
+// LDS: max(BM * (BN + 8) * 2, 32 KB) bytes; the caller's main loop has finished with its images.
+constexpr int store_tile_lds(int BN) { return BM * (BN + 8) * 2 > 32768 ? BM * (BN + 8) * 2 : 32768; }
+
+template <int TM, int WTM, int WGM, int BN, int EPI, class RowOff>
+__device__ __forceinline__ void store_tile(const f32x16 (&acc)[TM][2], int wm, int wn, int lane, u16* lds,
+                                           RowOff rowoff, u16* __restrict__ y, const u16* __restrict__ add,
+                                           float* __restrict__ part_row, int Co) {
+  constexpr int LP = BN + 8;
+  const int h = lane >> 5;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = wn * 64 + 32 * j + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * WTM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        lds[row * LP + col] = f2bf(acc[i][j][r]);
+      }
+    }
+  __syncthreads();
+  constexpr int CPR = BN / 8;    // 16-B chunks per row
+  constexpr int RPP = NT / CPR;  // rows per pass
+  const int t = threadIdx.x, c = t % CPR, r0 = t / CPR;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+#pragma unroll
+  for (int k = 0; k < BM / RPP; ++k) {
+    const int rr = r0 + k * RPP;
+    const long long off = rowoff(rr);
+    if (off < 0) continue;
+    u16x8 v = *reinterpret_cast<const u16x8*>(lds + rr * LP + 8 * c);
+    if constexpr (EPI == 1) {
+      if (add) {
+        const u16x8 av = *reinterpret_cast<const u16x8*>(add + off + 8 * c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(av[e]));
+      }
+      if (part_row) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = bf2f(v[e]);
+          s1[e] += f;
+          s2[e] = __builtin_fmaf(f, f, s2[e]);
+        }
+      }
+    }
+    *reinterpret_cast<u16x8*>(y + off + 8 * c) = v;
+  }
+  if constexpr (EPI == 1) {
+    if (!part_row) return;
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);  // [RPP][2][BN]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(r0 * 2 + 0) * BN + 8 * c + e] = s1[e];
+      red[(r0 * 2 + 1) * BN + 8 * c + e] = s2[e];
+    }
+    __syncthreads();
+    // QN adjacent lanes per output, each summing RPP / QN row groups in order, then a fixed xor tree
+    constexpr int QN = NT / (2 * BN), PER = RPP / QN;
+    const int o = t / QN, q = t % QN, k = o / BN, cc = o % BN;
+    float v = 0.f;
+#pragma unroll
+    for (int g = q * PER; g < (q + 1) * PER; ++g) v += red[(g * 2 + k) * BN + cc];
+#pragma unroll
+    for (int m = 1; m < QN; m <<= 1) v += __shfl_xor(v, m);
+    if (q == 0) part_row[(size_t)k * Co + cc] = v;
+  }
+}
+
+// the im2col / halo kernels' output: tile row r = pixel m0 + r of y [M][Co]
+template <int TM, int WTM, int WGM, int BN, int EPI>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x16 (&acc)[TM][2], int tm, int m0, int n0,
+                                              int wm, int wn, int lane, u16* lds) {
+  const int M = a.M, Co = a.Co;
+  auto rowoff = [=](int r) -> long long { return m0 + r < M ? (long long)(m0 + r) * Co + n0 : -1; };
+  store_tile<TM, WTM, WGM, BN, EPI>(acc, wm, wn, lane, lds, rowoff, a.y, a.add,
+                                    a.part ? a.part + (size_t)tm * 2 * Co + n0 : nullptr, Co);
+}
+
+template <int BN, int EPI>  // EPI: 0 plain store, 1 addend and/or BatchNorm partials (conv_epilogue)
 __global__ void __launch_bounds__(NT) conv3x3_fwd_kernel(ConvArgs a) {
   constexpr int WGN = BN / 64;           // 2 (BN 128) or 1 (BN 64)
   constexpr int WGM = 8 / WGN;           // 4 or 8
@@ -158,18 +253,196 @@ __global__ void __launch_bounds__(NT) conv3x3_fwd_kernel(ConvArgs a) {
     }
     __syncthreads();
   }
-  // epilogue: C/D map col = lane&31 (cout), row = (r&3) + 8(r>>2) + 4h (pixel)
+  conv_epilogue<TM, WTM, WGM, BN, EPI>(a, acc, tm, m0, n0, wm, wn, lane, smem);
+}
+
+// ---- input gradient of a stride-2 convolution (3x3 pad 1 / 1x1 pad 0): parity-class GEMMs ------
+// dx[n][iy][ix][ci] = sum over (ky, kx, co) with iy + P - ky = 2 oy, ix + P - kx = 2 ox of
+// dy[n][oy][ox][co] * w[co][ci][ky][kx]. Which taps reach an input pixel depends only on the parity
+// (py, px) of (iy, ix): ky = ky0 + 2j with ky0 = (py + P) & 1 (3x3 pad 1: one tap for even rows, two
+// for odd ones; 1x1 pad 0: one for even rows, none for odd ones). Each of the four parity classes is
+// a dense implicit GEMM - M = its pixels, N = Cin, K = its taps x Cout, A gathered from dy (a K-step
+// of 64 lies inside one tap), B = the class's weights packed [Cin][taps][Cout] - so no MAC is spent
+// on the zeros of the transposed convolution, and one launch covers all four classes (class-major
+// tile order, most taps first; a class without taps writes its zeros through the same epilogue).
+struct DgArgs {
+  const u16* dy;  // [Nb][OH][OW][Cg] (the convolution's output gradient, NHWC)
+  const u16* w;   // the classes' packed weights, class-major in dg_order, each [Cn][taps][Cg]
+  u16* dx;        // [Nb][H][W][Cn]
+  const u16* add;  // optional addend in dx's layout (dx = bf16(acc + add))
+  int Nb, H, W, OH, OW, Cg, Cn, KS, P, tiles_n, tiles;
+};
+
+struct DgClass {
+  int py, px, ky0, kx0, nkx, taps, Ha, Wb, M, tiles_m, woff, tile0;
+};
+
+// class processed j-th: most taps first (3x3: (1,1) 4, (0,1) 2, (1,0) 2, (0,0) 1; 1x1: (0,0) only)
+__host__ __device__ inline int dg_order(int j, int KS) { return KS == 3 ? (j == 0 ? 3 : j == 3 ? 0 : j) : j; }
+
+__host__ __device__ inline DgClass dg_class(int j, int Nb, int H, int W, int KS, int P, int Cg, int Cn, int tiles_n) {
+  DgClass c{};
+  int woff = 0, tile0 = 0;
+  for (int i = 0; i <= j; ++i) {
+    const int cls = dg_order(i, KS);
+    c.py = cls >> 1;
+    c.px = cls & 1;
+    c.ky0 = (c.py + P) & 1;
+    c.kx0 = (c.px + P) & 1;
+    const int nky = (KS - c.ky0 + 1) / 2;
+    c.nkx = (KS - c.kx0 + 1) / 2;
+    c.taps = nky * c.nkx;
+    c.Ha = (H - c.py + 1) / 2;
+    c.Wb = (W - c.px + 1) / 2;
+    c.M = Nb * c.Ha * c.Wb;
+    c.tiles_m = (c.M + BM - 1) / BM;
+    c.woff = woff;
+    c.tile0 = tile0;
+    woff += c.taps * Cn * Cg;
+    tile0 += c.tiles_m * tiles_n;
+  }
+  return c;
+}
+
+template <int BN>
+__global__ void __launch_bounds__(NT) conv_dgrad_s2_kernel(DgArgs a) {
+  constexpr int WGN = BN / 64;
+  constexpr int WGM = 8 / WGN;
+  constexpr int WTM = BM / WGM;
+  constexpr int TM = WTM / 32;
+  constexpr int AI = BM * BK, BI = BN * BK;
+  constexpr int NB = BN * 8 / NT;
+  __shared__ __attribute__((aligned(16))) u16 smem[2 * (AI + BI)];
+  const int orig = blockIdx.x;
+  int wg = orig;
+  if (a.tiles >= 16) {  // XCD-aware bijective remap
+    const int q = a.tiles / 8, r = a.tiles % 8, xcd = orig % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  }
+  int j = 0;
+  DgClass c = dg_class(0, a.Nb, a.H, a.W, a.KS, a.P, a.Cg, a.Cn, a.tiles_n);
+  for (int jj = 1; jj < 4; ++jj) {
+    const DgClass d = dg_class(jj, a.Nb, a.H, a.W, a.KS, a.P, a.Cg, a.Cn, a.tiles_n);
+    if (wg >= d.tile0 && d.tiles_m > 0) {
+      c = d;
+      j = jj;
+    }
+  }
+  (void)j;
+  const int local = wg - c.tile0;
+  const int tn = local % a.tiles_n, tm = local / a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int K = c.taps * a.Cg;
+  const u16* __restrict__ wc = a.w + c.woff;
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % WGM, wn = wave / WGM;
+  const int t = threadIdx.x, ch = t & 7;
+
+  int pn[4], py[4], px[4];  // this thread's 4 A rows: image, input row / column of the class pixel
+  bool pv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int p = m0 + (t >> 3) + 64 * u;
+    pv[u] = p < c.M;
+    const int pp = pv[u] ? p : 0;
+    px[u] = 2 * (pp % c.Wb) + c.px;
+    const int q = pp / c.Wb;
+    py[u] = 2 * (q % c.Ha) + c.py;
+    pn[u] = q / c.Ha;
+  }
+  u16x8 va[4], vb[NB];
+  bool ok[4];
+  auto load = [&](int k0) {
+    const int kk = min(k0, K - BK);
+    const int tt = kk / a.Cg, co0 = kk % a.Cg;
+    const int ky = c.ky0 + 2 * (tt / c.nkx), kx = c.kx0 + 2 * (tt % c.nkx);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int dh = py[u] + a.P - ky, dw = px[u] + a.P - kx;  // even by the class
+      const int oy = dh >> 1, ox = dw >> 1;
+      ok[u] = pv[u] && k0 < K && dh >= 0 && oy < a.OH && dw >= 0 && ox < a.OW;
+      const size_t off = ok[u] ? (((size_t)pn[u] * a.OH + oy) * a.OW + ox) * a.Cg + co0 + 8 * ch : 0;
+      va[u] = *reinterpret_cast<const u16x8*>(a.dy + off);
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int n = n0 + (t >> 3) + 64 * u;
+      vb[u] = *reinterpret_cast<const u16x8*>(wc + (size_t)n * K + kk + 8 * ch);
+    }
+  };
+  auto store = [&](u16* L) {
+    const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) *reinterpret_cast<u16x8*>(L + swz((t >> 3) + 64 * u, ch)) = ok[u] ? va[u] : z;
+#pragma unroll
+    for (int u = 0; u < NB; ++u) *reinterpret_cast<u16x8*>(L + AI + swz((t >> 3) + 64 * u, ch)) = vb[u];
+  };
+
+  f32x16 acc[TM][2];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int co = n0 + wn * 64 + 32 * j + (lane & 31);
+    for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int p = m0 + wm * WTM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (p < a.M) a.y[(size_t)p * a.Co + co] = f2bf(acc[i][j][r]);
+      for (int r = 0; r < 16; ++r) acc[i][jn][r] = 0.f;
+
+  const int nk = K / BK;
+  if (nk > 0) {
+    load(0);
+    store(smem);
+    load(BK);
+    __syncthreads();
+    for (int it = 0; it < nk; ++it) {
+      const u16* L = smem + (it & 1) * (AI + BI);
+      u16* Ln = smem + ((it + 1) & 1) * (AI + BI);
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        bf16x8 af[TM], bf[2];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = rowf(L, wm * WTM + 32 * i + (lane & 31), s, h);
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn) bf[jn] = rowf(L + AI, wn * 64 + 32 * jn + (lane & 31), s, h);
+        if (s == 0) {
+          store(Ln);
+          load((it + 2) * BK);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int jn = 0; jn < 2; ++jn) acc[i][jn] = mfma(af[i], bf[jn], acc[i][jn]);
       }
+      __syncthreads();
     }
+  }
+  const int H = a.H, W = a.W, Cn = a.Cn, Ha = c.Ha, Wb = c.Wb, cpy = c.py, cpx = c.px, Mc = c.M;
+  auto rowoff = [=](int r) -> long long {  // class pixel m0 + r -> dx element offset of channel n0
+    const int p = m0 + r;
+    if (p >= Mc) return -1;
+    const int ix = 2 * (p % Wb) + cpx, q = p / Wb;
+    const int iy = 2 * (q % Ha) + cpy, n = q / Ha;
+    return (((long long)n * H + iy) * W + ix) * Cn + n0;
+  };
+  store_tile<TM, WTM, WGM, BN, 1>(acc, wm, wn, lane, smem, rowoff, a.dx, a.add, nullptr, Cn);
+}
+
+// torch weight [Cg][Cn][KS][KS] -> the parity classes' packed [Cn][taps][Cg] images (dg_class)
+__global__ void __launch_bounds__(256) conv_dgrad_s2_weight_kernel(const u16* __restrict__ w, u16* __restrict__ out,
+                                                                   int Cg, int Cn, int KS, int P) {
+  const int64_t n = (int64_t)Cg * Cn * KS * KS;
+  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    DgClass c = dg_class(0, 1, 2, 2, KS, P, Cg, Cn, 1);
+    for (int j = 1; j < 4; ++j) {
+      const DgClass d = dg_class(j, 1, 2, 2, KS, P, Cg, Cn, 1);
+      if (e >= d.woff && d.taps > 0) c = d;
+    }
+    const int64_t r = e - c.woff;  // [ci][t][co]
+    const int co = (int)(r % Cg);
+    const int64_t q = r / Cg;
+    const int tt = (int)(q % c.taps), ci = (int)(q / c.taps);
+    const int ky = c.ky0 + 2 * (tt / c.nkx), kx = c.kx0 + 2 * (tt % c.nkx);
+    out[e] = w[(((int64_t)co * Cn + ci) * KS + ky) * KS + kx];
+  }
 }
 
 // ---- forward / dgrad, halo-staged ("direct") variant ------------------------------------------
@@ -187,7 +460,7 @@ constexpr int HALO_MAX_W = 95;
 constexpr int halo_hl(int W) { return (BM + 2 * W + 2) * 8 <= 5 * NT ? 5 : 7; }
 constexpr int halo_occ(int BN, int HL) { return BN == 64 && HL == 5 ? 4 : 2; }
 
-template <int BN, int HL>
+template <int BN, int HL, int EPI>
 __global__ void __launch_bounds__(NT, halo_occ(BN, HL)) conv3x3_halo_kernel(ConvArgs a) {
   constexpr int WGN = BN / 64;
   constexpr int WGM = 8 / WGN;
@@ -323,17 +596,7 @@ __global__ void __launch_bounds__(NT, halo_occ(BN, HL)) conv3x3_halo_kernel(Conv
     step(std::integral_constant<int, 1>(), st + 1);
   }
   if (st < NS) step(std::integral_constant<int, 0>(), st);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int co = n0 + wn * 64 + 32 * j + (lane & 31);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int p = m0 + wm * WTM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (p < a.M) a.y[(size_t)p * a.Co + co] = f2bf(acc[i][j][r]);
-      }
-    }
+  conv_epilogue<TM, WTM, WGM, BN, EPI>(a, acc, tm, m0, n0, wm, wn, lane, dsm);
 }
 
 // ---- weight gradient: dw[co][tap][ci] (fp32 slabs) = sum_p dy[p][co] x[p + off(tap)][ci] ---------
@@ -671,9 +934,23 @@ void conv3x3_weight_transform_bf16(const void* w_torch, void* fwd, void* dgrad, 
                      static_cast<const u16*>(w_torch), static_cast<u16*>(fwd), static_cast<u16*>(dgrad), Co, C);
 }
 
+int conv_part_rows(int Nb, int OH, int OW) { return (Nb * OH * OW + BM - 1) / BM; }
+
+static void launch_im2col(ConvArgs& a, bool bn128, hipStream_t stream) {
+  a.tiles_n = a.Co / (bn128 ? 128 : 64);
+  const dim3 grid(a.tiles_m * a.tiles_n), block(NT);
+  const bool epi = a.add || a.part;
+  if (bn128 && epi) hipLaunchKernelGGL((conv3x3_fwd_kernel<128, 1>), grid, block, 0, stream, a);
+  else if (bn128) hipLaunchKernelGGL((conv3x3_fwd_kernel<128, 0>), grid, block, 0, stream, a);
+  else if (epi) hipLaunchKernelGGL((conv3x3_fwd_kernel<64, 1>), grid, block, 0, stream, a);
+  else hipLaunchKernelGGL((conv3x3_fwd_kernel<64, 0>), grid, block, 0, stream, a);
+}
+
 void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co,
-                      hipStream_t stream) {
+                      hipStream_t stream, const void* add, float* part) {
   ConvArgs a;
+  a.add = static_cast<const u16*>(add);
+  a.part = part;
   a.x = static_cast<const u16*>(x);
   a.w = static_cast<const u16*>(wt);
   a.y = static_cast<u16*>(y);
@@ -701,31 +978,35 @@ void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int
     const bool big = Co % 128 == 0 && a.tiles_m * (Co / 128) >= bn128_min;
     const int bn = big ? 128 : 64;
     a.tiles_n = Co / bn;
-    const size_t lds = (size_t)((C > 64 ? 2 : 1) * (BM + 2 * W + 2) * 64 + 2 * bn * BK) * sizeof(u16);
+    const size_t lds = std::max<size_t>((size_t)((C > 64 ? 2 : 1) * (BM + 2 * W + 2) * 64 + 2 * bn * BK) * sizeof(u16),
+                                        (size_t)store_tile_lds(bn));
     static bool attr = [] {
-      for (const void* f : {reinterpret_cast<const void*>(conv3x3_halo_kernel<128, 5>),
-                             reinterpret_cast<const void*>(conv3x3_halo_kernel<128, 7>),
-                             reinterpret_cast<const void*>(conv3x3_halo_kernel<64, 5>),
-                             reinterpret_cast<const void*>(conv3x3_halo_kernel<64, 7>)})
-        hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      for (const void* f : {reinterpret_cast<const void*>(conv3x3_halo_kernel<128, 5, 0>),
+                             reinterpret_cast<const void*>(conv3x3_halo_kernel<128, 7, 0>),
+                             reinterpret_cast<const void*>(conv3x3_halo_kernel<64, 5, 0>),
+                             reinterpret_cast<const void*>(conv3x3_halo_kernel<64, 7, 0>),
+                             reinterpret_cast<const void*>(conv3x3_halo_kernel<128, 5, 1>),
+                             reinterpret_cast<const void*>(conv3x3_halo_kernel<128, 7, 1>),
+                             reinterpret_cast<const void*>(conv3x3_halo_kernel<64, 5, 1>),
+                             reinterpret_cast<const void*>(conv3x3_halo_kernel<64, 7, 1>)})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       return true;
     }();
     (void)attr;
     const dim3 grid(a.tiles_m * a.tiles_n), block(NT);
     const bool h5 = halo_hl(W) == 5;
-    if (big && h5) hipLaunchKernelGGL((conv3x3_halo_kernel<128, 5>), grid, block, lds, stream, a);
-    else if (big) hipLaunchKernelGGL((conv3x3_halo_kernel<128, 7>), grid, block, lds, stream, a);
-    else if (h5) hipLaunchKernelGGL((conv3x3_halo_kernel<64, 5>), grid, block, lds, stream, a);
-    else hipLaunchKernelGGL((conv3x3_halo_kernel<64, 7>), grid, block, lds, stream, a);
+    auto go = [&](auto epi) {
+      constexpr int E = decltype(epi)::value;
+      if (big && h5) hipLaunchKernelGGL((conv3x3_halo_kernel<128, 5, E>), grid, block, lds, stream, a);
+      else if (big) hipLaunchKernelGGL((conv3x3_halo_kernel<128, 7, E>), grid, block, lds, stream, a);
+      else if (h5) hipLaunchKernelGGL((conv3x3_halo_kernel<64, 5, E>), grid, block, lds, stream, a);
+      else hipLaunchKernelGGL((conv3x3_halo_kernel<64, 7, E>), grid, block, lds, stream, a);
+    };
+    if (a.add || a.part) go(std::integral_constant<int, 1>());
+    else go(std::integral_constant<int, 0>());
     return;
   }
-  if (Co % 128 == 0) {
-    a.tiles_n = Co / 128;
-    hipLaunchKernelGGL(conv3x3_fwd_kernel<128>, dim3(a.tiles_m * a.tiles_n), dim3(NT), 0, stream, a);
-  } else {
-    a.tiles_n = Co / 64;
-    hipLaunchKernelGGL(conv3x3_fwd_kernel<64>, dim3(a.tiles_m * a.tiles_n), dim3(NT), 0, stream, a);
-  }
+  launch_im2col(a, Co % 128 == 0, stream);
 }
 
 int conv_out_size(int in, int ks, int stride, int pad) { return (in + 2 * pad - ks) / stride + 1; }
@@ -736,8 +1017,10 @@ bool conv_general_supported(int C, int Co, int ks, int stride, int pad) {
 }
 
 void conv_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co, int ks, int stride,
-                   int pad, hipStream_t stream) {
+                   int pad, hipStream_t stream, const void* add, float* part) {
   ConvArgs a;
+  a.add = static_cast<const u16*>(add);
+  a.part = part;
   a.x = static_cast<const u16*>(x);
   a.w = static_cast<const u16*>(wt);
   a.y = static_cast<u16*>(y);
@@ -753,13 +1036,46 @@ void conv_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W,
   a.P = pad;
   a.M = Nb * a.OH * a.OW;
   a.tiles_m = (a.M + BM - 1) / BM;
-  if (Co % 128 == 0 && a.tiles_m * (Co / 128) >= 160) {
-    a.tiles_n = Co / 128;
-    hipLaunchKernelGGL(conv3x3_fwd_kernel<128>, dim3(a.tiles_m * a.tiles_n), dim3(NT), 0, stream, a);
-  } else {
-    a.tiles_n = Co / 64;
-    hipLaunchKernelGGL(conv3x3_fwd_kernel<64>, dim3(a.tiles_m * a.tiles_n), dim3(NT), 0, stream, a);
+  launch_im2col(a, Co % 128 == 0 && a.tiles_m * (Co / 128) >= 160, stream);
+}
+
+size_t conv_dgrad_s2_weight_elems(int Co, int C, int ks) { return (size_t)Co * C * ks * ks; }
+
+void conv_dgrad_s2_weight_bf16(const void* w_torch, void* packed, int Co, int C, int ks, int pad, hipStream_t stream) {
+  const int64_t n = (int64_t)Co * C * ks * ks;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(conv_dgrad_s2_weight_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<const u16*>(w_torch),
+                     static_cast<u16*>(packed), Co, C, ks, pad);
+}
+
+void conv_dgrad_s2_bf16(const void* dy, const void* packed, void* dx, int Nb, int H, int W, int C, int Co, int ks,
+                        int pad, hipStream_t stream, const void* add) {
+  DgArgs a;
+  a.add = static_cast<const u16*>(add);
+  a.dy = static_cast<const u16*>(dy);
+  a.w = static_cast<const u16*>(packed);
+  a.dx = static_cast<u16*>(dx);
+  a.Nb = Nb;
+  a.H = H;
+  a.W = W;
+  a.OH = conv_out_size(H, ks, 2, pad);
+  a.OW = conv_out_size(W, ks, 2, pad);
+  a.Cg = Co;
+  a.Cn = C;
+  a.KS = ks;
+  a.P = pad;
+  // BN 128 when that still gives >= 160 workgroups, else BN 64 (more workgroups)
+  int bn = 64;
+  if (C % 128 == 0) {
+    const DgClass last = dg_class(3, Nb, H, W, ks, pad, Co, C, C / 128);
+    if (last.tile0 + last.tiles_m * (C / 128) >= 160) bn = 128;
   }
+  a.tiles_n = C / bn;
+  const DgClass last = dg_class(3, Nb, H, W, ks, pad, Co, C, a.tiles_n);
+  a.tiles = last.tile0 + last.tiles_m * a.tiles_n;
+  if (a.tiles <= 0) return;
+  if (bn == 128) hipLaunchKernelGGL(conv_dgrad_s2_kernel<128>, dim3(a.tiles), dim3(NT), 0, stream, a);
+  else hipLaunchKernelGGL(conv_dgrad_s2_kernel<64>, dim3(a.tiles), dim3(NT), 0, stream, a);
 }
 
 static int wgrad_rows(int Co) {

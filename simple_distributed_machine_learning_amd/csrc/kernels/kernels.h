@@ -286,16 +286,26 @@ void wgrad_bf16(const void* gy, const void* x, void* gw, void* gb, float* worksp
 bool conv3x3_bf16_supported(int C, int Co);
 // torch [Co][C][3][3] weight -> forward layout [Co][9][C] and/or dgrad layout [C][9][Co] (flipped taps); either may be null
 void conv3x3_weight_transform_bf16(const void* w_torch, void* fwd, void* dgrad, int Co, int C, hipStream_t stream);
-void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co, hipStream_t stream);
+// add (optional, y's layout): y = bf16(conv + add). part (optional): BatchNorm partials of y,
+// [conv_part_rows(Nb, OH, OW)][2][Co] fp32 (per 256-pixel tile: sum y, sum y^2), for bn_nhwc_fwd_bf16.
+int conv_part_rows(int Nb, int OH, int OW);
+void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co, hipStream_t stream,
+                      const void* add = nullptr, float* part = nullptr);
 // gw_torch [Co][C][3][3] bf16 += dw; workspace: conv3x3_wgrad_workspace_floats(...) fp32
 // general bf16 NHWC convolution on the implicit-GEMM kernels: kernel 3 (pad 1) or 1 (pad 0), stride 1
 // or 2, C and Co multiples of 64. Forward (im2col kernel; wt = [Co][ks*ks][C]) and weight gradient
-// (accumulated into the bf16 torch-layout [Co][C][ks][ks] gradient); the input gradient of strided
-// convolutions stays with MIOpen.
+// (accumulated into the bf16 torch-layout [Co][C][ks][ks] gradient). The input gradient of a stride-2
+// one: four parity-class GEMMs in one launch (conv_dgrad_s2_bf16) on the packed weights of
+// conv_dgrad_s2_weight_bf16 (conv_dgrad_s2_weight_elems bf16 elements); dx [Nb][H][W][C] NHWC is
+// written in full.
 int conv_out_size(int in, int ks, int stride, int pad);
 bool conv_general_supported(int C, int Co, int ks, int stride, int pad);
 void conv_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co, int ks, int stride,
-                   int pad, hipStream_t stream);
+                   int pad, hipStream_t stream, const void* add = nullptr, float* part = nullptr);
+size_t conv_dgrad_s2_weight_elems(int Co, int C, int ks);
+void conv_dgrad_s2_weight_bf16(const void* w_torch, void* packed, int Co, int C, int ks, int pad, hipStream_t stream);
+void conv_dgrad_s2_bf16(const void* dy, const void* packed, void* dx, int Nb, int H, int W, int C, int Co, int ks,
+                        int pad, hipStream_t stream, const void* add = nullptr);
 size_t conv_wgrad_workspace_floats(int Nb, int H, int W, int C, int Co, int ks, int stride, int pad);
 void conv_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* workspace, int Nb, int H, int W, int C,
                      int Co, int ks, int stride, int pad, hipStream_t stream);
@@ -318,7 +328,8 @@ bool bn_nhwc_supported(int C);
 size_t bn_nhwc_workspace_floats(int M, int C);
 void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const void* beta, void* rmean, void* rvar,
                       int M, int C, float eps, float momentum, bool relu, void* y, float* mean, float* rstd,
-                      float* workspace, hipStream_t stream, int64_t* num_batches_tracked = nullptr);
+                      float* workspace, hipStream_t stream, int64_t* num_batches_tracked = nullptr,
+                      const float* part = nullptr, int part_rows = 0);
 // backward: g = dy * (y > 0 if relu); dx, dres = g (optional), ggamma/gbeta (bf16, accumulated; optional)
 void bn_nhwc_bwd_bf16(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
                       const void* gamma, int M, int C, bool relu, void* dx, void* dres, void* ggamma, void* gbeta,

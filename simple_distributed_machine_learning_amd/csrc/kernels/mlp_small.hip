@@ -5,7 +5,8 @@
 // of work and the multi-kernel step (6 launches + the host work between them) is launch-bound:
 //
 //   kernel A (block g owns hidden units 2g, 2g+1; 64 blocks): h[:, own] = relu(x W1[own]^T + b1[own])
-//   kernel B (every block, redundantly): logits of all rows from the full h, log_softmax, NLL,
+//   kernel B (every block, redundantly): logits of all rows from the full h (one thread per (row, class)
+//            dot product), log_softmax, NLL,
 //            dl = scale (softmax - onehot) (identical bits in every block: same operations, same order)
 //            own part: dz = (dl W2[:, own]) * (h > 0); gW1[own] = dz^T x; gb1[own]; gW2[:, own]; block 0:
 //            gb2, loss, correct; then torch.optim.SGD's update of exactly the parameters the block owns
@@ -114,29 +115,35 @@ __global__ void __launch_bounds__(ST) mlp_small_fwd_kernel(SmallArgs a) {
 
 template <bool X8>
 __global__ void __launch_bounds__(ST) mlp_small_bwd_kernel(SmallArgs a) {
-  __shared__ float w2s[SC][SH];
+  __shared__ float w2s[SC][SH + 1];  // padded: the (row, class) threads of a wave read 10 rows of it at once
   __shared__ float b2s[SC];
   __shared__ float hs[SMAXB][SH + 1];
   __shared__ float dls[SMAXB][SC];
   __shared__ float dzs[SMAXB][2];
-  __shared__ float red[ST / 64][2];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  __shared__ float zs[SMAXB][SC];
+  __shared__ float rowl[SMAXB][2];
+  const int t = threadIdx.x;
   const int j0 = 2 * blockIdx.x;
   const int B = a.B;
   for (int i = t; i < SC * SH; i += ST) w2s[i / SH][i % SH] = a.snap[i];
   if (t < SC) b2s[t] = a.snap[SC * SH + t];
   for (int i = t; i < B * SH; i += ST) hs[i / SH][i % SH] = a.h[i];
   __syncthreads();
-  float lsum = 0.f, csum = 0.f;
-  for (int b = wave; b < B; b += ST / 64) {
+  // logits: one (row, class) dot product of length 128 per thread (no cross-lane reductions on the
+  // critical path), then one thread per row: log_softmax, NLL, argmax, dl
+  for (int i = t; i < B * SC; i += ST) {
+    const int b = i / SC, c = i % SC;
+    float p = b2s[c];
+#pragma unroll 16
+    for (int k = 0; k < SH; ++k) p = __builtin_fmaf(hs[b][k], w2s[c][k], p);
+    zs[b][c] = p;
+  }
+  __syncthreads();
+  if (t < B) {
+    const int b = t;
     float z[SC];
 #pragma unroll
-    for (int c = 0; c < SC; ++c) {
-      float p = 0.f;
-      p = __builtin_fmaf(hs[b][2 * lane], w2s[c][2 * lane], p);
-      p = __builtin_fmaf(hs[b][2 * lane + 1], w2s[c][2 * lane + 1], p);
-      z[c] = wave_sum(p) + b2s[c];
-    }
+    for (int c = 0; c < SC; ++c) z[c] = zs[b][c];
     float mx = z[0];
     int am = 0;
 #pragma unroll
@@ -153,25 +160,17 @@ __global__ void __launch_bounds__(ST) mlp_small_bwd_kernel(SmallArgs a) {
     float zt = 0.f;
 #pragma unroll
     for (int c = 0; c < SC; ++c) zt = c == tg ? z[c] : zt;
-    lsum += lse - zt;
-    csum += am == tg ? 1.f : 0.f;
-    if (lane < SC) {
-      float zl = z[0];
+    rowl[b][0] = lse - zt;
+    rowl[b][1] = am == tg ? 1.f : 0.f;
 #pragma unroll
-      for (int c = 1; c < SC; ++c) zl = lane == c ? z[c] : zl;
-      dls[b][lane] = a.scale * (__expf(zl - lse) - (lane == tg ? 1.f : 0.f));
-    }
-  }
-  if (lane == 0) {
-    red[wave][0] = lsum;
-    red[wave][1] = csum;
+    for (int c = 0; c < SC; ++c) dls[b][c] = a.scale * (__expf(z[c] - lse) - (c == tg ? 1.f : 0.f));
   }
   __syncthreads();
-  if (blockIdx.x == 0 && t == 0) {
+  if (blockIdx.x == 0 && t == 0) {  // loss sum and correct count, in row order
     float l = 0.f, c = 0.f;
-    for (int w = 0; w < ST / 64; ++w) {
-      l += red[w][0];
-      c += red[w][1];
+    for (int b = 0; b < B; ++b) {
+      l += rowl[b][0];
+      c += rowl[b][1];
     }
     a.stats[0] = l;
     a.stats[1] = c;
@@ -188,21 +187,19 @@ __global__ void __launch_bounds__(ST) mlp_small_bwd_kernel(SmallArgs a) {
   // gW1[own rows] = dz^T x, then the update of those rows (each element by the thread that reduced it)
   for (int k = t; k < SK; k += ST) {
     float g0 = 0.f, g1 = 0.f;
-    int b = 0;
-    for (; b + 16 <= B; b += 16) {  // 16 loads in flight, then the fmas in row order
-      float xv[16];
+    for (int b = 0; b < B; b += 32) {
+      // 32 unconditional loads in flight (ragged-tail rows clamped to row B - 1, their terms skipped),
+      // then the fmas in row order
+      float xv[32];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) xv[u] = xval<X8>(a, b + u, k);
+      for (int u = 0; u < 32; ++u) xv[u] = xval<X8>(a, min(b + u, B - 1), k);
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        g0 = __builtin_fmaf(dzs[b + u][0], xv[u], g0);
-        g1 = __builtin_fmaf(dzs[b + u][1], xv[u], g1);
+      for (int u = 0; u < 32; ++u) {
+        if (b + u < B) {
+          g0 = __builtin_fmaf(dzs[b + u][0], xv[u], g0);
+          g1 = __builtin_fmaf(dzs[b + u][1], xv[u], g1);
+        }
       }
-    }
-    for (; b < B; ++b) {
-      const float xv = xval<X8>(a, b, k);
-      g0 = __builtin_fmaf(dzs[b][0], xv, g0);
-      g1 = __builtin_fmaf(dzs[b][1], xv, g1);
     }
     const size_t o0 = (size_t)j0 * SK + k, o1 = o0 + SK;
     sgd1(a.w1 + o0, a.m1 ? a.m1 + o0 : nullptr, g0, a);

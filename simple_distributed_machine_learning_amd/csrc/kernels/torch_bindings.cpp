@@ -434,14 +434,37 @@ std::tuple<torch::Tensor, torch::Tensor> conv3x3_weights_bf16(torch::Tensor w) {
 }
 
 // y (channels-last [N][Co][H][W]) = conv3x3(x, w) with wt from conv3x3_weight_bf16(w, dgrad=false)
-torch::Tensor conv3x3_fwd_bf16(torch::Tensor x, torch::Tensor wt) {
+// the optional epilogue operands of the implicit-GEMM convolutions: an addend in the output's layout
+// and the BatchNorm partials [conv_part_rows][2][Co] fp32 of the output
+static const void* conv_addend(const c10::optional<torch::Tensor>& add, const torch::Tensor& y, const char* fn) {
+  if (!add.has_value() || !add->defined()) return nullptr;
+  check_cl_bf16(*add, "add");
+  TORCH_CHECK(add->sizes() == y.sizes(), fn, ": addend shape mismatch");
+  return add->data_ptr();
+}
+static float* conv_part(const c10::optional<torch::Tensor>& part, int64_t N, int64_t OH, int64_t OW, int64_t Co,
+                        const char* fn) {
+  if (!part.has_value() || !part->defined()) return nullptr;
+  TORCH_CHECK(part->is_cuda() && part->is_contiguous() && part->scalar_type() == torch::kFloat32 &&
+                  part->numel() == (int64_t)sdml::conv_part_rows(N, OH, OW) * 2 * Co,
+              fn, ": part must be a contiguous fp32 [conv_part_rows][2][Co] tensor");
+  return part->data_ptr<float>();
+}
+
+int64_t conv_part_rows(int64_t N, int64_t OH, int64_t OW) { return sdml::conv_part_rows(N, OH, OW); }
+
+torch::Tensor conv3x3_fwd_bf16(torch::Tensor x, torch::Tensor wt, c10::optional<torch::Tensor> add,
+                               c10::optional<torch::Tensor> part) {
   check_cl_bf16(x, "x");
   TORCH_CHECK(wt.dim() == 3 && wt.size(1) == 9 && wt.size(2) == x.size(1) && wt.is_contiguous() &&
               wt.scalar_type() == torch::kBFloat16, "conv3x3_fwd_bf16: wt must be [Co][9][C] bf16");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), Co = wt.size(0);
   TORCH_CHECK(sdml::conv3x3_bf16_supported(C, Co), "conv3x3_fwd_bf16: channels must be multiples of 64");
   auto y = torch::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  if (N * H * W > 0) sdml::conv3x3_fwd_bf16(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, C, Co, cur_stream());
+  const void* ap = conv_addend(add, y, "conv3x3_fwd_bf16");
+  float* pp = conv_part(part, N, H, W, Co, "conv3x3_fwd_bf16");
+  if (N * H * W > 0)
+    sdml::conv3x3_fwd_bf16(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, C, Co, cur_stream(), ap, pp);
   return y;
 }
 
@@ -473,7 +496,8 @@ static void check_bn_vec(const c10::optional<torch::Tensor>& t, int64_t C, const
 
 // general convolution (kernel 3 pad 1 / kernel 1 pad 0, stride 1 or 2), channels-last bf16; wt from
 // conv3x3_weight_bf16(w, false) for 3x3 or the [Co][C][1][1] weight itself for 1x1
-torch::Tensor conv_fwd_bf16(torch::Tensor x, torch::Tensor wt, int64_t ks, int64_t stride, int64_t pad) {
+torch::Tensor conv_fwd_bf16(torch::Tensor x, torch::Tensor wt, int64_t ks, int64_t stride, int64_t pad,
+                            c10::optional<torch::Tensor> add, c10::optional<torch::Tensor> part) {
   check_cl_bf16(x, "x");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), Co = wt.size(0);
   TORCH_CHECK(wt.is_contiguous() && wt.scalar_type() == torch::kBFloat16 && wt.numel() == Co * ks * ks * C,
@@ -481,9 +505,33 @@ torch::Tensor conv_fwd_bf16(torch::Tensor x, torch::Tensor wt, int64_t ks, int64
   TORCH_CHECK(sdml::conv_general_supported(C, Co, ks, stride, pad), "conv_fwd_bf16: unsupported geometry");
   const int64_t OH = sdml::conv_out_size(H, ks, stride, pad), OW = sdml::conv_out_size(W, ks, stride, pad);
   auto y = torch::empty({N, Co, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const void* ap = conv_addend(add, y, "conv_fwd_bf16");
+  float* pp = conv_part(part, N, OH, OW, Co, "conv_fwd_bf16");
   if (N * OH * OW > 0)
-    sdml::conv_fwd_bf16(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, C, Co, ks, stride, pad, cur_stream());
+    sdml::conv_fwd_bf16(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, C, Co, ks, stride, pad, cur_stream(), ap,
+                        pp);
   return y;
+}
+
+// input gradient of a stride-2 convolution (3x3 pad 1 / 1x1 pad 0): dx (channels-last [N][C][H][W]) from
+// dy (channels-last [N][Co][OH][OW]) and the torch weight [Co][C][ks][ks]
+torch::Tensor conv_dgrad_s2_bf16(torch::Tensor dy, torch::Tensor w, int64_t H, int64_t W, int64_t pad,
+                                 c10::optional<torch::Tensor> add) {
+  check_cl_bf16(dy, "dy");
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == torch::kBFloat16 && w.dim() == 4 &&
+              w.size(2) == w.size(3) && w.size(0) == dy.size(1), "conv_dgrad_s2_bf16: w must be [Co][C][k][k] bf16");
+  const int64_t N = dy.size(0), Co = dy.size(1), C = w.size(1), ks = w.size(2);
+  TORCH_CHECK(sdml::conv_general_supported(C, Co, ks, 2, pad), "conv_dgrad_s2_bf16: unsupported geometry");
+  TORCH_CHECK(dy.size(2) == sdml::conv_out_size(H, ks, 2, pad) && dy.size(3) == sdml::conv_out_size(W, ks, 2, pad),
+              "conv_dgrad_s2_bf16: dy does not match the input size");
+  auto dx = torch::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (dx.numel() == 0) return dx;
+  conv_addend(add, dx, "conv_dgrad_s2_bf16");
+  auto packed = torch::empty({(int64_t)sdml::conv_dgrad_s2_weight_elems(Co, C, ks)}, w.options());
+  sdml::conv_dgrad_s2_weight_bf16(w.data_ptr(), packed.data_ptr(), Co, C, ks, pad, cur_stream());
+  sdml::conv_dgrad_s2_bf16(dy.data_ptr(), packed.data_ptr(), dx.data_ptr(), N, H, W, C, Co, ks, pad, cur_stream(),
+                           conv_addend(add, dx, "conv_dgrad_s2_bf16"));
+  return dx;
 }
 
 void conv_wgrad_bf16_(torch::Tensor dy, torch::Tensor x, torch::Tensor gw, int64_t stride, int64_t pad) {
@@ -533,7 +581,7 @@ void conv_c1_wgrad_bf16_(torch::Tensor dy, torch::Tensor x, torch::Tensor gw) {
 std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> bn_nhwc_fwd(
     torch::Tensor x, c10::optional<torch::Tensor> res, torch::Tensor gamma, torch::Tensor beta,
     c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar, double eps, double momentum, bool relu,
-    c10::optional<torch::Tensor> num_batches_tracked) {
+    c10::optional<torch::Tensor> num_batches_tracked, c10::optional<torch::Tensor> part) {
   check_cl_bf16(x, "x");
   int64_t* nbt = nullptr;
   if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
@@ -555,10 +603,14 @@ std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> bn_nhwc_fwd(
   auto f = x.options().dtype(torch::kFloat32).memory_format(at::MemoryFormat::Contiguous);
   auto mean = torch::empty({C}, f), rstd = torch::empty({C}, f);
   auto ws = torch::empty({(int64_t)sdml::bn_nhwc_workspace_floats(M, C)}, f);
+  // part: the producing convolution's per-tile partials of x (conv_part_rows(N, H, W) rows), instead of
+  // the statistics pass over x
+  const float* pp = conv_part(part, N, H, W, C, "bn_nhwc_fwd");
+  const int prow = pp ? sdml::conv_part_rows(N, H, W) : 0;
   if (M > 0)
     sdml::bn_nhwc_fwd_bf16(x.data_ptr(), opt_data(res), gamma.data_ptr(), beta.data_ptr(), opt_data(rmean),
                            opt_data(rvar), M, C, (float)eps, (float)momentum, relu, y.data_ptr(), mean.data_ptr<float>(),
-                           rstd.data_ptr<float>(), ws.data_ptr<float>(), cur_stream(), nbt);
+                           rstd.data_ptr<float>(), ws.data_ptr<float>(), cur_stream(), nbt, pp, prow);
   return {y, mean, rstd};
 }
 
@@ -1499,15 +1551,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bf16_supported", &wgrad_bf16_supported_op, "shape check for wgrad_bf16_ (contiguous operands)");
   m.def("conv3x3_weight_bf16", &conv3x3_weight_bf16, "3x3 conv weight -> kernel layout (forward / dgrad)");
   m.def("conv3x3_weights_bf16", &conv3x3_weights_bf16, "3x3 conv weight -> (forward, dgrad) kernel layouts");
-  m.def("conv3x3_fwd_bf16", &conv3x3_fwd_bf16, "3x3 stride-1 pad-1 conv, channels-last bf16 (implicit GEMM)");
+  m.def("conv3x3_fwd_bf16", &conv3x3_fwd_bf16, "3x3 stride-1 pad-1 conv, channels-last bf16 (implicit GEMM)",
+        py::arg("x"), py::arg("wt"), py::arg("add") = py::none(), py::arg("part") = py::none());
+  m.def("conv_part_rows", &conv_part_rows, "rows of the BatchNorm partials a convolution epilogue writes");
   m.def("conv3x3_wgrad_bf16_", &conv3x3_wgrad_bf16_, "3x3 conv weight gradient, accumulated into bf16 grad");
-  m.def("conv_fwd_bf16", &conv_fwd_bf16, "conv (3x3 pad 1 / 1x1, stride 1|2), channels-last bf16 (implicit GEMM)");
+  m.def("conv_fwd_bf16", &conv_fwd_bf16, "conv (3x3 pad 1 / 1x1, stride 1|2), channels-last bf16 (implicit GEMM)",
+        py::arg("x"), py::arg("wt"), py::arg("ks"), py::arg("stride"), py::arg("pad"), py::arg("add") = py::none(),
+        py::arg("part") = py::none());
+  m.def("conv_dgrad_s2_bf16", &conv_dgrad_s2_bf16, "input gradient of a stride-2 conv (3x3 pad 1 / 1x1), parity-class GEMMs",
+        py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"), py::arg("pad"), py::arg("add") = py::none());
   m.def("conv_wgrad_bf16_", &conv_wgrad_bf16_, "conv weight gradient (3x3 / 1x1, stride 1|2), accumulated");
   m.def("conv_c1_fwd_bf16", &conv_c1_fwd_bf16, "stem 3x3 conv with one input channel -> channels-last bf16");
   m.def("conv_c1_wgrad_bf16_", &conv_c1_wgrad_bf16_, "stem conv weight gradient, accumulated into bf16 grad");
   m.def("bn_nhwc_fwd", &bn_nhwc_fwd, "training BatchNorm (+residual)(+ReLU), channels-last bf16", py::arg("x"),
         py::arg("res"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("eps"),
-        py::arg("momentum"), py::arg("relu"), py::arg("num_batches_tracked") = py::none());
+        py::arg("momentum"), py::arg("relu"), py::arg("num_batches_tracked") = py::none(), py::arg("part") = py::none());
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "BatchNorm (+residual)(+ReLU) backward, channels-last bf16", py::arg("x"),
         py::arg("dy"), py::arg("y"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("relu"),
         py::arg("need_dres"), py::arg("ggamma"), py::arg("gbeta"), py::arg("beta") = py::none());

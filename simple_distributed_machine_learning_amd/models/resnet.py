@@ -43,11 +43,23 @@ class BasicBlock(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x):
-        # conv (HIP implicit GEMM when stride-1 bf16 NHWC) -> BN+ReLU / BN+residual+ReLU in one
-        # pass each (ops/conv.py; PyTorch ops elsewhere)
-        out = conv_ops.batch_norm(self.bn1, conv_ops.conv2d(self.conv1, x), relu=True)
-        sc = x if self.shortcut is None else conv_ops.batch_norm(self.shortcut[1], conv_ops.conv2d(self.shortcut[0], x))
-        return conv_ops.batch_norm(self.bn2, conv_ops.conv2d(self.conv2, out), res=sc, relu=True)
+        # conv (HIP implicit GEMM when bf16 NHWC; the epilogue also writes the BatchNorm statistics
+        # partials) -> BN+ReLU / BN+residual+ReLU in one pass each (ops/conv.py; PyTorch ops elsewhere).
+        # The residual branch's input gradient is added in conv1's input-gradient epilogue
+        # (ResidualLink): the tap on x is created after the main branch's convolutions so autograd
+        # runs it first.
+        link = (conv_ops.ResidualLink() if (conv_ops.FUSE_RESIDUAL and x.requires_grad and x.is_cuda
+                                             and x.dtype == torch.bfloat16) else None)
+        y1, p1 = conv_ops.conv_stats(self.conv1, self.bn1, x, link)
+        out = conv_ops.batch_norm(self.bn1, y1, relu=True, part=p1)
+        if self.shortcut is None:
+            y2, p2 = conv_ops.conv_stats(self.conv2, self.bn2, out)
+            sc = conv_ops.grad_tap(x, link)
+        else:
+            ys, ps = conv_ops.conv_stats(self.shortcut[0], self.shortcut[1], conv_ops.grad_tap(x, link))
+            sc = conv_ops.batch_norm(self.shortcut[1], ys, part=ps)
+            y2, p2 = conv_ops.conv_stats(self.conv2, self.bn2, out)
+        return conv_ops.batch_norm(self.bn2, y2, res=sc, relu=True, part=p2)
 
 
 def block_defs(in_ch: int = 1):

@@ -4,8 +4,8 @@ with flipped/transposed weights, weight gradient accumulated into ``weight.grad`
 
 Used by the ResNet-18-style stages (models/resnet.py) when they run in bf16 channels-last: the
 twelve stride-1 3x3 convolutions, the one-channel stem, and the stride-2 3x3 / 1x1 shortcut
-convolutions (forward and weight gradient; their input gradient stays on MIOpen). Every other
-dtype/layout goes through ``F.conv2d``.
+convolutions (forward, weight gradient and - as four parity-class GEMMs - input gradient), so a bf16
+ResNet step launches no MIOpen convolution. Every other dtype/layout goes through ``F.conv2d``.
 """
 from __future__ import annotations
 
@@ -15,17 +15,73 @@ import torch.nn.functional as F
 from .._native import kernels
 
 
+# ResidualLink joins (set False to let autograd add the two gradients of a block input, for A/B tests)
+FUSE_RESIDUAL = True
+
+
+class ResidualLink:
+    """Joins the two input gradients of a residual block's input x without an add kernel: the
+    residual branch's gradient (through ``grad_tap``) is handed to the main branch's first
+    convolution, whose input-gradient epilogue adds it (dx = bf16(conv + addend)).
+
+    The tap is created after the main branch's convolutions in the forward pass, so autograd
+    (ready nodes run in decreasing creation order) runs it first. Either order stays correct:
+    a convolution that finds no addend marks the link consumed, and a tap that comes later then
+    returns its gradient to autograd as usual. ``fused`` counts the joins done in an epilogue."""
+
+    __slots__ = ("addend", "consumed")
+    fused = 0
+
+    def __init__(self):
+        self.addend = None
+        self.consumed = False
+
+    def take(self):
+        add, self.addend = self.addend, None
+        if add is None:
+            self.consumed = True
+        else:
+            ResidualLink.fused += 1
+        return add
+
+
+class _GradTapFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, link):
+        ctx.link = link
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        link = ctx.link
+        if link.consumed:
+            return g, None
+        link.addend = g.contiguous(memory_format=torch.channels_last)
+        return None, None
+
+
+def grad_tap(x: torch.Tensor, link) -> torch.Tensor:
+    """x, with its gradient routed through ``link`` (see ResidualLink); identity without a link."""
+    if link is None or not x.requires_grad:
+        return x
+    return _GradTapFn.apply(x, link)
+
+
+def _take_addend(link):
+    return link.take() if link is not None else None
+
+
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w):
+    def forward(ctx, x, w, part=None, link=None):
         K = kernels()
         if ctx.needs_input_grad[0]:  # both layouts in one pass; the dgrad one waits for backward
             wt, ctx.wd = K.conv3x3_weights_bf16(w)
         else:
             wt, ctx.wd = K.conv3x3_weight_bf16(w, False), None
-        y = K.conv3x3_fwd_bf16(x, wt)
+        y = K.conv3x3_fwd_bf16(x, wt, part=part)
         ctx.save_for_backward(x)
-        ctx.w = w
+        ctx.w, ctx.link = w, link
         return y
 
     @staticmethod
@@ -34,7 +90,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         w = ctx.w
         K = kernels()
         dy = dy.contiguous(memory_format=torch.channels_last)
-        dx = K.conv3x3_fwd_bf16(dy, ctx.wd) if ctx.needs_input_grad[0] else None
+        dx = K.conv3x3_fwd_bf16(dy, ctx.wd, add=_take_addend(ctx.link)) if ctx.needs_input_grad[0] else None
         ctx.wd = None
         gw = None
         if ctx.needs_input_grad[1]:
@@ -43,7 +99,7 @@ class _Conv3x3Fn(torch.autograd.Function):
             else:
                 gw = torch.zeros_like(w)
                 K.conv3x3_wgrad_bf16_(dy, x, gw)
-        return dx, gw
+        return dx, gw, None, None
 
 
 def hip_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
@@ -55,18 +111,33 @@ def hip_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
 
 
+def _general_dgrad(dy, x, w, st, pd, add=None):
+    """Input gradient of a general_eligible convolution (+ add): stride 2 -> the parity-class GEMM
+    kernel (conv_bf16.hip conv_dgrad_s2_kernel); stride-1 1x1 -> the forward kernel on dy with the
+    transposed [C][1][Co] weights; stride-1 3x3 -> the forward kernel with the flipped dgrad weights."""
+    K = kernels()
+    H, W = x.shape[2], x.shape[3]
+    if st == 2:
+        return K.conv_dgrad_s2_bf16(dy, w, H, W, pd, add=add)
+    if w.shape[2] == 1:
+        return K.conv_fwd_bf16(dy, w.reshape(w.shape[0], w.shape[1]).t().contiguous(), 1, 1, 0, add=add)
+    _, wd = K.conv3x3_weights_bf16(w)
+    return K.conv3x3_fwd_bf16(dy, wd, add=add)
+
+
 class _ConvGeneralFn(torch.autograd.Function):
-    """Strided 3x3 / 1x1 convolution (the downsampling blocks): forward and weight gradient on the
-    im2col implicit-GEMM kernels; the input gradient (a transposed strided convolution) on MIOpen."""
+    """Strided 3x3 / 1x1 convolution (the downsampling blocks), all three passes on HIP kernels:
+    forward and weight gradient on the im2col implicit-GEMM kernels, the input gradient (a transposed
+    strided convolution) on the parity-class GEMMs (``_general_dgrad``)."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, pad):
+    def forward(ctx, x, w, stride, pad, part=None, link=None):
         K = kernels()
         ks = w.shape[2]
         wt = K.conv3x3_weight_bf16(w, False) if ks == 3 else w  # [Co][C][1][1] is already [Co][1][C]
-        y = K.conv_fwd_bf16(x, wt, ks, stride, pad)
+        y = K.conv_fwd_bf16(x, wt, ks, stride, pad, part=part)
         ctx.save_for_backward(x)
-        ctx.w, ctx.stride, ctx.pad = w, stride, pad
+        ctx.w, ctx.stride, ctx.pad, ctx.link = w, stride, pad, link
         return y
 
     @staticmethod
@@ -76,8 +147,7 @@ class _ConvGeneralFn(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.ops.aten.convolution_backward(dy, x, w, None, [st, st], [pd, pd], [1, 1], False, [0, 0], 1,
-                                                     [True, False, False])[0]
+            dx = _general_dgrad(dy, x, w, st, pd, add=_take_addend(ctx.link))
         gw = None
         if ctx.needs_input_grad[1]:
             if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
@@ -85,7 +155,7 @@ class _ConvGeneralFn(torch.autograd.Function):
             else:
                 gw = torch.zeros_like(w)
                 kernels().conv_wgrad_bf16_(dy, x, gw, st, pd)
-        return dx, gw, None, None
+        return dx, gw, None, None, None, None
 
 
 def general_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
@@ -134,27 +204,43 @@ def stem_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and conv.groups == 1 and conv.out_channels % 16 == 0 and conv.out_channels <= 512)
 
 
-def conv2d(conv: torch.nn.Conv2d, x: torch.Tensor) -> torch.Tensor:
+def conv2d(conv: torch.nn.Conv2d, x: torch.Tensor, part=None, link=None) -> torch.Tensor:
     """``conv(x)``, on the HIP kernels where they apply: stride-1 3x3 on the halo kernel, strided
-    3x3 / 1x1 on the im2col kernel (input gradient on MIOpen), the streaming stem kernels for a
-    one-channel input."""
+    3x3 / 1x1 on the im2col kernel (input gradient on the parity-class kernel), the streaming stem
+    kernels for a one-channel input. ``part`` / ``link``: see ``conv_stats`` / ``ResidualLink`` (the
+    implicit-GEMM paths only)."""
     if hip_eligible(x, conv):
-        return _Conv3x3Fn.apply(x, conv.weight)
+        return _Conv3x3Fn.apply(x, conv.weight, part, link)
     if general_eligible(x, conv):
-        return _ConvGeneralFn.apply(x, conv.weight, conv.stride[0], conv.padding[0])
+        return _ConvGeneralFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], part, link)
     if stem_eligible(x, conv):
         return _StemConvFn.apply(x, conv.weight)
     return conv(x)
 
 
+def conv_stats(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x: torch.Tensor, link=None):
+    """(y, part): y = conv(x); part = the BatchNorm partials of y written by the convolution's
+    epilogue (per 256-pixel tile: channel sums of y and y^2) when the convolution runs on an
+    implicit-GEMM kernel and ``bn`` trains on the HIP path, else None. ``batch_norm(bn, y,
+    part=part)`` then skips its statistics pass over y."""
+    part = None
+    if bn.training and (hip_eligible(x, conv) or general_eligible(x, conv)) and bn.weight.dtype == torch.bfloat16:
+        N, Co = x.shape[0], conv.out_channels
+        OH = (x.shape[2] + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1
+        OW = (x.shape[3] + 2 * conv.padding[1] - conv.kernel_size[1]) // conv.stride[1] + 1
+        part = torch.empty(kernels().conv_part_rows(N, OH, OW) * 2 * Co, device=x.device, dtype=torch.float32)
+    return conv2d(conv, x, part, link), part
+
+
 # ---- BatchNorm (+ residual) (+ ReLU), channels-last bf16 (csrc/kernels/batchnorm_nhwc.hip) -----
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, gamma, beta, bn: torch.nn.BatchNorm2d, relu: bool):
+    def forward(ctx, x, res, gamma, beta, bn: torch.nn.BatchNorm2d, relu: bool, part=None):
         momentum = 0.1 if bn.momentum is None else bn.momentum
         nbt = bn.num_batches_tracked  # incremented inside the statistics kernel
         y, mean, rstd = kernels().bn_nhwc_fwd(x, res, gamma, beta, bn.running_mean, bn.running_var, bn.eps,
-                                              momentum, relu, nbt if nbt is not None and nbt.is_cuda else None)
+                                              momentum, relu, nbt if nbt is not None and nbt.is_cuda else None,
+                                              part=part)
         if nbt is not None and not nbt.is_cuda:
             nbt.add_(1)
         # BatchNorm + ReLU without a residual: the backward recomputes the mask from x, so y is
@@ -179,7 +265,7 @@ class _BNFn(torch.autograd.Function):
         gb, own_b = acc(beta)
         dx, dres = kernels().bn_nhwc_bwd(x, dy, y if ctx.relu else None, mean, rstd, gamma, ctx.relu, ctx.has_res,
                                           gg, gb, beta)
-        return dx, dres, (gg if own_g else None), (gb if own_b else None), None, None
+        return dx, dres, (gg if own_g else None), (gb if own_b else None), None, None, None
 
 
 def bn_eligible(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res=None) -> bool:
@@ -191,8 +277,9 @@ def bn_eligible(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res=None) -> bool:
     return ok
 
 
-def batch_norm(bn: torch.nn.BatchNorm2d, x: torch.Tensor, res=None, relu: bool = False) -> torch.Tensor:
-    """``relu?(bn(x) (+ res))`` — one pass per direction on the HIP kernels where they apply."""
+def batch_norm(bn: torch.nn.BatchNorm2d, x: torch.Tensor, res=None, relu: bool = False, part=None) -> torch.Tensor:
+    """``relu?(bn(x) (+ res))`` — one pass per direction on the HIP kernels where they apply; ``part``:
+    x's statistics partials from its convolution's epilogue (``conv_stats``)."""
     if x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4:
         # MIOpen may hand back NCHW (e.g. the 1-channel stem): one copy beats PyTorch's NCHW
         # BatchNorm backward (~0.8 ms per call at batch 512)
@@ -201,7 +288,7 @@ def batch_norm(bn: torch.nn.BatchNorm2d, x: torch.Tensor, res=None, relu: bool =
             res = res.contiguous(memory_format=torch.channels_last)
     if bn_eligible(x, bn, res):
         if bn.training:
-            return _BNFn.apply(x, res, bn.weight, bn.bias, bn, relu)
+            return _BNFn.apply(x, res, bn.weight, bn.bias, bn, relu, part)
         with torch.no_grad():
             scale = (bn.weight.float() * torch.rsqrt(bn.running_var.float() + bn.eps)).contiguous()
             shift = (bn.bias.float() - bn.running_mean.float() * scale).contiguous()

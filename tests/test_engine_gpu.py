@@ -84,7 +84,9 @@ def test_resnet_bf16_hip_kernels_match_library_path(monkeypatch):
         out = [float(e.run(ds, 0, 64, train=True).loss_sum) / 64 for _ in range(3)]
         return out, e.flat.params.float().clone()
 
+    fused0 = conv_ops.ResidualLink.fused
     hip_losses, hip_p = run()
+    assert conv_ops.ResidualLink.fused - fused0 == 3 * 8  # every block joins its input gradient in an epilogue
     monkeypatch.setattr(conv_ops, "hip_eligible", lambda x, conv: False)
     monkeypatch.setattr(conv_ops, "bn_eligible", lambda x, bn, res=None: False)
     lib_losses, lib_p = run()

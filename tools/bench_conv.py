@@ -1,71 +1,65 @@
-"""Per-layer timing of the ResNet-18 stride-1 3x3 convolutions (batch 512, MNIST-shape stages) on the
-hand-written kernels (csrc/kernels/conv_bf16.hip) next to MIOpen, with a numerics check of each
-kernel against F.conv2d (fp32 accumulate of the same bf16 operands).
+"""Per-call time of the ResNet convolution kernels at the bf16 ResNet-18 (batch 512, 28x28 MNIST)
+shapes, with and without the fused epilogue operands (BatchNorm partials, residual addend).
 
-    python tools/bench_conv.py [--batch 512] [--iters 20]
-    SDML_CONV_FWD=im2col python tools/bench_conv.py     # A/B the forward kernel variants
+    python tools/bench_conv.py            -> one JSON line per (kernel, shape, epilogue)
 """
-import argparse
 import json
 import os
 import sys
 
 import torch
-import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from simple_distributed_machine_learning_amd._native import kernels  # noqa: E402
+from simple_distributed_machine_learning_amd import _native  # noqa: E402
 
-LAYERS = [(28, 64), (14, 128), (7, 256), (4, 512)]  # (H = W, channels) of layer1..layer4
+K = _native.kernels()
+DEV = torch.device("cuda", 0)
 
 
-def timed(fn, iters):
-    fn()
+def cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def timed(fn, iters=50):
+    for _ in range(5):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
+    a.record()
     for _ in range(iters):
         fn()
-    e.record()
+    b.record()
     torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters * 1e3  # us
+    return a.elapsed_time(b) / iters * 1e3  # us
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=512)
-    ap.add_argument("--iters", type=int, default=20)
-    a = ap.parse_args()
-    K = kernels()
-    g = torch.Generator(device="cpu").manual_seed(0)
-    cl = torch.channels_last
-    for hw, c in LAYERS:
-        N = a.batch
-        x = torch.randn(N, c, hw, hw, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=cl)
-        dy = torch.randn(N, c, hw, hw, generator=g).to("cuda", torch.bfloat16).contiguous(memory_format=cl)
-        w = (torch.randn(c, c, 3, 3, generator=g) * (2.0 / (9 * c)) ** 0.5).to("cuda", torch.bfloat16)
-        wt, wd = K.conv3x3_weight_bf16(w, False), K.conv3x3_weight_bf16(w, True)
-        gw = torch.zeros_like(w)
-        flops = 2 * N * hw * hw * c * c * 9
-        y = K.conv3x3_fwd_bf16(x, wt)
-        yr = F.conv2d(x.float(), w.float(), padding=1)
-        err_f = float((y.float() - yr).abs().max() / yr.abs().max())
-        dx = K.conv3x3_fwd_bf16(dy, wd)
-        dxr = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), padding=1)
-        err_d = float((dx.float() - dxr).abs().max() / dxr.abs().max())
-        gw.zero_()
-        K.conv3x3_wgrad_bf16_(dy, x, gw)
-        gwr = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), padding=1)
-        err_w = float((gw.float() - gwr).abs().max() / gwr.abs().max())
-        t_f = timed(lambda: K.conv3x3_fwd_bf16(x, wt), a.iters)
-        t_d = timed(lambda: K.conv3x3_fwd_bf16(dy, wd), a.iters)
-        t_w = timed(lambda: K.conv3x3_wgrad_bf16_(dy, x, gw), a.iters)
-        t_mf = timed(lambda: F.conv2d(x, w, padding=1), a.iters)
-        print(json.dumps({"hw": hw, "c": c, "fwd_us": round(t_f, 1), "dgrad_us": round(t_d, 1),
-                          "wgrad_us": round(t_w, 1), "fwd_tflops": round(flops / t_f / 1e6, 1),
-                          "wgrad_tflops": round(flops / t_w / 1e6, 1), "miopen_fwd_us": round(t_mf, 1),
-                          "rel_err": [round(err_f, 5), round(err_d, 5), round(err_w, 5)],
-                          "engine": os.environ.get("SDML_CONV_FWD", "halo")}), flush=True)
+    N = int(os.environ.get("BATCH", "512"))
+    for C, Co, H in [(64, 64, 28), (128, 128, 14), (256, 256, 7), (512, 512, 4)]:
+        x = cl(torch.randn(N, C, H, H, device=DEV).to(torch.bfloat16))
+        w = (torch.randn(Co, C, 3, 3, device=DEV) * 0.05).to(torch.bfloat16)
+        wt = K.conv3x3_weight_bf16(w, False)
+        add = cl(torch.randn(N, Co, H, H, device=DEV).to(torch.bfloat16))
+        part = torch.empty(K.conv_part_rows(N, H, H) * 2 * Co, device=DEV)
+        flops = 2 * N * H * H * Co * C * 9
+        for name, fn in [("plain", lambda: K.conv3x3_fwd_bf16(x, wt)),
+                         ("part", lambda: K.conv3x3_fwd_bf16(x, wt, part=part)),
+                         ("add", lambda: K.conv3x3_fwd_bf16(x, wt, add=add))]:
+            us = timed(fn)
+            print(json.dumps({"kernel": "conv3x3_s1", "C": C, "Co": Co, "H": H, "epi": name, "us": round(us, 2),
+                              "tflops": round(flops / us / 1e6, 1)}))
+    for C, Co, H in [(64, 128, 28), (128, 256, 14), (256, 512, 7)]:
+        OH = (H + 1) // 2
+        dy = cl(torch.randn(N, Co, OH, OH, device=DEV).to(torch.bfloat16))
+        add = cl(torch.randn(N, C, H, H, device=DEV).to(torch.bfloat16))
+        for ks, pd in [(3, 1), (1, 0)]:
+            w = (torch.randn(Co, C, ks, ks, device=DEV) * 0.05).to(torch.bfloat16)
+            flops = 2 * N * OH * OH * Co * C * ks * ks
+            for name, fn in [("plain", lambda: K.conv_dgrad_s2_bf16(dy, w, H, H, pd)),
+                             ("add", lambda: K.conv_dgrad_s2_bf16(dy, w, H, H, pd, add=add))]:
+                us = timed(fn)
+                print(json.dumps({"kernel": f"dgrad_s2_{ks}x{ks}", "C": C, "Co": Co, "H": H, "epi": name,
+                                  "us": round(us, 2), "tflops": round(flops / us / 1e6, 1)}))
 
 
 if __name__ == "__main__":

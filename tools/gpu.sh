@@ -37,7 +37,14 @@ case "$task" in
     rc=$?
     if [ $rc -ne 0 ]; then tail -20 "$d/run.log"; exit $rc; fi
     f=$(find "$d/raw" -name "*kernel_stats.csv" | head -1)
-    python tools/summarize_profile.py stats "$f" 30 > "$d/kernel_stats.txt"
+    # per-step divisor: the command's --steps + --warmup (STEPS=<n> overrides; 30 if neither is given)
+    n=0; prev=""
+    for x in "$@"; do
+      case "$prev" in --steps|--warmup) n=$((n + x)) ;; esac
+      prev=$x
+    done
+    [ "$n" -gt 0 ] || n=30
+    python tools/summarize_profile.py stats "$f" "${STEPS:-$n}" > "$d/kernel_stats.txt"
     grep -v amdgpu.ids "$d/run.log" | grep "^{" | cut -c1-300
     head -14 "$d/kernel_stats.txt" | cut -c1-150 ;;
   pmc)

@@ -109,6 +109,7 @@ class ModelSpec:
     input_kind: str = "image"   # image | tokens
     param_dtype: torch.dtype = torch.float32
     vocab_size: int = 0         # token models: vocabulary size
+    num_classes: int = 10       # image models: classifier outputs (label range checked under debug_sync)
     seq_len: int = 0            # token models: sequence length of the boundary tensors
 
 

@@ -250,6 +250,17 @@ class PipelineEngine:
             scale = scale / float(dataset.seq_len)
         return scale
 
+    def _check_targets(self, dataset, start: int, n: int):
+        """debug_sync: a label outside [0, classes) raises here. The fused heads (head_xent.hip,
+        mlp_u8.hip) give such a row no loss term and no gradient, where torch's nll_loss in the
+        reference (/root/reference/simple_distributed.py:111) raises."""
+        spec = self.spec
+        C = spec.vocab_size if spec.input_kind == "tokens" else spec.num_classes
+        t = dataset.targets(start, n)
+        lo, hi = int(t.min()), int(t.max())
+        if lo < 0 or hi >= C:
+            raise ValueError(f"target out of range [0, {C}) in samples [{start}, {start + n}): min {lo}, max {hi}")
+
     def run(self, dataset, start: int, batch_size: int, train: bool, global_batch: Optional[int] = None,
             step_optimizer: bool = True) -> StepResult:
         """One pipeline step over samples [start, start+batch_size) of ``dataset``.
@@ -260,6 +271,8 @@ class PipelineEngine:
         """
         t0 = time.perf_counter()
         dev = self.device
+        if self.debug_sync and batch_size > 0:
+            self._check_targets(dataset, start, batch_size)
         if batch_size <= 0:  # a DP replica with no samples in a ragged last batch
             if train:
                 self.flat.zero_grad()

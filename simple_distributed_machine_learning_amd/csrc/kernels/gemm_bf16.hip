@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "gelu.h"
 #include "kernels.h"
@@ -105,6 +106,54 @@ __device__ __forceinline__ void issue_stage(const GP& p, unsigned char* st, int 
 __device__ __forceinline__ bf16x8 ld_b128(const unsigned char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 __device__ __forceinline__ s16x4 ds_tr16(const unsigned char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+// epilogue shared by both main loops: bf16 rows through the (free) stage buffers, 16-B row pieces to HBM
+template <int EPI>
+__device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&acc)[8][4], unsigned char* smem, int m0,
+                                                   int n0, int wave, int lane) {
+  const int wm = wave >> 2, wn = wave & 3;
+  const int g = lane >> 4, l16 = lane & 15;
+  // wave image [128 rows][64 cols] bf16 (128 B rows, 16-B chunks swizzled like the A image)
+  unsigned char* W = smem + wave * (128 * 128);
+  float bj[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = min(n0 + wn * 64 + 16 * j + l16, p.N - 1);
+      bj[j] = bf2f(p.bias[col]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * i + 4 * g + r, col = 16 * j + l16;
+        const float v = acc[i][j][r] + bj[j];
+        *reinterpret_cast<u16*>(W + row * 128 + 16 * ((col >> 3) ^ rk_swz(row)) + 2 * (col & 7)) = f2bf(v);
+      }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+  for (int it = 0; it < 16; ++it) {
+    const int row = 8 * it + (lane >> 3), ch = lane & 7;
+    const u16x8 v = *reinterpret_cast<const u16x8*>(W + row * 128 + 16 * (ch ^ rk_swz(row)));
+    const int grow = m0 + wm * 128 + row, gcol = n0 + wn * 64 + 8 * ch;
+    if (grow >= p.M || gcol >= p.N) continue;  // (N % 8 == 0: a chunk is all in or all out)
+    u16x8 o = v;
+    if constexpr (EPI == EPI_BIAS_GELU) {
+      *reinterpret_cast<u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol) = v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_f(bf2f(v[e])));
+    } else if constexpr (EPI == EPI_DGELU) {
+      const u16x8 u = *reinterpret_cast<const u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_grad_f(bf2f(v[e]), bf2f(u[e])));
+    }
+    *reinterpret_cast<u16x8*>(p.C + (size_t)grow * p.ldc + gcol) = o;
+  }
 }
 
 template <int BL, int EPI>
@@ -189,47 +238,172 @@ __global__ void __launch_bounds__(GT) gemm_bf16_kernel(GP p) {
     asm volatile("" ::: "memory");
   }
 
-  // ---- epilogue: bf16 rows through the (free) stage buffers, 16-B row pieces to HBM ----
-  // wave image [128 rows][64 cols] bf16 (128 B rows, 16-B chunks swizzled like the A image)
-  unsigned char* W = smem + wave * (128 * 128);
-  float bj[4] = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+  gemm_bf16_epilogue<EPI>(p, acc, smem, m0, n0, wave, lane);
+}
+
+// ---- NT form, 4-phase K-step schedule ("8-phase" per two K-steps; cdna_hip_programming.md §5) --------
+// Same tile, waves and fragments as above, but each 64-deep K-step runs as 4 phases, one per 64 x 32
+// quadrant of every wave's 128 x 64 output (16 MFMAs each, at raised priority), and the LDS-DMA prefetch
+// is cut into half-tiles of 128 rows x 64 k (16 KiB, 2 global_load_lds per thread) streamed one per
+// phase, 3 in flight: the counted `s_waitcnt vmcnt(6)` at the last phase of K-step t retires exactly
+// K-step t+1, so loads stay in flight across every barrier (never vmcnt(0) in the loop).
+// The two wave rows run one barrier apart (ping-pong): while one issues its LDS reads and DMA, the other
+// is in its MFMAs. Half-tile q of K-step u (h = 4u + q) lives in LDS slot h % 10 (10 x 16 KiB = all
+// 160 KiB):
+//   q 0: A rows of quadrant-row 0 (tile rows wm*128 + i, i < 64, for both wm; slot row wm*64 + i)
+//   q 1: B rows of quadrant-col 0 (tile rows wn*64 + i, i < 32; slot row wn*32 + i)
+//   q 2: B rows of quadrant-col 1 (tile rows wn*64 + 32 + i)
+//   q 3: A rows of quadrant-row 1 (tile rows wm*128 + 64 + i)
+// Phase p of K-step t reads (p0: q0 -> A regs, q1 -> B0 regs; p1: q2 -> B1 regs; p2: q3 -> A regs;
+// p3: nothing), computes quadrant (0,0), (0,1), (1,1), (1,0), and issues half-tile h = 4t + p + 7.
+// RAW: a half-tile is retired by every wave's vmcnt(6) before that wave's barrier of phase 4t+3, and
+// read only after the next barrier. WAR: with 10 slots a slot is re-filled >= 3 phases after its last
+// read, so the lagging wave row's reads (retired by its lgkmcnt(0) after the following barrier) are
+// long done. Half-tiles past the last K-step re-read it into consumed slots (uniform vmcnt counting).
+constexpr int HT = 16384, NSLOT = 10;
+
+template <int Q>
+__device__ __forceinline__ void issue_half(const GP& p, unsigned char* smem, int h, int nk, int m0, int n0, int wave,
+                                           int lane) {
+  const int k0 = min(h >> 2, nk - 1) * TK;
+  unsigned char* slot = smem + (h % NSLOT) * HT;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = min(n0 + wn * 64 + 16 * j + l16, p.N - 1);
-      bj[j] = bf2f(p.bias[col]);
+  for (int v = 0; v < 2; ++v) {
+    const int qq = wave + 8 * v;         // 1-KiB DMA block of the slot
+    const int lr = 8 * qq + (lane >> 3);  // slot row 0..127
+    const int c = (lane & 7) ^ rk_swz(lr);
+    if constexpr (Q == 0 || Q == 3) {
+      const int tr = (lr >> 6) * 128 + (Q == 3 ? 64 : 0) + (lr & 63);
+      glds16(p.A + (size_t)min(m0 + tr, p.M - 1) * p.lda + k0 + 8 * c, slot + 1024 * qq);
+    } else {
+      const int tr = (lr >> 5) * 64 + (Q == 2 ? 32 : 0) + (lr & 31);
+      glds16(p.B + (size_t)min(n0 + tr, p.N - 1) * p.ldb + k0 + 8 * c, slot + 1024 * qq);
     }
   }
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NSLOT * HT];  // the epilogue reuses it
+  const int nwg = p.tiles_m * p.tiles_n;
+  int wg = blockIdx.x;
+  if (nwg >= 16) {
+    const int q = nwg / 8, r = nwg % 8, xcd = wg % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
+  }
+  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int g = lane >> 4, l16 = lane & 15;
+
+  f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment byte offsets inside a slot: A (m-tile i of the quadrant, substep s), B (n-tile jj, substep s)
+  int aoff[4][2], boff[2][2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * i + 4 * g + r, col = 16 * j + l16;
-        const float v = acc[i][j][r] + bj[j];
-        *reinterpret_cast<u16*>(W + row * 128 + 16 * ((col >> 3) ^ rk_swz(row)) + 2 * (col & 7)) = f2bf(v);
-      }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll 4
-  for (int it = 0; it < 16; ++it) {
-    const int row = 8 * it + (lane >> 3), ch = lane & 7;
-    const u16x8 v = *reinterpret_cast<const u16x8*>(W + row * 128 + 16 * (ch ^ rk_swz(row)));
-    const int grow = m0 + wm * 128 + row, gcol = n0 + wn * 64 + 8 * ch;
-    if (grow >= p.M || gcol >= p.N) continue;  // (N % 8 == 0: a chunk is all in or all out)
-    u16x8 o = v;
-    if constexpr (EPI == EPI_BIAS_GELU) {
-      *reinterpret_cast<u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol) = v;
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_f(bf2f(v[e])));
-    } else if constexpr (EPI == EPI_DGELU) {
-      const u16x8 u = *reinterpret_cast<const u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_grad_f(bf2f(v[e]), bf2f(u[e])));
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r = wm * 64 + 16 * i + l16;
+      aoff[i][s2] = r * 128 + 16 * ((4 * s2 + g) ^ rk_swz(r));
     }
-    *reinterpret_cast<u16x8*>(p.C + (size_t)grow * p.ldc + gcol) = o;
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r = wn * 32 + 16 * jj + l16;
+      boff[jj][s2] = r * 128 + 16 * ((4 * s2 + g) ^ rk_swz(r));
+    }
+
+  const int nk = p.K / TK;
+  issue_half<0>(p, smem, 0, nk, m0, n0, wave, lane);
+  issue_half<1>(p, smem, 1, nk, m0, n0, wave, lane);
+  issue_half<2>(p, smem, 2, nk, m0, n0, wave, lane);
+  issue_half<3>(p, smem, 3, nk, m0, n0, wave, lane);
+  issue_half<0>(p, smem, 4, nk, m0, n0, wave, lane);
+  issue_half<1>(p, smem, 5, nk, m0, n0, wave, lane);
+  issue_half<2>(p, smem, 6, nk, m0, n0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // K-step 0's 4 half-tiles
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // wave row 1 runs one barrier behind row 0
+
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  auto mfma_quadrant = [&](int qm, const bf16x8 (&bb)[2][2], int qn) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          acc[4 * qm + i][2 * qn + jj] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], bb[jj][s2], acc[4 * qm + i][2 * qn + jj], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync_mid = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto sync_end = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  for (int t = 0; t < nk; ++t) {
+    const int h = 4 * t + 7;
+    const unsigned char* s0 = smem + ((4 * t) % NSLOT) * HT;
+    const unsigned char* s1 = smem + ((4 * t + 1) % NSLOT) * HT;
+    const unsigned char* s2p = smem + ((4 * t + 2) % NSLOT) * HT;
+    const unsigned char* s3 = smem + ((4 * t + 3) % NSLOT) * HT;
+    // phase 0: A quadrant-row 0 + B quadrant-col 0; quadrant (0, 0)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) b0[jj][s2] = ld_b128(s1 + boff[jj][s2]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = ld_b128(s0 + aoff[i][s2]);
+    issue_half<3>(p, smem, h, nk, m0, n0, wave, lane);
+    sync_mid();
+    mfma_quadrant(0, b0, 0);
+    sync_end();
+    // phase 1: B quadrant-col 1; quadrant (0, 1)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) b1[jj][s2] = ld_b128(s2p + boff[jj][s2]);
+    issue_half<0>(p, smem, h + 1, nk, m0, n0, wave, lane);
+    sync_mid();
+    mfma_quadrant(0, b1, 1);
+    sync_end();
+    // phase 2: A quadrant-row 1; quadrant (1, 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = ld_b128(s3 + aoff[i][s2]);
+    issue_half<1>(p, smem, h + 2, nk, m0, n0, wave, lane);
+    sync_mid();
+    mfma_quadrant(1, b1, 1);
+    sync_end();
+    // phase 3: no reads; quadrant (1, 0); retire K-step t + 1
+    issue_half<2>(p, smem, h + 3, nk, m0, n0, wave, lane);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    sync_mid();
+    mfma_quadrant(1, b0, 0);
+    sync_end();
   }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // rejoin wave row 1
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the past-the-end half-tiles, before the epilogue reuses LDS
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  gemm_bf16_epilogue<EPI>(p, acc, smem, m0, n0, wave, lane);
 }
 
 }  // namespace
@@ -268,8 +442,22 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
       default: GB_LAUNCH(BLV, EPI_STORE); break;           \
     }                                                     \
   } while (0)
-  if (b_kn) GB_EPI(1);
-  else GB_EPI(0);
+  static const bool nt4 = [] {  // SDML_GEMM_BF16_NT=2phase: the one-barrier-per-K-step loop (A/B)
+    const char* e = std::getenv("SDML_GEMM_BF16_NT");
+    return !(e && std::string(e) == "2phase");
+  }();
+  if (b_kn) {
+    GB_EPI(1);
+  } else if (nt4) {
+    switch (epi) {
+      case EPI_BIAS: hipLaunchKernelGGL((gemm_bf16_nt4_kernel<EPI_BIAS>), grid, dim3(GT), 0, stream, p); break;
+      case EPI_BIAS_GELU: hipLaunchKernelGGL((gemm_bf16_nt4_kernel<EPI_BIAS_GELU>), grid, dim3(GT), 0, stream, p); break;
+      case EPI_DGELU: hipLaunchKernelGGL((gemm_bf16_nt4_kernel<EPI_DGELU>), grid, dim3(GT), 0, stream, p); break;
+      default: hipLaunchKernelGGL((gemm_bf16_nt4_kernel<EPI_STORE>), grid, dim3(GT), 0, stream, p); break;
+    }
+  } else {
+    GB_EPI(0);
+  }
 #undef GB_EPI
 #undef GB_LAUNCH
 }

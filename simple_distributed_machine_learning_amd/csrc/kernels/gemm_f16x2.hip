@@ -1,0 +1,602 @@
+// fp32-accurate GEMMs of the 4x1024 MLP's hidden layers (BASELINE config 3) on the fp16 matrix cores,
+// from operands PRE-SPLIT into two fp16 planes (round 3; the bf16x3 engine in gemm_f32x3.hip splits both
+// operands into three bf16 planes inside its K loop and pays 6 MFMAs per product).
+//
+// Numerics. An fp32 tensor X is stored as two fp16 planes of X * 2^s: hi = fp16(X 2^s), lo = fp16(X 2^s -
+// hi) (the difference is exact in fp32), with 2^s chosen from a bound |X| < 2^E as 2^(14 - E): every
+// element fits fp16's range, and hi + lo carries 22 significant bits (|hi + lo - X 2^s| <= 2^-23 |X 2^s|)
+// for |X| >= 2^(E - 17); smaller elements keep an absolute error below 2^(E - 39). A product is then
+//   a b ~= (ah + al)(bh + bl) ~= ah bh + ah bl + al bh      (al bl <= 2^-22 |a b| is dropped),
+// three exact fp16 x fp16 MFMA products accumulated in fp32: half the MFMAs of the bf16x3 split, and no
+// split work in the GEMM at all. The three products are ONE fp16 GEMM over a K axis three times as long,
+//   A' = [Ah | Ah | Al],  B' = [Bh ; Bl ; Bh],
+// so the kernels below are plain LDS-DMA fp16 GEMMs whose K-step t reads plane pair (t / nk) of
+// {(h, h), (h, l), (l, h)}; the epilogue multiplies by 2^-(sA + sB).
+// Reference numerics: the reference's fp32 nn.Linear on the CPU (/root/reference/simple_distributed.py:63-64,
+// :75-77); tests/test_gemm_x2_gpu.py compares against fp64 within the fp32 GEMM error bound.
+//
+// Kernels:
+//   x2_split_kernel   fp32 [M][K] -> planes [2][M][K] (K % 8 == 0), scale from a bound (a max over `namax` floats:
+//                     a torch inf-norm, the producing GEMM's per-wave maxima or the head's per-block bounds)
+//   x2_gemm_kernel    C[M][N] = A'[M][K'] . op(B') : BL = 0 "NT" (B [N][K], forward), BL = 1 "NN" (B [K][N],
+//                     input gradient); 256 x 256 tile, 8 waves of 128 x 64 (v_mfma_f32_16x16x32_f16),
+//                     K-step 64 by LDS-DMA into 2 x 64 KiB stages (gemm_bf16.hip's 2-phase loop and swizzles);
+//                     fp32 epilogue through LDS (16-B row stores): bias, ReLU, ReLU mask of the layer input,
+//                     per-wave max |C| for the consumer's split
+//   x2_wgrad_kernel   gW[N][K] += sum_m dz[m][n] x[m][k] (both operands k-major, hardware transpose reads),
+//                     the 3 plane pairs as 3 token segments split over workgroups, fp32 slabs reduced in a
+//                     fixed order (deterministic) with the bias gradient (column sums of dz: hi in segment 0,
+//                     lo in segment 2)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "kernels.h"
+
+namespace sdml {
+namespace {
+
+typedef unsigned short u16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef u16 u16x4 __attribute__((ext_vector_type(4)));
+typedef u16 u16x8 __attribute__((ext_vector_type(8)));
+
+// exponent E with |v| < 2^E for finite v >= 0, clamped so 2^(14 - E) and 2^(E - 14) stay normal floats
+__device__ __forceinline__ int bound_exp(float v) {
+  const unsigned b = __float_as_uint(v);
+  const int e = (int)((b >> 23) & 0xffu) - 126;
+  return (b & 0x7fffffffu) == 0u ? -100 : min(max(e, -100), 120);
+}
+__device__ __forceinline__ float pow2f(int e) { return __uint_as_float((unsigned)(e + 127) << 23); }
+
+// ================================================================================================
+// split: planes [2][rows][ld] of X * 2^(14 - E); scale_out = 2^(E - 14) (the dequantisation factor)
+__global__ void __launch_bounds__(256) x2_split_kernel(const float* __restrict__ X, int rows, int cols, int ldx,
+                                                       const float* __restrict__ amax, int namax, u16* __restrict__ P,
+                                                       int64_t ps, int ldp, float* __restrict__ scale_out) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < namax; i += 256) m = fmaxf(m, fabsf(amax[i]));
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const int E = bound_exp(m);
+  const float up = pow2f(14 - E);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *scale_out = pow2f(E - 14);
+  // 8 consecutive columns per thread (cols % 8 == 0): two 16-B loads, one 16-B store per plane
+  const unsigned c8 = (unsigned)cols / 8u;
+  const unsigned n8 = (unsigned)rows * c8;
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n8; i += gridDim.x * 256u) {
+    const unsigned r = i / c8, c = 8u * (i - r * c8);
+    const float* src = X + (int64_t)r * ldx + c;
+    const f32x4 v0 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src));
+    const f32x4 v1 = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src) + 1);
+    u16x8 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = (e < 4 ? v0[e] : v1[e - 4]) * up;  // exact (power of two)
+      const _Float16 h = static_cast<_Float16>(x);
+      hi[e] = __builtin_bit_cast(u16, h);
+      lo[e] = __builtin_bit_cast(u16, static_cast<_Float16>(x - static_cast<float>(h)));
+    }
+    *reinterpret_cast<u16x8*>(P + (int64_t)r * ldp + c) = hi;
+    *reinterpret_cast<u16x8*>(P + ps + (int64_t)r * ldp + c) = lo;
+  }
+}
+
+// ================================================================================================
+// GEMM
+constexpr int GT = 512, TM = 256, TN = 256, TK = 64;
+constexpr int A_BYTES = TM * TK * 2;     // 32 KiB
+constexpr int STAGE = 2 * A_BYTES;       // A + B
+constexpr int SMEM = 2 * STAGE;          // 128 KiB
+constexpr int GLDS = STAGE / 1024 / 8;   // DMA instructions per wave per stage (8)
+
+enum : int { X2_RELU = 1, X2_MASK = 2 };
+
+struct X2Gemm {
+  const u16* A;  // plane 0 (hi) [M][lda]; plane 1 (lo) at A + a_ps
+  const u16* B;  // NT: [N][ldb]; NN: [K][ldb]; plane 1 at B + b_ps
+  int64_t a_ps, b_ps;
+  float* C;
+  const float* bias;  // [N] or nullptr
+  const float* mask;  // X2_MASK: [M][ldm], C element kept where mask > 0
+  const float* sa;    // dequantisation factors 2^(E - 14) of A and B (device scalars, x2_split)
+  const float* sb;
+  float* wmax;        // optional [grid][8]: per-wave max |C| (after the epilogue ops)
+  int M, N, K, lda, ldb, ldc, ldm;
+  int tiles_m, tiles_n;
+};
+
+__device__ __forceinline__ void glds16(const void* src, unsigned char* lds_block) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_block, 16, 0, 0);
+}
+
+__device__ __forceinline__ int rk_swz(int r) { return (r >> 1) & 7; }                          // [rows][64]
+__device__ __forceinline__ int kn_swz(int r) { return ((r & 3) | ((r >> 1) & 4)) << 1; }       // [64][256]
+
+// K-step t of the extended K axis: plane pair (t / nk) of {(hi, hi), (hi, lo), (lo, hi)}, k0 in the segment
+template <int BL>
+__device__ __forceinline__ void issue_stage(const X2Gemm& p, unsigned char* st, int m0, int n0, int t, int nk,
+                                            int wave, int lane) {
+  const int seg = t / nk, k0 = (t - seg * nk) * TK;
+  const u16* A = p.A + (seg == 2 ? p.a_ps : 0);
+  const u16* B = p.B + (seg == 1 ? p.b_ps : 0);
+#pragma unroll
+  for (int u = 0; u < GLDS / 2; ++u) {  // A: 32 instructions of 8 rows x 128 B
+    const int q = wave + 8 * u;
+    const int r = 8 * q + (lane >> 3);
+    const int c = (lane & 7) ^ rk_swz(r);
+    const int gr = min(m0 + r, p.M - 1);
+    glds16(A + (size_t)gr * p.lda + k0 + 8 * c, st + 1024 * q);
+  }
+#pragma unroll
+  for (int u = 0; u < GLDS / 2; ++u) {
+    const int q = wave + 8 * u;
+    if constexpr (BL == 0) {  // B [N][K]: like A
+      const int r = 8 * q + (lane >> 3);
+      const int c = (lane & 7) ^ rk_swz(r);
+      const int gr = min(n0 + r, p.N - 1);
+      glds16(B + (size_t)gr * p.ldb + k0 + 8 * c, st + A_BYTES + 1024 * q);
+    } else {  // B [K][N]: 2 k-rows x 512 B
+      const int r = 2 * q + (lane >> 5);
+      const int c = (lane & 31) ^ kn_swz(r);
+      const int gc = min(n0 + 8 * c, p.N - 8);
+      glds16(B + (size_t)(k0 + r) * p.ldb + gc, st + A_BYTES + 1024 * q);
+    }
+  }
+}
+
+__device__ __forceinline__ f16x8 ld_b128(const unsigned char* p) { return *reinterpret_cast<const f16x8*>(p); }
+__device__ __forceinline__ s16x4 ds_tr16(const unsigned char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+// fp32 epilogue: each wave's 128 x 64 tile in two 64-row halves through a wave-private [64][64] fp32 LDS
+// image (16-B chunk c of row r at c ^ (((r >> 2) & 3) << 2): conflict-free writes from the MFMA layout
+// and conflict-free 16-B row reads), then every lane moves whole 16-B row pieces
+template <int EPI>
+__device__ __forceinline__ void x2_epilogue(const X2Gemm& p, const f32x4 (&acc)[8][4], unsigned char* smem, int m0,
+                                            int n0, int wave, int lane) {
+  const int wm = wave >> 2, wn = wave & 3;
+  const int g = lane >> 4, l16 = lane & 15;
+  float* W = reinterpret_cast<float*>(smem) + wave * (64 * 64);
+  const float sc = *p.sa * *p.sb;
+  const int ch = lane & 15;
+  const int gcol = n0 + wn * 64 + 4 * ch;
+  f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias && gcol < p.N) bv = *reinterpret_cast<const f32x4*>(p.bias + gcol);
+  float vmax = 0.f;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    if (hh) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // half 0's reads done before the overwrite
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * i + 4 * g + r, col = 16 * j + l16;
+          W[row * 64 + 4 * ((col >> 2) ^ (((row >> 2) & 3) << 2)) + (col & 3)] = acc[4 * hh + i][j][r];
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int rr = 4 * it + (lane >> 4);
+      f32x4 v = *reinterpret_cast<const f32x4*>(W + rr * 64 + 4 * (ch ^ (((rr >> 2) & 3) << 2)));
+      const int grow = m0 + wm * 128 + 64 * hh + rr;
+      if (grow >= p.M || gcol >= p.N) continue;  // (N % 4 == 0: a chunk is all in or all out)
+      v = v * sc + bv;
+      if constexpr (EPI & X2_RELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if constexpr (EPI & X2_MASK) {
+        const f32x4 mk = *reinterpret_cast<const f32x4*>(p.mask + (size_t)grow * p.ldm + gcol);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = mk[e] > 0.f ? v[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) vmax = fmaxf(vmax, fabsf(v[e]));
+      *reinterpret_cast<f32x4*>(p.C + (size_t)grow * p.ldc + gcol) = v;
+    }
+  }
+  if (p.wmax) {
+    for (int off = 32; off > 0; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off));
+    if (lane == 0) p.wmax[(size_t)blockIdx.x * 8 + wave] = vmax;
+  }
+}
+
+template <int BL, int EPI>
+__global__ void __launch_bounds__(GT) x2_gemm_kernel(X2Gemm p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  const int nwg = p.tiles_m * p.tiles_n;
+  int wg = blockIdx.x;
+  if (nwg >= 16) {  // XCD-aware bijective remap: blocks sharing an XCD get consecutive tile ids
+    const int q = nwg / 8, r = nwg % 8, xcd = wg % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
+  }
+  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;  // M fastest: neighbours share the B panel
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, l16 = lane & 15;
+  int aoff[2][8];  // [substep][m-tile]: A row wm*128 + 16 i + l16, chunk 4 s + g
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = wm * 128 + 16 * i + l16;
+      aoff[s][i] = r * 128 + 16 * ((4 * s + g) ^ rk_swz(r));
+    }
+  int boff[2][4][2];  // NT: [s][j][0]; NN: the two transposed reads
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (BL == 0) {
+        const int r = wn * 64 + 16 * j + l16;
+        boff[s][j][0] = A_BYTES + r * 128 + 16 * ((4 * s + g) ^ rk_swz(r));
+        boff[s][j][1] = 0;
+      } else {
+        const int q = l16 >> 2, pp = l16 & 3;
+        const int n = wn * 64 + 16 * j + 4 * pp;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int r = 32 * s + 8 * g + 4 * h + q;
+          boff[s][j][h] = A_BYTES + r * 512 + 16 * ((n >> 3) ^ kn_swz(r)) + 2 * (n & 7);
+        }
+      }
+    }
+
+  const int nkseg = p.K / TK, nk = 3 * nkseg;
+  issue_stage<BL>(p, smem, m0, n0, 0, nkseg, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const unsigned char* st = smem + (t & 1) * STAGE;
+    if (t + 1 < nk) issue_stage<BL>(p, smem + ((t + 1) & 1) * STAGE, m0, n0, t + 1, nkseg, wave, lane);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      f16x8 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (BL == 0) {
+          b[j] = ld_b128(st + boff[s][j][0]);
+        } else {
+          const s16x4 lo = ds_tr16(st + boff[s][j][0]), hi = ds_tr16(st + boff[s][j][1]);
+          b[j] = __builtin_bit_cast(f16x8, s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const f16x8 a = ld_b128(st + aoff[s][i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  x2_epilogue<EPI>(p, acc, smem, m0, n0, wave, lane);
+}
+
+// ================================================================================================
+// weight gradient: gW[M][N] += sum_t A[t][m] B[t][n] with A = dz planes [T][lda], B = x planes [T][ldb]
+// (gemm_bf16_wgrad.hip's geometry: 256 x 128 tile, 8 waves of 64 x 64, 32x32x16 MFMAs, register-staged
+// k-major images read by ds_read_b64_tr_b16). Split s covers tokens [sub * tps, ...) of plane pair
+// seg = s / sps.
+constexpr int WNT = 512, WBM = 256, WBN = 128, WBK = 64;
+constexpr int IMG = WBK * 128;  // u16 per 128-column image
+
+struct X2Wg {
+  const u16* A;  // dz planes
+  const u16* B;  // x planes
+  int64_t a_ps, b_ps;
+  float* slab;  // [splits][M][N] fp32, then [splits][M] bias partials
+  int M, N, T, lda, ldb;
+  int tps, sps, splits;  // tokens per split, splits per plane pair, total splits (3 sps)
+  int tiles_m, tiles_n;
+};
+
+__device__ __forceinline__ int km_off(int k, int ch) { return k * 128 + 8 * (ch ^ (((k & 3) << 2) | ((k >> 2) & 3))); }
+
+__device__ __forceinline__ f16x8 trfrag(const u16* P, int c0, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int k = 16 * s + 8 * (g >> 1) + q;
+  const int col = c0 + 16 * (g & 1) + 4 * pp;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(P + km_off(k, col >> 3) + (col & 7)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(P + km_off(k + 4, col >> 3) + (col & 7)));
+  return __builtin_bit_cast(f16x8, s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+}
+
+__device__ __forceinline__ float h2f(u16 v) { return static_cast<float>(__builtin_bit_cast(_Float16, v)); }
+
+template <int COLS>
+struct KmTile {
+  static constexpr int CPR = COLS / 8;      // chunks per k-row
+  static constexpr int NV = WBK * CPR / WNT;  // chunks per thread
+  u16x8 v[NV];
+  __device__ __forceinline__ void load(const u16* __restrict__ P, int ld, int cols, int c0, int k0, int T) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int id = threadIdx.x + WNT * u;
+      const int k = min(k0 + id / CPR, T - 1);
+      const int c = min(c0 + 8 * (id % CPR), cols - 8);
+      v[u] = *reinterpret_cast<const u16x8*>(P + (size_t)k * ld + c);
+    }
+  }
+  template <bool ROWSUM>
+  __device__ __forceinline__ void store(u16* L, int k0, int kend, float (&colsum)[8]) const {
+    const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int id = threadIdx.x + WNT * u;
+      const int k = id / CPR, ch = id % CPR;
+      const u16x8 val = (k0 + k < kend) ? v[u] : z;
+      *reinterpret_cast<u16x8*>(L + (ch >> 4) * IMG + km_off(k, ch & 15)) = val;
+      if constexpr (ROWSUM) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) colsum[e] += h2f(val[e]);
+      }
+    }
+  }
+};
+
+template <bool BIAS>
+__global__ void __launch_bounds__(WNT) x2_wgrad_kernel(X2Wg p) {
+  constexpr int BUF = 3 * IMG;  // A: two 128-col images, B: one
+  __shared__ __attribute__((aligned(16))) u16 smem[2 * BUF];
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int nwg = ntiles * p.splits;
+  const int orig = blockIdx.x;
+  int wg = orig;
+  if (nwg >= 16) {
+    const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  }
+  const int split = wg / ntiles, tile = wg % ntiles;
+  const int seg = split / p.sps, sub = split - seg * p.sps;
+  const u16* A = p.A + (seg == 2 ? p.a_ps : 0);
+  const u16* B = p.B + (seg == 1 ? p.b_ps : 0);
+  const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
+  const int m0 = tm * WBM, n0 = tn * WBN;
+  const int kbeg = sub * p.tps, kend = min(p.T, kbeg + p.tps);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave & 3, wn = wave >> 2;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+
+  KmTile<WBM> ta;
+  KmTile<WBN> tb;
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float dummy[8];
+  const bool do_bias = BIAS && tn == 0 && seg != 1;  // dz hi (segment 0) + dz lo (segment 2)
+  const int nk = kend > kbeg ? (kend - kbeg + WBK - 1) / WBK : 0;
+  if (nk > 0) {
+    ta.load(A, p.lda, p.M, m0, kbeg, p.T);
+    tb.load(B, p.ldb, p.N, n0, kbeg, p.T);
+    if (do_bias) ta.template store<true>(smem, kbeg, kend, cs);
+    else ta.template store<false>(smem, kbeg, kend, dummy);
+    tb.template store<false>(smem + 2 * IMG, kbeg, kend, dummy);
+    ta.load(A, p.lda, p.M, m0, kbeg + WBK, p.T);
+    tb.load(B, p.ldb, p.N, n0, kbeg + WBK, p.T);
+  }
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const u16* L = smem + (t & 1) * BUF;
+    u16* Ln = smem + ((t + 1) & 1) * BUF;
+#pragma unroll
+    for (int s = 0; s < WBK / 16; ++s) {
+      f16x8 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = trfrag(L + (wm >> 1) * IMG, (wm & 1) * 64 + 32 * i, s, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = trfrag(L + 2 * IMG, wn * 64 + 32 * j, s, lane);
+      if (s == 0) {  // tile t+1 (registers) -> the other buffer; tile t+2 -> registers
+        if (do_bias) ta.template store<true>(Ln, kbeg + (t + 1) * WBK, kend, cs);
+        else ta.template store<false>(Ln, kbeg + (t + 1) * WBK, kend, dummy);
+        tb.template store<false>(Ln + 2 * IMG, kbeg + (t + 1) * WBK, kend, dummy);
+        ta.load(A, p.lda, p.M, m0, kbeg + (t + 2) * WBK, p.T);
+        tb.load(B, p.ldb, p.N, n0, kbeg + (t + 2) * WBK, p.T);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  if (BIAS && tn == 0) {  // every tn == 0 block writes its bias partial (0 for segment 1)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [16][256]
+    const int chn = threadIdx.x & 31, part = threadIdx.x >> 5;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[part * 256 + 8 * chn + e] = cs[e];
+    __syncthreads();
+    if (threadIdx.x < WBM) {
+      float sum = 0.f;
+      for (int q = 0; q < 16; ++q) sum += red[q * 256 + threadIdx.x];
+      const int m = m0 + threadIdx.x;
+      if (m < p.M) p.slab[(size_t)p.splits * p.M * p.N + (size_t)split * p.M + m] = sum;
+    }
+  }
+
+  // partial tile -> slab; C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  const int h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+      if (col >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= p.M) continue;
+        p.slab[((size_t)split * p.M + row) * p.N + col] = acc[i][j][r];
+      }
+    }
+}
+
+// gW[m][n] (fp32) += sa sb sum_s slab[s][m][n] (fixed order); gb[m] += sa sum_{s not in pair 1} bias_slab[s][m]
+__global__ void __launch_bounds__(256) x2_wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int sps,
+                                                              int M, int N, float* __restrict__ C, int ldc,
+                                                              float* __restrict__ gb, const float* __restrict__ sa,
+                                                              const float* __restrict__ sb) {
+  const float da = *sa, dq = da * *sb;
+  const int64_t MN = (int64_t)M * N;
+  if (gb) {
+    const float* bs = slab + (size_t)splits * MN;
+    for (int64_t m = blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
+      float s = 0.f;
+      for (int k = 0; k < splits; ++k)
+        if (k / sps != 1) s += bs[(size_t)k * M + m];
+      gb[m] += da * s;
+    }
+  }
+  const int64_t n4 = MN / 4;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    f32x4 s = *reinterpret_cast<const f32x4*>(slab + 4 * i);
+    for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(slab + k * MN + 4 * i);
+    const int64_t e = 4 * i;
+    const int m = (int)(e / N), n = (int)(e % N);
+    f32x4* dst = reinterpret_cast<f32x4*>(C + (size_t)m * ldc + n);
+    *dst += s * dq;
+  }
+}
+
+int x2_wgrad_sps(int M, int N, int T) {
+  const int tiles = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
+  int s = std::max(1, 256 / (3 * tiles));  // 3 plane pairs x sps splits x tiles ~ one grid wave
+  const int max_by_t = std::max(1, T / (8 * WBK));
+  return std::min(s, max_by_t);
+}
+
+}  // namespace
+
+bool x2_gemm_supported(int M, int N, int K, int lda, int ldb, int ldc, bool b_kn) {
+  return M >= 1 && N >= 8 && K >= TK && K % TK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0 &&
+         (b_kn ? ldb >= N : ldb >= K) && lda >= K && ldc >= N;
+}
+
+int x2_gemm_wmax_slots(int M, int N) { return ((M + TM - 1) / TM) * ((N + TN - 1) / TN) * 8; }
+
+void x2_split(const float* X, int rows, int cols, int ldx, const float* amax, int namax, void* planes, int64_t ps,
+              int ldp, float* scale_out, hipStream_t stream) {
+  const int64_t n8 = (int64_t)rows * (cols / 8);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n8 + 255) / 256, 4096));
+  hipLaunchKernelGGL(x2_split_kernel, dim3(blocks), dim3(256), 0, stream, X, rows, cols, ldx, amax, namax,
+                     static_cast<u16*>(planes), ps, ldp, scale_out);
+}
+
+void x2_gemm(const void* A, int64_t a_ps, const void* B, int64_t b_ps, float* C, int M, int N, int K, int lda, int ldb,
+             int ldc, bool b_kn, const float* sa, const float* sb, const float* bias, bool relu, const float* mask,
+             int ldm, float* wmax, hipStream_t stream) {
+  X2Gemm p;
+  p.A = static_cast<const u16*>(A);
+  p.B = static_cast<const u16*>(B);
+  p.a_ps = a_ps;
+  p.b_ps = b_ps;
+  p.C = C;
+  p.bias = bias;
+  p.mask = mask;
+  p.sa = sa;
+  p.sb = sb;
+  p.wmax = wmax;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = ldb;
+  p.ldc = ldc;
+  p.ldm = ldm;
+  p.tiles_m = (M + TM - 1) / TM;
+  p.tiles_n = (N + TN - 1) / TN;
+  const dim3 grid(p.tiles_m * p.tiles_n);
+  const int epi = (relu ? X2_RELU : 0) | (mask ? X2_MASK : 0);
+#define X2_LAUNCH(BLV, E) hipLaunchKernelGGL((x2_gemm_kernel<BLV, E>), grid, dim3(GT), 0, stream, p)
+#define X2_EPI(BLV)                                            \
+  do {                                                         \
+    switch (epi) {                                             \
+      case X2_RELU: X2_LAUNCH(BLV, X2_RELU); break;            \
+      case X2_MASK: X2_LAUNCH(BLV, X2_MASK); break;            \
+      case X2_RELU | X2_MASK: X2_LAUNCH(BLV, X2_RELU | X2_MASK); break; \
+      default: X2_LAUNCH(BLV, 0); break;                       \
+    }                                                          \
+  } while (0)
+  if (b_kn) X2_EPI(1);
+  else X2_EPI(0);
+#undef X2_EPI
+#undef X2_LAUNCH
+}
+
+bool x2_wgrad_supported(int M, int N, int T, int lda, int ldb) {
+  return M >= 8 && N >= 8 && T >= 1 && M % 8 == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0;
+}
+
+size_t x2_wgrad_workspace_floats(int M, int N, int T) {
+  const int splits = 3 * x2_wgrad_sps(M, N, T);
+  return (size_t)splits * M * N + (size_t)splits * M;
+}
+
+void x2_wgrad(const void* dz, int64_t dz_ps, const void* x, int64_t x_ps, const float* sdz, const float* sx, float* gw,
+              int ldc, float* gb, float* workspace, int M, int N, int T, int lda, int ldb, hipStream_t stream) {
+  X2Wg p;
+  p.A = static_cast<const u16*>(dz);
+  p.B = static_cast<const u16*>(x);
+  p.a_ps = dz_ps;
+  p.b_ps = x_ps;
+  p.slab = workspace;
+  p.M = M;
+  p.N = N;
+  p.T = T;
+  p.lda = lda;
+  p.ldb = ldb;
+  int sps = x2_wgrad_sps(M, N, T);
+  int tps = (T + sps - 1) / sps;
+  tps = (tps + WBK - 1) / WBK * WBK;
+  sps = (T + tps - 1) / tps;  // (never more than x2_wgrad_sps: the workspace was sized with it)
+  p.tps = tps;
+  p.sps = sps;
+  p.splits = 3 * sps;
+  p.tiles_m = (M + WBM - 1) / WBM;
+  p.tiles_n = (N + WBN - 1) / WBN;
+  const dim3 grid(p.tiles_m * p.tiles_n * p.splits);
+  if (gb) hipLaunchKernelGGL(x2_wgrad_kernel<true>, grid, dim3(WNT), 0, stream, p);
+  else hipLaunchKernelGGL(x2_wgrad_kernel<false>, grid, dim3(WNT), 0, stream, p);
+  const int64_t n4 = (int64_t)M * N / 4;
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(x2_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, workspace, p.splits, sps, M, N, gw,
+                     ldc, gb, sdz, sx);
+}
+
+}  // namespace sdml

@@ -269,6 +269,25 @@ bool gemm_bf16_supported(int M, int N, int K, int lda, int ldb, int ldc, bool b_
 void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool b_kn,
                int epi, const void* bias, void* aux, int ldaux, hipStream_t stream);
 
+// ---- fp32-accurate GEMMs from pre-split fp16 planes (gemm_f16x2.hip) ---------------------------
+// An fp32 tensor X [rows][cols] becomes planes [2][rows][ldp] (hi, lo of X * 2^(14 - E), |X| < 2^E from
+// the max of |amax[0..namax)|); scale_out receives 2^(E - 14). Products use 3 fp16 MFMA products.
+void x2_split(const float* X, int rows, int cols, int ldx, const float* amax, int namax, void* planes, int64_t ps,
+              int ldp, float* scale_out, hipStream_t stream);
+// C[M][N] (fp32) = sa sb A'[M][K] . (b_kn ? B'[K][N] : B'[N][K]^T) (+ bias[n]) (relu) (* (mask[m][n] > 0));
+// A/B: plane 0, plane 1 at + a_ps / b_ps (elements). wmax (optional, x2_gemm_wmax_slots floats): per-wave
+// max |C|, a bound source for the next x2_split. K % 64 == 0, N % 8 == 0 (x2_gemm_supported).
+bool x2_gemm_supported(int M, int N, int K, int lda, int ldb, int ldc, bool b_kn);
+int x2_gemm_wmax_slots(int M, int N);
+void x2_gemm(const void* A, int64_t a_ps, const void* B, int64_t b_ps, float* C, int M, int N, int K, int lda, int ldb,
+             int ldc, bool b_kn, const float* sa, const float* sb, const float* bias, bool relu, const float* mask,
+             int ldm, float* wmax, hipStream_t stream);
+// gw[M][N] (fp32, ldc) += sdz sx sum_t dz'[t][m] x'[t][n]; gb (optional) [M] += sdz sum_t dz'[t][m]
+bool x2_wgrad_supported(int M, int N, int T, int lda, int ldb);
+size_t x2_wgrad_workspace_floats(int M, int N, int T);
+void x2_wgrad(const void* dz, int64_t dz_ps, const void* x, int64_t x_ps, const float* sdz, const float* sx, float* gw,
+              int ldc, float* gb, float* workspace, int M, int N, int T, int lda, int ldb, hipStream_t stream);
+
 // ---- weight gradient of a bf16 Linear: gw[M,N] (bf16) += gy[T,M]^T x[T,N] -------------------
 // fp32 accumulation, token range split over workgroups, deterministic slab reduction.
 // workspace: wgrad_bf16_workspace_floats(M, N, T) fp32 (0 = none needed)

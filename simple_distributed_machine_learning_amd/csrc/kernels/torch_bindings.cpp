@@ -397,6 +397,100 @@ void wgrad_bf16_(torch::Tensor gy, torch::Tensor x, torch::Tensor gw, c10::optio
                    gy.stride(0), x.stride(0), gw.stride(0), cur_stream());
 }
 
+// ---- fp32-accurate GEMMs from pre-split fp16 planes (gemm_f16x2.hip) ----
+// x [R, C] fp32 (unit column stride) -> (planes int16 [2, R, C], scale fp32 [1] = 2^(E - 14)); amax: any fp32
+// device tensor whose max |.| bounds |x| (an inf-norm, a producer's per-wave maxima, the head's bounds)
+std::tuple<torch::Tensor, torch::Tensor> x2_split_op(torch::Tensor x, torch::Tensor amax) {
+  check_f32_cuda(x, "x");
+  check_f32_cuda(amax, "amax");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(1) % 8 == 0 && x.stride(0) % 4 == 0 &&
+                  x.numel() < (int64_t(1) << 34),
+              "x2_split: 2-D row-major fp32 with a multiple of 8 columns (and < 2^34 elements) expected");
+  TORCH_CHECK(amax.is_contiguous() && amax.numel() >= 1, "x2_split: amax must be a non-empty contiguous tensor");
+  const int64_t R = x.size(0), C = x.size(1);
+  auto planes = torch::empty({2, R, C}, x.options().dtype(torch::kInt16));
+  auto scale = torch::empty({1}, x.options());
+  if (R > 0)
+    sdml::x2_split(x.data_ptr<float>(), (int)R, (int)C, (int)x.stride(0), amax.data_ptr<float>(), (int)amax.numel(),
+                   planes.data_ptr(), R * C, (int)C, scale.data_ptr<float>(), cur_stream());
+  return {planes, scale};
+}
+
+static void check_planes(const torch::Tensor& p, const char* name) {
+  TORCH_CHECK(p.is_cuda() && p.scalar_type() == torch::kInt16 && p.dim() == 3 && p.size(0) == 2 && p.is_contiguous(),
+              name, ": planes must be a contiguous int16 [2, rows, cols] device tensor (x2_split)");
+}
+
+// C = sa sb A' . (b_kn ? B' : B'^T) (+ bias) (relu) (* (mask > 0)); A planes [2, M, K], B planes [2, N, K] or
+// [2, K, N]. Returns (C fp32 [M, N], per-wave max |C| or None)
+std::tuple<torch::Tensor, c10::optional<torch::Tensor>> x2_gemm_op(torch::Tensor A, torch::Tensor sa, torch::Tensor B,
+                                                                   torch::Tensor sb, bool b_kn,
+                                                                   c10::optional<torch::Tensor> bias, bool relu,
+                                                                   c10::optional<torch::Tensor> mask, bool want_wmax) {
+  check_planes(A, "x2_gemm A");
+  check_planes(B, "x2_gemm B");
+  check_f32_cuda(sa, "sa");
+  check_f32_cuda(sb, "sb");
+  const int64_t M = A.size(1), K = A.size(2), N = b_kn ? B.size(2) : B.size(1);
+  TORCH_CHECK((b_kn ? B.size(1) : B.size(2)) == K, "x2_gemm: inner dimensions ", A.sizes(), " vs ", B.sizes());
+  TORCH_CHECK(sdml::x2_gemm_supported((int)M, (int)N, (int)K, (int)K, (int)B.size(2), (int)N, b_kn),
+              "x2_gemm: unsupported shape (x2_gemm_supported)");
+  auto C = torch::empty({M, N}, A.options().dtype(torch::kFloat32));
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_f32_cuda(*bias, "bias");
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == N, "x2_gemm: bias shape");
+    bp = bias->data_ptr<float>();
+  }
+  const float* mp = nullptr;
+  int64_t ldm = 0;
+  if (mask.has_value() && mask->defined()) {
+    check_f32_cuda(*mask, "mask");
+    TORCH_CHECK(mask->dim() == 2 && mask->size(0) == M && mask->size(1) == N && mask->stride(1) == 1 &&
+                    mask->stride(0) % 4 == 0,
+                "x2_gemm: mask must be a row-major fp32 [M, N] tensor");
+    mp = mask->data_ptr<float>();
+    ldm = mask->stride(0);
+  }
+  c10::optional<torch::Tensor> wm;
+  if (want_wmax) wm = torch::empty({(int64_t)sdml::x2_gemm_wmax_slots((int)M, (int)N)}, C.options());
+  if (M > 0)
+    sdml::x2_gemm(A.data_ptr(), M * K, B.data_ptr(), B.size(1) * B.size(2), C.data_ptr<float>(), (int)M, (int)N,
+                  (int)K, (int)K, (int)B.size(2), (int)N, b_kn, sa.data_ptr<float>(), sb.data_ptr<float>(), bp, relu, mp,
+                  (int)ldm, want_wmax ? wm->data_ptr<float>() : nullptr, cur_stream());
+  return {C, wm};
+}
+
+bool x2_gemm_supported_op(int64_t M, int64_t N, int64_t K, bool b_kn) {
+  return sdml::x2_gemm_supported((int)M, (int)N, (int)K, (int)K, (int)(b_kn ? N : K), (int)N, b_kn);
+}
+
+// gw [M, N] (fp32) += sdz sx dz'^T x'; gb [M] += sdz colsum(dz'). dz planes [2, T, M], x planes [2, T, N]
+void x2_wgrad_(torch::Tensor dz, torch::Tensor sdz, torch::Tensor x, torch::Tensor sx, torch::Tensor gw,
+               c10::optional<torch::Tensor> gb) {
+  check_planes(dz, "x2_wgrad dz");
+  check_planes(x, "x2_wgrad x");
+  check_f32_cuda(sdz, "sdz");
+  check_f32_cuda(sx, "sx");
+  check_f32_cuda(gw, "gw");
+  const int64_t T = dz.size(1), M = dz.size(2), N = x.size(2);
+  TORCH_CHECK(x.size(1) == T && gw.dim() == 2 && gw.size(0) == M && gw.size(1) == N && gw.stride(1) == 1 &&
+                  gw.stride(0) % 4 == 0 && N % 4 == 0,
+              "x2_wgrad_: shape mismatch");
+  TORCH_CHECK(sdml::x2_wgrad_supported((int)M, (int)N, (int)T, (int)M, (int)N), "x2_wgrad_: unsupported shape");
+  float* gbp = nullptr;
+  if (gb.has_value() && gb->defined()) {
+    check_f32_cuda(*gb, "gb");
+    TORCH_CHECK(gb->is_contiguous() && gb->numel() == M, "x2_wgrad_: gb must be a contiguous fp32 [M] tensor");
+    gbp = gb->data_ptr<float>();
+  }
+  if (T == 0) return;
+  auto ws = torch::empty({(int64_t)sdml::x2_wgrad_workspace_floats((int)M, (int)N, (int)T)}, gw.options());
+  sdml::x2_wgrad(dz.data_ptr(), T * M, x.data_ptr(), T * N, sdz.data_ptr<float>(), sx.data_ptr<float>(),
+                 gw.data_ptr<float>(), (int)gw.stride(0), gbp, ws.data_ptr<float>(), (int)M, (int)N, (int)T, (int)M,
+                 (int)N, cur_stream());
+}
+
 bool wgrad_bf16_supported_op(int64_t M, int64_t N, int64_t T) {
   return sdml::wgrad_bf16_supported(M, N, T, M, N, N);
 }
@@ -1485,6 +1579,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_bf16", &gemm_bf16_op, "bf16 GEMM with fused bias / bias+GELU / GELU-backward epilogues",
         py::arg("A"), py::arg("B"), py::arg("bias") = py::none(), py::arg("b_kn") = false, py::arg("epi") = 0,
         py::arg("aux") = py::none());
+  m.def("x2_split", &x2_split_op, "fp32 -> two fp16 planes of x * 2^(14 - E) (+ the dequantisation scale)",
+        py::arg("x"), py::arg("amax"));
+  m.def("x2_gemm", &x2_gemm_op, "fp32-accurate GEMM from fp16 planes (3 MFMA products) with fused epilogues",
+        py::arg("A"), py::arg("sa"), py::arg("B"), py::arg("sb"), py::arg("b_kn") = false,
+        py::arg("bias") = py::none(), py::arg("relu") = false, py::arg("mask") = py::none(),
+        py::arg("want_wmax") = false);
+  m.def("x2_gemm_supported", &x2_gemm_supported_op, "shape check for x2_gemm (M, N, K, b_kn)");
+  m.def("x2_wgrad_", &x2_wgrad_, "gw += dz^T x, gb += colsum(dz) from fp16 planes (fp32-accurate)",
+        py::arg("dz"), py::arg("sdz"), py::arg("x"), py::arg("sx"), py::arg("gw"), py::arg("gb") = py::none());
   m.def("gemm_bf16_supported", &gemm_bf16_supported_op, "shape check for gemm_bf16 (M, N, K, lda, ldb, b_kn)");
   m.def("mlp_small_step", &mlp_small_step, "784-128-10 MLP training step (fwd, loss, bwd, SGD) in one launch");
   m.def("mlp_small_step_max_batch", &sdml::mlp_small_step_max_batch);

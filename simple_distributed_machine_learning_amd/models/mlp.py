@@ -7,7 +7,8 @@
 
 On a ROCm device every stage runs hand-written gfx950 kernels with no autograd graph:
 
-* hidden layer forward  : fp32 MFMA GEMM with fused bias + ReLU epilogue
+* hidden layer forward  : fp32 MFMA GEMM with fused bias + ReLU epilogue (large shapes: operands split
+                          once into two fp16 planes, 3 MFMA products per product, ops.linear_relu_fwd_x2)
 * hidden layer backward : dX GEMM with the ReLU mask fused into the A-operand load,
                           dW/db split-K MFMA GEMM accumulating straight into the flat grad buffer
 * classifier head       : ONE kernel for fc2 -> log_softmax -> NLL -> backward (dlogits, dW2,
@@ -109,6 +110,7 @@ class MLPStage(PipelineStage):
         elif x.dtype != torch.float32 or not x.is_contiguous():
             x = x.float().contiguous()
         acts = [x]
+        x2 = {}  # layer index -> two-fp16-plane operands kept for its backward (ops.linear_relu_fwd_x2)
         for i, lin in enumerate(self.layers()):
             assert not self._is_classifier(i), "classifier layers run in head_fwd"
             if x.dtype == torch.uint8:
@@ -118,11 +120,17 @@ class MLPStage(PipelineStage):
                 x = ops.linear_relu_fwd_u8(x, lin.weight, lin.bias, cache, epoch, mask_out=m)
                 if m is not None:
                     ctx["mask"] = m
+            elif ops.x2_ok(x, lin.weight):
+                x, pl = ops.linear_relu_fwd_x2(x, lin.weight, lin.bias)
+                if train:
+                    x2[i] = pl
             else:
                 x = ops.linear_relu_fwd(x, lin.weight, lin.bias)
             acts.append(x)
         if train:
             ctx["acts"] = acts
+            if x2:
+                ctx["x2"] = x2
         return x
 
     # Fused-path boundary protocol: the gradient an MLP stage sends back is already multiplied
@@ -133,7 +141,8 @@ class MLPStage(PipelineStage):
         if "acts" not in ctx:
             return super().bwd(grad_y, ctx)
         acts = ctx.pop("acts")
-        g = grad_y.contiguous()
+        x2 = ctx.pop("x2", {})
+        g = grad_y.contiguous() if not grad_y.is_contiguous() else grad_y
         layers = self.layers()
         for i in range(len(layers) - 1, -1, -1):
             lin = layers[i]
@@ -141,8 +150,11 @@ class MLPStage(PipelineStage):
                 ops.linear_wgrad_u8(acts[i], g, lin.weight.grad, lin.bias.grad)
                 return None
             need_dx = (i > 0) or (not self.is_first)
-            g = ops.linear_relu_bwd(acts[i], acts[i + 1], g, lin.weight, lin.weight.grad, lin.bias.grad, need_dx,
-                                    gy_masked=True, mask_dx=need_dx)
+            if i in x2:
+                g = ops.linear_relu_bwd_x2(acts[i], g, lin.weight.grad, lin.bias.grad, x2.pop(i), need_dx, need_dx)
+            else:
+                g = ops.linear_relu_bwd(acts[i], acts[i + 1], g, lin.weight, lin.weight.grad, lin.bias.grad, need_dx,
+                                        gy_masked=True, mask_dx=need_dx)
         return g
 
     # head_fwd(stats=..., stats_init=True) overwrites ``stats`` instead of adding to it (an engine
@@ -161,8 +173,12 @@ class MLPStage(PipelineStage):
             x = x.float().contiguous()
         layers = self.layers()
         acts = [x]
+        x2 = {}
         for i in range(len(layers) - 1):
-            x = ops.linear_relu_fwd(x, layers[i].weight, layers[i].bias)
+            if train and ops.x2_ok(x, layers[i].weight):
+                x, x2[i] = ops.linear_relu_fwd_x2(x, layers[i].weight, layers[i].bias)
+            else:
+                x = ops.linear_relu_fwd(x, layers[i].weight, layers[i].bias)
             acts.append(x)
         head = layers[-1]
         need_dx = train and (len(layers) > 1 or not self.is_first)
@@ -173,6 +189,8 @@ class MLPStage(PipelineStage):
         if train:
             ctx["acts"] = acts
             ctx["dx"] = dx
+            if x2:
+                ctx["x2"] = x2
         return loss, correct, target.numel()
 
     # Factored boundary gradient (rotate placement): the gradient this single-Linear head sends back,
@@ -267,11 +285,16 @@ class MLPStage(PipelineStage):
             return super().head_bwd(ctx)
         acts = ctx.pop("acts")
         g = ctx.pop("dx")
+        x2 = ctx.pop("x2", {})
         layers = self.layers()
         for i in range(len(layers) - 2, -1, -1):
             need_dx = (i > 0) or (not self.is_first)
-            g = ops.linear_relu_bwd(acts[i], acts[i + 1], g, layers[i].weight, layers[i].weight.grad,
-                                    layers[i].bias.grad, need_dx, gy_masked=True, mask_dx=need_dx)
+            if i in x2:
+                g = ops.linear_relu_bwd_x2(acts[i], g, layers[i].weight.grad, layers[i].bias.grad, x2.pop(i), need_dx,
+                                           need_dx)
+            else:
+                g = ops.linear_relu_bwd(acts[i], acts[i + 1], g, layers[i].weight, layers[i].weight.grad,
+                                        layers[i].bias.grad, need_dx, gy_masked=True, mask_dx=need_dx)
         return g
 
 

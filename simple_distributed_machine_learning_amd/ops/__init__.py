@@ -185,6 +185,72 @@ def linear_relu_bwd(x, y, gy, w, gw, gb, need_dx: bool, gy_masked: bool = False,
     return dx
 
 
+# ---- fp32-accurate hidden layers on two fp16 planes (csrc/kernels/gemm_f16x2.hip) -------------------
+# Every operand is split ONCE into fp16 planes (hi, lo of x * 2^s) and each product costs 3 fp16 MFMAs
+# (the bf16x3 engine: 6, with the split redone inside every GEMM). The planes of a layer's input serve its
+# forward (A operand) and its weight gradient (B operand); the weight's planes serve forward and input
+# gradient. Bounds for the splits come from the producing kernel where it has one (the GEMM epilogues'
+# per-wave maxima ``_sdml_wmax``, the head's per-block bounds ``_sdml_amax``), else from an inf-norm pass.
+# SDML_F32_GEMM=x3 keeps the bf16x3 engine (A/B).
+
+_X2_MIN_ROWS = 2048
+
+
+def _x2_env_ok() -> bool:
+    import os
+
+    return os.environ.get("SDML_F32_GEMM", "x2") not in ("x3", "mfma")
+
+
+def x2_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Whether the layer y = x @ w.T runs on the two-plane engine (ROCm fp32, large enough shapes)."""
+    if not (x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 2
+            and x.is_contiguous() and w.is_contiguous() and x.shape[0] >= _X2_MIN_ROWS and _x2_env_ok()):
+        return False
+    M, K = x.shape
+    N = w.shape[0]
+    k = _k()
+    return bool(K % 64 == 0 and N % 64 == 0 and k.x2_gemm_supported(M, N, K, False)
+                and k.x2_gemm_supported(M, K, N, True))
+
+
+def _bound_of(t: torch.Tensor) -> torch.Tensor:
+    b = getattr(t, "_sdml_wmax", None)
+    if b is None:
+        b = getattr(t, "_sdml_amax", None)
+    if b is None:
+        b = torch.linalg.vector_norm(t, float("inf")).reshape(1)
+    return b
+
+
+def x2_split(t: torch.Tensor):
+    """(planes int16 [2, rows, cols], dequantisation scale [1]) of an fp32 matrix."""
+    return _k().x2_split(t, _bound_of(t))
+
+
+def linear_relu_fwd_x2(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], relu: bool = True):
+    """relu(x @ w.T + b) on the two-plane engine. Returns (y, planes) with planes = (x planes, x scale,
+    w planes, w scale) for :func:`linear_relu_bwd_x2`; y carries its per-wave maxima for the next split."""
+    xp, sx = x2_split(x)
+    wp, sw = _k().x2_split(w, torch.linalg.vector_norm(w, float("inf")).reshape(1))
+    y, wm = _k().x2_gemm(xp, sx, wp, sw, False, b, relu, None, True)
+    y._sdml_wmax = wm
+    return y, (xp, sx, wp, sw)
+
+
+def linear_relu_bwd_x2(x: torch.Tensor, gz: torch.Tensor, gw, gb, planes, need_dx: bool, mask_dx: bool):
+    """Backward of y = relu(x @ w.T + b) given gz = dL/d(pre-activation) (already masked): gw += gz.T @ x,
+    gb += sum(gz) and, when ``need_dx``, returns gz @ w (times (x > 0) with ``mask_dx``), all from planes."""
+    xp, sx, wp, sw = planes
+    gp, sg = x2_split(gz.contiguous())
+    dx = None
+    if need_dx:
+        dx, wm = _k().x2_gemm(gp, sg, wp, sw, True, None, False, x if mask_dx else None, True)
+        dx._sdml_wmax = wm
+    _k().x2_wgrad_(gp, sg, xp, sx, gw, gb)
+    return dx
+
+
 def _put_stats(stats, loss, correct, init: bool):
     if init:
         stats[0] = loss

@@ -215,7 +215,22 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
     if (want_mask) mask_out->copy_(relu_bits(y));
     return y;
   };
-  if (!direct) return with_mask(linear_fwd_f32(pixels_f32(x, scale), w, b, relu));
+  // a caller-owned plane cache is marked current by the caller after this call (ops.linear_relu_fwd_u8), so
+  // the paths that do not read it still refresh it when it is stale (a later fused forward+head reads it)
+  auto refresh_cache = [&]() {
+    if (!planes.has_value() || !planes->defined() || planes_valid) return;
+    const int Kp = sdml::u8_fwd_kpad((int)K);
+    TORCH_CHECK(planes->is_cuda() && planes->scalar_type() == torch::kInt16 && planes->is_contiguous() &&
+                    planes->dim() == 3 && planes->size(0) == sdml::kU8FwdPlanes && planes->size(1) == N &&
+                    planes->size(2) == Kp,
+                "linear_fwd_u8: planes must be a [u8_fwd_planes()][N][u8_fwd_kpad(K)] int16 device tensor");
+    sdml::split_planes_pad(w.data_ptr<float>(), reinterpret_cast<unsigned short*>(planes->data_ptr<int16_t>()),
+                           (int)N, (int)K, Kp, cur_stream());
+  };
+  if (!direct) {
+    refresh_cache();
+    return with_mask(linear_fwd_f32(pixels_f32(x, scale), w, b, relu));
+  }
   auto y = torch::empty({M, N}, w.options());
   static const bool legacy = [] {
     const char* e = getenv("SDML_U8_FWD");
@@ -239,6 +254,7 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
                  want_mask ? reinterpret_cast<unsigned*>(mask_out->data_ptr<int32_t>()) : nullptr);
     return y;
   }
+  refresh_cache();
   auto wsplit = torch::empty({3, N, K}, w.options().dtype(torch::kInt16));
   sdml::split3_planes(w.data_ptr<float>(), reinterpret_cast<unsigned short*>(wsplit.data_ptr<int16_t>()), N * K,
                       cur_stream());

@@ -180,3 +180,18 @@ def test_fused_optimizer_step_bitwise_equals_optimizer_step(M, opt, monkeypatch)
     assert torch.equal(p0, p1)
     assert (b0 is None and b1 is None) or torch.equal(b0, b1)
     assert torch.equal(c0, c1)
+
+
+def test_small_batch_forward_keeps_the_plane_cache_current():
+    """A uint8 forward on a batch the uint8 kernel does not take (< 4096 rows: ToTensor + fp32 GEMM) still
+    refreshes a stale weight-plane cache, because ops.linear_relu_fwd_u8 marks it current afterwards and
+    a later fused forward+head reads it (the rotate placement runs the cross rows of a wave that way)."""
+    g = torch.Generator(device="cpu").manual_seed(4)
+    w = (torch.rand(128, 784, generator=g) - 0.5).mul_(0.1).to(DEV)
+    b = torch.rand(128, generator=g).to(DEV)
+    x = torch.randint(0, 256, (2048, 784), generator=g, dtype=torch.uint8).to(DEV)
+    cache, ref = ops.PlaneCache(w), ops.PlaneCache(w)
+    ops.linear_relu_fwd_u8(x, w, b, cache, 0)
+    ops.linear_relu_fwd_u8(torch.cat([x, x]), w, b, ref, 0)  # 4096 rows: the kernel path splits into its cache
+    assert cache.token == ops.PlaneCache.token_of(w, 0)
+    assert torch.equal(cache.planes, ref.planes)

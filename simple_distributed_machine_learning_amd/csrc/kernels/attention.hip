@@ -155,6 +155,12 @@ struct AttnArgs {
   int causal;
 };
 
+// XCD-aware block order: the dispatcher deals consecutive workgroup ids round-robin to the 8 XCDs, so
+// the blocks of one (batch, head) - which all read the same K/V (or Q/dO) tiles - would land on 8
+// different L2s. Logical block L = (id % 8) * (n / 8) + id / 8 keeps consecutive L (same (b, h)) on one
+// XCD (bijective when n % 8 == 0; otherwise the plain order).
+__device__ __forceinline__ int xcd_block(int id, int n) { return (n % 8 == 0) ? (id % 8) * (n / 8) + id / 8 : id; }
+
 // ============================================================================================
 // forward
 template <int KBT>  // keys per tile (64 or 128)
@@ -163,8 +169,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) u16 Ks[2][KBT * HD];
   __shared__ __attribute__((aligned(16))) u16 Vs[2][KBT * HD];
   const int nqb = (a.S + QB - 1) / QB;
-  const int bh = blockIdx.x / nqb;
-  const int qb = nqb - 1 - (blockIdx.x % nqb);  // heaviest (causal) blocks first
+  const int blk = xcd_block(blockIdx.x, gridDim.x);
+  const int bh = blk / nqb;
+  const int qb = nqb - 1 - (blk % nqb);  // heaviest (causal) blocks first
   const int b = bh / a.H, hh = bh % a.H;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31,
             h = lane >> 5;
@@ -309,8 +316,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) u16 Ds[2][TR * HD];
   __shared__ float Ls[2][BQ], Dl[2][BQ];
   const int nkb = (a.S + QB - 1) / QB;
-  const int bh = blockIdx.x / nkb;
-  const int kb = blockIdx.x % nkb;
+  const int blk = xcd_block(blockIdx.x, gridDim.x);
+  const int bh = blk / nkb;
+  const int kb = blk % nkb;
   const int b = bh / a.H, hh = bh % a.H;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31,
             h = lane >> 5;
@@ -427,8 +435,9 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) u16 Ks[2][TR * HD];
   __shared__ __attribute__((aligned(16))) u16 Vs[2][TR * HD];
   const int nqb = (a.S + QB - 1) / QB;
-  const int bh = blockIdx.x / nqb;
-  const int qb = nqb - 1 - (blockIdx.x % nqb);
+  const int blk = xcd_block(blockIdx.x, gridDim.x);
+  const int bh = blk / nqb;
+  const int qb = nqb - 1 - (blk % nqb);
   const int b = bh / a.H, hh = bh % a.H;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), r = lane & 31,
             h = lane >> 5;

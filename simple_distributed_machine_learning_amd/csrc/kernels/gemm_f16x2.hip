@@ -24,13 +24,15 @@
 //                     fp32 epilogue through LDS (16-B row stores): bias, ReLU, ReLU mask of the layer input,
 //                     per-wave max |C| for the consumer's split
 //   x2_wgrad_kernel   gW[N][K] += sum_m dz[m][n] x[m][k] (both operands k-major, hardware transpose reads),
-//                     the 3 plane pairs as 3 token segments split over workgroups, fp32 slabs reduced in a
-//                     fixed order (deterministic) with the bias gradient (column sums of dz: hi in segment 0,
-//                     lo in segment 2)
+//                     the 3 plane pairs as 3 token segments of one extended K axis, cut into equal splits over
+//                     workgroups (one grid wave), fp32 slabs reduced in a fixed order (deterministic) with the
+//                     bias gradient (column sums of dz: hi in segment 0, lo in segment 2)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
+#include <string>
 
 #include "kernels.h"
 
@@ -301,11 +303,194 @@ __global__ void __launch_bounds__(GT) x2_gemm_kernel(X2Gemm p) {
   x2_epilogue<EPI>(p, acc, smem, m0, n0, wave, lane);
 }
 
+// ---- NT form, 4-phase K-step schedule (gemm_bf16.hip's gemm_bf16_nt4_kernel with plane pairs) -----------
+// Each 64-deep K-step runs as 4 phases, one per 64 x 32 quadrant of every wave's 128 x 64 output (16 MFMAs
+// at raised priority); the LDS-DMA prefetch is cut into half-tiles of 128 rows x 64 k (16 KiB) streamed one
+// per phase, 3 in flight behind a counted vmcnt(6); the two wave rows run one barrier apart. Half-tile q of
+// K-step u (h = 4u + q) lives in slot h % 10 (10 x 16 KiB = all 160 KiB): q 0 / 3 = A rows of quadrant-row
+// 0 / 1, q 1 / 2 = B rows of quadrant-col 0 / 1. RAW/WAR reasoning: gemm_bf16.hip.
+constexpr int HT = 16384, NSLOT = 10;
+
+template <int Q>
+__device__ __forceinline__ void issue_half(const X2Gemm& p, unsigned char* smem, int h, int nk, int nkseg, int m0,
+                                           int n0, int wave, int lane) {
+  const int t = min(h >> 2, nk - 1);
+  const int seg = t / nkseg, k0 = (t - seg * nkseg) * TK;
+  unsigned char* slot = smem + (h % NSLOT) * HT;
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    const int qq = wave + 8 * v;          // 1-KiB DMA block of the slot
+    const int lr = 8 * qq + (lane >> 3);  // slot row 0..127
+    const int c = (lane & 7) ^ rk_swz(lr);
+    if constexpr (Q == 0 || Q == 3) {
+      const int tr = (lr >> 6) * 128 + (Q == 3 ? 64 : 0) + (lr & 63);
+      const u16* A = p.A + (seg == 2 ? p.a_ps : 0);
+      glds16(A + (size_t)min(m0 + tr, p.M - 1) * p.lda + k0 + 8 * c, slot + 1024 * qq);
+    } else {
+      const int tr = (lr >> 5) * 64 + (Q == 2 ? 32 : 0) + (lr & 31);
+      const u16* B = p.B + (seg == 1 ? p.b_ps : 0);
+      glds16(B + (size_t)min(n0 + tr, p.N - 1) * p.ldb + k0 + 8 * c, slot + 1024 * qq);
+    }
+  }
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(GT) x2_gemm_nt4_kernel(X2Gemm p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NSLOT * HT];  // the epilogue reuses it
+  const int nwg = p.tiles_m * p.tiles_n;
+  int wg = blockIdx.x;
+  if (nwg >= 16) {
+    const int q = nwg / 8, r = nwg % 8, xcd = wg % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
+  }
+  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int g = lane >> 4, l16 = lane & 15;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int aoff[4][2], boff[2][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r = wm * 64 + 16 * i + l16;
+      aoff[i][s2] = r * 128 + 16 * ((4 * s2 + g) ^ rk_swz(r));
+    }
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r = wn * 32 + 16 * jj + l16;
+      boff[jj][s2] = r * 128 + 16 * ((4 * s2 + g) ^ rk_swz(r));
+    }
+
+  const int nkseg = p.K / TK, nk = 3 * nkseg;
+  issue_half<0>(p, smem, 0, nk, nkseg, m0, n0, wave, lane);
+  issue_half<1>(p, smem, 1, nk, nkseg, m0, n0, wave, lane);
+  issue_half<2>(p, smem, 2, nk, nkseg, m0, n0, wave, lane);
+  issue_half<3>(p, smem, 3, nk, nkseg, m0, n0, wave, lane);
+  issue_half<0>(p, smem, 4, nk, nkseg, m0, n0, wave, lane);
+  issue_half<1>(p, smem, 5, nk, nkseg, m0, n0, wave, lane);
+  issue_half<2>(p, smem, 6, nk, nkseg, m0, n0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // K-step 0's 4 half-tiles
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // wave row 1 runs one barrier behind row 0
+
+  f16x8 a[4][2], b0[2][2], b1[2][2];
+  auto mfma_quadrant = [&](int qm, const f16x8 (&bb)[2][2], int qn) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          acc[4 * qm + i][2 * qn + jj] =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][s2], bb[jj][s2], acc[4 * qm + i][2 * qn + jj], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync_mid = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto sync_end = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  for (int t = 0; t < nk; ++t) {
+    const int h = 4 * t + 7;
+    const unsigned char* s0 = smem + ((4 * t) % NSLOT) * HT;
+    const unsigned char* s1 = smem + ((4 * t + 1) % NSLOT) * HT;
+    const unsigned char* s2p = smem + ((4 * t + 2) % NSLOT) * HT;
+    const unsigned char* s3 = smem + ((4 * t + 3) % NSLOT) * HT;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) b0[jj][s2] = ld_b128(s1 + boff[jj][s2]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = ld_b128(s0 + aoff[i][s2]);
+    issue_half<3>(p, smem, h, nk, nkseg, m0, n0, wave, lane);
+    sync_mid();
+    mfma_quadrant(0, b0, 0);
+    sync_end();
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) b1[jj][s2] = ld_b128(s2p + boff[jj][s2]);
+    issue_half<0>(p, smem, h + 1, nk, nkseg, m0, n0, wave, lane);
+    sync_mid();
+    mfma_quadrant(0, b1, 1);
+    sync_end();
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = ld_b128(s3 + aoff[i][s2]);
+    issue_half<1>(p, smem, h + 2, nk, nkseg, m0, n0, wave, lane);
+    sync_mid();
+    mfma_quadrant(1, b1, 1);
+    sync_end();
+    issue_half<2>(p, smem, h + 3, nk, nkseg, m0, n0, wave, lane);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    sync_mid();
+    mfma_quadrant(1, b0, 0);
+    sync_end();
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // rejoin wave row 1
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the past-the-end half-tiles, before the epilogue reuses LDS
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  x2_epilogue<EPI>(p, acc, smem, m0, n0, wave, lane);
+}
+
+// W [rows][cols] fp32 -> planes of W^T [cols][rows] (the input gradient's NT operand): 64 x 64 tiles through LDS
+__global__ void __launch_bounds__(256) x2_split_t_kernel(const float* __restrict__ X, int rows, int cols, int ldx,
+                                                         const float* __restrict__ amax, int namax,
+                                                         u16* __restrict__ P, int64_t ps, int ldp,
+                                                         float* __restrict__ scale_out) {
+  __shared__ float tile[64][65];
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < namax; i += 256) m = fmaxf(m, fabsf(amax[i]));
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const int E = bound_exp(m);
+  const float up = pow2f(14 - E);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *scale_out = pow2f(E - 14);
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int r = i >> 6, c = i & 63;
+    tile[r][c] = (r0 + r < rows && c0 + c < cols) ? X[(int64_t)(r0 + r) * ldx + c0 + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int c = i >> 6, r = i & 63;  // output row c0 + c, column r0 + r
+    if (c0 + c >= cols || r0 + r >= rows) continue;
+    const float x = tile[r][c] * up;
+    const _Float16 h = static_cast<_Float16>(x);
+    const int64_t o = (int64_t)(c0 + c) * ldp + r0 + r;
+    P[o] = __builtin_bit_cast(u16, h);
+    P[ps + o] = __builtin_bit_cast(u16, static_cast<_Float16>(x - static_cast<float>(h)));
+  }
+}
+
 // ================================================================================================
 // weight gradient: gW[M][N] += sum_t A[t][m] B[t][n] with A = dz planes [T][lda], B = x planes [T][ldb]
 // (gemm_bf16_wgrad.hip's geometry: 256 x 128 tile, 8 waves of 64 x 64, 32x32x16 MFMAs, register-staged
-// k-major images read by ds_read_b64_tr_b16). Split s covers tokens [sub * tps, ...) of plane pair
-// seg = s / sps.
+// k-major images read by ds_read_b64_tr_b16). The 3 plane pairs form one extended K axis of 3 ceil(T / 64)
+// K-steps; split s covers K-steps [s kps, (s + 1) kps), and every tile of one split runs on one XCD.
 constexpr int WNT = 512, WBM = 256, WBN = 128, WBK = 64;
 constexpr int IMG = WBK * 128;  // u16 per 128-column image
 
@@ -315,7 +500,9 @@ struct X2Wg {
   int64_t a_ps, b_ps;
   float* slab;  // [splits][M][N] fp32, then [splits][M] bias partials
   int M, N, T, lda, ldb;
-  int tps, sps, splits;  // tokens per split, splits per plane pair, total splits (3 sps)
+  int nks;     // K-steps per plane pair (ceil(T / WBK)); the extended axis has 3 nks K-steps
+  int kps;     // K-steps per split
+  int splits;
   int tiles_m, tiles_n;
 };
 
@@ -339,6 +526,7 @@ struct KmTile {
   static constexpr int CPR = COLS / 8;      // chunks per k-row
   static constexpr int NV = WBK * CPR / WNT;  // chunks per thread
   u16x8 v[NV];
+  // the K-step's rows k0 .. k0 + 63 of plane P (rows past T re-read row T - 1; zeroed in store)
   __device__ __forceinline__ void load(const u16* __restrict__ P, int ld, int cols, int c0, int k0, int T) {
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
@@ -348,23 +536,28 @@ struct KmTile {
       v[u] = *reinterpret_cast<const u16x8*>(P + (size_t)k * ld + c);
     }
   }
+  // rows k0 + k >= T are stored as zeros; colsum[e] += the staged values when `sum`
   template <bool ROWSUM>
-  __device__ __forceinline__ void store(u16* L, int k0, int kend, float (&colsum)[8]) const {
+  __device__ __forceinline__ void store(u16* L, int k0, int T, bool sum, float (&colsum)[8]) const {
     const u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
       const int id = threadIdx.x + WNT * u;
       const int k = id / CPR, ch = id % CPR;
-      const u16x8 val = (k0 + k < kend) ? v[u] : z;
+      const u16x8 val = (k0 + k < T) ? v[u] : z;
       *reinterpret_cast<u16x8*>(L + (ch >> 4) * IMG + km_off(k, ch & 15)) = val;
       if constexpr (ROWSUM) {
+        if (sum) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) colsum[e] += h2f(val[e]);
+          for (int e = 0; e < 8; ++e) colsum[e] += h2f(val[e]);
+        }
       }
     }
   }
 };
 
+// K-step e of the extended axis: plane pair seg = e / nks ({(dz hi, x hi), (dz hi, x lo), (dz lo, x hi)}),
+// tokens (e - seg nks) * 64 ..; a split covers K-steps [split * kps, ...) and may cross a pair boundary
 template <bool BIAS>
 __global__ void __launch_bounds__(WNT) x2_wgrad_kernel(X2Wg p) {
   constexpr int BUF = 3 * IMG;  // A: two 128-col images, B: one
@@ -373,17 +566,14 @@ __global__ void __launch_bounds__(WNT) x2_wgrad_kernel(X2Wg p) {
   const int nwg = ntiles * p.splits;
   const int orig = blockIdx.x;
   int wg = orig;
-  if (nwg >= 16) {
+  if (nwg >= 16) {  // XCD-aware: the tiles of one split (same token range) share an XCD's L2
     const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
   }
   const int split = wg / ntiles, tile = wg % ntiles;
-  const int seg = split / p.sps, sub = split - seg * p.sps;
-  const u16* A = p.A + (seg == 2 ? p.a_ps : 0);
-  const u16* B = p.B + (seg == 1 ? p.b_ps : 0);
   const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
   const int m0 = tm * WBM, n0 = tn * WBN;
-  const int kbeg = sub * p.tps, kend = min(p.T, kbeg + p.tps);
+  const int ebeg = split * p.kps, eend = min(3 * p.nks, ebeg + p.kps);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave & 3, wn = wave >> 2;
@@ -397,17 +587,24 @@ __global__ void __launch_bounds__(WNT) x2_wgrad_kernel(X2Wg p) {
   KmTile<WBM> ta;
   KmTile<WBN> tb;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float dummy[8];
-  const bool do_bias = BIAS && tn == 0 && seg != 1;  // dz hi (segment 0) + dz lo (segment 2)
-  const int nk = kend > kbeg ? (kend - kbeg + WBK - 1) / WBK : 0;
+  const bool do_bias = BIAS && tn == 0;
+  auto seg_of = [&](int e) { return e / p.nks; };
+  auto load = [&](int e) {
+    const int seg = seg_of(e), k0 = (e - seg * p.nks) * WBK;
+    ta.load(p.A + (seg == 2 ? p.a_ps : 0), p.lda, p.M, m0, k0, p.T);
+    tb.load(p.B + (seg == 1 ? p.b_ps : 0), p.ldb, p.N, n0, k0, p.T);
+  };
+  auto store = [&](u16* L, int e) {  // bias: dz hi (pair 0) + dz lo (pair 2)
+    const int seg = seg_of(e), k0 = (e - seg * p.nks) * WBK;
+    if (do_bias) ta.template store<true>(L, k0, p.T, seg != 1, cs);
+    else ta.template store<false>(L, k0, p.T, false, cs);
+    tb.template store<false>(L + 2 * IMG, k0, p.T, false, cs);
+  };
+  const int nk = max(0, eend - ebeg);
   if (nk > 0) {
-    ta.load(A, p.lda, p.M, m0, kbeg, p.T);
-    tb.load(B, p.ldb, p.N, n0, kbeg, p.T);
-    if (do_bias) ta.template store<true>(smem, kbeg, kend, cs);
-    else ta.template store<false>(smem, kbeg, kend, dummy);
-    tb.template store<false>(smem + 2 * IMG, kbeg, kend, dummy);
-    ta.load(A, p.lda, p.M, m0, kbeg + WBK, p.T);
-    tb.load(B, p.ldb, p.N, n0, kbeg + WBK, p.T);
+    load(ebeg);
+    store(smem, ebeg);
+    if (nk > 1) load(ebeg + 1);
   }
   __syncthreads();
   for (int t = 0; t < nk; ++t) {
@@ -420,12 +617,9 @@ __global__ void __launch_bounds__(WNT) x2_wgrad_kernel(X2Wg p) {
       for (int i = 0; i < 2; ++i) a[i] = trfrag(L + (wm >> 1) * IMG, (wm & 1) * 64 + 32 * i, s, lane);
 #pragma unroll
       for (int j = 0; j < 2; ++j) b[j] = trfrag(L + 2 * IMG, wn * 64 + 32 * j, s, lane);
-      if (s == 0) {  // tile t+1 (registers) -> the other buffer; tile t+2 -> registers
-        if (do_bias) ta.template store<true>(Ln, kbeg + (t + 1) * WBK, kend, cs);
-        else ta.template store<false>(Ln, kbeg + (t + 1) * WBK, kend, dummy);
-        tb.template store<false>(Ln + 2 * IMG, kbeg + (t + 1) * WBK, kend, dummy);
-        ta.load(A, p.lda, p.M, m0, kbeg + (t + 2) * WBK, p.T);
-        tb.load(B, p.ldb, p.N, n0, kbeg + (t + 2) * WBK, p.T);
+      if (s == 0 && t + 1 < nk) {  // K-step t+1 (registers) -> the other buffer; K-step t+2 -> registers
+        store(Ln, ebeg + t + 1);
+        if (t + 2 < nk) load(ebeg + t + 2);
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -435,7 +629,7 @@ __global__ void __launch_bounds__(WNT) x2_wgrad_kernel(X2Wg p) {
     __syncthreads();
   }
 
-  if (BIAS && tn == 0) {  // every tn == 0 block writes its bias partial (0 for segment 1)
+  if (do_bias) {
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);  // [16][256]
     const int chn = threadIdx.x & 31, part = threadIdx.x >> 5;
@@ -467,9 +661,9 @@ __global__ void __launch_bounds__(WNT) x2_wgrad_kernel(X2Wg p) {
     }
 }
 
-// gW[m][n] (fp32) += sa sb sum_s slab[s][m][n] (fixed order); gb[m] += sa sum_{s not in pair 1} bias_slab[s][m]
-__global__ void __launch_bounds__(256) x2_wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int sps,
-                                                              int M, int N, float* __restrict__ C, int ldc,
+// gW[m][n] (fp32) += sa sb sum_s slab[s][m][n] (fixed order); gb[m] += sa sum_s bias_slab[s][m]
+__global__ void __launch_bounds__(256) x2_wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N,
+                                                              float* __restrict__ C, int ldc,
                                                               float* __restrict__ gb, const float* __restrict__ sa,
                                                               const float* __restrict__ sb) {
   const float da = *sa, dq = da * *sb;
@@ -478,8 +672,7 @@ __global__ void __launch_bounds__(256) x2_wgrad_reduce_kernel(const float* __res
     const float* bs = slab + (size_t)splits * MN;
     for (int64_t m = blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
       float s = 0.f;
-      for (int k = 0; k < splits; ++k)
-        if (k / sps != 1) s += bs[(size_t)k * M + m];
+      for (int k = 0; k < splits; ++k) s += bs[(size_t)k * M + m];
       gb[m] += da * s;
     }
   }
@@ -494,11 +687,12 @@ __global__ void __launch_bounds__(256) x2_wgrad_reduce_kernel(const float* __res
   }
 }
 
-int x2_wgrad_sps(int M, int N, int T) {
+// splits of the extended K axis (3 ceil(T / 64) K-steps): enough to cover the 256 CUs once, >= 8 K-steps each
+int x2_wgrad_splits(int M, int N, int T) {
   const int tiles = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
-  int s = std::max(1, 256 / (3 * tiles));  // 3 plane pairs x sps splits x tiles ~ one grid wave
-  const int max_by_t = std::max(1, T / (8 * WBK));
-  return std::min(s, max_by_t);
+  const int steps = 3 * ((T + WBK - 1) / WBK);
+  int s = std::max(1, 256 / tiles);
+  return std::max(1, std::min(s, steps / 8));
 }
 
 }  // namespace
@@ -515,6 +709,13 @@ void x2_split(const float* X, int rows, int cols, int ldx, const float* amax, in
   const int64_t n8 = (int64_t)rows * (cols / 8);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n8 + 255) / 256, 4096));
   hipLaunchKernelGGL(x2_split_kernel, dim3(blocks), dim3(256), 0, stream, X, rows, cols, ldx, amax, namax,
+                     static_cast<u16*>(planes), ps, ldp, scale_out);
+}
+
+void x2_split_t(const float* X, int rows, int cols, int ldx, const float* amax, int namax, void* planes, int64_t ps,
+                int ldp, float* scale_out, hipStream_t stream) {
+  const dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+  hipLaunchKernelGGL(x2_split_t_kernel, grid, dim3(256), 0, stream, X, rows, cols, ldx, amax, namax,
                      static_cast<u16*>(planes), ps, ldp, scale_out);
 }
 
@@ -553,8 +754,24 @@ void x2_gemm(const void* A, int64_t a_ps, const void* B, int64_t b_ps, float* C,
       default: X2_LAUNCH(BLV, 0); break;                       \
     }                                                          \
   } while (0)
-  if (b_kn) X2_EPI(1);
-  else X2_EPI(0);
+#define X2_NT4(E) hipLaunchKernelGGL((x2_gemm_nt4_kernel<E>), grid, dim3(GT), 0, stream, p)
+  static const bool nt4 = [] {  // SDML_X2_NT=2phase: the one-barrier-per-K-step loop (A/B)
+    const char* e = std::getenv("SDML_X2_NT");
+    return !(e && std::string(e) == "2phase");
+  }();
+  if (b_kn) {
+    X2_EPI(1);
+  } else if (nt4) {
+    switch (epi) {
+      case X2_RELU: X2_NT4(X2_RELU); break;
+      case X2_MASK: X2_NT4(X2_MASK); break;
+      case X2_RELU | X2_MASK: X2_NT4(X2_RELU | X2_MASK); break;
+      default: X2_NT4(0); break;
+    }
+  } else {
+    X2_EPI(0);
+  }
+#undef X2_NT4
 #undef X2_EPI
 #undef X2_LAUNCH
 }
@@ -564,7 +781,7 @@ bool x2_wgrad_supported(int M, int N, int T, int lda, int ldb) {
 }
 
 size_t x2_wgrad_workspace_floats(int M, int N, int T) {
-  const int splits = 3 * x2_wgrad_sps(M, N, T);
+  const int splits = x2_wgrad_splits(M, N, T);
   return (size_t)splits * M * N + (size_t)splits * M;
 }
 
@@ -581,13 +798,11 @@ void x2_wgrad(const void* dz, int64_t dz_ps, const void* x, int64_t x_ps, const 
   p.T = T;
   p.lda = lda;
   p.ldb = ldb;
-  int sps = x2_wgrad_sps(M, N, T);
-  int tps = (T + sps - 1) / sps;
-  tps = (tps + WBK - 1) / WBK * WBK;
-  sps = (T + tps - 1) / tps;  // (never more than x2_wgrad_sps: the workspace was sized with it)
-  p.tps = tps;
-  p.sps = sps;
-  p.splits = 3 * sps;
+  p.nks = (T + WBK - 1) / WBK;
+  int splits = x2_wgrad_splits(M, N, T);
+  p.kps = (3 * p.nks + splits - 1) / splits;
+  splits = (3 * p.nks + p.kps - 1) / p.kps;  // (never more than the workspace was sized for)
+  p.splits = splits;
   p.tiles_m = (M + WBM - 1) / WBM;
   p.tiles_n = (N + WBN - 1) / WBN;
   const dim3 grid(p.tiles_m * p.tiles_n * p.splits);
@@ -595,8 +810,8 @@ void x2_wgrad(const void* dz, int64_t dz_ps, const void* x, int64_t x_ps, const 
   else hipLaunchKernelGGL(x2_wgrad_kernel<false>, grid, dim3(WNT), 0, stream, p);
   const int64_t n4 = (int64_t)M * N / 4;
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
-  hipLaunchKernelGGL(x2_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, workspace, p.splits, sps, M, N, gw,
-                     ldc, gb, sdz, sx);
+  hipLaunchKernelGGL(x2_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, workspace, p.splits, M, N, gw, ldc,
+                     gb, sdz, sx);
 }
 
 }  // namespace sdml

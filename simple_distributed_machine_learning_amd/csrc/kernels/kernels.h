@@ -274,6 +274,9 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
 // the max of |amax[0..namax)|); scale_out receives 2^(E - 14). Products use 3 fp16 MFMA products.
 void x2_split(const float* X, int rows, int cols, int ldx, const float* amax, int namax, void* planes, int64_t ps,
               int ldp, float* scale_out, hipStream_t stream);
+// the same for X^T: planes [2][cols][ldp] of the transpose (the input gradient's NT weight operand)
+void x2_split_t(const float* X, int rows, int cols, int ldx, const float* amax, int namax, void* planes, int64_t ps,
+                int ldp, float* scale_out, hipStream_t stream);
 // C[M][N] (fp32) = sa sb A'[M][K] . (b_kn ? B'[K][N] : B'[N][K]^T) (+ bias[n]) (relu) (* (mask[m][n] > 0));
 // A/B: plane 0, plane 1 at + a_ps / b_ps (elements). wmax (optional, x2_gemm_wmax_slots floats): per-wave
 // max |C|, a bound source for the next x2_split. K % 64 == 0, N % 8 == 0 (x2_gemm_supported).

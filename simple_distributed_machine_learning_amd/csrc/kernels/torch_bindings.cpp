@@ -432,6 +432,21 @@ std::tuple<torch::Tensor, torch::Tensor> x2_split_op(torch::Tensor x, torch::Ten
   return {planes, scale};
 }
 
+// planes of x^T: (planes int16 [2, C, R], scale)
+std::tuple<torch::Tensor, torch::Tensor> x2_split_t_op(torch::Tensor x, torch::Tensor amax) {
+  check_f32_cuda(x, "x");
+  check_f32_cuda(amax, "amax");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x2_split_t: 2-D row-major fp32 expected");
+  TORCH_CHECK(amax.is_contiguous() && amax.numel() >= 1, "x2_split_t: amax must be a non-empty contiguous tensor");
+  const int64_t R = x.size(0), C = x.size(1);
+  auto planes = torch::empty({2, C, R}, x.options().dtype(torch::kInt16));
+  auto scale = torch::empty({1}, x.options());
+  if (R > 0 && C > 0)
+    sdml::x2_split_t(x.data_ptr<float>(), (int)R, (int)C, (int)x.stride(0), amax.data_ptr<float>(),
+                     (int)amax.numel(), planes.data_ptr(), R * C, (int)R, scale.data_ptr<float>(), cur_stream());
+  return {planes, scale};
+}
+
 static void check_planes(const torch::Tensor& p, const char* name) {
   TORCH_CHECK(p.is_cuda() && p.scalar_type() == torch::kInt16 && p.dim() == 3 && p.size(0) == 2 && p.is_contiguous(),
               name, ": planes must be a contiguous int16 [2, rows, cols] device tensor (x2_split)");
@@ -1597,6 +1612,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("aux") = py::none());
   m.def("x2_split", &x2_split_op, "fp32 -> two fp16 planes of x * 2^(14 - E) (+ the dequantisation scale)",
         py::arg("x"), py::arg("amax"));
+  m.def("x2_split_t", &x2_split_t_op, "planes of x^T (the input gradient's NT weight operand)", py::arg("x"),
+        py::arg("amax"));
   m.def("x2_gemm", &x2_gemm_op, "fp32-accurate GEMM from fp16 planes (3 MFMA products) with fused epilogues",
         py::arg("A"), py::arg("sa"), py::arg("B"), py::arg("sb"), py::arg("b_kn") = false,
         py::arg("bias") = py::none(), py::arg("relu") = false, py::arg("mask") = py::none(),

@@ -104,7 +104,7 @@ class MLPStage(PipelineStage):
                 ctx["mask"] = mask_out
                 return y
             return super().fwd(x, ctx, train)
-        x = x.reshape(x.shape[0], -1)
+        x = ops.carry_bounds(x.reshape(x.shape[0], -1), x)
         if x.dtype == torch.uint8:
             x = x.contiguous()
         elif x.dtype != torch.float32 or not x.is_contiguous():
@@ -168,7 +168,7 @@ class MLPStage(PipelineStage):
                 ops._put_stats(stats, loss.float(), correct.float(), stats_init)
                 return None, None, n
             return loss, correct, n
-        x = ops.pixels_to_float(x.reshape(x.shape[0], -1))
+        x = ops.carry_bounds(ops.pixels_to_float(x.reshape(x.shape[0], -1)), x)
         if x.dtype != torch.float32 or not x.is_contiguous():
             x = x.float().contiguous()
         layers = self.layers()

@@ -127,10 +127,13 @@ def linear_wgrad_u8(x: torch.Tensor, gz: torch.Tensor, gw: torch.Tensor, gb: Opt
 
     ROCm: gz enters the kernel as fp16 planes scaled from a bound on |gz|: ``amax`` (any float
     tensor whose max bounds |gz|), else the bounds the fused head attached to the dx it returned
-    (:func:`linear_logsoftmax_nll`), else a torch amax of gz."""
+    (:func:`linear_logsoftmax_nll`) or the per-wave maxima of the x2 GEMM that produced it, else a torch
+    amax of gz."""
     if x.is_cuda:
-        if amax is None:
+        if amax is None:  # the head's per-block bounds, or the producing GEMM's per-wave maxima (x2 engine)
             amax = getattr(gz, "_sdml_amax", None)
+            if amax is None:
+                amax = getattr(gz, "_sdml_wmax", None)
         _k().linear_wgrad_u8(x, gz, gw, gb, PIXEL_SCALE, amax)
         return
     gw += gz.t() @ pixels_to_float(x)
@@ -194,6 +197,7 @@ def linear_relu_bwd(x, y, gy, w, gw, gb, need_dx: bool, gy_masked: bool = False,
 # SDML_F32_GEMM=x3 keeps the bf16x3 engine (A/B).
 
 _X2_MIN_ROWS = 2048
+_X2_DX_NT = __import__("os").environ.get("SDML_X2_DX", "nt") != "nn"  # A/B: SDML_X2_DX=nn (w planes, NN kernel)
 
 
 def _x2_env_ok() -> bool:
@@ -223,6 +227,16 @@ def _bound_of(t: torch.Tensor) -> torch.Tensor:
     return b
 
 
+def carry_bounds(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    """Keep the bound attributes of ``src`` on ``dst`` (a reshaped view / same-data alias of it)."""
+    if dst is not src:
+        for a in ("_sdml_wmax", "_sdml_amax"):
+            v = getattr(src, a, None)
+            if v is not None:
+                setattr(dst, a, v)
+    return dst
+
+
 def x2_split(t: torch.Tensor):
     """(planes int16 [2, rows, cols], dequantisation scale [1]) of an fp32 matrix."""
     return _k().x2_split(t, _bound_of(t))
@@ -231,11 +245,15 @@ def x2_split(t: torch.Tensor):
 def linear_relu_fwd_x2(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], relu: bool = True):
     """relu(x @ w.T + b) on the two-plane engine. Returns (y, planes) with planes = (x planes, x scale,
     w planes, w scale) for :func:`linear_relu_bwd_x2`; y carries its per-wave maxima for the next split."""
+    k = _k()
     xp, sx = x2_split(x)
-    wp, sw = _k().x2_split(w, torch.linalg.vector_norm(w, float("inf")).reshape(1))
-    y, wm = _k().x2_gemm(xp, sx, wp, sw, False, b, relu, None, True)
+    wn = torch.linalg.vector_norm(w, float("inf")).reshape(1)
+    wp, sw = k.x2_split(w, wn)
+    y, wm = k.x2_gemm(xp, sx, wp, sw, False, b, relu, None, True)
     y._sdml_wmax = wm
-    return y, (xp, sx, wp, sw)
+    # the input gradient dz @ w runs as an NT GEMM against w^T's planes (the 4-phase NT kernel)
+    wtp, swt = k.x2_split_t(w, wn) if _X2_DX_NT else (wp, sw)
+    return y, (xp, sx, wtp, swt)
 
 
 def linear_relu_bwd_x2(x: torch.Tensor, gz: torch.Tensor, gw, gb, planes, need_dx: bool, mask_dx: bool):
@@ -245,7 +263,7 @@ def linear_relu_bwd_x2(x: torch.Tensor, gz: torch.Tensor, gw, gb, planes, need_d
     gp, sg = x2_split(gz.contiguous())
     dx = None
     if need_dx:
-        dx, wm = _k().x2_gemm(gp, sg, wp, sw, True, None, False, x if mask_dx else None, True)
+        dx, wm = _k().x2_gemm(gp, sg, wp, sw, not _X2_DX_NT, None, False, x if mask_dx else None, True)
         dx._sdml_wmax = wm
     _k().x2_wgrad_(gp, sg, xp, sx, gw, gb)
     return dx

@@ -122,3 +122,25 @@ def test_x2_zero_operand():
     pb, sb = split(B)
     C, _ = K.x2_gemm(pa, sa, pb, sb, False)
     assert (C == 0).all()
+
+
+def test_x2_split_t_is_the_split_of_the_transpose():
+    w = rnd(320, 192, seed=17) * 3.0
+    pt, st = K.x2_split_t(w, inf_norm(w))
+    p, s = K.x2_split(w.t().contiguous(), inf_norm(w))
+    assert torch.equal(pt, p) and torch.equal(st, s)
+
+
+def test_x2_input_gradient_nt_matches_nn():
+    # dx = dz @ W (W [N_out, K_in] = nn.Linear's weight) as NT against W^T's planes and as NN against W's
+    M, Nout, Kin = 1024, 512, 384
+    dz, W, x = rnd(M, Nout, seed=18), rnd(Nout, Kin, seed=19), rnd(M, Kin, seed=20)
+    pd, sd = split(dz)
+    pw, sw = split(W)
+    pt, st = K.x2_split_t(W, inf_norm(W))
+    c_nn, _ = K.x2_gemm(pd, sd, pw, sw, True, None, False, x)
+    c_nt, _ = K.x2_gemm(pd, sd, pt, st, False, None, False, x)
+    want = (dz.double() @ W.double()) * (x > 0)
+    b = bound(dz, W.t(), Nout)
+    assert ((c_nn.double() - want).abs() <= b).all()
+    assert ((c_nt.double() - want).abs() <= b).all()

@@ -54,12 +54,16 @@ def main():
     r["split_us"] = round(timeit(lambda: K.x2_split(x, inf(x))), 1)
     r["x2_fwd_us"] = round(timeit(lambda: K.x2_gemm(px, sx, pw, sw, False, b, True)), 1)
     r["x2_dx_us"] = round(timeit(lambda: K.x2_gemm(pd, sd, pw, sw, True, None, False, x, True)), 1)
+    pwt, swt = K.x2_split_t(w, inf(w))
+    r["x2_dx_nt_us"] = round(timeit(lambda: K.x2_gemm(pd, sd, pwt, swt, False, None, False, x, True)), 1)
+    r["split_only_us"] = round(timeit(lambda: K.x2_split(x, sx)), 1)
+    r["infnorm_us"] = round(timeit(lambda: inf(x)), 1)
     r["x2_wgrad_us"] = round(timeit(lambda: K.x2_wgrad_(pd, sd, px, sx, gw, gb)), 1)
     C = torch.empty(M, N, device=dev)
     r["x3_fwd_us"] = round(timeit(lambda: K.gemm_f32x3(x, w, C, False, False, 2, b)), 1)
     dx = torch.empty(M, Kd, device=dev)
     r["x3_dx_us"] = round(timeit(lambda: K.gemm_f32x3(dz, w, dx, False, True, 0, None, None, None, x)), 1)
-    for k in ("x2_fwd", "x2_dx", "x2_wgrad", "x3_fwd", "x3_dx"):
+    for k in ("x2_fwd", "x2_dx", "x2_dx_nt", "x2_wgrad", "x3_fwd", "x3_dx"):
         r[k + "_fp32_TFs"] = round(flops / r[k + "_us"] / 1e6, 1)
     print(json.dumps(r))
 

@@ -269,6 +269,15 @@ bool gemm_bf16_supported(int M, int N, int K, int lda, int ldb, int ldc, bool b_
 void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool b_kn,
                int epi, const void* bias, void* aux, int ldaux, hipStream_t stream);
 
+// ---- the reference CNN's whole training step (both stages on one rank) in two launches (ref_cnn.hip) ----
+// params / bufs: conv1.w, conv1.b, conv2.w, conv2.b, fc1.w, fc1.b, fc2.w, fc2.b (bufs[i] nullptr: no momentum);
+// rec: [B][ref_cnn_step_record_floats()] scratch; stats [2] = (loss sum, correct) (overwritten); *ctr += 1
+int ref_cnn_step_record_floats();
+void ref_cnn_step(const float* x, const int64_t* target, int B, float* const* params, float* const* bufs,
+                  unsigned long long seed0, unsigned long long seed1, long long* ctr, float p0, bool drop0, float p1,
+                  bool drop1, float scale, float lr, float mom, float damp, float wd, bool nesterov, bool first,
+                  float* rec, float* stats, hipStream_t stream, long long* stamps = nullptr);
+
 // ---- fp32-accurate GEMMs from pre-split fp16 planes (gemm_f16x2.hip) ---------------------------
 // An fp32 tensor X [rows][cols] becomes planes [2][rows][ldp] (hi, lo of X * 2^(14 - E), |X| < 2^E from
 // the max of |amax[0..namax)|); scale_out receives 2^(E - 14). Products use 3 fp16 MFMA products.

@@ -433,6 +433,390 @@ __global__ void __launch_bounds__(T1) cnn_s1_kernel(const float* __restrict__ x,
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The whole training step of the 2-stage CNN (both stages on one rank, the reference's B = 60) in two
+// launches: cnn_step_sample runs, per sample, stage 0's forward, stage 1's forward + NLL + backward and
+// stage 0's backward in ONE workgroup (the sample's activations never leave LDS), and writes the sample's
+// weight-gradient contributions as one record (no float atomics: the per-block atomics of the three-kernel
+// form queued 60 deep on every conv weight); cnn_step_update sums the records in sample order
+// (deterministic), applies torch.optim.SGD's update to all 8 parameter tensors, writes (loss sum, correct)
+// and advances the device dropout counter. The fc layers' gradients are rank 1 per sample (dh z3^T,
+// dl hd^T), so a record holds the factors (380 + 60 floats), not the 16,500-float products.
+constexpr int TS = 1024;
+// diagnostic phase stamps (stamps != nullptr, tools/probes): s_memtime after each barrier, per block
+#define STAMP(k)                                                                  \
+  do {                                                                            \
+    if (stamps && t == 0) stamps[(size_t)blockIdx.x * 16 + (k)] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+constexpr int R_W2C = 0, R_B2C = R_W2C + C2 * C1 * KS * KS, R_W1C = R_B2C + C2, R_B1C = R_W1C + C1 * KS * KS,
+              R_DH = R_B1C + C1, R_Z3 = R_DH + HID, R_DL = R_Z3 + FLAT, R_HD = R_DL + NCLS, R_LOSS = R_HD + HID,
+              REC = R_LOSS + 2;
+static_assert(REC == 5712, "record layout");
+
+__global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __restrict__ x, const int64_t* __restrict__ tgt,
+                                                             const float* __restrict__ cw1, const float* __restrict__ cb1,
+                                                             const float* __restrict__ cw2, const float* __restrict__ cb2,
+                                                             const float* __restrict__ fw1, const float* __restrict__ fb1,
+                                                             const float* __restrict__ fw2, const float* __restrict__ fb2,
+                                                             unsigned long long seed0, unsigned long long seed1,
+                                                             const long long* ctr, float p0, int drop0, float p1,
+                                                             int drop1, float scale, float* __restrict__ rec,
+                                                             long long* __restrict__ stamps) {
+  __shared__ float xs[IMG * IMG];
+  __shared__ float w1s[C1 * KS * KS];
+  __shared__ float w2s[C2 * C1 * KS * KS];
+  __shared__ float z1[NZ1];
+  __shared__ unsigned char a1[NZ1];
+  __shared__ float c2[C2 * O2 * O2];  // conv2 output, then its gradient G2
+  __shared__ float c2p[5][C2 * O2 * O2];  // conv2 partials per group of 2 input channels
+  __shared__ float z3[FLAT];
+  __shared__ unsigned char a2[FLAT];
+  __shared__ float g1[NZ1];
+  __shared__ float dsc[C2];
+  __shared__ float hraw[HID], hd[HID], msk[HID], dh[HID], dl[NCLS];
+  const int n = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  float* R = rec + (size_t)n * REC;
+  STAMP(0);
+  // fc1 rows of this wave (hidden units wv, wv + 16, wv + 32, wv + 48 < 50), 5 per lane: loaded here so their
+  // HBM latency (the weights were just rewritten by the previous step's update) hides under the conv phases
+  float w1r[4][5];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = wv + 16 * u;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) w1r[u][i] = j < HID ? fw1[(size_t)j * FLAT + lane + 64 * i] : 0.f;
+  }
+  const float* xn = x + (size_t)n * IMG * IMG;
+  for (int i = t; i < IMG * IMG; i += TS) xs[i] = xn[i];
+  for (int i = t; i < C1 * KS * KS; i += TS) w1s[i] = cw1[i];
+  for (int i = t; i < C2 * C1 * KS * KS; i += TS) w2s[i] = cw2[i];
+  for (int i = t; i < NZ1; i += TS) g1[i] = 0.f;
+  if (t < C2) dsc[t] = drop0 ? keep_scale(eff_seed(seed0, ctr), n, t, p0) : 1.f;
+  __syncthreads();
+  STAMP(1);
+  // ---- stage 0 forward (cnn_s0_fwd_kernel's arithmetic) ----
+  for (int o = t; o < NZ1; o += TS) {
+    const int c = o / (P1 * P1), py = (o / P1) % P1, px = o % P1;
+    float win[6][6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) win[r][q] = xs[(2 * py + r) * IMG + 2 * px + q];
+    float acc[4];
+    const float bias = cb1[c];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[d] = bias;
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) {
+        const float w = w1s[(c * KS + ky) * KS + kx];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) acc[d] += w * win[(d >> 1) + ky][(d & 1) + kx];
+      }
+    float best = acc[0];
+    int arg = 0;
+#pragma unroll
+    for (int d = 1; d < 4; ++d)
+      if (acc[d] > best) {
+        best = acc[d];
+        arg = d;
+      }
+    z1[o] = fmaxf(best, 0.f);
+    a1[o] = (unsigned char)arg;
+  }
+  __syncthreads();
+  STAMP(2);
+  // conv2 as 800 items (output row (c, y) x 5 groups of 2 input channels; the 160-row form left 864 of the
+  // 1024 threads idle on a 2000-FMA chain), group partials summed in a fixed order below
+  for (int it = t; it < C2 * O2 * 5; it += TS) {
+    const int cg = it / (C2 * O2), c = (it / O2) % C2, y = it % O2;
+    float acc[O2];
+#pragma unroll
+    for (int xo = 0; xo < O2; ++xo) acc[xo] = 0.f;
+#pragma unroll
+    for (int ci = 2 * cg; ci < 2 * cg + 2; ++ci)
+#pragma unroll
+      for (int ky = 0; ky < KS; ++ky) {
+        const float* zr = z1 + (ci * P1 + y + ky) * P1;
+        const float* wr = w2s + ((c * C1 + ci) * KS + ky) * KS;
+        float zv[P1], wv5[KS];
+#pragma unroll
+        for (int q = 0; q < P1; ++q) zv[q] = zr[q];
+#pragma unroll
+        for (int kx = 0; kx < KS; ++kx) wv5[kx] = wr[kx];
+#pragma unroll
+        for (int xo = 0; xo < O2; ++xo)
+#pragma unroll
+          for (int kx = 0; kx < KS; ++kx) acc[xo] += wv5[kx] * zv[xo + kx];
+      }
+#pragma unroll
+    for (int xo = 0; xo < O2; ++xo) c2p[cg][(c * O2 + y) * O2 + xo] = acc[xo];
+  }
+  __syncthreads();
+  STAMP(3);
+  for (int o = t; o < C2 * O2 * O2; o += TS) {
+    const int c = o / (O2 * O2);
+    const float v = (((c2p[0][o] + c2p[1][o]) + (c2p[2][o] + c2p[3][o])) + c2p[4][o]) + cb2[c];
+    c2[o] = v * dsc[c];
+  }
+  __syncthreads();
+  STAMP(4);
+  for (int o = t; o < FLAT; o += TS) {
+    const int c = o / (P2 * P2), py = (o / P2) % P2, px = o % P2;
+    float best = -INFINITY;
+    int arg = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const float v = c2[(c * O2 + 2 * py + (d >> 1)) * O2 + 2 * px + (d & 1)];
+      if (v > best) {
+        best = v;
+        arg = d;
+      }
+    }
+    const float v = fmaxf(best, 0.f);
+    z3[o] = v;
+    a2[o] = (unsigned char)arg;
+    R[R_Z3 + o] = v;
+  }
+  __syncthreads();
+  STAMP(5);
+  for (int i = t; i < C2 * O2 * O2; i += TS) c2[i] = 0.f;  // becomes G2
+  // ---- stage 1: fc1 + relu + dropout (wave w: hidden units w, w + 16, w + 32, w + 48) ----
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = wv + 16 * u;
+    if (j >= HID) break;
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) a += w1r[u][i] * z3[lane + 64 * i];
+    for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
+    if (lane == 0) {
+      const float h = fmaxf(fb1[j] + a, 0.f);
+      const float ms = drop1 ? keep_scale(eff_seed(seed1, ctr), n, j, p1) : 1.f;
+      hraw[j] = h;
+      msk[j] = ms;
+      hd[j] = h * ms;
+      R[R_HD + j] = h * ms;
+    }
+  }
+  __syncthreads();
+  STAMP(6);
+  // fc2 + log_softmax + NLL + dlogits, then dh = (W2^T dl) * relu' * dropout (wave 0)
+  if (wv == 0) {
+    float z = -INFINITY;
+    if (lane < NCLS) {
+      float acc = fb2[lane];
+      for (int j = 0; j < HID; ++j) acc += fw2[lane * HID + j] * hd[j];
+      z = acc;
+    }
+    float mx = z;
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float se = lane < NCLS ? __expf(z - mx) : 0.f;
+    for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
+    const float lse = mx + __logf(se);
+    const int y = (int)tgt[n];
+    const unsigned long long bal = __ballot(lane < NCLS && z == mx);  // first max = torch argmax
+    const int am = __ffsll((long long)bal) - 1;
+    const float zy = __shfl(z, y);
+    const float d = lane < NCLS ? scale * (__expf(z - lse) - (lane == y ? 1.f : 0.f)) : 0.f;
+    if (lane < NCLS) {
+      dl[lane] = d;
+      R[R_DL + lane] = d;
+    }
+    if (lane == 0) {
+      R[R_LOSS] = lse - zy;
+      R[R_LOSS + 1] = (am == y) ? 1.f : 0.f;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < HID) {
+      float dd = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCLS; ++c) dd += fw2[c * HID + lane] * dl[c];
+      const float v = hraw[lane] > 0.f ? dd * msk[lane] : 0.f;
+      dh[lane] = v;
+      R[R_DH + lane] = v;
+    }
+  }
+  __syncthreads();
+  STAMP(7);
+  // dz3 = W1^T dh, routed through relu (z3 > 0), pool argmax and the Dropout2d scale into G2
+  if (t < FLAT) {
+    float acc = 0.f;
+#pragma unroll 10
+    for (int j = 0; j < HID; ++j) acc += fw1[(size_t)j * FLAT + t] * dh[j];
+    const int c = t / (P2 * P2), py = (t / P2) % P2, px = t % P2, d = a2[t];
+    c2[(c * O2 + 2 * py + (d >> 1)) * O2 + 2 * px + (d & 1)] = z3[t] > 0.f ? acc * dsc[c] : 0.f;
+  }
+  __syncthreads();
+  STAMP(8);
+  const float* G2 = c2;
+  // ---- stage 0 backward (cnn_s0_bwd_kernel's phases), contributions into the record ----
+  if (t < C2 * C1 * KS) {
+    // dW2 from the 16 nonzeros of each channel's G2 (one per pooled cell, at its argmax; the other 48 of
+    // the 64 positions are zero): 16 instead of 64 terms per weight
+    const int c = t / (C1 * KS), ci = (t / KS) % C1, ky = t % KS;
+    float acc[KS] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int q = 0; q < P2 * P2; ++q) {
+      const int py = q / P2, px = q % P2, d = a2[c * P2 * P2 + q];
+      const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
+      const float g = G2[(c * O2 + y) * O2 + x];
+      const float* zr = z1 + (ci * P1 + y + ky) * P1 + x;
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) acc[kx] += g * zr[kx];
+    }
+#pragma unroll
+    for (int kx = 0; kx < KS; ++kx) R[R_W2C + ((c * C1 + ci) * KS + ky) * KS + kx] = acc[kx];
+  } else if (t < C2 * C1 * KS + C2) {
+    const int c = t - C2 * C1 * KS;
+    float acc = 0.f;
+    for (int i = 0; i < O2 * O2; ++i) acc += G2[c * O2 * O2 + i];
+    R[R_B2C + c] = acc;
+  }
+  if (stamps) {
+    __syncthreads();
+    STAMP(10);
+  }
+  // dZ1 as 3-wide strips: 2 halves x 10 ci x 12 rows x 4 strips = 960 items (720 4-wide strips left 304
+  // threads idle on the phase's critical path)
+  for (int it = t; it < 2 * C1 * P1 * (P1 / 3); it += TS) {
+    const int half = it / (C1 * P1 * 4), r = it % (C1 * P1 * 4);
+    const int ci = r / (P1 * 4), Y = (r / 4) % P1, X0 = (r % 4) * 3;
+    float acc[3] = {0.f, 0.f, 0.f};
+    for (int c = half * (C2 / 2); c < (half + 1) * (C2 / 2); ++c)
+#pragma unroll
+      for (int ky = 0; ky < KS; ++ky) {
+        const int y = Y - ky;
+        if (y < 0 || y >= O2) continue;
+        const float* gr = G2 + (c * O2 + y) * O2;
+        const float* wr = w2s + ((c * C1 + ci) * KS + ky) * KS;
+        float gv[7], wv5[KS];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {  // G2 row at x = X0 - 4 + q (zero outside 0..7)
+          const int xx = X0 - 4 + q;
+          gv[q] = (xx >= 0 && xx < O2) ? gr[xx] : 0.f;
+        }
+#pragma unroll
+        for (int kx = 0; kx < KS; ++kx) wv5[kx] = wr[kx];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int kx = 0; kx < KS; ++kx) acc[j] += wv5[kx] * gv[j - kx + 4];
+      }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int o = (ci * P1 + Y) * P1 + X0 + j;
+      if (z1[o] > 0.f) atomicAdd(&g1[o], acc[j]);  // ReLU mask; LDS, two halves (a + b == b + a: deterministic)
+    }
+  }
+  __syncthreads();
+  STAMP(9);
+  if (t < C1 * KS * KS * 4) {
+    const int wi = t >> 2, prt = t & 3;
+    const int c = wi / (KS * KS), ky = (wi / KS) % KS, kx = wi % KS;
+    float acc = 0.f;
+    for (int q = prt; q < P1 * P1; q += 4) {
+      const int o = c * P1 * P1 + q;
+      const int py = q / P1, px = q % P1, d = a1[o];
+      acc += g1[o] * xs[(2 * py + (d >> 1) + ky) * IMG + 2 * px + (d & 1) + kx];
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (prt == 0) R[R_W1C + wi] = acc;
+  } else if (t < C1 * KS * KS * 4 + C1) {
+    const int c = t - C1 * KS * KS * 4;
+    float acc = 0.f;
+    for (int q = 0; q < P1 * P1; ++q) acc += g1[c * P1 * P1 + q];
+    R[R_B1C + c] = acc;
+  }
+  __syncthreads();
+  STAMP(15);
+}
+
+struct CnnParams {
+  float* p[8];    // conv1.w, conv1.b, conv2.w, conv2.b, fc1.w, fc1.b, fc2.w, fc2.b
+  float* buf[8];  // momentum buffers (nullptr without momentum)
+  float lr, mom, damp, wd;
+  int nesterov, first;
+};
+
+// torch.optim.SGD on one parameter (sgd_rule.h's operations, explicit fmas)
+__device__ __forceinline__ void sgd_update1(float* pp, float* bp, float d, const CnnParams& a) {
+#pragma clang fp contract(off)
+  const float pv = *pp;
+  if (a.wd != 0.f) d = __builtin_fmaf(a.wd, pv, d);
+  if (a.mom != 0.f) {
+    float b = d;
+    if (!a.first) b = __builtin_fmaf(a.mom, *bp, (1.f - a.damp) * d);
+    *bp = b;
+    d = a.nesterov ? __builtin_fmaf(a.mom, b, d) : b;
+  }
+  *pp = __builtin_fmaf(-a.lr, d, pv);
+}
+
+// sum over samples of rec[s][o] (or of the rank-1 product rec[s][o] rec[s][o2]) as 8 interleaved partial
+// sums combined in a fixed order: deterministic, and 8 independent loads in flight per thread instead of a
+// 60-deep chain of dependent L2 round trips
+template <bool PROD>
+__device__ __forceinline__ float sample_sum(const float* __restrict__ rec, int B, int o, int o2) {
+  float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + 8 <= B; s += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float* r = rec + (size_t)(s + u) * REC;
+      g[u] = PROD ? __builtin_fmaf(r[o], r[o2], g[u]) : g[u] + r[o];
+    }
+  }
+  for (; s < B; ++s) {  // the tail (B % 8 samples) into the first partial
+    const float* r = rec + (size_t)s * REC;
+    g[0] = PROD ? __builtin_fmaf(r[o], r[o2], g[0]) : g[0] + r[o];
+  }
+  return ((g[0] + g[1]) + (g[2] + g[3])) + ((g[4] + g[5]) + (g[6] + g[7]));
+}
+
+__global__ void __launch_bounds__(256) cnn_step_update_kernel(const float* __restrict__ rec, int B, CnnParams a,
+                                                              float* __restrict__ stats, long long* ctr) {
+  constexpr int n0 = C1 * KS * KS, n1 = C1, n2 = C2 * C1 * KS * KS, n3 = C2, n4 = HID * FLAT, n5 = HID,
+                n6 = NCLS * HID, n7 = NCLS;
+  constexpr int total = n0 + n1 + n2 + n3 + n4 + n5 + n6 + n7;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < total) {
+    int ti, e = i;
+    float g;
+    if (e < n0) {
+      ti = 0;
+      g = sample_sum<false>(rec, B, R_W1C + e, 0);
+    } else if ((e -= n0) < n1) {
+      ti = 1;
+      g = sample_sum<false>(rec, B, R_B1C + e, 0);
+    } else if ((e -= n1) < n2) {
+      ti = 2;
+      g = sample_sum<false>(rec, B, R_W2C + e, 0);
+    } else if ((e -= n2) < n3) {
+      ti = 3;
+      g = sample_sum<false>(rec, B, R_B2C + e, 0);
+    } else if ((e -= n3) < n4) {
+      ti = 4;
+      g = sample_sum<true>(rec, B, R_DH + e / FLAT, R_Z3 + e % FLAT);
+    } else if ((e -= n4) < n5) {
+      ti = 5;
+      g = sample_sum<false>(rec, B, R_DH + e, 0);
+    } else if ((e -= n5) < n6) {
+      ti = 6;
+      g = sample_sum<true>(rec, B, R_DL + e / HID, R_HD + e % HID);
+    } else {
+      e -= n6;
+      ti = 7;
+      g = sample_sum<false>(rec, B, R_DL + e, 0);
+    }
+    sgd_update1(a.p[ti] + e, a.buf[ti] ? a.buf[ti] + e : nullptr, g, a);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 2) stats[threadIdx.x] = sample_sum<false>(rec, B, R_LOSS + threadIdx.x, 0);
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && ctr) *ctr += 1;  // this step's masks are drawn
+}
+
 }  // namespace
 
 int ref_cnn_idx_bytes() { return NIDX; }
@@ -468,6 +852,31 @@ void ref_cnn_stage1(const float* x, const float* w1, const float* b1, const floa
     hipLaunchKernelGGL(cnn_s1_kernel<32>, dim3((B + 31) / 32), dim3(T1), 0, stream, x, w1, b1, w2, b2, target, B,
                        seed, ctr, sample0, p, drop ? 1 : 0, scale, stats, dx, gw1, gb1, gw2, gb2);
   }
+}
+
+int ref_cnn_step_record_floats() { return REC; }
+
+void ref_cnn_step(const float* x, const int64_t* target, int B, float* const* params, float* const* bufs,
+                  unsigned long long seed0, unsigned long long seed1, long long* ctr, float p0, bool drop0, float p1,
+                  bool drop1, float scale, float lr, float mom, float damp, float wd, bool nesterov, bool first,
+                  float* rec, float* stats, hipStream_t stream, long long* stamps) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(cnn_step_sample_kernel, dim3(B), dim3(TS), 0, stream, x, target, params[0], params[1], params[2],
+                     params[3], params[4], params[5], params[6], params[7], seed0, seed1, ctr, p0, drop0 ? 1 : 0, p1,
+                     drop1 ? 1 : 0, scale, rec, stamps);
+  CnnParams a;
+  for (int i = 0; i < 8; ++i) {
+    a.p[i] = params[i];
+    a.buf[i] = bufs[i];
+  }
+  a.lr = lr;
+  a.mom = mom;
+  a.damp = damp;
+  a.wd = wd;
+  a.nesterov = nesterov ? 1 : 0;
+  a.first = first ? 1 : 0;
+  constexpr int total = C1 * KS * KS + C1 + C2 * C1 * KS * KS + C2 + HID * FLAT + HID + NCLS * HID + NCLS;
+  hipLaunchKernelGGL(cnn_step_update_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, rec, B, a, stats, ctr);
 }
 
 }  // namespace sdml

@@ -1204,6 +1204,49 @@ bool mlp_small_step(torch::Tensor x, torch::Tensor target, torch::Tensor w1, tor
                               h.data_ptr<float>() + B * 128, stats.data_ptr<float>(), cur_stream());
 }
 
+// the reference CNN's training step (both stages, SGD of all 8 tensors) in two launches (ref_cnn.hip)
+void ref_cnn_step_op(torch::Tensor x, torch::Tensor target, std::vector<torch::Tensor> params,
+                     std::vector<c10::optional<torch::Tensor>> bufs, int64_t seed0, int64_t seed1,
+                     c10::optional<torch::Tensor> ctr, double p0, bool drop0, double p1, bool drop1, double scale,
+                     double lr, double mom, double damp, double wd, bool nesterov, bool first, torch::Tensor stats,
+                     c10::optional<torch::Tensor> stamps) {
+  check_f32_cuda(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 784 == 0, "ref_cnn_step: x must be contiguous [B, 1, 28, 28]");
+  const int64_t B = x.numel() / 784;
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == torch::kInt64 && target.is_contiguous() &&
+                  target.numel() == B,
+              "ref_cnn_step: target");
+  TORCH_CHECK(params.size() == 8 && bufs.size() == 8, "ref_cnn_step: 8 parameter tensors");
+  static const int64_t sizes[8] = {250, 10, 5000, 20, 16000, 50, 500, 10};
+  float* pp[8];
+  float* bp[8];
+  for (int i = 0; i < 8; ++i) {
+    check_f32_cuda(params[i], "param");
+    TORCH_CHECK(params[i].is_contiguous() && params[i].numel() == sizes[i], "ref_cnn_step: parameter ", i, " shape");
+    pp[i] = params[i].data_ptr<float>();
+    bp[i] = nullptr;
+    if (bufs[i].has_value() && bufs[i]->defined()) {
+      check_f32_cuda(*bufs[i], "momentum");
+      TORCH_CHECK(bufs[i]->is_contiguous() && bufs[i]->numel() == sizes[i], "ref_cnn_step: momentum ", i, " shape");
+      bp[i] = bufs[i]->data_ptr<float>();
+    }
+    TORCH_CHECK(mom == 0 || bp[i], "ref_cnn_step: momentum buffers required");
+  }
+  check_f32_cuda(stats, "stats");
+  long long* cp = nullptr;
+  if (ctr.has_value() && ctr->defined()) {
+    TORCH_CHECK(ctr->is_cuda() && ctr->scalar_type() == torch::kInt64 && ctr->numel() == 1, "ref_cnn_step: ctr");
+    cp = reinterpret_cast<long long*>(ctr->data_ptr<int64_t>());
+  }
+  auto rec = torch::empty({B * sdml::ref_cnn_step_record_floats()}, x.options());
+  sdml::ref_cnn_step(x.data_ptr<float>(), target.data_ptr<int64_t>(), (int)B, pp, bp, (unsigned long long)seed0,
+                     (unsigned long long)seed1, cp, (float)p0, drop0, (float)p1, drop1, (float)scale, (float)lr,
+                     (float)mom, (float)damp, (float)wd, nesterov, first, rec.data_ptr<float>(),
+                     stats.data_ptr<float>(), cur_stream(),
+                     stamps.has_value() && stamps->defined() ? reinterpret_cast<long long*>(stamps->data_ptr<int64_t>())
+                                                              : nullptr);
+}
+
 // C = A . (b_kn ? B : B^T) with a fused epilogue (gemm_bf16.hip); A [M, K] (row stride lda), B [N, K] or
 // [K, N]; returns C [M, N] bf16. epi: 0 store, 1 bias, 5 bias+GELU (aux out, allocated here and returned),
 // 6 gelu' (aux in).
@@ -1622,6 +1665,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("x2_wgrad_", &x2_wgrad_, "gw += dz^T x, gb += colsum(dz) from fp16 planes (fp32-accurate)",
         py::arg("dz"), py::arg("sdz"), py::arg("x"), py::arg("sx"), py::arg("gw"), py::arg("gb") = py::none());
   m.def("gemm_bf16_supported", &gemm_bf16_supported_op, "shape check for gemm_bf16 (M, N, K, lda, ldb, b_kn)");
+  m.def("ref_cnn_step", &ref_cnn_step_op, "reference CNN training step (both stages + SGD) in two launches",
+        py::arg("x"), py::arg("target"), py::arg("params"), py::arg("bufs"), py::arg("seed0"), py::arg("seed1"),
+        py::arg("ctr"), py::arg("p0"), py::arg("drop0"), py::arg("p1"), py::arg("drop1"), py::arg("scale"),
+        py::arg("lr"), py::arg("mom"), py::arg("damp"), py::arg("wd"), py::arg("nesterov"), py::arg("first"),
+        py::arg("stats"), py::arg("stamps") = py::none());
   m.def("mlp_small_step", &mlp_small_step, "784-128-10 MLP training step (fwd, loss, bwd, SGD) in one launch");
   m.def("mlp_small_step_max_batch", &sdml::mlp_small_step_max_batch);
   m.def("gelu_fwd_bf16", &gelu_fwd_bf16, "tanh-GELU forward (bf16)");

@@ -193,6 +193,7 @@ class PipelineEngine:
         # stay on their owner (models/mlp.py fwd_head_fused); SDML_FUSE_HEAD=0 keeps them separate
         self.fuse_head = os.environ.get("SDML_FUSE_HEAD", "1") != "0"
         self._small_step = None  # one-launch reference-size MLP step available (decided on first use)
+        self._cnn_step = None  # two-launch reference CNN step available (decided on first use)
         self._small_args = None
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
@@ -288,6 +289,8 @@ class PipelineEngine:
             res = self._run_small_mlp_step(dataset, start, batch_size, global_batch, t0)
             if res is not None:
                 return res
+        if train and step_optimizer and self._cnn_step_ok(batch_size):
+            return self._run_cnn_step(dataset, start, batch_size, global_batch, t0)
         if self.kind == "rotate" and self.use_alltoall and self.P == 2:
             return self._run_rotate_alltoall(dataset, start, batch_size, train, global_batch, step_optimizer, t0)
         if self.kind == "rotate":
@@ -750,6 +753,51 @@ class PipelineEngine:
         self.optimizer.commit_fused(zero_grad=True, planes_current=False)
         self.global_step += 1
         self._advance_rng()
+        self.last_timing = {}
+        return StepResult(stats[0], stats[1], batch_size, time.perf_counter() - t0)
+
+    def _cnn_step_ok(self, batch_size: int) -> bool:
+        """Both stages of the reference CNN on this (only) rank, training mode, fp32 weights, no gradients
+        pending from an earlier step_optimizer=False call: the two-launch step (ops.ref_cnn_step)."""
+        if self._cnn_step is None:
+            from ..models.ref_cnn import Network1Stage, Network2Stage
+
+            s = self.stages
+            self._cnn_step = bool(
+                self.device.type == "cuda" and self.mesh.world_size == 1 and self.P == 2 and 0 in s and 1 in s
+                and isinstance(s[0], Network1Stage) and isinstance(s[1], Network2Stage)
+                and os.environ.get("SDML_SMALL_STEP", "1") != "0" and not self.timing and not self.debug_sync
+                and self.optimizer.master is None)
+        return (self._cnn_step and 0 < batch_size <= 4096 and self.flat.grads_zero and self.training
+                and self.stages[0].training and self.stages[1].training)
+
+    def _run_cnn_step(self, dataset, start, batch_size, global_batch, t0):
+        """The reference's own workload (its CNN at B = 60) as ONE per-sample kernel (stage 0 forward, stage 1
+        forward + NLL + backward, stage 0 backward) + ONE reduction/SGD kernel: the three-kernel step with
+        per-block weight-gradient atomics, a separate SGD launch and a dropout-counter launch was launch- and
+        atomic-bound (profiles/r3_ref_cnn_kernel_stats.txt). Dropout seeds are drawn in the same order as the
+        per-stage path (stage 0, then stage 1), so both draw the same masks."""
+        from ..models.ref_cnn import _draw_seed
+
+        dev = self.device
+        x = dataset.inputs(start, batch_size)
+        if x.device != dev:
+            x = x.to(dev, non_blocking=True)
+        x = pixels_to_float(x)
+        if x.dtype != torch.float32:
+            x = x.float()
+        tgt = dataset.targets(start, batch_size)
+        if tgt.device != dev:
+            tgt = tgt.to(dev, non_blocking=True)
+        s0, s1 = self.stages[0], self.stages[1]
+        seed0 = _draw_seed() if s0.conv2_drop.p > 0 else 0
+        seed1 = _draw_seed() if s1.p > 0 else 0
+        stats = torch.empty(2, device=dev, dtype=torch.float32)
+        scale = self._loss_scale(dataset, batch_size, global_batch)
+        ops.ref_cnn_step(x.contiguous(), tgt.contiguous(), s0, s1, self.optimizer, scale, stats,
+                         self.step_ctr if self._uses_rng else None, seed0, seed1)
+        self.optimizer.commit_fused(zero_grad=True, planes_current=False)
+        self.global_step += 1  # (the kernel advanced the device dropout counter)
         self.last_timing = {}
         return StepResult(stats[0], stats[1], batch_size, time.perf_counter() - t0)
 

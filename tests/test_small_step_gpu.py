@@ -61,3 +61,38 @@ def test_small_step_then_large_batch_uses_fresh_weight_planes():
     ds = SyntheticMNIST(8192, seed=10, device=DEV, pixels="u8")
     r = e.run(ds, 0, 8192, train=True)
     assert torch.isfinite(r.loss_sum)
+
+
+def _run_cnn(B, steps, opt, dropout=0.5):
+    mesh = init_mesh(pp=1, schedule_kind="1f1b", rank=0, world_size=1, device=DEV)
+    torch.manual_seed(1)  # the host RNG draws the dropout seeds: same stream for both runs
+    e = PipelineEngine(get_model_spec("ref_cnn", 2, dropout=dropout), mesh, schedule_kind="1f1b", num_microbatches=1,
+                       lr=0.1, momentum=opt.get("momentum", 0.5), weight_decay=opt.get("wd", 0.0), seed=3)
+    e.optimizer.dampening, e.optimizer.nesterov = opt.get("damp", 0.0), opt.get("nesterov", False)
+    ds = SyntheticMNIST(B * steps, seed=9, device=DEV)
+    out = []
+    for s in range(steps):
+        r = e.run(ds, s * B, B, train=True)
+        out.append((float(r.loss_sum), int(r.correct), r.count))
+    torch.cuda.synchronize()
+    return e, out
+
+
+@pytest.mark.parametrize("B", [60, 7, 300])
+@pytest.mark.parametrize("opt", [dict(), dict(momentum=0.0), dict(wd=1e-4, damp=0.1, nesterov=True)])
+def test_cnn_step_matches_per_stage_kernels(B, opt, monkeypatch):
+    """The reference CNN's two-launch step (ref_cnn.hip cnn_step_*) against the per-stage kernels + SGD it
+    replaces: same dropout masks (same host seeds, same device counter), fp32 agreement (fixed-order sums vs
+    atomics), and the dropout counter advanced once per step."""
+    monkeypatch.setenv("SDML_SMALL_STEP", "0")
+    e0, r0 = _run_cnn(B, 4, opt)
+    monkeypatch.setenv("SDML_SMALL_STEP", "1")
+    e1, r1 = _run_cnn(B, 4, opt)
+    assert e1._cnn_step is True and e0._cnn_step is False
+    for (l0, c0, n0), (l1, c1, n1) in zip(r0, r1):
+        assert n0 == n1 == B
+        assert l1 == pytest.approx(l0, rel=1e-4, abs=1e-4)
+        assert abs(c0 - c1) <= 1
+    torch.testing.assert_close(e1.flat.params, e0.flat.params, rtol=1e-4, atol=2e-6)
+    assert int(e1.step_ctr) == int(e0.step_ctr) == 4
+    assert float(e1.flat.grads.abs().max()) == 0.0

@@ -338,9 +338,11 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
                                                        const int64_t* __restrict__ target, int M, int K, float scale,
                                                        float* __restrict__ stats, float* __restrict__ dx,
                                                        float* __restrict__ dz_out, int mask_dx,
-                                                       float* __restrict__ part) {
+                                                       float* __restrict__ part, float* __restrict__ dx_amax) {
   extern __shared__ float4 Ws4[];  // [C][K / 4]
   __shared__ float red[8];
+  __shared__ float amx[4];
+  float vmax = 0.f;  // max |dx| this wave wrote (dx_amax: per-block bounds for the next split)
   const int nch = K / 4;
   for (int i = threadIdx.x; i < C * nch; i += 256) Ws4[i] = reinterpret_cast<const float4*>(W)[i];
   __syncthreads();
@@ -474,12 +476,19 @@ __global__ void __launch_bounds__(256) head_lds_kernel(const float* __restrict__
             o[rr].w = xv[rr][j].w <= 0.f ? 0.f : o[rr].w;
           }
           reinterpret_cast<float4*>(dx + (size_t)(row0 + rr) * K)[ch] = o[rr];
+          vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(o[rr].x), fabsf(o[rr].y))), fmaxf(fabsf(o[rr].z), fabsf(o[rr].w)));
         }
       }
   }
   if (lane == 0) {
     red[2 * wave] = loss_acc;
     red[2 * wave + 1] = corr_acc;
+  }
+  if (dx_amax) {
+    for (int off = 32; off > 0; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off));
+    if (lane == 0) amx[wave] = vmax;
+    __syncthreads();
+    if (threadIdx.x == 0) dx_amax[blockIdx.x] = fmaxf(fmaxf(amx[0], amx[1]), fmaxf(amx[2], amx[3]));
   }
   if constexpr (DW) {
     __shared__ float gbs[4][C];
@@ -950,8 +959,10 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
     const int lblocks = head_lds_blocks(M);
     const size_t lds = (size_t)C * K * sizeof(float);
     if (gW && gb && workspace && dz_out == nullptr) {
+      float* am = (dx && dx_amax && n_amax && lblocks <= kHeadAmaxMax) ? dx_amax : nullptr;
       hipLaunchKernelGGL((head_lds_kernel<10, true>), dim3(lblocks), dim3(256), lds, stream, x, W, b, target, M, K,
-                         scale, stats, dx, nullptr, mask_dx ? 1 : 0, workspace);
+                         scale, stats, dx, nullptr, mask_dx ? 1 : 0, workspace, am);
+      if (am) *n_amax = lblocks;  // exact per-block max |dx|
       HeadReduceArgs ra;
       ra.part = workspace;
       ra.nblocks = lblocks;
@@ -965,7 +976,7 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
     } else {
       if (stats_overwrite) (void)hipMemsetAsync(stats, 0, 2 * sizeof(float), stream);  // this variant adds
       hipLaunchKernelGGL((head_lds_kernel<10, false>), dim3(lblocks), dim3(256), lds, stream, x, W, b, target, M, K,
-                         scale, stats, dx, dz_out, mask_dx ? 1 : 0, nullptr);
+                         scale, stats, dx, dz_out, mask_dx ? 1 : 0, nullptr, nullptr);
     }
     return;
   }

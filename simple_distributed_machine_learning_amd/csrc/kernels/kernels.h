@@ -124,7 +124,9 @@ void split_planes_pad(const float* w, unsigned short* out, int N, int K, int Kp,
 // mask the factored weight gradient (u8_wgrad_dl) reads instead of y itself
 void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
             const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream,
-            unsigned* mask = nullptr);
+            unsigned* mask = nullptr, float* wmax = nullptr);
+// wmax slots u8_fwd writes for M x N (per-wave max |output|, a split bound for the next two-plane GEMM)
+int u8_fwd_wmax_slots(int M, int N);
 // The uint8 first layer and the classifier head in ONE kernel (N = 128 hidden, C in {2, 10, 16}, training):
 // h = relu(scale X W^T + b) stays in the workgroup (LDS, from the MFMA accumulators), the head
 // (head_tile.h: logits, log_softmax, NLL, argmax, dl = loss_scale (softmax - onehot), dW2^T/db2 partials)
@@ -189,9 +191,10 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
                          float* workspace, bool mask_dx, hipStream_t stream, float* dl = nullptr,
                          bool stats_overwrite = false,  // stats_overwrite: stats = this call's totals
                          float* dx_amax = nullptr, int* n_amax = nullptr, HeadReduceArgs* defer = nullptr);
-// dx_amax (capacity kHeadAmaxMax floats): where the MFMA head path writes per-block bounds on |dx|
-// (*n_amax of them; 0 when another head variant ran) - the uint8 weight gradient's dz bound
-constexpr int kHeadAmaxMax = 512;
+// dx_amax (capacity kHeadAmaxMax floats): where the MFMA head path writes per-block bounds on |dx| and the
+// wide-K (LDS) head its per-block max |dx| (*n_amax of them; 0 when another head variant ran) - the uint8
+// weight gradient's dz bound, the two-plane split's bound
+constexpr int kHeadAmaxMax = 1024;
 // dx = (dl @ W) * (x > 0 if mask): the fused head's dx rebuilt bit-identically from its factor dl
 // (K == 128, C in {2, 10, 16}: head_fused_supported)
 void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx, int M, int K, int C, bool mask,

@@ -126,6 +126,8 @@ struct FwdParams {
   float scale;
   int relu;
   unsigned* mask;  // optional [M][N / 32] ReLU bits (plain epilogue)
+  float* wmax;     // optional [blocks][WAVES] per-wave max of the stored outputs (plain epilogue): a bound the
+                   // next layer's two-plane split (gemm_f16x2.hip) reads instead of an inf-norm pass
   U8HeadArgs head;  // fused head epilogue (HEADC > 0)
 };
 
@@ -319,6 +321,7 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
   float bv[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bv[j] = p.bias ? p.bias[n0 + wn * 64 + 32 * j + r32] : 0.f;
+  float vmax = 0.f;
 #pragma unroll
   for (int ip = 0; ip < WMT / NI2; ++ip) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous piece's reads are done
@@ -343,6 +346,7 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
         if (v[0] == 12345.f && row < 0) *reinterpret_cast<f32x4*>(p.C) = v;
       } else if (row < p.M) {
         *reinterpret_cast<f32x4*>(p.C + (size_t)row * p.ldc + n0 + wn * 64 + 4 * (lane & 15)) = v;
+        vmax = fmaxf(fmaxf(vmax, fmaxf(fabsf(v[0]), fabsf(v[1]))), fmaxf(fabsf(v[2]), fabsf(v[3])));
       }
       if (p.mask) {  // ReLU bits: the 8 lanes holding 32 columns of the row OR their nibbles into one word
         unsigned w = ((v[0] > 0.f ? 1u : 0u) | (v[1] > 0.f ? 2u : 0u) | (v[2] > 0.f ? 4u : 0u) |
@@ -354,6 +358,10 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
           p.mask[(size_t)row * (p.N / 32) + (n0 + wn * 64) / 32 + ((lane & 15) >> 3)] = w;
       }
     }
+  }
+  if (p.wmax) {
+    for (int off = 32; off > 0; off >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, off));
+    if (lane == 0) p.wmax[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * G::WAVES + wave] = vmax;
   }
 }
 
@@ -1012,11 +1020,40 @@ void split_planes_pad(const float* w, unsigned short* out, int N, int K, int Kp,
   hipLaunchKernelGGL(split_planes_pad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, w, out, N, K, Kp);
 }
 
+// the forward's block geometry for M rows: 16 waves of 512 rows, or 8 waves of 128 WMT rows
+static void u8_fwd_geometry(int M, bool& w16, int& wmt, int& bm) {
+  static const int wmt_env = [] {
+    const char* e = getenv("SDML_U8_FWD_WMT");
+    return e ? atoi(e) : 0;
+  }();
+  static const int waves_env = [] {  // 8 (512 threads) or 16 (1024 threads, 4 waves per SIMD)
+    const char* e = getenv("SDML_U8_FWD_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  // 512-row blocks (half the LDS weight traffic per MFMA) once they still cover every CU, as 16
+  // waves of 64 x 64 (4 waves per SIMD at 115 VGPRs; 8 waves of 128 x 64 need 199: 63.9-65.3 vs
+  // 66.5-67.3 us at 131072 rows, tools/gpu_fwd16.sh); smaller batches: 256-row blocks of 8 waves
+  const bool big = M >= 256 * Geo<4>::BM;
+  w16 = waves_env ? waves_env == 16 : (big && !wmt_env);
+  wmt = wmt_env ? wmt_env : (big ? 4 : 2);
+  if (w16) wmt = 2;
+  bm = w16 ? Geo<2, 8>::BM : (wmt == 4 ? Geo<4>::BM : Geo<2>::BM);
+}
+
+int u8_fwd_wmax_slots(int M, int N) {
+  bool w16;
+  int wmt, bm;
+  u8_fwd_geometry(M, w16, wmt, bm);
+  return ((M + bm - 1) / bm) * (N / FBN) * (w16 ? 16 : 8);
+}
+
 void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
-            const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream, unsigned* mask) {
+            const float* bias, float* C, int ldc, bool relu, float scale, hipStream_t stream, unsigned* mask,
+            float* wmax) {
   if (mask && !relu) abort();  // host contract: the ReLU bits need the ReLU epilogue
   FwdParams p{};
   p.mask = mask;
+  p.wmax = wmax;
   p.X = X;
   p.Wp = w_planes;
   p.bias = bias;
@@ -1037,22 +1074,9 @@ void u8_fwd(const unsigned char* X, int M, int K, int ldx, const unsigned short*
 #else
   constexpr int mode = 0;
 #endif
-  static const int wmt_env = [] {
-    const char* e = getenv("SDML_U8_FWD_WMT");
-    return e ? atoi(e) : 0;
-  }();
-  static const int waves_env = [] {  // 8 (512 threads) or 16 (1024 threads, 4 waves per SIMD)
-    const char* e = getenv("SDML_U8_FWD_WAVES");
-    return e ? atoi(e) : 0;
-  }();
-  // 512-row blocks (half the LDS weight traffic per MFMA) once they still cover every CU, as 16
-  // waves of 64 x 64 (4 waves per SIMD at 115 VGPRs; 8 waves of 128 x 64 need 199: 63.9-65.3 vs
-  // 66.5-67.3 us at 131072 rows, tools/gpu_fwd16.sh); smaller batches: 256-row blocks of 8 waves
-  const bool big = M >= 256 * Geo<4>::BM;
-  const bool w16 = waves_env ? waves_env == 16 : (big && !wmt_env);
-  int wmt = wmt_env ? wmt_env : (big ? 4 : 2);
-  if (w16) wmt = 2;
-  const int bm = w16 ? Geo<2, 8>::BM : (wmt == 4 ? Geo<4>::BM : Geo<2>::BM);
+  bool w16;
+  int wmt, bm;
+  u8_fwd_geometry(M, w16, wmt, bm);
   const dim3 grid((M + bm - 1) / bm, N / FBN);
   const int tail = tail_substeps(K);
 #define FWD_LAUNCH(MD, W, T, R) \

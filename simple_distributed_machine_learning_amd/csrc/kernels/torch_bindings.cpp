@@ -198,7 +198,7 @@ void check_mask_out(const c10::optional<torch::Tensor>& m, int64_t M, int64_t N)
 // mask_out (optional, relu): also write the ReLU bits of y (relu_bits' layout)
 torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> b, bool relu,
                             double scale, c10::optional<torch::Tensor> planes, bool planes_valid,
-                            c10::optional<torch::Tensor> mask_out) {
+                            c10::optional<torch::Tensor> mask_out, c10::optional<torch::Tensor> wmax_out) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
               "linear_fwd_u8: x must be a contiguous 2-D uint8 ROCm tensor");
   check_f32_cuda(w, "w");
@@ -211,8 +211,10 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
   TORCH_CHECK(!want_mask || relu, "linear_fwd_u8: mask_out needs the relu epilogue");
   const bool direct = M >= 4096 && K % 16 == 0 && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
                       M * K < (int64_t(1) << 31);
-  auto with_mask = [&](torch::Tensor y) {
+  auto with_mask = [&](torch::Tensor y) {  // (the paths without the uint8 kernel's epilogue extras)
     if (want_mask) mask_out->copy_(relu_bits(y));
+    if (wmax_out.has_value() && wmax_out->defined())
+      wmax_out->copy_(at::linalg_vector_norm(y, INFINITY).reshape({1}).expand_as(*wmax_out));
     return y;
   };
   // a caller-owned plane cache is marked current by the caller after this call (ops.linear_relu_fwd_u8), so
@@ -249,9 +251,16 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
     auto wp = cache ? *planes : torch::empty({sdml::kU8FwdPlanes, N, Kp}, w.options().dtype(torch::kInt16));
     auto* wpp = reinterpret_cast<unsigned short*>(wp.data_ptr<int16_t>());
     if (!cache || !planes_valid) sdml::split_planes_pad(w.data_ptr<float>(), wpp, (int)N, (int)K, Kp, cur_stream());
+    float* wm = nullptr;
+    if (wmax_out.has_value() && wmax_out->defined()) {  // per-wave output maxima (a split bound downstream)
+      check_f32_cuda(*wmax_out, "wmax_out");
+      TORCH_CHECK(wmax_out->is_contiguous() && wmax_out->numel() == sdml::u8_fwd_wmax_slots((int)M, (int)N),
+                  "linear_fwd_u8: wmax_out must hold u8_fwd_wmax_slots(M, N) floats");
+      wm = wmax_out->data_ptr<float>();
+    }
     sdml::u8_fwd(x.data_ptr<uint8_t>(), (int)M, (int)K, (int)K, wpp, (int)N, Kp, opt_ptr(b), y.data_ptr<float>(),
                  (int)N, relu, (float)scale, cur_stream(),
-                 want_mask ? reinterpret_cast<unsigned*>(mask_out->data_ptr<int32_t>()) : nullptr);
+                 want_mask ? reinterpret_cast<unsigned*>(mask_out->data_ptr<int32_t>()) : nullptr, wm);
     return y;
   }
   refresh_cache();
@@ -1645,7 +1654,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "sdml gfx950 HIP kernels";
   m.def("linear_fwd_u8", &linear_fwd_u8, "act(scale * x_u8 @ w.T + b): uint8-pixel first layer", py::arg("x"),
         py::arg("w"), py::arg("b"), py::arg("relu"), py::arg("scale"), py::arg("planes") = py::none(),
-        py::arg("planes_valid") = false, py::arg("mask_out") = py::none());
+        py::arg("planes_valid") = false, py::arg("mask_out") = py::none(), py::arg("wmax_out") = py::none());
+  m.def("u8_fwd_wmax_slots", &sdml::u8_fwd_wmax_slots, "per-wave maxima linear_fwd_u8 writes into wmax_out (M, N)");
   m.def("linear_relu_head_u8", &linear_relu_head_u8,
         "uint8 first layer + classifier head in one launch (h stays on chip): dl, ReLU bits, head slab");
   m.def("u8_fwd_head_supported", &u8_fwd_head_supported_op, "shape check for linear_relu_head_u8 (M, N, K, C)");

@@ -78,11 +78,16 @@ def linear_relu_fwd_u8(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, cache:
     ``cache`` (and the flat buffer's ``epoch``) the weight planes are reused when still current.
     ``mask_out`` (int32 [M, N/32]): also receives the output's ReLU bits (:func:`relu_bits`)."""
     if x.is_cuda:
+        k = _k()
+        # per-wave output maxima: the bound of the next layer's two-plane split (no inf-norm pass over y)
+        wm = torch.empty(int(k.u8_fwd_wmax_slots(x.shape[0], w.shape[0])), device=x.device, dtype=torch.float32)
         if cache is None:
-            return _k().linear_fwd_u8(x, w, b, True, PIXEL_SCALE, None, False, mask_out)
-        tok = PlaneCache.token_of(w, epoch)
-        y = _k().linear_fwd_u8(x, w, b, True, PIXEL_SCALE, cache.planes, cache.token == tok, mask_out)
-        cache.token = tok
+            y = k.linear_fwd_u8(x, w, b, True, PIXEL_SCALE, None, False, mask_out, wm)
+        else:
+            tok = PlaneCache.token_of(w, epoch)
+            y = k.linear_fwd_u8(x, w, b, True, PIXEL_SCALE, cache.planes, cache.token == tok, mask_out, wm)
+            cache.token = tok
+        y._sdml_wmax = wm
         return y
     y = ref.linear_relu_fwd(pixels_to_float(x), w, b)
     if mask_out is not None:

@@ -32,8 +32,9 @@ DEFAULTS = {  # model -> (schedule, micro-batches, batch, seq_len)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="mlp4x1024", choices=sorted(DEFAULTS))
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 10; 200 for the batch-60 configs, whose ~0.06 ms steps need more)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 3; 20 for the batch-60 configs)")
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--seq_len", type=int, default=None)
@@ -44,6 +45,11 @@ def main():
                     help="image models: pixel storage (auto: uint8 for the MLPs at batches the uint8 kernels take)")
     a = ap.parse_args()
     kind, M, B, S = DEFAULTS[a.config]
+    small = a.config in ("mlp", "ref_cnn") and (a.batch or B) <= 128
+    if a.steps is None:
+        a.steps = 200 if small else 10
+    if a.warmup is None:
+        a.warmup = 20 if small else 3
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
     if world0 == 1 and a.config in ("gpt2", "resnet18", "mlp4x1024"):
         # all stages local: micro-batching only shrinks the GEMMs / convolutions (measured: GPT-2

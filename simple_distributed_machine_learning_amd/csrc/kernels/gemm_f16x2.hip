@@ -26,7 +26,11 @@
 //   x2_wgrad_kernel   gW[N][K] += sum_m dz[m][n] x[m][k] (both operands k-major, hardware transpose reads),
 //                     the 3 plane pairs as 3 token segments of one extended K axis, cut into equal splits over
 //                     workgroups (one grid wave), fp32 slabs reduced in a fixed order (deterministic) with the
-//                     bias gradient (column sums of dz: hi in segment 0, lo in segment 2)
+//                     bias gradient (column sums of dz: hi in segment 0, lo in segment 2). Two main loops:
+//                     x2_wgrad_dma_kernel (T % 64 == 0, default) fills a 3-stage LDS ring by LDS-DMA with two
+//                     K-steps in flight (gemm_bf16_wgrad.hip's wgrad_dma_kernel); x2_wgrad_kernel stages
+//                     through VGPRs (any T; SDML_WGRAD_DMA=0). 588 -> 502 us at 65536 x 1024 x 1024
+//                     (profiles/r3_wgrad_dma_vs_staged.json)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -504,6 +508,7 @@ struct X2Wg {
   int kps;     // K-steps per split
   int splits;
   int tiles_m, tiles_n;
+  int bparts;  // bias partials per split (x2_wgrad_dma_kernel: tiles_n, block tn sums K-steps e % tiles_n == tn)
 };
 
 __device__ __forceinline__ int km_off(int k, int ch) { return k * 128 + 8 * (ch ^ (((k & 3) << 2) | ((k >> 2) & 3))); }
@@ -555,6 +560,42 @@ struct KmTile {
     }
   }
 };
+
+// bias partials (16 row groups -> LDS -> 256 column sums) and the partial tile -> slab; smem must be free
+__device__ __forceinline__ void x2w_finish(const X2Wg& p, const f32x16 (&acc)[2][2], const float (&cs)[8], u16* smem,
+                                           bool do_bias, int split, int bslot, int m0, int n0, int wm, int wn,
+                                           int lane) {
+  if (do_bias) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [16][256]
+    const int chn = threadIdx.x & 31, part = threadIdx.x >> 5;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[part * 256 + 8 * chn + e] = cs[e];
+    __syncthreads();
+    if (threadIdx.x < WBM) {
+      float sum = 0.f;
+      for (int q = 0; q < 16; ++q) sum += red[q * 256 + threadIdx.x];
+      const int m = m0 + threadIdx.x;
+      if (m < p.M) p.slab[(size_t)p.splits * p.M * p.N + ((size_t)split * p.bparts + bslot) * p.M + m] = sum;
+    }
+  }
+
+  // partial tile -> slab; C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+  const int h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 64 + j * 32 + (lane & 31);
+      if (col >= p.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= p.M) continue;
+        p.slab[((size_t)split * p.M + row) * p.N + col] = acc[i][j][r];
+      }
+    }
+}
 
 // K-step e of the extended axis: plane pair seg = e / nks ({(dz hi, x hi), (dz hi, x lo), (dz lo, x hi)}),
 // tokens (e - seg nks) * 64 ..; a split covers K-steps [split * kps, ...) and may cross a pair boundary
@@ -629,55 +670,164 @@ __global__ void __launch_bounds__(WNT) x2_wgrad_kernel(X2Wg p) {
     __syncthreads();
   }
 
-  if (do_bias) {
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [16][256]
-    const int chn = threadIdx.x & 31, part = threadIdx.x >> 5;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) red[part * 256 + 8 * chn + e] = cs[e];
-    __syncthreads();
-    if (threadIdx.x < WBM) {
-      float sum = 0.f;
-      for (int q = 0; q < 16; ++q) sum += red[q * 256 + threadIdx.x];
-      const int m = m0 + threadIdx.x;
-      if (m < p.M) p.slab[(size_t)p.splits * p.M * p.N + (size_t)split * p.M + m] = sum;
-    }
-  }
+  x2w_finish(p, acc, cs, smem, do_bias, split, 0, m0, n0, wm, wn, lane);
+}
 
-  // partial tile -> slab; C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
-  const int h = lane >> 5;
+// ---- LDS-DMA form of the weight gradient (T % 64 == 0; gemm_bf16_wgrad.hip's wgrad_dma_kernel with the
+// plane pair chosen per K-step): 3-stage ring of [A 2 x 128 cols | B 128 cols] images filled by
+// global_load_lds (the km_off swizzle on the per-lane source address), two K-steps in flight, one
+// counted vmcnt(6) + barrier per K-step, fragments by inline-asm transposed reads (see x2w_tr16).
+__device__ __forceinline__ void x2w_issue(const X2Wg& p, u16* st, int m0, int n0, int e, int wave, int lane) {
+  const int seg = e / p.nks, k0 = (e - seg * p.nks) * WBK;
+  const u16* A = p.A + (seg == 2 ? p.a_ps : 0);
+  const u16* B = p.B + (seg == 1 ? p.b_ps : 0);
+#pragma unroll
+  for (int u = 0; u < 6; ++u) {
+    const int q = wave + 8 * u;
+    const int img = u >> 1, r = 4 * (wave + 8 * (u & 1)) + (lane >> 4);
+    const int c = (lane & 15) ^ (((r & 3) << 2) | ((r >> 2) & 3));
+    const u16* src = img < 2 ? A + (size_t)(k0 + r) * p.lda + min(m0 + 128 * img + 8 * c, p.M - 8)
+                             : B + (size_t)(k0 + r) * p.ldb + min(n0 + 8 * c, p.N - 8);
+    glds16(src, reinterpret_cast<unsigned char*>(st + q * 512));
+  }
+}
+
+// inline-asm ds_read_b64_tr_b16: the builtin makes the compiler wait for every LDS-DMA in flight
+// (vmcnt(0)) before each read; these are invisible to its wait pass, so lgkmcnt is waited explicitly
+// with the fragments as "+v" operands (no MFMA can move above the wait)
+__device__ __forceinline__ s16x4 x2w_tr16(const u16* p) {
+  const unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) u16*)p;
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+
+__device__ __forceinline__ void x2w_read(const u16* L, int wm, int wn, int s, int lane, s16x4 (&f)[8]) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int k = 16 * s + 8 * (g >> 1) + q;
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    const u16* P = x < 2 ? L + (wm >> 1) * IMG : L + 2 * IMG;
+    const int c0 = x < 2 ? (wm & 1) * 64 + 32 * x : wn * 64 + 32 * (x - 2);
+    const int col = c0 + 16 * (g & 1) + 4 * pp;
+    f[2 * x] = x2w_tr16(P + km_off(k, col >> 3) + (col & 7));
+    f[2 * x + 1] = x2w_tr16(P + km_off(k + 4, col >> 3) + (col & 7));
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void x2w_wait(s16x4 (&f)[8]) {
+  asm volatile("s_waitcnt lgkmcnt(%8)"
+               : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5]), "+v"(f[6]), "+v"(f[7])
+               : "n"(N));
+}
+
+__device__ __forceinline__ f16x8 x2w_cat(s16x4 lo, s16x4 hi) {
+  return __builtin_bit_cast(f16x8, s16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]});
+}
+
+template <bool BIAS>
+__global__ void __launch_bounds__(WNT) x2_wgrad_dma_kernel(X2Wg p) {
+  constexpr int BUF = 3 * IMG;
+  __shared__ __attribute__((aligned(16))) u16 smem[3 * BUF];
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int nwg = ntiles * p.splits;
+  const int orig = blockIdx.x;
+  int wg = orig;
+  if (nwg >= 16) {
+    const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  }
+  const int split = wg / ntiles, tile = wg % ntiles;
+  const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
+  const int m0 = tm * WBM, n0 = tn * WBN;
+  const int ebeg = split * p.kps, eend = min(3 * p.nks, ebeg + p.kps);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave & 3, wn = wave >> 2;
+
+  f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + wn * 64 + j * 32 + (lane & 31);
-      if (col >= p.N) continue;
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int nk = max(0, eend - ebeg);
+  auto estep = [&](int t) { return ebeg + min(t, nk - 1); };  // past the end: re-read the last K-step
+  if (nk > 0) {
+    x2w_issue(p, smem, m0, n0, estep(0), wave, lane);
+    x2w_issue(p, smem + BUF, m0, n0, estep(1), wave, lane);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  const int bch = threadIdx.x & 31, brg = threadIdx.x >> 5;
+  for (int t = 0; t < nk; ++t) {
+    const u16* L = smem + (t % 3) * BUF;
+    x2w_issue(p, smem + ((t + 2) % 3) * BUF, m0, n0, estep(t + 2), wave, lane);
+    const int e = ebeg + t;
+    if (BIAS && e / p.nks != 1 && e % p.bparts == tn) {  // dz hi (pair 0) + dz lo (pair 2)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row >= p.M) continue;
-        p.slab[((size_t)split * p.M + row) * p.N + col] = acc[i][j][r];
+      for (int u = 0; u < 4; ++u) {
+        const u16x8 v = *reinterpret_cast<const u16x8*>(L + (bch >> 4) * IMG + km_off(brg + 16 * u, bch & 15));
+#pragma unroll
+        for (int x = 0; x < 8; ++x) cs[x] += h2f(v[x]);
       }
     }
+    s16x4 fr[2][8];
+    x2w_read(L, wm, wn, 0, lane, fr[0]);
+#pragma unroll
+    for (int s = 0; s < WBK / 16; ++s) {
+      if (s + 1 < WBK / 16) {
+        x2w_read(L, wm, wn, s + 1, lane, fr[(s + 1) & 1]);
+        x2w_wait<8>(fr[s & 1]);
+      } else {
+        x2w_wait<0>(fr[s & 1]);
+      }
+      const f16x8 a[2] = {x2w_cat(fr[s & 1][0], fr[s & 1][1]), x2w_cat(fr[s & 1][2], fr[s & 1][3])};
+      const f16x8 b[2] = {x2w_cat(fr[s & 1][4], fr[s & 1][5]), x2w_cat(fr[s & 1][6], fr[s & 1][7])};
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  x2w_finish(p, acc, cs, smem, BIAS, split, tn, m0, n0, wm, wn, lane);
 }
 
-// gW[m][n] (fp32) += sa sb sum_s slab[s][m][n] (fixed order); gb[m] += sa sum_s bias_slab[s][m]
-__global__ void __launch_bounds__(256) x2_wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N,
-                                                              float* __restrict__ C, int ldc,
+// gW[m][n] (fp32) += sa sb sum_s slab[s][m][n] (fixed order); gb[m] += sa sum_j bias_slab[j][m]
+// (j < splits * bparts) in the blocks past `main_blocks`: 16 columns x 16 row groups, combined in a fixed order
+__global__ void __launch_bounds__(256) x2_wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int bparts,
+                                                              int M, int N, float* __restrict__ C, int ldc,
                                                               float* __restrict__ gb, const float* __restrict__ sa,
-                                                              const float* __restrict__ sb) {
+                                                              const float* __restrict__ sb, int main_blocks) {
   const float da = *sa, dq = da * *sb;
   const int64_t MN = (int64_t)M * N;
-  if (gb) {
+  if ((int)blockIdx.x >= main_blocks) {
+    __shared__ float red[16][16];
+    const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const int m = ((int)blockIdx.x - main_blocks) * 16 + c;
     const float* bs = slab + (size_t)splits * MN;
-    for (int64_t m = blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
-      float s = 0.f;
-      for (int k = 0; k < splits; ++k) s += bs[(size_t)k * M + m];
-      gb[m] += da * s;
+    float s = 0.f;
+    if (m < M)
+      for (int k = g; k < splits * bparts; k += 16) s += bs[(size_t)k * M + m];
+    red[g][c] = s;
+    __syncthreads();
+    if (g == 0 && m < M) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t += red[q][c];
+      gb[m] += da * t;
     }
+    return;
   }
   const int64_t n4 = MN / 4;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)main_blocks * 256) {
     f32x4 s = *reinterpret_cast<const f32x4*>(slab + 4 * i);
     for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(slab + k * MN + 4 * i);
     const int64_t e = 4 * i;
@@ -782,7 +932,8 @@ bool x2_wgrad_supported(int M, int N, int T, int lda, int ldb) {
 
 size_t x2_wgrad_workspace_floats(int M, int N, int T) {
   const int splits = x2_wgrad_splits(M, N, T);
-  return (size_t)splits * M * N + (size_t)splits * M;
+  const int tiles_n = (N + WBN - 1) / WBN;  // bias partials: splits x tiles_n rows of M (the DMA loop)
+  return (size_t)splits * M * N + (size_t)splits * tiles_n * M;
 }
 
 void x2_wgrad(const void* dz, int64_t dz_ps, const void* x, int64_t x_ps, const float* sdz, const float* sx, float* gw,
@@ -806,12 +957,24 @@ void x2_wgrad(const void* dz, int64_t dz_ps, const void* x, int64_t x_ps, const 
   p.tiles_m = (M + WBM - 1) / WBM;
   p.tiles_n = (N + WBN - 1) / WBN;
   const dim3 grid(p.tiles_m * p.tiles_n * p.splits);
-  if (gb) hipLaunchKernelGGL(x2_wgrad_kernel<true>, grid, dim3(WNT), 0, stream, p);
-  else hipLaunchKernelGGL(x2_wgrad_kernel<false>, grid, dim3(WNT), 0, stream, p);
+  const char* env = std::getenv("SDML_WGRAD_DMA");  // read per call: tests A/B the two loops
+  const bool dma = !(env && std::string(env) == "0") && T % WBK == 0 &&
+                   (reinterpret_cast<uintptr_t>(dz) & 15) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                   (dz_ps % 8) == 0 && (x_ps % 8) == 0;
+  p.bparts = dma ? p.tiles_n : 1;
+  if (dma) {
+    if (gb) hipLaunchKernelGGL(x2_wgrad_dma_kernel<true>, grid, dim3(WNT), 0, stream, p);
+    else hipLaunchKernelGGL(x2_wgrad_dma_kernel<false>, grid, dim3(WNT), 0, stream, p);
+  } else if (gb) {
+    hipLaunchKernelGGL(x2_wgrad_kernel<true>, grid, dim3(WNT), 0, stream, p);
+  } else {
+    hipLaunchKernelGGL(x2_wgrad_kernel<false>, grid, dim3(WNT), 0, stream, p);
+  }
   const int64_t n4 = (int64_t)M * N / 4;
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
-  hipLaunchKernelGGL(x2_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, workspace, p.splits, M, N, gw, ldc,
-                     gb, sdz, sx);
+  const int bblocks = gb ? (M + 15) / 16 : 0;
+  hipLaunchKernelGGL(x2_wgrad_reduce_kernel, dim3(blocks + bblocks), dim3(256), 0, stream, workspace, p.splits,
+                     p.bparts, M, N, gw, ldc, gb, sdz, sx, blocks);
 }
 
 }  // namespace sdml

@@ -144,3 +144,22 @@ def test_x2_input_gradient_nt_matches_nn():
     b = bound(dz, W.t(), Nout)
     assert ((c_nn.double() - want).abs() <= b).all()
     assert ((c_nt.double() - want).abs() <= b).all()
+
+
+@pytest.mark.parametrize("T,M,N", [(16384, 1024, 1024), (4096, 520, 136)])
+def test_x2_wgrad_dma_loop_matches_staged_loop(T, M, N, monkeypatch):
+    # the LDS-DMA main loop (T % 64 == 0, default) vs the register-staged one: the same MFMA sequence and
+    # slab order (bit-identical gw); the bias sums are split differently, so gb is checked against fp64
+    dz, x = rnd(T, M, seed=21), rnd(T, N, seed=22)
+    gw0, gb0 = rnd(M, N, seed=23), rnd(M, seed=24)
+    pd, sd = split(dz)
+    px, sx = split(x)
+    out = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SDML_WGRAD_DMA", mode)
+        gw, gb = gw0.clone(), gb0.clone()
+        K.x2_wgrad_(pd, sd, px, sx, gw, gb)
+        out.append((gw, gb))
+    assert torch.equal(out[0][0], out[1][0])
+    for _, gb in out:
+        torch.testing.assert_close(gb.double(), gb0.double() + dz.double().sum(0), rtol=1e-5, atol=1e-4)

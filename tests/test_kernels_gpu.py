@@ -445,6 +445,36 @@ def test_wgrad_bf16(T, M, N):
     assert ((gb.double() - want_b).abs() <= 2 ** -7 * scale_b + 1e-6).all()
 
 
+@pytest.mark.parametrize("T,M,N", [(16384, 2304, 768), (4096, 768, 3072), (2368, 520, 136), (64, 8, 16)])
+def test_wgrad_bf16_dma_loop_matches_staged_loop(T, M, N, monkeypatch):
+    """The LDS-DMA main loop (T % 64 == 0, the default) and the register-staged one run the same MFMA
+    sequence per split and the same slab order: bit-identical gw. The bias sums are split differently
+    (the DMA loop spreads them over the column tiles), so gb is checked against fp64."""
+    g = torch.Generator(device="cpu").manual_seed(T + N)
+    gy = torch.randn(T, M, generator=g).to(DEV, torch.bfloat16)
+    x = torch.randn(T, N, generator=g).to(DEV, torch.bfloat16)
+    gw0 = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    gb0 = torch.randn(M, generator=g).to(DEV, torch.bfloat16)
+    K = _native.kernels()
+    out = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SDML_WGRAD_DMA", mode)
+        gw, gb = gw0.clone(), gb0.clone()
+        K.wgrad_bf16_(gy, x, gw, gb)
+        gw2 = gw0.clone()
+        K.wgrad_bf16_(gy, x, gw2)
+        out.append((gw, gb, gw2))
+    assert torch.equal(out[0][0], out[1][0])
+    want_b = gb0.double() + gy.double().sum(0)
+    scale_b = gy.double().abs().sum(0) + gb0.double().abs()
+    for o in out:
+        assert ((o[1].double() - want_b).abs() <= 2 ** -7 * scale_b + 1e-6).all()
+    assert torch.equal(out[0][2], out[1][2]) and torch.equal(out[0][0], out[0][2])
+    want = gw0.double() + gy.double().t() @ x.double()
+    scale = (gy.double().abs().t() @ x.double().abs()) + gw0.double().abs()
+    assert ((out[0][0].double() - want).abs() <= 2 ** -7 * scale + 1e-6).all()
+
+
 @pytest.mark.parametrize("M", [60, 70001])
 def test_head_stats_init_overwrites(M):
     """stats_init: the head overwrites a garbage-filled stats tensor with its own totals (the engine's

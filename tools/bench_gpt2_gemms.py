@@ -53,6 +53,8 @@ def main():
         res["dW addmm_"] = timeit(lambda: gw.addmm_(gy.t(), x))
         res["dW mm fp32out"] = timeit(lambda: torch.mm(gy.t(), x, out_dtype=torch.float32))
         res["dW wgrad_bf16 (HIP)"] = timeit(lambda: K.wgrad_bf16_(gy, x, gw))
+        gb = torch.zeros(outf, device=dev, dtype=bf)
+        res["dW+db wgrad_bf16 (HIP)"] = timeit(lambda: K.wgrad_bf16_(gy, x, gw, gb))
         for S in (8,):
             gs = gy.view(S, T // S, outf).transpose(1, 2)
             xs = x.view(S, T // S, inf)

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <cstdlib>
 #include <string>
 #include <type_traits>
@@ -754,6 +755,175 @@ __global__ void __launch_bounds__(NT) conv3x3_wgrad_kernel(WgArgs a) {
     }
 }
 
+// ---- LDS-DMA form of the weight gradient (opt-in: SDML_CONV_WGRAD_DMA=1) ---------------------------
+// Measured on ResNet-18 bf16 (batch 512, one MI355X): 40.6 us vs the staged loop's 40.9 for the 128-row
+// tile, 78.9 vs 72.4 for the 64-row one, the 3-stage ring slower still (4.89 vs 4.57 ms per step) — unlike
+// the dense weight gradients (gemm_bf16_wgrad.hip), this loop is not bound by the LDS staging writes, so
+// the staged loop stays the default.
+// Same tile, waves, images and slab as conv3x3_wgrad_kernel, but both images are filled by
+// global_load_lds (16 B per lane, 2 + 2 instructions per wave per K-step) into a 3-stage ring with two
+// K-steps in flight and one counted vmcnt(4) + barrier per K-step: no VGPR staging and no ds_write of
+// the 32 KiB per K-step. A DMA instruction writes 4 image rows lane-linearly, so lane l owns rows
+// 4 wave + l/16 (+ 32) and the logical chunk (l % 16) ^ swz(row) of both images (swz(r) = swz(r + 32)).
+// Taps outside the image, pixels past the split and dy rows past it read a zero page in global memory
+// (a DMA cannot zero-fill). Fragments by inline-asm transposed reads (the builtin made the compiler wait
+// for every DMA in flight before each read), lgkmcnt waited explicitly.
+__device__ __attribute__((aligned(16))) u16 g_zero16[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+__device__ __forceinline__ void glds16(const void* src, u16* lds_block) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_block, 16, 0, 0);
+}
+
+__device__ __forceinline__ s16x4 ds_tr16_asm(const u16* p) {
+  const unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) u16*)p;
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+
+template <int NR>
+__device__ __forceinline__ void lgkm_wait6(s16x4 (&f)[6]) {
+  asm volatile("s_waitcnt lgkmcnt(%6)"
+               : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]), "+v"(f[4]), "+v"(f[5])
+               : "n"(NR));
+}
+
+// NSTG = 2: 64 KiB of LDS, two workgroups per CU, one K-step in flight; 3: 96 KiB, one workgroup, two
+template <int TMR, int NSTG>
+__global__ void __launch_bounds__(NT) conv3x3_wgrad_dma_kernel(WgArgs a) {
+  constexpr int IMG = 64 * 128;
+  constexpr int TI = TMR / 64;
+  constexpr int NR = 2 * (TI + 1);  // transposed reads per substep
+  constexpr int BUF = 2 * IMG;      // A (dy) image, B (x) image
+  __shared__ __attribute__((aligned(16))) u16 smem[NSTG * BUF];
+  const int ntiles = a.tiles_m * a.tiles_n;
+  const int nwg = ntiles * a.splits;
+  const int orig = blockIdx.x;
+  int wg = orig;
+  if (nwg >= 16) {
+    const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  }
+  const int split = wg / ntiles, tile = wg % ntiles;
+  const int tm = tile % a.tiles_m, tn = tile / a.tiles_m;
+  const int m0 = tm * TMR, n0 = tn * 128;
+  const int K9 = a.KS * a.KS * a.C;
+  const int pbeg = split * a.pps, pend = min(a.M, pbeg + a.pps);
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  // this lane's DMA rows r0 = 4 wave + lane / 16 and r0 + 32, logical chunk c of both images
+  const int r0 = 4 * wave + (lane >> 4);
+  const int c = (lane & 15) ^ (((r0 & 3) << 2) | ((r0 >> 2) & 3));
+  const int acol = min(m0 + 8 * c, a.Co - 8);
+  const int nb_col = min(n0 + 8 * c, K9 - 8);
+  const int tap = nb_col / a.C, ci = nb_col % a.C, dh = tap / a.KS - a.P, dw = tap % a.KS - a.P;
+  const int HW = a.OH * a.OW;
+  const int st_n = 64 / HW, st_h = (64 % HW) / a.OW, st_w = 64 % a.OW;
+  int pn[2], ph[2], pw[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int p = pbeg + r0 + 32 * u;
+    pw[u] = p % a.OW;
+    ph[u] = (p / a.OW) % a.OH;
+    pn[u] = p / HW;
+  }
+  int pnext = pbeg;  // first pixel of the next K-step to issue
+  auto issue = [&](u16* st) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int p = pnext + r0 + 32 * u;
+      const bool in = p < pend;
+      glds16(in ? a.dy + (size_t)p * a.Co + acol : g_zero16, st + (wave + 8 * u) * 512);
+      const int ih = ph[u] * a.S + dh, iw = pw[u] * a.S + dw;
+      const bool ok = in && pn[u] < a.Nb && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      glds16(ok ? a.x + (((size_t)pn[u] * a.H + ih) * a.W + iw) * a.C + ci : g_zero16,
+             st + IMG + (wave + 8 * u) * 512);
+      pw[u] += st_w;
+      if (pw[u] >= a.OW) {
+        pw[u] -= a.OW;
+        ++ph[u];
+      }
+      ph[u] += st_h;
+      if (ph[u] >= a.OH) {
+        ph[u] -= a.OH;
+        ++pn[u];
+      }
+      pn[u] += st_n;
+    }
+    pnext += 64;
+  };
+  f32x16 acc[TI];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  const int nk = (pend - pbeg + 63) / 64;
+  if (nk > 0) {
+    issue(smem);
+    if constexpr (NSTG == 3) {
+      issue(smem + BUF);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  // fragment read addresses: trfrag's (k, col) for the A blocks (wm * TMR/2 + 32 i) and the B block (wn * 32)
+  const int g = lane >> 4, il = lane & 15, qq = il >> 2, pp = il & 3;
+  auto rd = [&](const u16* L, int s, s16x4 (&f)[6]) {
+    const int k = 16 * s + 8 * (g >> 1) + qq;
+#pragma unroll
+    for (int x = 0; x <= TI; ++x) {
+      const u16* P = x < TI ? L : L + IMG;
+      const int col = (x < TI ? wm * (TMR / 2) + 32 * x : wn * 32) + 16 * (g & 1) + 4 * pp;
+      f[2 * x] = ds_tr16_asm(P + km_off(k, col >> 3) + (col & 7));
+      f[2 * x + 1] = ds_tr16_asm(P + km_off(k + 4, col >> 3) + (col & 7));
+    }
+  };
+  for (int it = 0; it < nk; ++it) {
+    const u16* L = smem + (it % NSTG) * BUF;
+    issue(smem + ((it + NSTG - 1) % NSTG) * BUF);
+    s16x4 fr[2][6];
+    rd(L, 0, fr[0]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (s < 3) {
+        rd(L, s + 1, fr[(s + 1) & 1]);
+        lgkm_wait6<NR>(fr[s & 1]);
+      } else {
+        lgkm_wait6<0>(fr[s & 1]);
+      }
+      const s16x4* f = fr[s & 1];
+      const bf16x8 bfr = {f[2 * TI][0], f[2 * TI][1], f[2 * TI][2], f[2 * TI][3],
+                          f[2 * TI + 1][0], f[2 * TI + 1][1], f[2 * TI + 1][2], f[2 * TI + 1][3]};
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const bf16x8 af = {f[2 * i][0], f[2 * i][1], f[2 * i][2], f[2 * i][3],
+                           f[2 * i + 1][0], f[2 * i + 1][1], f[2 * i + 1][2], f[2 * i + 1][3]};
+        acc[i] = mfma(af, bfr, acc[i]);
+      }
+    }
+    if constexpr (NSTG == 3) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the past-the-end stages (zero-page reads)
+  const int col = n0 + wn * 32 + (lane & 31);
+  if (col >= K9) return;
+  float* S = a.slab + (size_t)split * a.Co * K9;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = m0 + wm * (TMR / 2) + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (co < a.Co) S[(size_t)co * K9 + col] = acc[i][r];
+    }
+}
+
 // gw[co][ci][kh][kw] (bf16, torch layout, accumulated) += sum_s slab[s][co][tap][ci]. A block is 32
 // float4 outputs (slab order, coalesced) x 8 split groups: group g sums splits g, g + 8, ... in
 // order, then the 8 partials are added in fixed order through LDS (deterministic); the 4 results
@@ -1138,10 +1308,24 @@ void conv_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* works
   const int tr = wgrad_rows(Co);
   a.tiles_m = (Co + tr - 1) / tr;
   a.tiles_n = (T * C + 127) / 128;
-  if (tr == 128)
-    hipLaunchKernelGGL(conv3x3_wgrad_kernel<128>, dim3(a.tiles_m * a.tiles_n * s), dim3(NT), 0, stream, a);
+  const dim3 grid(a.tiles_m * a.tiles_n * s);
+  const char* env = std::getenv("SDML_CONV_WGRAD_DMA");  // read per call: tests A/B the loops
+  const bool dma = env && std::string(env) == "1" && C % 8 == 0 && Co % 8 == 0 &&
+                   (reinterpret_cast<uintptr_t>(dy) & 15) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  const char* se = std::getenv("SDML_CONV_WGRAD_STAGES");
+  const bool st3 = se && std::string(se) == "3";
+  if (dma && tr == 128 && st3)
+    hipLaunchKernelGGL((conv3x3_wgrad_dma_kernel<128, 3>), grid, dim3(NT), 0, stream, a);
+  else if (dma && tr == 128)
+    hipLaunchKernelGGL((conv3x3_wgrad_dma_kernel<128, 2>), grid, dim3(NT), 0, stream, a);
+  else if (dma && st3)
+    hipLaunchKernelGGL((conv3x3_wgrad_dma_kernel<64, 3>), grid, dim3(NT), 0, stream, a);
+  else if (dma)
+    hipLaunchKernelGGL((conv3x3_wgrad_dma_kernel<64, 2>), grid, dim3(NT), 0, stream, a);
+  else if (tr == 128)
+    hipLaunchKernelGGL(conv3x3_wgrad_kernel<128>, grid, dim3(NT), 0, stream, a);
   else
-    hipLaunchKernelGGL(conv3x3_wgrad_kernel<64>, dim3(a.tiles_m * a.tiles_n * s), dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL(conv3x3_wgrad_kernel<64>, grid, dim3(NT), 0, stream, a);
   const int64_t n4 = (int64_t)Co * T * C / 4;
   const int blocks = (int)std::min<int64_t>((n4 + RD_OUT - 1) / RD_OUT, 8192);
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(RD_OUT * RD_GRP), 0, stream, workspace, s, Co, C, T,

@@ -258,3 +258,26 @@ def test_basic_block_fused_residual_gradient(stride, cin, cout):
     for (n, _), pf, pr in zip(blk.named_parameters(), grads[True][1], ref.parameters()):
         e = (pf - pr.grad).norm() / (pr.grad.norm() + 1e-6)
         assert e < 8e-2, (n, float(e))
+
+
+@pytest.mark.parametrize("N,C,Co,H,W,ks,st", [(4, 64, 128, 28, 28, 3, 2), (3, 64, 64, 9, 11, 1, 1),
+                                               (2, 256, 512, 7, 7, 3, 2), (3, 64, 128, 10, 12, 3, 1),
+                                               (8, 64, 64, 14, 14, 3, 1)])
+def test_wgrad_dma_loops_match_staged_loop(N, C, Co, H, W, ks, st, monkeypatch):
+    """The opt-in LDS-DMA weight-gradient loops (2- and 3-stage rings; zero page for padding taps and pixels
+    past a split) and the register-staged default run the same MFMA sequence: bit-identical gradients."""
+    g = torch.Generator(device="cpu").manual_seed(N * C + Co + H + ks)
+    pd = (ks - 1) // 2
+    conv = torch.nn.Conv2d(C, Co, ks, st, pd, bias=False).to(DEV, torch.bfloat16)
+    x = cl(torch.randn(N, C, H, W, generator=g).to(DEV, torch.bfloat16))
+    y = F.conv2d(x.float(), conv.weight.float(), stride=st, padding=pd)
+    dy = cl(torch.randn(y.shape, generator=g).to(DEV, torch.bfloat16))
+    out = []
+    for dma, stages in (("0", "2"), ("1", "2"), ("1", "3")):
+        monkeypatch.setenv("SDML_CONV_WGRAD_DMA", dma)
+        monkeypatch.setenv("SDML_CONV_WGRAD_STAGES", stages)
+        conv.weight.grad = None
+        xx = x.clone().requires_grad_(True)
+        conv_ops._ConvGeneralFn.apply(xx, conv.weight, st, pd).backward(dy)
+        out.append(conv.weight.grad.clone())
+    assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])

@@ -349,15 +349,6 @@ __global__ void __launch_bounds__(NT) wgrad_dma_kernel(WgParams p) {
   for (int t = 0; t < nk; ++t) {
     const u16* L = smem + (t % 3) * BUF;
     wgrad_issue(p, smem + ((t + 2) % 3) * BUF, m0, n0, kstep(t + 2), wave, lane);
-    if (do_bias && (p.bparts == 1 || t % p.bparts == tn)) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int r = brg + 16 * u;
-        const u16x8 v = *reinterpret_cast<const u16x8*>(L + (bch >> 4) * IMG + km_off(r, bch & 15));
-#pragma unroll
-        for (int e = 0; e < 8; ++e) cs[e] += bf2f(v[e]);
-      }
-    }
     s16x4 fr[2][8];  // substep s's fragments in fr[s & 1]; s + 1's reads are issued before s's MFMAs
     read_substep(L, wm, wn, 0, lane, fr[0]);
 #pragma unroll
@@ -374,6 +365,16 @@ __global__ void __launch_bounds__(NT) wgrad_dma_kernel(WgParams p) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = mfma(a[i], b[j], acc[i][j]);
+    }
+    // bias: after the K-step's MFMAs are issued (its VALU work overlaps their tail), before the barrier
+    if (do_bias && (p.bparts == 1 || t % p.bparts == tn)) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = brg + 16 * u;
+        const u16x8 v = *reinterpret_cast<const u16x8*>(L + (bch >> 4) * IMG + km_off(r, bch & 15));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs[e] += bf2f(v[e]);
+      }
     }
     asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");  // K-step t+1 landed; this wave's reads done
     __builtin_amdgcn_s_barrier();

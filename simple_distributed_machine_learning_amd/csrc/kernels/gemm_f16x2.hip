@@ -765,15 +765,6 @@ __global__ void __launch_bounds__(WNT) x2_wgrad_dma_kernel(X2Wg p) {
   for (int t = 0; t < nk; ++t) {
     const u16* L = smem + (t % 3) * BUF;
     x2w_issue(p, smem + ((t + 2) % 3) * BUF, m0, n0, estep(t + 2), wave, lane);
-    const int e = ebeg + t;
-    if (BIAS && e / p.nks != 1 && e % p.bparts == tn) {  // dz hi (pair 0) + dz lo (pair 2)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const u16x8 v = *reinterpret_cast<const u16x8*>(L + (bch >> 4) * IMG + km_off(brg + 16 * u, bch & 15));
-#pragma unroll
-        for (int x = 0; x < 8; ++x) cs[x] += h2f(v[x]);
-      }
-    }
     s16x4 fr[2][8];
     x2w_read(L, wm, wn, 0, lane, fr[0]);
 #pragma unroll
@@ -790,6 +781,16 @@ __global__ void __launch_bounds__(WNT) x2_wgrad_dma_kernel(X2Wg p) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    // bias (dz hi in pair 0 + dz lo in pair 2), after the K-step's MFMAs are issued, before the barrier
+    const int e = ebeg + t;
+    if (BIAS && e / p.nks != 1 && e % p.bparts == tn) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const u16x8 v = *reinterpret_cast<const u16x8*>(L + (bch >> 4) * IMG + km_off(brg + 16 * u, bch & 15));
+#pragma unroll
+        for (int x = 0; x < 8; ++x) cs[x] += h2f(v[x]);
+      }
     }
     asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();

@@ -58,6 +58,7 @@ struct GP {
   u16* aux;         // EPI_BIAS_GELU: U out; EPI_DGELU: U in ([M][ldaux])
   int M, N, K, lda, ldb, ldc, ldaux;
   int tiles_m, tiles_n;
+  int nostore;  // timing probe (SDML_GEMM_BF16_NOSTORE=1): the epilogue runs but skips its HBM stores
 };
 
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((unsigned)v) << 16); }
@@ -141,7 +142,7 @@ __device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&ac
     const int row = 8 * it + (lane >> 3), ch = lane & 7;
     const u16x8 v = *reinterpret_cast<const u16x8*>(W + row * 128 + 16 * (ch ^ rk_swz(row)));
     const int grow = m0 + wm * 128 + row, gcol = n0 + wn * 64 + 8 * ch;
-    if (grow >= p.M || gcol >= p.N) continue;  // (N % 8 == 0: a chunk is all in or all out)
+    if (grow >= p.M || gcol >= p.N || p.nostore) continue;  // (N % 8 == 0: a chunk is all in or all out)
     u16x8 o = v;
     if constexpr (EPI == EPI_BIAS_GELU) {
       *reinterpret_cast<u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol) = v;
@@ -431,6 +432,10 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
   p.ldaux = ldaux;
   p.tiles_m = (M + TM - 1) / TM;
   p.tiles_n = (N + TN - 1) / TN;
+  {
+    const char* e = std::getenv("SDML_GEMM_BF16_NOSTORE");
+    p.nostore = e && std::string(e) == "1";
+  }
   const dim3 grid(p.tiles_m * p.tiles_n);
 #define GB_LAUNCH(BLV, E) hipLaunchKernelGGL((gemm_bf16_kernel<BLV, E>), grid, dim3(GT), 0, stream, p)
 #define GB_EPI(BLV)                                       \

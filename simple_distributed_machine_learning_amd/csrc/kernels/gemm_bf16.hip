@@ -58,6 +58,7 @@ struct GP {
   u16* aux;         // EPI_BIAS_GELU: U out; EPI_DGELU: U in ([M][ldaux])
   int M, N, K, lda, ldb, ldc, ldaux;
   int tiles_m, tiles_n;
+  int ntstore;  // SDML_GEMM_NT_STORE=1: nontemporal epilogue stores (A/B)
   int nostore;  // timing probe (SDML_GEMM_BF16_NOSTORE=1): the epilogue runs but skips its HBM stores
 };
 
@@ -145,7 +146,9 @@ __device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&ac
     if (grow >= p.M || gcol >= p.N || p.nostore) continue;  // (N % 8 == 0: a chunk is all in or all out)
     u16x8 o = v;
     if constexpr (EPI == EPI_BIAS_GELU) {
-      *reinterpret_cast<u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol) = v;
+      u16x8* ap = reinterpret_cast<u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
+      if (p.ntstore) __builtin_nontemporal_store(v, ap);
+      else *ap = v;
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_f(bf2f(v[e])));
     } else if constexpr (EPI == EPI_DGELU) {
@@ -153,7 +156,9 @@ __device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&ac
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_grad_f(bf2f(v[e]), bf2f(u[e])));
     }
-    *reinterpret_cast<u16x8*>(p.C + (size_t)grow * p.ldc + gcol) = o;
+    u16x8* cp = reinterpret_cast<u16x8*>(p.C + (size_t)grow * p.ldc + gcol);
+    if (p.ntstore) __builtin_nontemporal_store(o, cp);
+    else *cp = o;
   }
 }
 
@@ -435,6 +440,8 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
   {
     const char* e = std::getenv("SDML_GEMM_BF16_NOSTORE");
     p.nostore = e && std::string(e) == "1";
+    const char* n = std::getenv("SDML_GEMM_NT_STORE");
+    p.ntstore = n && std::string(n) == "1";
   }
   const dim3 grid(p.tiles_m * p.tiles_n);
 #define GB_LAUNCH(BLV, E) hipLaunchKernelGGL((gemm_bf16_kernel<BLV, E>), grid, dim3(GT), 0, stream, p)

@@ -118,6 +118,7 @@ struct X2Gemm {
   float* wmax;        // optional [grid][8]: per-wave max |C| (after the epilogue ops)
   int M, N, K, lda, ldb, ldc, ldm;
   int tiles_m, tiles_n;
+  int ntstore;  // SDML_GEMM_NT_STORE=1: nontemporal epilogue stores (A/B)
 };
 
 __device__ __forceinline__ void glds16(const void* src, unsigned char* lds_block) {
@@ -215,7 +216,9 @@ __device__ __forceinline__ void x2_epilogue(const X2Gemm& p, const f32x4 (&acc)[
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) vmax = fmaxf(vmax, fabsf(v[e]));
-      *reinterpret_cast<f32x4*>(p.C + (size_t)grow * p.ldc + gcol) = v;
+      f32x4* cp = reinterpret_cast<f32x4*>(p.C + (size_t)grow * p.ldc + gcol);
+      if (p.ntstore) __builtin_nontemporal_store(v, cp);
+      else *cp = v;
     }
   }
   if (p.wmax) {
@@ -893,6 +896,10 @@ void x2_gemm(const void* A, int64_t a_ps, const void* B, int64_t b_ps, float* C,
   p.ldm = ldm;
   p.tiles_m = (M + TM - 1) / TM;
   p.tiles_n = (N + TN - 1) / TN;
+  {
+    const char* n = std::getenv("SDML_GEMM_NT_STORE");
+    p.ntstore = n && std::string(n) == "1";
+  }
   const dim3 grid(p.tiles_m * p.tiles_n);
   const int epi = (relu ? X2_RELU : 0) | (mask ? X2_MASK : 0);
 #define X2_LAUNCH(BLV, E) hipLaunchKernelGGL((x2_gemm_kernel<BLV, E>), grid, dim3(GT), 0, stream, p)

@@ -37,6 +37,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -114,13 +115,46 @@ def _parallelism(placement, n, mesh, phi, kind):
             f"over xGMI, gradient all-reduce")
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _launch_ranks(n: int) -> int:
+    """``--gpus N > 1`` without a launcher: start the N ranks as child processes (one per GPU,
+    torch.distributed.run on 127.0.0.1) BEFORE anything in this process touches the GPU, relay their
+    output and return rank 0's exit status. ``torch.cuda.device_count()`` does not initialise the
+    GPU on this image, so it is safe to check here; the host-staged transport (SDML_TRANSPORT=host)
+    lets N ranks share fewer GPUs."""
+    host_staged = os.environ.get("SDML_TRANSPORT") == "host"
+    have = torch.cuda.device_count()
+    if not host_staged and 0 < have < n:  # (no GPU at all: the CPU/Gloo rehearsal)
+        print(f"[bench] --gpus {n} but only {have} GPU(s) visible (SDML_TRANSPORT=host shares one GPU)",
+              file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ, SDML_BENCH_LAUNCHED="1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(_launch_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world != a.gpus:
+        # a mislabelled run (e.g. --gpus 8 on a 1-rank launch) would report a flat scaling curve
         if rank == 0:
-            print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+            print(f"[bench] --gpus {a.gpus} but WORLD_SIZE={world}: refusing to run", file=sys.stderr)
+        sys.exit(2)
     n = world
     place = a.placement
     predicted = plc.table(n, a.batch_per_gpu)
@@ -204,6 +238,11 @@ def main():
         l, c, cnt = engine.reduce_metrics(res)
         loss = l / max(1, cnt)
     sps = GB * a.steps / el
+    # what the process group really saw (1 and None for a single-GPU run without collectives)
+    seen_world = dist.get_world_size() if dist.is_initialized() else 1
+    seen_backend = dist.get_backend() if dist.is_initialized() else None
+    if seen_world != n:
+        raise SystemExit(f"[bench] process group has {seen_world} ranks, expected {n}")
     if rank == 0:
         out = {
             "metric": "samples/sec (whole node), 2-stage MLP on MNIST-shape synthetic",
@@ -229,6 +268,8 @@ def main():
                 "cross_fraction": phi if place != "rotate" else round((n - 1) / n, 4),
                 "boundary_bytes_across_gpus_per_step": int(cross_bytes),
                 "transport": engine.transport.name if engine.transport else None,
+                "world_size_seen": seen_world,
+                "backend": seen_backend,
                 "link_model": plc.model_dict(),
                 "predicted": predicted,
                 "microbatches": M,

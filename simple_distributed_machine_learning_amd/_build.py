@@ -130,9 +130,13 @@ def build_kernels(verbose: bool = False) -> Path:
     common = [str(kdir), str(CSRC / "common")]
     kflags = [HIPCC, "-O3", "-std=c++17", "-fPIC", f"--offload-arch={OFFLOAD_ARCH}",
               "-munsafe-fp-atomics", "-Wno-unused-result"] + [f"-I{d}" for d in common]
+    # SDML_KERNEL_EXPERIMENTS=1: timing-probe switches live, env-settable knobs (csrc/kernels/knobs.h).
+    # Never the build that ships: build() / the driver compile without it.
+    exp = ["-DSDML_KERNEL_EXPERIMENTS"] if os.environ.get("SDML_KERNEL_EXPERIMENTS") == "1" else []
+    kflags += exp
     bflags = [HIPCC, "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
               "-DTORCH_EXTENSION_NAME=_kernels", "-DTORCH_API_INCLUDE_EXTENSION_H",
-              "-Wno-unused-result", "-Wno-deprecated-declarations"]
+              "-Wno-unused-result", "-Wno-deprecated-declarations"] + exp
     binc = common + tinc + [_python_include(), "/opt/rocm/include"]
     bflags += [f"-I{d}" for d in binc]
     jobs = []

@@ -1136,14 +1136,8 @@ void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int
   a.KS = 3;
   a.P = 1;
   a.tiles_m = (a.M + BM - 1) / BM;
-  static const int engine = [] {  // SDML_CONV_FWD=im2col forces the im2col kernel (A/B tuning)
-    const char* e = std::getenv("SDML_CONV_FWD");
-    return (e && std::string(e) == "im2col") ? 0 : 1;
-  }();
-  static const int bn128_min = [] {  // BN 128 needs this many tiles, else BN 64 (more workgroups)
-    const char* e = std::getenv("SDML_CONV_BN128_MIN");
-    return e ? std::atoi(e) : 160;
-  }();
+  const int engine = knob(KNOB_CONV_FWD_IM2COL) ? 0 : 1;  // im2col kernel on request (A/B tuning)
+  const int bn128_min = knob(KNOB_CONV_BN128_MIN);  // BN 128 needs this many tiles, else BN 64 (more workgroups)
   if (engine == 1 && W <= HALO_MAX_W) {
     const bool big = Co % 128 == 0 && a.tiles_m * (Co / 128) >= bn128_min;
     const int bn = big ? 128 : 64;
@@ -1249,19 +1243,13 @@ void conv_dgrad_s2_bf16(const void* dy, const void* packed, void* dx, int Nb, in
 }
 
 static int wgrad_rows(int Co) {
-  static const bool rows64 = [] {  // SDML_CONV_WG_ROWS64=0: 128-row tiles (half idle) for Cout = 64 too
-    const char* e = std::getenv("SDML_CONV_WG_ROWS64");
-    return !(e && std::string(e) == "0");
-  }();
+  const bool rows64 = knob(KNOB_CONV_WG_ROWS64) != 0;  // 0: 128-row tiles (half idle) for Cout = 64 too
   return Co % 128 == 0 || !rows64 ? 128 : 64;
 }
 
 static int wgrad_splits(int M, int KT, int Co) {
   // the pixel range is split until the grid reaches ~two workgroups per CU (64 KB LDS, <= 128 VGPRs)
-  static const int target = [] {
-    const char* e = std::getenv("SDML_CONV_WG_BLOCKS");
-    return e ? std::max(1, std::atoi(e)) : 512;
-  }();
+  const int target = std::max(1, knob(KNOB_CONV_WG_BLOCKS));
   const int tr = wgrad_rows(Co);
   const int tiles = ((Co + tr - 1) / tr) * ((KT + 127) / 128);
   int s = target / tiles;
@@ -1309,11 +1297,9 @@ void conv_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* works
   a.tiles_m = (Co + tr - 1) / tr;
   a.tiles_n = (T * C + 127) / 128;
   const dim3 grid(a.tiles_m * a.tiles_n * s);
-  const char* env = std::getenv("SDML_CONV_WGRAD_DMA");  // read per call: tests A/B the loops
-  const bool dma = env && std::string(env) == "1" && C % 8 == 0 && Co % 8 == 0 &&
+  const bool dma = knob(KNOB_CONV_WGRAD_DMA) == 1 && C % 8 == 0 && Co % 8 == 0 &&  // (tests A/B the loops)
                    (reinterpret_cast<uintptr_t>(dy) & 15) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-  const char* se = std::getenv("SDML_CONV_WGRAD_STAGES");
-  const bool st3 = se && std::string(se) == "3";
+  const bool st3 = knob(KNOB_CONV_WGRAD_STAGES) == 3;
   if (dma && tr == 128 && st3)
     hipLaunchKernelGGL((conv3x3_wgrad_dma_kernel<128, 3>), grid, dim3(NT), 0, stream, a);
   else if (dma && tr == 128)

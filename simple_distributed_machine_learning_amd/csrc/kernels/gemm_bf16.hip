@@ -437,12 +437,8 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
   p.ldaux = ldaux;
   p.tiles_m = (M + TM - 1) / TM;
   p.tiles_n = (N + TN - 1) / TN;
-  {
-    const char* e = std::getenv("SDML_GEMM_BF16_NOSTORE");
-    p.nostore = e && std::string(e) == "1";
-    const char* n = std::getenv("SDML_GEMM_NT_STORE");
-    p.ntstore = n && std::string(n) == "1";
-  }
+  p.nostore = knob(KNOB_GEMM_BF16_NOSTORE) == 1;  // timing probe: pinned to 0 in production builds
+  p.ntstore = knob(KNOB_GEMM_NT_STORE) == 1;
   const dim3 grid(p.tiles_m * p.tiles_n);
 #define GB_LAUNCH(BLV, E) hipLaunchKernelGGL((gemm_bf16_kernel<BLV, E>), grid, dim3(GT), 0, stream, p)
 #define GB_EPI(BLV)                                       \
@@ -454,10 +450,7 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
       default: GB_LAUNCH(BLV, EPI_STORE); break;           \
     }                                                     \
   } while (0)
-  static const bool nt4 = [] {  // SDML_GEMM_BF16_NT=2phase: the one-barrier-per-K-step loop (A/B)
-    const char* e = std::getenv("SDML_GEMM_BF16_NT");
-    return !(e && std::string(e) == "2phase");
-  }();
+  const bool nt4 = knob(KNOB_GEMM_BF16_2PHASE) == 0;  // 1: the one-barrier-per-K-step loop (A/B)
   if (b_kn) {
     GB_EPI(1);
   } else if (nt4) {

@@ -434,10 +434,7 @@ int wgrad_bf16_splits(int M, int N, int T) {
   // cover the 256 CUs (default 1: floor(256 / tiles) splits); >= 8 K-steps per split. Measured on
   // the GPT-2 shapes (tools/bench_gpt2_gemms.py): 2 or 3 grid waves are 5-25 % slower — the larger
   // fp32 slab reduction costs more than the idle CUs of one partial wave.
-  static const int waves = [] {
-    const char* e = std::getenv("SDML_WGRAD_WAVES");
-    return e ? std::max(1, std::atoi(e)) : 1;
-  }();
+  const int waves = std::max(1, knob(KNOB_WGRAD_WAVES));
   int s = 256 * waves / tiles;
   const int max_by_t = T / (8 * BK);
   if (s > max_by_t) s = max_by_t;
@@ -473,8 +470,7 @@ void wgrad_bf16(const void* gy, const void* x, void* gw, void* gb, float* worksp
   p.tiles_m = (M + BM - 1) / BM;
   p.tiles_n = (N + BN - 1) / BN;
   const dim3 grid(p.tiles_m * p.tiles_n * s);
-  const char* e = std::getenv("SDML_WGRAD_DMA");  // read per call: tests A/B the two loops
-  const bool dma = !(e && std::string(e) == "0") && T % BK == 0 &&
+  const bool dma = knob(KNOB_WGRAD_DMA) != 0 && T % BK == 0 &&  // (tests A/B the two loops)
                    (reinterpret_cast<uintptr_t>(gy) & 15) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   p.bparts = dma && s > 1 ? p.tiles_n : 1;
   if (dma) {

@@ -896,10 +896,7 @@ void x2_gemm(const void* A, int64_t a_ps, const void* B, int64_t b_ps, float* C,
   p.ldm = ldm;
   p.tiles_m = (M + TM - 1) / TM;
   p.tiles_n = (N + TN - 1) / TN;
-  {
-    const char* n = std::getenv("SDML_GEMM_NT_STORE");
-    p.ntstore = n && std::string(n) == "1";
-  }
+  p.ntstore = knob(KNOB_GEMM_NT_STORE) == 1;
   const dim3 grid(p.tiles_m * p.tiles_n);
   const int epi = (relu ? X2_RELU : 0) | (mask ? X2_MASK : 0);
 #define X2_LAUNCH(BLV, E) hipLaunchKernelGGL((x2_gemm_kernel<BLV, E>), grid, dim3(GT), 0, stream, p)
@@ -913,10 +910,7 @@ void x2_gemm(const void* A, int64_t a_ps, const void* B, int64_t b_ps, float* C,
     }                                                          \
   } while (0)
 #define X2_NT4(E) hipLaunchKernelGGL((x2_gemm_nt4_kernel<E>), grid, dim3(GT), 0, stream, p)
-  static const bool nt4 = [] {  // SDML_X2_NT=2phase: the one-barrier-per-K-step loop (A/B)
-    const char* e = std::getenv("SDML_X2_NT");
-    return !(e && std::string(e) == "2phase");
-  }();
+  const bool nt4 = knob(KNOB_X2_2PHASE) == 0;  // 1: the one-barrier-per-K-step loop (A/B)
   if (b_kn) {
     X2_EPI(1);
   } else if (nt4) {
@@ -965,8 +959,7 @@ void x2_wgrad(const void* dz, int64_t dz_ps, const void* x, int64_t x_ps, const 
   p.tiles_m = (M + WBM - 1) / WBM;
   p.tiles_n = (N + WBN - 1) / WBN;
   const dim3 grid(p.tiles_m * p.tiles_n * p.splits);
-  const char* env = std::getenv("SDML_WGRAD_DMA");  // read per call: tests A/B the two loops
-  const bool dma = !(env && std::string(env) == "0") && T % WBK == 0 &&
+  const bool dma = knob(KNOB_WGRAD_DMA) != 0 && T % WBK == 0 &&  // (tests A/B the two loops)
                    (reinterpret_cast<uintptr_t>(dz) & 15) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
                    (dz_ps % 8) == 0 && (x_ps % 8) == 0;
   p.bparts = dma ? p.tiles_n : 1;

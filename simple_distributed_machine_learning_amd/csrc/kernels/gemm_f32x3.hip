@@ -673,21 +673,14 @@ static int g_x3_variant = 0;  // pipeline A/B: 0 = EARLY split (default), 1 = sp
 // gradient 161 us 1-deep (167 us with 2 workgroups/CU) vs 154 us DEEP. SDML_X3_DEEP=0/1 forces one
 // for both (A/B).
 static bool x3_deep(bool dflt) {
-  static const int force = [] {
-    const char* e = getenv("SDML_X3_DEEP");
-    return e ? (e[0] == '0' ? 0 : 1) : -1;
-  }();
+  const int force = knob(KNOB_X3_DEEP);
   return force < 0 ? dflt : force == 1;
 }
 
 // experiment selector for the uint8 kernels (SDML_U8_VARIANT). Forward (engine path, SDML_U8_FWD=x3):
 // 1 = no FRESH partials, 2 = no epilogue (timing only), 3 = both. Weight gradient: 1 = FRESH partials.
 static int u8_variant() {
-  static const int v = [] {
-    const char* e = getenv("SDML_U8_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
+  return knob(KNOB_U8_VARIANT);  // timing variants: pinned to 0 in production builds
 }
 
 bool gemm_f32x3_eligible(const GemmArgs& g) {

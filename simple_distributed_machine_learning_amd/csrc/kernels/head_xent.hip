@@ -774,11 +774,7 @@ int head_rows_per_chunk(int M) { return M <= SMALL_BATCH ? HTHR / 16 : HTHR / 4;
 
 // the MFMA head (default) or the 4-lanes-per-row VALU head (SDML_HEAD=v1, A/B only)
 static bool head_use_mfma() {
-  static const bool v = [] {
-    const char* e = getenv("SDML_HEAD");
-    return !(e && e[0] == 'v' && e[1] == '1');
-  }();
-  return v;
+  return knob(KNOB_HEAD_VALU) == 0;
 }
 
 // MFMA head grid: 16-row tiles, ~2 waves per SIMD, each wave several tiles (its dW partial stays
@@ -796,10 +792,7 @@ int head_fused_blocks(int M, int* chunks_per_block) {
   if (head_use_mfma()) return head_mfma_blocks(M, chunks_per_block);
   const int rows = head_rows_per_chunk(M);
   const int chunks = (M + rows - 1) / rows;
-  static const int max_blocks = [] {  // A/B knob (SDML_HEAD_MAX_BLOCKS)
-    const char* e = getenv("SDML_HEAD_MAX_BLOCKS");
-    return e ? std::max(1, atoi(e)) : 512;
-  }();
+  const int max_blocks = std::max(1, knob(KNOB_HEAD_MAX_BLOCKS));  // A/B knob
   int blocks = chunks < max_blocks ? chunks : max_blocks;
   int cpb = (chunks + blocks - 1) / blocks;
   blocks = (chunks + cpb - 1) / cpb;

@@ -5,6 +5,8 @@
 
 #include <cstdint>
 
+#include "knobs.h"
+
 namespace sdml {
 
 // The head's deferred slab reduction (head_logsoftmax_nll with `defer`): the per-block slabs and where

@@ -1,0 +1,52 @@
+// Kernel-variant switches, read on every launch from one table (no getenv on the hot path).
+//
+// Two kinds:
+//  * variant switches pick between two CORRECT implementations of the same op (e.g. the LDS-DMA
+//    weight-gradient loop vs the register-staged one). Tests A/B them through set_knob() (the
+//    _kernels.set_knob binding); the value stays until it is set again.
+//  * probe switches exist only to time a kernel with part of its work removed (e.g. the bf16 GEMM
+//    without its output stores). Their results are WRONG by design, so in production builds they are
+//    pinned to their defaults: knob() returns the default and set_knob() refuses them.
+//
+// Environment variables (SDML_<NAME>) are consulted only in builds compiled with
+// -DSDML_KERNEL_EXPERIMENTS (SDML_KERNEL_EXPERIMENTS=1 python -m ..._build kernels), once, at first use.
+#pragma once
+
+namespace sdml {
+
+enum KnobId : int {
+  KNOB_CONV_FWD_IM2COL = 0,  // 1: the im2col conv forward instead of the halo kernel
+  KNOB_CONV_BN128_MIN,       // tiles needed before a conv forward uses 128-wide column tiles
+  KNOB_CONV_WG_ROWS64,       // 0: 128-row conv weight-gradient tiles for Cout = 64 too
+  KNOB_CONV_WG_BLOCKS,       // conv weight-gradient target workgroups
+  KNOB_CONV_WGRAD_DMA,       // 1: LDS-DMA conv weight-gradient loop
+  KNOB_CONV_WGRAD_STAGES,    // its ring depth (2 or 3)
+  KNOB_GEMM_NT_STORE,        // 1: nontemporal epilogue stores (bf16 / two-plane GEMMs)
+  KNOB_GEMM_BF16_2PHASE,     // 1: the one-barrier-per-K-step bf16 NT loop
+  KNOB_WGRAD_WAVES,          // bf16 weight-gradient grid waves
+  KNOB_WGRAD_DMA,            // 0: register-staged weight-gradient loop (bf16 and two-plane)
+  KNOB_X2_2PHASE,            // 1: the one-barrier-per-K-step two-plane NT loop
+  KNOB_X3_DEEP,              // -1 auto, 0/1: force the bf16x3 engine's pipelining depth
+  KNOB_HEAD_VALU,            // 1: the VALU classifier head instead of the MFMA head
+  KNOB_HEAD_MAX_BLOCKS,      // VALU head grid cap
+  KNOB_U8_WGRAD_XCD,         // uint8 weight gradient: XCD-aware tile order
+  KNOB_U8_FWD_WMT,           // uint8 forward wave-tile rows (0 auto)
+  KNOB_U8_FWD_WAVES,         // uint8 forward waves per block (0 auto)
+  KNOB_U8_FWD_X3,            // 1: uint8 forward on the older bf16x3 kernel
+  KNOB_U8_WGRAD_X3,          // 1: uint8 weight gradient on the older bf16x3 kernel
+  // ---- probe switches (pinned in production builds) ----
+  KNOB_GEMM_BF16_NOSTORE,    // 1: bf16 GEMM skips its output stores (timing only)
+  KNOB_U8_VARIANT,           // bf16x3 uint8 kernels' timing variants
+  KNOB_COUNT
+};
+
+// current value of a switch
+int knob(KnobId id);
+// set a switch by name (the enum name without KNOB_); false if unknown or a pinned probe switch
+bool set_knob(const char* name, int value);
+// reset every switch to its default
+void reset_knobs();
+// whether probe switches are live in this build
+bool kernel_experiments_build();
+
+}  // namespace sdml

@@ -910,11 +910,7 @@ __global__ void __launch_bounds__(1024) slab_head_reduce_kernel(const float* __r
 // substeps of the last K-step that hold k < K (lane half 0 covers its first FBK / 2 k; the rest
 // multiply zero-padded weights)
 static int wgrad_xcd() {
-  static const int v = [] {
-    const char* e = getenv("SDML_U8_WGRAD_XCD");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
+  return knob(KNOB_U8_WGRAD_XCD);
 }
 
 static int tail_substeps(int K) {
@@ -1022,14 +1018,8 @@ void split_planes_pad(const float* w, unsigned short* out, int N, int K, int Kp,
 
 // the forward's block geometry for M rows: 16 waves of 512 rows, or 8 waves of 128 WMT rows
 static void u8_fwd_geometry(int M, bool& w16, int& wmt, int& bm) {
-  static const int wmt_env = [] {
-    const char* e = getenv("SDML_U8_FWD_WMT");
-    return e ? atoi(e) : 0;
-  }();
-  static const int waves_env = [] {  // 8 (512 threads) or 16 (1024 threads, 4 waves per SIMD)
-    const char* e = getenv("SDML_U8_FWD_WAVES");
-    return e ? atoi(e) : 0;
-  }();
+  const int wmt_env = knob(KNOB_U8_FWD_WMT);
+  const int waves_env = knob(KNOB_U8_FWD_WAVES);  // 8 (512 threads) or 16 (1024 threads, 4 waves per SIMD)
   // 512-row blocks (half the LDS weight traffic per MFMA) once they still cover every CU, as 16
   // waves of 64 x 64 (4 waves per SIMD at 115 VGPRs; 8 waves of 128 x 64 need 199: 63.9-65.3 vs
   // 66.5-67.3 us at 131072 rows, tools/gpu_fwd16.sh); smaller batches: 256-row blocks of 8 waves

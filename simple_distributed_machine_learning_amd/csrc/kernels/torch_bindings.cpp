@@ -234,10 +234,7 @@ torch::Tensor linear_fwd_u8(torch::Tensor x, torch::Tensor w, c10::optional<torc
     return with_mask(linear_fwd_f32(pixels_f32(x, scale), w, b, relu));
   }
   auto y = torch::empty({M, N}, w.options());
-  static const bool legacy = [] {
-    const char* e = getenv("SDML_U8_FWD");
-    return e && std::string(e) == "x3";
-  }();
+  const bool legacy = sdml::knob(sdml::KNOB_U8_FWD_X3) == 1;
   if (!legacy && sdml::u8_fwd_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr())) {
     const int Kp = sdml::u8_fwd_kpad((int)K);
     // planes: a caller-owned cache [2][N][Kp] (fp16 bits of W * 2^8, zero padding columns; kept
@@ -292,10 +289,7 @@ void linear_wgrad_u8(torch::Tensor x, torch::Tensor gz, torch::Tensor gw, c10::o
     linear_bwd_f32(pixels_f32(x, scale), c10::nullopt, gz, /*w=*/gw, gw, gb, false, false, false);
     return;
   }
-  static const bool legacy_wgrad = [] {
-    const char* e = getenv("SDML_U8_WGRAD");
-    return e && std::string(e) == "x3";
-  }();
+  const bool legacy_wgrad = sdml::knob(sdml::KNOB_U8_WGRAD_X3) == 1;
   // mlp_u8.hip's kernel writes gw and gb through one [N * K + N] span: gb must follow gw
   const bool gb_follows = opt_ptr(gb) && gw.is_contiguous() && gb->is_contiguous() &&
                           opt_ptr(gb) == gw.data_ptr<float>() + N * K;
@@ -1764,6 +1758,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dy"), py::arg("y"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("relu"),
         py::arg("need_dres"), py::arg("ggamma"), py::arg("gbeta"), py::arg("beta") = py::none());
   m.def("bn_nhwc_eval", &bn_nhwc_eval, "BatchNorm with running statistics (+residual)(+ReLU)");
+  m.def("set_knob", [](const std::string& name, int value) {
+          TORCH_CHECK(sdml::set_knob(name.c_str(), value), "unknown kernel knob, or a timing probe that only ",
+                      "SDML_KERNEL_EXPERIMENTS builds accept: ", name);
+        }, "set a kernel-variant switch (csrc/kernels/knobs.h)", py::arg("name"), py::arg("value"));
+  m.def("reset_knobs", &sdml::reset_knobs, "every kernel-variant switch back to its default");
+  m.def("kernel_experiments_build", &sdml::kernel_experiments_build,
+        "whether timing-probe switches are live (SDML_KERNEL_EXPERIMENTS build)");
   m.def("gemm_f32_set_mode", &sdml::gemm_f32_set_mode, "fp32 GEMM engine: 1 = bf16x3 split (default), 0 = fp32 MFMA");
   m.def("gemm_f32_mode", &sdml::gemm_f32_mode, "current fp32 GEMM engine");
   m.def("gemm_f32_set_variant", &sdml::gemm_f32_set_variant, "fp32 GEMM variant (tuning: 0 auto, 16, 32)");

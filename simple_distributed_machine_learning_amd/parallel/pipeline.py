@@ -272,13 +272,21 @@ class PipelineEngine:
         """
         t0 = time.perf_counter()
         dev = self.device
+        rotate_a2a = self.kind == "rotate" and self.use_alltoall and self.P == 2
         if self.debug_sync and batch_size > 0:
-            self._check_targets(dataset, start, batch_size)
+            # rotate: heads run on rows of every owner of the replica group's block, not just this shard
+            n_chk = batch_size * (self.mesh.pp if self.kind == "rotate" else 1)
+            self._check_targets(dataset, start, n_chk)
         if batch_size <= 0:  # a DP replica with no samples in a ragged last batch
             if train:
                 self.flat.zero_grad()
                 self.grad_sync.reset()
-                self.grad_sync.finish()  # still joins the collectives of its replica group
+                # still joins the collectives of its replica group, with the SAME collective sequence the
+                # data-bearing ranks issue (rotate all-to-all: one all-reduce over the whole flat buffer)
+                if rotate_a2a:
+                    self.grad_sync.finish_all()
+                else:
+                    self.grad_sync.finish()
                 if step_optimizer:
                     self.optimizer.step()
                     self.global_step += 1
@@ -291,7 +299,7 @@ class PipelineEngine:
                 return res
         if train and step_optimizer and self._cnn_step_ok(batch_size):
             return self._run_cnn_step(dataset, start, batch_size, global_batch, t0)
-        if self.kind == "rotate" and self.use_alltoall and self.P == 2:
+        if rotate_a2a:
             return self._run_rotate_alltoall(dataset, start, batch_size, train, global_batch, step_optimizer, t0)
         if self.kind == "rotate":
             # every rank owns a shard of ``batch_size`` samples at start + owner*batch_size,
@@ -719,15 +727,16 @@ class PipelineEngine:
     def _small_step_ok(self, batch_size: int) -> bool:
         """Both stages of the 784-128-10 MLP on this (only) rank, fp32 weights, a batch the one-launch
         step kernel takes, and no gradients pending from an earlier step_optimizer=False call."""
-        if self._small_step is None:
+        if self._small_step is None:  # static: model shapes and placement only
             s = self.stages
             self._small_step = bool(
                 self.device.type == "cuda" and self.mesh.world_size == 1 and self.P == 2 and 0 in s and 1 in s
-                and os.environ.get("SDML_SMALL_STEP", "1") != "0" and not self.timing and not self.debug_sync
                 and self.optimizer.master is None and hasattr(s[0], "layers") and hasattr(s[1], "layers")
                 and [tuple(l.weight.shape) for l in s[0].layers()] == [(128, 784)]
                 and [tuple(l.weight.shape) for l in s[1].layers()] == [(10, 128)])
-        return self._small_step and batch_size <= 128 and self.flat.grads_zero
+        # per call: timing / debug_sync may be switched on after the first step
+        return (self._small_step and batch_size <= 128 and self.flat.grads_zero and not self.timing
+                and not self.debug_sync and os.environ.get("SDML_SMALL_STEP", "1") != "0")
 
     def _run_small_mlp_step(self, dataset, start, batch_size, global_batch, t0):
         """The reference-size training step (B <= 128, e.g. its B = 60) in two kernel launches (ops.mlp_small_step):
@@ -766,17 +775,20 @@ class PipelineEngine:
             self._cnn_step = bool(
                 self.device.type == "cuda" and self.mesh.world_size == 1 and self.P == 2 and 0 in s and 1 in s
                 and isinstance(s[0], Network1Stage) and isinstance(s[1], Network2Stage)
-                and os.environ.get("SDML_SMALL_STEP", "1") != "0" and not self.timing and not self.debug_sync
                 and self.optimizer.master is None)
-        return (self._cnn_step and 0 < batch_size <= 4096 and self.flat.grads_zero and self.training
-                and self.stages[0].training and self.stages[1].training)
+        # M == 1 only: the per-stage path draws one host dropout seed per micro-batch and stage, the
+        # two-launch step draws two per step, so only at M == 1 do both paths draw the same masks
+        return (self._cnn_step and self.M == 1 and 0 < batch_size <= 4096 and self.flat.grads_zero
+                and self.training and self.stages[0].training and self.stages[1].training and not self.timing
+                and not self.debug_sync and os.environ.get("SDML_SMALL_STEP", "1") != "0")
 
     def _run_cnn_step(self, dataset, start, batch_size, global_batch, t0):
         """The reference's own workload (its CNN at B = 60) as ONE per-sample kernel (stage 0 forward, stage 1
         forward + NLL + backward, stage 0 backward) + ONE reduction/SGD kernel: the three-kernel step with
         per-block weight-gradient atomics, a separate SGD launch and a dropout-counter launch was launch- and
         atomic-bound (profiles/r3_ref_cnn_kernel_stats.txt). Dropout seeds are drawn in the same order as the
-        per-stage path (stage 0, then stage 1), so both draw the same masks."""
+        per-stage path (stage 0, then stage 1), so at M = 1 (the only case _cnn_step_ok admits) both draw the
+        same masks."""
         from ..models.ref_cnn import _draw_seed
 
         dev = self.device

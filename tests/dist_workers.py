@@ -41,3 +41,41 @@ def train_worker(rank, world, model, kind, M, pp, steps, B, seed=3, kw=None, tp=
             "eval": (el, ec, en), "bytes_sent": eng.transport.bytes_sent if eng.transport else 0,
             "transport": eng.transport.name if eng.transport else None,
             "pool_allocs": eng.bufs.allocations, "pool_allocs_first": allocs_first}
+
+
+def empty_replica_worker(rank, world, pp, B, steps, seed=3):
+    """rotate, dp replicas of a pp-rank group: replica 1 gets NO samples every step (batch 0), replica 0
+    gets B per owner; global_batch is fixed to replica 0's samples. Returns the trained weights."""
+    from simple_distributed_machine_learning_amd.data import SyntheticMNIST
+    from simple_distributed_machine_learning_amd.models import get_model_spec
+    from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh
+
+    mesh = init_mesh(pp=pp, schedule_kind="rotate", rank=rank, world_size=world, device=torch.device("cpu"),
+                     backend="gloo", timeout_s=120)
+    eng = PipelineEngine(get_model_spec("mlp", 2), mesh, schedule_kind="rotate", num_microbatches=2 * pp, lr=0.1,
+                         momentum=0.5, seed=seed)
+    ds = SyntheticMNIST(B * pp * steps, seed=7)
+    for step in range(steps):
+        n = B if mesh.dp_rank == 0 else 0
+        eng.run(ds, step * B * pp, n, train=True, global_batch=B * pp)
+    return {"state": eng.state_dicts(), "dp_rank": mesh.dp_rank}
+
+
+def debug_sync_rotate_worker(rank, world, B):
+    """rotate, debug_sync: a bad label in a PEER's shard (rows every head may see) must be refused on every
+    rank before any collective. Returns the error text (None if nothing was raised)."""
+    from simple_distributed_machine_learning_amd.data import SyntheticMNIST
+    from simple_distributed_machine_learning_amd.models import get_model_spec
+    from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh
+
+    mesh = init_mesh(pp=world, schedule_kind="rotate", rank=rank, world_size=world, device=torch.device("cpu"),
+                     backend="gloo", timeout_s=60)
+    eng = PipelineEngine(get_model_spec("mlp", 2), mesh, schedule_kind="rotate", num_microbatches=2 * world,
+                         lr=0.1, momentum=0.5, seed=1, debug_sync=True)
+    ds = SyntheticMNIST(B * world, seed=7)
+    ds.y[(world - 1) * B + 3] = 10  # owned by the last rank
+    try:
+        eng.run(ds, 0, B, train=True)
+    except ValueError as e:
+        return str(e)
+    return None

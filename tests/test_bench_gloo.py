@@ -34,6 +34,7 @@ def _run(world, extra=()):
     assert d["n_gpus"] == world and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
     assert d["config"]["global_batch"] == world * 256 and d["value"] > 0 and d["higher_is_better"] is True
     assert d["final_loss"] is not None and d["final_loss"] == d["final_loss"]  # finite
+    assert d["config"]["world_size_seen"] == world and d["config"]["backend"] == "gloo"
     return d
 
 
@@ -55,3 +56,23 @@ def test_bench_four_ranks_one_json_line(placement):
 def test_bench_two_ranks_cross_fraction_override():
     d = _run(2, ["--placement", "rotate", "--cross_fraction", "0.25"])
     assert d["config"]["boundary_bytes_across_gpus_per_step"] == 2 * 64 * (512 + 40)
+
+
+def test_bench_gpus_flag_spawns_ranks_on_cpu(tmp_path):
+    """No launcher: ``bench.py --gpus 2`` starts 2 ranks itself; a WORLD_SIZE/--gpus mismatch exits
+    non-zero without printing a result."""
+    import subprocess
+
+    env = dict(os.environ, SDML_BENCH_BATCH="256", PYTHONPATH=ROOT)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["world_size_seen"] == 2
+    r = subprocess.run(cmd, env=dict(env, WORLD_SIZE="1", RANK="0"), capture_output=True, text=True, timeout=120,
+                       cwd=str(tmp_path))
+    assert r.returncode == 2 and not [l for l in r.stdout.splitlines() if l.startswith("{")]

@@ -273,11 +273,14 @@ def test_wgrad_dma_loops_match_staged_loop(N, C, Co, H, W, ks, st, monkeypatch):
     y = F.conv2d(x.float(), conv.weight.float(), stride=st, padding=pd)
     dy = cl(torch.randn(y.shape, generator=g).to(DEV, torch.bfloat16))
     out = []
-    for dma, stages in (("0", "2"), ("1", "2"), ("1", "3")):
-        monkeypatch.setenv("SDML_CONV_WGRAD_DMA", dma)
-        monkeypatch.setenv("SDML_CONV_WGRAD_STAGES", stages)
-        conv.weight.grad = None
-        xx = x.clone().requires_grad_(True)
-        conv_ops._ConvGeneralFn.apply(xx, conv.weight, st, pd).backward(dy)
-        out.append(conv.weight.grad.clone())
+    try:
+        for dma, stages in ((0, 2), (1, 2), (1, 3)):
+            K.set_knob("CONV_WGRAD_DMA", dma)
+            K.set_knob("CONV_WGRAD_STAGES", stages)
+            conv.weight.grad = None
+            xx = x.clone().requires_grad_(True)
+            conv_ops._ConvGeneralFn.apply(xx, conv.weight, st, pd).backward(dy)
+            out.append(conv.weight.grad.clone())
+    finally:
+        K.reset_knobs()
     assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])

@@ -155,11 +155,14 @@ def test_x2_wgrad_dma_loop_matches_staged_loop(T, M, N, monkeypatch):
     pd, sd = split(dz)
     px, sx = split(x)
     out = []
-    for mode in ("1", "0"):
-        monkeypatch.setenv("SDML_WGRAD_DMA", mode)
-        gw, gb = gw0.clone(), gb0.clone()
-        K.x2_wgrad_(pd, sd, px, sx, gw, gb)
-        out.append((gw, gb))
+    try:
+        for mode in (1, 0):
+            K.set_knob("WGRAD_DMA", mode)
+            gw, gb = gw0.clone(), gb0.clone()
+            K.x2_wgrad_(pd, sd, px, sx, gw, gb)
+            out.append((gw, gb))
+    finally:
+        K.reset_knobs()
     assert torch.equal(out[0][0], out[1][0])
     for _, gb in out:
         torch.testing.assert_close(gb.double(), gb0.double() + dz.double().sum(0), rtol=1e-5, atol=1e-4)

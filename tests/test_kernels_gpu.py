@@ -457,13 +457,16 @@ def test_wgrad_bf16_dma_loop_matches_staged_loop(T, M, N, monkeypatch):
     gb0 = torch.randn(M, generator=g).to(DEV, torch.bfloat16)
     K = _native.kernels()
     out = []
-    for mode in ("1", "0"):
-        monkeypatch.setenv("SDML_WGRAD_DMA", mode)
-        gw, gb = gw0.clone(), gb0.clone()
-        K.wgrad_bf16_(gy, x, gw, gb)
-        gw2 = gw0.clone()
-        K.wgrad_bf16_(gy, x, gw2)
-        out.append((gw, gb, gw2))
+    try:
+        for mode in (1, 0):
+            K.set_knob("WGRAD_DMA", mode)
+            gw, gb = gw0.clone(), gb0.clone()
+            K.wgrad_bf16_(gy, x, gw, gb)
+            gw2 = gw0.clone()
+            K.wgrad_bf16_(gy, x, gw2)
+            out.append((gw, gb, gw2))
+    finally:
+        K.reset_knobs()
     assert torch.equal(out[0][0], out[1][0])
     want_b = gb0.double() + gy.double().sum(0)
     scale_b = gy.double().abs().sum(0) + gb0.double().abs()

@@ -47,12 +47,15 @@ def _compare(results, ref, rtol=1e-4, atol=1e-5):
 
 
 @pytest.mark.parametrize("world,mode", [(2, "factored"), (4, "factored"), (2, "whole_grad"), (2, "u8"),
-                                        (4, "u8"), (2, "u8_phi")])
+                                        (4, "u8"), (2, "u8_phi"), (2, "u8_dp"), (4, "u8_dp")])
 def test_rotate_multirank_on_device(world, mode, monkeypatch):
     """rotate on the device engine at R = 2, 4: factored boundary gradient (the head's dl crosses),
     the whole gradient (SDML_ROTATE_FACTORED=0), and uint8 pixels where the received factor goes
     straight into the first layer's weight-gradient kernel (4096-row waves: the uint8 kernels'
-    shapes); u8_phi: a quarter of each wave crosses (balanced placement)."""
+    shapes); u8_phi: a quarter of each wave crosses (balanced placement); u8_dp: nothing crosses
+    (cross_fraction 0, the placement the N > 1 benchmark picks): the fused forward+head kernel, the
+    deferred head reduction inside the weight-gradient reduction, the gradient all-reduce and the
+    unfused SGD, at the uint8 kernels' shapes."""
     kw = dict(GPU)
     steps, M = 2, 2 * world
     B = 48
@@ -63,10 +66,13 @@ def test_rotate_multirank_on_device(world, mode, monkeypatch):
         B = 8192
     if mode == "u8_phi":
         kw["cross_fraction"] = 0.25
+    if mode == "u8_dp":
+        kw["cross_fraction"] = 0.0
+        M = world  # one wave per rank, as bench.py runs dp
     res = run_ranks(train_worker, world, "mlp", "rotate", M, world, steps, B, 3, kw, timeout=400)
     ref = _single("mlp", M, steps, world * B, "rotate", {"pixels": kw.get("pixels", "f32")})
     _compare(res, ref)
-    assert all(r["bytes_sent"] > 0 for r in res)
+    assert all((r["bytes_sent"] > 0) == (mode != "u8_dp") for r in res)
     assert all(r["pool_allocs"] == r["pool_allocs_first"] for r in res)  # persistent boundary buffers
 
 
@@ -83,10 +89,16 @@ def test_neighbour_pipelines_on_device(kind, world, pp, M):
     assert all(r["pool_allocs"] == r["pool_allocs_first"] for r in res)
 
 
+def _bench_json(r):
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
 def test_bench_two_ranks_on_one_gpu():
     """bench.py exactly as the driver launches it for N = 2 (torch.distributed.run, one rank per
     process), its ranks sharing the GPU through the host-staged transport: one JSON line, the
-    placement's measured boundary bytes."""
+    placement's measured boundary bytes, the rank count the process group saw."""
     env = dict(os.environ, SDML_TRANSPORT="host", SDML_BENCH_BATCH="8192", PYTHONPATH=ROOT)
     for place, cross in (("rotate", True), ("auto", None)):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
@@ -94,9 +106,25 @@ def test_bench_two_ranks_on_one_gpu():
                "--gpus", "2", "--steps", "3", "--warmup", "1", "--placement", place]
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-        lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-        assert len(lines) == 1, r.stdout
-        d = json.loads(lines[0])
+        d = _bench_json(r)
         assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["transport"] == "host"
+        assert d["config"]["world_size_seen"] == 2 and d["config"]["backend"] == "gloo"
         if cross:
             assert d["config"]["boundary_bytes_across_gpus_per_step"] == 2 * 4096 * (512 + 40)
+
+
+def test_bench_spawns_its_ranks_without_a_launcher():
+    """``python bench.py --gpus 2`` with no WORLD_SIZE in the environment starts its own two ranks
+    (before touching the GPU) instead of silently running one: n_gpus and world_size_seen are 2."""
+    env = dict(os.environ, SDML_TRANSPORT="host", SDML_BENCH_BATCH="8192", PYTHONPATH=ROOT)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = _bench_json(r)
+    assert d["n_gpus"] == 2 and d["config"]["world_size_seen"] == 2 and d["value"] > 0
+    # a launcher/flag mismatch is fatal, not a relabelled 1-rank run
+    env1 = dict(env, WORLD_SIZE="1", RANK="0")
+    r = subprocess.run(cmd, env=env1, capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode != 0 and not [l for l in r.stdout.splitlines() if l.startswith("{")]

@@ -129,3 +129,20 @@ def test_debug_sync_rejects_out_of_range_targets():
     ds.y[40] = -100
     with pytest.raises(ValueError, match="target out of range"):
         e.run(ds, 32, 32, train=True)
+
+
+def test_kernel_knobs_pin_timing_probes_in_production_builds():
+    """a production build cannot switch on a probe that skips work (the bf16 GEMM
+    without its output stores); variant switches between correct kernels are explicit setters."""
+    import pytest
+
+    from simple_distributed_machine_learning_amd import _native
+
+    K = _native.kernels()
+    assert not K.kernel_experiments_build()
+    with pytest.raises(RuntimeError, match="probe"):
+        K.set_knob("GEMM_BF16_NOSTORE", 1)
+    with pytest.raises(RuntimeError, match="unknown"):
+        K.set_knob("NO_SUCH_KNOB", 1)
+    K.set_knob("WGRAD_DMA", 0)
+    K.reset_knobs()

@@ -217,3 +217,27 @@ def test_host_staged_transport_matches_direct(kind, world, pp, M):
         assert a["losses"] == b["losses"]
         # persistent boundary buffers: nothing new after the first step
         assert a["pool_allocs"] == a["pool_allocs_first"]
+
+
+def test_rotate_replica_with_no_samples_joins_the_same_collectives():
+    """rotate with dp = 2 replicas of a 2-rank group, replica 1 given 0 samples: it must post the same
+    gradient collective as the data-bearing replica (one all-reduce over the whole flat buffer), so
+    nothing hangs and every rank ends with replica 0's weights (= a 2-rank run on its data alone)."""
+    from dist_workers import empty_replica_worker
+
+    B, steps = 24, 2
+    res = run_ranks(empty_replica_worker, 4, 2, B, steps, timeout=200)
+    ref = run_ranks(empty_replica_worker, 2, 2, B, steps, timeout=200)
+    for r in res:
+        for s, sd in r["state"].items():
+            for k, v in sd.items():
+                torch.testing.assert_close(v, ref[0]["state"][s][k], rtol=1e-5, atol=1e-6, msg=f"stage {s} {k}")
+
+
+def test_debug_sync_rotate_checks_every_owners_rows():
+    """under rotate a head runs on rows of every owner, so debug_sync checks the whole replica
+    group's block: a bad label in the last rank's shard is refused on rank 0 as well."""
+    from dist_workers import debug_sync_rotate_worker
+
+    res = run_ranks(debug_sync_rotate_worker, 2, 24, timeout=120)
+    assert all(r is not None and "target out of range" in r for r in res), res

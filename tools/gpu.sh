@@ -9,6 +9,8 @@
 #                                                           -> gpurun_out/<name>/kernel_stats.txt
 #   tools/gpu.sh pmc   <name> <counters> <cmd...>           one PMC pass (SIGKILL after 90 s)
 #                                                           -> gpurun_out/<name>/pmc.txt
+#   tools/gpu.sh configs <timeout_s> [config...]            tools/bench_configs.py per config (default: all
+#                                                           five) -> gpurun_out/configs.jsonl
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -57,6 +59,15 @@ case "$task" in
     if [ $rc -ne 0 ]; then tail -20 "$d/run.log"; exit $rc; fi
     python tools/summarize_profile.py pmc $(find "$d/raw" -name "*counter_collection.csv") > "$d/pmc.txt"
     head -30 "$d/pmc.txt" | cut -c1-200 ;;
+  configs)
+    t=$1; shift
+    [ $# -gt 0 ] || set -- mlp ref_cnn mlp4x1024 resnet18 gpt2
+    : > gpurun_out/configs.jsonl
+    for c in "$@"; do
+      timeout -k 10 "$t" python tools/bench_configs.py --config "$c" > "gpurun_out/cfg_$c.log" 2>&1 || {
+        tail -20 "gpurun_out/cfg_$c.log"; exit 1; }
+      grep '^{' "gpurun_out/cfg_$c.log" | tail -1 | tee -a gpurun_out/configs.jsonl | cut -c1-300
+    done ;;
   *)
-    echo "usage: tools/gpu.sh {test|run|stats|pmc} ..." >&2; exit 2 ;;
+    echo "usage: tools/gpu.sh {test|run|stats|pmc|configs} ..." >&2; exit 2 ;;
 esac

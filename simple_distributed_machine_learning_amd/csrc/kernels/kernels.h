@@ -155,7 +155,8 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
 // memory (gwb = gw, gwb + N * 784 = gb: the flat gradient buffer's layout). slab: workspace of
 // u8_wgrad_slab_floats(M, N) floats; deterministic (fixed-order reduction).
 bool u8_wgrad_supported(int M, int N, int K, int ldx, const void* X, const void* dz);
-int64_t u8_wgrad_slab_floats(int M, int N);
+// (blocks > 0: the slab of a hidden-group range launched with that many row splits, WgradGroups)
+int64_t u8_wgrad_slab_floats(int M, int N, int blocks = 0);
 // dz enters as two fp16 planes scaled by a power of two chosen from a bound: amax [namax] with
 // |dz| <= max(amax) (required here: the fused head's per-block maxima or a torch amax).
 void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
@@ -166,11 +167,19 @@ void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, fl
 // result is bit-identical to head_dx_from_dl + u8_wgrad. The ReLU mask comes from h [M][N] OR from
 // its bits (mask [M][N / 32], u8_fwd / u8_fwd_head): exactly one of h / mask is non-null.
 bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const void* h, int C);
+// A range of 64-unit hidden groups [g_first, g_first + g_count) of the weight gradient, in ~`blocks` row
+// splits (the data-parallel step computes the gradient in two such ranges, so that the first range's
+// all-reduce overlaps the second range's kernel; parallel/pipeline.py). Deterministic for a given
+// (M, blocks); the partition differs from the whole-gradient launch, so the sums round differently.
+struct WgradGroups {
+  int g_first, g_count, blocks;
+};
 // head (optional): a deferred head reduction run in the same launch as this one's slab reduction
+// grp (optional): only that hidden-group range (reduced with its bias entries; no fused optimizer step)
 void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigned* mask, int C,
                  const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
                  const float* amax, int namax, hipStream_t stream, const HeadReduceArgs* head = nullptr,
-                 const SgdFuse* sgd = nullptr);
+                 const SgdFuse* sgd = nullptr, const WgradGroups* grp = nullptr);
 // out[i] += sum_s slab[s * stride + i] in split order (n % 4 == 0, 16-B aligned)
 void slab_reduce(const float* slab, int64_t stride, int splits, float* out, int64_t n, hipStream_t stream);
 

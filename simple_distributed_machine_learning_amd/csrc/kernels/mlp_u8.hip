@@ -609,7 +609,8 @@ struct WgradParams {
   const float* h;            // [M][N] (FD == 1)
   const unsigned* mask;      // [M][N / 32] ReLU bits (FD == 2)
   int C;                     // <= 16
-  int groups, splits;        // N / GHN hidden groups x row splits (1-D grid, XCD-aware order)
+  int groups, splits;        // hidden groups launched x row splits (1-D grid, XCD-aware order)
+  int g0;                    // first hidden group launched (hidden units GHN g0 ..)
   int xcd;                   // 0: plain order (split-major), A/B only (SDML_U8_WGRAD_XCD=0)
 };
 
@@ -649,7 +650,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   const int L = blockIdx.x, G8 = 8 * p.groups;
   const int split = p.xcd ? (L / G8) * 8 + L % 8 : L / p.groups;
   if (split >= p.splits) return;
-  const int n0 = (p.xcd ? (L % G8) / 8 : L % p.groups) * GHN;
+  const int n0 = (p.g0 + (p.xcd ? (L % G8) / 8 : L % p.groups)) * GHN;
   const int r0 = split * p.rows_per_split;
   const int nk = min(p.rows_per_split, p.M - r0) / GBK;  // host: M % GBK == 0
 
@@ -865,8 +866,16 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
 // Saves the head reduction's own launch (~5 us of latency-bound work) on the one-rank MLP step.
 // sg.p set: these are the step's last gradients, and the optimizer step is applied here (sgd_rule.h)
 // instead of by a separate SGD launch over the flat buffer.
+// Segments: blocks [0, nA) reduce [a_off, a_end), blocks [nA, nslab) reduce [b_off, b_end) (offsets into the
+// [N * 784 + N] gradient, multiples of 4): the whole gradient is one segment; one hidden-group range of a
+// split weight gradient is its weight rows plus its bias entries.
+struct SlabSegs {
+  int64_t a_off, a_end, b_off, b_end;
+  int nA;
+};
+
 __global__ void __launch_bounds__(1024) slab_head_reduce_kernel(const float* __restrict__ slab, int64_t stride,
-                                                                int splits, float* __restrict__ out, int64_t n,
+                                                                int splits, float* __restrict__ out, SlabSegs sgs,
                                                                 int nslab, HeadReduceArgs head, SgdFuse sg) {
   __shared__ f32x4 part[16][64];
   if ((int)blockIdx.x >= nslab) {
@@ -874,7 +883,9 @@ __global__ void __launch_bounds__(1024) slab_head_reduce_kernel(const float* __r
     return;
   }
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int64_t i = ((int64_t)blockIdx.x * 64 + l) * 4;
+  const bool segA = (int)blockIdx.x < sgs.nA;
+  const int64_t i = (segA ? sgs.a_off : sgs.b_off) + ((int64_t)(segA ? blockIdx.x : blockIdx.x - sgs.nA) * 64 + l) * 4;
+  const int64_t n = segA ? sgs.a_end : sgs.b_end;
   f32x4 a[4] = {};
   if (i < n) {
     int s = w;  // wave w: splits w, w + 16, ...
@@ -944,8 +955,14 @@ int u8_wgrad_splits(int M, int N) {
   return (M + rps - 1) / rps;
 }
 
-int64_t u8_wgrad_slab_floats(int M, int N) {
-  return (int64_t)u8_wgrad_splits(M, N) * ((int64_t)N * GKC + N);
+int u8_wgrad_group_splits(int M, int blocks) {
+  const int rps = ((M + std::max(1, blocks) - 1) / std::max(1, blocks) + GBK - 1) / GBK * GBK;
+  return (M + rps - 1) / rps;
+}
+
+int64_t u8_wgrad_slab_floats(int M, int N, int blocks) {
+  const int splits = blocks > 0 ? u8_wgrad_group_splits(M, blocks) : u8_wgrad_splits(M, N);
+  return (int64_t)splits * ((int64_t)N * GKC + N);
 }
 
 void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
@@ -976,8 +993,11 @@ bool u8_wgrad_dl_supported(int M, int N, int K, int ldx, const void* X, const vo
 
 void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigned* mask, int C,
                  const unsigned char* X, int M, int N, int ldx, float* slab, float* gwb, float scale,
-                 const float* amax, int namax, hipStream_t stream, const HeadReduceArgs* head, const SgdFuse* sgd) {
+                 const float* amax, int namax, hipStream_t stream, const HeadReduceArgs* head, const SgdFuse* sgd,
+                 const WgradGroups* grp) {
   if ((h == nullptr) == (mask == nullptr)) abort();  // host contract: exactly one ReLU-mask source
+  if (grp && (grp->g_count < 1 || grp->g_first < 0 || (grp->g_first + grp->g_count) * GHN > N || grp->blocks < 1))
+    abort();  // host contract: a range of whole hidden groups
   WgradParams p{};
   p.amax = namax > 0 ? amax : nullptr;
   p.namax = namax;
@@ -992,19 +1012,33 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigne
   p.h = h;
   p.mask = mask;
   p.C = C;
-  const int splits = u8_wgrad_splits(M, N);
+  p.groups = grp ? grp->g_count : N / GHN;
+  p.g0 = grp ? grp->g_first : 0;
+  const int splits = grp ? u8_wgrad_group_splits(M, grp->blocks) : u8_wgrad_splits(M, N);
   p.rows_per_split = ((M + splits - 1) / splits + GBK - 1) / GBK * GBK;
-  p.groups = N / GHN;
   p.splits = splits;
   p.xcd = wgrad_xcd();
   const dim3 wgrid(((splits + 7) / 8) * 8 * p.groups);
   if (mask) hipLaunchKernelGGL(u8_wgrad_kernel<2>, wgrid, dim3(GT), 0, stream, p);
   else hipLaunchKernelGGL(u8_wgrad_kernel<1>, wgrid, dim3(GT), 0, stream, p);
   const int64_t n = (int64_t)N * GKC + N;
-  if (head && head->part) {
+  if (grp) {  // this hidden-group range only: its weight rows, then its bias entries (+ the head's reduction)
+    if (sgd && sgd->p) abort();  // host contract: the split weight gradient is not the fused optimizer step
+    SlabSegs sgs;
+    sgs.a_off = (int64_t)grp->g_first * GHN * GKC;
+    sgs.a_end = (int64_t)(grp->g_first + grp->g_count) * GHN * GKC;
+    sgs.b_off = (int64_t)N * GKC + grp->g_first * GHN;
+    sgs.b_end = sgs.b_off + grp->g_count * GHN;
+    sgs.nA = (int)(((sgs.a_end - sgs.a_off) / 4 + 63) / 64);
+    const int nslab = sgs.nA + (int)(((sgs.b_end - sgs.b_off) / 4 + 63) / 64);
+    const bool hd = head && head->part;
+    hipLaunchKernelGGL(slab_head_reduce_kernel, dim3(nslab + (hd ? head_reduce_blocks(*head) : 0)), dim3(1024), 0,
+                       stream, slab, n, splits, gwb, sgs, nslab, hd ? *head : HeadReduceArgs(), SgdFuse());
+  } else if (head && head->part) {
     const int nslab = (int)((n / 4 + 63) / 64);
+    SlabSegs sgs{0, n, n, n, nslab};
     hipLaunchKernelGGL(slab_head_reduce_kernel, dim3(nslab + head_reduce_blocks(*head)), dim3(1024), 0, stream, slab, n,
-                       splits, gwb, n, nslab, *head, sgd ? *sgd : SgdFuse());
+                       splits, gwb, sgs, nslab, *head, sgd ? *sgd : SgdFuse());
   } else {
     if (sgd && sgd->p) abort();  // host contract: the fused step needs the head reduction in the same launch
     slab_reduce(slab, n, splits, gwb, n, stream);

@@ -966,7 +966,8 @@ torch::Tensor head_dx_from_dl(torch::Tensor dl, torch::Tensor w, torch::Tensor x
 // linear_relu_head_u8) - only the mask is used
 bool linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, torch::Tensor act, torch::Tensor gw,
                         torch::Tensor gb, double scale, c10::optional<torch::Tensor> amax,
-                        std::shared_ptr<HeadPending> head, c10::optional<py::tuple> sgd) {
+                        std::shared_ptr<HeadPending> head, c10::optional<py::tuple> sgd,
+                        c10::optional<py::tuple> groups) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kUInt8 && x.is_contiguous() && x.dim() == 2,
               "linear_wgrad_u8_dl: x must be a contiguous 2-D uint8 ROCm tensor");
   check_f32_cuda(dl, "dl");
@@ -986,7 +987,19 @@ bool linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, tor
   const bool gb_follows = gw.is_contiguous() && gb.is_contiguous() && gb.data_ptr<float>() == gw.data_ptr<float>() + N * K;
   if (gb_follows && sdml::head_fused_supported((int)N, (int)C) &&
       sdml::u8_wgrad_dl_supported((int)M, (int)N, (int)K, (int)K, x.data_ptr(), act.data_ptr(), (int)C)) {
-    auto ws = torch::empty({sdml::u8_wgrad_slab_floats((int)M, (int)N)}, gw.options());
+    sdml::WgradGroups grp{0, 0, 0};
+    if (groups.has_value()) {  // (g_first, g_count, blocks): one hidden-group range (data-parallel split)
+      const py::tuple& g = *groups;
+      TORCH_CHECK(g.size() == 3, "linear_wgrad_u8_dl: groups = (g_first, g_count, blocks)");
+      grp.g_first = g[0].cast<int>();
+      grp.g_count = g[1].cast<int>();
+      grp.blocks = g[2].cast<int>();
+      TORCH_CHECK(grp.g_first >= 0 && grp.g_count >= 1 && (grp.g_first + grp.g_count) * 64 <= N && grp.blocks >= 1 &&
+                      !sgd.has_value(),
+                  "linear_wgrad_u8_dl: groups must be whole 64-unit hidden groups inside N, without sgd");
+    }
+    auto ws = torch::empty({sdml::u8_wgrad_slab_floats((int)M, (int)N, groups.has_value() ? grp.blocks : 0)},
+                           gw.options());
     const bool has_am = amax.has_value() && amax->defined();
     if (has_am) {
       check_f32_cuda(*amax, "amax");
@@ -1039,7 +1052,7 @@ bool linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, tor
                       bits ? reinterpret_cast<const unsigned*>(act.data_ptr<int32_t>()) : nullptr, (int)C,
                       x.data_ptr<uint8_t>(), (int)M, (int)N, (int)K, ws.data_ptr<float>(), gw.data_ptr<float>(), (float)scale,
                       has_am ? amax->data_ptr<float>() : nullptr, has_am ? (int)amax->numel() : 0, cur_stream(),
-                      fuse_head ? &head->args : nullptr, sg.p ? &sg : nullptr);
+                      fuse_head ? &head->args : nullptr, sg.p ? &sg : nullptr, groups.has_value() ? &grp : nullptr);
     if (fuse_head) head->done();
     return sg.p != nullptr;
   }
@@ -1048,6 +1061,14 @@ bool linear_wgrad_u8_dl(torch::Tensor x, torch::Tensor dl, torch::Tensor w2, tor
   if (bits) dz = at::matmul(dl, w2).mul_(relu_bits_unpack(act));
   else dz = sdml::head_fused_supported((int)N, (int)C) ? head_dx_from_dl(dl, w2, act, true)
                                                        : at::matmul(dl, w2).mul_((act > 0).to(act.scalar_type()));
+  if (groups.has_value()) {  // only the hidden-group range asked for
+    const py::tuple& g = *groups;
+    const int64_t lo = g[0].cast<int64_t>() * 64, cnt = g[1].cast<int64_t>() * 64;
+    TORCH_CHECK(lo >= 0 && cnt > 0 && lo + cnt <= N, "linear_wgrad_u8_dl: bad hidden-group range");
+    auto gws = gw.narrow(0, lo, cnt), gbs = gb.narrow(0, lo, cnt);
+    linear_wgrad_u8(x, dz.narrow(1, lo, cnt).contiguous(), gws, gbs, scale, c10::nullopt);
+    return false;
+  }
   linear_wgrad_u8(x, dz, gw, gb, scale, amax);
   return false;
 }
@@ -1710,7 +1731,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_wgrad_u8_dl", &linear_wgrad_u8_dl,
         "gw += scale * dz^T x_u8, gb += colsum(dz), dz = (dl @ w2) * (h > 0) (factored boundary gradient)",
         py::arg("x"), py::arg("dl"), py::arg("w2"), py::arg("h"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
-        py::arg("amax") = py::none(), py::arg("head") = nullptr, py::arg("sgd") = py::none());
+        py::arg("amax") = py::none(), py::arg("head") = nullptr, py::arg("sgd") = py::none(),
+        py::arg("groups") = py::none());
   m.def("head_dx_from_dl", &head_dx_from_dl, "dx = (dl @ w) * (x > 0): boundary gradient from its factor",
         py::arg("dl"), py::arg("w"), py::arg("x"), py::arg("mask"));
   m.def("sgd_momentum_", &sgd_momentum_, "fused SGD with momentum over a flat buffer (optionally also writing a "

@@ -102,6 +102,8 @@ class MLPStage(PipelineStage):
                 y = super().fwd(x, ctx, train)
                 mask_out.copy_(ops.relu_bits(y))
                 ctx["mask"] = mask_out
+                if x.dtype == torch.uint8 and len(self.layers()) == 1 and train:
+                    ctx["acts"] = [x.reshape(x.shape[0], -1)]  # bwd_from_factor's operands, as on ROCm
                 return y
             return super().fwd(x, ctx, train)
         x = ops.carry_bounds(x.reshape(x.shape[0], -1), x)
@@ -237,23 +239,32 @@ class MLPStage(PipelineStage):
                 return None
         return ps[0].grad, sum(p.numel() for p in ps)
 
-    def bwd_from_factor(self, dl, w2, ctx, head_pending=None, sgd=None) -> bool:
+    def bwd_from_factor(self, dl, w2, ctx, head_pending=None, sgd=None, groups=None, final=True) -> bool:
         """Stage-0 backward fed by the factored boundary gradient dl (dz = (dl @ w2) * (h > 0), h this
         stage's output). A single uint8-fed layer takes it straight into its weight-gradient kernel
         (dz never materialised; a deferred head reduction ``head_pending`` shares its reduction
         launch, and with ``sgd`` so does the optimizer step: ``self.sgd_fused`` tells whether it
-        ran); returns False (nothing done, ``head_pending`` untouched) for other stages."""
+        ran); returns False (nothing done, ``head_pending`` untouched) for other stages. ``groups``: one
+        hidden-group range only (ops.linear_wgrad_u8_dl); ``final=False`` keeps ctx for the next range."""
         self.sgd_fused = False
         acts = ctx.get("acts")
         layers = self.layers()
         if acts is None or len(layers) != 1 or acts[0].dtype != torch.uint8:
             return False
-        ctx.pop("acts")
-        mask = ctx.pop("mask", None)  # the output's ReLU bits (fwd(mask_out=) / fwd_head_fused), else h itself
+        mask = ctx.get("mask")  # the output's ReLU bits (fwd(mask_out=) / fwd_head_fused), else h itself
+        if final:
+            ctx.pop("acts")
+            ctx.pop("mask", None)
         lin = layers[0]
         self.sgd_fused = ops.linear_wgrad_u8_dl(acts[0], dl, w2, mask if mask is not None else acts[1],
-                                                lin.weight.grad, lin.bias.grad, head_pending=head_pending, sgd=sgd)
+                                                lin.weight.grad, lin.bias.grad, head_pending=head_pending, sgd=sgd,
+                                                groups=groups)
         return True
+
+    def hidden_groups(self) -> int:
+        """64-unit hidden groups of a single-layer stage's output (the weight gradient's split unit)."""
+        n = self.layers()[0].out_features
+        return n // 64 if len(self.layers()) == 1 and n % 64 == 0 else 0
 
     # ---- stage 0 + stage 1 in ONE launch (both stages on this rank) -------------------------
     def can_fuse_head(self, head: "MLPStage", x: torch.Tensor) -> bool:

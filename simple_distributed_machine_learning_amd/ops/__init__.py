@@ -147,7 +147,7 @@ def linear_wgrad_u8(x: torch.Tensor, gz: torch.Tensor, gw: torch.Tensor, gb: Opt
 
 
 def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, amax: Optional[torch.Tensor] = None, head_pending=None,
-                       sgd=None) -> bool:
+                       sgd=None, groups=None) -> bool:
     """First-layer weight gradient from the FACTORED boundary gradient: with dz = (dl @ w2) * (h > 0)
     (dl [M, C] the head's factor, w2 [C, N] the head weight, h [M, N] this layer's ReLU output - or its
     ReLU bits, int32 [M, N/32] (:func:`relu_bits`), which is all that is read),
@@ -160,16 +160,24 @@ def linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, amax: Optional[torch.Tensor] = None
     launch as this one's slab reduction (or before it, on the paths without one).
     ``sgd`` (with ``head_pending``; ops.optim.FusedSGD.fused_args): these are the step's last
     gradients - apply the optimizer step inside the same launch. Returns True if it was applied (the
-    caller then commits it with FusedSGD.commit_fused instead of stepping)."""
+    caller then commits it with FusedSGD.commit_fused instead of stepping).
+    ``groups`` = (g_first, g_count, blocks): only hidden units [64 g_first, 64 (g_first + g_count)) of gw/gb,
+    in ~``blocks`` row splits (no ``sgd``): the data-parallel step computes the gradient in two such ranges
+    so the first range's all-reduce runs under the second range's kernel (parallel/pipeline.py)."""
     if x.is_cuda:
         if amax is None:
             amax = getattr(dl, "_sdml_amax", None)
-        return bool(_k().linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, PIXEL_SCALE, amax, head_pending, sgd))
+        return bool(_k().linear_wgrad_u8_dl(x, dl, w2, h, gw, gb, PIXEL_SCALE, amax, head_pending, sgd,
+                                            None if groups is None else tuple(int(g) for g in groups)))
     if head_pending is not None:
         head_pending.run()
     with torch.no_grad():
         mask = relu_bits_unpack(h) if h.dtype == torch.int32 else (h > 0).to(dl.dtype)
         dz = (dl @ w2) * mask
+        if groups is not None:
+            lo, n = 64 * int(groups[0]), 64 * int(groups[1])
+            dz = dz[:, lo:lo + n]
+            gw, gb = gw[lo:lo + n], gb[lo:lo + n]
         gw += dz.t() @ pixels_to_float(x)
         gb += dz.sum(0)
     return False

@@ -74,6 +74,7 @@ class GradSync:
         self._done = set()
         self._ptr = 0
         self._works = []
+        self._span_hi = 0  # issue_span: gradient prefix [0, _span_hi) already handed to all-reduces
         # merge consecutive stages into one contiguous bucket when they are adjacent in memory
         self.group = mesh.grad_group
 
@@ -81,6 +82,7 @@ class GradSync:
         self._done.clear()
         self._ptr = 0
         self._works = []
+        self._span_hi = 0
 
     def stage_done(self, stage: int):
         if not self.enabled:
@@ -92,13 +94,33 @@ class GradSync:
             self._works.append(self.transport.all_reduce(t, channel="grad"))
             self._ptr += 1
 
+    def issue_span(self, lo: int, hi: int):
+        """All-reduce ``flat.grads[lo:hi]`` now: a finished, contiguous range of the gradient whose
+        collective then runs (RCCL stream) under the kernels that still compute the rest. Spans are issued
+        in buffer order and must end up covering the whole buffer (checked by :meth:`finish_all`)."""
+        if not self.enabled:
+            return
+        if lo != self._span_hi or hi <= lo or hi > self.flat.grads.numel():
+            raise RuntimeError(f"GradSync.issue_span [{lo}, {hi}) does not continue [0, {self._span_hi})")
+        self._works.append(self.transport.all_reduce(self.flat.grads[lo:hi], channel="grad"))
+        self._span_hi = hi
+
     def finish_all(self):
         """ONE all-reduce over the whole flat gradient buffer (every local stage at once): fewer
-        collectives when nothing is left to overlap them with (rotate / dp placements)."""
+        collectives when nothing is left to overlap them with (rotate / dp placements). After
+        :meth:`issue_span` calls it waits for those instead (every rank issues the same spans)."""
         if not self.enabled:
             return
         if self._ptr:
             raise RuntimeError("GradSync.finish_all after per-stage all-reduces were issued")
+        if self._works:
+            if self._span_hi != self.flat.grads.numel():
+                raise RuntimeError("GradSync.finish_all: the issued spans do not cover the gradient")
+            for w in self._works:
+                w.wait()
+            self._works = []
+            self._span_hi = 0
+            return
         self.transport.all_reduce(self.flat.grads, channel="grad").wait()
 
     def finish(self):
@@ -192,6 +214,14 @@ class PipelineEngine:
         # rotate: stage 0's forward and stage 1's forward+loss+backward in one kernel for the rows that
         # stay on their owner (models/mlp.py fwd_head_fused); SDML_FUSE_HEAD=0 keeps them separate
         self.fuse_head = os.environ.get("SDML_FUSE_HEAD", "1") != "0"
+        # data-parallel gradient all-reduce overlapped with backward (rotate all-to-all, nothing crossing,
+        # uint8 first layer): the first layer's weight gradient runs as two hidden-unit ranges, the first
+        # range's rows are all-reduced while the second range's kernel runs (_dp_split_spans).
+        # SDML_DP_SPLIT=0: one weight-gradient launch, one all-reduce after it. SDML_DP_SPLIT_BLOCKS: row
+        # splits per range (< 256 leaves CUs free for the RCCL kernel).
+        self.dp_split = os.environ.get("SDML_DP_SPLIT", "1") != "0"
+        self.dp_split_blocks = int(os.environ.get("SDML_DP_SPLIT_BLOCKS", "240"))
+        self.dp_split_steps = 0  # training steps that ran the split (tests)
         self._small_step = None  # one-launch reference-size MLP step available (decided on first use)
         self._cnn_step = None  # two-launch reference CNN step available (decided on first use)
         self._small_args = None
@@ -603,6 +633,9 @@ class PipelineEngine:
                 pend[w].run()
                 pend[w] = None
 
+        # the gradient all-reduce overlapped with the last wave's first-layer weight gradient (see __init__)
+        dp_spans = self._dp_split_spans(s0) if (defer and train and self.grad_sync.enabled and self.dp_split) else None
+
         def head(xin, tgt, w):  # stage 1 forward + loss (+ its backward) on one block of rows
             nonlocal fresh, count
             if tgt.device != dev:
@@ -636,6 +669,21 @@ class PipelineEngine:
                 with tm.span("recv_wait", 1):
                     bwork[w].wait()
             gz = back[w]
+            if factored and fuse0 and dp_spans is not None and w == W - 1:
+                G, a1 = dp_spans
+                ga = G // 2
+                with tm.span("bwd", 0):
+                    ok = s0.bwd_from_factor(gz, s1.factor_weight(), ctx0[w], head_pending=pend[w],
+                                            groups=(0, ga, self.dp_split_blocks), final=False)
+                    if ok:  # range 0 (and the head's reduction) done: its weight rows go on the links now
+                        pend[w] = None
+                        self.grad_sync.issue_span(0, a1)
+                        s0.bwd_from_factor(gz, s1.factor_weight(), ctx0[w], groups=(ga, G - ga, self.dp_split_blocks))
+                        # the rest: range 1's rows, every bias, the head (all written by now)
+                        self.grad_sync.issue_span(a1, self.flat.grads.numel())
+                        self.dp_split_steps += 1
+                        hkeep[w] = back[w] = None
+                        return
             if factored and fuse0:  # the factor goes straight into stage 0's weight-gradient kernel
                 with tm.span("bwd", 0):
                     if pend[w] is not None:
@@ -722,6 +770,21 @@ class PipelineEngine:
             stats.zero_()
         self.last_timing = tm.result()
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
+
+    def _dp_split_spans(self, s0):
+        """(hidden groups G, end of range 0 in the flat gradient) when the first layer's weight gradient can
+        run as two hidden-unit ranges with range 0's weight rows a prefix of the flat gradient buffer (then
+        range 1's rows, the biases and the head's gradients form the contiguous rest), else None."""
+        if not hasattr(s0, "hidden_groups"):
+            return None
+        G = s0.hidden_groups()
+        if G < 2:
+            return None
+        lin = s0.layers()[0]
+        g = lin.weight.grad
+        if g is None or g.data_ptr() != self.flat.grads.data_ptr():
+            return None
+        return G, (G // 2) * 64 * lin.in_features
 
     # ---------------------------------------------------------------------------------------
     def _small_step_ok(self, batch_size: int) -> bool:

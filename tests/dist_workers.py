@@ -40,7 +40,8 @@ def train_worker(rank, world, model, kind, M, pp, steps, B, seed=3, kw=None, tp=
             "tp_rank": mesh.tp_rank,
             "eval": (el, ec, en), "bytes_sent": eng.transport.bytes_sent if eng.transport else 0,
             "transport": eng.transport.name if eng.transport else None,
-            "pool_allocs": eng.bufs.allocations, "pool_allocs_first": allocs_first}
+            "pool_allocs": eng.bufs.allocations, "pool_allocs_first": allocs_first,
+            "dp_split_steps": eng.dp_split_steps}
 
 
 def empty_replica_worker(rank, world, pp, B, steps, seed=3):

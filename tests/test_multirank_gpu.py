@@ -73,6 +73,8 @@ def test_rotate_multirank_on_device(world, mode, monkeypatch):
     ref = _single("mlp", M, steps, world * B, "rotate", {"pixels": kw.get("pixels", "f32")})
     _compare(res, ref)
     assert all((r["bytes_sent"] > 0) == (mode != "u8_dp") for r in res)
+    if mode == "u8_dp":  # the gradient all-reduce split over two weight-gradient ranges (GradSync.issue_span)
+        assert all(r["dp_split_steps"] == steps for r in res)
     assert all(r["pool_allocs"] == r["pool_allocs_first"] for r in res)  # persistent boundary buffers
 
 

@@ -198,6 +198,9 @@ def test_mlp_rotate_cross_fraction_matches_single_process(world, phi, pixels):
     ref = _single("mlp", M, steps, world * B, "rotate", {"pixels": pixels})
     _compare(res, ref, rtol=1e-4, atol=1e-5)
     assert all((r["bytes_sent"] > 0) == (phi > 0) for r in res)
+    # nothing crossing, uint8 first layer: the weight gradient ran as two hidden ranges with the first
+    # range's all-reduce issued before the second range (GradSync.issue_span)
+    assert all((r["dp_split_steps"] == steps) == (phi == 0 and pixels == "u8") for r in res)
 
 
 @pytest.mark.parametrize("kind,world,pp,M", [("rotate", 2, 2, 4), ("1f1b", 2, 2, 3), ("1f1b", 4, 2, 2),

@@ -354,6 +354,14 @@ class PipelineEngine:
         sched = self.schedule(M, forward_only=not train)
         prog = sched.program(self.mesh.pp_rank)
         scale = self._loss_scale(dataset, batch_size, global_batch)
+        # factored boundary gradient on a 2-stage neighbour pipeline whose ranks hold BOTH stages (Chimera's
+        # mirror pipelines, the pp2dp placement): the head sends back its rank-C factor dl [mb, C] (40 B per row
+        # for 784-128-10) instead of dx [mb, 128] (512 B), and the stage-0 rank rebuilds dx bit-identically with
+        # its own replica of W2 (the mirror all-reduce keeps the replicas equal). Lossless: the same bytes of
+        # information, 1024 -> 552 B per row over the pair's link.
+        fact = (train and self.factored_boundary_grad and self.P == 2 and self.mesh.pp > 1 and 0 in self.stages
+                and 1 in self.stages and getattr(self.stages[1], "supports_factored_grad", False))
+        n_cls = self.stages[1].layers()[-1].out_features if fact else 0
 
         if train:
             self.flat.zero_grad()  # no-op when the previous optimizer step already cleared them
@@ -387,7 +395,10 @@ class PipelineEngine:
             if op == OP_RECV:
                 mbsz = sizes[ins.mb]
                 prod = ins.stage if ins.payload == PL_ACT else ins.stage - 1
-                shape, dt = self._boundary(prod, mbsz)
+                if fact and ins.payload == PL_GRAD:
+                    shape, dt = (mbsz, n_cls), torch.float32
+                else:
+                    shape, dt = self._boundary(prod, mbsz)
                 buf = self.bufs.get(("recv", ins.payload, ins.pipe, ins.stage, ins.mb), shape, dt)
                 src = self.mesh.global_rank(self.mesh.dp_rank, ins.peer)
                 w = self.transport.irecv(buf, src, message_tag(ins.payload, ins.pipe, ins.stage, ins.mb))
@@ -414,12 +425,17 @@ class PipelineEngine:
                     tgt = dataset.targets(off, mbsz)
                     if tgt.device != dev:
                         tgt = tgt.to(dev, non_blocking=True)
-                    with tm.span("fwd", ins.stage):
-                        l, c, n = mod.head_fwd(x, tgt, ctx, train, scale, stats=stats)
-                    if l is not None:  # stage did not accumulate in-kernel
-                        stats[0] += l.float()
-                        stats[1] += c.float()
-                    count += n
+                    if fact:  # forward + loss + backward at once; dl waits in ctx for this micro-batch's OP_BWD
+                        with tm.span("fwd", ins.stage):
+                            ctx["dl"], n = mod.head_fwd_factored(x, tgt, scale, stats)
+                        count += n
+                    else:
+                        with tm.span("fwd", ins.stage):
+                            l, c, n = mod.head_fwd(x, tgt, ctx, train, scale, stats=stats)
+                        if l is not None:  # stage did not accumulate in-kernel
+                            stats[0] += l.float()
+                            stats[1] += c.float()
+                        count += n
                 else:
                     with tm.span("fwd", ins.stage):
                         y = mod.fwd(x, ctx, train)
@@ -434,13 +450,23 @@ class PipelineEngine:
                 mod = self.stages[ins.stage]
                 ctx = ctxs.pop((ins.pipe, ins.stage, ins.mb))
                 if mod.is_last:
-                    with tm.span("bwd", ins.stage):
-                        gx = mod.head_bwd(ctx)
+                    if fact:
+                        gx = ctx.pop("dl")
+                    else:
+                        with tm.span("bwd", ins.stage):
+                            gx = mod.head_bwd(ctx)
                 else:
                     nxt_local = sched.task_rank(ins.mb, ins.stage + 1) == self.mesh.pp_rank
                     gy = take((PL_GRAD, ins.pipe, ins.stage + 1, ins.mb), nxt_local)
                     with tm.span("bwd", ins.stage):
-                        gx = mod.bwd(gy, ctx)
+                        if fact:  # gy is the head's factor dl
+                            s1 = self.stages[1]
+                            gx = None
+                            if not mod.bwd_from_factor(gy, s1.factor_weight(), ctx):
+                                h = ctx["acts"][-1] if "acts" in ctx else ctx["y"]
+                                gx = mod.bwd(s1.boundary_grad_from_factor(gy, h.detach()), ctx)
+                        else:
+                            gx = mod.bwd(gy, ctx)
                 if ins.stage > 0:
                     key = (PL_GRAD, ins.pipe, ins.stage, ins.mb)
                     if sched.task_rank(ins.mb, ins.stage - 1) == self.mesh.pp_rank:

@@ -49,8 +49,8 @@ def test_bench_four_ranks_one_json_line(placement):
         assert c["boundary_bytes_across_gpus_per_step"] == 4 * (rows - rows // 4) * (512 + 40)
     if c["placement"] == "dp":
         assert c["boundary_bytes_across_gpus_per_step"] == 0
-    if c["placement"] == "pp2dp":  # every row's activation and full gradient cross the pair's link
-        assert c["boundary_bytes_across_gpus_per_step"] == 4 * rows * (512 + 512)
+    if c["placement"] == "pp2dp":  # every row's activation and its factored gradient (dl, 10 fp32) cross the link
+        assert c["boundary_bytes_across_gpus_per_step"] == 4 * rows * (512 + 40)
 
 
 def test_bench_two_ranks_cross_fraction_override():

@@ -144,6 +144,43 @@ def _launch_ranks(n: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def _measure_pp2dp(a, n, rank, world, dev, steps=10, warmup=3):
+    """The reference's own placement (stage 0 | stage 1 on different GPUs of a pair, Chimera, dp over the
+    pairs), timed for a few steps AFTER the headline measurement so the JSON carries a measured number
+    for it next to the placement the model chose (same per-GPU batch, weak scaling)."""
+    mesh = init_mesh(pp=2, schedule_kind="chimera", timeout_s=900, rank=rank, world_size=world, p2p_channels=True)
+    spec = get_model_spec(a.model, 2)
+    eng = PipelineEngine(spec, mesh, schedule_kind="chimera", num_microbatches=4, lr=0.1, momentum=0.5, seed=1)
+    eng.train()
+    B = a.batch_per_gpu * 2
+    GB = B * eng.data_shards
+    own_lo = eng.local_start(0, B)
+    ds = _ShardedSynth(GB, own_lo, B, 2, dev, pixels=a.pixels)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        mesh.barrier()
+
+    for i in range(warmup):
+        eng.run(ds, eng.local_start((i % 2) * GB, B), B, train=True, global_batch=GB)
+    sync()
+    eng.transport.reset_counters()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        eng.run(ds, eng.local_start((i % 2) * GB, B), B, train=True, global_batch=GB)
+    sync()
+    t = torch.tensor([time.perf_counter() - t0, float(eng.transport.bytes_sent)], dtype=torch.float64, device=dev)
+    tmax = t[:1].clone()
+    eng.transport.all_reduce(tmax, channel="world", op=dist.ReduceOp.MAX, async_op=False)
+    eng.transport.all_reduce(t, channel="world", async_op=False)
+    el = float(tmax.item())
+    return {"placement": "pp2dp", "schedule": "chimera", "microbatches": 4, "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 4), "samples_per_s": round(GB * steps / el, 1),
+            "boundary_bytes_across_gpus_per_step": int(float(t[1].item()) / steps),
+            "predicted": plc.predict("pp2dp", n, a.batch_per_gpu)}
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -238,6 +275,11 @@ def main():
         l, c, cnt = engine.reduce_metrics(res)
         loss = l / max(1, cnt)
     sps = GB * a.steps / el
+    # the reference's own placement, measured next to the chosen one (after the timed region)
+    alternatives = {}
+    if (n > 1 and n % 2 == 0 and place != "pp2dp" and a.model == "mlp"
+            and os.environ.get("SDML_BENCH_ALTERNATIVES", "1") != "0"):
+        alternatives["pp2dp"] = _measure_pp2dp(a, n, rank, world, dev)
     # what the process group really saw (1 and None for a single-GPU run without collectives)
     seen_world = dist.get_world_size() if dist.is_initialized() else 1
     seen_backend = dist.get_backend() if dist.is_initialized() else None
@@ -272,6 +314,7 @@ def main():
                 "backend": seen_backend,
                 "link_model": plc.model_dict(),
                 "predicted": predicted,
+                "measured_alternatives": alternatives,
                 "microbatches": M,
                 "batch_per_gpu": a.batch_per_gpu,
                 "optimizer": "SGD lr=0.1 momentum=0.5",

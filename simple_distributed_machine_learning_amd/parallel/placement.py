@@ -25,7 +25,11 @@ The model (documented in README "Multi-GPU placement") is deliberately simple:
   waves and of the local rows): step = max(compute, link) + the part that cannot overlap (the
   first wave's forward exchange when nothing local is left to compute, a fixed ``exposed``
   fraction of the link time);
-* gradient all-reduce: ring over N GPUs of the parameter bytes, after the last backward.
+* gradient all-reduce: ring over N GPUs of the parameter bytes. With nothing crossing GPUs (dp) the
+  first layer's weight gradient runs as two hidden-unit ranges and range 0's all-reduce overlaps range 1's
+  kernel (parallel/pipeline.py, SDML_DP_SPLIT), so only range 1's half plus what range 0's collective does
+  not hide is exposed: ``half + max(0, half - wgrad/2)``; the other placements all-reduce after the last
+  backward.
 
 ``choose`` returns the placement with the smallest predicted step; among placements within 2% of
 it, the one that moves the most boundary bytes across GPUs (the split the benchmark is about).
@@ -51,12 +55,15 @@ class LinkModel:
 
 @dataclass
 class ComputeModel:
-    """Per-row costs of the 784-128-10 stages on one MI355X at 131072 rows per GPU
-    (profiles/r2_fused_step_bench_n1_kernel_stats.txt: uint8 forward 61 us + weight gradient 78 us
-    + reduction/SGD 12 us for stage 0; fused head 25.6 us for stage 1)."""
-    s0_ns: float = 1.06
-    s1_ns: float = 0.195
-    fixed_us: float = 12.0
+    """Per-row costs of the 784-128-10 stages on one MI355X at 131072 rows per GPU, from the round-3 kernel
+    tables: profiles/r3_unfused_bench_n1_kernel_stats.txt (uint8 forward 61.6 us + weight gradient 78.9 us for
+    stage 0; head 25.8 us for stage 1) and profiles/r3_bench_n1_kernel_stats.txt (reduction/SGD 11.6 us; the
+    step's 174.4 us minus its kernels' 170.7 us of launch gaps). ``wgrad_ns``: the weight gradient alone (the
+    dp split hides range 0's all-reduce under half of it)."""
+    s0_ns: float = 1.072
+    s1_ns: float = 0.197
+    fixed_us: float = 15.3
+    wgrad_ns: float = 0.571
     act_bytes: int = 512          # boundary activation per row (128 fp32)
     grad_bytes: int = 40          # factored boundary gradient per row (10 fp32)
     param_bytes: int = 101_770 * 4
@@ -91,6 +98,9 @@ def predict(placement: str, n: int, batch_per_gpu: int, waves: int = 2, phi: Opt
     link_us = link_bytes / (link.gbps * 1e3) + ncoll * link.collective_us
     if n > 1:  # ring all-reduce of the gradients (2 (n-1)/n of the bytes per GPU, over 2 ring links)
         ar_us = 2 * (n - 1) / n * comp.param_bytes / (2 * link.gbps * 1e3) + link.collective_us
+        if placement == "dp" or (placement != "pp2dp" and phi == 0):  # split: two half collectives, one hidden
+            half = (ar_us - link.collective_us) / 2 + link.collective_us
+            ar_us = half + max(0.0, half - B * comp.wgrad_ns / 2e3)
     else:
         ar_us = 0.0
     if link_bytes > 0:

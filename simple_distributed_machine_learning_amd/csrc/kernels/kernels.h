@@ -211,6 +211,16 @@ constexpr int kHeadAmaxMax = 1024;
 void head_dx_from_dl(const float* dl, const float* W, const float* x, float* dx, int M, int K, int C, bool mask,
                      hipStream_t stream);
 
+// head_pool.hip: global average pool + Linear(K -> C) + log_softmax + NLL + the whole backward (ResNet's last
+// layer). x [M][P][K] channels-last, W [C][K], b [C], dx like x, gW / gb accumulated, all bf16 (bf16 = true) or
+// fp32; stats [2] (loss sum, correct) added, or overwritten with stats_overwrite. ws:
+// head_pool_workspace_floats(M, K, C) floats. Deterministic (fixed-order slab reduction).
+bool head_pool_supported(int M, int P, int K, int C);
+int64_t head_pool_workspace_floats(int M, int K, int C);
+void head_pool_xent(const void* x, const void* W, const void* b, const int64_t* tgt, int M, int P, int K, int C,
+                    float scale, void* dx, void* gW, void* gb, float* stats, bool stats_overwrite, float* ws, bool bf16,
+                    hipStream_t stream);
+
 // ---- SGD with momentum over a flat buffer ------------------------------------------------
 // zero_grad: also writes g = 0 after reading it (fuses the next step's zero_grad)
 // optional bf16 weight-plane cache written from the updated weights (see sgd_kernel)

@@ -822,10 +822,26 @@ __global__ void __launch_bounds__(256) cnn_step_update_kernel(const float* __res
                      ((part[4][j] + part[5][j]) + (part[6][j] + part[7][j]));
     sgd_update1(a.p[ti] + e, a.buf[ti] ? a.buf[ti] + e : nullptr, gr, a);
   }
-  if (blockIdx.x == 0 && threadIdx.x < 2) {  // (loss sum, correct), samples in order
-    float t = 0.f;
-    for (int s = 0; s < B; ++s) t += rec[(size_t)s * REC + R_LOSS + threadIdx.x];
-    stats[threadIdx.x] = t;
+  if (blockIdx.x == 0) {  // (loss sum, correct): 256 strided partials, then a fixed-order tree (deterministic).
+    // (A serial loop over the B records on two threads was B dependent round trips to records other XCDs had
+    // just written: it set this kernel's length, ~14 us at B = 60.)
+    __shared__ float st[2][256];
+    float l = 0.f, c = 0.f;
+    for (int s = threadIdx.x; s < B; s += 256) {
+      l += rec[(size_t)s * REC + R_LOSS];
+      c += rec[(size_t)s * REC + R_LOSS + 1];
+    }
+    st[0][threadIdx.x] = l;
+    st[1][threadIdx.x] = c;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) {
+        st[0][threadIdx.x] += st[0][threadIdx.x + w];
+        st[1][threadIdx.x] += st[1][threadIdx.x + w];
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x < 2) stats[threadIdx.x] = st[threadIdx.x][0];
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && ctr) *ctr += 1;  // this step's masks are drawn
 }

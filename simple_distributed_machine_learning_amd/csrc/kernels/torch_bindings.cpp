@@ -939,6 +939,32 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>, std::shared_ptr<HeadPend
   return {dl, n_am > 0 ? c10::optional<torch::Tensor>(am.narrow(0, 0, n_am)) : c10::nullopt, out};
 }
 
+// ResNet's last layer: average pool over P positions + Linear + log_softmax + NLL + backward (head_pool.hip).
+// x [M, P, K] contiguous (a channels-last activation viewed as [M, H*W, C]); w [C, K]; b [C]; gw/gb the
+// parameter gradients (accumulated); stats [2] accumulated (overwritten with stats_init). Returns dx like x.
+torch::Tensor head_pool_xent(torch::Tensor x, torch::Tensor w, torch::Tensor b, torch::Tensor target, torch::Tensor gw,
+                             torch::Tensor gb, double scale, torch::Tensor stats, bool stats_init) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 3 && x.is_contiguous(), "head_pool_xent: x must be a contiguous [M, P, K] device tensor");
+  const auto dt = x.scalar_type();
+  TORCH_CHECK(dt == torch::kBFloat16 || dt == torch::kFloat32, "head_pool_xent: bf16 or fp32");
+  for (auto* t : {&w, &b, &gw, &gb})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == dt && t->is_contiguous(), "head_pool_xent: w/b/gw/gb must match x");
+  check_f32_cuda(stats, "stats");
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == torch::kInt64 && target.is_contiguous(),
+              "target must be a contiguous int64 device tensor");
+  const int64_t M = x.size(0), P = x.size(1), K = x.size(2), C = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && b.numel() == C && gw.numel() == C * K && gb.numel() == C &&
+                  target.numel() == M && stats.numel() == 2,
+              "head_pool_xent: shape mismatch");
+  TORCH_CHECK(sdml::head_pool_supported((int)M, (int)P, (int)K, (int)C), "head_pool_xent: unsupported shape");
+  auto dx = torch::empty_like(x);
+  auto ws = torch::empty({sdml::head_pool_workspace_floats((int)M, (int)K, (int)C)}, stats.options());
+  sdml::head_pool_xent(x.data_ptr(), w.data_ptr(), b.data_ptr(), target.data_ptr<int64_t>(), (int)M, (int)P, (int)K,
+                       (int)C, (float)scale, dx.data_ptr(), gw.data_ptr(), gb.data_ptr(), stats.data_ptr<float>(),
+                       stats_init, ws.data_ptr<float>(), dt == torch::kBFloat16, cur_stream());
+  return dx;
+}
+
 // dx = (dl @ w) * (x > 0 if mask): the fused head's boundary gradient rebuilt from its factor
 torch::Tensor head_dx_from_dl(torch::Tensor dl, torch::Tensor w, torch::Tensor x, bool mask) {
   check_f32_cuda(dl, "dl");
@@ -1728,6 +1754,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<HeadPending, std::shared_ptr<HeadPending>>(m, "HeadPending")
       .def("run", &HeadPending::run, "launch the deferred head reduction now (once)")
       .def_property_readonly("pending", &HeadPending::pending);
+  m.def("head_pool_supported", &sdml::head_pool_supported, "head_pool_xent shape support (M, P, K, C)");
+  m.def("head_pool_xent", &head_pool_xent,
+        "avg-pool + Linear + log_softmax + NLL + backward (ResNet head); returns dx, accumulates gw/gb/stats",
+        py::arg("x"), py::arg("w"), py::arg("b"), py::arg("target"), py::arg("gw"), py::arg("gb"), py::arg("scale"),
+        py::arg("stats"), py::arg("stats_init") = false);
   m.def("linear_wgrad_u8_dl", &linear_wgrad_u8_dl,
         "gw += scale * dz^T x_u8, gb += colsum(dz), dz = (dl @ w2) * (h > 0) (factored boundary gradient)",
         py::arg("x"), py::arg("dl"), py::arg("w2"), py::arg("h"), py::arg("gw"), py::arg("gb"), py::arg("scale"),

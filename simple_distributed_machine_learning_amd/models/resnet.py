@@ -23,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .base import ModelSpec, PipelineStage
+from .. import ops
 from ..ops import conv as conv_ops
 
 WIDTHS = (64, 128, 256, 512)
@@ -101,11 +102,12 @@ class ResNetStage(PipelineStage):
         if stage_id == num_stages - 1:
             self.fc = nn.Linear(512, num_classes)
 
-    def forward(self, x):
-        # NHWC inside the stage for bf16 (SDML_RESNET_NHWC=auto; 1/0 force it on/off). Measured on
-        # MI355X (8 stages on one GPU, batch 512, 8 micro-batches): MIOpen picks slower solutions
-        # for channels-last fp32 (9.6K vs 14.6K samples/s), so fp32 stays NCHW. The boundary
-        # tensor is NCHW, or [N, H, W, C] in channels-last runs (boundary_nhwc).
+    def trunk(self, x):
+        """Everything but the last stage's pool + fc.
+        NHWC inside the stage for bf16 (SDML_RESNET_NHWC=auto; 1/0 force it on/off). Measured on
+        MI355X (8 stages on one GPU, batch 512, 8 micro-batches): MIOpen picks slower solutions
+        for channels-last fp32 (9.6K vs 14.6K samples/s), so fp32 stays NCHW. The boundary
+        tensor is NCHW, or [N, H, W, C] in channels-last runs (boundary_nhwc)."""
         if self.stage_id == 0:
             x = x.to(self.stem_conv.weight.dtype)
         elif self.boundary_nhwc:
@@ -117,6 +119,10 @@ class ResNetStage(PipelineStage):
             x = conv_ops.batch_norm(self.stem_bn, conv_ops.conv2d(self.stem_conv, x), relu=True)
         for n in self.block_names:
             x = getattr(self, n)(x)
+        return x
+
+    def forward(self, x):
+        x = self.trunk(x)
         if self.stage_id == self.num_stages - 1:
             x = F.adaptive_avg_pool2d(x, 1).flatten(1)
             x = self.fc(x)
@@ -124,6 +130,33 @@ class ResNetStage(PipelineStage):
         if self.boundary_nhwc:
             return x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1)
         return x.contiguous()
+
+    # Training head on ROCm: pool + fc + log_softmax + NLL + backward in one kernel (+ its reduction),
+    # ops.pooled_head_xent / head_pool.hip, instead of ATen pooling, a hipBLASLt GEMM and ATen
+    # log_softmax / nll_loss forward and backward (the reference's loss: simple_distributed.py:111).
+    # SDML_RESNET_HEAD=aten keeps the autograd head.
+    def head_fwd(self, x, target, ctx, train, loss_scale, stats=None):
+        fc = getattr(self, "fc", None)
+        if not (train and x.is_cuda and fc is not None and stats is not None and fc.weight.grad is not None
+                and os.environ.get("SDML_RESNET_HEAD", "fused") != "aten"):
+            return super().head_fwd(x, target, ctx, train, loss_scale, stats)
+        if not self.is_first:
+            x = x.detach().requires_grad_(True)
+        with torch.enable_grad():
+            y = self.trunk(x)
+        if not ops.pooled_head_ok(y, fc.weight):
+            return super().head_fwd(x.detach(), target, ctx, train, loss_scale, stats)
+        ctx["x"], ctx["y"] = x, y
+        ctx["gy"] = ops.pooled_head_xent(y.detach(), fc.weight, fc.bias, target, fc.weight.grad, fc.bias.grad,
+                                         loss_scale, stats)
+        return None, None, target.numel()
+
+    def head_bwd(self, ctx):
+        if "gy" not in ctx:
+            return super().head_bwd(ctx)
+        y, gy, x = ctx.pop("y"), ctx.pop("gy"), ctx.pop("x")
+        torch.autograd.backward(y, gy)
+        return None if self.is_first else x.grad
 
 
 def _out_shape(stage: int, num_stages: int, hw: int = 28):

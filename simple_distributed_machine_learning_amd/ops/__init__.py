@@ -341,6 +341,26 @@ def linear_logsoftmax_nll_dl(x, w, b, target, gw, gb, scale: float, stats, stats
     return (dl, None) if defer_reduce else dl
 
 
+def pooled_head_xent(y, w, b, target, gw, gb, scale: float, stats, stats_init: bool = False):
+    """Training head of a convolutional stage (ResNet's last layer): global average pool of ``y``
+    ([N, C, H, W], channels-last memory) -> Linear(w, b) -> log_softmax -> NLL (sum), with the whole backward:
+    gw/gb accumulated (scaled by ``scale``), loss sum / correct count into ``stats`` [2] (added; overwritten
+    with ``stats_init``). Returns dy (the gradient w.r.t. ``y``, same layout). ROCm only:
+    csrc/kernels/head_pool.hip (one launch + one fixed-order reduction)."""
+    N, C, H, W = y.shape
+    yl = y.permute(0, 2, 3, 1)  # channels-last memory as [N, H, W, C]: contiguous
+    if not yl.is_contiguous():
+        yl = yl.contiguous()
+    dy = _k().head_pool_xent(yl.view(N, H * W, C), w.detach(), b.detach(), target, gw, gb, float(scale), stats,
+                             bool(stats_init))
+    return dy.view(N, H, W, C).permute(0, 3, 1, 2)
+
+
+def pooled_head_ok(y, w) -> bool:
+    return bool(y.is_cuda and y.dim() == 4 and y.dtype in (torch.bfloat16, torch.float32) and w.dtype == y.dtype
+                and _k().head_pool_supported(y.shape[0], y.shape[2] * y.shape[3], y.shape[1], w.shape[0]))
+
+
 def head_dx_from_dlogits(dl, w, x, mask: bool = True):
     """Boundary gradient from its factor: ``(dl @ w) * (x > 0)`` (the ReLU backward of the stage
     that produced ``x``, fused), with the fused head's exact arithmetic on ROCm."""

@@ -224,6 +224,7 @@ class PipelineEngine:
         self.dp_split_steps = 0  # training steps that ran the split (tests)
         self._small_step = None  # one-launch reference-size MLP step available (decided on first use)
         self._cnn_step = None  # two-launch reference CNN step available (decided on first use)
+        self.fast_steps = {"mlp_small": 0, "cnn": 0}  # steps that ran the one/two-launch paths (tests)
         self._small_args = None
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
@@ -852,6 +853,7 @@ class PipelineEngine:
         self.global_step += 1
         self._advance_rng()
         self.last_timing = {}
+        self.fast_steps["mlp_small"] += 1
         return StepResult(stats[0], stats[1], batch_size, time.perf_counter() - t0)
 
     def _cnn_step_ok(self, batch_size: int) -> bool:
@@ -900,6 +902,7 @@ class PipelineEngine:
         self.optimizer.commit_fused(zero_grad=True, planes_current=False)
         self.global_step += 1  # (the kernel advanced the device dropout counter)
         self.last_timing = {}
+        self.fast_steps["cnn"] += 1
         return StepResult(stats[0], stats[1], batch_size, time.perf_counter() - t0)
 
     def reduce_metrics(self, res: StepResult, group=None) -> Tuple[float, int, int]:

@@ -284,3 +284,37 @@ def test_wgrad_dma_loops_match_staged_loop(N, C, Co, H, W, ks, st, monkeypatch):
     finally:
         K.reset_knobs()
     assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])
+
+
+def test_resnet_last_stage_fused_head_matches_autograd_head(monkeypatch):
+    """ResNetStage.head_fwd on ROCm (pool + fc + loss + backward in head_pool.hip) against the autograd head
+    (SDML_RESNET_HEAD=aten): same loss, same stage gradients within bf16 tolerance."""
+    from simple_distributed_machine_learning_amd.models import get_model_spec
+
+    spec = get_model_spec("resnet18", 8, dtype=torch.bfloat16)
+    res = []
+    for mode in ("aten", "fused"):
+        monkeypatch.setenv("SDML_RESNET_HEAD", mode)
+        torch.manual_seed(0)
+        m = spec.build_stage(7)
+        m.stage_id, m.num_stages = 7, 8
+        m = m.to(DEV, torch.bfloat16)
+        for p in m.parameters():
+            p.grad = torch.zeros_like(p)
+        g = torch.Generator().manual_seed(1)
+        x = torch.randn(64, 4, 4, 512, generator=g).to(DEV, torch.bfloat16)  # [N, H, W, C] boundary
+        t = torch.randint(0, 10, (64,), generator=g).to(DEV)
+        stats = torch.zeros(2, device=DEV)
+        ctx = {}
+        l, c, n = m.head_fwd(x, t, ctx, True, 1 / 64, stats=stats)
+        if l is not None:
+            stats[0] += l.float()
+            stats[1] += c.float()
+        dx = m.head_bwd(ctx)
+        torch.cuda.synchronize()
+        res.append((stats.clone(), dx.float(), [p.grad.float().clone() for p in m.parameters()]))
+    (s0, d0, g0), (s1, d1, g1) = res
+    assert float(s1[0]) == pytest.approx(float(s0[0]), rel=2e-2)
+    torch.testing.assert_close(d1, d0, rtol=5e-2, atol=5e-2 * float(d0.abs().max()))
+    for a, b in zip(g1, g0):
+        torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2 * float(b.abs().max()) + 1e-6)

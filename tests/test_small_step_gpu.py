@@ -39,7 +39,7 @@ def test_small_step_matches_multi_kernel_step(B, pixels, opt, monkeypatch):
     e0, r0 = _run("1f1b", B, 5, pixels, opt)
     monkeypatch.setenv("SDML_SMALL_STEP", "1")
     e1, r1 = _run("1f1b", B, 5, pixels, opt)
-    assert e1._small_step is True and e0._small_step is False
+    assert e1.fast_steps["mlp_small"] > 0 and e0.fast_steps["mlp_small"] == 0
     for (l0, c0, n0), (l1, c1, n1) in zip(r0, r1):
         assert n0 == n1 == B
         assert l1 == pytest.approx(l0, rel=1e-5, abs=1e-5)
@@ -88,7 +88,7 @@ def test_cnn_step_matches_per_stage_kernels(B, opt, monkeypatch):
     e0, r0 = _run_cnn(B, 4, opt)
     monkeypatch.setenv("SDML_SMALL_STEP", "1")
     e1, r1 = _run_cnn(B, 4, opt)
-    assert e1._cnn_step is True and e0._cnn_step is False
+    assert e1.fast_steps["cnn"] == 4 and e0.fast_steps["cnn"] == 0
     for (l0, c0, n0), (l1, c1, n1) in zip(r0, r1):
         assert n0 == n1 == B
         assert l1 == pytest.approx(l0, rel=1e-4, abs=1e-4)

@@ -23,9 +23,12 @@ constexpr int HKT = 128;  // hidden width
 constexpr int DTP = 16;   // dz transpose pitch
 
 // x tile image [16 rows][128] with the 16-B chunk c of row rho's 16-float group at c ^ swz(rho) and
-// group q at q ^ (rho & 3): rows r and r + 4 of a ds_write_b128 phase land in different banks, and
-// the column reads (rows 4kk + g, columns 16t + r) cover 64 distinct banks
-__device__ __forceinline__ int swz(int rho) { return 4 * ((rho >> 2) & 3); }
+// group q at q ^ (rho & 3): the column reads (rows 4kk + g, columns 16t + r) cover 64 distinct banks, and
+// the row reads xt_at(r, u, 4g) (ds_read_b128, lane (r, g)) are conflict-free: in each 16-lane group of a
+// b128 read the four (g, r >> 2) classes present get the 4 distinct chunk slots g ^ h(r >> 2), h = {0, 2,
+// 3, 1} (with h(r >> 2) = r >> 2 two classes shared a slot: 2-way conflicts on every x-tile read of the
+// fused uint8 forward's head epilogue; checked by enumeration, r4).
+__device__ __forceinline__ int swz(int rho) { return 4 * ((0x78 >> (2 * ((rho >> 2) & 3))) & 3); }
 __device__ __forceinline__ int xt_at(int rho, int q, int j) {
   return rho * HKT + 16 * (q ^ (rho & 3)) + (j ^ swz(rho));
 }

@@ -566,16 +566,34 @@ __device__ __forceinline__ f16x8 frag_tr(const u16* img, int c0, int s, int lane
 }
 
 // dz plane images: the 8-byte granule g (4 hidden units) of k-row r is stored at g ^ dz_swz(r). The
-// factored staging writes one 16-row x 4-column block per 16 lanes (the fd_dz MFMA layout); on the
-// 48-dword pitch those rows repeat every 4 rows in the banks (4-way conflicts, SQ_LDS_BANK_CONFLICT
-// 7.1e6 for this kernel). The XOR by (r >> 2) & 3 (doubled) spreads them; the transposed reads keep
-// whole 4-row blocks under one XOR value, so they stay conflict-free.
-__device__ __forceinline__ int dz_swz(int r) { return ((r >> 2) & 3) << 1; }
+// factored staging writes one 16-row x 4-column block per 16 lanes (the fd_dz MFMA layout): on the
+// 48-dword pitch the even rows of the block share one 16-dword bank half and the odd rows the other, so
+// the 8 even (odd) rows need 8 distinct granule slots: (r >> 1) & 7. (Round 3's ((r >> 2) & 3) << 1 gave
+// 4, i.e. 2-way write conflicts; no swizzle: 4-way, 7.1e6 conflict cycles.) A transposed read stays
+// conflict-free under any XOR below 8: it permutes each row's 8-granule block in place.
+__device__ __forceinline__ int dz_swz(int r) { return (r >> 1) & 7; }
+
+// pixel image rows (GXP = 800 fp16): the low 8 fp16 of every 16-column chunk cc at 8 cc, the high 8 at
+// 400 + 8 cc. The staging's 16-B stores (lane = chunk, two per chunk) then hit 32 consecutive dwords per
+// 8-lane group (the chunk-contiguous row of round 3 put lanes cc and cc + 4 on the same banks: 2-way on
+// 400 of 512 store groups); the transposed reads of 4 columns stay inside one half-chunk, conflict-free.
+__device__ __forceinline__ int px_col(int col) { return ((col >> 3) & 1) * 400 + (col >> 4) * 8 + (col & 7); }
+
+// frag_tr for the pixel image (px_col layout)
+__device__ __forceinline__ f16x8 frag_px(const u16* img, int c0, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const u16* p = img + (16 * s + 8 * (g >> 1) + (i >> 2)) * GXP + px_col(c0 + 16 * (g & 1) + 4 * (i & 3));
+  const s16x4 lo = tr16(p), hi = tr16(p + 4 * GXP);
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return __builtin_bit_cast(f16x8, f);
+}
 
 template <int PITCH>
 __device__ __forceinline__ f16x8 frag_tr_dz(const u16* img, int c0, int s, int lane) {
   const int g = lane >> 4, i = lane & 15;
-  const int r = 16 * s + 8 * (g >> 1) + (i >> 2);  // the 4 rows of one transposed read share dz_swz
+  const int r = 16 * s + 8 * (g >> 1) + (i >> 2);
   const int col = c0 + 16 * (g & 1) + 4 * (i & 3);
   const s16x4 lo = tr16(img + r * PITCH + (((col >> 2) ^ dz_swz(r)) << 2));
   const s16x4 hi = tr16(img + (r + 4) * PITCH + (((col >> 2) ^ dz_swz(r + 4)) << 2));
@@ -731,7 +749,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     const int row = c / 50, cc = c % 50;
     xload[u] = cc < 49;
     xp[u] = p.X + (size_t)(r0 + row) * p.ldx + 16 * min(cc, 48);
-    xoff[u] = row * GXP + 16 * cc;
+    xoff[u] = row * GXP + 8 * cc;  // (px_col: high half at + 400)
   }
   const size_t x_step = (size_t)GBK * p.ldx;
   f32x4 dv;
@@ -769,7 +787,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     for (int u = 0; u < XU; ++u) {
       const u32x4 v = xload[u] ? xv[u] : u32x4{0u, 0u, 0u, 0u};
       *reinterpret_cast<f16x8*>(B + xoff[u]) = widen8h(v[0], v[1]);
-      *reinterpret_cast<f16x8*>(B + xoff[u] + 8) = widen8h(v[2], v[3]);
+      *reinterpret_cast<f16x8*>(B + xoff[u] + 400) = widen8h(v[2], v[3]);
     }
   };
 
@@ -795,7 +813,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
           for (int pl = 0; pl < GNPL; ++pl) a[i][pl] = frag_tr_dz<GDP>(B + GX_U16 + pl * GD_U16, 32 * i, s, lane);
 #pragma unroll
         for (int j = 0; j < NCT; ++j) {
-          const f16x8 b = frag_tr<GXP>(B, 32 * (ct0 + j), s, lane);
+          const f16x8 b = frag_px(B, 32 * (ct0 + j), s, lane);
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             acc[i][j] = mfma(a[i][1], b, acc[i][j]);  // lo

@@ -229,6 +229,11 @@ def main():
     mesh = init_mesh(pp=pp, schedule_kind=kind, timeout_s=900, rank=rank, world_size=world,
                      p2p_channels=(kind != "rotate"))
     dev = mesh.device
+    knobs = {}
+    if dev.type == "cuda":
+        from simple_distributed_machine_learning_amd import _native
+
+        knobs = _native.apply_knobs_from_env()  # A/B runs only (SDML_KNOBS="NAME=V,..."); default: none
     spec = get_model_spec(a.model, 2)
     engine = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=1,
                             cross_fraction=phi if kind == "rotate" else None)
@@ -315,6 +320,7 @@ def main():
                 "link_model": plc.model_dict(),
                 "predicted": predicted,
                 "measured_alternatives": alternatives,
+                "kernel_knobs": knobs,
                 "microbatches": M,
                 "batch_per_gpu": a.batch_per_gpu,
                 "optimizer": "SGD lr=0.1 momentum=0.5",

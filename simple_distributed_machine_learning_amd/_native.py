@@ -77,3 +77,20 @@ def kernels_available() -> bool:
 def use_hip(t) -> bool:
     """True when tensor ``t`` lives on a ROCm device -> the HIP kernels must be used."""
     return getattr(t, "is_cuda", False)
+
+
+def apply_knobs_from_env(var: str = "SDML_KNOBS") -> dict:
+    """Set kernel-variant switches (csrc/kernels/knobs.h) from ``NAME=V,NAME=V`` in the environment: the A/B
+    runs of tools/ and bench.py use it; production code never reads it per launch. Returns what was set."""
+    import os
+
+    spec = os.environ.get(var, "").strip()
+    out = {}
+    if not spec:
+        return out
+    k = kernels()
+    for item in spec.split(","):
+        name, _, val = item.partition("=")
+        k.set_knob(name.strip(), int(val))
+        out[name.strip()] = int(val)
+    return out

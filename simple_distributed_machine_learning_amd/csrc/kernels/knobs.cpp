@@ -35,6 +35,7 @@ const Entry kTable[KNOB_COUNT] = {
     {"U8_FWD_WAVES", 0, false, nullptr},
     {"U8_FWD_X3", 0, false, "x3"},
     {"U8_WGRAD_X3", 0, false, "x3"},
+    {"U8_FH_STAGES", 2, false, nullptr},
     {"GEMM_BF16_NOSTORE", 0, true, nullptr},
     {"U8_VARIANT", 0, true, nullptr},
 };

@@ -69,7 +69,7 @@ static_assert(FBK == 32 || FBK == 64, "swizzles below are written for 32- and 64
 // block geometry per WMT = 32-row MFMA tiles per wave and NWR = row waves (the block is NWR x 2
 // waves; wave tile 32 WMT x 64, block 32 WMT NWR x 128). NWR = 4: 512 threads (2 waves per SIMD);
 // NWR = 8: 1024 threads (4 waves per SIMD, <= 128 VGPRs)
-template <int WMT, int NWR = 4>
+template <int WMT, int NWR = 4, int NSG = NS>
 struct Geo {
   static constexpr int THREADS = 128 * NWR;
   static constexpr int WAVES = THREADS / 64;
@@ -82,7 +82,7 @@ struct Geo {
   static_assert(GLDS_X * 1024 * WAVES == A_BYTES && GLDS_W * 1024 * WAVES == NPL * B_PLANE, "DMA split");
   // the epilogue transposes EPR x 64 fp32 per wave through the (then free) stage buffers
   static constexpr int EPR = WAVES * 64 * 64 * 4 <= 128 * 1024 ? 64 : 32;
-  static constexpr int SMEM = std::max(NS * STAGE, WAVES * EPR * 64 * 4);
+  static constexpr int SMEM = std::max(NSG * STAGE, WAVES * EPR * 64 * 4);
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
 
@@ -184,9 +184,12 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
 
 // HEADC = 0: store h = act(scale acc + b) (+ its ReLU bits when p.mask); HEADC = C > 0: the fused
 // classifier head on h (fused_head_epilogue), h is never stored
-template <int MODE, int WMT, int TAIL, int NWR, int HEADC = 0>
+// NSK: LDS ring stages. The fused-head variant may take 3 (the head epilogue needs 148 KiB anyway, so a third
+// 48 KiB stage costs no occupancy: two K-steps of pixel DMA in flight instead of one).
+template <int MODE, int WMT, int TAIL, int NWR, int HEADC = 0, int NSK = NS>
 __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
-  using G = Geo<WMT, NWR>;
+  constexpr int NS = NSK;  // (shadows the file-wide default inside this kernel)
+  using G = Geo<WMT, NWR, NSK>;
   static_assert(HEADC == 0 || (WMT == 2 && NWR == 4), "the fused head epilogue is written for 8 waves of 64 x 64");
   constexpr int STAGE = G::STAGE, GLDS_PER_STAGE = G::GLDS_PER_STAGE;
   constexpr int SMEM_BYTES = HEADC ? std::max(G::SMEM, FH_FLOATS * 4) : G::SMEM;
@@ -1180,6 +1183,7 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
   const dim3 grid(u8_fwd_head_blocks(M), 1);
   const int tail = tail_substeps(K);
 #define FH_LAUNCH(T, CC) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC>), grid, dim3(512), 0, stream, p)
+#define FH_LAUNCH3(T) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, 10, 3>), grid, dim3(512), 0, stream, p)
 #define FH_TAILS(CC)                      \
   do {                                    \
     switch (tail) {                       \
@@ -1189,6 +1193,15 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
       default: FH_LAUNCH(NSUB, CC);       \
     }                                     \
   } while (0)
+  if (head.C == 10 && knob(KNOB_U8_FH_STAGES) == 3) {  // 3-stage ring (the 784-128-10 MLP)
+    switch (tail) {
+      case 1: FH_LAUNCH3(1); break;
+      case 2: FH_LAUNCH3(2); break;
+      case 3: FH_LAUNCH3(3); break;
+      default: FH_LAUNCH3(NSUB);
+    }
+    return;
+  }
   switch (head.C) {
     case 10: FH_TAILS(10); break;
     case 2: FH_TAILS(2); break;
@@ -1196,6 +1209,7 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
     default: abort();  // host contract: u8_fwd_head_supported
   }
 #undef FH_TAILS
+#undef FH_LAUNCH3
 #undef FH_LAUNCH
 }
 

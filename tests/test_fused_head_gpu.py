@@ -195,3 +195,30 @@ def test_small_batch_forward_keeps_the_plane_cache_current():
     ops.linear_relu_fwd_u8(torch.cat([x, x]), w, b, ref, 0)  # 4096 rows: the kernel path splits into its cache
     assert cache.token == ops.PlaneCache.token_of(w, 0)
     assert torch.equal(cache.planes, ref.planes)
+
+
+@pytest.mark.parametrize("M", [4096 + 100, 131072])
+def test_fused_forward_head_three_stage_ring_is_bit_identical(M):
+    """The fused uint8 forward + head with a 3-stage LDS ring (knob U8_FH_STAGES=3: two K-steps of DMA in
+    flight) runs the same MFMA / epilogue arithmetic as the 2-stage ring: bit-identical outputs."""
+    from simple_distributed_machine_learning_amd import _native
+
+    K = _native.kernels()
+    x8, w1, b1, w2, b2, tgt = _problem(M, 10, seed=7)
+    outs = []
+    try:
+        for stages in (2, 3):
+            K.set_knob("U8_FH_STAGES", stages)
+            cache = ops.PlaneCache(w1)
+            dl = torch.empty(M, 10, device=DEV)
+            mask = torch.empty(M, N // 32, dtype=torch.int32, device=DEV)
+            gw, gb = torch.zeros(10, N, device=DEV), torch.zeros(10, device=DEV)
+            st = torch.empty(2, device=DEV)
+            bound, pend = ops.linear_relu_head_u8(x8, w1, b1, cache, 0, w2, b2, tgt, gw, gb, 1.0 / M, st, True, dl,
+                                                  mask, defer=False)
+            torch.cuda.synchronize()
+            outs.append((dl, mask, gw, gb, st, bound))
+    finally:
+        K.reset_knobs()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)

@@ -297,6 +297,8 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
 // params / bufs: conv1.w, conv1.b, conv2.w, conv2.b, fc1.w, fc1.b, fc2.w, fc2.b (bufs[i] nullptr: no momentum);
 // rec: [B][ref_cnn_step_record_floats()] scratch; stats [2] = (loss sum, correct) (overwritten); *ctr += 1
 int ref_cnn_step_record_floats();
+// records + the split backward's per-sample workspace (B <= 128)
+int ref_cnn_step_workspace_floats(int B);
 void ref_cnn_step(const float* x, const int64_t* target, int B, float* const* params, float* const* bufs,
                   unsigned long long seed0, unsigned long long seed1, long long* ctr, float p0, bool drop0, float p1,
                   bool drop1, float scale, float lr, float mom, float damp, float wd, bool nesterov, bool first,

@@ -452,6 +452,8 @@ constexpr int R_W2C = 0, R_B2C = R_W2C + C2 * C1 * KS * KS, R_W1C = R_B2C + C2, 
               R_DH = R_B1C + C1, R_Z3 = R_DH + HID, R_DL = R_Z3 + FLAT, R_HD = R_DL + NCLS, R_LOSS = R_HD + HID,
               REC = R_LOSS + 2;
 static_assert(REC == 5712, "record layout");
+// split-backward workspace per sample: G2 [20][8][8], z1 [10][12][12], the conv1 pool argmaxes (bytes)
+constexpr int BWS = C2 * O2 * O2 + NZ1 + NZ1 / 4;
 
 __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __restrict__ x, const int64_t* __restrict__ tgt,
                                                              const float* __restrict__ cw1, const float* __restrict__ cb1,
@@ -461,7 +463,7 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
                                                              unsigned long long seed0, unsigned long long seed1,
                                                              const long long* ctr, float p0, int drop0, float p1,
                                                              int drop1, float scale, float* __restrict__ rec,
-                                                             long long* __restrict__ stamps) {
+                                                             long long* __restrict__ stamps, float* __restrict__ bws) {
   __shared__ float xs[IMG * IMG];
   __shared__ float w1s[C1 * KS * KS];
   __shared__ float w2s[C2 * C1 * KS * KS];
@@ -650,6 +652,14 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
   }
   __syncthreads();
   STAMP(8);
+  if (bws) {  // split backward: hand G2, z1 and the conv1 pool argmaxes to cnn_step_bwd_kernel (10 workgroups per sample)
+    float* wsn = bws + (size_t)n * BWS;
+    for (int i = t; i < C2 * O2 * O2; i += TS) wsn[i] = c2[i];
+    for (int i = t; i < NZ1; i += TS) wsn[C2 * O2 * O2 + i] = z1[i];
+    unsigned char* ab = reinterpret_cast<unsigned char*>(wsn + C2 * O2 * O2 + NZ1);
+    for (int i = t; i < NZ1; i += TS) ab[i] = a1[i];
+    return;
+  }
   const float* G2 = c2;
   // ---- stage 0 backward (cnn_s0_bwd_kernel's phases), contributions into the record ----
   if (t < C2 * C1 * KS) {
@@ -732,6 +742,111 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
   }
   __syncthreads();
   STAMP(15);
+}
+
+// Stage 0's backward of one sample, split over its 10 conv1 channels (one workgroup per (sample, ci), 576
+// threads): the batch of 60 then spreads over 600 workgroups instead of 60, which cuts the sample kernel's
+// critical path roughly in half (its backward phases ran on one CU per sample). Partitioning by the conv1
+// channel ci keeps every output private to one workgroup: dW2[:, ci], dZ1[ci] (all 20 conv2 channels
+// contribute, summed as 4 fixed quarters), the ReLU mask, dW1[ci], db1[ci]; db2 by the ci = 0 workgroup.
+// Fixed summation orders: deterministic. Inputs: x, W2, the forward's G2 / z1 / argmaxes (workspace bws).
+constexpr int TBW = 576;
+__global__ void __launch_bounds__(TBW) cnn_step_bwd_kernel(const float* __restrict__ x, const float* __restrict__ cw2,
+                                                           const float* __restrict__ bws, float* __restrict__ rec) {
+  __shared__ float G2[C2 * O2 * O2];
+  __shared__ float z1c[P1 * P1];
+  __shared__ unsigned char a1c[P1 * P1];
+  __shared__ unsigned char a2s[FLAT];
+  __shared__ float xs[IMG * IMG];
+  __shared__ float w2c[C2 * KS * KS];  // W2[c][ci][ky][kx] of this ci
+  __shared__ float gq[4][P1 * P1];     // dZ1 quarter sums (conv2 channels 5 q .. 5 q + 4)
+  __shared__ float g1[P1 * P1];
+  const int n = blockIdx.x / C1, ci = blockIdx.x % C1, t = threadIdx.x;
+  const float* wsn = bws + (size_t)n * BWS;
+  float* R = rec + (size_t)n * REC;
+  for (int i = t; i < C2 * O2 * O2; i += TBW) G2[i] = wsn[i];
+  for (int i = t; i < P1 * P1; i += TBW) {
+    z1c[i] = wsn[C2 * O2 * O2 + ci * P1 * P1 + i];
+    a1c[i] = reinterpret_cast<const unsigned char*>(wsn + C2 * O2 * O2 + NZ1)[ci * P1 * P1 + i];
+  }
+  for (int i = t; i < IMG * IMG; i += TBW) xs[i] = x[(size_t)n * IMG * IMG + i];
+  for (int i = t; i < C2 * KS * KS; i += TBW) {
+    const int c = i / (KS * KS), k = i % (KS * KS);
+    w2c[i] = cw2[(c * C1 + ci) * KS * KS + k];
+  }
+  __syncthreads();
+  // the conv2 pool argmax of every pooled cell: the one nonzero of G2 in it (G2 is zero elsewhere)
+  for (int o = t; o < FLAT; o += TBW) {
+    const int c = o / (P2 * P2), py = (o / P2) % P2, px = o % P2;
+    int arg = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+      if (G2[(c * O2 + 2 * py + (d >> 1)) * O2 + 2 * px + (d & 1)] != 0.f) arg = d;
+    a2s[o] = (unsigned char)arg;
+  }
+  __syncthreads();
+  if (t < C2 * KS) {
+    // dW2[c][ci][ky][:] from the 16 cells of channel c (their argmax entries; G2 is 0 at the other 48)
+    const int c = t / KS, ky = t % KS;
+    float acc[KS] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int q = 0; q < P2 * P2; ++q) {
+      const int py = q / P2, px = q % P2, d = a2s[c * P2 * P2 + q];
+      const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
+      const float g = G2[(c * O2 + y) * O2 + xx];
+      const float* zr = z1c + (y + ky) * P1 + xx;
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) acc[kx] += g * zr[kx];
+    }
+#pragma unroll
+    for (int kx = 0; kx < KS; ++kx) R[R_W2C + ((c * C1 + ci) * KS + ky) * KS + kx] = acc[kx];
+  } else if (ci == 0 && t >= 128 && t < 128 + C2) {
+    const int c = t - 128;
+    float acc = 0.f;
+    for (int i = 0; i < O2 * O2; ++i) acc += G2[c * O2 * O2 + i];
+    R[R_B2C + c] = acc;
+  }
+  // dZ1[ci][Y][X] = sum_c sum_{ky,kx} G2[c][Y - ky][X - kx] W2[c][ci][ky][kx]: 4 channel quarters x 144 positions
+  {
+    const int q = t / (P1 * P1), pos = t % (P1 * P1);  // t < 576 = 4 x 144
+    const int Y = pos / P1, X = pos % P1;
+    float acc = 0.f;
+    for (int c = 5 * q; c < 5 * q + 5; ++c)
+#pragma unroll
+      for (int ky = 0; ky < KS; ++ky) {
+        const int y = Y - ky;
+        if (y < 0 || y >= O2) continue;
+#pragma unroll
+        for (int kx = 0; kx < KS; ++kx) {
+          const int xx = X - kx;
+          if (xx >= 0 && xx < O2) acc += G2[(c * O2 + y) * O2 + xx] * w2c[(c * KS + ky) * KS + kx];
+        }
+      }
+    gq[q][pos] = acc;
+  }
+  __syncthreads();
+  if (t < P1 * P1) g1[t] = z1c[t] > 0.f ? (gq[0][t] + gq[1][t]) + (gq[2][t] + gq[3][t]) : 0.f;  // ReLU mask
+  __syncthreads();
+  // dW1[ci][ky][kx] = sum over the 144 pooled positions of g1 * x at the argmax tap: 16 lanes per weight
+  // (positions p, p + 16, ...), then a fixed xor tree over the 16; db1 by the threads after them
+  if (t < KS * KS * 16) {
+    const int wi = t >> 4, prt = t & 15;
+    const int ky = wi / KS, kx = wi % KS;
+    float acc = 0.f;
+    for (int q = prt; q < P1 * P1; q += 16) {
+      const int py = q / P1, px = q % P1, d = a1c[q];
+      acc += g1[q] * xs[(2 * py + (d >> 1) + ky) * IMG + 2 * px + (d & 1) + kx];
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    acc += __shfl_xor(acc, 8);
+    if (prt == 0) R[R_W1C + ci * KS * KS + wi] = acc;
+  } else if (t == KS * KS * 16) {
+    float acc = 0.f;
+    for (int q = 0; q < P1 * P1; ++q) acc += g1[q];
+    R[R_B1C + ci] = acc;
+  }
 }
 
 struct CnnParams {
@@ -885,15 +1000,19 @@ void ref_cnn_stage1(const float* x, const float* w1, const float* b1, const floa
 }
 
 int ref_cnn_step_record_floats() { return REC; }
+int ref_cnn_step_workspace_floats(int B) { return B * REC + (B <= 128 ? B * BWS : 0); }
 
 void ref_cnn_step(const float* x, const int64_t* target, int B, float* const* params, float* const* bufs,
                   unsigned long long seed0, unsigned long long seed1, long long* ctr, float p0, bool drop0, float p1,
                   bool drop1, float scale, float lr, float mom, float damp, float wd, bool nesterov, bool first,
                   float* rec, float* stats, hipStream_t stream, long long* stamps) {
   if (B <= 0) return;
+  // B <= 128 (the reference's 60): stage 0's backward as its own launch over 10 workgroups per sample
+  float* bws = (B <= 128 && knob(KNOB_CNN_SPLIT_BWD) && !stamps) ? rec + (size_t)B * REC : nullptr;
   hipLaunchKernelGGL(cnn_step_sample_kernel, dim3(B), dim3(TS), 0, stream, x, target, params[0], params[1], params[2],
                      params[3], params[4], params[5], params[6], params[7], seed0, seed1, ctr, p0, drop0 ? 1 : 0, p1,
-                     drop1 ? 1 : 0, scale, rec, stamps);
+                     drop1 ? 1 : 0, scale, rec, stamps, bws);
+  if (bws) hipLaunchKernelGGL(cnn_step_bwd_kernel, dim3(B * C1), dim3(TBW), 0, stream, x, params[2], bws, rec);
   CnnParams a;
   for (int i = 0; i < 8; ++i) {
     a.p[i] = params[i];

@@ -1288,7 +1288,7 @@ void ref_cnn_step_op(torch::Tensor x, torch::Tensor target, std::vector<torch::T
     TORCH_CHECK(ctr->is_cuda() && ctr->scalar_type() == torch::kInt64 && ctr->numel() == 1, "ref_cnn_step: ctr");
     cp = reinterpret_cast<long long*>(ctr->data_ptr<int64_t>());
   }
-  auto rec = torch::empty({B * sdml::ref_cnn_step_record_floats()}, x.options());
+  auto rec = torch::empty({(int64_t)sdml::ref_cnn_step_workspace_floats((int)B)}, x.options());
   sdml::ref_cnn_step(x.data_ptr<float>(), target.data_ptr<int64_t>(), (int)B, pp, bp, (unsigned long long)seed0,
                      (unsigned long long)seed1, cp, (float)p0, drop0, (float)p1, drop1, (float)scale, (float)lr,
                      (float)mom, (float)damp, (float)wd, nesterov, first, rec.data_ptr<float>(),

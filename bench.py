@@ -98,6 +98,9 @@ def parse():
                    help="pp2dp: pipeline schedule (default chimera)")
     p.add_argument("--dataset_batches", type=int, default=4, help="distinct batches cycled through")
     p.add_argument("--model", default="mlp")
+    p.add_argument("--alternatives", default="auto", choices=["auto", "on", "off"],
+                   help="after the timed steps, also time the reference's placement (pp2dp) for the JSON; "
+                        "auto: at N = 2 only (the reference's own world size)")
     p.add_argument("--pixels", default="u8", choices=["u8", "f32"],
                    help="image storage: MNIST's uint8 bytes (ToTensor's /255 fused into fc1) or float32")
     return p.parse_args()
@@ -282,9 +285,12 @@ def main():
     sps = GB * a.steps / el
     # the reference's own placement, measured next to the chosen one (after the timed region)
     alternatives = {}
-    if (n > 1 and n % 2 == 0 and place != "pp2dp" and a.model == "mlp"
-            and os.environ.get("SDML_BENCH_ALTERNATIVES", "1") != "0"):
-        alternatives["pp2dp"] = _measure_pp2dp(a, n, rank, world, dev)
+    want_alt = a.alternatives == "on" or (a.alternatives == "auto" and n == 2)
+    if want_alt and n > 1 and n % 2 == 0 and place != "pp2dp" and a.model == "mlp":
+        try:
+            alternatives["pp2dp"] = _measure_pp2dp(a, n, rank, world, dev)
+        except Exception as e:  # noqa: BLE001 - the headline number above stands on its own
+            alternatives["pp2dp"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     # what the process group really saw (1 and None for a single-GPU run without collectives)
     seen_world = dist.get_world_size() if dist.is_initialized() else 1
     seen_backend = dist.get_backend() if dist.is_initialized() else None

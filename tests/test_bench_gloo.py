@@ -76,3 +76,12 @@ def test_bench_gpus_flag_spawns_ranks_on_cpu(tmp_path):
     r = subprocess.run(cmd, env=dict(env, WORLD_SIZE="1", RANK="0"), capture_output=True, text=True, timeout=120,
                        cwd=str(tmp_path))
     assert r.returncode == 2 and not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_two_ranks_measures_the_reference_placement():
+    """At N = 2 (the reference's world size) the JSON also carries a measured pp2dp step (stage 0 | stage 1 on
+    the two ranks, Chimera, factored boundary gradient: 512 + 40 B per row over the link)."""
+    d = _run(2)
+    alt = d["config"]["measured_alternatives"]["pp2dp"]
+    assert "error" not in alt, alt
+    assert alt["samples_per_s"] > 0 and alt["boundary_bytes_across_gpus_per_step"] == 2 * 256 * (512 + 40)

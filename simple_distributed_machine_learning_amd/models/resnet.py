@@ -6,12 +6,14 @@ Architecture (CIFAR-style stem for 28x28 inputs): conv3x3(1->64)+BN+ReLU, then 4
 The 8 BasicBlocks are the cut units: stage k gets ``8 / num_stages`` consecutive blocks;
 the stem rides with the first stage and pool+fc with the last.
 
-BatchNorm runs per micro-batch (GPipe semantics). ``dtype=bf16`` runs the stages in bf16
-channels-last (fp32 master weights in the optimizer): every convolution then runs on the
-hand-written kernels of csrc/kernels/conv_bf16.hip — the twelve stride-1 3x3 convolutions (88 % of
-the MACs: forward, input and weight gradients), the stride-2 3x3 and 1x1 shortcut convolutions
-(forward and weight gradient; input gradient on MIOpen) and the one-channel stem — and every
-BatchNorm(+residual)(+ReLU) on csrc/kernels/batchnorm_nhwc.hip. The fp32 default uses MIOpen.
+BatchNorm runs per micro-batch (GPipe semantics). ``dtype=bf16`` (the GPU default of the benchmarks)
+runs the stages in bf16 channels-last (fp32 master weights in the optimizer) on hand-written kernels
+only: every convolution in csrc/kernels/conv_bf16.hip — the stride-1 3x3 convolutions (forward, input
+and weight gradients), the stride-2 3x3 and 1x1 shortcut convolutions (forward, weight gradient, and the
+input gradient as parity-class GEMMs), the one-channel stem — every BatchNorm(+residual)(+ReLU) in
+csrc/kernels/batchnorm_nhwc.hip, and the last stage's average pool + fc + log_softmax + NLL + backward
+in csrc/kernels/head_pool.hip. ``dtype=fp32`` is the CPU / reference-numerics path; on a GPU it runs
+PyTorch's convolutions (MIOpen) and is not a benchmarked configuration.
 """
 from __future__ import annotations
 

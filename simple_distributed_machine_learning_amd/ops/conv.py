@@ -71,14 +71,47 @@ def _take_addend(link):
     return link.take() if link is not None else None
 
 
+# The kernels' weight layouts (conv3x3_weights_bf16: the forward [Co][9][C] and the flipped / transposed dgrad
+# one) depend only on the weight, which is constant within an optimizer step: every micro-batch of a step used
+# to re-derive them (16 launches per ResNet-18 step, 0.14 ms of 4.69: profiles/r3_resnet18_bf16_final_kernel_
+# stats.txt). They are cached per weight, keyed on (storage, version, WEIGHT_GEN): the fused SGD kernels
+# rewrite parameters through raw pointers (no version bump) and so bump WEIGHT_GEN (ops/optim.py); a torch
+# in-place write bumps the version. Never used while a hipGraph is being captured (the replays must
+# re-derive the layouts from the weights they update).
+WEIGHT_GEN = [0]
+_WCACHE = {}
+_WCACHE_ON = __import__("os").environ.get("SDML_CONV_WCACHE", "1") != "0"
+
+
+def bump_weight_generation():
+    WEIGHT_GEN[0] += 1
+    _WCACHE.clear()
+
+
+def _weight_layouts(w, need_dgrad: bool):
+    K = kernels()
+    capturing = torch.cuda.is_current_stream_capturing() or not _WCACHE_ON
+    key = (w.data_ptr(), w._version, WEIGHT_GEN[0], tuple(w.shape))
+    hit = None if capturing else _WCACHE.get(id(w))
+    if hit is not None and hit[0] == key and (hit[2] is not None or not need_dgrad):
+        return hit[1], hit[2]
+    if need_dgrad:
+        wt, wd = K.conv3x3_weights_bf16(w)
+    else:
+        wt, wd = K.conv3x3_weight_bf16(w, False), None
+    if not capturing:
+        _WCACHE[id(w)] = (key, wt, wd)
+    return wt, wd
+
+
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, part=None, link=None):
+        # both layouts in one pass when an input gradient is needed; the dgrad one waits for backward
+        wt, ctx.wd = _weight_layouts(w, ctx.needs_input_grad[0])
         K = kernels()
-        if ctx.needs_input_grad[0]:  # both layouts in one pass; the dgrad one waits for backward
-            wt, ctx.wd = K.conv3x3_weights_bf16(w)
-        else:
-            wt, ctx.wd = K.conv3x3_weight_bf16(w, False), None
+        if not ctx.needs_input_grad[0]:
+            ctx.wd = None
         y = K.conv3x3_fwd_bf16(x, wt, part=part)
         ctx.save_for_backward(x)
         ctx.w, ctx.link = w, link
@@ -121,7 +154,7 @@ def _general_dgrad(dy, x, w, st, pd, add=None):
         return K.conv_dgrad_s2_bf16(dy, w, H, W, pd, add=add)
     if w.shape[2] == 1:
         return K.conv_fwd_bf16(dy, w.reshape(w.shape[0], w.shape[1]).t().contiguous(), 1, 1, 0, add=add)
-    _, wd = K.conv3x3_weights_bf16(w)
+    _, wd = _weight_layouts(w, True)
     return K.conv3x3_fwd_bf16(dy, wd, add=add)
 
 
@@ -134,7 +167,7 @@ class _ConvGeneralFn(torch.autograd.Function):
     def forward(ctx, x, w, stride, pad, part=None, link=None):
         K = kernels()
         ks = w.shape[2]
-        wt = K.conv3x3_weight_bf16(w, False) if ks == 3 else w  # [Co][C][1][1] is already [Co][1][C]
+        wt = _weight_layouts(w, False)[0] if ks == 3 else w  # [Co][C][1][1] is already [Co][1][C]
         y = K.conv_fwd_bf16(x, wt, ks, stride, pad, part=part)
         ctx.save_for_backward(x)
         ctx.w, ctx.stride, ctx.pad, ctx.link = w, stride, pad, link

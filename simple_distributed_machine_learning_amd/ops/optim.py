@@ -61,6 +61,7 @@ class FusedSGD:
             self.flat.grads_zero = True
         self.steps += 1
         self.flat.param_epoch += 1
+        _weights_rewritten()
         if self.plane_cache is not None:
             from . import PlaneCache
 
@@ -95,6 +96,7 @@ class FusedSGD:
             self.flat.grads_zero = True
         self.steps += 1
         self.flat.param_epoch += 1
+        _weights_rewritten()
         if self.plane_cache is not None:
             from . import PlaneCache
 
@@ -140,3 +142,11 @@ class FusedSGD:
                 dst.copy_(src.reshape(-1) if src is not None else
                           self.flat.params[seg.offset:seg.offset + seg.numel].float())
         self.steps = max(self.steps, int(sd.get("steps", 0)))
+
+
+def _weights_rewritten():
+    """The step kernels rewrote parameters through raw pointers: drop weight-derived caches keyed on tensor
+    versions (ops/conv.py's kernel weight layouts)."""
+    from .conv import bump_weight_generation
+
+    bump_weight_generation()

@@ -318,3 +318,39 @@ def test_resnet_last_stage_fused_head_matches_autograd_head(monkeypatch):
     torch.testing.assert_close(d1, d0, rtol=5e-2, atol=5e-2 * float(d0.abs().max()))
     for a, b in zip(g1, g0):
         torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2 * float(b.abs().max()) + 1e-6)
+
+
+def test_resnet_weight_layout_cache_is_exact_across_steps():
+    """ops/conv.py caches the kernels' weight layouts within an optimizer step (keyed on the weight's storage,
+    version and the optimizer's WEIGHT_GEN): 3 training steps of an 8-stage ResNet-18 with M = 4 micro-batches
+    give bit-identical parameters with and without the cache (run in subprocesses: the switch is read at
+    import)."""
+    import os
+    import subprocess
+    import sys
+    import textwrap
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent("""
+        import sys, torch
+        from simple_distributed_machine_learning_amd.data import SyntheticMNIST
+        from simple_distributed_machine_learning_amd.models import get_model_spec
+        from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh
+        dev = torch.device("cuda", 0)
+        mesh = init_mesh(pp=1, schedule_kind="gpipe", rank=0, world_size=1, device=dev)
+        e = PipelineEngine(get_model_spec("resnet18", 8, dtype=torch.bfloat16), mesh, schedule_kind="gpipe",
+                           num_microbatches=4, lr=0.05, momentum=0.9, seed=2)
+        ds = SyntheticMNIST(64 * 3, seed=4, device=dev)
+        for i in range(3):
+            e.run(ds, 64 * i, 64, train=True)
+        torch.cuda.synchronize()
+        torch.save(e.flat.params.cpu(), sys.argv[1])
+    """)
+    outs = []
+    for on in ("1", "0"):
+        path = f"/tmp/sdml_wcache_{on}.pt"
+        env = dict(os.environ, SDML_CONV_WCACHE=on, PYTHONPATH=root)
+        r = subprocess.run([sys.executable, "-c", code, path], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs.append(torch.load(path, weights_only=True))
+    assert torch.equal(outs[0], outs[1])

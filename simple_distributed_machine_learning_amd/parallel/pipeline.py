@@ -217,9 +217,12 @@ class PipelineEngine:
         # data-parallel gradient all-reduce overlapped with backward (rotate all-to-all, nothing crossing,
         # uint8 first layer): the first layer's weight gradient runs as two hidden-unit ranges, the first
         # range's rows are all-reduced while the second range's kernel runs (_dp_split_spans).
-        # SDML_DP_SPLIT=0: one weight-gradient launch, one all-reduce after it. SDML_DP_SPLIT_BLOCKS: row
-        # splits per range (< 256 leaves CUs free for the RCCL kernel).
-        self.dp_split = os.environ.get("SDML_DP_SPLIT", "1") != "0"
+        # SDML_DP_SPLIT_BLOCKS: row splits per range (< 256 leaves CUs free for the RCCL kernel).
+        # Opt-in (SDML_DP_SPLIT=1): measured on one MI355X (profiles/r4_dpsplit_one_rank_rccl*), the two
+        # range launches cost 2 x 45 us against 77 us for the whole gradient (each range writes a full-size
+        # partial slab: twice the slab traffic) plus a second reduction launch, +33 us per step in all,
+        # more than the half all-reduce it can hide is expected to take at 8 ranks.
+        self.dp_split = os.environ.get("SDML_DP_SPLIT", "0") == "1"
         self.dp_split_blocks = int(os.environ.get("SDML_DP_SPLIT_BLOCKS", "240"))
         self.dp_split_steps = 0  # training steps that ran the split (tests)
         self._small_step = None  # one-launch reference-size MLP step available (decided on first use)

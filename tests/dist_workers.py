@@ -14,11 +14,14 @@ def train_worker(rank, world, model, kind, M, pp, steps, B, seed=3, kw=None, tp=
     dev = torch.device(kw.pop("device", "cpu"))
     transport = kw.pop("transport", None)
     eng_kw = {k: kw.pop(k) for k in ("cross_fraction",) if k in kw}
+    dp_split = kw.pop("dp_split", False)
     mesh = init_mesh(pp=pp, schedule_kind=kind, rank=rank, world_size=world, device=dev,
                      backend="gloo", timeout_s=120, tp=tp, transport=transport)
     spec = get_model_spec(model, kw.get("stages"), **{k: v for k, v in kw.items() if k not in ("stages", "pixels")})
     eng = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.1, momentum=0.5, seed=seed,
                          **eng_kw)
+    if dp_split:
+        eng.dp_split = True
     S = eng.data_shards
     if spec.input_kind == "tokens":
         ds = SyntheticTokens(B * S * steps, kw.get("seq_len", 16), 97, seed=7, device=dev)

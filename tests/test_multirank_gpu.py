@@ -68,6 +68,7 @@ def test_rotate_multirank_on_device(world, mode, monkeypatch):
         kw["cross_fraction"] = 0.25
     if mode == "u8_dp":
         kw["cross_fraction"] = 0.0
+        kw["dp_split"] = True  # the opt-in split all-reduce (parity of both weight-gradient ranges)
         M = world  # one wave per rank, as bench.py runs dp
     res = run_ranks(train_worker, world, "mlp", "rotate", M, world, steps, B, 3, kw, timeout=400)
     ref = _single("mlp", M, steps, world * B, "rotate", {"pixels": kw.get("pixels", "f32")})

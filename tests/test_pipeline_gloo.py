@@ -193,7 +193,7 @@ def test_mlp_rotate_cross_fraction_matches_single_process(world, phi, pixels):
     replicated stages (no boundary collective at all), 1.0 sends every row to a peer; every split trains
     to the single-process weights."""
     B, steps, M = 24, 2, 2 * world
-    kw = {"cross_fraction": phi, "pixels": pixels}
+    kw = {"cross_fraction": phi, "pixels": pixels, "dp_split": True}  # (the opt-in all-reduce overlap)
     res = run_ranks(train_worker, world, "mlp", "rotate", M, world, steps, B, 3, kw)
     ref = _single("mlp", M, steps, world * B, "rotate", {"pixels": pixels})
     _compare(res, ref, rtol=1e-4, atol=1e-5)

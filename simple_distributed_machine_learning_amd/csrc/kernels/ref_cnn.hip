@@ -34,6 +34,8 @@
 namespace sdml {
 namespace {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 constexpr int IMG = 28, KS = 5, C1 = 10, O1 = 24, P1 = 12, C2 = 20, O2 = 8, P2 = 4;
 constexpr int FLAT = C2 * P2 * P2;  // 320
 constexpr int HID = 50, NCLS = 10;
@@ -489,9 +491,19 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
     for (int i = 0; i < 5; ++i) w1r[u][i] = j < HID ? fw1[(size_t)j * FLAT + lane + 64 * i] : 0.f;
   }
   const float* xn = x + (size_t)n * IMG * IMG;
-  for (int i = t; i < IMG * IMG; i += TS) xs[i] = xn[i];
-  for (int i = t; i < C1 * KS * KS; i += TS) w1s[i] = cw1[i];
-  for (int i = t; i < C2 * C1 * KS * KS; i += TS) w2s[i] = cw2[i];
+  {  // every global load issued before the first LDS store: one latency instead of one per loop round
+    constexpr int NW2 = (C2 * C1 * KS * KS + TS - 1) / TS;  // 5
+    float w2v[NW2];
+#pragma unroll
+    for (int u = 0; u < NW2; ++u) w2v[u] = t + TS * u < C2 * C1 * KS * KS ? cw2[t + TS * u] : 0.f;
+    const float xv = t < IMG * IMG ? xn[t] : 0.f;
+    const float w1v = t < C1 * KS * KS ? cw1[t] : 0.f;
+#pragma unroll
+    for (int u = 0; u < NW2; ++u)
+      if (t + TS * u < C2 * C1 * KS * KS) w2s[t + TS * u] = w2v[u];
+    if (t < IMG * IMG) xs[t] = xv;
+    if (t < C1 * KS * KS) w1s[t] = w1v;
+  }
   for (int i = t; i < NZ1; i += TS) g1[i] = 0.f;
   if (t < C2) dsc[t] = drop0 ? keep_scale(eff_seed(seed0, ctr), n, t, p0) : 1.f;
   __syncthreads();
@@ -753,26 +765,36 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
 constexpr int TBW = 576;
 __global__ void __launch_bounds__(TBW) cnn_step_bwd_kernel(const float* __restrict__ x, const float* __restrict__ cw2,
                                                            const float* __restrict__ bws, float* __restrict__ rec) {
-  __shared__ float G2[C2 * O2 * O2];
+  __shared__ __attribute__((aligned(16))) float G2[C2 * O2 * O2];
   __shared__ float z1c[P1 * P1];
   __shared__ unsigned char a1c[P1 * P1];
   __shared__ unsigned char a2s[FLAT];
-  __shared__ float xs[IMG * IMG];
+  __shared__ __attribute__((aligned(16))) float xs[IMG * IMG];
   __shared__ float w2c[C2 * KS * KS];  // W2[c][ci][ky][kx] of this ci
   __shared__ float gq[4][P1 * P1];     // dZ1 quarter sums (conv2 channels 5 q .. 5 q + 4)
   __shared__ float g1[P1 * P1];
   const int n = blockIdx.x / C1, ci = blockIdx.x % C1, t = threadIdx.x;
   const float* wsn = bws + (size_t)n * BWS;
   float* R = rec + (size_t)n * REC;
-  for (int i = t; i < C2 * O2 * O2; i += TBW) G2[i] = wsn[i];
-  for (int i = t; i < P1 * P1; i += TBW) {
-    z1c[i] = wsn[C2 * O2 * O2 + ci * P1 * P1 + i];
-    a1c[i] = reinterpret_cast<const unsigned char*>(wsn + C2 * O2 * O2 + NZ1)[ci * P1 * P1 + i];
+  // every global load of the workgroup is issued before the first LDS store (one latency, not one per loop
+  // round: these bytes were just written by the sample kernel on other XCDs); 16-B loads where aligned
+  // (BWS and 784 floats are multiples of 4)
+  f32x4 g2v = {}, xv = {};
+  float w2v = 0.f, z1v = 0.f;
+  unsigned char a1v = 0;
+  if (t < C2 * O2 * O2 / 4) g2v = reinterpret_cast<const f32x4*>(wsn)[t];
+  if (t < IMG * IMG / 4) xv = reinterpret_cast<const f32x4*>(x + (size_t)n * IMG * IMG)[t];
+  if (t < C2 * KS * KS) w2v = cw2[((t / (KS * KS)) * C1 + ci) * KS * KS + t % (KS * KS)];
+  if (t < P1 * P1) {
+    z1v = wsn[C2 * O2 * O2 + ci * P1 * P1 + t];
+    a1v = reinterpret_cast<const unsigned char*>(wsn + C2 * O2 * O2 + NZ1)[ci * P1 * P1 + t];
   }
-  for (int i = t; i < IMG * IMG; i += TBW) xs[i] = x[(size_t)n * IMG * IMG + i];
-  for (int i = t; i < C2 * KS * KS; i += TBW) {
-    const int c = i / (KS * KS), k = i % (KS * KS);
-    w2c[i] = cw2[(c * C1 + ci) * KS * KS + k];
+  if (t < C2 * O2 * O2 / 4) reinterpret_cast<f32x4*>(G2)[t] = g2v;
+  if (t < IMG * IMG / 4) reinterpret_cast<f32x4*>(xs)[t] = xv;
+  if (t < C2 * KS * KS) w2c[t] = w2v;
+  if (t < P1 * P1) {
+    z1c[t] = z1v;
+    a1c[t] = a1v;
   }
   __syncthreads();
   // the conv2 pool argmax of every pooled cell: the one nonzero of G2 in it (G2 is zero elsewhere)
@@ -806,22 +828,28 @@ __global__ void __launch_bounds__(TBW) cnn_step_bwd_kernel(const float* __restri
     for (int i = 0; i < O2 * O2; ++i) acc += G2[c * O2 * O2 + i];
     R[R_B2C + c] = acc;
   }
-  // dZ1[ci][Y][X] = sum_c sum_{ky,kx} G2[c][Y - ky][X - kx] W2[c][ci][ky][kx]: 4 channel quarters x 144 positions
+  // dZ1[ci][Y][X] = sum_c sum_{ky,kx} G2[c][Y - ky][X - kx] W2[c][ci][ky][kx]: 4 channel quarters x 144 positions.
+  // G2 has one nonzero per pooled cell (at its argmax), so the 5 x 5 window of (Y, X) meets at most 3 x 3
+  // cells per channel: 45 candidate terms per thread instead of the dense 125 (fixed trip counts, predicated)
   {
     const int q = t / (P1 * P1), pos = t % (P1 * P1);  // t < 576 = 4 x 144
     const int Y = pos / P1, X = pos % P1;
+    const int py0 = max(Y - (KS - 1), 0) >> 1, px0 = max(X - (KS - 1), 0) >> 1;
     float acc = 0.f;
     for (int c = 5 * q; c < 5 * q + 5; ++c)
 #pragma unroll
-      for (int ky = 0; ky < KS; ++ky) {
-        const int y = Y - ky;
-        if (y < 0 || y >= O2) continue;
+      for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int kx = 0; kx < KS; ++kx) {
-          const int xx = X - kx;
-          if (xx >= 0 && xx < O2) acc += G2[(c * O2 + y) * O2 + xx] * w2c[(c * KS + ky) * KS + kx];
+        for (int j = 0; j < 3; ++j) {
+          const int py = py0 + i, px = px0 + j;
+          if (py < P2 && px < P2) {
+            const int d = a2s[c * P2 * P2 + py * P2 + px];
+            const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
+            const int ky = Y - y, kx = X - xx;
+            if (ky >= 0 && ky < KS && kx >= 0 && kx < KS)
+              acc += G2[(c * O2 + y) * O2 + xx] * w2c[(c * KS + ky) * KS + kx];
+          }
         }
-      }
     gq[q][pos] = acc;
   }
   __syncthreads();
@@ -856,14 +884,14 @@ struct CnnParams {
   int nesterov, first;
 };
 
-// torch.optim.SGD on one parameter (sgd_rule.h's operations, explicit fmas)
-__device__ __forceinline__ void sgd_update1(float* pp, float* bp, float d, const CnnParams& a) {
+// torch.optim.SGD on one parameter (sgd_rule.h's operations, explicit fmas); pv / bv: the parameter and its
+// momentum buffer, loaded by the caller ahead of the gradient sums (their latency overlaps the record loads)
+__device__ __forceinline__ void sgd_update1(float* pp, float* bp, float d, const CnnParams& a, float pv, float bv) {
 #pragma clang fp contract(off)
-  const float pv = *pp;
   if (a.wd != 0.f) d = __builtin_fmaf(a.wd, pv, d);
   if (a.mom != 0.f) {
     float b = d;
-    if (!a.first) b = __builtin_fmaf(a.mom, *bp, (1.f - a.damp) * d);
+    if (!a.first) b = __builtin_fmaf(a.mom, bv, (1.f - a.damp) * d);
     *bp = b;
     d = a.nesterov ? __builtin_fmaf(a.mom, b, d) : b;
   }
@@ -900,6 +928,21 @@ __global__ void __launch_bounds__(256) cnn_step_update_kernel(const float* __res
   __shared__ float part[UG][UP];
   const int j = threadIdx.x % UP, g = threadIdx.x / UP;
   const int i = blockIdx.x * UP + j;
+  // the parameter this column updates (tensor ti, element): its value and momentum are loaded now, under the
+  // record loads below
+  float pv = 0.f, bv = 0.f;
+  if (g == 0 && i < total) {
+    int tt = 0, ee = i;
+    const int sizes[8] = {n0, n1, n2, n3, n4, n5, n6, n7};
+#pragma unroll
+    for (int q = 0; q < 7; ++q)
+      if (tt == q && ee >= sizes[q]) {
+        ee -= sizes[q];
+        tt = q + 1;
+      }
+    pv = a.p[tt][ee];
+    if (a.buf[tt] && !a.first) bv = a.buf[tt][ee];
+  }
   int ti = -1, e = i;
   float v = 0.f;
   if (i < total) {
@@ -935,7 +978,7 @@ __global__ void __launch_bounds__(256) cnn_step_update_kernel(const float* __res
   if (g == 0 && ti >= 0) {
     const float gr = ((part[0][j] + part[1][j]) + (part[2][j] + part[3][j])) +
                      ((part[4][j] + part[5][j]) + (part[6][j] + part[7][j]));
-    sgd_update1(a.p[ti] + e, a.buf[ti] ? a.buf[ti] + e : nullptr, gr, a);
+    sgd_update1(a.p[ti] + e, a.buf[ti] ? a.buf[ti] + e : nullptr, gr, a, pv, bv);
   }
   if (blockIdx.x == 0) {  // (loss sum, correct): 256 strided partials, then a fixed-order tree (deterministic).
     // (A serial loop over the B records on two threads was B dependent round trips to records other XCDs had

@@ -957,6 +957,8 @@ torch::Tensor head_pool_xent(torch::Tensor x, torch::Tensor w, torch::Tensor b, 
                   target.numel() == M && stats.numel() == 2,
               "head_pool_xent: shape mismatch");
   TORCH_CHECK(sdml::head_pool_supported((int)M, (int)P, (int)K, (int)C), "head_pool_xent: unsupported shape");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(w.data_ptr()) & 15) == 0,
+              "head_pool_xent: x and w must be 16-B aligned (16-B loads)");
   auto dx = torch::empty_like(x);
   auto ws = torch::empty({sdml::head_pool_workspace_floats((int)M, (int)K, (int)C)}, stats.options());
   sdml::head_pool_xent(x.data_ptr(), w.data_ptr(), b.data_ptr(), target.data_ptr<int64_t>(), (int)M, (int)P, (int)K,

@@ -358,6 +358,7 @@ def pooled_head_xent(y, w, b, target, gw, gb, scale: float, stats, stats_init: b
 
 def pooled_head_ok(y, w) -> bool:
     return bool(y.is_cuda and y.dim() == 4 and y.dtype in (torch.bfloat16, torch.float32) and w.dtype == y.dtype
+                and w.is_contiguous() and w.data_ptr() % 16 == 0 and y.data_ptr() % 16 == 0
                 and _k().head_pool_supported(y.shape[0], y.shape[2] * y.shape[3], y.shape[1], w.shape[0]))
 
 

@@ -36,6 +36,8 @@ const Entry kTable[KNOB_COUNT] = {
     {"U8_FWD_X3", 0, false, "x3"},
     {"U8_WGRAD_X3", 0, false, "x3"},
     {"U8_FH_STAGES", 2, false, nullptr},
+    {"U8_FWD_PRIO", 0, false, nullptr},
+    {"U8_WGRAD_PRIO", 0, false, nullptr},
     {"CNN_SPLIT_BWD", 1, false, nullptr},
     {"GEMM_BF16_NOSTORE", 0, true, nullptr},
     {"U8_VARIANT", 0, true, nullptr},

@@ -35,6 +35,8 @@ enum KnobId : int {
   KNOB_U8_FWD_X3,            // 1: uint8 forward on the older bf16x3 kernel
   KNOB_U8_WGRAD_X3,          // 1: uint8 weight gradient on the older bf16x3 kernel
   KNOB_U8_FH_STAGES,         // LDS ring stages of the fused uint8 forward + head (2 or 3)
+  KNOB_U8_FWD_PRIO,          // 1: s_setprio 1 on the younger half of the uint8 forward's waves
+  KNOB_U8_WGRAD_PRIO,        // 1: the same in the uint8 weight gradient
   KNOB_CNN_SPLIT_BWD,        // reference CNN step, B <= 128: stage 0's backward over 10 workgroups per sample
   // ---- probe switches (pinned in production builds) ----
   KNOB_GEMM_BF16_NOSTORE,    // 1: bf16 GEMM skips its output stores (timing only)

@@ -125,6 +125,7 @@ struct FwdParams {
   int M, N, K, Kp, ldx, ldc;
   float scale;
   int relu;
+  int prio;        // 1: s_setprio 1 on the second half of the waves (each SIMD's younger wave; A/B knob U8_FWD_PRIO)
   unsigned* mask;  // optional [M][N / 32] ReLU bits (plain epilogue)
   float* wmax;     // optional [blocks][WAVES] per-wave max of the stored outputs (plain epilogue): a bound the
                    // next layer's two-plane split (gemm_f16x2.hip) reads instead of an inf-norm pass
@@ -198,6 +199,9 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave % NWR, wn = wave / NWR;
+  // static priority for the second-dispatched half (waves w and w + WAVES / 2 share a SIMD): the guide's
+  // MI355X_MICROARCH "Two waves per SIMD" item 4 (knob, off by default until measured here)
+  if (p.prio && wave >= G::WAVES / 2) __builtin_amdgcn_s_setprio(1);
   const int h = lane >> 5, r32 = lane & 31;
 
   f32x16 acc[WMT][2];
@@ -633,6 +637,7 @@ struct WgradParams {
   int groups, splits;        // hidden groups launched x row splits (1-D grid, XCD-aware order)
   int g0;                    // first hidden group launched (hidden units GHN g0 ..)
   int xcd;                   // 0: plain order (split-major), A/B only (SDML_U8_WGRAD_XCD=0)
+  int prio;                  // 1: s_setprio 1 on waves 4..7 (knob U8_WGRAD_PRIO)
 };
 
 // dx tile of head_xent.hip's MFMA head (dx_t / head_mfma_dx_from_dl_kernel), reproduced operation
@@ -665,6 +670,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) u16 smem[2 * GBUF_U16];
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (p.prio && wave >= GT / 128) __builtin_amdgcn_s_setprio(1);  // (knob U8_WGRAD_PRIO)
   // XCD-aware order: the hidden groups of one row split read the same pixel rows, so they are given
   // block ids 8 apart (same XCD under the round-robin dispatch, one L2) and run side by side:
   // L = 8 G (s / 8) + 8 g + s % 8. Ids past the last split (splits rounded up to 8) exit here.
@@ -1004,6 +1010,7 @@ void u8_wgrad(const float* dz, const unsigned char* X, int M, int N, int ldx, fl
   p.groups = N / GHN;
   p.splits = splits;
   p.xcd = wgrad_xcd();
+  p.prio = knob(KNOB_U8_WGRAD_PRIO);
   hipLaunchKernelGGL(u8_wgrad_kernel<0>, dim3(((splits + 7) / 8) * 8 * p.groups), dim3(GT), 0, stream, p);
   slab_reduce(slab, (int64_t)N * GKC + N, splits, gwb, (int64_t)N * GKC + N, stream);
 }
@@ -1039,6 +1046,7 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigne
   p.rows_per_split = ((M + splits - 1) / splits + GBK - 1) / GBK * GBK;
   p.splits = splits;
   p.xcd = wgrad_xcd();
+  p.prio = knob(KNOB_U8_WGRAD_PRIO);
   const dim3 wgrid(((splits + 7) / 8) * 8 * p.groups);
   if (mask) hipLaunchKernelGGL(u8_wgrad_kernel<2>, wgrid, dim3(GT), 0, stream, p);
   else hipLaunchKernelGGL(u8_wgrad_kernel<1>, wgrid, dim3(GT), 0, stream, p);
@@ -1180,6 +1188,7 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
   p.scale = scale / kU8FwdWScale;
   p.relu = 1;
   p.head = head;
+  p.prio = knob(KNOB_U8_FWD_PRIO);
   const dim3 grid(u8_fwd_head_blocks(M), 1);
   const int tail = tail_substeps(K);
 #define FH_LAUNCH(T, CC) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC>), grid, dim3(512), 0, stream, p)

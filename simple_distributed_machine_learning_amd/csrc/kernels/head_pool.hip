@@ -9,13 +9,16 @@
 // every load and store moves 16 B (bf16) per lane): feats = mean_p x (fp32), z = feats W^T + b (fp32),
 // loss = logsumexp(z) - z[y], correct = (first argmax == y), dl = scale (softmax(z) - onehot(y)),
 // dfeat = dl W, dx[m][p][k] = dfeat[k] / P (the pool's backward; written in x's type). A workgroup (4 waves)
-// runs HP_ROWS = 16 rows, 4 per wave, and writes its dW / db / (loss, correct) sums over those rows, in row
+// runs HP_ROWS = 4 rows, 1 per wave, and writes its dW / db / (loss, correct) sums over those rows, in row
 // order, to a workspace slab; head_pool_reduce adds the slabs (4 strided groups per entry, combined in a fixed
 // order) into gW / gb (accumulated, in the parameters' type) and stats (added, or overwritten) -
 // deterministic. Rows with a label outside [0, C) get no loss term and no gradient (as head_xent.hip's heads).
 //
 // Round 4 first version: one row per wave with scalar loads and a serial slab reduction ran 56 + 32 us at
-// ResNet's 512 x 16 x 512 (profiles/r4_resnet18_bf16_kernel_stats.txt), slower than the ATen head.
+// ResNet's 512 x 16 x 512 (profiles/r4_resnet18_bf16_kernel_stats.txt), slower than the ATen head. The second
+// (16 rows per workgroup, 4 per wave, one position load in flight per lane) still took 58 us: 32 workgroups, each
+// wave waiting out 64 dependent HBM round trips. Now: one row per wave (128 workgroups at M = 512) and the
+// positions' loads issued HP_PU at a time.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -26,7 +29,8 @@ namespace sdml {
 namespace {
 
 constexpr int HP_WAVES = 4;
-constexpr int HP_RPW = 4;                     // rows per wave
+constexpr int HP_RPW = 1;                     // rows per wave
+constexpr int HP_PU = 8;                      // positions loaded per batch (independent loads in flight)
 constexpr int HP_ROWS = HP_WAVES * HP_RPW;    // rows per workgroup
 constexpr int HP_MAXCH = 2;                   // 8-channel chunks per lane: K <= 1024
 constexpr int HP_MAXC = 16;
@@ -102,7 +106,17 @@ __global__ void __launch_bounds__(64 * HP_WAVES) head_pool_kernel(const T* __res
         for (int e = 0; e < 8; ++e) f[q][e] = 0.f;
         if (q < nch && k0 < K) {
           const T* xp = x + (size_t)m * P * K + k0;
-          for (int p = 0; p < P; ++p) {
+          int p = 0;
+          for (; p + HP_PU <= P; p += HP_PU) {  // HP_PU loads in flight, added in position order
+            float v[HP_PU][8];
+#pragma unroll
+            for (int u = 0; u < HP_PU; ++u) ld8(xp + (size_t)(p + u) * K, v[u]);
+#pragma unroll
+            for (int u = 0; u < HP_PU; ++u)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) f[q][e] += v[u][e];
+          }
+          for (; p < P; ++p) {
             float v[8];
             ld8(xp + (size_t)p * K, v);
 #pragma unroll

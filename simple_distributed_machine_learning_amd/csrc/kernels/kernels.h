@@ -148,6 +148,10 @@ struct U8HeadArgs {
 };
 bool u8_fwd_head_supported(int M, int N, int K, int ldx, const void* X, int C);
 int u8_fwd_head_blocks(int M);
+// experiments builds: the next u8_fwd_head launches write MODE 7 phase stamps into buf ([blocks][8][u8_stamp_slots()]
+// int64; nullptr turns them off); production builds return false and ignore it
+bool u8_set_stamps(void* buf);
+int u8_stamp_slots();
 void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
                  const float* bias, float scale, const U8HeadArgs& head, hipStream_t stream);
 // mlp_u8.hip: weight + bias gradient of the uint8-fed first layer (K = 784 pixel columns, N % 64 == 0,

@@ -40,6 +40,7 @@
 
 #include "head_reduce.h"
 #include "head_tile.h"
+#include "lds_dma.h"
 #include "kernels.h"
 #include "sgd_rule.h"
 #include "u8_planes.h"
@@ -130,7 +131,18 @@ struct FwdParams {
   float* wmax;     // optional [blocks][WAVES] per-wave max of the stored outputs (plain epilogue): a bound the
                    // next layer's two-plane split (gemm_f16x2.hip) reads instead of an inf-norm pass
   U8HeadArgs head;  // fused head epilogue (HEADC > 0)
+  long long* stamps;  // MODE 7 (experiments builds only): per-wave phase stamps, U8_NSTAMP per (block, wave)
 };
+
+// MODE 7 diagnostic stamps (tools/probes/u8_fwd_stamps.py): lane 0 of every wave writes s_memtime after each
+// phase (vector stores into a buffer nothing else reads); slots 0 / U8_NSTAMP - 1 hold s_memrealtime
+constexpr int U8_NSTAMP = 24;
+#define U8_STAMP(k, fn)                                                                                  \
+  do {                                                                                                   \
+    if constexpr (MODE == 7) {                                                                           \
+      if (lane == 0) p.stamps[((size_t)blockIdx.x * G::WAVES + wave) * U8_NSTAMP + (k)] = (long long)fn(); \
+    }                                                                                                    \
+  } while (0)
 
 // ---- fused classifier-head epilogue (HEADC > 0; NWR = 4, WMT = 2: 8 waves, 256 rows x 128 hidden per
 // block). LDS (floats): the block's h as 16 x-tile images of head_tile.h's xt_at layout [16][2048],
@@ -150,6 +162,10 @@ template <int WMT, int NWR>
 __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* st, int m0, int n0, int k0, int wave,
                                            int lane) {
   using G = Geo<WMT, NWR>;
+  // buffer-form DMA (lds_dma.h: keeps the fragment reads' lgkmcnt waits counted); u8_fwd_supported keeps
+  // M * ldx < 2^31, the planes are small
+  const __amdgpu_buffer_rsrc_t rx = dma_rsrc(p.X, (unsigned)((size_t)p.M * p.ldx));
+  const __amdgpu_buffer_rsrc_t rw = dma_rsrc(p.Wp, (unsigned)((size_t)NPL * p.N * p.Kp * 2));
   constexpr int XROWS = 1024 / FBK;  // pixel rows per DMA instruction
 #pragma unroll
   for (int u = 0; u < G::GLDS_X; ++u) {
@@ -159,7 +175,7 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
     const int ch = xpos(row, pos);  // xpos is an involution: the chunk stored at `pos`
     const int gr = min(m0 + row, p.M - 1);
     const int gk = min(k0 + 16 * ch, p.K - 16);  // past the end: finite bytes meeting zero weights
-    glds16(p.X + (size_t)gr * p.ldx + gk, st + 1024 * q);
+    bdma16(rx, (unsigned)((size_t)gr * p.ldx + gk), st + 1024 * q);
   }
   constexpr int WROWS = 1024 / (2 * FBK);  // weight rows per DMA instruction
   constexpr int WINST = FBN / WROWS;       // instructions per plane
@@ -170,7 +186,7 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
     const int pl = q / WINST;
     const int row = WROWS * (q % WINST) + lane / WCH;
     const int ch = wpos(row, lane % WCH);
-    glds16(p.Wp + pl * plane + (size_t)(n0 + row) * p.Kp + k0 + 8 * ch, st + G::A_BYTES + 1024 * q);
+    bdma16(rw, (unsigned)(2 * (pl * plane + (size_t)(n0 + row) * p.Kp + k0 + 8 * ch)), st + G::A_BYTES + 1024 * q);
   }
 }
 
@@ -181,7 +197,7 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
 // host so the kernel carries one straight-line tail)
 template <int C>
 __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
-                                                    int m0, int wave, int lane, int wm, int wn);
+                                                    int m0, int wave, int lane, int wm, int wn, long long* stamp);
 
 // HEADC = 0: store h = act(scale acc + b) (+ its ReLU bits when p.mask); HEADC = C > 0: the fused
 // classifier head on h (fused_head_epilogue), h is never stored
@@ -203,6 +219,8 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
   // MI355X_MICROARCH "Two waves per SIMD" item 4 (knob, off by default until measured here)
   if (p.prio && wave >= G::WAVES / 2) __builtin_amdgcn_s_setprio(1);
   const int h = lane >> 5, r32 = lane & 31;
+  U8_STAMP(0, __builtin_amdgcn_s_memrealtime);
+  U8_STAMP(1, __builtin_amdgcn_s_memtime);
 
   f32x16 acc[WMT][2];
 #pragma unroll
@@ -257,19 +275,46 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
         for (int pl = NPL - 1; pl >= 0; --pl) acc[i][j] = mfma(a, b[j][pl], acc[i][j]);  // lo first
     }
   };
-  auto kstep = [&](const unsigned char* st, auto ns_c) {
+  // DMA_AT: substep after whose MFMAs a K-step issues the next stage's DMA (-1: right after the barrier, the
+  // production schedule; MODE 8 / 9, experiments: after substep 0 / 1)
+  constexpr int DMA_AT = MODE == 8 ? 0 : (MODE == 9 ? 1 : -1);
+  // PIPE: the pipelined K-step (MODE 11, experiments)
+  constexpr bool PIPE = MODE == 11;
+  auto kstep = [&](const unsigned char* st, auto ns_c, auto&& dma) {
     constexpr int NS_ = decltype(ns_c)::value;
     if constexpr (MODE == 1) return;
     // (reading substep s+1's fragments ahead of substep s's MFMAs, pinned with sched_barrier,
     // measured no faster at either geometry: 87.2 vs 87.5 us; neither did s_setprio 1 around
     // each substep's MFMAs: 92.3-92.9 vs 91.5-93.4 us)
-    u32x4 ar[WMT];
-    f16x8 b[2][NPL];
+    if constexpr (PIPE) {
+      // register double buffer: substep s + 1's fragment reads are issued before substep s's MFMAs (pinned
+      // with sched_barrier), so each counted lgkmcnt wait covers reads that had a whole substep of MFMAs
+      // to land; the next stage's DMA goes out while substep 0's reads are in flight
+      u32x4 ar[2][WMT];
+      f16x8 b[2][2][NPL];
+      load_a(st, 0, ar[0]);
+      load_b(st, 0, b[0]);
+      dma();
 #pragma unroll
-    for (int s = 0; s < NS_; ++s) {
-      if (s % 2 == 0) load_a(st, s >> 1, ar);
-      load_b(st, s, b);
-      compute(s, ar, b);
+      for (int s = 0; s < NS_; ++s) {
+        if (s + 1 < NS_) {
+          if ((s + 1) % 2 == 0) load_a(st, (s + 1) >> 1, ar[((s + 1) >> 1) & 1]);
+          load_b(st, s + 1, b[(s + 1) & 1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        compute(s, ar[(s >> 1) & 1], b[s & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+      u32x4 ar[WMT];
+      f16x8 b[2][NPL];
+#pragma unroll
+      for (int s = 0; s < NS_; ++s) {
+        if (s % 2 == 0) load_a(st, s >> 1, ar);
+        load_b(st, s, b);
+        compute(s, ar, b);
+        if (s == DMA_AT) dma();
+      }
     }
   };
 
@@ -306,17 +351,37 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
         issue_stage<WMT, NWR>(p, smem + ((t + NS - 1) % NS) * STAGE, m0, n0, (t + NS - 1) * FBK, wave, lane);
     }
   };
+  auto no_dma = [] {};
   for (int t = 0; t + 1 < nk; ++t) {  // NS == 2: K-step t + 1 always exists here
-    sync_step(t, std::true_type{});
-    kstep(smem + (t % NS) * STAGE, std::integral_constant<int, NSUB>{});
+    sync_step(t, std::integral_constant<bool, (DMA_AT < 0 && !PIPE)>{});
+    if (t < 13) U8_STAMP(2 + t, __builtin_amdgcn_s_memtime);
+    kstep(smem + (t % NS) * STAGE, std::integral_constant<int, NSUB>{}, [&] {
+      if (NS == 2 || t + NS - 1 < nk)
+        issue_stage<WMT, NWR>(p, smem + ((t + NS - 1) % NS) * STAGE, m0, n0, (t + NS - 1) * FBK, wave, lane);
+    });
   }
   {  // last K-step: only the substeps holding k < K (lane half 0 covers the first FBK / 2 k)
     sync_step(nk - 1, std::integral_constant<bool, (NS > 2)>{});
-    kstep(smem + ((nk - 1) % NS) * STAGE, std::integral_constant<int, TAIL>{});
+    kstep(smem + ((nk - 1) % NS) * STAGE, std::integral_constant<int, TAIL>{}, no_dma);
+  }
+  U8_STAMP(15, __builtin_amdgcn_s_memtime);
+  if constexpr (MODE == 10) {  // timing only: the K loop alone (keep the accumulators alive)
+    float keep = 0.f;
+#pragma unroll
+    for (int i = 0; i < WMT; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) keep += acc[i][j][r];
+    if (keep == 12345.f && lane == 99) p.stamps[0] = 1;
+    return;
   }
 
   if constexpr (HEADC > 0) {
-    fused_head_epilogue<HEADC>(p, acc, smem, m0, wave, lane, wm, wn);
+    fused_head_epilogue<HEADC>(p, acc, smem, m0, wave, lane, wm, wn,
+                               MODE == 7 ? p.stamps + ((size_t)blockIdx.x * G::WAVES + wave) * U8_NSTAMP : nullptr);
+    U8_STAMP(22, __builtin_amdgcn_s_memtime);
+    U8_STAMP(U8_NSTAMP - 1, __builtin_amdgcn_s_memrealtime);
     return;
   }
   // epilogue: relu(scale * acc + bias), transposed through LDS so that every lane stores whole
@@ -380,7 +445,10 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
 //  3. wave partials meet in LDS in wave order -> one slab row + one |dl @ W2| bound per block
 template <int C>
 __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
-                                                    int m0, int wave, int lane, int wm, int wn) {
+                                                    int m0, int wave, int lane, int wm, int wn, long long* stamp) {
+  auto st = [&](int k) {  // MODE 7 only (stamp == nullptr otherwise, folded away)
+    if (stamp && lane == 0) stamp[k] = (long long)__builtin_amdgcn_s_memtime();
+  };
   using namespace headtile;
   const U8HeadArgs& hd = p.head;
   float* F = reinterpret_cast<float*>(smem);
@@ -390,6 +458,7 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
   float* red = F + FH_RED;  // [8][2 + 16] (loss, correct, db) then [8] dz bounds
   const int tid = threadIdx.x, h2 = lane >> 5, r32 = lane & 31;
   __syncthreads();  // every wave's last K-step reads are done: the stage buffers are free
+  st(16);
   for (int i = tid; i < 16 * 32; i += 512) {  // W2, zero-padded to 16 classes
     const int c = i >> 5, k4 = i & 31;
     *reinterpret_cast<f32x4m*>(ws + c * FH_WSP + 4 * k4) =
@@ -417,7 +486,9 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
     const int row = m0 + wm * 64 + lane;
     if (row < p.M) *reinterpret_cast<uint2*>(hd.mask + (size_t)row * 4 + 2 * wn) = uint2{mw[0], mw[1]};
   }
+  st(17);
   __syncthreads();
+  st(18);
 
   const int r = lane & 15, g = lane >> 4;
   f32x4m wl[8];  // wl[u][e] = W2[class r][16 u + 4 g + e]
@@ -442,8 +513,10 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
     logits_dz<C>(wl, bv, xv, tg[it], row < p.M, true, hd.loss_scale, g, a, dz, hd.dl + (size_t)row * C, true);
     dw_accum(xw, dzt, dz, r, g, a);
   }
+  st(19);
 
   __syncthreads();  // every tile done: the x images are free for the wave partials
+  st(20);
   float* mine = F + wave * (C * 128);
   if (r < C) {
 #pragma unroll
@@ -483,6 +556,7 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
     for (int w = 1; w < 8; ++w) am = fmaxf(am, red[8 * 18 + w]);
     if (lane == 0) hd.bound[blockIdx.x] = 2.f * am * wm2;
   }
+  st(21);
 }
 
 // fp32 [N][K] -> zero-padded fp16 planes [NPL][N][Kp] of W * 2^8 (u8_planes.h)
@@ -1172,6 +1246,20 @@ bool u8_fwd_head_supported(int M, int N, int K, int ldx, const void* X, int C) {
 
 int u8_fwd_head_blocks(int M) { return (M + FH_ROWS - 1) / FH_ROWS; }
 
+#ifdef SDML_KERNEL_EXPERIMENTS
+static long long* g_u8_stamps = nullptr;
+#endif
+bool u8_set_stamps(void* buf) {
+#ifdef SDML_KERNEL_EXPERIMENTS
+  g_u8_stamps = static_cast<long long*>(buf);
+  return true;
+#else
+  (void)buf;
+  return false;  // production builds carry no stamp variant
+#endif
+}
+int u8_stamp_slots() { return U8_NSTAMP; }
+
 void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
                  const float* bias, float scale, const U8HeadArgs& head, hipStream_t stream) {
   if (N != FBN || !head.dl || !head.mask || !head.part || !head.bound || !bias) abort();  // host contract
@@ -1191,6 +1279,40 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
   p.prio = knob(KNOB_U8_FWD_PRIO);
   const dim3 grid(u8_fwd_head_blocks(M), 1);
   const int tail = tail_substeps(K);
+#ifdef SDML_KERNEL_EXPERIMENTS  // timing variants (tools/u8_fwd_stamps.py): SDML_U8_FWD_MODE 1-6, 8-10
+  static const int fmode = [] {
+    const char* e = getenv("SDML_U8_FWD_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  if (head.C == 10 && fmode && fmode != 7 && !g_u8_stamps) {
+#define FHM(MD) hipLaunchKernelGGL((u8_fwd_kernel<MD, 2, NSUB, 4, 10>), grid, dim3(512), 0, stream, p)
+    switch (fmode) {
+      case 1: FHM(1); break;
+      case 2: FHM(2); break;
+      case 3: FHM(3); break;
+      case 4: FHM(4); break;
+      case 5: FHM(5); break;
+      case 8: FHM(8); break;
+      case 9: FHM(9); break;
+      case 10: FHM(10); break;
+      case 11: FHM(11); break;
+      default: abort();
+    }
+#undef FHM
+    return;
+  }
+  // MODE 7: phase stamps into the buffer set by u8_set_stamps
+  if (g_u8_stamps && head.C == 10) {
+    p.stamps = g_u8_stamps;
+    switch (tail) {
+      case 1: hipLaunchKernelGGL((u8_fwd_kernel<7, 2, 1, 4, 10>), grid, dim3(512), 0, stream, p); break;
+      case 2: hipLaunchKernelGGL((u8_fwd_kernel<7, 2, 2, 4, 10>), grid, dim3(512), 0, stream, p); break;
+      case 3: hipLaunchKernelGGL((u8_fwd_kernel<7, 2, 3, 4, 10>), grid, dim3(512), 0, stream, p); break;
+      default: hipLaunchKernelGGL((u8_fwd_kernel<7, 2, NSUB, 4, 10>), grid, dim3(512), 0, stream, p);
+    }
+    return;
+  }
+#endif
 #define FH_LAUNCH(T, CC) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC>), grid, dim3(512), 0, stream, p)
 #define FH_LAUNCH3(T) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, 10, 3>), grid, dim3(512), 0, stream, p)
 #define FH_TAILS(CC)                      \

@@ -144,16 +144,24 @@ constexpr int U8_NSTAMP = 24;
     }                                                                                                    \
   } while (0)
 
-// ---- fused classifier-head epilogue (HEADC > 0; NWR = 4, WMT = 2: 8 waves, 256 rows x 128 hidden per
-// block). LDS (floats): the block's h as 16 x-tile images of head_tile.h's xt_at layout [16][2048],
-// W2 zero-padded to 16 classes [16][FH_WSP], per-wave dz transposes [8][256], wave partials.
-constexpr int FH_ROWS = 256;
+// ---- fused classifier-head epilogue (HEADC > 0; WMT = 2, NWR = 4: 8 waves, 256 rows x 128 hidden per
+// block; NWR = 2: 4 waves, 128 rows - 80 KiB of LDS, so two blocks share a CU and one's head epilogue runs
+// beside the other's K loop). LDS (floats): the block's h as ROWS / 16 x-tile images of head_tile.h's xt_at
+// layout [ROWS / 16][2048], W2 zero-padded to 16 classes [16][FH_WSP], per-wave dz transposes [WAVES][256],
+// wave partials.
 constexpr int FH_WSP = 128 + 4;
-constexpr int FH_WS = FH_ROWS * 128;
-constexpr int FH_DZT = FH_WS + 16 * FH_WSP;
-constexpr int FH_RED = FH_DZT + 8 * 256;
-constexpr int FH_FLOATS = FH_RED + 8 * 18 + 8;
-static_assert(FH_FLOATS * 4 <= 160 * 1024, "LDS");
+template <int NWR>
+struct FhGeo {
+  static constexpr int WAVES = 2 * NWR;
+  static constexpr int ROWS = 64 * NWR;
+  static constexpr int TILES = ROWS / 16;  // 2 per wave
+  static constexpr int WS = ROWS * 128;
+  static constexpr int DZT = WS + 16 * FH_WSP;
+  static constexpr int RED = DZT + WAVES * 256;
+  static constexpr int FLOATS = RED + WAVES * 18 + WAVES;
+  static_assert(TILES == 2 * WAVES, "two row tiles per wave");
+};
+static_assert(FhGeo<4>::FLOATS * 4 <= 160 * 1024 && FhGeo<2>::FLOATS * 4 <= 80 * 1024, "LDS");
 
 // LDS images of one stage: X [BM rows][FBK bytes], W [NPL planes][128 rows][FBK fp16], chunks at
 // xpos / wpos. The DMA writes 1 KiB per wave-instruction lane-linearly (lane i -> bytes 16i..), so
@@ -195,7 +203,7 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
 // 2 = no DMA in the K loop (compute on stale LDS), 3 = no LDS reads (MFMA on register data)
 // TAIL = MFMA substeps of the last K-step (tail_substeps: only those holding k < K; chosen on the
 // host so the kernel carries one straight-line tail)
-template <int C>
+template <int C, int NWR>
 __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
                                                     int m0, int wave, int lane, int wm, int wn, long long* stamp);
 
@@ -204,12 +212,12 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
 // NSK: LDS ring stages. The fused-head variant may take 3 (the head epilogue needs 148 KiB anyway, so a third
 // 48 KiB stage costs no occupancy: two K-steps of pixel DMA in flight instead of one).
 template <int MODE, int WMT, int TAIL, int NWR, int HEADC = 0, int NSK = NS>
-__global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
+__global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(FwdParams p) {  // (4-wave blocks: 2 waves per SIMD, <= 256 VGPRs, two blocks per CU)
   constexpr int NS = NSK;  // (shadows the file-wide default inside this kernel)
   using G = Geo<WMT, NWR, NSK>;
-  static_assert(HEADC == 0 || (WMT == 2 && NWR == 4), "the fused head epilogue is written for 8 waves of 64 x 64");
+  static_assert(HEADC == 0 || (WMT == 2 && (NWR == 4 || NWR == 2)), "the fused head epilogue: waves of 64 x 64");
   constexpr int STAGE = G::STAGE, GLDS_PER_STAGE = G::GLDS_PER_STAGE;
-  constexpr int SMEM_BYTES = HEADC ? std::max(G::SMEM, FH_FLOATS * 4) : G::SMEM;
+  constexpr int SMEM_BYTES = HEADC ? std::max(G::SMEM, FhGeo<NWR>::FLOATS * 4) : G::SMEM;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
   const int m0 = blockIdx.x * G::BM, n0 = blockIdx.y * FBN;
   const int lane = threadIdx.x & 63;
@@ -378,7 +386,7 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
   }
 
   if constexpr (HEADC > 0) {
-    fused_head_epilogue<HEADC>(p, acc, smem, m0, wave, lane, wm, wn,
+    fused_head_epilogue<HEADC, NWR>(p, acc, smem, m0, wave, lane, wm, wn,
                                MODE == 7 ? p.stamps + ((size_t)blockIdx.x * G::WAVES + wave) * U8_NSTAMP : nullptr);
     U8_STAMP(22, __builtin_amdgcn_s_memtime);
     U8_STAMP(U8_NSTAMP - 1, __builtin_amdgcn_s_memrealtime);
@@ -443,9 +451,11 @@ __global__ void __launch_bounds__(128 * NWR) u8_fwd_kernel(FwdParams p) {
 //  2. every wave runs 2 of the block's 16 row tiles through head_tile.h (bit-identical dl to the
 //     standalone MFMA head on the same h); dW2^T, db2, loss, correct stay in registers
 //  3. wave partials meet in LDS in wave order -> one slab row + one |dl @ W2| bound per block
-template <int C>
+template <int C, int NWR>
 __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
                                                     int m0, int wave, int lane, int wm, int wn, long long* stamp) {
+  using FG = FhGeo<NWR>;
+  constexpr int NW = FG::WAVES, NT = 64 * NW;
   auto st = [&](int k) {  // MODE 7 only (stamp == nullptr otherwise, folded away)
     if (stamp && lane == 0) stamp[k] = (long long)__builtin_amdgcn_s_memtime();
   };
@@ -453,13 +463,13 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
   const U8HeadArgs& hd = p.head;
   float* F = reinterpret_cast<float*>(smem);
   float* himg = F;
-  float* ws = F + FH_WS;
-  float* dzt = F + FH_DZT + wave * 256;
-  float* red = F + FH_RED;  // [8][2 + 16] (loss, correct, db) then [8] dz bounds
+  float* ws = F + FG::WS;
+  float* dzt = F + FG::DZT + wave * 256;
+  float* red = F + FG::RED;  // [NW][2 + 16] (loss, correct, db) then [NW] dz bounds
   const int tid = threadIdx.x, h2 = lane >> 5, r32 = lane & 31;
   __syncthreads();  // every wave's last K-step reads are done: the stage buffers are free
   st(16);
-  for (int i = tid; i < 16 * 32; i += 512) {  // W2, zero-padded to 16 classes
+  for (int i = tid; i < 16 * 32; i += NT) {  // W2, zero-padded to 16 classes
     const int c = i >> 5, k4 = i & 31;
     *reinterpret_cast<f32x4m*>(ws + c * FH_WSP + 4 * k4) =
         c < C ? reinterpret_cast<const f32x4m*>(hd.w2)[c * 32 + k4] : f32x4m{0.f, 0.f, 0.f, 0.f};
@@ -501,10 +511,10 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
   a.zero();
   int tg[2];
 #pragma unroll
-  for (int it = 0; it < 2; ++it) tg[it] = (int)hd.target[min(m0 + 16 * (wave + 8 * it) + r, p.M - 1)];
+  for (int it = 0; it < 2; ++it) tg[it] = (int)hd.target[min(m0 + 16 * (wave + NW * it) + r, p.M - 1)];
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
-    const int T = wave + 8 * it, row = m0 + 16 * T + r;
+    const int T = wave + NW * it, row = m0 + 16 * T + r;
     const float* xw = himg + T * 2048;
     f32x4m xv[8];
 #pragma unroll
@@ -533,27 +543,28 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
   if (lane == 0) {
     red[wave * 18] = a.loss;
     red[wave * 18 + 1] = a.corr;
-    red[8 * 18 + wave] = a.amx;
+    red[NW * 18 + wave] = a.amx;
   }
   __syncthreads();
   float* slab = hd.part + (size_t)blockIdx.x * (C * 128 + C + 2);
-  auto sum8 = [&](auto at) {  // wave partials in wave order
-    return ((at(0) + at(1)) + (at(2) + at(3))) + ((at(4) + at(5)) + (at(6) + at(7)));
+  auto sumw = [&](auto at) {  // wave partials in wave order (pairwise tree)
+    if constexpr (NW == 8) return ((at(0) + at(1)) + (at(2) + at(3))) + ((at(4) + at(5)) + (at(6) + at(7)));
+    else return (at(0) + at(1)) + (at(2) + at(3));
   };
-  for (int o = tid; o < C * 128; o += 512) slab[o] = sum8([&](int w) { return F[w * (C * 128) + o]; });
-  if (tid < C) slab[C * 128 + tid] = sum8([&](int w) { return red[w * 18 + 2 + tid]; });
-  if (tid == 64) slab[C * 128 + C] = sum8([&](int w) { return red[w * 18]; });
-  if (tid == 128) slab[C * 128 + C + 1] = sum8([&](int w) { return red[w * 18 + 1]; });
-  if (wave == 7) {  // the |dl @ W2| bound: 2 max_row sum_c |dl_c| * max |W2| (head_xent.hip's formula)
+  for (int o = tid; o < C * 128; o += NT) slab[o] = sumw([&](int w) { return F[w * (C * 128) + o]; });
+  if (tid < C) slab[C * 128 + tid] = sumw([&](int w) { return red[w * 18 + 2 + tid]; });
+  if (tid == 64) slab[C * 128 + C] = sumw([&](int w) { return red[w * 18]; });
+  if (tid == 128) slab[C * 128 + C + 1] = sumw([&](int w) { return red[w * 18 + 1]; });
+  if (wave == NW - 1) {  // the |dl @ W2| bound: 2 max_row sum_c |dl_c| * max |W2| (head_xent.hip's formula)
     float wm2 = 0.f;
 #pragma unroll
     for (int u = 0; u < 8; ++u)
 #pragma unroll
       for (int e = 0; e < 4; ++e) wm2 = fmaxf(wm2, fabsf(wl[u][e]));
     for (int off = 32; off > 0; off >>= 1) wm2 = fmaxf(wm2, __shfl_xor(wm2, off));
-    float am = red[8 * 18];
+    float am = red[NW * 18];
 #pragma unroll
-    for (int w = 1; w < 8; ++w) am = fmaxf(am, red[8 * 18 + w]);
+    for (int w = 1; w < NW; ++w) am = fmaxf(am, red[NW * 18 + w]);
     if (lane == 0) hd.bound[blockIdx.x] = 2.f * am * wm2;
   }
   st(21);
@@ -1244,7 +1255,9 @@ bool u8_fwd_head_supported(int M, int N, int K, int ldx, const void* X, int C) {
   return u8_fwd_supported(M, N, K, ldx, X) && N == FBN && (C == 2 || C == 10 || C == 16);
 }
 
-int u8_fwd_head_blocks(int M) { return (M + FH_ROWS - 1) / FH_ROWS; }
+// rows per fused-head block: 256 (8 waves, one block per CU) or, with knob U8_FH_WAVES = 4, 128 (two per CU)
+static int fh_rows() { return knob(KNOB_U8_FH_WAVES) == 4 ? FhGeo<2>::ROWS : FhGeo<4>::ROWS; }
+int u8_fwd_head_blocks(int M) { return (M + fh_rows() - 1) / fh_rows(); }
 
 #ifdef SDML_KERNEL_EXPERIMENTS
 static long long* g_u8_stamps = nullptr;
@@ -1263,7 +1276,7 @@ int u8_stamp_slots() { return U8_NSTAMP; }
 void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
                  const float* bias, float scale, const U8HeadArgs& head, hipStream_t stream) {
   if (N != FBN || !head.dl || !head.mask || !head.part || !head.bound || !bias) abort();  // host contract
-  static_assert(Geo<2, 4>::BM == FH_ROWS, "one fused-head block = 256 rows");
+  static_assert(Geo<2, 4>::BM == FhGeo<4>::ROWS && Geo<2, 2>::BM == FhGeo<2>::ROWS, "one fused-head block = its rows");
   FwdParams p{};
   p.X = X;
   p.Wp = w_planes;
@@ -1324,6 +1337,27 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
       default: FH_LAUNCH(NSUB, CC);       \
     }                                     \
   } while (0)
+  if (fh_rows() == FhGeo<2>::ROWS) {  // 4-wave 128-row blocks, two per CU
+#define FH_LAUNCH4(T, CC) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 2, CC>), grid, dim3(256), 0, stream, p)
+#define FH_TAILS4(CC)                     \
+  do {                                    \
+    switch (tail) {                       \
+      case 1: FH_LAUNCH4(1, CC); break;   \
+      case 2: FH_LAUNCH4(2, CC); break;   \
+      case 3: FH_LAUNCH4(3, CC); break;   \
+      default: FH_LAUNCH4(NSUB, CC);      \
+    }                                     \
+  } while (0)
+    switch (head.C) {
+      case 10: FH_TAILS4(10); break;
+      case 2: FH_TAILS4(2); break;
+      case 16: FH_TAILS4(16); break;
+      default: abort();
+    }
+#undef FH_TAILS4
+#undef FH_LAUNCH4
+    return;
+  }
   if (head.C == 10 && knob(KNOB_U8_FH_STAGES) == 3) {  // 3-stage ring (the 784-128-10 MLP)
     switch (tail) {
       case 1: FH_LAUNCH3(1); break;

@@ -478,6 +478,8 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
   __shared__ float g1[NZ1];
   __shared__ float dsc[C2];
   __shared__ float hraw[HID], hd[HID], msk[HID], dh[HID], dl[NCLS];
+  __shared__ float fw2s[NCLS * HID], fb1s[HID], fb2s[NCLS];
+  __shared__ float dzp[TS / 64][FLAT];  // per-wave partials of W1^T dh (the wave's 4 fc1 rows)
   const int n = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   float* R = rec + (size_t)n * REC;
   STAMP(0);
@@ -498,11 +500,17 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
     for (int u = 0; u < NW2; ++u) w2v[u] = t + TS * u < C2 * C1 * KS * KS ? cw2[t + TS * u] : 0.f;
     const float xv = t < IMG * IMG ? xn[t] : 0.f;
     const float w1v = t < C1 * KS * KS ? cw1[t] : 0.f;
+    // stage 1's small operands too (fc2 weights, both biases): their phases then read LDS, not HBM
+    const float f2v = t < NCLS * HID ? fw2[t] : 0.f;
+    const float fbv = t < HID ? fb1[t] : (t >= 64 && t < 64 + NCLS ? fb2[t - 64] : 0.f);
 #pragma unroll
     for (int u = 0; u < NW2; ++u)
       if (t + TS * u < C2 * C1 * KS * KS) w2s[t + TS * u] = w2v[u];
     if (t < IMG * IMG) xs[t] = xv;
     if (t < C1 * KS * KS) w1s[t] = w1v;
+    if (t < NCLS * HID) fw2s[t] = f2v;
+    if (t < HID) fb1s[t] = fbv;
+    else if (t >= 64 && t < 64 + NCLS) fb2s[t - 64] = fbv;
   }
   for (int i = t; i < NZ1; i += TS) g1[i] = 0.f;
   if (t < C2) dsc[t] = drop0 ? keep_scale(eff_seed(seed0, ctr), n, t, p0) : 1.f;
@@ -606,7 +614,7 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
     for (int i = 0; i < 5; ++i) a += w1r[u][i] * z3[lane + 64 * i];
     for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
     if (lane == 0) {
-      const float h = fmaxf(fb1[j] + a, 0.f);
+      const float h = fmaxf(fb1s[j] + a, 0.f);
       const float ms = drop1 ? keep_scale(eff_seed(seed1, ctr), n, j, p1) : 1.f;
       hraw[j] = h;
       msk[j] = ms;
@@ -620,8 +628,8 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
   if (wv == 0) {
     float z = -INFINITY;
     if (lane < NCLS) {
-      float acc = fb2[lane];
-      for (int j = 0; j < HID; ++j) acc += fw2[lane * HID + j] * hd[j];
+      float acc = fb2s[lane];
+      for (int j = 0; j < HID; ++j) acc += fw2s[lane * HID + j] * hd[j];
       z = acc;
     }
     float mx = z;
@@ -646,7 +654,7 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
     if (lane < HID) {
       float dd = 0.f;
 #pragma unroll
-      for (int c = 0; c < NCLS; ++c) dd += fw2[c * HID + lane] * dl[c];
+      for (int c = 0; c < NCLS; ++c) dd += fw2s[c * HID + lane] * dl[c];
       const float v = hraw[lane] > 0.f ? dd * msk[lane] : 0.f;
       dh[lane] = v;
       R[R_DH + lane] = v;
@@ -654,11 +662,27 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
   }
   __syncthreads();
   STAMP(7);
-  // dz3 = W1^T dh, routed through relu (z3 > 0), pool argmax and the Dropout2d scale into G2
+  // dz3 = W1^T dh, routed through relu (z3 > 0), pool argmax and the Dropout2d scale into G2. Wave w holds fc1
+  // rows w + 16 u in registers (w1r, loaded for the forward): it writes its 4-row partial of every column, and
+  // column t sums the 16 wave partials in wave order (re-reading W1 column-wise from memory cost 50 loads per
+  // thread, 5 dependent L2 round trips)
+  {
+    float pz[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = wv + 16 * u;
+      const float dj = j < HID ? dh[j] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) pz[i] = __builtin_fmaf(w1r[u][i], dj, pz[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) dzp[wv][lane + 64 * i] = pz[i];
+  }
+  __syncthreads();
   if (t < FLAT) {
     float acc = 0.f;
-#pragma unroll 10
-    for (int j = 0; j < HID; ++j) acc += fw1[(size_t)j * FLAT + t] * dh[j];
+#pragma unroll
+    for (int w = 0; w < TS / 64; ++w) acc += dzp[w][t];
     const int c = t / (P2 * P2), py = (t / P2) % P2, px = t % P2, d = a2[t];
     c2[(c * O2 + 2 * py + (d >> 1)) * O2 + 2 * px + (d & 1)] = z3[t] > 0.f ? acc * dsc[c] : 0.f;
   }
@@ -763,17 +787,23 @@ __global__ void __launch_bounds__(TS) cnn_step_sample_kernel(const float* __rest
 // contribute, summed as 4 fixed quarters), the ReLU mask, dW1[ci], db1[ci]; db2 by the ci = 0 workgroup.
 // Fixed summation orders: deterministic. Inputs: x, W2, the forward's G2 / z1 / argmaxes (workspace bws).
 constexpr int TBW = 576;
-__global__ void __launch_bounds__(TBW) cnn_step_bwd_kernel(const float* __restrict__ x, const float* __restrict__ cw2,
-                                                           const float* __restrict__ bws, float* __restrict__ rec) {
+// the last phase: dW1 on threads 0..399, db1 on 400..415, dW2 on 416..515, db2 (ci == 0) on 520..559
+constexpr int DW2_T0 = 416, DB2_T0 = 520;
+__global__ void __launch_bounds__(TBW, 7) cnn_step_bwd_kernel(const float* __restrict__ x, const float* __restrict__ cw2,
+                                                           const float* __restrict__ bws, float* __restrict__ rec,
+                                                           long long* __restrict__ stamps) {
   __shared__ __attribute__((aligned(16))) float G2[C2 * O2 * O2];
   __shared__ float z1c[P1 * P1];
   __shared__ unsigned char a1c[P1 * P1];
   __shared__ unsigned char a2s[FLAT];
+  __shared__ float cellg[FLAT];        // G2 at each pooled cell's argmax (its one nonzero)
   __shared__ __attribute__((aligned(16))) float xs[IMG * IMG];
   __shared__ float w2c[C2 * KS * KS];  // W2[c][ci][ky][kx] of this ci
   __shared__ float gq[4][P1 * P1];     // dZ1 quarter sums (conv2 channels 5 q .. 5 q + 4)
   __shared__ float g1[P1 * P1];
   const int n = blockIdx.x / C1, ci = blockIdx.x % C1, t = threadIdx.x;
+  STAMP(0);
+  if (stamps && t == 0) stamps[(size_t)blockIdx.x * 16 + 14] = (long long)__builtin_amdgcn_s_memrealtime();
   const float* wsn = bws + (size_t)n * BWS;
   float* R = rec + (size_t)n * REC;
   // every global load of the workgroup is issued before the first LDS store (one latency, not one per loop
@@ -797,37 +827,25 @@ __global__ void __launch_bounds__(TBW) cnn_step_bwd_kernel(const float* __restri
     a1c[t] = a1v;
   }
   __syncthreads();
+  STAMP(1);
   // the conv2 pool argmax of every pooled cell: the one nonzero of G2 in it (G2 is zero elsewhere)
   for (int o = t; o < FLAT; o += TBW) {
     const int c = o / (P2 * P2), py = (o / P2) % P2, px = o % P2;
     int arg = 0;
+    float gv = 0.f;
 #pragma unroll
-    for (int d = 0; d < 4; ++d)
-      if (G2[(c * O2 + 2 * py + (d >> 1)) * O2 + 2 * px + (d & 1)] != 0.f) arg = d;
+    for (int d = 0; d < 4; ++d) {
+      const float v = G2[(c * O2 + 2 * py + (d >> 1)) * O2 + 2 * px + (d & 1)];
+      if (v != 0.f) {
+        arg = d;
+        gv = v;
+      }
+    }
     a2s[o] = (unsigned char)arg;
+    cellg[o] = gv;
   }
   __syncthreads();
-  if (t < C2 * KS) {
-    // dW2[c][ci][ky][:] from the 16 cells of channel c (their argmax entries; G2 is 0 at the other 48)
-    const int c = t / KS, ky = t % KS;
-    float acc[KS] = {0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int q = 0; q < P2 * P2; ++q) {
-      const int py = q / P2, px = q % P2, d = a2s[c * P2 * P2 + q];
-      const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
-      const float g = G2[(c * O2 + y) * O2 + xx];
-      const float* zr = z1c + (y + ky) * P1 + xx;
-#pragma unroll
-      for (int kx = 0; kx < KS; ++kx) acc[kx] += g * zr[kx];
-    }
-#pragma unroll
-    for (int kx = 0; kx < KS; ++kx) R[R_W2C + ((c * C1 + ci) * KS + ky) * KS + kx] = acc[kx];
-  } else if (ci == 0 && t >= 128 && t < 128 + C2) {
-    const int c = t - 128;
-    float acc = 0.f;
-    for (int i = 0; i < O2 * O2; ++i) acc += G2[c * O2 * O2 + i];
-    R[R_B2C + c] = acc;
-  }
+  STAMP(2);
   // dZ1[ci][Y][X] = sum_c sum_{ky,kx} G2[c][Y - ky][X - kx] W2[c][ci][ky][kx]: 4 channel quarters x 144 positions.
   // G2 has one nonzero per pooled cell (at its argmax), so the 5 x 5 window of (Y, X) meets at most 3 x 3
   // cells per channel: 45 candidate terms per thread instead of the dense 125 (fixed trip counts, predicated)
@@ -836,44 +854,102 @@ __global__ void __launch_bounds__(TBW) cnn_step_bwd_kernel(const float* __restri
     const int Y = pos / P1, X = pos % P1;
     const int py0 = max(Y - (KS - 1), 0) >> 1, px0 = max(X - (KS - 1), 0) >> 1;
     float acc = 0.f;
-    for (int c = 5 * q; c < 5 * q + 5; ++c)
+    // candidate cell k = (py, px) of the 3 x 3 around (Y, X): the cell's nonzero sits at (2 py + (d >> 1),
+    // 2 px + (d & 1)), d its argmax; tap (ky, kx) = (by - (d >> 1), bx - (d & 1)) with (by, bx) = (Y - 2 py,
+    // X - 2 px). Which d land inside the 5 x 5 window is fixed per candidate (a 4-bit mask), so per channel
+    // a candidate costs 3 LDS reads (argmax byte, the cell's G2 value, the W2 tap) and a select. The index
+    // math of the per-channel form was VALU-bound across the 27 waves a CU holds (13.8K of the block's 20K
+    // cycles); invalid candidates add an exact 0.
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 9; ++k) {
+      const int py = py0 + k / 3, px = px0 + k % 3;
+      const int by = Y - 2 * py, bx = X - 2 * px;
+      unsigned vm = 0u;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const int py = py0 + i, px = px0 + j;
-          if (py < P2 && px < P2) {
-            const int d = a2s[c * P2 * P2 + py * P2 + px];
-            const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
-            const int ky = Y - y, kx = X - xx;
-            if (ky >= 0 && ky < KS && kx >= 0 && kx < KS)
-              acc += G2[(c * O2 + y) * O2 + xx] * w2c[(c * KS + ky) * KS + kx];
-          }
-        }
+      for (int d = 0; d < 4; ++d) {
+        const int ky = by - (d >> 1), kx = bx - (d & 1);
+        vm |= (py < P2 && px < P2 && ky >= 0 && ky < KS && kx >= 0 && kx < KS) ? (1u << d) : 0u;
+      }
+      const int cell = min(py, P2 - 1) * P2 + min(px, P2 - 1);
+      const int wb = by * KS + bx;  // tap index of d = 0 (out of range for invalid candidates: clamped below)
+#pragma unroll
+      for (int c = 5 * q; c < 5 * q + 5; ++c) {
+        const int d = a2s[c * P2 * P2 + cell];
+        const float g = cellg[c * P2 * P2 + cell];
+        const float w = w2c[c * KS * KS + min(max(wb - (d >> 1) * KS - (d & 1), 0), KS * KS - 1)];
+        acc += ((vm >> d) & 1u) ? g * w : 0.f;
+      }
+    }
     gq[q][pos] = acc;
   }
   __syncthreads();
+  STAMP(3);
   if (t < P1 * P1) g1[t] = z1c[t] > 0.f ? (gq[0][t] + gq[1][t]) + (gq[2][t] + gq[3][t]) : 0.f;  // ReLU mask
   __syncthreads();
+  STAMP(4);
   // dW1[ci][ky][kx] = sum over the 144 pooled positions of g1 * x at the argmax tap: 16 lanes per weight
   // (positions p, p + 16, ...), then a fixed xor tree over the 16; db1 by the threads after them
   if (t < KS * KS * 16) {
     const int wi = t >> 4, prt = t & 15;
     const int ky = wi / KS, kx = wi % KS;
     float acc = 0.f;
-    for (int q = prt; q < P1 * P1; q += 16) {
+    float gv[9], xv9[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {  // (reads first, then the 9 FMAs in position order)
+      const int q = prt + 16 * k;
       const int py = q / P1, px = q % P1, d = a1c[q];
-      acc += g1[q] * xs[(2 * py + (d >> 1) + ky) * IMG + 2 * px + (d & 1) + kx];
+      gv[k] = g1[q];
+      xv9[k] = xs[(2 * py + (d >> 1) + ky) * IMG + 2 * px + (d & 1) + kx];
     }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc += gv[k] * xv9[k];
     acc += __shfl_xor(acc, 1);
     acc += __shfl_xor(acc, 2);
     acc += __shfl_xor(acc, 4);
     acc += __shfl_xor(acc, 8);
     if (prt == 0) R[R_W1C + ci * KS * KS + wi] = acc;
-  } else if (t == KS * KS * 16) {
+  } else if (t < KS * KS * 16 + 16) {  // db1: 16 lanes (9 positions each) and the same xor tree
+    const int prt = t & 15;
     float acc = 0.f;
-    for (int q = 0; q < P1 * P1; ++q) acc += g1[q];
-    R[R_B1C + ci] = acc;
+#pragma unroll
+    for (int q = prt; q < P1 * P1; q += 16) acc += g1[q];
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    acc += __shfl_xor(acc, 8);
+    if (prt == 0) R[R_B1C + ci] = acc;
+  } else if (t >= DW2_T0 && t < DW2_T0 + C2 * KS) {  // dW2 (moved here: beside dW1, not before dZ1)
+    // dW2[c][ci][ky][:] from the 16 cells of channel c (their argmax entries; G2 is 0 at the other 48)
+    const int c = (t - DW2_T0) / KS, ky = (t - DW2_T0) % KS;
+    float acc[KS] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    // all 16 argmax reads first, then every G2 / z1 read, then the FMAs in cell order (one LDS latency per
+    // step instead of one per cell)
+    int dq[P2 * P2];
+#pragma unroll
+    for (int q = 0; q < P2 * P2; ++q) dq[q] = a2s[c * P2 * P2 + q];
+#pragma unroll
+    for (int q = 0; q < P2 * P2; ++q) {
+      const int py = q / P2, px = q % P2, d = dq[q];
+      const int y = 2 * py + (d >> 1), xx = 2 * px + (d & 1);
+      const float g = G2[(c * O2 + y) * O2 + xx];
+      const float* zr = z1c + (y + ky) * P1 + xx;
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) acc[kx] += g * zr[kx];
+    }
+#pragma unroll
+    for (int kx = 0; kx < KS; ++kx) R[R_W2C + ((c * C1 + ci) * KS + ky) * KS + kx] = acc[kx];
+  } else if (ci == 0 && t >= DB2_T0 && t < DB2_T0 + 2 * C2) {  // db2: 2 lanes per channel (32 cells each)
+    const int c = (t - DB2_T0) >> 1, k = t & 1;
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < O2 * O2 / 2; ++i) acc += G2[c * O2 * O2 + k + 2 * i];
+    acc += __shfl_xor(acc, 1);
+    if (k == 0) R[R_B2C + c] = acc;
+  }
+  if (stamps) {
+    __syncthreads();
+    STAMP(5);
+    if (t == 0) stamps[(size_t)blockIdx.x * 16 + 15] = (long long)__builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -904,20 +980,43 @@ __device__ __forceinline__ void sgd_update1(float* pp, float* bp, float d, const
 // that other XCDs had just written (37 us at B = 60; 8-way unrolled, 14 us).
 constexpr int UP = 32, UG = 8;  // parameters and sample groups per block (256 threads)
 
+// (the loads are unconditional - past-the-end samples re-read sample B - 1 and are dropped by a select - so all
+// 8 (16) of them are in flight at once: with `if (s < B) acc += r[o]` hipcc put each load in its own branch with
+// a vmcnt(0) behind it, 8 serial round trips, 10.8 us at B = 60)
 template <bool PROD>
 __device__ __forceinline__ float group_sum(const float* __restrict__ rec, int B, int g, int o, int o2) {
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int s0 = g; s0 < B; s0 += UG * 8) {
+    float xa[8], xb[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int s = s0 + UG * u;
-      if (s < B) {
-        const float* r = rec + (size_t)s * REC;
-        acc[u] = PROD ? __builtin_fmaf(r[o], r[o2], acc[u]) : acc[u] + r[o];
-      }
+      const float* r = rec + (size_t)min(s0 + UG * u, B - 1) * REC;
+      xa[u] = r[o];
+      xb[u] = PROD ? r[o2] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float v = PROD ? __builtin_fmaf(xa[u], xb[u], acc[u]) : acc[u] + xa[u];
+      acc[u] = s0 + UG * u < B ? v : acc[u];
     }
   }
   return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
+// parameter tensor q's pointer without indexing the kernel-argument array by a per-thread value (that put the
+// array in scratch memory; a plain select chain became a vector load from the argument segment, one more
+// dependent round trip): the 8 pointers are pinned in SGPRs first, then selected per lane
+__device__ __forceinline__ float* pick8(float* const (&v)[8], int q) {
+  float* w[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    w[k] = v[k];
+    asm volatile("" : "+s"(w[k]));
+  }
+  float* r = w[0];
+#pragma unroll
+  for (int k = 1; k < 8; ++k) r = q == k ? w[k] : r;
+  return r;
 }
 
 __global__ void __launch_bounds__(256) cnn_step_update_kernel(const float* __restrict__ rec, int B, CnnParams a,
@@ -940,8 +1039,9 @@ __global__ void __launch_bounds__(256) cnn_step_update_kernel(const float* __res
         ee -= sizes[q];
         tt = q + 1;
       }
-    pv = a.p[tt][ee];
-    if (a.buf[tt] && !a.first) bv = a.buf[tt][ee];
+    pv = pick8(a.p, tt)[ee];
+    float* bq = pick8(a.buf, tt);
+    if (bq && !a.first) bv = bq[ee];
   }
   int ti = -1, e = i;
   float v = 0.f;
@@ -978,7 +1078,8 @@ __global__ void __launch_bounds__(256) cnn_step_update_kernel(const float* __res
   if (g == 0 && ti >= 0) {
     const float gr = ((part[0][j] + part[1][j]) + (part[2][j] + part[3][j])) +
                      ((part[4][j] + part[5][j]) + (part[6][j] + part[7][j]));
-    sgd_update1(a.p[ti] + e, a.buf[ti] ? a.buf[ti] + e : nullptr, gr, a, pv, bv);
+    float* bq = pick8(a.buf, ti);
+    sgd_update1(pick8(a.p, ti) + e, bq ? bq + e : nullptr, gr, a, pv, bv);
   }
   if (blockIdx.x == 0) {  // (loss sum, correct): 256 strided partials, then a fixed-order tree (deterministic).
     // (A serial loop over the B records on two threads was B dependent round trips to records other XCDs had
@@ -1051,11 +1152,16 @@ void ref_cnn_step(const float* x, const int64_t* target, int B, float* const* pa
                   float* rec, float* stats, hipStream_t stream, long long* stamps) {
   if (B <= 0) return;
   // B <= 128 (the reference's 60): stage 0's backward as its own launch over 10 workgroups per sample
-  float* bws = (B <= 128 && knob(KNOB_CNN_SPLIT_BWD) && !stamps) ? rec + (size_t)B * REC : nullptr;
+  // stamps (diagnostics, tools/probes): the sample kernel's phases on the unsplit path, or with knob CNN_SPLIT_BWD = 2
+  // the split backward kernel's ([B * 10][16] slots)
+  const int split = knob(KNOB_CNN_SPLIT_BWD);
+  float* bws = (B <= 128 && split && (!stamps || split == 2)) ? rec + (size_t)B * REC : nullptr;
   hipLaunchKernelGGL(cnn_step_sample_kernel, dim3(B), dim3(TS), 0, stream, x, target, params[0], params[1], params[2],
                      params[3], params[4], params[5], params[6], params[7], seed0, seed1, ctr, p0, drop0 ? 1 : 0, p1,
-                     drop1 ? 1 : 0, scale, rec, stamps, bws);
-  if (bws) hipLaunchKernelGGL(cnn_step_bwd_kernel, dim3(B * C1), dim3(TBW), 0, stream, x, params[2], bws, rec);
+                     drop1 ? 1 : 0, scale, rec, bws ? nullptr : stamps, bws);
+  if (bws)
+    hipLaunchKernelGGL(cnn_step_bwd_kernel, dim3(B * C1), dim3(TBW), 0, stream, x, params[2], bws, rec,
+                       split == 2 ? stamps : nullptr);
   CnnParams a;
   for (int i = 0; i < 8; ++i) {
     a.p[i] = params[i];

@@ -18,6 +18,9 @@ from simple_distributed_machine_learning_amd import ops  # noqa: E402
 from simple_distributed_machine_learning_amd._native import kernels  # noqa: E402
 
 K = kernels()
+from simple_distributed_machine_learning_amd import _native  # noqa: E402
+
+_native.apply_knobs_from_env()  # SDML_KNOBS="U8_FH_WAVES=4,..." (A/B)
 M, N, Kd, C = 131072, 128, 784, 10
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(5)
@@ -32,7 +35,7 @@ stats = torch.zeros(2, device=dev)
 dl = torch.empty(M, C, device=dev)
 mask = torch.empty(M, N // 32, dtype=torch.int32, device=dev)
 cache = ops.PlaneCache(w1)
-blocks = (M + 255) // 256
+blocks = K.u8_fwd_head_blocks(M) if hasattr(K, 'u8_fwd_head_blocks') else (M + 255) // 256
 S = K.u8_stamp_slots()
 stamps = torch.zeros(blocks * 8 * S, dtype=torch.int64, device=dev)
 

@@ -939,12 +939,20 @@ __global__ void __launch_bounds__(RD_OUT * RD_GRP) conv_wgrad_reduce_kernel(cons
     const int64_t i = base + o;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (i < n4)
-      for (int k = g; k < splits; k += RD_GRP) {
-        const float4 v = reinterpret_cast<const float4*>(slab + (size_t)k * n)[i];
-        acc.x += v.x;
-        acc.y += v.y;
-        acc.z += v.z;
-        acc.w += v.w;
+      // 4 splits per batch, loads unconditional (clamped split, the extra terms dropped by a select) so they
+      // are in flight together; the sum order is unchanged (k = g, g + RD_GRP, ... in sequence)
+      for (int k0 = g; k0 < splits; k0 += 4 * RD_GRP) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = reinterpret_cast<const float4*>(slab + (size_t)min(k0 + RD_GRP * u, splits - 1) * n)[i];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool in = k0 + RD_GRP * u < splits;  // (a select, not a branch: keeps the loads hoisted)
+          acc.x = in ? acc.x + v[u].x : acc.x;
+          acc.y = in ? acc.y + v[u].y : acc.y;
+          acc.z = in ? acc.z + v[u].z : acc.z;
+          acc.w = in ? acc.w + v[u].w : acc.w;
+        }
       }
     red[g][o] = acc;
     __syncthreads();
@@ -962,11 +970,11 @@ __global__ void __launch_bounds__(RD_OUT * RD_GRP) conv_wgrad_reduce_kernel(cons
       const int64_t r = e / C;
       const int tap = (int)(r % T), co = (int)(r / T);
       const float sv[4] = {t.x, t.y, t.z, t.w};
+      u16 old[4];  // the 4 reads first (before any store: the compiler cannot tell the addresses apart)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t dst = ((int64_t)co * C + ci + j) * T + tap;
-        gw[dst] = f2bf(bf2f(gw[dst]) + sv[j]);
-      }
+      for (int j = 0; j < 4; ++j) old[j] = gw[((int64_t)co * C + ci + j) * T + tap];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gw[((int64_t)co * C + ci + j) * T + tap] = f2bf(bf2f(old[j]) + sv[j]);
     }
     __syncthreads();
   }

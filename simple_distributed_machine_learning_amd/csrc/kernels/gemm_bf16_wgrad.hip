@@ -399,8 +399,15 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     const int m = ((int)blockIdx.x - main_blocks) * 16 + c;
     const float* bs = slab + (size_t)splits * MN;
     float s = 0.f;
+    const int nb = splits * bparts;
     if (m < M)
-      for (int k = g; k < splits * bparts; k += 16) s += bs[(size_t)k * M + m];
+      for (int k0 = g; k0 < nb; k0 += 64) {  // 4 per batch (clamped loads, in order)
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = bs[(size_t)min(k0 + 16 * u, nb - 1) * M + m];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s = k0 + 16 * u < nb ? s + v[u] : s;
+      }
     red[g][c] = s;
     __syncthreads();
     if (g == 0 && m < M) {
@@ -413,7 +420,14 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)main_blocks * 256) {
     f32x4 s = *reinterpret_cast<const f32x4*>(slab + 4 * i);
-    for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(slab + k * MN + 4 * i);
+    // 4 splits per batch with unconditional (clamped) loads, added in split order: one round trip per batch
+    for (int k0 = 1; k0 < splits; k0 += 4) {
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4*>(slab + (int64_t)min(k0 + u, splits - 1) * MN + 4 * i);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s = k0 + u < splits ? s + v[u] : s;  // (select: keeps the loads hoisted)
+    }
     const int64_t e = 4 * i;
     const int m = (int)(e / N), n = (int)(e % N);
     u16* dst = C + (size_t)m * ldc + n;

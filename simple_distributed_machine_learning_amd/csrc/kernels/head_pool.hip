@@ -241,12 +241,14 @@ __global__ void __launch_bounds__(64 * HP_RG) head_pool_reduce_kernel(const floa
   const int n = CK + C + 2;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (i < n) {
+    // loads unconditional (clamped block index, the extra terms dropped by a select): with `if (q < nblocks)`
+    // around each load hipcc waited out every load on its own (11 serial round trips, 11.8 us)
     for (int q0 = grp; q0 < nblocks; q0 += 8 * HP_RG) {
+      float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int q = q0 + HP_RG * u;
-        if (q < nblocks) acc[u] += part[(size_t)q * n + i];
-      }
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)min(q0 + HP_RG * u, nblocks - 1) * n + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] = q0 + HP_RG * u < nblocks ? acc[u] + v[u] : acc[u];
     }
   }
   red[grp][l] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));

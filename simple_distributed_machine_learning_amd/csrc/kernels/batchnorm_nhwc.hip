@@ -47,40 +47,59 @@ __global__ void __launch_bounds__(BT) bn_partial_kernel(const u16* __restrict__ 
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
   float mu[8], rs[8], sc[8], sh[8];
-  if (BWD) {
+  if (BWD) {  // (16-B loads, all issued before the first use)
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const f32x4 m0 = reinterpret_cast<const f32x4*>(mean + 8 * cg)[0], m1 = reinterpret_cast<const f32x4*>(mean + 8 * cg)[1];
+    const f32x4 q0 = reinterpret_cast<const f32x4*>(rstd + 8 * cg)[0], q1 = reinterpret_cast<const f32x4*>(rstd + 8 * cg)[1];
+    u16x8 gm = {0, 0, 0, 0, 0, 0, 0, 0}, bt = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (relu == 2) {  // (uniform)
+      gm = *reinterpret_cast<const u16x8*>(gamma + 8 * cg);
+      bt = *reinterpret_cast<const u16x8*>(beta + 8 * cg);
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      mu[e] = mean[8 * cg + e];
-      rs[e] = rstd[8 * cg + e];
-      if (relu == 2) {
-        sc[e] = bf2f(gamma[8 * cg + e]) * rs[e];
-        sh[e] = bf2f(beta[8 * cg + e]) - mu[e] * sc[e];
-      }
+      mu[e] = e < 4 ? m0[e & 3] : m1[e & 3];
+      rs[e] = e < 4 ? q0[e & 3] : q1[e & 3];
+      sc[e] = bf2f(gm[e]) * rs[e];
+      sh[e] = bf2f(bt[e]) - mu[e] * sc[e];
     }
   }
   const int r0 = blockIdx.x * rpb, r1 = min(M, r0 + rpb);
   if (rl < lanes) {
-    for (int r = r0 + rl; r < r1; r += lanes) {
-      const size_t o = (size_t)r * C + 8 * cg;
-      const u16x8 xv = *reinterpret_cast<const u16x8*>(x + o);
-      if (!BWD) {
+    // RU rows per round, all their loads issued before the first use (clamped row, the extra rows dropped by a
+    // select): a round is one memory latency, not RU. Rows are still added in order. (One row per round waited out
+    // ~25 dependent round trips per thread at C = 64, M = 401K: ~19 us per call.)
+    constexpr int RU = 4;
+    for (int rb = r0 + rl; rb < r1; rb += RU * lanes) {
+      u16x8 xv[RU], gv[RU], yv[RU];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float v = bf2f(xv[e]);
-          s1[e] += v;
-          s2[e] += v * v;
+      for (int u = 0; u < RU; ++u) {
+        const size_t o = (size_t)min(rb + u * lanes, r1 - 1) * C + 8 * cg;
+        xv[u] = *reinterpret_cast<const u16x8*>(x + o);
+        if (BWD) {
+          gv[u] = *reinterpret_cast<const u16x8*>(dy + o);
+          yv[u] = relu == 1 ? *reinterpret_cast<const u16x8*>(y + o) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
-      } else {
-        const u16x8 gv = *reinterpret_cast<const u16x8*>(dy + o);
-        u16x8 yv = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (relu == 1) yv = *reinterpret_cast<const u16x8*>(y + o);
+      }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float g = bf2f(gv[e]);
-          if (relu == 1 && !(bf2f(yv[e]) > 0.f)) g = 0.f;
-          if (relu == 2 && !(fmaf(bf2f(xv[e]), sc[e], sh[e]) > 0.f)) g = 0.f;
-          s1[e] += g;
-          s2[e] += g * (bf2f(xv[e]) - mu[e]) * rs[e];
+      for (int u = 0; u < RU; ++u) {
+        const bool in = rb + u * lanes < r1;
+        if (!BWD) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = bf2f(xv[u][e]);
+            s1[e] = in ? s1[e] + v : s1[e];
+            s2[e] = in ? s2[e] + v * v : s2[e];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float g = bf2f(gv[u][e]);
+            if (relu == 1 && !(bf2f(yv[u][e]) > 0.f)) g = 0.f;
+            if (relu == 2 && !(fmaf(bf2f(xv[u][e]), sc[e], sh[e]) > 0.f)) g = 0.f;
+            s1[e] = in ? s1[e] + g : s1[e];
+            s2[e] = in ? s2[e] + g * (bf2f(xv[u][e]) - mu[e]) * rs[e] : s2[e];
+          }
         }
       }
     }

@@ -22,6 +22,15 @@ __device__ __forceinline__ void head_reduce_block(const HeadReduceArgs& a, int b
   const int width = a.CK + a.C + 2;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int o = bx * 64 + lane;
+  // the fused step's epilogue operands (gW / gb, the head parameters and momentum), loaded with the slabs
+  const int o4p = bx * 64 + 4 * lane;
+  const bool pre = sg && sg->hp && (a.flags & 1) && w == 0 && lane < 16 && o4p + 4 <= a.CK + a.C;
+  sgd_f32x4 g0 = {0.f, 0.f, 0.f, 0.f}, p0 = {0.f, 0.f, 0.f, 0.f}, b0 = {0.f, 0.f, 0.f, 0.f};
+  if (pre) {
+    g0 = *reinterpret_cast<const sgd_f32x4*>(a.gW + o4p);
+    p0 = *reinterpret_cast<const sgd_f32x4*>(sg->hp + o4p);
+    if (sg->mom != 0.f && !sg->first) b0 = *reinterpret_cast<const sgd_f32x4*>(sg->hbuf + o4p);
+  }
   float s = 0.f;
   if (o < width) {  // 16 loads in flight per lane (512 slabs: two round trips per wave)
     float v[16];
@@ -50,12 +59,15 @@ __device__ __forceinline__ void head_reduce_block(const HeadReduceArgs& a, int b
       const int n4 = min(4, a.CK + a.C - o4);  // the last group may hold the 2 stats or padding
       float* gp = a.gW + o4;
       sgd_f32x4 d;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) d[j] = j < n4 ? gp[j] + acc[0][4 * lane + j] : 0.f;
       if (n4 == 4) {
-        sgd_update4(sg->hp + o4, sg->hbuf + o4, d, SgdRule{sg->lr, sg->mom, sg->damp, sg->wd, sg->nesterov, sg->first});
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = g0[j] + acc[0][4 * lane + j];
+        sgd_update4_pre(sg->hp + o4, sg->hbuf + o4, d, SgdRule{sg->lr, sg->mom, sg->damp, sg->wd, sg->nesterov, sg->first},
+                        p0, b0);
         *reinterpret_cast<sgd_f32x4*>(gp) = sg->zero_grad ? sgd_f32x4{0.f, 0.f, 0.f, 0.f} : d;
       } else {  // ragged tail (CK + C not a multiple of 4): the padding after gb is zero in every buffer
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = j < n4 ? gp[j] + acc[0][4 * lane + j] : 0.f;
         sgd_f32x4 pt, bt;  // 16-B aligned locals (hbuf is null without momentum: the rule then never reads it)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {

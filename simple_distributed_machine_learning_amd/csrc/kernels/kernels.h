@@ -152,6 +152,8 @@ int u8_fwd_head_blocks(int M);
 // int64; nullptr turns them off); production builds return false and ignore it
 bool u8_set_stamps(void* buf);
 int u8_stamp_slots();
+// experiments builds: weight-gradient phase stamps ([blocks][8][16] int64; nullptr off)
+bool u8_set_wgrad_stamps(void* buf);
 void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
                  const float* bias, float scale, const U8HeadArgs& head, hipStream_t stream);
 // mlp_u8.hip: weight + bias gradient of the uint8-fed first layer (K = 784 pixel columns, N % 64 == 0,

@@ -40,6 +40,7 @@ const Entry kTable[KNOB_COUNT] = {
     {"U8_WGRAD_PRIO", 0, false, nullptr},
     {"CNN_SPLIT_BWD", 1, false, nullptr},
     {"U8_FH_WAVES", 8, false, nullptr},
+    {"U8_WGRAD_ILV", 0, false, nullptr},
     {"GEMM_BF16_NOSTORE", 0, true, nullptr},
     {"U8_VARIANT", 0, true, nullptr},
 };

@@ -137,6 +137,10 @@ struct FwdParams {
 // MODE 7 diagnostic stamps (tools/probes/u8_fwd_stamps.py): lane 0 of every wave writes s_memtime after each
 // phase (vector stores into a buffer nothing else reads); slots 0 / U8_NSTAMP - 1 hold s_memrealtime
 constexpr int U8_NSTAMP = 24;
+#ifdef SDML_KERNEL_EXPERIMENTS
+long long* g_u8_stamps = nullptr;   // u8_set_stamps: the fused forward's MODE 7 buffer
+long long* g_u8w_stamps = nullptr;  // u8_set_wgrad_stamps: the weight gradient's phase stamps
+#endif
 #define U8_STAMP(k, fn)                                                                                  \
   do {                                                                                                   \
     if constexpr (MODE == 7) {                                                                           \
@@ -723,7 +727,21 @@ struct WgradParams {
   int g0;                    // first hidden group launched (hidden units GHN g0 ..)
   int xcd;                   // 0: plain order (split-major), A/B only (SDML_U8_WGRAD_XCD=0)
   int prio;                  // 1: s_setprio 1 on waves 4..7 (knob U8_WGRAD_PRIO)
+  long long* stamps;         // experiments builds only: [blocks][8 waves][16] phase stamps (u8_set_wgrad_stamps)
 };
+
+// experiments builds: s_memtime stamps of the weight gradient's phases (tools/u8_wgrad_stamps.py); slot 0 / 15 hold
+// s_memrealtime at start / end
+#ifdef SDML_KERNEL_EXPERIMENTS
+#define U8W_STAMP(k, fn)                                                                               \
+  do {                                                                                                 \
+    if (p.stamps && lane == 0) p.stamps[((size_t)blockIdx.x * 8 + wave) * 16 + (k)] = (long long)fn(); \
+  } while (0)
+#else
+#define U8W_STAMP(k, fn) \
+  do {                   \
+  } while (0)
+#endif
 
 // dx tile of head_xent.hip's MFMA head (dx_t / head_mfma_dx_from_dl_kernel), reproduced operation
 // for operation: lane (r, g) of a 16-row tile gets dz[row r][16 t + 4 g + v] =
@@ -750,7 +768,11 @@ __device__ __forceinline__ f32x4 fd_dz_bits(const float (&w4)[4], const float (&
 // is expanded here instead of by a separate kernel that writes dz to memory and reads it back -
 // with head_xent.hip's exact operations, so gW / gb are bit-identical to the unfused pair; the ReLU
 // mask comes from h (FD = 1, 16 B per thread and K-step) or from its bits (FD = 2, 4 B).
-template <int FD>
+// ILV: the K-step body carries an explicit instruction interleave (sched_group_barrier): the fragment reads of a
+// substep, then its MFMAs each followed by 3 of the staging VALU instructions, so the next K-step's staging runs in
+// the MFMA shadows of this one's (without it the compiler emitted compute, then staging, then the barrier: ~3.9K
+// cycles per K-step against ~1.8K of MFMA, stamps in profiles/r4_u8_wgrad_stamps.json)
+template <int FD, bool ILV = false>
 __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) u16 smem[2 * GBUF_U16];
   const int t = threadIdx.x, lane = t & 63;
@@ -762,6 +784,8 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   const int L = blockIdx.x, G8 = 8 * p.groups;
   const int split = p.xcd ? (L / G8) * 8 + L % 8 : L / p.groups;
   if (split >= p.splits) return;
+  U8W_STAMP(0, __builtin_amdgcn_s_memrealtime);
+  U8W_STAMP(1, __builtin_amdgcn_s_memtime);
   const int n0 = (p.g0 + (p.xcd ? (L % G8) / 8 : L % p.groups)) * GHN;
   const int r0 = split * p.rows_per_split;
   const int nk = min(p.rows_per_split, p.M - r0) / GBK;  // host: M % GBK == 0
@@ -833,6 +857,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     dz_up = pow2f(14 - E);
     out_scale = p.scale * pow2f(E - 14);
   }
+  U8W_STAMP(2, __builtin_amdgcn_s_memtime);
   constexpr int XU = (GXCH + GT - 1) / GT;  // 4 rounds
   const unsigned char* xp[XU];
   int xoff[XU];
@@ -922,12 +947,33 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     stage(0);
     if (nk > 1) gload(1);
     __syncthreads();
+    U8W_STAMP(3, __builtin_amdgcn_s_memtime);
     int kt = 0;
+    auto interleave = [&]() {
+      if constexpr (ILV) {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 8 + 2 * NCT, 0);  // this substep's fragment reads
+#pragma unroll
+          for (int m = 0; m < 4 * NCT; ++m) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // three staging VALU
+          }
+        }
+      }
+    };
     for (; kt + 2 < nk; ++kt) {
       compute(kt & 1);
+#ifdef SDML_KERNEL_EXPERIMENTS
+      if (kt == 0 || kt == 8 || kt == 16) U8W_STAMP(4 + kt / 8 * 2, __builtin_amdgcn_s_memtime);  // after compute
+#endif
       stage((kt + 1) & 1);
       gload(kt + 2);
+      interleave();
       __syncthreads();
+#ifdef SDML_KERNEL_EXPERIMENTS
+      if (kt == 0 || kt == 8 || kt == 16) U8W_STAMP(5 + kt / 8 * 2, __builtin_amdgcn_s_memtime);  // after barrier
+#endif
     }
     if (kt + 1 < nk) {
       compute(kt & 1);
@@ -936,6 +982,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
       ++kt;
     }
     compute(kt & 1);
+    U8W_STAMP(10, __builtin_amdgcn_s_memtime);
 
     // partial tile -> slab (plain stores); C map: column = lane & 31, row = (r&3) + 8(r>>2) + 4h
     float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
@@ -951,6 +998,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
           out[(size_t)n * GKC + col] = acc[i][j][r] * out_scale;
         }
     }
+    U8W_STAMP(11, __builtin_amdgcn_s_memtime);
   };
   if (nk > 0) {
     if (wave == 0) run(std::integral_constant<int, 4>{});
@@ -970,6 +1018,8 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     }
     out[(size_t)p.N * GKC + n0 + t] = sacc;
   }
+  U8W_STAMP(12, __builtin_amdgcn_s_memtime);
+  U8W_STAMP(15, __builtin_amdgcn_s_memrealtime);
 }
 
 // The step's two deterministic reductions in one launch: blocks [0, nslab) sum the weight
@@ -998,6 +1048,16 @@ __global__ void __launch_bounds__(1024) slab_head_reduce_kernel(const float* __r
   const bool segA = (int)blockIdx.x < sgs.nA;
   const int64_t i = (segA ? sgs.a_off : sgs.b_off) + ((int64_t)(segA ? blockIdx.x : blockIdx.x - sgs.nA) * 64 + l) * 4;
   const int64_t n = segA ? sgs.a_end : sgs.b_end;
+  // wave 0's epilogue operands (the gradient it adds into, the parameter, its momentum) are loaded first, with the
+  // partials: one memory round trip for all of them instead of two more after the sum
+  f32x4 acc0 = {}, pv0 = {}, bv0 = {};
+  if (w == 0 && i < n) {
+    acc0 = *reinterpret_cast<const f32x4*>(out + i);
+    if (sg.p) {
+      pv0 = *reinterpret_cast<const f32x4*>(sg.p + i);
+      if (sg.mom != 0.f && !sg.first) bv0 = *reinterpret_cast<const f32x4*>(sg.buf + i);
+    }
+  }
   f32x4 a[4] = {};
   if (i < n) {
     int s = w;  // wave w: splits w, w + 16, ...
@@ -1010,13 +1070,14 @@ __global__ void __launch_bounds__(1024) slab_head_reduce_kernel(const float* __r
   part[w][l] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
   if (w == 0 && i < n) {
-    f32x4 acc = *reinterpret_cast<const f32x4*>(out + i);
+    f32x4 acc = acc0;
     f32x4 t = part[0][l];
 #pragma unroll
     for (int q = 1; q < 16; ++q) t += part[q][l];
     acc += t;
     if (sg.p) {
-      const f32x4 nv = sgd_update4(sg.p + i, sg.buf + i, acc, SgdRule{sg.lr, sg.mom, sg.damp, sg.wd, sg.nesterov, sg.first});
+      const f32x4 nv = sgd_update4_pre(sg.p + i, sg.buf + i, acc, SgdRule{sg.lr, sg.mom, sg.damp, sg.wd, sg.nesterov, sg.first},
+                                       pv0, bv0);
       const int64_t i4 = i / 4;
       if (sg.planes && i4 >= sg.pl_off4 && i4 < sg.pl_off4 + sg.pl_n4) {
         const int64_t e = i - 4 * sg.pl_off4;
@@ -1132,9 +1193,15 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigne
   p.splits = splits;
   p.xcd = wgrad_xcd();
   p.prio = knob(KNOB_U8_WGRAD_PRIO);
+#ifdef SDML_KERNEL_EXPERIMENTS
+  p.stamps = g_u8w_stamps;
+#endif
   const dim3 wgrid(((splits + 7) / 8) * 8 * p.groups);
-  if (mask) hipLaunchKernelGGL(u8_wgrad_kernel<2>, wgrid, dim3(GT), 0, stream, p);
-  else hipLaunchKernelGGL(u8_wgrad_kernel<1>, wgrid, dim3(GT), 0, stream, p);
+  const bool ilv = knob(KNOB_U8_WGRAD_ILV) != 0;
+  if (mask && ilv) hipLaunchKernelGGL((u8_wgrad_kernel<2, true>), wgrid, dim3(GT), 0, stream, p);
+  else if (mask) hipLaunchKernelGGL((u8_wgrad_kernel<2, false>), wgrid, dim3(GT), 0, stream, p);
+  else if (ilv) hipLaunchKernelGGL((u8_wgrad_kernel<1, true>), wgrid, dim3(GT), 0, stream, p);
+  else hipLaunchKernelGGL((u8_wgrad_kernel<1, false>), wgrid, dim3(GT), 0, stream, p);
   const int64_t n = (int64_t)N * GKC + N;
   if (grp) {  // this hidden-group range only: its weight rows, then its bias entries (+ the head's reduction)
     if (sgd && sgd->p) abort();  // host contract: the split weight gradient is not the fused optimizer step
@@ -1259,9 +1326,7 @@ bool u8_fwd_head_supported(int M, int N, int K, int ldx, const void* X, int C) {
 static int fh_rows() { return knob(KNOB_U8_FH_WAVES) == 4 ? FhGeo<2>::ROWS : FhGeo<4>::ROWS; }
 int u8_fwd_head_blocks(int M) { return (M + fh_rows() - 1) / fh_rows(); }
 
-#ifdef SDML_KERNEL_EXPERIMENTS
-static long long* g_u8_stamps = nullptr;
-#endif
+
 bool u8_set_stamps(void* buf) {
 #ifdef SDML_KERNEL_EXPERIMENTS
   g_u8_stamps = static_cast<long long*>(buf);
@@ -1272,6 +1337,15 @@ bool u8_set_stamps(void* buf) {
 #endif
 }
 int u8_stamp_slots() { return U8_NSTAMP; }
+bool u8_set_wgrad_stamps(void* buf) {
+#ifdef SDML_KERNEL_EXPERIMENTS
+  g_u8w_stamps = static_cast<long long*>(buf);
+  return true;
+#else
+  (void)buf;
+  return false;
+#endif
+}
 
 void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
                  const float* bias, float scale, const U8HeadArgs& head, hipStream_t stream) {

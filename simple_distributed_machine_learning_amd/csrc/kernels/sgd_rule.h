@@ -22,9 +22,11 @@ struct SgdRule {
 // Every multiply-add is an explicit fma and contraction is off, so each kernel that inlines this rule
 // (the SGD kernel, the reductions that apply the step themselves) produces the same bits: left to the
 // compiler, "mom * b + (1 - damp) * d" may be fused around either product depending on the context.
-__device__ __forceinline__ sgd_f32x4 sgd_update4(float* p4, float* buf4, sgd_f32x4 d, const SgdRule& r) {
+// pv / bv0: the parameter and momentum values, loaded by the caller (ahead of its other loads: one memory round trip
+// instead of a dependent one after the gradient sum); bv0 is read only with momentum and !first
+__device__ __forceinline__ sgd_f32x4 sgd_update4_pre(float* p4, float* buf4, sgd_f32x4 d, const SgdRule& r,
+                                                    const sgd_f32x4 pv, const sgd_f32x4 bv0) {
 #pragma clang fp contract(off)
-  const sgd_f32x4 pv = *reinterpret_cast<const sgd_f32x4*>(p4);
   if (r.wd != 0.f) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) d[j] = __builtin_fmaf(r.wd, pv[j], d[j]);
@@ -34,7 +36,7 @@ __device__ __forceinline__ sgd_f32x4 sgd_update4(float* p4, float* buf4, sgd_f32
     if (r.first) {
       b = d;
     } else {
-      b = *reinterpret_cast<const sgd_f32x4*>(buf4);
+      b = bv0;
       const float keep = 1.f - r.damp;
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = __builtin_fmaf(r.mom, b[j], keep * d[j]);
@@ -55,6 +57,12 @@ __device__ __forceinline__ sgd_f32x4 sgd_update4(float* p4, float* buf4, sgd_f32
 }
 
 // the uint8 forward's fp16 weight planes of 4 updated weights at plane element q (u8_planes.h)
+__device__ __forceinline__ sgd_f32x4 sgd_update4(float* p4, float* buf4, sgd_f32x4 d, const SgdRule& r) {
+  const sgd_f32x4 pv = *reinterpret_cast<const sgd_f32x4*>(p4);
+  const sgd_f32x4 bv = (r.mom != 0.f && !r.first) ? *reinterpret_cast<const sgd_f32x4*>(buf4) : sgd_f32x4{0.f, 0.f, 0.f, 0.f};
+  return sgd_update4_pre(p4, buf4, d, r, pv, bv);
+}
+
 __device__ __forceinline__ void sgd_write_planes4(unsigned short* q, int64_t plane_stride, sgd_f32x4 nv) {
   sgd_u16x4 h, l;
 #pragma unroll

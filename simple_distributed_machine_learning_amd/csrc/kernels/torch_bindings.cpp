@@ -1711,6 +1711,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       },
       "experiments builds: phase stamps of the fused uint8 forward + head (tools/probes/u8_fwd_stamps.py)");
   m.def("u8_stamp_slots", &sdml::u8_stamp_slots, "stamps per (block, wave) of u8_set_stamps");
+  m.def(
+      "u8_set_wgrad_stamps",
+      [](c10::optional<torch::Tensor> buf) {
+        if (!buf) return sdml::u8_set_wgrad_stamps(nullptr);
+        TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == torch::kInt64 && buf->is_contiguous(),
+                    "u8_set_wgrad_stamps: contiguous int64 device tensor");
+        return sdml::u8_set_wgrad_stamps(buf->data_ptr());
+      },
+      "experiments builds: phase stamps of the uint8 weight gradient (tools/u8_wgrad_stamps.py)");
   m.def("u8_fwd_head_supported", &u8_fwd_head_supported_op, "shape check for linear_relu_head_u8 (M, N, K, C)");
   m.def("relu_bits", &relu_bits, "int32 [M, N/32] ReLU bits of y (the uint8 kernels' mask layout)");
   m.def("gemm_bf16", &gemm_bf16_op, "bf16 GEMM with fused bias / bias+GELU / GELU-backward epilogues",

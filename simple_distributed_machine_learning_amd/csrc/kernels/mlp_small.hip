@@ -85,7 +85,17 @@ __global__ void __launch_bounds__(ST) mlp_small_fwd_kernel(SmallArgs a) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int j0 = 2 * blockIdx.x;
   const int B = a.B;
-  for (int i = t; i < 2 * SK; i += ST) w1s[i / SK][i % SK] = a.w1[(size_t)(j0 + i / SK) * SK + i % SK];
+  {  // (both loads per thread issued before the stores)
+    float wv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = min(t + ST * u, 2 * SK - 1);
+      wv[u] = a.w1[(size_t)(j0 + i / SK) * SK + i % SK];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (t + ST * u < 2 * SK) w1s[(t + ST * u) / SK][(t + ST * u) % SK] = wv[u];
+  }
   const float bj0 = a.b1[j0], bj1 = a.b1[j0 + 1];
   // snapshot of W2 / b2 for kernel B: its blocks update W2's columns (and block 0 b2) while other blocks
   // may still be starting, so they read the values of this step from here (stream order: A before B)
@@ -125,9 +135,27 @@ __global__ void __launch_bounds__(ST) mlp_small_bwd_kernel(SmallArgs a) {
   const int t = threadIdx.x;
   const int j0 = 2 * blockIdx.x;
   const int B = a.B;
-  for (int i = t; i < SC * SH; i += ST) w2s[i / SH][i % SH] = a.snap[i];
-  if (t < SC) b2s[t] = a.snap[SC * SH + t];
-  for (int i = t; i < B * SH; i += ST) hs[i / SH][i % SH] = a.h[i];
+  // staging: 8 loads per thread in flight per round (clamped index, stored only when in range); a plain
+  // strided copy loop waited out each load before the next (8 serial round trips for h at B = 60)
+  {
+    float wv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) wv[u] = a.snap[min(t + ST * u, SC * SH - 1)];
+    const float bv = t < SC ? a.snap[SC * SH + t] : 0.f;
+    const int n = B * SH;
+    for (int i0 = t; i0 < n; i0 += 8 * ST) {
+      float hv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) hv[u] = a.h[min(i0 + ST * u, n - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + ST * u < n) hs[(i0 + ST * u) / SH][(i0 + ST * u) % SH] = hv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (t + ST * u < SC * SH) w2s[(t + ST * u) / SH][(t + ST * u) % SH] = wv[u];
+    if (t < SC) b2s[t] = bv;
+  }
   __syncthreads();
   // logits: one (row, class) dot product of length 128 per thread (no cross-lane reductions on the
   // critical path), then one thread per row: log_softmax, NLL, argmax, dl

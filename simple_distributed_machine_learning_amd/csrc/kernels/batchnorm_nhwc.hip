@@ -126,9 +126,22 @@ __device__ __forceinline__ void wave_sum2(const float* __restrict__ part, int nb
   const int lane = threadIdx.x & 63;
   s1 = 0.0;
   s2 = 0.0;
-  for (int b = lane; b < nblk; b += 64) {
-    s1 += part[(size_t)b * 2 * C + c];
-    s2 += part[(size_t)b * 2 * C + C + c];
+  // 4 partials per lane per round, loads unconditional (clamped) and added in block order: one memory latency per
+  // round (the one-at-a-time loop waited ~25 round trips at 1568 conv tiles)
+  for (int b0 = lane; b0 < nblk; b0 += 4 * 64) {
+    float v1[4], v2[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int b = min(b0 + 64 * u, nblk - 1);
+      v1[u] = part[(size_t)b * 2 * C + c];
+      v2[u] = part[(size_t)b * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool in = b0 + 64 * u < nblk;
+      s1 = in ? s1 + v1[u] : s1;
+      s2 = in ? s2 + v2[u] : s2;
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {

@@ -34,6 +34,7 @@
 
 #include "gelu.h"
 #include "kernels.h"
+#include "lds_dma.h"
 
 namespace sdml {
 namespace {
@@ -111,10 +112,11 @@ __device__ __forceinline__ s16x4 ds_tr16(const unsigned char* p) {
 }
 
 // epilogue shared by both main loops: bf16 rows through the (free) stage buffers, 16-B row pieces to HBM
-template <int EPI>
+// WNW: waves along N (4: the 256 x 256 tile's 2 x 4 waves; 2: the 256 x 128 tile's 2 x 2)
+template <int EPI, int WNW = 4>
 __device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&acc)[8][4], unsigned char* smem, int m0,
                                                    int n0, int wave, int lane) {
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WNW, wn = wave % WNW;
   const int g = lane >> 4, l16 = lane & 15;
   // wave image [128 rows][64 cols] bf16 (128 B rows, 16-B chunks swizzled like the A image)
   unsigned char* W = smem + wave * (128 * 128);
@@ -412,12 +414,112 @@ __global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
   gemm_bf16_epilogue<EPI>(p, acc, smem, m0, n0, wave, lane);
 }
 
+// ---- NT form, 256 x 128 tiles of 4 waves, two workgroups per CU ---------------------------------------
+// The 256 x 256 kernels above take all 160 KiB of LDS, so one workgroup runs per CU and every CU reaches its
+// epilogue (the bf16 stores of its tile) at the same moment, with no main loop left to hide them under
+// (docs/TUNING_NOTES.md: the stores were never overlapped). Here a workgroup is 4 waves (2 x 2, each 128 x 64, the
+// same 8 x 4 accumulators) on a 256 x 128 tile, 32-deep K-steps in a 3-stage ring of 24 KiB (72 KiB in all, the
+// epilogue's 64 KiB of row images fit in it), and __launch_bounds__(256, 2) keeps it at <= 256 VGPRs: two
+// workgroups share each CU, so one's epilogue / prologue runs beside the other's main loop.
+// LDS images [rows][32 k] (64-B rows): 16-B chunk c of row r at c ^ ((r >> 2) & 3), so the 16 rows of a
+// ds_read_b128 lane group hit 16 distinct 4-bank slots. Operands arrive by buffer-form LDS-DMA (lds_dma.h):
+// 6 x 1 KiB per wave per stage, one counted vmcnt(6) + one barrier per K-step, past-the-end K-steps re-read the
+// last one into the free stage (uniform counts).
+constexpr int T2_TM = 256, T2_TN = 128, T2_TK = 32, T2_GT = 256, T2_NST = 3;
+constexpr int T2_A = T2_TM * T2_TK * 2, T2_B = T2_TN * T2_TK * 2, T2_STAGE = T2_A + T2_B;  // 16 + 8 KiB
+static_assert(T2_NST * T2_STAGE >= 4 * 128 * 128, "the epilogue's 4 wave images (16 KiB each) fit the ring");
+
+__device__ __forceinline__ int t2_swz(int r) { return (r >> 2) & 3; }
+
+__device__ __forceinline__ void t2_issue(const GP& p, const __amdgpu_buffer_rsrc_t& ra, const __amdgpu_buffer_rsrc_t& rb,
+                                         unsigned char* st, int m0, int n0, int k0, int wave, int lane) {
+  // A: 16 instructions of 16 rows x 64 B (wave w: w, w + 4, w + 8, w + 12); B: 8 (w, w + 4)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = wave + 4 * u;
+    const int r = 16 * q + (lane >> 2);
+    const int c = (lane & 3) ^ t2_swz(r);
+    const int gr = min(m0 + r, p.M - 1);
+    bdma16(ra, (unsigned)(2 * ((size_t)gr * p.lda + k0 + 8 * c)), st + 1024 * q);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = wave + 4 * u;
+    const int r = 16 * q + (lane >> 2);
+    const int c = (lane & 3) ^ t2_swz(r);
+    const int gr = min(n0 + r, p.N - 1);
+    bdma16(rb, (unsigned)(2 * ((size_t)gr * p.ldb + k0 + 8 * c)), st + T2_A + 1024 * q);
+  }
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(T2_GT, 2) gemm_bf16_t2_kernel(GP p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[T2_NST * T2_STAGE];
+  const int nwg = p.tiles_m * p.tiles_n;
+  int wg = blockIdx.x;
+  if (nwg >= 16) {  // XCD-aware bijective remap (as the kernels above)
+    const int q = nwg / 8, r = nwg % 8, xcd = wg % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
+  }
+  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;
+  const int m0 = tm * T2_TM, n0 = tn * T2_TN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, l16 = lane & 15;
+  // gemm_bf16_supported keeps every operand < 2^31 bytes
+  const __amdgpu_buffer_rsrc_t ra = dma_rsrc(p.A, (unsigned)((size_t)(p.M - 1) * p.lda * 2 + (size_t)p.K * 2));
+  const __amdgpu_buffer_rsrc_t rb = dma_rsrc(p.B, (unsigned)((size_t)(p.N - 1) * p.ldb * 2 + (size_t)p.K * 2));
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int aoff[8], boff[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = wm * 128 + 16 * i + l16;
+    aoff[i] = r * 64 + 16 * (g ^ t2_swz(r));
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = wn * 64 + 16 * j + l16;
+    boff[j] = T2_A + r * 64 + 16 * (g ^ t2_swz(r));
+  }
+
+  const int nk = p.K / T2_TK;
+  t2_issue(p, ra, rb, smem, m0, n0, 0, wave, lane);
+  t2_issue(p, ra, rb, smem + T2_STAGE, m0, n0, min(1, nk - 1) * T2_TK, wave, lane);
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // stage t landed (only stage t + 1's 6 DMAs younger)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of stage t - 1 done before its refill
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    t2_issue(p, ra, rb, smem + ((t + 2) % T2_NST) * T2_STAGE, m0, n0, min(t + 2, nk - 1) * T2_TK, wave, lane);
+    const unsigned char* st = smem + (t % T2_NST) * T2_STAGE;
+    bf16x8 b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = ld_b128(st + boff[j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bf16x8 a = ld_b128(st + aoff[i]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the past-the-end stages, before the epilogue reuses LDS
+  __syncthreads();
+  gemm_bf16_epilogue<EPI, 2>(p, acc, smem, m0, n0, wave, lane);
+}
+
 }  // namespace
 
 bool gemm_bf16_supported(int M, int N, int K, int lda, int ldb, int ldc, bool b_kn) {
   // K whole K-steps; 16-B aligned rows for the DMA and the row-piece stores
   return M >= 1 && N >= 8 && K >= TK && K % TK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
-         ldc % 8 == 0 && (b_kn ? ldb >= N : ldb >= K) && lda >= K && ldc >= N;
+         ldc % 8 == 0 && (b_kn ? ldb >= N : ldb >= K) && lda >= K && ldc >= N &&
+         (int64_t)M * lda * 2 < (int64_t(1) << 31) && (int64_t)(b_kn ? K : N) * ldb * 2 < (int64_t(1) << 31);
 }
 
 void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc, bool b_kn,
@@ -451,6 +553,18 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
     }                                                     \
   } while (0)
   const bool nt4 = knob(KNOB_GEMM_BF16_2PHASE) == 0;  // 1: the one-barrier-per-K-step loop (A/B)
+  if (!b_kn && knob(KNOB_GEMM_BF16_T2) == 1) {  // 256 x 128 tiles, two workgroups per CU
+    p.tiles_m = (M + T2_TM - 1) / T2_TM;
+    p.tiles_n = (N + T2_TN - 1) / T2_TN;
+    const dim3 g2(p.tiles_m * p.tiles_n);
+    switch (epi) {
+      case EPI_BIAS: hipLaunchKernelGGL((gemm_bf16_t2_kernel<EPI_BIAS>), g2, dim3(T2_GT), 0, stream, p); break;
+      case EPI_BIAS_GELU: hipLaunchKernelGGL((gemm_bf16_t2_kernel<EPI_BIAS_GELU>), g2, dim3(T2_GT), 0, stream, p); break;
+      case EPI_DGELU: hipLaunchKernelGGL((gemm_bf16_t2_kernel<EPI_DGELU>), g2, dim3(T2_GT), 0, stream, p); break;
+      default: hipLaunchKernelGGL((gemm_bf16_t2_kernel<EPI_STORE>), g2, dim3(T2_GT), 0, stream, p); break;
+    }
+    return;
+  }
   if (b_kn) {
     GB_EPI(1);
   } else if (nt4) {

@@ -147,3 +147,36 @@ def test_mlp_gelu_fused_matches_composed():
     for a, b in zip(run(True), run(False)):
         scale = float(b.float().abs().max())
         torch.testing.assert_close(a.float(), b.float(), rtol=3e-2, atol=3e-2 * scale)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 128, 32), (300, 776, 192), (4096, 2304, 768), (1000, 768, 3072)])
+def test_gemm_bf16_t2_tiles_match_fp32_and_the_256_tile(M, N, Kd):
+    """Knob GEMM_BF16_T2: the NT GEMM on 256 x 128 tiles of 4 waves (two workgroups per CU). Same products over
+    the same 32-deep MFMAs as the 256 x 256 kernel's substeps: equal to it bit for bit, and to fp32 within bf16
+    rounding; every epilogue (store, bias, bias + GELU) and the identity / asymmetric-B check."""
+    g = torch.Generator(device="cpu").manual_seed(M + 3 * N)
+    A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    outs = {}
+    try:
+        for t2 in (0, 1):
+            K.set_knob("GEMM_BF16_T2", t2)
+            C0, _ = K.gemm_bf16(A, W, None, False, 0)
+            C1, _ = K.gemm_bf16(A, W, bias, False, 1)
+            y, u = K.gemm_bf16(A, W, bias, False, 5)
+            outs[t2] = (C0, C1, y, u)
+            torch.testing.assert_close(C0.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+            torch.testing.assert_close(C1.float(), ref + bias.float(), rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+            assert torch.equal(u, C1) and torch.equal(y, K.gelu_fwd_bf16(C1))
+        n = 256
+        K.set_knob("GEMM_BF16_T2", 1)
+        I = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+        B = (torch.arange(n * n, device=DEV, dtype=torch.float32).reshape(n, n) % 251 / 8).to(torch.bfloat16)
+        Ci, _ = K.gemm_bf16(I, B, None, False, 0)
+        assert torch.equal(Ci, B.t().contiguous())
+    finally:
+        K.reset_knobs()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)

@@ -11,6 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from simple_distributed_machine_learning_amd import _native  # noqa: E402
 
 K = _native.kernels()
+_native.apply_knobs_from_env()  # e.g. SDML_KNOBS=GEMM_BF16_T2=1 (the 256 x 128, two-workgroups-per-CU NT kernel)
 dev = torch.device("cuda", 0)
 T = int(os.environ.get("T", 16384))
 SHAPES = [("c_attn", 2304, 768), ("attn.c_proj", 768, 768), ("c_fc", 3072, 768), ("mlp.c_proj", 768, 3072),

@@ -32,11 +32,50 @@ import torch.nn.functional as F
 from .._native import kernels
 
 
+# SDML_GPT2_GEMM=hand: the forward and input-gradient GEMMs of these Linears on gemm_bf16.hip's NT kernel with
+# 256 x 128 tiles, two workgroups per CU (knob GEMM_BF16_T2) instead of hipBLASLt; the input gradient dY W runs as
+# NT against W^T, derived once per weight per optimizer step (keyed like the conv layouts: ops/conv.py WEIGHT_GEN).
+# Default "lib" (hipBLASLt) until the hand path measures faster on the GPT-2 step (tools/bench_gemm_bf16.py).
+_HAND = os.environ.get("SDML_GPT2_GEMM", "lib") == "hand"
+_WT = {}
+EPI_STORE, EPI_BIAS = 0, 1  # csrc/kernels/kernels.h GemmEpi
+
+
+def _hand_ok(x2, w) -> bool:
+    if not (_HAND and x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x2.stride(-1) == 1
+            and w.is_contiguous()):
+        return False
+    k = kernels()
+    k.set_knob("GEMM_BF16_T2", 1)
+    M, Kd, N = x2.shape[0], x2.shape[1], w.shape[0]
+    return bool(k.gemm_bf16_supported(M, N, Kd, x2.stride(0), Kd, N, False)
+                and k.gemm_bf16_supported(M, Kd, N, N, N, Kd, False))
+
+
+def _w_t(w):
+    """w^T, contiguous, cached for the optimizer step (not while a hipGraph is being captured)."""
+    from .conv import WEIGHT_GEN
+
+    if torch.cuda.is_current_stream_capturing():
+        return w.t().contiguous()
+    key = (w.data_ptr(), w._version, WEIGHT_GEN[0], tuple(w.shape))
+    hit = _WT.get(id(w))
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    wt = w.t().contiguous()
+    _WT[id(w)] = (key, wt)
+    return wt
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(b, x2, w.t()) if b is not None else x2 @ w.t()
+        ctx.hand = _hand_ok(x2, w)
+        if ctx.hand:
+            y, _ = kernels().gemm_bf16(x2, w, b, False, EPI_BIAS if b is not None else EPI_STORE)
+        else:
+            y = torch.addmm(b, x2, w.t()) if b is not None else x2 @ w.t()
         ctx.save_for_backward(x2)
         ctx.w, ctx.b = w, b  # the Parameters themselves: their .grad is written in backward
         ctx.in_shape = x.shape
@@ -47,7 +86,13 @@ class _LinearFn(torch.autograd.Function):
         (x2,) = ctx.saved_tensors
         w, b = ctx.w, ctx.b
         g2 = gy.reshape(-1, gy.shape[-1])
-        dx = (g2 @ w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if ctx.hand and g2.stride(-1) == 1:
+                dx, _ = kernels().gemm_bf16(g2, _w_t(w), None, False, EPI_STORE)
+                dx = dx.view(ctx.in_shape)
+            else:
+                dx = (g2 @ w).view(ctx.in_shape)
         gw, gb = _param_grads(g2, x2, w, b, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         return dx, gw, gb
 
@@ -89,7 +134,7 @@ class _MLPFn(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2):
         x2 = x.reshape(-1, x.shape[-1])
         a, u = kernels().gemm_bf16(x2, w1, b1, False, EPI_BIAS_GELU)
-        y = torch.addmm(b2, a, w2.t())
+        y = kernels().gemm_bf16(a, w2, b2, False, EPI_BIAS)[0] if _HAND else torch.addmm(b2, a, w2.t())
         ctx.save_for_backward(x2, u, a)
         ctx.params = (w1, b1, w2, b2)
         ctx.in_shape = x.shape
@@ -100,9 +145,18 @@ class _MLPFn(torch.autograd.Function):
         x2, u, a = ctx.saved_tensors
         w1, b1, w2, b2 = ctx.params
         g2 = gy.reshape(-1, gy.shape[-1])
-        du, _ = kernels().gemm_bf16(g2, w2, None, True, EPI_DGELU, u)  # (dY W2) * gelu'(U)
+        if _HAND and g2.stride(-1) == 1:  # NT against W2^T (the 256 x 128 two-workgroups-per-CU kernel)
+            du, _ = kernels().gemm_bf16(g2, _w_t(w2), None, False, EPI_DGELU, u)
+        else:
+            du, _ = kernels().gemm_bf16(g2, w2, None, True, EPI_DGELU, u)  # (dY W2) * gelu'(U)
         gw2, gb2 = _param_grads(g2, a, w2, b2, ctx.needs_input_grad[3], ctx.needs_input_grad[4])
-        dx = (du @ w1).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if _HAND and du.stride(-1) == 1:
+                dx, _ = kernels().gemm_bf16(du, _w_t(w1), None, False, EPI_STORE)
+                dx = dx.view(ctx.in_shape)
+            else:
+                dx = (du @ w1).view(ctx.in_shape)
         gw1, gb1 = _param_grads(du, x2, w1, b1, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         return dx, gw1, gb1, gw2, gb2
 
@@ -113,7 +167,9 @@ def mlp_gelu(x, w1, b1, w2, b2):
     at 16 x 1024 tokens (fused c_fc 124.5 us vs 77 + GELU; fused c_proj dX 160 us vs 78 + GELU':
     profiles/r3_gpt2_kernel_stats.txt), because the GEMM mainloop still trails hipBLASLt's."""
     if (x.is_cuda and x.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16 and b1 is not None
-            and b2 is not None and os.environ.get("SDML_FUSED_GELU_GEMM", "0") == "1"):
+            and b2 is not None and (_HAND or os.environ.get("SDML_FUSED_GELU_GEMM", "0") == "1")):
+        if _HAND:
+            kernels().set_knob("GEMM_BF16_T2", 1)
         T, C = x.numel() // x.shape[-1], x.shape[-1]
         k = kernels()
         if (k.gemm_bf16_supported(T, w1.shape[0], C, C, C, False)

@@ -32,10 +32,11 @@ import torch.nn.functional as F
 from .._native import kernels
 
 
-# SDML_GPT2_GEMM=hand: the forward and input-gradient GEMMs of these Linears on gemm_bf16.hip's NT kernel with
-# 256 x 128 tiles, two workgroups per CU (knob GEMM_BF16_T2) instead of hipBLASLt; the input gradient dY W runs as
-# NT against W^T, derived once per weight per optimizer step (keyed like the conv layouts: ops/conv.py WEIGHT_GEN).
-# Default "lib" (hipBLASLt) until the hand path measures faster on the GPT-2 step (tools/bench_gemm_bf16.py).
+# SDML_GPT2_GEMM=hand: the forward and input-gradient GEMMs of these Linears on gemm_bf16.hip's NT kernel instead
+# of hipBLASLt (the 4-phase 256 x 256 kernel, or with knob GEMM_BF16_T2 the 256 x 128 two-workgroups-per-CU one);
+# the input gradient dY W runs as NT against W^T, derived once per weight per optimizer step (keyed like the conv
+# layouts: ops/conv.py WEIGHT_GEN). Default "lib": hipBLASLt is faster at the GPT-2 shapes (c_fc forward 76.7 us vs
+# 99.5 for the 4-phase kernel and 122.6 for the 256 x 128 one: profiles/r4_gemm_bf16_t2_vs_nt4_vs_hipblaslt.jsonl).
 _HAND = os.environ.get("SDML_GPT2_GEMM", "lib") == "hand"
 _WT = {}
 EPI_STORE, EPI_BIAS = 0, 1  # csrc/kernels/kernels.h GemmEpi
@@ -46,10 +47,9 @@ def _hand_ok(x2, w) -> bool:
             and w.is_contiguous()):
         return False
     k = kernels()
-    k.set_knob("GEMM_BF16_T2", 1)
     M, Kd, N = x2.shape[0], x2.shape[1], w.shape[0]
-    return bool(k.gemm_bf16_supported(M, N, Kd, x2.stride(0), Kd, N, False)
-                and k.gemm_bf16_supported(M, Kd, N, N, N, Kd, False))
+    return bool(k.gemm_bf16_supported(M, N, Kd, x2.stride(0), Kd, False)
+                and k.gemm_bf16_supported(M, Kd, N, N, N, False))
 
 
 def _w_t(w):
@@ -168,8 +168,6 @@ def mlp_gelu(x, w1, b1, w2, b2):
     profiles/r3_gpt2_kernel_stats.txt), because the GEMM mainloop still trails hipBLASLt's."""
     if (x.is_cuda and x.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16 and b1 is not None
             and b2 is not None and (_HAND or os.environ.get("SDML_FUSED_GELU_GEMM", "0") == "1")):
-        if _HAND:
-            kernels().set_knob("GEMM_BF16_T2", 1)
         T, C = x.numel() // x.shape[-1], x.shape[-1]
         k = kernels()
         if (k.gemm_bf16_supported(T, w1.shape[0], C, C, C, False)

@@ -982,13 +982,11 @@ __global__ void __launch_bounds__(RD_OUT * RD_GRP) conv_wgrad_reduce_kernel(cons
 
 // torch weight [co][ci][3][3] -> the forward layout [co][tap][ci] and/or the dgrad layout
 // [ci][8 - tap][co] (either output may be null)
-// One 64 (co) x 64 (ci) x 9 (tap) tile per workgroup through LDS, so both outputs are written as 128-byte rows:
-// fwd[co][tap][ci] (64 consecutive ci) and dgrad[ci][8 - tap][co] (64 consecutive co); the element-wise form
-// scattered every dgrad store 2 bytes wide across rows Co elements apart (8.8 us per call at ResNet's shapes).
-constexpr int WT_T = 256, WT_TILE = 64;
-// any shape (channel counts not multiples of 64: the strided / general convolutions' callers)
-__global__ void __launch_bounds__(256) conv_weight_transform_any_kernel(const u16* __restrict__ w, u16* __restrict__ fwd,
-                                                                        u16* __restrict__ dgrad, int Co, int C) {
+// element-wise: one load, two stores per weight element (8.8 us per call at ResNet's shapes). A 64 x 64 x 9 LDS-tile
+// form (128-byte rows on both outputs) measured slower in round 4 (ResNet step 4.49 -> 4.87 ms): 64 workgroups at
+// 512 channels, each thread's 144 tile loads waited out one by one
+__global__ void __launch_bounds__(256) conv_weight_transform_kernel(const u16* __restrict__ w, u16* __restrict__ fwd,
+                                                                    u16* __restrict__ dgrad, int Co, int C) {
   const int64_t n = (int64_t)Co * C * 9;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int tap = (int)(i % 9);
@@ -997,29 +995,6 @@ __global__ void __launch_bounds__(256) conv_weight_transform_any_kernel(const u1
     const u16 v = w[i];
     if (fwd) fwd[((int64_t)co * 9 + tap) * C + ci] = v;
     if (dgrad) dgrad[((int64_t)ci * 9 + (8 - tap)) * Co + co] = v;
-  }
-}
-__global__ void __launch_bounds__(WT_T) conv_weight_transform_kernel(const u16* __restrict__ w, u16* __restrict__ fwd,
-                                                                    u16* __restrict__ dgrad, int Co, int C) {
-  __shared__ u16 tl[WT_TILE][WT_TILE * 9 + 2];  // [co][ci * 9 + tap] (+2: odd word pitch)
-  const int co0 = blockIdx.x * WT_TILE, ci0 = blockIdx.y * WT_TILE, t = threadIdx.x;
-  // load: co row a holds 64 * 9 = 576 consecutive elements of w
-  for (int i = t; i < WT_TILE * WT_TILE * 9; i += WT_T) {
-    const int a = i / (WT_TILE * 9), e = i % (WT_TILE * 9);
-    tl[a][e] = w[((int64_t)(co0 + a) * C + ci0) * 9 + e];
-  }
-  __syncthreads();
-  if (fwd) {
-    for (int i = t; i < WT_TILE * 9 * WT_TILE; i += WT_T) {  // (co a, tap) rows of 64 ci
-      const int row = i / WT_TILE, b = i % WT_TILE, a = row / 9, tap = row % 9;
-      fwd[((int64_t)(co0 + a) * 9 + tap) * C + ci0 + b] = tl[a][b * 9 + tap];
-    }
-  }
-  if (dgrad) {
-    for (int i = t; i < WT_TILE * 9 * WT_TILE; i += WT_T) {  // (ci b, tap) rows of 64 co
-      const int row = i / WT_TILE, a = i % WT_TILE, b = row / 9, tap = row % 9;
-      dgrad[((int64_t)(ci0 + b) * 9 + (8 - tap)) * Co + co0 + a] = tl[a][b * 9 + tap];
-    }
   }
 }
 
@@ -1134,14 +1109,9 @@ __global__ void __launch_bounds__(STEM_T) conv_c1_wgrad_reduce_kernel(const floa
 bool conv3x3_bf16_supported(int C, int Co) { return C >= 64 && Co >= 64 && C % 64 == 0 && Co % 64 == 0; }
 
 void conv3x3_weight_transform_bf16(const void* w_torch, void* fwd, void* dgrad, int Co, int C, hipStream_t stream) {
-  if (Co % WT_TILE || C % WT_TILE) {
-    const int64_t n = (int64_t)Co * C * 9;
-    const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(conv_weight_transform_any_kernel, dim3(blocks), dim3(256), 0, stream,
-                       static_cast<const u16*>(w_torch), static_cast<u16*>(fwd), static_cast<u16*>(dgrad), Co, C);
-    return;
-  }
-  hipLaunchKernelGGL(conv_weight_transform_kernel, dim3(Co / WT_TILE, C / WT_TILE), dim3(WT_T), 0, stream,
+  const int64_t n = (int64_t)Co * C * 9;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(conv_weight_transform_kernel, dim3(blocks), dim3(256), 0, stream,
                      static_cast<const u16*>(w_torch), static_cast<u16*>(fwd), static_cast<u16*>(dgrad), Co, C);
 }
 

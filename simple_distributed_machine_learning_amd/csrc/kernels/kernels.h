@@ -152,6 +152,8 @@ int u8_fwd_head_blocks(int M);
 // int64; nullptr turns them off); production builds return false and ignore it
 bool u8_set_stamps(void* buf);
 int u8_stamp_slots();
+// test probe: ds_read_b64_tr_b8 over a 1-KiB image (img [1024] bytes, addr [64] byte offsets, out [64][2] int32)
+void u8_tr8_probe(const unsigned char* img, const int* addr, int* out, hipStream_t stream);
 // experiments builds: weight-gradient phase stamps ([blocks][8][16] int64; nullptr off)
 bool u8_set_wgrad_stamps(void* buf);
 void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,

@@ -764,6 +764,88 @@ __device__ __forceinline__ f32x4 fd_dz_bits(const float (&w4)[4], const float (&
   return o;
 }
 
+// dz bound -> plane scale dz_up = 2^(14 - E) and the partial tile's out_scale = scale 2^(E - 14): block max through
+// LDS (red: >= 16 free floats; every thread of the GT-thread block calls this)
+template <int FD>
+__device__ __forceinline__ void wgrad_scales(const WgradParams& p, int n0, int r0, int t, float* red, float& dz_up,
+                                             float& out_scale) {
+  const int lane = t & 63, wave = t >> 6;
+  float bnd = 0.f;
+  if (p.amax) {
+    for (int i = t; i < p.namax; i += GT) bnd = fmaxf(bnd, p.amax[i]);
+  } else if constexpr (FD != 0) {  // max_row sum_c |dl| over this workgroup's rows, times max |W2| here
+    const int nrows = min(p.rows_per_split, p.M - r0);
+    for (int i = t; i < nrows; i += GT) {
+      const float* d = p.dl + (size_t)(r0 + i) * p.C;
+      float sa = 0.f;
+      for (int c = 0; c < p.C; ++c) sa += fabsf(d[c]);
+      bnd = fmaxf(bnd, sa);
+    }
+  }
+  float wmx = 0.f;
+  if constexpr (FD != 0) {
+    if (!p.amax)
+      for (int i = t; i < p.C * GHN; i += GT) wmx = fmaxf(wmx, fabsf(p.w2[(size_t)(i / GHN) * p.N + n0 + i % GHN]));
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    bnd = fmaxf(bnd, __shfl_xor(bnd, off));
+    wmx = fmaxf(wmx, __shfl_xor(wmx, off));
+  }
+  if (lane == 0) {
+    red[wave] = bnd;
+    red[8 + wave] = wmx;
+  }
+  __syncthreads();
+  bnd = red[0];
+  wmx = red[8];
+#pragma unroll
+  for (int w = 1; w < GT / 64; ++w) {
+    bnd = fmaxf(bnd, red[w]);
+    wmx = fmaxf(wmx, red[8 + w]);
+  }
+  __syncthreads();
+  // FD without amax: |dz_n| <= sum_c |dl_c| |W2_cn|; the product is rounded, so bound it by 2x
+  const int E = bound_exp((FD != 0 && !p.amax) ? 2.f * bnd * wmx : bnd);
+  dz_up = pow2f(14 - E);
+  out_scale = p.scale * pow2f(E - 14);
+}
+
+// partial tile -> slab (plain stores); C map: column = lane & 31, row = (r&3) + 8(r>>2) + 4h
+template <int NCT>
+__device__ __forceinline__ void wgrad_store_tile(const WgradParams& p, const f32x16 (&acc)[2][NCT], int split, int n0,
+                                                 int ct0, int lane, float out_scale) {
+  float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
+#pragma unroll
+  for (int j = 0; j < NCT; ++j) {
+    const int col = 32 * (ct0 + j) + (lane & 31);
+    if (col >= GKC) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        out[(size_t)n * GKC + col] = acc[i][j][r] * out_scale;
+      }
+  }
+}
+
+// bias-gradient partial: the 32 threads of each hidden float4 meet in LDS (red: 4 GT free floats, after a barrier)
+template <int FD>
+__device__ __forceinline__ void wgrad_store_bias(const WgradParams& p, const f32x4& bsum, int split, int n0, int t,
+                                                 float* red) {
+  float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
+  *reinterpret_cast<f32x4*>(red + 4 * t) = bsum;
+  __syncthreads();
+  if (t < GHN) {  // rows rr = 0 .. 31 in order, whichever thread staged them
+    float sacc = 0.f;
+    for (int rr = 0; rr < GBK; ++rr) {
+      const int owner = FD != 0 ? 64 * ((rr >> 4) * 4 + (t >> 4)) + 16 * ((t >> 2) & 3) + (rr & 15) : rr * 16 + (t >> 2);
+      sacc += red[4 * owner + (t & 3)];
+    }
+    out[(size_t)p.N * GKC + n0 + t] = sacc;
+  }
+}
+
 // FD = 0: dz read as [M][N]. FD > 0: the factored boundary gradient (rotate placement, one-rank step)
 // is expanded here instead of by a separate kernel that writes dz to memory and reads it back -
 // with head_xent.hip's exact operations, so gW / gb are bit-identical to the unfused pair; the ReLU
@@ -815,48 +897,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   }
   float d4[4] = {0.f, 0.f, 0.f, 0.f};
 
-  // ---- dz bound -> plane scale 2^(14 - E): block max through LDS (the buffers are free here) ----
-  {
-    float bnd = 0.f;
-    if (p.amax) {
-      for (int i = t; i < p.namax; i += GT) bnd = fmaxf(bnd, p.amax[i]);
-    } else if constexpr (FD != 0) {  // max_row sum_c |dl| over this workgroup's rows, times max |W2| here
-      const int nrows = min(p.rows_per_split, p.M - r0);
-      for (int i = t; i < nrows; i += GT) {
-        const float* d = p.dl + (size_t)(r0 + i) * p.C;
-        float sa = 0.f;
-        for (int c = 0; c < p.C; ++c) sa += fabsf(d[c]);
-        bnd = fmaxf(bnd, sa);
-      }
-    }
-    float* red = reinterpret_cast<float*>(smem);
-    float wmx = 0.f;
-    if constexpr (FD != 0) {
-      if (!p.amax)
-        for (int i = t; i < p.C * GHN; i += GT) wmx = fmaxf(wmx, fabsf(p.w2[(size_t)(i / GHN) * p.N + n0 + i % GHN]));
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-      bnd = fmaxf(bnd, __shfl_xor(bnd, off));
-      wmx = fmaxf(wmx, __shfl_xor(wmx, off));
-    }
-    if (lane == 0) {
-      red[wave] = bnd;
-      red[8 + wave] = wmx;
-    }
-    __syncthreads();
-    bnd = red[0];
-    wmx = red[8];
-#pragma unroll
-    for (int w = 1; w < GT / 64; ++w) {
-      bnd = fmaxf(bnd, red[w]);
-      wmx = fmaxf(wmx, red[8 + w]);
-    }
-    __syncthreads();
-    // FD without amax: |dz_n| <= sum_c |dl_c| |W2_cn|; the product is rounded, so bound it by 2x
-    const int E = bound_exp((FD != 0 && !p.amax) ? 2.f * bnd * wmx : bnd);
-    dz_up = pow2f(14 - E);
-    out_scale = p.scale * pow2f(E - 14);
-  }
+  wgrad_scales<FD>(p, n0, r0, t, reinterpret_cast<float*>(smem), dz_up, out_scale);
   U8W_STAMP(2, __builtin_amdgcn_s_memtime);
   constexpr int XU = (GXCH + GT - 1) / GT;  // 4 rounds
   const unsigned char* xp[XU];
@@ -984,20 +1025,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     compute(kt & 1);
     U8W_STAMP(10, __builtin_amdgcn_s_memtime);
 
-    // partial tile -> slab (plain stores); C map: column = lane & 31, row = (r&3) + 8(r>>2) + 4h
-    float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
-#pragma unroll
-    for (int j = 0; j < NCT; ++j) {
-      const int col = 32 * (ct0 + j) + (lane & 31);
-      if (col >= GKC) continue;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int n = n0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          out[(size_t)n * GKC + col] = acc[i][j][r] * out_scale;
-        }
-    }
+    wgrad_store_tile<NCT>(p, acc, split, n0, ct0, lane, out_scale);
     U8W_STAMP(11, __builtin_amdgcn_s_memtime);
   };
   if (nk > 0) {
@@ -1005,19 +1033,214 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
     else run(std::integral_constant<int, 3>{});
   }
   __syncthreads();
-  float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
-  // bias-gradient partial: the 32 threads of each hidden float4 meet in LDS (buffers are free)
-  float* red = reinterpret_cast<float*>(smem);
-  *reinterpret_cast<f32x4*>(red + 4 * t) = bsum;
-  __syncthreads();
-  if (t < GHN) {  // rows rr = 0 .. 31 in order, whichever thread staged them
-    float sacc = 0.f;
-    for (int rr = 0; rr < GBK; ++rr) {
-      const int owner = FD != 0 ? 64 * ((rr >> 4) * 4 + (t >> 4)) + 16 * ((t >> 2) & 3) + (rr & 15) : rr * 16 + (t >> 2);
-      sacc += red[4 * owner + (t & 3)];
+  wgrad_store_bias<FD>(p, bsum, split, n0, t, reinterpret_cast<float*>(smem));
+  U8W_STAMP(12, __builtin_amdgcn_s_memtime);
+  U8W_STAMP(15, __builtin_amdgcn_s_memrealtime);
+}
+
+// ---- the same weight gradient with its operands on an LDS-DMA ring (FD = 2: dl + ReLU bits) ----------------
+// Why: u8_wgrad_kernel stages a K-step's pixels through registers (global -> VGPR -> fp16 -> LDS), so one K-step of
+// loads (25 KB per CU) is all it can have in flight; at ~3.9K cycles per K-step against ~1.8K of MFMA its waves sat
+// in s_waitcnt (SQ_WAIT_INST_ANY 35 % of wave cycles, profiles/r4_pmc_fused_fwd_head_and_wgrad.txt). Here the raw
+// pixel bytes, the K-step's dl rows and its ReLU bits go to LDS by buffer-DMA into a 4-stage ring (three K-steps,
+// ~84 KB per CU, in flight), issued as inline assembly (lds_dma.h bdma16_asm: the builtin form made the compiler
+// drain the ring, s_waitcnt vmcnt(0), before every transposed fragment read). Pixel fragments come straight from the byte image through ds_read_b64_tr_b8 (a 16-lane
+// group reads 8 rows x 16 columns: lane = column, byte q = row q) and are widened in registers by the wave that owns
+// the column tile (each pixel once per block, as before); the waves only write the dz planes (8 KB per K-step instead
+// of 59 KB of ds_write). Numerics, tile ownership, k order and the partial-tile / bias outputs are those of
+// u8_wgrad_kernel<2>: the results are bit-identical.
+constexpr int RX_PITCH = 800;                   // bytes per pixel row in LDS (50 16-B chunks, the last one a pad)
+constexpr int RX_PIECES = GBK * RX_PITCH / 1024;  // 25 1-KiB DMA pieces of pixels per K-step
+constexpr int RDL_OFF = RX_PIECES * 1024;         // dl rows of the K-step: 2 pieces (8 C <= 128 chunks)
+constexpr int RMK_OFF = RDL_OFF + 2048;           // ReLU bits of the K-step: 1 piece (N / 4 <= 64 chunks)
+constexpr int RPIECES = RX_PIECES + 3;            // wave w issues pieces w, w + 8, w + 16 (and w + 24 for w < 4)
+constexpr int RSTAGE = RPIECES * 1024;
+constexpr int RNS = 4;                            // ring stages
+constexpr int RDZ_OFF = RNS * RSTAGE;             // two dz-plane buffers [GNPL][GBK][GDP] fp16
+constexpr int RSMEM = RDZ_OFF + 2 * GNPL * GD_U16 * 2;
+static_assert(GBK * RX_PITCH % 1024 == 0 && RSMEM <= 160 * 1024, "ring LDS");
+static_assert((RX_PITCH / 16) % 16 == 2, "tr_b8 reads: rows q = 0..7 of a chunk pair on 16 distinct 16-B bank slots");
+
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+
+// 32x32x16 f16 B operand of the 32 columns c0.. of the byte image at k-substep s, same lane map as frag_px:
+// lane l (r = l & 31, h = l >> 5) gets column c0 + r, k-rows 16 s + 8 h + j. Lane 2q + p of 16-lane group g
+// addresses row 16 s + 8 (g >> 1) + q, columns c0 + 16 (g & 1) + 8 p .. +7.
+__device__ __forceinline__ f16x8 frag_x8(const unsigned char* img, int c0, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const unsigned char* a = img + (16 * s + 8 * (g >> 1) + (i >> 1)) * RX_PITCH + c0 + 16 * (g & 1) + 8 * (i & 1);
+  const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2*)(a));
+  return widen8h((unsigned)v[0], (unsigned)v[1]);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char rsm[RSMEM];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int L = blockIdx.x, G8 = 8 * p.groups;
+  const int split = p.xcd ? (L / G8) * 8 + L % 8 : L / p.groups;
+  if (split >= p.splits) return;
+  U8W_STAMP(0, __builtin_amdgcn_s_memrealtime);
+  U8W_STAMP(1, __builtin_amdgcn_s_memtime);
+  const int n0 = (p.g0 + (p.xcd ? (L % G8) / 8 : L % p.groups)) * GHN;
+  const int r0 = split * p.rows_per_split;
+  const int nk = min(p.rows_per_split, p.M - r0) / GBK;  // host: M % GBK == 0
+  float dz_up, out_scale;
+  wgrad_scales<2>(p, n0, r0, t, reinterpret_cast<float*>(rsm), dz_up, out_scale);
+  if (nk <= 0) return;  // (block-uniform; after wgrad_scales' barriers)
+  U8W_STAMP(2, __builtin_amdgcn_s_memtime);
+
+  // DMA sources: one resource per operand from this split's first row (rows past M read as zero); per piece a
+  // per-lane offset (chunk 64 j + lane), per K-step a scalar advance
+  const int C = p.C, NW = p.N / 32;
+  const dma_i32x4 rx = dma_rsrc4(p.X + (size_t)r0 * p.ldx, (unsigned)((p.M - r0) * p.ldx));
+  const dma_i32x4 rdl = dma_rsrc4(p.dl + (size_t)r0 * C, (unsigned)((p.M - r0) * C * 4));
+  const dma_i32x4 rmk = dma_rsrc4(p.mask + (size_t)r0 * NW, (unsigned)((p.M - r0) * NW * 4));
+  const unsigned xstep = GBK * p.ldx, dlstep = GBK * C * 4, mkstep = GBK * NW * 4;
+  unsigned voff[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = wave + 8 * u;
+    if (j < RX_PIECES) {  // pixel chunk ci: row ci / 50, 16-B column chunk ci % 50 (49 = pad: repeats chunk 48)
+      const int ci = 64 * j + lane, row = ci / (RX_PITCH / 16), cc = ci % (RX_PITCH / 16);
+      voff[u] = (unsigned)(row * p.ldx + 16 * min(cc, GKC / 16 - 1));
+    } else if (j < RX_PIECES + 2) {  // dl chunk (clamped: chunks past 8 C repeat the last one into unused bytes)
+      voff[u] = 16u * (unsigned)min(64 * (j - RX_PIECES) + lane, 8 * C - 1);
+    } else {
+      voff[u] = 16u * (unsigned)min(lane, 8 * NW - 1);  // ReLU-bit chunk
     }
-    out[(size_t)p.N * GKC + n0 + t] = sacc;
   }
+  auto issue = [&](int kt) {
+    unsigned char* st = rsm + (kt % RNS) * RSTAGE;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = wave + 8 * u;
+      if (j < RX_PIECES) bdma16_asm(rx, voff[u], (unsigned)kt * xstep, st + 1024 * j);
+      else if (j < RX_PIECES + 2) bdma16_asm(rdl, voff[u], (unsigned)kt * dlstep, st + 1024 * j);
+      else if (j < RPIECES) bdma16_asm(rmk, voff[u], (unsigned)kt * mkstep, st + 1024 * j);
+    }
+  };
+  // wait until this wave's pieces of a K-step have landed while `later` (0..2) younger K-steps stay in flight
+  // (waves 0..3 issue 4 pieces per K-step, waves 4..7 three)
+  auto wait_dma = [&](int later) {
+    if (later >= 2) {
+      if (wave < 4) wait_vm<8>();
+      else wait_vm<6>();
+    } else if (later == 1) {
+      if (wave < 4) wait_vm<4>();
+      else wait_vm<3>();
+    } else {
+      wait_vm<0>();
+    }
+  };
+
+  // dz tile of wave w: rows 16 (w >> 2) + (lane & 15), hidden 16 (w & 3) + 4 (lane >> 4) .. +3 (as u8_wgrad_kernel<2>)
+  const int fr = 16 * (wave >> 2) + (lane & 15), fc = 16 * (wave & 3) + 4 * (lane >> 4);
+  const int mword = (n0 + fc) / 32, mshift = (n0 + fc) & 31;
+  float w4[4];
+  {
+    const int g = lane >> 4;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      w4[kk] = 4 * g + kk < C ? p.w2[(size_t)(4 * g + kk) * p.N + n0 + 16 * (wave & 3) + (lane & 15)] : 0.f;
+  }
+  f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
+  u16* dzb = reinterpret_cast<u16*>(rsm + RDZ_OFF);
+  const int doff = fr * GDP + (((fc >> 2) ^ dz_swz(fr)) << 2);
+  auto build_dz = [&](int kt) {
+    const unsigned char* st = rsm + (kt % RNS) * RSTAGE;
+    const float* sdl = reinterpret_cast<const float*>(st + RDL_OFF) + fr * C;
+    const unsigned bits = reinterpret_cast<const unsigned*>(st + RMK_OFF)[fr * NW + mword];
+    float d4[4];
+    const int g = lane >> 4;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const float v = sdl[min(4 * g + kk, C - 1)];
+      d4[kk] = 4 * g + kk < C ? v : 0.f;
+    }
+    const f32x4 dv = fd_dz_bits(w4, d4, (bits >> mshift) & 15u);
+    bsum += dv;
+    u16x4 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x = dv[e] * dz_up;  // exact (power of two), |x| < 2^14
+      const _Float16 h = static_cast<_Float16>(x);
+      hi[e] = __builtin_bit_cast(u16, h);
+      lo[e] = __builtin_bit_cast(u16, static_cast<_Float16>(x - static_cast<float>(h)));
+    }
+    u16* B = dzb + (kt & 1) * GNPL * GD_U16;
+    *reinterpret_cast<u16x4*>(B + doff) = hi;
+    *reinterpret_cast<u16x4*>(B + doff + GD_U16) = lo;
+  };
+
+  auto run = [&](auto nct_c) {
+    constexpr int NCT = decltype(nct_c)::value;
+    const int ct0 = NCT == 4 ? 0 : 4 + 3 * (wave - 1);  // first 32-column tile
+    f32x16 acc[2][NCT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) acc[i][j] = f32x16{};
+    auto compute = [&](int kt) {
+      const unsigned char* X8 = rsm + (kt % RNS) * RSTAGE;
+      const u16* D = dzb + (kt & 1) * GNPL * GD_U16;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f16x8 a[2][GNPL];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int pl = 0; pl < GNPL; ++pl) a[i][pl] = frag_tr_dz<GDP>(D + pl * GD_U16, 32 * i, s, lane);
+#pragma unroll
+        for (int j = 0; j < NCT; ++j) {
+          const f16x8 b = frag_x8(X8, 32 * (ct0 + j), s, lane);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            acc[i][j] = mfma(a[i][1], b, acc[i][j]);  // lo
+            acc[i][j] = mfma(a[i][0], b, acc[i][j]);  // hi
+          }
+        }
+      }
+    };
+    // K-step kt: its DMA was issued 3 K-steps ahead; at the top of step kt the pieces of kt + 1 are waited for (their
+    // dl / bits become dz planes in this step), the barrier publishes them and frees stage (kt - 1) % RNS and dz
+    // buffer (kt + 1) & 1 (last read by step kt - 1), which kt + 3's DMA and kt + 1's dz then reuse
+    // W2 values in registers before the first DMA: the compiler's own wait for them (it does not see the asm DMAs)
+    // would otherwise be a vmcnt(0) behind three K-steps of DMA
+    asm volatile("" ::"v"(w4[0]), "v"(w4[1]), "v"(w4[2]), "v"(w4[3]));
+    issue(0);
+    if (nk > 1) issue(1);
+    if (nk > 2) issue(2);
+    wait_dma(min(nk - 1, 2));
+    __syncthreads();
+    build_dz(0);
+    U8W_STAMP(3, __builtin_amdgcn_s_memtime);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) wait_dma(kt + 2 < nk ? 1 : 0);
+      __syncthreads();
+#ifdef SDML_KERNEL_EXPERIMENTS
+      if (kt == 1 || kt == 9 || kt == 17) U8W_STAMP(5 + (kt - 1) / 8 * 2, __builtin_amdgcn_s_memtime);  // after barrier
+#endif
+      if (kt + 3 < nk) issue(kt + 3);
+      if (kt + 1 < nk) build_dz(kt + 1);
+      compute(kt);
+#ifdef SDML_KERNEL_EXPERIMENTS
+      if (kt == 0 || kt == 8 || kt == 16) U8W_STAMP(4 + kt / 8 * 2, __builtin_amdgcn_s_memtime);  // after compute
+#endif
+    }
+    U8W_STAMP(10, __builtin_amdgcn_s_memtime);
+    wgrad_store_tile<NCT>(p, acc, split, n0, ct0, lane, out_scale);
+    U8W_STAMP(11, __builtin_amdgcn_s_memtime);
+  };
+  if (wave == 0) run(std::integral_constant<int, 4>{});
+  else run(std::integral_constant<int, 3>{});
+  __syncthreads();
+  wgrad_store_bias<2>(p, bsum, split, n0, t, reinterpret_cast<float*>(rsm));
   U8W_STAMP(12, __builtin_amdgcn_s_memtime);
   U8W_STAMP(15, __builtin_amdgcn_s_memrealtime);
 }
@@ -1198,7 +1421,11 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigne
 #endif
   const dim3 wgrid(((splits + 7) / 8) * 8 * p.groups);
   const bool ilv = knob(KNOB_U8_WGRAD_ILV) != 0;
-  if (mask && ilv) hipLaunchKernelGGL((u8_wgrad_kernel<2, true>), wgrid, dim3(GT), 0, stream, p);
+  // the DMA-ring form: ReLU bits, one DMA piece of them and two of dl rows per K-step, 16-B aligned sources
+  const bool ring = mask && !ilv && knob(KNOB_U8_WGRAD_RING) != 0 && N <= 256 && C <= 16 &&
+                    (reinterpret_cast<uintptr_t>(dl) & 15) == 0 && (reinterpret_cast<uintptr_t>(mask) & 15) == 0;
+  if (ring) hipLaunchKernelGGL(u8_wgrad_ring_kernel, wgrid, dim3(GT), 0, stream, p);
+  else if (mask && ilv) hipLaunchKernelGGL((u8_wgrad_kernel<2, true>), wgrid, dim3(GT), 0, stream, p);
   else if (mask) hipLaunchKernelGGL((u8_wgrad_kernel<2, false>), wgrid, dim3(GT), 0, stream, p);
   else if (ilv) hipLaunchKernelGGL((u8_wgrad_kernel<1, true>), wgrid, dim3(GT), 0, stream, p);
   else hipLaunchKernelGGL((u8_wgrad_kernel<1, false>), wgrid, dim3(GT), 0, stream, p);
@@ -1337,6 +1564,25 @@ bool u8_set_stamps(void* buf) {
 #endif
 }
 int u8_stamp_slots() { return U8_NSTAMP; }
+
+namespace {
+// one wave: a 1-KiB byte image in LDS, ds_read_b64_tr_b8 at per-lane byte addresses (multiples of 8), the 8 bytes
+// each lane gets -> out[lane][2] (tests/test_fused_head_gpu.py pins the lane map frag_x8 assumes)
+__global__ void __launch_bounds__(64) tr8_probe_kernel(const unsigned char* img, const int* addr, int* out) {
+  __shared__ __attribute__((aligned(16))) unsigned char s[1024];
+  const int l = threadIdx.x;
+  *reinterpret_cast<u32x4*>(s + 16 * l) = *reinterpret_cast<const u32x4*>(img + 16 * l);
+  __syncthreads();
+  const int a = addr[l] & 1016;
+  const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2*)(s + a));
+  out[2 * l] = v[0];
+  out[2 * l + 1] = v[1];
+}
+}  // namespace
+
+void u8_tr8_probe(const unsigned char* img, const int* addr, int* out, hipStream_t stream) {
+  hipLaunchKernelGGL(tr8_probe_kernel, dim3(1), dim3(64), 0, stream, img, addr, out);
+}
 bool u8_set_wgrad_stamps(void* buf) {
 #ifdef SDML_KERNEL_EXPERIMENTS
   g_u8w_stamps = static_cast<long long*>(buf);

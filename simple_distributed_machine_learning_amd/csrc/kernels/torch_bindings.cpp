@@ -1712,6 +1712,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       "experiments builds: phase stamps of the fused uint8 forward + head (tools/probes/u8_fwd_stamps.py)");
   m.def("u8_stamp_slots", &sdml::u8_stamp_slots, "stamps per (block, wave) of u8_set_stamps");
   m.def(
+      "u8_tr8_probe",
+      [](torch::Tensor img, torch::Tensor addr) {
+        TORCH_CHECK(img.is_cuda() && img.scalar_type() == torch::kUInt8 && img.is_contiguous() && img.numel() == 1024,
+                    "u8_tr8_probe: img uint8 [1024]");
+        TORCH_CHECK(addr.is_cuda() && addr.scalar_type() == torch::kInt32 && addr.is_contiguous() && addr.numel() == 64,
+                    "u8_tr8_probe: addr int32 [64]");
+        auto out = torch::empty({64, 2}, addr.options());
+        sdml::u8_tr8_probe(img.data_ptr<uint8_t>(), addr.data_ptr<int>(), out.data_ptr<int>(), cur_stream());
+        return out;
+      },
+      "test probe: the 8 bytes ds_read_b64_tr_b8 gives each lane of one wave (img in LDS, per-lane byte addresses)");
+  m.def(
       "u8_set_wgrad_stamps",
       [](c10::optional<torch::Tensor> buf) {
         if (!buf) return sdml::u8_set_wgrad_stamps(nullptr);

@@ -260,3 +260,61 @@ def test_fused_forward_head_four_wave_blocks(M, C, defer):
     torch.testing.assert_close(st4[0], st8[0], rtol=1e-5, atol=1e-3)
     assert float(st4[1]) == float(st8[1])
     assert float(b4.max()) == float(b8.max())  # max over rows of the same per-row terms
+
+
+def test_ds_read_tr8_lane_map():
+    """ds_read_b64_tr_b8 (the ring weight gradient's pixel-fragment read, mlp_u8.hip frag_x8): per 16-lane group,
+    lane 2q + p addresses row q, bytes 8p .. 8p + 7 of an 8-row x 16-byte block; lane i of the group receives byte
+    column i of the 8 rows, row q in byte q. Checked on an 800-byte-pitch image as frag_x8 addresses it."""
+    from simple_distributed_machine_learning_amd import _native
+
+    K = _native.kernels()
+    g = torch.Generator(device="cpu").manual_seed(3)
+    img = torch.randint(0, 256, (1024,), generator=g, dtype=torch.uint8)
+    pitch = 64  # rows of the probe image (any multiple of 8 works for the map)
+    lane = torch.arange(64)
+    grp, i = lane // 16, lane % 16
+    row0 = 8 * (grp // 2)  # groups 2, 3: the next 8 rows (frag_x8's lane half h)
+    col0 = 16 * (grp % 2) + 32  # groups 1, 3: the next 16 columns
+    addr = (row0 + i // 2) * pitch + col0 + 8 * (i % 2)
+    out = K.u8_tr8_probe(img.to(DEV), addr.to(torch.int32).to(DEV)).cpu()
+    got = out.contiguous().view(torch.uint8).view(64, 8)
+    want = torch.empty(64, 8, dtype=torch.uint8)
+    for l in range(64):
+        for q in range(8):
+            want[l, q] = img[(int(row0[l]) + q) * pitch + int(col0[l]) + int(i[l])]
+    assert torch.equal(got, want), (got[:4], want[:4])
+
+
+@pytest.mark.parametrize("M,C,Nh", [(4096, 10, 128), (4096 + 96, 10, 128), (131072, 10, 128), (8192, 2, 64),
+                                    (8192, 16, 256)])
+def test_wgrad_dma_ring_bit_identical_to_register_staged(M, C, Nh):
+    """Knob U8_WGRAD_RING: the weight gradient from dl + ReLU bits with its operands on a 4-stage LDS-DMA ring
+    (pixel fragments by transposed byte reads, widened in registers) against the register-staged kernel: the same
+    dz planes, k order and MFMA sequence, so bit-identical gW / gb, with and without the head's bound."""
+    from simple_distributed_machine_learning_amd import _native
+
+    K = _native.kernels()
+    x8 = pixels(M, 51)
+    h = rnd(M, Nh, seed=52).relu()
+    dl = rnd(M, C, seed=53, scale=1e-3)
+    w2 = rnd(C, Nh, seed=54, scale=0.1)
+    g0 = rnd(Nh * KD + Nh, seed=55)
+    bits = ops.relu_bits(h)
+    try:
+        for amax in (None, (dl.abs().sum(1).max() * w2.abs().max() * 2).reshape(1)):
+            bufs = []
+            for ring in (0, 1):
+                K.set_knob("U8_WGRAD_RING", ring)
+                b = g0.clone()
+                ops.linear_wgrad_u8_dl(x8, dl, w2, bits, b[:Nh * KD].view(Nh, KD), b[Nh * KD:], amax=amax)
+                torch.cuda.synchronize()
+                bufs.append(b)
+            assert torch.equal(bufs[0], bufs[1])
+    finally:
+        K.reset_knobs()
+    # and against fp64
+    dz = (dl.double() @ w2.double()) * (h > 0).double()
+    want = dz.t() @ (x8.double() / 255.0)
+    got = bufs[1][:Nh * KD].view(Nh, KD).double() - g0[:Nh * KD].view(Nh, KD).double()
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-6)

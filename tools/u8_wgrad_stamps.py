@@ -1,5 +1,7 @@
 """Phase timing of the uint8 weight gradient (mlp_u8.hip u8_wgrad_kernel<2>: ReLU bits + factored dl, the
-headline step's second kernel) at 131072 x 784 -> 128 from its s_memtime stamps (experiments build only).
+headline step's second kernel, or u8_wgrad_ring_kernel when knob U8_WGRAD_RING is on - the default) at 131072 x 784
+-> 128 from its s_memtime stamps (experiments build only). Ring kernel: "stage+gload+barrier" is the DMA wait + barrier
+at the top of the next K-step, and the compute intervals include the next K-step's dz build and DMA issue.
 
 Per (block, wave): 1 start, 2 after the dz-bound reduction, 3 after the prologue (first K-step staged), 4 / 5 after
 K-step 0's compute / barrier, 6 / 7 the same for K-step 8, 8 / 9 for K-step 16, 10 after the last compute,
@@ -43,6 +45,9 @@ def timed(n=30):
     return e0.elapsed_time(e1) / n * 1e3
 
 
+if len(sys.argv) > 1:  # e.g. U8_WGRAD_RING=0
+    name, v = sys.argv[1].split("=")
+    K.set_knob(name, int(v))
 plain = timed()
 NB = 4096
 stamps = torch.zeros(NB * 8 * 16, dtype=torch.int64, device=dev)

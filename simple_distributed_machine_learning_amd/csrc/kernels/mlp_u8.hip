@@ -1038,26 +1038,32 @@ __global__ void __launch_bounds__(GT) u8_wgrad_kernel(WgradParams p) {
   U8W_STAMP(15, __builtin_amdgcn_s_memrealtime);
 }
 
-// ---- the same weight gradient with its operands on an LDS-DMA ring (FD = 2: dl + ReLU bits) ----------------
-// Why: u8_wgrad_kernel stages a K-step's pixels through registers (global -> VGPR -> fp16 -> LDS), so one K-step of
-// loads (25 KB per CU) is all it can have in flight; at ~3.9K cycles per K-step against ~1.8K of MFMA its waves sat
-// in s_waitcnt (SQ_WAIT_INST_ANY 35 % of wave cycles, profiles/r4_pmc_fused_fwd_head_and_wgrad.txt). Here the raw
-// pixel bytes, the K-step's dl rows and its ReLU bits go to LDS by buffer-DMA into a 4-stage ring (three K-steps,
-// ~84 KB per CU, in flight), issued as inline assembly (lds_dma.h bdma16_asm: the builtin form made the compiler
-// drain the ring, s_waitcnt vmcnt(0), before every transposed fragment read). Pixel fragments come straight from the byte image through ds_read_b64_tr_b8 (a 16-lane
-// group reads 8 rows x 16 columns: lane = column, byte q = row q) and are widened in registers by the wave that owns
-// the column tile (each pixel once per block, as before); the waves only write the dz planes (8 KB per K-step instead
-// of 59 KB of ds_write). Numerics, tile ownership, k order and the partial-tile / bias outputs are those of
-// u8_wgrad_kernel<2>: the results are bit-identical.
-constexpr int RX_PITCH = 800;                   // bytes per pixel row in LDS (50 16-B chunks, the last one a pad)
+// ---- the same weight gradient with its operands on LDS-DMA rings (FD = 2: dl + ReLU bits) ----------------------
+// Why: u8_wgrad_kernel stages a K-step's pixels through registers (global -> VGPR -> fp16 -> LDS) and reads each
+// K-step's fragments only after that K-step's barrier; at ~3.9K cycles per K-step against ~2K of MFMA on its busiest
+// SIMD its waves sat in s_waitcnt (SQ_WAIT_INST_ANY 35 % of wave cycles, profiles/r4_pmc_fused_fwd_head_and_wgrad.txt).
+// Here:
+//  * the raw pixel bytes go to LDS by buffer-DMA into a 4-stage ring, issued three K-steps ahead; the K-step's dl rows
+//    and ReLU bits into a 4-stage side ring, four K-steps ahead. The DMA is inline assembly (lds_dma.h bdma16_asm:
+//    with the builtin form the compiler drained the ring, s_waitcnt vmcnt(0), before every transposed fragment read);
+//  * pixel fragments come straight from the byte image through ds_read_b64_tr_b8 (a 16-lane group reads 8 rows x 16
+//    columns: lane = column, byte q = row q) and are widened in registers by the wave that owns the column tile (each
+//    pixel once per block, as before); the waves only write the dz planes (8 KB per K-step instead of 59 KB);
+//  * software pipeline: the dz planes of K-step kt + 2 are built during kt (three dz buffers), so when the barrier
+//    ending kt - 1 has passed, kt + 1's planes and pixels are both published; k-substep 0's fragments of kt + 1 are
+//    read into registers during kt's last MFMAs and the MFMAs of kt + 1 start right after its barrier.
+// Numerics, tile ownership, k order and the partial-tile / bias outputs are those of u8_wgrad_kernel<2>: the results
+// are bit-identical. Measured stamps: tools/u8_wgrad_stamps.py.
+constexpr int RX_PITCH = 800;                     // bytes per pixel row in LDS (50 16-B chunks, the last one a pad)
 constexpr int RX_PIECES = GBK * RX_PITCH / 1024;  // 25 1-KiB DMA pieces of pixels per K-step
-constexpr int RDL_OFF = RX_PIECES * 1024;         // dl rows of the K-step: 2 pieces (8 C <= 128 chunks)
-constexpr int RMK_OFF = RDL_OFF + 2048;           // ReLU bits of the K-step: 1 piece (N / 4 <= 64 chunks)
-constexpr int RPIECES = RX_PIECES + 3;            // wave w issues pieces w, w + 8, w + 16 (and w + 24 for w < 4)
-constexpr int RSTAGE = RPIECES * 1024;
-constexpr int RNS = 4;                            // ring stages
-constexpr int RDZ_OFF = RNS * RSTAGE;             // two dz-plane buffers [GNPL][GBK][GDP] fp16
-constexpr int RSMEM = RDZ_OFF + 2 * GNPL * GD_U16 * 2;
+constexpr int RX_STAGE = RX_PIECES * 1024;
+constexpr int RNS = 4;                            // stages of both rings
+constexpr int RS_STAGE = 3072;                    // side stage: dl rows (2 pieces, 8 C <= 128 chunks), ReLU bits (1)
+constexpr int RS_OFF = RNS * RX_STAGE;
+constexpr int RDZ_OFF = RS_OFF + RNS * RS_STAGE;  // three dz-plane buffers [GNPL][GBK][GDP] fp16
+constexpr int RDZ_BUF = GNPL * GD_U16;            // u16 per dz buffer
+constexpr int RSCR_OFF = RDZ_OFF + 3 * RDZ_BUF * 2;  // 1 KiB the null DMA pieces write
+constexpr int RSMEM = RSCR_OFF + 1024;
 static_assert(GBK * RX_PITCH % 1024 == 0 && RSMEM <= 160 * 1024, "ring LDS");
 static_assert((RX_PITCH / 16) % 16 == 2, "tr_b8 reads: rows q = 0..7 of a chunk pair on 16 distinct 16-B bank slots");
 
@@ -1066,10 +1072,15 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 // 32x32x16 f16 B operand of the 32 columns c0.. of the byte image at k-substep s, same lane map as frag_px:
 // lane l (r = l & 31, h = l >> 5) gets column c0 + r, k-rows 16 s + 8 h + j. Lane 2q + p of 16-lane group g
 // addresses row 16 s + 8 (g >> 1) + q, columns c0 + 16 (g & 1) + 8 p .. +7.
+template <bool RAW = false>
 __device__ __forceinline__ f16x8 frag_x8(const unsigned char* img, int c0, int s, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const unsigned char* a = img + (16 * s + 8 * (g >> 1) + (i >> 1)) * RX_PITCH + c0 + 16 * (g & 1) + 8 * (i & 1);
   const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2*)(a));
+  if constexpr (RAW) {  // (timing experiment)
+    u32x4 r = {(unsigned)v[0], (unsigned)v[1], (unsigned)v[0], (unsigned)v[1]};
+    return __builtin_bit_cast(f16x8, r);
+  }
   return widen8h((unsigned)v[0], (unsigned)v[1]);
 }
 
@@ -1078,6 +1089,9 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// MODE (experiments builds, knob U8_VARIANT; wrong results by design): 1 no dz build in the K loop, 2 no byte
+// widening (raw bytes as fp16 bits), 3 no barrier in the K loop, 4 no MFMA
+template <int MODE = 0>
 __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char rsm[RSMEM];
   const int t = threadIdx.x, lane = t & 63;
@@ -1095,48 +1109,53 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
   if (nk <= 0) return;  // (block-uniform; after wgrad_scales' barriers)
   U8W_STAMP(2, __builtin_amdgcn_s_memtime);
 
-  // DMA sources: one resource per operand from this split's first row (rows past M read as zero); per piece a
-  // per-lane offset (chunk 64 j + lane), per K-step a scalar advance
+  // DMA: one resource per operand from this split's first row (rows past M read as zero), a per-lane offset per piece
+  // (chunk 64 j + lane), a scalar advance per K-step. Every wave issues 4 pieces per group, so the loop body has no
+  // branches: pixel pieces w, w + 8, w + 16, and a 4th - wave 0 pixel piece 24, waves 1 and 2 the dl pieces, wave 3
+  // the ReLU-bit piece, waves 4..7 a null resource (num_records 0: no memory access, zeros into a scratch KiB)
   const int C = p.C, NW = p.N / 32;
   const dma_i32x4 rx = dma_rsrc4(p.X + (size_t)r0 * p.ldx, (unsigned)((p.M - r0) * p.ldx));
-  const dma_i32x4 rdl = dma_rsrc4(p.dl + (size_t)r0 * C, (unsigned)((p.M - r0) * C * 4));
-  const dma_i32x4 rmk = dma_rsrc4(p.mask + (size_t)r0 * NW, (unsigned)((p.M - r0) * NW * 4));
-  const unsigned xstep = GBK * p.ldx, dlstep = GBK * C * 4, mkstep = GBK * NW * 4;
+  const dma_i32x4 rnull = dma_rsrc4(p.X, 0u);
+  dma_i32x4 r3 = rnull;
+  const unsigned xstep = GBK * p.ldx;
+  unsigned step3 = 0u;
   unsigned voff[4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int j = wave + 8 * u;
-    if (j < RX_PIECES) {  // pixel chunk ci: row ci / 50, 16-B column chunk ci % 50 (49 = pad: repeats chunk 48)
-      const int ci = 64 * j + lane, row = ci / (RX_PITCH / 16), cc = ci % (RX_PITCH / 16);
-      voff[u] = (unsigned)(row * p.ldx + 16 * min(cc, GKC / 16 - 1));
-    } else if (j < RX_PIECES + 2) {  // dl chunk (clamped: chunks past 8 C repeat the last one into unused bytes)
-      voff[u] = 16u * (unsigned)min(64 * (j - RX_PIECES) + lane, 8 * C - 1);
-    } else {
-      voff[u] = 16u * (unsigned)min(lane, 8 * NW - 1);  // ReLU-bit chunk
-    }
+  for (int u = 0; u < 3; ++u) {  // pixel chunk ci: row ci / 50, 16-B column chunk ci % 50 (49 = pad: repeats 48)
+    const int ci = 64 * (wave + 8 * u) + lane, row = ci / (RX_PITCH / 16), cc = ci % (RX_PITCH / 16);
+    voff[u] = (unsigned)(row * p.ldx + 16 * min(cc, GKC / 16 - 1));
   }
-  auto issue = [&](int kt) {
-    unsigned char* st = rsm + (kt % RNS) * RSTAGE;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = wave + 8 * u;
-      if (j < RX_PIECES) bdma16_asm(rx, voff[u], (unsigned)kt * xstep, st + 1024 * j);
-      else if (j < RX_PIECES + 2) bdma16_asm(rdl, voff[u], (unsigned)kt * dlstep, st + 1024 * j);
-      else if (j < RPIECES) bdma16_asm(rmk, voff[u], (unsigned)kt * mkstep, st + 1024 * j);
-    }
+  voff[3] = 0u;
+  if (wave == 0) {
+    const int ci = 64 * (RX_PIECES - 1) + lane, row = ci / (RX_PITCH / 16), cc = ci % (RX_PITCH / 16);
+    voff[3] = (unsigned)(row * p.ldx + 16 * min(cc, GKC / 16 - 1));
+    r3 = rx;
+    step3 = xstep;
+  } else if (wave < 3) {  // dl chunk (clamped: chunks past 8 C repeat the last one into unused bytes)
+    voff[3] = 16u * (unsigned)min(64 * (wave - 1) + lane, 8 * C - 1);
+    r3 = dma_rsrc4(p.dl + (size_t)r0 * C, (unsigned)((p.M - r0) * C * 4));
+    step3 = GBK * C * 4;
+  } else if (wave == 3) {
+    voff[3] = 16u * (unsigned)min(lane, 8 * NW - 1);  // ReLU-bit chunk
+    r3 = dma_rsrc4(p.mask + (size_t)r0 * NW, (unsigned)((p.M - r0) * NW * 4));
+    step3 = GBK * NW * 4;
+  }
+  // the 4th piece's LDS destination: wave 0 the x stage, waves 1..3 the side stage, waves 4..7 the scratch KiB
+  auto dst3 = [&](int kx, int ks) -> unsigned char* {
+    if (wave == 0) return rsm + (kx & (RNS - 1)) * RX_STAGE + 1024 * (RX_PIECES - 1);
+    if (wave < 4) return rsm + RS_OFF + (ks & (RNS - 1)) * RS_STAGE + 1024 * (wave - 1);
+    return rsm + RSCR_OFF;
   };
-  // wait until this wave's pieces of a K-step have landed while `later` (0..2) younger K-steps stay in flight
-  // (waves 0..3 issue 4 pieces per K-step, waves 4..7 three)
-  auto wait_dma = [&](int later) {
-    if (later >= 2) {
-      if (wave < 4) wait_vm<8>();
-      else wait_vm<6>();
-    } else if (later == 1) {
-      if (wave < 4) wait_vm<4>();
-      else wait_vm<3>();
-    } else {
-      wait_vm<0>();
-    }
+  auto issue_x3 = [&](int kx) {  // the three pixel pieces of K-step kx
+    unsigned char* st = rsm + (kx & (RNS - 1)) * RX_STAGE;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) bdma16_asm(rx, voff[u], (unsigned)kx * xstep, st + 1024 * (wave + 8 * u));
+  };
+  // group of K-step kt of the steady loop: pixels of kx = kt + 3 and side data of ks = kt + 4 (null past the end)
+  auto issue_group = [&](int kx, int ks, bool side_ok) {
+    issue_x3(kx);
+    const dma_i32x4 r = (wave == 0 || side_ok) ? r3 : rnull;
+    bdma16_asm(r, voff[3], (unsigned)(wave == 0 ? kx : ks) * step3, dst3(kx, ks));
   };
 
   // dz tile of wave w: rows 16 (w >> 2) + (lane & 15), hidden 16 (w & 3) + 4 (lane >> 4) .. +3 (as u8_wgrad_kernel<2>)
@@ -1153,9 +1172,12 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
   u16* dzb = reinterpret_cast<u16*>(rsm + RDZ_OFF);
   const int doff = fr * GDP + (((fc >> 2) ^ dz_swz(fr)) << 2);
   auto build_dz = [&](int kt) {
-    const unsigned char* st = rsm + (kt % RNS) * RSTAGE;
-    const float* sdl = reinterpret_cast<const float*>(st + RDL_OFF) + fr * C;
-    const unsigned bits = reinterpret_cast<const unsigned*>(st + RMK_OFF)[fr * NW + mword];
+    if constexpr (MODE == 1) {
+      if (kt > 1) return;
+    }
+    const unsigned char* st = rsm + RS_OFF + (kt & (RNS - 1)) * RS_STAGE;
+    const float* sdl = reinterpret_cast<const float*>(st) + fr * C;
+    const unsigned bits = reinterpret_cast<const unsigned*>(st + 2048)[fr * NW + mword];
     float d4[4];
     const int g = lane >> 4;
 #pragma unroll
@@ -1173,7 +1195,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
       hi[e] = __builtin_bit_cast(u16, h);
       lo[e] = __builtin_bit_cast(u16, static_cast<_Float16>(x - static_cast<float>(h)));
     }
-    u16* B = dzb + (kt & 1) * GNPL * GD_U16;
+    u16* B = dzb + (kt % 3) * RDZ_BUF;
     *reinterpret_cast<u16x4*>(B + doff) = hi;
     *reinterpret_cast<u16x4*>(B + doff + GD_U16) = lo;
   };
@@ -1186,52 +1208,88 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < NCT; ++j) acc[i][j] = f32x16{};
-    auto compute = [&](int kt) {
-      const unsigned char* X8 = rsm + (kt % RNS) * RSTAGE;
-      const u16* D = dzb + (kt & 1) * GNPL * GD_U16;
+    // the fragments of one k-substep: dz planes (2 hidden tiles x 2 planes) and the wave's pixel tiles
+    struct Frag {
+      f16x8 a[2][GNPL];
+      f16x8 b[NCT];
+    };
+    auto load = [&](int kt, int s, Frag& f) {
+      const unsigned char* X8 = rsm + (kt & (RNS - 1)) * RX_STAGE;
+      const u16* D = dzb + (kt % 3) * RDZ_BUF;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        f16x8 a[2][GNPL];
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int pl = 0; pl < GNPL; ++pl) f.a[i][pl] = frag_tr_dz<GDP>(D + pl * GD_U16, 32 * i, s, lane);
 #pragma unroll
-          for (int pl = 0; pl < GNPL; ++pl) a[i][pl] = frag_tr_dz<GDP>(D + pl * GD_U16, 32 * i, s, lane);
+      for (int j = 0; j < NCT; ++j) f.b[j] = frag_x8<MODE == 2>(X8, 32 * (ct0 + j), s, lane);
+    };
+    auto mma = [&](const Frag& f) {
 #pragma unroll
-        for (int j = 0; j < NCT; ++j) {
-          const f16x8 b = frag_x8(X8, 32 * (ct0 + j), s, lane);
+      for (int j = 0; j < NCT; ++j)
 #pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            acc[i][j] = mfma(a[i][1], b, acc[i][j]);  // lo
-            acc[i][j] = mfma(a[i][0], b, acc[i][j]);  // hi
+        for (int i = 0; i < 2; ++i) {
+          if constexpr (MODE == 4) {  // no MFMA: keep the fragments alive with one VALU add each
+            acc[i][j][0] += (float)(f.a[i][1][0] + f.a[i][0][1] + f.b[j][i]);
+          } else {
+            acc[i][j] = mfma(f.a[i][1], f.b[j], acc[i][j]);  // lo
+            acc[i][j] = mfma(f.a[i][0], f.b[j], acc[i][j]);  // hi
           }
         }
-      }
     };
-    // K-step kt: its DMA was issued 3 K-steps ahead; at the top of step kt the pieces of kt + 1 are waited for (their
-    // dl / bits become dz planes in this step), the barrier publishes them and frees stage (kt - 1) % RNS and dz
-    // buffer (kt + 1) & 1 (last read by step kt - 1), which kt + 3's DMA and kt + 1's dz then reuse
-    // W2 values in registers before the first DMA: the compiler's own wait for them (it does not see the asm DMAs)
-    // would otherwise be a vmcnt(0) behind three K-steps of DMA
+    // prologue: side data of K-steps 0..3 (one group), pixels of 0, 1, 2 (a group each); wait for all but the last
+    // pixel group, build dz 0 and 1, publish them, read k-substep 0 of K-step 0
+    // (W2 values in registers first: the compiler's own wait for them would be a vmcnt(0) behind the DMA it cannot see)
     asm volatile("" ::"v"(w4[0]), "v"(w4[1]), "v"(w4[2]), "v"(w4[3]));
-    issue(0);
-    if (nk > 1) issue(1);
-    if (nk > 2) issue(2);
-    wait_dma(min(nk - 1, 2));
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      bdma16_asm(wave > 0 && wave < 4 && ks < nk ? r3 : rnull, voff[3], (unsigned)ks * step3,
+                 wave > 0 && wave < 4 ? dst3(0, ks) : rsm + RSCR_OFF);
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      issue_x3(kx < nk ? kx : 0);  // (K-steps past the end re-read step 0 into unused stages)
+      bdma16_asm(wave == 0 ? r3 : rnull, voff[3], (unsigned)(kx < nk ? kx : 0) * step3,
+                 wave == 0 ? dst3(kx, 0) : rsm + RSCR_OFF);
+    }
+    wait_vm<4>();
     __syncthreads();
     build_dz(0);
+    if (nk > 1) build_dz(1);
+    __syncthreads();
+    Frag f0, f1;
+    load(0, 0, f0);
     U8W_STAMP(3, __builtin_amdgcn_s_memtime);
-    for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) wait_dma(kt + 2 < nk ? 1 : 0);
-      __syncthreads();
+    // K-step kt (one barrier, at its end): pixel group kt + 3 and side group kt + 4 issued; k-substep 1 read and both
+    // substeps' MFMAs; dz of kt + 2 built; k-substep 0 of kt + 1 read (published by the barrier that ended kt - 1).
+    // The barrier ending kt waits for every DMA group but kt's own: pixels of kt + 2 and side data of kt + 3, which
+    // step kt + 1 reads. Stage reuse: pixel stage (kt + 3) % 4 was last read in step kt - 1, side stage (kt + 4) % 4 in
+    // step kt - 2, dz buffer (kt + 2) % 3 in step kt - 1.
+    int kt = 0;
+    for (; kt + 3 < nk; ++kt) {
+      issue_group(kt + 3, kt + 4, kt + 4 < nk);
+      load(kt, 1, f1);
+      mma(f0);
+      build_dz(kt + 2);
+      mma(f1);
+      load(kt + 1, 0, f0);
 #ifdef SDML_KERNEL_EXPERIMENTS
-      if (kt == 1 || kt == 9 || kt == 17) U8W_STAMP(5 + (kt - 1) / 8 * 2, __builtin_amdgcn_s_memtime);  // after barrier
+      if (kt == 0 || kt == 8 || kt == 16) U8W_STAMP(4 + kt / 8 * 2, __builtin_amdgcn_s_memtime);  // before barrier
 #endif
-      if (kt + 3 < nk) issue(kt + 3);
-      if (kt + 1 < nk) build_dz(kt + 1);
-      compute(kt);
+      wait_vm<4>();
+      if constexpr (MODE != 3) __syncthreads();
 #ifdef SDML_KERNEL_EXPERIMENTS
-      if (kt == 0 || kt == 8 || kt == 16) U8W_STAMP(4 + kt / 8 * 2, __builtin_amdgcn_s_memtime);  // after compute
+      if (kt == 0 || kt == 8 || kt == 16) U8W_STAMP(5 + kt / 8 * 2, __builtin_amdgcn_s_memtime);  // after barrier
 #endif
+    }
+    for (; kt < nk; ++kt) {  // the last three K-steps: no further DMA
+      load(kt, 1, f1);
+      mma(f0);
+      if (kt + 2 < nk) build_dz(kt + 2);
+      mma(f1);
+      if (kt + 1 < nk) {
+        load(kt + 1, 0, f0);
+        wait_vm<0>();
+        __syncthreads();
+      }
     }
     U8W_STAMP(10, __builtin_amdgcn_s_memtime);
     wgrad_store_tile<NCT>(p, acc, split, n0, ct0, lane, out_scale);
@@ -1424,7 +1482,19 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigne
   // the DMA-ring form: ReLU bits, one DMA piece of them and two of dl rows per K-step, 16-B aligned sources
   const bool ring = mask && !ilv && knob(KNOB_U8_WGRAD_RING) != 0 && N <= 256 && C <= 16 &&
                     (reinterpret_cast<uintptr_t>(dl) & 15) == 0 && (reinterpret_cast<uintptr_t>(mask) & 15) == 0;
-  if (ring) hipLaunchKernelGGL(u8_wgrad_ring_kernel, wgrid, dim3(GT), 0, stream, p);
+  if (ring) {
+#ifdef SDML_KERNEL_EXPERIMENTS
+    switch (knob(KNOB_U8_VARIANT)) {
+      case 1: hipLaunchKernelGGL(u8_wgrad_ring_kernel<1>, wgrid, dim3(GT), 0, stream, p); break;
+      case 2: hipLaunchKernelGGL(u8_wgrad_ring_kernel<2>, wgrid, dim3(GT), 0, stream, p); break;
+      case 3: hipLaunchKernelGGL(u8_wgrad_ring_kernel<3>, wgrid, dim3(GT), 0, stream, p); break;
+      case 4: hipLaunchKernelGGL(u8_wgrad_ring_kernel<4>, wgrid, dim3(GT), 0, stream, p); break;
+      default: hipLaunchKernelGGL(u8_wgrad_ring_kernel<0>, wgrid, dim3(GT), 0, stream, p);
+    }
+#else
+    hipLaunchKernelGGL(u8_wgrad_ring_kernel<0>, wgrid, dim3(GT), 0, stream, p);
+#endif
+  }
   else if (mask && ilv) hipLaunchKernelGGL((u8_wgrad_kernel<2, true>), wgrid, dim3(GT), 0, stream, p);
   else if (mask) hipLaunchKernelGGL((u8_wgrad_kernel<2, false>), wgrid, dim3(GT), 0, stream, p);
   else if (ilv) hipLaunchKernelGGL((u8_wgrad_kernel<1, true>), wgrid, dim3(GT), 0, stream, p);

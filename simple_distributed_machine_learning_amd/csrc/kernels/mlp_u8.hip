@@ -1084,6 +1084,13 @@ __device__ __forceinline__ f16x8 frag_x8(const unsigned char* img, int c0, int s
   return widen8h((unsigned)v[0], (unsigned)v[1]);
 }
 
+// the same 8 bytes, not widened
+__device__ __forceinline__ i32x2 frag_x8_raw(const unsigned char* img, int c0, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const unsigned char* a = img + (16 * s + 8 * (g >> 1) + (i >> 1)) * RX_PITCH + c0 + 16 * (g & 1) + 8 * (i & 1);
+  return __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2*)(a));
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -1091,7 +1098,10 @@ __device__ __forceinline__ void wait_vm() {
 
 // MODE (experiments builds, knob U8_VARIANT; wrong results by design): 1 no dz build in the K loop, 2 no byte
 // widening (raw bytes as fp16 bits), 3 no barrier in the K loop, 4 no MFMA
-template <int MODE = 0>
+// BAL (knob U8_WGRAD_BAL): every wave owns 3 of the 24 full 32-column tiles, and the last 16 columns (768..783) run as
+// 16x16x32 MFMAs on waves 4..7 (16 hidden each): every SIMD carries 6 tiles + 1/4 half tile per K-step instead of 7 or
+// 6 (wave 0 owned 4 tiles). Those 16 columns then sum in a different MFMA order (fp32-equal, not bit-identical).
+template <int MODE = 0, bool BAL = false>
 __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char rsm[RSMEM];
   const int t = threadIdx.x, lane = t & 63;
@@ -1171,21 +1181,28 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
   f32x4 bsum = {0.f, 0.f, 0.f, 0.f};
   u16* dzb = reinterpret_cast<u16*>(rsm + RDZ_OFF);
   const int doff = fr * GDP + (((fc >> 2) ^ dz_swz(fr)) << 2);
-  auto build_dz = [&](int kt) {
-    if constexpr (MODE == 1) {
-      if (kt > 1) return;
-    }
+  // dz build of K-step kt in two parts: the side-data reads (issued early in a K-step) and the fp32 MFMAs, split and
+  // plane stores (after the first substep's MFMAs)
+  struct DzIn {
+    float d4[4];
+    unsigned bits;
+  };
+  auto build_dz_load = [&](int kt, DzIn& in) {
     const unsigned char* st = rsm + RS_OFF + (kt & (RNS - 1)) * RS_STAGE;
     const float* sdl = reinterpret_cast<const float*>(st) + fr * C;
-    const unsigned bits = reinterpret_cast<const unsigned*>(st + 2048)[fr * NW + mword];
-    float d4[4];
+    in.bits = reinterpret_cast<const unsigned*>(st + 2048)[fr * NW + mword];
     const int g = lane >> 4;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const float v = sdl[min(4 * g + kk, C - 1)];
-      d4[kk] = 4 * g + kk < C ? v : 0.f;
+      in.d4[kk] = 4 * g + kk < C ? v : 0.f;
     }
-    const f32x4 dv = fd_dz_bits(w4, d4, (bits >> mshift) & 15u);
+  };
+  auto build_dz_finish = [&](int kt, const DzIn& in) {
+    if constexpr (MODE == 1) {
+      if (kt > 1) return;
+    }
+    const f32x4 dv = fd_dz_bits(w4, in.d4, (in.bits >> mshift) & 15u);
     bsum += dv;
     u16x4 hi, lo;
 #pragma unroll
@@ -1199,11 +1216,51 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
     *reinterpret_cast<u16x4*>(B + doff) = hi;
     *reinterpret_cast<u16x4*>(B + doff + GD_U16) = lo;
   };
+  auto build_dz = [&](int kt) {
+    DzIn in;
+    build_dz_load(kt, in);
+    build_dz_finish(kt, in);
+  };
 
-  auto run = [&](auto nct_c) {
+  // EARLY: where the wave builds its dz tile in a K-step - after the first substep's MFMAs (waves 0..3) or after the
+  // second (waves 4..7). The two waves of a SIMD (w, w + 4) then never wait on the build's dependent chain (LDS reads,
+  // four fp32 MFMAs, the split) at the same time: one issues MFMAs while the other builds.
+  auto run = [&](auto nct_c, auto half_c, auto early_c) {
     constexpr int NCT = decltype(nct_c)::value;
-    const int ct0 = NCT == 4 ? 0 : 4 + 3 * (wave - 1);  // first 32-column tile
+    constexpr bool HALF = decltype(half_c)::value;  // BAL: this wave's 16 hidden of columns 768..783
+    constexpr bool EARLY = decltype(early_c)::value;
+    const int ct0 = BAL ? 3 * wave : NCT == 4 ? 0 : 4 + 3 * (wave - 1);  // first 32-column tile
     f32x16 acc[2][NCT];
+    f32x4 hacc = {0.f, 0.f, 0.f, 0.f};
+    f16x8 ha[GNPL], hb;
+    // 16x16x32 operands of the half tile for the whole K-step (k-rows 8 (lane >> 4) + j): dz rows through two tr16
+    // reads (hidden 16 (wave - 4) + (lane & 15)), pixel column 768 + (lane & 15) through one tr8 read
+    auto load_half = [&](int kt) {
+      if constexpr (HALF) {
+        const unsigned char* X8 = rsm + (kt & (RNS - 1)) * RX_STAGE;
+        const u16* D = dzb + (kt % 3) * RDZ_BUF;
+        const int g = lane >> 4, i = lane & 15;
+        const int r = 8 * g + (i >> 2), col = 16 * (wave - 4) + 4 * (i & 3);
+#pragma unroll
+        for (int pl = 0; pl < GNPL; ++pl) {
+          const s16x4 lo = tr16(D + pl * GD_U16 + r * GDP + (((col >> 2) ^ dz_swz(r)) << 2));
+          const s16x4 hi = tr16(D + pl * GD_U16 + (r + 4) * GDP + (((col >> 2) ^ dz_swz(r + 4)) << 2));
+          bf16x8 f;
+          f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+          f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+          ha[pl] = __builtin_bit_cast(f16x8, f);
+        }
+        const unsigned char* xa = X8 + (8 * g + (i >> 1)) * RX_PITCH + 768 + 8 * (i & 1);
+        const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2*)(xa));
+        hb = widen8h((unsigned)v[0], (unsigned)v[1]);
+      }
+    };
+    auto mma_half = [&]() {
+      if constexpr (HALF) {
+        hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha[1], hb, hacc, 0, 0, 0);  // lo
+        hacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha[0], hb, hacc, 0, 0, 0);  // hi
+      }
+    };
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1211,7 +1268,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
     // the fragments of one k-substep: dz planes (2 hidden tiles x 2 planes) and the wave's pixel tiles
     struct Frag {
       f16x8 a[2][GNPL];
-      f16x8 b[NCT];
+      i32x2 b[NCT];  // raw pixel bytes (widened next to their MFMAs)
     };
     auto load = [&](int kt, int s, Frag& f) {
       const unsigned char* X8 = rsm + (kt & (RNS - 1)) * RX_STAGE;
@@ -1221,20 +1278,28 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
 #pragma unroll
         for (int pl = 0; pl < GNPL; ++pl) f.a[i][pl] = frag_tr_dz<GDP>(D + pl * GD_U16, 32 * i, s, lane);
 #pragma unroll
-      for (int j = 0; j < NCT; ++j) f.b[j] = frag_x8<MODE == 2>(X8, 32 * (ct0 + j), s, lane);
+      for (int j = 0; j < NCT; ++j) f.b[j] = frag_x8_raw(X8, 32 * (ct0 + j), s, lane);
     };
     auto mma = [&](const Frag& f) {
 #pragma unroll
-      for (int j = 0; j < NCT; ++j)
+      for (int j = 0; j < NCT; ++j) {
+        f16x8 b;
+        if constexpr (MODE == 2) {  // (timing: raw bytes as fp16 bits)
+          const u32x4 r = {(unsigned)f.b[j][0], (unsigned)f.b[j][1], (unsigned)f.b[j][0], (unsigned)f.b[j][1]};
+          b = __builtin_bit_cast(f16x8, r);
+        } else {
+          b = widen8h((unsigned)f.b[j][0], (unsigned)f.b[j][1]);
+        }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           if constexpr (MODE == 4) {  // no MFMA: keep the fragments alive with one VALU add each
-            acc[i][j][0] += (float)(f.a[i][1][0] + f.a[i][0][1] + f.b[j][i]);
+            acc[i][j][0] += (float)(f.a[i][1][0] + f.a[i][0][1] + b[i]);
           } else {
-            acc[i][j] = mfma(f.a[i][1], f.b[j], acc[i][j]);  // lo
-            acc[i][j] = mfma(f.a[i][0], f.b[j], acc[i][j]);  // hi
+            acc[i][j] = mfma(f.a[i][1], b, acc[i][j]);  // lo
+            acc[i][j] = mfma(f.a[i][0], b, acc[i][j]);  // hi
           }
         }
+      }
     };
     // prologue: side data of K-steps 0..3 (one group), pixels of 0, 1, 2 (a group each); wait for all but the last
     // pixel group, build dz 0 and 1, publish them, read k-substep 0 of K-step 0
@@ -1267,24 +1332,37 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
     for (; kt + 3 < nk; ++kt) {
       issue_group(kt + 3, kt + 4, kt + 4 < nk);
       load(kt, 1, f1);
+      load_half(kt);
+      DzIn dzi;
+      build_dz_load(kt + 2, dzi);
       mma(f0);
-      build_dz(kt + 2);
+      if constexpr (EARLY) build_dz_finish(kt + 2, dzi);
       mma(f1);
+      mma_half();
+      if constexpr (!EARLY) build_dz_finish(kt + 2, dzi);
       load(kt + 1, 0, f0);
 #ifdef SDML_KERNEL_EXPERIMENTS
       if (kt == 0 || kt == 8 || kt == 16) U8W_STAMP(4 + kt / 8 * 2, __builtin_amdgcn_s_memtime);  // before barrier
 #endif
+      // The barrier publishes this step's dz-plane stores and the DMA of kt + 2 (wait_vm). Not __syncthreads: its
+      // fence would also wait for the substep-0 reads of kt + 1 just issued, which may stay in flight across it (what
+      // they read is not rewritten before the barrier ending kt + 1). The plane stores precede those 8 + NCT reads in
+      // program order (the compiler cannot separate their addresses) and LDS operations complete in order, so
+      // lgkmcnt(8 + NCT) covers the stores.
       wait_vm<4>();
-      if constexpr (MODE != 3) __syncthreads();
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(8 + NCT) : "memory");
+      if constexpr (MODE != 3) __builtin_amdgcn_s_barrier();
 #ifdef SDML_KERNEL_EXPERIMENTS
       if (kt == 0 || kt == 8 || kt == 16) U8W_STAMP(5 + kt / 8 * 2, __builtin_amdgcn_s_memtime);  // after barrier
 #endif
     }
     for (; kt < nk; ++kt) {  // the last three K-steps: no further DMA
       load(kt, 1, f1);
+      load_half(kt);
       mma(f0);
       if (kt + 2 < nk) build_dz(kt + 2);
       mma(f1);
+      mma_half();
       if (kt + 1 < nk) {
         load(kt + 1, 0, f0);
         wait_vm<0>();
@@ -1293,10 +1371,23 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
     }
     U8W_STAMP(10, __builtin_amdgcn_s_memtime);
     wgrad_store_tile<NCT>(p, acc, split, n0, ct0, lane, out_scale);
+    if constexpr (HALF) {  // C map of 16x16: column lane & 15, rows 4 (lane >> 4) + v
+      float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        out[(size_t)(n0 + 16 * (wave - 4) + 4 * (lane >> 4) + v) * GKC + 768 + (lane & 15)] = hacc[v] * out_scale;
+    }
     U8W_STAMP(11, __builtin_amdgcn_s_memtime);
   };
-  if (wave == 0) run(std::integral_constant<int, 4>{});
-  else run(std::integral_constant<int, 3>{});
+  using I3 = std::integral_constant<int, 3>;
+  if constexpr (BAL) {
+    if (wave >= 4) run(I3{}, std::true_type{}, std::false_type{});
+    else run(I3{}, std::false_type{}, std::true_type{});
+  } else {
+    if (wave == 0) run(std::integral_constant<int, 4>{}, std::false_type{}, std::true_type{});
+    else if (wave < 4) run(I3{}, std::false_type{}, std::true_type{});
+    else run(I3{}, std::false_type{}, std::false_type{});
+  }
   __syncthreads();
   wgrad_store_bias<2>(p, bsum, split, n0, t, reinterpret_cast<float*>(rsm));
   U8W_STAMP(12, __builtin_amdgcn_s_memtime);
@@ -1489,10 +1580,14 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigne
       case 2: hipLaunchKernelGGL(u8_wgrad_ring_kernel<2>, wgrid, dim3(GT), 0, stream, p); break;
       case 3: hipLaunchKernelGGL(u8_wgrad_ring_kernel<3>, wgrid, dim3(GT), 0, stream, p); break;
       case 4: hipLaunchKernelGGL(u8_wgrad_ring_kernel<4>, wgrid, dim3(GT), 0, stream, p); break;
-      default: hipLaunchKernelGGL(u8_wgrad_ring_kernel<0>, wgrid, dim3(GT), 0, stream, p);
+      case 5: hipLaunchKernelGGL((u8_wgrad_ring_kernel<0, true>), wgrid, dim3(GT), 0, stream, p); break;
+      default:
+        if (knob(KNOB_U8_WGRAD_BAL)) hipLaunchKernelGGL((u8_wgrad_ring_kernel<0, true>), wgrid, dim3(GT), 0, stream, p);
+        else hipLaunchKernelGGL((u8_wgrad_ring_kernel<0, false>), wgrid, dim3(GT), 0, stream, p);
     }
 #else
-    hipLaunchKernelGGL(u8_wgrad_ring_kernel<0>, wgrid, dim3(GT), 0, stream, p);
+    if (knob(KNOB_U8_WGRAD_BAL)) hipLaunchKernelGGL((u8_wgrad_ring_kernel<0, true>), wgrid, dim3(GT), 0, stream, p);
+    else hipLaunchKernelGGL((u8_wgrad_ring_kernel<0, false>), wgrid, dim3(GT), 0, stream, p);
 #endif
   }
   else if (mask && ilv) hipLaunchKernelGGL((u8_wgrad_kernel<2, true>), wgrid, dim3(GT), 0, stream, p);

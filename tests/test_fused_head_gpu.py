@@ -318,3 +318,36 @@ def test_wgrad_dma_ring_bit_identical_to_register_staged(M, C, Nh):
     want = dz.t() @ (x8.double() / 255.0)
     got = bufs[1][:Nh * KD].view(Nh, KD).double() - g0[:Nh * KD].view(Nh, KD).double()
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("M,C,Nh", [(4096 + 96, 10, 128), (131072, 10, 128), (8192, 16, 256)])
+def test_wgrad_ring_balanced_tiles(M, C, Nh):
+    """Knob U8_WGRAD_BAL: 3 full column tiles per wave and the last 16 columns on 16x16x32 MFMAs (waves 4..7). Columns
+    0..767 and the bias keep the unbalanced ring kernel's MFMA sequence (bit-identical); columns 768..783 sum in a
+    different MFMA order (fp32-equal)."""
+    from simple_distributed_machine_learning_amd import _native
+
+    K = _native.kernels()
+    x8 = pixels(M, 61)
+    h = rnd(M, Nh, seed=62).relu()
+    dl = rnd(M, C, seed=63, scale=1e-3)
+    w2 = rnd(C, Nh, seed=64, scale=0.1)
+    bits = ops.relu_bits(h)
+    outs = []
+    try:
+        for bal in (0, 1):
+            K.set_knob("U8_WGRAD_BAL", bal)
+            b = torch.zeros(Nh * KD + Nh, device=DEV)
+            ops.linear_wgrad_u8_dl(x8, dl, w2, bits, b[:Nh * KD].view(Nh, KD), b[Nh * KD:])
+            torch.cuda.synchronize()
+            outs.append(b)
+    finally:
+        K.reset_knobs()
+    g0, g1 = (o[:Nh * KD].view(Nh, KD) for o in outs)
+    assert torch.equal(g0[:, :768], g1[:, :768])
+    assert torch.equal(outs[0][Nh * KD:], outs[1][Nh * KD:])
+    # (a sum over M rows with cancellation: compare at the scale of the gradient's largest entries)
+    torch.testing.assert_close(g1[:, 768:], g0[:, 768:], rtol=1e-4, atol=1e-6 * float(g0.abs().max()))
+    dz = (dl.double() @ w2.double()) * (h > 0).double()
+    want = dz.t() @ (x8.double() / 255.0)
+    torch.testing.assert_close(g1.double(), want, rtol=1e-4, atol=1e-6)

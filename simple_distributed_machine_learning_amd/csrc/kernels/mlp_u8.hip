@@ -1097,7 +1097,9 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // MODE (experiments builds, knob U8_VARIANT; wrong results by design): 1 no dz build in the K loop, 2 no byte
-// widening (raw bytes as fp16 bits), 3 no barrier in the K loop, 4 no MFMA
+// widening (raw bytes as fp16 bits), 3 no barrier in the K loop, 4 no MFMA, 6 the DMA ring alone (no LDS reads,
+// no MFMA, no dz build in the K loop). Measured (tools/u8_wgrad_stamps.py, cycles per K-step, headline shape): normal
+// 2.85K, 1: 2.29K, 4: 2.24K, 6: 1.04K; fencing the K-step's phases off from the scheduler (sched_barrier) 3.42K.
 // BAL (knob U8_WGRAD_BAL): every wave owns 3 of the 24 full 32-column tiles, and the last 16 columns (768..783) run as
 // 16x16x32 MFMAs on waves 4..7 (16 hidden each): every SIMD carries 6 tiles + 1/4 half tile per K-step instead of 7 or
 // 6 (wave 0 owned 4 tiles). Those 16 columns then sum in a different MFMA order (fp32-equal, not bit-identical).
@@ -1331,16 +1333,18 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
     int kt = 0;
     for (; kt + 3 < nk; ++kt) {
       issue_group(kt + 3, kt + 4, kt + 4 < nk);
-      load(kt, 1, f1);
-      load_half(kt);
-      DzIn dzi;
-      build_dz_load(kt + 2, dzi);
-      mma(f0);
-      if constexpr (EARLY) build_dz_finish(kt + 2, dzi);
-      mma(f1);
-      mma_half();
-      if constexpr (!EARLY) build_dz_finish(kt + 2, dzi);
-      load(kt + 1, 0, f0);
+      if constexpr (MODE != 6) {  // (MODE 6, timing: the DMA ring alone)
+        load(kt, 1, f1);
+        load_half(kt);
+        DzIn dzi;
+        build_dz_load(kt + 2, dzi);
+        mma(f0);
+        if constexpr (EARLY) build_dz_finish(kt + 2, dzi);
+        mma(f1);
+        mma_half();
+        if constexpr (!EARLY) build_dz_finish(kt + 2, dzi);
+        load(kt + 1, 0, f0);
+      }
 #ifdef SDML_KERNEL_EXPERIMENTS
       if (kt == 0 || kt == 8 || kt == 16) U8W_STAMP(4 + kt / 8 * 2, __builtin_amdgcn_s_memtime);  // before barrier
 #endif
@@ -1580,6 +1584,7 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigne
       case 2: hipLaunchKernelGGL(u8_wgrad_ring_kernel<2>, wgrid, dim3(GT), 0, stream, p); break;
       case 3: hipLaunchKernelGGL(u8_wgrad_ring_kernel<3>, wgrid, dim3(GT), 0, stream, p); break;
       case 4: hipLaunchKernelGGL(u8_wgrad_ring_kernel<4>, wgrid, dim3(GT), 0, stream, p); break;
+      case 6: hipLaunchKernelGGL(u8_wgrad_ring_kernel<6>, wgrid, dim3(GT), 0, stream, p); break;
       case 5: hipLaunchKernelGGL((u8_wgrad_ring_kernel<0, true>), wgrid, dim3(GT), 0, stream, p); break;
       default:
         if (knob(KNOB_U8_WGRAD_BAL)) hipLaunchKernelGGL((u8_wgrad_ring_kernel<0, true>), wgrid, dim3(GT), 0, stream, p);

@@ -1111,6 +1111,9 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
   const int L = blockIdx.x, G8 = 8 * p.groups;
   const int split = p.xcd ? (L / G8) * 8 + L % 8 : L / p.groups;
   if (split >= p.splits) return;
+  // waves 4..7 (each SIMD's second wave) at priority 1 (knob U8_WGRAD_PRIO): stamped K-steps 2.98K vs 3.21K cycles on
+  // one box, but the un-stamped kernel and the headline step the same (0.1569 / 0.1567 vs 0.1574 / 0.1566 ms): off
+  if (p.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   U8W_STAMP(0, __builtin_amdgcn_s_memrealtime);
   U8W_STAMP(1, __builtin_amdgcn_s_memtime);
   const int n0 = (p.g0 + (p.xcd ? (L % G8) / 8 : L % p.groups)) * GHN;

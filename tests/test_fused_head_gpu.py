@@ -351,3 +351,34 @@ def test_wgrad_ring_balanced_tiles(M, C, Nh):
     dz = (dl.double() @ w2.double()) * (h > 0).double()
     want = dz.t() @ (x8.double() / 255.0)
     torch.testing.assert_close(g1.double(), want, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("ring", [0, 1])
+def test_wgrad_hidden_group_ranges_match_the_whole_gradient(ring):
+    """linear_wgrad_u8_dl(groups=(g_first, g_count, blocks)) - the data-parallel step's two hidden-unit ranges
+    (SDML_DP_SPLIT) - on both kernel forms: each range writes only its rows of gW / entries of gb, and the two ranges
+    together equal the one-launch gradient to fp32 summation order (the row splits differ)."""
+    from simple_distributed_machine_learning_amd import _native
+
+    K = _native.kernels()
+    M, C, Nh = 16384, 10, 128
+    x8 = pixels(M, 71)
+    h = rnd(M, Nh, seed=72).relu()
+    dl = rnd(M, C, seed=73, scale=1e-3)
+    w2 = rnd(C, Nh, seed=74, scale=0.1)
+    bits = ops.relu_bits(h)
+    try:
+        K.set_knob("U8_WGRAD_RING", ring)
+        full = torch.zeros(Nh * KD + Nh, device=DEV)
+        ops.linear_wgrad_u8_dl(x8, dl, w2, bits, full[:Nh * KD].view(Nh, KD), full[Nh * KD:])
+        part = torch.zeros(Nh * KD + Nh, device=DEV)
+        gw, gb = part[:Nh * KD].view(Nh, KD), part[Nh * KD:]
+        ops.linear_wgrad_u8_dl(x8, dl, w2, bits, gw, gb, groups=(0, 1, 128))
+        torch.cuda.synchronize()
+        # (gW += ...: range 1's gradient is nonzero, so a touch would show)
+        assert bool((gw[64:] == 0).all()) and bool((gb[64:] == 0).all()) and bool((gb[:64] != 0).all())
+        ops.linear_wgrad_u8_dl(x8, dl, w2, bits, gw, gb, groups=(1, 1, 128))
+        torch.cuda.synchronize()
+    finally:
+        K.reset_knobs()
+    torch.testing.assert_close(part, full, rtol=1e-5, atol=1e-6 * float(full.abs().max()))

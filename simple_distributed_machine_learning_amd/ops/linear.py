@@ -17,9 +17,9 @@ the bias gradient with a generic reduction. This module avoids both:
 When a parameter has no ``.grad`` yet (standalone use), the gradients are returned to
 autograd in the usual way. CPU tensors and non-bf16 dtypes keep the plain ``F.linear``
 path. The forward / input-gradient GEMMs of a plain Linear are library GEMMs (hipBLASLt, faster at these
-shapes than gemm_bf16.hip's current schedule: tools/bench_gemm_bf16.py); with SDML_FUSED_GELU_GEMM=1 the MLP's
-c_fc forward and c_proj input gradient run on gemm_bf16.hip with the GELU fused into their epilogues
-(:func:`mlp_gelu`).
+shapes than gemm_bf16.hip's current schedule: tools/bench_gemm_bf16.py); the MLP's c_fc forward and c_proj input
+gradient run on gemm_bf16.hip with the GELU fused into their epilogues (:func:`mlp_gelu`; SDML_FUSED_GELU_GEMM=0
+puts them back on the library).
 """
 from __future__ import annotations
 
@@ -162,12 +162,14 @@ class _MLPFn(torch.autograd.Function):
 
 
 def mlp_gelu(x, w1, b1, w2, b2):
-    """c_proj(gelu_tanh(c_fc(x))). SDML_FUSED_GELU_GEMM=1: the fused-epilogue GEMMs (gemm_bf16.hip) on ROCm
-    bf16; default: library GEMMs + the standalone GELU kernels (gpt2_ops.hip), measured faster on one MI355X
-    at 16 x 1024 tokens (fused c_fc 124.5 us vs 77 + GELU; fused c_proj dX 160 us vs 78 + GELU':
-    profiles/r3_gpt2_kernel_stats.txt), because the GEMM mainloop still trails hipBLASLt's."""
+    """c_proj(gelu_tanh(c_fc(x))). On ROCm bf16 (default; SDML_FUSED_GELU_GEMM=0 turns it off): the c_fc forward
+    and the c_proj input gradient on gemm_bf16.hip with the GELU / GELU' fused into their epilogues (no standalone
+    GELU passes), the other two on hipBLASLt. Round 4, one MI355X, GPT-2 step at 16 x 1024 tokens: 21.82 vs
+    21.79 ms with library GEMMs + the standalone GELU kernels (profiles/r4_gpt2_fused_gelu_ab.jsonl) - the 4-phase
+    NT mainloop still trails hipBLASLt's per GEMM (99.5 vs 76.7 us at c_fc), the fusion pays the difference back.
+    (Round 3, before the 4-phase loop: fused c_fc 124.5 us vs 77 + GELU, so it was off.)"""
     if (x.is_cuda and x.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16 and b1 is not None
-            and b2 is not None and (_HAND or os.environ.get("SDML_FUSED_GELU_GEMM", "0") == "1")):
+            and b2 is not None and (_HAND or os.environ.get("SDML_FUSED_GELU_GEMM", "1") == "1")):
         T, C = x.numel() // x.shape[-1], x.shape[-1]
         k = kernels()
         if (k.gemm_bf16_supported(T, w1.shape[0], C, C, C, False)

@@ -264,12 +264,21 @@ def main():
     sync()
     if engine.transport is not None:
         engine.transport.reset_counters()
+    # per-step device time: one event before every timed step and one after the last, recorded on the
+    # compute stream (host cost ~1 us each); read after the timed region. They describe the window the
+    # wall clock measures (first step vs steady state), they do not replace it.
+    evs = ([torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)] if dev.type == "cuda" else [])
     t0 = time.perf_counter()
     res = None
     for i in range(a.steps):
+        if evs:
+            evs[i].record()
         res = step(a.warmup + i)
+    if evs:
+        evs[a.steps].record()
     sync()
     el = time.perf_counter() - t0
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps)] if evs else []
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     sent = torch.tensor([float(engine.transport.bytes_sent if engine.transport else 0)], dtype=torch.float64,
                         device=dev)
@@ -337,6 +346,11 @@ def main():
             "baseline": BASELINE_NOTE,
             "final_loss": None if loss is None else round(loss, 5),
         }
+        if step_ms:  # rank 0's per-step device times (HIP events on the compute stream)
+            srt = sorted(step_ms)
+            out["step_ms_events"] = {"first": round(step_ms[0], 4), "median": round(srt[len(srt) // 2], 4),
+                                     "min": round(srt[0], 4), "max": round(srt[-1], 4),
+                                     "all": [round(x, 4) for x in step_ms]}
         print(json.dumps(out), flush=True)
     if world > 1:
         sync()

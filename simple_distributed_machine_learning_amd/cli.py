@@ -73,6 +73,8 @@ def add_engine_args(parser: argparse.ArgumentParser):
     g.add_argument("--backend", default="auto", choices=["auto", "nccl", "rccl", "gloo"])
     g.add_argument("--timeout", type=float, default=600.0, help="process-group timeout (s), finite")
     g.add_argument("--heartbeat", type=float, default=0.0, help="peer heartbeat timeout (s); 0 = off")
+    g.add_argument("--dropout", type=float, default=0.5,
+                   help="ref_cnn: Dropout2d / dropout probability (reference: 0.5; 0 makes a run deterministic)")
     g.add_argument("--eval_dropout", type=int, default=1,
                    help="ref_cnn: keep stage-1 dropout active in test() like the reference (1) or not (0)")
     g.add_argument("--ckpt_dir", default=None)

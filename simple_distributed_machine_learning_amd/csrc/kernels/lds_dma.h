@@ -30,8 +30,8 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, unsigned voff, 
 // them, waits for all of them. Reads through the ds_read_b64_tr_* builtins carry no alias information, so each
 // one got s_waitcnt vmcnt(0): a full drain of a multi-stage DMA ring in front of every fragment read. The pass
 // does not see an asm DMA; the caller then owns every wait on it (s_waitcnt vmcnt(N) and a barrier before the
-// block reads what it wrote). M0 (the LDS destination) is written here: the kernels that use this issue no other
-// M0-based instruction (check the assembly when adding one).
+// block reads what it wrote). M0 (the LDS destination) is written here and declared clobbered, so compiler-generated
+// M0 users (the builtin LDS-DMA forms, ds_*_addtid) reload it after the asm.
 typedef int dma_i32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ dma_i32x4 dma_rsrc4(const void* base, unsigned bytes) {
@@ -49,7 +49,7 @@ __device__ __forceinline__ void bdma16_asm(dma_i32x4 r, unsigned voff, unsigned 
       (unsigned)(unsigned long long)(const __attribute__((address_space(3))) void*)lds_block);
   asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(r),
                "s"(__builtin_amdgcn_readfirstlane(soff)), "s"(a)
-               : "memory");
+               : "memory", "m0");
 }
 
 }  // namespace sdml

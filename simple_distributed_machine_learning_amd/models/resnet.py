@@ -12,8 +12,9 @@ only: every convolution in csrc/kernels/conv_bf16.hip — the stride-1 3x3 convo
 and weight gradients), the stride-2 3x3 and 1x1 shortcut convolutions (forward, weight gradient, and the
 input gradient as parity-class GEMMs), the one-channel stem — every BatchNorm(+residual)(+ReLU) in
 csrc/kernels/batchnorm_nhwc.hip, and the last stage's average pool + fc + log_softmax + NLL + backward
-in csrc/kernels/head_pool.hip. ``dtype=fp32`` is the CPU / reference-numerics path; on a GPU it runs
-PyTorch's convolutions (MIOpen) and is not a benchmarked configuration.
+in csrc/kernels/head_pool.hip. ``dtype=fp32`` is the CPU / reference-numerics path; on a GPU it is refused
+(ops/conv.py ``_refuse_library``: no MIOpen / ATen convolution on the device), and ``train.py`` picks bf16 for
+``--model resnet18`` on a GPU unless ``--dtype`` says otherwise.
 """
 from __future__ import annotations
 
@@ -146,8 +147,13 @@ class ResNetStage(PipelineStage):
             x = x.detach().requires_grad_(True)
         with torch.enable_grad():
             y = self.trunk(x)
-        if not ops.pooled_head_ok(y, fc.weight):
-            return super().head_fwd(x.detach(), target, ctx, train, loss_scale, stats)
+            if not ops.pooled_head_ok(y, fc.weight):
+                # finish the autograd head on this y (the trunk - and its BatchNorm running-stat updates - ran
+                # once; re-running the whole forward through super().head_fwd would run them twice)
+                out = fc(F.adaptive_avg_pool2d(y, 1).flatten(1))
+                loss, correct, n = self.loss_terms(out, target)
+                ctx["x"], ctx["loss"] = x, loss * loss_scale
+                return loss.detach(), correct.detach(), n
         ctx["x"], ctx["y"] = x, y
         ctx["gy"] = ops.pooled_head_xent(y.detach(), fc.weight, fc.bias, target, fc.weight.grad, fc.bias.grad,
                                          loss_scale, stats)

@@ -5,9 +5,12 @@ with flipped/transposed weights, weight gradient accumulated into ``weight.grad`
 Used by the ResNet-18-style stages (models/resnet.py) when they run in bf16 channels-last: the
 twelve stride-1 3x3 convolutions, the one-channel stem, and the stride-2 3x3 / 1x1 shortcut
 convolutions (forward, weight gradient and - as four parity-class GEMMs - input gradient), so a bf16
-ResNet step launches no MIOpen convolution. Every other dtype/layout goes through ``F.conv2d``.
+ResNet step launches no MIOpen convolution. Other dtypes/layouts run ``F.conv2d`` on the CPU only: on a GPU
+they are refused (``_refuse_library``).
 """
 from __future__ import annotations
+
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -77,9 +80,30 @@ def _take_addend(link):
 # stats.txt). They are cached per weight, keyed on (storage, version, WEIGHT_GEN): the fused SGD kernels
 # rewrite parameters through raw pointers (no version bump) and so bump WEIGHT_GEN (ops/optim.py); a torch
 # in-place write bumps the version. Never used while a hipGraph is being captured (the replays must
-# re-derive the layouts from the weights they update).
+# re-derive the layouts from the weights they update). An entry holds a weak reference to its weight: a hit
+# requires the very same tensor object (not just a reused id / allocator block of a freed model), and the entry
+# is dropped when the weight is freed.
 WEIGHT_GEN = [0]
 _WCACHE = {}
+
+
+def _cache_put(cache, w, entry):
+    """cache[id(w)] = (weakref to w, *entry); the entry leaves with w."""
+    k = id(w)
+
+    def _gone(r, k=k, cache=cache):
+        if cache.get(k, (None,))[0] is r:
+            cache.pop(k, None)
+
+    cache[k] = (weakref.ref(w, _gone),) + tuple(entry)
+
+
+def _cache_get(cache, w):
+    """The entry stored for exactly this tensor object (without the reference), or None."""
+    hit = cache.get(id(w))
+    if hit is None or hit[0]() is not w:
+        return None
+    return hit[1:]
 _WCACHE_ON = __import__("os").environ.get("SDML_CONV_WCACHE", "1") != "0"
 
 
@@ -92,7 +116,7 @@ def _weight_layouts(w, need_dgrad: bool):
     K = kernels()
     capturing = torch.cuda.is_current_stream_capturing() or not _WCACHE_ON
     key = (w.data_ptr(), w._version, WEIGHT_GEN[0], tuple(w.shape))
-    hit = None if capturing else _WCACHE.get(id(w))
+    hit = None if capturing else _cache_get(_WCACHE, w)
     if hit is not None and hit[0] == key and (hit[2] is not None or not need_dgrad):
         return hit[1], hit[2]
     if need_dgrad:
@@ -100,7 +124,7 @@ def _weight_layouts(w, need_dgrad: bool):
     else:
         wt, wd = K.conv3x3_weight_bf16(w, False), None
     if not capturing:
-        _WCACHE[id(w)] = (key, wt, wd)
+        _cache_put(_WCACHE, w, (key, wt, wd))
     return wt, wd
 
 
@@ -237,6 +261,21 @@ def stem_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and conv.groups == 1 and conv.out_channels % 16 == 0 and conv.out_channels <= 512)
 
 
+# A GPU tensor that no hand-written kernel takes (an fp32 ResNet, an NCHW or odd-width activation) is refused, not
+# sent to MIOpen / ATen: on a ROCm device the ResNet runs on conv_bf16.hip / batchnorm_nhwc.hip only, in bf16
+# channels-last (fp32 is the CPU / reference-numerics dtype). SDML_CONV_LIBRARY=1 (or LIBRARY_ON_GPU = True) lets
+# the A/B tests run the library path as a reference.
+LIBRARY_ON_GPU = __import__("os").environ.get("SDML_CONV_LIBRARY", "0") == "1"
+
+
+def _refuse_library(x: torch.Tensor, what: str):
+    if x.is_cuda and not LIBRARY_ON_GPU:
+        raise RuntimeError(
+            f"{what} on a ROCm device with a {x.dtype} {tuple(x.shape)} activation: no hand-written gfx950 kernel "
+            "takes it (the ResNet kernels are bf16 channels-last; run --model resnet18 with --dtype bf16 on the GPU, "
+            "fp32 on the CPU). SDML_CONV_LIBRARY=1 allows the MIOpen/ATen path for A/B comparisons.")
+
+
 def conv2d(conv: torch.nn.Conv2d, x: torch.Tensor, part=None, link=None) -> torch.Tensor:
     """``conv(x)``, on the HIP kernels where they apply: stride-1 3x3 on the halo kernel, strided
     3x3 / 1x1 on the im2col kernel (input gradient on the parity-class kernel), the streaming stem
@@ -248,6 +287,7 @@ def conv2d(conv: torch.nn.Conv2d, x: torch.Tensor, part=None, link=None) -> torc
         return _ConvGeneralFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], part, link)
     if stem_eligible(x, conv):
         return _StemConvFn.apply(x, conv.weight)
+    _refuse_library(x, "convolution")
     return conv(x)
 
 
@@ -326,6 +366,7 @@ def batch_norm(bn: torch.nn.BatchNorm2d, x: torch.Tensor, res=None, relu: bool =
             scale = (bn.weight.float() * torch.rsqrt(bn.running_var.float() + bn.eps)).contiguous()
             shift = (bn.bias.float() - bn.running_mean.float() * scale).contiguous()
         return kernels().bn_nhwc_eval(x, res, scale, shift, relu)
+    _refuse_library(x, "BatchNorm")
     y = bn(x)
     if res is not None:
         y = y + res

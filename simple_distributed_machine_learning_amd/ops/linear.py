@@ -54,16 +54,16 @@ def _hand_ok(x2, w) -> bool:
 
 def _w_t(w):
     """w^T, contiguous, cached for the optimizer step (not while a hipGraph is being captured)."""
-    from .conv import WEIGHT_GEN
+    from .conv import WEIGHT_GEN, _cache_get, _cache_put
 
     if torch.cuda.is_current_stream_capturing():
         return w.t().contiguous()
     key = (w.data_ptr(), w._version, WEIGHT_GEN[0], tuple(w.shape))
-    hit = _WT.get(id(w))
+    hit = _cache_get(_WT, w)
     if hit is not None and hit[0] == key:
         return hit[1]
     wt = w.t().contiguous()
-    _WT[id(w)] = (key, wt)
+    _cache_put(_WT, w, (key, wt))
     return wt
 
 

@@ -316,8 +316,10 @@ class PipelineEngine:
                 self.flat.zero_grad()
                 self.grad_sync.reset()
                 # still joins the collectives of its replica group, with the SAME collective sequence the
-                # data-bearing ranks issue (rotate all-to-all: one all-reduce over the whole flat buffer)
+                # data-bearing ranks issue (rotate all-to-all: one all-reduce over the whole flat buffer, or the
+                # two spans of the split weight gradient when the replicas run it: _planned_dp_spans)
                 if rotate_a2a:
+                    self._issue_planned_spans(self._planned_dp_spans())
                     self.grad_sync.finish_all()
                 else:
                     self.grad_sync.finish()
@@ -663,8 +665,12 @@ class PipelineEngine:
                 pend[w].run()
                 pend[w] = None
 
-        # the gradient all-reduce overlapped with the last wave's first-layer weight gradient (see __init__)
-        dp_spans = self._dp_split_spans(s0) if (defer and train and self.grad_sync.enabled and self.dp_split) else None
+        # the gradient all-reduce overlapped with the last wave's first-layer weight gradient (see __init__). The
+        # decision depends only on rank-independent facts (model, placement, knob), so every replica issues the same
+        # two spans; a rank whose batch the split kernels do not take issues them after its whole gradient
+        dp_spans = self._planned_dp_spans() if (defer and train) else None
+
+        spans_left = [dp_spans is not None]  # planned spans not issued yet (the split kernels did not run)
 
         def head(xin, tgt, w):  # stage 1 forward + loss (+ its backward) on one block of rows
             nonlocal fresh, count
@@ -712,6 +718,7 @@ class PipelineEngine:
                         # the rest: range 1's rows, every bias, the head (all written by now)
                         self.grad_sync.issue_span(a1, self.flat.grads.numel())
                         self.dp_split_steps += 1
+                        spans_left[0] = False
                         hkeep[w] = back[w] = None
                         return
             if factored and fuse0:  # the factor goes straight into stage 0's weight-gradient kernel
@@ -786,6 +793,8 @@ class PipelineEngine:
                     stage0_bwd(w)
             for w in range(W):  # (nothing is left unless a stage-0 backward was skipped)
                 run_pending(w)
+            if spans_left[0]:  # the same two collectives as the replicas that ran the split
+                self._issue_planned_spans(dp_spans)
             with tm.span("grad_sync"):  # both stages' gradients in one collective
                 self.grad_sync.finish_all()
             if step_optimizer:
@@ -800,6 +809,28 @@ class PipelineEngine:
             stats.zero_()
         self.last_timing = tm.result()
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
+
+    def _planned_dp_spans(self):
+        """The split all-reduce spans every replica issues this step, or None. Only rank-independent facts decide
+        (the knob, a gradient all-reduce, the rotate all-to-all form with nothing crossing GPUs, the model's first
+        layer): a replica with no rows or a batch the split kernels do not take still issues the same spans."""
+        if not (self.dp_split and self.grad_sync.enabled and self.kind == "rotate" and self.use_alltoall
+                and self.P == 2 and 0 in self.stages and 1 in self.stages):
+            return None
+        R = self.mesh.pp
+        if R > 1 and (self.cross_fraction is None or self.cross_fraction > 0):
+            return None  # rows cross GPUs: one whole-buffer all-reduce (finish_all)
+        if not (self.factored_boundary_grad and (R > 1 or self.factored_r1)
+                and getattr(self.stages[1], "supports_factored_grad", False)
+                and hasattr(self.stages[0], "bwd_from_factor") and hasattr(self.stages[1], "factor_weight")):
+            return None
+        return self._dp_split_spans(self.stages[0])
+
+    def _issue_planned_spans(self, spans):
+        if spans is not None:
+            _, a1 = spans
+            self.grad_sync.issue_span(0, a1)
+            self.grad_sync.issue_span(a1, self.flat.grads.numel())
 
     def _dp_split_spans(self, s0):
         """(hidden groups G, end of range 0 in the flat gradient) when the first layer's weight gradient can

@@ -25,11 +25,14 @@ The model (documented in README "Multi-GPU placement") is deliberately simple:
   waves and of the local rows): step = max(compute, link) + the part that cannot overlap (the
   first wave's forward exchange when nothing local is left to compute, a fixed ``exposed``
   fraction of the link time);
-* gradient all-reduce: ring over N GPUs of the parameter bytes. With nothing crossing GPUs (dp) the
-  first layer's weight gradient runs as two hidden-unit ranges and range 0's all-reduce overlaps range 1's
-  kernel (parallel/pipeline.py, SDML_DP_SPLIT), so only range 1's half plus what range 0's collective does
-  not hide is exposed: ``half + max(0, half - wgrad/2)``; the other placements all-reduce after the last
-  backward.
+* gradient all-reduce: ring over N GPUs of the parameter bytes, priced by the path the engine runs
+  (``dp_split``, default: what ``dp_split_default()`` says the engine does). With the split on and nothing
+  crossing GPUs (dp) the first layer's weight gradient runs as two hidden-unit ranges and range 0's
+  all-reduce overlaps range 1's kernel (parallel/pipeline.py, SDML_DP_SPLIT), so only range 1's half plus
+  what range 0's collective does not hide is exposed: ``half + max(0, half - wgrad/2)`` plus the split's
+  own cost (``ComputeModel.split_us``); with it off (and for the other placements) the whole all-reduce
+  follows the last backward, exposed, plus the separate optimizer launch the all-reduce forces
+  (``ComputeModel.dp_step_us``).
 
 ``choose`` returns the placement with the smallest predicted step; among placements within 2% of
 it, the one that moves the most boundary bytes across GPUs (the split the benchmark is about).
@@ -67,11 +70,28 @@ class ComputeModel:
     act_bytes: int = 512          # boundary activation per row (128 fp32)
     grad_bytes: int = 40          # factored boundary gradient per row (10 fp32)
     param_bytes: int = 101_770 * 4
+    # N > 1 with a gradient all-reduce: the reduction can no longer apply SGD in the same launch, so a separate
+    # optimizer launch follows the collective (one-rank RCCL harness, profiles/r4_dpsplit_one_rank_rccl.jsonl:
+    # 0.188 vs 0.172 ms per step before any link time)
+    dp_step_us: float = 16.0
+    # the split weight gradient's own extra cost over the whole-gradient kernel (same harness)
+    split_us: float = 33.0
+
+
+def dp_split_default() -> bool:
+    """Whether the engine splits the data-parallel gradient all-reduce (parallel/pipeline.py reads the same
+    variable): the model must price the path that runs."""
+    import os
+
+    return os.environ.get("SDML_DP_SPLIT", "0") == "1"
 
 
 def predict(placement: str, n: int, batch_per_gpu: int, waves: int = 2, phi: Optional[float] = None,
-            link: LinkModel = LinkModel(), comp: ComputeModel = ComputeModel()) -> Dict[str, float]:
+            link: LinkModel = LinkModel(), comp: ComputeModel = ComputeModel(),
+            dp_split: Optional[bool] = None) -> Dict[str, float]:
     """Predicted step of ``placement`` at ``n`` GPUs (weak scaling: ``batch_per_gpu`` rows per GPU)."""
+    if dp_split is None:
+        dp_split = dp_split_default()
     B = float(batch_per_gpu)
     row = comp.act_bytes + comp.grad_bytes
     if n == 1:
@@ -98,9 +118,11 @@ def predict(placement: str, n: int, batch_per_gpu: int, waves: int = 2, phi: Opt
     link_us = link_bytes / (link.gbps * 1e3) + ncoll * link.collective_us
     if n > 1:  # ring all-reduce of the gradients (2 (n-1)/n of the bytes per GPU, over 2 ring links)
         ar_us = 2 * (n - 1) / n * comp.param_bytes / (2 * link.gbps * 1e3) + link.collective_us
-        if placement == "dp" or (placement != "pp2dp" and phi == 0):  # split: two half collectives, one hidden
+        if dp_split and (placement == "dp" or (placement != "pp2dp" and phi == 0)):
+            # split: two half collectives, range 0's under range 1's kernel
             half = (ar_us - link.collective_us) / 2 + link.collective_us
-            ar_us = half + max(0.0, half - B * comp.wgrad_ns / 2e3)
+            ar_us = half + max(0.0, half - B * comp.wgrad_ns / 2e3) + comp.split_us
+        ar_us += comp.dp_step_us
     else:
         ar_us = 0.0
     if link_bytes > 0:

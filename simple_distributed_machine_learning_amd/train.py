@@ -74,8 +74,11 @@ def run(args) -> dict:
     if args.heartbeat > 0 and mesh.world_size > 1:
         hb = Heartbeat(mesh.rank, range(mesh.world_size), timeout_s=args.heartbeat).start()
     dt = {"fp32": torch.float32, "bf16": torch.bfloat16}.get(getattr(args, "dtype", "auto"))
+    if dt is None and args.model == "resnet18" and device.type == "cuda":
+        dt = torch.bfloat16  # the ResNet's GPU kernels are bf16 channels-last (ops/conv.py); fp32 is the CPU path
     kw = {"dtype": dt} if dt is not None and args.model in ("resnet18", "gpt2_tiny") else {}
-    spec = get_model_spec(args.model, stages, eval_dropout=bool(args.eval_dropout), seq_len=args.seq_len, **kw)
+    spec = get_model_spec(args.model, stages, eval_dropout=bool(args.eval_dropout), seq_len=args.seq_len,
+                          dropout=getattr(args, "dropout", 0.5), **kw)
     if dt is not None and spec.param_dtype != dt:
         raise SystemExit(f"--dtype {args.dtype} is not supported for --model {args.model}")
     engine = PipelineEngine(spec, mesh, schedule_kind=args.schedule, num_microbatches=args.microbatches,

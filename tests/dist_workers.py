@@ -47,9 +47,10 @@ def train_worker(rank, world, model, kind, M, pp, steps, B, seed=3, kw=None, tp=
             "dp_split_steps": eng.dp_split_steps}
 
 
-def empty_replica_worker(rank, world, pp, B, steps, seed=3):
+def empty_replica_worker(rank, world, pp, B, steps, seed=3, dp_split=False, cross_fraction=None):
     """rotate, dp replicas of a pp-rank group: replica 1 gets NO samples every step (batch 0), replica 0
-    gets B per owner; global_batch is fixed to replica 0's samples. Returns the trained weights."""
+    gets B per owner; global_batch is fixed to replica 0's samples. Returns the trained weights.
+    ``dp_split``: the split gradient all-reduce is planned (two spans per step on every replica)."""
     from simple_distributed_machine_learning_amd.data import SyntheticMNIST
     from simple_distributed_machine_learning_amd.models import get_model_spec
     from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh
@@ -57,12 +58,16 @@ def empty_replica_worker(rank, world, pp, B, steps, seed=3):
     mesh = init_mesh(pp=pp, schedule_kind="rotate", rank=rank, world_size=world, device=torch.device("cpu"),
                      backend="gloo", timeout_s=120)
     eng = PipelineEngine(get_model_spec("mlp", 2), mesh, schedule_kind="rotate", num_microbatches=2 * pp, lr=0.1,
-                         momentum=0.5, seed=seed)
+                         momentum=0.5, seed=seed, cross_fraction=cross_fraction)
+    eng.dp_split = dp_split
+    spans = []
+    real_issue = eng.grad_sync.issue_span
+    eng.grad_sync.issue_span = lambda lo, hi: (spans.append((lo, hi)), real_issue(lo, hi))
     ds = SyntheticMNIST(B * pp * steps, seed=7)
     for step in range(steps):
         n = B if mesh.dp_rank == 0 else 0
         eng.run(ds, step * B * pp, n, train=True, global_batch=B * pp)
-    return {"state": eng.state_dicts(), "dp_rank": mesh.dp_rank}
+    return {"state": eng.state_dicts(), "dp_rank": mesh.dp_rank, "spans": spans}
 
 
 def debug_sync_rotate_worker(rank, world, B):

@@ -48,7 +48,18 @@ def test_gpu_eval_and_ref_cnn_runs():
     assert r.count == 40
 
 
-@pytest.mark.parametrize("model,B,kw", [("resnet18", 16, {}), ("resnet18", 16, {"dtype": torch.bfloat16}),
+def test_resnet_fp32_refused_on_gpu():
+    """no MIOpen / ATen convolution on a GPU code path. The ResNet's device kernels are bf16
+    channels-last; an fp32 ResNet on the GPU raises instead of silently running the library (ops/conv.py)."""
+    mesh = init_mesh(pp=1, schedule_kind="1f1b", rank=0, world_size=1, device=DEV)
+    e = PipelineEngine(get_model_spec("resnet18", None), mesh, schedule_kind="1f1b", num_microbatches=1, lr=0.01,
+                       momentum=0.5, seed=3)
+    ds = SyntheticMNIST(16, seed=1, device=DEV)
+    with pytest.raises(RuntimeError, match="no hand-written gfx950 kernel"):
+        e.run(ds, 0, 16, train=True)
+
+
+@pytest.mark.parametrize("model,B,kw", [("resnet18", 16, {"dtype": torch.bfloat16}),
                                         ("gpt2_tiny", 8, {"seq_len": 16}), ("gpt2", 2, {"seq_len": 64})])
 def test_gpu_models_train(model, B, kw):
     from simple_distributed_machine_learning_amd.data import SyntheticTokens
@@ -87,6 +98,7 @@ def test_resnet_bf16_hip_kernels_match_library_path(monkeypatch):
     fused0 = conv_ops.ResidualLink.fused
     hip_losses, hip_p = run()
     assert conv_ops.ResidualLink.fused - fused0 == 3 * 8  # every block joins its input gradient in an epilogue
+    monkeypatch.setattr(conv_ops, "LIBRARY_ON_GPU", True)  # the library path as the reference
     monkeypatch.setattr(conv_ops, "hip_eligible", lambda x, conv: False)
     monkeypatch.setattr(conv_ops, "bn_eligible", lambda x, bn, res=None: False)
     lib_losses, lib_p = run()

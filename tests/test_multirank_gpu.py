@@ -114,6 +114,14 @@ def test_bench_two_ranks_on_one_gpu():
         assert d["config"]["world_size_seen"] == 2 and d["config"]["backend"] == "gloo"
         if cross:
             assert d["config"]["boundary_bytes_across_gpus_per_step"] == 2 * 4096 * (512 + 40)
+        else:  # auto: the placement the cost model picks for this N and batch, and its prediction in the JSON
+            from simple_distributed_machine_learning_amd.parallel import placement as plc
+
+            want, phi, table = plc.choose(2, 8192)
+            assert d["config"]["placement"] == want, (d["config"]["placement"], want)
+            assert d["config"]["predicted"] == table
+            if want == "dp":
+                assert d["config"]["boundary_bytes_across_gpus_per_step"] == 0
 
 
 def test_bench_spawns_its_ranks_without_a_launcher():
@@ -131,3 +139,109 @@ def test_bench_spawns_its_ranks_without_a_launcher():
     env1 = dict(env, WORLD_SIZE="1", RANK="0")
     r = subprocess.run(cmd, env=env1, capture_output=True, text=True, timeout=120, cwd=ROOT)
     assert r.returncode != 0 and not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+# ---- the reference's own workload and BASELINE configs 3-5 across processes on the device ----
+TRAIN_RE = __import__("re").compile(r"^Train Epoch: (\d+) \[(\d+)/(\d+) \((\d+)%\)\]\tLoss: (\d+\.\d{6})$")
+TEST_RE = __import__("re").compile(r"^Test set: Average loss: (\d+\.\d{4}), Accuracy: (\d+)/(\d+) \((\d+)%\)$")
+
+
+def _launch_reference_cli(extra, world=2, timeout=400):
+    """``python simple_distributed.py --rank=R --world_size=2 --interface=lo --master_addr=127.0.0.1 ...`` (the
+    reference's command line, README.txt:19) as ``world`` processes sharing cuda:0 through the host-staged
+    transport."""
+    port = free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, SDML_TRANSPORT="host")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        env.pop(k, None)
+    procs = []
+    for r in range(world):
+        cmd = [sys.executable, os.path.join(ROOT, "simple_distributed.py"), f"--rank={r}", f"--world_size={world}",
+               "--interface=lo", "--master_addr=127.0.0.1", f"--master_port={port}", "--device=cuda"] + extra
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env,
+                                      cwd=ROOT))
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append(out)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out[-4000:]
+    return outs
+
+
+def test_reference_command_line_two_ranks_on_device(tmp_path):
+    """The reference's CNN split exactly as its README runs it - conv stage on rank 0, fc stage on rank 1
+    (/root/reference/simple_distributed.py:33-37, :47-49, :71, :138-186) - as two processes on the MI355X: the
+    per-stage fused CNN kernels hand the [60, 320] boundary and its gradient across processes. The log lines keep
+    the reference's format; at dropout 0 the trained per-stage weights (reference key names, from the stage
+    checkpoints) equal the single-process GPU engine's after the same 12 steps."""
+    import torch as _t
+
+    from simple_distributed_machine_learning_amd.data import SyntheticMNIST
+    from simple_distributed_machine_learning_amd.models import get_model_spec
+    from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh
+
+    steps, B = 12, 60
+    outs = _launch_reference_cli(["--epochs=1", f"--train_size={steps * B}", "--test_size=120", "--dropout=0",
+                                  f"--ckpt_dir={tmp_path}"])
+    lines = outs[0].splitlines()
+    train = [m for m in map(TRAIN_RE.match, lines) if m]
+    test = [m for m in map(TEST_RE.match, lines) if m]
+    assert [(m.group(1), m.group(2), m.group(3), m.group(4)) for m in train] == [
+        ("1", "0", "720", "0"), ("1", "600", "720", "83")], lines
+    assert len(test) == 1 and test[0].group(3) == "120"
+    i = lines.index(test[0].group(0))
+    assert lines[i - 1] == "" and lines[i + 1] == ""
+    assert not any(TRAIN_RE.match(l) for l in outs[1].splitlines())  # master-only logging
+    got = {s: _t.load(tmp_path / f"stage{s}.pt", weights_only=True)["model"] for s in (0, 1)}
+    assert set(got[0]) == {"conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias"}
+    assert set(got[1]) == {"fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"}
+    # the same run in one process on the device (default seed 1, data seed 1234, lr 0.1, momentum 0.5)
+    mesh = init_mesh(pp=1, schedule_kind="1f1b", rank=0, world_size=1, device=_t.device("cuda:0"))
+    e = PipelineEngine(get_model_spec("ref_cnn", 2, dropout=0.0), mesh, schedule_kind="1f1b", num_microbatches=1,
+                       lr=0.1, momentum=0.5, seed=1)
+    ds = SyntheticMNIST(steps * B, seed=1234, device="cuda:0", mode="learnable", offset=0)
+    for k in range(steps):
+        e.run(ds, k * B, B, train=True, global_batch=B)
+    want = e.state_dicts()
+    for s in (0, 1):
+        for k, v in got[s].items():
+            _t.testing.assert_close(v, want[s][k], rtol=1e-4, atol=1e-5, msg=f"stage {s} {k}")
+
+
+def test_mlp4x1024_gpipe_four_ranks_on_device():
+    """BASELINE config 3: the 4-stage 4x1024 MLP, one stage per process, GPipe (fill-drain) on the device
+    engine (two-fp16-plane hidden-layer GEMMs), against the single-process GPU engine."""
+    B, steps, M = 512, 2, 4
+    res = run_ranks(train_worker, 4, "mlp4x1024", "gpipe", M, 4, steps, B, 3, dict(GPU), timeout=400)
+    ref = _single("mlp4x1024", M, steps, B, "gpipe")
+    _compare(res, ref)
+    assert all(r["bytes_sent"] > 0 for r in res)
+
+
+def test_resnet18_bf16_eight_stages_four_ranks_1f1b_on_device():
+    """BASELINE config 4: ResNet-18-style CNN in 8 stages on 4 processes (two stages each), 1F1B, bf16
+    channels-last on the hand-written conv / BatchNorm / pooled-head kernels; boundaries [N, H, W, C] bf16 between
+    processes. Same kernels in the same order as one process, so the weights agree to bf16 rounding."""
+    B, steps, M = 16, 2, 2
+    kw = dict(GPU, stages=8, dtype=torch.bfloat16)
+    res = run_ranks(train_worker, 4, "resnet18", "1f1b", M, 4, steps, B, 3, kw, timeout=400)
+    ref = _single("resnet18", M, steps, B, "1f1b", {"stages": 8, "dtype": torch.bfloat16})
+    _compare(res, ref, rtol=2e-2, atol=2e-3)
+    assert all(r["bytes_sent"] > 0 for r in res)
+
+
+def test_gpt2_tiny_two_ranks_on_device():
+    """BASELINE config 5's code path (the GPT-2 stage modules, flash attention, LayerNorm, fused vocab
+    cross-entropy) in two processes on the device: the [B, S, d] boundary and its gradient cross processes."""
+    B, steps, M = 4, 2, 2
+    kw = dict(GPU, stages=2, seq_len=16)
+    res = run_ranks(train_worker, 2, "gpt2_tiny", "1f1b", M, 2, steps, B, 3, kw, timeout=400)
+    ref = _single("gpt2_tiny", M, steps, B, "1f1b", {"stages": 2, "seq_len": 16})
+    _compare(res, ref)
+    assert all(r["bytes_sent"] > 0 for r in res)

@@ -237,6 +237,23 @@ def test_rotate_replica_with_no_samples_joins_the_same_collectives():
                 torch.testing.assert_close(v, ref[0]["state"][s][k], rtol=1e-5, atol=1e-6, msg=f"stage {s} {k}")
 
 
+def test_empty_replica_with_planned_dp_split():
+    """with the split gradient all-reduce planned (SDML_DP_SPLIT), a replica with no rows must issue the
+    same two span all-reduces as the replica with data (which, on CPU, computes its gradient whole and then issues
+    the spans): the same collective sequence, so no hang, and the weights of the data-only run."""
+    from dist_workers import empty_replica_worker
+
+    B, steps = 24, 2
+    res = run_ranks(empty_replica_worker, 4, 2, B, steps, 3, True, 0.0, timeout=200)
+    ref = run_ranks(empty_replica_worker, 2, 2, B, steps, 3, False, 0.0, timeout=200)
+    for r in res:
+        assert len(r["spans"]) == 2 * steps and r["spans"][0][0] == 0 and r["spans"][1][0] == r["spans"][0][1], r["spans"]
+        for s, sd in r["state"].items():
+            for k, v in sd.items():
+                torch.testing.assert_close(v, ref[0]["state"][s][k], rtol=1e-5, atol=1e-6, msg=f"stage {s} {k}")
+    assert all(not r["spans"] for r in ref)
+
+
 def test_debug_sync_rotate_checks_every_owners_rows():
     """under rotate a head runs on rows of every owner, so debug_sync checks the whole replica
     group's block: a bad label in the last rank's shard is refused on rank 0 as well."""

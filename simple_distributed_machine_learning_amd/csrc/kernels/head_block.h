@@ -1,0 +1,314 @@
+// The 784-128-10 MLP's classifier head on a 256-row block of h, on fp16 MFMAs (16x16x32), shared by
+// mlp_u8.hip's fused uint8 forward + head (h straight from the forward's accumulators) and head_xent.hip's
+// standalone block head (h read from HBM): both feed the same function the same registers, so their logits,
+// dl and dW2 are the same operations in the same order (the fused kernel's dl is bit-identical to the
+// standalone head's on the same rows).
+//
+// Reference ops: /root/reference/simple_distributed.py:77-79 (fc2, log_softmax), :111 (nll_loss).
+//
+// Numerics (fp32-accurate, as the first layer's GEMMs): every fp32 operand is two fp16 planes of v * 2^s,
+// hi = fp16(v 2^s), lo = fp16(v 2^s - hi) (u8_planes.h's split: each element to within one fp32 ulp above
+// 2^(E-15) when |v| < 2^E, an absolute error below 2^(E-39) under it), and a product is the three exact fp16
+// MFMA products hi*lo + lo*hi + hi*hi accumulated in fp32 (lo*lo <= 2^-22 |ab| is dropped). Plane scales, all
+// exact powers of two: h by 2^(14 - E) from the block's max |h| (one LDS exchange), W2 by its max |W2| (every
+// wave computes the same value from registers), dl by the a-priori bound |dl| <= loss_scale
+// (|softmax - onehot| <= 1). The round-4 head ran the same math on fp32 MFMAs (v_mfma_f32_16x16x4_f32, 16x
+// slower per product) and cost ~12K of the fused forward's ~27K-cycle epilogue per block.
+//
+// Block = 8 waves, wave w = (wm = w % 4, wn = w / 4) holding h[64 wm + ..][64 wn + ..] in the 32x32 MFMA C
+// layout: y[i][j][r] = h[64 wm + 32 i + 8 (r >> 2) + 4 (lane >> 5) + (r & 3)][64 wn + 32 j + (lane & 31)].
+//  1. h planes into an LDS image [plane][hid][row] of 8-byte granules (4 rows of one hidden unit): the C
+//     layout gives a lane exactly one granule per register quad, so the image is written with 32
+//     ds_write_b64 per lane (round 4: 64 ds_write_b32 of fp32). Granule q of hidden unit h sits at q ^ gswz(h):
+//     the writes (16 lanes = 16 hidden units), the logits' transposed reads and the dW2 reads are all
+//     bank-conflict-free (checked by enumeration in tests/test_head_block_layout.py).
+//  2. logits^T = W2 h^T, 16 classes x 16 rows per 16x16x32 MFMA: A = W2 planes (lane: class), B = the h image
+//     read transposed (ds_read_b64_tr_b16: lane = row, 8 consecutive hidden units), 4 k-steps x 3 products;
+//     wave w runs the row tiles w and w + 8. The accumulator leaves lane (r, g) with row r's logits of classes
+//     4g .. 4g+3, the layout head_tile.h's softmax_dz works on.
+//  3. dW2 = dl^T h over the block's 256 rows, 16 hidden units per wave (no cross-wave reduction): A = dl^T
+//     planes from a small LDS image (lane: class), B = the h image (lane: hidden unit, 8 consecutive rows).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "head_tile.h"
+
+namespace sdml {
+namespace hblk {
+
+typedef float hb_f32x16 __attribute__((ext_vector_type(16)));
+typedef float hb_f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 hb_f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 hb_f16x4 __attribute__((ext_vector_type(4)));
+typedef short hb_s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int ROWS = 256, HID = 128, NW = 8, NT = 512;
+constexpr int PLANE_B = HID * ROWS * 2;              // bytes per h plane (fp16)
+constexpr int DLT_OFF = 2 * PLANE_B;                  // dl^T planes [2][16][ROWS] fp16
+constexpr int DLT_PLANE_B = 16 * ROWS * 2;
+constexpr int RED_OFF = DLT_OFF + 2 * DLT_PLANE_B;    // floats below
+// red: [0, 8) wave max |h|, [8, 136) db partials [wave][16], [136, 144) loss, [144, 152) correct, [152, 160) amx
+constexpr int RED_FLOATS = 160;
+constexpr int LDS_BYTES = RED_OFF + RED_FLOATS * 4;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+
+// granule swizzle of hidden unit (or class) h: bits (h2, h3, h0, h1, h3) -> bits 0..4
+__device__ __forceinline__ int gswz(int h) {
+  return ((h >> 2) & 1) | (((h >> 3) & 1) << 1) | ((h & 1) << 2) | (((h >> 1) & 1) << 3) | (((h >> 3) & 1) << 4);
+}
+// byte offset of granule q (rows 4q .. 4q+3) of hidden unit h in plane p of the h image
+__device__ __forceinline__ int hoff(int p, int h, int q) { return p * PLANE_B + h * (ROWS * 2) + 8 * (q ^ gswz(h)); }
+// byte offset of row rho of class c in plane p of the dl^T image
+__device__ __forceinline__ int doff(int p, int c, int rho) {
+  return DLT_OFF + p * DLT_PLANE_B + c * (ROWS * 2) + 8 * ((rho >> 2) ^ gswz(c)) + 2 * (rho & 3);
+}
+
+// exponent E with |v| < 2^E for finite v >= 0, clamped so 2^(14 - E) and 2^(E - 14) stay normal floats
+__device__ __forceinline__ int bexp(float v) {
+  const unsigned b = __float_as_uint(v);
+  const int e = (int)((b >> 23) & 0xffu) - 126;
+  return (b & 0x7fffffffu) == 0u ? -100 : min(max(e, -100), 120);
+}
+__device__ __forceinline__ float p2(int e) { return __uint_as_float((unsigned)(e + 127) << 23); }
+
+// two fp16 planes of x (already scaled): hi = fp16(x), lo = fp16(x - hi)
+__device__ __forceinline__ void split2(float x, _Float16& hi, _Float16& lo) {
+  hi = static_cast<_Float16>(x);
+  lo = static_cast<_Float16>(x - static_cast<float>(hi));
+}
+
+__device__ __forceinline__ hb_f32x4 mfma16(hb_f16x8 a, hb_f16x8 b, hb_f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ hb_s16x4 tr16(const unsigned char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) hb_s16x4*)(p));
+}
+__device__ __forceinline__ hb_f16x8 cat8(hb_s16x4 a, hb_s16x4 b) {
+  hb_s16x4 v[2] = {a, b};
+  return *reinterpret_cast<const hb_f16x8*>(v);
+}
+
+struct Args {
+  const float* w2;             // [C][HID]
+  const float* b2;             // [C]
+  const int64_t* target;       // [M]
+  float loss_scale;
+  bool train;
+  float* dl;                   // optional [M][C]
+  float* part;                 // this block's slab row [C * HID + C + 2] (train: dW2, db2; always loss, correct)
+  float* bound;                // optional: this block's 2 max_row sum_c |dl_c| * max |W2|
+};
+
+// y: this wave's 64 x 64 tile of h (rows >= M zero), C layout above. smem: LDS_BYTES, free (the caller's previous
+// use finished with a barrier or not yet started: the first thing here is a barrier). hook(T, row, valid, dz):
+// called per row tile after the softmax with the lane's dz (the standalone head's dx pass; a no-op when fused).
+template <int C, class Hook>
+__device__ __forceinline__ void block_head(const hb_f32x16 (&y)[2][2], unsigned char* smem, const Args& a, int m0,
+                                           int M, int wave, int lane, Hook&& hook, long long* stamp) {
+  static_assert(C >= 1 && C <= 16, "one 16-class tile");
+  auto st = [&](int k) {
+    if (stamp && lane == 0) stamp[k] = (long long)__builtin_amdgcn_s_memtime();
+  };
+  float* red = reinterpret_cast<float*>(smem + RED_OFF);
+  const int wm = wave & 3, wn = wave >> 2, h2 = lane >> 5, r32 = lane & 31;
+  const int r = lane & 15, g = lane >> 4;
+  const int tid = wave * 64 + lane;
+
+  // W2 (fp32, registers): lane (class r, k-group g) holds W2[r][32 kk + 8 g + e]; bias of classes 4g.., targets
+  float wv[4][8];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const float* src = a.w2 + (size_t)min(r, C - 1) * HID + 32 * kk + 8 * g;
+    const hb_f32x4 u0 = *reinterpret_cast<const hb_f32x4*>(src), u1 = *reinterpret_cast<const hb_f32x4*>(src + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      wv[kk][e] = r < C ? u0[e] : 0.f;
+      wv[kk][4 + e] = r < C ? u1[e] : 0.f;
+    }
+  }
+  headtile::f32x4m bv;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) bv[v] = (4 * g + v) < C ? a.b2[4 * g + v] : 0.f;
+  int tg[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) tg[it] = (int)a.target[min(m0 + 16 * (wave + NW * it) + r, M - 1)];
+
+  // block max |h| -> plane scale (all waves, after one exchange)
+  float hm = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) hm = fmaxf(hm, fabsf(y[i][j][q]));
+  for (int off = 32; off > 0; off >>= 1) hm = fmaxf(hm, __shfl_xor(hm, off));
+  if (lane == 0) red[wave] = hm;
+  float wm2 = 0.f;  // max |W2| (every wave holds all of W2 in registers: the same value in every wave)
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wm2 = fmaxf(wm2, fabsf(wv[kk][e]));
+  for (int off = 32; off > 0; off >>= 1) wm2 = fmaxf(wm2, __shfl_xor(wm2, off));
+  __syncthreads();  // (B1) the maxima are in LDS; the caller's buffers are free
+  st(17);
+  float bm = red[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) bm = fmaxf(bm, red[w]);
+  const int Eh = bexp(bm), Ew = bexp(wm2), Ed = bexp(a.loss_scale);
+  const float sh = p2(14 - Eh), sw = p2(14 - Ew), sd = p2(14 - Ed);
+
+  // 1. the h image: granule (4 rows) of hidden unit 64 wn + 32 j + r32, rows 64 wm + 32 i + 8 rq + 4 h2 ..
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int hid = 64 * wn + 32 * j + r32;
+#pragma unroll
+      for (int rq = 0; rq < 4; ++rq) {
+        hb_f16x4 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          _Float16 a0, a1;
+          split2(y[i][j][4 * rq + e] * sh, a0, a1);
+          hi[e] = a0;
+          lo[e] = a1;
+        }
+        const int q = 16 * wm + 8 * i + 2 * rq + h2;
+        *reinterpret_cast<hb_f16x4*>(smem + hoff(0, hid, q)) = hi;
+        *reinterpret_cast<hb_f16x4*>(smem + hoff(1, hid, q)) = lo;
+      }
+    }
+  // W2 planes (A operands of the logits): wp[kk][0] hi, [1] lo
+  hb_f16x8 wp[4][2];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      _Float16 a0, a1;
+      split2(wv[kk][e] * sw, a0, a1);
+      wp[kk][0][e] = a0;
+      wp[kk][1][e] = a1;
+    }
+  __syncthreads();  // (B2) the h image is complete
+  st(18);
+
+  // 2. logits of row tiles wave, wave + 8; softmax, NLL, dl (+ its planes into the dl^T image)
+  headtile::TileAcc acc;
+  acc.zero();
+  const float zsc = p2(Eh - 14) * p2(Ew - 14);  // 2^-(sh + sw) as one exact power of two
+  hb_f32x4 dbs = {0.f, 0.f, 0.f, 0.f};          // this lane's dz sums of classes 4g .. 4g+3
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int T = wave + NW * it;
+    // B operand lanes: row 16 T + (i16 = lane & 15); image rows (hidden) 32 kk + 8 g + (i16 >> 2) (+ 4), granule
+    // 4 T + (i16 & 3)
+    hb_f16x8 hp[4][2];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int hid = 32 * kk + 8 * g + (r >> 2), q = 4 * T + (r & 3);
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        hp[kk][p] = cat8(tr16(smem + hoff(p, hid, q)), tr16(smem + hoff(p, hid + 4, q)));
+    }
+    hb_f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      d = mfma16(wp[kk][0], hp[kk][1], d);  // hi * lo
+      d = mfma16(wp[kk][1], hp[kk][0], d);  // lo * hi
+      d = mfma16(wp[kk][0], hp[kk][0], d);  // hi * hi
+    }
+    headtile::f32x4m z;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) z[v] = fmaf(d[v], zsc, bv[v]);
+    const int row = m0 + 16 * T + r;
+    const bool valid = row < M;
+    float dz[4];
+    headtile::softmax_dz<C>(z, tg[it], valid, a.train, a.loss_scale, g, acc, dz, a.dl ? a.dl + (size_t)row * C : nullptr,
+                            a.bound != nullptr);
+    if (a.train) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        dbs[v] += dz[v];
+        _Float16 dh, dlo;
+        split2(dz[v] * sd, dh, dlo);
+        *reinterpret_cast<_Float16*>(smem + doff(0, 4 * g + v, 16 * T + r)) = dh;
+        *reinterpret_cast<_Float16*>(smem + doff(1, 4 * g + v, 16 * T + r)) = dlo;
+      }
+      hook(T, row, valid, dz);
+    }
+  }
+  st(19);
+  // per-wave partials: loss, correct, |dl| bound, db (16 rows of each tile summed over the lane's row index)
+  for (int off = 32; off > 0; off >>= 1) {
+    acc.loss += __shfl_xor(acc.loss, off);
+    acc.corr += __shfl_xor(acc.corr, off);
+    acc.amx = fmaxf(acc.amx, __shfl_xor(acc.amx, off));
+  }
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) dbs[v] += __shfl_xor(dbs[v], off);
+  if (lane == 0) {
+    red[136 + wave] = acc.loss;
+    red[144 + wave] = acc.corr;
+    red[152 + wave] = acc.amx;
+  }
+  if (r == 0) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) red[8 + 16 * wave + 4 * g + v] = dbs[v];
+  }
+  __syncthreads();  // (B3) the dl^T image and the wave partials are complete
+  st(20);
+
+  // 3. dW2 of hidden units 16 wave .. +15 over the block's rows: lane (class r / hidden r, row group g)
+  if (a.train) {
+    hb_f32x4 gacc = {0.f, 0.f, 0.f, 0.f};
+    const int hid = 16 * wave + r;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int q = 8 * ks + 2 * g;  // granules q, q + 1 = rows 32 ks + 8 g .. +7
+      hb_f16x8 dp[2], hq[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const hb_s16x4 d0 = *reinterpret_cast<const hb_s16x4*>(smem + DLT_OFF + p * DLT_PLANE_B + r * (ROWS * 2) +
+                                                                 8 * (q ^ gswz(r)));
+        const hb_s16x4 d1 = *reinterpret_cast<const hb_s16x4*>(smem + DLT_OFF + p * DLT_PLANE_B + r * (ROWS * 2) +
+                                                                 8 * ((q + 1) ^ gswz(r)));
+        dp[p] = cat8(d0, d1);
+        const hb_s16x4 h0 = *reinterpret_cast<const hb_s16x4*>(smem + hoff(p, hid, q));
+        const hb_s16x4 h1 = *reinterpret_cast<const hb_s16x4*>(smem + hoff(p, hid, q + 1));
+        hq[p] = cat8(h0, h1);
+      }
+      gacc = mfma16(dp[0], hq[1], gacc);  // hi * lo
+      gacc = mfma16(dp[1], hq[0], gacc);  // lo * hi
+      gacc = mfma16(dp[0], hq[0], gacc);  // hi * hi
+    }
+    // lane (hidden r, g) holds dW2[class 4 g + v][16 wave + r]
+    const float gsc = p2(Ed - 14) * p2(Eh - 14);
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      if (4 * g + v < C) a.part[(4 * g + v) * HID + hid] = gacc[v] * gsc;
+  }
+  auto sumw = [&](int base) {  // the 8 wave partials in wave order (pairwise tree)
+    return ((red[base] + red[base + 1]) + (red[base + 2] + red[base + 3])) +
+           ((red[base + 4] + red[base + 5]) + (red[base + 6] + red[base + 7]));
+  };
+  if (a.train && tid < C) {
+    const int c = tid;
+    a.part[C * HID + c] = ((red[8 + c] + red[8 + 16 + c]) + (red[8 + 32 + c] + red[8 + 48 + c])) +
+                          ((red[8 + 64 + c] + red[8 + 80 + c]) + (red[8 + 96 + c] + red[8 + 112 + c]));
+  }
+  if (tid == 64) a.part[C * HID + C] = sumw(136);
+  if (tid == 128) a.part[C * HID + C + 1] = sumw(144);
+  if (tid == 192 && a.bound) {
+    float am = red[152];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) am = fmaxf(am, red[152 + w]);
+    *a.bound = 2.f * am * wm2;
+  }
+  st(21);
+}
+
+}  // namespace hblk
+}  // namespace sdml

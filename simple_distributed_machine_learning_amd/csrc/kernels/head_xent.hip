@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "head_reduce.h"
+#include "head_block.h"
 #include "head_tile.h"
 #include "kernels.h"
 
@@ -603,133 +604,6 @@ __device__ __forceinline__ f32x4m dx_t(const float (&w4)[4], const float (&dz)[4
   return o;
 }
 
-// DXP = false: no dx pass (the factored form writes dl instead, or evaluation): the dx operands
-// (wd, 32 VGPRs) are not loaded
-template <int C, bool DXP>
-__global__ void __launch_bounds__(64 * MW, 2) head_mfma_kernel(const float* __restrict__ x, const float* __restrict__ W,
-                                                            const float* __restrict__ bias,
-                                                            const int64_t* __restrict__ target, int M, float scale,
-                                                            float* __restrict__ part, float* __restrict__ dx,
-                                                            int tiles_per_wave, int mask_dx, float* __restrict__ dl,
-                                                            float* __restrict__ dxmax) {
-  // dxmax (optional, [gridDim.x]): a bound on the block's |dx| (dx = dl @ W, whether dx itself or
-  // its factor dl is written), 2 max_row sum_c |dz_c| * max |W|
-  // (|dx_k| = |sum_c dz_c W_ck| <= sum_c |dz_c| max |W|; the 2 covers fp32 rounding), which the uint8
-  // weight-gradient kernel scales its fp16 dz planes with (mlp_u8.hip). The row sums cost a few
-  // VALU ops per tile; an exact max over the dx values measured 4 us more per step (40 vs 36 us).
-  static_assert(C <= 16, "one 16-class MFMA tile");
-  __shared__ __attribute__((aligned(16))) float ws[16 * WSP];            // W, zero-padded to 16 classes
-  __shared__ __attribute__((aligned(16))) float xt[MW][16 * HK];         // per-wave transposes / final reduce
-  __shared__ __attribute__((aligned(16))) float dzt[MW][16 * DTP];
-  __shared__ float red[MW][2 + 16];
-  __shared__ float redm[MW];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const bool train = dx != nullptr || dl != nullptr;
-  stage_w16(W, C, ws, tid, 64 * MW);
-  __syncthreads();
-  f32x4m wl[8];  // wl[u][e] = W[class r][16 u + 4 g + e]
-#pragma unroll
-  for (int u = 0; u < 8; ++u) wl[u] = *reinterpret_cast<const f32x4m*>(ws + r * WSP + 16 * u + 4 * g);
-  float wd[8][4];
-  if constexpr (DXP) load_wd(ws, r, g, wd);
-  f32x4m bv;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) bv[v] = (4 * g + v) < C ? bias[4 * g + v] : 0.f;
-
-  headtile::TileAcc acc;  // dW^T tiles, db, loss, correct and |dx| bound partials of this wave
-  acc.zero();
-  float* xw = xt[wave];
-  float* dw = dzt[wave];
-
-  // one 16-row tile; FULL: all 16 rows < M (wave-uniform), stores unpredicated
-  auto tile = [&](auto full_c, int row0, const f32x4m (&xv)[8], int tg_raw) {
-    constexpr bool FULL = decltype(full_c)::value;
-    const int row = row0 + r;
-    const bool valid = FULL || row < M;
-    float dz[4];
-    headtile::logits_dz<C>(wl, bv, xv, tg_raw, valid, train, scale, g, acc, dz, dl ? dl + (size_t)row * C : nullptr,
-                           dxmax != nullptr);
-    if (!train) return;
-    if (DXP && dx) {
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const f32x4m o = dx_t(wd[t], dz, xv[t], mask_dx);
-        if (valid) *reinterpret_cast<f32x4m*>(dx + (size_t)row * HK + 16 * t + 4 * g) = o;
-      }
-    }
-    // dW^T += x^T dz through the wave-private transpose
-#pragma unroll
-    for (int u = 0; u < 8; ++u) *reinterpret_cast<f32x4m*>(xw + xt_at(r, u, 4 * g)) = xv[u];
-    headtile::dw_accum(xw, dw, dz, r, g, acc);
-  };
-  auto run = [&](int row0, const f32x4m (&xv)[8], int tg) {
-    if (row0 + 16 <= M) tile(std::true_type{}, row0, xv, tg);
-    else tile(std::false_type{}, row0, xv, tg);
-  };
-  const int tile0 = (blockIdx.x * MW + wave) * tiles_per_wave;
-  auto fetch = [&](int row0, f32x4m (&xv)[8], int& tg) {
-    const int row = min(row0 + r, M - 1);
-    load_x_tile(x, row, g, xv);
-    tg = (int)target[row];
-  };
-  f32x4m xa[8], xb[8];
-  int ta = 0, tb = 0;
-  fetch(tile0 * 16, xa, ta);
-  for (int it = 0; it < tiles_per_wave; it += 2) {
-    const int row0 = (tile0 + it) * 16;
-    if (row0 >= M) break;
-    if (it + 1 < tiles_per_wave) fetch(row0 + 16, xb, tb);
-    run(row0, xa, ta);
-    if (it + 1 >= tiles_per_wave || row0 + 16 >= M) break;
-    if (it + 2 < tiles_per_wave) fetch(row0 + 32, xa, ta);
-    run(row0 + 16, xb, tb);
-  }
-
-  // ---- block partials -> slab row ----
-  float* slab = part + (size_t)blockIdx.x * (C * HK + C + 2);
-  if (train) {
-    __syncthreads();  // all waves done with their transposes: xt holds the wave partials now
-    float* mine = xt[wave];  // [C][HK] of this wave
-    if (r < C) {
-#pragma unroll
-      for (int t = 0; t < 8; ++t) *reinterpret_cast<f32x4m*>(mine + r * HK + 16 * t + 4 * g) = acc.gw[t];
-    }
-    acc.gbp += __shfl_xor(acc.gbp, 16);
-    acc.gbp += __shfl_xor(acc.gbp, 32);
-    if (g == 0) red[wave][2 + r] = acc.gbp;
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    acc.loss += __shfl_xor(acc.loss, off);
-    acc.corr += __shfl_xor(acc.corr, off);
-    acc.amx = fmaxf(acc.amx, __shfl_xor(acc.amx, off));
-  }
-  if (lane == 0) {
-    red[wave][0] = acc.loss;
-    red[wave][1] = acc.corr;
-    redm[wave] = acc.amx;
-  }
-  __syncthreads();
-  static_assert(MW == 4, "wave-partial sums below are written for 4 waves");
-  if (dxmax && wave == 0) {  // times max |W| over the staged classes (wl: every class and hidden unit)
-    float wm = 0.f;
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wm = fmaxf(wm, fabsf(wl[u][e]));
-    for (int off = 32; off > 0; off >>= 1) wm = fmaxf(wm, __shfl_xor(wm, off));
-    if (tid == 0) dxmax[blockIdx.x] = 2.f * fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3])) * wm;
-  }
-  if (train) {
-    for (int o = tid; o < C * HK; o += 64 * MW) slab[o] = (xt[0][o] + xt[1][o]) + (xt[2][o] + xt[3][o]);
-    if (tid < C) slab[C * HK + tid] = (red[0][2 + tid] + red[1][2 + tid]) + (red[2][2 + tid] + red[3][2 + tid]);
-  }
-  if (tid == 0) {
-    slab[C * HK + C] = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
-    slab[C * HK + C + 1] = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
-  }
-}
-
 // dx from the factor dl with the MFMA head's exact operations (bit-identical to its dx)
 template <int C>
 __global__ void __launch_bounds__(256) head_mfma_dx_from_dl_kernel(const float* __restrict__ dl, const float* __restrict__ W,
@@ -759,6 +633,66 @@ __global__ void __launch_bounds__(256) head_mfma_dx_from_dl_kernel(const float* 
   }
 }
 
+// The standalone head for K = 128, C <= 16: head_block.h on 256-row blocks of x read from HBM, in the C layout the
+// fused uint8 forward holds its accumulators in, so this kernel and the fused one run identical operations on the
+// same rows (bit-identical logits, dl, loss). dx (DXP) from dl with dx_t, as head_mfma_dx_from_dl_kernel.
+template <int C, bool DXP>
+__global__ void __launch_bounds__(hblk::NT) head_block_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                               const float* __restrict__ bias,
+                                                               const int64_t* __restrict__ target, int M, float scale,
+                                                               float* __restrict__ part, float* __restrict__ dx,
+                                                               int mask_dx, float* __restrict__ dl,
+                                                               float* __restrict__ dxmax) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[hblk::LDS_BYTES];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave & 3, wn = wave >> 2, h2 = lane >> 5, r32 = lane & 31;
+  const int r = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.x * hblk::ROWS;
+  hblk::hb_f32x16 y[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = m0 + 64 * wm + 32 * i + 8 * (q >> 2) + 4 * h2 + (q & 3);
+        const float v = x[(size_t)min(row, M - 1) * HK + 64 * wn + 32 * j + r32];
+        y[i][j][q] = row < M ? v : 0.f;
+      }
+  float wd[8][4];  // wd[t][kk] = W[class 4 g + kk][hidden 16 t + r] (zero for classes >= C)
+  if constexpr (DXP) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) wd[t][kk] = 4 * g + kk < C ? W[(size_t)(4 * g + kk) * HK + 16 * t + r] : 0.f;
+  }
+  hblk::Args a;
+  a.w2 = W;
+  a.b2 = bias;
+  a.target = target;
+  a.loss_scale = scale;
+  a.train = dx != nullptr || dl != nullptr;
+  a.dl = dl;
+  a.part = part + (size_t)blockIdx.x * (C * HK + C + 2);
+  a.bound = dxmax ? dxmax + blockIdx.x : nullptr;
+  hblk::block_head<C>(
+      y, smem, a, m0, M, wave, lane,
+      [&](int, int row, bool valid, const float (&dz)[4]) {
+        if constexpr (DXP) {
+          if (dx) {
+            f32x4m xv[8];
+            load_x_tile(x, min(row, M - 1), g, xv);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const f32x4m o = dx_t(wd[t], dz, xv[t], mask_dx);
+              if (valid) *reinterpret_cast<f32x4m*>(dx + (size_t)row * HK + 16 * t + 4 * g) = o;
+            }
+          }
+        }
+      },
+      nullptr);
+}
+
 }  // namespace
 
 bool head_fused_supported(int K, int C) { return K == HK && (C == 10 || C == 2 || C == 16); }
@@ -780,12 +714,8 @@ static bool head_use_mfma() {
 // MFMA head grid: 16-row tiles, ~2 waves per SIMD, each wave several tiles (its dW partial stays
 // in registers across them)
 static int head_mfma_blocks(int M, int* tiles_per_wave) {
-  const int tiles = (M + 15) / 16;
-  int blocks = std::min(kHeadAmaxMax, (tiles + MW - 1) / MW);  // (<= 512: one dx max per block)
-  const int tpw = (tiles + blocks * MW - 1) / (blocks * MW);
-  blocks = (tiles + MW * tpw - 1) / (MW * tpw);
-  *tiles_per_wave = tpw;
-  return blocks;
+  *tiles_per_wave = hblk::ROWS / 16;  // (head_block_kernel: one 256-row block per workgroup)
+  return (M + hblk::ROWS - 1) / hblk::ROWS;
 }
 
 int head_fused_blocks(int M, int* chunks_per_block) {
@@ -887,16 +817,16 @@ void head_logsoftmax_nll(const float* x, const float* W, const float* b, const i
   if (head_fused_supported(K, C) && dz_out == nullptr && workspace != nullptr && head_use_mfma()) {
     int tpw = 0;
     const int blocks = head_mfma_blocks(M, &tpw);
-    float* amx = ((dx || dl) && dx_amax && n_amax) ? dx_amax : nullptr;
+    float* amx = ((dx || dl) && dx_amax && n_amax && blocks <= kHeadAmaxMax) ? dx_amax : nullptr;
     if (amx) *n_amax = blocks;
 #define HEAD_MFMA(CC)                                                                                          \
   do {                                                                                                     \
     if (dx)                                                                                                \
-      hipLaunchKernelGGL((head_mfma_kernel<CC, true>), dim3(blocks), dim3(64 * MW), 0, stream, x, W, b, target, M, \
-                         scale, workspace, dx, tpw, mask_dx ? 1 : 0, dl, amx);                              \
+      hipLaunchKernelGGL((head_block_kernel<CC, true>), dim3(blocks), dim3(hblk::NT), 0, stream, x, W, b, target, M, \
+                         scale, workspace, dx, mask_dx ? 1 : 0, dl, amx);                                   \
     else                                                                                                   \
-      hipLaunchKernelGGL((head_mfma_kernel<CC, false>), dim3(blocks), dim3(64 * MW), 0, stream, x, W, b, target, M, \
-                         scale, workspace, dx, tpw, mask_dx ? 1 : 0, dl, amx);                              \
+      hipLaunchKernelGGL((head_block_kernel<CC, false>), dim3(blocks), dim3(hblk::NT), 0, stream, x, W, b, target, \
+                         M, scale, workspace, dx, mask_dx ? 1 : 0, dl, amx);                                \
   } while (0)
     switch (C) {
       case 10: HEAD_MFMA(10); break;

@@ -39,7 +39,6 @@ const Entry kTable[KNOB_COUNT] = {
     {"U8_FWD_PRIO", 0, false, nullptr},
     {"U8_WGRAD_PRIO", 0, false, nullptr},
     {"CNN_SPLIT_BWD", 1, false, nullptr},
-    {"U8_FH_WAVES", 8, false, nullptr},
     {"U8_WGRAD_ILV", 0, false, nullptr},
     {"GEMM_BF16_T2", 0, false, nullptr},
     {"U8_WGRAD_RING", 1, false, nullptr},

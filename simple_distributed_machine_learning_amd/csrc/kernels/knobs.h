@@ -38,7 +38,6 @@ enum KnobId : int {
   KNOB_U8_FWD_PRIO,          // 1: s_setprio 1 on the younger half of the uint8 forward's waves
   KNOB_U8_WGRAD_PRIO,        // 1: the same in the uint8 weight gradient
   KNOB_CNN_SPLIT_BWD,        // reference CNN step, B <= 128: stage 0's backward over 10 workgroups per sample
-  KNOB_U8_FH_WAVES,          // fused uint8 forward + head: 8 (256-row blocks) or 4 (128-row blocks, two per CU)
   KNOB_U8_WGRAD_ILV,         // 1: uint8 weight gradient with the explicit MFMA / staging interleave
   KNOB_GEMM_BF16_T2,         // 1: bf16 NT GEMM on 256 x 128 tiles, two workgroups per CU
   KNOB_U8_WGRAD_RING,        // 1: uint8 weight gradient (dl + ReLU bits) with its operands on an LDS-DMA ring

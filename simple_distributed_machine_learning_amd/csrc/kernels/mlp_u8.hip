@@ -38,6 +38,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "head_block.h"
 #include "head_reduce.h"
 #include "head_tile.h"
 #include "lds_dma.h"
@@ -148,24 +149,9 @@ long long* g_u8w_stamps = nullptr;  // u8_set_wgrad_stamps: the weight gradient'
     }                                                                                                    \
   } while (0)
 
-// ---- fused classifier-head epilogue (HEADC > 0; WMT = 2, NWR = 4: 8 waves, 256 rows x 128 hidden per
-// block; NWR = 2: 4 waves, 128 rows - 80 KiB of LDS, so two blocks share a CU and one's head epilogue runs
-// beside the other's K loop). LDS (floats): the block's h as ROWS / 16 x-tile images of head_tile.h's xt_at
-// layout [ROWS / 16][2048], W2 zero-padded to 16 classes [16][FH_WSP], per-wave dz transposes [WAVES][256],
-// wave partials.
-constexpr int FH_WSP = 128 + 4;
-template <int NWR>
-struct FhGeo {
-  static constexpr int WAVES = 2 * NWR;
-  static constexpr int ROWS = 64 * NWR;
-  static constexpr int TILES = ROWS / 16;  // 2 per wave
-  static constexpr int WS = ROWS * 128;
-  static constexpr int DZT = WS + 16 * FH_WSP;
-  static constexpr int RED = DZT + WAVES * 256;
-  static constexpr int FLOATS = RED + WAVES * 18 + WAVES;
-  static_assert(TILES == 2 * WAVES, "two row tiles per wave");
-};
-static_assert(FhGeo<4>::FLOATS * 4 <= 160 * 1024 && FhGeo<2>::FLOATS * 4 <= 80 * 1024, "LDS");
+// ---- fused classifier-head epilogue (HEADC > 0; WMT = 2, NWR = 4: 8 waves, 256 rows x 128 hidden per block):
+// head_block.h (fp16-plane MFMA head, its LDS image in the then free stage buffers). Round 4's 4-wave 128-row
+// variant (knob U8_FH_WAVES = 4, two blocks per CU) measured slower and is gone with the fp32-MFMA epilogue.
 
 // LDS images of one stage: X [BM rows][FBK bytes], W [NPL planes][128 rows][FBK fp16], chunks at
 // xpos / wpos. The DMA writes 1 KiB per wave-instruction lane-linearly (lane i -> bytes 16i..), so
@@ -219,9 +205,9 @@ template <int MODE, int WMT, int TAIL, int NWR, int HEADC = 0, int NSK = NS>
 __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(FwdParams p) {  // (4-wave blocks: 2 waves per SIMD, <= 256 VGPRs, two blocks per CU)
   constexpr int NS = NSK;  // (shadows the file-wide default inside this kernel)
   using G = Geo<WMT, NWR, NSK>;
-  static_assert(HEADC == 0 || (WMT == 2 && (NWR == 4 || NWR == 2)), "the fused head epilogue: waves of 64 x 64");
+  static_assert(HEADC == 0 || (WMT == 2 && NWR == 4), "the fused head epilogue: 8 waves of 64 x 64");
   constexpr int STAGE = G::STAGE, GLDS_PER_STAGE = G::GLDS_PER_STAGE;
-  constexpr int SMEM_BYTES = HEADC ? std::max(G::SMEM, FhGeo<NWR>::FLOATS * 4) : G::SMEM;
+  constexpr int SMEM_BYTES = HEADC ? std::max(G::SMEM, hblk::LDS_BYTES) : G::SMEM;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
   const int m0 = blockIdx.x * G::BM, n0 = blockIdx.y * FBN;
   const int lane = threadIdx.x & 63;
@@ -450,37 +436,22 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
 }
 
 // The classifier head on the block's h, straight from the forward's accumulators (no HBM round trip):
-//  1. h = relu(scale acc + b1) into the block's LDS x-tile images (the K loop's stage buffers are free);
-//     the ReLU bits leave by one 8-byte store per lane (lane = row of the wave, bits from ballots)
-//  2. every wave runs 2 of the block's 16 row tiles through head_tile.h (bit-identical dl to the
-//     standalone MFMA head on the same h); dW2^T, db2, loss, correct stay in registers
-//  3. wave partials meet in LDS in wave order -> one slab row + one |dl @ W2| bound per block
+//  1. h = relu(scale acc + b1) (rows past M zero); the ReLU bits leave by one 8-byte store per lane (lane = row
+//     of the wave, bits from ballots)
+//  2. head_block.h on h: fp16-plane MFMA logits, softmax / NLL / dl, dW2 and the block's slab row, bit-identical
+//     dl to head_xent.hip's standalone block head on the same rows
 template <int C, int NWR>
 __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
                                                     int m0, int wave, int lane, int wm, int wn, long long* stamp) {
-  using FG = FhGeo<NWR>;
-  constexpr int NW = FG::WAVES, NT = 64 * NW;
-  auto st = [&](int k) {  // MODE 7 only (stamp == nullptr otherwise, folded away)
-    if (stamp && lane == 0) stamp[k] = (long long)__builtin_amdgcn_s_memtime();
-  };
-  using namespace headtile;
+  static_assert(NWR == 4, "head_block.h: 8 waves of 64 x 64, 256 rows");
   const U8HeadArgs& hd = p.head;
-  float* F = reinterpret_cast<float*>(smem);
-  float* himg = F;
-  float* ws = F + FG::WS;
-  float* dzt = F + FG::DZT + wave * 256;
-  float* red = F + FG::RED;  // [NW][2 + 16] (loss, correct, db) then [NW] dz bounds
-  const int tid = threadIdx.x, h2 = lane >> 5, r32 = lane & 31;
-  __syncthreads();  // every wave's last K-step reads are done: the stage buffers are free
-  st(16);
-  for (int i = tid; i < 16 * 32; i += NT) {  // W2, zero-padded to 16 classes
-    const int c = i >> 5, k4 = i & 31;
-    *reinterpret_cast<f32x4m*>(ws + c * FH_WSP + 4 * k4) =
-        c < C ? reinterpret_cast<const f32x4m*>(hd.w2)[c * 32 + k4] : f32x4m{0.f, 0.f, 0.f, 0.f};
-  }
+  const int h2 = lane >> 5, r32 = lane & 31;
+  if (stamp && lane == 0) stamp[16] = (long long)__builtin_amdgcn_s_memtime();
   float bv1[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bv1[j] = p.bias[wn * 64 + 32 * j + r32];
+  const bool ragged = m0 + hblk::ROWS > p.M;  // block-uniform: the last block may hold rows past M
+  f32x16 y[2][2];
   unsigned mw[2] = {0u, 0u};  // lane L: mask words 2 wn + j of the wave's row L
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -488,11 +459,11 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float y = fmaxf(acc[i][j][r] * p.scale + bv1[j], 0.f);  // the plain epilogue's arithmetic
-        const int rw = 32 * i + (r & 3) + 8 * (r >> 2);               // + 4 h2: row within the wave tile
-        const int row = wm * 64 + rw + 4 * h2, col = wn * 64 + 32 * j + r32;
-        himg[(row >> 4) * 2048 + xt_at(row & 15, col >> 4, col & 15)] = y;
-        const unsigned long long b = __ballot(y > 0.f);
+        const int rw = 32 * i + (r & 3) + 8 * (r >> 2);  // + 4 h2: row within the wave tile
+        float v = fmaxf(acc[i][j][r] * p.scale + bv1[j], 0.f);  // the plain epilogue's arithmetic
+        if (ragged && m0 + wm * 64 + rw + 4 * h2 >= p.M) v = 0.f;
+        y[i][j][r] = v;
+        const unsigned long long b = __ballot(v > 0.f);
         if (lane == rw) mw[j] = (unsigned)b;
         if (lane == rw + 4) mw[j] = (unsigned)(b >> 32);
       }
@@ -500,78 +471,16 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
     const int row = m0 + wm * 64 + lane;
     if (row < p.M) *reinterpret_cast<uint2*>(hd.mask + (size_t)row * 4 + 2 * wn) = uint2{mw[0], mw[1]};
   }
-  st(17);
-  __syncthreads();
-  st(18);
-
-  const int r = lane & 15, g = lane >> 4;
-  f32x4m wl[8];  // wl[u][e] = W2[class r][16 u + 4 g + e]
-#pragma unroll
-  for (int u = 0; u < 8; ++u) wl[u] = *reinterpret_cast<const f32x4m*>(ws + r * FH_WSP + 16 * u + 4 * g);
-  f32x4m bv;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) bv[v] = (4 * g + v) < C ? hd.b2[4 * g + v] : 0.f;
-  TileAcc a;
-  a.zero();
-  int tg[2];
-#pragma unroll
-  for (int it = 0; it < 2; ++it) tg[it] = (int)hd.target[min(m0 + 16 * (wave + NW * it) + r, p.M - 1)];
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int T = wave + NW * it, row = m0 + 16 * T + r;
-    const float* xw = himg + T * 2048;
-    f32x4m xv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) xv[u] = *reinterpret_cast<const f32x4m*>(xw + xt_at(r, u, 4 * g));
-    float dz[4];
-    logits_dz<C>(wl, bv, xv, tg[it], row < p.M, true, hd.loss_scale, g, a, dz, hd.dl + (size_t)row * C, true);
-    dw_accum(xw, dzt, dz, r, g, a);
-  }
-  st(19);
-
-  __syncthreads();  // every tile done: the x images are free for the wave partials
-  st(20);
-  float* mine = F + wave * (C * 128);
-  if (r < C) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t) *reinterpret_cast<f32x4m*>(mine + r * 128 + 16 * t + 4 * g) = a.gw[t];
-  }
-  a.gbp += __shfl_xor(a.gbp, 16);
-  a.gbp += __shfl_xor(a.gbp, 32);
-  if (g == 0) red[wave * 18 + 2 + r] = a.gbp;
-  for (int off = 32; off > 0; off >>= 1) {
-    a.loss += __shfl_xor(a.loss, off);
-    a.corr += __shfl_xor(a.corr, off);
-    a.amx = fmaxf(a.amx, __shfl_xor(a.amx, off));
-  }
-  if (lane == 0) {
-    red[wave * 18] = a.loss;
-    red[wave * 18 + 1] = a.corr;
-    red[NW * 18 + wave] = a.amx;
-  }
-  __syncthreads();
-  float* slab = hd.part + (size_t)blockIdx.x * (C * 128 + C + 2);
-  auto sumw = [&](auto at) {  // wave partials in wave order (pairwise tree)
-    if constexpr (NW == 8) return ((at(0) + at(1)) + (at(2) + at(3))) + ((at(4) + at(5)) + (at(6) + at(7)));
-    else return (at(0) + at(1)) + (at(2) + at(3));
-  };
-  for (int o = tid; o < C * 128; o += NT) slab[o] = sumw([&](int w) { return F[w * (C * 128) + o]; });
-  if (tid < C) slab[C * 128 + tid] = sumw([&](int w) { return red[w * 18 + 2 + tid]; });
-  if (tid == 64) slab[C * 128 + C] = sumw([&](int w) { return red[w * 18]; });
-  if (tid == 128) slab[C * 128 + C + 1] = sumw([&](int w) { return red[w * 18 + 1]; });
-  if (wave == NW - 1) {  // the |dl @ W2| bound: 2 max_row sum_c |dl_c| * max |W2| (head_xent.hip's formula)
-    float wm2 = 0.f;
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wm2 = fmaxf(wm2, fabsf(wl[u][e]));
-    for (int off = 32; off > 0; off >>= 1) wm2 = fmaxf(wm2, __shfl_xor(wm2, off));
-    float am = red[NW * 18];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) am = fmaxf(am, red[NW * 18 + w]);
-    if (lane == 0) hd.bound[blockIdx.x] = 2.f * am * wm2;
-  }
-  st(21);
+  hblk::Args a;
+  a.w2 = hd.w2;
+  a.b2 = hd.b2;
+  a.target = hd.target;
+  a.loss_scale = hd.loss_scale;
+  a.train = true;
+  a.dl = hd.dl;
+  a.part = hd.part + (size_t)blockIdx.x * (C * 128 + C + 2);
+  a.bound = hd.bound + blockIdx.x;
+  hblk::block_head<C>(y, smem, a, m0, p.M, wave, lane, [](int, int, bool, const float (&)[4]) {}, stamp);
 }
 
 // fp32 [N][K] -> zero-padded fp16 planes [NPL][N][Kp] of W * 2^8 (u8_planes.h)
@@ -1722,8 +1631,8 @@ bool u8_fwd_head_supported(int M, int N, int K, int ldx, const void* X, int C) {
   return u8_fwd_supported(M, N, K, ldx, X) && N == FBN && (C == 2 || C == 10 || C == 16);
 }
 
-// rows per fused-head block: 256 (8 waves, one block per CU) or, with knob U8_FH_WAVES = 4, 128 (two per CU)
-static int fh_rows() { return knob(KNOB_U8_FH_WAVES) == 4 ? FhGeo<2>::ROWS : FhGeo<4>::ROWS; }
+// rows per fused-head block: 256 (8 waves, one block per CU; head_block.h)
+static int fh_rows() { return hblk::ROWS; }
 int u8_fwd_head_blocks(int M) { return (M + fh_rows() - 1) / fh_rows(); }
 
 
@@ -1769,7 +1678,7 @@ bool u8_set_wgrad_stamps(void* buf) {
 void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned short* w_planes, int N, int Kp,
                  const float* bias, float scale, const U8HeadArgs& head, hipStream_t stream) {
   if (N != FBN || !head.dl || !head.mask || !head.part || !head.bound || !bias) abort();  // host contract
-  static_assert(Geo<2, 4>::BM == FhGeo<4>::ROWS && Geo<2, 2>::BM == FhGeo<2>::ROWS, "one fused-head block = its rows");
+  static_assert(Geo<2, 4>::BM == hblk::ROWS, "one fused-head block = its rows");
   FwdParams p{};
   p.X = X;
   p.Wp = w_planes;
@@ -1830,27 +1739,6 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
       default: FH_LAUNCH(NSUB, CC);       \
     }                                     \
   } while (0)
-  if (fh_rows() == FhGeo<2>::ROWS) {  // 4-wave 128-row blocks, two per CU
-#define FH_LAUNCH4(T, CC) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 2, CC>), grid, dim3(256), 0, stream, p)
-#define FH_TAILS4(CC)                     \
-  do {                                    \
-    switch (tail) {                       \
-      case 1: FH_LAUNCH4(1, CC); break;   \
-      case 2: FH_LAUNCH4(2, CC); break;   \
-      case 3: FH_LAUNCH4(3, CC); break;   \
-      default: FH_LAUNCH4(NSUB, CC);      \
-    }                                     \
-  } while (0)
-    switch (head.C) {
-      case 10: FH_TAILS4(10); break;
-      case 2: FH_TAILS4(2); break;
-      case 16: FH_TAILS4(16); break;
-      default: abort();
-    }
-#undef FH_TAILS4
-#undef FH_LAUNCH4
-    return;
-  }
   if (head.C == 10 && knob(KNOB_U8_FH_STAGES) == 3) {  // 3-stage ring (the 784-128-10 MLP)
     switch (tail) {
       case 1: FH_LAUNCH3(1); break;

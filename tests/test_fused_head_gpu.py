@@ -224,44 +224,6 @@ def test_fused_forward_head_three_stage_ring_is_bit_identical(M):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("M", [4096 + 100, 131072])
-@pytest.mark.parametrize("C", [10, 2])
-@pytest.mark.parametrize("defer", [False, True])
-def test_fused_forward_head_four_wave_blocks(M, C, defer):
-    """Knob U8_FH_WAVES=4: 128-row blocks of 4 waves (80 KiB of LDS, two blocks per CU). Per-row results (dl, the
-    ReLU bits) are bit-identical to the 8-wave 256-row blocks (same h, same head_tile.h sequence); the block sums
-    (gW2, gb2, loss, the dl bound) differ only in their blocking."""
-    from simple_distributed_machine_learning_amd import _native
-
-    K = _native.kernels()
-    x8, w1, b1, w2, b2, tgt = _problem(M, C, seed=11)
-    outs = []
-    try:
-        for waves in (8, 4):
-            K.set_knob("U8_FH_WAVES", waves)
-            cache = ops.PlaneCache(w1)
-            dl = torch.full((M, C), float("nan"), device=DEV)
-            mask = torch.zeros(M, N // 32, dtype=torch.int32, device=DEV)
-            gw, gb = torch.zeros(C, N, device=DEV), torch.zeros(C, device=DEV)
-            st = torch.full((2,), 7.0, device=DEV)
-            bound, pend = ops.linear_relu_head_u8(x8, w1, b1, cache, 0, w2, b2, tgt, gw, gb, 1.0 / M, st, True, dl,
-                                                  mask, defer=defer)
-            if defer:
-                pend.run()
-            torch.cuda.synchronize()
-            assert bound.numel() == (M + (256 if waves == 8 else 128) - 1) // (256 if waves == 8 else 128)
-            outs.append((dl, mask, gw, gb, st, bound))
-    finally:
-        K.reset_knobs()
-    (dl8, m8, gw8, gb8, st8, b8), (dl4, m4, gw4, gb4, st4, b4) = outs
-    assert torch.equal(dl4, dl8) and torch.equal(m4, m8)
-    torch.testing.assert_close(gw4, gw8, rtol=1e-5, atol=1e-7)
-    torch.testing.assert_close(gb4, gb8, rtol=1e-5, atol=1e-7)
-    torch.testing.assert_close(st4[0], st8[0], rtol=1e-5, atol=1e-3)
-    assert float(st4[1]) == float(st8[1])
-    assert float(b4.max()) == float(b8.max())  # max over rows of the same per-row terms
-
-
 def test_ds_read_tr8_lane_map():
     """ds_read_b64_tr_b8 (the ring weight gradient's pixel-fragment read, mlp_u8.hip frag_x8): per 16-lane group,
     lane 2q + p addresses row q, bytes 8p .. 8p + 7 of an 8-row x 16-byte block; lane i of the group receives byte

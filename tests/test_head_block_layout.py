@@ -1,0 +1,79 @@
+"""Bank-conflict freedom of head_block.h's LDS images, by enumeration of every lane's address (no GPU).
+
+The fused uint8 forward + head (mlp_u8.hip) and the standalone block head (head_xent.hip) stage h as fp16 planes
+in an image of 8-byte granules (4 rows of one hidden unit), granule q of hidden unit h at q ^ gswz(h); the dl^T
+image uses the same swizzle per class. This replays the kernel's address arithmetic for each access and checks,
+per LDS lane group, that no bank is hit by two different addresses (MI355X_MICROARCH.md, LDS table):
+ds_write_b64 in 4 groups of 16 lanes (bank = dword mod 32), ds_read_b64 / ds_read_b64_tr_b16 in 2 groups of 32
+lanes (bank = dword mod 64).
+"""
+ROWS = 256
+PLANE_B = 128 * ROWS * 2
+
+
+def gswz(h):
+    return ((h >> 2) & 1) | (((h >> 3) & 1) << 1) | ((h & 1) << 2) | (((h >> 1) & 1) << 3) | (((h >> 3) & 1) << 4)
+
+
+def hoff(p, h, q):
+    return p * PLANE_B + h * (ROWS * 2) + 8 * (q ^ gswz(h))
+
+
+def _conflicts(addrs, groups, banks):
+    """max over groups and banks of the number of DISTINCT dwords hitting one bank (1 = conflict-free);
+    addrs: lane -> byte address of its 8-byte access"""
+    worst = 1
+    for grp in groups:
+        per_bank = {}
+        for lane in grp:
+            for d in (addrs[lane] // 4, addrs[lane] // 4 + 1):
+                per_bank.setdefault(d % banks, set()).add(d)
+        worst = max(worst, max(len(v) for v in per_bank.values()))
+    return worst
+
+
+W16 = [list(range(16 * k, 16 * k + 16)) for k in range(4)]   # ds_write_b64
+R32 = [list(range(32)), list(range(32, 64))]                  # ds_read_b64, ds_read_b64_tr_b16
+
+
+def test_h_image_writes_conflict_free():
+    # wave (wm, wn), tile (i, j), register quad rq: lane -> hidden 64 wn + 32 j + (lane & 31),
+    # granule 16 wm + 8 i + 2 rq + (lane >> 5)
+    for wm in range(4):
+        for wn in range(2):
+            for i in range(2):
+                for j in range(2):
+                    for rq in range(4):
+                        for p in range(2):
+                            addrs = [hoff(p, 64 * wn + 32 * j + (l & 31), 16 * wm + 8 * i + 2 * rq + (l >> 5))
+                                     for l in range(64)]
+                            assert _conflicts(addrs, W16, 32) == 1
+
+
+def test_logits_transposed_reads_conflict_free():
+    # B operand of the 16x16x32 logits MFMA: lane (r = l & 15, g = l >> 4) reads image row (hidden)
+    # 32 kk + 8 g + (r >> 2) (+ 4), granule 4 T + (r & 3)
+    for T in range(16):
+        for kk in range(4):
+            for plus in (0, 4):
+                addrs = [hoff(0, 32 * kk + 8 * (l >> 4) + ((l & 15) >> 2) + plus, 4 * T + (l & 3)) for l in range(64)]
+                assert _conflicts(addrs, R32, 64) == 1
+
+
+def test_dw2_reads_conflict_free():
+    # B operand of the dW2 MFMA: lane (r, g) reads hidden 16 w + r, granules 8 ks + 2 g (+ 1); the dl^T image the
+    # same with the class r
+    for w in range(8):
+        for ks in range(8):
+            for e in (0, 1):
+                addrs = [hoff(1, 16 * w + (l & 15), 8 * ks + 2 * (l >> 4) + e) for l in range(64)]
+                assert _conflicts(addrs, R32, 64) == 1
+    for ks in range(8):
+        for e in (0, 1):
+            addrs = [(l & 15) * (ROWS * 2) + 8 * ((8 * ks + 2 * (l >> 4) + e) ^ gswz(l & 15)) for l in range(64)]
+            assert _conflicts(addrs, R32, 64) == 1
+
+
+def test_swizzle_is_a_bijection_per_row():
+    for h in range(128):
+        assert sorted(q ^ gswz(h) for q in range(64)) == list(range(64))

@@ -20,7 +20,7 @@ from simple_distributed_machine_learning_amd._native import kernels  # noqa: E40
 K = kernels()
 from simple_distributed_machine_learning_amd import _native  # noqa: E402
 
-_native.apply_knobs_from_env()  # SDML_KNOBS="U8_FH_WAVES=4,..." (A/B)
+_native.apply_knobs_from_env()  # SDML_KNOBS="U8_FH_STAGES=3,..." (A/B)
 M, N, Kd, C = 131072, 128, 784, 10
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(5)

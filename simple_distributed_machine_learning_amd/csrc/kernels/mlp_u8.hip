@@ -156,7 +156,8 @@ long long* g_u8w_stamps = nullptr;  // u8_set_wgrad_stamps: the weight gradient'
 // LDS images of one stage: X [BM rows][FBK bytes], W [NPL planes][128 rows][FBK fp16], chunks at
 // xpos / wpos. The DMA writes 1 KiB per wave-instruction lane-linearly (lane i -> bytes 16i..), so
 // the swizzle goes on the per-lane SOURCE address.
-template <int WMT, int NWR>
+// pieces [U0, U1) of the wave's GLDS_X + GLDS_W DMA pieces of the stage (the spread K-step issues them in parts)
+template <int WMT, int NWR, int U0 = 0, int U1 = 1 << 20>
 __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* st, int m0, int n0, int k0, int wave,
                                            int lane) {
   using G = Geo<WMT, NWR>;
@@ -167,6 +168,7 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
   constexpr int XROWS = 1024 / FBK;  // pixel rows per DMA instruction
 #pragma unroll
   for (int u = 0; u < G::GLDS_X; ++u) {
+    if (u < U0 || u >= U1) continue;
     const int q = wave + G::WAVES * u;
     const int row = XROWS * q + lane / XCH;
     const int pos = lane % XCH;
@@ -180,6 +182,7 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
   const size_t plane = (size_t)p.N * p.Kp;
 #pragma unroll
   for (int u = 0; u < G::GLDS_W; ++u) {
+    if (G::GLDS_X + u < U0 || G::GLDS_X + u >= U1) continue;
     const int q = wave + G::WAVES * u;
     const int pl = q / WINST;
     const int row = WROWS * (q % WINST) + lane / WCH;
@@ -201,7 +204,11 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
 // classifier head on h (fused_head_epilogue), h is never stored
 // NSK: LDS ring stages. The fused-head variant may take 3 (the head epilogue needs 148 KiB anyway, so a third
 // 48 KiB stage costs no occupancy: two K-steps of pixel DMA in flight instead of one).
-template <int MODE, int WMT, int TAIL, int NWR, int HEADC = 0, int NSK = NS>
+// DMAS: 0 = the next stage's DMA issued right after the K-step's barrier (all pieces before the first MFMA), 1 = spread
+// over the first substeps (two pieces after each substep's MFMAs: the issue cost of a piece hides under MFMAs instead
+// of delaying the first ones; knob U8_FWD_DMA_SPREAD, NS == 2 only), 2 = 1 + each substep's fragments read one substep
+// ahead
+template <int MODE, int WMT, int TAIL, int NWR, int HEADC = 0, int NSK = NS, int DMAS = 0>
 __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(FwdParams p) {  // (4-wave blocks: 2 waves per SIMD, <= 256 VGPRs, two blocks per CU)
   constexpr int NS = NSK;  // (shadows the file-wide default inside this kernel)
   using G = Geo<WMT, NWR, NSK>;
@@ -276,9 +283,11 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
   // DMA_AT: substep after whose MFMAs a K-step issues the next stage's DMA (-1: right after the barrier, the
   // production schedule; MODE 8 / 9, experiments: after substep 0 / 1)
   constexpr int DMA_AT = MODE == 8 ? 0 : (MODE == 9 ? 1 : -1);
+  static_assert(DMAS == 0 || (NSK == 2 && DMA_AT < 0 && MODE != 11 && GLDS_PER_STAGE == 6),
+                "spread DMA: the 2-stage production loop, 6 pieces per wave");
   // PIPE: the pipelined K-step (MODE 11, experiments)
   constexpr bool PIPE = MODE == 11;
-  auto kstep = [&](const unsigned char* st, auto ns_c, auto&& dma) {
+  auto kstep = [&](const unsigned char* st, auto ns_c, auto&& dma, auto&& dma_part) {
     constexpr int NS_ = decltype(ns_c)::value;
     if constexpr (MODE == 1) return;
     // (reading substep s+1's fragments ahead of substep s's MFMAs, pinned with sched_barrier,
@@ -303,6 +312,22 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
         compute(s, ar[(s >> 1) & 1], b[s & 1]);
         __builtin_amdgcn_sched_barrier(0);
       }
+    } else if constexpr (DMAS == 2) {
+      // spread DMA + substep s + 1's fragment reads issued ahead of substep s's MFMAs (register double buffer, the
+      // compiler's own placement: no sched_barrier)
+      u32x4 ar[2][WMT];
+      f16x8 b[2][2][NPL];
+      load_a(st, 0, ar[0]);
+      load_b(st, 0, b[0]);
+#pragma unroll
+      for (int s = 0; s < NS_; ++s) {
+        if (s + 1 < NS_) {
+          if ((s + 1) % 2 == 0) load_a(st, (s + 1) >> 1, ar[((s + 1) >> 1) & 1]);
+          load_b(st, s + 1, b[(s + 1) & 1]);
+        }
+        compute(s, ar[(s >> 1) & 1], b[s & 1]);
+        dma_part(s);
+      }
     } else {
       u32x4 ar[WMT];
       f16x8 b[2][NPL];
@@ -312,6 +337,7 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
         load_b(st, s, b);
         compute(s, ar, b);
         if (s == DMA_AT) dma();
+        if constexpr (DMAS == 1) dma_part(s);
       }
     }
   };
@@ -350,17 +376,26 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
     }
   };
   auto no_dma = [] {};
+  auto no_dma_part = [](int) {};
   for (int t = 0; t + 1 < nk; ++t) {  // NS == 2: K-step t + 1 always exists here
-    sync_step(t, std::integral_constant<bool, (DMA_AT < 0 && !PIPE)>{});
+    sync_step(t, std::integral_constant<bool, (DMA_AT < 0 && !PIPE && DMAS == 0)>{});
     if (t < 13) U8_STAMP(2 + t, __builtin_amdgcn_s_memtime);
-    kstep(smem + (t % NS) * STAGE, std::integral_constant<int, NSUB>{}, [&] {
-      if (NS == 2 || t + NS - 1 < nk)
-        issue_stage<WMT, NWR>(p, smem + ((t + NS - 1) % NS) * STAGE, m0, n0, (t + NS - 1) * FBK, wave, lane);
-    });
+    unsigned char* nxt = smem + ((t + NS - 1) % NS) * STAGE;
+    const int k1 = (t + NS - 1) * FBK;
+    kstep(
+        smem + (t % NS) * STAGE, std::integral_constant<int, NSUB>{},
+        [&] {
+          if (NS == 2 || t + NS - 1 < nk) issue_stage<WMT, NWR>(p, nxt, m0, n0, k1, wave, lane);
+        },
+        [&](int sub) {  // DMAS == 1 (NS == 2): two of the 6 pieces after each of the first three substeps
+          if (sub == 0) issue_stage<WMT, NWR, 0, 2>(p, nxt, m0, n0, k1, wave, lane);
+          else if (sub == 1) issue_stage<WMT, NWR, 2, 4>(p, nxt, m0, n0, k1, wave, lane);
+          else if (sub == 2) issue_stage<WMT, NWR, 4, 1 << 20>(p, nxt, m0, n0, k1, wave, lane);
+        });
   }
   {  // last K-step: only the substeps holding k < K (lane half 0 covers the first FBK / 2 k)
     sync_step(nk - 1, std::integral_constant<bool, (NS > 2)>{});
-    kstep(smem + ((nk - 1) % NS) * STAGE, std::integral_constant<int, TAIL>{}, no_dma);
+    kstep(smem + ((nk - 1) % NS) * STAGE, std::integral_constant<int, TAIL>{}, no_dma, no_dma_part);
   }
   U8_STAMP(15, __builtin_amdgcn_s_memtime);
   if constexpr (MODE == 10) {  // timing only: the K loop alone (keep the accumulators alive)
@@ -1694,6 +1729,7 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
   p.prio = knob(KNOB_U8_FWD_PRIO);
   const dim3 grid(u8_fwd_head_blocks(M), 1);
   const int tail = tail_substeps(K);
+  const int spread = knob(KNOB_U8_FWD_DMA_SPREAD);  // 0, 1 (spread DMA), 2 (+ fragment reads one substep ahead)
 #ifdef SDML_KERNEL_EXPERIMENTS  // timing variants (tools/u8_fwd_stamps.py): SDML_U8_FWD_MODE 1-6, 8-10
   static const int fmode = [] {
     const char* e = getenv("SDML_U8_FWD_MODE");
@@ -1728,7 +1764,12 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
     return;
   }
 #endif
-#define FH_LAUNCH(T, CC) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC>), grid, dim3(512), 0, stream, p)
+#define FH_LAUNCH(T, CC)                                                                                    \
+  do {                                                                                                      \
+    if (spread == 2) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC, NS, 2>), grid, dim3(512), 0, stream, p); \
+    else if (spread) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC, NS, 1>), grid, dim3(512), 0, stream, p); \
+    else hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC>), grid, dim3(512), 0, stream, p);               \
+  } while (0)
 #define FH_LAUNCH3(T) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, 10, 3>), grid, dim3(512), 0, stream, p)
 #define FH_TAILS(CC)                      \
   do {                                    \

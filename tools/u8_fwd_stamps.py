@@ -2,9 +2,11 @@
 shape from its s_memtime stamps. Needs the experiments build of _kernels (SDML_KERNEL_EXPERIMENTS=1); the
 production build has no MODE 7 variant and this script exits.
 
-Per (block, wave) the kernel stamps: 1 start, 2..13 after the barriers of K-steps 0..11, 15 after the K loop, 16 after
-the head's entry barrier, 17 h image written, 18 after the barrier, 19 head tiles done, 20 after the barrier,
-21 slab written, 22 end; slots 0 / 23 hold s_memrealtime (100 MHz) at start / end.
+Per (block, wave) the kernel stamps: 1 start, 2..13 after the barriers of K-steps 0..11, 15 after the K loop, 16 at
+the head epilogue's entry, 17 after its first barrier (block max |h| exchanged: h, the ReLU bits and W2 in
+registers), 18 after the second (the fp16 h image written), 19 logits / softmax / dl done, 20 after the third barrier
+(dl^T image), 21 dW2 and the slab row written, 22 end; slots 0 / 23 hold s_memrealtime (100 MHz) at start / end
+(head_block.h).
 Prints medians over workgroups of each phase, split into the first and second round of workgroups (by start time).
 """
 import json
@@ -80,8 +82,8 @@ rank = torch.empty_like(order)
 rank.scatter_(1, order, torch.arange(blocks).expand_as(order))
 rnd = (rank >= 256).double()
 names = {(1, 2): "prologue", (2, 13): "k-steps 0..11 (11 intervals)", (13, 15): "k-steps 11, 12 + tail",
-         (15, 16): "head entry barrier", (16, 17): "h image + mask", (17, 18): "barrier", (18, 19): "head tiles",
-         (19, 20): "barrier", (20, 21): "slab", (21, 22): "exit"}
+         (15, 16): "to epilogue", (16, 17): "h, mask, W2, max + barrier", (17, 18): "h image + barrier",
+         (18, 19): "logits/softmax/dl", (19, 20): "barrier", (20, 21): "dW2 + slab", (21, 22): "exit"}
 for wv in (0, 4, 7):
     for r in (0, 1):
         sel = rnd == r

@@ -42,6 +42,8 @@ typedef float hb_f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 hb_f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 hb_f16x4 __attribute__((ext_vector_type(4)));
 typedef short hb_s16x4 __attribute__((ext_vector_type(4)));
+typedef float hb_f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 hb_f16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int ROWS = 256, HID = 128, NW = 8, NT = 512;
 constexpr int PLANE_B = HID * ROWS * 2;              // bytes per h plane (fp16)
@@ -77,7 +79,6 @@ __device__ __forceinline__ void split2(float x, _Float16& hi, _Float16& lo) {
   hi = static_cast<_Float16>(x);
   lo = static_cast<_Float16>(x - static_cast<float>(hi));
 }
-
 __device__ __forceinline__ hb_f32x4 mfma16(hb_f16x8 a, hb_f16x8 b, hb_f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
@@ -100,12 +101,13 @@ struct Args {
   float* bound;                // optional: this block's 2 max_row sum_c |dl_c| * max |W2|
 };
 
-// y: this wave's 64 x 64 tile of h (rows >= M zero), C layout above. smem: LDS_BYTES, free (the caller's previous
-// use finished with a barrier or not yet started: the first thing here is a barrier). hook(T, row, valid, dz):
-// called per row tile after the softmax with the lane's dz (the standalone head's dx pass; a no-op when fused).
-template <int C, class Hook>
-__device__ __forceinline__ void block_head(const hb_f32x16 (&y)[2][2], unsigned char* smem, const Args& a, int m0,
-                                           int M, int wave, int lane, Hook&& hook, long long* stamp) {
+// prep(y) fills y: this wave's 64 x 64 tile of h (rows >= M zero), C layout above; it runs after W2, the biases and
+// the targets are requested, so their latency hides under it. smem: LDS_BYTES, free (the caller's previous use
+// finished with a barrier or not yet started: the first thing here is a barrier). hook(T, row, valid, dz): called per
+// row tile after the softmax with the lane's dz (the standalone head's dx pass; a no-op when fused).
+template <int C, class Prep, class Hook>
+__device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, const Args& a, int m0, int M, int wave,
+                                           int lane, Hook&& hook, long long* stamp) {
   static_assert(C >= 1 && C <= 16, "one 16-class tile");
   auto st = [&](int k) {
     if (stamp && lane == 0) stamp[k] = (long long)__builtin_amdgcn_s_memtime();
@@ -134,6 +136,8 @@ __device__ __forceinline__ void block_head(const hb_f32x16 (&y)[2][2], unsigned 
 #pragma unroll
   for (int it = 0; it < 2; ++it) tg[it] = (int)a.target[min(m0 + 16 * (wave + NW * it) + r, M - 1)];
 
+  hb_f32x16 y[2][2];
+  prep(y);
   // block max |h| -> plane scale (all waves, after one exchange)
   float hm = 0.f;
 #pragma unroll
@@ -142,14 +146,14 @@ __device__ __forceinline__ void block_head(const hb_f32x16 (&y)[2][2], unsigned 
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) hm = fmaxf(hm, fabsf(y[i][j][q]));
-  for (int off = 32; off > 0; off >>= 1) hm = fmaxf(hm, __shfl_xor(hm, off));
+  hm = wv::max64(hm);
   if (lane == 0) red[wave] = hm;
   float wm2 = 0.f;  // max |W2| (every wave holds all of W2 in registers: the same value in every wave)
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
     for (int e = 0; e < 8; ++e) wm2 = fmaxf(wm2, fabsf(wv[kk][e]));
-  for (int off = 32; off > 0; off >>= 1) wm2 = fmaxf(wm2, __shfl_xor(wm2, off));
+  wm2 = wv::max64(wm2);
   __syncthreads();  // (B1) the maxima are in LDS; the caller's buffers are free
   st(17);
   float bm = red[0];
@@ -157,6 +161,7 @@ __device__ __forceinline__ void block_head(const hb_f32x16 (&y)[2][2], unsigned 
   for (int w = 1; w < NW; ++w) bm = fmaxf(bm, red[w]);
   const int Eh = bexp(bm), Ew = bexp(wm2), Ed = bexp(a.loss_scale);
   const float sh = p2(14 - Eh), sw = p2(14 - Ew), sd = p2(14 - Ed);
+  const hb_f32x2 sh2 = {sh, sh};
 
   // 1. the h image: granule (4 rows) of hidden unit 64 wn + 32 j + r32, rows 64 wm + 32 i + 8 rq + 4 h2 ..
 #pragma unroll
@@ -166,14 +171,14 @@ __device__ __forceinline__ void block_head(const hb_f32x16 (&y)[2][2], unsigned 
       const int hid = 64 * wn + 32 * j + r32;
 #pragma unroll
       for (int rq = 0; rq < 4; ++rq) {
-        hb_f16x4 hi, lo;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          _Float16 a0, a1;
-          split2(y[i][j][4 * rq + e] * sh, a0, a1);
-          hi[e] = a0;
-          lo[e] = a1;
-        }
+        // split2's operations on pairs (v_pk_mul_f32, v_cvt_pk_f16_f32, v_pk_add_f32: the same IEEE results as the
+        // scalar form, half the VALU issue - the epilogue is VALU-bound)
+        const hb_f32x2 x01 = hb_f32x2{y[i][j][4 * rq], y[i][j][4 * rq + 1]} * sh2;
+        const hb_f32x2 x23 = hb_f32x2{y[i][j][4 * rq + 2], y[i][j][4 * rq + 3]} * sh2;
+        const hb_f16x2 h01 = __builtin_convertvector(x01, hb_f16x2), h23 = __builtin_convertvector(x23, hb_f16x2);
+        const hb_f16x2 l01 = __builtin_convertvector(x01 - __builtin_convertvector(h01, hb_f32x2), hb_f16x2);
+        const hb_f16x2 l23 = __builtin_convertvector(x23 - __builtin_convertvector(h23, hb_f32x2), hb_f16x2);
+        const hb_f16x4 hi = {h01[0], h01[1], h23[0], h23[1]}, lo = {l01[0], l01[1], l23[0], l23[1]};
         const int q = 16 * wm + 8 * i + 2 * rq + h2;
         *reinterpret_cast<hb_f16x4*>(smem + hoff(0, hid, q)) = hi;
         *reinterpret_cast<hb_f16x4*>(smem + hoff(1, hid, q)) = lo;
@@ -240,15 +245,11 @@ __device__ __forceinline__ void block_head(const hb_f32x16 (&y)[2][2], unsigned 
   }
   st(19);
   // per-wave partials: loss, correct, |dl| bound, db (16 rows of each tile summed over the lane's row index)
-  for (int off = 32; off > 0; off >>= 1) {
-    acc.loss += __shfl_xor(acc.loss, off);
-    acc.corr += __shfl_xor(acc.corr, off);
-    acc.amx = fmaxf(acc.amx, __shfl_xor(acc.amx, off));
-  }
+  acc.loss = wv::sum64(acc.loss);
+  acc.corr = wv::sum64(acc.corr);
+  acc.amx = wv::max64(acc.amx);
 #pragma unroll
-  for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) dbs[v] += __shfl_xor(dbs[v], off);
+  for (int v = 0; v < 4; ++v) dbs[v] = wv::sum16(dbs[v]);
   if (lane == 0) {
     red[136 + wave] = acc.loss;
     red[144 + wave] = acc.corr;

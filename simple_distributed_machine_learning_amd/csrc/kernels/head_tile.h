@@ -7,13 +7,15 @@
 // Lane l = (r = l % 16, g = l / 16), fp32 MFMAs (v_mfma_f32_16x16x4_f32):
 //   logits^T = W x^T : A = W (lane: class r), B = x^T (lane: row r), k = 16u + 4g + e over 32 MFMAs;
 //     lane (r, g) ends with row r's logits of classes 4g .. 4g+3 (bias as the initial value), so
-//     softmax / NLL / argmax reduce 4 values in-lane plus two symmetric xor-shuffles
+//     softmax / NLL / argmax reduce 4 values in-lane plus two symmetric permlane swaps (wave_ops.h)
 //   dW^T += x^T dz : x read back transposed from the tile's LDS image (xt_at layout) and dz through a
 //     wave-private 16 x 16 transpose; dW^T stays in registers across the wave's tiles.
 // Reference op: /root/reference/simple_distributed.py:77-79 (fc2, log_softmax), :111 (nll_loss).
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include "wave_ops.h"
 
 namespace sdml {
 namespace headtile {
@@ -68,19 +70,11 @@ __device__ __forceinline__ void softmax_dz(const f32x4m& z, int tg_raw, bool val
       mx = zc[v];
       am = 4 * g + v;
     }
-#pragma unroll
-  for (int off = 16; off <= 32; off <<= 1) {
-    const float om = __shfl_xor(mx, off);
-    const int oa = __shfl_xor(am, off);
-    const bool take = om > mx || (om == mx && oa < am);
-    mx = take ? om : mx;
-    am = take ? oa : am;
-  }
+  wv::argmax_rows(mx, am);
   float se = 0.f;
 #pragma unroll
   for (int v = 0; v < 4; ++v) se += __expf(zc[v] - mx);
-  se += __shfl_xor(se, 16);
-  se += __shfl_xor(se, 32);
+  se = wv::sum_rows(se);
   const float lse = mx + __logf(se);
   const int tg = valid ? tg_raw : -1;
   float zt = zc[0];
@@ -101,9 +95,7 @@ __device__ __forceinline__ void softmax_dz(const f32x4m& z, int tg_raw, bool val
   }
   if (track_amax) {  // (invalid rows and classes >= C hold dz == 0)
     float sa = (fabsf(dz[0]) + fabsf(dz[1])) + (fabsf(dz[2]) + fabsf(dz[3]));
-    sa += __shfl_xor(sa, 16);
-    sa += __shfl_xor(sa, 32);
-    a.amx = fmaxf(a.amx, sa);
+    a.amx = fmaxf(a.amx, wv::sum_rows(sa));
   }
 }
 

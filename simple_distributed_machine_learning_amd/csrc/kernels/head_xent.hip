@@ -648,17 +648,18 @@ __global__ void __launch_bounds__(hblk::NT) head_block_kernel(const float* __res
   const int wm = wave & 3, wn = wave >> 2, h2 = lane >> 5, r32 = lane & 31;
   const int r = lane & 15, g = lane >> 4;
   const int m0 = blockIdx.x * hblk::ROWS;
-  hblk::hb_f32x16 y[2][2];
+  auto prep = [&](hblk::hb_f32x16 (&y)[2][2]) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int row = m0 + 64 * wm + 32 * i + 8 * (q >> 2) + 4 * h2 + (q & 3);
-        const float v = x[(size_t)min(row, M - 1) * HK + 64 * wn + 32 * j + r32];
-        y[i][j][q] = row < M ? v : 0.f;
-      }
+        for (int q = 0; q < 16; ++q) {
+          const int row = m0 + 64 * wm + 32 * i + 8 * (q >> 2) + 4 * h2 + (q & 3);
+          const float v = x[(size_t)min(row, M - 1) * HK + 64 * wn + 32 * j + r32];
+          y[i][j][q] = row < M ? v : 0.f;
+        }
+  };
   float wd[8][4];  // wd[t][kk] = W[class 4 g + kk][hidden 16 t + r] (zero for classes >= C)
   if constexpr (DXP) {
 #pragma unroll
@@ -676,7 +677,7 @@ __global__ void __launch_bounds__(hblk::NT) head_block_kernel(const float* __res
   a.part = part + (size_t)blockIdx.x * (C * HK + C + 2);
   a.bound = dxmax ? dxmax + blockIdx.x : nullptr;
   hblk::block_head<C>(
-      y, smem, a, m0, M, wave, lane,
+      prep, smem, a, m0, M, wave, lane,
       [&](int, int row, bool valid, const float (&dz)[4]) {
         if constexpr (DXP) {
           if (dx) {

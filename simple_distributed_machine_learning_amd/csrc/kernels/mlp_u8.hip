@@ -470,11 +470,35 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
   }
 }
 
-// The classifier head on the block's h, straight from the forward's accumulators (no HBM round trip):
-//  1. h = relu(scale acc + b1) (rows past M zero); the ReLU bits leave by one 8-byte store per lane (lane = row
-//     of the wave, bits from ballots)
-//  2. head_block.h on h: fp16-plane MFMA logits, softmax / NLL / dl, dW2 and the block's slab row, bit-identical
-//     dl to head_xent.hip's standalone block head on the same rows
+// ReLU-bit words of tile (i, j) = (Q >> 5, (Q >> 4) & 1), registers r = Q & 15 .. +3 (rows rw = 32 i + 8 (r >> 2) + e
+// and rw + 4 of the wave, e = 0..3): each ballot's halves go to lanes rw and rw + 4 of mw[j] (lane selects inline
+// constants). The ballots are VALU writes of SGPRs that v_writelane reads as data: the hazard recognizer does not look
+// into the asm string, so it opens with the wait states itself (without them a writelane read the previous ballot).
+template <int Q>
+__device__ __forceinline__ void mask_words(const f32x16 (&y)[2][2], int (&mw)[2]) {
+  if constexpr (Q < 64) {
+    constexpr int i = Q >> 5, j = (Q >> 4) & 1, r = Q & 15, rw = 32 * i + 8 * (r >> 2);
+    const unsigned long long b0 = __ballot(y[i][j][r] > 0.f), b1 = __ballot(y[i][j][r + 1] > 0.f);
+    const unsigned long long b2 = __ballot(y[i][j][r + 2] > 0.f), b3 = __ballot(y[i][j][r + 3] > 0.f);
+    asm("s_nop 4\n\t"
+        "v_writelane_b32 %0, %1, %9\n\tv_writelane_b32 %0, %2, %10\n\t"
+        "v_writelane_b32 %0, %3, %11\n\tv_writelane_b32 %0, %4, %12\n\t"
+        "v_writelane_b32 %0, %5, %13\n\tv_writelane_b32 %0, %6, %14\n\t"
+        "v_writelane_b32 %0, %7, %15\n\tv_writelane_b32 %0, %8, %16"
+        : "+v"(mw[j])
+        : "s"((unsigned)b0), "s"((unsigned)(b0 >> 32)), "s"((unsigned)b1), "s"((unsigned)(b1 >> 32)),
+          "s"((unsigned)b2), "s"((unsigned)(b2 >> 32)), "s"((unsigned)b3), "s"((unsigned)(b3 >> 32)),
+          "i"(rw), "i"(rw + 4), "i"(rw + 1), "i"(rw + 5), "i"(rw + 2), "i"(rw + 6), "i"(rw + 3), "i"(rw + 7));
+    mask_words<Q + 4>(y, mw);
+  }
+}
+
+// The classifier head on the block's h, straight from the forward's accumulators (no HBM round trip): h = relu(scale
+// acc + b1) (rows past M zero) handed to head_block.h: fp16-plane MFMA logits, softmax / NLL / dl, dW2 and the block's
+// slab row, bit-identical dl to head_xent.hip's standalone block head on the same rows. The ReLU bits leave by one
+// 8-byte store per lane: each register's ballot holds one word of two rows of the wave (lanes 0..31: row rw, 32..63:
+// row rw + 4), deposited straight into those rows' lanes by v_writelane (round 4 selected them with compares, and the
+// 64 ballot SGPR pairs spilled)
 template <int C, int NWR>
 __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
                                                     int m0, int wave, int lane, int wm, int wn, long long* stamp) {
@@ -482,30 +506,6 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
   const U8HeadArgs& hd = p.head;
   const int h2 = lane >> 5, r32 = lane & 31;
   if (stamp && lane == 0) stamp[16] = (long long)__builtin_amdgcn_s_memtime();
-  float bv1[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) bv1[j] = p.bias[wn * 64 + 32 * j + r32];
-  const bool ragged = m0 + hblk::ROWS > p.M;  // block-uniform: the last block may hold rows past M
-  f32x16 y[2][2];
-  unsigned mw[2] = {0u, 0u};  // lane L: mask words 2 wn + j of the wave's row L
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rw = 32 * i + (r & 3) + 8 * (r >> 2);  // + 4 h2: row within the wave tile
-        float v = fmaxf(acc[i][j][r] * p.scale + bv1[j], 0.f);  // the plain epilogue's arithmetic
-        if (ragged && m0 + wm * 64 + rw + 4 * h2 >= p.M) v = 0.f;
-        y[i][j][r] = v;
-        const unsigned long long b = __ballot(v > 0.f);
-        if (lane == rw) mw[j] = (unsigned)b;
-        if (lane == rw + 4) mw[j] = (unsigned)(b >> 32);
-      }
-  {
-    const int row = m0 + wm * 64 + lane;
-    if (row < p.M) *reinterpret_cast<uint2*>(hd.mask + (size_t)row * 4 + 2 * wn) = uint2{mw[0], mw[1]};
-  }
   hblk::Args a;
   a.w2 = hd.w2;
   a.b2 = hd.b2;
@@ -515,7 +515,31 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
   a.dl = hd.dl;
   a.part = hd.part + (size_t)blockIdx.x * (C * 128 + C + 2);
   a.bound = hd.bound + blockIdx.x;
-  hblk::block_head<C>(y, smem, a, m0, p.M, wave, lane, [](int, int, bool, const float (&)[4]) {}, stamp);
+  auto prep = [&](hblk::hb_f32x16 (&y)[2][2]) {
+    float bv1[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bv1[j] = p.bias[wn * 64 + 32 * j + r32];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y[i][j][r] = fmaxf(acc[i][j][r] * p.scale + bv1[j], 0.f);  // the plain epilogue's
+    if (m0 + hblk::ROWS > p.M) {  // (block-uniform) the last block's rows past M
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h2 >= p.M) y[i][j][r] = 0.f;
+    }
+    int mw[2] = {0, 0};  // lane L: mask words 2 wn + j of the wave's row L
+    mask_words<0>(y, mw);
+    const int row = m0 + wm * 64 + lane;
+    if (row < p.M) *reinterpret_cast<uint2*>(hd.mask + (size_t)row * 4 + 2 * wn) = uint2{(unsigned)mw[0], (unsigned)mw[1]};
+  };
+  hblk::block_head<C>(prep, smem, a, m0, p.M, wave, lane, [](int, int, bool, const float (&)[4]) {}, stamp);
 }
 
 // fp32 [N][K] -> zero-padded fp16 planes [NPL][N][Kp] of W * 2^8 (u8_planes.h)

@@ -50,9 +50,16 @@ constexpr int PLANE_B = HID * ROWS * 2;              // bytes per h plane (fp16)
 constexpr int DLT_OFF = 2 * PLANE_B;                  // dl^T planes [2][16][ROWS] fp16
 constexpr int DLT_PLANE_B = 16 * ROWS * 2;
 constexpr int RED_OFF = DLT_OFF + 2 * DLT_PLANE_B;    // floats below
-// red: [0, 8) wave max |h|, [8, 136) db partials [wave][16], [136, 144) loss, [144, 152) correct, [152, 160) amx
-constexpr int RED_FLOATS = 160;
-constexpr int LDS_BYTES = RED_OFF + RED_FLOATS * 4;
+// red: [0, 8) wave max |h|, [8, 136) db partials [wave][16], [136, 144) loss, [144, 152) correct, [152, 160) amx,
+// [160, 168) wave max |W2|
+constexpr int RED_FLOATS = 168;
+// W2 staged once per block: [16][W2P] bytes, rows padded by 16 B (the A-operand reads, 16 rows per 16-lane group,
+// hit 64 distinct banks). Past everything else: the fused forward's LDS ring (<= 144 KiB) ends before RED_OFF, so the
+// block may write it while slower waves still read their last K-step
+constexpr int W2P = HID * 4 + 16;
+constexpr int W2_OFF = RED_OFF + RED_FLOATS * 4;
+constexpr int LDS_BYTES = W2_OFF + 16 * W2P;
+static_assert(W2_OFF % 16 == 0, "W2 staging alignment");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 
 // granule swizzle of hidden unit (or class) h: bits (h2, h3, h0, h1, h3) -> bits 0..4
@@ -79,6 +86,17 @@ __device__ __forceinline__ void split2(float x, _Float16& hi, _Float16& lo) {
   hi = static_cast<_Float16>(x);
   lo = static_cast<_Float16>(x - static_cast<float>(hi));
 }
+// the lo planes of a pair: fp16(x - hi) as fma(hi, -1, x) rounded once (x - hi is exact in fp32: the same bits as
+// split2). Written out because hipcc turns the scalar form back into conversions and a packed fma (6 instead of 4
+// instructions per pair with the hi plane's v_pk_mul_f32 + v_cvt_pk_f16_f32)
+__device__ __forceinline__ hb_f16x2 lo_pair(hb_f16x2 h, hb_f32x2 x) {
+  unsigned lo;
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(lo)
+      : "v"(__builtin_bit_cast(unsigned, h)), "v"(x[0]), "v"(x[1]));
+  return __builtin_bit_cast(hb_f16x2, lo);
+}
 __device__ __forceinline__ hb_f32x4 mfma16(hb_f16x8 a, hb_f16x8 b, hb_f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
@@ -101,13 +119,35 @@ struct Args {
   float* bound;                // optional: this block's 2 max_row sum_c |dl_c| * max |W2|
 };
 
-// prep(y) fills y: this wave's 64 x 64 tile of h (rows >= M zero), C layout above; it runs after W2, the biases and
-// the targets are requested, so their latency hides under it. smem: LDS_BYTES, free (the caller's previous use
-// finished with a barrier or not yet started: the first thing here is a barrier). hook(T, row, valid, dz): called per
-// row tile after the softmax with the lane's dz (the standalone head's dx pass; a no-op when fused).
+// The block's global operands of the head, as loaded (clamped addresses; the masks for classes >= C are applied in
+// block_head): one float4 of W2 per thread (flat index tid: the block stages W2 in LDS once - each wave loading all of
+// W2 in its A-operand layout cost 8 waves x 8 KB of vector-memory traffic per block, ~2K cycles per round by the
+// stamps), the biases of classes 4g .. 4g+3 and the targets of the lane's two row tiles. The fused forward loads them
+// inside its K loop (their latency hides there; no value is used before the epilogue - a select on them in the
+// prologue made hipcc wait for the loads before the first DMA); the standalone head right before block_head.
+struct Operands {
+  hb_f32x4 w2c;
+  headtile::f32x4m b;
+  int tg[2];
+};
+template <int C>
+__device__ __forceinline__ void load_operands(const Args& a, int m0, int M, int wave, int lane, Operands& o) {
+  const int r = lane & 15, g = lane >> 4;
+  o.w2c = reinterpret_cast<const hb_f32x4*>(a.w2)[min(wave * 64 + lane, C * HID / 4 - 1)];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) o.b[v] = a.b2[min(4 * g + v, C - 1)];
+#pragma unroll
+  for (int it = 0; it < 2; ++it)  // the low word of the int64 class index (a dwordx2 load whose dead high half hipcc
+                                  // reused as a register made it wait for the load right away)
+    o.tg[it] = reinterpret_cast<const int*>(a.target)[2 * (size_t)min(m0 + 16 * (wave + NW * it) + r, M - 1)];
+}
+
+// prep(y) fills y: this wave's 64 x 64 tile of h (rows >= M zero), C layout above. smem: LDS_BYTES, free (the caller's
+// previous use finished with a barrier or not yet started: the first thing here is a barrier). hook(T, row, valid, dz):
+// called per row tile after the softmax with the lane's dz (the standalone head's dx pass; a no-op when fused).
 template <int C, class Prep, class Hook>
-__device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, const Args& a, int m0, int M, int wave,
-                                           int lane, Hook&& hook, long long* stamp) {
+__device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, const Args& a, const Operands& ops, int m0,
+                                           int M, int wave, int lane, Hook&& hook, long long* stamp) {
   static_assert(C >= 1 && C <= 16, "one 16-class tile");
   auto st = [&](int k) {
     if (stamp && lane == 0) stamp[k] = (long long)__builtin_amdgcn_s_memtime();
@@ -116,25 +156,11 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
   const int wm = wave & 3, wn = wave >> 2, h2 = lane >> 5, r32 = lane & 31;
   const int r = lane & 15, g = lane >> 4;
   const int tid = wave * 64 + lane;
-
-  // W2 (fp32, registers): lane (class r, k-group g) holds W2[r][32 kk + 8 g + e]; bias of classes 4g.., targets
-  float wv[4][8];
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    const float* src = a.w2 + (size_t)min(r, C - 1) * HID + 32 * kk + 8 * g;
-    const hb_f32x4 u0 = *reinterpret_cast<const hb_f32x4*>(src), u1 = *reinterpret_cast<const hb_f32x4*>(src + 4);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      wv[kk][e] = r < C ? u0[e] : 0.f;
-      wv[kk][4 + e] = r < C ? u1[e] : 0.f;
-    }
-  }
+  if (tid < C * HID / 4) *reinterpret_cast<hb_f32x4*>(smem + W2_OFF + (tid >> 5) * W2P + 16 * (tid & 31)) = ops.w2c;
   headtile::f32x4m bv;
 #pragma unroll
-  for (int v = 0; v < 4; ++v) bv[v] = (4 * g + v) < C ? a.b2[4 * g + v] : 0.f;
-  int tg[2];
-#pragma unroll
-  for (int it = 0; it < 2; ++it) tg[it] = (int)a.target[min(m0 + 16 * (wave + NW * it) + r, M - 1)];
+  for (int v = 0; v < 4; ++v) bv[v] = (4 * g + v) < C ? ops.b[v] : 0.f;
+  const int tg[2] = {ops.tg[0], ops.tg[1]};
 
   hb_f32x16 y[2][2];
   prep(y);
@@ -147,18 +173,33 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
 #pragma unroll
       for (int q = 0; q < 16; ++q) hm = fmaxf(hm, fabsf(y[i][j][q]));
   hm = wv::max64(hm);
-  if (lane == 0) red[wave] = hm;
-  float wm2 = 0.f;  // max |W2| (every wave holds all of W2 in registers: the same value in every wave)
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) wm2 = fmaxf(wm2, fabsf(wv[kk][e]));
-  wm2 = wv::max64(wm2);
-  __syncthreads();  // (B1) the maxima are in LDS; the caller's buffers are free
+  // max |W2| over the staged chunks (threads past C * HID / 4 hold a clamped duplicate)
+  const float wc = fmaxf(fmaxf(fabsf(ops.w2c[0]), fabsf(ops.w2c[1])), fmaxf(fabsf(ops.w2c[2]), fabsf(ops.w2c[3])));
+  const float wmw = wv::max64(wc);
+  if (lane == 0) {
+    red[wave] = hm;
+    red[160 + wave] = wmw;
+  }
+  __syncthreads();  // (B1) the maxima and W2 are in LDS; the caller's buffers are free
   st(17);
-  float bm = red[0];
+  float bm = red[0], wm2 = red[160];
 #pragma unroll
-  for (int w = 1; w < NW; ++w) bm = fmaxf(bm, red[w]);
+  for (int w = 1; w < NW; ++w) {
+    bm = fmaxf(bm, red[w]);
+    wm2 = fmaxf(wm2, red[160 + w]);
+  }
+  // W2 (A operands of the logits): lane (class r, k-group g) takes W2[r][32 kk + 8 g + e] (zero for classes >= C)
+  float wv[4][8];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const unsigned char* src = smem + W2_OFF + min(r, C - 1) * W2P + 4 * (32 * kk + 8 * g);
+    const hb_f32x4 u0 = *reinterpret_cast<const hb_f32x4*>(src), u1 = *reinterpret_cast<const hb_f32x4*>(src + 16);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      wv[kk][e] = r < C ? u0[e] : 0.f;
+      wv[kk][4 + e] = r < C ? u1[e] : 0.f;
+    }
+  }
   const int Eh = bexp(bm), Ew = bexp(wm2), Ed = bexp(a.loss_scale);
   const float sh = p2(14 - Eh), sw = p2(14 - Ew), sd = p2(14 - Ed);
   const hb_f32x2 sh2 = {sh, sh};
@@ -171,14 +212,15 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
       const int hid = 64 * wn + 32 * j + r32;
 #pragma unroll
       for (int rq = 0; rq < 4; ++rq) {
-        // split2's operations on pairs (v_pk_mul_f32, v_cvt_pk_f16_f32, v_pk_add_f32: the same IEEE results as the
-        // scalar form, half the VALU issue - the epilogue is VALU-bound)
+        // split2's operations, the hi planes on pairs (v_pk_mul_f32, v_cvt_pk_f16_f32) and each lo as one mixed
+        // fma (v_fma_mix{lo,hi}_f16: fp16(x - hi) from the f32 x and the f16 hi): the same IEEE results as the
+        // scalar form in 4 instead of 8 instructions per pair - the epilogue is VALU-bound
         const hb_f32x2 x01 = hb_f32x2{y[i][j][4 * rq], y[i][j][4 * rq + 1]} * sh2;
         const hb_f32x2 x23 = hb_f32x2{y[i][j][4 * rq + 2], y[i][j][4 * rq + 3]} * sh2;
         const hb_f16x2 h01 = __builtin_convertvector(x01, hb_f16x2), h23 = __builtin_convertvector(x23, hb_f16x2);
-        const hb_f16x2 l01 = __builtin_convertvector(x01 - __builtin_convertvector(h01, hb_f32x2), hb_f16x2);
-        const hb_f16x2 l23 = __builtin_convertvector(x23 - __builtin_convertvector(h23, hb_f32x2), hb_f16x2);
-        const hb_f16x4 hi = {h01[0], h01[1], h23[0], h23[1]}, lo = {l01[0], l01[1], l23[0], l23[1]};
+        const hb_f16x4 hi = {h01[0], h01[1], h23[0], h23[1]};
+        const hb_f16x2 l01 = lo_pair(h01, x01), l23 = lo_pair(h23, x23);
+        const hb_f16x4 lo = {l01[0], l01[1], l23[0], l23[1]};
         const int q = 16 * wm + 8 * i + 2 * rq + h2;
         *reinterpret_cast<hb_f16x4*>(smem + hoff(0, hid, q)) = hi;
         *reinterpret_cast<hb_f16x4*>(smem + hoff(1, hid, q)) = lo;

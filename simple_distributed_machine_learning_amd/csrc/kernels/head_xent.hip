@@ -676,8 +676,10 @@ __global__ void __launch_bounds__(hblk::NT) head_block_kernel(const float* __res
   a.dl = dl;
   a.part = part + (size_t)blockIdx.x * (C * HK + C + 2);
   a.bound = dxmax ? dxmax + blockIdx.x : nullptr;
+  hblk::Operands ops;
+  hblk::load_operands<C>(a, m0, M, wave, lane, ops);
   hblk::block_head<C>(
-      prep, smem, a, m0, M, wave, lane,
+      prep, smem, a, ops, m0, M, wave, lane,
       [&](int, int row, bool valid, const float (&dz)[4]) {
         if constexpr (DXP) {
           if (dx) {

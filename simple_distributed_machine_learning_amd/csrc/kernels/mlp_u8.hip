@@ -44,6 +44,7 @@
 #include "lds_dma.h"
 #include "kernels.h"
 #include "sgd_rule.h"
+#include "wave_ops.h"
 #include "u8_planes.h"
 
 namespace sdml {
@@ -198,7 +199,11 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
 // host so the kernel carries one straight-line tail)
 template <int C, int NWR>
 __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
-                                                    int m0, int wave, int lane, int wm, int wn, long long* stamp);
+                                                    int m0, int wave, int lane, int wm, int wn,
+                                                    const hblk::Operands& ops, const float (&bv1)[2], long long* stamp);
+template <int C>
+__device__ __forceinline__ void fused_head_prefetch(const FwdParams& p, int m0, int wave, int lane, int wn,
+                                                    hblk::Operands& ops, float (&bv1)[2]);
 
 // HEADC = 0: store h = act(scale acc + b) (+ its ReLU bits when p.mask); HEADC = C > 0: the fused
 // classifier head on h (fused_head_epilogue), h is never stored
@@ -226,6 +231,11 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
   const int h = lane >> 5, r32 = lane & 31;
   U8_STAMP(0, __builtin_amdgcn_s_memrealtime);
   U8_STAMP(1, __builtin_amdgcn_s_memtime);
+  // the head's W2, biases and targets (and fc1's bias): requested inside the K loop (K-step nk - 4), used after it.
+  // (Requested here, at the start, they cost as much in the prologue as they saved in the epilogue: 256 blocks x 8
+  // waves x 8 KB of W2 reads in one burst with the first DMA stages, stamps r5)
+  hblk::Operands hops;
+  float hb1[2];
 
   f32x16 acc[WMT][2];
 #pragma unroll
@@ -380,6 +390,9 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
   for (int t = 0; t + 1 < nk; ++t) {  // NS == 2: K-step t + 1 always exists here
     sync_step(t, std::integral_constant<bool, (DMA_AT < 0 && !PIPE && DMAS == 0)>{});
     if (t < 13) U8_STAMP(2 + t, __builtin_amdgcn_s_memtime);
+    if constexpr (HEADC > 0) {
+      if (t == nk - 4) fused_head_prefetch<HEADC>(p, m0, wave, lane, wn, hops, hb1);
+    }
     unsigned char* nxt = smem + ((t + NS - 1) % NS) * STAGE;
     const int k1 = (t + NS - 1) * FBK;
     kstep(
@@ -411,7 +424,7 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
   }
 
   if constexpr (HEADC > 0) {
-    fused_head_epilogue<HEADC, NWR>(p, acc, smem, m0, wave, lane, wm, wn,
+    fused_head_epilogue<HEADC, NWR>(p, acc, smem, m0, wave, lane, wm, wn, hops, hb1,
                                MODE == 7 ? p.stamps + ((size_t)blockIdx.x * G::WAVES + wave) * U8_NSTAMP : nullptr);
     U8_STAMP(22, __builtin_amdgcn_s_memtime);
     U8_STAMP(U8_NSTAMP - 1, __builtin_amdgcn_s_memrealtime);
@@ -499,13 +512,9 @@ __device__ __forceinline__ void mask_words(const f32x16 (&y)[2][2], int (&mw)[2]
 // 8-byte store per lane: each register's ballot holds one word of two rows of the wave (lanes 0..31: row rw, 32..63:
 // row rw + 4), deposited straight into those rows' lanes by v_writelane (round 4 selected them with compares, and the
 // 64 ballot SGPR pairs spilled)
-template <int C, int NWR>
-__device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
-                                                    int m0, int wave, int lane, int wm, int wn, long long* stamp) {
-  static_assert(NWR == 4, "head_block.h: 8 waves of 64 x 64, 256 rows");
+template <int C>
+__device__ __forceinline__ hblk::Args fused_head_args(const FwdParams& p) {
   const U8HeadArgs& hd = p.head;
-  const int h2 = lane >> 5, r32 = lane & 31;
-  if (stamp && lane == 0) stamp[16] = (long long)__builtin_amdgcn_s_memtime();
   hblk::Args a;
   a.w2 = hd.w2;
   a.b2 = hd.b2;
@@ -515,16 +524,41 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
   a.dl = hd.dl;
   a.part = hd.part + (size_t)blockIdx.x * (C * 128 + C + 2);
   a.bound = hd.bound + blockIdx.x;
-  auto prep = [&](hblk::hb_f32x16 (&y)[2][2]) {
-    float bv1[2];
+  return a;
+}
+
+template <int C>
+__device__ __forceinline__ void fused_head_prefetch(const FwdParams& p, int m0, int wave, int lane, int wn,
+                                                    hblk::Operands& ops, float (&bv1)[2]) {
+  hblk::load_operands<C>(fused_head_args<C>(p), m0, p.M, wave, lane, ops);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bv1[j] = p.bias[wn * 64 + 32 * j + r32];
+  for (int j = 0; j < 2; ++j) bv1[j] = p.bias[wn * 64 + 32 * j + (lane & 31)];
+}
+
+template <int C, int NWR>
+__device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
+                                                    int m0, int wave, int lane, int wm, int wn,
+                                                    const hblk::Operands& ops, const float (&bv1)[2], long long* stamp) {
+  static_assert(NWR == 4, "head_block.h: 8 waves of 64 x 64, 256 rows");
+  const U8HeadArgs& hd = p.head;
+  const int h2 = lane >> 5;
+  if (stamp && lane == 0) stamp[16] = (long long)__builtin_amdgcn_s_memtime();
+  const hblk::Args a = fused_head_args<C>(p);
+  auto prep = [&](hblk::hb_f32x16 (&y)[2][2]) {
+    // the plain epilogue's fmaxf(fma(acc, scale, b), 0), the fmas on pairs (v_pk_fma_f32: the same roundings)
+    const hblk::hb_f32x2 sc2 = {p.scale, p.scale};
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j) {
+        const hblk::hb_f32x2 b2 = {bv1[j], bv1[j]};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) y[i][j][r] = fmaxf(acc[i][j][r] * p.scale + bv1[j], 0.f);  // the plain epilogue's
+        for (int r = 0; r < 16; r += 2) {
+          const hblk::hb_f32x2 v = __builtin_elementwise_fma(hblk::hb_f32x2{acc[i][j][r], acc[i][j][r + 1]}, sc2, b2);
+          y[i][j][r] = fmaxf(v[0], 0.f);
+          y[i][j][r + 1] = fmaxf(v[1], 0.f);
+        }
+      }
     if (m0 + hblk::ROWS > p.M) {  // (block-uniform) the last block's rows past M
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -539,7 +573,7 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
     const int row = m0 + wm * 64 + lane;
     if (row < p.M) *reinterpret_cast<uint2*>(hd.mask + (size_t)row * 4 + 2 * wn) = uint2{(unsigned)mw[0], (unsigned)mw[1]};
   };
-  hblk::block_head<C>(prep, smem, a, m0, p.M, wave, lane, [](int, int, bool, const float (&)[4]) {}, stamp);
+  hblk::block_head<C>(prep, smem, a, ops, m0, p.M, wave, lane, [](int, int, bool, const float (&)[4]) {}, stamp);
 }
 
 // fp32 [N][K] -> zero-padded fp16 planes [NPL][N][Kp] of W * 2^8 (u8_planes.h)
@@ -1087,9 +1121,15 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
   const int n0 = (p.g0 + (p.xcd ? (L % G8) / 8 : L % p.groups)) * GHN;
   const int r0 = split * p.rows_per_split;
   const int nk = min(p.rows_per_split, p.M - r0) / GBK;  // host: M % GBK == 0
-  float dz_up, out_scale;
-  wgrad_scales<2>(p, n0, r0, t, reinterpret_cast<float*>(rsm), dz_up, out_scale);
+  float dz_up = 0.f, out_scale = 0.f;
+  // The head's per-block bounds (one per thread): their load goes out with W2's and their block max travels with the
+  // prologue's barrier (float slots in dz buffer 2, first written in K-step 0), instead of a phase of its own in front
+  // of the DMA (wgrad_scales: a global round trip and two barriers, ~2.5K cycles by the stamps)
+  const bool fast_bound = p.amax != nullptr && p.namax <= GT;
+  if (!fast_bound) wgrad_scales<2>(p, n0, r0, t, reinterpret_cast<float*>(rsm), dz_up, out_scale);
   if (nk <= 0) return;  // (block-uniform; after wgrad_scales' barriers)
+  const float av = fast_bound ? p.amax[min(t, p.namax - 1)] : 0.f;
+  float* bred = reinterpret_cast<float*>(rsm + RDZ_OFF + 2 * RDZ_BUF * 2);
   U8W_STAMP(2, __builtin_amdgcn_s_memtime);
 
   // DMA: one resource per operand from this split's first row (rows past M read as zero), a per-lane offset per piece
@@ -1277,7 +1317,7 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
     // prologue: side data of K-steps 0..3 (one group), pixels of 0, 1, 2 (a group each); wait for all but the last
     // pixel group, build dz 0 and 1, publish them, read k-substep 0 of K-step 0
     // (W2 values in registers first: the compiler's own wait for them would be a vmcnt(0) behind the DMA it cannot see)
-    asm volatile("" ::"v"(w4[0]), "v"(w4[1]), "v"(w4[2]), "v"(w4[3]));
+    asm volatile("" ::"v"(w4[0]), "v"(w4[1]), "v"(w4[2]), "v"(w4[3]), "v"(av));  // (and the bound: waited here, not behind the DMA)
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
       bdma16_asm(wave > 0 && wave < 4 && ks < nk ? r3 : rnull, voff[3], (unsigned)ks * step3,
@@ -1288,8 +1328,20 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
       bdma16_asm(wave == 0 ? r3 : rnull, voff[3], (unsigned)(kx < nk ? kx : 0) * step3,
                  wave == 0 ? dst3(kx, 0) : rsm + RSCR_OFF);
     }
+    if (fast_bound) {
+      const float bw = wv::max64(av);
+      if (lane == 0) bred[wave] = bw;
+    }
     wait_vm<4>();
     __syncthreads();
+    if (fast_bound) {  // = wgrad_scales' amax path
+      float bnd = bred[0];
+#pragma unroll
+      for (int w = 1; w < GT / 64; ++w) bnd = fmaxf(bnd, bred[w]);
+      const int E = bound_exp(bnd);
+      dz_up = pow2f(14 - E);
+      out_scale = p.scale * pow2f(E - 14);
+    }
     build_dz(0);
     if (nk > 1) build_dz(1);
     __syncthreads();

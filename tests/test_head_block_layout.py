@@ -77,3 +77,20 @@ def test_dw2_reads_conflict_free():
 def test_swizzle_is_a_bijection_per_row():
     for h in range(128):
         assert sorted(q ^ gswz(h) for q in range(64)) == list(range(64))
+
+
+def test_w2_staging_reads_conflict_free():
+    # W2 staged as [16][W2P] bytes (W2P = 128 * 4 + 16); lane (r = l & 15, g = l >> 4) reads row min(r, C - 1),
+    # bytes 4 (32 kk + 8 g) (+ 16) with ds_read_b128: 4 groups of 16 lanes, bank = dword mod 64
+    W2P = 128 * 4 + 16
+    W16 = [list(range(16 * k, 16 * k + 16)) for k in range(4)]
+    for C in (2, 10, 16):
+        for kk in range(4):
+            for e in (0, 16):
+                addrs = [min(l & 15, C - 1) * W2P + 4 * (32 * kk + 8 * (l >> 4)) + e for l in range(64)]
+                for grp in W16:
+                    per_bank = {}
+                    for lane in grp:
+                        for d in range(addrs[lane] // 4, addrs[lane] // 4 + 4):
+                            per_bank.setdefault(d % 64, set()).add(d)
+                    assert max(len(v) for v in per_bank.values()) == 1

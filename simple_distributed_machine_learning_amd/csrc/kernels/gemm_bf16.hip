@@ -31,6 +31,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "gelu.h"
 #include "kernels.h"
@@ -113,25 +114,26 @@ __device__ __forceinline__ s16x4 ds_tr16(const unsigned char* p) {
 
 // epilogue shared by both main loops: bf16 rows through the (free) stage buffers, 16-B row pieces to HBM
 // WNW: waves along N (4: the 256 x 256 tile's 2 x 4 waves; 2: the 256 x 128 tile's 2 x 2)
-template <int EPI, int WNW = 4>
-__device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&acc)[8][4], unsigned char* smem, int m0,
+// NJ: 16-column tiles per wave (4: the wave owns 64 columns; 3: 48, the 256 x 192 tile)
+template <int EPI, int WNW = 4, int NJ = 4>
+__device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&acc)[8][NJ], unsigned char* smem, int m0,
                                                    int n0, int wave, int lane) {
   const int wm = wave / WNW, wn = wave % WNW;
   const int g = lane >> 4, l16 = lane & 15;
-  // wave image [128 rows][64 cols] bf16 (128 B rows, 16-B chunks swizzled like the A image)
+  // wave image [128 rows][64 cols] bf16 (128 B rows, 16-B chunks swizzled like the A image; NJ = 3 uses 48 of them)
   unsigned char* W = smem + wave * (128 * 128);
-  float bj[4] = {0.f, 0.f, 0.f, 0.f};
+  float bj[NJ] = {};
   if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = min(n0 + wn * 64 + 16 * j + l16, p.N - 1);
+    for (int j = 0; j < NJ; ++j) {
+      const int col = min(n0 + wn * 16 * NJ + 16 * j + l16, p.N - 1);
       bj[j] = bf2f(p.bias[col]);
     }
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * i + 4 * g + r, col = 16 * j + l16;
@@ -144,8 +146,8 @@ __device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&ac
   for (int it = 0; it < 16; ++it) {
     const int row = 8 * it + (lane >> 3), ch = lane & 7;
     const u16x8 v = *reinterpret_cast<const u16x8*>(W + row * 128 + 16 * (ch ^ rk_swz(row)));
-    const int grow = m0 + wm * 128 + row, gcol = n0 + wn * 64 + 8 * ch;
-    if (grow >= p.M || gcol >= p.N || p.nostore) continue;  // (N % 8 == 0: a chunk is all in or all out)
+    const int grow = m0 + wm * 128 + row, gcol = n0 + wn * 16 * NJ + 8 * ch;
+    if (ch >= 2 * NJ || grow >= p.M || gcol >= p.N || p.nostore) continue;  // (N % 8 == 0: a chunk is all in or out)
     u16x8 o = v;
     if constexpr (EPI == EPI_BIAS_GELU) {
       u16x8* ap = reinterpret_cast<u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
@@ -270,13 +272,19 @@ __global__ void __launch_bounds__(GT) gemm_bf16_kernel(GP p) {
 // long done. Half-tiles past the last K-step re-read it into consumed slots (uniform vmcnt counting).
 constexpr int HT = 16384, NSLOT = 10;
 
-template <int Q>
+// DMA pieces (1 KiB per wave) of half-tile Q: 2, except the B half-tile of n-tiles 2.. when NJ == 3 (16 rows per wave)
+template <int Q, int NJ>
+constexpr int half_pieces() {
+  return (Q == 2 && NJ == 3) ? 1 : 2;
+}
+
+template <int Q, int NJ = 4>
 __device__ __forceinline__ void issue_half(const GP& p, unsigned char* smem, int h, int nk, int m0, int n0, int wave,
                                            int lane) {
   const int k0 = min(h >> 2, nk - 1) * TK;
   unsigned char* slot = smem + (h % NSLOT) * HT;
 #pragma unroll
-  for (int v = 0; v < 2; ++v) {
+  for (int v = 0; v < half_pieces<Q, NJ>(); ++v) {
     const int qq = wave + 8 * v;         // 1-KiB DMA block of the slot
     const int lr = 8 * qq + (lane >> 3);  // slot row 0..127
     const int c = (lane & 7) ^ rk_swz(lr);
@@ -284,14 +292,23 @@ __device__ __forceinline__ void issue_half(const GP& p, unsigned char* smem, int
       const int tr = (lr >> 6) * 128 + (Q == 3 ? 64 : 0) + (lr & 63);
       glds16(p.A + (size_t)min(m0 + tr, p.M - 1) * p.lda + k0 + 8 * c, slot + 1024 * qq);
     } else {
-      const int tr = (lr >> 5) * 64 + (Q == 2 ? 32 : 0) + (lr & 31);
+      // wave wn's columns wn * 16 NJ ..: n-tiles 0, 1 in half-tile 1 (32 rows each), the rest in half-tile 2
+      constexpr int R2 = 16 * (NJ - 2);  // rows per wave in half-tile 2
+      const int tr = Q == 1 ? (lr >> 5) * 16 * NJ + (lr & 31) : (lr / R2) * 16 * NJ + 32 + (lr % R2);
       glds16(p.B + (size_t)min(n0 + tr, p.N - 1) * p.ldb + k0 + 8 * c, slot + 1024 * qq);
     }
   }
 }
 
-template <int EPI>
+// NJ = 3 (256 x 192 tiles, wave tile 128 x 48): half-tile 2 carries one 16-row n-tile per wave (1 DMA piece instead of
+// 2), quadrant-col 1 is that one n-tile, and the counted waits keep exactly the last three half-tiles in flight
+// (2 + 2 + 1 pieces). It exists for wave quantization: at N = 768 the 256-wide tiles make 192 tiles of a 16384-row
+// GEMM, 3/4 of the 256 CUs; 192-wide ones make 256.
+template <int EPI, int NJ = 4>
 __global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
+  static_assert(NJ == 3 || NJ == 4, "n-tiles per wave");
+  constexpr int BN = 64 * NJ, NJ1 = NJ - 2;  // tile width; n-tiles of quadrant-col 1
+  constexpr int INFLIGHT = half_pieces<0, NJ>() + half_pieces<1, NJ>() + half_pieces<2, NJ>();
   __shared__ __attribute__((aligned(16))) unsigned char smem[NSLOT * HT];  // the epilogue reuses it
   const int nwg = p.tiles_m * p.tiles_n;
   int wg = blockIdx.x;
@@ -300,20 +317,21 @@ __global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
   }
   const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;
-  const int m0 = tm * TM, n0 = tn * TN;
+  const int m0 = tm * TM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int g = lane >> 4, l16 = lane & 15;
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // fragment byte offsets inside a slot: A (m-tile i of the quadrant, substep s), B (n-tile jj, substep s)
-  int aoff[4][2], boff[2][2];
+  // fragment byte offsets inside a slot: A (m-tile i of the quadrant, substep s), B (n-tile jj, substep s: boff in
+  // half-tile 1, boff1 in half-tile 2)
+  int aoff[4][2], boff[2][2], boff1[NJ1][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -328,33 +346,44 @@ __global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
       const int r = wn * 32 + 16 * jj + l16;
       boff[jj][s2] = r * 128 + 16 * ((4 * s2 + g) ^ rk_swz(r));
     }
+#pragma unroll
+  for (int jj = 0; jj < NJ1; ++jj)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r = wn * 16 * NJ1 + 16 * jj + l16;
+      boff1[jj][s2] = r * 128 + 16 * ((4 * s2 + g) ^ rk_swz(r));
+    }
 
   const int nk = p.K / TK;
-  issue_half<0>(p, smem, 0, nk, m0, n0, wave, lane);
-  issue_half<1>(p, smem, 1, nk, m0, n0, wave, lane);
-  issue_half<2>(p, smem, 2, nk, m0, n0, wave, lane);
-  issue_half<3>(p, smem, 3, nk, m0, n0, wave, lane);
-  issue_half<0>(p, smem, 4, nk, m0, n0, wave, lane);
-  issue_half<1>(p, smem, 5, nk, m0, n0, wave, lane);
-  issue_half<2>(p, smem, 6, nk, m0, n0, wave, lane);
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // K-step 0's 4 half-tiles
+  issue_half<0, NJ>(p, smem, 0, nk, m0, n0, wave, lane);
+  issue_half<1, NJ>(p, smem, 1, nk, m0, n0, wave, lane);
+  issue_half<2, NJ>(p, smem, 2, nk, m0, n0, wave, lane);
+  issue_half<3, NJ>(p, smem, 3, nk, m0, n0, wave, lane);
+  issue_half<0, NJ>(p, smem, 4, nk, m0, n0, wave, lane);
+  issue_half<1, NJ>(p, smem, 5, nk, m0, n0, wave, lane);
+  issue_half<2, NJ>(p, smem, 6, nk, m0, n0, wave, lane);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");  // K-step 0's 4 half-tiles
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if (wm == 1) __builtin_amdgcn_s_barrier();  // wave row 1 runs one barrier behind row 0
 
-  bf16x8 a[4][2], b0[2][2], b1[2][2];
-  auto mfma_quadrant = [&](int qm, const bf16x8 (&bb)[2][2], int qn) {
+  bf16x8 a[4][2], b0[2][2], b1[NJ1][2];
+  auto mfma_quadrant = [&](int qm, const auto& bb, auto qn_c) {
+    constexpr int QN = decltype(qn_c)::value;
+    constexpr int NQ = QN == 0 ? 2 : NJ1;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-          acc[4 * qm + i][2 * qn + jj] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], bb[jj][s2], acc[4 * qm + i][2 * qn + jj], 0, 0, 0);
+        for (int jj = 0; jj < NQ; ++jj)
+          acc[4 * qm + i][2 * QN + jj] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], bb[jj][s2], acc[4 * qm + i][2 * QN + jj], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, 1>;
   auto sync_mid = [&]() {
     __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -378,40 +407,40 @@ __global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = ld_b128(s0 + aoff[i][s2]);
-    issue_half<3>(p, smem, h, nk, m0, n0, wave, lane);
+    issue_half<3, NJ>(p, smem, h, nk, m0, n0, wave, lane);
     sync_mid();
-    mfma_quadrant(0, b0, 0);
+    mfma_quadrant(0, b0, Q0{});
     sync_end();
     // phase 1: B quadrant-col 1; quadrant (0, 1)
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj)
+    for (int jj = 0; jj < NJ1; ++jj)
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) b1[jj][s2] = ld_b128(s2p + boff[jj][s2]);
-    issue_half<0>(p, smem, h + 1, nk, m0, n0, wave, lane);
+      for (int s2 = 0; s2 < 2; ++s2) b1[jj][s2] = ld_b128(s2p + boff1[jj][s2]);
+    issue_half<0, NJ>(p, smem, h + 1, nk, m0, n0, wave, lane);
     sync_mid();
-    mfma_quadrant(0, b1, 1);
+    mfma_quadrant(0, b1, Q1{});
     sync_end();
     // phase 2: A quadrant-row 1; quadrant (1, 1)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = ld_b128(s3 + aoff[i][s2]);
-    issue_half<1>(p, smem, h + 2, nk, m0, n0, wave, lane);
+    issue_half<1, NJ>(p, smem, h + 2, nk, m0, n0, wave, lane);
     sync_mid();
-    mfma_quadrant(1, b1, 1);
+    mfma_quadrant(1, b1, Q1{});
     sync_end();
     // phase 3: no reads; quadrant (1, 0); retire K-step t + 1
-    issue_half<2>(p, smem, h + 3, nk, m0, n0, wave, lane);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    issue_half<2, NJ>(p, smem, h + 3, nk, m0, n0, wave, lane);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
     sync_mid();
-    mfma_quadrant(1, b0, 0);
+    mfma_quadrant(1, b0, Q0{});
     sync_end();
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // rejoin wave row 1
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the past-the-end half-tiles, before the epilogue reuses LDS
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  gemm_bf16_epilogue<EPI>(p, acc, smem, m0, n0, wave, lane);
+  gemm_bf16_epilogue<EPI, 4, NJ>(p, acc, smem, m0, n0, wave, lane);
 }
 
 // ---- NT form, 256 x 128 tiles of 4 waves, two workgroups per CU ---------------------------------------
@@ -515,6 +544,27 @@ __global__ void __launch_bounds__(T2_GT, 2) gemm_bf16_t2_kernel(GP p) {
 
 }  // namespace
 
+// 256 x 192 tiles instead of 256 x 256 when they fill the CUs' rounds better (wave quantization): time ~ rounds x tile
+// width, rounds = ceil(tiles / CUs). Knob GEMM_BF16_N192: -1 auto (default), 0 never, 1 always (A/B).
+static int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t pr;
+    cus = hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0 ? pr.multiProcessorCount : 256;
+  }
+  return cus;
+}
+static bool nt4_use_192(int tiles_m, int N) {
+  const int k = knob(KNOB_GEMM_BF16_N192);
+  if (k >= 0) return k == 1;
+  const int64_t cus = device_cus();
+  const int64_t r256 = ((int64_t)tiles_m * ((N + 255) / 256) + cus - 1) / cus;
+  const int64_t r192 = ((int64_t)tiles_m * ((N + 191) / 192) + cus - 1) / cus;
+  return r192 * 192 * 100 < r256 * 256 * 97;  // a clear (>3 %) win only: the 192-wide loop is less efficient per flop
+}
+
 bool gemm_bf16_supported(int M, int N, int K, int lda, int ldb, int ldc, bool b_kn) {
   // K whole K-steps; 16-B aligned rows for the DMA and the row-piece stores
   return M >= 1 && N >= 8 && K >= TK && K % TK == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
@@ -568,12 +618,21 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
   if (b_kn) {
     GB_EPI(1);
   } else if (nt4) {
+    const bool n192 = nt4_use_192(p.tiles_m, N);
+    if (n192) p.tiles_n = (N + 191) / 192;
+    const dim3 g4(p.tiles_m * p.tiles_n);
+#define NT4_LAUNCH(E)                                                                                  \
+  do {                                                                                                 \
+    if (n192) hipLaunchKernelGGL((gemm_bf16_nt4_kernel<E, 3>), g4, dim3(GT), 0, stream, p);            \
+    else hipLaunchKernelGGL((gemm_bf16_nt4_kernel<E, 4>), g4, dim3(GT), 0, stream, p);                 \
+  } while (0)
     switch (epi) {
-      case EPI_BIAS: hipLaunchKernelGGL((gemm_bf16_nt4_kernel<EPI_BIAS>), grid, dim3(GT), 0, stream, p); break;
-      case EPI_BIAS_GELU: hipLaunchKernelGGL((gemm_bf16_nt4_kernel<EPI_BIAS_GELU>), grid, dim3(GT), 0, stream, p); break;
-      case EPI_DGELU: hipLaunchKernelGGL((gemm_bf16_nt4_kernel<EPI_DGELU>), grid, dim3(GT), 0, stream, p); break;
-      default: hipLaunchKernelGGL((gemm_bf16_nt4_kernel<EPI_STORE>), grid, dim3(GT), 0, stream, p); break;
+      case EPI_BIAS: NT4_LAUNCH(EPI_BIAS); break;
+      case EPI_BIAS_GELU: NT4_LAUNCH(EPI_BIAS_GELU); break;
+      case EPI_DGELU: NT4_LAUNCH(EPI_DGELU); break;
+      default: NT4_LAUNCH(EPI_STORE); break;
     }
+#undef NT4_LAUNCH
   } else {
     GB_EPI(0);
   }

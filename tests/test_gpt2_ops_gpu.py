@@ -180,3 +180,30 @@ def test_gemm_bf16_t2_tiles_match_fp32_and_the_256_tile(M, N, Kd):
         K.reset_knobs()
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 192, 64), (300, 776, 192), (4096, 768, 768), (1000, 2304, 3072)])
+def test_gemm_bf16_192_wide_tiles_bit_identical_to_256(M, N, Kd):
+    """Knob GEMM_BF16_N192: the 4-phase NT GEMM on 256 x 192 tiles (wave tile 128 x 48, chosen automatically where it
+    fills the CUs' rounds better, e.g. N = 768 at 16384 rows). Every output element sums the same 32-deep MFMA products
+    in the same k order as on 256 x 256 tiles: bit-identical for each epilogue, and equal to fp32 within bf16."""
+    g = torch.Generator(device="cpu").manual_seed(M + 5 * N)
+    A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    u_in = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    outs = {}
+    try:
+        for n192 in (0, 1):
+            K.set_knob("GEMM_BF16_N192", n192)
+            C0, _ = K.gemm_bf16(A, W, None, False, 0)
+            C1, _ = K.gemm_bf16(A, W, bias, False, 1)
+            y, u = K.gemm_bf16(A, W, bias, False, 5)
+            du, _ = K.gemm_bf16(A, W, None, False, 6, u_in)
+            outs[n192] = (C0, C1, y, u, du)
+            torch.testing.assert_close(C0.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+    finally:
+        K.reset_knobs()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)

@@ -50,9 +50,12 @@ for name, N, Kd in SHAPES:
     err_b = float((dx.float() - ref).abs().max() / ref.abs().max())
     t_mine_b = timeit(lambda: K.gemm_bf16(gy, w, None, True, 0))
     t_lib_b = timeit(lambda: gy @ w)
+    wt = w.t().contiguous()  # the engine's dX path: NT against W^T (ops/linear.py _w_t)
+    t_mine_bt = timeit(lambda: K.gemm_bf16(gy, wt, None, False, 0))
     print(json.dumps({"gemm": name, "M": T, "N": N, "K": Kd,
                       "fwd_us": round(t_mine, 1), "fwd_TFs": round(flops / t_mine / 1e6, 1),
                       "fwd_lib_us": round(t_lib, 1), "fwd_lib_TFs": round(flops / t_lib / 1e6, 1), "fwd_relerr": err_f,
                       "dx_us": round(t_mine_b, 1), "dx_TFs": round(flops / t_mine_b / 1e6, 1),
+                      "dx_nt_us": round(t_mine_bt, 1), "dx_nt_TFs": round(flops / t_mine_bt / 1e6, 1),
                       "dx_lib_us": round(t_lib_b, 1), "dx_lib_TFs": round(flops / t_lib_b / 1e6, 1),
                       "dx_relerr": err_b}), flush=True)

@@ -18,8 +18,8 @@ the main decision of a multi-GPU run, and it is made here from a model instead o
 
 The model (documented in README "Multi-GPU placement") is deliberately simple:
 
-* compute per GPU = rows x ns/row of each stage it runs + a fixed per-step cost (measured on one
-  MI355X, ``ComputeModel``);
+* compute per GPU = rows x ns/row of what it runs (fused stage 0 + 1 for the rows it keeps, stage 0 or stage 1
+  alone for crossing rows) + a fixed per-step cost (measured on one MI355X, ``ComputeModel``);
 * link time = the busiest link's bytes / ``LinkModel.gbps`` + one launch latency per collective;
 * the exchange overlaps compute (the transfers run on RCCL streams beside the kernels of other
   waves and of the local rows): step = max(compute, link) + the part that cannot overlap (the
@@ -58,24 +58,31 @@ class LinkModel:
 
 @dataclass
 class ComputeModel:
-    """Per-row costs of the 784-128-10 stages on one MI355X at 131072 rows per GPU, from the round-3 kernel
-    tables: profiles/r3_unfused_bench_n1_kernel_stats.txt (uint8 forward 61.6 us + weight gradient 78.9 us for
-    stage 0; head 25.8 us for stage 1) and profiles/r3_bench_n1_kernel_stats.txt (reduction/SGD 11.6 us; the
-    step's 174.4 us minus its kernels' 170.7 us of launch gaps). ``wgrad_ns``: the weight gradient alone (the
-    dp split hides range 0's all-reduce under half of it)."""
-    s0_ns: float = 1.072
-    s1_ns: float = 0.197
-    fixed_us: float = 15.3
-    wgrad_ns: float = 0.571
+    """Per-row costs of the 784-128-10 stages on one MI355X at 131072 rows per GPU, from the round-5 kernel tables.
+
+    * rows that stay on their owner run the fused uint8 forward + classifier head and the factored weight gradient:
+      69.3 + 68.5 us (profiles/r5_bench_n1_w2_staged_kernel_stats.txt) -> ``fused_ns``;
+    * rows whose stage 1 runs elsewhere (and pp2dp) run the plain uint8 forward + weight gradient on the owner, 61.8
+      + 72.1 us -> ``s0_ns``, and the standalone block head on the peer, 28.5 us -> ``s1_ns``
+      (profiles/r5_bench_n1_unfused_kernel_stats.txt, SDML_FUSE_HEAD=0);
+    * ``fixed_us``: the slab + head reduction with the fused SGD (11 us) and the launch gaps, i.e. the N = 1 step
+      (0.1515 ms, profiles/r5_bench_n1_head_dpp.jsonl..w2_staged runs) minus its fused kernels;
+    * ``dp_step_us``: what a step with a gradient all-reduce costs on top at N > 1 before any link time - the
+      reduction can no longer apply SGD in the same launch, a separate optimizer launch follows the collective, plus
+      the collective's host and stream overhead: the one-rank RCCL harness (tools/bench_dp_split.py) runs the N > 1
+      path in 0.1754 ms against 0.1515 (profiles/r5_dpsplit_one_rank_rccl.jsonl);
+    * ``split_us``: the split weight gradient's own extra cost (same harness: 0.2099 vs 0.1754 ms);
+    * ``wgrad_ns``: the weight gradient alone (the split hides range 0's all-reduce under half of it)."""
+    fused_ns: float = 1.051
+    s0_ns: float = 1.022
+    s1_ns: float = 0.217
+    fixed_us: float = 13.7
+    wgrad_ns: float = 0.523
     act_bytes: int = 512          # boundary activation per row (128 fp32)
     grad_bytes: int = 40          # factored boundary gradient per row (10 fp32)
     param_bytes: int = 101_770 * 4
-    # N > 1 with a gradient all-reduce: the reduction can no longer apply SGD in the same launch, so a separate
-    # optimizer launch follows the collective (one-rank RCCL harness, profiles/r4_dpsplit_one_rank_rccl.jsonl:
-    # 0.188 vs 0.172 ms per step before any link time)
-    dp_step_us: float = 16.0
-    # the split weight gradient's own extra cost over the whole-gradient kernel (same harness)
-    split_us: float = 33.0
+    dp_step_us: float = 24.0
+    split_us: float = 34.5
 
 
 def dp_split_default() -> bool:
@@ -100,7 +107,11 @@ def predict(placement: str, n: int, batch_per_gpu: int, waves: int = 2, phi: Opt
         phi = (n - 1) / n
     if placement == "dp":
         phi = 0.0
-    compute_us = B * (comp.s0_ns + comp.s1_ns) / 1e3 + comp.fixed_us
+    if placement == "pp2dp":
+        compute_us = B * (comp.s0_ns + comp.s1_ns) / 1e3 + comp.fixed_us
+    else:  # rows kept on their owner run fused; for the crossing share the owner runs stage 0, a peer stage 1
+        phi_c = (n - 1) / n if placement == "rotate" else float(phi or 0.0)
+        compute_us = B * ((1 - phi_c) * comp.fused_ns + phi_c * (comp.s0_ns + comp.s1_ns)) / 1e3 + comp.fixed_us
     if placement == "pp2dp":
         if n % 2:
             raise ValueError("pp2dp needs an even number of GPUs")
@@ -144,7 +155,7 @@ def balanced_fraction(n: int, batch_per_gpu: int, link: LinkModel = LinkModel(),
     if n == 1:
         return 0.0
     B = float(batch_per_gpu)
-    compute_us = B * (comp.s0_ns + comp.s1_ns) / 1e3 + comp.fixed_us
+    compute_us = B * comp.fused_ns / 1e3 + comp.fixed_us  # (phi small: most rows stay)
     budget_us = link.link_budget * compute_us - 2 * waves * link.collective_us
     if budget_us <= 0:
         return 0.0
@@ -178,3 +189,20 @@ def choose(n: int, batch_per_gpu: int, waves: int = 2, link: LinkModel = LinkMod
 
 def model_dict(link: LinkModel = LinkModel(), comp: ComputeModel = ComputeModel()) -> Dict[str, Dict[str, float]]:
     return {"link": asdict(link), "compute": asdict(comp)}
+
+
+def markdown_table(ns=(2, 4, 8), batch_per_gpu: int = 131072) -> str:
+    """README's placement table ("Multi-GPU placement"), generated from :func:`table` (tests/test_placement_doc.py
+    checks that README holds exactly this text)."""
+    rows = ["| N | predicted step (ms) and samples/s: `dp` | `balanced` (φ of the rows cross) | `rotate` (all links) "
+            "| `pp2dp` (the reference's cut, per pair) |", "|---|---|---|---|---|"]
+    for n in ns:
+        t = table(n, batch_per_gpu)
+
+        def cell(p):
+            v = t[p]
+            extra = f" (φ = {v['cross_fraction']})" if p == "balanced" else ""
+            return f"{v['step_ms']:.3f} · {v['samples_per_s'] / 1e9:.2f} G{extra}"
+
+        rows.append(f"| {n} | " + " | ".join(cell(p) for p in ("dp", "balanced", "rotate", "pp2dp")) + " |")
+    return "\n".join(rows)

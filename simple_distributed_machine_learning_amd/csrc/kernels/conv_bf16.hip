@@ -998,6 +998,51 @@ __global__ void __launch_bounds__(256) conv_weight_transform_kernel(const u16* _
   }
 }
 
+// every 3x3 weight of a step in one launch (ResNet-18: 16 weights, 16 launches of ~9 us, mostly launch latency):
+// block b works on the weight whose block range holds it (a uniform scan of the kernel-argument table)
+struct WtBatch {
+  const u16* w[kWtBatchMax];
+  u16* fwd[kWtBatchMax];
+  u16* dgrad[kWtBatchMax];
+  int Co[kWtBatchMax], C[kWtBatchMax], block0[kWtBatchMax + 1];
+  int n;
+};
+
+// A block transposes a tile of 32 output x 32 input channels through LDS: it reads the 32 rows of 32 x 9
+// contiguous weights (576 B each) and writes 64-B runs of both layouts (fwd [co][tap][ci0..+31], dgrad
+// [ci][8 - tap][co0..+31]); an element-wise loop wrote each layout with 2-byte stores strided by C or 9 Co (36 us
+// for ResNet-18's 11M weights, most of it write amplification).
+constexpr int WT_T = 32;
+
+__global__ void __launch_bounds__(256) conv_weight_transform_batched_kernel(WtBatch b) {
+  __shared__ u16 tile[WT_T][WT_T * 9 + 2];  // [co][ci * 9 + tap] (+2: row starts on distinct banks)
+  int k = 0;
+  for (int j = 1; j < b.n; ++j) k = (int)blockIdx.x >= b.block0[j] ? j : k;
+  const int Co = b.Co[k], C = b.C[k];
+  const int tiles_c = (C + WT_T - 1) / WT_T;
+  const int t = blockIdx.x - b.block0[k];
+  const int co0 = (t / tiles_c) * WT_T, ci0 = (t % tiles_c) * WT_T;
+  const int nco = min(WT_T, Co - co0), nci = min(WT_T, C - ci0);
+  const u16* w = b.w[k];
+  for (int i = threadIdx.x; i < WT_T * WT_T * 9; i += 256) {
+    const int r = i / (WT_T * 9), c = i % (WT_T * 9);
+    if (r < nco && c < nci * 9) tile[r][c] = w[((int64_t)(co0 + r) * C + ci0) * 9 + c];
+  }
+  __syncthreads();
+  u16* fwd = b.fwd[k];
+  for (int i = threadIdx.x; i < WT_T * 9 * WT_T; i += 256) {  // fwd: (co, tap) rows of ci0..
+    const int ci = i % WT_T, rt = i / WT_T, tap = rt % 9, co = rt / 9;
+    if (co < nco && ci < nci) fwd[((int64_t)(co0 + co) * 9 + tap) * C + ci0 + ci] = tile[co][ci * 9 + tap];
+  }
+  u16* dgrad = b.dgrad[k];
+  if (dgrad) {
+    for (int i = threadIdx.x; i < WT_T * 9 * WT_T; i += 256) {  // dgrad: (ci, tap) rows of co0..
+      const int co = i % WT_T, rt = i / WT_T, tap = rt % 9, ci = rt / 9;
+      if (co < nco && ci < nci) dgrad[((int64_t)(ci0 + ci) * 9 + (8 - tap)) * Co + co0 + co] = tile[co][ci * 9 + tap];
+    }
+  }
+}
+
 // ---- stem: one input channel (MNIST), 3x3 / stride 1 / pad 1 -----------------------------------
 // K = 9 is far too short for the matrix cores: both passes are plain streaming kernels at the
 // output/gradient bandwidth. Forward: a thread owns 16 output channels of one pixel (weights in
@@ -1113,6 +1158,24 @@ void conv3x3_weight_transform_bf16(const void* w_torch, void* fwd, void* dgrad, 
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(conv_weight_transform_kernel, dim3(blocks), dim3(256), 0, stream,
                      static_cast<const u16*>(w_torch), static_cast<u16*>(fwd), static_cast<u16*>(dgrad), Co, C);
+}
+
+void conv3x3_weight_transform_batched_bf16(const void* const* w, void* const* fwd, void* const* dgrad, const int* Co,
+                                           const int* C, int n, hipStream_t stream) {
+  WtBatch b{};
+  b.n = n;
+  int blocks = 0;
+  for (int k = 0; k < n; ++k) {
+    b.w[k] = static_cast<const u16*>(w[k]);
+    b.fwd[k] = static_cast<u16*>(fwd[k]);
+    b.dgrad[k] = static_cast<u16*>(dgrad[k]);
+    b.Co[k] = Co[k];
+    b.C[k] = C[k];
+    b.block0[k] = blocks;
+    blocks += ((Co[k] + WT_T - 1) / WT_T) * ((C[k] + WT_T - 1) / WT_T);  // one 32 x 32-channel tile per block
+  }
+  b.block0[n] = blocks;
+  if (blocks > 0) hipLaunchKernelGGL(conv_weight_transform_batched_kernel, dim3(blocks), dim3(256), 0, stream, b);
 }
 
 int conv_part_rows(int Nb, int OH, int OW) { return (Nb * OH * OW + BM - 1) / BM; }

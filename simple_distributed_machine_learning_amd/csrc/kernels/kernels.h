@@ -351,6 +351,10 @@ void wgrad_bf16(const void* gy, const void* x, void* gw, void* gb, float* worksp
 bool conv3x3_bf16_supported(int C, int Co);
 // torch [Co][C][3][3] weight -> forward layout [Co][9][C] and/or dgrad layout [C][9][Co] (flipped taps); either may be null
 void conv3x3_weight_transform_bf16(const void* w_torch, void* fwd, void* dgrad, int Co, int C, hipStream_t stream);
+// up to kWtBatchMax weights' forward (and, where dgrad[k] is set, dgrad) layouts in one launch
+constexpr int kWtBatchMax = 32;
+void conv3x3_weight_transform_batched_bf16(const void* const* w, void* const* fwd, void* const* dgrad, const int* Co,
+                                           const int* C, int n, hipStream_t stream);
 // add (optional, y's layout): y = bf16(conv + add). part (optional): BatchNorm partials of y,
 // [conv_part_rows(Nb, OH, OW)][2][Co] fp32 (per 256-pixel tile: sum y, sum y^2), for bn_nhwc_fwd_bf16.
 int conv_part_rows(int Nb, int OH, int OW);

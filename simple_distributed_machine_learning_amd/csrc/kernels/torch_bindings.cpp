@@ -561,6 +561,40 @@ std::tuple<torch::Tensor, torch::Tensor> conv3x3_weights_bf16(torch::Tensor w) {
   return {f, d};
 }
 
+// the kernel layouts of several 3x3 weights in one launch, into caller-owned buffers (ops/conv.py keeps one pair per
+// weight across optimizer steps): fwd[k] [Co][9][C], dgrad[k] [C][9][Co] or None (forward layout only)
+void conv3x3_weights_batched_bf16(std::vector<torch::Tensor> ws, std::vector<torch::Tensor> fwd,
+                                  std::vector<c10::optional<torch::Tensor>> dgrad) {
+  TORCH_CHECK(ws.size() == fwd.size() && ws.size() == dgrad.size(), "conv3x3_weights_batched_bf16: list lengths");
+  const void* wp[sdml::kWtBatchMax];
+  void* fp[sdml::kWtBatchMax];
+  void* dp[sdml::kWtBatchMax];
+  int co[sdml::kWtBatchMax], ci[sdml::kWtBatchMax];
+  for (size_t b0 = 0; b0 < ws.size(); b0 += sdml::kWtBatchMax) {
+    const int n = (int)std::min<size_t>(sdml::kWtBatchMax, ws.size() - b0);
+    for (int k = 0; k < n; ++k) {
+      const torch::Tensor& w = ws[b0 + k];
+      check_conv_w(w);
+      const int64_t Co = w.size(0), C = w.size(1);
+      const torch::Tensor& f = fwd[b0 + k];
+      TORCH_CHECK(f.is_cuda() && f.scalar_type() == torch::kBFloat16 && f.is_contiguous() && f.numel() == Co * 9 * C,
+                  "conv3x3_weights_batched_bf16: forward layout buffer");
+      wp[k] = w.data_ptr();
+      fp[k] = f.data_ptr();
+      dp[k] = nullptr;
+      if (dgrad[b0 + k].has_value() && dgrad[b0 + k]->defined()) {
+        const torch::Tensor& d = *dgrad[b0 + k];
+        TORCH_CHECK(d.is_cuda() && d.scalar_type() == torch::kBFloat16 && d.is_contiguous() && d.numel() == Co * 9 * C,
+                    "conv3x3_weights_batched_bf16: dgrad layout buffer");
+        dp[k] = d.data_ptr();
+      }
+      co[k] = (int)Co;
+      ci[k] = (int)C;
+    }
+    sdml::conv3x3_weight_transform_batched_bf16(wp, fp, dp, co, ci, n, cur_stream());
+  }
+}
+
 // y (channels-last [N][Co][H][W]) = conv3x3(x, w) with wt from conv3x3_weight_bf16(w, dgrad=false)
 // the optional epilogue operands of the implicit-GEMM convolutions: an addend in the output's layout
 // and the BatchNorm partials [conv_part_rows][2][Co] fp32 of the output
@@ -1825,6 +1859,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bf16_supported", &wgrad_bf16_supported_op, "shape check for wgrad_bf16_ (contiguous operands)");
   m.def("conv3x3_weight_bf16", &conv3x3_weight_bf16, "3x3 conv weight -> kernel layout (forward / dgrad)");
   m.def("conv3x3_weights_bf16", &conv3x3_weights_bf16, "3x3 conv weight -> (forward, dgrad) kernel layouts");
+  m.def("conv3x3_weights_batched_bf16", &conv3x3_weights_batched_bf16,
+        "several 3x3 conv weights -> their kernel layouts in caller-owned buffers, one launch");
   m.def("conv3x3_fwd_bf16", &conv3x3_fwd_bf16, "3x3 stride-1 pad-1 conv, channels-last bf16 (implicit GEMM)",
         py::arg("x"), py::arg("wt"), py::arg("add") = py::none(), py::arg("part") = py::none());
   m.def("conv_part_rows", &conv_part_rows, "rows of the BatchNorm partials a convolution epilogue writes");

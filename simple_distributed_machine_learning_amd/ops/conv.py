@@ -112,6 +112,24 @@ def bump_weight_generation():
     _WCACHE.clear()
 
 
+# Every 3x3 weight seen so far keeps one pair of layout buffers across optimizer steps (_KNOWN: id -> (weakref, wt,
+# wd or None)). The first layout request of a step re-derives them for ALL live known weights in one launch
+# (conv3x3_weights_batched_bf16): a ResNet-18 step made 16 transform launches of ~9 us each, mostly launch
+# latency (profiles/r5_resnet18_kernel_stats.txt). Reusing the buffers is safe: a step's backward reads its layouts
+# before the optimizer step that bumps WEIGHT_GEN, and the next step's forward rewrites them after it.
+_KNOWN = {}
+
+
+def _known_put(w, wt, wd):
+    k = id(w)
+
+    def _gone(r, k=k):
+        if _KNOWN.get(k, (None,))[0] is r:
+            _KNOWN.pop(k, None)
+
+    _KNOWN[k] = (weakref.ref(w, _gone), wt, wd)
+
+
 def _weight_layouts(w, need_dgrad: bool):
     K = kernels()
     capturing = torch.cuda.is_current_stream_capturing() or not _WCACHE_ON
@@ -119,13 +137,32 @@ def _weight_layouts(w, need_dgrad: bool):
     hit = None if capturing else _cache_get(_WCACHE, w)
     if hit is not None and hit[0] == key and (hit[2] is not None or not need_dgrad):
         return hit[1], hit[2]
-    if need_dgrad:
-        wt, wd = K.conv3x3_weights_bf16(w)
-    else:
-        wt, wd = K.conv3x3_weight_bf16(w, False), None
-    if not capturing:
-        _cache_put(_WCACHE, w, (key, wt, wd))
-    return wt, wd
+    if capturing:
+        if need_dgrad:
+            return K.conv3x3_weights_bf16(w)
+        return K.conv3x3_weight_bf16(w, False), None
+    kn = _KNOWN.get(id(w))
+    if kn is None or kn[0]() is not w or (need_dgrad and kn[2] is None):
+        Co, C = w.shape[0], w.shape[1]
+        wt = torch.empty((Co, 9, C), dtype=w.dtype, device=w.device)
+        wd = torch.empty((C, 9, Co), dtype=w.dtype, device=w.device) if need_dgrad else None
+        _known_put(w, wt, wd)
+    # this weight and every other live known weight whose layouts are stale, in one launch
+    todo = []
+    for k, (ref, wt, wd) in list(_KNOWN.items()):
+        ww = ref()
+        if ww is None or ww.device != w.device or ww.dtype != w.dtype or not ww.is_contiguous():
+            continue
+        kk = (ww.data_ptr(), ww._version, WEIGHT_GEN[0], tuple(ww.shape))
+        h = _cache_get(_WCACHE, ww)
+        if h is not None and h[0] == kk and (h[2] is not None or wd is None):
+            continue
+        todo.append((ww, wt, wd, kk))
+    K.conv3x3_weights_batched_bf16([t[0] for t in todo], [t[1] for t in todo], [t[2] for t in todo])
+    for ww, wt, wd, kk in todo:
+        _cache_put(_WCACHE, ww, (kk, wt, wd))
+    h = _cache_get(_WCACHE, w)
+    return h[1], h[2]
 
 
 class _Conv3x3Fn(torch.autograd.Function):

@@ -36,6 +36,12 @@ def test_conv3x3_fwd_dgrad_wgrad(N, C, Co, H, W):
     # forward; the fused two-layout transform matches the single ones
     wf, wd = K.conv3x3_weights_bf16(w)
     assert torch.equal(wf, K.conv3x3_weight_bf16(w, False)) and torch.equal(wd, K.conv3x3_weight_bf16(w, True))
+    # and the batched transform (several weights, one launch; a forward-only entry) into caller buffers
+    w2 = (torch.randn(C, Co, 3, 3, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    bufs = [torch.empty_like(wf), torch.empty_like(wd), torch.empty(C, 9, Co, device=DEV, dtype=torch.bfloat16)]
+    K.conv3x3_weights_batched_bf16([w, w2], [bufs[0], bufs[2]], [bufs[1], None])
+    assert torch.equal(bufs[0], wf) and torch.equal(bufs[1], wd)
+    assert torch.equal(bufs[2], K.conv3x3_weight_bf16(w2, False))
     y = K.conv3x3_fwd_bf16(cl(x), wf)
     assert y.is_contiguous(memory_format=torch.channels_last)
     scale = F.conv2d(x.float().abs(), w.float().abs(), padding=1) + 1e-3

@@ -58,24 +58,27 @@ struct TileAcc {
 template <int C>
 __device__ __forceinline__ void softmax_dz(const f32x4m& z, int tg_raw, bool valid, bool train, float scale, int g,
                                            TileAcc& a, float (&dz)[4], float* dl_row, bool track_amax) {
+  constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
   float zc[4];
 #pragma unroll
   for (int v = 0; v < 4; ++v) zc[v] = (4 * g + v) < C ? z[v] : -INFINITY;
-  // row max and first argmax over the 4 lane groups (symmetric combines)
+  // row max and first argmax over the 4 lane groups (symmetric, branch-free combines)
   float mx = zc[0];
   int am = 4 * g;
 #pragma unroll
-  for (int v = 1; v < 4; ++v)
-    if (zc[v] > mx) {
-      mx = zc[v];
-      am = 4 * g + v;
-    }
+  for (int v = 1; v < 4; ++v) {
+    const bool t = zc[v] > mx;
+    mx = t ? zc[v] : mx;
+    am = t ? 4 * g + v : am;
+  }
   wv::argmax_rows(mx, am);
-  float se = 0.f;
+  // p = exp(z - max) once (one fma + v_exp each); the softmax is p / sum p, the log-sum-exp max + log(sum p)
+  const float mxl = mx * LOG2E;
+  float p[4];
 #pragma unroll
-  for (int v = 0; v < 4; ++v) se += __expf(zc[v] - mx);
-  se = wv::sum_rows(se);
-  const float lse = mx + __logf(se);
+  for (int v = 0; v < 4; ++v) p[v] = __builtin_amdgcn_exp2f(fmaf(zc[v], LOG2E, -mxl));
+  const float se = wv::sum_rows((p[0] + p[1]) + (p[2] + p[3]));
+  const float lse = fmaf(__builtin_amdgcn_logf(se), LN2, mx);
   const int tg = valid ? tg_raw : -1;
   float zt = zc[0];
 #pragma unroll
@@ -83,10 +86,11 @@ __device__ __forceinline__ void softmax_dz(const f32x4m& z, int tg_raw, bool val
   a.loss += (valid && (tg >> 2) == g) ? lse - zt : 0.f;
   a.corr += (valid && g == 0 && am == tg) ? 1.f : 0.f;
   if (!train) return;
+  const float rs = scale * __builtin_amdgcn_rcpf(se);
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const int c = 4 * g + v;
-    dz[v] = (valid && c < C) ? scale * (__expf(zc[v] - lse) - (c == tg ? 1.f : 0.f)) : 0.f;
+    dz[v] = (valid && c < C) ? fmaf(p[v], rs, c == tg ? -scale : 0.f) : 0.f;
   }
   if (dl_row) {
 #pragma unroll
@@ -94,7 +98,7 @@ __device__ __forceinline__ void softmax_dz(const f32x4m& z, int tg_raw, bool val
       if (valid && 4 * g + v < C) dl_row[4 * g + v] = dz[v];
   }
   if (track_amax) {  // (invalid rows and classes >= C hold dz == 0)
-    float sa = (fabsf(dz[0]) + fabsf(dz[1])) + (fabsf(dz[2]) + fabsf(dz[3]));
+    const float sa = (fabsf(dz[0]) + fabsf(dz[1])) + (fabsf(dz[2]) + fabsf(dz[3]));
     a.amx = fmaxf(a.amx, wv::sum_rows(sa));
   }
 }

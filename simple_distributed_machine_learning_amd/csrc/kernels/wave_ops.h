@@ -81,12 +81,12 @@ __device__ __forceinline__ void argmax_rows(float& mx, int& am) {
   int a0, a1;
   pair16(mx, m0, m1);
   pair16(am, a0, a1);
-  bool take = m1 > m0 || (m1 == m0 && a1 < a0);
+  bool take = (m1 > m0) | ((m1 == m0) & (a1 < a0));  // (bitwise: no short-circuit branches)
   mx = take ? m1 : m0;
   am = take ? a1 : a0;
   pair32(mx, m0, m1);
   pair32(am, a0, a1);
-  take = m1 > m0 || (m1 == m0 && a1 < a0);
+  take = (m1 > m0) | ((m1 == m0) & (a1 < a0));
   mx = take ? m1 : m0;
   am = take ? a1 : a0;
 }

@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include "head_tile.h"
+#include "lds_dma.h"
 
 namespace sdml {
 namespace hblk {
@@ -44,10 +45,11 @@ typedef _Float16 hb_f16x4 __attribute__((ext_vector_type(4)));
 typedef short hb_s16x4 __attribute__((ext_vector_type(4)));
 typedef float hb_f32x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 hb_f16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned hb_u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int ROWS = 256, HID = 128, NW = 8, NT = 512;
 constexpr int PLANE_B = HID * ROWS * 2;              // bytes per h plane (fp16)
-constexpr int DLT_OFF = 2 * PLANE_B;                  // dl^T planes [2][16][ROWS] fp16
+constexpr int DLT_OFF = 2 * PLANE_B;                  // dl planes [2][ROWS][16 classes] fp16 (dl_off)
 constexpr int DLT_PLANE_B = 16 * ROWS * 2;
 constexpr int RED_OFF = DLT_OFF + 2 * DLT_PLANE_B;    // floats below
 // red: [0, 8) wave max |h|, [8, 136) db partials [wave][16], [136, 144) loss, [144, 152) correct, [152, 160) amx,
@@ -68,9 +70,14 @@ __device__ __forceinline__ int gswz(int h) {
 }
 // byte offset of granule q (rows 4q .. 4q+3) of hidden unit h in plane p of the h image
 __device__ __forceinline__ int hoff(int p, int h, int q) { return p * PLANE_B + h * (ROWS * 2) + 8 * (q ^ gswz(h)); }
-// byte offset of row rho of class c in plane p of the dl^T image
-__device__ __forceinline__ int doff(int p, int c, int rho) {
-  return DLT_OFF + p * DLT_PLANE_B + c * (ROWS * 2) + 8 * ((rho >> 2) ^ gswz(c)) + 2 * (rho & 3);
+// byte offset of classes 4s .. 4s+3 of row R in plane p of the dl image: rows of 16 classes (32 B), row R at physical
+// row R ^ (bit 3 of R) << 2 and its 8-byte class slots swizzled by that row's bits 2..3, so the 8-byte writes (lane:
+// one row's 4 classes) and the dW2 A-operand reads (ds_read_b64_tr_b16: a 16-lane group takes 4 rows x 4 slots and
+// hands lane r class r of the 4 rows) are conflict-free (tests/test_head_block_layout.py). Round 4's dl^T image
+// [class][row] took 8 ds_write_b16 per lane and row tile.
+__device__ __forceinline__ int dl_off(int p, int R, int s) {
+  const int P = R ^ (((R >> 3) & 1) << 2);
+  return DLT_OFF + p * DLT_PLANE_B + P * 32 + 8 * (s ^ ((P >> 2) & 3));
 }
 
 // exponent E with |v| < 2^E for finite v >= 0, clamped so 2^(14 - E) and 2^(E - 14) stay normal floats
@@ -148,7 +155,7 @@ __device__ __forceinline__ void load_operands(const Args& a, int m0, int M, int 
 template <int C, class Prep, class Hook>
 __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, const Args& a, const Operands& ops, int m0,
                                            int M, int wave, int lane, Hook&& hook, long long* stamp) {
-  static_assert(C >= 1 && C <= 16, "one 16-class tile");
+  static_assert(C >= 2 && C <= 16 && C % 2 == 0, "one 16-class tile; dl stored by class pairs");
   auto st = [&](int k) {
     if (stamp && lane == 0) stamp[k] = (long long)__builtin_amdgcn_s_memtime();
   };
@@ -202,7 +209,7 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
   }
   const int Eh = bexp(bm), Ew = bexp(wm2), Ed = bexp(a.loss_scale);
   const float sh = p2(14 - Eh), sw = p2(14 - Ew), sd = p2(14 - Ed);
-  const hb_f32x2 sh2 = {sh, sh};
+  const hb_f32x2 sh2 = {sh, sh}, sd2 = {sd, sd};
 
   // 1. the h image: granule (4 rows) of hidden unit 64 wn + 32 j + r32, rows 64 wm + 32 i + 8 rq + 4 h2 ..
 #pragma unroll
@@ -245,6 +252,7 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
   acc.zero();
   const float zsc = p2(Eh - 14) * p2(Ew - 14);  // 2^-(sh + sw) as one exact power of two
   hb_f32x4 dbs = {0.f, 0.f, 0.f, 0.f};          // this lane's dz sums of classes 4g .. 4g+3
+  const __amdgpu_buffer_rsrc_t dlr = dma_rsrc(a.dl, (unsigned)((size_t)M * C * 4));
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int T = wave + NW * it;
@@ -271,17 +279,24 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
     const int row = m0 + 16 * T + r;
     const bool valid = row < M;
     float dz[4];
-    headtile::softmax_dz<C>(z, tg[it], valid, a.train, a.loss_scale, g, acc, dz, a.dl ? a.dl + (size_t)row * C : nullptr,
-                            a.bound != nullptr);
+    headtile::softmax_dz<C>(z, tg[it], valid, a.train, a.loss_scale, g, acc, dz, a.bound != nullptr);
+    if (a.train && a.dl) {  // classes 4g, 4g+1 | 4g+2, 4g+3 as two 8-byte buffer stores; invalid pairs (rows past
+                            // M, classes >= C; C is even) get an out-of-range offset, which the store drops -
+                            // no exec-mask branches around the stores
+      const unsigned o = (unsigned)(((size_t)row * C + 4 * g) * 4);
+      const unsigned o0 = valid && 4 * g + 1 < C ? o : 0x80000000u, o1 = valid && 4 * g + 3 < C ? o + 8 : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b64(hb_u32x2{__float_as_uint(dz[0]), __float_as_uint(dz[1])}, dlr, o0, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(hb_u32x2{__float_as_uint(dz[2]), __float_as_uint(dz[3])}, dlr, o1, 0, 0);
+    }
     if (a.train) {
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        dbs[v] += dz[v];
-        _Float16 dh, dlo;
-        split2(dz[v] * sd, dh, dlo);
-        *reinterpret_cast<_Float16*>(smem + doff(0, 4 * g + v, 16 * T + r)) = dh;
-        *reinterpret_cast<_Float16*>(smem + doff(1, 4 * g + v, 16 * T + r)) = dlo;
-      }
+      for (int v = 0; v < 4; ++v) dbs[v] += dz[v];
+      // the planes of dz * sd (split2's bits, as the h image: packed hi, mixed-fma lo)
+      const hb_f32x2 x01 = hb_f32x2{dz[0], dz[1]} * sd2, x23 = hb_f32x2{dz[2], dz[3]} * sd2;
+      const hb_f16x2 h01 = __builtin_convertvector(x01, hb_f16x2), h23 = __builtin_convertvector(x23, hb_f16x2);
+      const hb_f16x2 l01 = lo_pair(h01, x01), l23 = lo_pair(h23, x23);
+      *reinterpret_cast<hb_f16x4*>(smem + dl_off(0, 16 * T + r, g)) = hb_f16x4{h01[0], h01[1], h23[0], h23[1]};
+      *reinterpret_cast<hb_f16x4*>(smem + dl_off(1, 16 * T + r, g)) = hb_f16x4{l01[0], l01[1], l23[0], l23[1]};
       hook(T, row, valid, dz);
     }
   }
@@ -301,26 +316,32 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
 #pragma unroll
     for (int v = 0; v < 4; ++v) red[8 + 16 * wave + 4 * g + v] = dbs[v];
   }
-  __syncthreads();  // (B3) the dl^T image and the wave partials are complete
+  __syncthreads();  // (B3) the dl image and the wave partials are complete
   st(20);
 
   // 3. dW2 of hidden units 16 wave .. +15 over the block's rows: lane (class r / hidden r, row group g)
   if (a.train) {
     hb_f32x4 gacc = {0.f, 0.f, 0.f, 0.f};
     const int hid = 16 * wave + r;
+    // Lane-constant bases, so each address below is the base plus an immediate or one XOR with a constant:
+    // dl_off(p, 32 ks + X, s) = dl_off(p, X, s) + 1024 ks (X < 32), and granule 8 ks + 2 g + e of hidden unit hid sits
+    // at byte hid * 512 + 64 (ks ^ (gswz(hid) >> 3)) + 8 ((2 g + e) ^ (gswz(hid) & 7)), whose bits 6..8 are ks's alone
+    const int db0 = dl_off(0, 8 * g + (r >> 2), r & 3), db1 = dl_off(0, 8 * g + 4 + (r >> 2), r & 3);
+    const int sw = gswz(hid);
+    const int hb0 = (hid * (ROWS * 2) + 8 * ((2 * g) ^ (sw & 7))) | (64 * (sw >> 3));
+    const int hb1 = (hid * (ROWS * 2) + 8 * ((2 * g + 1) ^ (sw & 7))) | (64 * (sw >> 3));
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
-      const int q = 8 * ks + 2 * g;  // granules q, q + 1 = rows 32 ks + 8 g .. +7
       hb_f16x8 dp[2], hq[2];
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
-        const hb_s16x4 d0 = *reinterpret_cast<const hb_s16x4*>(smem + DLT_OFF + p * DLT_PLANE_B + r * (ROWS * 2) +
-                                                                 8 * (q ^ gswz(r)));
-        const hb_s16x4 d1 = *reinterpret_cast<const hb_s16x4*>(smem + DLT_OFF + p * DLT_PLANE_B + r * (ROWS * 2) +
-                                                                 8 * ((q + 1) ^ gswz(r)));
+        // A = dl^T: lane (class r, g) gets rows 32 ks + 8 g .. +7 of class r through two transposed reads
+        const hb_s16x4 d0 = tr16(smem + db0 + p * DLT_PLANE_B + 1024 * ks);
+        const hb_s16x4 d1 = tr16(smem + db1 + p * DLT_PLANE_B + 1024 * ks);
         dp[p] = cat8(d0, d1);
-        const hb_s16x4 h0 = *reinterpret_cast<const hb_s16x4*>(smem + hoff(p, hid, q));
-        const hb_s16x4 h1 = *reinterpret_cast<const hb_s16x4*>(smem + hoff(p, hid, q + 1));
+        // B = h: lane (hidden r, g) gets rows 32 ks + 8 g .. +7 (granules 8 ks + 2 g, + 1)
+        const hb_s16x4 h0 = *reinterpret_cast<const hb_s16x4*>(smem + p * PLANE_B + (hb0 ^ (64 * ks)));
+        const hb_s16x4 h1 = *reinterpret_cast<const hb_s16x4*>(smem + p * PLANE_B + (hb1 ^ (64 * ks)));
         hq[p] = cat8(h0, h1);
       }
       gacc = mfma16(dp[0], hq[1], gacc);  // hi * lo

@@ -49,15 +49,13 @@ struct TileAcc {
   }
 };
 
-// logits, log_softmax, NLL (loss accumulated for valid rows), argmax (correct), and when `train`
-// dz = scale (softmax - onehot) for the lane's 4 classes (0 for invalid rows / classes >= C),
-// optionally stored to dl [row][C]; amx tracks max_row sum_c |dz_c| (the |dl @ W| bound).
-// wl[u][e] = W[class r][16u + 4g + e]; xv[u][e] = x[row r][16u + 4g + e]; bv = bias of classes 4g..
-// softmax_dz: the part after the logits, given lane (r, g)'s logits z of classes 4g .. 4g+3 of row r (the layout of a
+// softmax_dz: log_softmax, NLL (loss accumulated for valid rows), argmax (correct), and when `train`
+// dz = scale (softmax - onehot) for the lane's 4 classes (0 for invalid rows / classes >= C); amx tracks
+// max_row sum_c |dz_c| (the |dl @ W| bound). Given lane (r, g)'s logits z of classes 4g .. 4g+3 of row r (the layout of a
 // 16x16 MFMA accumulator: head_block.h's fp16-plane head produces it too)
 template <int C>
 __device__ __forceinline__ void softmax_dz(const f32x4m& z, int tg_raw, bool valid, bool train, float scale, int g,
-                                           TileAcc& a, float (&dz)[4], float* dl_row, bool track_amax) {
+                                           TileAcc& a, float (&dz)[4], bool track_amax) {
   constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
   float zc[4];
 #pragma unroll
@@ -92,27 +90,10 @@ __device__ __forceinline__ void softmax_dz(const f32x4m& z, int tg_raw, bool val
     const int c = 4 * g + v;
     dz[v] = (valid && c < C) ? fmaf(p[v], rs, c == tg ? -scale : 0.f) : 0.f;
   }
-  if (dl_row) {
-#pragma unroll
-    for (int v = 0; v < 4; ++v)
-      if (valid && 4 * g + v < C) dl_row[4 * g + v] = dz[v];
-  }
   if (track_amax) {  // (invalid rows and classes >= C hold dz == 0)
     const float sa = (fabsf(dz[0]) + fabsf(dz[1])) + (fabsf(dz[2]) + fabsf(dz[3]));
     a.amx = fmaxf(a.amx, wv::sum_rows(sa));
   }
-}
-
-template <int C>
-__device__ __forceinline__ void logits_dz(const f32x4m (&wl)[8], const f32x4m& bv, const f32x4m (&xv)[8], int tg_raw,
-                                          bool valid, bool train, float scale, int g, TileAcc& a, float (&dz)[4],
-                                          float* dl_row, bool track_amax) {
-  f32x4m z = bv;
-#pragma unroll
-  for (int u = 0; u < 8; ++u)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) z = mfma4(wl[u][e], xv[u][e], z);
-  softmax_dz<C>(z, tg_raw, valid, train, scale, g, a, dz, dl_row, track_amax);
 }
 
 // dW^T += x^T dz, db += dz: xw = this tile's x image (xt_at layout, complete and visible to the wave),

@@ -94,3 +94,27 @@ def test_w2_staging_reads_conflict_free():
                         for d in range(addrs[lane] // 4, addrs[lane] // 4 + 4):
                             per_bank.setdefault(d % 64, set()).add(d)
                     assert max(len(v) for v in per_bank.values()) == 1
+
+
+# dl image [plane][row][16 classes] fp16: row R stored at physical row P(R) = R ^ (bit 3 of R) << 2, its four 8-byte
+# class-group slots at s ^ ((P >> 2) & 3)
+def dl_off(R, s):
+    P = R ^ (((R >> 3) & 1) << 2)
+    return P * 32 + 8 * (s ^ ((P >> 2) & 3))
+
+
+def test_dl_image_writes_and_dw2_reads_conflict_free():
+    # writes: lane (r, g) of row tile T stores classes 4g..4g+3 of row 16 T + r (ds_write_b64, 4 groups of 16)
+    for T in range(16):
+        addrs = [dl_off(16 * T + (l & 15), l >> 4) for l in range(64)]
+        assert _conflicts(addrs, W16, 32) == 1
+    # dW2 A operand: lane (r, g) supplies row 32 ks + 8 g + (r >> 2) (+ 4), slot r & 3 (ds_read_b64_tr_b16)
+    for ks in range(8):
+        for plus in (0, 4):
+            addrs = [dl_off(32 * ks + 8 * (l >> 4) + ((l & 15) >> 2) + plus, l & 3) for l in range(64)]
+            assert _conflicts(addrs, R32, 64) == 1
+
+
+def test_dl_image_is_a_bijection():
+    offs = sorted(dl_off(R, s) for R in range(256) for s in range(4))
+    assert offs == list(range(0, 256 * 32, 8))

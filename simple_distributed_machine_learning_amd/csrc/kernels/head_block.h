@@ -55,13 +55,14 @@ constexpr int RED_OFF = DLT_OFF + 2 * DLT_PLANE_B;    // floats below
 // red: [0, 8) wave max |h|, [8, 136) db partials [wave][16], [136, 144) loss, [144, 152) correct, [152, 160) amx,
 // [160, 168) wave max |W2|
 constexpr int RED_FLOATS = 168;
-// W2 staged once per block: [16][W2P] bytes, rows padded by 16 B (the A-operand reads, 16 rows per 16-lane group,
-// hit 64 distinct banks). Past everything else: the fused forward's LDS ring (<= 144 KiB) ends before RED_OFF, so the
-// block may write it while slower waves still read their last K-step
-constexpr int W2P = HID * 4 + 16;
+// W2's fp16 planes, split once per block: [plane][16 classes][W2PP] bytes, rows padded to 288 B so the A-operand
+// reads (ds_read_b128 in its 4 lane groups) are conflict-free (tests/test_head_block_layout.py); classes >= C are
+// zero rows
+constexpr int W2PP = HID * 2 + 32;
+constexpr int W2PL = 16 * W2PP;
 constexpr int W2_OFF = RED_OFF + RED_FLOATS * 4;
-constexpr int LDS_BYTES = W2_OFF + 16 * W2P;
-static_assert(W2_OFF % 16 == 0, "W2 staging alignment");
+constexpr int LDS_BYTES = W2_OFF + 2 * W2PL;
+static_assert(W2_OFF % 16 == 0 && W2PP % 16 == 0, "W2 plane alignment");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 
 // granule swizzle of hidden unit (or class) h: bits (h2, h3, h0, h1, h3) -> bits 0..4
@@ -163,7 +164,6 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
   const int wm = wave & 3, wn = wave >> 2, h2 = lane >> 5, r32 = lane & 31;
   const int r = lane & 15, g = lane >> 4;
   const int tid = wave * 64 + lane;
-  if (tid < C * HID / 4) *reinterpret_cast<hb_f32x4*>(smem + W2_OFF + (tid >> 5) * W2P + 16 * (tid & 31)) = ops.w2c;
   headtile::f32x4m bv;
 #pragma unroll
   for (int v = 0; v < 4; ++v) bv[v] = (4 * g + v) < C ? ops.b[v] : 0.f;
@@ -187,7 +187,7 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
     red[wave] = hm;
     red[160 + wave] = wmw;
   }
-  __syncthreads();  // (B1) the maxima and W2 are in LDS; the caller's buffers are free
+  __syncthreads();  // (B1) the maxima are in LDS; the caller's buffers are free
   st(17);
   float bm = red[0], wm2 = red[160];
 #pragma unroll
@@ -195,21 +195,21 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
     bm = fmaxf(bm, red[w]);
     wm2 = fmaxf(wm2, red[160 + w]);
   }
-  // W2 (A operands of the logits): lane (class r, k-group g) takes W2[r][32 kk + 8 g + e] (zero for classes >= C)
-  float wv[4][8];
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    const unsigned char* src = smem + W2_OFF + min(r, C - 1) * W2P + 4 * (32 * kk + 8 * g);
-    const hb_f32x4 u0 = *reinterpret_cast<const hb_f32x4*>(src), u1 = *reinterpret_cast<const hb_f32x4*>(src + 16);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      wv[kk][e] = r < C ? u0[e] : 0.f;
-      wv[kk][4 + e] = r < C ? u1[e] : 0.f;
-    }
-  }
   const int Eh = bexp(bm), Ew = bexp(wm2), Ed = bexp(a.loss_scale);
   const float sh = p2(14 - Eh), sw = p2(14 - Ew), sd = p2(14 - Ed);
   const hb_f32x2 sh2 = {sh, sh}, sd2 = {sd, sd};
+  {  // W2's planes, split once per block: thread tid holds W2 row tid / 32, columns 4 (tid % 32) .. +3 (each wave
+     // splitting all of W2 for its own A operands took ~120 VALU per lane)
+    const bool ok = tid < C * HID / 4;
+    const hb_f32x2 sw2 = {sw, sw};
+    const hb_f32x2 x01 = hb_f32x2{ok ? ops.w2c[0] : 0.f, ok ? ops.w2c[1] : 0.f} * sw2;
+    const hb_f32x2 x23 = hb_f32x2{ok ? ops.w2c[2] : 0.f, ok ? ops.w2c[3] : 0.f} * sw2;
+    const hb_f16x2 h01 = __builtin_convertvector(x01, hb_f16x2), h23 = __builtin_convertvector(x23, hb_f16x2);
+    const hb_f16x2 l01 = lo_pair(h01, x01), l23 = lo_pair(h23, x23);
+    unsigned char* dst = smem + W2_OFF + (tid >> 5) * W2PP + 8 * (tid & 31);
+    *reinterpret_cast<hb_f16x4*>(dst) = hb_f16x4{h01[0], h01[1], h23[0], h23[1]};
+    *reinterpret_cast<hb_f16x4*>(dst + W2PL) = hb_f16x4{l01[0], l01[1], l23[0], l23[1]};
+  }
 
   // 1. the h image: granule (4 rows) of hidden unit 64 wn + 32 j + r32, rows 64 wm + 32 i + 8 rq + 4 h2 ..
 #pragma unroll
@@ -233,19 +233,15 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
         *reinterpret_cast<hb_f16x4*>(smem + hoff(1, hid, q)) = lo;
       }
     }
-  // W2 planes (A operands of the logits): wp[kk][0] hi, [1] lo
+  __syncthreads();  // (B2) the h image and W2's planes are complete
+  st(18);
+  // W2 planes (A operands of the logits): lane (class r, k-group g) takes W2[r][32 kk + 8 g .. +7], wp[kk][0] hi, [1] lo
   hb_f16x8 wp[4][2];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      _Float16 a0, a1;
-      split2(wv[kk][e] * sw, a0, a1);
-      wp[kk][0][e] = a0;
-      wp[kk][1][e] = a1;
-    }
-  __syncthreads();  // (B2) the h image is complete
-  st(18);
+    for (int p = 0; p < 2; ++p)
+      wp[kk][p] = *reinterpret_cast<const hb_f16x8*>(smem + W2_OFF + p * W2PL + r * W2PP + 2 * (32 * kk + 8 * g));
 
   // 2. logits of row tiles wave, wave + 8; softmax, NLL, dl (+ its planes into the dl^T image)
   headtile::TileAcc acc;

@@ -79,21 +79,31 @@ def test_swizzle_is_a_bijection_per_row():
         assert sorted(q ^ gswz(h) for q in range(64)) == list(range(64))
 
 
-def test_w2_staging_reads_conflict_free():
-    # W2 staged as [16][W2P] bytes (W2P = 128 * 4 + 16); lane (r = l & 15, g = l >> 4) reads row min(r, C - 1),
-    # bytes 4 (32 kk + 8 g) (+ 16) with ds_read_b128: 4 groups of 16 lanes, bank = dword mod 64
-    W2P = 128 * 4 + 16
-    W16 = [list(range(16 * k, 16 * k + 16)) for k in range(4)]
-    for C in (2, 10, 16):
-        for kk in range(4):
-            for e in (0, 16):
-                addrs = [min(l & 15, C - 1) * W2P + 4 * (32 * kk + 8 * (l >> 4)) + e for l in range(64)]
-                for grp in W16:
-                    per_bank = {}
-                    for lane in grp:
-                        for d in range(addrs[lane] // 4, addrs[lane] // 4 + 4):
-                            per_bank.setdefault(d % 64, set()).add(d)
-                    assert max(len(v) for v in per_bank.values()) == 1
+# ds_read_b128 is serviced in 4 lane groups of 16 that are not contiguous (MI355X_MICROARCH.md, LDS table)
+G128 = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+        list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
+G128 += [[l + 32 for l in grp] for grp in G128]
+
+
+def _conflicts16(addrs, groups):
+    worst = 1
+    for grp in groups:
+        per_bank = {}
+        for lane in grp:
+            for d in range(addrs[lane] // 4, addrs[lane] // 4 + 4):
+                per_bank.setdefault(d % 64, set()).add(d)
+        worst = max(worst, max(len(v) for v in per_bank.values()))
+    return worst
+
+
+def test_w2_plane_reads_conflict_free():
+    # W2 planes [16 classes][W2PP = 288 B]: lane (r = l & 15, g = l >> 4) reads class r, halves 32 kk + 8 g .. +7
+    W2PP = 128 * 2 + 32
+    for kk in range(4):
+        addrs = [(l & 15) * W2PP + 2 * (32 * kk + 8 * (l >> 4)) for l in range(64)]
+        assert _conflicts16(addrs, G128) == 1
+    # (an unpadded 256-B pitch would be 8-way)
+    assert _conflicts16([(l & 15) * 256 + 16 * (l >> 4) for l in range(64)], G128) == 8
 
 
 # dl image [plane][row][16 classes] fp16: row R stored at physical row P(R) = R ^ (bit 3 of R) << 2, its four 8-byte

@@ -326,23 +326,31 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
     const int sw = gswz(hid);
     const int hb0 = (hid * (ROWS * 2) + 8 * ((2 * g) ^ (sw & 7))) | (64 * (sw >> 3));
     const int hb1 = (hid * (ROWS * 2) + 8 * ((2 * g + 1) ^ (sw & 7))) | (64 * (sw >> 3));
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      hb_f16x8 dp[2], hq[2];
+    // operands of k-step ks into buffer b; the next k-step's reads are issued before this one's MFMAs (left to
+    // itself hipcc reused one register set and exposed two LDS round trips per k-step)
+    hb_f16x8 dp[2][2], hq[2][2];  // [buffer][plane]
+    auto ld = [&](int ks, int b) {
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         // A = dl^T: lane (class r, g) gets rows 32 ks + 8 g .. +7 of class r through two transposed reads
         const hb_s16x4 d0 = tr16(smem + db0 + p * DLT_PLANE_B + 1024 * ks);
         const hb_s16x4 d1 = tr16(smem + db1 + p * DLT_PLANE_B + 1024 * ks);
-        dp[p] = cat8(d0, d1);
+        dp[b][p] = cat8(d0, d1);
         // B = h: lane (hidden r, g) gets rows 32 ks + 8 g .. +7 (granules 8 ks + 2 g, + 1)
         const hb_s16x4 h0 = *reinterpret_cast<const hb_s16x4*>(smem + p * PLANE_B + (hb0 ^ (64 * ks)));
         const hb_s16x4 h1 = *reinterpret_cast<const hb_s16x4*>(smem + p * PLANE_B + (hb1 ^ (64 * ks)));
-        hq[p] = cat8(h0, h1);
+        hq[b][p] = cat8(h0, h1);
       }
-      gacc = mfma16(dp[0], hq[1], gacc);  // hi * lo
-      gacc = mfma16(dp[1], hq[0], gacc);  // lo * hi
-      gacc = mfma16(dp[0], hq[0], gacc);  // hi * hi
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int b = ks & 1;
+      if (ks + 1 < 8) ld(ks + 1, b ^ 1);
+      __builtin_amdgcn_sched_barrier(0);  // (the scheduler sank those reads below the MFMAs: lgkmcnt(0) per k-step)
+      gacc = mfma16(dp[b][0], hq[b][1], gacc);  // hi * lo
+      gacc = mfma16(dp[b][1], hq[b][0], gacc);  // lo * hi
+      gacc = mfma16(dp[b][0], hq[b][0], gacc);  // hi * hi
     }
     // lane (hidden r, g) holds dW2[class 4 g + v][16 wave + r]
     const float gsc = p2(Ed - 14) * p2(Eh - 14);

@@ -69,8 +69,14 @@ static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 __device__ __forceinline__ int gswz(int h) {
   return ((h >> 2) & 1) | (((h >> 3) & 1) << 1) | ((h & 1) << 2) | (((h >> 1) & 1) << 3) | (((h >> 3) & 1) << 4);
 }
-// byte offset of granule q (rows 4q .. 4q+3) of hidden unit h in plane p of the h image
-__device__ __forceinline__ int hoff(int p, int h, int q) { return p * PLANE_B + h * (ROWS * 2) + 8 * (q ^ gswz(h)); }
+// byte offset of granule q (rows 4q .. 4q+3) of hidden unit h in plane p of the h image: the two planes of a hidden
+// unit are adjacent 512-B rows (HPL apart: an immediate offset for the second plane's access; 65536 is not), which
+// leaves every access's banks as they were (both offsets are multiples of 256 B)
+constexpr int HPL = ROWS * 2;
+__device__ __forceinline__ int hoff(int p, int h, int q) { return h * (2 * HPL) + p * HPL + 8 * (q ^ gswz(h)); }
+// hoff(0, h, qb) for a granule index qb whose bits 1..3 are zero: hoff(0, h, qb | c) == hid_base(h, qb) ^ 8 c for
+// c in [0, 16) with bit 0 clear (tests/test_head_block_layout.py)
+__device__ __forceinline__ int hid_base(int h, int qb) { return h * (2 * HPL) + 8 * (qb ^ gswz(h)); }
 // byte offset of classes 4s .. 4s+3 of row R in plane p of the dl image: rows of 16 classes (32 B), row R at physical
 // row R ^ (bit 3 of R) << 2 and its 8-byte class slots swizzled by that row's bits 2..3, so the 8-byte writes (lane:
 // one row's 4 classes) and the dW2 A-operand reads (ds_read_b64_tr_b16: a 16-lane group takes 4 rows x 4 slots and
@@ -112,8 +118,7 @@ __device__ __forceinline__ hb_s16x4 tr16(const unsigned char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) hb_s16x4*)(p));
 }
 __device__ __forceinline__ hb_f16x8 cat8(hb_s16x4 a, hb_s16x4 b) {
-  hb_s16x4 v[2] = {a, b};
-  return *reinterpret_cast<const hb_f16x8*>(v);
+  return __builtin_bit_cast(hb_f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 struct Args {
@@ -212,11 +217,13 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
   }
 
   // 1. the h image: granule (4 rows) of hidden unit 64 wn + 32 j + r32, rows 64 wm + 32 i + 8 rq + 4 h2 ..
+  // granule q = (16 wm + h2) | (8 i + 2 rq): its byte offset hoff(p, hid, q) is a lane base XOR 8 (8 i + 2 rq) (the
+  // granule's varying bits 1..3 never carry; the swizzle is lane-constant), one VALU per address
+  const int ib0 = hid_base(64 * wn + r32, 16 * wm + h2), ib1 = hid_base(64 * wn + 32 + r32, 16 * wm + h2);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int hid = 64 * wn + 32 * j + r32;
 #pragma unroll
       for (int rq = 0; rq < 4; ++rq) {
         // split2's operations, the hi planes on pairs (v_pk_mul_f32, v_cvt_pk_f16_f32) and each lo as one mixed
@@ -228,9 +235,9 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
         const hb_f16x4 hi = {h01[0], h01[1], h23[0], h23[1]};
         const hb_f16x2 l01 = lo_pair(h01, x01), l23 = lo_pair(h23, x23);
         const hb_f16x4 lo = {l01[0], l01[1], l23[0], l23[1]};
-        const int q = 16 * wm + 8 * i + 2 * rq + h2;
-        *reinterpret_cast<hb_f16x4*>(smem + hoff(0, hid, q)) = hi;
-        *reinterpret_cast<hb_f16x4*>(smem + hoff(1, hid, q)) = lo;
+        const int o = (j ? ib1 : ib0) ^ (8 * (8 * i + 2 * rq));  // = hoff(0, hid, q)
+        *reinterpret_cast<hb_f16x4*>(smem + o) = hi;
+        *reinterpret_cast<hb_f16x4*>(smem + HPL + o) = lo;
       }
     }
   __syncthreads();  // (B2) the h image and W2's planes are complete
@@ -248,19 +255,22 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
   acc.zero();
   const float zsc = p2(Eh - 14) * p2(Ew - 14);  // 2^-(sh + sw) as one exact power of two
   hb_f32x4 dbs = {0.f, 0.f, 0.f, 0.f};          // this lane's dz sums of classes 4g .. 4g+3
+  const int lb0 = hoff(0, 8 * g + (r >> 2), 4 * wave + (r & 3)), lb1 = hoff(0, 8 * g + 4 + (r >> 2), 4 * wave + (r & 3));
   const __amdgpu_buffer_rsrc_t dlr = dma_rsrc(a.dl, (unsigned)((size_t)M * C * 4));
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
     const int T = wave + NW * it;
     // B operand lanes: row 16 T + (i16 = lane & 15); image rows (hidden) 32 kk + 8 g + (i16 >> 2) (+ 4), granule
     // 4 T + (i16 & 3)
+    // hoff(p, 32 kk + hx, 4 T + (r & 3)) = lb[hx] + 32768 kk + 512 p + 256 it (hx = 8 g + (r >> 2) (+ 4) < 32: the
+    // swizzle is lane-constant, and 4 wave + (r & 3) < 32 keeps the tile bit 5 of the granule out of it)
     hb_f16x8 hp[4][2];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      const int hid = 32 * kk + 8 * g + (r >> 2), q = 4 * T + (r & 3);
 #pragma unroll
       for (int p = 0; p < 2; ++p)
-        hp[kk][p] = cat8(tr16(smem + hoff(p, hid, q)), tr16(smem + hoff(p, hid + 4, q)));
+        hp[kk][p] = cat8(tr16(smem + lb0 + 32768 * kk + HPL * p + 256 * it),
+                         tr16(smem + lb1 + 32768 * kk + HPL * p + 256 * it));
     }
     hb_f32x4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -324,8 +334,12 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
     // at byte hid * 512 + 64 (ks ^ (gswz(hid) >> 3)) + 8 ((2 g + e) ^ (gswz(hid) & 7)), whose bits 6..8 are ks's alone
     const int db0 = dl_off(0, 8 * g + (r >> 2), r & 3), db1 = dl_off(0, 8 * g + 4 + (r >> 2), r & 3);
     const int sw = gswz(hid);
-    const int hb0 = (hid * (ROWS * 2) + 8 * ((2 * g) ^ (sw & 7))) | (64 * (sw >> 3));
-    const int hb1 = (hid * (ROWS * 2) + 8 * ((2 * g + 1) ^ (sw & 7))) | (64 * (sw >> 3));
+    const int hb0 = (hid * (2 * HPL) + 8 * ((2 * g) ^ (sw & 7))) | (64 * (sw >> 3));
+    const int hb1 = (hid * (2 * HPL) + 8 * ((2 * g + 1) ^ (sw & 7))) | (64 * (sw >> 3));
+    // the lo plane's bases, opaque to hipcc: otherwise it merges each hi/lo pair into one ds_read2st64_b64 and then
+    // spends 4 v_mov per k-step regrouping the granules by plane (bit 9, which HPL sets, is clear in hb0 / hb1)
+    int hb0l = hb0 + HPL, hb1l = hb1 + HPL;
+    asm volatile("" : "+v"(hb0l), "+v"(hb1l));
     // operands of k-step ks into buffer b; the next k-step's reads are issued before this one's MFMAs (left to
     // itself hipcc reused one register set and exposed two LDS round trips per k-step)
     hb_f16x8 dp[2][2], hq[2][2];  // [buffer][plane]
@@ -337,8 +351,8 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
         const hb_s16x4 d1 = tr16(smem + db1 + p * DLT_PLANE_B + 1024 * ks);
         dp[b][p] = cat8(d0, d1);
         // B = h: lane (hidden r, g) gets rows 32 ks + 8 g .. +7 (granules 8 ks + 2 g, + 1)
-        const hb_s16x4 h0 = *reinterpret_cast<const hb_s16x4*>(smem + p * PLANE_B + (hb0 ^ (64 * ks)));
-        const hb_s16x4 h1 = *reinterpret_cast<const hb_s16x4*>(smem + p * PLANE_B + (hb1 ^ (64 * ks)));
+        const hb_s16x4 h0 = *reinterpret_cast<const hb_s16x4*>(smem + ((p ? hb0l : hb0) ^ (64 * ks)));
+        const hb_s16x4 h1 = *reinterpret_cast<const hb_s16x4*>(smem + ((p ? hb1l : hb1) ^ (64 * ks)));
         hq[b][p] = cat8(h0, h1);
       }
     };

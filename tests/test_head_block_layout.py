@@ -15,8 +15,8 @@ def gswz(h):
     return ((h >> 2) & 1) | (((h >> 3) & 1) << 1) | ((h & 1) << 2) | (((h >> 1) & 1) << 3) | (((h >> 3) & 1) << 4)
 
 
-def hoff(p, h, q):
-    return p * PLANE_B + h * (ROWS * 2) + 8 * (q ^ gswz(h))
+def hoff(p, h, q):  # the two planes of a hidden unit are adjacent 512-B rows
+    return h * (4 * ROWS) + p * (2 * ROWS) + 8 * (q ^ gswz(h))
 
 
 def _conflicts(addrs, groups, banks):
@@ -128,3 +128,16 @@ def test_dl_image_writes_and_dw2_reads_conflict_free():
 def test_dl_image_is_a_bijection():
     offs = sorted(dl_off(R, s) for R in range(256) for s in range(4))
     assert offs == list(range(0, 256 * 32, 8))
+
+
+def test_h_image_write_addresses_as_base_xor():
+    # head_block.h hid_base: hoff(0, h, qb | c) == hid_base(h, qb) ^ 8 c (qb with bits 1..3 clear, c = 8 i + 2 rq)
+    for h in range(128):
+        for wm in range(4):
+            for h2 in range(2):
+                qb = 16 * wm + h2
+                base = h * (4 * ROWS) + 8 * (qb ^ gswz(h))
+                for i in range(2):
+                    for rq in range(4):
+                        c = 8 * i + 2 * rq
+                        assert hoff(0, h, qb | c) == base ^ (8 * c)

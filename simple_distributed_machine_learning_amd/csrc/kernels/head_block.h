@@ -158,9 +158,14 @@ __device__ __forceinline__ void load_operands(const Args& a, int m0, int M, int 
 // prep(y) fills y: this wave's 64 x 64 tile of h (rows >= M zero), C layout above. smem: LDS_BYTES, free (the caller's
 // previous use finished with a barrier or not yet started: the first thing here is a barrier). hook(T, row, valid, dz):
 // called per row tile after the softmax with the lane's dz (the standalone head's dx pass; a no-op when fused).
-template <int C, class Prep, class Hook>
+struct NoOp {
+  __device__ void operator()() const {}
+};
+// post_b1(): run right after the first barrier (the fused forward issues its next-block pixel prefetch there)
+template <int C, class Prep, class Hook, class PostB1 = NoOp>
 __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, const Args& a, const Operands& ops, int m0,
-                                           int M, int wave, int lane, Hook&& hook, long long* stamp) {
+                                           int M, int wave, int lane, Hook&& hook, long long* stamp,
+                                           PostB1&& post_b1 = PostB1{}) {
   static_assert(C >= 2 && C <= 16 && C % 2 == 0, "one 16-class tile; dl stored by class pairs");
   auto st = [&](int k) {
     if (stamp && lane == 0) stamp[k] = (long long)__builtin_amdgcn_s_memtime();
@@ -194,6 +199,7 @@ __device__ __forceinline__ void block_head(Prep&& prep, unsigned char* smem, con
   }
   __syncthreads();  // (B1) the maxima are in LDS; the caller's buffers are free
   st(17);
+  post_b1();
   float bm = red[0], wm2 = red[160];
 #pragma unroll
   for (int w = 1; w < NW; ++w) {

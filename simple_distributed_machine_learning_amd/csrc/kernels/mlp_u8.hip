@@ -133,6 +133,8 @@ struct FwdParams {
   float* wmax;     // optional [blocks][WAVES] per-wave max of the stored outputs (plain epilogue): a bound the
                    // next layer's two-plane split (gemm_f16x2.hip) reads instead of an inf-norm pass
   U8HeadArgs head;  // fused head epilogue (HEADC > 0)
+  int pf_stride;   // fused head: > 0 = during the epilogue, LDS-DMA block blockIdx + pf_stride's first two K-steps of
+                   // pixels into a scratch KiB, so they sit in this XCD's L2 when that block starts (knob U8_FWD_PREFETCH)
   long long* stamps;  // MODE 7 (experiments builds only): per-wave phase stamps, U8_NSTAMP per (block, wave)
 };
 
@@ -218,8 +220,9 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
   constexpr int NS = NSK;  // (shadows the file-wide default inside this kernel)
   using G = Geo<WMT, NWR, NSK>;
   static_assert(HEADC == 0 || (WMT == 2 && NWR == 4), "the fused head epilogue: 8 waves of 64 x 64");
+  static_assert(HEADC == 0 || G::SMEM <= hblk::LDS_BYTES, "the prefetch scratch KiB sits past the ring and the head");
   constexpr int STAGE = G::STAGE, GLDS_PER_STAGE = G::GLDS_PER_STAGE;
-  constexpr int SMEM_BYTES = HEADC ? std::max(G::SMEM, hblk::LDS_BYTES) : G::SMEM;
+  constexpr int SMEM_BYTES = HEADC ? std::max(G::SMEM, hblk::LDS_BYTES) + 1024 : G::SMEM;  // (+ the prefetch scratch)
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
   const int m0 = blockIdx.x * G::BM, n0 = blockIdx.y * FBN;
   const int lane = threadIdx.x & 63;
@@ -573,7 +576,26 @@ __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f3
     const int row = m0 + wm * 64 + lane;
     if (row < p.M) *reinterpret_cast<uint2*>(hd.mask + (size_t)row * 4 + 2 * wn) = uint2{(unsigned)mw[0], (unsigned)mw[1]};
   };
-  hblk::block_head<C>(prep, smem, a, ops, m0, p.M, wave, lane, [](int, int, bool, const float (&)[4]) {}, stamp);
+  // after the first barrier (past the epilogue's last compiler-counted load wait, so nothing below waits for these):
+  // the pixels of the workgroup that runs next on this XCD - block blockIdx + pf_stride, its first K-step (the one its
+  // DMA prologue waits for), 256 rows x 64 B - into this XCD's L2 by LDS-DMA into a scratch KiB. Round-2 workgroups
+  // started with ~4.8K cycles of DMA prologue from HBM (stamps: ~2.6-3.2K with the prefetch).
+  const bool pf = p.pf_stride > 0 && (int)blockIdx.x + p.pf_stride < (int)gridDim.x;  // (block-uniform)
+  auto post_b1 = [&]() {
+    if (pf) {
+      const int m1 = ((int)blockIdx.x + p.pf_stride) * hblk::ROWS;
+      const dma_i32x4 rx = dma_rsrc4(p.X, (unsigned)((size_t)p.M * p.ldx));
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {  // 16 pieces of 16 rows x 64 B, 2 per wave
+        const int row = 16 * (wave + 8 * u) + (lane >> 2);
+        const unsigned voff = (unsigned)((size_t)min(m1 + row, p.M - 1) * p.ldx + 16 * (lane & 3));
+        bdma16_asm(rx, voff, 0u, smem + hblk::LDS_BYTES);  // (past the ring and the head's LDS)
+      }
+    }
+  };
+  hblk::block_head<C>(prep, smem, a, ops, m0, p.M, wave, lane, [](int, int, bool, const float (&)[4]) {}, stamp,
+                      post_b1);
+  if (pf) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the scratch DMA lands before the LDS is released)
 }
 
 // fp32 [N][K] -> zero-padded fp16 planes [NPL][N][Kp] of W * 2^8 (u8_planes.h)
@@ -1804,6 +1826,16 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
   p.head = head;
   p.prio = knob(KNOB_U8_FWD_PRIO);
   const dim3 grid(u8_fwd_head_blocks(M), 1);
+  {  // the next workgroup on an XCD (blocks are dispatched round-robin over the 8 XCDs) is blockIdx + the CU count
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      hipDeviceProp_t pr;
+      cus = hipGetDeviceProperties(&pr, dev) == hipSuccess && pr.multiProcessorCount > 0 ? pr.multiProcessorCount : 256;
+    }
+    p.pf_stride = knob(KNOB_U8_FWD_PREFETCH) ? cus : 0;
+  }
   const int tail = tail_substeps(K);
   const int spread = knob(KNOB_U8_FWD_DMA_SPREAD);  // 0, 1 (spread DMA), 2 (+ fragment reads one substep ahead)
 #ifdef SDML_KERNEL_EXPERIMENTS  // timing variants (tools/u8_fwd_stamps.py): SDML_U8_FWD_MODE 1-6, 8-10

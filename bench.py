@@ -101,6 +101,9 @@ def parse():
     p.add_argument("--alternatives", default="auto", choices=["auto", "on", "off"],
                    help="after the timed steps, also time the reference's placement (pp2dp) for the JSON; "
                         "auto: at N = 2 only (the reference's own world size)")
+    p.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                   help="replay each step from a HIP graph (parallel/graphs.py, one graph per cycled batch reading "
+                        "the device-resident data in place); auto = off: measured slower in steady state (README)")
     p.add_argument("--pixels", default="u8", choices=["u8", "f32"],
                    help="image storage: MNIST's uint8 bytes (ToTensor's /255 fused into fc1) or float32")
     return p.parse_args()
@@ -250,8 +253,21 @@ def main():
         own_lo = engine.local_start(0, B) + (mesh.pp_rank * B if kind == "rotate" else 0)
         ds = _ShardedSynth(GB, own_lo, B, a.dataset_batches, dev, pixels=a.pixels)
 
+    # A graph replay is one host call for the whole step (full forward + backward + SGD, same kernels): it removes the
+    # host enqueue the first timed step carries after the synchronising barrier, but the replayed kernels ran ~4 us
+    # per step slower than the same kernels launched eagerly (profiles/r5_ab_graph_replay.jsonl), so it is opt-in.
+    use_graph = dev.type == "cuda" and a.graph == "on"
+    graphed = None
+    if use_graph:
+        from simple_distributed_machine_learning_amd.parallel.graphs import GraphedStep
+
+        graphed = GraphedStep(engine, allow_collectives=world > 1, direct_data=True,
+                              max_direct=max(1, a.dataset_batches))
+
     def step(i):
         start = (i % a.dataset_batches) * GB
+        if graphed is not None:
+            return graphed(ds, engine.local_start(start, B), B, global_batch=GB)
         return engine.run(ds, engine.local_start(start, B), B, train=True, global_batch=GB)
 
     def sync():
@@ -336,6 +352,9 @@ def main():
                 "predicted": predicted,
                 "measured_alternatives": alternatives,
                 "kernel_knobs": knobs,
+                "hip_graph": None if graphed is None else {"graphs": len(graphed.graphs), "replays": graphed.replays,
+                                                           "eager_steps": graphed.eager_steps,
+                                                           "disabled": graphed.disabled},
                 "microbatches": M,
                 "batch_per_gpu": a.batch_per_gpu,
                 "optimizer": "SGD lr=0.1 momentum=0.5",

@@ -1443,13 +1443,17 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
   U8W_STAMP(15, __builtin_amdgcn_s_memrealtime);
 }
 
-// The step's two deterministic reductions in one launch: blocks [0, nslab) sum the weight
-// gradient's split slabs (64 float4 columns per block, 16 waves over the splits w, w + 16, ..., wave
-// partials added in wave order), the blocks after them run the fused head's reduction (head_reduce.h).
-// Saves the head reduction's own launch (~5 us of latency-bound work) on the one-rank MLP step.
+// The step's two deterministic reductions in one launch: blocks [0, nhead) run the fused head's reduction
+// (head_reduce.h: two dependent round trips of 4-byte loads, so they start first instead of trailing the grid),
+// the blocks after them sum the weight gradient's split slabs. Saves the head reduction's own launch (~5 us of
+// latency-bound work) on the one-rank MLP step.
+// Slab blocks, COLS float4 columns each: wave w's partial of a column is ((a0 + a1) + (a2 + a3)), a[u & 3] summing
+// splits w + 16u (u = 0..7, then w + 128, ... into a0), and the 16 wave partials are added in wave order. COLS = 64:
+// one lane per column; COLS = 32: lanes 32..63 take a2, a3 of the lane 32 below (twice the blocks, half the loads
+// per lane; the same sums in the same order, so the same bits).
 // sg.p set: these are the step's last gradients, and the optimizer step is applied here (sgd_rule.h)
 // instead of by a separate SGD launch over the flat buffer.
-// Segments: blocks [0, nA) reduce [a_off, a_end), blocks [nA, nslab) reduce [b_off, b_end) (offsets into the
+// Segments: slab blocks [0, nA) reduce [a_off, a_end), blocks [nA, nslab) reduce [b_off, b_end) (offsets into the
 // [N * 784 + N] gradient, multiples of 4): the whole gradient is one segment; one hidden-group range of a
 // split weight gradient is its weight rows plus its bias entries.
 struct SlabSegs {
@@ -1457,22 +1461,28 @@ struct SlabSegs {
   int nA;
 };
 
+template <int COLS>
 __global__ void __launch_bounds__(1024) slab_head_reduce_kernel(const float* __restrict__ slab, int64_t stride,
                                                                 int splits, float* __restrict__ out, SlabSegs sgs,
-                                                                int nslab, HeadReduceArgs head, SgdFuse sg) {
+                                                                int nslab, int nhead, HeadReduceArgs head,
+                                                                SgdFuse sg) {
+  static_assert(COLS == 64 || COLS == 32, "one or two lanes per column");
   __shared__ f32x4 part[16][64];
-  if ((int)blockIdx.x >= nslab) {
-    head_reduce_block(head, blockIdx.x - nslab, reinterpret_cast<float(*)[64]>(&part[0][0]), sg.p ? &sg : nullptr);
+  if ((int)blockIdx.x < nhead) {
+    head_reduce_block(head, blockIdx.x, reinterpret_cast<float(*)[64]>(&part[0][0]), sg.p ? &sg : nullptr);
     return;
   }
+  const int bx = (int)blockIdx.x - nhead;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const bool segA = (int)blockIdx.x < sgs.nA;
-  const int64_t i = (segA ? sgs.a_off : sgs.b_off) + ((int64_t)(segA ? blockIdx.x : blockIdx.x - sgs.nA) * 64 + l) * 4;
+  const int c = l % COLS, half = l / COLS;  // (COLS = 64: half = 0)
+  const bool segA = bx < sgs.nA;
+  const int64_t i = (segA ? sgs.a_off : sgs.b_off) + ((int64_t)(segA ? bx : bx - sgs.nA) * COLS + c) * 4;
   const int64_t n = segA ? sgs.a_end : sgs.b_end;
+  const bool lead = half == 0;
   // wave 0's epilogue operands (the gradient it adds into, the parameter, its momentum) are loaded first, with the
   // partials: one memory round trip for all of them instead of two more after the sum
   f32x4 acc0 = {}, pv0 = {}, bv0 = {};
-  if (w == 0 && i < n) {
+  if (w == 0 && lead && i < n) {
     acc0 = *reinterpret_cast<const f32x4*>(out + i);
     if (sg.p) {
       pv0 = *reinterpret_cast<const f32x4*>(sg.p + i);
@@ -1482,19 +1492,34 @@ __global__ void __launch_bounds__(1024) slab_head_reduce_kernel(const float* __r
   f32x4 a[4] = {};
   if (i < n) {
     int s = w;  // wave w: splits w, w + 16, ...
-    for (; s + 16 * 7 < splits; s += 16 * 8) {
+    if constexpr (COLS == 64) {
+      for (; s + 16 * 7 < splits; s += 16 * 8) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) a[u & 3] += *reinterpret_cast<const f32x4*>(slab + (int64_t)(s + 16 * u) * stride + i);
+        for (int u = 0; u < 8; ++u) a[u & 3] += *reinterpret_cast<const f32x4*>(slab + (int64_t)(s + 16 * u) * stride + i);
+      }
+    } else {  // this lane's two of the four: u & 3 in {2 half, 2 half + 1}
+      for (; s + 16 * 7 < splits; s += 16 * 8) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int u = (v & 1) + 2 * half + 4 * (v >> 1);
+          a[v & 1] += *reinterpret_cast<const f32x4*>(slab + (int64_t)(s + 16 * u) * stride + i);
+        }
+      }
     }
-    for (; s < splits; s += 16) a[0] += *reinterpret_cast<const f32x4*>(slab + (int64_t)s * stride + i);
+    if (lead)
+      for (; s < splits; s += 16) a[0] += *reinterpret_cast<const f32x4*>(slab + (int64_t)s * stride + i);
   }
-  part[w][l] = (a[0] + a[1]) + (a[2] + a[3]);
+  if constexpr (COLS == 64) {
+    part[w][l] = (a[0] + a[1]) + (a[2] + a[3]);
+  } else {
+    part[w][l] = a[0] + a[1];  // lanes c: a0 + a1, lanes 32 + c: a2 + a3
+  }
   __syncthreads();
-  if (w == 0 && i < n) {
+  if (w == 0 && lead && i < n) {
     f32x4 acc = acc0;
-    f32x4 t = part[0][l];
+    f32x4 t = COLS == 64 ? part[0][l] : part[0][l] + part[0][l + 32];
 #pragma unroll
-    for (int q = 1; q < 16; ++q) t += part[q][l];
+    for (int q = 1; q < 16; ++q) t += COLS == 64 ? part[q][l] : part[q][l] + part[q][l + 32];
     acc += t;
     if (sg.p) {
       const f32x4 nv = sgd_update4_pre(sg.p + i, sg.buf + i, acc, SgdRule{sg.lr, sg.mom, sg.damp, sg.wd, sg.nesterov, sg.first},
@@ -1508,6 +1533,26 @@ __global__ void __launch_bounds__(1024) slab_head_reduce_kernel(const float* __r
     }
     *reinterpret_cast<f32x4*>(out + i) = acc;
   }
+}
+
+// launch: the segments' slab blocks at COLS columns each, the head's blocks in front
+static void launch_slab_head_reduce(const float* slab, int64_t stride, int splits, float* out, int64_t a_off,
+                                    int64_t a_end, int64_t b_off, int64_t b_end, const HeadReduceArgs* head,
+                                    const SgdFuse* sg, hipStream_t stream) {
+  const int cols = knob(KNOB_U8_SLAB_COLS) == 32 ? 32 : 64;
+  SlabSegs sgs{a_off, a_end, b_off, b_end, (int)(((a_end - a_off) / 4 + cols - 1) / cols)};
+  const int nslab = sgs.nA + (int)(((b_end - b_off) / 4 + cols - 1) / cols);
+  const bool hd = head && head->part;
+  const int nhead = hd ? head_reduce_blocks(*head) : 0;
+  const dim3 grid(nslab + nhead);
+  const HeadReduceArgs ha = hd ? *head : HeadReduceArgs();
+  const SgdFuse sf = sg ? *sg : SgdFuse();
+  if (cols == 32)
+    hipLaunchKernelGGL(slab_head_reduce_kernel<32>, grid, dim3(1024), 0, stream, slab, stride, splits, out, sgs, nslab,
+                       nhead, ha, sf);
+  else
+    hipLaunchKernelGGL(slab_head_reduce_kernel<64>, grid, dim3(1024), 0, stream, slab, stride, splits, out, sgs, nslab,
+                       nhead, ha, sf);
 }
 
 }  // namespace
@@ -1647,21 +1692,12 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigne
   const int64_t n = (int64_t)N * GKC + N;
   if (grp) {  // this hidden-group range only: its weight rows, then its bias entries (+ the head's reduction)
     if (sgd && sgd->p) abort();  // host contract: the split weight gradient is not the fused optimizer step
-    SlabSegs sgs;
-    sgs.a_off = (int64_t)grp->g_first * GHN * GKC;
-    sgs.a_end = (int64_t)(grp->g_first + grp->g_count) * GHN * GKC;
-    sgs.b_off = (int64_t)N * GKC + grp->g_first * GHN;
-    sgs.b_end = sgs.b_off + grp->g_count * GHN;
-    sgs.nA = (int)(((sgs.a_end - sgs.a_off) / 4 + 63) / 64);
-    const int nslab = sgs.nA + (int)(((sgs.b_end - sgs.b_off) / 4 + 63) / 64);
-    const bool hd = head && head->part;
-    hipLaunchKernelGGL(slab_head_reduce_kernel, dim3(nslab + (hd ? head_reduce_blocks(*head) : 0)), dim3(1024), 0,
-                       stream, slab, n, splits, gwb, sgs, nslab, hd ? *head : HeadReduceArgs(), SgdFuse());
+    const int64_t b_off = (int64_t)N * GKC + grp->g_first * GHN;
+    launch_slab_head_reduce(slab, n, splits, gwb, (int64_t)grp->g_first * GHN * GKC,
+                            (int64_t)(grp->g_first + grp->g_count) * GHN * GKC, b_off, b_off + grp->g_count * GHN, head,
+                            nullptr, stream);
   } else if (head && head->part) {
-    const int nslab = (int)((n / 4 + 63) / 64);
-    SlabSegs sgs{0, n, n, n, nslab};
-    hipLaunchKernelGGL(slab_head_reduce_kernel, dim3(nslab + head_reduce_blocks(*head)), dim3(1024), 0, stream, slab, n,
-                       splits, gwb, sgs, nslab, *head, sgd ? *sgd : SgdFuse());
+    launch_slab_head_reduce(slab, n, splits, gwb, 0, n, n, n, head, sgd, stream);
   } else {
     if (sgd && sgd->p) abort();  // host contract: the fused step needs the head reduction in the same launch
     slab_reduce(slab, n, splits, gwb, n, stream);

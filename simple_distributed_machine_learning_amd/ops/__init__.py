@@ -487,16 +487,22 @@ def mlp_small_step(x, target, fc1, fc2, optimizer, scale: float, stats, args=Non
                                  float(o.weight_decay), bool(o.nesterov), o.steps == 0, float(scale), stats))
 
 
-def ref_cnn_step(x, target, s0, s1, optimizer, scale: float, stats, ctr, seed0: int, seed1: int) -> None:
+def ref_cnn_step_args(s0, s1, optimizer):
+    """The parameter / momentum views :func:`ref_cnn_step` takes, built once per engine (the flat buffers never
+    move; rebuilding the 8 momentum views was ~40 % of the step's host time at B = 60)."""
+    params = [s0.conv1.weight, s0.conv1.bias, s0.conv2.weight, s0.conv2.bias,
+              s1.fc1.weight, s1.fc1.bias, s1.fc2.weight, s1.fc2.bias]
+    return [p.data for p in params], [optimizer.buffer_view(p) for p in params]
+
+
+def ref_cnn_step(x, target, s0, s1, optimizer, scale: float, stats, ctr, seed0: int, seed1: int, args=None) -> None:
     """ROCm: the reference CNN's whole training step - stage 0 forward, stage 1 forward + NLL + backward,
     stage 0 backward and torch.optim.SGD on all 8 tensors - in two launches (ref_cnn.hip: one workgroup per
     sample, then a fixed-order reduction of the per-sample records that applies the update). ``stats`` [2]
     receives (loss sum, correct); the dropout counter ``ctr`` is advanced on the device."""
-    params = [s0.conv1.weight, s0.conv1.bias, s0.conv2.weight, s0.conv2.bias,
-              s1.fc1.weight, s1.fc1.bias, s1.fc2.weight, s1.fc2.bias]
     o = optimizer
-    bufs = [o.buffer_view(p) for p in params]
+    params, bufs = args if args is not None else ref_cnn_step_args(s0, s1, optimizer)
     p0, p1 = float(s0.conv2_drop.p), float(s1.p)
-    _k().ref_cnn_step(x, target, [p.data for p in params], bufs, int(seed0), int(seed1), ctr, p0, p0 > 0, p1, p1 > 0,
+    _k().ref_cnn_step(x, target, params, bufs, int(seed0), int(seed1), ctr, p0, p0 > 0, p1, p1 > 0,
                       float(scale), float(o.lr), float(o.momentum), float(o.dampening), float(o.weight_decay),
                       bool(o.nesterov), o.steps == 0, stats)

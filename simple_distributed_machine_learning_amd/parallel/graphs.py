@@ -14,6 +14,11 @@ What changes between replays, and how it gets into the graph:
   pool. A buffer allocated inside the pool could alias memory that earlier nodes of the
   same graph reuse. Before each replay the step's real slices are copied into the buffers.
   These are device-to-device copies, because the datasets already live in HBM.
+  ``direct_data=True`` (a device-resident dataset that a training loop cycles through, e.g.
+  bench.py's synthetic batches): one graph per (dataset, start) that reads the dataset's own
+  slices, so a replay moves no data at all (at batch 131072 the copy would be 103 MB of
+  uint8 pixels, ~25 us of HBM traffic, per step). At most ``max_direct`` such graphs; a step
+  past that cap runs eagerly.
 * dropout: the fused kernels mix the engine's device step counter into their seeds. The
   graph increments that counter, so each replay draws fresh masks.
 * the optimizer: the first step (momentum-buffer initialisation) runs eagerly, so the
@@ -91,13 +96,17 @@ class GraphedStep:
     """``step(dataset, start, batch_size, global_batch)`` == ``engine.run(..., train=True)``
     replayed from a captured HIP graph (one graph per (batch_size, global_batch))."""
 
-    def __init__(self, engine: PipelineEngine, allow_collectives: bool = False):
+    def __init__(self, engine: PipelineEngine, allow_collectives: bool = False, direct_data: bool = False,
+                 max_direct: int = 16):
         if engine.device.type != "cuda":
             raise ValueError("GraphedStep needs a ROCm device engine")
         if engine.mesh.world_size > 1 and not allow_collectives:
             raise ValueError("GraphedStep: multi-process capture (RCCL in the graph) is opt-in: "
                              "pass allow_collectives=True")
         self.engine = engine
+        self.direct = direct_data
+        self.max_direct = max_direct
+        self.eager_steps = 0
         # (graph, window, result, start, planes_current, relies_on_planes) per (batch, global batch)
         self.graphs: Dict[Tuple[int, Optional[int]], tuple] = {}
         self._planes_current = True
@@ -146,6 +155,12 @@ class GraphedStep:
         return g, res
 
     def _capture(self, dataset, start: int, batch_size: int, global_batch: Optional[int]):
+        if self.direct:  # the graph reads the dataset's own slices: keyed by (dataset, start), holds the dataset
+            g, res = self._record(dataset, start, batch_size, global_batch, self.pool)
+            if self.pool is None:
+                self.pool = g.pool()
+            self.engine.flat.grads_zero = True
+            return g, dataset, res, start, self._planes_current, self._relies_on_planes
         win = _StaticWindow(dataset)
         g, _ = self._record(win, start, batch_size, global_batch, None)  # discover the data slices
         del g
@@ -169,12 +184,15 @@ class GraphedStep:
         eng = self.engine
         if self.disabled or eng.optimizer.steps == 0:
             return self._eager(dataset, start, batch_size, global_batch)
-        key = (batch_size, global_batch)
+        key = (batch_size, global_batch) + ((id(dataset), start) if self.direct else ())
         t0 = time.perf_counter()
         if any(gr[5] for gr in self.graphs.values()) and not self._caches_current():
             # weights changed outside the captured step: graphs that read the cached weight planes would
             # use stale ones. Drop them; this step runs eagerly (re-splitting) and the next one recaptures.
             self.graphs = {k: gr for k, gr in self.graphs.items() if not gr[5]}
+            return self._eager(dataset, start, batch_size, global_batch)
+        if key not in self.graphs and self.direct and len(self.graphs) >= self.max_direct:
+            self.eager_steps += 1
             return self._eager(dataset, start, batch_size, global_batch)
         if key not in self.graphs:
             try:
@@ -185,7 +203,8 @@ class GraphedStep:
                 torch.cuda.synchronize(eng.device)
                 return self._eager(dataset, start, batch_size, global_batch)
         g, win, res, cap_start, planes_current, _ = self.graphs[key]
-        win.load(dataset, start - cap_start)
+        if not self.direct:
+            win.load(dataset, start - cap_start)
         g.replay()
         eng.global_step += 1
         # the captured step's update: steps, epoch, cache tokens

@@ -229,6 +229,7 @@ class PipelineEngine:
         self._cnn_step = None  # two-launch reference CNN step available (decided on first use)
         self.fast_steps = {"mlp_small": 0, "cnn": 0}  # steps that ran the one/two-launch paths (tests)
         self._small_args = None
+        self._cnn_args = None
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
 
@@ -931,8 +932,10 @@ class PipelineEngine:
         seed1 = _draw_seed() if s1.p > 0 else 0
         stats = torch.empty(2, device=dev, dtype=torch.float32)
         scale = self._loss_scale(dataset, batch_size, global_batch)
+        if self._cnn_args is None:
+            self._cnn_args = ops.ref_cnn_step_args(s0, s1, self.optimizer)
         ops.ref_cnn_step(x.contiguous(), tgt.contiguous(), s0, s1, self.optimizer, scale, stats,
-                         self.step_ctr if self._uses_rng else None, seed0, seed1)
+                         self.step_ctr if self._uses_rng else None, seed0, seed1, self._cnn_args)
         self.optimizer.commit_fused(zero_grad=True, planes_current=False)
         self.global_step += 1  # (the kernel advanced the device dropout counter)
         self.last_timing = {}

@@ -163,6 +163,29 @@ def test_engine_fused_head_step_matches_unfused(M, monkeypatch):
 
 
 @pytest.mark.parametrize("M", [1, 2])
+def test_slab_reduce_geometries_bitwise_equal(M):
+    """Knob U8_SLAB_COLS: the weight-gradient slab reduction (+ head reduction + fused SGD) with one lane per float4
+    column (64 per block) or two (32 per block, each lane half of a wave's split partial) adds the same numbers in
+    the same order: bitwise equal parameters, momentum and weight planes after 3 engine steps."""
+    from simple_distributed_machine_learning_amd import _native
+
+    K = _native.kernels()
+    runs = []
+    try:
+        for cols in (64, 32):
+            K.set_knob("U8_SLAB_COLS", cols)
+            e = _engine(M)
+            losses = _train(e)
+            runs.append((losses, e.flat.params.clone(), e.optimizer.momentum_buffer.clone(),
+                         e.stages[0].plane_cache.planes.clone()))
+    finally:
+        K.reset_knobs()
+    (l0, p0, b0, c0), (l1, p1, b1, c1) = runs
+    assert l0 == l1
+    assert torch.equal(p0, p1) and torch.equal(b0, b1) and torch.equal(c0, c1)
+
+
+@pytest.mark.parametrize("M", [1, 2])
 @pytest.mark.parametrize("opt", [dict(), dict(momentum=0.0), dict(wd=1e-4), dict(damp=0.1), dict(nesterov=True)])
 def test_fused_optimizer_step_bitwise_equals_optimizer_step(M, opt, monkeypatch):
     """the SGD update applied inside the last reduction launch (FusedSGD.fused_args) against
@@ -315,8 +338,8 @@ def test_wgrad_ring_balanced_tiles(M, C, Nh):
     torch.testing.assert_close(g1.double(), want, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("ring", [0, 1])
-def test_wgrad_hidden_group_ranges_match_the_whole_gradient(ring):
+@pytest.mark.parametrize("ring,cols", [(0, 64), (1, 64), (1, 32)])
+def test_wgrad_hidden_group_ranges_match_the_whole_gradient(ring, cols):
     """linear_wgrad_u8_dl(groups=(g_first, g_count, blocks)) - the data-parallel step's two hidden-unit ranges
     (SDML_DP_SPLIT) - on both kernel forms: each range writes only its rows of gW / entries of gb, and the two ranges
     together equal the one-launch gradient to fp32 summation order (the row splits differ)."""
@@ -331,6 +354,7 @@ def test_wgrad_hidden_group_ranges_match_the_whole_gradient(ring):
     bits = ops.relu_bits(h)
     try:
         K.set_knob("U8_WGRAD_RING", ring)
+        K.set_knob("U8_SLAB_COLS", cols)
         full = torch.zeros(Nh * KD + Nh, device=DEV)
         ops.linear_wgrad_u8_dl(x8, dl, w2, bits, full[:Nh * KD].view(Nh, KD), full[Nh * KD:])
         part = torch.zeros(Nh * KD + Nh, device=DEV)

@@ -38,7 +38,9 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--seq_len", type=int, default=None)
-    ap.add_argument("--graph", action="store_true", help="replay the step from a captured hipGraph")
+    ap.add_argument("--graph", nargs="?", const="copy", default=None, choices=["copy", "direct"],
+                    help="replay the step from a captured hipGraph (copy: static data buffers refilled per step; "
+                         "direct: one graph per cycled batch reading the device-resident data in place)")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel ranks per stage (gpt2)")
     ap.add_argument("--dtype", default=None, choices=[None, "fp32", "bf16"], help="resnet18: compute dtype")
     ap.add_argument("--pixels", default="auto", choices=["auto", "f32", "u8"],
@@ -94,7 +96,7 @@ def main():
     if a.graph:
         from simple_distributed_machine_learning_amd.parallel.graphs import GraphedStep
 
-        graphed = GraphedStep(eng)
+        graphed = GraphedStep(eng, direct_data=a.graph == "direct", max_direct=nb)
 
     def step(i):
         st = (i % nb) * GB
@@ -119,7 +121,7 @@ def main():
     l, c, n = eng.reduce_metrics(res)
     if rank == 0:
         print(json.dumps({"config": a.config, "schedule": kind, "stages": stages, "ranks": world, "tp": a.tp,
-                          "microbatches": M, "batch": GB, "seq_len": S, "dtype": str(spec.param_dtype), "graph": bool(a.graph), "tuned_gemms": tuned,
+                          "microbatches": M, "batch": GB, "seq_len": S, "dtype": str(spec.param_dtype), "graph": a.graph or False, "tuned_gemms": tuned,
                           "pixels": a.pixels,
                           "value": round(GB * per_sample * a.steps / el, 1), "unit": unit,
                           "ms_per_step": round(el / a.steps * 1e3, 3), "loss": round(l / max(1, n), 4),

@@ -103,7 +103,8 @@ def parse():
                         "auto: at N = 2 only (the reference's own world size)")
     p.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                    help="replay each step from a HIP graph (parallel/graphs.py, one graph per cycled batch reading "
-                        "the device-resident data in place); auto = off: measured slower in steady state (README)")
+                        "the device-resident data in place, the gradient all-reduce inside); auto: on for the dp "
+                        "placement over RCCL at N > 1, off at N = 1 (measured, README 'HIP graphs')")
     p.add_argument("--pixels", default="u8", choices=["u8", "f32"],
                    help="image storage: MNIST's uint8 bytes (ToTensor's /255 fused into fc1) or float32")
     return p.parse_args()
@@ -253,10 +254,14 @@ def main():
         own_lo = engine.local_start(0, B) + (mesh.pp_rank * B if kind == "rotate" else 0)
         ds = _ShardedSynth(GB, own_lo, B, a.dataset_batches, dev, pixels=a.pixels)
 
-    # A graph replay is one host call for the whole step (full forward + backward + SGD, same kernels): it removes the
-    # host enqueue the first timed step carries after the synchronising barrier, but the replayed kernels ran ~4 us
-    # per step slower than the same kernels launched eagerly (profiles/r5_ab_graph_replay.jsonl), so it is opt-in.
-    use_graph = dev.type == "cuda" and a.graph == "on"
+    # A graph replay is one host call for the whole step (full forward + backward + all-reduce + SGD, same kernels).
+    # N > 1, dp over RCCL: the eager step waits ~25 us on the device between the gradient reduction and the optimizer
+    # launch (the cross-stream hand-offs to and from the collective's stream); replayed, those are graph edges and the
+    # step runs within ~3.5 us of the one-GPU step (profiles/r5_dp_graph_one_rank_rccl.jsonl). N = 1 has no collective,
+    # and there the replayed kernels ran ~4 us per step slower than eager launches (profiles/r5_ab_graph_replay.jsonl).
+    rccl = engine.transport is not None and engine.transport.name == "direct"
+    use_graph = dev.type == "cuda" and (a.graph == "on" or (
+        a.graph == "auto" and world > 1 and place == "dp" and rccl and not engine.dp_split))
     graphed = None
     if use_graph:
         from simple_distributed_machine_learning_amd.parallel.graphs import GraphedStep

@@ -75,7 +75,12 @@ class MLPStage(PipelineStage):
         return True
 
     def layers(self) -> List[nn.Linear]:
-        return [getattr(self, n) for n in self.names]
+        # (the submodules are fixed at construction; nn.Module attribute lookups cost ~1 us each on the step path)
+        ls = self.__dict__.get("_layer_list")
+        if ls is None or any(l is not self._modules.get(n) for l, n in zip(ls, self.names)):
+            ls = [getattr(self, n) for n in self.names]
+            self.__dict__["_layer_list"] = ls
+        return list(ls)
 
     def _is_classifier(self, i: int) -> bool:
         return self.layer_ids[i] == self.n_total - 1

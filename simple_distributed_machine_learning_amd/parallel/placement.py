@@ -32,7 +32,8 @@ The model (documented in README "Multi-GPU placement") is deliberately simple:
   what range 0's collective does not hide is exposed: ``half + max(0, half - wgrad/2)`` plus the split's
   own cost (``ComputeModel.split_us``); with it off (and for the other placements) the whole all-reduce
   follows the last backward, exposed, plus the separate optimizer launch the all-reduce forces
-  (``ComputeModel.dp_step_us``).
+  (``ComputeModel.dp_step_us``), which bench.py's HIP-graph replay of the ``dp`` step mostly removes
+  (``ComputeModel.dp_graph_step_us``: the stream hand-offs to and from the collective are graph edges).
 
 ``choose`` returns the placement with the smallest predicted step; among placements within 2% of
 it, the one that moves the most boundary bytes across GPUs (the split the benchmark is about).
@@ -71,6 +72,10 @@ class ComputeModel:
       reduction can no longer apply SGD in the same launch, a separate optimizer launch follows the collective, plus
       the collective's host and stream overhead: the one-rank RCCL harness (tools/bench_dp_split.py) runs the N > 1
       path in 0.1754 ms against 0.1515 (profiles/r5_dpsplit_one_rank_rccl.jsonl);
+    * ``dp_graph_step_us``: the same when the step (collective included) replays from a HIP graph, as bench.py runs
+      ``dp`` at N > 1: 0.1533 vs 0.1498 ms on the same harness, where the eager step pays ~25 us between the
+      reduction and the optimizer launch for the two cross-stream waits around the collective
+      (profiles/r5_dp_graph_one_rank_rccl.jsonl);
     * ``split_us``: the split weight gradient's own extra cost (same harness: 0.2099 vs 0.1754 ms);
     * ``wgrad_ns``: the weight gradient alone (the split hides range 0's all-reduce under half of it)."""
     fused_ns: float = 1.051
@@ -82,6 +87,7 @@ class ComputeModel:
     grad_bytes: int = 40          # factored boundary gradient per row (10 fp32)
     param_bytes: int = 101_770 * 4
     dp_step_us: float = 24.0
+    dp_graph_step_us: float = 3.5
     split_us: float = 34.5
 
 
@@ -95,10 +101,13 @@ def dp_split_default() -> bool:
 
 def predict(placement: str, n: int, batch_per_gpu: int, waves: int = 2, phi: Optional[float] = None,
             link: LinkModel = LinkModel(), comp: ComputeModel = ComputeModel(),
-            dp_split: Optional[bool] = None) -> Dict[str, float]:
-    """Predicted step of ``placement`` at ``n`` GPUs (weak scaling: ``batch_per_gpu`` rows per GPU)."""
+            dp_split: Optional[bool] = None, graph: Optional[bool] = None) -> Dict[str, float]:
+    """Predicted step of ``placement`` at ``n`` GPUs (weak scaling: ``batch_per_gpu`` rows per GPU). ``graph``:
+    the step replays from a HIP graph (default: what bench.py does, i.e. for ``dp`` without the split)."""
     if dp_split is None:
         dp_split = dp_split_default()
+    if graph is None:
+        graph = placement == "dp" and not dp_split
     B = float(batch_per_gpu)
     row = comp.act_bytes + comp.grad_bytes
     if n == 1:
@@ -133,7 +142,7 @@ def predict(placement: str, n: int, batch_per_gpu: int, waves: int = 2, phi: Opt
             # split: two half collectives, range 0's under range 1's kernel
             half = (ar_us - link.collective_us) / 2 + link.collective_us
             ar_us = half + max(0.0, half - B * comp.wgrad_ns / 2e3) + comp.split_us
-        ar_us += comp.dp_step_us
+        ar_us += comp.dp_graph_step_us if graph else comp.dp_step_us
     else:
         ar_us = 0.0
     if link_bytes > 0:

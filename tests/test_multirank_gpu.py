@@ -124,6 +124,22 @@ def test_bench_two_ranks_on_one_gpu():
                 assert d["config"]["boundary_bytes_across_gpus_per_step"] == 0
 
 
+def test_bench_graph_replay_trains_identically():
+    """bench.py --graph on (one HIP graph per cycled batch, the data read in place): the same kernels as the eager
+    step, so the same final loss bit for bit; every step after the first (eager: momentum init) replays."""
+    env = dict(os.environ, SDML_BENCH_BATCH="16384", PYTHONPATH=ROOT)
+    out = {}
+    for g in ("off", "on"):
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "5", "--graph", g]
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+        out[g] = _bench_json(r)
+    assert out["off"]["config"]["hip_graph"] is None
+    hg = out["on"]["config"]["hip_graph"]
+    assert hg == {"graphs": 4, "replays": 7, "eager_steps": 0, "disabled": False}, hg
+    assert out["on"]["final_loss"] == out["off"]["final_loss"]
+
+
 def test_bench_spawns_its_ranks_without_a_launcher():
     """``python bench.py --gpus 2`` with no WORLD_SIZE in the environment starts its own two ranks
     (before touching the GPU) instead of silently running one: n_gpus and world_size_seen are 2."""

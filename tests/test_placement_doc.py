@@ -21,10 +21,23 @@ def test_split_priced_only_when_the_engine_splits(monkeypatch):
     on = plc.predict("dp", 8, 131072)
     c = plc.ComputeModel()
     assert off["allreduce_ms"] != on["allreduce_ms"]
-    # the default path: the whole all-reduce exposed plus the separate optimizer launch
+    # the default path: the whole all-reduce exposed plus the separate optimizer launch, replayed from a HIP graph
+    # (bench.py's dp step at N > 1); eager, the cross-stream hand-offs cost dp_step_us instead
     link = plc.LinkModel()
-    ar = 2 * 7 / 8 * c.param_bytes / (2 * link.gbps * 1e3) + link.collective_us + c.dp_step_us
-    assert abs(off["allreduce_ms"] - round(ar / 1e3, 4)) < 1e-4
+    ar = 2 * 7 / 8 * c.param_bytes / (2 * link.gbps * 1e3) + link.collective_us
+    assert abs(off["allreduce_ms"] - round((ar + c.dp_graph_step_us) / 1e3, 4)) < 1e-4
+    monkeypatch.delenv("SDML_DP_SPLIT", raising=False)
+    eager = plc.predict("dp", 8, 131072, graph=False)
+    assert abs(eager["allreduce_ms"] - round((ar + c.dp_step_us) / 1e3, 4)) < 1e-4
+
+
+def test_bench_graph_default_matches_the_model():
+    """bench.py replays the dp step from a HIP graph at N > 1 over RCCL (not split); the model prices that path."""
+    import pathlib
+    import re
+
+    src = pathlib.Path(__file__).resolve().parents[1].joinpath("bench.py").read_text()
+    assert re.search(r'a\.graph == "auto" and world > 1 and place == "dp" and rccl and not engine\.dp_split', src)
 
 
 def test_one_gpu_prediction_matches_the_fused_step():

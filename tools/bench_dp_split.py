@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--batch", type=int, default=131072)
     ap.add_argument("--modes", default="1,0")
     ap.add_argument("--blocks", type=int, default=None)
+    ap.add_argument("--graph", action="store_true", help="replay the step (collective included) from a HIP graph")
     a = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
@@ -47,15 +48,23 @@ def main():
         if a.blocks:
             eng.dp_split_blocks = a.blocks
         assert eng.grad_sync.enabled
+        run = eng.run
+        if a.graph:
+            from simple_distributed_machine_learning_amd.parallel.graphs import GraphedStep
+
+            g = GraphedStep(eng, allow_collectives=True, direct_data=True, max_direct=4)
+
+            def run(ds_, st, b, train=True):
+                return g(ds_, st, b)
         for i in range(a.warmup):
-            eng.run(ds, (i % 4) * B, B, train=True)
+            run(ds, (i % 4) * B, B, train=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(a.steps):
-            res = eng.run(ds, (i % 4) * B, B, train=True)
+            res = run(ds, (i % 4) * B, B, train=True)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        print(json.dumps({"dp_split": eng.dp_split, "blocks": eng.dp_split_blocks, "split_steps": eng.dp_split_steps,
+        print(json.dumps({"graph": a.graph, "dp_split": eng.dp_split, "blocks": eng.dp_split_blocks, "split_steps": eng.dp_split_steps,
                           "ms_per_step": round(el / a.steps * 1e3, 4), "samples_per_s": round(B * a.steps / el, 1),
                           "loss": round(float(res.loss_sum) / res.count, 5), "collectives": eng.transport.ops}),
               flush=True)

@@ -75,12 +75,17 @@ class MLPStage(PipelineStage):
         return True
 
     def layers(self) -> List[nn.Linear]:
-        # (the submodules are fixed at construction; nn.Module attribute lookups cost ~1 us each on the step path)
+        # cached: the step path asks ~10 times per step and each nn.Module attribute lookup costs ~1 us; a
+        # reassigned layer attribute drops the cache (__setattr__)
         ls = self.__dict__.get("_layer_list")
-        if ls is None or any(l is not self._modules.get(n) for l, n in zip(ls, self.names)):
-            ls = [getattr(self, n) for n in self.names]
-            self.__dict__["_layer_list"] = ls
+        if ls is None:
+            ls = self.__dict__["_layer_list"] = [getattr(self, n) for n in self.names]
         return list(ls)
+
+    def __setattr__(self, name, value):
+        if name in self.__dict__.get("names", ()):
+            self.__dict__.pop("_layer_list", None)
+        super().__setattr__(name, value)
 
     def _is_classifier(self, i: int) -> bool:
         return self.layer_ids[i] == self.n_total - 1

@@ -16,10 +16,10 @@ the bias gradient with a generic reduction. This module avoids both:
 
 When a parameter has no ``.grad`` yet (standalone use), the gradients are returned to
 autograd in the usual way. CPU tensors and non-bf16 dtypes keep the plain ``F.linear``
-path. The forward / input-gradient GEMMs of a plain Linear are library GEMMs (hipBLASLt, faster at these
-shapes than gemm_bf16.hip's current schedule: tools/bench_gemm_bf16.py); the MLP's c_fc forward and c_proj input
-gradient run on gemm_bf16.hip with the GELU fused into their epilogues (:func:`mlp_gelu`; SDML_FUSED_GELU_GEMM=0
-puts them back on the library).
+path. The forward / input-gradient GEMMs run on gemm_bf16.hip's NT kernel (SDML_GPT2_GEMM=hand, the default since
+its 256 x 192 tiles; SDML_GPT2_GEMM=lib puts them on hipBLASLt); the MLP's c_fc forward and c_proj input gradient
+carry the GELU in their epilogues (:func:`mlp_gelu`). A shape the hand kernel does not take (the 50257-wide
+lm_head: N % 8 != 0) stays on the library.
 """
 from __future__ import annotations
 
@@ -32,12 +32,12 @@ import torch.nn.functional as F
 from .._native import kernels
 
 
-# SDML_GPT2_GEMM=hand: the forward and input-gradient GEMMs of these Linears on gemm_bf16.hip's NT kernel instead
-# of hipBLASLt (the 4-phase 256 x 256 kernel, or with knob GEMM_BF16_T2 the 256 x 128 two-workgroups-per-CU one);
-# the input gradient dY W runs as NT against W^T, derived once per weight per optimizer step (keyed like the conv
-# layouts: ops/conv.py WEIGHT_GEN). Default "lib": hipBLASLt is faster at the GPT-2 shapes (c_fc forward 76.7 us vs
-# 99.5 for the 4-phase kernel and 122.6 for the 256 x 128 one: profiles/r4_gemm_bf16_t2_vs_nt4_vs_hipblaslt.jsonl).
-_HAND = os.environ.get("SDML_GPT2_GEMM", "lib") == "hand"
+# SDML_GPT2_GEMM=hand (default): the forward and input-gradient GEMMs of these Linears on gemm_bf16.hip's 4-phase NT
+# kernel (256 x 256 or 256 x 192 tiles, whichever fills the 256 CUs' rounds better) instead of hipBLASLt; the input
+# gradient dY W runs as NT against W^T, derived once per weight per optimizer step (keyed like the conv layouts:
+# ops/conv.py WEIGHT_GEN). Round 5, GPT-2 step at 16 x 1024 tokens on one MI355X: 21.69 / 21.67 ms hand vs 21.83 /
+# 21.75 ms on hipBLASLt with its tuned solution table (profiles/r5_gpt2_hand_vs_lib.jsonl). "lib": hipBLASLt.
+_HAND = os.environ.get("SDML_GPT2_GEMM", "hand") == "hand"
 _WT = {}
 EPI_STORE, EPI_BIAS = 0, 1  # csrc/kernels/kernels.h GemmEpi
 
@@ -164,7 +164,8 @@ class _MLPFn(torch.autograd.Function):
 def mlp_gelu(x, w1, b1, w2, b2):
     """c_proj(gelu_tanh(c_fc(x))). On ROCm bf16 (default; SDML_FUSED_GELU_GEMM=0 turns it off): the c_fc forward
     and the c_proj input gradient on gemm_bf16.hip with the GELU / GELU' fused into their epilogues (no standalone
-    GELU passes), the other two on hipBLASLt. Round 4, one MI355X, GPT-2 step at 16 x 1024 tokens: 21.82 vs
+    GELU passes), the other two on the hand NT kernel too (SDML_GPT2_GEMM=lib: hipBLASLt). Round 4, one MI355X, GPT-2
+    step at 16 x 1024 tokens, the other two on hipBLASLt: 21.82 vs
     21.79 ms with library GEMMs + the standalone GELU kernels (profiles/r4_gpt2_fused_gelu_ab.jsonl) - the 4-phase
     NT mainloop still trails hipBLASLt's per GEMM (99.5 vs 76.7 us at c_fc), the fusion pays the difference back.
     (Round 3, before the 4-phase loop: fused c_fc 124.5 us vs 77 + GELU, so it was off.)"""

@@ -115,31 +115,55 @@ __device__ __forceinline__ s16x4 ds_tr16(const unsigned char* p) {
 // epilogue shared by both main loops: bf16 rows through the (free) stage buffers, 16-B row pieces to HBM
 // WNW: waves along N (4: the 256 x 256 tile's 2 x 4 waves; 2: the 256 x 128 tile's 2 x 2)
 // NJ: 16-column tiles per wave (4: the wave owns 64 columns; 3: 48, the 256 x 192 tile)
-template <int EPI, int WNW = 4, int NJ = 4>
+// TR: the accumulators hold the transposed product (the MFMA called with the B fragment as its A operand): lane
+// (l16, g) then has row 16 i + l16, columns 16 j + 4 g .. + 3 of tile (i, j) - 4 consecutive bf16, one ds_write_b64
+// (32 per lane) instead of 4 ds_write_b16 (128 per lane) of one column's 4 rows
+template <int EPI, int WNW = 4, int NJ = 4, bool TR = false>
 __device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&acc)[8][NJ], unsigned char* smem, int m0,
                                                    int n0, int wave, int lane) {
   const int wm = wave / WNW, wn = wave % WNW;
   const int g = lane >> 4, l16 = lane & 15;
   // wave image [128 rows][64 cols] bf16 (128 B rows, 16-B chunks swizzled like the A image; NJ = 3 uses 48 of them)
   unsigned char* W = smem + wave * (128 * 128);
-  float bj[NJ] = {};
-  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+  if constexpr (TR) {
+    float bj[NJ][4] = {};
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int col = min(n0 + wn * 16 * NJ + 16 * j + l16, p.N - 1);
-      bj[j] = bf2f(p.bias[col]);
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bj[j][r] = bf2f(p.bias[min(n0 + wn * 16 * NJ + 16 * j + 4 * g + r, p.N - 1)]);
     }
-  }
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+      for (int j = 0; j < NJ; ++j) {
+        const int row = 16 * i + l16, col = 16 * j + 4 * g;
+        typedef u16 u16x4 __attribute__((ext_vector_type(4)));
+        u16x4 v;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * i + 4 * g + r, col = 16 * j + l16;
-        const float v = acc[i][j][r] + bj[j];
-        *reinterpret_cast<u16*>(W + row * 128 + 16 * ((col >> 3) ^ rk_swz(row)) + 2 * (col & 7)) = f2bf(v);
+        for (int r = 0; r < 4; ++r) v[r] = f2bf(acc[i][j][r] + bj[j][r]);
+        *reinterpret_cast<u16x4*>(W + row * 128 + 16 * ((col >> 3) ^ rk_swz(row)) + 2 * (col & 7)) = v;
       }
+  } else {
+    float bj[NJ] = {};
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = min(n0 + wn * 16 * NJ + 16 * j + l16, p.N - 1);
+        bj[j] = bf2f(p.bias[col]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * i + 4 * g + r, col = 16 * j + l16;
+          const float v = acc[i][j][r] + bj[j];
+          *reinterpret_cast<u16*>(W + row * 128 + 16 * ((col >> 3) ^ rk_swz(row)) + 2 * (col & 7)) = f2bf(v);
+        }
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
 #pragma unroll 4
@@ -304,7 +328,7 @@ __device__ __forceinline__ void issue_half(const GP& p, unsigned char* smem, int
 // 2), quadrant-col 1 is that one n-tile, and the counted waits keep exactly the last three half-tiles in flight
 // (2 + 2 + 1 pieces). It exists for wave quantization: at N = 768 the 256-wide tiles make 192 tiles of a 16384-row
 // GEMM, 3/4 of the 256 CUs; 192-wide ones make 256.
-template <int EPI, int NJ = 4>
+template <int EPI, int NJ = 4, bool TR = false>
 __global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
   static_assert(NJ == 3 || NJ == 4, "n-tiles per wave");
   constexpr int BN = 64 * NJ, NJ1 = NJ - 2;  // tile width; n-tiles of quadrant-col 1
@@ -379,7 +403,8 @@ __global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
 #pragma unroll
         for (int jj = 0; jj < NQ; ++jj)
           acc[4 * qm + i][2 * QN + jj] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], bb[jj][s2], acc[4 * qm + i][2 * QN + jj], 0, 0, 0);
+              TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[jj][s2], a[i][s2], acc[4 * qm + i][2 * QN + jj], 0, 0, 0)
+                 : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], bb[jj][s2], acc[4 * qm + i][2 * QN + jj], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
   using Q0 = std::integral_constant<int, 0>;
@@ -440,7 +465,7 @@ __global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the past-the-end half-tiles, before the epilogue reuses LDS
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  gemm_bf16_epilogue<EPI, 4, NJ>(p, acc, smem, m0, n0, wave, lane);
+  gemm_bf16_epilogue<EPI, 4, NJ, TR>(p, acc, smem, m0, n0, wave, lane);
 }
 
 // ---- NT form, 256 x 128 tiles of 4 waves, two workgroups per CU ---------------------------------------
@@ -621,9 +646,12 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
     const bool n192 = nt4_use_192(p.tiles_m, N);
     if (n192) p.tiles_n = (N + 191) / 192;
     const dim3 g4(p.tiles_m * p.tiles_n);
+    const bool tr = knob(KNOB_GEMM_BF16_TR) != 0;
 #define NT4_LAUNCH(E)                                                                                  \
   do {                                                                                                 \
-    if (n192) hipLaunchKernelGGL((gemm_bf16_nt4_kernel<E, 3>), g4, dim3(GT), 0, stream, p);            \
+    if (n192 && tr) hipLaunchKernelGGL((gemm_bf16_nt4_kernel<E, 3, true>), g4, dim3(GT), 0, stream, p); \
+    else if (n192) hipLaunchKernelGGL((gemm_bf16_nt4_kernel<E, 3>), g4, dim3(GT), 0, stream, p);       \
+    else if (tr) hipLaunchKernelGGL((gemm_bf16_nt4_kernel<E, 4, true>), g4, dim3(GT), 0, stream, p);   \
     else hipLaunchKernelGGL((gemm_bf16_nt4_kernel<E, 4>), g4, dim3(GT), 0, stream, p);                 \
   } while (0)
     switch (epi) {

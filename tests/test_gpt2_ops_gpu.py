@@ -207,3 +207,38 @@ def test_gemm_bf16_192_wide_tiles_bit_identical_to_256(M, N, Kd):
         K.reset_knobs()
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(256, 192, 64), (300, 776, 192), (4096, 768, 768), (1000, 2304, 3072)])
+def test_gemm_bf16_transposed_accumulators(M, N, Kd):
+    """Knob GEMM_BF16_TR: the 4-phase NT GEMM with the MFMA operands swapped, so each lane accumulates 4 consecutive
+    columns of one output row (8-byte epilogue writes) - on both tile widths and every epilogue. The same products
+    summed per output element; equal to the untransposed kernel within one bf16 rounding and to fp32 within bf16."""
+    g = torch.Generator(device="cpu").manual_seed(M + 7 * N)
+    A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    u_in = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    outs = {}
+    try:
+        for n192 in (0, 1):
+            for tr in (0, 1):
+                K.set_knob("GEMM_BF16_N192", n192)
+                K.set_knob("GEMM_BF16_TR", tr)
+                C0, _ = K.gemm_bf16(A, W, None, False, 0)
+                C1, _ = K.gemm_bf16(A, W, bias, False, 1)
+                y, u = K.gemm_bf16(A, W, bias, False, 5)
+                du, _ = K.gemm_bf16(A, W, None, False, 6, u_in)
+                outs[(n192, tr)] = (C0, C1, y, u, du)
+                torch.testing.assert_close(C0.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+                torch.testing.assert_close(C1.float(), ref + bias.float(), rtol=1e-2,
+                                           atol=1e-2 * float(ref.abs().max()))
+    finally:
+        K.reset_knobs()
+    for n192 in (0, 1):
+        for a, b in zip(outs[(n192, 0)], outs[(n192, 1)]):
+            # (one bf16 rounding apart at most: the MFMA may sum a dot product in another internal order)
+            torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * float(a.float().abs().max()))
+    for a, b in zip(outs[(0, 1)], outs[(1, 1)]):
+        assert torch.equal(a, b)

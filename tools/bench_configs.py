@@ -81,6 +81,10 @@ def main():
 
         tuned = use_tuned_gemms()
     dev = mesh.device
+    if dev.type == "cuda":
+        from simple_distributed_machine_learning_amd import _native
+
+        _native.apply_knobs_from_env()  # A/B runs only (SDML_KNOBS="NAME=V,..."); default: none
     nb = 2
     if spec.input_kind == "tokens":
         ds = SyntheticTokens(B * eng.data_shards * nb, S, 50257, seed=5, device=dev)

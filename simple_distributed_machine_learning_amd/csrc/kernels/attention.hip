@@ -135,6 +135,16 @@ __device__ __forceinline__ void tile_load(TileRegs<ROWS>& t, const u16* G, long 
     t.v[u] = v;
   }
 }
+// rows past S re-read row S - 1 (unconditional loads, no exec-masked branches): only for consumers that mask those
+// keys themselves (the forward's edge tiles set their scores to -inf, so their V rows meet P = 0)
+template <int ROWS>
+__device__ __forceinline__ void tile_load_clamped(TileRegs<ROWS>& t, const u16* G, long srow, int r0, int S) {
+#pragma unroll
+  for (int u = 0; u < ROWS / 32; ++u) {
+    const int idx = threadIdx.x + 256 * u, r = idx >> 3, ch = idx & 7;
+    t.v[u] = *reinterpret_cast<const u16x8*>(G + (long)min(r0 + r, S - 1) * srow + 8 * ch);
+  }
+}
 template <int ROWS>
 __device__ __forceinline__ void tile_store(u16* L, const TileRegs<ROWS>& t) {
 #pragma unroll
@@ -193,8 +203,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   f32x16 o[2] = {zero16(), zero16()};  // O^T[d][q]: d tile 0..1
   const int kend = a.causal ? min(a.S, qb * QB + QB) : a.S;
   TileRegs<KBT> kr, vr;
-  tile_load(kr, K, a.sqs, 0, a.S);
-  tile_load(vr, V, a.sqs, 0, a.S);
+  tile_load_clamped(kr, K, a.sqs, 0, a.S);
+  tile_load_clamped(vr, V, a.sqs, 0, a.S);
   tile_store(Ks[0], kr);
   tile_store(Vs[0], vr);
   __syncthreads();
@@ -202,8 +212,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   for (int k0 = 0; k0 < kend; k0 += KBT, buf ^= 1) {
     const bool more = k0 + KBT < kend;
     if (more) {  // next tile's loads fly during this tile's MFMAs
-      tile_load(kr, K, a.sqs, k0 + KBT, a.S);
-      tile_load(vr, V, a.sqs, k0 + KBT, a.S);
+      tile_load_clamped(kr, K, a.sqs, k0 + KBT, a.S);
+      tile_load_clamped(vr, V, a.sqs, k0 + KBT, a.S);
     }
     if (!(a.causal && k0 > q0w + QW - 1)) {  // else: all this wave's queries precede k0
       const u16* Kt = Ks[buf];
@@ -219,17 +229,20 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
       // mask (diagonal / ragged tiles only) and running max on the RAW scores; the softmax scale
       // is folded into one FMA per score: p = exp2(s * c - max * c), c = scale * log2(e) > 0
       const bool edge = (a.causal && k0 + KBT - 1 > q0w) || k0 + KBT > a.S;
+      if (edge) {  // (one uniform branch; per element a compare + select: hipcc turned the per-element `if` into 2
+                   // scalar branches per score, on the unmasked tiles too)
+        const int lim = (a.causal ? min(qi, a.S - 1) : a.S - 1) - (k0 + 4 * h);  // last key this lane may see
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            s[c][i] = (32 * c + (i & 3) + 8 * (i >> 2) > lim) ? -INFINITY : s[c][i];
+      }
       float mr = -INFINITY;
 #pragma unroll
       for (int c = 0; c < NC; ++c)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if (edge) {
-            const int kj = k0 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (kj >= a.S || (a.causal && kj > qi)) s[c][i] = -INFINITY;
-          }
-          mr = fmaxf(mr, s[c][i]);
-        }
+        for (int i = 0; i < 16; ++i) mr = fmaxf(mr, s[c][i]);
       mr = fmaxf(mr, __shfl_xor(mr, 32));
       const float mx = fmaxf(m, mr * sl2);  // running max, log2 domain
       const float alpha = (m == -INFINITY) ? 0.f : ex2(m - mx);
@@ -487,10 +500,11 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
           s = mfma(rowf(Kt, 32 * c + r, t, h), qf[t], s);
           dp = mfma(rowf(Vt, 32 * c + r, t, h), df[t], dp);
         }
+        const int lim = edge ? qi - (k0 + 32 * c + 4 * h) : 1000000;  // (branch-free causal mask, as in the forward)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           float p = ex2(s[i] * sl2 - lse);
-          if (edge && k0 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p = 0.f;
+          p = ((i & 3) + 8 * (i >> 2) > lim) ? 0.f : p;
           dp[i] = p * (dp[i] - dl);
         }
 #pragma unroll

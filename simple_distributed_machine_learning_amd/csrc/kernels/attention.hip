@@ -18,8 +18,8 @@
 //   O^T += V^T P^T (A = V^T from a transposed V image in LDS, B = P straight from registers)
 //     -> O^T has the query on the lane too, so the rescale by exp(m_old - m_new) is a per-lane
 //        scalar multiply. LSE (log2 domain) is saved for the backward pass.
-// Backward: dK/dV kernel (workgroup = 128 keys; loops over query blocks) and dQ kernel
-// (workgroup = 128 queries; loops over key blocks) — no atomics, P recomputed from LSE.
+// Backward: dQ kernel (workgroup = 128 queries; loops over key blocks; also writes delta = rowsum(dO * O)), then
+// dK/dV kernel (workgroup = 128 keys; loops over query blocks) — no atomics, P recomputed from LSE.
 //
 // Tiles (64 rows x 64 d, bf16) live in LDS as ONE swizzled row-major image each, read two ways:
 //   * by rows with ds_read_b128 (operands whose MFMA k is d: S = K Q^T, dP = dO V^T, ...)
@@ -295,26 +295,6 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 }
 
 // ============================================================================================
-// backward, part 0: delta[q] = sum_d dO[q][d] * O[q][d]   (one thread per query row)
-__global__ void __launch_bounds__(256) attn_delta_kernel(AttnArgs a) {
-  const long rows = (long)a.B * a.H * a.S;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < rows; i += (long)gridDim.x * 256) {
-    const int qi = (int)(i % a.S);
-    const long bh = i / a.S;
-    const int b = (int)(bh / a.H), hh = (int)(bh % a.H);
-    const long off = (long)b * a.sob + (long)hh * a.soh + (long)qi * a.sos;
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      u16x8 x = *reinterpret_cast<const u16x8*>(a.o + off + 8 * c);
-      u16x8 y = *reinterpret_cast<const u16x8*>(a.dout + off + 8 * c);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s += bf2f(x[e]) * bf2f(y[e]);
-    }
-    a.delta[i] = s;
-  }
-}
-
 // backward, part 1: dK, dV. Workgroup = 128 keys (wave = 32 keys); loop over query blocks of 64.
 //   S  = Q K^T      (A = Q rows, B = K rows of this wave -> registers); C: key on lane
 //   P  = exp2(S*c - lse[q])                       (lse per register row, from LDS)
@@ -469,7 +449,19 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(AttnArgs a) {
     }
   }
   const float lse = qi < a.S ? a.lse[(long)bh * a.S + qi] : 0.f;
-  const float dl = qi < a.S ? a.delta[(long)bh * a.S + qi] : 0.f;
+  // delta[q] = sum_d dO[q][d] O[q][d] from the dO fragments already in registers (this lane: d = 16t + 8h + j) and
+  // the same elements of O, the two lane halves combined by one xor-32 exchange; written for the dK/dV kernel, which
+  // runs after this one (no separate delta pass over O and dO)
+  float dl = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    bf16x8 of = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (qi < a.S) of = *reinterpret_cast<const bf16x8*>(a.o + ooff + (long)qi * a.sos + 16 * t + 8 * h);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl = fmaf(bf2f((u16)df[t][j]), bf2f((u16)of[j]), dl);
+  }
+  dl += __shfl_xor(dl, 32);
+  if (h == 0 && qi < a.S) a.delta[(long)bh * a.S + qi] = dl;
   const float sl2 = a.scale * LOG2E;
   f32x16 dq[2] = {zero16(), zero16()};
   const int kend = a.causal ? min(a.S, qb * QB + QB) : a.S;
@@ -577,13 +569,10 @@ void attention_fwd_bf16(const AttnShape& s, hipStream_t stream) {
 
 void attention_bwd_bf16(const AttnShape& s, hipStream_t stream) {
   AttnArgs a = make_args(s);
-  const long rows = (long)s.B * s.H * s.S;
-  long db = (rows + 255) / 256;
-  if (db > 4096) db = 4096;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)db), dim3(256), 0, stream, a);
   const int nb = (s.S + QB - 1) / QB;
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(nb * s.B * s.H), dim3(256), 0, stream, a);
+  // dQ first: it computes delta = rowsum(dO * O) for its own queries and writes it for dK/dV
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nb * s.B * s.H), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(nb * s.B * s.H), dim3(256), 0, stream, a);
 }
 
 }  // namespace sdml

@@ -123,6 +123,47 @@ int grid_for(int64_t n8) {
   return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
 }
 
+// ---- batched 2-D transpose (the hand NT GEMM's W^T operands, once per optimizer step) ----------------------
+// dst[c][r] = src[r][c] for up to kTransposeBatchMax bf16 matrices in ONE launch: a ResNet-like per-weight loop of 48
+// small copies per GPT-2 step was 48 launches of ~5 us. 64 x 64 tiles through LDS (pitch 66 u16: the column reads
+// of the write phase spread over the banks), 16-B loads and stores (R, C multiples of 8).
+struct TrBatch {
+  const u16* src[kTransposeBatchMax];
+  u16* dst[kTransposeBatchMax];
+  int R[kTransposeBatchMax], C[kTransposeBatchMax], block0[kTransposeBatchMax + 1];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) transpose_batched_kernel(TrBatch b) {
+  __shared__ u16 tile[64][66];
+  const int blk = blockIdx.x;
+  int e = 0;
+  while (e + 1 < b.n && b.block0[e + 1] <= blk) ++e;
+  const int R = b.R[e], C = b.C[e];
+  const int tcn = (C + 63) / 64;
+  const int t = blk - b.block0[e], r0 = (t / tcn) * 64, c0 = (t % tcn) * 64;
+  const u16* src = b.src[e];
+  u16* dst = b.dst[e];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {  // 64 rows x 8 chunks of 8
+    const int idx = threadIdx.x + 256 * u, rr = idx >> 3, ch = idx & 7;
+    u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r0 + rr < R && c0 + 8 * ch < C) v = *reinterpret_cast<const u16x8*>(src + (size_t)(r0 + rr) * C + c0 + 8 * ch);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tile[rr][8 * ch + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {  // dst rows c0 + cc, 8 chunks of 8 source rows each
+    const int idx = threadIdx.x + 256 * u, cc = idx >> 3, ch = idx & 7;
+    if (c0 + cc >= C || r0 + 8 * ch >= R) continue;
+    u16x8 v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = tile[8 * ch + k][cc];
+    *reinterpret_cast<u16x8*>(dst + (size_t)(c0 + cc) * R + r0 + 8 * ch) = v;
+  }
+}
+
 }  // namespace
 
 void gelu_fwd_bf16(const void* x, void* y, int64_t n, hipStream_t stream) {
@@ -156,6 +197,24 @@ void embedding_bwd_bf16(const void* g, const int64_t* sorted_tok, const int64_t*
   if (gwte)
     hipLaunchKernelGGL(wte_bwd_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, reinterpret_cast<const u16*>(g),
                        sorted_tok, perm, reinterpret_cast<u16*>(gwte), n, C, V);
+}
+
+void transpose_batched_bf16(const void* const* src, void* const* dst, const int* R, const int* C, int n,
+                            hipStream_t stream) {
+  if (n <= 0) return;
+  TrBatch b{};
+  int blocks = 0;
+  for (int k = 0; k < n; ++k) {
+    b.src[k] = static_cast<const u16*>(src[k]);
+    b.dst[k] = static_cast<u16*>(dst[k]);
+    b.R[k] = R[k];
+    b.C[k] = C[k];
+    b.block0[k] = blocks;
+    blocks += ((R[k] + 63) / 64) * ((C[k] + 63) / 64);
+  }
+  b.block0[n] = blocks;
+  b.n = n;
+  hipLaunchKernelGGL(transpose_batched_kernel, dim3(blocks), dim3(256), 0, stream, b);
 }
 
 }  // namespace sdml

@@ -285,6 +285,10 @@ bool mlp_small_step(const void* x, bool x_u8, const int64_t* target, int B, floa
 // ---- GPT-2 elementwise / embedding kernels (gpt2_ops.hip) ------------------------------------
 // tanh-GELU (n % 8 == 0, 16-B aligned): y = gelu(x); gx = gy * gelu'(x) (gx may alias gy)
 void gelu_fwd_bf16(const void* x, void* y, int64_t n, hipStream_t stream);
+// dst[k] = src[k]^T ([R][C] -> [C][R], bf16, R and C multiples of 8) for n <= kTransposeBatchMax matrices, one launch
+constexpr int kTransposeBatchMax = 64;
+void transpose_batched_bf16(const void* const* src, void* const* dst, const int* R, const int* C, int n,
+                            hipStream_t stream);
 void gelu_bwd_bf16(const void* gy, const void* x, void* gx, int64_t n, hipStream_t stream);
 // out[r] = wte[tok[r]] + wpe[r % S]  (rows = B * S, C % 4 == 0)
 void embedding_fwd_bf16(const int64_t* tok, const void* wte, const void* wpe, void* out, int rows, int S, int C, int V,

@@ -563,6 +563,32 @@ std::tuple<torch::Tensor, torch::Tensor> conv3x3_weights_bf16(torch::Tensor w) {
 
 // the kernel layouts of several 3x3 weights in one launch, into caller-owned buffers (ops/conv.py keeps one pair per
 // weight across optimizer steps): fwd[k] [Co][9][C], dgrad[k] [C][9][Co] or None (forward layout only)
+void transpose_batched_bf16(std::vector<torch::Tensor> src, std::vector<torch::Tensor> dst) {
+  TORCH_CHECK(src.size() == dst.size(), "transpose_batched_bf16: list lengths");
+  const void* sp[sdml::kTransposeBatchMax];
+  void* dp[sdml::kTransposeBatchMax];
+  int R[sdml::kTransposeBatchMax], C[sdml::kTransposeBatchMax];
+  for (size_t b0 = 0; b0 < src.size(); b0 += sdml::kTransposeBatchMax) {
+    const int n = (int)std::min<size_t>(sdml::kTransposeBatchMax, src.size() - b0);
+    for (int k = 0; k < n; ++k) {
+      const torch::Tensor& s = src[b0 + k];
+      const torch::Tensor& d = dst[b0 + k];
+      TORCH_CHECK(s.is_cuda() && s.scalar_type() == torch::kBFloat16 && s.is_contiguous() && s.dim() == 2,
+                  "transpose_batched_bf16: src must be a contiguous 2-D bf16 CUDA tensor");
+      TORCH_CHECK(d.is_cuda() && d.scalar_type() == torch::kBFloat16 && d.is_contiguous() && d.dim() == 2 &&
+                      d.size(0) == s.size(1) && d.size(1) == s.size(0) && d.device() == s.device(),
+                  "transpose_batched_bf16: dst must be a contiguous [C][R] bf16 tensor on the same device");
+      TORCH_CHECK(s.size(0) % 8 == 0 && s.size(1) % 8 == 0 && s.size(0) < (1 << 30) && s.size(1) < (1 << 30),
+                  "transpose_batched_bf16: R and C must be multiples of 8");
+      sp[k] = s.data_ptr();
+      dp[k] = d.data_ptr();
+      R[k] = (int)s.size(0);
+      C[k] = (int)s.size(1);
+    }
+    sdml::transpose_batched_bf16(sp, dp, R, C, n, cur_stream());
+  }
+}
+
 void conv3x3_weights_batched_bf16(std::vector<torch::Tensor> ws, std::vector<torch::Tensor> fwd,
                                   std::vector<c10::optional<torch::Tensor>> dgrad) {
   TORCH_CHECK(ws.size() == fwd.size() && ws.size() == dgrad.size(), "conv3x3_weights_batched_bf16: list lengths");
@@ -1859,6 +1885,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bf16_supported", &wgrad_bf16_supported_op, "shape check for wgrad_bf16_ (contiguous operands)");
   m.def("conv3x3_weight_bf16", &conv3x3_weight_bf16, "3x3 conv weight -> kernel layout (forward / dgrad)");
   m.def("conv3x3_weights_bf16", &conv3x3_weights_bf16, "3x3 conv weight -> (forward, dgrad) kernel layouts");
+  m.def("transpose_batched_bf16", &transpose_batched_bf16,
+        "dst[k] = src[k]^T for a list of contiguous 2-D bf16 matrices (R, C multiples of 8), one launch");
   m.def("conv3x3_weights_batched_bf16", &conv3x3_weights_batched_bf16,
         "several 3x3 conv weights -> their kernel layouts in caller-owned buffers, one launch");
   m.def("conv3x3_fwd_bf16", &conv3x3_fwd_bf16, "3x3 stride-1 pad-1 conv, channels-last bf16 (implicit GEMM)",

@@ -52,6 +52,15 @@ def _hand_ok(x2, w) -> bool:
                 and k.gemm_bf16_supported(M, Kd, N, N, N, False))
 
 
+# Every weight whose W^T the hand GEMMs asked for keeps one transposed buffer across optimizer steps (_WT_KNOWN: id ->
+# (weakref, buffer)). The first W^T request after an optimizer step re-derives it for ALL live known weights in one
+# launch (transpose_batched_bf16): per weight it was one copy launch of ~5 us, 48 per GPT-2 step. Reusing the buffers is
+# safe as for the conv layouts (ops/conv.py _KNOWN): a step's backward reads them before the optimizer step that bumps
+# WEIGHT_GEN, and the next step's backward re-derives them after it.
+_WT_KNOWN = {}
+_WT_BATCH = os.environ.get("SDML_WT_BATCH", "1") != "0"  # (A/B: 0 = one transpose copy per weight)
+
+
 def _w_t(w):
     """w^T, contiguous, cached for the optimizer step (not while a hipGraph is being captured)."""
     from .conv import WEIGHT_GEN, _cache_get, _cache_put
@@ -62,9 +71,36 @@ def _w_t(w):
     hit = _cache_get(_WT, w)
     if hit is not None and hit[0] == key:
         return hit[1]
-    wt = w.t().contiguous()
-    _cache_put(_WT, w, (key, wt))
-    return wt
+    if not (_WT_BATCH and w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous()
+            and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0):
+        wt = w.t().contiguous()
+        _cache_put(_WT, w, (key, wt))
+        return wt
+    import weakref
+
+    kn = _WT_KNOWN.get(id(w))
+    if kn is None or kn[0]() is not w:
+        k = id(w)
+
+        def _gone(r, k=k):
+            if _WT_KNOWN.get(k, (None,))[0] is r:
+                _WT_KNOWN.pop(k, None)
+
+        _WT_KNOWN[k] = (weakref.ref(w, _gone), torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device))
+    todo = []  # this weight and every other live known one whose W^T is stale
+    for ref, buf in list(_WT_KNOWN.values()):
+        ww = ref()
+        if ww is None or ww.device != w.device or not ww.is_contiguous() or tuple(buf.shape) != tuple(ww.shape[::-1]):
+            continue
+        kk = (ww.data_ptr(), ww._version, WEIGHT_GEN[0], tuple(ww.shape))
+        h = _cache_get(_WT, ww)
+        if h is not None and h[0] == kk:
+            continue
+        todo.append((ww, buf, kk))
+    kernels().transpose_batched_bf16([t[0] for t in todo], [t[1] for t in todo])
+    for ww, buf, kk in todo:
+        _cache_put(_WT, ww, (kk, buf))
+    return _cache_get(_WT, w)[1]
 
 
 class _LinearFn(torch.autograd.Function):

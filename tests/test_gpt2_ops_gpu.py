@@ -242,3 +242,36 @@ def test_gemm_bf16_transposed_accumulators(M, N, Kd):
             torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * float(a.float().abs().max()))
     for a, b in zip(outs[(0, 1)], outs[(1, 1)]):
         assert torch.equal(a, b)
+
+
+def test_transpose_batched_bf16():
+    """transpose_batched_bf16: the hand GEMMs' W^T operands, every stale weight in one launch - exact transposes for
+    shapes with partial 64 x 64 tiles, across more matrices than one launch descriptor holds."""
+    g = torch.Generator(device="cpu").manual_seed(11)
+    shapes = [(2304, 768), (768, 768), (776, 200), (8, 8), (3072, 768), (64, 136)] * 12  # 72 > kTransposeBatchMax
+    src = [torch.randn(r, c, generator=g).to(DEV, torch.bfloat16) for r, c in shapes]
+    dst = [torch.empty(c, r, device=DEV, dtype=torch.bfloat16) for r, c in shapes]
+    K.transpose_batched_bf16(src, dst)
+    torch.cuda.synchronize()
+    for s_, d_ in zip(src, dst):
+        assert torch.equal(d_, s_.t())
+
+
+def test_hand_linear_wt_cache_batches_and_refreshes():
+    """ops.linear._w_t: after a weight generation bump every known weight's W^T is re-derived (one batched launch) and
+    equals the new transpose."""
+    from simple_distributed_machine_learning_amd.ops import conv as conv_ops
+    from simple_distributed_machine_learning_amd.ops import linear as lin
+
+    ws = [torch.randn(r, c, device=DEV).to(torch.bfloat16) for r, c in [(2304, 768), (768, 3072), (768, 768)]]
+    for w in ws:
+        assert torch.equal(lin._w_t(w), w.t())
+    conv_ops.bump_weight_generation()
+    with torch.no_grad():
+        for w in ws:
+            w.mul_(2)  # (bumps the version too)
+    t0 = lin._w_t(ws[0])
+    assert torch.equal(t0, ws[0].t())
+    for w in ws[1:]:  # refreshed by the same batched launch: cache hits now
+        hit = conv_ops._cache_get(lin._WT, w)
+        assert hit is not None and torch.equal(hit[1], w.t())

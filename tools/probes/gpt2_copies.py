@@ -1,0 +1,32 @@
+"""Where the GPT-2 step's device-to-device copies come from (torch.profiler, aten::copy_ / aten::cat call stacks)."""
+import sys
+import os
+
+import torch
+
+sys.path.insert(0, os.getcwd())
+from simple_distributed_machine_learning_amd.data import SyntheticTokens  # noqa: E402
+from simple_distributed_machine_learning_amd.models import get_model_spec  # noqa: E402
+from simple_distributed_machine_learning_amd.parallel import PipelineEngine, init_mesh  # noqa: E402
+
+mesh = init_mesh(pp=2, schedule_kind="1f1b", rank=0, world_size=1)
+spec = get_model_spec("gpt2", 2, seq_len=1024)
+eng = PipelineEngine(spec, mesh, schedule_kind="1f1b", num_microbatches=1, lr=0.01, momentum=0.5, seed=1)
+B = 16
+ds = SyntheticTokens(B * 2, 1024, 50257, seed=5, device=mesh.device)
+for i in range(3):
+    eng.run(ds, (i % 2) * B, B, train=True, global_batch=B)
+torch.cuda.synchronize()
+from torch.profiler import ProfilerActivity, profile  # noqa: E402
+
+with profile(activities=[ProfilerActivity.CPU], with_stack=True, record_shapes=True) as prof:
+    eng.run(ds, 0, B, train=True, global_batch=B)
+    torch.cuda.synchronize()
+ka = prof.key_averages(group_by_stack_n=6)
+rows = [e for e in ka if e.key in ("aten::copy_", "aten::cat", "aten::contiguous", "aten::clone", "aten::to",
+                                   "aten::_to_copy", "aten::add", "aten::add_", "aten::zero_", "aten::fill_")]
+rows.sort(key=lambda e: -e.count)
+for e in rows[:25]:
+    print(e.key, e.count, e.input_shapes[:3] if e.input_shapes else "")
+    for fr in (e.stack or [])[:6]:
+        print("    ", fr)

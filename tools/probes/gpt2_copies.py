@@ -22,11 +22,23 @@ from torch.profiler import ProfilerActivity, profile  # noqa: E402
 with profile(activities=[ProfilerActivity.CPU], with_stack=True, record_shapes=True) as prof:
     eng.run(ds, 0, B, train=True, global_batch=B)
     torch.cuda.synchronize()
-ka = prof.key_averages(group_by_stack_n=6)
+ka = prof.key_averages(group_by_input_shape=True)
 rows = [e for e in ka if e.key in ("aten::copy_", "aten::cat", "aten::contiguous", "aten::clone", "aten::to",
-                                   "aten::_to_copy", "aten::add", "aten::add_", "aten::zero_", "aten::fill_")]
+                                   "aten::_to_copy", "aten::add", "aten::add_", "aten::zero_", "aten::fill_",
+                                   "aten::reshape", "aten::empty_like")]
 rows.sort(key=lambda e: -e.count)
-for e in rows[:25]:
-    print(e.key, e.count, e.input_shapes[:3] if e.input_shapes else "")
-    for fr in (e.stack or [])[:6]:
-        print("    ", fr)
+for e in rows[:30]:
+    print(e.key, e.count, e.input_shapes)
+# who calls copy_: the parents in the event tree
+import collections
+par = collections.Counter()
+for ev in prof.events():
+    if ev.name == "aten::copy_":
+        p = ev.cpu_parent
+        chain = []
+        while p is not None and len(chain) < 4:
+            chain.append(p.name)
+            p = p.cpu_parent
+        par[" <- ".join(chain)] += 1
+for k, v in par.most_common(15):
+    print(v, k)

@@ -230,6 +230,8 @@ class PipelineEngine:
         self.fast_steps = {"mlp_small": 0, "cnn": 0}  # steps that ran the one/two-launch paths (tests)
         self._small_args = None
         self._cnn_args = None
+        self._fuse_ok = {}  # _can_fuse_head memo
+        self._wave_bufs = {}  # fused waves' persistent (ReLU bits, gradient) buffers
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
 
@@ -613,9 +615,10 @@ class PipelineEngine:
             if x.dtype == torch.uint8 and not s0.accepts_u8_pixels:
                 x = pixels_to_float(x)
             L = P[w][me][me]
-            if fuse_fh and L > 0 and s0.can_fuse_head(s1, x[:L]):
-                mask = torch.empty((bw, s0.layers()[0].out_features // 32), dtype=torch.int32, device=dev)
-                G = self.bufs.get(("grad_own", w), (bw,) + gshape, gdt)
+            if fuse_fh and L > 0 and self._can_fuse_head(s0, s1, x[:L]):
+                # persistent per-wave buffers (stream-ordered reuse: this step's weight gradient consumes them before
+                # the next step's forward rewrites them): no allocator / pool calls ahead of the step's first launch
+                mask, G = self._fused_wave_bufs(w, bw, s0.layers()[0].out_features // 32, gshape, gdt)
                 h = None
                 if L < bw:  # the rows whose stage 1 runs on peers: plain forward, h is sent
                     with tm.span("fwd", 0):
@@ -810,6 +813,22 @@ class PipelineEngine:
             stats.zero_()
         self.last_timing = tm.result()
         return StepResult(stats[0], stats[1], count, time.perf_counter() - t0)
+
+    def _can_fuse_head(self, s0, s1, x) -> bool:
+        """s0.can_fuse_head(s1, x), memoised on what it depends on (stages, shape, strides, dtype, 16-B alignment)."""
+        key = (id(s0), id(s1), tuple(x.shape), x.stride(), x.dtype, x.data_ptr() % 16, s0.plane_cache is not None)
+        hit = self._fuse_ok.get(key)
+        if hit is None:
+            hit = self._fuse_ok[key] = bool(s0.can_fuse_head(s1, x))
+        return hit
+
+    def _fused_wave_bufs(self, w, bw, nw, gshape, gdt):
+        key = (w, bw, nw, tuple(gshape), gdt)
+        hit = self._wave_bufs.get(key)
+        if hit is None:
+            mask = torch.empty((bw, nw), dtype=torch.int32, device=self.device)
+            hit = self._wave_bufs[key] = (mask, self.bufs.get(("grad_own", w), (bw,) + tuple(gshape), gdt))
+        return hit
 
     def _planned_dp_spans(self):
         """The split all-reduce spans every replica issues this step, or None. Only rank-independent facts decide

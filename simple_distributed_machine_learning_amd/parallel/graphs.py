@@ -142,7 +142,9 @@ class GraphedStep:
         self._relies_on_planes = bool(self._plane_caches()) and self._caches_current()
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(eng.device)
-        with torch.cuda.graph(g, pool=pool, stream=self.stream):
+        # thread_local: only this thread's unsafe API calls invalidate the capture - not the RCCL process group's
+        # watchdog thread, which polls the events of earlier (eager) collectives while a step is being captured
+        with torch.cuda.graph(g, pool=pool, stream=self.stream, capture_error_mode="thread_local"):
             res = eng.run(win, start, batch_size, train=True, global_batch=global_batch)
         # whether the captured step keeps the weight planes current (the one-launch small-batch step
         # does not write them: its replays must leave the caches invalid, as the eager step does)

@@ -282,6 +282,13 @@ def main():
 
     for i in range(a.warmup):
         step(i)
+    if graphed is not None and world > 1:
+        # every rank replays or none does (a capture that failed on one rank leaves that rank eager; the collective
+        # sequence would still match, but the timed steps should run one code path everywhere)
+        ok = torch.tensor([0.0 if graphed.disabled else 1.0], device=dev)
+        engine.transport.all_reduce(ok, channel="world", op=dist.ReduceOp.MIN, async_op=False)
+        if float(ok.item()) < 1.0:
+            graphed.disabled = True
     sync()
     if engine.transport is not None:
         engine.transport.reset_counters()

@@ -819,6 +819,8 @@ class PipelineEngine:
         key = (id(s0), id(s1), tuple(x.shape), x.stride(), x.dtype, x.data_ptr() % 16, s0.plane_cache is not None)
         hit = self._fuse_ok.get(key)
         if hit is None:
+            if len(self._fuse_ok) > 64:  # (a stream of odd shapes must not grow it without bound)
+                self._fuse_ok.clear()
             hit = self._fuse_ok[key] = bool(s0.can_fuse_head(s1, x))
         return hit
 
@@ -826,6 +828,8 @@ class PipelineEngine:
         key = (w, bw, nw, tuple(gshape), gdt)
         hit = self._wave_bufs.get(key)
         if hit is None:
+            if len(self._wave_bufs) > 16:  # (ragged batches: keep a bounded set; a dropped pair is freed by the allocator
+                self._wave_bufs.clear()  # once the stream no longer uses it)
             mask = torch.empty((bw, nw), dtype=torch.int32, device=self.device)
             hit = self._wave_bufs[key] = (mask, self.bufs.get(("grad_own", w), (bw,) + tuple(gshape), gdt))
         return hit

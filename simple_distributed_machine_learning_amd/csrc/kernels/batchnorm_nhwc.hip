@@ -150,6 +150,24 @@ __device__ __forceinline__ void wave_sum2(const float* __restrict__ part, int nb
   }
 }
 
+// the 4 waves of a block split channel c's partials into 4 contiguous quarters (each summed as wave_sum2 does), the
+// quarters added in order: a quarter of the dependent load rounds per wave (the conv epilogue writes ~1.5K partial
+// rows, 6 rounds for one wave). sum4 = ((q0 + q1) + q2) + q3 in fp64.
+__device__ __forceinline__ void block_sum2(const float* __restrict__ part, int nblk, int C, int c, double& s1,
+                                           double& s2, double (*red)[2]) {
+  const int w = threadIdx.x >> 6;
+  const int q = (nblk + 3) / 4, b0 = min(nblk, w * q), b1 = min(nblk, b0 + q);
+  double a1, a2;
+  wave_sum2(part + (size_t)b0 * 2 * C, b1 - b0, C, c, a1, a2);
+  if ((threadIdx.x & 63) == 0) {
+    red[w][0] = a1;
+    red[w][1] = a2;
+  }
+  __syncthreads();
+  s1 = ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0];
+  s2 = ((red[0][1] + red[1][1]) + red[2][1]) + red[3][1];
+}
+
 __global__ void __launch_bounds__(BT) bn_fwd_finalize_kernel(const float* __restrict__ part, int nblk, int C, int M,
                                                              float eps, float momentum, const u16* __restrict__ gamma,
                                                              const u16* __restrict__ beta, u16* __restrict__ rmean,
@@ -157,11 +175,11 @@ __global__ void __launch_bounds__(BT) bn_fwd_finalize_kernel(const float* __rest
                                                              float* __restrict__ rstd, float* __restrict__ scale,
                                                              float* __restrict__ shift, int64_t* __restrict__ nbt) {
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) ++*nbt;  // BatchNorm2d.num_batches_tracked (one launch less)
-  const int c = blockIdx.x * (BT / 64) + (threadIdx.x >> 6);
-  if (c >= C) return;
+  __shared__ double red[BT / 64][2];
+  const int c = blockIdx.x;  // one channel per block, its partials over the block's 4 waves
   double s1, s2;
-  wave_sum2(part, nblk, C, c, s1, s2);
-  if ((threadIdx.x & 63) != 0) return;
+  block_sum2(part, nblk, C, c, s1, s2, red);
+  if (threadIdx.x != 0) return;
   const double mu = s1 / M;
   double var = s2 / M - mu * mu;
   if (var < 0.0) var = 0.0;
@@ -326,7 +344,7 @@ void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const v
     hipLaunchKernelGGL(bn_partial_kernel<false>, dim3(nblk), dim3(BT), 0, stream, static_cast<const u16*>(x), nullptr,
                        nullptr, nullptr, nullptr, nullptr, nullptr, M, C, rpb, 0, workspace);
   }
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + BT / 64 - 1) / (BT / 64)), dim3(BT), 0, stream, part, nblk, C, M, eps,
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(C), dim3(BT), 0, stream, part, nblk, C, M, eps,
                      momentum, static_cast<const u16*>(gamma), static_cast<const u16*>(beta), static_cast<u16*>(rmean),
                      static_cast<u16*>(rvar), mean, rstd, scale, shift, num_batches_tracked);
   const int64_t n8 = (int64_t)M * C / 8;

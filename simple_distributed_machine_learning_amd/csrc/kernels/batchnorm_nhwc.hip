@@ -236,11 +236,11 @@ __global__ void __launch_bounds__(BT) bn_bwd_finalize_kernel(const float* __rest
                                                              const float* __restrict__ rstd,
                                                              const u16* __restrict__ gamma, u16* __restrict__ ggamma,
                                                              u16* __restrict__ gbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * (BT / 64) + (threadIdx.x >> 6);
-  if (c >= C) return;
+  __shared__ double red[BT / 64][2];
+  const int c = blockIdx.x;  // one channel per block (block_sum2)
   double s1, s2;
-  wave_sum2(part, nblk, C, c, s1, s2);
-  if ((threadIdx.x & 63) != 0) return;
+  block_sum2(part, nblk, C, c, s1, s2, red);
+  if (threadIdx.x != 0) return;
   const float a = bf2f(gamma[c]) * rstd[c];
   coef[c] = a;
   coef[C + c] = (float)(s1 / M);
@@ -364,7 +364,7 @@ void bn_nhwc_bwd_bf16(const void* x, const void* dy, const void* y, const float*
   hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(nblk), dim3(BT), 0, stream, static_cast<const u16*>(x),
                      static_cast<const u16*>(dy), static_cast<const u16*>(y), mean, rstd, gp, bp, M, C, rpb, rmode,
                      part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + BT / 64 - 1) / (BT / 64)), dim3(BT), 0, stream, part, nblk, C, M,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(BT), 0, stream, part, nblk, C, M,
                      rstd, gp, static_cast<u16*>(ggamma), static_cast<u16*>(gbeta), coef);
   const int64_t n8 = (int64_t)M * C / 8;
   const dim3 g(elem_blocks(n8, apply_threads(C))), b(apply_threads(C));

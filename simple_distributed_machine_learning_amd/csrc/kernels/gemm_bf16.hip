@@ -25,6 +25,8 @@
 //   EPI_BIAS        C = bf16(acc + b)
 //   EPI_BIAS_GELU   U = bf16(acc + b) -> aux, C = bf16(gelu(U))            (exactly the unfused pair)
 //   EPI_DGELU       C = bf16(gelu'(U) * bf16(acc)), U read from aux       (exactly the unfused pair)
+//   EPI_BIAS_GELU_SAVE_GRAD / EPI_MUL_GRAD: the same pair with bf16(gelu'(U)) in aux instead of U (the forward
+//     already holds the sigmoid; the backward epilogue is then one multiply, C = bf16(aux * bf16(acc)))
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 
@@ -61,6 +63,7 @@ struct GP {
   int M, N, K, lda, ldb, ldc, ldaux;
   int tiles_m, tiles_n;
   int ntstore;  // SDML_GEMM_NT_STORE=1: nontemporal epilogue stores (A/B)
+  int gsave;    // EPI_BIAS_GELU: aux = bf16(gelu'(U)); EPI_DGELU: aux holds it (EPI_*_GRAD host values)
   int nostore;  // timing probe (SDML_GEMM_BF16_NOSTORE=1): the epilogue runs but skips its HBM stores
 };
 
@@ -175,14 +178,31 @@ __device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&ac
     u16x8 o = v;
     if constexpr (EPI == EPI_BIAS_GELU) {
       u16x8* ap = reinterpret_cast<u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
-      if (p.ntstore) __builtin_nontemporal_store(v, ap);
-      else *ap = v;
+      if (p.gsave) {
+        u16x8 d;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_f(bf2f(v[e])));
+        for (int e = 0; e < 8; ++e) {
+          const float x = bf2f(v[e]), sg = gelu_sig(x);
+          o[e] = f2bf(x * sg);  // gelu_f's bits
+          d[e] = f2bf(gelu_grad_f(1.f, x));
+        }
+        if (p.ntstore) __builtin_nontemporal_store(d, ap);
+        else *ap = d;
+      } else {
+        if (p.ntstore) __builtin_nontemporal_store(v, ap);
+        else *ap = v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_f(bf2f(v[e])));
+      }
     } else if constexpr (EPI == EPI_DGELU) {
       const u16x8 u = *reinterpret_cast<const u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
+      if (p.gsave) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_grad_f(bf2f(v[e]), bf2f(u[e])));
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(u[e]) * bf2f(v[e]));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_grad_f(bf2f(v[e]), bf2f(u[e])));
+      }
     }
     u16x8* cp = reinterpret_cast<u16x8*>(p.C + (size_t)grow * p.ldc + gcol);
     if (p.ntstore) __builtin_nontemporal_store(o, cp);
@@ -605,6 +625,9 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
   p.C = static_cast<u16*>(C);
   p.bias = static_cast<const u16*>(bias);
   p.aux = static_cast<u16*>(aux);
+  p.gsave = epi == EPI_BIAS_GELU_SAVE_GRAD || epi == EPI_MUL_GRAD;
+  if (epi == EPI_BIAS_GELU_SAVE_GRAD) epi = EPI_BIAS_GELU;
+  if (epi == EPI_MUL_GRAD) epi = EPI_DGELU;
   p.M = M;
   p.N = N;
   p.K = K;

@@ -52,6 +52,8 @@ enum GemmEpi : int {
   EPI_ATOMIC = 4,         // atomicAdd(C, acc)           (split-K capable)
   EPI_BIAS_GELU = 5,      // gemm_bf16 only: U = acc + bias -> aux, C = gelu(U)
   EPI_DGELU = 6,          // gemm_bf16 only: C = acc * gelu'(U), U read from aux
+  EPI_BIAS_GELU_SAVE_GRAD = 7,  // gemm_bf16 only: C = gelu(acc + bias), aux = gelu'(acc + bias)
+  EPI_MUL_GRAD = 8,             // gemm_bf16 only: C = acc * aux (aux from EPI_BIAS_GELU_SAVE_GRAD)
 };
 
 struct GemmArgs {

@@ -1376,7 +1376,7 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> gemm_bf16_op(torch::Tens
   auto C = torch::empty({M, N}, A.options());
   c10::optional<torch::Tensor> u;
   const void* bp = nullptr;
-  if (epi == sdml::EPI_BIAS || epi == sdml::EPI_BIAS_GELU) {
+  if (epi == sdml::EPI_BIAS || epi == sdml::EPI_BIAS_GELU || epi == sdml::EPI_BIAS_GELU_SAVE_GRAD) {
     TORCH_CHECK(bias.has_value() && bias->defined(), "gemm_bf16: bias required");
     check_bf16_cuda(*bias, "bias");
     TORCH_CHECK(bias->numel() == N, "gemm_bf16: bias shape");
@@ -1384,10 +1384,10 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> gemm_bf16_op(torch::Tens
   }
   void* ap = nullptr;
   int64_t ldaux = N;
-  if (epi == sdml::EPI_BIAS_GELU) {
+  if (epi == sdml::EPI_BIAS_GELU || epi == sdml::EPI_BIAS_GELU_SAVE_GRAD) {
     u = torch::empty({M, N}, A.options());
     ap = u->data_ptr();
-  } else if (epi == sdml::EPI_DGELU) {
+  } else if (epi == sdml::EPI_DGELU || epi == sdml::EPI_MUL_GRAD) {
     TORCH_CHECK(aux.has_value() && aux->defined(), "gemm_bf16: pre-activation required");
     check_bf16_cuda(*aux, "aux");
     TORCH_CHECK(aux->numel() == M * N, "gemm_bf16: pre-activation shape");

@@ -157,19 +157,25 @@ def _param_grads(g2, x2, w, b, need_w: bool, need_b: bool):
 
 
 EPI_BIAS_GELU, EPI_DGELU = 5, 6  # csrc/kernels/kernels.h GemmEpi
+EPI_BIAS_GELU_SAVE_GRAD, EPI_MUL_GRAD = 7, 8
+# SDML_GELU_SAVE=grad (default): the c_fc forward saves bf16(gelu'(U)) instead of U, so the c_proj input-gradient
+# epilogue is one multiply (its tanh moves into the forward epilogue, which already evaluates the sigmoid);
+# "u" keeps U and evaluates gelu'(U) in the backward (exactly the unfused GELU kernels' bits)
+_GELU_EPI = ((EPI_BIAS_GELU_SAVE_GRAD, EPI_MUL_GRAD) if os.environ.get("SDML_GELU_SAVE", "grad") == "grad"
+             else (EPI_BIAS_GELU, EPI_DGELU))
 
 
 class _MLPFn(torch.autograd.Function):
     """GPT-2's MLP, y = c_proj(gelu(c_fc(x))), with the activation fused into the GEMMs on both sides
-    (gemm_bf16.hip): the c_fc forward writes the pre-activation U and gelu(U) from its epilogue, and the
-    c_proj input-gradient GEMM multiplies by gelu'(U) in its epilogue - no standalone GELU passes over
+    (gemm_bf16.hip): the c_fc forward writes gelu(U) and gelu'(U) (or U, SDML_GELU_SAVE=u) from its epilogue, and
+    the c_proj input-gradient GEMM multiplies by gelu'(U) in its epilogue - no standalone GELU passes over
     the [tokens, 3072] activations. The remaining GEMMs (c_proj forward, c_fc input gradient) stay on the
     library path, which is faster at these shapes (tools/bench_gemm_bf16.py); weight gradients as Linear."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2):
         x2 = x.reshape(-1, x.shape[-1])
-        a, u = kernels().gemm_bf16(x2, w1, b1, False, EPI_BIAS_GELU)
+        a, u = kernels().gemm_bf16(x2, w1, b1, False, _GELU_EPI[0])
         y = kernels().gemm_bf16(a, w2, b2, False, EPI_BIAS)[0] if _HAND else torch.addmm(b2, a, w2.t())
         ctx.save_for_backward(x2, u, a)
         ctx.params = (w1, b1, w2, b2)
@@ -182,9 +188,9 @@ class _MLPFn(torch.autograd.Function):
         w1, b1, w2, b2 = ctx.params
         g2 = gy.reshape(-1, gy.shape[-1])
         if _HAND and g2.stride(-1) == 1:  # NT against W2^T (the 256 x 128 two-workgroups-per-CU kernel)
-            du, _ = kernels().gemm_bf16(g2, _w_t(w2), None, False, EPI_DGELU, u)
+            du, _ = kernels().gemm_bf16(g2, _w_t(w2), None, False, _GELU_EPI[1], u)
         else:
-            du, _ = kernels().gemm_bf16(g2, w2, None, True, EPI_DGELU, u)  # (dY W2) * gelu'(U)
+            du, _ = kernels().gemm_bf16(g2, w2, None, True, _GELU_EPI[1], u)  # (dY W2) * gelu'(U)
         gw2, gb2 = _param_grads(g2, a, w2, b2, ctx.needs_input_grad[3], ctx.needs_input_grad[4])
         dx = None
         if ctx.needs_input_grad[0]:

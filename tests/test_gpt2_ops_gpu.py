@@ -122,6 +122,20 @@ def test_gemm_bf16_gelu_epilogues_match_unfused():
     du, _ = K.gemm_bf16(gy, w2, None, True, 6, u)
     da, _ = K.gemm_bf16(gy, w2, None, True, 0)
     assert torch.equal(du, K.gelu_bwd_bf16(da, u, False))
+    # the gelu'-saving pair (7, 8): the same activation bits; aux = bf16(gelu'(U)); dU = bf16(aux * bf16(dY W2))
+    ones = torch.ones_like(u)
+    for t2 in (0, 1):
+        K.set_knob("GEMM_BF16_T2", t2)
+        try:
+            y7, d7 = K.gemm_bf16(x, w, b, False, 7)
+        finally:
+            K.set_knob("GEMM_BF16_T2", 0)
+        assert torch.equal(y7, y)
+        assert torch.equal(d7, K.gelu_bwd_bf16(ones, u, False))
+    for b_kn, w2x in ((True, w2), (False, w2.t().contiguous())):
+        du8, _ = K.gemm_bf16(gy, w2x, None, b_kn, 8, d7)
+        assert torch.equal(du8, (d7.float() * da.float()).to(torch.bfloat16))
+    torch.testing.assert_close(du8.float(), K.gelu_bwd_bf16(da, u, False).float(), rtol=1.6e-2, atol=1e-2)
 
 
 def test_mlp_gelu_fused_matches_composed():

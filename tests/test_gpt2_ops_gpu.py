@@ -138,10 +138,15 @@ def test_gemm_bf16_gelu_epilogues_match_unfused():
     torch.testing.assert_close(du8.float(), K.gelu_bwd_bf16(da, u, False).float(), rtol=1.6e-2, atol=1e-2)
 
 
-def test_mlp_gelu_fused_matches_composed():
+@pytest.mark.parametrize("save", ["grad", "u"])
+def test_mlp_gelu_fused_matches_composed(save, monkeypatch):
     """GPT-2's MLP with the GELU fused into the GEMM epilogues (ops.linear._MLPFn) against
-    c_proj(gelu(c_fc(x))) composed from separate kernels: forward and every gradient."""
+    c_proj(gelu(c_fc(x))) composed from separate kernels: forward and every gradient; the forward saving
+    gelu'(U) (SDML_GELU_SAVE=grad, the default) or U."""
+    from simple_distributed_machine_learning_amd.ops import linear as L
     from simple_distributed_machine_learning_amd.ops.linear import _MLPFn, linear
+
+    monkeypatch.setattr(L, "_GELU_EPI", (7, 8) if save == "grad" else (5, 6))
 
     g = torch.Generator(device="cpu").manual_seed(9)
     T, C = 1024, 768

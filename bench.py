@@ -100,7 +100,10 @@ def parse():
     p.add_argument("--model", default="mlp")
     p.add_argument("--alternatives", default="auto", choices=["auto", "on", "off"],
                    help="after the timed steps, also time the reference's placement (pp2dp) for the JSON; "
-                        "auto: at N = 2 only (the reference's own world size)")
+                        "auto: at every even N (the reference's cut at 2, 4, 8 GPUs)")
+    p.add_argument("--link_probe", default="auto", choices=["auto", "on", "off"],
+                   help="N > 1: measure the all-reduce / all-to-all / pair exchange on the job's process group before "
+                        "choosing the placement, and feed the measured link model to it (parallel/linkprobe.py)")
     p.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                    help="replay each step from a HIP graph (parallel/graphs.py, one graph per cycled batch reading "
                         "the device-resident data in place, the gradient all-reduce inside); auto: on for the dp "
@@ -188,6 +191,38 @@ def _measure_pp2dp(a, n, rank, world, dev, steps=10, warmup=3):
             "predicted": plc.predict("pp2dp", n, a.batch_per_gpu)}
 
 
+def _replica_check(engine, mesh, dev, rank):
+    """After the timed steps: every replica of a stage must hold bit-identical parameters (the gradient all-reduce
+    keeps them so). Per rank, an exact integer checksum of each stage's flat parameters it holds (the fp32 bit
+    patterns summed as int64, plus a position-weighted sum); MIN and MAX over ranks must agree for every stage.
+    SDML_BENCH_PERTURB_RANK=k (tests only) flips one parameter bit on rank k first, so the check must fail."""
+    P = engine.P
+    big, small = 2 ** 62, -(2 ** 62)
+    lo = torch.full((2 * P,), big, dtype=torch.int64)
+    hi = torch.full((2 * P,), small, dtype=torch.int64)
+    perturb = os.environ.get("SDML_BENCH_PERTURB_RANK")
+    for s, mod in engine.stages.items():
+        flat = torch.cat([p.detach().reshape(-1).float() for p in mod.parameters()])
+        if perturb is not None and int(perturb) == rank:
+            flat = flat.clone()
+            flat[0] = torch.nextafter(flat[0], torch.tensor(float("inf"), device=flat.device))
+        bits = flat.contiguous().view(torch.int32).to(torch.int64).cpu()
+        w = torch.arange(1, bits.numel() + 1, dtype=torch.int64) % 65521
+        c = torch.stack([bits.sum(), (bits * w).sum()])
+        lo[2 * s:2 * s + 2] = c
+        hi[2 * s:2 * s + 2] = c
+    t_lo, t_hi = lo.to(dev), hi.to(dev)
+    if mesh.backend == "gloo":
+        t_lo, t_hi = lo, hi
+    dist.all_reduce(t_lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(t_hi, op=dist.ReduceOp.MAX)
+    lo, hi = t_lo.cpu(), t_hi.cpu()
+    held = [s for s in range(P) if int(lo[2 * s]) != big]
+    same = all(int(lo[2 * s + j]) == int(hi[2 * s + j]) for s in held for j in range(2))
+    return {"identical": bool(same), "stages_checked": held,
+            "checksums": {str(s): [int(lo[2 * s]), int(lo[2 * s + 1])] for s in held}}
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -201,12 +236,25 @@ def main():
         sys.exit(2)
     n = world
     place = a.placement
-    predicted = plc.table(n, a.batch_per_gpu)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    link_meas, link = None, plc.LinkModel()
+    if n > 1 and a.link_probe != "off":
+        # join the default process group first (init_mesh below reuses it) and measure the links the placements use
+        from simple_distributed_machine_learning_amd.parallel import linkprobe
+
+        m0 = init_mesh(pp=1, schedule_kind="rotate", timeout_s=900, rank=rank, world_size=world, p2p_channels=False)
+        pdev = m0.device if m0.backend == "nccl" else torch.device("cpu")
+        link_meas = linkprobe.measure(pdev, boundary_bytes=a.batch_per_gpu * (512 + 40))
+        link = linkprobe.link_model(link_meas)
+        link.allreduce_us = link_meas["allreduce_us"]
+    rccl_world = n > 1 and os.environ.get("SDML_TRANSPORT", "direct") == "direct" and torch.cuda.device_count() > 0
+    graph_dp = rccl_world and a.graph != "off" and not plc.dp_split_default()
+    predicted = plc.table(n, a.batch_per_gpu, link=link, graph_dp=graph_dp if n > 1 else None)
     phi = None
     if n == 1:
         place = "dp"
     elif place == "auto":
-        place, phi, _ = plc.choose(n, a.batch_per_gpu)
+        place, phi, _ = plc.choose(n, a.batch_per_gpu, link=link, graph_dp=graph_dp)
     if a.schedule is not None and n > 1:
         place = "pp2dp"
     if place == "pp2dp" and n % 2:
@@ -223,7 +271,7 @@ def main():
         if place == "dp":
             phi = 0.0
         elif place == "balanced":
-            phi = plc.balanced_fraction(n, a.batch_per_gpu)
+            phi = plc.balanced_fraction(n, a.batch_per_gpu, link)
         elif place == "rotate":
             phi = None
         if a.cross_fraction is not None:
@@ -231,7 +279,6 @@ def main():
         W = a.waves or (1 if (n == 1 or phi == 0) else 2)
         M = W * pp
         B = a.batch_per_gpu  # per owner shard
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     # rotate on a 2-stage model runs its boundary as all-to-all collectives: no p2p channels
     mesh = init_mesh(pp=pp, schedule_kind=kind, timeout_s=900, rank=rank, world_size=world,
                      p2p_channels=(kind != "rotate"))
@@ -263,14 +310,18 @@ def main():
     use_graph = dev.type == "cuda" and (a.graph == "on" or (
         a.graph == "auto" and world > 1 and place == "dp" and rccl and not engine.dp_split))
     graphed = None
+    nbatches = a.dataset_batches
     if use_graph:
+        # one graph per cycled batch, captured on its first visit (the first step runs eagerly): cycle over at most
+        # warmup - 1 batches so every capture happens during warm-up, none inside the timed region
+        nbatches = max(1, min(a.dataset_batches, a.warmup - 1))
         from simple_distributed_machine_learning_amd.parallel.graphs import GraphedStep
 
         graphed = GraphedStep(engine, allow_collectives=world > 1, direct_data=True,
                               max_direct=max(1, a.dataset_batches))
 
     def step(i):
-        start = (i % a.dataset_batches) * GB
+        start = (i % nbatches) * GB
         if graphed is not None:
             return graphed(ds, engine.local_start(start, B), B, global_batch=GB)
         return engine.run(ds, engine.local_start(start, B), B, train=True, global_batch=GB)
@@ -282,6 +333,7 @@ def main():
 
     for i in range(a.warmup):
         step(i)
+    graphs_before_timing = len(graphed.graphs) if graphed is not None else 0
     if graphed is not None and world > 1:
         # every rank replays or none does (a capture that failed on one rank leaves that rank eager; the collective
         # sequence would still match, but the timed steps should run one code path everywhere)
@@ -315,6 +367,7 @@ def main():
         engine.transport.all_reduce(sent, channel="world", async_op=False)
     el = float(t.item())
     cross_bytes = float(sent.item()) / a.steps
+    replicas = _replica_check(engine, mesh, dev, rank) if world > 1 else None
     loss = None
     if res is not None:
         l, c, cnt = engine.reduce_metrics(res)
@@ -322,7 +375,7 @@ def main():
     sps = GB * a.steps / el
     # the reference's own placement, measured next to the chosen one (after the timed region)
     alternatives = {}
-    want_alt = a.alternatives == "on" or (a.alternatives == "auto" and n == 2)
+    want_alt = a.alternatives == "on" or (a.alternatives == "auto" and n % 2 == 0)
     if want_alt and n > 1 and n % 2 == 0 and place != "pp2dp" and a.model == "mlp":
         try:
             alternatives["pp2dp"] = _measure_pp2dp(a, n, rank, world, dev)
@@ -360,13 +413,20 @@ def main():
                 "transport": engine.transport.name if engine.transport else None,
                 "world_size_seen": seen_world,
                 "backend": seen_backend,
-                "link_model": plc.model_dict(),
+                "link_model": plc.model_dict(link),
+                "link_model_assumed": plc.model_dict()["link"],
+                "link_measured": link_meas,
+                "replicas_identical": None if replicas is None else replicas["identical"],
+                "replica_check": replicas,
                 "predicted": predicted,
                 "measured_alternatives": alternatives,
                 "kernel_knobs": knobs,
                 "hip_graph": None if graphed is None else {"graphs": len(graphed.graphs), "replays": graphed.replays,
                                                            "eager_steps": graphed.eager_steps,
-                                                           "disabled": graphed.disabled},
+                                                           "disabled": graphed.disabled,
+                                                           "captures_in_timed_region":
+                                                               len(graphed.graphs) - graphs_before_timing,
+                                                           "dataset_batches_cycled": nbatches},
                 "microbatches": M,
                 "batch_per_gpu": a.batch_per_gpu,
                 "optimizer": "SGD lr=0.1 momentum=0.5",
@@ -386,6 +446,10 @@ def main():
     if world > 1:
         sync()
         dist.destroy_process_group()
+    if replicas is not None and not replicas["identical"]:
+        if rank == 0:
+            print("[bench] replicas diverged: " + json.dumps(replicas), file=sys.stderr)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -86,8 +86,7 @@ def _rel(text: str) -> str:
 
 def _compile(cmd_base, src: Path, include_dirs, tag: str) -> Path:
     BUILD_DIR.mkdir(parents=True, exist_ok=True)
-    key = hashlib.sha256((_rel(" ".join(cmd_base)) + _headers_hash(src, include_dirs)).encode()).hexdigest()[:16]
-    obj = BUILD_DIR / f"{tag}_{src.stem}_{key}.o"
+    obj = _obj_path(cmd_base, src, include_dirs, tag)
     if obj.exists():
         return obj
     cmd = list(cmd_base) + ["-c", str(src), "-o", str(obj) + ".tmp"]
@@ -106,27 +105,29 @@ def _link(cmd, out: Path):
     os.replace(tmp, out)
 
 
-def build_runtime(verbose: bool = False) -> Path:
-    srcs = sorted((CSRC / "runtime").glob("*.cpp"))
-    incs = [str(CSRC / "runtime"), str(CSRC / "common"), _pybind_include(), _python_include()]
-    base = [CXX, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"]
-    base += [f"-I{d}" for d in incs]
-    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
-        objs = list(ex.map(lambda s: _compile(base, s, incs, "rt"), srcs))
-    out = PKG_DIR / f"_runtime{EXT_SUFFIX}"
-    if _needs_link(out, objs):
-        _link([CXX, "-shared", "-fPIC"] + [str(o) for o in objs], out)
-        _write_stamp(out, objs)
-        if verbose:
-            print(f"[sdml build] linked {out.name}")
-    return out
+def _obj_path(cmd_base, src: Path, include_dirs, tag: str) -> Path:
+    key = hashlib.sha256((_rel(" ".join(cmd_base)) + _headers_hash(src, include_dirs)).encode()).hexdigest()[:16]
+    return BUILD_DIR / f"{tag}_{src.stem}_{key}.o"
 
 
-def build_kernels(verbose: bool = False) -> Path:
-    tinc, tlib = _torch_paths()
+# ---- build key: a content hash of every object a module links, embedded in the module at link time ----------------
+# The key is the hash of the sorted object names; each name already carries the hash of its compile command and of its
+# source with every quoted include (``_obj_path``), so the key changes with any source, header or flag edit.
+# ``_native`` computes the key the current tree WANTS (no compiler needed) and compares it with the marker string in
+# the .so file before importing it, so a module built from other sources is refused (or rebuilt) instead of loaded.
+KEY_MARKER = b"SDML_BUILD_KEY="
+
+
+def _plan(what: str):
+    """(compile command, source, include dirs, tag) of every object the module ``what`` links."""
+    if what == "runtime":
+        srcs = sorted((CSRC / "runtime").glob("*.cpp"))
+        incs = [str(CSRC / "runtime"), str(CSRC / "common"), _pybind_include(), _python_include()]
+        base = [CXX, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"]
+        base += [f"-I{d}" for d in incs]
+        return [(base, s, incs, "rt") for s in srcs]
+    tinc, _ = _torch_paths()
     kdir = CSRC / "kernels"
-    hip_srcs = sorted(kdir.glob("*.hip"))
-    bind_srcs = sorted(kdir.glob("*.cpp"))
     common = [str(kdir), str(CSRC / "common")]
     kflags = [HIPCC, "-O3", "-std=c++17", "-fPIC", f"--offload-arch={OFFLOAD_ARCH}",
               "-munsafe-fp-atomics", "-Wno-unused-result"] + [f"-I{d}" for d in common]
@@ -139,14 +140,69 @@ def build_kernels(verbose: bool = False) -> Path:
               "-Wno-unused-result", "-Wno-deprecated-declarations"] + exp
     binc = common + tinc + [_python_include(), "/opt/rocm/include"]
     bflags += [f"-I{d}" for d in binc]
-    jobs = []
+    return ([(kflags, s, common, "k") for s in sorted(kdir.glob("*.hip"))]
+            + [(bflags, s, binc, "b") for s in sorted(kdir.glob("*.cpp"))])
+
+
+def source_key(what: str) -> str:
+    """The build key the current sources and flags call for (``what`` = "runtime" | "kernels")."""
+    names = sorted(_obj_path(*job).name for job in _plan(what))
+    return hashlib.sha256("\n".join(names).encode()).hexdigest()[:24]
+
+
+def embedded_key(so_path) -> str | None:
+    """The key a built module carries (None: no marker, i.e. built before keys existed)."""
+    try:
+        data = Path(so_path).read_bytes()
+    except OSError:
+        return None
+    i = data.find(KEY_MARKER)
+    if i < 0:
+        return None
+    return data[i + len(KEY_MARKER):i + len(KEY_MARKER) + 24].decode("ascii", "replace")
+
+
+def _key_object(what: str, key: str) -> Path:
+    """A one-symbol object holding the marker string; linked into the module."""
+    BUILD_DIR.mkdir(parents=True, exist_ok=True)
+    obj = BUILD_DIR / f"key_{what}_{key}.o"
+    if obj.exists():
+        return obj
+    src = BUILD_DIR / f"key_{what}_{key}.c"
+    src.write_text('__attribute__((used, visibility("default"))) const char sdml_build_key[] = "'
+                   + KEY_MARKER.decode() + key + '";\n')
+    r = subprocess.run(["gcc", "-fPIC", "-c", str(src), "-o", str(obj) + ".tmp"], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: build key object\n{r.stdout}\n{r.stderr}")
+    os.replace(str(obj) + ".tmp", obj)
+    return obj
+
+
+def module_path(what: str) -> Path:
+    return PKG_DIR / f"_{what}{EXT_SUFFIX}"
+
+
+def build_runtime(verbose: bool = False) -> Path:
+    jobs = _plan("runtime")
     with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
-        for s in hip_srcs:
-            jobs.append(ex.submit(_compile, kflags, s, common, "k"))
-        for s in bind_srcs:
-            jobs.append(ex.submit(_compile, bflags, s, binc, "b"))
-        objs = [j.result() for j in jobs]
-    out = PKG_DIR / f"_kernels{EXT_SUFFIX}"
+        objs = list(ex.map(lambda j: _compile(*j), jobs))
+    objs.append(_key_object("runtime", source_key("runtime")))
+    out = module_path("runtime")
+    if _needs_link(out, objs):
+        _link([CXX, "-shared", "-fPIC"] + [str(o) for o in objs], out)
+        _write_stamp(out, objs)
+        if verbose:
+            print(f"[sdml build] linked {out.name}")
+    return out
+
+
+def build_kernels(verbose: bool = False) -> Path:
+    _, tlib = _torch_paths()
+    jobs = _plan("kernels")
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(lambda j: _compile(*j), jobs))
+    objs.append(_key_object("kernels", source_key("kernels")))
+    out = module_path("kernels")
     if _needs_link(out, objs):
         link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={OFFLOAD_ARCH}"] + [str(o) for o in objs]
         link += [f"-L{tlib}", f"-Wl,-rpath,{tlib}", "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python",

@@ -4,6 +4,12 @@ Policy: the C++ runtime is always required (it is built on CPU by ``__graft_entr
 The HIP kernel module is required whenever a CUDA (ROCm) device is used: GPU code paths call
 :func:`kernels` which raises loudly instead of silently falling back to PyTorch ops.  The CPU
 path (Gloo multi-process tests) uses PyTorch reference ops by design.
+
+Stale binaries: every module carries the content-hash build key it was linked from
+(``_build.source_key``). Before a module is imported its key is compared with the key the tree's
+current sources call for; a mismatch (a ``.so`` built from other sources, e.g. pushed from another
+checkout) triggers one in-tree rebuild, or, under ``SDML_NO_AUTOBUILD=1``, an error. The key of the
+loaded module is ``loaded_key(what)``; ``smoke()`` prints it.
 """
 from __future__ import annotations
 
@@ -15,6 +21,43 @@ _lock = threading.Lock()
 _rt = None
 _k = None
 _k_err = None
+
+
+_loaded_keys = {}
+
+
+class StaleModuleError(RuntimeError):
+    """A built module whose embedded build key does not match the current sources."""
+
+
+def check_key(so_path, want: str):
+    """Raise :class:`StaleModuleError` unless the module file at ``so_path`` carries ``want``."""
+    from . import _build
+
+    got = _build.embedded_key(so_path)
+    if got != want:
+        raise StaleModuleError(f"sdml: {so_path} was built from other sources (build key {got}, the tree wants "
+                               f"{want}); rebuild with `python -m {__package__}._build`")
+    return got
+
+
+def _fresh(what: str):
+    """Make sure the module file for ``what`` matches the tree (rebuild once if allowed), return its key."""
+    from . import _build
+
+    want = _build.source_key(what)
+    path = _build.module_path(what)
+    try:
+        return check_key(path, want)
+    except StaleModuleError:
+        if os.environ.get("SDML_NO_AUTOBUILD") == "1":
+            raise
+    _auto_build(what)
+    return check_key(path, want)
+
+
+def loaded_key(what: str):
+    return _loaded_keys.get(what)
 
 
 def _auto_build(what: str):
@@ -34,12 +77,9 @@ def runtime():
         return _rt
     with _lock:
         if _rt is None:
-            try:
-                _rt = importlib.import_module(f"{__package__}._runtime")
-            except ImportError:
-                _auto_build("runtime")
-                importlib.invalidate_caches()
-                _rt = importlib.import_module(f"{__package__}._runtime")
+            _loaded_keys["runtime"] = _fresh("runtime")
+            importlib.invalidate_caches()
+            _rt = importlib.import_module(f"{__package__}._runtime")
     return _rt
 
 
@@ -50,19 +90,15 @@ def kernels():
         return _k
     with _lock:
         if _k is None:
-            try:
+            try:  # the module must match the tree's sources: rebuild once (CPU container / dev box) or refuse
+                _loaded_keys["kernels"] = _fresh("kernels")
+                importlib.invalidate_caches()
                 _k = importlib.import_module(f"{__package__}._kernels")
-            except ImportError as e:  # try an in-tree build once (CPU container / dev box)
-                try:
-                    _auto_build("kernels")
-                    importlib.invalidate_caches()
-                    _k = importlib.import_module(f"{__package__}._kernels")
-                except Exception as e2:  # noqa: BLE001
-                    _k_err = e2
-                    raise RuntimeError(
-                        "sdml: HIP kernel extension '_kernels' is not available "
-                        f"({e}; build attempt: {e2}). Run `python -m "
-                        f"{__package__}._build kernels`.") from e2
+            except Exception as e:  # noqa: BLE001
+                _k_err = e
+                raise RuntimeError(
+                    "sdml: HIP kernel extension '_kernels' is not available "
+                    f"({type(e).__name__}: {e}). Run `python -m {__package__}._build kernels`.") from e
     return _k
 
 

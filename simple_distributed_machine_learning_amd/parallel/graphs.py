@@ -141,6 +141,9 @@ class GraphedStep:
         # are only valid while they stay current (see __call__)
         self._relies_on_planes = bool(self._plane_caches()) and self._caches_current()
         g = torch.cuda.CUDAGraph()
+        # from now on buffers the engine replaces stay alive: this graph replays into their addresses
+        eng.graph_retain = True
+        eng.bufs.retain = True
         torch.cuda.synchronize(eng.device)
         # thread_local: only this thread's unsafe API calls invalidate the capture - not the RCCL process group's
         # watchdog thread, which polls the events of earlier (eager) collectives while a step is being captured

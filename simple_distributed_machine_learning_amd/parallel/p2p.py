@@ -56,11 +56,18 @@ class BufferPool:
     at most once, and every consumer of a buffer is stream-ordered before the next step's producer
     (RCCL waits for the compute stream when a collective is enqueued), so reuse across steps is
     safe without host synchronisation. ``allocations`` counts real allocations (tests assert it
-    stops growing after the first step)."""
+    stops growing after the first step).
+
+    ``retain``: set once a HIP graph has been captured over these buffers (parallel/graphs.py). A graph
+    keeps raw addresses, not tensor references, so a buffer replaced by a larger one must stay alive
+    while a graph may replay into it: replaced buffers then move to ``_retired`` instead of going back
+    to the allocator."""
 
     def __init__(self, device: torch.device):
         self.device = device
         self._bufs: Dict[tuple, torch.Tensor] = {}
+        self._retired = []
+        self.retain = False
         self.allocations = 0
 
     def get(self, key: tuple, shape: Sequence[int], dtype: torch.dtype) -> torch.Tensor:
@@ -68,6 +75,8 @@ class BufferPool:
         n = math.prod(shape)
         buf = self._bufs.get(key)
         if buf is None or buf.dtype != dtype or buf.numel() < n:
+            if buf is not None and self.retain:
+                self._retired.append(buf)
             buf = torch.empty(max(n, 1), dtype=dtype, device=self.device)
             self._bufs[key] = buf
             self.allocations += 1

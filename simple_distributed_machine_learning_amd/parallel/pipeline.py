@@ -232,6 +232,10 @@ class PipelineEngine:
         self._cnn_args = None
         self._fuse_ok = {}  # _can_fuse_head memo
         self._wave_bufs = {}  # fused waves' persistent (ReLU bits, gradient) buffers
+        # set by GraphedStep once a graph is captured: evicted wave buffers then stay alive (a graph holds their
+        # addresses, not references), see _fused_wave_bufs and BufferPool.retain
+        self.graph_retain = False
+        self._wave_bufs_retired = []
         if self.kind == "rotate" and self.P == 2 and not self.use_alltoall and mesh.pp > 1 and not mesh.p2p_groups:
             raise ValueError("rotate with p2p transfers needs a mesh built with p2p_channels=True")
 
@@ -829,7 +833,9 @@ class PipelineEngine:
         hit = self._wave_bufs.get(key)
         if hit is None:
             if len(self._wave_bufs) > 16:  # (ragged batches: keep a bounded set; a dropped pair is freed by the allocator
-                self._wave_bufs.clear()  # once the stream no longer uses it)
+                if self.graph_retain:  # once the stream no longer uses it - unless a captured graph may still write it)
+                    self._wave_bufs_retired.extend(self._wave_bufs.values())
+                self._wave_bufs.clear()
             mask = torch.empty((bw, nw), dtype=torch.int32, device=self.device)
             hit = self._wave_bufs[key] = (mask, self.bufs.get(("grad_own", w), (bw,) + tuple(gshape), gdt))
         return hit

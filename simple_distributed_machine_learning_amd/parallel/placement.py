@@ -55,6 +55,8 @@ class LinkModel:
     collective_us: float = 12.0   # launch + handshake per collective
     exposed: float = 0.15         # fraction of the link time that cannot hide under compute
     link_budget: float = 0.75     # balanced: keep the busiest link busy at most this share of the step
+    # measured gradient all-reduce of the parameters (parallel/linkprobe.py); None: the ring formula below
+    allreduce_us: Optional[float] = None
 
 
 @dataclass
@@ -136,8 +138,9 @@ def predict(placement: str, n: int, batch_per_gpu: int, waves: int = 2, phi: Opt
         link_bytes = cross_bytes / max(1, n - 1)
         ncoll = 2 * waves if phi > 0 else 0
     link_us = link_bytes / (link.gbps * 1e3) + ncoll * link.collective_us
-    if n > 1:  # ring all-reduce of the gradients (2 (n-1)/n of the bytes per GPU, over 2 ring links)
-        ar_us = 2 * (n - 1) / n * comp.param_bytes / (2 * link.gbps * 1e3) + link.collective_us
+    if n > 1:  # ring all-reduce of the gradients (2 (n-1)/n of the bytes per GPU, over 2 ring links), or as measured
+        ar_us = (link.allreduce_us if link.allreduce_us is not None
+                 else 2 * (n - 1) / n * comp.param_bytes / (2 * link.gbps * 1e3) + link.collective_us)
         if dp_split and (placement == "dp" or (placement != "pp2dp" and phi == 0)):
             # split: two half collectives, range 0's under range 1's kernel
             half = (ar_us - link.collective_us) / 2 + link.collective_us
@@ -175,21 +178,25 @@ def balanced_fraction(n: int, batch_per_gpu: int, link: LinkModel = LinkModel(),
 
 
 def table(n: int, batch_per_gpu: int, waves: int = 2, link: LinkModel = LinkModel(),
-          comp: ComputeModel = ComputeModel()) -> Dict[str, Dict[str, float]]:
+          comp: ComputeModel = ComputeModel(), graph_dp: Optional[bool] = None) -> Dict[str, Dict[str, float]]:
+    """Predictions of every placement. ``graph_dp``: whether the caller replays the ``dp`` step from a HIP graph
+    (bench.py: RCCL transport at N > 1, graphs not off, no split); None: assume it does (predict's default)."""
     out = {}
     for p in ("balanced", "rotate", "dp", "pp2dp"):
         if p == "pp2dp" and (n % 2 or n == 1):
             continue
         phi = balanced_fraction(n, batch_per_gpu, link, comp, waves) if p == "balanced" else None
-        out[p] = predict(p, n, batch_per_gpu, waves, phi, link, comp)
+        graph = None if graph_dp is None else (bool(graph_dp) if p == "dp" else False)
+        out[p] = predict(p, n, batch_per_gpu, waves, phi, link, comp, graph=graph)
     return out
 
 
 def choose(n: int, batch_per_gpu: int, waves: int = 2, link: LinkModel = LinkModel(),
-           comp: ComputeModel = ComputeModel()) -> Tuple[str, float, Dict[str, Dict[str, float]]]:
+           comp: ComputeModel = ComputeModel(),
+           graph_dp: Optional[bool] = None) -> Tuple[str, float, Dict[str, Dict[str, float]]]:
     """(placement, cross_fraction, predictions): the fastest predicted placement; within 2% of it,
     the one that sends the most boundary bytes across GPUs."""
-    t = table(n, batch_per_gpu, waves, link, comp)
+    t = table(n, batch_per_gpu, waves, link, comp, graph_dp)
     best = min(v["step_ms"] for v in t.values())
     near = [p for p, v in t.items() if v["step_ms"] <= best * 1.02]
     pick = max(near, key=lambda p: (t[p]["boundary_bytes_per_gpu"], -t[p]["step_ms"]))

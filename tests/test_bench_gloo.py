@@ -20,14 +20,21 @@ def _bench_worker(rank, world, argv):
 
     sys.argv = ["bench.py"] + list(argv)
     buf = io.StringIO()
+    code = 0
     with contextlib.redirect_stdout(buf):
-        bench.main()
-    return buf.getvalue()
+        try:
+            bench.main()
+        except SystemExit as e:  # bench.py exits non-zero on a failed self-check
+            code = e.code
+    return buf.getvalue() + (f"\n__EXIT__={code}" if code else "")
 
 
 def _run(world, extra=()):
     outs = run_ranks(_bench_worker, world, ["--gpus", str(world), "--steps", "2", "--warmup", "1", *extra],
                      timeout=300)
+    exits = [o.split("__EXIT__=")[1].strip() for o in outs if "__EXIT__=" in o]
+    if exits:
+        raise RuntimeError(f"bench exited {exits}")
     lines = [l for l in outs[0].splitlines() if l.startswith("{")]
     assert len(lines) == 1 and all(not o.strip() for o in outs[1:])
     d = json.loads(lines[0])
@@ -35,6 +42,14 @@ def _run(world, extra=()):
     assert d["config"]["global_batch"] == world * 256 and d["value"] > 0 and d["higher_is_better"] is True
     assert d["final_loss"] is not None and d["final_loss"] == d["final_loss"]  # finite
     assert d["config"]["world_size_seen"] == world and d["config"]["backend"] == "gloo"
+    # self-checks of a multi-rank run: replicas bit-identical after the timed steps, links measured before the
+    # placement was chosen (and the measured model is the one the JSON reports)
+    assert d["config"]["replicas_identical"] is True, d["config"]["replica_check"]
+    lm = d["config"]["link_measured"]
+    assert lm["world_size"] == world and lm["allreduce_us"] > 0 and lm["collective_us"] > 0 and lm["gbps"] > 0
+    assert d["config"]["link_model"]["link"]["gbps"] == lm["gbps"]
+    assert d["config"]["link_model"]["link"]["allreduce_us"] == lm["allreduce_us"]
+    assert d["config"]["link_model_assumed"]["gbps"] == 50.0
     return d
 
 
@@ -78,10 +93,23 @@ def test_bench_gpus_flag_spawns_ranks_on_cpu(tmp_path):
     assert r.returncode == 2 and not [l for l in r.stdout.splitlines() if l.startswith("{")]
 
 
-def test_bench_two_ranks_measures_the_reference_placement():
-    """At N = 2 (the reference's world size) the JSON also carries a measured pp2dp step (stage 0 | stage 1 on
-    the two ranks, Chimera, factored boundary gradient: 512 + 40 B per row over the link)."""
-    d = _run(2)
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_measures_the_reference_placement_at_every_even_n(world):
+    """At every even N the JSON also carries a measured pp2dp step (stage 0 | stage 1 on the GPUs of each pair,
+    Chimera, factored boundary gradient: 512 + 40 B per row over the link), next to the placement the measured
+    link model chose."""
+    d = _run(world, ["--placement", "dp"])
     alt = d["config"]["measured_alternatives"]["pp2dp"]
     assert "error" not in alt, alt
-    assert alt["samples_per_s"] > 0 and alt["boundary_bytes_across_gpus_per_step"] == 2 * 256 * (512 + 40)
+    assert alt["samples_per_s"] > 0 and alt["boundary_bytes_across_gpus_per_step"] == world * 256 * (512 + 40)
+
+
+def test_bench_exits_nonzero_when_replicas_diverge():
+    """A test hook flips one parameter bit on rank 1 after the timed steps: the replica check must see it, report
+    replicas_identical = false and make bench.py exit non-zero (3)."""
+    os.environ["SDML_BENCH_PERTURB_RANK"] = "1"
+    try:
+        with pytest.raises(RuntimeError, match=r"bench exited \['3', '3'\]"):
+            _run(2, ["--placement", "dp", "--alternatives", "off"])
+    finally:
+        os.environ.pop("SDML_BENCH_PERTURB_RANK", None)

@@ -109,3 +109,30 @@ def test_graphed_step_with_rccl_allreduce_on_one_rank():
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), PYTHONPATH=root)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=200)
     assert r.returncode == 0 and "graph+rccl ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def test_graphed_step_many_waves_ragged_keeps_buffers_alive():
+    """more than 16 fused waves evict the engine's per-wave (ReLU bits, gradient) buffers; a captured graph
+    keeps their addresses, so evicted buffers must stay alive while the graph can replay. 18 waves (rotate schedule,
+    one rank) plus a ragged batch with its own graph: the replays must match an eager engine step for step."""
+    ds = SyntheticMNIST(18 * 256 * 8, seed=6, device=DEV, pixels="u8")
+
+    def eng():
+        mesh = init_mesh(pp=1, schedule_kind="rotate", rank=0, world_size=1, device=DEV)
+        return PipelineEngine(get_model_spec("mlp", 2), mesh, schedule_kind="rotate", num_microbatches=18, lr=0.1,
+                              momentum=0.5, seed=7)
+
+    e1, e2 = eng(), eng()
+    g = GraphedStep(e2)
+    B = 18 * 256
+    sizes = [B, B, B - 100, B, B - 100, B, B - 100]
+    start = 0
+    for n in sizes:
+        r1 = e1.run(ds, start, n, train=True)
+        r2 = g(ds, start, n)
+        assert abs(float(r1.loss_sum) - float(r2.loss_sum)) <= 1e-4 * max(1.0, abs(float(r1.loss_sum)))
+        start += n
+    torch.cuda.synchronize()
+    assert g.replays == len(sizes) - 1 and len(g.graphs) == 2 and not g.disabled
+    assert len(e2._wave_bufs) + len(e2._wave_bufs_retired) >= 17  # the eviction path ran with graphs alive
+    torch.testing.assert_close(e1.flat.params, e2.flat.params, rtol=1e-5, atol=1e-6)

@@ -114,14 +114,30 @@ def test_bench_two_ranks_on_one_gpu():
         assert d["config"]["world_size_seen"] == 2 and d["config"]["backend"] == "gloo"
         if cross:
             assert d["config"]["boundary_bytes_across_gpus_per_step"] == 2 * 4096 * (512 + 40)
-        else:  # auto: the placement the cost model picks for this N and batch, and its prediction in the JSON
+        else:  # auto: the placement the cost model picks for this N and batch from the MEASURED link constants
             from simple_distributed_machine_learning_amd.parallel import placement as plc
 
-            want, phi, table = plc.choose(2, 8192)
+            lm = d["config"]["link_measured"]
+            assert lm["allreduce_us"] > 0 and lm["collective_us"] > 0 and lm["gbps"] > 0 and lm["pair_gbps"] > 0
+            link = plc.LinkModel(**d["config"]["link_model"]["link"])
+            want, phi, table = plc.choose(2, 8192, link=link, graph_dp=False)
             assert d["config"]["placement"] == want, (d["config"]["placement"], want)
             assert d["config"]["predicted"] == table
             if want == "dp":
                 assert d["config"]["boundary_bytes_across_gpus_per_step"] == 0
+        # self-checks: replicas bit-identical after the timed steps, the reference's cut measured at this even N
+        assert d["config"]["replicas_identical"] is True, d["config"]["replica_check"]
+        alt = d["config"]["measured_alternatives"]
+        if d["config"]["placement"] != "pp2dp":
+            assert "error" not in alt["pp2dp"] and alt["pp2dp"]["samples_per_s"] > 0, alt
+    # a perturbed replica (test hook: one parameter bit flipped on rank 1 after the timed steps) fails the run
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--placement", "dp", "--alternatives", "off"]
+    r = subprocess.run(cmd, env=dict(env, SDML_BENCH_PERTURB_RANK="1"), capture_output=True, text=True, timeout=300,
+                       cwd=ROOT)
+    assert r.returncode != 0 and "replicas diverged" in r.stderr, r.stdout[-2000:] + r.stderr[-3000:]
+    assert _bench_json(r)["config"]["replicas_identical"] is False
 
 
 def test_bench_graph_replay_trains_identically():
@@ -136,7 +152,8 @@ def test_bench_graph_replay_trains_identically():
         out[g] = _bench_json(r)
     assert out["off"]["config"]["hip_graph"] is None
     hg = out["on"]["config"]["hip_graph"]
-    assert hg == {"graphs": 4, "replays": 7, "eager_steps": 0, "disabled": False}, hg
+    assert hg == {"graphs": 4, "replays": 7, "eager_steps": 0, "disabled": False, "captures_in_timed_region": 0,
+                  "dataset_batches_cycled": 4}, hg
     assert out["on"]["final_loss"] == out["off"]["final_loss"]
 
 

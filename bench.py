@@ -347,18 +347,24 @@ def main():
     # per-step device time: one event before every timed step and one after the last, recorded on the
     # compute stream (host cost ~1 us each); read after the timed region. They describe the window the
     # wall clock measures (first step vs steady state), they do not replace it.
-    evs = ([torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)] if dev.type == "cuda" else [])
+    # SDML_BENCH_EVENTS (A/B): "all" = an event before every step, "ends" = around the first step and at the end only,
+    # "none"
+    # (measured, profiles/r6_bench_events_ab.jsonl: an event before every step costs ~4.5 us of device time per step -
+    # a marker between two kernels of one stream stops the next dispatch from overlapping the previous one's tail)
+    ev_mode = os.environ.get("SDML_BENCH_EVENTS", "ends") if dev.type == "cuda" else "none"
+    rec = set(range(a.steps + 1)) if ev_mode == "all" else ({0, 1, a.steps} if ev_mode == "ends" else set())
+    evs = {i: torch.cuda.Event(enable_timing=True) for i in rec}
     t0 = time.perf_counter()
     res = None
     for i in range(a.steps):
-        if evs:
+        if i in evs:
             evs[i].record()
         res = step(a.warmup + i)
-    if evs:
+    if a.steps in evs:
         evs[a.steps].record()
     sync()
     el = time.perf_counter() - t0
-    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps)] if evs else []
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps)] if ev_mode == "all" else []
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     sent = torch.tensor([float(engine.transport.bytes_sent if engine.transport else 0)], dtype=torch.float64,
                         device=dev)
@@ -437,6 +443,9 @@ def main():
             "baseline": BASELINE_NOTE,
             "final_loss": None if loss is None else round(loss, 5),
         }
+        if ev_mode == "ends" and a.steps >= 2:
+            out["step_ms_events"] = {"first": round(evs[0].elapsed_time(evs[1]), 4),
+                                     "rest_mean": round(evs[1].elapsed_time(evs[a.steps]) / (a.steps - 1), 4)}
         if step_ms:  # rank 0's per-step device times (HIP events on the compute stream)
             srt = sorted(step_ms)
             out["step_ms_events"] = {"first": round(step_ms[0], 4), "median": round(srt[len(srt) // 2], 4),

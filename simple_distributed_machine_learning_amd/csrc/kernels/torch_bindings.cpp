@@ -1474,16 +1474,20 @@ void check_bf16_cuda(const torch::Tensor& t, const char* name) {
 // returns (row_loss fp32 [rows], row_correct fp32 [rows], dlogits bf16 or None)
 std::tuple<torch::Tensor, torch::Tensor, c10::optional<torch::Tensor>> cross_entropy_bf16(
     torch::Tensor logits, torch::Tensor target, double scale, int64_t ignore_index, bool need_grad) {
-  check_bf16_cuda(logits, "logits");
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == torch::kBFloat16, "logits must be a bf16 device tensor");
   TORCH_CHECK(logits.dim() == 2, "logits [rows, V]");
-  TORCH_CHECK(target.is_cuda() && target.scalar_type() == torch::kInt64 && target.is_contiguous(), "target int64");
+  // rows may be padded (row stride ld >= V, e.g. the lm_head's padded vocabulary): dlogits gets the same row stride,
+  // its pad columns written as zeros by the kernel, and is returned as the [rows, V] view
   const int64_t rows = logits.size(0), V = logits.size(1);
+  const int64_t ld = rows > 1 ? logits.stride(0) : V;
+  TORCH_CHECK(logits.stride(1) == 1 && ld >= V, "logits rows must be contiguous (row stride >= V)");
+  TORCH_CHECK(target.is_cuda() && target.scalar_type() == torch::kInt64 && target.is_contiguous(), "target int64");
   TORCH_CHECK(target.numel() == rows, "target size");
   auto f = logits.options().dtype(torch::kFloat32);
   auto loss = torch::empty({rows}, f), ok = torch::empty({rows}, f);
   c10::optional<torch::Tensor> g;
-  if (need_grad) g = torch::empty_like(logits);
-  sdml::cross_entropy_bf16(logits.data_ptr(), target.data_ptr<int64_t>(), rows, V, V, (float)scale, (int)ignore_index,
+  if (need_grad) g = torch::empty({rows, ld}, logits.options()).narrow(1, 0, V);
+  sdml::cross_entropy_bf16(logits.data_ptr(), target.data_ptr<int64_t>(), rows, V, ld, (float)scale, (int)ignore_index,
                            loss.data_ptr<float>(), ok.data_ptr<float>(), need_grad ? g->data_ptr() : nullptr,
                            cur_stream());
   return {loss, ok, g};
@@ -1753,6 +1757,19 @@ c10::optional<torch::Tensor> ref_cnn_stage1(torch::Tensor x, torch::Tensor w1, t
 }
 }  // namespace
 
+// ---- stream memory operations for the IPC transport (parallel/p2p.py IpcTransport): the command processor of the
+// current stream writes / waits for a 32-bit word in device memory (this process's or a peer process's buffer opened
+// through hipIPC), so a boundary hand-off between processes is ordered on the device, with no host round trip.
+void stream_write_value32(int64_t ptr, int64_t value) {
+  const hipError_t e = hipStreamWriteValue32(cur_stream(), reinterpret_cast<void*>(ptr), (uint32_t)value, 0);
+  TORCH_CHECK(e == hipSuccess, "hipStreamWriteValue32: ", hipGetErrorString(e));
+}
+void stream_wait_value32(int64_t ptr, int64_t value) {
+  const hipError_t e = hipStreamWaitValue32(cur_stream(), reinterpret_cast<void*>(ptr), (uint32_t)value,
+                                            hipStreamWaitValueGte, 0xFFFFFFFFu);
+  TORCH_CHECK(e == hipSuccess, "hipStreamWaitValue32: ", hipGetErrorString(e));
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "sdml gfx950 HIP kernels";
   m.def("linear_fwd_u8", &linear_fwd_u8, "act(scale * x_u8 @ w.T + b): uint8-pixel first layer", py::arg("x"),
@@ -1922,4 +1939,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ref_cnn_stage0_bwd", &ref_cnn_stage0_bwd, "reference CNN stage 0 backward (one launch)");
   m.def("ref_cnn_stage1", &ref_cnn_stage1, "reference CNN stage 1 forward+loss+backward (one launch)");
   m.def("synth_mnist", &synth_mnist, "on-device synthetic MNIST-shape data");
+  m.def("stream_write_value32", &stream_write_value32, "current stream: *ptr = value (uint32) after prior work");
+  m.def("stream_wait_value32", &stream_wait_value32, "current stream: later work waits until *ptr >= value (uint32)");
 }

@@ -120,6 +120,7 @@ __global__ void __launch_bounds__(CE_T) ce_fwd_bwd_kernel(const u16* __restrict_
       g[i] = f2bf(sc * (p - (i == y ? 1.f : 0.f)));
     }
   }
+  for (int i = V + t; i < ld; i += CE_T) g[i] = 0;  // padded rows (ld > V): zero gradient columns
 }
 
 // Register-resident variant (V <= 512 threads * 8 * CE_NVMAX): the row is read from HBM ONCE
@@ -224,6 +225,9 @@ __global__ void __launch_bounds__(CER_T) ce_reg_kernel(const u16* __restrict__ l
   }
   if (t < head) g[t] = f2bf(sc * (__expf(xh - lse) - (t == y ? 1.f : 0.f)));
   if (t < ntail) g[tail0 + t] = f2bf(sc * (__expf(xt - lse) - (tail0 + t == y ? 1.f : 0.f)));
+  // padded rows (ld > V, the lm_head's vocabulary padded to a multiple of 64 in ops/linear.py lm_head): the pad
+  // columns' gradient is zero, so the GEMMs that read the padded dlogits (input and weight gradient) see exact zeros
+  for (int i = V + t; i < ld; i += CER_T) g[i] = 0;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .base import ModelSpec, PipelineStage
-from ..ops.linear import Linear, linear, mlp_gelu
+from ..ops.linear import Linear, linear, lm_head, mlp_gelu
 from ..ops.transformer import LayerNorm, add_layer_norm, causal_attention, cross_entropy_sum, embedding, gelu
 from ..parallel.tp import TPContext, column_slice, copy_to_tp, reduce_from_tp, shard_parameter
 
@@ -115,6 +115,9 @@ class GPT2Stage(PipelineStage):
         if stage_id == num_stages - 1:
             self.ln_f = LayerNorm(cfg.n_embd)
             self.lm_head = Linear(cfg.n_embd, cfg.vocab_size, bias=False)
+            # the vocabulary padded to a multiple of 64 rows in the flat storage (zero rows, zero gradient): the
+            # lm_head's three GEMMs run on the hand-written kernels as 50304-wide GEMMs (ops/linear.py lm_head)
+            self.flat_row_multiple = {"lm_head.weight": 64}
         self._init()
 
     supports_tp = True
@@ -165,7 +168,7 @@ class GPT2Stage(PipelineStage):
         last = self.stage_id == self.num_stages - 1
         blocks = list(self.h.values())
         if not blocks:
-            return self.lm_head(self.ln_f(x)) if last else x
+            return lm_head(self.ln_f(x), self.lm_head.weight) if last else x
         # each residual add is fused into the LayerNorm that reads its sum (ln_2 of the same block,
         # ln_1 of the next, ln_f at the end); the block maths is exactly Block.forward
         y = blocks[0].ln_1(x)
@@ -177,7 +180,7 @@ class GPT2Stage(PipelineStage):
                 x = x + m
             else:
                 x, y = add_layer_norm(x, m, nxt)
-        return self.lm_head(y) if last else x
+        return lm_head(y, self.lm_head.weight) if last else x
 
 
 def gpt2_spec(num_stages: int = 2, cfg: GPT2Config = None, seq_len: int = None, dtype=torch.bfloat16,

@@ -18,8 +18,8 @@ When a parameter has no ``.grad`` yet (standalone use), the gradients are return
 autograd in the usual way. CPU tensors and non-bf16 dtypes keep the plain ``F.linear``
 path. The forward / input-gradient GEMMs run on gemm_bf16.hip's NT kernel (SDML_GPT2_GEMM=hand, the default since
 its 256 x 192 tiles; SDML_GPT2_GEMM=lib puts them on hipBLASLt); the MLP's c_fc forward and c_proj input gradient
-carry the GELU in their epilogues (:func:`mlp_gelu`). A shape the hand kernel does not take (the 50257-wide
-lm_head: N % 8 != 0) stays on the library.
+carry the GELU in their epilogues (:func:`mlp_gelu`). GPT-2's 50257-wide lm_head runs padded to 50304 rows in place
+(:func:`lm_head`), so no GEMM of the GPT-2 step is left on the library.
 """
 from __future__ import annotations
 
@@ -240,6 +240,93 @@ def _wgrad_ok(g2, x2, gw) -> bool:
             and g2.stride(-1) == 1 and x2.stride(-1) == 1 and gw.is_contiguous()
             and g2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0
             and kernels().wgrad_bf16_supported(gw.shape[0], gw.shape[1], g2.shape[0]))
+
+
+def _padded(t, rows):
+    """``t`` [V, C] (a parameter or its .grad, inside FlatParams' row-padded storage) as the [rows, C] matrix."""
+    C = t.shape[1]
+    if (not t.is_contiguous() or t.untyped_storage().nbytes() < (t.storage_offset() + rows * C) * t.element_size()):
+        return None
+    return t.as_strided((rows, C), (C, 1))
+
+
+def _w_padded(w):
+    """The lm_head weight as its padded [Vp, C] matrix, cached on the parameter (the same storage every step)."""
+    rows = getattr(w, "_sdml_rows_padded", 0)
+    if rows < w.shape[0]:
+        return None
+    wp = getattr(w, "_sdml_wpad", None)
+    if wp is None or wp.data_ptr() != w.data_ptr() or wp.shape[0] != rows:
+        wp = _padded(w, rows)
+        w._sdml_wpad = wp
+    return wp
+
+
+class _LMHeadFn(torch.autograd.Function):
+    """GPT-2's untied vocabulary head, logits = x W^T (no bias), on the hand-written bf16 kernels.
+
+    The vocabulary (50257) is not a multiple of 8, so W lives in FlatParams' row-padded storage (models/gpt2.py
+    ``flat_row_multiple``): the [Vp = 50304, 768] matrix in place, rows past V zero in the weight and in its
+    gradient. All three GEMMs then run at Vp: the forward (NT, N = Vp) writes [T, Vp] logits whose pad columns are
+    exact zeros and returns the [T, V] view (row stride Vp); the cross-entropy kernel reads that view and writes
+    dlogits with the same row stride, zeroing the pad columns (transformer.hip); the input gradient is dlogits W as
+    NT against the padded W^T (K = Vp) and the weight gradient dlogits^T x accumulates into the padded gradient
+    (its pad rows get exact zeros, so SGD keeps them zero). The results on the V real columns are those of the
+    unpadded GEMMs (the pad terms are products with zeros). Reference Linear layers: /root/reference/
+    simple_distributed.py:63-64, :75-77; BASELINE config 5 (the lm_head was round 5's last library GEMM)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        wp = _w_padded(w)
+        V, C = w.shape
+        x2 = x.reshape(-1, C)
+        y, _ = kernels().gemm_bf16(x2, wp, None, False, EPI_STORE)
+        ctx.save_for_backward(x2)
+        ctx.w, ctx.in_shape = w, x.shape
+        return y.narrow(1, 0, V).view(*x.shape[:-1], V)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x2,) = ctx.saved_tensors
+        w = ctx.w
+        V, C = w.shape
+        wp = _w_padded(w)
+        Vp = wp.shape[0]
+        g2 = gy.reshape(-1, V)
+        T = g2.shape[0]
+        gp = None
+        if (g2.stride(-1) == 1 and (T == 1 or g2.stride(0) == Vp)
+                and g2.untyped_storage().nbytes() >= (g2.storage_offset() + T * Vp) * g2.element_size()):
+            gp = g2.as_strided((T, Vp), (Vp, 1))  # the cross-entropy's padded dlogits (pad columns zero)
+        if gp is None:  # an unpadded gradient (another loss): pad a copy
+            gp = torch.zeros((T, Vp), dtype=g2.dtype, device=g2.device)
+            gp[:, :V] = g2
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx, _ = kernels().gemm_bf16(gp, _w_t(wp), None, False, EPI_STORE)
+            dx = dx.view(ctx.in_shape)
+        gw = None
+        if ctx.needs_input_grad[1]:
+            gpad = _padded(w.grad, Vp) if w.grad is not None else None
+            if gpad is not None and _wgrad_ok(gp, x2, gpad):
+                kernels().wgrad_bf16_(gp, x2, gpad, None)
+            else:
+                gw = gp[:, :V].t() @ x2
+        return dx, gw
+
+
+def lm_head(x, w):
+    """logits = x W^T (GPT-2's vocabulary head): the padded hand-written path when W sits in row-padded storage on
+    ROCm bf16 (see _LMHeadFn), else the plain Linear."""
+    if (_HAND and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.stride(-1) == 1
+            and _w_padded(w) is not None):
+        wp = _w_padded(w)
+        k = kernels()
+        T, C = x.numel() // x.shape[-1], x.shape[-1]
+        Vp = wp.shape[0]
+        if (k.gemm_bf16_supported(T, Vp, C, C, C, False) and k.gemm_bf16_supported(T, C, Vp, Vp, Vp, False)):
+            return _LMHeadFn.apply(x, w)
+    return linear(x, w)
 
 
 def linear(x, w, b=None):

@@ -93,7 +93,9 @@ def cross_entropy_sum(logits, target, scale: float, need_grad: bool, ignore_inde
     logits dtype (None unless ``need_grad``). bf16 on ROCm uses the fused single-row kernel
     (never materialises fp32 logits)."""
     if _hip_bf16(logits):
-        loss, ok, g = kernels().cross_entropy_bf16(logits.contiguous(), target.contiguous(), float(scale),
+        if not (logits.stride(-1) == 1 and (logits.shape[0] <= 1 or logits.stride(0) >= logits.shape[1])):
+            logits = logits.contiguous()  # (rows may be padded: the lm_head's [T, 50304]-strided logits stay in place)
+        loss, ok, g = kernels().cross_entropy_bf16(logits, target.contiguous(), float(scale),
                                                    ignore_index, need_grad)
         valid = int((target != ignore_index).sum()) if ignore_index >= 0 else target.numel()
         return loss.sum(), ok.sum(), valid, g

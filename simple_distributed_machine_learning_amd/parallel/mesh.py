@@ -163,7 +163,9 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
 
     ``transport`` (default: env ``SDML_TRANSPORT``, else ``"direct"``): ``"host"`` stages device
     tensors through host memory over Gloo, so several ranks can share one GPU (RCCL refuses
-    that); the process group is then Gloo even on a ROCm device.
+    that); the process group is then Gloo even on a ROCm device. ``"ipc"`` moves the
+    point-to-point boundary tensors device to device through hipIPC (parallel/p2p.py
+    IpcTransport; same GPU or peers), its collectives host-staged over the Gloo group.
     """
     if rank is None:
         rank = int(os.environ.get("RANK", "0"))
@@ -174,11 +176,13 @@ def init_mesh(pp: int, schedule_kind: str = "1f1b", backend: Optional[str] = Non
     if device is None:
         device = select_device(local_rank)
     transport = transport or os.environ.get("SDML_TRANSPORT", "direct")
-    if transport not in ("direct", "host"):
-        raise ValueError(f"unknown transport {transport!r} (direct | host)")
+    if transport not in ("direct", "host", "ipc"):
+        raise ValueError(f"unknown transport {transport!r} (direct | host | ipc)")
+    if transport == "ipc" and device.type != "cuda":
+        transport = "direct"  # (no device: the CPU test path has nothing to map)
     if backend is None:
-        backend = "gloo" if transport == "host" else default_backend(device)
-    if backend == "gloo" and device.type == "cuda":
+        backend = "gloo" if transport in ("host", "ipc") else default_backend(device)
+    if backend == "gloo" and device.type == "cuda" and transport != "ipc":
         transport = "host"  # Gloo cannot run the engine's collectives on device tensors
     tp = max(1, int(tp))
     if world_size % tp != 0:

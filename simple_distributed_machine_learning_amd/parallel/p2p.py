@@ -21,6 +21,11 @@ transport seam"):
   one GPU, so this is what lets a 1-GPU box run 2..16 ranks of the real device engine (every
   kernel, every orchestration branch of the R > 1 paths) in separate processes sharing
   ``cuda:0`` (``SDML_TRANSPORT=host``; tests/test_multirank_gpu.py).
+* :class:`IpcTransport` moves point-to-point boundary tensors DEVICE to DEVICE between processes:
+  persistent send slots exported once as hipIPC memory handles, ordered on the device by stream
+  memory operations (``hipStreamWriteValue32`` / ``hipStreamWaitValue32``), no host round trip
+  (``SDML_TRANSPORT=ipc``; SURVEY.md §2c "hipIPC peer-write fast path with pre-registered
+  persistent buffers"). Collectives stay host-staged.
 
 :class:`BufferPool` holds the persistent boundary buffers: one per (role, slot), sized on first
 use and reused by every later step, so the step loop allocates no communication memory.
@@ -268,7 +273,167 @@ class HostStagedTransport(Transport):
         dist.barrier()
 
 
-TRANSPORTS = {"direct": DirectTransport, "host": HostStagedTransport}
+class _IpcRecv:
+    """An irecv of the IPC transport: ``wait()`` enqueues, on the caller's current stream, the wait for the sender's
+    ready word, the copy out of the sender's slot and the acknowledgement (nothing blocks the host once the slot is
+    mapped)."""
+
+    def __init__(self, tr, src, t, seq):
+        self.tr, self.src, self.t, self.seq = tr, src, t, seq
+        self._done = False
+
+    def wait(self):
+        if not self._done:
+            self.tr._consume(self.src, self.t, self.seq)
+            self._done = True
+        return True
+
+    def is_completed(self):
+        return self._done
+
+
+class IpcTransport(HostStagedTransport):
+    """Point-to-point device tensors between processes through hipIPC (same GPU or peer GPUs of one node).
+
+    Per ordered channel src -> dst the SENDER owns ``SLOTS`` persistent slot buffers and one control block of int32
+    words: ``ready[s]`` (the sequence number of the last message written into slot s) and ``ack[s]`` (the last one the
+    receiver copied out). Both are exported once as IPC memory handles through the job's rendezvous store and opened
+    once by the receiver. Messages on a channel are FIFO (the schedule matches every send with a recv in order), so
+    message k of a channel uses slot (k - 1) % SLOTS on both sides and nothing but the payload travels per message:
+
+    * ``isend`` (sender's current stream): wait until ``ack[s] >= k - SLOTS`` (the slot's previous message was taken),
+      copy the tensor into the slot, write ``ready[s] = k``;
+    * ``irecv(...).wait()`` (receiver's current stream): wait until ``ready[s] >= k``, copy the slot into the tensor,
+      write ``ack[s] = k``.
+
+    Slot buffers come in power-of-two capacity classes (>= 64 KiB) that both sides derive from the message size, so
+    a ragged last batch uses its own buffer without any negotiation. The words are written and waited on by the
+    streams' command processors (hipStreamWriteValue32 / hipStreamWaitValue32 in ``_kernels``), so the hand-off is
+    ordered on the device like an RCCL send / recv; all-to-all and all-reduce stay on the host-staged Gloo path
+    (the engine's rotate and data-parallel collectives). The reference's hand-off this replaces is
+    ``RRef(z3)`` + ``rpc_sync().forward`` + ``to_here()`` (/root/reference/simple_distributed.py:47-49, :71) and the
+    gradient's way back (:112)."""
+
+    name = "ipc"
+    SLOTS = 16
+    MIN_CLASS = 1 << 16
+    _instances = 0  # per process; every rank builds its transports in the same order (SPMD), so the ids match
+
+    def __init__(self, mesh):
+        super().__init__(mesh)
+        if mesh.device.type != "cuda":
+            raise ValueError("the IPC transport moves device tensors: it needs a ROCm device")
+        IpcTransport._instances += 1
+        self.prefix = f"sdml_ipc/{IpcTransport._instances}"
+        self.store = dist.distributed_c10d._get_default_store()
+        self._send_seq: Dict[int, int] = {}
+        self._recv_seq: Dict[int, int] = {}
+        self._send_ctrl: Dict[int, torch.Tensor] = {}
+        self._recv_ctrl: Dict[int, torch.Tensor] = {}
+        self._send_bufs: Dict[tuple, torch.Tensor] = {}
+        self._recv_bufs: Dict[tuple, torch.Tensor] = {}
+        self.registered = 0  # buffers exported (sender side) + opened (receiver side): tests assert it stops growing
+        from .._native import kernels
+
+        self.k = kernels()
+
+    # ---- registration (once per channel / slot / capacity class) ------------------------------------------------
+    def _key(self, src, dst, what):
+        return f"{self.prefix}/{src}->{dst}/{what}"
+
+    def _export(self, key, t):
+        import pickle
+
+        from torch.multiprocessing.reductions import reduce_tensor
+
+        self.store.set(key, pickle.dumps(reduce_tensor(t)))
+        self.registered += 1
+
+    def _open(self, key):
+        import pickle
+
+        fn, args = pickle.loads(self.store.get(key))  # blocks until the peer has exported it (store timeout)
+        self.registered += 1
+        return fn(*args)
+
+    @classmethod
+    def _cls(cls, nbytes):
+        return max(cls.MIN_CLASS, 1 << max(0, int(nbytes - 1).bit_length()))
+
+    def _ctrl_out(self, dst):
+        c = self._send_ctrl.get(dst)
+        if c is None:
+            c = self._send_ctrl[dst] = torch.zeros(2 * self.SLOTS, dtype=torch.int32, device=self.mesh.device)
+            torch.cuda.synchronize(self.mesh.device)  # zeroed before the peer can map it
+            self._export(self._key(self.mesh.rank, dst, "ctrl"), c)
+        return c
+
+    def _ctrl_in(self, src):
+        c = self._recv_ctrl.get(src)
+        if c is None:
+            c = self._recv_ctrl[src] = self._open(self._key(src, self.mesh.rank, "ctrl"))
+        return c
+
+    def _slot_out(self, dst, slot, cls):
+        b = self._send_bufs.get((dst, slot, cls))
+        if b is None:
+            b = self._send_bufs[(dst, slot, cls)] = torch.empty(cls, dtype=torch.uint8, device=self.mesh.device)
+            self._export(self._key(self.mesh.rank, dst, f"s{slot}c{cls}"), b)
+        return b
+
+    def _slot_in(self, src, slot, cls):
+        b = self._recv_bufs.get((src, slot, cls))
+        if b is None:
+            b = self._recv_bufs[(src, slot, cls)] = self._open(self._key(src, self.mesh.rank, f"s{slot}c{cls}"))
+        return b
+
+    @staticmethod
+    def _bytes(t):
+        return t.reshape(-1).view(torch.uint8)
+
+    # ---- point to point ------------------------------------------------------------------------------------------
+    def isend(self, t, dst, tag):
+        t = t.detach().contiguous()
+        n = t.numel() * t.element_size()
+        k = self._send_seq.get(dst, 0) + 1
+        self._send_seq[dst] = k
+        slot = (k - 1) % self.SLOTS
+        ctrl = self._ctrl_out(dst)
+        buf = self._slot_out(dst, slot, self._cls(n))
+        if k > self.SLOTS:  # the receiver has copied out this slot's previous message
+            self.k.stream_wait_value32(ctrl.data_ptr() + 4 * (self.SLOTS + slot), k - self.SLOTS)
+        if n:
+            buf[:n].copy_(self._bytes(t))
+        self.k.stream_write_value32(ctrl.data_ptr() + 4 * slot, k)
+        self.bytes_sent += n
+        self.ops += 1
+        return _Done()
+
+    def irecv(self, t, src, tag):
+        k = self._recv_seq.get(src, 0) + 1
+        self._recv_seq[src] = k
+        self.bytes_recv += t.numel() * t.element_size()
+        self.ops += 1
+        return _IpcRecv(self, src, t, k)
+
+    def _consume(self, src, t, k):
+        n = t.numel() * t.element_size()
+        slot = (k - 1) % self.SLOTS
+        ctrl = self._ctrl_in(src)
+        buf = self._slot_in(src, slot, self._cls(n))
+        self.k.stream_wait_value32(ctrl.data_ptr() + 4 * slot, k)
+        if n:
+            if t.is_contiguous():
+                self._bytes(t).copy_(buf[:n])
+            else:
+                t.copy_(buf[:n].view(t.dtype).view(t.shape))
+        self.k.stream_write_value32(ctrl.data_ptr() + 4 * (self.SLOTS + slot), k)
+
+    def drain_sends(self):
+        self._pending_sends.clear()  # (sends are stream-ordered device copies: nothing to wait for on the host)
+
+
+TRANSPORTS = {"direct": DirectTransport, "host": HostStagedTransport, "ipc": IpcTransport}
 
 
 def make_transport(mesh) -> Transport:

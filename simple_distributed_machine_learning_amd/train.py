@@ -85,10 +85,10 @@ def run(args) -> dict:
                             lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay, seed=args.seed,
                             debug_sync=args.debug_sync, timing=getattr(args, "timing", False))
     torch.manual_seed(args.seed * 7 + mesh.rank)  # dropout streams (reference: unseeded)
-    if spec.input_kind == "tokens" and device.type == "cuda":
+    if spec.input_kind == "tokens" and device.type == "cuda" and os.environ.get("SDML_GPT2_GEMM") == "lib":
         from .utils.tuned_gemm import use_tuned_gemms
 
-        use_tuned_gemms()  # committed hipBLASLt solution table (TunableOp replay, no tuning)
+        use_tuned_gemms()  # A/B only: the library GEMMs with the committed hipBLASLt solution table (TunableOp replay)
     train_ds, test_ds = make_datasets(args, spec, device)
     metrics = JsonlMetrics(args.metrics if mesh.is_master() else None, mesh.rank)
     master = mesh.is_master()

@@ -50,12 +50,23 @@ class FlatParams:
         self.stage_ranges: Dict[int, Tuple[int, int]] = {}
         off = 0
         plist = []
+        padded = []
         for sid, m in mods:
             start = off
+            # a module may ask for zero rows after a 2-D parameter (flat_row_multiple = {name: multiple}): the rows
+            # up to the next multiple stay zero in the parameter, gradient, master and momentum buffers (their
+            # gradient is zero, so SGD keeps them zero), so a kernel may treat the weight as the padded
+            # [rows rounded up][cols] matrix in place (ops/linear.py lm_head: GPT-2's 50257-row vocabulary -> 50304)
+            mult = getattr(m, "flat_row_multiple", None) or {}
             for name, p in m.named_parameters():
                 self.segments.append(Segment(sid, name, off, p.numel(), tuple(p.shape)))
                 plist.append(p)
-                off += _pad(p.numel())
+                n = p.numel()
+                if name in mult and p.dim() == 2:
+                    rows = -(-p.shape[0] // mult[name]) * mult[name]
+                    n = rows * p.shape[1]
+                    padded.append((p, rows))
+                off += _pad(n)
             self.stage_ranges[sid] = (start, off)
         self.numel = max(off, ALIGN)
         self.device = torch.device(device)
@@ -67,6 +78,8 @@ class FlatParams:
             view.copy_(p.detach().to(self.device, dtype))
             p.data = view
             p.grad = self.grads[seg.offset:seg.offset + seg.numel].view(seg.shape)
+        for p, rows in padded:
+            p._sdml_rows_padded = rows  # the storage holds `rows` rows (params and grads); the extra rows are zero
         self._plist = plist
         self.grads_zero = True  # grads known to be all-zero (skip the next zero_grad launch)
         # bumped by every optimizer step (whose kernels write the parameters through raw pointers,

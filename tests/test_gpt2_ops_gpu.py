@@ -294,3 +294,41 @@ def test_hand_linear_wt_cache_batches_and_refreshes():
     for w in ws[1:]:  # refreshed by the same batched launch: cache hits now
         hit = conv_ops._cache_get(lin._WT, w)
         assert hit is not None and torch.equal(hit[1], w.t())
+
+
+@pytest.mark.parametrize("T,C,V", [(2048, 768, 50257), (512, 64, 97)])
+def test_lm_head_padded_vocabulary_matches_fp32(T, C, V):
+    """GPT-2's lm_head on the hand-written kernels with the vocabulary padded in place (ops/linear.py _LMHeadFn;
+    FlatParams row padding): logits, the cross-entropy's dlogits, the input gradient and the weight gradient against
+    a PyTorch fp32 reference of the same op on the same bf16 operands; the pad rows of the weight gradient stay
+    exactly zero."""
+    from simple_distributed_machine_learning_amd.ops.linear import _LMHeadFn, lm_head
+    from simple_distributed_machine_learning_amd.ops.transformer import cross_entropy_sum
+    from simple_distributed_machine_learning_amd.utils.flat import FlatParams
+
+    g = torch.Generator(device="cpu").manual_seed(V)
+    head = torch.nn.Linear(C, V, bias=False)
+    head.flat_row_multiple = {"weight": 64}
+    with torch.no_grad():
+        head.weight.copy_(torch.randn(V, C, generator=g) * 0.02)
+    flat = FlatParams([(0, head)], DEV, torch.bfloat16)
+    w = head.weight
+    Vp = -(-V // 64) * 64
+    assert w._sdml_rows_padded == Vp and w.grad is not None
+    x = (torch.randn(T, C, generator=g)).to(DEV, torch.bfloat16).requires_grad_(True)
+    tgt = torch.randint(0, V, (T,), generator=g).to(DEV)
+    logits = lm_head(x, w)
+    assert logits.grad_fn is not None and type(logits.grad_fn).__name__.startswith("_LMHeadFn")
+    assert logits.shape == (T, V) and logits.stride() == (Vp, 1)
+    ref = x.detach().float() @ w.detach().float().t()
+    torch.testing.assert_close(logits.float(), ref, rtol=2e-2, atol=2e-2)
+    l, c, n, gl = cross_entropy_sum(logits.detach(), tgt, 1.0 / T, True)
+    assert gl.stride() == (Vp, 1)
+    pad = gl.as_strided((T, Vp), (Vp, 1))[:, V:]
+    assert int((pad != 0).sum()) == 0  # the CE kernel zeroed the pad columns
+    torch.autograd.backward(logits, gl)
+    gref = gl.float()
+    torch.testing.assert_close(x.grad.float(), gref @ w.detach().float(), rtol=2e-2, atol=2e-3)
+    gw = flat.grads[:Vp * C].view(Vp, C)
+    torch.testing.assert_close(gw[:V].float(), gref.t() @ x.detach().float(), rtol=2e-2, atol=2e-3)
+    assert int((gw[V:] != 0).sum()) == 0 and int((flat.params[V * C:Vp * C] != 0).sum()) == 0

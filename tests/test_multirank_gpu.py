@@ -31,10 +31,10 @@ def _single(model, M, steps, B, kind, kw=None):
     return train_worker(0, 1, model, kind, M, 1, steps, B, 3, kw)
 
 
-def _compare(results, ref, rtol=1e-4, atol=1e-5):
+def _compare(results, ref, rtol=1e-4, atol=1e-5, transport="host"):
     seen = {}
     for r in results:
-        assert r["transport"] == "host"
+        assert r["transport"] == transport
         for s, sd in r["state"].items():
             for k, v in sd.items():
                 if (s, k) in seen:  # replicas agree exactly (same all-reduced gradients)
@@ -79,17 +79,31 @@ def test_rotate_multirank_on_device(world, mode, monkeypatch):
     assert all(r["pool_allocs"] == r["pool_allocs_first"] for r in res)  # persistent boundary buffers
 
 
+_NEIGHBOUR = {}
+
+
+@pytest.mark.parametrize("transport", ["host", "ipc"])
 @pytest.mark.parametrize("kind,world,pp,M", [("1f1b", 2, 2, 3), ("chimera", 2, 2, 4), ("1f1b", 4, 2, 2)])
-def test_neighbour_pipelines_on_device(kind, world, pp, M):
+def test_neighbour_pipelines_on_device(kind, world, pp, M, transport):
     """The reference's placement (stage 0 | stage 1 on different ranks, isend/irecv), with 1F1B,
-    Chimera, and dp2 x pp2 (gradient all-reduce between the replicas)."""
+    Chimera, and dp2 x pp2 (gradient all-reduce between the replicas). ``ipc``: the boundary tensors
+    go device to device between the processes (hipIPC slots, stream-ordered ready / ack words): the
+    trained weights must equal the host-staged run's bit for bit (only the transport differs)."""
     B, steps = 64, 2
     dp = world // pp
-    res = run_ranks(train_worker, world, "mlp", kind, M, pp, steps, B, 3, dict(GPU), timeout=400)
+    res = run_ranks(train_worker, world, "mlp", kind, M, pp, steps, B, 3, dict(GPU, transport=transport),
+                    timeout=400)
     ref = _single("mlp", M, steps, dp * B, kind)
-    _compare(res, ref)
+    _compare(res, ref, transport=transport)
     assert all(r["bytes_sent"] > 0 for r in res)
     assert all(r["pool_allocs"] == r["pool_allocs_first"] for r in res)
+    _NEIGHBOUR[(kind, world, transport)] = res
+    other = _NEIGHBOUR.get((kind, world, "host" if transport == "ipc" else "ipc"))
+    if other is not None:  # both transports ran: identical bytes delivered -> identical training
+        for a, b in zip(res, other):
+            for s, sd in a["state"].items():
+                for k, v in sd.items():
+                    torch.testing.assert_close(v, b["state"][s][k], rtol=0, atol=0, msg=f"{transport} {s} {k}")
 
 
 def _bench_json(r):
@@ -179,12 +193,12 @@ TRAIN_RE = __import__("re").compile(r"^Train Epoch: (\d+) \[(\d+)/(\d+) \((\d+)%
 TEST_RE = __import__("re").compile(r"^Test set: Average loss: (\d+\.\d{4}), Accuracy: (\d+)/(\d+) \((\d+)%\)$")
 
 
-def _launch_reference_cli(extra, world=2, timeout=400):
+def _launch_reference_cli(extra, world=2, timeout=400, transport="host"):
     """``python simple_distributed.py --rank=R --world_size=2 --interface=lo --master_addr=127.0.0.1 ...`` (the
     reference's command line, README.txt:19) as ``world`` processes sharing cuda:0 through the host-staged
-    transport."""
+    (or the IPC) transport."""
     port = free_port()
-    env = dict(os.environ, PYTHONPATH=ROOT, SDML_TRANSPORT="host")
+    env = dict(os.environ, PYTHONPATH=ROOT, SDML_TRANSPORT=transport)
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
         env.pop(k, None)
     procs = []
@@ -207,7 +221,8 @@ def _launch_reference_cli(extra, world=2, timeout=400):
     return outs
 
 
-def test_reference_command_line_two_ranks_on_device(tmp_path):
+@pytest.mark.parametrize("transport", ["ipc", "host"])
+def test_reference_command_line_two_ranks_on_device(tmp_path, transport):
     """The reference's CNN split exactly as its README runs it - conv stage on rank 0, fc stage on rank 1
     (/root/reference/simple_distributed.py:33-37, :47-49, :71, :138-186) - as two processes on the MI355X: the
     per-stage fused CNN kernels hand the [60, 320] boundary and its gradient across processes. The log lines keep
@@ -221,7 +236,7 @@ def test_reference_command_line_two_ranks_on_device(tmp_path):
 
     steps, B = 12, 60
     outs = _launch_reference_cli(["--epochs=1", f"--train_size={steps * B}", "--test_size=120", "--dropout=0",
-                                  f"--ckpt_dir={tmp_path}"])
+                                  f"--ckpt_dir={tmp_path}"], transport=transport)
     lines = outs[0].splitlines()
     train = [m for m in map(TRAIN_RE.match, lines) if m]
     test = [m for m in map(TEST_RE.match, lines) if m]
@@ -251,9 +266,10 @@ def test_mlp4x1024_gpipe_four_ranks_on_device():
     """BASELINE config 3: the 4-stage 4x1024 MLP, one stage per process, GPipe (fill-drain) on the device
     engine (two-fp16-plane hidden-layer GEMMs), against the single-process GPU engine."""
     B, steps, M = 512, 2, 4
-    res = run_ranks(train_worker, 4, "mlp4x1024", "gpipe", M, 4, steps, B, 3, dict(GPU), timeout=400)
+    res = run_ranks(train_worker, 4, "mlp4x1024", "gpipe", M, 4, steps, B, 3, dict(GPU, transport="ipc"),
+                    timeout=400)
     ref = _single("mlp4x1024", M, steps, B, "gpipe")
-    _compare(res, ref)
+    _compare(res, ref, transport="ipc")
     assert all(r["bytes_sent"] > 0 for r in res)
 
 
@@ -262,10 +278,10 @@ def test_resnet18_bf16_eight_stages_four_ranks_1f1b_on_device():
     channels-last on the hand-written conv / BatchNorm / pooled-head kernels; boundaries [N, H, W, C] bf16 between
     processes. Same kernels in the same order as one process, so the weights agree to bf16 rounding."""
     B, steps, M = 16, 2, 2
-    kw = dict(GPU, stages=8, dtype=torch.bfloat16)
+    kw = dict(GPU, stages=8, dtype=torch.bfloat16, transport="ipc")
     res = run_ranks(train_worker, 4, "resnet18", "1f1b", M, 4, steps, B, 3, kw, timeout=400)
     ref = _single("resnet18", M, steps, B, "1f1b", {"stages": 8, "dtype": torch.bfloat16})
-    _compare(res, ref, rtol=2e-2, atol=2e-3)
+    _compare(res, ref, rtol=2e-2, atol=2e-3, transport="ipc")
     assert all(r["bytes_sent"] > 0 for r in res)
 
 

@@ -76,7 +76,7 @@ def main():
     spec = get_model_spec(a.config, stages, seq_len=S, **({"dtype": dt} if dt is not None else {}))
     eng = PipelineEngine(spec, mesh, schedule_kind=kind, num_microbatches=M, lr=0.01, momentum=0.5, seed=1)
     tuned = False
-    if spec.input_kind == "tokens" and mesh.device.type == "cuda":
+    if spec.input_kind == "tokens" and mesh.device.type == "cuda" and os.environ.get("SDML_GPT2_GEMM") == "lib":
         from simple_distributed_machine_learning_amd.utils.tuned_gemm import use_tuned_gemms
 
         tuned = use_tuned_gemms()

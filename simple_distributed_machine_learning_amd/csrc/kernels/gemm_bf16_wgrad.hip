@@ -60,6 +60,8 @@ struct WgParams {
   int tps;  // tokens per split (multiple of BK)
   int tiles_m, tiles_n, splits;
   int bparts;  // bias partial sums per split (the DMA loop: tiles_n, each tn block sums K-steps t % tiles_n == tn)
+  int nfast;   // tile order: 0 = M fastest (neighbouring blocks share the x panel), 1 = N fastest (they share the gy
+               // panel: the lm_head's 1.6 GB dlogits, read once from HBM instead of once per column tile)
 };
 
 __device__ __forceinline__ int km_off(int k, int ch) { return k * 128 + 8 * (ch ^ (((k & 3) << 2) | ((k >> 2) & 3))); }
@@ -185,7 +187,7 @@ __global__ void __launch_bounds__(NT) wgrad_kernel(WgParams p) {
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
   }
   const int split = wg / ntiles, tile = wg % ntiles;
-  const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
+  const int tm = p.nfast ? tile / p.tiles_n : tile % p.tiles_m, tn = p.nfast ? tile % p.tiles_n : tile / p.tiles_m;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = split * p.tps, kend = min(p.T, kbeg + p.tps);
   const int lane = threadIdx.x & 63;
@@ -317,7 +319,7 @@ __global__ void __launch_bounds__(NT) wgrad_dma_kernel(WgParams p) {
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
   }
   const int split = wg / ntiles, tile = wg % ntiles;
-  const int tm = tile % p.tiles_m, tn = tile / p.tiles_m;
+  const int tm = p.nfast ? tile / p.tiles_n : tile % p.tiles_m, tn = p.nfast ? tile % p.tiles_n : tile / p.tiles_m;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = split * p.tps, kend = min(p.T, kbeg + p.tps);
   const int lane = threadIdx.x & 63;
@@ -483,6 +485,12 @@ void wgrad_bf16(const void* gy, const void* x, void* gw, void* gb, float* worksp
   p.splits = s;
   p.tiles_m = (M + BM - 1) / BM;
   p.tiles_n = (N + BN - 1) / BN;
+  // N fastest when gy (the M-side operand, read once per column tile in M-fastest order) cannot stay in the 256 MiB
+  // Infinity Cache between its column tiles: GPT-2's lm_head, M = 50304 vocabulary rows x 16384 tokens (1.6 GB).
+  // Round 6, one MI355X: 1.60 ms per lm_head weight gradient in M-fastest order (~6 TB/s: gy streamed from HBM six
+  // times, gpurun_out/gpt2_r6 kernel trace); the order is knob WGRAD_NFAST (-1 auto, 0, 1)
+  const int nf = knob(KNOB_WGRAD_NFAST);
+  p.nfast = nf >= 0 ? nf : ((int64_t)M * T * 2 > ((int64_t)128 << 20) && p.tiles_n <= 8 ? 1 : 0);
   const dim3 grid(p.tiles_m * p.tiles_n * s);
   const bool dma = knob(KNOB_WGRAD_DMA) != 0 && T % BK == 0 &&  // (tests A/B the two loops)
                    (reinterpret_cast<uintptr_t>(gy) & 15) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;

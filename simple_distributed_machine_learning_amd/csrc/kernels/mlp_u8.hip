@@ -202,7 +202,8 @@ __device__ __forceinline__ void issue_stage(const FwdParams& p, unsigned char* s
 template <int C, int NWR>
 __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
                                                     int m0, int wave, int lane, int wm, int wn,
-                                                    const hblk::Operands& ops, const float (&bv1)[2], long long* stamp);
+                                                    const hblk::Operands& ops, const float (&bv1)[2], long long* stamp,
+                                                    int hb);
 template <int C>
 __device__ __forceinline__ void fused_head_prefetch(const FwdParams& p, int m0, int wave, int lane, int wn,
                                                     hblk::Operands& ops, float (&bv1)[2]);
@@ -219,7 +220,14 @@ template <int MODE, int WMT, int TAIL, int NWR, int HEADC = 0, int NSK = NS, int
 __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(FwdParams p) {  // (4-wave blocks: 2 waves per SIMD, <= 256 VGPRs, two blocks per CU)
   constexpr int NS = NSK;  // (shadows the file-wide default inside this kernel)
   using G = Geo<WMT, NWR, NSK>;
-  static_assert(HEADC == 0 || (WMT == 2 && NWR == 4), "the fused head epilogue: 8 waves of 64 x 64");
+  static_assert(HEADC == 0 || ((WMT == 2 || WMT == 4) && NWR == 4), "the fused head epilogue: 8 waves of 64 x 64");
+  // HALVES (fused head, WMT = 4: 512-row blocks): a wave's four 32-row tiles are rows 64 wm + {0, 32} of each 256-row
+  // half of the block (not 128 consecutive rows), so tiles 0, 1 of every wave are the first half's h in exactly the
+  // layout head_block.h takes for a 256-row block, and tiles 2, 3 the second's: the head runs twice on unchanged code.
+  // Why 512 rows: every block streams all of W's planes through LDS per K-step (32 KiB), once per 256 rows before;
+  // now once per 512 (a third less LDS-DMA per row), one block per CU in one round instead of two.
+  constexpr bool HALVES = HEADC > 0 && WMT == 4;
+  auto tile_row = [](int i) { return HALVES ? 32 * (i & 1) + 256 * (i >> 1) : 32 * i; };
   static_assert(HEADC == 0 || G::SMEM <= hblk::LDS_BYTES, "the prefetch scratch KiB sits past the ring and the head");
   constexpr int STAGE = G::STAGE, GLDS_PER_STAGE = G::GLDS_PER_STAGE;
   constexpr int SMEM_BYTES = HEADC ? std::max(G::SMEM, hblk::LDS_BYTES) + 1024 : G::SMEM;  // (+ the prefetch scratch)
@@ -252,7 +260,7 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
   // (the swizzles use row bits below 5 only, so tiles 32 rows apart differ by a constant offset)
   int aoff[XCH / 2], boff[NSUB];
   {
-    const int row = wm * 32 * WMT + r32;
+    const int row = (HALVES ? wm * 64 : wm * 32 * WMT) + r32;
 #pragma unroll
     for (int c = 0; c < XCH / 2; ++c) aoff[c] = row * FBK + 16 * xpos(row, (XCH / 2) * h + c);
   }
@@ -268,7 +276,7 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
 #pragma unroll
     for (int i = 0; i < WMT; ++i) {
       if constexpr (MODE == 3) ar[i] = u32x4{(unsigned)aoff[s2], 1u, 2u, 3u};
-      else ar[i] = *reinterpret_cast<const u32x4*>(st + aoff[s2] + 32 * FBK * i);
+      else ar[i] = *reinterpret_cast<const u32x4*>(st + aoff[s2] + FBK * tile_row(i));
     }
   };
   auto load_b = [&](const unsigned char* st, int s, f16x8 (&b)[2][NPL]) {
@@ -427,8 +435,20 @@ __global__ void __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) u8_fwd_kernel(Fwd
   }
 
   if constexpr (HEADC > 0) {
-    fused_head_epilogue<HEADC, NWR>(p, acc, smem, m0, wave, lane, wm, wn, hops, hb1,
-                               MODE == 7 ? p.stamps + ((size_t)blockIdx.x * G::WAVES + wave) * U8_NSTAMP : nullptr);
+    long long* stp = MODE == 7 ? p.stamps + ((size_t)blockIdx.x * G::WAVES + wave) * U8_NSTAMP : nullptr;
+    if constexpr (!HALVES) {
+      fused_head_epilogue<HEADC, NWR>(p, acc, smem, m0, wave, lane, wm, wn, hops, hb1, stp, (int)blockIdx.x);
+    } else {  // two 256-row head blocks: tiles 0, 1 then 2, 3 of every wave (see HALVES)
+      typedef const f32x16 Half[2][2];
+      fused_head_epilogue<HEADC, NWR>(p, *reinterpret_cast<Half*>(&acc[0][0]), smem, m0, wave, lane, wm, wn, hops, hb1,
+                                      stp, 2 * (int)blockIdx.x);
+      if (m0 + hblk::ROWS < p.M) {  // (block-uniform) the second half holds rows
+        __syncthreads();  // every wave is done with the first head's LDS
+        fused_head_prefetch<HEADC>(p, m0 + hblk::ROWS, wave, lane, wn, hops, hb1);
+        fused_head_epilogue<HEADC, NWR>(p, *reinterpret_cast<Half*>(&acc[2][0]), smem, m0 + hblk::ROWS, wave, lane, wm,
+                                        wn, hops, hb1, nullptr, 2 * (int)blockIdx.x + 1);
+      }
+    }
     U8_STAMP(22, __builtin_amdgcn_s_memtime);
     U8_STAMP(U8_NSTAMP - 1, __builtin_amdgcn_s_memrealtime);
     return;
@@ -516,7 +536,7 @@ __device__ __forceinline__ void mask_words(const f32x16 (&y)[2][2], int (&mw)[2]
 // row rw + 4), deposited straight into those rows' lanes by v_writelane (round 4 selected them with compares, and the
 // 64 ballot SGPR pairs spilled)
 template <int C>
-__device__ __forceinline__ hblk::Args fused_head_args(const FwdParams& p) {
+__device__ __forceinline__ hblk::Args fused_head_args(const FwdParams& p, int hb) {  // hb: 256-row head block index
   const U8HeadArgs& hd = p.head;
   hblk::Args a;
   a.w2 = hd.w2;
@@ -525,15 +545,15 @@ __device__ __forceinline__ hblk::Args fused_head_args(const FwdParams& p) {
   a.loss_scale = hd.loss_scale;
   a.train = true;
   a.dl = hd.dl;
-  a.part = hd.part + (size_t)blockIdx.x * (C * 128 + C + 2);
-  a.bound = hd.bound + blockIdx.x;
+  a.part = hd.part + (size_t)hb * (C * 128 + C + 2);
+  a.bound = hd.bound + hb;
   return a;
 }
 
 template <int C>
 __device__ __forceinline__ void fused_head_prefetch(const FwdParams& p, int m0, int wave, int lane, int wn,
                                                     hblk::Operands& ops, float (&bv1)[2]) {
-  hblk::load_operands<C>(fused_head_args<C>(p), m0, p.M, wave, lane, ops);
+  hblk::load_operands<C>(fused_head_args<C>(p, 0), m0, p.M, wave, lane, ops);
 #pragma unroll
   for (int j = 0; j < 2; ++j) bv1[j] = p.bias[wn * 64 + 32 * j + (lane & 31)];
 }
@@ -541,12 +561,13 @@ __device__ __forceinline__ void fused_head_prefetch(const FwdParams& p, int m0, 
 template <int C, int NWR>
 __device__ __forceinline__ void fused_head_epilogue(const FwdParams& p, const f32x16 (&acc)[2][2], unsigned char* smem,
                                                     int m0, int wave, int lane, int wm, int wn,
-                                                    const hblk::Operands& ops, const float (&bv1)[2], long long* stamp) {
+                                                    const hblk::Operands& ops, const float (&bv1)[2], long long* stamp,
+                                                    int hb) {
   static_assert(NWR == 4, "head_block.h: 8 waves of 64 x 64, 256 rows");
   const U8HeadArgs& hd = p.head;
   const int h2 = lane >> 5;
   if (stamp && lane == 0) stamp[16] = (long long)__builtin_amdgcn_s_memtime();
-  const hblk::Args a = fused_head_args<C>(p);
+  const hblk::Args a = fused_head_args<C>(p, hb);
   auto prep = [&](hblk::hb_f32x16 (&y)[2][2]) {
     // the plain epilogue's fmaxf(fma(acc, scale, b), 0), the fmas on pairs (v_pk_fma_f32: the same roundings)
     const hblk::hb_f32x2 sc2 = {p.scale, p.scale};
@@ -1874,6 +1895,10 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
   }
   const int tail = tail_substeps(K);
   const int spread = knob(KNOB_U8_FWD_DMA_SPREAD);  // 0, 1 (spread DMA), 2 (+ fragment reads one substep ahead)
+  // 512-row blocks (u8_fwd_kernel HALVES: two head passes per block) once they still give every CU a block
+  const int r512k = knob(KNOB_U8_FH_ROWS512);
+  const bool rows512 = (r512k >= 0 ? r512k == 1 : M >= 256 * Geo<4, 4>::BM) && spread == 0 &&
+                       knob(KNOB_U8_FH_STAGES) != 3;
 #ifdef SDML_KERNEL_EXPERIMENTS  // timing variants (tools/u8_fwd_stamps.py): SDML_U8_FWD_MODE 1-6, 8-10
   static const int fmode = [] {
     const char* e = getenv("SDML_U8_FWD_MODE");
@@ -1908,9 +1933,12 @@ void u8_fwd_head(const unsigned char* X, int M, int K, int ldx, const unsigned s
     return;
   }
 #endif
+  const dim3 grid512((M + Geo<4, 4>::BM - 1) / Geo<4, 4>::BM, 1);
+  if (rows512) p.pf_stride = 0;  // (one round of blocks: nothing runs next on the CU)
 #define FH_LAUNCH(T, CC)                                                                                    \
   do {                                                                                                      \
-    if (spread == 2) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC, NS, 2>), grid, dim3(512), 0, stream, p); \
+    if (rows512) hipLaunchKernelGGL((u8_fwd_kernel<0, 4, T, 4, CC>), grid512, dim3(512), 0, stream, p);       \
+    else if (spread == 2) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC, NS, 2>), grid, dim3(512), 0, stream, p); \
     else if (spread) hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC, NS, 1>), grid, dim3(512), 0, stream, p); \
     else hipLaunchKernelGGL((u8_fwd_kernel<0, 2, T, 4, CC>), grid, dim3(512), 0, stream, p);               \
   } while (0)

@@ -368,3 +368,33 @@ def test_wgrad_hidden_group_ranges_match_the_whole_gradient(ring, cols):
     finally:
         K.reset_knobs()
     torch.testing.assert_close(part, full, rtol=1e-5, atol=1e-6 * float(full.abs().max()))
+
+
+@pytest.mark.parametrize("M", [4096 + 100, 4096 + 300, 131072])
+def test_fused_forward_head_512_row_blocks_are_bit_identical(M):
+    """512-row blocks (knob U8_FH_ROWS512: every wave holds 4 row tiles, two per 256-row half, and the head runs once
+    per half) against the 256-row blocks: the same K order per element and the same head per 256 rows, so every
+    output is bit-identical; the ragged cases end in a block whose second half is partly empty (+300) or empty
+    (+100, that pass is skipped)."""
+    from simple_distributed_machine_learning_amd import _native
+
+    K = _native.kernels()
+    x8, w1, b1, w2, b2, tgt = _problem(M, 10, seed=11)
+    outs = []
+    try:
+        for r512 in (0, 1):
+            K.set_knob("U8_FH_ROWS512", r512)
+            cache = ops.PlaneCache(w1)
+            dl = torch.full((M, 10), float("nan"), device=DEV)
+            mask = torch.zeros(M, N // 32, dtype=torch.int32, device=DEV)
+            gw, gb = torch.zeros(10, N, device=DEV), torch.zeros(10, device=DEV)
+            st = torch.empty(2, device=DEV)
+            bound, pend = ops.linear_relu_head_u8(x8, w1, b1, cache, 0, w2, b2, tgt, gw, gb, 1.0 / M, st, True, dl,
+                                                  mask, defer=False)
+            torch.cuda.synchronize()
+            outs.append((dl, mask, gw, gb, st, bound))
+    finally:
+        K.reset_knobs()
+    assert not torch.isnan(outs[1][0]).any()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)

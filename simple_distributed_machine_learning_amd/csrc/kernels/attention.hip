@@ -304,11 +304,17 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
 //   dK^T[d][k] += Q^T[d][q] dS[q][k]              (A = Q^T by transposed reads, B = dS registers)
 constexpr int BQ = 64;  // queries per iteration (backward)
 
-__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
+// NKT: 32-key tiles per wave (1: 128 keys per workgroup, 2 waves per SIMD; 2: 256 keys per workgroup, one wave per
+// SIMD with up to 512 registers: every Q / dO fragment read from LDS (rows and transposed) feeds both key tiles'
+// MFMAs, so the LDS reads per MFMA halve and each wave carries two independent accumulation chains)
+template <int NKT>
+__global__ void __launch_bounds__(256, NKT == 1 ? 2 : 1) attn_bwd_dkdv_kernel(AttnArgs a) {
+  constexpr int KW = QW * NKT;  // keys per wave
+  constexpr int KBW = KW * NW;  // keys per workgroup
   __shared__ __attribute__((aligned(16))) u16 Qs[2][TR * HD];
   __shared__ __attribute__((aligned(16))) u16 Ds[2][TR * HD];
   __shared__ float Ls[2][BQ], Dl[2][BQ];
-  const int nkb = (a.S + QB - 1) / QB;
+  const int nkb = (a.S + KBW - 1) / KBW;
   const int blk = xcd_block(blockIdx.x, gridDim.x);
   const int bh = blk / nkb;
   const int kb = blk % nkb;
@@ -317,21 +323,29 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
             h = lane >> 5;
   const long off = (long)b * a.sqb + (long)hh * a.sqh;
   const long ooff = (long)b * a.sob + (long)hh * a.soh;
-  const int k0w = kb * QB + w * QW;
-  const int kj = k0w + r;  // this lane's key (column of S, dP, dV^T, dK^T)
-  bf16x8 kf[4], vf[4];     // B operands: K[kj][16t + 8h + j], V[kj][...]
+  const int k0w = kb * KBW + w * KW;
+  int kj[NKT];  // this lane's keys (column of S, dP, dV^T, dK^T), one per key tile
+  bf16x8 kf[NKT][4], vf[NKT][4];  // B operands: K[kj][16t + 8h + j], V[kj][...]
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (kj < a.S) {
-      kf[t] = *reinterpret_cast<const bf16x8*>(a.k + off + (long)kj * a.sqs + 16 * t + 8 * h);
-      vf[t] = *reinterpret_cast<const bf16x8*>(a.v + off + (long)kj * a.sqs + 16 * t + 8 * h);
-    } else {
-      kf[t] = vf[t] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  for (int kt = 0; kt < NKT; ++kt) {
+    kj[kt] = k0w + QW * kt + r;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (kj[kt] < a.S) {
+        kf[kt][t] = *reinterpret_cast<const bf16x8*>(a.k + off + (long)kj[kt] * a.sqs + 16 * t + 8 * h);
+        vf[kt][t] = *reinterpret_cast<const bf16x8*>(a.v + off + (long)kj[kt] * a.sqs + 16 * t + 8 * h);
+      } else {
+        kf[kt][t] = vf[kt][t] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
     }
   }
   const float sl2 = a.scale * LOG2E;
-  f32x16 dv[2] = {zero16(), zero16()}, dk[2] = {zero16(), zero16()};
-  const int qstart = a.causal ? (kb * QB) / BQ * BQ : 0;
+  f32x16 dv[NKT][2], dk[NKT][2];
+#pragma unroll
+  for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+    for (int d = 0; d < 2; ++d) dv[kt][d] = dk[kt][d] = zero16();
+  const int qstart = a.causal ? (kb * KBW) / BQ * BQ : 0;
   const float* LSE = a.lse + (long)bh * a.S;
   const float* DEL = a.delta + (long)bh * a.S;
   TileRegs<TR> qr, dr;
@@ -367,31 +381,46 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
       const u16* Dt = Ds[buf];
       // only the causal diagonal needs a mask: rows past S are zero-filled Q/dO (their P and dS
       // terms multiply zero rows), and lanes with kj >= S are never stored
-      const bool edge = a.causal && q0 < k0w + QW - 1;
-#pragma unroll
+      const bool edge = a.causal && q0 < k0w + KW - 1;
+      // (NKT == 2: the two 32-query sub-blocks one after the other; unrolled, hipcc overlapped their score
+      // registers and spilled)
+#pragma unroll (NKT == 1 ? 2 : 1)
       for (int c = 0; c < 2; ++c) {  // 32-query sub-blocks
-        f32x16 s = zero16(), dp = zero16();
+        f32x16 s[NKT], dp[NKT];
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) s[kt] = dp[kt] = zero16();
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          s = mfma(rowf(Qt, 32 * c + r, t, h), kf[t], s);
-          dp = mfma(rowf(Dt, 32 * c + r, t, h), vf[t], dp);
+          const bf16x8 qa = rowf(Qt, 32 * c + r, t, h), da = rowf(Dt, 32 * c + r, t, h);
+#pragma unroll
+          for (int kt = 0; kt < NKT; ++kt) {
+            s[kt] = mfma(qa, kf[kt][t], s[kt]);
+            dp[kt] = mfma(da, vf[kt][t], dp[kt]);
+          }
         }
         // rows of s/dp are queries: q = q0 + 32c + (i&3) + 8(i>>2) + 4h
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int ql = 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
-          float p = ex2(s[i] * sl2 - Ls[buf][ql]);
-          if (edge && kj > q0 + ql) p = 0.f;
-          s[i] = p;
-          dp[i] = p * (dp[i] - Dl[buf][ql]);  // dS (scale applied to dK at the end)
+          const float lq = Ls[buf][ql], dq = Dl[buf][ql];
+#pragma unroll
+          for (int kt = 0; kt < NKT; ++kt) {
+            float p = ex2(s[kt][i] * sl2 - lq);
+            if (edge && kj[kt] > q0 + ql) p = 0.f;
+            s[kt][i] = p;
+            dp[kt][i] = p * (dp[kt][i] - dq);  // dS (scale applied to dK at the end)
+          }
         }
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
-          bf16x8 pb = pack8(s, st), db = pack8(dp, st);
 #pragma unroll
           for (int d = 0; d < 2; ++d) {
-            dv[d] = mfma(trf(Dt, 32 * c + 16 * st, 32 * d, lane), pb, dv[d]);
-            dk[d] = mfma(trf(Qt, 32 * c + 16 * st, 32 * d, lane), db, dk[d]);
+            const bf16x8 dta = trf(Dt, 32 * c + 16 * st, 32 * d, lane), qta = trf(Qt, 32 * c + 16 * st, 32 * d, lane);
+#pragma unroll
+            for (int kt = 0; kt < NKT; ++kt) {
+              dv[kt][d] = mfma(dta, pack8(s[kt], st), dv[kt][d]);
+              dk[kt][d] = mfma(qta, pack8(dp[kt], st), dk[kt][d]);
+            }
           }
         }
       }
@@ -399,23 +428,26 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv_kernel(AttnArgs a) {
     if (more) store(buf ^ 1);
     __syncthreads();
   }
-  if (kj >= a.S) return;
   // dV^T / dK^T: lane = key, register rows = d
-  u16* DV = a.dv + off + (long)kj * a.sqs;  // grads use the q/k/v layout
-  u16* DK = a.dk + off + (long)kj * a.sqs;
 #pragma unroll
-  for (int d = 0; d < 2; ++d)
+  for (int kt = 0; kt < NKT; ++kt) {
+    if (kj[kt] >= a.S) continue;
+    u16* DV = a.dv + off + (long)kj[kt] * a.sqs;  // grads use the q/k/v layout
+    u16* DK = a.dk + off + (long)kj[kt] * a.sqs;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      u16x4 x, y;
+    for (int d = 0; d < 2; ++d)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        x[e] = f2bf(dv[d][4 * g + e]);
-        y[e] = f2bf(dk[d][4 * g + e] * a.scale);
+      for (int g = 0; g < 4; ++g) {
+        u16x4 x, y;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x[e] = f2bf(dv[kt][d][4 * g + e]);
+          y[e] = f2bf(dk[kt][d][4 * g + e] * a.scale);
+        }
+        *reinterpret_cast<u16x4*>(DV + 32 * d + 8 * g + 4 * h) = x;
+        *reinterpret_cast<u16x4*>(DK + 32 * d + 8 * g + 4 * h) = y;
       }
-      *reinterpret_cast<u16x4*>(DV + 32 * d + 8 * g + 4 * h) = x;
-      *reinterpret_cast<u16x4*>(DK + 32 * d + 8 * g + 4 * h) = y;
-    }
+  }
 }
 
 // backward, part 2: dQ. Workgroup = 128 queries (wave = 32); loop over key blocks of 64.
@@ -572,7 +604,13 @@ void attention_bwd_bf16(const AttnShape& s, hipStream_t stream) {
   const int nb = (s.S + QB - 1) / QB;
   // dQ first: it computes delta = rowsum(dO * O) for its own queries and writes it for dK/dV
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nb * s.B * s.H), dim3(256), 0, stream, a);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3(nb * s.B * s.H), dim3(256), 0, stream, a);
+  // dK/dV: 256 keys per workgroup (two 32-key tiles per wave, one wave per SIMD) unless knob ATTN_DKDV_KT = 1
+  if (knob(KNOB_ATTN_DKDV_KT) == 2) {
+    const int nk2 = (s.S + 2 * QB - 1) / (2 * QB);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, dim3(nk2 * s.B * s.H), dim3(256), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, dim3(nb * s.B * s.H), dim3(256), 0, stream, a);
+  }
 }
 
 }  // namespace sdml

@@ -49,6 +49,7 @@ const Entry kTable[KNOB_COUNT] = {
     {"U8_SLAB_COLS", 64, false, nullptr},
     {"GEMM_BF16_TR", 1, false, nullptr},
     {"WGRAD_NFAST", -1, false, nullptr},
+    {"ATTN_DKDV_KT", 1, false, nullptr},
     {"U8_FH_ROWS512", 0, false, nullptr},
     {"GEMM_BF16_NOSTORE", 0, true, nullptr},
     {"U8_VARIANT", 0, true, nullptr},

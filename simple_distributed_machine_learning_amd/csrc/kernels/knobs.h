@@ -48,6 +48,7 @@ enum KnobId : int {
   KNOB_U8_SLAB_COLS,         // weight-gradient slab reduction: float4 columns per 1024-thread block (64 or 32)
   KNOB_GEMM_BF16_TR,         // 1 (default): bf16 NT GEMM (4-phase) accumulates C^T: 8-byte row pieces in the epilogue
   KNOB_WGRAD_NFAST,          // bf16 weight gradient tile order: -1 auto (N fastest when gy is larger than the MALL), 0, 1
+  KNOB_ATTN_DKDV_KT,         // attention dK/dV: 32-key tiles per wave (1: 2 waves per SIMD, 2: 1 wave per SIMD)
   KNOB_U8_FH_ROWS512,        // fused uint8 forward + head: 512-row blocks (two head passes): 0 (default, measured no
                              // faster: profiles/r6_fused_rows512_ab.jsonl), 1, -1 auto (when they cover every CU)
   // ---- probe switches (pinned in production builds) ----

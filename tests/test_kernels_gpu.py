@@ -234,6 +234,31 @@ def test_flash_attention_fwd_bwd(B, S, H):
     close(qkv.grad.float(), x.grad, rtol=5e-2, atol=5e-2)
 
 
+@pytest.mark.parametrize("B,S,H", [(1, 64, 1), (1, 200, 3), (2, 1024, 12), (1, 33, 1), (1, 300, 2)])
+def test_flash_attention_dkdv_two_key_tiles_per_wave_bit_identical(B, S, H):
+    """The dK/dV kernel with two 32-key tiles per wave (256 keys per workgroup, one wave per SIMD; knob ATTN_DKDV_KT=2)
+    runs every key tile's MFMA chains in the same order as one tile per wave: bit-identical gradients (ragged S
+    included: the last workgroup's second tile may hold no valid key)."""
+    from simple_distributed_machine_learning_amd import _native
+    from simple_distributed_machine_learning_amd.ops.transformer import causal_attention
+
+    K = _native.kernels()
+    C = 64 * H
+    qkv0 = (rnd(B, S, 3 * C, seed=42) * 1.5).to(torch.bfloat16)
+    gy = rnd(B, S, C, seed=43).to(torch.bfloat16)
+    grads = []
+    try:
+        for kt in (1, 2):
+            K.set_knob("ATTN_DKDV_KT", kt)
+            qkv = qkv0.clone().requires_grad_(True)
+            causal_attention(qkv, H).backward(gy)
+            torch.cuda.synchronize()
+            grads.append(qkv.grad.clone())
+    finally:
+        K.reset_knobs()
+    assert torch.equal(grads[0], grads[1])
+
+
 def test_fused_relu_mask_protocol():
     # head: dx *= (x > 0); linear bwd: skip the gy mask, mask dx by (x > 0)
     M, Kd, C = 1000, 128, 10

@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
     K = kernels()
+    from simple_distributed_machine_learning_amd._native import apply_knobs_from_env
+
+    knobs = apply_knobs_from_env()  # A/B: SDML_KNOBS="ATTN_DKDV_KT=2", ...
     B, S, H, D = a.B, a.S, a.H, 64
     C = H * D
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -58,7 +61,7 @@ def main():
     t_f = timed(lambda: K.attention_fwd(q, k, v, scale, True))
     t_b = timed(lambda: K.attention_bwd(q, k, v, out, dout, lse, dq, dk, dv, scale, True))
     fl_f = 4 * B * H * S * S * D / 2  # causal: half of QK^T and PV
-    print(json.dumps({"B": B, "S": S, "H": H, "fwd_us": round(t_f, 1), "bwd_us": round(t_b, 1),
+    print(json.dumps({"knobs": knobs, "B": B, "S": S, "H": H, "fwd_us": round(t_f, 1), "bwd_us": round(t_b, 1),
                       "fwd_tflops": round(fl_f / t_f / 1e6, 1), "bwd_tflops": round(2.5 * fl_f / t_b / 1e6, 1),
                       "rel_err": {n: round(x, 5) for n, x in err.items()}}), flush=True)
 

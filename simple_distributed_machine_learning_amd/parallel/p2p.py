@@ -25,7 +25,8 @@ transport seam"):
   persistent send slots exported once as hipIPC memory handles, ordered on the device by stream
   memory operations (``hipStreamWriteValue32`` / ``hipStreamWaitValue32``), no host round trip
   (``SDML_TRANSPORT=ipc``; SURVEY.md §2c "hipIPC peer-write fast path with pre-registered
-  persistent buffers"). Collectives stay host-staged.
+  persistent buffers"), the rotate placement's all-to-alls over the same pairwise channels. All-reduces
+  stay host-staged.
 
 :class:`BufferPool` holds the persistent boundary buffers: one per (role, slot), sized on first
 use and reused by every later step, so the step loop allocates no communication memory.
@@ -276,15 +277,16 @@ class HostStagedTransport(Transport):
 class _IpcRecv:
     """An irecv of the IPC transport: ``wait()`` enqueues, on the caller's current stream, the wait for the sender's
     ready word, the copy out of the sender's slot and the acknowledgement (nothing blocks the host once the slot is
-    mapped)."""
+    mapped). ``parts``: several such receives completed by one ``wait()`` (the all-to-all)."""
 
-    def __init__(self, tr, src, t, seq):
-        self.tr, self.src, self.t, self.seq = tr, src, t, seq
+    def __init__(self, tr, parts):
+        self.tr, self.parts = tr, parts
         self._done = False
 
     def wait(self):
         if not self._done:
-            self.tr._consume(self.src, self.t, self.seq)
+            for src, chan, t, seq in self.parts:
+                self.tr._consume(src, chan, t, seq)
             self._done = True
         return True
 
@@ -293,13 +295,15 @@ class _IpcRecv:
 
 
 class IpcTransport(HostStagedTransport):
-    """Point-to-point device tensors between processes through hipIPC (same GPU or peer GPUs of one node).
+    """Device tensors between processes through hipIPC (same GPU or peer GPUs of one node): point-to-point boundary
+    tensors and the rotate placement's all-to-alls; the all-reduces stay host-staged.
 
-    Per ordered channel src -> dst the SENDER owns ``SLOTS`` persistent slot buffers and one control block of int32
-    words: ``ready[s]`` (the sequence number of the last message written into slot s) and ``ack[s]`` (the last one the
-    receiver copied out). Both are exported once as IPC memory handles through the job's rendezvous store and opened
-    once by the receiver. Messages on a channel are FIFO (the schedule matches every send with a recv in order), so
-    message k of a channel uses slot (k - 1) % SLOTS on both sides and nothing but the payload travels per message:
+    Per ordered channel (src -> dst, stream name) the SENDER owns ``SLOTS`` persistent slot buffers and one control
+    block of int32 words: ``ready[s]`` (the sequence number of the last message written into slot s) and ``ack[s]``
+    (the last one the receiver copied out). Both are exported once as IPC memory handles through the job's rendezvous
+    store and opened once by the receiver. Messages on a channel are FIFO (the schedule matches every send with a recv
+    in order; an all-to-all is one message per peer on its own stream name), so message k of a channel uses slot
+    (k - 1) % SLOTS on both sides and nothing but the payload travels per message:
 
     * ``isend`` (sender's current stream): wait until ``ack[s] >= k - SLOTS`` (the slot's previous message was taken),
       copy the tensor into the slot, write ``ready[s] = k``;
@@ -309,10 +313,9 @@ class IpcTransport(HostStagedTransport):
     Slot buffers come in power-of-two capacity classes (>= 64 KiB) that both sides derive from the message size, so
     a ragged last batch uses its own buffer without any negotiation. The words are written and waited on by the
     streams' command processors (hipStreamWriteValue32 / hipStreamWaitValue32 in ``_kernels``), so the hand-off is
-    ordered on the device like an RCCL send / recv; all-to-all and all-reduce stay on the host-staged Gloo path
-    (the engine's rotate and data-parallel collectives). The reference's hand-off this replaces is
-    ``RRef(z3)`` + ``rpc_sync().forward`` + ``to_here()`` (/root/reference/simple_distributed.py:47-49, :71) and the
-    gradient's way back (:112)."""
+    ordered on the device like an RCCL send / recv. The reference's hand-off this replaces is ``RRef(z3)`` +
+    ``rpc_sync().forward`` + ``to_here()`` (/root/reference/simple_distributed.py:47-49, :71) and the gradient's way
+    back (:112)."""
 
     name = "ipc"
     SLOTS = 16
@@ -326,20 +329,21 @@ class IpcTransport(HostStagedTransport):
         IpcTransport._instances += 1
         self.prefix = f"sdml_ipc/{IpcTransport._instances}"
         self.store = dist.distributed_c10d._get_default_store()
-        self._send_seq: Dict[int, int] = {}
-        self._recv_seq: Dict[int, int] = {}
-        self._send_ctrl: Dict[int, torch.Tensor] = {}
-        self._recv_ctrl: Dict[int, torch.Tensor] = {}
+        self._send_seq: Dict[tuple, int] = {}
+        self._recv_seq: Dict[tuple, int] = {}
+        self._send_ctrl: Dict[tuple, torch.Tensor] = {}
+        self._recv_ctrl: Dict[tuple, torch.Tensor] = {}
         self._send_bufs: Dict[tuple, torch.Tensor] = {}
         self._recv_bufs: Dict[tuple, torch.Tensor] = {}
+        self._group_ranks: Dict[str, List[int]] = {}
         self.registered = 0  # buffers exported (sender side) + opened (receiver side): tests assert it stops growing
         from .._native import kernels
 
         self.k = kernels()
 
     # ---- registration (once per channel / slot / capacity class) ------------------------------------------------
-    def _key(self, src, dst, what):
-        return f"{self.prefix}/{src}->{dst}/{what}"
+    def _key(self, src, dst, chan, what):
+        return f"{self.prefix}/{src}->{dst}/{chan}/{what}"
 
     def _export(self, key, t):
         import pickle
@@ -360,31 +364,32 @@ class IpcTransport(HostStagedTransport):
     def _cls(cls, nbytes):
         return max(cls.MIN_CLASS, 1 << max(0, int(nbytes - 1).bit_length()))
 
-    def _ctrl_out(self, dst):
-        c = self._send_ctrl.get(dst)
+    def _ctrl_out(self, dst, chan):
+        c = self._send_ctrl.get((dst, chan))
         if c is None:
-            c = self._send_ctrl[dst] = torch.zeros(2 * self.SLOTS, dtype=torch.int32, device=self.mesh.device)
+            c = self._send_ctrl[(dst, chan)] = torch.zeros(2 * self.SLOTS, dtype=torch.int32, device=self.mesh.device)
             torch.cuda.synchronize(self.mesh.device)  # zeroed before the peer can map it
-            self._export(self._key(self.mesh.rank, dst, "ctrl"), c)
+            self._export(self._key(self.mesh.rank, dst, chan, "ctrl"), c)
         return c
 
-    def _ctrl_in(self, src):
-        c = self._recv_ctrl.get(src)
+    def _ctrl_in(self, src, chan):
+        c = self._recv_ctrl.get((src, chan))
         if c is None:
-            c = self._recv_ctrl[src] = self._open(self._key(src, self.mesh.rank, "ctrl"))
+            c = self._recv_ctrl[(src, chan)] = self._open(self._key(src, self.mesh.rank, chan, "ctrl"))
         return c
 
-    def _slot_out(self, dst, slot, cls):
-        b = self._send_bufs.get((dst, slot, cls))
+    def _slot_out(self, dst, chan, slot, cls):
+        b = self._send_bufs.get((dst, chan, slot, cls))
         if b is None:
-            b = self._send_bufs[(dst, slot, cls)] = torch.empty(cls, dtype=torch.uint8, device=self.mesh.device)
-            self._export(self._key(self.mesh.rank, dst, f"s{slot}c{cls}"), b)
+            b = self._send_bufs[(dst, chan, slot, cls)] = torch.empty(cls, dtype=torch.uint8, device=self.mesh.device)
+            self._export(self._key(self.mesh.rank, dst, chan, f"s{slot}c{cls}"), b)
         return b
 
-    def _slot_in(self, src, slot, cls):
-        b = self._recv_bufs.get((src, slot, cls))
+    def _slot_in(self, src, chan, slot, cls):
+        b = self._recv_bufs.get((src, chan, slot, cls))
         if b is None:
-            b = self._recv_bufs[(src, slot, cls)] = self._open(self._key(src, self.mesh.rank, f"s{slot}c{cls}"))
+            b = self._recv_bufs[(src, chan, slot, cls)] = self._open(self._key(src, self.mesh.rank, chan,
+                                                                               f"s{slot}c{cls}"))
         return b
 
     @staticmethod
@@ -392,35 +397,41 @@ class IpcTransport(HostStagedTransport):
         return t.reshape(-1).view(torch.uint8)
 
     # ---- point to point ------------------------------------------------------------------------------------------
-    def isend(self, t, dst, tag):
+    def _send(self, t, dst, chan):
         t = t.detach().contiguous()
         n = t.numel() * t.element_size()
-        k = self._send_seq.get(dst, 0) + 1
-        self._send_seq[dst] = k
+        k = self._send_seq.get((dst, chan), 0) + 1
+        self._send_seq[(dst, chan)] = k
         slot = (k - 1) % self.SLOTS
-        ctrl = self._ctrl_out(dst)
-        buf = self._slot_out(dst, slot, self._cls(n))
+        ctrl = self._ctrl_out(dst, chan)
+        buf = self._slot_out(dst, chan, slot, self._cls(n))
         if k > self.SLOTS:  # the receiver has copied out this slot's previous message
             self.k.stream_wait_value32(ctrl.data_ptr() + 4 * (self.SLOTS + slot), k - self.SLOTS)
         if n:
             buf[:n].copy_(self._bytes(t))
         self.k.stream_write_value32(ctrl.data_ptr() + 4 * slot, k)
-        self.bytes_sent += n
+        return n
+
+    def _post_recv(self, src, chan, t):
+        k = self._recv_seq.get((src, chan), 0) + 1
+        self._recv_seq[(src, chan)] = k
+        return (src, chan, t, k)
+
+    def isend(self, t, dst, tag):
+        self.bytes_sent += self._send(t, dst, "p2p")
         self.ops += 1
         return _Done()
 
     def irecv(self, t, src, tag):
-        k = self._recv_seq.get(src, 0) + 1
-        self._recv_seq[src] = k
         self.bytes_recv += t.numel() * t.element_size()
         self.ops += 1
-        return _IpcRecv(self, src, t, k)
+        return _IpcRecv(self, [self._post_recv(src, "p2p", t)])
 
-    def _consume(self, src, t, k):
+    def _consume(self, src, chan, t, k):
         n = t.numel() * t.element_size()
         slot = (k - 1) % self.SLOTS
-        ctrl = self._ctrl_in(src)
-        buf = self._slot_in(src, slot, self._cls(n))
+        ctrl = self._ctrl_in(src, chan)
+        buf = self._slot_in(src, chan, slot, self._cls(n))
         self.k.stream_wait_value32(ctrl.data_ptr() + 4 * slot, k)
         if n:
             if t.is_contiguous():
@@ -428,6 +439,42 @@ class IpcTransport(HostStagedTransport):
             else:
                 t.copy_(buf[:n].view(t.dtype).view(t.shape))
         self.k.stream_write_value32(ctrl.data_ptr() + 4 * (self.SLOTS + slot), k)
+
+    # ---- all-to-all over the pairwise channels ---------------------------------------------------------------------
+    def _ranks(self, channel):
+        r = self._group_ranks.get(channel)
+        if r is None:
+            g = self._channel(channel)
+            r = self._group_ranks[channel] = (list(range(dist.get_world_size())) if g is None
+                                              else dist.get_process_group_ranks(g))
+        return r
+
+    def all_to_all(self, out, inp, out_splits, in_splits, channel="fwd"):
+        """``out`` gets out_splits[j] rows from group member j, member j gets in_splits[j] rows of ``inp`` (the
+        torch all_to_all_single contract, first dimension split): one message per peer on stream name
+        ``a2a-<channel>``, the own part copied locally; ``wait()`` consumes the peers' parts on the caller's stream."""
+        row = (inp[0].numel() if inp.dim() > 1 else 1) * inp.element_size() if inp.numel() else 0
+        self._count_a2a(out_splits, in_splits, row)
+        self.ops += 1
+        ranks = self._ranks(channel)
+        me = self.mesh.rank
+        chan = f"a2a-{channel}"
+        io = [0]
+        for s in in_splits:
+            io.append(io[-1] + int(s))
+        oo = [0]
+        for s in out_splits:
+            oo.append(oo[-1] + int(s))
+        parts = []
+        for j, r in enumerate(ranks):
+            src_part, dst_part = inp[io[j]:io[j + 1]], out[oo[j]:oo[j + 1]]
+            if r == me:
+                if dst_part.numel():
+                    dst_part.copy_(src_part)
+                continue
+            self._send(src_part, r, chan)
+            parts.append(self._post_recv(r, chan, dst_part))
+        return _IpcRecv(self, parts)
 
     def drain_sends(self):
         self._pending_sends.clear()  # (sends are stream-ordered device copies: nothing to wait for on the host)

@@ -79,6 +79,31 @@ def test_rotate_multirank_on_device(world, mode, monkeypatch):
     assert all(r["pool_allocs"] == r["pool_allocs_first"] for r in res)  # persistent boundary buffers
 
 
+@pytest.mark.parametrize("world,mode", [(2, "factored"), (4, "u8"), (2, "u8_phi")])
+def test_rotate_multirank_ipc_all_to_all(world, mode):
+    """The rotate placement with its boundary all-to-alls device to device between the processes (IpcTransport: one
+    message per peer over the pairwise slot channels, the own part copied locally): same weights as the host-staged
+    run, bit for bit (only the transport differs), and as the single-process GPU engine."""
+    runs = {}
+    for tr in ("host", "ipc"):
+        kw = dict(GPU, transport=tr)
+        steps, M, B = 2, 2 * world, 48
+        if mode.startswith("u8"):
+            kw["pixels"] = "u8"
+            B = 8192
+        if mode == "u8_phi":
+            kw["cross_fraction"] = 0.25
+        runs[tr] = run_ranks(train_worker, world, "mlp", "rotate", M, world, steps, B, 3, kw, timeout=400)
+    ref = _single("mlp", M, steps, world * B, "rotate", {"pixels": "u8" if mode.startswith("u8") else "f32"})
+    _compare(runs["ipc"], ref, transport="ipc")
+    assert all(r["bytes_sent"] > 0 for r in runs["ipc"])
+    for a, b in zip(runs["ipc"], runs["host"]):
+        assert a["bytes_sent"] == b["bytes_sent"]
+        for s_, sd in a["state"].items():
+            for k, v in sd.items():
+                torch.testing.assert_close(v, b["state"][s_][k], rtol=0, atol=0, msg=f"{s_} {k}")
+
+
 _NEIGHBOUR = {}
 
 

@@ -38,7 +38,10 @@ def _time(fn, dev, reps: int, warm: int = 2) -> float:
     _sync(dev)
     ts = []
     for _ in range(reps):
-        dist.barrier()
+        if dev.type == "cuda" and dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[dev.index])
+        else:
+            dist.barrier()
         _sync(dev)
         t0 = time.perf_counter()
         fn()

@@ -295,8 +295,9 @@ class _IpcRecv:
 
 
 class IpcTransport(HostStagedTransport):
-    """Device tensors between processes through hipIPC (same GPU or peer GPUs of one node): point-to-point boundary
-    tensors and the rotate placement's all-to-alls; the all-reduces stay host-staged.
+    """Device tensors between processes through hipIPC: point-to-point boundary tensors and the rotate placement's
+    all-to-alls; the all-reduces stay host-staged. Exercised with processes sharing one GPU (the 1-GPU pool); between
+    GPUs of a node the same handles need peer access between the devices.
 
     Per ordered channel (src -> dst, stream name) the SENDER owns ``SLOTS`` persistent slot buffers and one control
     block of int32 words: ``ready[s]`` (the sequence number of the last message written into slot s) and ``ack[s]``

@@ -146,3 +146,31 @@ def test_kernel_knobs_pin_timing_probes_in_production_builds():
         K.set_knob("NO_SUCH_KNOB", 1)
     K.set_knob("WGRAD_DMA", 0)
     K.reset_knobs()
+
+
+def test_flat_params_row_padding_stays_zero_under_sgd():
+    """FlatParams row padding (a module's ``flat_row_multiple``, GPT-2's lm_head vocabulary): the rows past the
+    parameter's own are zero in the parameter and gradient storage, views are unchanged in shape and name, and SGD with
+    momentum keeps the pad rows zero (their gradient is zero)."""
+    from simple_distributed_machine_learning_amd.ops.optim import FusedSGD
+
+    torch.manual_seed(0)
+    m = torch.nn.Linear(6, 13, bias=True)
+    m.flat_row_multiple = {"weight": 8}
+    flat = FlatParams([(0, m)], "cpu")
+    w = m.weight
+    assert tuple(w.shape) == (13, 6) and w._sdml_rows_padded == 16
+    padded = w.as_strided((16, 6), (6, 1))
+    assert torch.equal(padded[:13], w) and int((padded[13:] != 0).sum()) == 0
+    gpad = w.grad.as_strided((16, 6), (6, 1))
+    opt = FusedSGD(flat, lr=0.1, momentum=0.5)
+    for _ in range(3):
+        flat.zero_grad(force=True)
+        x = torch.randn(4, 6)
+        m(x).square().sum().backward()
+        opt.step()
+    assert int((padded[13:] != 0).sum()) == 0 and int((gpad[13:] != 0).sum()) == 0
+    assert set(dict(m.named_parameters())) == {"weight", "bias"}
+    # the bias segment starts after the padded rows (64-element aligned offsets)
+    seg = {s.name: s for s in flat.segments}
+    assert seg["bias"].offset >= seg["weight"].offset + 16 * 6

@@ -25,8 +25,8 @@ transport seam"):
   persistent send slots exported once as hipIPC memory handles, ordered on the device by stream
   memory operations (``hipStreamWriteValue32`` / ``hipStreamWaitValue32``), no host round trip
   (``SDML_TRANSPORT=ipc``; SURVEY.md §2c "hipIPC peer-write fast path with pre-registered
-  persistent buffers"), the rotate placement's all-to-alls over the same pairwise channels. All-reduces
-  stay host-staged.
+  persistent buffers"), the rotate placement's all-to-alls over the same pairwise channels, and the
+  gradient all-reduce over the mapped flat-gradient slices.
 
 :class:`BufferPool` holds the persistent boundary buffers: one per (role, slot), sized on first
 use and reused by every later step, so the step loop allocates no communication memory.
@@ -295,9 +295,9 @@ class _IpcRecv:
 
 
 class IpcTransport(HostStagedTransport):
-    """Device tensors between processes through hipIPC: point-to-point boundary tensors and the rotate placement's
-    all-to-alls; the all-reduces stay host-staged. Exercised with processes sharing one GPU (the 1-GPU pool); between
-    GPUs of a node the same handles need peer access between the devices.
+    """Device tensors between processes through hipIPC: point-to-point boundary tensors, the rotate placement's
+    all-to-alls and the data-parallel gradient all-reduce (other all-reduces stay host-staged). Exercised with
+    processes sharing one GPU (the 1-GPU pool); between GPUs of a node the same handles need peer access.
 
     Per ordered channel (src -> dst, stream name) the SENDER owns ``SLOTS`` persistent slot buffers and one control
     block of int32 words: ``ready[s]`` (the sequence number of the last message written into slot s) and ``ack[s]``
@@ -337,6 +337,9 @@ class IpcTransport(HostStagedTransport):
         self._send_bufs: Dict[tuple, torch.Tensor] = {}
         self._recv_bufs: Dict[tuple, torch.Tensor] = {}
         self._group_ranks: Dict[str, List[int]] = {}
+        self._ar_reg: Dict[tuple, dict] = {}
+        self._ar_ctrl = None
+        self._ar_seq = 0
         self.registered = 0  # buffers exported (sender side) + opened (receiver side): tests assert it stops growing
         from .._native import kernels
 
@@ -476,6 +479,49 @@ class IpcTransport(HostStagedTransport):
             self._send(src_part, r, chan)
             parts.append(self._post_recv(r, chan, dst_part))
         return _IpcRecv(self, parts)
+
+    # ---- gradient all-reduce over the mapped buffers -------------------------------------------------------------
+    def all_reduce(self, t, group=None, channel=None, op=dist.ReduceOp.SUM, async_op=True):
+        """The data-parallel gradient sum (channel "grad": slices of the persistent flat gradient buffer) device to
+        device: every member maps every other member's buffer once (registered in call order, which is the same on
+        every rank), then per call, on the caller's stream: publish ``ready`` = k, wait for every member's ``ready``,
+        sum the members' buffers in rank order into a temporary (the same bits on every rank), publish ``done`` = k,
+        wait for every member's ``done`` (nobody still reads this buffer), copy the sum back. Other all-reduces
+        (metrics, tensor-parallel partial sums on fresh tensors, MIN / MAX) stay host-staged."""
+        if (channel != "grad" or op != dist.ReduceOp.SUM or t.device.type != "cuda" or not t.is_contiguous()
+                or t.numel() == 0):
+            return super().all_reduce(t, group=group, channel=channel, op=op, async_op=async_op)
+        ranks = self._ranks("grad")
+        me = self.mesh.rank
+        self.ops += 1
+        key = (t.data_ptr(), t.numel(), t.dtype)
+        reg = self._ar_reg.get(key)
+        if reg is None:  # first use of this buffer: export it, map every member's (same registration index)
+            idx = len(self._ar_reg)
+            self._export(self._key(me, "all", "ar", f"b{idx}"), t)
+            peers = {r: (t if r == me else self._open(self._key(r, "all", "ar", f"b{idx}"))) for r in ranks}
+            reg = self._ar_reg[key] = peers
+        if self._ar_ctrl is None:  # [ready, done] words per member
+            c = torch.zeros(2, dtype=torch.int32, device=self.mesh.device)
+            torch.cuda.synchronize(self.mesh.device)
+            self._export(self._key(me, "all", "ar", "ctrl"), c)
+            self._ar_ctrl = {r: (c if r == me else self._open(self._key(r, "all", "ar", "ctrl"))) for r in ranks}
+        self._ar_seq += 1
+        k = self._ar_seq
+        ctrl = self._ar_ctrl
+        self.k.stream_write_value32(ctrl[me].data_ptr(), k)
+        for r in ranks:
+            if r != me:
+                self.k.stream_wait_value32(ctrl[r].data_ptr(), k)
+        acc = reg[ranks[0]].clone()
+        for r in ranks[1:]:
+            acc.add_(reg[r])
+        self.k.stream_write_value32(ctrl[me].data_ptr() + 4, k)
+        for r in ranks:
+            if r != me:
+                self.k.stream_wait_value32(ctrl[r].data_ptr() + 4, k)
+        t.copy_(acc)  # (bytes_sent counts boundary tensors only, as in the other transports)
+        return _Done()
 
     def drain_sends(self):
         self._pending_sends.clear()  # (sends are stream-ordered device copies: nothing to wait for on the host)

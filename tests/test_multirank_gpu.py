@@ -158,14 +158,15 @@ def test_bench_two_ranks_on_one_gpu():
     process), its ranks sharing the GPU through the host-staged transport: one JSON line, the
     placement's measured boundary bytes, the rank count the process group saw."""
     env = dict(os.environ, SDML_TRANSPORT="host", SDML_BENCH_BATCH="8192", PYTHONPATH=ROOT)
-    for place, cross in (("rotate", True), ("auto", None)):
+    for place, cross, tr in (("rotate", True, "host"), ("auto", None, "host"), ("rotate", True, "ipc")):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
                "--gpus", "2", "--steps", "3", "--warmup", "1", "--placement", place]
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+        r = subprocess.run(cmd, env=dict(env, SDML_TRANSPORT=tr), capture_output=True, text=True, timeout=300,
+                           cwd=ROOT)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
         d = _bench_json(r)
-        assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["transport"] == "host"
+        assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["transport"] == tr
         assert d["config"]["world_size_seen"] == 2 and d["config"]["backend"] == "gloo"
         if cross:
             assert d["config"]["boundary_bytes_across_gpus_per_step"] == 2 * 4096 * (512 + 40)

@@ -353,17 +353,22 @@ void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const v
 
 void bn_nhwc_bwd_bf16(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
                       const void* gamma, int M, int C, bool relu, void* dx, void* dres, void* ggamma, void* gbeta,
-                      float* workspace, hipStream_t stream, const void* beta) {
+                      float* workspace, hipStream_t stream, const void* beta, const float* part_in, int part_rows) {
   int rpb;
-  const int nblk = bn_blocks(M, C, &rpb);
-  float* part = workspace;
+  int nblk = bn_blocks(M, C, &rpb);
+  const float* part = workspace;
   float* coef = workspace + (size_t)nblk * 2 * C;  // [3][C]
   // ReLU mask: from y when given, else recomputed from x (needs beta; BatchNorm + ReLU, no residual)
   const int rmode = !relu ? 0 : (y ? 1 : 2);
   const u16 *gp = static_cast<const u16*>(gamma), *bp = static_cast<const u16*>(beta);
-  hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(nblk), dim3(BT), 0, stream, static_cast<const u16*>(x),
-                     static_cast<const u16*>(dy), static_cast<const u16*>(y), mean, rstd, gp, bp, M, C, rpb, rmode,
-                     part);
+  if (part_in) {  // the convolution that produced dy summed g and g * xhat per tile (conv_bf16.hip BnBack)
+    part = part_in;
+    nblk = part_rows;
+  } else {
+    hipLaunchKernelGGL(bn_partial_kernel<true>, dim3(nblk), dim3(BT), 0, stream, static_cast<const u16*>(x),
+                       static_cast<const u16*>(dy), static_cast<const u16*>(y), mean, rstd, gp, bp, M, C, rpb, rmode,
+                       workspace);
+  }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(BT), 0, stream, part, nblk, C, M,
                      rstd, gp, static_cast<u16*>(ggamma), static_cast<u16*>(gbeta), coef);
   const int64_t n8 = (int64_t)M * C / 8;

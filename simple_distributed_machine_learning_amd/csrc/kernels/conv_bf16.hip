@@ -49,6 +49,21 @@ __device__ __forceinline__ bf16x8 rowf(const u16* X, int row, int s, int h) {
   return *reinterpret_cast<const bf16x8*>(X + swz(row, 2 * s + h));
 }
 
+// BatchNorm backward statistics of a stored output tile: when the output is the input gradient dy of a
+// training BatchNorm (x its forward input, same layout), the epilogue sums g = dy * mask and g * xhat per
+// channel (xhat = (x - mean) * rstd; mask 1, y > 0 from its saved output, or x * gamma rstd + beta - mean
+// gamma rstd > 0 recomputed from x, exactly as batchnorm_nhwc.hip's bn_partial_kernel), so the backward
+// skips its statistics pass over dy and x.
+struct BnBack {
+  const u16* x = nullptr;  // null: off
+  const u16* y = nullptr;  // relu 1: the saved output
+  const float* mean = nullptr;
+  const float* rstd = nullptr;
+  const u16* gamma = nullptr;
+  const u16* beta = nullptr;
+  int relu = 0;  // 0 none, 1 mask from y, 2 mask recomputed from x
+};
+
 struct ConvArgs {
   const u16* x;  // NHWC input [Nb][H][W][C]
   const u16* w;  // [Co][KS*KS][C]
@@ -59,6 +74,7 @@ struct ConvArgs {
   int OH, OW, S, KS, P;  // output size, stride, kernel size (3 or 1), padding (the halo kernel: 1 / 3 / 1)
   const u16* add;  // optional addend in y's layout: y = bf16(acc + add) (the residual branch's input gradient)
   float* part;     // optional BatchNorm partials [tiles_m][2][Co]: per-tile sums of y and y^2 (bf16-rounded y)
+  BnBack bb;       // bb.x set: part holds the backward sums of g and g * xhat instead (BnBack)
 };
 
 // Output tile store shared by the im2col, halo and strided-dgrad kernels. The MFMA accumulators
@@ -70,16 +86,22 @@ struct ConvArgs {
 // the rounding of the separate add it replaces) and the optional BatchNorm partials of the stored y:
 // per channel, sums of y and y^2 over the tile's rows in a fixed order (the thread's rows, then the
 // row groups through LDS), written to part_row[0][0..BN) and part_row[0][Co..Co+BN) - the forward
-// BatchNorm (batchnorm_nhwc.hip) then finalizes these rows instead of re-reading y.
+// BatchNorm (batchnorm_nhwc.hip) then finalizes these rows instead of re-reading y. With bb.x set the two sums
+// are the BatchNorm backward's instead (BnBack: sums of g and g * xhat of the stored y as that BatchNorm's dy).
 // LDS: max(BM * (BN + 8) * 2, 32 KB) bytes; the caller's main loop has finished with its images.
 constexpr int store_tile_lds(int BN) { return BM * (BN + 8) * 2 > 32768 ? BM * (BN + 8) * 2 : 32768; }
 
 template <int TM, int WTM, int WGM, int BN, int EPI, class RowOff>
 __device__ __forceinline__ void store_tile(const f32x16 (&acc)[TM][2], int wm, int wn, int lane, u16* lds,
                                            RowOff rowoff, u16* __restrict__ y, const u16* __restrict__ add,
-                                           float* __restrict__ part_row, int Co) {
+                                           float* __restrict__ part_row, int Co, const BnBack& bb = BnBack(),
+                                           int n0 = 0) {
   constexpr int LP = BN + 8;
+  constexpr int CPR = BN / 8;    // 16-B chunks per row
+  constexpr int RPP = NT / CPR;  // rows per pass
+  constexpr int NR = BM / RPP;   // rows per thread
   const int h = lane >> 5;
+  const int t = threadIdx.x, c = t % CPR, r0 = t / CPR;
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -92,26 +114,60 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[TM][2], int wm, i
         lds[row * LP + col] = f2bf(acc[i][j][r]);
       }
     }
+  // every global operand of the thread's rows is loaded before the barrier (one memory latency for the whole
+  // epilogue instead of one per row: the stores to y would otherwise order each row's loads after the last row's)
+  long long offs[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) offs[k] = rowoff(r0 + k * RPP);
+  const bool bwd = EPI == 1 && part_row && bb.x;
+  u16x8 av[NR], xv[NR], yv[NR];
+  float mu[8], rs[8], sc[8], sh[8];  // backward statistics (bb.x): this thread's 8 channels' coefficients
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const long long o = (offs[k] < 0 ? 0 : offs[k]) + 8 * c;
+      av[k] = add ? *reinterpret_cast<const u16x8*>(add + o) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      xv[k] = bwd ? *reinterpret_cast<const u16x8*>(bb.x + o) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      yv[k] = bwd && bb.relu == 1 ? *reinterpret_cast<const u16x8*>(bb.y + o) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    if (bwd) {
+      const u16x8 gm = *reinterpret_cast<const u16x8*>(bb.gamma + n0 + 8 * c);
+      const u16x8 bt = *reinterpret_cast<const u16x8*>(bb.beta + n0 + 8 * c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        mu[e] = bb.mean[n0 + 8 * c + e];
+        rs[e] = bb.rstd[n0 + 8 * c + e];
+        sc[e] = bf2f(gm[e]) * rs[e];
+        sh[e] = bf2f(bt[e]) - mu[e] * sc[e];
+      }
+    }
+  }
   __syncthreads();
-  constexpr int CPR = BN / 8;    // 16-B chunks per row
-  constexpr int RPP = NT / CPR;  // rows per pass
-  const int t = threadIdx.x, c = t % CPR, r0 = t / CPR;
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
 #pragma unroll
-  for (int k = 0; k < BM / RPP; ++k) {
+  for (int k = 0; k < NR; ++k) {
     const int rr = r0 + k * RPP;
-    const long long off = rowoff(rr);
+    const long long off = offs[k];
     if (off < 0) continue;
     u16x8 v = *reinterpret_cast<const u16x8*>(lds + rr * LP + 8 * c);
     if constexpr (EPI == 1) {
       if (add) {
-        const u16x8 av = *reinterpret_cast<const u16x8*>(add + off + 8 * c);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(av[e]));
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) + bf2f(av[k][e]));
       }
-      if (part_row) {
+      if (bwd) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float g = bf2f(v[e]);
+          const float xf = bf2f(xv[k][e]);
+          if (bb.relu == 1 && !(bf2f(yv[k][e]) > 0.f)) g = 0.f;
+          if (bb.relu == 2 && !(__builtin_fmaf(xf, sc[e], sh[e]) > 0.f)) g = 0.f;
+          s1[e] += g;
+          s2[e] += g * (xf - mu[e]) * rs[e];
+        }
+      } else if (part_row) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float f = bf2f(v[e]);
@@ -151,7 +207,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, const f32x16 (&
   const int M = a.M, Co = a.Co;
   auto rowoff = [=](int r) -> long long { return m0 + r < M ? (long long)(m0 + r) * Co + n0 : -1; };
   store_tile<TM, WTM, WGM, BN, EPI>(acc, wm, wn, lane, lds, rowoff, a.y, a.add,
-                                    a.part ? a.part + (size_t)tm * 2 * Co + n0 : nullptr, Co);
+                                    a.part ? a.part + (size_t)tm * 2 * Co + n0 : nullptr, Co, a.bb, n0);
 }
 
 template <int BN, int EPI>  // EPI: 0 plain store, 1 addend and/or BatchNorm partials (conv_epilogue)
@@ -272,6 +328,8 @@ struct DgArgs {
   u16* dx;        // [Nb][H][W][Cn]
   const u16* add;  // optional addend in dx's layout (dx = bf16(acc + add))
   int Nb, H, W, OH, OW, Cg, Cn, KS, P, tiles_n, tiles;
+  float* part;     // optional BatchNorm backward partials of dx (BnBack), one row per class pixel tile:
+  BnBack bb;       // [sum over classes of tiles_m][2][Cn], the classes in dg_order
 };
 
 struct DgClass {
@@ -424,7 +482,8 @@ __global__ void __launch_bounds__(NT) conv_dgrad_s2_kernel(DgArgs a) {
     const int iy = 2 * (q % Ha) + cpy, n = q / Ha;
     return (((long long)n * H + iy) * W + ix) * Cn + n0;
   };
-  store_tile<TM, WTM, WGM, BN, 1>(acc, wm, wn, lane, smem, rowoff, a.dx, a.add, nullptr, Cn);
+  float* prow = a.part ? a.part + ((size_t)(c.tile0 / a.tiles_n + tm) * 2 * Cn + n0) : nullptr;
+  store_tile<TM, WTM, WGM, BN, 1>(acc, wm, wn, lane, smem, rowoff, a.dx, a.add, prow, Cn, a.bb, n0);
 }
 
 // torch weight [Cg][Cn][KS][KS] -> the parity classes' packed [Cn][taps][Cg] images (dg_class)
@@ -1190,11 +1249,29 @@ static void launch_im2col(ConvArgs& a, bool bn128, hipStream_t stream) {
   else hipLaunchKernelGGL((conv3x3_fwd_kernel<64, 0>), grid, block, 0, stream, a);
 }
 
+static BnBack bn_back(const ConvBnBack* b) {
+  BnBack r;
+  if (b && b->x) {
+    r.x = static_cast<const u16*>(b->x);
+    r.y = static_cast<const u16*>(b->y);
+    r.mean = b->mean;
+    r.rstd = b->rstd;
+    r.gamma = static_cast<const u16*>(b->gamma);
+    r.beta = static_cast<const u16*>(b->beta);
+    r.relu = b->relu;
+    if (r.relu == 1 && !r.y) abort();  // host contract: the mask source is given
+    if (!r.mean || !r.rstd || !r.gamma || !r.beta) abort();
+  }
+  return r;
+}
+
 void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co,
-                      hipStream_t stream, const void* add, float* part) {
+                      hipStream_t stream, const void* add, float* part, const ConvBnBack* bnb) {
   ConvArgs a;
   a.add = static_cast<const u16*>(add);
   a.part = part;
+  a.bb = bn_back(bnb);
+  if (a.bb.x && !part) abort();  // host contract: the backward statistics need their partial rows
   a.x = static_cast<const u16*>(x);
   a.w = static_cast<const u16*>(wt);
   a.y = static_cast<u16*>(y);
@@ -1259,6 +1336,7 @@ void conv_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W,
   ConvArgs a;
   a.add = static_cast<const u16*>(add);
   a.part = part;
+  a.bb = BnBack();
   a.x = static_cast<const u16*>(x);
   a.w = static_cast<const u16*>(wt);
   a.y = static_cast<u16*>(y);
@@ -1277,6 +1355,11 @@ void conv_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W,
   launch_im2col(a, Co % 128 == 0 && a.tiles_m * (Co / 128) >= 160, stream);
 }
 
+int conv_dgrad_s2_part_rows(int Nb, int H, int W, int ks, int pad) {
+  const DgClass last = dg_class(3, Nb, H, W, ks, pad, 64, 64, 1);
+  return last.tile0 + last.tiles_m;  // tiles_n = 1: tile0 counts the earlier classes' pixel tiles
+}
+
 size_t conv_dgrad_s2_weight_elems(int Co, int C, int ks) { return (size_t)Co * C * ks * ks; }
 
 void conv_dgrad_s2_weight_bf16(const void* w_torch, void* packed, int Co, int C, int ks, int pad, hipStream_t stream) {
@@ -1287,9 +1370,12 @@ void conv_dgrad_s2_weight_bf16(const void* w_torch, void* packed, int Co, int C,
 }
 
 void conv_dgrad_s2_bf16(const void* dy, const void* packed, void* dx, int Nb, int H, int W, int C, int Co, int ks,
-                        int pad, hipStream_t stream, const void* add) {
+                        int pad, hipStream_t stream, const void* add, float* part, const ConvBnBack* bnb) {
   DgArgs a;
   a.add = static_cast<const u16*>(add);
+  a.part = part;
+  a.bb = bn_back(bnb);
+  if (a.bb.x && !part) abort();  // host contract: the backward statistics need their partial rows
   a.dy = static_cast<const u16*>(dy);
   a.w = static_cast<const u16*>(packed);
   a.dx = static_cast<u16*>(dx);

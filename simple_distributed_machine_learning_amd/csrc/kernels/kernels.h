@@ -364,8 +364,21 @@ void conv3x3_weight_transform_batched_bf16(const void* const* w, void* const* fw
 // add (optional, y's layout): y = bf16(conv + add). part (optional): BatchNorm partials of y,
 // [conv_part_rows(Nb, OH, OW)][2][Co] fp32 (per 256-pixel tile: sum y, sum y^2), for bn_nhwc_fwd_bf16.
 int conv_part_rows(int Nb, int OH, int OW);
+// bnb (optional, with part): y is the input gradient dy of a training BatchNorm whose forward input x has y's layout;
+// part then receives that BatchNorm backward's per-tile sums of g = dy * mask and g * (x - mean) * rstd (for
+// bn_nhwc_bwd_bf16's part) instead of the forward statistics. relu: 0 none, 1 mask y_bn > 0 (y_bn = the
+// BatchNorm's saved output), 2 mask recomputed from x, gamma, beta, mean, rstd.
+struct ConvBnBack {
+  const void* x = nullptr;
+  const void* y = nullptr;
+  const float* mean = nullptr;
+  const float* rstd = nullptr;
+  const void* gamma = nullptr;
+  const void* beta = nullptr;
+  int relu = 0;
+};
 void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W, int C, int Co, hipStream_t stream,
-                      const void* add = nullptr, float* part = nullptr);
+                      const void* add = nullptr, float* part = nullptr, const ConvBnBack* bnb = nullptr);
 // gw_torch [Co][C][3][3] bf16 += dw; workspace: conv3x3_wgrad_workspace_floats(...) fp32
 // general bf16 NHWC convolution on the implicit-GEMM kernels: kernel 3 (pad 1) or 1 (pad 0), stride 1
 // or 2, C and Co multiples of 64. Forward (im2col kernel; wt = [Co][ks*ks][C]) and weight gradient
@@ -379,8 +392,11 @@ void conv_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int W,
                    int pad, hipStream_t stream, const void* add = nullptr, float* part = nullptr);
 size_t conv_dgrad_s2_weight_elems(int Co, int C, int ks);
 void conv_dgrad_s2_weight_bf16(const void* w_torch, void* packed, int Co, int C, int ks, int pad, hipStream_t stream);
+// part / bnb: as conv3x3_fwd_bf16's, conv_dgrad_s2_part_rows rows (the parity classes' pixel tiles)
+int conv_dgrad_s2_part_rows(int Nb, int H, int W, int ks, int pad);
 void conv_dgrad_s2_bf16(const void* dy, const void* packed, void* dx, int Nb, int H, int W, int C, int Co, int ks,
-                        int pad, hipStream_t stream, const void* add = nullptr);
+                        int pad, hipStream_t stream, const void* add = nullptr, float* part = nullptr,
+                        const ConvBnBack* bnb = nullptr);
 size_t conv_wgrad_workspace_floats(int Nb, int H, int W, int C, int Co, int ks, int stride, int pad);
 void conv_wgrad_bf16(const void* dy, const void* x, void* gw_torch, float* workspace, int Nb, int H, int W, int C,
                      int Co, int ks, int stride, int pad, hipStream_t stream);
@@ -408,7 +424,8 @@ void bn_nhwc_fwd_bf16(const void* x, const void* res, const void* gamma, const v
 // backward: g = dy * (y > 0 if relu); dx, dres = g (optional), ggamma/gbeta (bf16, accumulated; optional)
 void bn_nhwc_bwd_bf16(const void* x, const void* dy, const void* y, const float* mean, const float* rstd,
                       const void* gamma, int M, int C, bool relu, void* dx, void* dres, void* ggamma, void* gbeta,
-                      float* workspace, hipStream_t stream, const void* beta = nullptr);
+                      float* workspace, hipStream_t stream, const void* beta = nullptr, const float* part = nullptr,
+                      int part_rows = 0);
 void bn_nhwc_eval_bf16(const void* x, const void* res, const float* scale, const float* shift, int M, int C, bool relu,
                        void* y, hipStream_t stream);
 

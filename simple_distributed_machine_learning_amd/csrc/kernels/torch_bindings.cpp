@@ -640,9 +640,52 @@ static float* conv_part(const c10::optional<torch::Tensor>& part, int64_t N, int
 }
 
 int64_t conv_part_rows(int64_t N, int64_t OH, int64_t OW) { return sdml::conv_part_rows(N, OH, OW); }
+int64_t conv_dgrad_s2_part_rows(int64_t N, int64_t H, int64_t W, int64_t ks, int64_t pad) {
+  return sdml::conv_dgrad_s2_part_rows(N, H, W, ks, pad);
+}
+
+static void check_bn_vec(const c10::optional<torch::Tensor>& t, int64_t C, const char* name);
+
+// the BatchNorm whose input gradient a convolution's output is (sdml::ConvBnBack): x (and y for relu 1) in the
+// output's layout, fp32 [C] mean / rstd, bf16 [C] gamma / beta; relu 0 / 1 / 2
+static sdml::ConvBnBack conv_bn_back(const c10::optional<torch::Tensor>& bx, const c10::optional<torch::Tensor>& by,
+                                     const c10::optional<torch::Tensor>& mean, const c10::optional<torch::Tensor>& rstd,
+                                     const c10::optional<torch::Tensor>& gamma, const c10::optional<torch::Tensor>& beta,
+                                     int64_t relu, const torch::Tensor& out, bool have_part, const char* fn) {
+  sdml::ConvBnBack b;
+  if (!bx.has_value() || !bx->defined()) return b;
+  TORCH_CHECK(have_part, fn, ": bn_x needs part");
+  check_cl_bf16(*bx, "bn_x");
+  TORCH_CHECK(bx->sizes() == out.sizes(), fn, ": bn_x must have the output's shape");
+  const int64_t C = out.size(1);
+  TORCH_CHECK(relu >= 0 && relu <= 2, fn, ": bn_relu must be 0, 1 or 2");
+  if (relu == 1) {
+    TORCH_CHECK(by.has_value() && by->defined(), fn, ": bn_relu 1 needs bn_y");
+    check_cl_bf16(*by, "bn_y");
+    TORCH_CHECK(by->sizes() == out.sizes(), fn, ": bn_y must have the output's shape");
+    b.y = by->data_ptr();
+  }
+  for (const auto* t : {&mean, &rstd})
+    TORCH_CHECK(t->has_value() && (*t)->defined() && (*t)->is_cuda() && (*t)->scalar_type() == torch::kFloat32 &&
+                    (*t)->is_contiguous() && (*t)->numel() == C, fn, ": bn_mean / bn_rstd must be fp32 [C]");
+  TORCH_CHECK(gamma.has_value() && gamma->defined() && beta.has_value() && beta->defined(), fn,
+              ": bn_gamma and bn_beta are needed");
+  check_bn_vec(gamma, C, "bn_gamma");
+  check_bn_vec(beta, C, "bn_beta");
+  b.x = bx->data_ptr();
+  b.mean = mean->data_ptr<float>();
+  b.rstd = rstd->data_ptr<float>();
+  b.gamma = gamma->data_ptr();
+  b.beta = beta->data_ptr();
+  b.relu = (int)relu;
+  return b;
+}
 
 torch::Tensor conv3x3_fwd_bf16(torch::Tensor x, torch::Tensor wt, c10::optional<torch::Tensor> add,
-                               c10::optional<torch::Tensor> part) {
+                               c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> bn_x,
+                               c10::optional<torch::Tensor> bn_y, c10::optional<torch::Tensor> bn_mean,
+                               c10::optional<torch::Tensor> bn_rstd, c10::optional<torch::Tensor> bn_gamma,
+                               c10::optional<torch::Tensor> bn_beta, int64_t bn_relu) {
   check_cl_bf16(x, "x");
   TORCH_CHECK(wt.dim() == 3 && wt.size(1) == 9 && wt.size(2) == x.size(1) && wt.is_contiguous() &&
               wt.scalar_type() == torch::kBFloat16, "conv3x3_fwd_bf16: wt must be [Co][9][C] bf16");
@@ -651,8 +694,10 @@ torch::Tensor conv3x3_fwd_bf16(torch::Tensor x, torch::Tensor wt, c10::optional<
   auto y = torch::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   const void* ap = conv_addend(add, y, "conv3x3_fwd_bf16");
   float* pp = conv_part(part, N, H, W, Co, "conv3x3_fwd_bf16");
+  const sdml::ConvBnBack bb = conv_bn_back(bn_x, bn_y, bn_mean, bn_rstd, bn_gamma, bn_beta, bn_relu, y, pp != nullptr,
+                                           "conv3x3_fwd_bf16");
   if (N * H * W > 0)
-    sdml::conv3x3_fwd_bf16(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, C, Co, cur_stream(), ap, pp);
+    sdml::conv3x3_fwd_bf16(x.data_ptr(), wt.data_ptr(), y.data_ptr(), N, H, W, C, Co, cur_stream(), ap, pp, &bb);
   return y;
 }
 
@@ -704,7 +749,11 @@ torch::Tensor conv_fwd_bf16(torch::Tensor x, torch::Tensor wt, int64_t ks, int64
 // input gradient of a stride-2 convolution (3x3 pad 1 / 1x1 pad 0): dx (channels-last [N][C][H][W]) from
 // dy (channels-last [N][Co][OH][OW]) and the torch weight [Co][C][ks][ks]
 torch::Tensor conv_dgrad_s2_bf16(torch::Tensor dy, torch::Tensor w, int64_t H, int64_t W, int64_t pad,
-                                 c10::optional<torch::Tensor> add) {
+                                 c10::optional<torch::Tensor> add, c10::optional<torch::Tensor> part,
+                                 c10::optional<torch::Tensor> bn_x, c10::optional<torch::Tensor> bn_y,
+                                 c10::optional<torch::Tensor> bn_mean, c10::optional<torch::Tensor> bn_rstd,
+                                 c10::optional<torch::Tensor> bn_gamma, c10::optional<torch::Tensor> bn_beta,
+                                 int64_t bn_relu) {
   check_cl_bf16(dy, "dy");
   TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == torch::kBFloat16 && w.dim() == 4 &&
               w.size(2) == w.size(3) && w.size(0) == dy.size(1), "conv_dgrad_s2_bf16: w must be [Co][C][k][k] bf16");
@@ -717,8 +766,18 @@ torch::Tensor conv_dgrad_s2_bf16(torch::Tensor dy, torch::Tensor w, int64_t H, i
   conv_addend(add, dx, "conv_dgrad_s2_bf16");
   auto packed = torch::empty({(int64_t)sdml::conv_dgrad_s2_weight_elems(Co, C, ks)}, w.options());
   sdml::conv_dgrad_s2_weight_bf16(w.data_ptr(), packed.data_ptr(), Co, C, ks, pad, cur_stream());
+  float* pp = nullptr;
+  if (part.has_value() && part->defined()) {
+    TORCH_CHECK(part->is_cuda() && part->is_contiguous() && part->scalar_type() == torch::kFloat32 &&
+                    part->numel() == (int64_t)sdml::conv_dgrad_s2_part_rows(N, H, W, ks, pad) * 2 * C,
+                "conv_dgrad_s2_bf16: part must be a contiguous fp32 [conv_dgrad_s2_part_rows][2][C] tensor");
+    pp = part->data_ptr<float>();
+  }
+  const sdml::ConvBnBack bb = conv_bn_back(bn_x, bn_y, bn_mean, bn_rstd, bn_gamma, bn_beta, bn_relu, dx, pp != nullptr,
+                                           "conv_dgrad_s2_bf16");
+  TORCH_CHECK(!pp || bb.x, "conv_dgrad_s2_bf16: part is only written for bn_x (the backward statistics)");
   sdml::conv_dgrad_s2_bf16(dy.data_ptr(), packed.data_ptr(), dx.data_ptr(), N, H, W, C, Co, ks, pad, cur_stream(),
-                           conv_addend(add, dx, "conv_dgrad_s2_bf16"));
+                           conv_addend(add, dx, "conv_dgrad_s2_bf16"), pp, &bb);
   return dx;
 }
 
@@ -806,7 +865,8 @@ std::tuple<torch::Tensor, torch::Tensor, torch::Tensor> bn_nhwc_fwd(
 std::tuple<torch::Tensor, c10::optional<torch::Tensor>> bn_nhwc_bwd(
     torch::Tensor x, torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor mean, torch::Tensor rstd,
     torch::Tensor gamma, bool relu, bool need_dres, c10::optional<torch::Tensor> ggamma,
-    c10::optional<torch::Tensor> gbeta, c10::optional<torch::Tensor> beta) {
+    c10::optional<torch::Tensor> gbeta, c10::optional<torch::Tensor> beta, c10::optional<torch::Tensor> part,
+    int64_t part_rows) {
   check_cl_bf16(x, "x");
   check_cl_bf16(dy, "dy");
   TORCH_CHECK(dy.sizes() == x.sizes(), "bn_nhwc_bwd: dy shape mismatch");
@@ -827,11 +887,19 @@ std::tuple<torch::Tensor, c10::optional<torch::Tensor>> bn_nhwc_bwd(
   if (need_dres) dres = torch::empty_like(x, cl);
   auto ws = torch::empty({(int64_t)sdml::bn_nhwc_workspace_floats(M, C)},
                          x.options().dtype(torch::kFloat32).memory_format(at::MemoryFormat::Contiguous));
+  // part: the per-tile backward sums the convolution that produced dy wrote (conv3x3_fwd_bf16 / conv_dgrad_s2_bf16
+  // with bn_x = x), part_rows rows of [2][C]
+  const float* pp = nullptr;
+  if (part.has_value() && part->defined()) {
+    TORCH_CHECK(part->is_cuda() && part->is_contiguous() && part->scalar_type() == torch::kFloat32 && part_rows > 0 &&
+                    part->numel() == part_rows * 2 * C, "bn_nhwc_bwd: part must be a contiguous fp32 [part_rows][2][C]");
+    pp = part->data_ptr<float>();
+  }
   if (M > 0)
     sdml::bn_nhwc_bwd_bf16(x.data_ptr(), dy.data_ptr(), (relu && have_y) ? y->data_ptr() : nullptr,
                            mean.data_ptr<float>(), rstd.data_ptr<float>(), gamma.data_ptr(), M, C, relu, dx.data_ptr(),
                            need_dres ? dres->data_ptr() : nullptr, opt_data(ggamma), opt_data(gbeta),
-                           ws.data_ptr<float>(), cur_stream(), opt_data(beta));
+                           ws.data_ptr<float>(), cur_stream(), opt_data(beta), pp, (int)part_rows);
   return {dx, dres};
 }
 
@@ -1907,14 +1975,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_weights_batched_bf16", &conv3x3_weights_batched_bf16,
         "several 3x3 conv weights -> their kernel layouts in caller-owned buffers, one launch");
   m.def("conv3x3_fwd_bf16", &conv3x3_fwd_bf16, "3x3 stride-1 pad-1 conv, channels-last bf16 (implicit GEMM)",
-        py::arg("x"), py::arg("wt"), py::arg("add") = py::none(), py::arg("part") = py::none());
+        py::arg("x"), py::arg("wt"), py::arg("add") = py::none(), py::arg("part") = py::none(),
+        py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(), py::arg("bn_mean") = py::none(),
+        py::arg("bn_rstd") = py::none(), py::arg("bn_gamma") = py::none(), py::arg("bn_beta") = py::none(),
+        py::arg("bn_relu") = 0);
   m.def("conv_part_rows", &conv_part_rows, "rows of the BatchNorm partials a convolution epilogue writes");
+  m.def("conv_dgrad_s2_part_rows", &conv_dgrad_s2_part_rows,
+        "rows of the BatchNorm backward partials conv_dgrad_s2_bf16 writes", py::arg("N"), py::arg("H"), py::arg("W"),
+        py::arg("ks"), py::arg("pad"));
   m.def("conv3x3_wgrad_bf16_", &conv3x3_wgrad_bf16_, "3x3 conv weight gradient, accumulated into bf16 grad");
   m.def("conv_fwd_bf16", &conv_fwd_bf16, "conv (3x3 pad 1 / 1x1, stride 1|2), channels-last bf16 (implicit GEMM)",
         py::arg("x"), py::arg("wt"), py::arg("ks"), py::arg("stride"), py::arg("pad"), py::arg("add") = py::none(),
         py::arg("part") = py::none());
   m.def("conv_dgrad_s2_bf16", &conv_dgrad_s2_bf16, "input gradient of a stride-2 conv (3x3 pad 1 / 1x1), parity-class GEMMs",
-        py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"), py::arg("pad"), py::arg("add") = py::none());
+        py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"), py::arg("pad"), py::arg("add") = py::none(),
+        py::arg("part") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(),
+        py::arg("bn_mean") = py::none(), py::arg("bn_rstd") = py::none(), py::arg("bn_gamma") = py::none(),
+        py::arg("bn_beta") = py::none(), py::arg("bn_relu") = 0);
   m.def("conv_wgrad_bf16_", &conv_wgrad_bf16_, "conv weight gradient (3x3 / 1x1, stride 1|2), accumulated");
   m.def("conv_c1_fwd_bf16", &conv_c1_fwd_bf16, "stem 3x3 conv with one input channel -> channels-last bf16");
   m.def("conv_c1_wgrad_bf16_", &conv_c1_wgrad_bf16_, "stem conv weight gradient, accumulated into bf16 grad");
@@ -1923,7 +2000,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("momentum"), py::arg("relu"), py::arg("num_batches_tracked") = py::none(), py::arg("part") = py::none());
   m.def("bn_nhwc_bwd", &bn_nhwc_bwd, "BatchNorm (+residual)(+ReLU) backward, channels-last bf16", py::arg("x"),
         py::arg("dy"), py::arg("y"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"), py::arg("relu"),
-        py::arg("need_dres"), py::arg("ggamma"), py::arg("gbeta"), py::arg("beta") = py::none());
+        py::arg("need_dres"), py::arg("ggamma"), py::arg("gbeta"), py::arg("beta") = py::none(),
+        py::arg("part") = py::none(), py::arg("part_rows") = 0);
   m.def("bn_nhwc_eval", &bn_nhwc_eval, "BatchNorm with running statistics (+residual)(+ReLU)");
   m.def("set_knob", [](const std::string& name, int value) {
           TORCH_CHECK(sdml::set_knob(name.c_str(), value), "unknown kernel knob, or a timing probe that only ",

@@ -46,24 +46,32 @@ class BasicBlock(nn.Module):
         if stride != 1 or cin != cout:
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
-    def forward(self, x):
-        # conv (HIP implicit GEMM when bf16 NHWC; the epilogue also writes the BatchNorm statistics
-        # partials) -> BN+ReLU / BN+residual+ReLU in one pass each (ops/conv.py; PyTorch ops elsewhere).
-        # The residual branch's input gradient is added in conv1's input-gradient epilogue
-        # (ResidualLink): the tap on x is created after the main branch's convolutions so autograd
-        # runs it first.
-        link = (conv_ops.ResidualLink() if (conv_ops.FUSE_RESIDUAL and x.requires_grad and x.is_cuda
-                                             and x.dtype == torch.bfloat16) else None)
-        y1, p1 = conv_ops.conv_stats(self.conv1, self.bn1, x, link)
-        out = conv_ops.batch_norm(self.bn1, y1, relu=True, part=p1)
+    def forward(self, x, back=None):
+        return self.forward_linked(x, back)[0]
+
+    def forward_linked(self, x, back=None):
+        """(out, link). conv (HIP implicit GEMM when bf16 NHWC; the epilogue also writes the BatchNorm statistics
+        partials) -> BN+ReLU / BN+residual+ReLU in one pass each (ops/conv.py; PyTorch ops elsewhere).
+        The residual branch's input gradient is added in conv1's input-gradient epilogue (ResidualLink): the tap
+        on x is created after the main branch's convolutions so autograd runs it first. BatchNorm backward
+        statistics come from the input-gradient epilogue of the convolution consuming the BatchNorm's output
+        (BNBackLink): bn1's from conv2's, and ``back`` (the BatchNorm that produced x) from conv1's when the
+        residual gradient was fused there; ``link`` is bn2's, for the next block's conv1."""
+        gpu_bf16 = x.is_cuda and x.dtype == torch.bfloat16
+        link = conv_ops.ResidualLink() if (conv_ops.FUSE_RESIDUAL and x.requires_grad and gpu_bf16) else None
+        fuse = conv_ops.FUSE_BN_BACK and gpu_bf16 and torch.is_grad_enabled() and self.training
+        b1 = conv_ops.BNBackLink() if fuse else None
+        b2 = conv_ops.BNBackLink(needs_addend=True) if fuse else None
+        y1, p1 = conv_ops.conv_stats(self.conv1, self.bn1, x, link, back=back)
+        out = conv_ops.batch_norm(self.bn1, y1, relu=True, part=p1, back=b1)
         if self.shortcut is None:
-            y2, p2 = conv_ops.conv_stats(self.conv2, self.bn2, out)
+            y2, p2 = conv_ops.conv_stats(self.conv2, self.bn2, out, back=b1)
             sc = conv_ops.grad_tap(x, link)
         else:
             ys, ps = conv_ops.conv_stats(self.shortcut[0], self.shortcut[1], conv_ops.grad_tap(x, link))
             sc = conv_ops.batch_norm(self.shortcut[1], ys, part=ps)
-            y2, p2 = conv_ops.conv_stats(self.conv2, self.bn2, out)
-        return conv_ops.batch_norm(self.bn2, y2, res=sc, relu=True, part=p2)
+            y2, p2 = conv_ops.conv_stats(self.conv2, self.bn2, out, back=b1)
+        return conv_ops.batch_norm(self.bn2, y2, res=sc, relu=True, part=p2, back=b2), b2
 
 
 def block_defs(in_ch: int = 1):
@@ -118,10 +126,13 @@ class ResNetStage(PipelineStage):
         nhwc = _nhwc(x.dtype)
         if x.is_cuda and nhwc:
             x = x.contiguous(memory_format=torch.channels_last)
+        back = None  # BNBackLink of the BatchNorm that produced x (BasicBlock.forward_linked)
         if self.stage_id == 0:
-            x = conv_ops.batch_norm(self.stem_bn, conv_ops.conv2d(self.stem_conv, x), relu=True)
+            if conv_ops.FUSE_BN_BACK and x.is_cuda and nhwc and torch.is_grad_enabled() and self.training:
+                back = conv_ops.BNBackLink(needs_addend=True)
+            x = conv_ops.batch_norm(self.stem_bn, conv_ops.conv2d(self.stem_conv, x), relu=True, back=back)
         for n in self.block_names:
-            x = getattr(self, n)(x)
+            x, back = getattr(self, n).forward_linked(x, back)
         return x
 
     def forward(self, x):

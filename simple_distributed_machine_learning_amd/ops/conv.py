@@ -74,6 +74,59 @@ def _take_addend(link):
     return link.take() if link is not None else None
 
 
+# BNBackLink joins a BatchNorm's backward statistics pass to the convolution whose input gradient is that BatchNorm's
+# output gradient dy (ResNet: bn1 -> conv2, and a block's closing BatchNorm -> the next block's conv1 with the residual
+# addend fused). Set False for A/B runs.
+FUSE_BN_BACK = __import__("os").environ.get("SDML_BN_BACK_FUSE", "1") != "0"
+
+
+class BNBackLink:
+    """Hands a training BatchNorm's backward statistics (per-channel sums of g = dy * relu-mask and g * xhat) to the
+    epilogue of the convolution that produces its dy (conv_bf16.hip ``BnBack``), so ``bn_nhwc_bwd`` skips its pass
+    over dy and x (batchnorm_nhwc.hip ``bn_partial_kernel<true>``).
+
+    The BatchNorm's forward fills ``args`` (detached x, the saved output when the ReLU mask comes from it, mean, rstd,
+    gamma, beta, mask mode); the consuming convolution's backward writes ``part`` for its output and records that
+    output's address; the BatchNorm's backward uses ``part`` only when its dy IS that output (so a gradient that
+    autograd accumulated from another consumer is never paired with partial sums of one summand).
+    ``needs_addend``: the BatchNorm output also feeds a residual branch, so the convolution's output is the whole dy
+    only when the branch's gradient was added in its epilogue (ResidualLink). ``fused`` counts the fused passes."""
+
+    __slots__ = ("args", "part", "rows", "dy_ptr", "needs_addend")
+    fused = 0
+
+    def __init__(self, needs_addend: bool = False):
+        self.args = None
+        self.part = None
+        self.rows = 0
+        self.dy_ptr = None
+        self.needs_addend = needs_addend
+
+    def request(self, add):
+        """The BatchNorm's saved state for the consumer's dgrad epilogue, or None (then nothing is fused)."""
+        if self.args is None or (self.needs_addend and add is None):
+            return None
+        return self.args
+
+    def fill(self, part, rows, dy):
+        self.part, self.rows, self.dy_ptr = part, rows, dy.data_ptr()
+        self.args = None
+
+    def take(self, dy):
+        """(part, rows) for this dy, or (None, 0); the link is emptied either way."""
+        part, rows, ptr = self.part, self.rows, self.dy_ptr
+        self.args = self.part = self.dy_ptr = None
+        if part is None or ptr != dy.data_ptr():
+            return None, 0
+        BNBackLink.fused += 1
+        return part, rows
+
+
+def _bn_kwargs(args):
+    x, y, mean, rstd, gamma, beta, relu = args
+    return dict(bn_x=x, bn_y=y, bn_mean=mean, bn_rstd=rstd, bn_gamma=gamma, bn_beta=beta, bn_relu=relu)
+
+
 # The kernels' weight layouts (conv3x3_weights_bf16: the forward [Co][9][C] and the flipped / transposed dgrad
 # one) depend only on the weight, which is constant within an optimizer step: every micro-batch of a step used
 # to re-derive them (16 launches per ResNet-18 step, 0.14 ms of 4.69: profiles/r3_resnet18_bf16_final_kernel_
@@ -167,7 +220,7 @@ def _weight_layouts(w, need_dgrad: bool):
 
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, part=None, link=None):
+    def forward(ctx, x, w, part=None, link=None, back=None):
         # both layouts in one pass when an input gradient is needed; the dgrad one waits for backward
         wt, ctx.wd = _weight_layouts(w, ctx.needs_input_grad[0])
         K = kernels()
@@ -175,7 +228,7 @@ class _Conv3x3Fn(torch.autograd.Function):
             ctx.wd = None
         y = K.conv3x3_fwd_bf16(x, wt, part=part)
         ctx.save_for_backward(x)
-        ctx.w, ctx.link = w, link
+        ctx.w, ctx.link, ctx.back = w, link, back
         return y
 
     @staticmethod
@@ -184,8 +237,18 @@ class _Conv3x3Fn(torch.autograd.Function):
         w = ctx.w
         K = kernels()
         dy = dy.contiguous(memory_format=torch.channels_last)
-        dx = K.conv3x3_fwd_bf16(dy, ctx.wd, add=_take_addend(ctx.link)) if ctx.needs_input_grad[0] else None
-        ctx.wd = None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            add = _take_addend(ctx.link)
+            req = ctx.back.request(add) if ctx.back is not None else None
+            if req is not None:  # dx is the preceding BatchNorm's dy: its backward statistics come from this epilogue
+                rows = K.conv_part_rows(dy.shape[0], dy.shape[2], dy.shape[3])
+                part = torch.empty(rows * 2 * x.shape[1], device=dy.device, dtype=torch.float32)
+                dx = K.conv3x3_fwd_bf16(dy, ctx.wd, add=add, part=part, **_bn_kwargs(req))
+                ctx.back.fill(part, rows, dx)
+            else:
+                dx = K.conv3x3_fwd_bf16(dy, ctx.wd, add=add)
+        ctx.wd = ctx.back = None
         gw = None
         if ctx.needs_input_grad[1]:
             if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
@@ -193,7 +256,7 @@ class _Conv3x3Fn(torch.autograd.Function):
             else:
                 gw = torch.zeros_like(w)
                 K.conv3x3_wgrad_bf16_(dy, x, gw)
-        return dx, gw, None, None
+        return dx, gw, None, None, None
 
 
 def hip_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
@@ -205,13 +268,21 @@ def hip_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0)
 
 
-def _general_dgrad(dy, x, w, st, pd, add=None):
+def _general_dgrad(dy, x, w, st, pd, add=None, back=None):
     """Input gradient of a general_eligible convolution (+ add): stride 2 -> the parity-class GEMM
     kernel (conv_bf16.hip conv_dgrad_s2_kernel); stride-1 1x1 -> the forward kernel on dy with the
-    transposed [C][1][Co] weights; stride-1 3x3 -> the forward kernel with the flipped dgrad weights."""
+    transposed [C][1][Co] weights; stride-1 3x3 -> the forward kernel with the flipped dgrad weights.
+    ``back`` (BNBackLink, stride 2): the preceding BatchNorm's backward statistics from the epilogue."""
     K = kernels()
     H, W = x.shape[2], x.shape[3]
     if st == 2:
+        req = back.request(add) if back is not None else None
+        if req is not None:
+            rows = K.conv_dgrad_s2_part_rows(x.shape[0], H, W, w.shape[2], pd)
+            part = torch.empty(rows * 2 * x.shape[1], device=dy.device, dtype=torch.float32)
+            dx = K.conv_dgrad_s2_bf16(dy, w, H, W, pd, add=add, part=part, **_bn_kwargs(req))
+            back.fill(part, rows, dx)
+            return dx
         return K.conv_dgrad_s2_bf16(dy, w, H, W, pd, add=add)
     if w.shape[2] == 1:
         return K.conv_fwd_bf16(dy, w.reshape(w.shape[0], w.shape[1]).t().contiguous(), 1, 1, 0, add=add)
@@ -225,13 +296,13 @@ class _ConvGeneralFn(torch.autograd.Function):
     strided convolution) on the parity-class GEMMs (``_general_dgrad``)."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, pad, part=None, link=None):
+    def forward(ctx, x, w, stride, pad, part=None, link=None, back=None):
         K = kernels()
         ks = w.shape[2]
         wt = _weight_layouts(w, False)[0] if ks == 3 else w  # [Co][C][1][1] is already [Co][1][C]
         y = K.conv_fwd_bf16(x, wt, ks, stride, pad, part=part)
         ctx.save_for_backward(x)
-        ctx.w, ctx.stride, ctx.pad, ctx.link = w, stride, pad, link
+        ctx.w, ctx.stride, ctx.pad, ctx.link, ctx.back = w, stride, pad, link, back
         return y
 
     @staticmethod
@@ -241,7 +312,8 @@ class _ConvGeneralFn(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = _general_dgrad(dy, x, w, st, pd, add=_take_addend(ctx.link))
+            dx = _general_dgrad(dy, x, w, st, pd, add=_take_addend(ctx.link), back=ctx.back)
+        ctx.back = None
         gw = None
         if ctx.needs_input_grad[1]:
             if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
@@ -249,7 +321,7 @@ class _ConvGeneralFn(torch.autograd.Function):
             else:
                 gw = torch.zeros_like(w)
                 kernels().conv_wgrad_bf16_(dy, x, gw, st, pd)
-        return dx, gw, None, None, None, None
+        return dx, gw, None, None, None, None, None
 
 
 def general_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
@@ -313,22 +385,22 @@ def _refuse_library(x: torch.Tensor, what: str):
             "fp32 on the CPU). SDML_CONV_LIBRARY=1 allows the MIOpen/ATen path for A/B comparisons.")
 
 
-def conv2d(conv: torch.nn.Conv2d, x: torch.Tensor, part=None, link=None) -> torch.Tensor:
+def conv2d(conv: torch.nn.Conv2d, x: torch.Tensor, part=None, link=None, back=None) -> torch.Tensor:
     """``conv(x)``, on the HIP kernels where they apply: stride-1 3x3 on the halo kernel, strided
     3x3 / 1x1 on the im2col kernel (input gradient on the parity-class kernel), the streaming stem
-    kernels for a one-channel input. ``part`` / ``link``: see ``conv_stats`` / ``ResidualLink`` (the
-    implicit-GEMM paths only)."""
+    kernels for a one-channel input. ``part`` / ``link`` / ``back``: see ``conv_stats`` / ``ResidualLink`` /
+    ``BNBackLink`` (the implicit-GEMM paths only)."""
     if hip_eligible(x, conv):
-        return _Conv3x3Fn.apply(x, conv.weight, part, link)
+        return _Conv3x3Fn.apply(x, conv.weight, part, link, back)
     if general_eligible(x, conv):
-        return _ConvGeneralFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], part, link)
+        return _ConvGeneralFn.apply(x, conv.weight, conv.stride[0], conv.padding[0], part, link, back)
     if stem_eligible(x, conv):
         return _StemConvFn.apply(x, conv.weight)
     _refuse_library(x, "convolution")
     return conv(x)
 
 
-def conv_stats(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x: torch.Tensor, link=None):
+def conv_stats(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x: torch.Tensor, link=None, back=None):
     """(y, part): y = conv(x); part = the BatchNorm partials of y written by the convolution's
     epilogue (per 256-pixel tile: channel sums of y and y^2) when the convolution runs on an
     implicit-GEMM kernel and ``bn`` trains on the HIP path, else None. ``batch_norm(bn, y,
@@ -339,13 +411,13 @@ def conv_stats(conv: torch.nn.Conv2d, bn: torch.nn.BatchNorm2d, x: torch.Tensor,
         OH = (x.shape[2] + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1
         OW = (x.shape[3] + 2 * conv.padding[1] - conv.kernel_size[1]) // conv.stride[1] + 1
         part = torch.empty(kernels().conv_part_rows(N, OH, OW) * 2 * Co, device=x.device, dtype=torch.float32)
-    return conv2d(conv, x, part, link), part
+    return conv2d(conv, x, part, link, back), part
 
 
 # ---- BatchNorm (+ residual) (+ ReLU), channels-last bf16 (csrc/kernels/batchnorm_nhwc.hip) -----
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, gamma, beta, bn: torch.nn.BatchNorm2d, relu: bool, part=None):
+    def forward(ctx, x, res, gamma, beta, bn: torch.nn.BatchNorm2d, relu: bool, part=None, back=None):
         momentum = 0.1 if bn.momentum is None else bn.momentum
         nbt = bn.num_batches_tracked  # incremented inside the statistics kernel
         y, mean, rstd = kernels().bn_nhwc_fwd(x, res, gamma, beta, bn.running_mean, bn.running_var, bn.eps,
@@ -358,6 +430,10 @@ class _BNFn(torch.autograd.Function):
         keep_y = relu and res is not None
         ctx.save_for_backward(x, y if keep_y else None, mean, rstd)
         ctx.gamma, ctx.beta, ctx.relu, ctx.has_res = gamma, beta, relu, res is not None
+        ctx.back = back
+        if back is not None:  # detached views: the link must not hold this node's own output (no reference cycle)
+            back.args = (x.detach(), y.detach() if keep_y else None, mean, rstd, gamma.detach(), beta.detach(),
+                         0 if not relu else (1 if keep_y else 2))
         return y
 
     @staticmethod
@@ -373,9 +449,11 @@ class _BNFn(torch.autograd.Function):
 
         gg, own_g = acc(gamma)
         gb, own_b = acc(beta)
+        part, rows = ctx.back.take(dy) if ctx.back is not None else (None, 0)
+        ctx.back = None
         dx, dres = kernels().bn_nhwc_bwd(x, dy, y if ctx.relu else None, mean, rstd, gamma, ctx.relu, ctx.has_res,
-                                          gg, gb, beta)
-        return dx, dres, (gg if own_g else None), (gb if own_b else None), None, None, None
+                                          gg, gb, beta, part=part, part_rows=rows)
+        return dx, dres, (gg if own_g else None), (gb if own_b else None), None, None, None, None
 
 
 def bn_eligible(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res=None) -> bool:
@@ -387,9 +465,11 @@ def bn_eligible(x: torch.Tensor, bn: torch.nn.BatchNorm2d, res=None) -> bool:
     return ok
 
 
-def batch_norm(bn: torch.nn.BatchNorm2d, x: torch.Tensor, res=None, relu: bool = False, part=None) -> torch.Tensor:
+def batch_norm(bn: torch.nn.BatchNorm2d, x: torch.Tensor, res=None, relu: bool = False, part=None,
+               back=None) -> torch.Tensor:
     """``relu?(bn(x) (+ res))`` — one pass per direction on the HIP kernels where they apply; ``part``:
-    x's statistics partials from its convolution's epilogue (``conv_stats``)."""
+    x's statistics partials from its convolution's epilogue (``conv_stats``); ``back``: a ``BNBackLink`` the
+    convolution consuming the output takes, so the backward statistics come from its input-gradient epilogue."""
     if x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4:
         # MIOpen may hand back NCHW (e.g. the 1-channel stem): one copy beats PyTorch's NCHW
         # BatchNorm backward (~0.8 ms per call at batch 512)
@@ -398,7 +478,7 @@ def batch_norm(bn: torch.nn.BatchNorm2d, x: torch.Tensor, res=None, relu: bool =
             res = res.contiguous(memory_format=torch.channels_last)
     if bn_eligible(x, bn, res):
         if bn.training:
-            return _BNFn.apply(x, res, bn.weight, bn.bias, bn, relu, part)
+            return _BNFn.apply(x, res, bn.weight, bn.bias, bn, relu, part, back)
         with torch.no_grad():
             scale = (bn.weight.float() * torch.rsqrt(bn.running_var.float() + bn.eps)).contiguous()
             shift = (bn.bias.float() - bn.running_mean.float() * scale).contiguous()

@@ -360,3 +360,115 @@ def test_resnet_weight_layout_cache_is_exact_across_steps():
         assert r.returncode == 0, r.stderr[-3000:]
         outs.append(torch.load(path, weights_only=True))
     assert torch.equal(outs[0], outs[1])
+
+
+def _bn_back_sums(dx, x, y, mean, rstd, gamma, beta, relu, rows=None):
+    """fp64 per-channel sums of g = dx * mask and g * (x - mean) * rstd over rows of 256 pixels (rows=None: one sum
+    over every pixel), the mask as batchnorm_nhwc.hip forms it (relu 1: y > 0; 2: x * sc + sh > 0, sc = gamma rstd)."""
+    C = x.shape[1]
+    f = lambda t: t.permute(0, 2, 3, 1).reshape(-1, C).double()  # noqa: E731
+    g, xf = f(dx.float()), f(x.float())
+    if relu == 1:
+        g = torch.where(f(y.float()) > 0, g, torch.zeros_like(g))
+    elif relu == 2:
+        sc = gamma.float() * rstd
+        sh = beta.float() - mean * sc
+        g = torch.where(f(x.float() * sc.view(1, C, 1, 1) + sh.view(1, C, 1, 1)) > 0, g, torch.zeros_like(g))
+    gx = g * (xf - mean.double()) * rstd.double()
+    if rows is None:
+        return g.sum(0), gx.sum(0)
+    pad = (-g.shape[0]) % rows
+    g, gx = torch.cat([g, g.new_zeros(pad, C)]), torch.cat([gx, gx.new_zeros(pad, C)])
+    return g.view(-1, rows, C).sum(1), gx.view(-1, rows, C).sum(1)
+
+
+@pytest.mark.parametrize("relu", [0, 1, 2])
+@pytest.mark.parametrize("N,C,Co,H,W,ks,st", [(4, 64, 128, 14, 14, 3, 1), (2, 128, 64, 28, 28, 3, 1),
+                                               (4, 64, 128, 28, 28, 3, 2), (3, 128, 256, 7, 7, 3, 2),
+                                               (2, 64, 128, 9, 11, 3, 2)])
+def test_dgrad_epilogue_bn_backward_partials(N, C, Co, H, W, ks, st, relu):
+    """The input-gradient epilogue's BatchNorm backward statistics (conv_bf16.hip BnBack): dx is unchanged, the
+    partial rows are the sums of g = dx * mask and g * xhat (per 256-pixel tile for the stride-1 kernel; in total
+    for the stride-2 parity classes), and the BatchNorm backward fed them matches the one running its own pass."""
+    g = torch.Generator(device="cpu").manual_seed(N * C + Co + H + st + relu)
+    pd = (ks - 1) // 2
+    x = cl(torch.randn(N, C, H, W, generator=g).mul(1.5).add(0.3).to(DEV, torch.bfloat16))  # the BatchNorm's input
+    res = cl(torch.randn(N, C, H, W, generator=g).to(DEV, torch.bfloat16)) if relu == 1 else None
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV, torch.bfloat16)
+    beta = (torch.randn(C, generator=g) * 0.2).to(DEV, torch.bfloat16)
+    yb, mean, rstd = K.bn_nhwc_fwd(x, res, gamma, beta, None, None, 1e-5, 0.1, relu != 0)
+    w = (torch.randn(Co, C, ks, ks, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    OH, OW = (H + 2 * pd - ks) // st + 1, (W + 2 * pd - ks) // st + 1
+    dyc = cl(torch.randn(N, Co, OH, OW, generator=g).to(DEV, torch.bfloat16))  # the convolution's output gradient
+    bnk = dict(bn_x=x, bn_y=yb if relu == 1 else None, bn_mean=mean, bn_rstd=rstd, bn_gamma=gamma, bn_beta=beta,
+               bn_relu=relu)
+    if st == 1:
+        wd = K.conv3x3_weight_bf16(w, True)
+        rows = K.conv_part_rows(N, H, W)
+        part = torch.full((rows * 2 * C,), float("nan"), device=DEV)
+        dx0 = K.conv3x3_fwd_bf16(dyc, wd)
+        dx = K.conv3x3_fwd_bf16(dyc, wd, part=part, **bnk)
+    else:
+        rows = K.conv_dgrad_s2_part_rows(N, H, W, ks, pd)
+        part = torch.full((rows * 2 * C,), float("nan"), device=DEV)
+        dx0 = K.conv_dgrad_s2_bf16(dyc, w, H, W, pd)
+        dx = K.conv_dgrad_s2_bf16(dyc, w, H, W, pd, part=part, **bnk)
+    assert torch.equal(dx, dx0)
+    p = part.view(rows, 2, C).double()
+    assert torch.isfinite(p).all()  # every row written
+    s1, s2 = _bn_back_sums(dx, x, yb, mean, rstd, gamma, beta, relu, rows=256 if st == 1 else None)
+    if st == 1:
+        torch.testing.assert_close(p[:, 0], s1, rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(p[:, 1], s2, rtol=1e-4, atol=1e-3)
+    else:
+        torch.testing.assert_close(p[:, 0].sum(0), s1, rtol=1e-4, atol=1e-2)
+        torch.testing.assert_close(p[:, 1].sum(0), s2, rtol=1e-4, atol=1e-2)
+    # BatchNorm backward from these partials vs its own statistics pass
+    outs = []
+    for pp in (part, None):
+        gg = torch.zeros(C, device=DEV, dtype=torch.bfloat16)
+        gb = torch.zeros(C, device=DEV, dtype=torch.bfloat16)
+        d, dr = K.bn_nhwc_bwd(x, dx, yb if relu == 1 else None, mean, rstd, gamma, relu != 0, relu == 1, gg, gb, beta,
+                              part=pp, part_rows=rows if pp is not None else 0)
+        outs.append((d.float(), None if dr is None else dr.float(), gg.float(), gb.float()))
+    (d1, r1, g1, b1), (d0, r0, g0, b0) = outs
+    torch.testing.assert_close(d1, d0, rtol=1e-2, atol=1e-2 * float(d0.abs().max()))
+    if relu == 1:
+        assert torch.equal(r1, r0)
+    torch.testing.assert_close(g1, g0, rtol=1e-2, atol=1e-2 * float(g0.abs().max()) + 1e-3)
+    torch.testing.assert_close(b1, b0, rtol=1e-2, atol=1e-2 * float(b0.abs().max()) + 1e-3)
+
+
+def test_resnet_stage_bn_backward_statistics_from_dgrad_epilogues():
+    """A one-stage bf16 ResNet-18 forward + backward with BNBackLink (every bn1 from conv2's input-gradient epilogue,
+    every BatchNorm closing a block or the stem from the next conv1's when the residual gradient was fused there)
+    against the same step with the BatchNorm backward running its own statistics passes: same loss, gradients within
+    bf16 tolerance."""
+    from simple_distributed_machine_learning_amd.models import get_model_spec
+
+    spec = get_model_spec("resnet18", 1, dtype=torch.bfloat16)
+    res, fused = [], []
+    try:
+        for on in (True, False):
+            conv_ops.FUSE_BN_BACK = on
+            torch.manual_seed(0)
+            m = spec.build_stage(0).to(DEV, torch.bfloat16)
+            g = torch.Generator().manual_seed(3)
+            x = torch.randn(32, 1, 28, 28, generator=g).to(DEV, torch.bfloat16)
+            t = torch.randint(0, 10, (32,), generator=g).to(DEV)
+            f0 = conv_ops.BNBackLink.fused
+            out = m(x)
+            loss = F.cross_entropy(out.float(), t)
+            loss.backward()
+            torch.cuda.synchronize()
+            fused.append(conv_ops.BNBackLink.fused - f0)
+            res.append((float(loss), [(n, p.grad.float().clone()) for n, p in m.named_parameters()]))
+    finally:
+        conv_ops.FUSE_BN_BACK = True
+    # 8 bn1 (conv2's epilogue) + the stem's and the closing BatchNorms of blocks 0-6 whose next conv1 fused the
+    # residual gradient (the downsampling blocks' taps may run after their conv1: then that one is not fused)
+    assert fused[1] == 0 and 8 + 5 <= fused[0] <= 16, fused
+    assert res[0][0] == pytest.approx(res[1][0], rel=1e-3)
+    for (n, a), (_, b) in zip(res[0][1], res[1][1]):
+        e = float((a - b).norm() / (b.norm() + 1e-6))
+        assert e < 3e-2, (n, e)

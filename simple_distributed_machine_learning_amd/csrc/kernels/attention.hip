@@ -120,16 +120,17 @@ __device__ __forceinline__ bf16x8 trf(const u16* X, int k0, int c0, int lane) {
   r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
   return r;
 }
-// a tile of ROWS rows in registers (ROWS/32 x 16 B per thread) on its way from global memory to LDS
-template <int ROWS>
+// a tile of ROWS rows in registers (ROWS * 8 / NTH x 16 B per thread of an NTH-thread block) on its way from global
+// memory to LDS
+template <int ROWS, int NTH = 256>
 struct TileRegs {
-  u16x8 v[ROWS / 32];
+  u16x8 v[ROWS * 8 / NTH];
 };
-template <int ROWS>
-__device__ __forceinline__ void tile_load(TileRegs<ROWS>& t, const u16* G, long srow, int r0, int S) {
+template <int ROWS, int NTH>
+__device__ __forceinline__ void tile_load(TileRegs<ROWS, NTH>& t, const u16* G, long srow, int r0, int S) {
 #pragma unroll
-  for (int u = 0; u < ROWS / 32; ++u) {
-    const int idx = threadIdx.x + 256 * u, r = idx >> 3, ch = idx & 7;
+  for (int u = 0; u < ROWS * 8 / NTH; ++u) {
+    const int idx = threadIdx.x + NTH * u, r = idx >> 3, ch = idx & 7;
     u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
     if (r0 + r < S) v = *reinterpret_cast<const u16x8*>(G + (long)(r0 + r) * srow + 8 * ch);
     t.v[u] = v;
@@ -137,19 +138,19 @@ __device__ __forceinline__ void tile_load(TileRegs<ROWS>& t, const u16* G, long 
 }
 // rows past S re-read row S - 1 (unconditional loads, no exec-masked branches): only for consumers that mask those
 // keys themselves (the forward's edge tiles set their scores to -inf, so their V rows meet P = 0)
-template <int ROWS>
-__device__ __forceinline__ void tile_load_clamped(TileRegs<ROWS>& t, const u16* G, long srow, int r0, int S) {
+template <int ROWS, int NTH>
+__device__ __forceinline__ void tile_load_clamped(TileRegs<ROWS, NTH>& t, const u16* G, long srow, int r0, int S) {
 #pragma unroll
-  for (int u = 0; u < ROWS / 32; ++u) {
-    const int idx = threadIdx.x + 256 * u, r = idx >> 3, ch = idx & 7;
+  for (int u = 0; u < ROWS * 8 / NTH; ++u) {
+    const int idx = threadIdx.x + NTH * u, r = idx >> 3, ch = idx & 7;
     t.v[u] = *reinterpret_cast<const u16x8*>(G + (long)min(r0 + r, S - 1) * srow + 8 * ch);
   }
 }
-template <int ROWS>
-__device__ __forceinline__ void tile_store(u16* L, const TileRegs<ROWS>& t) {
+template <int ROWS, int NTH>
+__device__ __forceinline__ void tile_store(u16* L, const TileRegs<ROWS, NTH>& t) {
 #pragma unroll
-  for (int u = 0; u < ROWS / 32; ++u) {
-    const int idx = threadIdx.x + 256 * u, r = idx >> 3, ch = idx & 7;
+  for (int u = 0; u < ROWS * 8 / NTH; ++u) {
+    const int idx = threadIdx.x + NTH * u, r = idx >> 3, ch = idx & 7;
     *reinterpret_cast<u16x8*>(L + swz(r, ch)) = t.v[u];
   }
 }
@@ -173,12 +174,19 @@ __device__ __forceinline__ int xcd_block(int id, int n) { return (n % 8 == 0) ? 
 
 // ============================================================================================
 // forward
-template <int KBT>  // keys per tile (64 or 128)
-__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
+// QS: 32-query sub-blocks per wave (1: 32 queries per wave; 2: 64). With QS = 2 each K / V fragment read from LDS
+// feeds both sub-blocks' MFMAs and the wave carries two independent score -> softmax -> PV chains, so one sub-block's
+// exp / max / sum VALU work can issue beside the other's MFMAs. NWV waves per workgroup (4, or 2 with QS = 2: the
+// same 128 queries per workgroup, four workgroups per CU).
+template <int KBT, int QS, int NWV = NW>  // keys per tile (64 or 128)
+__global__ void __launch_bounds__(64 * NWV, 8 / NWV) attn_fwd_kernel(AttnArgs a) {
   constexpr int NC = KBT / 32;  // 32-key sub-blocks per tile
+  constexpr int QWV = QW * QS;  // queries per wave
+  constexpr int QBW = QWV * NWV;  // queries per workgroup
+  constexpr int NTH = 64 * NWV;
   __shared__ __attribute__((aligned(16))) u16 Ks[2][KBT * HD];
   __shared__ __attribute__((aligned(16))) u16 Vs[2][KBT * HD];
-  const int nqb = (a.S + QB - 1) / QB;
+  const int nqb = (a.S + QBW - 1) / QBW;
   const int blk = xcd_block(blockIdx.x, gridDim.x);
   const int bh = blk / nqb;
   const int qb = nqb - 1 - (blk % nqb);  // heaviest (causal) blocks first
@@ -189,20 +197,30 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
   const u16* Q = a.q + qoff;
   const u16* K = a.k + qoff;
   const u16* V = a.v + qoff;
-  const int q0w = qb * QB + w * QW;  // this wave's first query
-  const int qi = q0w + r;            // this lane's query
+  const int q0w = qb * QBW + w * QWV;  // this wave's first query
+  int qi[QS];                          // this lane's query in each sub-block
   // Q fragments (B operand of S^T = K Q^T): element j = Q[qi][16t + 8h + j]
-  bf16x8 qf[4];
+  bf16x8 qf[QS][4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (qi < a.S) qf[t] = *reinterpret_cast<const bf16x8*>(Q + (long)qi * a.sqs + 16 * t + 8 * h);
-    else qf[t] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  for (int u = 0; u < QS; ++u) {
+    qi[u] = q0w + QW * u + r;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (qi[u] < a.S) qf[u][t] = *reinterpret_cast<const bf16x8*>(Q + (long)qi[u] * a.sqs + 16 * t + 8 * h);
+      else qf[u][t] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
   }
   const float sl2 = a.scale * LOG2E;
-  float m = -INFINITY, l = 0.f;
-  f32x16 o[2] = {zero16(), zero16()};  // O^T[d][q]: d tile 0..1
-  const int kend = a.causal ? min(a.S, qb * QB + QB) : a.S;
-  TileRegs<KBT> kr, vr;
+  float m[QS], l[QS];
+  f32x16 o[QS][2];  // O^T[d][q]: d tile 0..1
+#pragma unroll
+  for (int u = 0; u < QS; ++u) {
+    m[u] = -INFINITY;
+    l[u] = 0.f;
+    o[u][0] = o[u][1] = zero16();
+  }
+  const int kend = a.causal ? min(a.S, qb * QBW + QBW) : a.S;
+  TileRegs<KBT, NTH> kr, vr;
   tile_load_clamped(kr, K, a.sqs, 0, a.S);
   tile_load_clamped(vr, V, a.sqs, 0, a.S);
   tile_store(Ks[0], kr);
@@ -215,62 +233,79 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
       tile_load_clamped(kr, K, a.sqs, k0 + KBT, a.S);
       tile_load_clamped(vr, V, a.sqs, k0 + KBT, a.S);
     }
-    if (!(a.causal && k0 > q0w + QW - 1)) {  // else: all this wave's queries precede k0
+    if (!(a.causal && k0 > q0w + QWV - 1)) {  // else: all this wave's queries precede k0
       const u16* Kt = Ks[buf];
       const u16* Vt = Vs[buf];
-      // S^T for two 32-key sub-blocks
-      f32x16 s[NC];
+      // S^T for the 32-key sub-blocks of every query sub-block (one K fragment read feeds all QS of them). A query
+      // sub-block that lies wholly before k0 (QS = 2, diagonal tiles) computes scores that the mask turns to -inf:
+      // its p are 0 and its m, l, o stay unchanged (alpha = 1)
+      f32x16 s[QS][NC];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        s[c] = zero16();
 #pragma unroll
-        for (int t = 0; t < 4; ++t) s[c] = mfma(rowf(Kt, 32 * c + r, t, h), qf[t], s[c]);
+        for (int u = 0; u < QS; ++u) s[u][c] = zero16();
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const bf16x8 kfr = rowf(Kt, 32 * c + r, t, h);
+#pragma unroll
+          for (int u = 0; u < QS; ++u) s[u][c] = mfma(kfr, qf[u][t], s[u][c]);
+        }
       }
       // mask (diagonal / ragged tiles only) and running max on the RAW scores; the softmax scale
       // is folded into one FMA per score: p = exp2(s * c - max * c), c = scale * log2(e) > 0
       const bool edge = (a.causal && k0 + KBT - 1 > q0w) || k0 + KBT > a.S;
-      if (edge) {  // (one uniform branch; per element a compare + select: hipcc turned the per-element `if` into 2
-                   // scalar branches per score, on the unmasked tiles too)
-        const int lim = (a.causal ? min(qi, a.S - 1) : a.S - 1) - (k0 + 4 * h);  // last key this lane may see
+      float alpha[QS];
+#pragma unroll
+      for (int u = 0; u < QS; ++u) {
+        if (edge) {  // (one uniform branch; per element a compare + select: hipcc turned the per-element `if` into 2
+                     // scalar branches per score, on the unmasked tiles too)
+          const int lim = (a.causal ? min(qi[u], a.S - 1) : a.S - 1) - (k0 + 4 * h);  // last key this lane may see
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              s[u][c][i] = (32 * c + (i & 3) + 8 * (i >> 2) > lim) ? -INFINITY : s[u][c][i];
+        }
+        float mr = -INFINITY;
 #pragma unroll
         for (int c = 0; c < NC; ++c)
 #pragma unroll
-          for (int i = 0; i < 16; ++i)
-            s[c][i] = (32 * c + (i & 3) + 8 * (i >> 2) > lim) ? -INFINITY : s[c][i];
+          for (int i = 0; i < 16; ++i) mr = fmaxf(mr, s[u][c][i]);
+        mr = fmaxf(mr, __shfl_xor(mr, 32));
+        const float mx = fmaxf(m[u], mr * sl2);  // running max, log2 domain
+        alpha[u] = (m[u] == -INFINITY) ? 0.f : ex2(m[u] - mx);
+        const float msub = (mx == -INFINITY) ? 0.f : mx;  // all-masked so far: exp2(-inf) = 0
+        float rs = 0.f;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float p = ex2(__builtin_fmaf(s[u][c][i], sl2, -msub));
+            s[u][c][i] = p;
+            rs += p;
+          }
+        rs += __shfl_xor(rs, 32);
+        l[u] = l[u] * alpha[u] + rs;
+        m[u] = mx;
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[u][d][i] *= alpha[u];
       }
-      float mr = -INFINITY;
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) mr = fmaxf(mr, s[c][i]);
-      mr = fmaxf(mr, __shfl_xor(mr, 32));
-      const float mx = fmaxf(m, mr * sl2);  // running max, log2 domain
-      const float alpha = (m == -INFINITY) ? 0.f : ex2(m - mx);
-      const float msub = (mx == -INFINITY) ? 0.f : mx;  // all-masked so far: exp2(-inf) = 0
-      float rs = 0.f;
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = ex2(__builtin_fmaf(s[c][i], sl2, -msub));
-          s[c][i] = p;
-          rs += p;
-        }
-      rs += __shfl_xor(rs, 32);
-      l = l * alpha + rs;
-      m = mx;
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
-      // O^T[d][q] += sum_k V^T[d][k] P^T[k][q]   (V^T by transposed reads of the V image)
+      // O^T[d][q] += sum_k V^T[d][k] P^T[k][q]   (V^T by transposed reads of the V image, shared by the sub-blocks)
 #pragma unroll
       for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
-          bf16x8 pb = pack8(s[c], st);
+          bf16x8 pb[QS];
 #pragma unroll
-          for (int d = 0; d < 2; ++d) o[d] = mfma(trf(Vt, 32 * c + 16 * st, 32 * d, lane), pb, o[d]);
+          for (int u = 0; u < QS; ++u) pb[u] = pack8(s[u][c], st);
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const bf16x8 vt = trf(Vt, 32 * c + 16 * st, 32 * d, lane);
+#pragma unroll
+            for (int u = 0; u < QS; ++u) o[u][d] = mfma(vt, pb[u], o[u][d]);
+          }
         }
     }
     if (more) {
@@ -279,19 +314,22 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs a) {
     }
     __syncthreads();
   }
-  if (qi >= a.S) return;
-  const float inv = l > 0.f ? 1.f / l : 0.f;
-  u16* O = a.out + (long)b * a.sob + (long)hh * a.soh + (long)qi * a.sos;
 #pragma unroll
-  for (int d = 0; d < 2; ++d)
+  for (int u = 0; u < QS; ++u) {
+    if (qi[u] >= a.S) continue;
+    const float inv = l[u] > 0.f ? 1.f / l[u] : 0.f;
+    u16* O = a.out + (long)b * a.sob + (long)hh * a.soh + (long)qi[u] * a.sos;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      u16x4 v;
+    for (int d = 0; d < 2; ++d)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = f2bf(o[d][4 * g + e] * inv);
-      *reinterpret_cast<u16x4*>(O + 32 * d + 8 * g + 4 * h) = v;
-    }
-  if (h == 0) a.lse[(long)bh * a.S + qi] = m + log2f(l);
+      for (int g = 0; g < 4; ++g) {
+        u16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = f2bf(o[u][d][4 * g + e] * inv);
+        *reinterpret_cast<u16x4*>(O + 32 * d + 8 * g + 4 * h) = v;
+      }
+    if (h == 0) a.lse[(long)bh * a.S + qi[u]] = m[u] + log2f(l[u]);
+  }
 }
 
 // ============================================================================================
@@ -592,11 +630,22 @@ void attention_set_fwd_kb(int kb) { g_fwd_kb = kb; }
 
 void attention_fwd_bf16(const AttnShape& s, hipStream_t stream) {
   AttnArgs a = make_args(s);
+  const int qs = knob(KNOB_ATTN_FWD_QS);
+  if (qs == 2) {  // 64 queries per wave (two sub-blocks), 4 waves: 256 per workgroup
+    const int nqb = (s.S + 2 * QB - 1) / (2 * QB);
+    hipLaunchKernelGGL((attn_fwd_kernel<64, 2>), dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
+    return;
+  }
+  if (qs == 3) {  // 64 queries per wave, 2 waves: 128 per workgroup (the QS = 1 grid)
+    const int nqb = (s.S + QB - 1) / QB;
+    hipLaunchKernelGGL((attn_fwd_kernel<64, 2, 2>), dim3(nqb * s.B * s.H), dim3(128), 0, stream, a);
+    return;
+  }
   const int nqb = (s.S + QB - 1) / QB;
   if (g_fwd_kb == 128)
-    hipLaunchKernelGGL(attn_fwd_kernel<128>, dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<128, 1>), dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
   else
-    hipLaunchKernelGGL(attn_fwd_kernel<64>, dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
 }
 
 void attention_bwd_bf16(const AttnShape& s, hipStream_t stream) {
@@ -604,7 +653,7 @@ void attention_bwd_bf16(const AttnShape& s, hipStream_t stream) {
   const int nb = (s.S + QB - 1) / QB;
   // dQ first: it computes delta = rowsum(dO * O) for its own queries and writes it for dK/dV
   hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3(nb * s.B * s.H), dim3(256), 0, stream, a);
-  // dK/dV: 256 keys per workgroup (two 32-key tiles per wave, one wave per SIMD) unless knob ATTN_DKDV_KT = 1
+  // dK/dV: 128 keys per workgroup (one 32-key tile per wave); knob ATTN_DKDV_KT = 2: 256 (measured slower)
   if (knob(KNOB_ATTN_DKDV_KT) == 2) {
     const int nk2 = (s.S + 2 * QB - 1) / (2 * QB);
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, dim3(nk2 * s.B * s.H), dim3(256), 0, stream, a);

@@ -259,6 +259,33 @@ def test_flash_attention_dkdv_two_key_tiles_per_wave_bit_identical(B, S, H):
     assert torch.equal(grads[0], grads[1])
 
 
+@pytest.mark.parametrize("B,S,H", [(2, 1024, 3), (1, 333, 2), (2, 97, 1)])
+def test_flash_attention_forward_two_query_subblocks_bit_identical(B, S, H):
+    """The forward with two 32-query sub-blocks per wave (256 queries per workgroup; knob ATTN_FWD_QS=2) runs each
+    sub-block's score, softmax and PV chain in the same order as one sub-block per wave: bit-identical outputs and
+    gradients (the backward reads the forward's LSE), ragged S included."""
+    from simple_distributed_machine_learning_amd import _native
+    from simple_distributed_machine_learning_amd.ops.transformer import causal_attention
+
+    K = _native.kernels()
+    C = 64 * H
+    qkv0 = (rnd(B, S, 3 * C, seed=44) * 1.5).to(torch.bfloat16)
+    gy = rnd(B, S, C, seed=45).to(torch.bfloat16)
+    res = []
+    try:
+        for qs in (1, 2, 3):  # 3: two sub-blocks per wave in 2-wave workgroups
+            K.set_knob("ATTN_FWD_QS", qs)
+            qkv = qkv0.clone().requires_grad_(True)
+            y = causal_attention(qkv, H)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            res.append((y.detach().clone(), qkv.grad.clone()))
+    finally:
+        K.reset_knobs()
+    for y, g in res[1:]:
+        assert torch.equal(res[0][0], y) and torch.equal(res[0][1], g)
+
+
 def test_fused_relu_mask_protocol():
     # head: dx *= (x > 0); linear bwd: skip the gy mask, mask dx by (x > 0)
     M, Kd, C = 1000, 128, 10

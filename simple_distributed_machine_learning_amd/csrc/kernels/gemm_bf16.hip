@@ -38,6 +38,7 @@
 #include "gelu.h"
 #include "kernels.h"
 #include "lds_dma.h"
+#include "tile_order.h"
 
 namespace sdml {
 namespace {
@@ -65,7 +66,9 @@ struct GP {
   int ntstore;  // SDML_GEMM_NT_STORE=1: nontemporal epilogue stores (A/B)
   int gsave;    // EPI_BIAS_GELU: aux = bf16(gelu'(U)); EPI_DGELU: aux holds it (EPI_*_GRAD host values)
   int nostore;  // timing probe (SDML_GEMM_BF16_NOSTORE=1): the epilogue runs but skips its HBM stores
+  int group_m;  // tile order (tile_order.h): 0 = M fastest; g > 0 = groups of g m-tiles x every n-tile
 };
+
 
 __device__ __forceinline__ float bf2f(u16 v) { return __uint_as_float(((unsigned)v) << 16); }
 __device__ __forceinline__ u16 f2bf(float f) {
@@ -219,7 +222,8 @@ __global__ void __launch_bounds__(GT) gemm_bf16_kernel(GP p) {
     const int q = nwg / 8, r = nwg % 8, xcd = wg % 8;
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
   }
-  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;  // M fastest: neighbours share the B panel
+  int tm, tn;
+  tile_of(wg, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
   const int m0 = tm * TM, n0 = tn * TN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -360,7 +364,8 @@ __global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
     const int q = nwg / 8, r = nwg % 8, xcd = wg % 8;
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
   }
-  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;
+  int tm, tn;
+  tile_of(wg, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
   const int m0 = tm * TM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -535,7 +540,8 @@ __global__ void __launch_bounds__(T2_GT, 2) gemm_bf16_t2_kernel(GP p) {
     const int q = nwg / 8, r = nwg % 8, xcd = wg % 8;
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
   }
-  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;
+  int tm, tn;
+  tile_of(wg, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
   const int m0 = tm * T2_TM, n0 = tn * T2_TN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -639,6 +645,7 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
   p.tiles_n = (N + TN - 1) / TN;
   p.nostore = knob(KNOB_GEMM_BF16_NOSTORE) == 1;  // timing probe: pinned to 0 in production builds
   p.ntstore = knob(KNOB_GEMM_NT_STORE) == 1;
+  p.group_m = std::max(0, knob(KNOB_GEMM_GROUP_M));
   const dim3 grid(p.tiles_m * p.tiles_n);
 #define GB_LAUNCH(BLV, E) hipLaunchKernelGGL((gemm_bf16_kernel<BLV, E>), grid, dim3(GT), 0, stream, p)
 #define GB_EPI(BLV)                                       \

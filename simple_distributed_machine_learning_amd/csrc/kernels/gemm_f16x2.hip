@@ -39,6 +39,7 @@
 #include <string>
 
 #include "kernels.h"
+#include "tile_order.h"
 
 namespace sdml {
 namespace {
@@ -119,6 +120,7 @@ struct X2Gemm {
   int M, N, K, lda, ldb, ldc, ldm;
   int tiles_m, tiles_n;
   int ntstore;  // SDML_GEMM_NT_STORE=1: nontemporal epilogue stores (A/B)
+  int group_m;  // tile order (tile_order.h): 0 = M fastest; g > 0 = groups of g m-tiles x every n-tile
 };
 
 __device__ __forceinline__ void glds16(const void* src, unsigned char* lds_block) {
@@ -236,7 +238,8 @@ __global__ void __launch_bounds__(GT) x2_gemm_kernel(X2Gemm p) {
     const int q = nwg / 8, r = nwg % 8, xcd = wg % 8;
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
   }
-  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;  // M fastest: neighbours share the B panel
+  int tm, tn;
+  tile_of(wg, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
   const int m0 = tm * TM, n0 = tn * TN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -350,7 +353,8 @@ __global__ void __launch_bounds__(GT) x2_gemm_nt4_kernel(X2Gemm p) {
     const int q = nwg / 8, r = nwg % 8, xcd = wg % 8;
     wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
   }
-  const int tm = wg % p.tiles_m, tn = wg / p.tiles_m;
+  int tm, tn;
+  tile_of(wg, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
   const int m0 = tm * TM, n0 = tn * TN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -897,6 +901,7 @@ void x2_gemm(const void* A, int64_t a_ps, const void* B, int64_t b_ps, float* C,
   p.tiles_m = (M + TM - 1) / TM;
   p.tiles_n = (N + TN - 1) / TN;
   p.ntstore = knob(KNOB_GEMM_NT_STORE) == 1;
+  p.group_m = std::max(0, knob(KNOB_GEMM_GROUP_M));
   const dim3 grid(p.tiles_m * p.tiles_n);
   const int epi = (relu ? X2_RELU : 0) | (mask ? X2_MASK : 0);
 #define X2_LAUNCH(BLV, E) hipLaunchKernelGGL((x2_gemm_kernel<BLV, E>), grid, dim3(GT), 0, stream, p)

@@ -228,6 +228,37 @@ def test_gemm_bf16_192_wide_tiles_bit_identical_to_256(M, N, Kd):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("M,N,Kd", [(256, 192, 64), (3000, 776, 192), (4096, 768, 768), (1000, 2304, 3072),
+                                    (5000, 3072, 128)])
+def test_gemm_bf16_grouped_tile_order_bit_identical(M, N, Kd):
+    """Knob GEMM_GROUP_M: the NT / NN GEMMs visit their tiles in groups of g m-tiles x every n-tile (ragged last
+    group included) instead of M fastest. Only the order in which workgroups take tiles changes: bit-identical
+    outputs for every epilogue, both tile widths and the NN layout."""
+    g = torch.Generator(device="cpu").manual_seed(M + 11 * N)
+    A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    Wkn = W.t().contiguous()
+    bias = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    u_in = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    outs = {}
+    try:
+        for gm in (0, 3, 8):
+            for n192 in (0, 1):
+                K.set_knob("GEMM_GROUP_M", gm)
+                K.set_knob("GEMM_BF16_N192", n192)
+                C0, _ = K.gemm_bf16(A, W, None, False, 0)
+                C1, _ = K.gemm_bf16(A, W, bias, False, 1)
+                y, u = K.gemm_bf16(A, W, bias, False, 5)
+                du, _ = K.gemm_bf16(A, W, None, False, 6, u_in)
+                Cn, _ = K.gemm_bf16(A, Wkn, None, True, 0)
+                outs[(gm, n192)] = (C0, C1, y, u, du, Cn)
+    finally:
+        K.reset_knobs()
+    for key, o in outs.items():
+        for a, b in zip(outs[(0, key[1])], o):
+            assert torch.equal(a, b), key
+
+
 @pytest.mark.parametrize("M,N,Kd", [(256, 192, 64), (300, 776, 192), (4096, 768, 768), (1000, 2304, 3072)])
 def test_gemm_bf16_transposed_accumulators(M, N, Kd):
     """Knob GEMM_BF16_TR: the 4-phase NT GEMM with the MFMA operands swapped, so each lane accumulates 4 consecutive

@@ -47,6 +47,7 @@ typedef unsigned short u16;
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef u16 u16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int GT = 512, TM = 256, TN = 256, TK = 64;
@@ -118,6 +119,44 @@ __device__ __forceinline__ s16x4 ds_tr16(const unsigned char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
 }
 
+// the elementwise part of the epilogues on one 16-B row piece v (bf16(acc (+ bias)) of 8 columns gcol.. of row grow),
+// then its store (shared by the 8-wave and 4-wave kernels)
+template <int EPI>
+__device__ __forceinline__ void store_piece(const GP& p, const u16x8 v, int grow, int gcol) {
+  u16x8 o = v;
+  if constexpr (EPI == EPI_BIAS_GELU) {
+    u16x8* ap = reinterpret_cast<u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
+    if (p.gsave) {
+      u16x8 d;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = bf2f(v[e]), sg = gelu_sig(x);
+        o[e] = f2bf(x * sg);  // gelu_f's bits
+        d[e] = f2bf(gelu_grad_f(1.f, x));
+      }
+      if (p.ntstore) __builtin_nontemporal_store(d, ap);
+      else *ap = d;
+    } else {
+      if (p.ntstore) __builtin_nontemporal_store(v, ap);
+      else *ap = v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_f(bf2f(v[e])));
+    }
+  } else if constexpr (EPI == EPI_DGELU) {
+    const u16x8 u = *reinterpret_cast<const u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
+    if (p.gsave) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(u[e]) * bf2f(v[e]));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_grad_f(bf2f(v[e]), bf2f(u[e])));
+    }
+  }
+  u16x8* cp = reinterpret_cast<u16x8*>(p.C + (size_t)grow * p.ldc + gcol);
+  if (p.ntstore) __builtin_nontemporal_store(o, cp);
+  else *cp = o;
+}
+
 // epilogue shared by both main loops: bf16 rows through the (free) stage buffers, 16-B row pieces to HBM
 // WNW: waves along N (4: the 256 x 256 tile's 2 x 4 waves; 2: the 256 x 128 tile's 2 x 2)
 // NJ: 16-column tiles per wave (4: the wave owns 64 columns; 3: 48, the 256 x 192 tile)
@@ -178,38 +217,7 @@ __device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&ac
     const u16x8 v = *reinterpret_cast<const u16x8*>(W + row * 128 + 16 * (ch ^ rk_swz(row)));
     const int grow = m0 + wm * 128 + row, gcol = n0 + wn * 16 * NJ + 8 * ch;
     if (ch >= 2 * NJ || grow >= p.M || gcol >= p.N || p.nostore) continue;  // (N % 8 == 0: a chunk is all in or out)
-    u16x8 o = v;
-    if constexpr (EPI == EPI_BIAS_GELU) {
-      u16x8* ap = reinterpret_cast<u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
-      if (p.gsave) {
-        u16x8 d;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float x = bf2f(v[e]), sg = gelu_sig(x);
-          o[e] = f2bf(x * sg);  // gelu_f's bits
-          d[e] = f2bf(gelu_grad_f(1.f, x));
-        }
-        if (p.ntstore) __builtin_nontemporal_store(d, ap);
-        else *ap = d;
-      } else {
-        if (p.ntstore) __builtin_nontemporal_store(v, ap);
-        else *ap = v;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_f(bf2f(v[e])));
-      }
-    } else if constexpr (EPI == EPI_DGELU) {
-      const u16x8 u = *reinterpret_cast<const u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
-      if (p.gsave) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(u[e]) * bf2f(v[e]));
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_grad_f(bf2f(v[e]), bf2f(u[e])));
-      }
-    }
-    u16x8* cp = reinterpret_cast<u16x8*>(p.C + (size_t)grow * p.ldc + gcol);
-    if (p.ntstore) __builtin_nontemporal_store(o, cp);
-    else *cp = o;
+    store_piece<EPI>(p, v, grow, gcol);
   }
 }
 
@@ -493,6 +501,143 @@ __global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
   gemm_bf16_epilogue<EPI, 4, NJ, TR>(p, acc, smem, m0, n0, wave, lane);
 }
 
+// ---- NT form, 4 waves x 128 x 128 (one wave per SIMD) --------------------------------------------------------
+// 256 x 256 tile per 256-thread workgroup, waves 2 (M) x 2 (N), each wave a 128 x 128 output = 4 x 4
+// v_mfma_f32_32x32x16_bf16 accumulators (256 registers: one wave per SIMD, up to 512). The 8-wave kernels above
+// synchronise every phase (8 barriers per K-step, the two wave rows ping-ponging); here one barrier per 64-deep K-step
+// separates 64 MFMAs per wave (2048 cycles). Fragments: A rows and B rows (both k-contiguous) by ds_read_b128 from
+// [rows][64 k] images (the rk_swz chunk swizzle), double-buffered in registers one 16-deep substep ahead. Operands
+// arrive by LDS-DMA (inline-asm buffer_load ... lds, so the compiler counts only the fragment reads) into two 64 KiB
+// stages: K-step t + 1's 16 pieces per wave are issued 8 before each of K-step t's first two substeps' MFMAs and
+// retired by one vmcnt(0) before the K-step's barrier. The MFMA takes the B fragment as its first operand, so each lane accumulates
+// 4 consecutive output columns of one row (C^T layout): the epilogue writes 8-byte pieces into a [256][264] bf16 image,
+// then every thread stores 16-B row pieces through store_piece (all epilogues).
+constexpr int W4_GT = 256, W4_STAGE = 2 * A_BYTES, W4_LP = TN + 8;  // 64 KiB per stage; epilogue image pitch (bf16)
+constexpr int W4_SMEM = TM * W4_LP * 2 > 2 * W4_STAGE ? TM * W4_LP * 2 : 2 * W4_STAGE;
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(W4_GT, 1) gemm_bf16_w4_kernel(GP p) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[W4_SMEM];
+  const int nwg = p.tiles_m * p.tiles_n;
+  int wg = blockIdx.x;
+  if (nwg >= 16) {
+    const int q = nwg / 8, r = nwg % 8, xcd = wg % 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + wg / 8;
+  }
+  int tm, tn;
+  tile_of(wg, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int lane = threadIdx.x & 63, r32 = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // DMA pieces of one stage: 64 x 1 KiB, A rows 8q .. 8q + 7 (q < 32) then B rows; wave w issues q = w + 4u
+  const dma_i32x4 ra = dma_rsrc4(p.A, (unsigned)((size_t)p.M * p.lda * 2));
+  const dma_i32x4 rb = dma_rsrc4(p.B, (unsigned)((size_t)p.N * p.ldb * 2));
+  unsigned voff[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int q = wave + 4 * u, lr = 8 * (q & 31) + (lane >> 3);
+    const int c = (lane & 7) ^ rk_swz(lr);
+    voff[u] = u < 8 ? (unsigned)(((size_t)min(m0 + lr, p.M - 1) * p.lda + 8 * c) * 2)
+                    : (unsigned)(((size_t)min(n0 + lr, p.N - 1) * p.ldb + 8 * c) * 2);
+  }
+  auto issue4 = [&](int kt, unsigned char* stage, int u0) {  // pieces u0 .. u0 + 3 of K-step kt
+#pragma unroll
+    for (int u = u0; u < u0 + 4; ++u)
+      bdma16_asm(u < 8 ? ra : rb, voff[u], (unsigned)kt * TK * 2, stage + 1024 * (wave + 4 * u));
+  };
+  // fragment byte offsets (stage-relative): row base + the lane's swizzled chunk of substep s; tile i / j at +4096 i
+  const int xr = (r32 >> 1) & 7;  // rk_swz of every fragment row (rows 32 i + r32 + multiples of 32)
+  const int abase = (wm * 128 + r32) * 128, bbase = A_BYTES + (wn * 128 + r32) * 128;
+  int xo[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) xo[s2] = 16 * ((2 * s2 + h) ^ xr);
+
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nk = p.K / TK;
+  issue4(0, smem, 0);
+  issue4(0, smem, 4);
+  issue4(0, smem, 8);
+  issue4(0, smem, 12);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16x8 fa[2][4], fb[2][4];
+  for (int t = 0; t < nk; ++t) {
+    const unsigned char* st = smem + (t & 1) * W4_STAGE;
+    unsigned char* nx = smem + ((t + 1) & 1) * W4_STAGE;
+    const bool more = t + 1 < nk;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[0][i] = ld_b128(st + abase + 4096 * i + xo[0]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[0][j] = ld_b128(st + bbase + 4096 * j + xo[0]);
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+      const int cb = s2 & 1;
+      if (s2 < 3) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[cb ^ 1][i] = ld_b128(st + abase + 4096 * i + xo[s2 + 1]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[cb ^ 1][j] = ld_b128(st + bbase + 4096 * j + xo[s2 + 1]);
+      }
+      if (more && s2 < 2) {  // the next K-step's DMA early: 8 pieces before substep 0's MFMAs, 8 before substep 1's
+        issue4(t + 1, nx, 8 * s2);
+        issue4(t + 1, nx, 8 * s2 + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma32(fb[cb][j], fa[cb][i], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  // epilogue: acc[i][j] (C^T layout: lane = output row m = wm*128 + 32 i + r32; register e -> column
+  // n = wn*128 + 32 j + (e & 3) + 8 (e >> 2) + 4 h) -> bf16(acc (+ bias)) image [256][W4_LP], 8 B per 4 registers
+  u16* img = reinterpret_cast<u16*>(smem);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int col = wn * 128 + 32 * j + 8 * g + 4 * h;
+      float bj[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bj[e] = bf2f(p.bias[min(n0 + col + e, p.N - 1)]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        typedef u16 u16x4 __attribute__((ext_vector_type(4)));
+        u16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = f2bf(acc[i][j][4 * g + e] + bj[e]);
+        *reinterpret_cast<u16x4*>(img + (wm * 128 + 32 * i + r32) * W4_LP + col) = v;
+      }
+    }
+  __syncthreads();
+#pragma unroll 4
+  for (int it = 0; it < 32; ++it) {
+    const int row = 8 * it + (threadIdx.x >> 5), ch = threadIdx.x & 31;
+    const int grow = m0 + row, gcol = n0 + 8 * ch;
+    if (grow >= p.M || gcol >= p.N || p.nostore) continue;  // (N % 8 == 0: a piece is all in or out)
+    store_piece<EPI>(p, *reinterpret_cast<const u16x8*>(img + row * W4_LP + 8 * ch), grow, gcol);
+  }
+}
+
 // ---- NT form, 256 x 128 tiles of 4 waves, two workgroups per CU ---------------------------------------
 // The 256 x 256 kernels above take all 160 KiB of LDS, so one workgroup runs per CU and every CU reaches its
 // epilogue (the bf16 stores of its tile) at the same moment, with no main loop left to hide them under
@@ -672,6 +817,13 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
   }
   if (b_kn) {
     GB_EPI(1);
+  } else if (knob(KNOB_GEMM_BF16_W4) == 1) {  // 4 waves x 128 x 128, one barrier per K-step
+    switch (epi) {
+      case EPI_BIAS: hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI_BIAS>), grid, dim3(W4_GT), 0, stream, p); break;
+      case EPI_BIAS_GELU: hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI_BIAS_GELU>), grid, dim3(W4_GT), 0, stream, p); break;
+      case EPI_DGELU: hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI_DGELU>), grid, dim3(W4_GT), 0, stream, p); break;
+      default: hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI_STORE>), grid, dim3(W4_GT), 0, stream, p); break;
+    }
   } else if (nt4) {
     const bool n192 = nt4_use_192(p.tiles_m, N);
     if (n192) p.tiles_n = (N + 191) / 192;

@@ -52,6 +52,7 @@ const Entry kTable[KNOB_COUNT] = {
     {"ATTN_DKDV_KT", 1, false, nullptr},
     {"U8_FH_ROWS512", 0, false, nullptr},
     {"GEMM_GROUP_M", 8, false, nullptr},
+    {"GEMM_BF16_W4", 0, false, nullptr},
     {"ATTN_FWD_QS", 1, false, nullptr},
     {"GEMM_BF16_NOSTORE", 0, true, nullptr},
     {"U8_VARIANT", 0, true, nullptr},

@@ -259,6 +259,35 @@ def test_gemm_bf16_grouped_tile_order_bit_identical(M, N, Kd):
             assert torch.equal(a, b), key
 
 
+@pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 776, 192), (4096, 768, 768), (1000, 2304, 3072),
+                                    (16384, 3072, 768)])
+def test_gemm_bf16_four_wave_kernel_matches_fp32(M, N, Kd):
+    """Knob GEMM_BF16_W4: the NT GEMM on 4 waves of 128 x 128 (32x32x16 MFMAs, one barrier per K-step) against fp32 and
+    against the 8-wave kernel, for every epilogue (a different MFMA shape sums each dot product in another internal
+    order: equal within one bf16 rounding)."""
+    g = torch.Generator(device="cpu").manual_seed(M + 13 * N)
+    A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    u_in = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    ref = A.float() @ W.float().t()
+    outs = {}
+    try:
+        for w4 in (0, 1):
+            K.set_knob("GEMM_BF16_W4", w4)
+            C0, _ = K.gemm_bf16(A, W, None, False, 0)
+            C1, _ = K.gemm_bf16(A, W, bias, False, 1)
+            y, u = K.gemm_bf16(A, W, bias, False, 5)
+            du, _ = K.gemm_bf16(A, W, None, False, 6, u_in)
+            outs[w4] = (C0, C1, y, u, du)
+            torch.testing.assert_close(C0.float(), ref, rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+            torch.testing.assert_close(C1.float(), ref + bias.float(), rtol=1e-2, atol=1e-2 * float(ref.abs().max()))
+    finally:
+        K.reset_knobs()
+    for a, b in zip(outs[0], outs[1]):
+        torch.testing.assert_close(a.float(), b.float(), rtol=1e-2, atol=1e-2 * float(a.float().abs().max()) + 1e-3)
+
+
 @pytest.mark.parametrize("M,N,Kd", [(256, 192, 64), (300, 776, 192), (4096, 768, 768), (1000, 2304, 3072)])
 def test_gemm_bf16_transposed_accumulators(M, N, Kd):
     """Knob GEMM_BF16_TR: the 4-phase NT GEMM with the MFMA operands swapped, so each lane accumulates 4 consecutive

@@ -59,7 +59,7 @@ def pmc(paths):
     for p in paths:
         for r in csv.DictReader(open(p)):
             n = r["Kernel_Name"]
-            if "sdml" not in n:
+            if "sdml" not in n and "Cijk" not in n:  # (hipBLASLt's GEMMs kept for A/B passes)
                 continue
             key = n.replace("sdml::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
             agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))

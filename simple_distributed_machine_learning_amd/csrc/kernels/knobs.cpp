@@ -53,6 +53,7 @@ const Entry kTable[KNOB_COUNT] = {
     {"U8_FH_ROWS512", 0, false, nullptr},
     {"GEMM_GROUP_M", 8, false, nullptr},
     {"GEMM_BF16_W4", 0, false, nullptr},
+    {"U8_WGRAD_PAIR", 0, false, nullptr},
     {"ATTN_FWD_QS", 1, false, nullptr},
     {"GEMM_BF16_NOSTORE", 0, true, nullptr},
     {"U8_VARIANT", 0, true, nullptr},

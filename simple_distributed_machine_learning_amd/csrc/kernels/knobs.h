@@ -53,6 +53,7 @@ enum KnobId : int {
                              // faster: profiles/r6_fused_rows512_ab.jsonl), 1, -1 auto (when they cover every CU)
   KNOB_GEMM_GROUP_M,         // bf16 / fp16-plane GEMM tile order: 0 M fastest, g > 0 groups of g m-tiles (tile_order.h)
   KNOB_GEMM_BF16_W4,         // bf16 NT GEMM: 1 = the 4-wave 128 x 128-per-wave kernel (one barrier per K-step)
+  KNOB_U8_WGRAD_PAIR,        // ring uint8 weight gradient: pairwise in-kernel combine of splits s and s + S/2
   KNOB_ATTN_FWD_QS,          // attention forward: 32-query sub-blocks per wave (1, or 2: two independent softmax chains; 3: 2 in 2-wave blocks)
   // ---- probe switches (pinned in production builds) ----
   KNOB_GEMM_BF16_NOSTORE,    // 1: bf16 GEMM skips its output stores (timing only)

@@ -773,6 +773,8 @@ struct WgradParams {
   int xcd;                   // 0: plain order (split-major), A/B only (SDML_U8_WGRAD_XCD=0)
   int prio;                  // 1: s_setprio 1 on waves 4..7 (knob U8_WGRAD_PRIO)
   long long* stamps;         // experiments builds only: [blocks][8 waves][16] phase stamps (u8_set_wgrad_stamps)
+  unsigned* pair;            // ring kernel, pairwise combine (knob U8_WGRAD_PAIR): [groups][splits / 2][2] ticket and
+                             // flag words, zero between launches (the second arriver of a pair resets them); null: off
 };
 
 // experiments builds: s_memtime stamps of the weight gradient's phases (tools/u8_wgrad_stamps.py); slot 0 / 15 hold
@@ -856,28 +858,91 @@ __device__ __forceinline__ void wgrad_scales(const WgradParams& p, int n0, int r
 }
 
 // partial tile -> slab (plain stores); C map: column = lane & 31, row = (r&3) + 8(r>>2) + 4h
+// add (pairwise combine, the second arriver): the partner's partial is read from slab row `add_row` and each element
+// stored is (own partial) + (partner's) - one fp32 add, commutative, so the pair sum has the same bits whichever of the
+// two arrived first
+// pairwise-combine memory forms (the write-through hand-off of cdna_hip_programming.md Guideline 16, R1): the first
+// arriver stores its partial sc1 (agent-scope relaxed atomic stores), the second loads it sc1 (agent-scope relaxed
+// atomic loads, past this CU's L1), so neither needs an L2-wide release / acquire fence
+__device__ __forceinline__ void st_sc1(float* a, float v) { __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ float ld_sc1(const float* a) {
+  return __hip_atomic_load(const_cast<float*>(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// role: -1 no pairing (plain stores), 0 first arriver (sc1 stores, row = own split), 1 second arriver (the partner's
+// partial read from add_row, (own + partner) stored plain)
 template <int NCT>
 __device__ __forceinline__ void wgrad_store_tile(const WgradParams& p, const f32x16 (&acc)[2][NCT], int split, int n0,
-                                                 int ct0, int lane, float out_scale) {
+                                                 int ct0, int lane, float out_scale, int role = -1, int add_row = 0) {
+#pragma clang fp contract(off)  // the pair sum is (rounded product) + partner: never one fma, which would be role-dependent
   float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
+  const float* pin = p.slab + (size_t)add_row * ((size_t)p.N * GKC + p.N);
 #pragma unroll
   for (int j = 0; j < NCT; ++j) {
     const int col = 32 * (ct0 + j) + (lane & 31);
     if (col >= GKC) continue;
+    float other[2][16];
+    if (role == 1) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          other[i][r] = ld_sc1(pin + (size_t)(n0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * GKC + col);
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int n = n0 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        out[(size_t)n * GKC + col] = acc[i][j][r] * out_scale;
+        const float v = acc[i][j][r] * out_scale;
+        if (role == 0) st_sc1(out + (size_t)n * GKC + col, v);
+        else out[(size_t)n * GKC + col] = role == 1 ? v + other[i][r] : v;
       }
   }
+}
+
+// Pairwise combine of the ring weight gradient's row splits (knob U8_WGRAD_PAIR): split s < S/2 and split s + S/2 of
+// one hidden group (the same XCD under the XCD-aware order) draw a ticket when their K loop ends. The first arriver
+// stores its partial into its own slab row and publishes it (every wave's stores drained, barrier, agent-scope release,
+// flag); the second waits for the flag (the first is resident and only storing: a bounded wait), acquires, and stores
+// (own + partner) into row s, then resets both words for the next launch. The reduction that follows reads S/2 rows
+// instead of S. Returns the role: 0 first arriver, 1 second; `red` holds a free LDS int for the broadcast. The
+// payload is handed over write-through (st_sc1 / ld_sc1): a release / acquire pair of agent-scope fences instead
+// (an L2 write-back on every first arriver) made the kernel ~20 us slower.
+__device__ __forceinline__ int wgrad_pair_role(const WgradParams& p, int group, int split, int t, int* red) {
+  unsigned* w = p.pair + 2 * ((size_t)group * (p.splits / 2) + (split % (p.splits / 2)));
+  __syncthreads();  // every wave's last fragment reads are done before red is written
+  if (t == 0) red[0] = (int)__hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int role = red[0];
+  __syncthreads();
+  if (role == 1) {
+    if (t == 0) {
+      for (int it = 0; it < (1 << 26) && __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+           ++it)
+        __builtin_amdgcn_s_sleep(1);
+      __hip_atomic_store(w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(w + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // every load of the partner's bytes is sc1 (ld_sc1): no acquire, only keep the compiler from hoisting them
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+  }
+  return role;
+}
+
+// the first arriver's publish, after all of its slab stores
+__device__ __forceinline__ void wgrad_pair_publish(const WgradParams& p, int group, int split, int t) {
+  unsigned* w = p.pair + 2 * ((size_t)group * (p.splits / 2) + (split % (p.splits / 2)));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(w + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // bias-gradient partial: the 32 threads of each hidden float4 meet in LDS (red: 4 GT free floats, after a barrier)
 template <int FD>
 __device__ __forceinline__ void wgrad_store_bias(const WgradParams& p, const f32x4& bsum, int split, int n0, int t,
-                                                 float* red) {
+                                                 float* red, int role = -1, int add_row = 0) {
   float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
   *reinterpret_cast<f32x4*>(red + 4 * t) = bsum;
   __syncthreads();
@@ -887,7 +952,9 @@ __device__ __forceinline__ void wgrad_store_bias(const WgradParams& p, const f32
       const int owner = FD != 0 ? 64 * ((rr >> 4) * 4 + (t >> 4)) + 16 * ((t >> 2) & 3) + (rr & 15) : rr * 16 + (t >> 2);
       sacc += red[4 * owner + (t & 3)];
     }
-    out[(size_t)p.N * GKC + n0 + t] = sacc;
+    if (role == 1) sacc += ld_sc1(p.slab + (size_t)add_row * ((size_t)p.N * GKC + p.N) + (size_t)p.N * GKC + n0 + t);
+    if (role == 0) st_sc1(out + (size_t)p.N * GKC + n0 + t, sacc);
+    else out[(size_t)p.N * GKC + n0 + t] = sacc;
   }
 }
 
@@ -1161,7 +1228,11 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
   if (p.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   U8W_STAMP(0, __builtin_amdgcn_s_memrealtime);
   U8W_STAMP(1, __builtin_amdgcn_s_memtime);
-  const int n0 = (p.g0 + (p.xcd ? (L % G8) / 8 : L % p.groups)) * GHN;
+  const int group = p.xcd ? (L % G8) / 8 : L % p.groups;
+  const int n0 = (p.g0 + group) * GHN;
+  // pairwise combine of splits s and s + S/2 (wgrad_pair_role); role 0 when off
+  const bool pairing = p.pair != nullptr;
+  int role = -1;
   const int r0 = split * p.rows_per_split;
   const int nk = min(p.rows_per_split, p.M - r0) / GBK;  // host: M % GBK == 0
   float dz_up = 0.f, out_scale = 0.f;
@@ -1440,12 +1511,21 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
       }
     }
     U8W_STAMP(10, __builtin_amdgcn_s_memtime);
-    wgrad_store_tile<NCT>(p, acc, split, n0, ct0, lane, out_scale);
+    if (pairing) role = wgrad_pair_role(p, group, split, t, reinterpret_cast<int*>(rsm));
+    const int row = role == 1 ? split % (p.splits / 2) : split;  // the pair sum goes to the lower split's row
+    const int add_row = split < p.splits / 2 ? split + p.splits / 2 : split - p.splits / 2;
+    wgrad_store_tile<NCT>(p, acc, row, n0, ct0, lane, out_scale, role, add_row);
     if constexpr (HALF) {  // C map of 16x16: column lane & 15, rows 4 (lane >> 4) + v
-      float* out = p.slab + (size_t)split * ((size_t)p.N * GKC + p.N);
+#pragma clang fp contract(off)
+      float* out = p.slab + (size_t)row * ((size_t)p.N * GKC + p.N);
+      const float* pin = p.slab + (size_t)add_row * ((size_t)p.N * GKC + p.N);
 #pragma unroll
-      for (int v = 0; v < 4; ++v)
-        out[(size_t)(n0 + 16 * (wave - 4) + 4 * (lane >> 4) + v) * GKC + 768 + (lane & 15)] = hacc[v] * out_scale;
+      for (int v = 0; v < 4; ++v) {
+        const size_t e = (size_t)(n0 + 16 * (wave - 4) + 4 * (lane >> 4) + v) * GKC + 768 + (lane & 15);
+        const float o = hacc[v] * out_scale;
+        if (role == 0) st_sc1(out + e, o);
+        else out[e] = role == 1 ? o + ld_sc1(pin + e) : o;
+      }
     }
     U8W_STAMP(11, __builtin_amdgcn_s_memtime);
   };
@@ -1459,7 +1539,12 @@ __global__ void __launch_bounds__(GT) u8_wgrad_ring_kernel(WgradParams p) {
     else run(I3{}, std::false_type{}, std::false_type{});
   }
   __syncthreads();
-  wgrad_store_bias<2>(p, bsum, split, n0, t, reinterpret_cast<float*>(rsm));
+  {
+    const int row = role == 1 ? split % (p.splits / 2) : split;
+    const int add_row = split < p.splits / 2 ? split + p.splits / 2 : split - p.splits / 2;
+    wgrad_store_bias<2>(p, bsum, row, n0, t, reinterpret_cast<float*>(rsm), role, add_row);
+  }
+  if (pairing && role == 0) wgrad_pair_publish(p, group, split, t);
   U8W_STAMP(12, __builtin_amdgcn_s_memtime);
   U8W_STAMP(15, __builtin_amdgcn_s_memrealtime);
 }
@@ -1584,6 +1669,23 @@ static int wgrad_xcd() {
   return knob(KNOB_U8_WGRAD_XCD);
 }
 
+// the pairwise combine's ticket / flag words: one zeroed allocation per device, made on the first eager call (none is
+// made while a stream is being captured: the combine is then off for that launch); the kernel leaves them zero
+static unsigned* wgrad_pair_words(hipStream_t stream) {
+  static unsigned* words[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!words[dev]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    void* w = nullptr;
+    if (hipMalloc(&w, 4096 * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(w, 0, 4096 * sizeof(unsigned)) != hipSuccess) return nullptr;
+    words[dev] = static_cast<unsigned*>(w);
+  }
+  return words[dev];
+}
+
 static int tail_substeps(int K) {
   const int v = K - ((K + FBK - 1) / FBK - 1) * FBK;
   if (v > FBK / 2 - 8) return NSUB;
@@ -1685,6 +1787,11 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigne
 #endif
   const dim3 wgrid(((splits + 7) / 8) * 8 * p.groups);
   const bool ilv = knob(KNOB_U8_WGRAD_ILV) != 0;
+  // pairwise combine (ring kernel, whole weight gradient, XCD-aware order so splits s and s + S/2 share an XCD)
+  p.pair = nullptr;
+  if (!grp && p.xcd && splits % 16 == 0 && p.groups * splits <= 4096 && knob(KNOB_U8_WGRAD_PAIR) != 0 && mask && !ilv &&
+      knob(KNOB_U8_WGRAD_RING) != 0)
+    p.pair = wgrad_pair_words(stream);
   // the DMA-ring form: ReLU bits, one DMA piece of them and two of dl rows per K-step, 16-B aligned sources
   const bool ring = mask && !ilv && knob(KNOB_U8_WGRAD_RING) != 0 && N <= 256 && C <= 16 &&
                     (reinterpret_cast<uintptr_t>(dl) & 15) == 0 && (reinterpret_cast<uintptr_t>(mask) & 15) == 0;
@@ -1711,6 +1818,8 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigne
   else if (ilv) hipLaunchKernelGGL((u8_wgrad_kernel<1, true>), wgrid, dim3(GT), 0, stream, p);
   else hipLaunchKernelGGL((u8_wgrad_kernel<1, false>), wgrid, dim3(GT), 0, stream, p);
   const int64_t n = (int64_t)N * GKC + N;
+  const int rsplits = (ring && p.pair) ? splits / 2 : splits;  // rows left for the reduction
+  if (!ring) p.pair = nullptr;
   if (grp) {  // this hidden-group range only: its weight rows, then its bias entries (+ the head's reduction)
     if (sgd && sgd->p) abort();  // host contract: the split weight gradient is not the fused optimizer step
     const int64_t b_off = (int64_t)N * GKC + grp->g_first * GHN;
@@ -1718,10 +1827,10 @@ void u8_wgrad_dl(const float* dl, const float* w2, const float* h, const unsigne
                             (int64_t)(grp->g_first + grp->g_count) * GHN * GKC, b_off, b_off + grp->g_count * GHN, head,
                             nullptr, stream);
   } else if (head && head->part) {
-    launch_slab_head_reduce(slab, n, splits, gwb, 0, n, n, n, head, sgd, stream);
+    launch_slab_head_reduce(slab, n, rsplits, gwb, 0, n, n, n, head, sgd, stream);
   } else {
     if (sgd && sgd->p) abort();  // host contract: the fused step needs the head reduction in the same launch
-    slab_reduce(slab, n, splits, gwb, n, stream);
+    slab_reduce(slab, n, rsplits, gwb, n, stream);
   }
 }
 

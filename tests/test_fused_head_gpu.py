@@ -338,6 +338,38 @@ def test_wgrad_ring_balanced_tiles(M, C, Nh):
     torch.testing.assert_close(g1.double(), want, rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("M,C,Nh", [(131072, 10, 128), (65536, 10, 128), (131072 + 256, 10, 128), (8192, 16, 256)])
+def test_wgrad_ring_pairwise_combine(M, C, Nh):
+    """Knob U8_WGRAD_PAIR: splits s and s + S/2 of the ring weight gradient add their partials in-kernel (ticket, the
+    first arriver publishes, the second adds and stores into row s) and the reduction reads S/2 rows. Equal to the
+    unpaired gradient to fp32 summation order, repeatable bit for bit over launches (the pair sum is one commutative
+    add, whoever arrives first; the ticket words reset themselves), and within the fp64 bound. Shapes whose split
+    count is not a multiple of 16 run unpaired."""
+    from simple_distributed_machine_learning_amd import _native
+
+    K = _native.kernels()
+    x8 = pixels(M, 81)
+    h = rnd(M, Nh, seed=82).relu()
+    dl = rnd(M, C, seed=83, scale=1e-3)
+    w2 = rnd(C, Nh, seed=84, scale=0.1)
+    bits = ops.relu_bits(h)
+    outs = []
+    try:
+        for pair in (0, 1, 1, 1):
+            K.set_knob("U8_WGRAD_PAIR", pair)
+            b = torch.zeros(Nh * KD + Nh, device=DEV)
+            ops.linear_wgrad_u8_dl(x8, dl, w2, bits, b[:Nh * KD].view(Nh, KD), b[Nh * KD:])
+            torch.cuda.synchronize()
+            outs.append(b)
+    finally:
+        K.reset_knobs()
+    assert torch.equal(outs[1], outs[2]) and torch.equal(outs[1], outs[3])
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-5, atol=1e-6 * float(outs[0].abs().max()))
+    dz = (dl.double() @ w2.double()) * (h > 0).double()
+    want = dz.t() @ (x8.double() / 255.0)
+    torch.testing.assert_close(outs[1][:Nh * KD].view(Nh, KD).double(), want, rtol=1e-4, atol=1e-6)
+
+
 @pytest.mark.parametrize("ring,cols", [(0, 64), (1, 64), (1, 32)])
 def test_wgrad_hidden_group_ranges_match_the_whole_gradient(ring, cols):
     """linear_wgrad_u8_dl(groups=(g_first, g_count, blocks)) - the data-parallel step's two hidden-unit ranges

@@ -128,15 +128,67 @@ class _LinearFn(torch.autograd.Function):
         (x2,) = ctx.saved_tensors
         w, b = ctx.w, ctx.b
         g2 = gy.reshape(-1, gy.shape[-1])
+        wt = _w_t(w) if (ctx.needs_input_grad[0] and ctx.hand and g2.stride(-1) == 1) else None
+        # the weight gradient first when it goes to the side stream (it then runs beside the input gradient)
+        side = _on_side(g2)
+        if side:
+            gw, gb = _param_grads(g2, x2, w, b, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         dx = None
         if ctx.needs_input_grad[0]:
-            if ctx.hand and g2.stride(-1) == 1:
-                dx, _ = kernels().gemm_bf16(g2, _w_t(w), None, False, EPI_STORE)
+            if wt is not None:
+                dx, _ = kernels().gemm_bf16(g2, wt, None, False, EPI_STORE)
                 dx = dx.view(ctx.in_shape)
             else:
                 dx = (g2 @ w).view(ctx.in_shape)
-        gw, gb = _param_grads(g2, x2, w, b, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        if not side:
+            gw, gb = _param_grads(g2, x2, w, b, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         return dx, gw, gb
+
+
+# The in-place weight-gradient GEMMs (into the flat-buffer .grad) run on a side stream, beside the input-gradient GEMMs
+# and the rest of the backward on the compute stream (GPT-2 step +1.8 %, profiles/r6_wgrad_side_stream_ab.jsonl).
+# The compute stream waits for them at the end of every backward pass (an autograd engine callback queued by the first
+# side launch of the pass) and wherever the engine synchronises or steps a stage's gradients (join_side_streams).
+# SDML_WGRAD_STREAM=0 keeps them on the compute stream.
+WGRAD_STREAM = os.environ.get("SDML_WGRAD_STREAM", "1") == "1"
+_SIDE = {}
+_PENDING = []
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def join_side_streams():
+    """The compute stream waits for every side-stream weight gradient issued since the last join."""
+    while _PENDING:
+        s = _PENDING.pop()
+        torch.cuda.current_stream(s.device).wait_stream(s)
+
+
+def _on_side(g2):
+    return WGRAD_STREAM and g2.is_cuda and not torch.cuda.is_current_stream_capturing()
+
+
+def _wgrad_launch(g2, x2, gw, gb):
+    """gw (+ gb) += the weight (bias) gradient, on the side stream when _on_side (see WGRAD_STREAM)."""
+    if not _on_side(g2):
+        kernels().wgrad_bf16_(g2, x2, gw, gb)
+        return
+    cur = torch.cuda.current_stream(g2.device)
+    side = _side_stream(g2.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        kernels().wgrad_bf16_(g2, x2, gw, gb)
+    g2.record_stream(side)  # (the caching allocator must not hand these to the compute stream before the side is done)
+    x2.record_stream(side)
+    if not _PENDING:  # first side launch of this backward pass: join when the pass ends
+        torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
+    if side not in _PENDING:
+        _PENDING.append(side)
 
 
 def _param_grads(g2, x2, w, b, need_w: bool, need_b: bool):
@@ -148,7 +200,7 @@ def _param_grads(g2, x2, w, b, need_w: bool, need_b: bool):
         if w.grad is not None and _wgrad_ok(g2, x2, w.grad):
             fuse_b = (b is not None and need_b and b.grad is not None
                       and b.grad.is_contiguous() and b.grad.dtype == torch.bfloat16)
-            kernels().wgrad_bf16_(g2, x2, w.grad, b.grad if fuse_b else None)
+            _wgrad_launch(g2, x2, w.grad, b.grad if fuse_b else None)
             bias_done = fuse_b
         elif w.grad is not None:
             w.grad.addmm_(g2.t(), x2)
@@ -203,14 +255,19 @@ class _MLPFn(torch.autograd.Function):
         else:
             du, _ = kernels().gemm_bf16(g2, w2, None, True, _GELU_EPI[1], u)  # (dY W2) * gelu'(U)
         gw2, gb2 = _param_grads(g2, a, w2, b2, ctx.needs_input_grad[3], ctx.needs_input_grad[4])
+        w1t = _w_t(w1) if (ctx.needs_input_grad[0] and _HAND and du.stride(-1) == 1) else None
+        side = _on_side(du)
+        if side:  # (as in _LinearFn: the side-stream weight gradient first)
+            gw1, gb1 = _param_grads(du, x2, w1, b1, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         dx = None
         if ctx.needs_input_grad[0]:
-            if _HAND and du.stride(-1) == 1:
-                dx, _ = kernels().gemm_bf16(du, _w_t(w1), None, False, EPI_STORE)
+            if w1t is not None:
+                dx, _ = kernels().gemm_bf16(du, w1t, None, False, EPI_STORE)
                 dx = dx.view(ctx.in_shape)
             else:
                 dx = (du @ w1).view(ctx.in_shape)
-        gw1, gb1 = _param_grads(du, x2, w1, b1, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        if not side:
+            gw1, gb1 = _param_grads(du, x2, w1, b1, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         return dx, gw1, gb1, gw2, gb2
 
 
@@ -301,17 +358,18 @@ class _LMHeadFn(torch.autograd.Function):
         if gp is None:  # an unpadded gradient (another loss): pad a copy
             gp = torch.zeros((T, Vp), dtype=g2.dtype, device=g2.device)
             gp[:, :V] = g2
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx, _ = kernels().gemm_bf16(gp, _w_t(wp), None, False, EPI_STORE)
-            dx = dx.view(ctx.in_shape)
+        wpt = _w_t(wp) if ctx.needs_input_grad[0] else None
         gw = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1]:  # (first: on the side stream it runs beside the input gradient)
             gpad = _padded(w.grad, Vp) if w.grad is not None else None
             if gpad is not None and _wgrad_ok(gp, x2, gpad):
-                kernels().wgrad_bf16_(gp, x2, gpad, None)
+                _wgrad_launch(gp, x2, gpad, None)
             else:
                 gw = gp[:, :V].t() @ x2
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx, _ = kernels().gemm_bf16(gp, wpt, None, False, EPI_STORE)
+            dx = dx.view(ctx.in_shape)
         return dx, gw
 
 

@@ -32,6 +32,7 @@ import torch
 from ..models.base import ModelSpec, PipelineStage, build_stages
 from .. import ops
 from ..ops import pixels_to_float
+from ..ops.linear import join_side_streams
 from ..ops.optim import FusedSGD
 from ..utils.flat import FlatParams
 from ..utils.timing import PhaseTimer
@@ -327,10 +328,13 @@ class PipelineEngine:
                 # two spans of the split weight gradient when the replicas run it: _planned_dp_spans)
                 if rotate_a2a:
                     self._issue_planned_spans(self._planned_dp_spans())
+                    join_side_streams()
                     self.grad_sync.finish_all()
                 else:
+                    join_side_streams()
                     self.grad_sync.finish()
                 if step_optimizer:
+                    join_side_streams()
                     self.optimizer.step()
                     self.global_step += 1
                 self._advance_rng()
@@ -487,6 +491,7 @@ class PipelineEngine:
                     else:
                         outbox[key] = gx
                 if last_bwd.get(ins.stage) == i:
+                    join_side_streams()  # side-stream weight gradients (ops/linear.py SDML_WGRAD_STREAM) are done
                     self.grad_sync.stage_done(ins.stage)
             if self.debug_sync and dev.type == "cuda":
                 torch.cuda.synchronize(dev)
@@ -498,9 +503,11 @@ class PipelineEngine:
                 self.transport.drain_sends()
         if train:
             with tm.span("grad_sync"):
+                join_side_streams()
                 self.grad_sync.finish()
             if step_optimizer:
                 with tm.span("optim"):
+                    join_side_streams()
                     self.optimizer.step()
                 self.global_step += 1
             self._advance_rng()
@@ -804,12 +811,14 @@ class PipelineEngine:
             if spans_left[0]:  # the same two collectives as the replicas that ran the split
                 self._issue_planned_spans(dp_spans)
             with tm.span("grad_sync"):  # both stages' gradients in one collective
+                join_side_streams()
                 self.grad_sync.finish_all()
             if step_optimizer:
                 with tm.span("optim"):
                     if step_fused[0]:  # applied by the last weight-gradient reduction
                         self.optimizer.commit_fused()
                     else:
+                        join_side_streams()
                         self.optimizer.step()
                 self.global_step += 1
             self._advance_rng()

@@ -16,6 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from .._native import kernels
+from . import side_stream
 
 
 # ResidualLink joins (set False to let autograd add the two gradients of a block input, for A/B tests)
@@ -237,6 +238,17 @@ class _Conv3x3Fn(torch.autograd.Function):
         w = ctx.w
         K = kernels()
         dy = dy.contiguous(memory_format=torch.channels_last)
+        gw = None
+        if ctx.needs_input_grad[1]:
+            if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
+                # straight into the flat gradient buffer (SDML_CONV_WGRAD_STREAM=1: on the side stream, launched first so
+                # it runs beside the input gradient below; ops/side_stream.py)
+                g = w.grad
+                side_stream.launch(lambda: K.conv3x3_wgrad_bf16_(dy, x, g), dy, x,
+                                   enabled=side_stream.CONV_WGRAD_STREAM)
+            else:
+                gw = torch.zeros_like(w)
+                K.conv3x3_wgrad_bf16_(dy, x, gw)
         dx = None
         if ctx.needs_input_grad[0]:
             add = _take_addend(ctx.link)
@@ -249,13 +261,6 @@ class _Conv3x3Fn(torch.autograd.Function):
             else:
                 dx = K.conv3x3_fwd_bf16(dy, ctx.wd, add=add)
         ctx.wd = ctx.back = None
-        gw = None
-        if ctx.needs_input_grad[1]:
-            if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
-                K.conv3x3_wgrad_bf16_(dy, x, w.grad)  # straight into the flat gradient buffer
-            else:
-                gw = torch.zeros_like(w)
-                K.conv3x3_wgrad_bf16_(dy, x, gw)
         return dx, gw, None, None, None
 
 
@@ -310,17 +315,19 @@ class _ConvGeneralFn(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         w, st, pd = ctx.w, ctx.stride, ctx.pad
         dy = dy.contiguous(memory_format=torch.channels_last)
+        gw = None
+        if ctx.needs_input_grad[1]:  # (first: on the side stream it runs beside the input gradient)
+            if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
+                g = w.grad
+                side_stream.launch(lambda: kernels().conv_wgrad_bf16_(dy, x, g, st, pd), dy, x,
+                                   enabled=side_stream.CONV_WGRAD_STREAM)
+            else:
+                gw = torch.zeros_like(w)
+                kernels().conv_wgrad_bf16_(dy, x, gw, st, pd)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _general_dgrad(dy, x, w, st, pd, add=_take_addend(ctx.link), back=ctx.back)
         ctx.back = None
-        gw = None
-        if ctx.needs_input_grad[1]:
-            if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
-                kernels().conv_wgrad_bf16_(dy, x, w.grad, st, pd)
-            else:
-                gw = torch.zeros_like(w)
-                kernels().conv_wgrad_bf16_(dy, x, gw, st, pd)
         return dx, gw, None, None, None, None, None
 
 

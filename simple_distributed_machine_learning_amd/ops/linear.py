@@ -30,6 +30,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .._native import kernels
+from . import side_stream
+from .side_stream import join_side_streams  # noqa: F401 (re-export for the engine)
 
 
 # SDML_GPT2_GEMM=hand (default): the forward and input-gradient GEMMs of these Linears on gemm_bf16.hip's 4-phase NT
@@ -145,50 +147,14 @@ class _LinearFn(torch.autograd.Function):
         return dx, gw, gb
 
 
-# The in-place weight-gradient GEMMs (into the flat-buffer .grad) run on a side stream, beside the input-gradient GEMMs
-# and the rest of the backward on the compute stream (GPT-2 step +1.8 %, profiles/r6_wgrad_side_stream_ab.jsonl).
-# The compute stream waits for them at the end of every backward pass (an autograd engine callback queued by the first
-# side launch of the pass) and wherever the engine synchronises or steps a stage's gradients (join_side_streams).
-# SDML_WGRAD_STREAM=0 keeps them on the compute stream.
-WGRAD_STREAM = os.environ.get("SDML_WGRAD_STREAM", "1") == "1"
-_SIDE = {}
-_PENDING = []
-
-
-def _side_stream(dev):
-    s = _SIDE.get(dev.index)
-    if s is None:
-        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
-    return s
-
-
-def join_side_streams():
-    """The compute stream waits for every side-stream weight gradient issued since the last join."""
-    while _PENDING:
-        s = _PENDING.pop()
-        torch.cuda.current_stream(s.device).wait_stream(s)
-
-
+# weight gradients on a side stream beside the input gradient (ops/side_stream.py)
 def _on_side(g2):
-    return WGRAD_STREAM and g2.is_cuda and not torch.cuda.is_current_stream_capturing()
+    return side_stream.on_side(g2)
 
 
 def _wgrad_launch(g2, x2, gw, gb):
-    """gw (+ gb) += the weight (bias) gradient, on the side stream when _on_side (see WGRAD_STREAM)."""
-    if not _on_side(g2):
-        kernels().wgrad_bf16_(g2, x2, gw, gb)
-        return
-    cur = torch.cuda.current_stream(g2.device)
-    side = _side_stream(g2.device)
-    side.wait_stream(cur)
-    with torch.cuda.stream(side):
-        kernels().wgrad_bf16_(g2, x2, gw, gb)
-    g2.record_stream(side)  # (the caching allocator must not hand these to the compute stream before the side is done)
-    x2.record_stream(side)
-    if not _PENDING:  # first side launch of this backward pass: join when the pass ends
-        torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
-    if side not in _PENDING:
-        _PENDING.append(side)
+    """gw (+ gb) += the weight (bias) gradient, on the side stream when it is on (ops/side_stream.py)."""
+    side_stream.launch(lambda: kernels().wgrad_bf16_(g2, x2, gw, gb), g2, x2)
 
 
 def _param_grads(g2, x2, w, b, need_w: bool, need_b: bool):

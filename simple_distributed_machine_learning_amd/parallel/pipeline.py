@@ -32,7 +32,7 @@ import torch
 from ..models.base import ModelSpec, PipelineStage, build_stages
 from .. import ops
 from ..ops import pixels_to_float
-from ..ops.linear import join_side_streams
+from ..ops.side_stream import join_side_streams
 from ..ops.optim import FusedSGD
 from ..utils.flat import FlatParams
 from ..utils.timing import PhaseTimer

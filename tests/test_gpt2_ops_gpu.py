@@ -392,3 +392,37 @@ def test_lm_head_padded_vocabulary_matches_fp32(T, C, V):
     gw = flat.grads[:Vp * C].view(Vp, C)
     torch.testing.assert_close(gw[:V].float(), gref.t() @ x.detach().float(), rtol=2e-2, atol=2e-3)
     assert int((gw[V:] != 0).sum()) == 0 and int((flat.params[V * C:Vp * C] != 0).sum()) == 0
+
+
+def test_side_stream_weight_gradients_are_joined_after_backward():
+    """ops/side_stream.py: with the weight gradients on the side stream, a plain loss.backward() returns with the
+    compute stream already waiting for them (the autograd-engine callback), so reading .grad right after it on the
+    compute stream - no synchronise, no engine join - gives the same bits as the one-stream order. Three layers, so
+    several side launches queue behind each other in one pass; the long first layer keeps the side stream busy."""
+    from simple_distributed_machine_learning_amd.ops import linear as lin
+    from simple_distributed_machine_learning_amd.ops import side_stream
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    dims = [(768, 3072), (3072, 768), (768, 768)]
+    ws = [(torch.randn(o, i, generator=g) * 0.02).to(DEV, torch.bfloat16).requires_grad_(True) for i, o in dims]
+    bs = [torch.zeros(o, device=DEV, dtype=torch.bfloat16).requires_grad_(True) for _, o in dims]
+    x0 = torch.randn(16384, 768, generator=g).to(DEV, torch.bfloat16)
+    grads = {}
+    saved = side_stream.WGRAD_STREAM
+    try:
+        for on in (False, True):
+            side_stream.WGRAD_STREAM = on
+            for p in ws + bs:  # the flat-buffer form: .grad exists, the kernels accumulate into it in place
+                p.grad = torch.zeros_like(p)
+            torch.cuda.synchronize()
+            y = x0
+            for w, b in zip(ws, bs):
+                y = lin.linear(y, w, b)
+            y.float().square().mean().backward()
+            grads[on] = [p.grad.clone() for p in ws + bs]  # on the compute stream, straight after backward
+            torch.cuda.synchronize()
+    finally:
+        side_stream.WGRAD_STREAM = saved
+        side_stream.join_side_streams()
+    for a, b in zip(grads[False], grads[True]):
+        assert torch.equal(a, b)

@@ -53,38 +53,98 @@ __device__ __forceinline__ unsigned short f32_to_bf16(float f) {
   return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));
 }
 
+// one 8-element chunk i: loads (issued by the caller before any use), then the update and its stores
+struct MixedIn {
+  f32x4 mv[2], bo[2];
+  u16x8 gr;
+};
+
+template <bool NT>
+__device__ __forceinline__ MixedIn mixed_load_(const float* master, const unsigned short* g, const float* buf, int64_t i,
+                                              bool use_buf) {
+  MixedIn in;
+  const f32x4* m4 = reinterpret_cast<const f32x4*>(master) + 2 * i;
+  const f32x4* b4 = reinterpret_cast<const f32x4*>(buf) + 2 * i;
+  const u16x8* g8 = reinterpret_cast<const u16x8*>(g) + i;
+  if constexpr (NT) {
+    in.mv[0] = __builtin_nontemporal_load(m4);
+    in.mv[1] = __builtin_nontemporal_load(m4 + 1);
+    in.gr = __builtin_nontemporal_load(g8);
+    if (use_buf) {
+      in.bo[0] = __builtin_nontemporal_load(b4);
+      in.bo[1] = __builtin_nontemporal_load(b4 + 1);
+    }
+  } else {
+    in.mv[0] = m4[0];
+    in.mv[1] = m4[1];
+    in.gr = *g8;
+    if (use_buf) {
+      in.bo[0] = b4[0];
+      in.bo[1] = b4[1];
+    }
+  }
+  return in;
+}
+
+// (nontemporal loads measured 2x slower on this stream: plain loads only)
+template <bool NT>
+__device__ __forceinline__ MixedIn mixed_load(const float* master, const unsigned short* g, const float* buf, int64_t i,
+                                              bool use_buf) {
+  return mixed_load_<false>(master, g, buf, i, use_buf);
+}
+
+template <bool NT, typename T>
+__device__ __forceinline__ void st(T* p, const T& v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <bool NT>
+__device__ __forceinline__ void mixed_update(MixedIn in, float* master, unsigned short* p, unsigned short* g,
+                                             float* buf, int64_t i, float lr, float mom, float damp, float wd,
+                                             int nesterov, int first, int zero_grad) {
+  if (zero_grad) st<NT>(reinterpret_cast<u16x8*>(g) + i, u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+  u16x8 po;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    f32x4 d = {bf16_to_f32(in.gr[4 * h]), bf16_to_f32(in.gr[4 * h + 1]), bf16_to_f32(in.gr[4 * h + 2]),
+               bf16_to_f32(in.gr[4 * h + 3])};
+    if (wd != 0.f) d += wd * in.mv[h];
+    if (mom != 0.f) {
+      const f32x4 b = first ? d : mom * in.bo[h] + (1.f - damp) * d;
+      st<NT>(reinterpret_cast<f32x4*>(buf) + 2 * i + h, b);
+      d = nesterov ? d + mom * b : b;
+    }
+    in.mv[h] = in.mv[h] - lr * d;
+    st<NT>(reinterpret_cast<f32x4*>(master) + 2 * i + h, in.mv[h]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) po[4 * h + e] = f32_to_bf16(in.mv[h][e]);
+  }
+  st<NT>(reinterpret_cast<u16x8*>(p) + i, po);
+}
+
+// V = 0: one chunk per loop trip; V = 1: two chunks (i, i + stride) per trip, both chunks' loads issued before either
+// update; V = 2: one chunk, nontemporal stores. Same arithmetic, bit-identical results.
+template <int V>
 __global__ void __launch_bounds__(256) sgd_mixed_kernel(float* __restrict__ master, unsigned short* __restrict__ p,
                                                         unsigned short* __restrict__ g, float* __restrict__ buf,
                                                         int64_t n8, float lr, float mom, float damp, float wd,
                                                         int nesterov, int first, int zero_grad) {
+  constexpr bool NT = V == 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
-    f32x4 mv[2] = {reinterpret_cast<f32x4*>(master)[2 * i], reinterpret_cast<f32x4*>(master)[2 * i + 1]};
-    const u16x8 gr = reinterpret_cast<u16x8*>(g)[i];
-    f32x4 bo[2];
-    if (mom != 0.f && !first) {
-      bo[0] = reinterpret_cast<f32x4*>(buf)[2 * i];
-      bo[1] = reinterpret_cast<f32x4*>(buf)[2 * i + 1];
+  const bool use_buf = mom != 0.f && !first;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if constexpr (V == 1) {
+    for (; i + stride < n8; i += 2 * stride) {
+      const MixedIn a = mixed_load<NT>(master, g, buf, i, use_buf);
+      const MixedIn b = mixed_load<NT>(master, g, buf, i + stride, use_buf);
+      mixed_update<NT>(a, master, p, g, buf, i, lr, mom, damp, wd, nesterov, first, zero_grad);
+      mixed_update<NT>(b, master, p, g, buf, i + stride, lr, mom, damp, wd, nesterov, first, zero_grad);
     }
-    if (zero_grad) reinterpret_cast<u16x8*>(g)[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    u16x8 po;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      f32x4 d = {bf16_to_f32(gr[4 * h]), bf16_to_f32(gr[4 * h + 1]), bf16_to_f32(gr[4 * h + 2]),
-                 bf16_to_f32(gr[4 * h + 3])};
-      if (wd != 0.f) d += wd * mv[h];
-      if (mom != 0.f) {
-        const f32x4 b = first ? d : mom * bo[h] + (1.f - damp) * d;
-        reinterpret_cast<f32x4*>(buf)[2 * i + h] = b;
-        d = nesterov ? d + mom * b : b;
-      }
-      mv[h] = mv[h] - lr * d;
-      reinterpret_cast<f32x4*>(master)[2 * i + h] = mv[h];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) po[4 * h + e] = f32_to_bf16(mv[h][e]);
-    }
-    reinterpret_cast<u16x8*>(p)[i] = po;
   }
+  for (; i < n8; i += stride)
+    mixed_update<NT>(mixed_load<NT>(master, g, buf, i, use_buf), master, p, g, buf, i, lr, mom, damp, wd, nesterov,
+                     first, zero_grad);
 }
 
 __global__ void __launch_bounds__(256) synth_kernel(uint64_t seed, int64_t start, int64_t n, int H, int W, int mode,
@@ -121,9 +181,11 @@ void sgd_momentum_mixed(float* master, void* p_bf16, void* g_bf16, float* buf, i
   int64_t blocks = (n8 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(sgd_mixed_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, master,
-                     static_cast<unsigned short*>(p_bf16), static_cast<unsigned short*>(g_bf16), buf, n8, lr, momentum,
-                     dampening, wd, nesterov ? 1 : 0, first ? 1 : 0, zero_grad ? 1 : 0);
+  const int v = knob(KNOB_SGD_MIXED_V);
+  auto* k = v == 1 ? sgd_mixed_kernel<1> : v == 2 ? sgd_mixed_kernel<2> : sgd_mixed_kernel<0>;
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), 0, stream, master, static_cast<unsigned short*>(p_bf16),
+                     static_cast<unsigned short*>(g_bf16), buf, n8, lr, momentum, dampening, wd, nesterov ? 1 : 0,
+                     first ? 1 : 0, zero_grad ? 1 : 0);
 }
 
 void synth_mnist(uint64_t seed, int64_t start, int64_t n, int H, int W, int mode, float* x, int64_t* y,

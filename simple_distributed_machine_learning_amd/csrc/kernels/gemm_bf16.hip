@@ -121,15 +121,16 @@ __device__ __forceinline__ s16x4 ds_tr16(const unsigned char* p) {
 
 // the elementwise part of the epilogues on one 16-B row piece v (bf16(acc (+ bias)) of 8 columns gcol.. of row grow),
 // then its store (shared by the 8-wave and 4-wave kernels)
-template <int EPI>
-__device__ __forceinline__ void store_piece(const GP& p, const u16x8 v, int grow, int gcol) {
-  u16x8 o = v;
+template <int EPI, typename V = u16x8>
+__device__ __forceinline__ void store_piece(const GP& p, const V v, int grow, int gcol) {
+  constexpr int W = sizeof(V) / sizeof(u16);  // 8 (16-B row pieces) or 4 (the persistent kernel's 8-B pieces)
+  V o = v;
   if constexpr (EPI == EPI_BIAS_GELU) {
-    u16x8* ap = reinterpret_cast<u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
+    V* ap = reinterpret_cast<V*>(p.aux + (size_t)grow * p.ldaux + gcol);
     if (p.gsave) {
-      u16x8 d;
+      V d;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < W; ++e) {
         const float x = bf2f(v[e]), sg = gelu_sig(x);
         o[e] = f2bf(x * sg);  // gelu_f's bits
         d[e] = f2bf(gelu_grad_f(1.f, x));
@@ -140,19 +141,19 @@ __device__ __forceinline__ void store_piece(const GP& p, const u16x8 v, int grow
       if (p.ntstore) __builtin_nontemporal_store(v, ap);
       else *ap = v;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_f(bf2f(v[e])));
+      for (int e = 0; e < W; ++e) o[e] = f2bf(gelu_f(bf2f(v[e])));
     }
   } else if constexpr (EPI == EPI_DGELU) {
-    const u16x8 u = *reinterpret_cast<const u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
+    const V u = *reinterpret_cast<const V*>(p.aux + (size_t)grow * p.ldaux + gcol);
     if (p.gsave) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(u[e]) * bf2f(v[e]));
+      for (int e = 0; e < W; ++e) o[e] = f2bf(bf2f(u[e]) * bf2f(v[e]));
     } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(gelu_grad_f(bf2f(v[e]), bf2f(u[e])));
+      for (int e = 0; e < W; ++e) o[e] = f2bf(gelu_grad_f(bf2f(v[e]), bf2f(u[e])));
     }
   }
-  u16x8* cp = reinterpret_cast<u16x8*>(p.C + (size_t)grow * p.ldc + gcol);
+  V* cp = reinterpret_cast<V*>(p.C + (size_t)grow * p.ldc + gcol);
   if (p.ntstore) __builtin_nontemporal_store(o, cp);
   else *cp = o;
 }
@@ -501,6 +502,255 @@ __global__ void __launch_bounds__(GT) gemm_bf16_nt4_kernel(GP p) {
   gemm_bf16_epilogue<EPI, 4, NJ, TR>(p, acc, smem, m0, n0, wave, lane);
 }
 
+// ---- NT form, persistent 4-phase loop (knob GEMM_BF16_PERSIST) ------------------------------------------------
+// The nt4 kernel above takes all 160 KiB of LDS, so one workgroup runs per CU and each tile pays a launch, a prologue
+// (the first K-step's DMA latency with nothing to compute) and an LDS epilogue behind two barriers. Here one
+// workgroup per CU walks the tiles v = blockIdx.x, + G, + 2G, ... (G = min(tiles, CUs); blockIdx % 8 is the XCD, so the
+// bijective remap above gives every XCD the same contiguous tile ranges as the one-tile-per-workgroup launch) and
+// the half-tile stream runs on across tiles: the global K-step T = nk * k + t (k-th tile of this workgroup) picks
+// the slots ((4T + q) % 10) exactly as in nt4, and the loop's past-the-end half-tiles of tile k (K-steps nk, nk + 1)
+// are the first K-steps of tile k + 1, so its DMA lands under tile k's last phases. The epilogue cannot take 128 KiB
+// of LDS (the ring is busy with tile k + 1): each wave stages its tile 32 rows at a time in a private 4 KiB of the
+// two slots that are free at the tile boundary (see the epilogue), then stores 16-B row pieces through store_piece
+// (same elementwise math, same bits). Storing the C^T accumulators' 8-B pieces straight from registers measured
+// 10-25 % slower per GEMM (four 32-B row fragments per 128-B line). The epilogue has no workgroup barrier: the wave
+// rows' one-barrier ping-pong carries on across tiles. The counted vmcnt waits stay
+// correct with the epilogue's loads / stores in the count: they are older than the half-tiles a wait leaves in
+// flight, so a wait only retires more. nk >= 2 (the next tile's reach is K-steps 0 and 1).
+template <int Q, int NJ = 4>
+__device__ __forceinline__ void issue_half_at(const GP& p, unsigned char* smem, int h, int ks, int m0, int n0,
+                                              int wave, int lane) {
+  const int k0 = ks * TK;
+  unsigned char* slot = smem + (h % NSLOT) * HT;
+#pragma unroll
+  for (int v = 0; v < half_pieces<Q, NJ>(); ++v) {
+    const int qq = wave + 8 * v;
+    const int lr = 8 * qq + (lane >> 3);
+    const int c = (lane & 7) ^ rk_swz(lr);
+    if constexpr (Q == 0 || Q == 3) {
+      const int tr = (lr >> 6) * 128 + (Q == 3 ? 64 : 0) + (lr & 63);
+      glds16(p.A + (size_t)min(m0 + tr, p.M - 1) * p.lda + k0 + 8 * c, slot + 1024 * qq);
+    } else {
+      constexpr int R2 = 16 * (NJ - 2);
+      const int tr = Q == 1 ? (lr >> 5) * 16 * NJ + (lr & 31) : (lr / R2) * 16 * NJ + 32 + (lr % R2);
+      glds16(p.B + (size_t)min(n0 + tr, p.N - 1) * p.ldb + k0 + 8 * c, slot + 1024 * qq);
+    }
+  }
+}
+
+template <int EPI, int NJ = 4>
+__global__ void __launch_bounds__(GT) gemm_bf16_nt4p_kernel(GP p) {
+  static_assert(NJ == 3 || NJ == 4, "n-tiles per wave");
+  constexpr int BN = 64 * NJ, NJ1 = NJ - 2;
+  constexpr int INFLIGHT = half_pieces<0, NJ>() + half_pieces<1, NJ>() + half_pieces<2, NJ>();
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NSLOT * HT];
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int G = gridDim.x;
+  auto tile_at = [&](int v, int& m0, int& n0) {
+    int wg = v;
+    if (ntiles >= 16) {
+      const int q = ntiles / 8, r = ntiles % 8, xcd = v % 8;
+      wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + v / 8;
+    }
+    int tm, tn;
+    tile_of(wg, p.tiles_m, p.tiles_n, p.group_m, tm, tn);
+    m0 = tm * TM;
+    n0 = tn * BN;
+  };
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int g = lane >> 4, l16 = lane & 15;
+
+  int aoff[4][2], boff[2][2], boff1[NJ1][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r = wm * 64 + 16 * i + l16;
+      aoff[i][s2] = r * 128 + 16 * ((4 * s2 + g) ^ rk_swz(r));
+    }
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r = wn * 32 + 16 * jj + l16;
+      boff[jj][s2] = r * 128 + 16 * ((4 * s2 + g) ^ rk_swz(r));
+    }
+#pragma unroll
+  for (int jj = 0; jj < NJ1; ++jj)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int r = wn * 16 * NJ1 + 16 * jj + l16;
+      boff1[jj][s2] = r * 128 + 16 * ((4 * s2 + g) ^ rk_swz(r));
+    }
+
+  const int nk = p.K / TK;  // >= 2 (host)
+  int v = blockIdx.x;
+  int m0, n0, nm0, nn0;
+  tile_at(v, m0, n0);
+  bool has_next = v + G < ntiles;
+  if (has_next) tile_at(v + G, nm0, nn0);
+  int kbase = 0;  // global K-step of this tile's K-step 0
+  // half-tile H (global): this tile's K-step, the next tile's first ones, or (last tile) a re-read of the last K-step
+  auto issue = [&](auto qc, int H) {
+    constexpr int Q = decltype(qc)::value;
+    const int lt = (H >> 2) - kbase;
+    if (lt < nk) issue_half_at<Q, NJ>(p, smem, H, lt, m0, n0, wave, lane);
+    else if (has_next) issue_half_at<Q, NJ>(p, smem, H, lt - nk, nm0, nn0, wave, lane);
+    else issue_half_at<Q, NJ>(p, smem, H, nk - 1, m0, n0, wave, lane);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  issue(I0{}, 0);
+  issue(I1{}, 1);
+  issue(I2{}, 2);
+  issue(I3{}, 3);
+  issue(I0{}, 4);
+  issue(I1{}, 5);
+  issue(I2{}, 6);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // wave row 1 runs one barrier behind row 0, across all tiles
+
+  f32x4 acc[8][NJ];
+  bf16x8 a[4][2], b0[2][2], b1[NJ1][2];
+  auto mfma_quadrant = [&](int qm, const auto& bb, auto qn_c) {
+    constexpr int QN = decltype(qn_c)::value;
+    constexpr int NQ = QN == 0 ? 2 : NJ1;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < NQ; ++jj)
+          acc[4 * qm + i][2 * QN + jj] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[jj][s2], a[i][s2], acc[4 * qm + i][2 * QN + jj], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync_mid = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto sync_end = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // K-steps t < nk - 2 fetch within this tile (no tile test per issue); the last two run on into the next tile
+    auto kstep = [&](int t, auto tail_c) {
+      constexpr bool TAIL = decltype(tail_c)::value;
+      const int T = kbase + t;
+      const int h = 4 * T + 7;
+      auto iss = [&](auto qc, int H) {
+        constexpr int Q = decltype(qc)::value;
+        if constexpr (TAIL) issue(qc, H);
+        else issue_half_at<Q, NJ>(p, smem, H, (H >> 2) - kbase, m0, n0, wave, lane);
+      };
+      const unsigned char* s0 = smem + ((4 * T) % NSLOT) * HT;
+      const unsigned char* s1 = smem + ((4 * T + 1) % NSLOT) * HT;
+      const unsigned char* s2p = smem + ((4 * T + 2) % NSLOT) * HT;
+      const unsigned char* s3 = smem + ((4 * T + 3) % NSLOT) * HT;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) b0[jj][s2] = ld_b128(s1 + boff[jj][s2]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = ld_b128(s0 + aoff[i][s2]);
+      iss(I3{}, h);
+      sync_mid();
+      mfma_quadrant(0, b0, I0{});
+      sync_end();
+#pragma unroll
+      for (int jj = 0; jj < NJ1; ++jj)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) b1[jj][s2] = ld_b128(s2p + boff1[jj][s2]);
+      iss(I0{}, h + 1);
+      sync_mid();
+      mfma_quadrant(0, b1, I1{});
+      sync_end();
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) a[i][s2] = ld_b128(s3 + aoff[i][s2]);
+      iss(I1{}, h + 2);
+      sync_mid();
+      mfma_quadrant(1, b1, I1{});
+      sync_end();
+      iss(I2{}, h + 3);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(INFLIGHT) : "memory");
+      sync_mid();
+      mfma_quadrant(1, b0, I0{});
+      sync_end();
+    };
+    using BF = std::integral_constant<bool, false>;
+    using BT = std::integral_constant<bool, true>;
+    for (int t = 0; t < nk - 2; ++t) kstep(t, BF{});
+    kstep(nk - 2, BT{});
+    kstep(nk - 1, BT{});
+    // epilogue through a wave-private 4 KiB of the ring, 32 rows per pass (16-B row pieces as in nt4). Free slots: the
+    // last K-step's q2 and q3 ((4T + 2) % 10, (4T + 3) % 10, T = kbase + nk - 1): no DMA in flight targets them, every
+    // wave's reads of them retired before the barrier that ends row 0's last phase, and the next tile refills them
+    // only after barriers that wave row 1 reaches past its own epilogue (row 1 runs one barrier behind row 0)
+    {
+      const int T = kbase + nk - 1;
+      unsigned char* E = smem + ((4 * T + 2 + (wave >> 2)) % NSLOT) * HT + (wave & 3) * 4096;
+      float bj[NJ][4] = {};
+      if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bj[j][r] = bf2f(p.bias[min(n0 + wn * 16 * NJ + 16 * j + 4 * g + r, p.N - 1)]);
+      }
+#pragma unroll
+      for (int pass = 0; pass < 4; ++pass) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int row = 16 * ii + l16, col = 16 * j + 4 * g;
+            typedef u16 u16x4 __attribute__((ext_vector_type(4)));
+            u16x4 pv;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pv[r] = f2bf(acc[2 * pass + ii][j][r] + bj[j][r]);
+            *reinterpret_cast<u16x4*>(E + row * 128 + 16 * ((col >> 3) ^ rk_swz(row)) + 2 * (col & 7)) = pv;
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int row = 8 * it + (lane >> 3), ch = lane & 7;
+          const u16x8 pv = *reinterpret_cast<const u16x8*>(E + row * 128 + 16 * (ch ^ rk_swz(row)));
+          const int grow = m0 + wm * 128 + 32 * pass + row, gcol = n0 + wn * 16 * NJ + 8 * ch;
+          if (ch >= 2 * NJ || grow >= p.M || gcol >= p.N || p.nostore) continue;
+          store_piece<EPI>(p, pv, grow, gcol);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this pass's reads done before the next pass rewrites E
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    v += G;
+    if (v >= ntiles) break;
+    kbase += nk;
+    m0 = nm0;
+    n0 = nn0;
+    has_next = v + G < ntiles;
+    if (has_next) tile_at(v + G, nm0, nn0);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // rejoin wave row 1
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last tile's past-the-end re-reads land before exit
+}
+
 // ---- NT form, 4 waves x 128 x 128 (one wave per SIMD) --------------------------------------------------------
 // 256 x 256 tile per 256-thread workgroup, waves 2 (M) x 2 (N), each wave a 128 x 128 output = 4 x 4
 // v_mfma_f32_32x32x16_bf16 accumulators (256 registers: one wave per SIMD, up to 512). The 8-wave kernels above
@@ -829,6 +1079,30 @@ void gemm_bf16(const void* A, const void* B, void* C, int M, int N, int K, int l
     if (n192) p.tiles_n = (N + 191) / 192;
     const dim3 g4(p.tiles_m * p.tiles_n);
     const bool tr = knob(KNOB_GEMM_BF16_TR) != 0;
+    // persistent workgroups (knob GEMM_BF16_PERSIST: -1 auto, 0, 1). Auto: where they measured faster at the GPT-2
+    // shapes (tools/probes/gemm_persist_ab.py, profiles/r6_gemm_persistent_ab.jsonl): many tiles per CU (the lm_head
+    // forward, 49 per CU: 1320 -> 1235 us) or a very long K (its input gradient, 786 K-steps: 1065 -> 1034 us); at 1-3
+    // tiles per CU it is level or slower, and the gelu'-multiply epilogue's aux reads stall it (92 -> 108 us)
+    const int pk = knob(KNOB_GEMM_BF16_PERSIST);
+    const bool persist = pk >= 0 ? pk == 1
+                                 : (epi != EPI_DGELU && ((int64_t)p.tiles_m * p.tiles_n >= 8 * (int64_t)device_cus() ||
+                                                         K / TK >= 256));
+    if (tr && K / TK >= 2 && persist) {
+      const dim3 gp((unsigned)std::min<int64_t>((int64_t)p.tiles_m * p.tiles_n, device_cus()));
+#define NT4P_LAUNCH(E)                                                                             \
+  do {                                                                                             \
+    if (n192) hipLaunchKernelGGL((gemm_bf16_nt4p_kernel<E, 3>), gp, dim3(GT), 0, stream, p);        \
+    else hipLaunchKernelGGL((gemm_bf16_nt4p_kernel<E, 4>), gp, dim3(GT), 0, stream, p);             \
+  } while (0)
+      switch (epi) {
+        case EPI_BIAS: NT4P_LAUNCH(EPI_BIAS); break;
+        case EPI_BIAS_GELU: NT4P_LAUNCH(EPI_BIAS_GELU); break;
+        case EPI_DGELU: NT4P_LAUNCH(EPI_DGELU); break;
+        default: NT4P_LAUNCH(EPI_STORE); break;
+      }
+#undef NT4P_LAUNCH
+      return;
+    }
 #define NT4_LAUNCH(E)                                                                                  \
   do {                                                                                                 \
     if (n192 && tr) hipLaunchKernelGGL((gemm_bf16_nt4_kernel<E, 3, true>), g4, dim3(GT), 0, stream, p); \

@@ -259,6 +259,40 @@ def test_gemm_bf16_grouped_tile_order_bit_identical(M, N, Kd):
             assert torch.equal(a, b), key
 
 
+@pytest.mark.parametrize("M,N,Kd", [(256, 192, 128), (3000, 776, 192), (4096, 768, 768), (16384, 3072, 768),
+                                    (20000, 2304, 256), (2048, 50304, 128)])
+def test_gemm_bf16_persistent_kernel_bit_identical(M, N, Kd):
+    """Knob GEMM_BF16_PERSIST: one workgroup per CU walks its tiles with the half-tile stream running on into the
+    next tile, and stores its epilogue from registers (8-B pieces). Same MFMAs in the same order and the same
+    elementwise math as the one-tile-per-workgroup kernel: bit-identical for every epilogue (incl. the gelu'-saving
+    pair), both tile widths, fewer tiles than CUs, several tiles per CU and a ragged last round."""
+    g = torch.Generator(device="cpu").manual_seed(M + 17 * N)
+    A = torch.randn(M, Kd, generator=g).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, Kd, generator=g) * 0.1).to(DEV, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(DEV, torch.bfloat16)
+    u_in = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    outs = {}
+    try:
+        for pers in (0, 1):
+            for n192 in (0, 1):
+                K.set_knob("GEMM_BF16_PERSIST", pers)
+                K.set_knob("GEMM_BF16_N192", n192)
+                C0, _ = K.gemm_bf16(A, W, None, False, 0)
+                C1, _ = K.gemm_bf16(A, W, bias, False, 1)
+                y, u = K.gemm_bf16(A, W, bias, False, 5)
+                ys, us = K.gemm_bf16(A, W, bias, False, 7)
+                du, _ = K.gemm_bf16(A, W, None, False, 6, u_in)
+                dm, _ = K.gemm_bf16(A, W, None, False, 8, u_in)
+                outs[(pers, n192)] = (C0, C1, y, u, ys, us, du, dm)
+    finally:
+        K.reset_knobs()
+    ref = A.float() @ W.float().t()
+    torch.testing.assert_close(outs[(1, 0)][0].float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()) / 8)
+    for key, o in outs.items():
+        for i, (a, b) in enumerate(zip(outs[(0, key[1])], o)):
+            assert torch.equal(a, b), (key, i)
+
+
 @pytest.mark.parametrize("M,N,Kd", [(256, 256, 64), (300, 776, 192), (4096, 768, 768), (1000, 2304, 3072),
                                     (16384, 3072, 768)])
 def test_gemm_bf16_four_wave_kernel_matches_fp32(M, N, Kd):

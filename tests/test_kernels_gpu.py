@@ -178,6 +178,32 @@ def test_sgd_mixed_bf16(first):
     assert float(g.float().abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("first", [True, False])
+def test_sgd_mixed_two_chunk_variant_bit_identical(first):
+    """Knob SGD_MIXED_V: the two-chunks-per-trip form and the nontemporal-store form of the mixed SGD write the same
+    bits as the one-chunk form (n spans several grid strides plus a partial one, so both loops and the tail run)."""
+    from simple_distributed_machine_learning_amd import _native
+
+    K = _native.kernels()
+    n = 8192 * 256 * 8 * 2 + 8 * 1000 + 64  # > 2 strides of the 8192-block grid, odd remainder
+    outs = []
+    try:
+        for v in (0, 1, 2):
+            K.set_knob("SGD_MIXED_V", v)
+            master = rnd(n, seed=40)
+            p = master.to(torch.bfloat16)
+            g = rnd(n, seed=41).to(torch.bfloat16)
+            buf = rnd(n, seed=42)
+            ops.sgd_momentum_mixed_(master, p, g, buf, 0.1, 0.5, 0.0, 1e-4, False, first, True)
+            assert float(g.float().abs().sum()) == 0.0
+            outs.append((master, p, buf))
+    finally:
+        K.reset_knobs()
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("rows,V", [(7, 97), (64, 50257), (33, 1000), (5, 4096), (3, 131073), (2, 7), (9, 50257 * 2)])
 def test_cross_entropy_bf16(rows, V):
     from simple_distributed_machine_learning_amd.ops.transformer import cross_entropy_sum

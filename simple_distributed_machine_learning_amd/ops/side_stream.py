@@ -8,6 +8,11 @@ pass (an autograd-engine callback queued by the first side launch of the pass, s
 by an optimizer step is safe) and wherever the engine synchronises or steps a stage's gradients
 (``join_side_streams``). Never used while a HIP graph is being captured. ``SDML_WGRAD_STREAM=0`` keeps every launch on
 the compute stream.
+
+Operand lifetime: by default (``SDML_SIDE_HOLD=1``) the operands of every side launch are held here until the join, and
+released only after the compute stream has waited for the side stream, so the caching allocator reuses their blocks in
+compute-stream order - the same blocks every step. ``SDML_SIDE_HOLD=0`` uses ``record_stream`` instead: a freed block
+then waits for the side stream's progress at reuse time, and the allocator's choices vary with timing.
 """
 from __future__ import annotations
 
@@ -16,12 +21,15 @@ import os
 import torch
 
 WGRAD_STREAM = os.environ.get("SDML_WGRAD_STREAM", "1") == "1"
-# the convolutions' weight gradients (ResNet) only on request: measured +3.7 % on one run and -12 / -26 % on two others
-# of the same A/B (profiles/r6_side_stream_ab.jsonl) - the side stream's record_stream holds back every activation
-# gradient's block from reuse until the side stream passes it, and the ResNet step's allocations then vary run to run
+# the convolutions' weight gradients (ResNet) only on request. With record_stream: +3.7 % on one run and -12 / -26 % on
+# two others of the same A/B (profiles/r6_side_stream_ab.jsonl). With the operands held to the join: 121.4-122.3 K
+# samples/s in 5 of 7 runs against 116.4-117.4 K, but 105.7 K and 113.6 K in the other two
+# (profiles/r6_side_hold_ab.jsonl): still not a stable default
 CONV_WGRAD_STREAM = os.environ.get("SDML_CONV_WGRAD_STREAM", "0") == "1"
+HOLD = os.environ.get("SDML_SIDE_HOLD", "1") == "1"
 _SIDE = {}
 _PENDING = []
+_HELD = []
 
 
 def _side_stream(dev):
@@ -36,6 +44,7 @@ def join_side_streams():
     while _PENDING:
         s = _PENDING.pop()
         torch.cuda.current_stream(s.device).wait_stream(s)
+    _HELD.clear()  # after the waits: the blocks return to the allocator in compute-stream order
 
 
 def on_side(t: torch.Tensor) -> bool:
@@ -44,8 +53,8 @@ def on_side(t: torch.Tensor) -> bool:
 
 def launch(fn, *operands, enabled: bool = True):
     """Run ``fn()`` (kernel launches that only accumulate into persistent gradient buffers) on the side stream when
-    ``enabled`` and ``on_side`` hold for the first operand, else in place; the operands are recorded on the side
-    stream."""
+    ``enabled`` and ``on_side`` hold for the first operand, else in place; the operands stay allocated until the
+    next join (see the module docstring)."""
     if not enabled or not operands or not on_side(operands[0]):
         fn()
         return
@@ -55,8 +64,12 @@ def launch(fn, *operands, enabled: bool = True):
     side.wait_stream(cur)
     with torch.cuda.stream(side):
         fn()
-    for t in operands:  # the caching allocator must not hand these to the compute stream before the side is done
-        t.record_stream(side)
+    # the caching allocator must not hand these to the compute stream before the side is done
+    if HOLD:
+        _HELD.extend(operands)
+    else:
+        for t in operands:
+            t.record_stream(side)
     if not _PENDING:  # first side launch of this backward pass: join when the pass ends
         torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
     if side not in _PENDING:

@@ -239,13 +239,13 @@ class _Conv3x3Fn(torch.autograd.Function):
         K = kernels()
         dy = dy.contiguous(memory_format=torch.channels_last)
         gw = None
+        late = None  # the side-stream weight gradient, enqueued after the input gradient (side_stream.CONV_WGRAD_AFTER)
         if ctx.needs_input_grad[1]:
             if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
-                # straight into the flat gradient buffer (SDML_CONV_WGRAD_STREAM=1: on the side stream, launched first so
-                # it runs beside the input gradient below; ops/side_stream.py)
+                # straight into the flat gradient buffer (SDML_CONV_WGRAD_STREAM=1: on the side stream, beside the input
+                # gradient below; ops/side_stream.py)
                 g = w.grad
-                side_stream.launch(lambda: K.conv3x3_wgrad_bf16_(dy, x, g), dy, x,
-                                   enabled=side_stream.CONV_WGRAD_STREAM)
+                late = _side_wgrad(lambda: K.conv3x3_wgrad_bf16_(dy, x, g), dy, x, ctx.needs_input_grad[0])
             else:
                 gw = torch.zeros_like(w)
                 K.conv3x3_wgrad_bf16_(dy, x, gw)
@@ -260,8 +260,24 @@ class _Conv3x3Fn(torch.autograd.Function):
                 ctx.back.fill(part, rows, dx)
             else:
                 dx = K.conv3x3_fwd_bf16(dy, ctx.wd, add=add)
+        if late is not None:
+            late()
         ctx.wd = ctx.back = None
         return dx, gw, None, None, None
+
+
+def _side_wgrad(fn, dy, x, dx_follows: bool):
+    """Launch a convolution's weight gradient ``fn`` (on the side stream when SDML_CONV_WGRAD_STREAM=1). Returns None
+    once launched, or - side stream on, ``CONV_WGRAD_AFTER``, an input gradient to come - a closure the caller runs
+    after enqueuing the input gradient: the side stream then waits for an event recorded here, before it, so the two
+    still overlap but the input gradient's workgroups reach the CUs first."""
+    on = side_stream.CONV_WGRAD_STREAM
+    if on and dx_follows and side_stream.CONV_WGRAD_AFTER:
+        ev = side_stream.ready_event(dy)
+        if ev is not None:
+            return lambda: side_stream.launch(fn, dy, x, ready=ev)
+    side_stream.launch(fn, dy, x, enabled=on)
+    return None
 
 
 def hip_eligible(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
@@ -316,17 +332,19 @@ class _ConvGeneralFn(torch.autograd.Function):
         w, st, pd = ctx.w, ctx.stride, ctx.pad
         dy = dy.contiguous(memory_format=torch.channels_last)
         gw = None
-        if ctx.needs_input_grad[1]:  # (first: on the side stream it runs beside the input gradient)
+        late = None
+        if ctx.needs_input_grad[1]:  # (on the side stream it runs beside the input gradient)
             if w.grad is not None and w.grad.is_contiguous() and w.grad.dtype == torch.bfloat16:
                 g = w.grad
-                side_stream.launch(lambda: kernels().conv_wgrad_bf16_(dy, x, g, st, pd), dy, x,
-                                   enabled=side_stream.CONV_WGRAD_STREAM)
+                late = _side_wgrad(lambda: kernels().conv_wgrad_bf16_(dy, x, g, st, pd), dy, x, ctx.needs_input_grad[0])
             else:
                 gw = torch.zeros_like(w)
                 kernels().conv_wgrad_bf16_(dy, x, gw, st, pd)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _general_dgrad(dy, x, w, st, pd, add=_take_addend(ctx.link), back=ctx.back)
+        if late is not None:
+            late()
         ctx.back = None
         return dx, gw, None, None, None, None, None
 

@@ -131,9 +131,11 @@ class _LinearFn(torch.autograd.Function):
         w, b = ctx.w, ctx.b
         g2 = gy.reshape(-1, gy.shape[-1])
         wt = _w_t(w) if (ctx.needs_input_grad[0] and ctx.hand and g2.stride(-1) == 1) else None
-        # the weight gradient first when it goes to the side stream (it then runs beside the input gradient)
+        # the weight gradient first when it goes to the side stream (it then runs beside the input gradient); with
+        # SDML_LINEAR_WGRAD_AFTER=1 it is enqueued after the input gradient, waiting on an event recorded before it
         side = _on_side(g2)
-        if side:
+        ready = side_stream.ready_event(g2) if side and _WGRAD_AFTER else None
+        if side and ready is None:
             gw, gb = _param_grads(g2, x2, w, b, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         dx = None
         if ctx.needs_input_grad[0]:
@@ -142,22 +144,25 @@ class _LinearFn(torch.autograd.Function):
                 dx = dx.view(ctx.in_shape)
             else:
                 dx = (g2 @ w).view(ctx.in_shape)
-        if not side:
-            gw, gb = _param_grads(g2, x2, w, b, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        if not side or ready is not None:
+            gw, gb = _param_grads(g2, x2, w, b, ctx.needs_input_grad[1], ctx.needs_input_grad[2], ready)
         return dx, gw, gb
 
 
 # weight gradients on a side stream beside the input gradient (ops/side_stream.py)
+_WGRAD_AFTER = os.environ.get("SDML_LINEAR_WGRAD_AFTER", "0") == "1"
+
+
 def _on_side(g2):
     return side_stream.on_side(g2)
 
 
-def _wgrad_launch(g2, x2, gw, gb):
+def _wgrad_launch(g2, x2, gw, gb, ready=None):
     """gw (+ gb) += the weight (bias) gradient, on the side stream when it is on (ops/side_stream.py)."""
-    side_stream.launch(lambda: kernels().wgrad_bf16_(g2, x2, gw, gb), g2, x2)
+    side_stream.launch(lambda: kernels().wgrad_bf16_(g2, x2, gw, gb), g2, x2, ready=ready)
 
 
-def _param_grads(g2, x2, w, b, need_w: bool, need_b: bool):
+def _param_grads(g2, x2, w, b, need_w: bool, need_b: bool, ready=None):
     """Weight / bias gradients of y = x w^T + b from g2 = dy: added in place into the flat-buffer .grad
     (returns None for those) or returned for autograd to accumulate."""
     gw = gb = None
@@ -166,7 +171,7 @@ def _param_grads(g2, x2, w, b, need_w: bool, need_b: bool):
         if w.grad is not None and _wgrad_ok(g2, x2, w.grad):
             fuse_b = (b is not None and need_b and b.grad is not None
                       and b.grad.is_contiguous() and b.grad.dtype == torch.bfloat16)
-            _wgrad_launch(g2, x2, w.grad, b.grad if fuse_b else None)
+            _wgrad_launch(g2, x2, w.grad, b.grad if fuse_b else None, ready)
             bias_done = fuse_b
         elif w.grad is not None:
             w.grad.addmm_(g2.t(), x2)
@@ -223,7 +228,8 @@ class _MLPFn(torch.autograd.Function):
         gw2, gb2 = _param_grads(g2, a, w2, b2, ctx.needs_input_grad[3], ctx.needs_input_grad[4])
         w1t = _w_t(w1) if (ctx.needs_input_grad[0] and _HAND and du.stride(-1) == 1) else None
         side = _on_side(du)
-        if side:  # (as in _LinearFn: the side-stream weight gradient first)
+        ready = side_stream.ready_event(du) if side and _WGRAD_AFTER else None
+        if side and ready is None:  # (as in _LinearFn: the side-stream weight gradient first)
             gw1, gb1 = _param_grads(du, x2, w1, b1, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         dx = None
         if ctx.needs_input_grad[0]:
@@ -232,8 +238,8 @@ class _MLPFn(torch.autograd.Function):
                 dx = dx.view(ctx.in_shape)
             else:
                 dx = (du @ w1).view(ctx.in_shape)
-        if not side:
-            gw1, gb1 = _param_grads(du, x2, w1, b1, ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+        if not side or ready is not None:
+            gw1, gb1 = _param_grads(du, x2, w1, b1, ctx.needs_input_grad[1], ctx.needs_input_grad[2], ready)
         return dx, gw1, gb1, gw2, gb2
 
 

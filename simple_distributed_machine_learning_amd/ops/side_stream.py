@@ -21,12 +21,15 @@ import os
 import torch
 
 WGRAD_STREAM = os.environ.get("SDML_WGRAD_STREAM", "1") == "1"
-# the convolutions' weight gradients (ResNet) only on request. With record_stream: +3.7 % on one run and -12 / -26 % on
-# two others of the same A/B (profiles/r6_side_stream_ab.jsonl). With the operands held to the join: 121.4-122.3 K
-# samples/s in 5 of 7 runs against 116.4-117.4 K, but 105.7 K and 113.6 K in the other two
-# (profiles/r6_side_hold_ab.jsonl): still not a stable default
-CONV_WGRAD_STREAM = os.environ.get("SDML_CONV_WGRAD_STREAM", "0") == "1"
+# the convolutions' weight gradients (ResNet). With record_stream: +3.7 % on one run and -12 / -26 % on two others of
+# the same A/B (profiles/r6_side_stream_ab.jsonl). With the operands held to the join and the weight gradient enqueued
+# after the input gradient (CONV_WGRAD_AFTER): 121.9-122.3 K samples/s in 3 of 4 runs, 113.7 K in one, against
+# 113.5-117.0 K on the compute stream (profiles/r6_conv_side_order_ab.jsonl): on by default
+CONV_WGRAD_STREAM = os.environ.get("SDML_CONV_WGRAD_STREAM", "1") == "1"
 HOLD = os.environ.get("SDML_SIDE_HOLD", "1") == "1"
+# conv weight gradients: enqueued after the input gradient (waiting on an event recorded before it), so the input
+# gradient's workgroups are dispatched first and the weight gradient fills the CUs its last round leaves free
+CONV_WGRAD_AFTER = os.environ.get("SDML_CONV_WGRAD_AFTER", "1") == "1"
 _SIDE = {}
 _PENDING = []
 _HELD = []
@@ -51,17 +54,31 @@ def on_side(t: torch.Tensor) -> bool:
     return WGRAD_STREAM and t.is_cuda and not torch.cuda.is_current_stream_capturing()
 
 
-def launch(fn, *operands, enabled: bool = True):
+def ready_event(t: torch.Tensor, enabled: bool = True):
+    """An event on the compute stream at this point (for a side launch enqueued later that must not wait for the work
+    enqueued in between), or None when the side stream is not in use."""
+    if not enabled or not on_side(t):
+        return None
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(t.device))
+    return ev
+
+
+def launch(fn, *operands, enabled: bool = True, ready=None):
     """Run ``fn()`` (kernel launches that only accumulate into persistent gradient buffers) on the side stream when
     ``enabled`` and ``on_side`` hold for the first operand, else in place; the operands stay allocated until the
-    next join (see the module docstring)."""
+    next join (see the module docstring). ``ready``: an event from ``ready_event`` to wait for instead of the compute
+    stream's current point."""
     if not enabled or not operands or not on_side(operands[0]):
         fn()
         return
     dev = operands[0].device
     cur = torch.cuda.current_stream(dev)
     side = _side_stream(dev)
-    side.wait_stream(cur)
+    if ready is None:
+        side.wait_stream(cur)
+    else:
+        side.wait_event(ready)
     with torch.cuda.stream(side):
         fn()
     # the caching allocator must not hand these to the compute stream before the side is done

@@ -178,8 +178,8 @@ __device__ __forceinline__ int xcd_block(int id, int n) { return (n % 8 == 0) ? 
 // feeds both sub-blocks' MFMAs and the wave carries two independent score -> softmax -> PV chains, so one sub-block's
 // exp / max / sum VALU work can issue beside the other's MFMAs. NWV waves per workgroup (4, or 2 with QS = 2: the
 // same 128 queries per workgroup, four workgroups per CU).
-template <int KBT, int QS, int NWV = NW>  // keys per tile (64 or 128)
-__global__ void __launch_bounds__(64 * NWV, 8 / NWV) attn_fwd_kernel(AttnArgs a) {
+template <int KBT, int QS, int NWV = NW, int MINW = 8 / NWV>  // keys per tile (64 or 128); MINW: waves per SIMD bound
+__global__ void __launch_bounds__(64 * NWV, MINW) attn_fwd_kernel(AttnArgs a) {
   constexpr int NC = KBT / 32;  // 32-key sub-blocks per tile
   constexpr int QWV = QW * QS;  // queries per wave
   constexpr int QBW = QWV * NWV;  // queries per workgroup
@@ -642,8 +642,13 @@ void attention_fwd_bf16(const AttnShape& s, hipStream_t stream) {
     return;
   }
   const int nqb = (s.S + QB - 1) / QB;
+  const int occ = knob(KNOB_ATTN_OCC);  // (A/B) register bound for 3 or 4 waves per SIMD instead of 2
   if (g_fwd_kb == 128)
     hipLaunchKernelGGL((attn_fwd_kernel<128, 1>), dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
+  else if (occ == 3)
+    hipLaunchKernelGGL((attn_fwd_kernel<64, 1, NW, 3>), dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
+  else if (occ == 4)
+    hipLaunchKernelGGL((attn_fwd_kernel<64, 1, NW, 4>), dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
   else
     hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), dim3(nqb * s.B * s.H), dim3(256), 0, stream, a);
 }

@@ -122,7 +122,7 @@ __device__ __forceinline__ s16x4 ds_tr16(const unsigned char* p) {
 // the elementwise part of the epilogues on one 16-B row piece v (bf16(acc (+ bias)) of 8 columns gcol.. of row grow),
 // then its store (shared by the 8-wave and 4-wave kernels)
 template <int EPI, typename V = u16x8>
-__device__ __forceinline__ void store_piece(const GP& p, const V v, int grow, int gcol) {
+__device__ __forceinline__ void store_piece(const GP& p, const V v, int grow, int gcol, const V* pre = nullptr) {
   constexpr int W = sizeof(V) / sizeof(u16);  // 8 (16-B row pieces) or 4 (the persistent kernel's 8-B pieces)
   V o = v;
   if constexpr (EPI == EPI_BIAS_GELU) {
@@ -144,7 +144,7 @@ __device__ __forceinline__ void store_piece(const GP& p, const V v, int grow, in
       for (int e = 0; e < W; ++e) o[e] = f2bf(gelu_f(bf2f(v[e])));
     }
   } else if constexpr (EPI == EPI_DGELU) {
-    const V u = *reinterpret_cast<const V*>(p.aux + (size_t)grow * p.ldaux + gcol);
+    const V u = pre ? *pre : *reinterpret_cast<const V*>(p.aux + (size_t)grow * p.ldaux + gcol);  // (pre: loaded early)
     if (p.gsave) {
 #pragma unroll
       for (int e = 0; e < W; ++e) o[e] = f2bf(bf2f(u[e]) * bf2f(v[e]));
@@ -169,6 +169,17 @@ __device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&ac
                                                    int n0, int wave, int lane) {
   const int wm = wave / WNW, wn = wave % WNW;
   const int g = lane >> 4, l16 = lane & 15;
+  // EPI_DGELU: every aux piece this lane will need, loaded now (rows / columns clamped into the operand: lanes that store
+  // nothing load valid memory and drop it)
+  u16x8 auxv[EPI == EPI_DGELU ? 16 : 1];
+  if constexpr (EPI == EPI_DGELU) {
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int row = 8 * it + (lane >> 3), ch = lane & 7;
+      const int grow = min(m0 + wm * 128 + row, p.M - 1), gcol = min(n0 + wn * 16 * NJ + 8 * ch, p.N - 8);
+      auxv[it] = *reinterpret_cast<const u16x8*>(p.aux + (size_t)grow * p.ldaux + gcol);
+    }
+  }
   // wave image [128 rows][64 cols] bf16 (128 B rows, 16-B chunks swizzled like the A image; NJ = 3 uses 48 of them)
   unsigned char* W = smem + wave * (128 * 128);
   if constexpr (TR) {
@@ -212,6 +223,18 @@ __device__ __forceinline__ void gemm_bf16_epilogue(const GP& p, const f32x4 (&ac
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
+  if constexpr (EPI == EPI_DGELU) {
+    // the 16 aux pieces were loaded before the image writes (one memory round trip instead of four)
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int row = 8 * it + (lane >> 3), ch = lane & 7;
+      const u16x8 v = *reinterpret_cast<const u16x8*>(W + row * 128 + 16 * (ch ^ rk_swz(row)));
+      const int grow = m0 + wm * 128 + row, gcol = n0 + wn * 16 * NJ + 8 * ch;
+      if (ch >= 2 * NJ || grow >= p.M || gcol >= p.N || p.nostore) continue;
+      store_piece<EPI>(p, v, grow, gcol, &auxv[it]);
+    }
+    return;
+  }
 #pragma unroll 4
   for (int it = 0; it < 16; ++it) {
     const int row = 8 * it + (lane >> 3), ch = lane & 7;

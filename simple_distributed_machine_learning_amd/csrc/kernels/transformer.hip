@@ -247,6 +247,14 @@ __global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const u16* __restrict__ x,
                                                       int D, float eps) {
   const int lane = threadIdx.x & 63;
   const int nch = D / 8;
+  // this lane's gamma / beta chunks, once (they were re-read for every row)
+  u16x8 wv[LN_MAXV], bv[LN_MAXV];
+#pragma unroll
+  for (int c = 0; c < LN_MAXV; ++c) {
+    const int ch = min(lane + 64 * c, nch - 1);
+    wv[c] = *reinterpret_cast<const u16x8*>(w + 8 * ch);
+    bv[c] = *reinterpret_cast<const u16x8*>(b + 8 * ch);
+  }
   for (int row = blockIdx.x * (LN_T / 64) + (threadIdx.x >> 6); row < rows; row += gridDim.x * (LN_T / 64)) {
     const u16* xr = x + (size_t)row * D;
     u16x8 v[LN_MAXV];
@@ -288,11 +296,9 @@ __global__ void __launch_bounds__(LN_T) ln_fwd_kernel(const u16* __restrict__ x,
     for (int c = 0; c < LN_MAXV; ++c) {
       int ch = lane + 64 * c;
       if (ch < nch) {
-        u16x8 wv = *reinterpret_cast<const u16x8*>(w + 8 * ch);
-        u16x8 bv = *reinterpret_cast<const u16x8*>(b + 8 * ch);
         u16x8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf((bf2f(v[c][e]) - mu) * rs * bf2f(wv[e]) + bf2f(bv[e]));
+        for (int e = 0; e < 8; ++e) o[e] = f2bf((bf2f(v[c][e]) - mu) * rs * bf2f(wv[c][e]) + bf2f(bv[c][e]));
         *reinterpret_cast<u16x8*>(yr + 8 * ch) = o;
       }
     }
@@ -314,19 +320,25 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const u16* __restrict__ x,
   for (int c = 0; c < LN_MAXV; ++c)
 #pragma unroll
     for (int e = 0; e < 8; ++e) pw[c][e] = pb[c][e] = 0.f;
+  // this lane's gamma chunks, once (they were re-read twice per row)
+  u16x8 wc[LN_MAXV];
+#pragma unroll
+  for (int c = 0; c < LN_MAXV; ++c) wc[c] = *reinterpret_cast<const u16x8*>(w + 8 * min(lane + 64 * c, nch - 1));
   for (int row = blockIdx.x * (LN_T / 64) + wv_id; row < rows; row += gridDim.x * (LN_T / 64)) {
     const u16* xr = x + (size_t)row * D;
     const u16* gr = gy + (size_t)row * D;
     const float mu = mean[row], rs = rstd[row];
     float s1 = 0.f, s2 = 0.f;
-    u16x8 xv[LN_MAXV], gv[LN_MAXV];
+    u16x8 xv[LN_MAXV], gv[LN_MAXV], av[LN_MAXV];
 #pragma unroll
     for (int c = 0; c < LN_MAXV; ++c) {
       int ch = lane + 64 * c;
       if (ch < nch) {
         xv[c] = *reinterpret_cast<const u16x8*>(xr + 8 * ch);
         gv[c] = *reinterpret_cast<const u16x8*>(gr + 8 * ch);
-        u16x8 wv = *reinterpret_cast<const u16x8*>(w + 8 * ch);
+        // the residual-path gradient with the row's other loads (it was a second round trip after the reductions)
+        av[c] = gadd ? *reinterpret_cast<const u16x8*>(gadd + (size_t)row * D + 8 * ch) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        const u16x8 wv = wc[c];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float xh = (bf2f(xv[c][e]) - mu) * rs;
@@ -346,14 +358,12 @@ __global__ void __launch_bounds__(LN_T) ln_bwd_kernel(const u16* __restrict__ x,
     for (int c = 0; c < LN_MAXV; ++c) {
       int ch = lane + 64 * c;
       if (ch < nch) {
-        u16x8 wv = *reinterpret_cast<const u16x8*>(w + 8 * ch);
-        u16x8 av = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (gadd) av = *reinterpret_cast<const u16x8*>(gadd + (size_t)row * D + 8 * ch);
+        const u16x8 wv = wc[c];
         u16x8 o;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float xh = (bf2f(xv[c][e]) - mu) * rs;
-          o[e] = f2bf(rs * (bf2f(gv[c][e]) * bf2f(wv[e]) - s1 - xh * s2) + bf2f(av[e]));
+          o[e] = f2bf(rs * (bf2f(gv[c][e]) * bf2f(wv[e]) - s1 - xh * s2) + bf2f(av[c][e]));
         }
         *reinterpret_cast<u16x8*>(dr + 8 * ch) = o;
       }

@@ -1293,8 +1293,9 @@ void conv3x3_fwd_bf16(const void* x, const void* wt, void* y, int Nb, int H, int
     const bool big = Co % 128 == 0 && a.tiles_m * (Co / 128) >= bn128_min;
     const int bn = big ? 128 : 64;
     a.tiles_n = Co / bn;
-    const size_t lds = std::max<size_t>((size_t)((C > 64 ? 2 : 1) * (BM + 2 * W + 2) * 64 + 2 * bn * BK) * sizeof(u16),
-                                        (size_t)store_tile_lds(bn));
+    size_t lds = std::max<size_t>((size_t)((C > 64 ? 2 : 1) * (BM + 2 * W + 2) * 64 + 2 * bn * BK) * sizeof(u16),
+                                  (size_t)store_tile_lds(bn));
+    if (knob(KNOB_CONV_HALO_1WG) == 1) lds = std::max<size_t>(lds, 81 * 1024);  // (A/B) one workgroup per CU
     static bool attr = [] {
       for (const void* f : {reinterpret_cast<const void*>(conv3x3_halo_kernel<128, 5, 0>),
                              reinterpret_cast<const void*>(conv3x3_halo_kernel<128, 7, 0>),

@@ -57,6 +57,7 @@ const Entry kTable[KNOB_COUNT] = {
     {"ATTN_FWD_QS", 1, false, nullptr},
     {"SGD_MIXED_V", 0, false, nullptr},
     {"ATTN_OCC", 2, false, nullptr},
+    {"CONV_HALO_1WG", 0, false, nullptr},
     {"GEMM_BF16_PERSIST", -1, false, nullptr},
     {"GEMM_BF16_NOSTORE", 0, true, nullptr},
     {"U8_VARIANT", 0, true, nullptr},

@@ -56,7 +56,8 @@ enum KnobId : int {
   KNOB_U8_WGRAD_PAIR,        // ring uint8 weight gradient: pairwise in-kernel combine of splits s and s + S/2
   KNOB_ATTN_FWD_QS,          // attention forward: 32-query sub-blocks per wave (1, or 2: two independent softmax chains; 3: 2 in 2-wave blocks)
   KNOB_SGD_MIXED_V,          // bf16 + fp32-master SGD: 0 one 8-element chunk per loop trip, 1 two chunks in flight, 2 nontemporal stores
-  KNOB_ATTN_OCC,             // attention forward: waves-per-SIMD register bound 2 (default), 3 or 4 (A/B)
+  KNOB_ATTN_OCC,
+  KNOB_CONV_HALO_1WG,        // (A/B) halo conv kernel padded to one workgroup per CU (wave quantization test)             // attention forward: waves-per-SIMD register bound 2 (default), 3 or 4 (A/B)
   KNOB_GEMM_BF16_PERSIST,    // bf16 NT GEMM (4-phase, C^T accumulators): persistent workgroups, the next tile's DMA under this one's last K-steps (-1 auto, 0, 1)
   // ---- probe switches (pinned in production builds) ----
   KNOB_GEMM_BF16_NOSTORE,    // 1: bf16 GEMM skips its output stores (timing only)

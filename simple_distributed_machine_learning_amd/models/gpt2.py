@@ -23,7 +23,8 @@ import torch.nn.functional as F
 
 from .base import ModelSpec, PipelineStage
 from ..ops.linear import Linear, linear, lm_head, mlp_gelu
-from ..ops.transformer import LayerNorm, add_layer_norm, causal_attention, cross_entropy_sum, embedding, gelu
+from ..ops.transformer import (LayerNorm, add_layer_norm, causal_attention, cross_entropy_sum, embedding, gelu,
+                               layer_norm_pass)
 from ..parallel.tp import TPContext, column_slice, copy_to_tp, reduce_from_tp, shard_parameter
 
 
@@ -171,7 +172,7 @@ class GPT2Stage(PipelineStage):
             return lm_head(self.ln_f(x), self.lm_head.weight) if last else x
         # each residual add is fused into the LayerNorm that reads its sum (ln_2 of the same block,
         # ln_1 of the next, ln_f at the end); the block maths is exactly Block.forward
-        y = blocks[0].ln_1(x)
+        x, y = layer_norm_pass(x, blocks[0].ln_1)  # (x feeds ln_1 and the residual: one backward node for both)
         for i, blk in enumerate(blocks):
             x, y = add_layer_norm(x, blk.attn(y), blk.ln_2)
             m = blk.mlp(y)

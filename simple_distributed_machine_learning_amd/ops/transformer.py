@@ -45,6 +45,43 @@ def layer_norm(x, w, b, eps: float = 1e-5):
     return F.layer_norm(x, (x.shape[-1],), w, b, eps)
 
 
+class _LayerNormPassFn(torch.autograd.Function):
+    """(x, LayerNorm(x)) for an x that also feeds a residual path: the backward adds the residual-path gradient inside
+    the LayerNorm backward kernel (fp32, rounded once) instead of autograd summing the two bf16 gradients with a
+    separate add kernel (GPT-2: each stage's first block)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        xc = x.contiguous()
+        y, mean, rstd = kernels().layernorm_fwd_bf16(xc, w, b, eps)
+        ctx.save_for_backward(xc, w, mean, rstd)
+        ctx.params = (w, b)
+        return xc.view_as(xc), y
+
+    @staticmethod
+    def backward(ctx, g_x, g_y):
+        x, w, mean, rstd = ctx.saved_tensors
+        wp, bp = ctx.params
+        g_x = None if g_x is None else g_x.contiguous()
+        if g_y is None:
+            return g_x, None, None, None
+        if wp.grad is not None and bp.grad is not None and wp.grad.is_contiguous() and bp.grad.is_contiguous():
+            d = kernels().layernorm_bwd_bf16_accum(x, w, g_y.contiguous(), mean, rstd, wp.grad, bp.grad, g_x)
+            return d, None, None, None
+        d, dw, db = kernels().layernorm_bwd_bf16(x, w, g_y.contiguous(), mean, rstd)
+        if g_x is not None:
+            d = d + g_x
+        return d, dw.to(w.dtype), db.to(w.dtype), None
+
+
+def layer_norm_pass(x, ln: nn.LayerNorm):
+    """(x, ln(x)), both differentiable; on ROCm bf16 the two gradients of x meet inside the LayerNorm backward."""
+    w, b = ln.weight, ln.bias
+    if _hip_bf16(x, w, b) and x.shape[-1] % 8 == 0 and x.shape[-1] <= 4096:
+        return _LayerNormPassFn.apply(x, w, b, ln.eps)
+    return x, ln(x)
+
+
 class _AddLayerNormFn(torch.autograd.Function):
     """xs = x + h; y = LayerNorm(xs) in one pass. Backward: dxs = g_xs + LN_bwd(g_y), added inside
     the LayerNorm backward kernel; both addends of the residual get dxs."""

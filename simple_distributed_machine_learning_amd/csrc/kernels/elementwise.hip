@@ -59,38 +59,20 @@ struct MixedIn {
   u16x8 gr;
 };
 
-template <bool NT>
-__device__ __forceinline__ MixedIn mixed_load_(const float* master, const unsigned short* g, const float* buf, int64_t i,
+// (plain loads: nontemporal loads measured 2x slower on this stream, round 3 tools/probes/sgd_nt_ab.py)
+__device__ __forceinline__ MixedIn mixed_load(const float* master, const unsigned short* g, const float* buf, int64_t i,
                                               bool use_buf) {
   MixedIn in;
   const f32x4* m4 = reinterpret_cast<const f32x4*>(master) + 2 * i;
   const f32x4* b4 = reinterpret_cast<const f32x4*>(buf) + 2 * i;
-  const u16x8* g8 = reinterpret_cast<const u16x8*>(g) + i;
-  if constexpr (NT) {
-    in.mv[0] = __builtin_nontemporal_load(m4);
-    in.mv[1] = __builtin_nontemporal_load(m4 + 1);
-    in.gr = __builtin_nontemporal_load(g8);
-    if (use_buf) {
-      in.bo[0] = __builtin_nontemporal_load(b4);
-      in.bo[1] = __builtin_nontemporal_load(b4 + 1);
-    }
-  } else {
-    in.mv[0] = m4[0];
-    in.mv[1] = m4[1];
-    in.gr = *g8;
-    if (use_buf) {
-      in.bo[0] = b4[0];
-      in.bo[1] = b4[1];
-    }
+  in.mv[0] = m4[0];
+  in.mv[1] = m4[1];
+  in.gr = *(reinterpret_cast<const u16x8*>(g) + i);
+  if (use_buf) {
+    in.bo[0] = b4[0];
+    in.bo[1] = b4[1];
   }
   return in;
-}
-
-// (nontemporal loads measured 2x slower on this stream: plain loads only)
-template <bool NT>
-__device__ __forceinline__ MixedIn mixed_load(const float* master, const unsigned short* g, const float* buf, int64_t i,
-                                              bool use_buf) {
-  return mixed_load_<false>(master, g, buf, i, use_buf);
 }
 
 template <bool NT, typename T>
@@ -136,14 +118,14 @@ __global__ void __launch_bounds__(256) sgd_mixed_kernel(float* __restrict__ mast
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if constexpr (V == 1) {
     for (; i + stride < n8; i += 2 * stride) {
-      const MixedIn a = mixed_load<NT>(master, g, buf, i, use_buf);
-      const MixedIn b = mixed_load<NT>(master, g, buf, i + stride, use_buf);
+      const MixedIn a = mixed_load(master, g, buf, i, use_buf);
+      const MixedIn b = mixed_load(master, g, buf, i + stride, use_buf);
       mixed_update<NT>(a, master, p, g, buf, i, lr, mom, damp, wd, nesterov, first, zero_grad);
       mixed_update<NT>(b, master, p, g, buf, i + stride, lr, mom, damp, wd, nesterov, first, zero_grad);
     }
   }
   for (; i < n8; i += stride)
-    mixed_update<NT>(mixed_load<NT>(master, g, buf, i, use_buf), master, p, g, buf, i, lr, mom, damp, wd, nesterov,
+    mixed_update<NT>(mixed_load(master, g, buf, i, use_buf), master, p, g, buf, i, lr, mom, damp, wd, nesterov,
                      first, zero_grad);
 }
 
